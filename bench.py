@@ -1,0 +1,200 @@
+"""Benchmark: matched publishes/sec of the MI355X TopicsIndex engine (BASELINE.json metric).
+
+A step is one pass of the hot path over one batch: Subscribers() for every topic of a
+1M-topic publish batch already resident in HBM — walk, scan, expand/merge/emit of every
+client, identifier, shared and inline row (mq_match_device). The index (10M subscriptions,
+config-2/3 mix) is built through the C-ABI bulk path and kept resident.
+
+Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`): one process
+per GPU, the index replicated on every GPU and each rank matching its own 1M-topic batch —
+topics are independent units, so there is no data-path collective ("scaling": "weak"); only
+the timing barrier and a max-over-ranks all-reduce of the elapsed time use the process group.
+
+Rank 0 prints one JSON line with the roofline of the dominant kernel (k_emit; HIP events on
+its launch stream) and the CPU baseline (the oracle restatement of the Go trie, all allotted
+host cores, on a bounded sample of the same batch).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mqtt-server_amd"))
+
+METRIC = "matched publishes/sec (whole node) at 10M subs; HBM GB/s fraction of peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(msg):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def host_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))  # the GPU box allots 16 host cores per GPU
+
+
+def read_traffic(path, n_subs):
+    """HBM bytes per k_emit launch from a committed rocprofv3 PMC summary, if present."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(str(n_subs))
+        return None if e is None else float(e["hbm_bytes_per_emit_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--subs", type=int, default=10_000_000)
+    ap.add_argument("--clients", type=int, default=0, help="default: subs/10 (SURVEY.md §8d)")
+    ap.add_argument("--topics", type=int, default=1_000_000, help="publish topics per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n_clients = args.clients or max(1, args.subs // 10)
+
+    t0 = time.time()
+    w = W.gen_subscriptions(args.subs, n_clients, seed=W.BASE_SEED)
+    log(f"generated {args.subs} subscriptions ({w['n_unique_filters']} distinct filters) in {time.time()-t0:.1f}s")
+    t0 = time.time()
+    eng = E.Engine(device=local, expected_subs=args.subs)
+    eng.subscribe_bulk(w)
+    log(f"engine index built in {time.time()-t0:.1f}s: {eng.stats()}")
+    tb, to = W.gen_topics(w, args.topics, seed=W.BASE_SEED + 1000 * rank)
+    n = len(to) - 1
+
+    stream = torch.cuda.current_stream()
+    d_tb = torch.from_numpy(tb).to(f"cuda:{local}")
+    d_to = torch.from_numpy(to.view(np.int64)).to(f"cuda:{local}")
+    t0 = time.time()
+    eng.sync(stream.cuda_stream)
+    torch.cuda.synchronize()
+    log(f"device image uploaded in {time.time()-t0:.1f}s")
+
+    def step():
+        return eng.match_device(d_tb.data_ptr(), d_to.data_ptr(), n, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    eng.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        r = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    prof = eng.profile_read()
+    eng.profile(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    chunks = eng.match_chunks()
+    log(f"timed {args.steps} steps in {elapsed:.3f}s; kernels {prof}; chunks/step {chunks}")
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    value = n * world * args.steps / elapsed
+    emit_launches, emit_ms = prof.get("emit", (0, 0.0))
+    out = {
+        "metric": METRIC, "value": value, "unit": "publishes/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (SURVEY.md §8d generator, seed 0x6D716D61)",
+        "config": {
+            "workload": f"config-3 mix: {args.subs} subscriptions (depth 4-8, 30% '+', 10% '#', "
+                        f"5% $share, 0.1% top-level wildcards), {n} publish topics per GPU per step",
+            "subs": args.subs, "clients": n_clients, "topics_per_gpu": n,
+            "parallelism": f"index replicated on {world} GPU(s), topic batch per GPU",
+        },
+        "kernels_ms_per_step": {k: v[1] / max(1, args.steps) for k, v in prof.items()},
+        "emit_chunks_per_step": chunks,
+    }
+
+    # Algorithmic bytes: B = 8L + 4 + 16P + 16S + 16O per topic, with L, P, S, O
+    # from the oracle's exact counters on a sample of this batch; k_emit moves 16S + 16O.
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+            "traffic": None}
+    cpu = None
+    if not args.no_cpu and world == 1:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle as O
+        from digest import engine_digests
+        t0 = time.time()
+        orc = O.OracleIndex()
+        orc.subscribe_bulk(w)
+        log(f"oracle index built in {time.time()-t0:.1f}s")
+        cores = host_cores()
+        # calibrate, then time a sample of about --cpu-seconds of CPU work
+        cal = min(n, 256 * cores)
+        secs, _ = orc.bench_subscribers(tb, to[:cal + 1], cores)
+        m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
+        secs, _ = orc.bench_subscribers(tb, to[:m + 1], cores)
+        cpu = {"value": m / secs, "unit": "publishes/s", "cores": cores, "kind": "port",
+               "sample": f"first {m} topics of the rank-0 batch on the same {args.subs}-subscription "
+                         f"index, {cores} threads, Subscribers() per topic (C++ restatement of the "
+                         f"Go particle trie, oracle/)"}
+        # oracle counters + parity on a sample
+        ns = min(m, 4096)
+        dg_o, cnt_o, tot = orc.digest_batch(tb, to[:ns + 1], cores)
+        res = eng.match_batch(tb, to[:ns + 1])
+        dg_e, _ = engine_digests(res)
+        out["parity_sample"] = {"topics": ns, "bit_exact": bool((dg_e == dg_o).all())}
+        per_topic = {k: v / ns for k, v in tot.items()}
+        b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"] + 16 * per_topic["S"] + 16 * per_topic["O"]
+        b_emit = 16 * per_topic["S"] + 16 * per_topic["O"]
+        out["alg_bytes_per_topic"] = {"B": b_topic, "emit": b_emit, "L": per_topic["L"],
+                                      "P": per_topic["P"], "S": per_topic["S"], "O": per_topic["O"],
+                                      "sample_topics": ns}
+        if emit_ms > 0:
+            launch_ms = emit_ms / emit_launches
+            topics_per_launch = n / max(1, chunks)
+            achieved = b_emit * topics_per_launch / (launch_ms * 1e-3) / 1e9
+            roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS)
+            tr = read_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), args.subs)
+            roof["traffic"] = tr
+            out["emit_avg_launch_ms"] = launch_ms
+    out["roofline"] = roof
+    out["cpu_baseline"] = cpu
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,231 @@
+/*
+ * mqmatch.h — C-ABI of the MI355X (gfx950) topic-matching engine that replaces the
+ * reference's `TopicsIndex` hot path (/root/reference/topics.go:349-698).
+ *
+ * The Go broker reaches this through a thin cgo shim; every entry point
+ * below names the reference interface it replaces. Conventions:
+ *   - plain pointers and sizes only; strings are (ptr, len) and borrowed for the call only
+ *     (cgo rule: nothing keeps Go memory);
+ *   - return codes: >= 0 success, < 0 negative errno (MQ_E*); mq_last_error() describes the
+ *     last failure on the calling thread;
+ *   - client ids, filter ids and inline ids are u32 keys interned by the caller (the Go shim
+ *     interns client-ID strings and full filter strings; handlers and packets.Packet values
+ *     never cross the ABI, only ids and opaque retained-message handles do);
+ *   - the handle is internally synchronised: updates are serialised (the analogue of
+ *     root.Lock(), topics.go:402) and a batch runs on the snapshot sealed when it starts,
+ *     which is at least as strong as the reference's lock-free readers (topics.go:583, Q11);
+ *   - result buffers are owned by the library until mq_result_free().
+ */
+#ifndef MQMATCH_H
+#define MQMATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MQ_ABI_VERSION 1
+
+/* error codes (negative errno) */
+#define MQ_EINVAL (-22)
+#define MQ_ENOMEM (-12)
+#define MQ_ENODEV (-19)
+#define MQ_EIO (-5)
+#define MQ_ERANGE (-34)
+
+/* packets.Subscription flag bits (packets/packets.go:172-182) for mq_subscribe() */
+#define MQ_SUB_NOLOCAL 0x1u         /* NoLocal */
+#define MQ_SUB_RAP 0x2u             /* RetainAsPublished */
+#define MQ_SUB_RH_SHIFT 2           /* RetainHandling, 2 bits */
+
+/* mq_client_row.meta layout */
+#define MQ_META_QOS_MASK 0x3u       /* merged Qos = max over the client's matches */
+#define MQ_META_NOLOCAL 0x100u      /* merged NoLocal = OR over the client's matches */
+#define MQ_META_RAP 0x200u          /* base RetainAsPublished */
+#define MQ_META_RH_SHIFT 10         /* base RetainHandling, 2 bits */
+#define MQ_META_MERGE 0x1000u       /* internal: subscription may merge with another of its client */
+
+typedef struct mq_index mq_index;
+
+typedef struct mq_config {
+  int32_t device;          /* HIP device ordinal; the device is first touched by mq_sync/match */
+  uint32_t flags;          /* reserved, 0 */
+  uint64_t expected_subs;  /* capacity hint (0 = default) */
+  uint64_t expected_nodes; /* capacity hint (0 = default) */
+} mq_config;
+
+/* ---- lifecycle: NewTopicsIndex (topics.go:356-364) ---- */
+int mq_index_create(const mq_config* cfg, mq_index** out);
+void mq_index_destroy(mq_index* idx);
+const char* mq_last_error(void);
+uint32_t mq_abi_version(void);
+
+/* ---- updates (serialised; visible to batches started after they return) ---- */
+
+/* TopicsIndex.Subscribe(client, sub) (topics.go:401-419). `$SHARE/<group>/...` filters
+ * (Unicode EqualFold on segment 0, Q9) are stored as shared subscriptions keyed by
+ * (group, client). flags = MQ_SUB_*. Returns 1 if new, 0 if it replaced an existing one. */
+int mq_subscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t client_id,
+                 uint32_t filter_id, uint8_t qos, uint8_t flags, int32_t identifier);
+
+/* TopicsIndex.Unsubscribe(filter, client) (topics.go:423-448). Returns 1 whenever the
+ * filter's particle exists (Q10), else 0. */
+int mq_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t client_id);
+
+/* TopicsIndex.InlineSubscribe (topics.go:368-378): keyed by the inline identifier, no
+ * $SHARE handling. Returns 1 if new. */
+int mq_inline_subscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier,
+                        uint32_t filter_id);
+
+/* TopicsIndex.InlineUnsubscribe(id, filter) (topics.go:382-397). Returns 1 if the particle
+ * exists (trims only when its inline set became empty). */
+int mq_inline_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier);
+
+/* TopicsIndex.RetainMessage(pk) (topics.go:453-476). `handle` is the caller's opaque id of
+ * the packet; payload_len and retain are pk.Payload's length and pk.FixedHeader.Retain.
+ * Returns 1 (stored), -1 (a retained packet with payload and Retain was cleared) or 0.
+ * Written through *out; the int return is the status code. */
+int mq_retain_message(mq_index* idx, const char* topic, uint32_t tlen, uint64_t handle,
+                      uint32_t payload_len, uint8_t retain, int64_t* out);
+
+/* TopicsIndex.Retained.Delete(topic) as called by the expiry sweep (server.go:1726): removes
+ * the map entry only; the particle keeps its retain path (Q12). Returns 1 if it existed. */
+int mq_retained_delete(mq_index* idx, const char* topic, uint32_t tlen);
+
+/* TopicsIndex.Retained.Len() (server.go:980) */
+uint64_t mq_retained_len(const mq_index* idx);
+
+/* Columnar bulk Subscribe for the restore path (server.go:1624-1640): n filters as
+ * concatenated bytes + n+1 u64 offsets. out_new (nullable) receives Subscribe's results. */
+int mq_subscribe_bulk(mq_index* idx, const uint8_t* filter_bytes, const uint64_t* offsets,
+                      const uint32_t* client_ids, const uint32_t* filter_ids, const uint8_t* qos,
+                      const uint8_t* flags, const int32_t* identifiers, uint64_t n,
+                      uint8_t* out_new);
+
+/* Columnar bulk RetainMessage with payload (server.go:1688-1692). */
+int mq_retain_bulk(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets,
+                   const uint64_t* handles, uint64_t n);
+
+/* ---- batched match: TopicsIndex.Subscribers (topics.go:583-628) ---- */
+
+/* Client row: the merged packets.Subscription of one client (gatherSubscriptions +
+ * Subscription.Merge, topics.go:631-648, packets/packets.go:254-274). filter_id/identifier/
+ * RetainAsPublished/RetainHandling come from the base (first-gathered) subscription; qos is
+ * the max and NoLocal the OR over all of the client's matching subscriptions. The Go
+ * Identifiers map is {base filter: base identifier} plus the client's ident rows. */
+typedef struct mq_client_row {
+  uint32_t client_id;
+  uint32_t filter_id;
+  int32_t identifier;
+  uint32_t meta; /* MQ_META_* */
+} mq_client_row;
+
+/* Identifiers-map entry other than the base one: a further matching filter of the client
+ * with identifier > 0 (packets/packets.go:261-263). */
+typedef struct mq_ident_row {
+  uint32_t client_id;
+  uint32_t filter_id;
+  int32_t identifier;
+  uint32_t reserved;
+} mq_ident_row;
+
+/* Subscribers.Shared[filter][client] (topics.go:651-665): the stored subscription's own
+ * filter and its client; the group members before the host's SelectShared pick. */
+typedef struct mq_shared_row {
+  uint32_t filter_id;
+  uint32_t client_id;
+} mq_shared_row;
+
+/* Subscribers.InlineSubscriptions[id] (topics.go:668-676), last write already applied. */
+typedef struct mq_inline_row {
+  int32_t identifier;
+  uint32_t filter_id;
+} mq_inline_row;
+
+/* Per-topic result descriptor. Client and ident rows share one 16-byte row region of
+ * `sub_cap` rows starting at `sub_base`: client rows at [sub_base, sub_base + n_client),
+ * ident rows at [sub_base + sub_cap - n_ident, sub_base + sub_cap). */
+typedef struct mq_topic_result {
+  uint64_t sub_base;
+  uint64_t shared_base;
+  uint64_t inline_base;
+  uint32_t sub_cap;
+  uint32_t n_client;
+  uint32_t n_ident;
+  uint32_t n_shared;
+  uint32_t n_inline;
+  uint32_t reserved;
+} mq_topic_result;
+
+typedef struct mq_match_result {
+  uint32_t n_topics;
+  uint32_t reserved;
+  const mq_topic_result* topics; /* n_topics */
+  const mq_client_row* sub_rows; /* client rows; ident rows are read as mq_ident_row */
+  const mq_shared_row* shared_rows;
+  const mq_inline_row* inline_rows;
+  uint64_t n_sub_rows, n_shared_rows, n_inline_rows;
+} mq_match_result;
+
+/* Match a batch of publish topics (n topics as concatenated bytes + n+1 u64 offsets, host
+ * memory). Results are copied to library-owned host memory; free with mq_result_free. */
+int mq_match_batch(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets, uint32_t n,
+                   mq_match_result** out);
+
+/* Device-resident variant (inputs already in HBM on the index's device, enqueued on
+ * `hip_stream`, a hipStream_t or NULL). `out` receives DEVICE pointers owned by the index and
+ * valid until its next match call. Batches whose rows exceed the output budget are processed
+ * in chunks; then only the last chunk's rows remain resident and out->topics covers that
+ * chunk (out->n_topics); mq_match_chunks() reports the chunk count of the last call. */
+int mq_match_device(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t* d_offsets,
+                    uint32_t n, void* hip_stream, mq_match_result* out);
+uint32_t mq_match_chunks(const mq_index* idx);
+
+/* ---- batched reverse retained scan: TopicsIndex.Messages (topics.go:525-579) ---- */
+typedef struct mq_msg_result {
+  uint32_t n_filters;
+  uint32_t reserved;
+  const uint64_t* base;    /* n_filters: first handle of each filter */
+  const uint32_t* count;   /* n_filters */
+  const uint64_t* handles; /* retained-message handles (set per filter, order unspecified) */
+  uint64_t n_handles;
+} mq_msg_result;
+
+int mq_messages_batch(mq_index* idx, const uint8_t* filter_bytes, const uint64_t* offsets,
+                      uint32_t n, mq_msg_result** out);
+int mq_messages_device(mq_index* idx, const uint8_t* d_filter_bytes, const uint64_t* d_offsets,
+                       uint32_t n, void* hip_stream, mq_msg_result* out);
+
+void mq_result_free(void* result);
+
+/* ---- device image, statistics and profiling ---- */
+
+/* Push pending updates to the device image (incremental: only dirty pages are copied). */
+int mq_sync(mq_index* idx, void* hip_stream);
+
+typedef struct mq_stats {
+  uint64_t nodes, edges, edge_capacity;
+  uint64_t subs, subs_merge, shared, inlines;
+  uint64_t retained, retained_live;
+  uint64_t device_bytes, upload_bytes_total, syncs;
+  uint32_t max_depth, reserved;
+} mq_stats;
+int mq_index_stats(const mq_index* idx, mq_stats* out);
+
+/* Kernel timing by HIP events recorded on the launch stream around each kernel. */
+typedef struct mq_kernel_time {
+  char name[32];
+  uint64_t launches;
+  double total_ms;
+} mq_kernel_time;
+int mq_profile_enable(mq_index* idx, int enable);
+int mq_profile_read(const mq_index* idx, mq_kernel_time* out, uint32_t cap); /* returns count */
+int mq_profile_reset(mq_index* idx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MQMATCH_H */

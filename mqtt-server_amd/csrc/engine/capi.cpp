@@ -1,0 +1,290 @@
+// extern "C" surface of the engine (include/mqmatch.h). Each entry point serialises on the
+// handle's mutex — the analogue of the reference's root.Lock() (topics.go:402) — and turns C++
+// and HIP failures into negative errno codes with a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <mutex>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+
+#include "device.h"
+#include "index.h"
+#include "mqmatch.h"
+
+using namespace mq;
+
+struct mq_index {
+  std::mutex mu;
+  mq_config cfg;
+  std::unique_ptr<Index> ix;
+  std::unique_ptr<Device> dev;
+  bool profile = false;
+
+  Device& device() {
+    if (!dev) {
+      dev.reset(new Device(cfg.device));
+      dev->prof.enable(profile);
+    }
+    return *dev;
+  }
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+struct MatchHolder {
+  mq_match_result pub;  // first member: the pointer handed out
+  HostMatch data;
+};
+struct MsgHolder {
+  mq_msg_result pub;
+  std::vector<uint64_t> base;
+  std::vector<uint32_t> count;
+  std::vector<uint64_t> handles;
+};
+std::mutex g_res_mu;
+std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+template <class F>
+int guarded(mq_index* idx, F&& f) {
+  if (!idx) return fail(MQ_EINVAL, "null index");
+  try {
+    std::lock_guard<std::mutex> lk(idx->mu);
+    return f();
+  } catch (const HipError& e) {
+    return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
+  } catch (const std::bad_alloc&) {
+    return fail(MQ_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(MQ_EIO, e.what());
+  }
+}
+
+bool bad_str(const void* p, uint32_t len) { return p == nullptr && len != 0; }
+
+}  // namespace
+
+extern "C" {
+
+uint32_t mq_abi_version(void) { return MQ_ABI_VERSION; }
+const char* mq_last_error(void) { return g_err.c_str(); }
+
+int mq_index_create(const mq_config* cfg, mq_index** out) {
+  if (!out) return fail(MQ_EINVAL, "null out");
+  try {
+    mq_index* idx = new mq_index();
+    idx->cfg = cfg ? *cfg : mq_config{0, 0, 0, 0};
+    idx->ix.reset(new Index(idx->cfg.expected_subs, idx->cfg.expected_nodes));
+    *out = idx;
+    return 0;
+  } catch (const std::bad_alloc&) {
+    return fail(MQ_ENOMEM, "out of host memory");
+  }
+}
+
+void mq_index_destroy(mq_index* idx) { delete idx; }
+
+int mq_subscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t client_id,
+                 uint32_t filter_id, uint8_t qos, uint8_t flags, int32_t identifier) {
+  if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
+  if (qos > 2) return fail(MQ_EINVAL, "qos > 2");
+  return guarded(idx, [&] {
+    return idx->ix->subscribe(std::string_view(filter, flen), client_id, filter_id, qos, flags, identifier);
+  });
+}
+
+int mq_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t client_id) {
+  if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
+  return guarded(idx, [&] { return idx->ix->unsubscribe(std::string_view(filter, flen), client_id); });
+}
+
+int mq_inline_subscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier,
+                        uint32_t filter_id) {
+  if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
+  return guarded(idx, [&] {
+    return idx->ix->inline_subscribe(std::string_view(filter, flen), identifier, filter_id);
+  });
+}
+
+int mq_inline_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier) {
+  if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
+  return guarded(idx, [&] { return idx->ix->inline_unsubscribe(std::string_view(filter, flen), identifier); });
+}
+
+int mq_retain_message(mq_index* idx, const char* topic, uint32_t tlen, uint64_t handle,
+                      uint32_t payload_len, uint8_t retain, int64_t* out) {
+  if (bad_str(topic, tlen)) return fail(MQ_EINVAL, "null topic");
+  return guarded(idx, [&] {
+    int64_t r = idx->ix->retain_message(std::string_view(topic, tlen), handle, payload_len, retain != 0);
+    if (out) *out = r;
+    return 0;
+  });
+}
+
+int mq_retained_delete(mq_index* idx, const char* topic, uint32_t tlen) {
+  if (bad_str(topic, tlen)) return fail(MQ_EINVAL, "null topic");
+  return guarded(idx, [&] { return idx->ix->retained_delete(std::string_view(topic, tlen)); });
+}
+
+uint64_t mq_retained_len(const mq_index* idx) {
+  if (!idx) return 0;
+  std::lock_guard<std::mutex> lk(const_cast<mq_index*>(idx)->mu);
+  return idx->ix->retained_len();
+}
+
+int mq_subscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint32_t* client_ids,
+                      const uint32_t* filter_ids, const uint8_t* qos, const uint8_t* flags,
+                      const int32_t* identifiers, uint64_t n, uint8_t* out_new) {
+  if (n && (!bytes || !offs || !client_ids || !filter_ids || !qos || !flags || !identifiers))
+    return fail(MQ_EINVAL, "null column");
+  return guarded(idx, [&] {
+    for (uint64_t i = 0; i < n; i++) {
+      if (qos[i] > 2) return fail(MQ_EINVAL, "qos > 2");
+      int r = idx->ix->subscribe(std::string_view((const char*)bytes + offs[i], offs[i + 1] - offs[i]),
+                                 client_ids[i], filter_ids[i], qos[i], flags[i], identifiers[i]);
+      if (out_new) out_new[i] = (uint8_t)r;
+    }
+    return 0;
+  });
+}
+
+int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint64_t* handles,
+                   uint64_t n) {
+  if (n && (!bytes || !offs || !handles)) return fail(MQ_EINVAL, "null column");
+  return guarded(idx, [&] {
+    for (uint64_t i = 0; i < n; i++)
+      idx->ix->retain_message(std::string_view((const char*)bytes + offs[i], offs[i + 1] - offs[i]),
+                              handles[i], 1, true);
+    return 0;
+  });
+}
+
+int mq_match_batch(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_match_result** out) {
+  if (!out || (n && (!to || (!tb && to[n] != 0)))) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    Device& d = idx->device();
+    std::unique_ptr<MatchHolder> h(new MatchHolder());
+    const uint8_t* dtb = nullptr;
+    const uint64_t* dto = nullptr;
+    mq_match_result dev_out;
+    if (n) d.stage_inputs(tb, to, n, nullptr, &dtb, &dto);
+    d.match(*idx->ix, dtb, dto, n, nullptr, &h->data, &dev_out);
+    hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    mq_match_result& r = h->pub;
+    r = mq_match_result{};
+    r.n_topics = n;
+    r.topics = h->data.topics.data();
+    r.sub_rows = reinterpret_cast<const mq_client_row*>(h->data.rows.data());
+    r.shared_rows = reinterpret_cast<const mq_shared_row*>(h->data.shr.data());
+    r.inline_rows = reinterpret_cast<const mq_inline_row*>(h->data.inl.data());
+    r.n_sub_rows = h->data.rows.size();
+    r.n_shared_rows = h->data.shr.size();
+    r.n_inline_rows = h->data.inl.size();
+    *out = &h->pub;
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    g_results[&h->pub] = 1;
+    h.release();
+    return 0;
+  });
+}
+
+int mq_match_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
+                    mq_match_result* out) {
+  if (!out || (n && !d_to)) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    idx->device().match(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, nullptr, out);
+    return 0;
+  });
+}
+
+uint32_t mq_match_chunks(const mq_index* idx) {
+  return idx && idx->dev ? idx->dev->last_chunks() : 0;
+}
+
+int mq_messages_batch(mq_index* idx, const uint8_t*, const uint64_t*, uint32_t, mq_msg_result** out) {
+  (void)idx;
+  if (out) *out = nullptr;
+  return fail(MQ_EINVAL, "mq_messages_batch: not implemented yet");
+}
+
+int mq_messages_device(mq_index* idx, const uint8_t*, const uint64_t*, uint32_t, void*, mq_msg_result* out) {
+  (void)idx;
+  (void)out;
+  return fail(MQ_EINVAL, "mq_messages_device: not implemented yet");
+}
+
+void mq_result_free(void* r) {
+  if (!r) return;
+  int kind = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    auto it = g_results.find(r);
+    if (it == g_results.end()) return;
+    kind = it->second;
+    g_results.erase(it);
+  }
+  if (kind == 1) delete reinterpret_cast<MatchHolder*>(r);
+  if (kind == 2) delete reinterpret_cast<MsgHolder*>(r);
+}
+
+int mq_sync(mq_index* idx, void* stream) {
+  return guarded(idx, [&] {
+    idx->device().sync(*idx->ix, (hipStream_t)stream);
+    return 0;
+  });
+}
+
+int mq_index_stats(const mq_index* cidx, mq_stats* out) {
+  mq_index* idx = const_cast<mq_index*>(cidx);
+  if (!out) return fail(MQ_EINVAL, "null out");
+  return guarded(idx, [&] {
+    const Index& x = *idx->ix;
+    *out = mq_stats{};
+    out->nodes = x.n_nodes();
+    out->edges = x.n_edges();
+    out->edge_capacity = x.edges.size();
+    out->subs = x.subs.live;
+    out->subs_merge = x.n_subs_merge();
+    out->shared = x.shr.live;
+    out->inlines = x.inl.live;
+    out->retained = x.retained_len();
+    out->max_depth = x.max_depth();
+    if (idx->dev) {
+      out->device_bytes = idx->dev->device_bytes();
+      out->upload_bytes_total = idx->dev->upload_bytes();
+      out->syncs = idx->dev->syncs();
+    }
+    return 0;
+  });
+}
+
+int mq_profile_enable(mq_index* idx, int enable) {
+  return guarded(idx, [&] {
+    idx->profile = enable != 0;
+    if (idx->dev) idx->dev->prof.enable(idx->profile);
+    return 0;
+  });
+}
+
+int mq_profile_read(const mq_index* cidx, mq_kernel_time* out, uint32_t cap) {
+  mq_index* idx = const_cast<mq_index*>(cidx);
+  return guarded(idx, [&] { return idx->dev ? idx->dev->prof.read(out, cap) : 0; });
+}
+
+int mq_profile_reset(mq_index* idx) {
+  return guarded(idx, [&] {
+    if (idx->dev) idx->dev->prof.reset();
+    return 0;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,364 @@
+// Device side of the engine (device.h): HBM mirror + batch pipeline.
+#include "device.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+namespace mq {
+
+void hip_check(hipError_t e, const char* where) {
+  if (e != hipSuccess) throw HipError{e, std::string(where) + ": " + hipGetErrorString(e)};
+}
+
+void DevBuf::ensure(size_t b) {
+  if (b <= bytes && p) return;
+  release();
+  size_t nb = std::max<size_t>(b, 256);
+  hip_check(hipMalloc(&p, nb), "hipMalloc");
+  bytes = nb;
+}
+
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+template <class T>
+void DevMirror<T>::release() {
+  if (d) (void)hipFree(d);
+  d = nullptr;
+  cap = 0;
+}
+
+template <class T>
+void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded) {
+  const size_t n = m.size();
+  bool full = m.all_dirty;
+  if (!d || m.epoch != epoch || cap < n) {
+    release();
+    cap = std::max<size_t>(std::max(m.h.capacity(), n), 1);
+    hip_check(hipMalloc(&d, cap * sizeof(T)), "hipMalloc(mirror)");
+    epoch = m.epoch;
+    full = true;
+  }
+  if (full) {
+    if (n) hip_check(hipMemcpyAsync(d, m.h.data(), n * sizeof(T), hipMemcpyHostToDevice, s), "H2D mirror");
+    *uploaded += n * sizeof(T);
+  } else {
+    const size_t pp = Mirror<T>::per_page();
+    const size_t npages = (n + pp - 1) / pp;
+    size_t p = 0;
+    while (p < npages) {
+      if (!(p / 64 < m.dirty.size() && (m.dirty[p / 64] >> (p % 64)) & 1)) {
+        p++;
+        continue;
+      }
+      size_t q = p;
+      while (q < npages && q / 64 < m.dirty.size() && ((m.dirty[q / 64] >> (q % 64)) & 1)) q++;
+      const size_t a = p * pp, b = std::min(n, q * pp);
+      hip_check(hipMemcpyAsync(d + a, m.h.data() + a, (b - a) * sizeof(T), hipMemcpyHostToDevice, s),
+                "H2D dirty pages");
+      *uploaded += (b - a) * sizeof(T);
+      p = q;
+    }
+  }
+  m.clear_dirty();
+}
+
+// ---- profiler ----------------------------------------------------------------------------------
+void Profiler::begin(hipStream_t s) {
+  if (!on_) return;
+  if (free_.empty()) {
+    hipEvent_t e;
+    hip_check(hipEventCreate(&e), "hipEventCreate");
+    free_.push_back(e);
+  }
+  cur_ = free_.back();
+  free_.pop_back();
+  hip_check(hipEventRecord(cur_, s), "hipEventRecord");
+}
+
+void Profiler::end(const char* name, hipStream_t s) {
+  if (!on_ || !cur_) return;
+  if (free_.empty()) {
+    hipEvent_t e;
+    hip_check(hipEventCreate(&e), "hipEventCreate");
+    free_.push_back(e);
+  }
+  hipEvent_t b = free_.back();
+  free_.pop_back();
+  hip_check(hipEventRecord(b, s), "hipEventRecord");
+  pending_.push_back(Pending{name, cur_, b});
+  cur_ = nullptr;
+  if (pending_.size() > 4096) drain();
+}
+
+void Profiler::drain() {
+  for (auto& p : pending_) {
+    hip_check(hipEventSynchronize(p.b), "hipEventSynchronize");
+    float ms = 0;
+    hip_check(hipEventElapsedTime(&ms, p.a, p.b), "hipEventElapsedTime");
+    auto it = std::find_if(totals_.begin(), totals_.end(), [&](const Total& t) { return t.name == p.name; });
+    if (it == totals_.end()) {
+      totals_.push_back(Total{p.name, 0, 0});
+      it = totals_.end() - 1;
+    }
+    it->launches++;
+    it->ms += ms;
+    free_.push_back(p.a);
+    free_.push_back(p.b);
+  }
+  pending_.clear();
+}
+
+int Profiler::read(mq_kernel_time* out, uint32_t cap) {
+  drain();
+  uint32_t n = 0;
+  for (auto& t : totals_) {
+    if (n >= cap) break;
+    memset(&out[n], 0, sizeof(out[n]));
+    strncpy(out[n].name, t.name.c_str(), sizeof(out[n].name) - 1);
+    out[n].launches = t.launches;
+    out[n].total_ms = t.ms;
+    n++;
+  }
+  return (int)n;
+}
+
+void Profiler::reset() {
+  drain();
+  totals_.clear();
+}
+
+// ---- device --------------------------------------------------------------------------------------
+Device::Device(int dev) : dev_(dev) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  const char* e = getenv("MQ_CHUNK_ROWS");
+  chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : (256ull << 20);  // 4 GiB of 16-B rows
+}
+
+Device::~Device() {
+  (void)hipSetDevice(dev_);
+  edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
+  segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
+  for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
+                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_})
+    b->release();
+}
+
+uint64_t Device::device_bytes() const {
+  uint64_t b = edges_.cap * sizeof(EdgeSlot) + walk_.cap * sizeof(NodeWalk) +
+               lists_.cap * sizeof(NodeLists) + msg_.cap * sizeof(NodeMsg) +
+               seginfo_.cap * sizeof(SegInfo) + segbytes_.cap + subs_.cap * sizeof(SubRec) +
+               shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4;
+  for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
+                          &shr_rows_, &inl_rows_, &tab_, &res_})
+    b += x->bytes;
+  return b;
+}
+
+void Device::sync(Index& ix, hipStream_t s) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  if (ix.version() == synced_version_ && edges_.d) return;
+  edges_.sync(ix.edges, s, &uploaded_);
+  walk_.sync(ix.walk, s, &uploaded_);
+  lists_.sync(ix.lists, s, &uploaded_);
+  msg_.sync(ix.msg, s, &uploaded_);
+  seginfo_.sync(ix.seginfo, s, &uploaded_);
+  segbytes_.sync(ix.segbytes, s, &uploaded_);
+  subs_.sync(ix.subs.m, s, &uploaded_);
+  shr_.sync(ix.shr.m, s, &uploaded_);
+  inl_.sync(ix.inl.m, s, &uploaded_);
+  children_.sync(ix.children.m, s, &uploaded_);
+  retained_len_ = ix.retained_len();
+  empty_live_ = ix.empty_topic_live;
+  empty_handle_ = ix.empty_topic_handle;
+  synced_version_ = ix.version();
+  syncs_++;
+}
+
+DevIndex Device::dev_index(const Index& ix) const {
+  DevIndex d;
+  d.edges = edges_.d;
+  d.edge_mask = ix.edge_mask();
+  d.walk = walk_.d;
+  d.lists = lists_.d;
+  d.msg = msg_.d;
+  d.seginfo = seginfo_.d;
+  d.segbytes = segbytes_.d;
+  d.subs = subs_.d;
+  d.shr = shr_.d;
+  d.inl = inl_.d;
+  d.children = children_.d;
+  d.retained_len = retained_len_;
+  d.empty_topic_handle = empty_handle_;
+  d.empty_topic_live = empty_live_ ? 1u : 0u;
+  d.pad = 0;
+  d.err = err_.as<uint32_t>();
+  return d;
+}
+
+void Device::check_err(hipStream_t s) {
+  uint32_t e = 0;
+  hip_check(hipMemcpyAsync(&e, err_.p, sizeof(e), hipMemcpyDeviceToHost, s), "D2H err");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (e) {
+    hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
+    throw HipError{hipErrorUnknown, std::string("device guard tripped: ") +
+                                        ((e & kErrWalkGuard) ? "walk iteration bound " : "") +
+                                        ((e & kErrTableFull) ? "merge table full" : "")};
+  }
+}
+
+void Device::stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hipStream_t s,
+                          const uint8_t** d_tb, const uint64_t** d_to) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  const uint64_t nbytes = to[n];
+  in_bytes_.ensure(nbytes + 16);
+  in_offs_.ensure((n + 1) * sizeof(uint64_t));
+  if (nbytes) hip_check(hipMemcpyAsync(in_bytes_.p, tb, nbytes, hipMemcpyHostToDevice, s), "H2D topics");
+  hip_check(hipMemcpyAsync(in_offs_.p, to, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s),
+            "H2D offsets");
+  *d_tb = in_bytes_.as<uint8_t>();
+  *d_to = in_offs_.as<uint64_t>();
+}
+
+void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+                   HostMatch* host, mq_match_result* out) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  sync(ix, s);
+  memset(out, 0, sizeof(*out));
+  last_chunks_ = 0;
+  if (host) *host = HostMatch{};
+  if (!err_.p) {
+    err_.ensure(sizeof(uint32_t));
+    hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
+  }
+  check_err(s);  // faults flagged by the previous batch's kernels
+  if (n == 0) return;
+  const DevIndex di = dev_index(ix);
+  const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+
+  counts_.ensure((size_t)n * sizeof(TopicCount));
+  offs_.ensure((size_t)(n + 1) * sizeof(TopicOff));
+  bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+  bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+
+  prof.begin(s);
+  launch_walk(false, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, nullptr, s);
+  prof.end("walk_count", s);
+  hip_check(hipGetLastError(), "k_walk<count>");
+  prof.begin(s);
+  launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
+  prof.end("scan", s);
+  hip_check(hipGetLastError(), "k_scan");
+
+  h_bpre_.resize(nb + 1);
+  hip_check(hipMemcpyAsync(h_bpre_.data(), bpre_.p, (nb + 1) * sizeof(TopicOff), hipMemcpyDeviceToHost, s),
+            "D2H block offsets");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  check_err(s);
+  const TopicOff tot = h_bpre_[nb];
+
+  gathers_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
+  prof.begin(s);
+  launch_walk(true, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), s);
+  prof.end("walk_fill", s);
+  hip_check(hipGetLastError(), "k_walk<fill>");
+
+  // plan output chunks on scan-block boundaries so each chunk's rows fit the budget
+  struct Chunk {
+    uint32_t b0, b1;
+  };
+  std::vector<Chunk> chunks;
+  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_tab = 1, max_topics = 1;
+  for (uint32_t b = 0; b < nb;) {
+    uint32_t e = b + 1;
+    while (e < nb && h_bpre_[e + 1].rows - h_bpre_[b].rows <= chunk_rows_budget_) e++;
+    chunks.push_back(Chunk{b, e});
+    max_rows = std::max(max_rows, h_bpre_[e].rows - h_bpre_[b].rows);
+    max_shr = std::max(max_shr, h_bpre_[e].shr - h_bpre_[b].shr);
+    max_inl = std::max(max_inl, h_bpre_[e].inl - h_bpre_[b].inl);
+    max_tab = std::max(max_tab, h_bpre_[e].tab - h_bpre_[b].tab);
+    max_topics = std::max<uint64_t>(max_topics, std::min<uint64_t>(n, (uint64_t)e * kScanBlock) - (uint64_t)b * kScanBlock);
+    b = e;
+  }
+  rows_.ensure(max_rows * sizeof(SubRec));
+  shr_rows_.ensure(max_shr * sizeof(ShrRec));
+  inl_rows_.ensure(max_inl * sizeof(InlRec));
+  tab_.ensure(max_tab * 3 * sizeof(uint32_t));
+  res_.ensure(max_topics * sizeof(mq_topic_result_dev));
+
+  if (host) {
+    host->topics.resize(n);
+    host->rows.resize(tot.rows);
+    host->shr.resize(tot.shr);
+    host->inl.resize(tot.inl);
+  }
+
+  std::vector<TopicOff> hoff;
+  for (const Chunk& c : chunks) {
+    EmitArgs a;
+    a.ix = di;
+    a.t0 = c.b0 * kScanBlock;
+    a.t1 = std::min<uint64_t>(n, (uint64_t)c.b1 * kScanBlock);
+    a.off = offs_.as<TopicOff>();
+    a.base = h_bpre_[c.b0];
+    a.gathers = gathers_.as<uint32_t>();
+    a.rows = rows_.as<SubRec>();
+    a.shr_rows = shr_rows_.as<ShrRec>();
+    a.inl_rows = inl_rows_.as<InlRec>();
+    a.tab = tab_.as<uint32_t>();
+    a.tab_cap = max_tab;
+    a.res = res_.as<mq_topic_result_dev>();
+    prof.begin(s);
+    launch_emit(a, s);
+    prof.end("emit", s);
+    hip_check(hipGetLastError(), "k_emit");
+    last_chunks_++;
+
+    const TopicOff& lo = h_bpre_[c.b0];
+    const TopicOff& hi = h_bpre_[c.b1];
+    const uint32_t nt = a.t1 - a.t0;
+    if (host) {
+      hip_check(hipMemcpyAsync(host->rows.data() + lo.rows, rows_.p, (hi.rows - lo.rows) * sizeof(SubRec),
+                               hipMemcpyDeviceToHost, s), "D2H rows");
+      hip_check(hipMemcpyAsync(host->shr.data() + lo.shr, shr_rows_.p, (hi.shr - lo.shr) * sizeof(ShrRec),
+                               hipMemcpyDeviceToHost, s), "D2H shared rows");
+      hip_check(hipMemcpyAsync(host->inl.data() + lo.inl, inl_rows_.p, (hi.inl - lo.inl) * sizeof(InlRec),
+                               hipMemcpyDeviceToHost, s), "D2H inline rows");
+      hip_check(hipMemcpyAsync(host->topics.data() + a.t0, res_.p, nt * sizeof(mq_topic_result),
+                               hipMemcpyDeviceToHost, s), "D2H topic results");
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      for (uint32_t i = 0; i < nt; i++) {
+        mq_topic_result& r = host->topics[a.t0 + i];
+        r.sub_base += lo.rows;
+        r.shared_base += lo.shr;
+        r.inline_base += lo.inl;
+      }
+    }
+    out->n_topics = nt;
+    out->topics = res_.as<mq_topic_result>();
+    out->sub_rows = rows_.as<mq_client_row>();
+    out->shared_rows = shr_rows_.as<mq_shared_row>();
+    out->inline_rows = inl_rows_.as<mq_inline_row>();
+    out->n_sub_rows = hi.rows - lo.rows;
+    out->n_shared_rows = hi.shr - lo.shr;
+    out->n_inline_rows = hi.inl - lo.inl;
+  }
+}
+
+template struct DevMirror<EdgeSlot>;
+template struct DevMirror<NodeWalk>;
+template struct DevMirror<NodeLists>;
+template struct DevMirror<NodeMsg>;
+template struct DevMirror<SegInfo>;
+template struct DevMirror<uint8_t>;
+template struct DevMirror<SubRec>;
+template struct DevMirror<ShrRec>;
+template struct DevMirror<InlRec>;
+template struct DevMirror<uint32_t>;
+
+}  // namespace mq

@@ -1,0 +1,125 @@
+// Device side of the engine: the HBM-resident mirror of the index image and the batched match
+// pipeline (walk-count -> scan -> walk-fill -> emit per output chunk).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "index.h"
+#include "kernels.h"
+#include "mqmatch.h"
+
+namespace mq {
+
+struct HipError {
+  hipError_t code;
+  std::string where;
+};
+void hip_check(hipError_t e, const char* where);
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b);
+  void release();
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+template <class T>
+struct DevMirror {
+  T* d = nullptr;
+  size_t cap = 0;
+  uint64_t epoch = ~0ull;
+  void sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded);
+  void release();
+};
+
+// Host-side destination of a batch's results (mq_match_batch).
+struct HostMatch {
+  std::vector<mq_topic_result> topics;
+  std::vector<SubRec> rows;
+  std::vector<ShrRec> shr;
+  std::vector<InlRec> inl;
+};
+
+class Profiler {
+ public:
+  void enable(bool on) { on_ = on; }
+  bool on() const { return on_; }
+  void begin(hipStream_t s);
+  void end(const char* name, hipStream_t s);
+  int read(mq_kernel_time* out, uint32_t cap);
+  void reset();
+
+ private:
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  struct Total {
+    std::string name;
+    uint64_t launches = 0;
+    double ms = 0;
+  };
+  void drain();
+  bool on_ = false;
+  hipEvent_t cur_ = nullptr;
+  std::vector<Pending> pending_;
+  std::vector<hipEvent_t> free_;
+  std::vector<Total> totals_;
+};
+
+class Device {
+ public:
+  explicit Device(int dev);
+  ~Device();
+  int device() const { return dev_; }
+
+  // Upload dirty pages of the index image (incremental device-side update).
+  void sync(Index& ix, hipStream_t s);
+  // Match n topics resident on the device. Fills `out` with device pointers of the last chunk;
+  // when `host` is set every chunk's rows are also copied into it (global offsets).
+  void match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+             HostMatch* host, mq_match_result* out);
+  // Copy host topics to the device input buffers and return their device pointers.
+  void stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hipStream_t s,
+                    const uint8_t** d_tb, const uint64_t** d_to);
+
+  uint32_t last_chunks() const { return last_chunks_; }
+  uint64_t device_bytes() const;
+  uint64_t upload_bytes() const { return uploaded_; }
+  uint64_t syncs() const { return syncs_; }
+  Profiler prof;
+
+ private:
+  DevIndex dev_index(const Index& ix) const;
+  void check_err(hipStream_t s);
+
+  int dev_;
+  uint64_t synced_version_ = ~0ull;
+  uint64_t uploaded_ = 0, syncs_ = 0;
+  uint32_t last_chunks_ = 0;
+  uint64_t chunk_rows_budget_;
+  DevMirror<EdgeSlot> edges_;
+  DevMirror<NodeWalk> walk_;
+  DevMirror<NodeLists> lists_;
+  DevMirror<NodeMsg> msg_;
+  DevMirror<SegInfo> seginfo_;
+  DevMirror<uint8_t> segbytes_;
+  DevMirror<SubRec> subs_;
+  DevMirror<ShrRec> shr_;
+  DevMirror<InlRec> inl_;
+  DevMirror<uint32_t> children_;
+  DevBuf in_bytes_, in_offs_;
+  DevBuf counts_, offs_, bsum_, bpre_, gathers_;
+  DevBuf rows_, shr_rows_, inl_rows_, tab_, res_, err_;
+  std::vector<TopicOff> h_bpre_;
+  uint64_t retained_len_ = 0;
+  uint64_t empty_handle_ = 0;
+  bool empty_live_ = false;
+};
+
+}  // namespace mq

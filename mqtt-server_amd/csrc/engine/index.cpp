@@ -1,0 +1,703 @@
+// Host side of the engine: incremental updates of the flat trie image (index.h).
+// Each public operation restates the reference semantics it replaces (topics.go:368-522).
+#include "index.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace mq {
+
+// ---- HashU64 ------------------------------------------------------------------------------------
+void HashU64::rehash(size_t cap) {
+  size_t c = 16;
+  while (c < cap) c <<= 1;
+  std::vector<uint64_t> ok;
+  std::vector<uint32_t> ov;
+  ok.swap(keys_);
+  ov.swap(vals_);
+  keys_.assign(c, kEmpty);
+  vals_.assign(c, 0);
+  n_ = tombs_ = 0;
+  for (size_t i = 0; i < ok.size(); i++)
+    if (ok[i] != kEmpty && ok[i] != kTomb) put(ok[i], ov[i]);
+}
+
+bool HashU64::get(uint64_t k, uint32_t* v) const {
+  size_t m = keys_.size() - 1, i = slot(k);
+  for (;;) {
+    uint64_t x = keys_[i];
+    if (x == kEmpty) return false;
+    if (x == k) {
+      *v = vals_[i];
+      return true;
+    }
+    i = (i + 1) & m;
+  }
+}
+
+void HashU64::put(uint64_t k, uint32_t v) {
+  if ((n_ + tombs_ + 1) * 2 > keys_.size()) rehash(n_ * 4 > keys_.size() ? keys_.size() * 2 : keys_.size());
+  size_t m = keys_.size() - 1, i = slot(k), tomb = SIZE_MAX;
+  for (;;) {
+    uint64_t x = keys_[i];
+    if (x == k) {
+      vals_[i] = v;
+      return;
+    }
+    if (x == kTomb && tomb == SIZE_MAX) tomb = i;
+    if (x == kEmpty) {
+      if (tomb != SIZE_MAX) {
+        i = tomb;
+        tombs_--;
+      }
+      keys_[i] = k;
+      vals_[i] = v;
+      n_++;
+      return;
+    }
+    i = (i + 1) & m;
+  }
+}
+
+bool HashU64::erase(uint64_t k) {
+  size_t m = keys_.size() - 1, i = slot(k);
+  for (;;) {
+    uint64_t x = keys_[i];
+    if (x == kEmpty) return false;
+    if (x == k) {
+      keys_[i] = kTomb;
+      n_--;
+      tombs_++;
+      return true;
+    }
+    i = (i + 1) & m;
+  }
+}
+
+// ---- string helpers -------------------------------------------------------------------------
+
+// strings.EqualFold(s, "$SHARE") (topics.go:407, Q9). Go decodes s rune by rune (invalid
+// bytes become U+FFFD); under unicode.SimpleFold the runes equal to the ASCII target are the
+// ASCII letter in either case, plus U+017F (LATIN SMALL LETTER LONG S, UTF-8 C5 BF) for 'S'.
+bool is_share_prefix(std::string_view s) {
+  static const char* up = "$SHARE";
+  size_t i = 0;
+  for (int j = 0; j < 6; j++) {
+    if (i >= s.size()) return false;
+    unsigned char c = (unsigned char)s[i];
+    if (c == 0xC5 && i + 1 < s.size() && (unsigned char)s[i + 1] == 0xBF) {  // U+017F
+      if (up[j] != 'S') return false;
+      i += 2;
+      continue;
+    }
+    if (c >= 0x80) return false;
+    unsigned char lc = (c >= 'A' && c <= 'Z') ? (unsigned char)(c + 32) : c;
+    unsigned char lt = (up[j] >= 'A' && up[j] <= 'Z') ? (unsigned char)(up[j] + 32) : (unsigned char)up[j];
+    if (lc != lt) return false;
+    i++;
+  }
+  return i == s.size();
+}
+
+// isolateParticle(filter, d) for every d from `d` on (topics.go:679-698): the segments
+// from index d, or — when d is past the last '/' — the last segment alone.
+void Index::path_of(std::string_view filter, int d, std::vector<std::string_view>& out) {
+  out.clear();
+  std::vector<std::string_view> segs;
+  size_t s = 0;
+  for (;;) {
+    size_t e = filter.find('/', s);
+    if (e == std::string_view::npos) {
+      segs.push_back(filter.substr(s));
+      break;
+    }
+    segs.push_back(filter.substr(s, e - s));
+    s = e + 1;
+  }
+  if ((size_t)d < segs.size())
+    out.assign(segs.begin() + d, segs.end());
+  else
+    out.push_back(segs.back());
+}
+
+static std::string_view segment_at(std::string_view filter, int d) {  // isolateParticle value
+  size_t s = 0;
+  for (int i = 0;; i++) {
+    size_t e = filter.find('/', s);
+    if (e == std::string_view::npos) return filter.substr(s);
+    if (i == d) return filter.substr(s, e - s);
+    s = e + 1;
+  }
+}
+
+uint32_t Index::intern_str(std::string_view s) {
+  auto it = str_ids_.find(std::string(s));
+  if (it != str_ids_.end()) return it->second;
+  uint32_t id = (uint32_t)strs_.size();
+  strs_.emplace_back(s);
+  str_ids_.emplace(std::string(s), id);
+  return id;
+}
+
+// ---- construction ----------------------------------------------------------------------------
+Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
+  intern_str("+");
+  intern_str("#");
+  size_t cap = 1024;
+  uint64_t want = expected_nodes ? expected_nodes : expected_subs * 3;
+  while (cap < want * 2) cap <<= 1;
+  edges.h.assign(cap, EdgeSlot{0, 0, kEdgeEmpty, kNone, 0, 0});
+  edges.epoch++;
+  if (want) {
+    walk.h.reserve(want);
+    lists.h.reserve(want);
+    msg.h.reserve(want);
+    nh_.reserve(want);
+    sub_pos_.reserve(expected_subs);
+    subs.m.h.reserve(expected_subs + expected_subs / 2);
+  }
+  // root particle (topics.go:359-362)
+  nh_.push_back(NodeHost{});
+  nh_[0].live = true;
+  walk.grow_to(1, NodeWalk{kNone, kNone, kParentMask, kNone});
+  lists.grow_to(1, NodeLists{});
+  msg.grow_to(1, NodeMsg{});
+  seginfo.grow_to(1, SegInfo{0, 0});
+  segbytes.grow_to(1, 0);
+}
+
+// ---- edge table -------------------------------------------------------------------------------
+uint32_t Index::find_child(uint32_t parent, const SegKey& k, std::string_view seg) const {
+  const uint64_t m = edges.size() - 1;
+  uint64_t i = edge_hash(parent, k) & m;
+  for (;;) {
+    const EdgeSlot& e = edges.h[i];
+    if (e.parent == kEdgeEmpty) return kNone;
+    if (e.parent == parent && e.k0 == k.k0 && e.k1 == k.k1) {
+      if (!seg_is_long(k)) return e.child;
+      const SegInfo& si = seginfo.h[walk.h[e.child].seg];
+      if (si.len == seg.size() && memcmp(&segbytes.h[si.off], seg.data(), si.len) == 0) return e.child;
+    }
+    i = (i + 1) & m;
+  }
+}
+
+void Index::edge_rehash(size_t cap) {
+  std::vector<EdgeSlot> old;
+  old.swap(edges.h);
+  edges.h.assign(cap, EdgeSlot{0, 0, kEdgeEmpty, kNone, 0, 0});
+  edges.epoch++;
+  edges.all_dirty = true;
+  n_edges_ = n_tombs_ = 0;
+  for (const EdgeSlot& e : old)
+    if (e.parent != kEdgeEmpty && e.parent != kEdgeTomb) edge_insert(e.parent, SegKey{e.k0, e.k1}, e.child);
+}
+
+void Index::edge_insert(uint32_t parent, const SegKey& k, uint32_t child) {
+  if ((n_edges_ + n_tombs_ + 1) * 2 > edges.size())
+    edge_rehash(n_edges_ * 4 > edges.size() ? edges.size() * 2 : edges.size());
+  const uint64_t m = edges.size() - 1;
+  uint64_t i = edge_hash(parent, k) & m;
+  for (;;) {
+    EdgeSlot& e = edges.h[i];
+    if (e.parent == kEdgeEmpty || e.parent == kEdgeTomb) {
+      if (e.parent == kEdgeTomb) n_tombs_--;
+      e = EdgeSlot{k.k0, k.k1, parent, child, 0, 0};
+      edges.mark(i);
+      n_edges_++;
+      return;
+    }
+    i = (i + 1) & m;
+  }
+}
+
+void Index::edge_erase(uint32_t parent, const SegKey& k, uint32_t child) {
+  const uint64_t m = edges.size() - 1;
+  uint64_t i = edge_hash(parent, k) & m;
+  for (;;) {
+    EdgeSlot& e = edges.h[i];
+    if (e.parent == kEdgeEmpty) return;
+    if (e.parent == parent && e.child == child) {
+      e.parent = kEdgeTomb;
+      edges.mark(i);
+      n_edges_--;
+      n_tombs_++;
+      return;
+    }
+    i = (i + 1) & m;
+  }
+}
+
+// ---- nodes ---------------------------------------------------------------------------------------
+template <class T, class Rec>
+void Index::list_push(SlabPool<T>& pool, uint32_t& off, uint32_t& cnt, uint32_t& cap, const Rec& r) {
+  if (cnt + 1 > cap) {
+    uint32_t nc = cap ? cap * 2 : 1;
+    uint32_t no = pool.alloc(nc);
+    for (uint32_t i = 0; i < cnt; i++) pool.m.at_w(no + i) = pool.m.h[off + i];
+    pool.release(off, cap);
+    off = no;
+    cap = nc;
+  }
+  pool.m.at_w(off + cnt) = r;
+  cnt++;
+  pool.live++;
+}
+
+uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k) {
+  uint32_t id;
+  if (!free_nodes_.empty()) {
+    id = free_nodes_.back();
+    free_nodes_.pop_back();
+  } else {
+    id = (uint32_t)nh_.size();
+    nh_.push_back(NodeHost{});
+    walk.grow_to(id + 1, NodeWalk{kNone, kNone, 0, kNone});
+    lists.grow_to(id + 1, NodeLists{});
+    msg.grow_to(id + 1, NodeMsg{});
+  }
+  NodeHost& h = nh_[id];
+  h = NodeHost{};
+  h.key = k;
+  h.str = intern_str(seg);
+  h.depth = (uint16_t)(nh_[parent].depth + 1);
+  h.live = true;
+  max_depth_ = std::max<uint32_t>(max_depth_, h.depth);
+
+  uint32_t flags = 0;
+  if (h.str == 0) flags |= kFlagPlusKey;
+  if (parent == kRoot) {
+    if (!seg.empty() && (seg[0] == '+' || seg[0] == '#')) flags |= kFlagSeg0Wild;
+  } else {
+    flags |= walk.h[parent].parent_flags & kFlagSeg0Wild;
+  }
+  uint32_t segref = kNone;
+  if (seg_is_long(k)) {
+    auto it = long_segs_.find(std::string(seg));
+    if (it == long_segs_.end()) {
+      segref = (uint32_t)seginfo.size();
+      uint32_t off = (uint32_t)segbytes.size();
+      segbytes.grow_to(off + seg.size(), 0);
+      memcpy(&segbytes.h[off], seg.data(), seg.size());
+      seginfo.grow_to(segref + 1, SegInfo{off, (uint32_t)seg.size()});
+      long_segs_.emplace(std::string(seg), segref);
+    } else {
+      segref = it->second;
+    }
+  }
+  walk.at_w(id) = NodeWalk{kNone, kNone, parent | flags, segref};
+  NodeLists L{};
+  L.flags = flags & kFlagSeg0Wild;
+  lists.at_w(id) = L;
+  NodeMsg M{};
+  M.depth = h.depth;
+  M.key_sys = (parent == kRoot && seg == "$SYS") ? 1u : 0u;
+  msg.at_w(id) = M;
+
+  edge_insert(parent, k, id);
+  if (h.str == 0) walk.at_w(parent).plus_child = id;
+  if (h.str == 1) walk.at_w(parent).hash_child = id;
+  NodeMsg& pm = msg.at_w(parent);
+  h.child_pos = pm.child_cnt;
+  list_push(children, pm.child_off, pm.child_cnt, nh_[parent].child_cap, id);
+  nh_[parent].n_children++;
+  n_live_nodes_++;
+  return id;
+}
+
+void Index::remove_node(uint32_t n) {
+  NodeHost& h = nh_[n];
+  uint32_t p = walk.h[n].parent_flags & kParentMask;
+  edge_erase(p, h.key, n);
+  if (h.str == 0) walk.at_w(p).plus_child = kNone;
+  if (h.str == 1) walk.at_w(p).hash_child = kNone;
+  NodeMsg& pm = msg.at_w(p);
+  uint32_t last = children.m.h[pm.child_off + pm.child_cnt - 1];
+  children.m.at_w(pm.child_off + h.child_pos) = last;
+  nh_[last].child_pos = h.child_pos;
+  pm.child_cnt--;
+  children.live--;
+  nh_[p].n_children--;
+  // release the node's (empty) slabs
+  subs.release(lists.h[n].sub_off, h.sub_cap);
+  shr.release(lists.h[n].shr_off, h.shr_cap);
+  inl.release(lists.h[n].inl_off, h.inl_cap);
+  children.release(msg.h[n].child_off, h.child_cap);
+  walk.at_w(n) = NodeWalk{kNone, kNone, 0, kNone};
+  lists.at_w(n) = NodeLists{};
+  msg.at_w(n) = NodeMsg{};
+  h = NodeHost{};
+  free_nodes_.push_back(n);
+  n_live_nodes_--;
+}
+
+uint32_t Index::set(std::string_view filter, int d) {  // topics.go:479-496
+  std::vector<std::string_view> path;
+  path_of(filter, d, path);
+  uint32_t n = kRoot;
+  for (std::string_view seg : path) {
+    SegKey k = seg_key((const uint8_t*)seg.data(), (uint32_t)seg.size());
+    uint32_t c = find_child(n, k, seg);
+    if (c == kNone) c = new_node(n, seg, k);
+    n = c;
+  }
+  return n;
+}
+
+uint32_t Index::seek(std::string_view filter, int d) const {  // topics.go:499-513
+  std::vector<std::string_view> path;
+  path_of(filter, d, path);
+  uint32_t n = kRoot;
+  for (std::string_view seg : path) {
+    SegKey k = seg_key((const uint8_t*)seg.data(), (uint32_t)seg.size());
+    n = find_child(n, k, seg);
+    if (n == kNone) return kNone;
+  }
+  return n;
+}
+
+void Index::trim(uint32_t n) {  // topics.go:516-522
+  while (n != kRoot && !nh_[n].retain_path && nh_[n].n_children == 0 && sub_count(n) == 0 &&
+         lists.h[n].shr_cnt == 0 && lists.h[n].inl_cnt == 0) {
+    uint32_t p = walk.h[n].parent_flags & kParentMask;
+    remove_node(n);
+    n = p;
+  }
+}
+
+// ---- subscription lists ----------------------------------------------------------------------------
+void Index::sub_ensure(uint32_t n, uint32_t need) {
+  uint32_t cap = nh_[n].sub_cap;
+  if (need <= cap) return;
+  uint32_t nc = cap ? cap : 1;
+  while (nc < need) nc *= 2;
+  NodeLists& L = lists.at_w(n);
+  uint32_t no = subs.alloc(nc), cnt = L.n_direct + L.n_merge;
+  for (uint32_t i = 0; i < cnt; i++) {
+    const SubRec r = subs.m.h[L.sub_off + i];
+    subs.m.at_w(no + i) = r;
+    sub_pos_.put((uint64_t)n << 32 | r.client, no + i);
+  }
+  subs.release(L.sub_off, cap);
+  L.sub_off = no;
+  nh_[n].sub_cap = nc;
+}
+
+static inline void move_sub(SlabPool<SubRec>& subs, HashU64& pos, uint32_t n, uint32_t from, uint32_t to) {
+  const SubRec r = subs.m.h[from];
+  subs.m.at_w(to) = r;
+  pos.put((uint64_t)n << 32 | r.client, to);
+}
+
+uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
+  sub_ensure(n, sub_count(n) + 1);
+  NodeLists& L = lists.at_w(n);
+  uint32_t base = L.sub_off, pos;
+  if (merge) {
+    pos = base + L.n_direct + L.n_merge;
+    L.n_merge++;
+    n_merge_++;
+  } else {
+    pos = base + L.n_direct;
+    if (L.n_merge) move_sub(subs, sub_pos_, n, pos, base + L.n_direct + L.n_merge);
+    L.n_direct++;
+  }
+  subs.m.at_w(pos) = r;
+  sub_pos_.put((uint64_t)n << 32 | r.client, pos);
+  subs.live++;
+  return pos;
+}
+
+void Index::sub_remove(uint32_t n, uint32_t pos) {
+  NodeLists& L = lists.at_w(n);
+  uint32_t base = L.sub_off;
+  if (pos < base + L.n_direct) {
+    uint32_t last_d = base + L.n_direct - 1;
+    if (pos != last_d) move_sub(subs, sub_pos_, n, last_d, pos);
+    if (L.n_merge) move_sub(subs, sub_pos_, n, base + L.n_direct + L.n_merge - 1, last_d);
+    L.n_direct--;
+  } else {
+    uint32_t last = base + L.n_direct + L.n_merge - 1;
+    if (pos != last) move_sub(subs, sub_pos_, n, last, pos);
+    L.n_merge--;
+    n_merge_--;
+  }
+  subs.live--;
+}
+
+void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
+  NodeLists& L = lists.at_w(n);
+  uint32_t base = L.sub_off;
+  bool is_merge = pos >= base + L.n_direct;
+  if (merge == is_merge) return;
+  uint32_t other = merge ? base + L.n_direct - 1 : base + L.n_direct;
+  SubRec a = subs.m.h[pos], b = subs.m.h[other];
+  subs.m.at_w(pos) = b;
+  sub_pos_.put((uint64_t)n << 32 | b.client, pos);
+  if (merge) {
+    a.meta |= 0x1000u;
+    L.n_direct--;
+    L.n_merge++;
+    n_merge_++;
+  } else {
+    a.meta &= ~0x1000u;
+    L.n_direct++;
+    L.n_merge--;
+    n_merge_--;
+  }
+  subs.m.at_w(other) = a;
+  sub_pos_.put((uint64_t)n << 32 | a.client, other);
+}
+
+void Index::path_strs(uint32_t n, uint32_t* out, int* len) const {
+  int d = nh_[n].depth;
+  *len = d;
+  while (n != kRoot) {
+    out[--d] = nh_[n].str;
+    n = walk.h[n].parent_flags & kParentMask;
+  }
+}
+
+// Could one publish topic match both node paths a and b (A.2 rules A/B/C)? A sound
+// over-approximation: '#' matches any suffix (including none), '+' any one level, and a
+// path may be one level longer than the other only through a trailing '#'.
+bool Index::compatible(uint32_t a, uint32_t b) const {
+  thread_local std::vector<uint32_t> pa, pb;
+  pa.resize(nh_[a].depth);
+  pb.resize(nh_[b].depth);
+  int la, lb;
+  path_strs(a, pa.data(), &la);
+  path_strs(b, pb.data(), &lb);
+  int m = std::min(la, lb);
+  for (int i = 0; i < m; i++) {
+    uint32_t x = pa[i], y = pb[i];
+    if (x == 1 || y == 1) return true;  // '#'
+    if (x == 0 || y == 0) continue;     // '+'
+    if (x != y) return false;
+  }
+  if (la == lb) return true;
+  const std::vector<uint32_t>& lo = la > lb ? pa : pb;
+  int llo = std::max(la, lb);
+  return llo == m + 1 && lo[m] == 1;
+}
+
+void Index::refresh_merge_flag(uint32_t client, uint32_t node) {
+  auto it = client_nodes_.find(client);
+  bool merge = false;
+  if (it != client_nodes_.end())
+    for (uint32_t m : it->second)
+      if (m != node && compatible(node, m)) {
+        merge = true;
+        break;
+      }
+  uint32_t pos;
+  if (sub_pos_.get((uint64_t)node << 32 | client, &pos)) sub_set_merge(node, pos, merge);
+}
+
+// ---- TopicsIndex operations ----------------------------------------------------------------------
+
+// topics.go:401-419
+int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_id, uint8_t qos,
+                     uint8_t flags, int32_t ident) {
+  version_++;
+  if (is_share_prefix(segment_at(filter, 0))) {
+    std::string group(segment_at(filter, 1));
+    auto git = group_ids_.find(group);
+    uint32_t gid;
+    if (git == group_ids_.end()) {
+      gid = (uint32_t)group_ids_.size();
+      group_ids_.emplace(group, gid);
+    } else {
+      gid = git->second;
+    }
+    uint32_t n = set(filter, 2);
+    ShrKey key{n, gid, client};
+    auto it = shr_pos_.find(key);
+    ShrRec rec{filter_id, client};
+    if (it != shr_pos_.end()) {
+      shr.m.at_w(it->second) = rec;
+      return 0;
+    }
+    NodeLists& L = lists.at_w(n);
+    uint32_t old_off = L.shr_off, cnt = L.shr_cnt;
+    list_push(shr, L.shr_off, L.shr_cnt, nh_[n].shr_cap, rec);
+    if (shr_group_.size() < shr.m.size()) shr_group_.resize(shr.m.size());
+    if (L.shr_off != old_off) {  // slab moved: carry the group ids and re-point the records
+      for (uint32_t i = 0; i < cnt; i++) {
+        uint32_t g = shr_group_[old_off + i];
+        shr_group_[L.shr_off + i] = g;
+        shr_pos_[ShrKey{n, g, shr.m.h[L.shr_off + i].client}] = L.shr_off + i;
+      }
+    }
+    shr_pos_[key] = L.shr_off + cnt;
+    shr_group_[L.shr_off + cnt] = gid;
+    return 1;
+  }
+  uint32_t n = set(filter, 0);
+  SubRec rec{client, filter_id, ident,
+             (uint32_t)(qos & 3) | ((flags & 1) ? kMetaNoLocal : 0) | ((flags & 2) ? kMetaRap : 0) |
+                 ((uint32_t)((flags >> 2) & 3) << kMetaRhShift)};
+  uint32_t pos;
+  if (sub_pos_.get((uint64_t)n << 32 | client, &pos)) {
+    rec.meta |= subs.m.h[pos].meta & 0x1000u;
+    subs.m.at_w(pos) = rec;
+    return 0;
+  }
+  std::vector<uint32_t>& mine = client_nodes_[client];
+  bool merge = false;
+  for (uint32_t m : mine) {
+    if (!compatible(n, m)) continue;
+    merge = true;
+    uint32_t mp;
+    if (sub_pos_.get((uint64_t)m << 32 | client, &mp) && !sub_is_merge(mp)) sub_set_merge(m, mp, true);
+  }
+  if (merge) rec.meta |= 0x1000u;
+  sub_add(n, rec, merge);
+  mine.push_back(n);
+  return 1;
+}
+
+// topics.go:423-448
+int Index::unsubscribe(std::string_view filter, uint32_t client) {
+  version_++;
+  bool share = is_share_prefix(segment_at(filter, 0));
+  uint32_t n = seek(filter, share ? 2 : 0);
+  if (n == kNone) return 0;
+  if (share) {
+    auto git = group_ids_.find(std::string(segment_at(filter, 1)));
+    if (git != group_ids_.end()) {
+      auto it = shr_pos_.find(ShrKey{n, git->second, client});
+      if (it != shr_pos_.end()) {
+        NodeLists& L = lists.at_w(n);
+        uint32_t pos = it->second, last = L.shr_off + L.shr_cnt - 1;
+        shr_pos_.erase(it);
+        if (pos != last) {
+          shr.m.at_w(pos) = shr.m.h[last];
+          shr_group_[pos] = shr_group_[last];
+          shr_pos_[ShrKey{n, shr_group_[pos], shr.m.h[pos].client}] = pos;
+        }
+        L.shr_cnt--;
+        shr.live--;
+      }
+    }
+  } else {
+    uint32_t pos;
+    uint64_t key = (uint64_t)n << 32 | client;
+    if (sub_pos_.get(key, &pos)) {
+      bool was_merge = sub_is_merge(pos);
+      sub_remove(n, pos);
+      sub_pos_.erase(key);
+      auto cit = client_nodes_.find(client);
+      if (cit != client_nodes_.end()) {
+        auto& v = cit->second;
+        v.erase(std::find(v.begin(), v.end(), n));
+        if (was_merge) {
+          std::vector<uint32_t> others = v;
+          for (uint32_t m : others) {
+            uint32_t mp;
+            if (sub_pos_.get((uint64_t)m << 32 | client, &mp) && sub_is_merge(mp))
+              refresh_merge_flag(client, m);
+          }
+        }
+        if (v.empty()) client_nodes_.erase(cit);
+      }
+    }
+  }
+  trim(n);
+  return 1;
+}
+
+// topics.go:368-378
+int Index::inline_subscribe(std::string_view filter, int32_t ident, uint32_t filter_id) {
+  version_++;
+  uint32_t n = set(filter, 0);
+  uint64_t key = (uint64_t)n << 32 | (uint32_t)ident;
+  InlRec rec{ident, filter_id};
+  uint32_t pos;
+  if (inl_pos_.get(key, &pos)) {
+    inl.m.at_w(pos) = rec;
+    return 0;
+  }
+  NodeLists& L = lists.at_w(n);
+  uint32_t old_off = L.inl_off, cnt = L.inl_cnt;
+  list_push(inl, L.inl_off, L.inl_cnt, nh_[n].inl_cap, rec);
+  if (L.inl_off != old_off)
+    for (uint32_t i = 0; i < cnt; i++)
+      inl_pos_.put((uint64_t)n << 32 | (uint32_t)inl.m.h[L.inl_off + i].ident, L.inl_off + i);
+  inl_pos_.put(key, L.inl_off + cnt);
+  return 1;
+}
+
+// topics.go:382-397
+int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
+  version_++;
+  uint32_t n = seek(filter, 0);
+  if (n == kNone) return 0;
+  uint64_t key = (uint64_t)n << 32 | (uint32_t)ident;
+  uint32_t pos;
+  if (inl_pos_.get(key, &pos)) {
+    NodeLists& L = lists.at_w(n);
+    uint32_t last = L.inl_off + L.inl_cnt - 1;
+    inl_pos_.erase(key);
+    if (pos != last) {
+      inl.m.at_w(pos) = inl.m.h[last];
+      inl_pos_.put((uint64_t)n << 32 | (uint32_t)inl.m.h[pos].ident, pos);
+    }
+    L.inl_cnt--;
+    inl.live--;
+  }
+  if (lists.h[n].inl_cnt == 0) trim(n);
+  return 1;
+}
+
+// topics.go:453-476
+int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
+                              bool retain) {
+  version_++;
+  uint32_t n = set(topic, 0);
+  std::string t(topic);
+  if (payload_len > 0) {
+    bool path = !topic.empty();  // retainPath = pk.TopicName; "" means no path
+    nh_[n].retain_path = path;
+    NodeMsg& M = msg.at_w(n);
+    M.flags = path ? (kRetainPath | kRetainLive) : 0;
+    M.handle = path ? handle : 0;
+    retained_[t] = RetEntry{handle, payload_len, retain};
+    if (topic.empty()) {
+      empty_topic_live = true;
+      empty_topic_handle = handle;
+    }
+    return 1;
+  }
+  int64_t out = 0;
+  auto it = retained_.find(t);
+  if (it != retained_.end() && it->second.payload_len > 0 && it->second.retain) out = -1;
+  nh_[n].retain_path = false;
+  NodeMsg& M = msg.at_w(n);
+  M.flags = 0;
+  M.handle = 0;
+  if (it != retained_.end()) retained_.erase(it);
+  if (topic.empty()) empty_topic_live = false;
+  trim(n);
+  return out;
+}
+
+// Retained.Delete (server.go:1726): the map entry only; the particle keeps retainPath (Q12).
+int Index::retained_delete(std::string_view topic) {
+  version_++;
+  auto it = retained_.find(std::string(topic));
+  if (it == retained_.end()) return 0;
+  retained_.erase(it);
+  if (topic.empty()) {
+    empty_topic_live = false;
+    return 1;
+  }
+  uint32_t n = seek(topic, 0);
+  if (n != kNone && nh_[n].retain_path) {
+    NodeMsg& M = msg.at_w(n);
+    M.flags &= ~kRetainLive;
+  }
+  return 1;
+}
+
+}  // namespace mq

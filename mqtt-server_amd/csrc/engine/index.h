@@ -1,0 +1,233 @@
+// Host side of the engine: the authoritative, incrementally updated trie image.
+//
+// The reference keeps a pointer trie of particles with per-node Go maps (topics.go:748-822).
+// Here the same trie is held as flat arrays in exactly the device layout (layout.h): an
+// open-addressing edge table, node records, and slab-allocated subscription lists. Updates
+// (Subscribe/Unsubscribe/RetainMessage...) edit these host arrays in place and mark dirty
+// pages; Device::sync() uploads only those pages, so the HBM image is updated incrementally
+// rather than rebuilt.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "layout.h"
+
+namespace mq {
+
+// A host vector mirrored into device memory; tracks which pages changed since the last sync.
+template <class T>
+struct Mirror {
+  static constexpr size_t kPageBytes = 1u << 16;
+  std::vector<T> h;
+  std::vector<uint64_t> dirty;  // bitmap of pages
+  bool all_dirty = true;
+  uint64_t epoch = 0;  // bumped when the host array is reallocated (device must realloc too)
+
+  static size_t per_page() { return kPageBytes / sizeof(T) ? kPageBytes / sizeof(T) : 1; }
+  size_t size() const { return h.size(); }
+  T& operator[](size_t i) { return h[i]; }
+  const T& operator[](size_t i) const { return h[i]; }
+  void mark(size_t i) {
+    size_t p = i / per_page();
+    if (p / 64 >= dirty.size()) dirty.resize(p / 64 + 1, 0);
+    dirty[p / 64] |= 1ull << (p % 64);
+  }
+  void mark_range(size_t i, size_t n) {
+    if (!n) return;
+    size_t p0 = i / per_page(), p1 = (i + n - 1) / per_page();
+    if (p1 / 64 >= dirty.size()) dirty.resize(p1 / 64 + 1, 0);
+    for (size_t p = p0; p <= p1; p++) dirty[p / 64] |= 1ull << (p % 64);
+  }
+  T& at_w(size_t i) {  // write access
+    mark(i);
+    return h[i];
+  }
+  void grow_to(size_t n, const T& fill) {
+    if (n <= h.size()) return;
+    size_t old = h.size();
+    if (n > h.capacity()) {
+      h.reserve(n < 2 * h.capacity() ? 2 * h.capacity() : n);
+      epoch++;
+      all_dirty = true;
+    }
+    h.resize(n, fill);
+    mark_range(old, n - old);
+  }
+  void clear_dirty() {
+    all_dirty = false;
+    dirty.assign(dirty.size(), 0);
+  }
+};
+
+// Power-of-two size-class slab allocator over a mirrored pool.
+template <class T>
+struct SlabPool {
+  Mirror<T> m;
+  std::vector<std::vector<uint32_t>> free_lists = std::vector<std::vector<uint32_t>>(33);
+  uint64_t live = 0;  // elements in use
+
+  static uint32_t cls_of(uint32_t cap) {
+    uint32_t c = 0;
+    while ((1u << c) < cap) c++;
+    return c;
+  }
+  uint32_t alloc(uint32_t cap) {  // cap must be a power of two
+    uint32_t c = cls_of(cap);
+    auto& fl = free_lists[c];
+    if (!fl.empty()) {
+      uint32_t off = fl.back();
+      fl.pop_back();
+      return off;
+    }
+    uint32_t off = (uint32_t)m.size();
+    m.grow_to(m.size() + (1u << c), T{});
+    return off;
+  }
+  void release(uint32_t off, uint32_t cap) {
+    if (cap) free_lists[cls_of(cap)].push_back(off);
+  }
+};
+
+// Open-addressing u64 -> u32 map (linear probing), used for (node, client) positions.
+class HashU64 {
+ public:
+  explicit HashU64(size_t cap = 1024) { rehash(cap); }
+  bool get(uint64_t k, uint32_t* v) const;
+  void put(uint64_t k, uint32_t v);
+  bool erase(uint64_t k);
+  size_t size() const { return n_; }
+  void reserve(size_t n) {
+    if (n * 2 > keys_.size()) rehash(n * 2);
+  }
+
+ private:
+  void rehash(size_t cap);
+  size_t slot(uint64_t k) const { return (size_t)(mix64(k) & (keys_.size() - 1)); }
+  static constexpr uint64_t kEmpty = ~0ull, kTomb = ~0ull - 1;
+  std::vector<uint64_t> keys_;
+  std::vector<uint32_t> vals_;
+  size_t n_ = 0, tombs_ = 0;
+};
+
+struct NodeHost {
+  SegKey key{0, 0};
+  uint32_t str = 0;        // interned segment string id (0 = "+", 1 = "#")
+  uint32_t n_children = 0;
+  uint32_t child_pos = 0;  // position in the parent's children slab
+  uint32_t sub_cap = 0, shr_cap = 0, inl_cap = 0, child_cap = 0;
+  uint16_t depth = 0;
+  bool live = false;
+  bool retain_path = false;
+};
+
+struct RetEntry {
+  uint64_t handle;
+  uint32_t payload_len;
+  bool retain;
+};
+
+class Index {
+ public:
+  explicit Index(uint64_t expected_subs = 0, uint64_t expected_nodes = 0);
+
+  // TopicsIndex API (topics.go:368-476); semantics and return values as the reference.
+  int subscribe(std::string_view filter, uint32_t client, uint32_t filter_id, uint8_t qos,
+                uint8_t flags, int32_t ident);
+  int unsubscribe(std::string_view filter, uint32_t client);
+  int inline_subscribe(std::string_view filter, int32_t ident, uint32_t filter_id);
+  int inline_unsubscribe(std::string_view filter, int32_t ident);
+  int64_t retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
+                         bool retain);
+  int retained_delete(std::string_view topic);
+  uint64_t retained_len() const { return retained_.size(); }
+
+  // Device image (layout.h); the Device uploads dirty pages of these.
+  Mirror<EdgeSlot> edges;
+  Mirror<NodeWalk> walk;
+  Mirror<NodeLists> lists;
+  Mirror<NodeMsg> msg;
+  Mirror<SegInfo> seginfo;
+  Mirror<uint8_t> segbytes;
+  SlabPool<SubRec> subs;
+  SlabPool<ShrRec> shr;
+  SlabPool<InlRec> inl;
+  SlabPool<uint32_t> children;
+  // Retained packet stored on topic "" (retainPath "" is "no path", Q6): literal-final
+  // lookups of particles without a retain path read this entry (topics.go:573).
+  bool empty_topic_live = false;
+  uint64_t empty_topic_handle = 0;
+
+  uint64_t edge_mask() const { return edges.size() - 1; }
+  uint64_t n_nodes() const { return n_live_nodes_; }
+  uint64_t n_edges() const { return n_edges_; }
+  uint64_t n_subs_merge() const { return n_merge_; }
+  uint32_t max_depth() const { return max_depth_; }
+  uint64_t version() const { return version_; }
+
+ private:
+  // path of `filter` from isolateParticle depth d on (topics.go:479-496 / 499-513)
+  static void path_of(std::string_view filter, int d, std::vector<std::string_view>& out);
+  uint32_t set(std::string_view filter, int d);           // create path, return node
+  uint32_t seek(std::string_view filter, int d) const;    // find path or kNone
+  void trim(uint32_t n);                                  // topics.go:516-522
+  uint32_t find_child(uint32_t parent, const SegKey& k, std::string_view seg) const;
+  uint32_t new_node(uint32_t parent, std::string_view seg, const SegKey& k);
+  void remove_node(uint32_t n);
+  void edge_insert(uint32_t parent, const SegKey& k, uint32_t child);
+  void edge_erase(uint32_t parent, const SegKey& k, uint32_t child);
+  void edge_rehash(size_t cap);
+  uint32_t intern_str(std::string_view s);
+
+  // subscription list primitives (positions are absolute pool indices)
+  void sub_ensure(uint32_t n, uint32_t need);
+  uint32_t sub_add(uint32_t n, const SubRec& r, bool merge);
+  void sub_remove(uint32_t n, uint32_t pos);
+  void sub_set_merge(uint32_t n, uint32_t pos, bool merge);
+  bool compatible(uint32_t a, uint32_t b) const;
+  void path_strs(uint32_t n, uint32_t* out, int* len) const;
+  void refresh_merge_flag(uint32_t client, uint32_t node);
+
+  template <class T, class Rec>
+  void list_push(SlabPool<T>& pool, uint32_t& off, uint32_t& cnt, uint32_t& cap, const Rec& r);
+
+  bool sub_is_merge(uint32_t pos) const { return (subs.m[pos].meta & 0x1000u) != 0; }
+  uint32_t sub_count(uint32_t n) const { return lists[n].n_direct + lists[n].n_merge; }
+
+  std::vector<NodeHost> nh_;
+  std::vector<uint32_t> free_nodes_;
+  uint64_t n_live_nodes_ = 0, n_edges_ = 0, n_tombs_ = 0, n_merge_ = 0;
+  uint32_t max_depth_ = 0;
+  uint64_t version_ = 0;
+
+  std::unordered_map<std::string, uint32_t> str_ids_;
+  std::vector<std::string> strs_;
+  std::unordered_map<std::string, uint32_t> long_segs_;  // long segment -> SegInfo index
+  std::unordered_map<std::string, uint32_t> group_ids_;
+
+  HashU64 sub_pos_{1024};  // (node << 32 | client) -> pool position
+  HashU64 inl_pos_{64};    // (node << 32 | ident) -> pool position
+  struct ShrKey {
+    uint32_t node, group, client;
+    bool operator==(const ShrKey& o) const {
+      return node == o.node && group == o.group && client == o.client;
+    }
+  };
+  struct ShrKeyHash {
+    size_t operator()(const ShrKey& k) const {
+      return (size_t)mix64(((uint64_t)k.node << 32 | k.client) ^ ((uint64_t)k.group * 0x9e3779b97f4a7c15ull));
+    }
+  };
+  std::unordered_map<ShrKey, uint32_t, ShrKeyHash> shr_pos_;
+  std::vector<uint32_t> shr_group_;  // group id per shared pool position
+  std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
+  std::unordered_map<std::string, RetEntry> retained_;
+};
+
+// strings.EqualFold(s, "$SHARE") under Go's Unicode simple folding (Q9: U+017F ~ 's').
+bool is_share_prefix(std::string_view s);
+
+}  // namespace mq

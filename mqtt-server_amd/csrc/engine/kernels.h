@@ -1,0 +1,68 @@
+// Kernel-side structures and launch wrappers of the engine (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "layout.h"
+
+namespace mq {
+
+constexpr uint32_t kLdsTab = 512;      // LDS merge-table slots per wavefront
+constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
+
+// Device pointers of the resident index image.
+struct DevIndex {
+  const EdgeSlot* edges;
+  uint64_t edge_mask;
+  const NodeWalk* walk;
+  const NodeLists* lists;
+  const NodeMsg* msg;
+  const SegInfo* seginfo;
+  const uint8_t* segbytes;
+  const SubRec* subs;
+  const ShrRec* shr;
+  const InlRec* inl;
+  const uint32_t* children;
+  uint64_t retained_len;
+  uint64_t empty_topic_handle;
+  uint32_t empty_topic_live;
+  uint32_t pad;
+  uint32_t* err;  // device error word (kErr*), checked by the host after each batch
+};
+
+constexpr uint32_t kErrWalkGuard = 1u;
+constexpr uint32_t kErrTableFull = 2u;
+constexpr uint64_t kWalkGuard = 1ull << 26;
+
+// Exclusive offsets of a topic's outputs (scan of TopicCount).
+struct TopicOff {
+  uint64_t g, rows, shr, inl, tab;
+};
+
+// Same layout as mq_topic_result (include/mqmatch.h).
+struct mq_topic_result_dev {
+  uint64_t sub_base, shared_base, inline_base;
+  uint32_t sub_cap, n_client, n_ident, n_shared, n_inline, reserved;
+};
+
+struct EmitArgs {
+  DevIndex ix;
+  uint32_t t0, t1;          // topic range of this chunk
+  const TopicOff* off;      // per-topic offsets (n + 1)
+  TopicOff base;            // off[t0]: the chunk's output buffers start here
+  const uint32_t* gathers;
+  SubRec* rows;
+  ShrRec* shr_rows;
+  InlRec* inl_rows;
+  uint32_t* tab;            // global merge tables: key | row | meta planes of tab_cap each
+  uint64_t tab_cap;
+  mq_topic_result_dev* res; // indexed t - t0
+};
+
+void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
+                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, hipStream_t s);
+void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
+                 hipStream_t s);
+void launch_emit(const EmitArgs& a, hipStream_t s);
+
+}  // namespace mq

@@ -1,0 +1,497 @@
+// gfx950 kernels of the topic-matching engine.
+//
+//   k_walk<false>   one thread per publish topic: tokenises the topic and walks the trie in the
+//                   reference's exact DFS order (scanSubscribers, topics.go:593-628) with no
+//                   stack — parent pointers in the node records replace recursion. Counts the
+//                   gathers and the rows each topic will emit.
+//   k_scan_*        exclusive scan of the per-topic counts into output offsets.
+//   k_walk<true>    the same walk again, writing the gather list (node + what to gather).
+//   k_emit          one wavefront (64 lanes) per topic: streams the gathered subscription
+//                   lists into the output rows (coalesced 16-byte rows), merges subscriptions of
+//                   clients with several matching filters through a per-wave LDS hash table
+//                   (gatherSubscriptions + Subscription.Merge, topics.go:631-648,
+//                   packets/packets.go:254-274), copies shared rows and applies the inline
+//                   last-write rule (topics.go:668-676) with ballot/mbcnt compaction.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace mq {
+
+// ---------------------------------------------------------------------------------------------
+// byte-level helpers over the topic buffer
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t find_slash(const uint8_t* __restrict__ b, uint64_t s, uint64_t end) {
+  while (s < end && b[s] != '/') s++;
+  return s;
+}
+
+// Start of the segment that ends at `e` (exclusive): one past the previous '/' or b0.
+__device__ __forceinline__ uint64_t seg_start_before(const uint8_t* __restrict__ b, uint64_t b0, uint64_t e) {
+  while (e > b0 && b[e - 1] != '/') e--;
+  return e;
+}
+
+// particles.get(key) (topics.go:803-807) through the global edge table.
+__device__ __forceinline__ uint32_t lookup(const DevIndex& ix, uint32_t parent, const SegKey& k,
+                                          const uint8_t* seg, uint32_t len) {
+  uint64_t i = edge_hash(parent, k) & ix.edge_mask;
+  for (uint64_t probes = 0; probes <= ix.edge_mask; probes++) {
+    const EdgeSlot e = ix.edges[i];
+    if (e.parent == kEdgeEmpty) return kNone;
+    if (e.parent == parent && e.k0 == k.k0 && e.k1 == k.k1) {
+      if (!seg_is_long(k)) return e.child;
+      const SegInfo si = ix.seginfo[ix.walk[e.child].seg];
+      bool eq = si.len == len;
+      for (uint32_t j = 0; eq && j < len; j++) eq = ix.segbytes[si.off + j] == seg[j];
+      if (eq) return e.child;
+    }
+    i = (i + 1) & ix.edge_mask;
+  }
+  return kNone;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_walk: the match walk (thread per topic)
+// ---------------------------------------------------------------------------------------------
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
+                                              const uint64_t* __restrict__ to, uint32_t n,
+                                              DevIndex ix, TopicCount* __restrict__ cnt,
+                                              const TopicOff* __restrict__ off,
+                                              uint32_t* __restrict__ gathers) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t b0 = to[t], b1 = to[t + 1];
+  uint32_t ng = 0, rows = 0, shared = 0, inl = 0, merge = 0;
+  uint32_t* gout = FILL ? gathers + off[t].g : nullptr;
+
+  if (b1 > b0) {  // Subscribers("") matches nothing (topics.go:598-600)
+    const bool dollar = tb[b0] == '$';
+    // gather{Subscriptions,SharedSubscriptions,InlineSubscriptions} of one particle
+    auto gather = [&](uint32_t node, bool with_inline) {
+      const NodeLists L = ix.lists[node];
+      // [MQTT-4.7.1-1]: '$' topics skip subscriptions whose filter starts with '+'/'#' (Q3)
+      const bool subs_ok = !(dollar && (L.flags & kFlagSeg0Wild));
+      if (FILL) {
+        gout[ng] = node | (subs_ok ? kGatherSubs : 0u) | (with_inline ? kGatherInline : 0u);
+      } else {
+        if (subs_ok) {
+          rows += L.n_direct + L.n_merge;
+          merge += L.n_merge;
+        }
+        shared += L.shr_cnt;
+        if (with_inline) inl += L.inl_cnt;
+      }
+      ng++;
+    };
+
+    uint32_t node = kRoot;
+    uint64_t s = b0, e = find_slash(tb, b0, b1);
+    int state = 0;  // 0: literal child next, 1: '+' child next, 2: '#' gather and return
+    for (uint64_t guard = 0;; guard++) {
+      if (guard > kWalkGuard) {  // never reached on a well-formed image; fail loudly, not hang
+        atomicOr(ix.err, kErrWalkGuard);
+        break;
+      }
+      const bool has_next = e < b1;
+      if (state == 0) {
+        state = 1;
+        const uint32_t len = (uint32_t)(e - s);
+        // A literal "+" segment makes the reference visit the '+' child twice with identical
+        // results (topics.go:603); the '+' branch below covers it.
+        if (!(len == 1 && tb[s] == '+')) {
+          const SegKey k = seg_key(tb + s, len);
+          const uint32_t p = lookup(ix, node, k, tb + s, len);
+          if (p != kNone) {
+            if (has_next) {
+              node = p;
+              s = e + 1;
+              e = find_slash(tb, s, b1);
+              state = 0;
+              continue;
+            }
+            gather(p, true);
+            const uint32_t w = ix.walk[p].hash_child;  // filter/# matches filter (topics.go:612)
+            if (w != kNone) gather(w, false);          // inline: the particle's own again (Q2)
+          }
+        }
+      }
+      if (state == 1) {
+        state = 2;
+        const uint32_t p = ix.walk[node].plus_child;
+        if (p != kNone) {
+          if (has_next) {
+            node = p;
+            s = e + 1;
+            e = find_slash(tb, s, b1);
+            state = 0;
+            continue;
+          }
+          gather(p, true);
+        }
+      }
+      const NodeWalk nw = ix.walk[node];
+      if (nw.hash_child != kNone) gather(nw.hash_child, true);  // topics.go:621-625
+      if (node == kRoot) break;
+      // return to the parent: restore its segment window and continue after this branch
+      node = nw.parent_flags & kParentMask;
+      e = s - 1;
+      s = seg_start_before(tb, b0, e);
+      state = (nw.parent_flags & kFlagPlusKey) ? 2 : 1;
+    }
+  }
+  if (!FILL) {
+    TopicCount c;
+    c.gathers = ng;
+    c.rows = rows;
+    c.shared = shared;
+    c.inlines = inl;
+    uint32_t tab = 0;
+    if (merge > kLdsTab / 2) {
+      tab = 1;
+      while (tab < 2 * merge) tab <<= 1;
+    }
+    c.table = tab;
+    cnt[t] = c;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// exclusive scan of TopicCount -> TopicOff (1024 topics per block)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void add_count(TopicOff& a, const TopicCount& c) {
+  a.g += c.gathers;
+  a.rows += c.rows;
+  a.shr += c.shared;
+  a.inl += c.inlines;
+  a.tab += c.table;
+}
+__device__ __forceinline__ void add_off(TopicOff& a, const TopicOff& b) {
+  a.g += b.g;
+  a.rows += b.rows;
+  a.shr += b.shr;
+  a.inl += b.inl;
+  a.tab += b.tab;
+}
+__device__ __forceinline__ TopicOff shfl_up_off(const TopicOff& v, int d) {
+  TopicOff r;
+  r.g = __shfl_up(v.g, d, 64);
+  r.rows = __shfl_up(v.rows, d, 64);
+  r.shr = __shfl_up(v.shr, d, 64);
+  r.inl = __shfl_up(v.inl, d, 64);
+  r.tab = __shfl_up(v.tab, d, 64);
+  return r;
+}
+
+// Block-wide inclusive scan of one TopicOff per thread (256 threads).
+__device__ TopicOff block_scan_incl(TopicOff v, TopicOff* wave_tot /*4*/) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    TopicOff u = shfl_up_off(v, d);
+    if (lane >= d) add_off(v, u);
+  }
+  if (lane == 63) wave_tot[wv] = v;
+  __syncthreads();
+  for (int w = 0; w < wv; w++) add_off(v, wave_tot[w]);
+  __syncthreads();
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const TopicCount* __restrict__ cnt, uint32_t n,
+                                                     TopicOff* __restrict__ bsum) {
+  __shared__ TopicOff wt[4];
+  TopicOff v{0, 0, 0, 0, 0};
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  for (int k = 0; k < 4; k++)
+    if (base + k < n) add_count(v, cnt[base + k]);
+  v = block_scan_incl(v, wt);
+  if (threadIdx.x == 255) bsum[blockIdx.x] = v;
+}
+
+// Single workgroup: exclusive scan of the block sums; bpre[nb] = total.
+__global__ __launch_bounds__(256) void k_scan_blocks(const TopicOff* __restrict__ bsum, uint32_t nb,
+                                                     TopicOff* __restrict__ bpre) {
+  __shared__ TopicOff wt[4];
+  __shared__ TopicOff carry;
+  if (threadIdx.x == 0) carry = TopicOff{0, 0, 0, 0, 0};
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint32_t b = b0 + threadIdx.x;
+    TopicOff v = b < nb ? bsum[b] : TopicOff{0, 0, 0, 0, 0};
+    TopicOff incl = block_scan_incl(v, wt);
+    TopicOff c = carry;
+    TopicOff ex = incl;
+    ex.g -= v.g; ex.rows -= v.rows; ex.shr -= v.shr; ex.inl -= v.inl; ex.tab -= v.tab;
+    add_off(ex, c);
+    if (b < nb) bpre[b] = ex;
+    __syncthreads();
+    if (threadIdx.x == 255) add_off(carry, incl);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bpre[nb] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const TopicCount* __restrict__ cnt, uint32_t n,
+                                                    const TopicOff* __restrict__ bpre,
+                                                    TopicOff* __restrict__ off) {
+  __shared__ TopicOff wt[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  TopicCount c[4];
+  TopicOff v{0, 0, 0, 0, 0};
+  for (int k = 0; k < 4; k++) {
+    c[k] = base + k < n ? cnt[base + k] : TopicCount{0, 0, 0, 0, 0};
+    add_count(v, c[k]);
+  }
+  TopicOff incl = block_scan_incl(v, wt);
+  TopicOff ex = bpre[blockIdx.x];
+  add_off(ex, incl);
+  ex.g -= v.g; ex.rows -= v.rows; ex.shr -= v.shr; ex.inl -= v.inl; ex.tab -= v.tab;
+  for (int k = 0; k < 4; k++) {
+    if (base + k < n) off[base + k] = ex;
+    add_count(ex, c[k]);
+  }
+  if (base + 3 >= (uint64_t)n - 1 && base < n) off[n] = bpre[gridDim.x];
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_emit: expand + merge + emit (one wavefront per topic)
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kTabEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kMetaDirty = 0x80000000u;
+constexpr uint32_t kMetaMergeBit = 0x1000u;
+
+struct TabRef {
+  uint32_t* key;
+  uint32_t* row;
+  uint32_t* meta;
+  uint32_t mask;
+};
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// Insert `key` (distinct across the active lanes); returns the slot and whether it was new.
+__device__ __forceinline__ uint32_t tab_insert(const TabRef& T, uint32_t key, bool* is_new,
+                                                uint32_t* err) {
+  uint32_t s = hash32(key) & T.mask;
+  for (uint32_t probes = 0; probes <= T.mask; probes++) {
+    uint32_t k = __hip_atomic_load(T.key + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (k == key) {
+      *is_new = false;
+      return s;
+    }
+    if (k == kTabEmpty) {
+      uint32_t old = atomicCAS(T.key + s, kTabEmpty, key);
+      if (old == kTabEmpty) {
+        *is_new = true;
+        return s;
+      }
+      if (old == key) {
+        *is_new = false;
+        return s;
+      }
+    }
+    s = (s + 1) & T.mask;
+  }
+  atomicOr(err, kErrTableFull);  // sized at <= 1/2 load by the count pass: unreachable
+  *is_new = false;
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint32_t prefix_before(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
+  __shared__ uint32_t lds_key[4][kLdsTab];
+  __shared__ uint32_t lds_row[4][kLdsTab];
+  __shared__ uint32_t lds_meta[4][kLdsTab];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t t = a.t0 + blockIdx.x * 4 + wv;
+  if (t >= a.t1) return;  // wave-uniform
+
+  const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+  const uint64_t rb = o0.rows - a.base.rows;
+  const uint32_t cap = (uint32_t)(o1.rows - o0.rows);
+  const uint64_t sb = o0.shr - a.base.shr, ib = o0.inl - a.base.inl;
+  const uint32_t tabn = (uint32_t)(o1.tab - o0.tab);
+  SubRec* __restrict__ rows = a.rows + rb;
+
+  TabRef T;
+  if (tabn) {
+    const uint64_t tb = o0.tab - a.base.tab;
+    T.key = a.tab + tb;
+    T.row = a.tab + a.tab_cap + tb;
+    T.meta = a.tab + 2 * a.tab_cap + tb;
+    T.mask = tabn - 1;
+  } else {
+    T.key = lds_key[wv];
+    T.row = lds_row[wv];
+    T.meta = lds_meta[wv];
+    T.mask = kLdsTab - 1;
+  }
+  bool tab_ready = false;
+
+  uint32_t n_cli = 0, n_ext = 0, n_shr = 0, n_inl = 0;
+  for (uint64_t g = o0.g; g < o1.g; g++) {
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(a.gathers[g]);
+    const uint32_t node = gw & kGatherNode;
+    const NodeLists L = a.ix.lists[node];
+    if (gw & kGatherSubs) {
+      // subscriptions that cannot merge: straight copy into client rows
+      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.ix.subs + L.sub_off);
+      uint4* __restrict__ dst = reinterpret_cast<uint4*>(rows + n_cli);
+      uint32_t i = lane;
+      for (; i + 192 < L.n_direct; i += 256) {
+        uint4 x0 = src[i], x1 = src[i + 64], x2 = src[i + 128], x3 = src[i + 192];
+        dst[i] = x0;
+        dst[i + 64] = x1;
+        dst[i + 128] = x2;
+        dst[i + 192] = x3;
+      }
+      for (; i < L.n_direct; i += 64) dst[i] = src[i];
+      n_cli += L.n_direct;
+
+      // subscriptions that may merge with another of the same client
+      if (L.n_merge) {
+        if (!tab_ready) {
+          for (uint32_t k = lane; k <= T.mask; k += 64) T.key[k] = kTabEmpty;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          tab_ready = true;
+        }
+        const SubRec* __restrict__ ms = a.ix.subs + L.sub_off + L.n_direct;
+        for (uint32_t i0 = 0; i0 < L.n_merge; i0 += 64) {
+          const uint32_t j = i0 + lane;
+          const bool v = j < L.n_merge;
+          SubRec r{0, 0, 0, 0};
+          uint32_t slot = 0;
+          bool is_new = false;
+          if (v) {
+            r = ms[j];
+            r.meta &= ~kMetaMergeBit;
+            slot = tab_insert(T, r.client, &is_new, a.ix.err);
+          }
+          const uint64_t bn = __ballot(v && is_new);
+          if (v && is_new) {  // first (minimum-rank) subscription of this client: the base
+            const uint32_t pos = n_cli + prefix_before(bn);
+            rows[pos] = r;
+            T.row[slot] = pos;
+            T.meta[slot] = r.meta;
+          }
+          n_cli += __popcll(bn);
+          const bool dup = v && !is_new;
+          if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
+            const uint32_t m = T.meta[slot];
+            const uint32_t q = max(m & kMetaQos, r.meta & kMetaQos);
+            const uint32_t nm = (m & ~kMetaQos) | q | (r.meta & kMetaNoLocal);
+            if ((nm & ~kMetaDirty) != (m & ~kMetaDirty)) T.meta[slot] = nm | kMetaDirty;
+          }
+          const uint64_t be = __ballot(dup && r.ident > 0);
+          if (dup && r.ident > 0) {  // Identifiers[n.Filter] = n.Identifier (id > 0)
+            const uint32_t k = n_ext + prefix_before(be);
+            SubRec x{r.client, r.filter_id, r.ident, 0};
+            rows[cap - 1 - k] = x;
+          }
+          n_ext += __popcll(be);
+        }
+      }
+    }
+    // Shared[sub.Filter][client] = sub (topics.go:656-663)
+    {
+      const uint2* __restrict__ src = reinterpret_cast<const uint2*>(a.ix.shr + L.shr_off);
+      uint2* __restrict__ dst = reinterpret_cast<uint2*>(a.shr_rows + sb + n_shr);
+      for (uint32_t i = lane; i < L.shr_cnt; i += 64) dst[i] = src[i];
+      n_shr += L.shr_cnt;
+    }
+    if (gw & kGatherInline) {
+      const uint2* __restrict__ src = reinterpret_cast<const uint2*>(a.ix.inl + L.inl_off);
+      uint2* __restrict__ dst = reinterpret_cast<uint2*>(a.inl_rows + ib + n_inl);
+      for (uint32_t i = lane; i < L.inl_cnt; i += 64) dst[i] = src[i];
+      n_inl += L.inl_cnt;
+    }
+  }
+
+  if (tab_ready) {  // write back merged Qos/NoLocal of bases that absorbed later matches
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t k = lane; k <= T.mask; k += 64) {
+      if (T.key[k] != kTabEmpty) {
+        const uint32_t m = T.meta[k];
+        if (m & kMetaDirty) rows[T.row[k]].meta = m & ~kMetaDirty;
+      }
+    }
+  }
+
+  if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    InlRec* __restrict__ ir = a.inl_rows + ib;
+    uint32_t kept = 0;
+    for (uint32_t i0 = 0; i0 < n_inl; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      bool keep = false;
+      InlRec r{0, 0};
+      if (i < n_inl) {
+        r = ir[i];
+        keep = true;
+        for (uint32_t j = i + 1; j < n_inl && keep; j++) keep = ir[j].ident != r.ident;
+      }
+      const uint64_t bk = __ballot(keep);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (keep) ir[kept + prefix_before(bk)] = r;
+      kept += __popcll(bk);
+    }
+    n_inl = kept;
+  }
+
+  if (lane == 0) {
+    mq_topic_result_dev res;
+    res.sub_base = rb;
+    res.shared_base = sb;
+    res.inline_base = ib;
+    res.sub_cap = cap;
+    res.n_client = n_cli;
+    res.n_ident = n_ext;
+    res.n_shared = n_shr;
+    res.n_inline = n_inl;
+    res.reserved = 0;
+    a.res[t - a.t0] = res;
+  }
+}
+
+}  // namespace mq
+
+namespace mq {
+
+void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
+                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, hipStream_t s) {
+  if (!n) return;
+  dim3 grid((n + 255) / 256);
+  if (fill)
+    hipLaunchKernelGGL(k_walk<true>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers);
+  else
+    hipLaunchKernelGGL(k_walk<false>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers);
+}
+
+void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
+                 hipStream_t s) {
+  if (!n) return;
+  const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(256), 0, s, cnt, n, bsum);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(256), 0, s, bsum, nb, bpre);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(256), 0, s, cnt, n, bpre, off);
+}
+
+void launch_emit(const EmitArgs& a, hipStream_t s) {
+  if (a.t1 <= a.t0) return;
+  const uint32_t waves = a.t1 - a.t0;
+  hipLaunchKernelGGL(k_emit, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+}
+
+}  // namespace mq

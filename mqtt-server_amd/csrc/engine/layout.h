@@ -1,0 +1,153 @@
+// Device-image layout shared by the host index builder (index.cpp) and the gfx950 kernels
+// (kernels.hip). Every array here lives resident in HBM and is mirrored on the host, which
+// applies updates and uploads only the dirty pages.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define MQ_HD __host__ __device__ __forceinline__
+#else
+#define MQ_HD inline
+#endif
+
+namespace mq {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kRoot = 0;
+
+// ---- segment keys -------------------------------------------------------------------------
+// A topic level ("segment") is keyed by 16 bytes. Segments of <= 15 bytes are stored inline
+// (bytes little-endian, length in the top byte of k1): exact and collision-free. Longer
+// segments carry two independent 64-bit hashes with 0xFF in the top byte of k1; a hit on
+// such a key is verified byte-for-byte against the segment pool, so matching stays exact.
+struct SegKey {
+  uint64_t k0, k1;
+};
+
+constexpr uint32_t kInlineSegMax = 15;
+constexpr uint64_t kLongMarker = 0xFFull << 56;
+
+MQ_HD uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+
+MQ_HD SegKey seg_key(const uint8_t* p, uint32_t len) {
+  SegKey k{0, 0};
+  if (len <= kInlineSegMax) {
+    for (uint32_t i = 0; i < len; i++) {
+      if (i < 8) k.k0 |= (uint64_t)p[i] << (8 * i);
+      else k.k1 |= (uint64_t)p[i] << (8 * (i - 8));
+    }
+    k.k1 |= (uint64_t)len << 56;
+  } else {
+    uint64_t a = 0xcbf29ce484222325ull ^ len, b = 0x84222325cbf29ce4ull + len;
+    for (uint32_t i = 0; i < len; i++) {
+      a = (a ^ p[i]) * 0x100000001b3ull;
+      b = (b + p[i] + 1) * 0x9e3779b97f4a7c15ull;
+      b ^= b >> 29;
+    }
+    k.k0 = mix64(a);
+    k.k1 = (mix64(b) & ~kLongMarker) | kLongMarker;
+  }
+  return k;
+}
+
+MQ_HD bool seg_is_long(const SegKey& k) { return (k.k1 & kLongMarker) == kLongMarker; }
+
+MQ_HD uint64_t edge_hash(uint32_t parent, const SegKey& k) {
+  return mix64(k.k0 ^ (k.k1 * 0x9e3779b97f4a7c15ull) ^ ((uint64_t)parent * 0xd6e8feb86659fd93ull));
+}
+
+// ---- trie edges -----------------------------------------------------------------------------
+// Global open-addressing table (linear probing, load <= 1/2): (parent node, segment key) ->
+// child node. Every child is here, '+' and '#' children included, so a literal topic
+// segment "+"/"#" walks exactly like the reference's particles.get(key) (topics.go:604).
+constexpr uint32_t kEdgeEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kEdgeTomb = 0xFFFFFFFEu;
+
+struct EdgeSlot {  // 32 B
+  uint64_t k0, k1;
+  uint32_t parent;  // kEdgeEmpty / kEdgeTomb for free slots
+  uint32_t child;
+  uint32_t pad0, pad1;
+};
+
+// ---- nodes (particles, topics.go:748-757) -----------------------------------------------------
+// Walk record, read by the match walk (16 B).
+constexpr uint32_t kParentMask = 0x3FFFFFFFu;
+constexpr uint32_t kFlagSeg0Wild = 1u << 30;  // path segment 0 starts with '+'/'#' (Q3 rule)
+constexpr uint32_t kFlagPlusKey = 1u << 31;   // this node's key is "+"
+
+struct NodeWalk {
+  uint32_t plus_child;    // child keyed "+" or kNone
+  uint32_t hash_child;    // child keyed "#" or kNone
+  uint32_t parent_flags;  // parent id | kFlagSeg0Wild | kFlagPlusKey
+  uint32_t seg;           // index into SegInfo for long keys (verification), else kNone
+};
+
+// Subscription lists of a node (32 B). Non-shared subscriptions sit in one slab:
+// [sub_off, sub_off + n_direct) can never merge with another subscription of the same client
+// for any topic; [sub_off + n_direct, + n_merge) may (the client has another filter that can
+// co-match), and go through the per-topic merge table.
+struct NodeLists {
+  uint32_t sub_off, n_direct, n_merge;
+  uint32_t shr_off, shr_cnt;
+  uint32_t inl_off, inl_cnt;
+  uint32_t flags;  // kFlagSeg0Wild
+};
+
+// Retained-message state and children of a node, for Messages (32 B).
+constexpr uint32_t kRetainPath = 1u;  // particle.retainPath != "" (topics.go:755)
+constexpr uint32_t kRetainLive = 2u;  // Retained map holds the path (Q12 decouples the two)
+struct NodeMsg {
+  uint32_t child_off, child_cnt;  // children slab (u32 node ids) for '+'/'#' enumeration
+  uint32_t flags;                 // kRetainPath | kRetainLive
+  uint32_t depth;
+  uint64_t handle;                // retained packet handle when kRetainLive
+  uint32_t key_sys, pad;          // key == "$SYS" (topics.go:549)
+};
+
+struct SegInfo {  // long segment bytes in the segment pool
+  uint32_t off, len;
+};
+
+// ---- subscription records -------------------------------------------------------------------
+// The record formats equal the output row formats (include/mqmatch.h) so that subscriptions
+// that cannot merge are copied straight to the output.
+struct SubRec {  // == mq_client_row
+  uint32_t client;
+  uint32_t filter_id;
+  int32_t ident;
+  uint32_t meta;  // qos | nolocal<<8 | rap<<9 | rh<<10 (| kMetaMerge, host-side only)
+};
+struct ShrRec {  // == mq_shared_row
+  uint32_t filter_id;
+  uint32_t client;
+};
+struct InlRec {  // == mq_inline_row
+  int32_t ident;
+  uint32_t filter_id;
+};
+
+constexpr uint32_t kMetaQos = 0x3u;
+constexpr uint32_t kMetaNoLocal = 0x100u;
+constexpr uint32_t kMetaRap = 0x200u;
+constexpr uint32_t kMetaRhShift = 10;
+
+// Gather word written by the walk: node | kGatherSubs | kGatherInline.
+constexpr uint32_t kGatherNode = 0x3FFFFFFFu;
+constexpr uint32_t kGatherSubs = 1u << 30;    // gather non-shared subscriptions
+constexpr uint32_t kGatherInline = 1u << 31;  // gather inline subscriptions
+
+// Per-topic counts from the walk (count pass), exclusive-scanned into offsets.
+struct TopicCount {
+  uint32_t gathers, rows, shared, inlines, table;
+};
+
+}  // namespace mq

@@ -1,0 +1,451 @@
+"""ctypes binding of lib/libmqmatch.so (include/mqmatch.h) and a host-side mirror of the
+reference Go `TopicsIndex` API (/root/reference/topics.go:349-698).
+
+The mirror does what the Go cgo shim does: it interns client-ID and filter
+strings to u32 ids, keeps the stored packets.Subscription values host-side, calls the engine
+through the C-ABI, and rematerialises the engine's id rows as Go-shaped `Subscribers`
+(topics.go:312-317). There is no CPU matching path: if the library or a GPU is missing, the
+calls raise.
+"""
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ._paths import LIB_DIR
+
+SHARE_PREFIX = "$SHARE"  # topics.go:16
+SYS_PREFIX = "$SYS"      # topics.go:17
+
+META_QOS = 0x3
+META_NOLOCAL = 0x100
+META_RAP = 0x200
+META_RH_SHIFT = 10
+
+_u8p = C.POINTER(C.c_uint8)
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+
+
+class MqConfig(C.Structure):
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("expected_subs", C.c_uint64),
+                ("expected_nodes", C.c_uint64)]
+
+
+class TopicResult(C.Structure):
+    _fields_ = [("sub_base", C.c_uint64), ("shared_base", C.c_uint64), ("inline_base", C.c_uint64),
+                ("sub_cap", C.c_uint32), ("n_client", C.c_uint32), ("n_ident", C.c_uint32),
+                ("n_shared", C.c_uint32), ("n_inline", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class MatchResult(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("reserved", C.c_uint32),
+                ("topics", C.c_void_p), ("sub_rows", C.c_void_p), ("shared_rows", C.c_void_p),
+                ("inline_rows", C.c_void_p), ("n_sub_rows", C.c_uint64),
+                ("n_shared_rows", C.c_uint64), ("n_inline_rows", C.c_uint64)]
+
+
+class MsgResult(C.Structure):
+    _fields_ = [("n_filters", C.c_uint32), ("reserved", C.c_uint32), ("base", C.c_void_p),
+                ("count", C.c_void_p), ("handles", C.c_void_p), ("n_handles", C.c_uint64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("nodes", "edges", "edge_capacity", "subs", "subs_merge",
+                                           "shared", "inlines", "retained", "retained_live",
+                                           "device_bytes", "upload_bytes_total", "syncs")] + \
+               [("max_depth", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class KernelTime(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("total_ms", C.c_double)]
+
+
+# Every symbol declared in include/mqmatch.h (checked by tests/test_capi.py).
+EXPORTS = [
+    "mq_index_create", "mq_index_destroy", "mq_last_error", "mq_abi_version", "mq_subscribe",
+    "mq_unsubscribe", "mq_inline_subscribe", "mq_inline_unsubscribe", "mq_retain_message",
+    "mq_retained_delete", "mq_retained_len", "mq_subscribe_bulk", "mq_retain_bulk",
+    "mq_match_batch", "mq_match_device", "mq_match_chunks", "mq_messages_batch",
+    "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
+    "mq_profile_read", "mq_profile_reset",
+]
+
+_LIB = None
+
+
+def lib_path():
+    return os.path.join(LIB_DIR, "libmqmatch.so")
+
+
+def lib():
+    """Load the engine library; raises if it is missing (there is no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = lib_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: build it with __graft_entry__.build()")
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    sig = {
+        "mq_index_create": (C.c_int, [C.POINTER(MqConfig), C.POINTER(vp)]),
+        "mq_index_destroy": (None, [vp]),
+        "mq_last_error": (C.c_char_p, []),
+        "mq_abi_version": (C.c_uint32, []),
+        "mq_subscribe": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint8,
+                                   C.c_uint8, C.c_int32]),
+        "mq_unsubscribe": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint32]),
+        "mq_inline_subscribe": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_int32, C.c_uint32]),
+        "mq_inline_unsubscribe": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_int32]),
+        "mq_retain_message": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                        C.c_uint8, _i64p]),
+        "mq_retained_delete": (C.c_int, [vp, C.c_char_p, C.c_uint32]),
+        "mq_retained_len": (C.c_uint64, [vp]),
+        "mq_subscribe_bulk": (C.c_int, [vp, _u8p, _u64p, _u32p, _u32p, _u8p, _u8p, _i32p,
+                                        C.c_uint64, _u8p]),
+        "mq_retain_bulk": (C.c_int, [vp, _u8p, _u64p, _u64p, C.c_uint64]),
+        "mq_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MatchResult))]),
+        "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
+        "mq_match_chunks": (C.c_uint32, [vp]),
+        "mq_messages_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MsgResult))]),
+        "mq_messages_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MsgResult)]),
+        "mq_result_free": (None, [vp]),
+        "mq_sync": (C.c_int, [vp, vp]),
+        "mq_index_stats": (C.c_int, [vp, C.POINTER(Stats)]),
+        "mq_profile_enable": (C.c_int, [vp, C.c_int]),
+        "mq_profile_read": (C.c_int, [vp, C.POINTER(KernelTime), C.c_uint32]),
+        "mq_profile_reset": (C.c_int, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _check(rc, what):
+    if rc < 0:
+        msg = lib().mq_last_error()
+        raise EngineError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+def _b(s):
+    return s.encode("utf-8", "surrogateescape") if isinstance(s, str) else bytes(s)
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def pack_strings(items):
+    """List of str/bytes -> (uint8 bytes, uint64 offsets)."""
+    bs = [_b(x) for x in items]
+    offs = np.zeros(len(bs) + 1, np.uint64)
+    if bs:
+        offs[1:] = np.cumsum([len(x) for x in bs], dtype=np.uint64)
+    raw = np.frombuffer(b"".join(bs) or b"\0", np.uint8).copy()
+    return raw, offs
+
+
+# ---- Go-shaped values (packets/packets.go:172-182, topics.go:306-317) -----------------------------
+@dataclass
+class Subscription:
+    filter: str = ""
+    identifier: int = 0
+    qos: int = 0
+    no_local: bool = False
+    retain_as_published: bool = False
+    retain_handling: int = 0
+    identifiers: Optional[Dict[str, int]] = None
+
+    def merge(self, n: "Subscription") -> "Subscription":
+        """Subscription.Merge (packets/packets.go:254-274)."""
+        s = Subscription(self.filter, self.identifier, self.qos, self.no_local,
+                         self.retain_as_published, self.retain_handling,
+                         None if self.identifiers is None else self.identifiers)
+        if s.identifiers is None:
+            s.identifiers = {s.filter: s.identifier}
+        if n.identifier > 0:
+            s.identifiers[n.filter] = n.identifier
+        if n.qos > s.qos:
+            s.qos = n.qos
+        if n.no_local:
+            s.no_local = True
+        return s
+
+
+@dataclass
+class InlineSubscription:
+    filter: str = ""
+    identifier: int = 0
+
+
+@dataclass
+class Subscribers:
+    shared: Dict[str, Dict[str, Subscription]] = field(default_factory=dict)
+    shared_selected: Dict[str, Subscription] = field(default_factory=dict)
+    subscriptions: Dict[str, Subscription] = field(default_factory=dict)
+    inline_subscriptions: Dict[int, InlineSubscription] = field(default_factory=dict)
+
+    def select_shared(self):
+        """SelectShared (topics.go:320-333). Go picks the first member in random map order;
+        this picks the first in sorted order, one of the orders Go can produce."""
+        self.shared_selected = {}
+        for _, subs in sorted(self.shared.items()):
+            for client, sub in sorted(subs.items()):
+                cls = self.shared_selected.get(client, sub)
+                self.shared_selected[client] = cls.merge(sub)
+                break
+
+    def merge_shared_selected(self):
+        """MergeSharedSelected (topics.go:338-347)."""
+        for client, sub in self.shared_selected.items():
+            cls = self.subscriptions.get(client, sub)
+            self.subscriptions[client] = cls.merge(sub)
+
+
+def is_share_prefix(seg: str) -> bool:
+    """strings.EqualFold(seg, "$SHARE") with Go simple folding (U+017F ~ 's', Q9)."""
+    if len(seg) != 6:
+        return False
+    for a, b in zip(seg, SHARE_PREFIX):
+        if a == "ſ" and b == "S":
+            continue
+        if not a.isascii() or a.lower() != b.lower():
+            return False
+    return True
+
+
+class Engine:
+    """Thin object wrapper over one mq_index handle (id-level C-ABI)."""
+
+    def __init__(self, device=0, expected_subs=0, expected_nodes=0):
+        L = lib()
+        cfg = MqConfig(device, 0, expected_subs, expected_nodes)
+        h = C.c_void_p()
+        _check(L.mq_index_create(C.byref(cfg), C.byref(h)), "mq_index_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().mq_index_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def subscribe(self, filter, client_id, filter_id, qos=0, flags=0, identifier=0):
+        fb = _b(filter)
+        return _check(lib().mq_subscribe(self.h, fb, len(fb), client_id, filter_id, qos, flags,
+                                         identifier), "mq_subscribe")
+
+    def unsubscribe(self, filter, client_id):
+        fb = _b(filter)
+        return _check(lib().mq_unsubscribe(self.h, fb, len(fb), client_id), "mq_unsubscribe")
+
+    def inline_subscribe(self, filter, identifier, filter_id):
+        fb = _b(filter)
+        return _check(lib().mq_inline_subscribe(self.h, fb, len(fb), identifier, filter_id),
+                      "mq_inline_subscribe")
+
+    def inline_unsubscribe(self, filter, identifier):
+        fb = _b(filter)
+        return _check(lib().mq_inline_unsubscribe(self.h, fb, len(fb), identifier),
+                      "mq_inline_unsubscribe")
+
+    def retain_message(self, topic, handle, payload_len, retain=True):
+        tb = _b(topic)
+        out = C.c_int64()
+        _check(lib().mq_retain_message(self.h, tb, len(tb), handle, payload_len,
+                                       1 if retain else 0, C.byref(out)), "mq_retain_message")
+        return out.value
+
+    def retained_delete(self, topic):
+        tb = _b(topic)
+        return _check(lib().mq_retained_delete(self.h, tb, len(tb)), "mq_retained_delete")
+
+    def retained_len(self):
+        return int(lib().mq_retained_len(self.h))
+
+    def subscribe_bulk(self, w):
+        n = len(w["client_ids"])
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(lib().mq_subscribe_bulk(self.h, _p(w["bytes"], _u8p), _p(w["offs"], _u64p),
+                                       _p(w["client_ids"], _u32p), _p(w["filter_ids"], _u32p),
+                                       _p(w["qos"], _u8p), _p(w["flags"], _u8p),
+                                       _p(w["idents"], _i32p), n, _p(out, _u8p)),
+               "mq_subscribe_bulk")
+        return out[:n]
+
+    def retain_bulk(self, bytes_, offs, handles):
+        _check(lib().mq_retain_bulk(self.h, _p(bytes_, _u8p), _p(offs, _u64p),
+                                    _p(handles, _u64p), len(offs) - 1), "mq_retain_bulk")
+
+    def sync(self, stream=None):
+        _check(lib().mq_sync(self.h, stream), "mq_sync")
+
+    def stats(self):
+        s = Stats()
+        _check(lib().mq_index_stats(self.h, C.byref(s)), "mq_index_stats")
+        return {n: getattr(s, n) for n, _ in Stats._fields_ if n != "reserved"}
+
+    def match_batch(self, bytes_, offs):
+        """mq_match_batch -> dict of numpy arrays (host copies)."""
+        n = len(offs) - 1
+        rp = C.POINTER(MatchResult)()
+        _check(lib().mq_match_batch(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)),
+               "mq_match_batch")
+        try:
+            r = rp.contents
+            def arr(ptr, count, dtype, width):
+                if count == 0 or not ptr:
+                    return np.zeros((0, width), dtype)
+                buf = (C.c_char * (count * width * np.dtype(dtype).itemsize)).from_address(ptr)
+                return np.frombuffer(buf, dtype).reshape(count, width).copy()
+            topics = arr(r.topics, n, np.uint32, 12)
+            out = {
+                # TopicResult as u32 words: sub_base(0,1) shared_base(2,3) inline_base(4,5)
+                # sub_cap(6) n_client(7) n_ident(8) n_shared(9) n_inline(10)
+                "sub_base": topics[:, 0].astype(np.uint64) | (topics[:, 1].astype(np.uint64) << np.uint64(32)),
+                "shared_base": topics[:, 2].astype(np.uint64) | (topics[:, 3].astype(np.uint64) << np.uint64(32)),
+                "inline_base": topics[:, 4].astype(np.uint64) | (topics[:, 5].astype(np.uint64) << np.uint64(32)),
+                "sub_cap": topics[:, 6].copy(), "n_client": topics[:, 7].copy(),
+                "n_ident": topics[:, 8].copy(), "n_shared": topics[:, 9].copy(),
+                "n_inline": topics[:, 10].copy(),
+                "rows": arr(r.sub_rows, r.n_sub_rows, np.uint32, 4),
+                "shared": arr(r.shared_rows, r.n_shared_rows, np.uint32, 2),
+                "inline": arr(r.inline_rows, r.n_inline_rows, np.uint32, 2),
+            }
+        finally:
+            lib().mq_result_free(rp)
+        return out
+
+    def match_device(self, d_bytes, d_offs, n, stream=None):
+        """mq_match_device on device pointers (ints); returns the MatchResult struct."""
+        r = MatchResult()
+        _check(lib().mq_match_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_offs), n,
+                                     C.c_void_p(stream) if stream else None, C.byref(r)),
+               "mq_match_device")
+        return r
+
+    def match_chunks(self):
+        return int(lib().mq_match_chunks(self.h))
+
+    def profile(self, enable=True):
+        _check(lib().mq_profile_enable(self.h, 1 if enable else 0), "mq_profile_enable")
+
+    def profile_read(self):
+        arr = (KernelTime * 32)()
+        n = _check(lib().mq_profile_read(self.h, arr, 32), "mq_profile_read")
+        return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms)) for i in range(n)}
+
+    def profile_reset(self):
+        _check(lib().mq_profile_reset(self.h), "mq_profile_reset")
+
+
+def topic_rows(res, t):
+    """Row views of topic t from a match_batch() dict."""
+    b, cap = int(res["sub_base"][t]), int(res["sub_cap"][t])
+    nc, ni = int(res["n_client"][t]), int(res["n_ident"][t])
+    sb, ns = int(res["shared_base"][t]), int(res["n_shared"][t])
+    ib, nl = int(res["inline_base"][t]), int(res["n_inline"][t])
+    return (res["rows"][b:b + nc], res["rows"][b + cap - ni:b + cap],
+            res["shared"][sb:sb + ns], res["inline"][ib:ib + nl])
+
+
+class TopicsIndex:
+    """Mirror of the Go TopicsIndex (topics.go:349-698) over the engine's C-ABI."""
+
+    def __init__(self, device=0):
+        self.engine = Engine(device)
+        self.client_ids: Dict[str, int] = {}
+        self.clients: List[str] = []
+        self.filter_ids: Dict[str, int] = {}
+        self.filters: List[str] = []
+        self.stored: Dict[tuple, Subscription] = {}  # (client, filter) -> stored subscription
+        self.inline_stored: Dict[tuple, InlineSubscription] = {}
+        self.handles: Dict[int, object] = {}
+        self._next_handle = 1
+
+    def _cid(self, c):
+        if c not in self.client_ids:
+            self.client_ids[c] = len(self.clients)
+            self.clients.append(c)
+        return self.client_ids[c]
+
+    def _fid(self, f):
+        if f not in self.filter_ids:
+            self.filter_ids[f] = len(self.filters)
+            self.filters.append(f)
+        return self.filter_ids[f]
+
+    def subscribe(self, client: str, sub: Subscription) -> bool:  # topics.go:401
+        flags = (1 if sub.no_local else 0) | (2 if sub.retain_as_published else 0) | \
+                ((sub.retain_handling & 3) << 2)
+        r = self.engine.subscribe(sub.filter, self._cid(client), self._fid(sub.filter), sub.qos,
+                                  flags, sub.identifier)
+        self.stored[(client, sub.filter)] = Subscription(
+            sub.filter, sub.identifier, sub.qos, sub.no_local, sub.retain_as_published,
+            sub.retain_handling)
+        return r == 1
+
+    def unsubscribe(self, filter: str, client: str) -> bool:  # topics.go:423
+        return self.engine.unsubscribe(filter, self._cid(client)) == 1
+
+    def inline_subscribe(self, sub: InlineSubscription) -> bool:  # topics.go:368
+        r = self.engine.inline_subscribe(sub.filter, sub.identifier, self._fid(sub.filter))
+        self.inline_stored[(sub.identifier, sub.filter)] = sub
+        return r == 1
+
+    def inline_unsubscribe(self, identifier: int, filter: str) -> bool:  # topics.go:382
+        return self.engine.inline_unsubscribe(filter, identifier) == 1
+
+    def retain_message(self, topic: str, payload: bytes, retain: bool = True, packet=None) -> int:
+        h = self._next_handle          # topics.go:453
+        self._next_handle += 1
+        self.handles[h] = packet if packet is not None else (topic, payload)
+        return self.engine.retain_message(topic, h, len(payload), retain)
+
+    def subscribers(self, topic: str) -> Subscribers:  # topics.go:583
+        return self.subscribers_batch([topic])[0]
+
+    def subscribers_batch(self, topics) -> List[Subscribers]:
+        """The batching stage's entry point: one engine call for many topics."""
+        raw, offs = pack_strings(topics)
+        res = self.engine.match_batch(raw, offs)
+        return [self._rebuild(res, t) for t in range(len(topics))]
+
+    def _rebuild(self, res, t) -> Subscribers:
+        cli, idn, shr, inl = topic_rows(res, t)
+        out = Subscribers()
+        for c, f, ident, meta in cli:
+            client, filt = self.clients[int(c)], self.filters[int(f)]
+            base = self.stored[(client, filt)]
+            s = Subscription(filt, int(np.int32(ident)), int(meta) & META_QOS,
+                             bool(int(meta) & META_NOLOCAL), bool(int(meta) & META_RAP),
+                             (int(meta) >> META_RH_SHIFT) & 3, {filt: int(np.int32(ident))})
+            assert base.identifier == s.identifier
+            out.subscriptions[client] = s
+        for c, f, ident, _ in idn:
+            out.subscriptions[self.clients[int(c)]].identifiers[self.filters[int(f)]] = int(np.int32(ident))
+        for f, c in shr:
+            client, filt = self.clients[int(c)], self.filters[int(f)]
+            out.shared.setdefault(filt, {})[client] = self.stored[(client, filt)]
+        for ident, f in inl:
+            out.inline_subscriptions[int(np.int32(ident))] = InlineSubscription(
+                self.filters[int(f)], int(np.int32(ident)))
+        return out

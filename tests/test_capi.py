@@ -1,0 +1,115 @@
+"""CPU tests of the engine library: it loads, exports every symbol include/mqmatch.h declares,
+and its host-side update logic (Subscribe/Unsubscribe/Inline*/RetainMessage return values,
+trie shape after trims) equals the oracle on random operation sequences. No GPU is touched:
+the device image is created lazily by the first sync/match."""
+import os
+import random
+import re
+
+import pytest
+
+from mqmatch import engine as E
+import oracle as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(REPO, "include", "mqmatch.h")).read()
+    return sorted(set(re.findall(r"\b(mq_[a-z_]+)\s*\(", hdr)))
+
+
+def test_header_declares_exports_list():
+    assert declared_symbols() == sorted(E.EXPORTS)
+
+
+def test_library_exports_all_symbols():
+    L = E.lib()
+    for name in declared_symbols():
+        assert hasattr(L, name), name
+    assert L.mq_abi_version() == 1
+
+
+def test_errors_are_reported():
+    eng = E.Engine()
+    with pytest.raises(E.EngineError):
+        eng.subscribe("a/b", 1, 1, qos=3)
+
+
+SEGS = ["a", "b", "c", "", "+", "#", "$SYS", "$share", "$SHARE", "$ſhare", "g",
+        "averyveryverylongsegment", "averyveryverylongsegmenz", "x"]
+
+
+def rand_filter(r):
+    return "/".join(r.choice(SEGS) for _ in range(r.randint(1, 5)))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_update_semantics_match_oracle(seed):
+    r = random.Random(seed)
+    eng = E.Engine()
+    orc = O.OracleIndex()
+    cids, fids = {}, {}
+    cid = lambda c: cids.setdefault(c, len(cids))
+    fid = lambda f: fids.setdefault(f, len(fids))
+    clients = [f"c{i}" for i in range(6)]
+    filters = [rand_filter(r) for _ in range(40)]
+    handle = 0
+    for step in range(1500):
+        op = r.random()
+        f = r.choice(filters)
+        c = r.choice(clients)
+        if op < 0.40:
+            qos, ident, flags = r.randint(0, 2), r.choice([0, 0, 5, 77]), r.randint(0, 15)
+            a = eng.subscribe(f, cid(c), fid(f), qos, flags, ident)
+            b = orc.subscribe(c, f, qos, ident, bool(flags & 1), bool(flags & 2), (flags >> 2) & 3,
+                              client_id=cid(c), filter_id=fid(f))
+            assert bool(a) == b, (step, "subscribe", f, c)
+        elif op < 0.65:
+            a = eng.unsubscribe(f, cid(c))
+            b = orc.unsubscribe(f, c)
+            assert bool(a) == b, (step, "unsubscribe", f, c)
+        elif op < 0.75:
+            i = r.randint(1, 4)
+            assert bool(eng.inline_subscribe(f, i, fid(f))) == orc.inline_subscribe(f, i, fid(f))
+        elif op < 0.82:
+            i = r.randint(1, 4)
+            assert bool(eng.inline_unsubscribe(f, i)) == orc.inline_unsubscribe(i, f)
+        elif op < 0.95:
+            t = f.replace("+", "p").replace("#", "h") if r.random() < 0.8 else f
+            handle += 1
+            plen, ret = r.choice([0, 5]), r.random() < 0.8
+            assert eng.retain_message(t, handle, plen, ret) == orc.retain_message(t, handle, plen, ret)
+        else:
+            t = f.replace("+", "p").replace("#", "h")
+            eng.retained_delete(t)
+            orc.retained_delete(t)
+        assert eng.retained_len() == orc.retained_len()
+        if step % 50 == 0:
+            assert eng.stats()["nodes"] == orc.particle_count(), step
+    assert eng.stats()["nodes"] == orc.particle_count()
+
+
+def test_bulk_subscribe_matches_oracle():
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(20000, 2000)
+    eng = E.Engine()
+    orc = O.OracleIndex()
+    a = eng.subscribe_bulk(w)
+    b = orc.subscribe_bulk(w)
+    assert (a == b).all()
+    st = eng.stats()
+    assert st["nodes"] == orc.particle_count()
+    assert st["subs"] + st["shared"] == int(a.sum())
+
+
+def test_unsubscribe_everything_empties_trie():
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(3000, 300, seed=7)
+    eng = E.Engine()
+    eng.subscribe_bulk(w)
+    fs = W.strings(w["bytes"], w["offs"])
+    for i, f in enumerate(fs):
+        eng.unsubscribe(f, int(w["client_ids"][i]))
+    st = eng.stats()
+    assert st["nodes"] == 0 and st["subs"] == 0 and st["shared"] == 0 and st["subs_merge"] == 0

@@ -1,0 +1,212 @@
+"""Parity of the HIP path (through the C-ABI) with the oracle, bit-exact on ids.
+
+Small cases compare the rematerialised Go-shaped Subscribers maps topic by topic; workload-scale
+cases compare per-topic canonical digests of every row (tests/digest.py). Edge cases follow the
+reference's tests and quirk register: empty topics, '$' topics, empty
+levels, literal '+'/'#' topic levels, long (hashed) segments, deep topics, Unicode $share,
+inline last-write, incremental updates between batches, chunked outputs.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from adapters import EngineAdapter, OracleAdapter, canonical
+from digest import engine_digests
+from kat_cases import KATS
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kat", KATS, ids=lambda f: f.__name__)
+def test_engine_kat(kat, gpu_available):
+    kat(EngineAdapter)
+
+
+SEGS = ["a", "b", "c", "", "+", "#", "$SYS", "$share", "$SHARE", "$ſhare", "g", "sport",
+        "averyveryverylongsegment", "averyveryverylongsegmenz", "x", "ü"]
+TSEGS = ["a", "b", "c", "", "$SYS", "$share", "g", "sport", "averyveryverylongsegment",
+         "averyveryverylongsegmenz", "x", "ü", "$x"]
+
+
+def rand_filter(r, segs=SEGS):
+    return "/".join(r.choice(segs) for _ in range(r.randint(1, 5)))
+
+
+def build_pair(r, n_subs, n_clients, n_inline=0):
+    e, o = EngineAdapter(), OracleAdapter()
+    for _ in range(n_subs):
+        f = rand_filter(r)
+        c = f"c{r.randrange(n_clients)}"
+        kw = dict(qos=r.randint(0, 2), identifier=r.choice([0, 0, 3, 9, 200]),
+                  no_local=r.random() < 0.2, rap=r.random() < 0.5, rh=r.randint(0, 2))
+        assert e.subscribe(c, f, **kw) == o.subscribe(c, f, **kw)
+    for _ in range(n_inline):
+        f, i = rand_filter(r), r.randint(1, 6)
+        assert e.inline_subscribe(f, i) == o.inline_subscribe(f, i)
+    return e, o
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_small_parity(seed, gpu_available):
+    r = random.Random(1000 + seed)
+    e, o = build_pair(r, 300, 12, n_inline=40)
+    topics = ["/".join(r.choice(TSEGS) for _ in range(r.randint(1, 6))) for _ in range(400)]
+    topics += ["", "a", "a/", "/", "//", "$SYS", "a/+", "+", "#", "a/#", "+/+", "a/b/c/+/#"]
+    got = e.subscribers_batch(topics)
+    for t, g in zip(topics, got):
+        assert g == o.subscribers(t), t
+
+
+def test_single_topic_batches_and_empty_batch(gpu_available):
+    e, o = build_pair(random.Random(5), 100, 5)
+    for t in ["a/b", "", "$SYS/x", "sport/a"]:
+        assert e.subscribers(t) == o.subscribers(t), t
+    assert e.subscribers_batch([]) == []
+
+
+def test_deep_and_long_topics(gpu_available):
+    e, o = EngineAdapter(), OracleAdapter()
+    deep = "/".join(f"l{i}" for i in range(60))
+    for f in [deep, deep[:200] + "/#", "/".join(["+"] * 60), "l0/#", "#",
+              "x" * 300, "x" * 300 + "/+", "a/" + "y" * 1000]:
+        for c in ("c1", "c2"):
+            assert e.subscribe(c, f, identifier=len(f) % 7) == o.subscribe(c, f, identifier=len(f) % 7)
+    topics = [deep, deep[:200], "/".join(f"l{i}" for i in range(61)), "x" * 300, "x" * 300 + "/q",
+              "x" * 299, "a/" + "y" * 1000, "a/" + "y" * 999 + "z"]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t[:40]
+
+
+def test_long_segment_hash_verification(gpu_available):
+    """Segments > 15 bytes are hashed; a hit is verified byte for byte (no false matches)."""
+    e, o = EngineAdapter(), OracleAdapter()
+    base = "s" * 40
+    for i in range(50):
+        f = base + str(i) + "/v"
+        e.subscribe("c", f)
+        o.subscribe("c", f)
+    topics = [base + str(i) + "/v" for i in range(60)] + [base + "x/v", base[:-1] + "/v"]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
+
+
+def test_unicode_share_prefix(gpu_available):
+    e, o = EngineAdapter(), OracleAdapter()
+    for f in ["$ſhare/g/a/b", "$SHARE/g/a/b", "$share/h/a/+", "$Share/g/a/#", "$ſhar/g/a/b",
+              "$sharE/g", "$share"]:
+        assert e.subscribe("c1", f) == o.subscribe("c1", f)
+        assert e.subscribe("c2", f) == o.subscribe("c2", f)
+    for t in ["a/b", "a", "g", "$share", "$ſhar/g/a/b"]:
+        assert e.subscribers(t) == o.subscribers(t), t
+
+
+def test_inline_last_write_wins(gpu_available):
+    e, o = EngineAdapter(), OracleAdapter()
+    for f, i in [("a/b", 1), ("a/+", 1), ("#", 1), ("a/#", 2), ("+/b", 2), ("a/b", 3), ("a/b/#", 3)]:
+        assert e.inline_subscribe(f, i) == o.inline_subscribe(f, i)
+    for t in ["a/b", "a", "a/b/c", "x/b", "$SYS/b"]:
+        assert e.subscribers(t) == o.subscribers(t), t
+
+
+def test_dollar_rule_shared_and_inline_not_excluded(gpu_available):
+    """Q3: the '$' rule drops only non-shared subscriptions whose filter starts with a wildcard."""
+    e, o = EngineAdapter(), OracleAdapter()
+    for c, f in [("c1", "#"), ("c2", "+/info"), ("c3", "$share/g/#"), ("c4", "$share/g/+/info"),
+                 ("c5", "$SYS/#"), ("c6", "+abc/info")]:
+        e.subscribe(c, f)
+        o.subscribe(c, f)
+    e.inline_subscribe("#", 9)
+    o.inline_subscribe("#", 9)
+    for t in ["$SYS/info", "$foo/info", "x/info", "+abc/info"]:
+        assert e.subscribers(t) == o.subscribers(t), t
+
+
+def _workload_pair(n_subs, n_clients, seed):
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(n_subs, n_clients, seed=seed)
+    eng = E.Engine()
+    orc = O.OracleIndex()
+    assert (eng.subscribe_bulk(w) == orc.subscribe_bulk(w)).all()
+    return w, eng, orc
+
+
+def _digest_parity(eng, orc, tb, to):
+    res = eng.match_batch(tb, to)
+    dg, cnt = engine_digests(res)
+    od, ocnt, _ = orc.digest_batch(tb, to, nthreads=os.cpu_count() or 8)
+    bad = np.nonzero(dg != od)[0]
+    assert len(bad) == 0, f"{len(bad)} topics differ, first {bad[:5]}, counts {cnt[bad[:3]]} vs {ocnt[bad[:3]]}"
+    return cnt
+
+
+@pytest.mark.parametrize("n_subs,n_clients,n_topics", [(10000, 1000, 20000), (200000, 20000, 20000)])
+def test_workload_digest_parity(n_subs, n_clients, n_topics, gpu_available):
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(n_subs, n_clients, seed=11)
+    tb, to = W.gen_topics(w, n_topics, seed=12)
+    cnt = _digest_parity(eng, orc, tb, to)
+    assert cnt[:, 0].sum() > n_topics  # the workload really fans out
+
+
+def test_iot_workload_parity(gpu_available):
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(50000, 50000, seed=21, mix=W.MIX_IOT)
+    from mqmatch import engine as E
+    eng, orc = E.Engine(), O.OracleIndex()
+    eng.subscribe_bulk(w)
+    orc.subscribe_bulk(w)
+    tb, to = W.gen_topics(w, 20000, seed=22, mix=W.MIX_IOT)
+    _digest_parity(eng, orc, tb, to)
+
+
+def test_incremental_updates_between_batches(gpu_available):
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(30000, 3000, seed=31)
+    tb, to = W.gen_topics(w, 5000, seed=32)
+    _digest_parity(eng, orc, tb, to)
+    fs = W.strings(w["bytes"], w["offs"])
+    r = random.Random(33)
+    for _ in range(3):
+        for _ in range(2000):  # unsubscribe / resubscribe / new subscriptions
+            i = r.randrange(len(fs))
+            c = int(w["client_ids"][i])
+            if r.random() < 0.5:
+                assert bool(eng.unsubscribe(fs[i], c)) == orc.unsubscribe(fs[i], f"c{c:07d}")
+            else:
+                c2 = r.randrange(3000)
+                fid = int(w["filter_ids"][i])
+                a = eng.subscribe(fs[i], c2, fid, 1, 0, 7)
+                b = orc.subscribe(f"c{c2:07d}", fs[i], 1, 7, client_id=c2, filter_id=fid)
+                assert bool(a) == b
+        st = eng.stats()
+        _digest_parity(eng, orc, tb, to)
+    assert st["upload_bytes_total"] > 0
+
+
+def test_chunked_outputs(gpu_available, monkeypatch):
+    from mqmatch import workload as W
+    monkeypatch.setenv("MQ_CHUNK_ROWS", "200000")
+    w, eng, orc = _workload_pair(50000, 5000, seed=41)
+    tb, to = W.gen_topics(w, 30000, seed=42)
+    _digest_parity(eng, orc, tb, to)
+    assert eng.match_chunks() > 1
+
+
+def test_match_device_stream(gpu_available):
+    """mq_match_device on torch-owned device buffers and a torch stream."""
+    import torch
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(20000, 2000, seed=51)
+    tb, to = W.gen_topics(w, 4096, seed=52)
+    d_tb = torch.from_numpy(tb).cuda()
+    d_to = torch.from_numpy(to.view(np.int64)).cuda()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        r = eng.match_device(d_tb.data_ptr(), d_to.data_ptr(), len(to) - 1, s.cuda_stream)
+    s.synchronize()
+    host = eng.match_batch(tb, to)
+    assert r.n_topics == len(to) - 1 and r.n_sub_rows == len(host["rows"])
