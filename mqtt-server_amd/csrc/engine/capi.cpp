@@ -210,16 +210,42 @@ uint32_t mq_match_chunks(const mq_index* idx) {
   return idx && idx->dev ? idx->dev->last_chunks() : 0;
 }
 
-int mq_messages_batch(mq_index* idx, const uint8_t*, const uint64_t*, uint32_t, mq_msg_result** out) {
-  (void)idx;
-  if (out) *out = nullptr;
-  return fail(MQ_EINVAL, "mq_messages_batch: not implemented yet");
+int mq_messages_batch(mq_index* idx, const uint8_t* fb, const uint64_t* fo, uint32_t n, mq_msg_result** out) {
+  if (!out || (n && (!fo || (!fb && fo[n] != 0)))) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    Device& d = idx->device();
+    std::unique_ptr<MsgHolder> h(new MsgHolder());
+    const uint8_t* dfb = nullptr;
+    const uint64_t* dfo = nullptr;
+    if (n) d.stage_inputs(fb, fo, n, nullptr, &dfb, &dfo);
+    mq_msg_result dev_out;
+    HostMsg hm;
+    d.messages(*idx->ix, dfb, dfo, n, nullptr, &hm, &dev_out);
+    h->base.swap(hm.base);
+    h->count.swap(hm.count);
+    h->handles.swap(hm.handles);
+    mq_msg_result& r = h->pub;
+    r = mq_msg_result{};
+    r.n_filters = n;
+    r.base = h->base.data();
+    r.count = h->count.data();
+    r.handles = h->handles.data();
+    r.n_handles = h->handles.size();
+    *out = &h->pub;
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    g_results[&h->pub] = 2;
+    h.release();
+    return 0;
+  });
 }
 
-int mq_messages_device(mq_index* idx, const uint8_t*, const uint64_t*, uint32_t, void*, mq_msg_result* out) {
-  (void)idx;
-  (void)out;
-  return fail(MQ_EINVAL, "mq_messages_device: not implemented yet");
+int mq_messages_device(mq_index* idx, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, void* stream,
+                       mq_msg_result* out) {
+  if (!out || (n && !d_fo)) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    idx->device().messages(*idx->ix, d_fb, d_fo, n, (hipStream_t)stream, nullptr, out);
+    return 0;
+  });
 }
 
 void mq_result_free(void* r) {

@@ -144,7 +144,7 @@ Device::~Device() {
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_})
+                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_})
     b->release();
 }
 
@@ -347,6 +347,61 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     out->n_sub_rows = hi.rows - lo.rows;
     out->n_shared_rows = hi.shr - lo.shr;
     out->n_inline_rows = hi.inl - lo.inl;
+  }
+}
+
+void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
+                      hipStream_t s, HostMsg* host, mq_msg_result* out) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  sync(ix, s);
+  *out = mq_msg_result{};
+  if (host) *host = HostMsg{};
+  if (!err_.p) {
+    err_.ensure(sizeof(uint32_t));
+    hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
+  }
+  check_err(s);
+  if (n == 0) return;
+  const DevIndex di = dev_index(ix);
+  const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+  counts_.ensure((size_t)n * sizeof(TopicCount));
+  offs_.ensure((size_t)(n + 1) * sizeof(TopicOff));
+  bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+  bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+  prof.begin(s);
+  launch_msg(false, d_fb, d_fo, n, di, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, s);
+  prof.end("msg_count", s);
+  hip_check(hipGetLastError(), "k_msg<count>");
+  launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
+  hip_check(hipGetLastError(), "k_scan");
+  TopicOff tot;
+  hip_check(hipMemcpyAsync(&tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H total");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  check_err(s);
+  msg_handles_.ensure(std::max<uint64_t>(tot.rows, 1) * sizeof(uint64_t));
+  msg_base_.ensure((size_t)n * sizeof(uint64_t));
+  msg_count_.ensure((size_t)n * sizeof(uint32_t));
+  prof.begin(s);
+  launch_msg(true, d_fb, d_fo, n, di, nullptr, offs_.as<TopicOff>(), msg_handles_.as<uint64_t>(),
+             msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), s);
+  prof.end("msg_fill", s);
+  hip_check(hipGetLastError(), "k_msg<fill>");
+  out->n_filters = n;
+  out->base = msg_base_.as<uint64_t>();
+  out->count = msg_count_.as<uint32_t>();
+  out->handles = msg_handles_.as<uint64_t>();
+  out->n_handles = tot.rows;
+  if (host) {
+    host->base.resize(n);
+    host->count.resize(n);
+    host->handles.resize(tot.rows);
+    hip_check(hipMemcpyAsync(host->base.data(), msg_base_.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s), "D2H");
+    hip_check(hipMemcpyAsync(host->count.data(), msg_count_.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+    if (tot.rows)
+      hip_check(hipMemcpyAsync(host->handles.data(), msg_handles_.p, tot.rows * sizeof(uint64_t),
+                               hipMemcpyDeviceToHost, s), "D2H handles");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    check_err(s);
   }
 }
 

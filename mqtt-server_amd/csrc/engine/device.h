@@ -37,6 +37,13 @@ struct DevMirror {
   void release();
 };
 
+// Host-side destination of a Messages batch (mq_messages_batch).
+struct HostMsg {
+  std::vector<uint64_t> base;
+  std::vector<uint32_t> count;
+  std::vector<uint64_t> handles;
+};
+
 // Host-side destination of a batch's results (mq_match_batch).
 struct HostMatch {
   std::vector<mq_topic_result> topics;
@@ -84,6 +91,9 @@ class Device {
   // when `host` is set every chunk's rows are also copied into it (global offsets).
   void match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
              HostMatch* host, mq_match_result* out);
+  // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
+  void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
+                HostMsg* host, mq_msg_result* out);
   // Copy host topics to the device input buffers and return their device pointers.
   void stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hipStream_t s,
                     const uint8_t** d_tb, const uint64_t** d_to);
@@ -116,6 +126,7 @@ class Device {
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   DevBuf rows_, shr_rows_, inl_rows_, tab_, res_, err_;
+  DevBuf msg_handles_, msg_base_, msg_count_;
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;
   uint64_t empty_handle_ = 0;

@@ -299,6 +299,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   if (h.str == 1) walk.at_w(parent).hash_child = id;
   NodeMsg& pm = msg.at_w(parent);
   h.child_pos = pm.child_cnt;
+  msg.h[id].child_pos = pm.child_cnt;
   list_push(children, pm.child_off, pm.child_cnt, nh_[parent].child_cap, id);
   nh_[parent].n_children++;
   n_live_nodes_++;
@@ -315,6 +316,7 @@ void Index::remove_node(uint32_t n) {
   uint32_t last = children.m.h[pm.child_off + pm.child_cnt - 1];
   children.m.at_w(pm.child_off + h.child_pos) = last;
   nh_[last].child_pos = h.child_pos;
+  msg.at_w(last).child_pos = h.child_pos;
   pm.child_cnt--;
   children.live--;
   nh_[p].n_children--;

@@ -64,5 +64,8 @@ void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, c
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_emit(const EmitArgs& a, hipStream_t s);
+void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
+                uint32_t* count, hipStream_t s);
 
 }  // namespace mq

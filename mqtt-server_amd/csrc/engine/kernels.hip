@@ -494,4 +494,143 @@ void launch_emit(const EmitArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_emit, dim3((waves + 3) / 4), dim3(256), 0, s, a);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// k_msg: Messages(filter), the reverse retained scan (topics.go:525-579). One thread per filter.
+// The recursion is a depth-first walk without a stack: a frame is (node, level d); a '+'/'#'
+// level enumerates the node's children slab and, after returning from child c, resumes at
+// c's slab position + 1 (NodeMsg.child_pos). Levels past the last segment repeat it
+// (isolateParticle, topics.go:679-698), which is how a trailing '#' covers the subtree.
+// FILL=false counts the packets per filter; FILL=true writes their handles.
+// ---------------------------------------------------------------------------------------------
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
+                                             const uint64_t* __restrict__ fo, uint32_t n,
+                                             DevIndex ix, TopicCount* __restrict__ cnt,
+                                             const TopicOff* __restrict__ off,
+                                             uint64_t* __restrict__ handles,
+                                             uint64_t* __restrict__ base_out,
+                                             uint32_t* __restrict__ count_out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t b0 = fo[t], b1 = fo[t + 1];
+  uint32_t c = 0;
+  uint64_t* out = FILL ? handles + off[t].rows : nullptr;
+  auto emit = [&](uint64_t h) {
+    if (FILL) out[c] = h;
+    c++;
+  };
+  // len(filter) == 0 || Retained.Len() == 0 (topics.go:535)
+  if (b1 > b0 && ix.retained_len != 0) {
+    bool wild = false;
+    for (uint64_t i = b0; i < b1; i++) wild |= (fb[i] == '+') | (fb[i] == '#');
+    if (!wild) {
+      // no wildcard: Retained.Get(filter) (topics.go:539-544)
+      uint32_t node = kRoot;
+      uint64_t s = b0;
+      for (;;) {
+        const uint64_t e = find_slash(fb, s, b1);
+        const uint32_t len = (uint32_t)(e - s);
+        node = lookup(ix, node, seg_key(fb + s, len), fb + s, len);
+        if (node == kNone || e >= b1) break;
+        s = e + 1;
+      }
+      if (node != kNone) {
+        const NodeMsg m = ix.msg[node];
+        if (m.flags & kRetainLive) emit(m.handle);
+      }
+    } else {
+      uint32_t node = kRoot, d = 0, wd = 0;  // wd: level of the segment in the window
+      uint64_t s = b0, e = find_slash(fb, b0, b1);
+      uint32_t cursor = 0;
+      bool resume = false;  // re-entering an enumeration frame after a child returned
+      for (uint64_t guard = 0;; guard++) {
+        if (guard > kWalkGuard * 64) {
+          atomicOr(ix.err, kErrWalkGuard);
+          break;
+        }
+        const bool has_next = (wd == d) && (e < b1);
+        const uint32_t len = (uint32_t)(e - s);
+        const bool plus = len == 1 && fb[s] == '+';
+        const bool hash = len == 1 && fb[s] == '#';
+        bool descended = false;
+        if (plus || hash) {  // topics.go:547-565
+          const NodeMsg nm = ix.msg[node];
+          if (!resume) cursor = 0;
+          while (cursor < nm.child_cnt) {
+            const uint32_t ch = ix.children[nm.child_off + cursor];
+            cursor++;
+            const NodeMsg cm = ix.msg[ch];
+            if (d == 0 && cm.key_sys) continue;  // only the exact $SYS particle, level 0 (Q4)
+            if (!has_next && (cm.flags & kRetainPath) && (cm.flags & kRetainLive)) emit(cm.handle);
+            if (has_next || hash) {
+              node = ch;
+              d++;
+              if (e < b1) {
+                s = e + 1;
+                e = find_slash(fb, s, b1);
+                wd++;
+              }
+              descended = true;
+              break;
+            }
+          }
+        } else if (!resume) {  // literal level (topics.go:568-576)
+          const uint32_t p = lookup(ix, node, seg_key(fb + s, len), fb + s, len);
+          if (p != kNone) {
+            if (has_next) {
+              node = p;
+              d++;
+              s = e + 1;
+              e = find_slash(fb, s, b1);
+              wd++;
+              descended = true;
+            } else {
+              const NodeMsg m = ix.msg[p];
+              if (m.flags & kRetainPath) {
+                if (m.flags & kRetainLive) emit(m.handle);
+              } else if (ix.empty_topic_live) {
+                emit(ix.empty_topic_handle);  // Retained.Get("") on a particle without a path (Q6)
+              }
+            }
+          }
+        }
+        if (descended) {
+          resume = false;
+          continue;
+        }
+        // frame finished: return to the parent frame
+        if (d == 0) break;
+        const NodeMsg cm = ix.msg[node];
+        node = ix.walk[node].parent_flags & kParentMask;
+        if (wd == d) {
+          e = s - 1;
+          s = seg_start_before(fb, b0, e);
+          wd--;
+        }
+        d--;
+        cursor = cm.child_pos + 1;
+        resume = true;
+      }
+    }
+  }
+  if (!FILL) {
+    cnt[t] = TopicCount{0, c, 0, 0, 0};
+  } else {
+    base_out[t] = off[t].rows;
+    count_out[t] = c;
+  }
+}
+
+void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
+                uint32_t* count, hipStream_t s) {
+  if (!n) return;
+  dim3 grid((n + 255) / 256);
+  if (fill)
+    hipLaunchKernelGGL(k_msg<true>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count);
+  else
+    hipLaunchKernelGGL(k_msg<false>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count);
+}
+
 }  // namespace mq

@@ -110,7 +110,8 @@ struct NodeMsg {
   uint32_t flags;                 // kRetainPath | kRetainLive
   uint32_t depth;
   uint64_t handle;                // retained packet handle when kRetainLive
-  uint32_t key_sys, pad;          // key == "$SYS" (topics.go:549)
+  uint32_t key_sys;               // key == "$SYS" under the root (topics.go:549)
+  uint32_t child_pos;             // position in the parent's children slab
 };
 
 struct SegInfo {  // long segment bytes in the segment pool

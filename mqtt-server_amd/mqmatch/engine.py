@@ -334,6 +334,33 @@ class Engine:
             lib().mq_result_free(rp)
         return out
 
+    def messages_batch(self, bytes_, offs):
+        """mq_messages_batch -> list of sorted handle arrays, one per filter."""
+        n = len(offs) - 1
+        rp = C.POINTER(MsgResult)()
+        _check(lib().mq_messages_batch(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)),
+               "mq_messages_batch")
+        try:
+            r = rp.contents
+            def arr(ptr, count, dtype):
+                if count == 0 or not ptr:
+                    return np.zeros(0, dtype)
+                buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+                return np.frombuffer(buf, dtype).copy()
+            base = arr(r.base, n, np.uint64)
+            count = arr(r.count, n, np.uint32)
+            hs = arr(r.handles, r.n_handles, np.uint64)
+        finally:
+            lib().mq_result_free(rp)
+        return base, count, hs
+
+    def messages_device(self, d_bytes, d_offs, n, stream=None):
+        r = MsgResult()
+        _check(lib().mq_messages_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_offs), n,
+                                        C.c_void_p(stream) if stream else None, C.byref(r)),
+               "mq_messages_device")
+        return r
+
     def match_device(self, d_bytes, d_offs, n, stream=None):
         """mq_match_device on device pointers (ints); returns the MatchResult struct."""
         r = MatchResult()
@@ -419,6 +446,15 @@ class TopicsIndex:
         self._next_handle += 1
         self.handles[h] = packet if packet is not None else (topic, payload)
         return self.engine.retain_message(topic, h, len(payload), retain)
+
+    def messages(self, filter: str):  # topics.go:525 — retained handles (set semantics)
+        return self.messages_batch([filter])[0]
+
+    def messages_batch(self, filters):
+        raw, offs = pack_strings(filters)
+        base, count, hs = self.engine.messages_batch(raw, offs)
+        return [sorted(int(x) for x in hs[int(base[i]):int(base[i]) + int(count[i])])
+                for i in range(len(filters))]
 
     def subscribers(self, topic: str) -> Subscribers:  # topics.go:583
         return self.subscribers_batch([topic])[0]

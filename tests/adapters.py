@@ -112,3 +112,6 @@ class EngineAdapter:
 
     def messages(self, filter):
         return self.x.messages(filter)
+
+    def messages_batch(self, filters):
+        return self.x.messages_batch(filters)

@@ -14,13 +14,13 @@ import pytest
 
 from adapters import EngineAdapter, OracleAdapter, canonical
 from digest import engine_digests
-from kat_cases import KATS
+from kat_cases import KATS, MESSAGE_KATS
 import oracle as O
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kat", KATS, ids=lambda f: f.__name__)
+@pytest.mark.parametrize("kat", KATS + MESSAGE_KATS, ids=lambda f: f.__name__)
 def test_engine_kat(kat, gpu_available):
     kat(EngineAdapter)
 
@@ -210,3 +210,66 @@ def test_match_device_stream(gpu_available):
     s.synchronize()
     host = eng.match_batch(tb, to)
     assert r.n_topics == len(to) - 1 and r.n_sub_rows == len(host["rows"])
+
+
+MSEGS = ["a", "b", "c", "", "$SYS", "$share", "g", "x", "averyveryverylongsegment", "ü", "$x"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_messages_random_parity(seed, gpu_available):
+    """Messages (topics.go:525-579) on random retained sets, including Q4 ($SYS at level 0
+    only), Q5 (x/# excludes x), Q6 (particles without a retain path), Q12 (expired entries)."""
+    r = random.Random(2000 + seed)
+    topics = ["/".join(r.choice(MSEGS) for _ in range(r.randint(1, 5))) for _ in range(300)]
+    e, o = EngineAdapter(), OracleAdapter()
+    for i, t in enumerate(topics):
+        pl = b"" if r.random() < 0.1 else b"p"
+        ret = r.random() < 0.9
+        a, _ = e.retain_message(t, pl, ret, handle=i + 1)
+        b, _ = o.retain_message(t, pl, ret, handle=i + 1)
+        assert a == b, t
+    for t in topics[::13]:  # expiry sweep deletes map entries only (Q12)
+        e.retained_delete(t)
+        o.retained_delete(t)
+    for f in ["a/b", "q", "x/y"]:  # subscription-only particles (no retain path)
+        e.subscribe("c", f)
+        o.subscribe("c", f)
+    filters = ["/".join(r.choice(MSEGS + ["+", "+", "#"]) for _ in range(r.randint(1, 5)))
+               for _ in range(300)]
+    filters += ["#", "+", "+/+", "$SYS/#", "$SYS/+", "a/#", "a/+/#", "", "a", "a/b", "#/a",
+                "+/#", "a/#/b"]
+    got = e.messages_batch(filters)
+    for f, g in zip(filters, got):
+        assert g == o.messages(f), f
+
+
+def test_messages_empty_topic_retained(gpu_available):
+    """Q6: a retained packet on topic "" is returned for literal-final particles without a
+    retain path (topics.go:573)."""
+    e, o = EngineAdapter(), OracleAdapter()
+    for ix in (e, o):
+        ix.retain_message("", b"p", True, handle=99)
+        ix.retain_message("a/b", b"p", True, handle=5)
+        ix.subscribe("c", "a/c")
+    for f in ["a/+", "+/c", "a/c", "+/+", "#", "a/b"]:
+        assert e.messages(f) == o.messages(f), f
+
+
+def test_messages_workload_parity(gpu_available):
+    from mqmatch import workload as W
+    from mqmatch import engine as E
+    rb, ro, hd, rh = W.gen_retained(100000, n_sys=1000, seed=61)
+    fb, fo = W.gen_msg_filters(rh, 5000, seed=62)
+    eng, orc = E.Engine(), O.OracleIndex()
+    eng.retain_bulk(rb, ro, hd)
+    orc.retain_bulk(rb, ro, hd)
+    base, count, hs = eng.messages_batch(fb, fo)
+    od, ocnt, _ = orc.messages_digest_batch(fb, fo)
+    assert (count == ocnt).all()
+    from digest import fold, SEED
+    for i in range(len(count)):
+        h = np.sort(hs[int(base[i]):int(base[i]) + int(count[i])])
+        d = fold(SEED, np.uint64(len(h)))
+        for x in h:
+            d = fold(d, x)
+        assert d == od[i], i
