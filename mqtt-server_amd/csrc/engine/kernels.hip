@@ -310,10 +310,53 @@ __device__ __forceinline__ uint32_t prefix_before(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
 }
 
+// Exclusive wave-wide prefix sum (64 lanes); *total receives the sum.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t* total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// Copy the concatenation of up to 64 record lists (list j: `cnt_j` records at src + off[j],
+// exclusive prefix pre[j], pre[64] = total) to dst[0, total): 64 consecutive rows per
+// wave-instruction, four in flight per lane. Each lane keeps a cursor j that only advances.
+template <class V>
+__device__ __forceinline__ void copy_lists(V* __restrict__ dst, const V* __restrict__ src,
+                                           const uint32_t* __restrict__ off,
+                                           const uint32_t* __restrict__ pre, uint32_t total,
+                                           uint32_t lane) {
+  uint32_t j = 0;
+  for (uint32_t r0 = 0; r0 < total; r0 += 256) {
+    V v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = r0 + k * 64 + lane;
+      if (r < total) {
+        while (pre[j + 1] <= r) j++;
+        v[k] = src[off[j] + (r - pre[j])];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = r0 + k * 64 + lane;
+      if (r < total) dst[r] = v[k];
+    }
+  }
+}
+
+constexpr uint32_t kGroup = 64;  // gathers staged per pass: one per lane
+
 __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   __shared__ uint32_t lds_key[4][kLdsTab];
   __shared__ uint32_t lds_row[4][kLdsTab];
   __shared__ uint32_t lds_meta[4][kLdsTab];
+  __shared__ uint32_t g_off[3][4][kGroup];      // direct-sub / shared / inline list offsets
+  __shared__ uint32_t g_pre[3][4][kGroup + 1];  // their exclusive prefixes (+ total)
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t t = a.t0 + blockIdx.x * 4 + wv;
   if (t >= a.t1) return;  // wave-uniform
@@ -341,81 +384,103 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   bool tab_ready = false;
 
   uint32_t n_cli = 0, n_ext = 0, n_shr = 0, n_inl = 0;
-  for (uint64_t g = o0.g; g < o1.g; g++) {
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(a.gathers[g]);
-    const uint32_t node = gw & kGatherNode;
-    const NodeLists L = a.ix.lists[node];
-    if (gw & kGatherSubs) {
-      // subscriptions that cannot merge: straight copy into client rows
-      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.ix.subs + L.sub_off);
-      uint4* __restrict__ dst = reinterpret_cast<uint4*>(rows + n_cli);
-      uint32_t i = lane;
-      for (; i + 192 < L.n_direct; i += 256) {
-        uint4 x0 = src[i], x1 = src[i + 64], x2 = src[i + 128], x3 = src[i + 192];
-        dst[i] = x0;
-        dst[i + 64] = x1;
-        dst[i + 128] = x2;
-        dst[i + 192] = x3;
+  for (uint64_t g0 = o0.g; g0 < o1.g; g0 += kGroup) {
+    // Stage up to 64 gathers at once (one per lane): the gather word and the node's lists.
+    const uint32_t ng = (uint32_t)min<uint64_t>(kGroup, o1.g - g0);
+    uint32_t dn = 0, mn = 0, sn = 0, in = 0, sub_off = 0, shr_off = 0, inl_off = 0;
+    if (lane < ng) {
+      const uint32_t gw = a.gathers[g0 + lane];
+      const NodeLists L = a.ix.lists[gw & kGatherNode];
+      if (gw & kGatherSubs) {
+        dn = L.n_direct;
+        mn = L.n_merge;
       }
-      for (; i < L.n_direct; i += 64) dst[i] = src[i];
-      n_cli += L.n_direct;
+      sub_off = L.sub_off;
+      sn = L.shr_cnt;
+      shr_off = L.shr_off;
+      if (gw & kGatherInline) {
+        in = L.inl_cnt;
+        inl_off = L.inl_off;
+      }
+    }
+    uint32_t dt, st, it;
+    const uint32_t dp = wave_excl_scan(dn, lane, &dt);
+    const uint32_t sp = wave_excl_scan(sn, lane, &st);
+    const uint32_t ip = wave_excl_scan(in, lane, &it);
+    g_off[0][wv][lane] = sub_off;
+    g_off[1][wv][lane] = shr_off;
+    g_off[2][wv][lane] = inl_off;
+    g_pre[0][wv][lane] = dp;
+    g_pre[1][wv][lane] = sp;
+    g_pre[2][wv][lane] = ip;
+    if (lane == 0) {
+      g_pre[0][wv][kGroup] = dt;
+      g_pre[1][wv][kGroup] = st;
+      g_pre[2][wv][kGroup] = it;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 
-      // subscriptions that may merge with another of the same client
-      if (L.n_merge) {
-        if (!tab_ready) {
-          for (uint32_t k = lane; k <= T.mask; k += 64) T.key[k] = kTabEmpty;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          tab_ready = true;
-        }
-        const SubRec* __restrict__ ms = a.ix.subs + L.sub_off + L.n_direct;
-        for (uint32_t i0 = 0; i0 < L.n_merge; i0 += 64) {
-          const uint32_t j = i0 + lane;
-          const bool v = j < L.n_merge;
-          SubRec r{0, 0, 0, 0};
-          uint32_t slot = 0;
-          bool is_new = false;
-          if (v) {
-            r = ms[j];
-            r.meta &= ~kMetaMergeBit;
-            slot = tab_insert(T, r.client, &is_new, a.ix.err);
-          }
-          const uint64_t bn = __ballot(v && is_new);
-          if (v && is_new) {  // first (minimum-rank) subscription of this client: the base
-            const uint32_t pos = n_cli + prefix_before(bn);
-            rows[pos] = r;
-            T.row[slot] = pos;
-            T.meta[slot] = r.meta;
-          }
-          n_cli += __popcll(bn);
-          const bool dup = v && !is_new;
-          if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
-            const uint32_t m = T.meta[slot];
-            const uint32_t q = max(m & kMetaQos, r.meta & kMetaQos);
-            const uint32_t nm = (m & ~kMetaQos) | q | (r.meta & kMetaNoLocal);
-            if ((nm & ~kMetaDirty) != (m & ~kMetaDirty)) T.meta[slot] = nm | kMetaDirty;
-          }
-          const uint64_t be = __ballot(dup && r.ident > 0);
-          if (dup && r.ident > 0) {  // Identifiers[n.Filter] = n.Identifier (id > 0)
-            const uint32_t k = n_ext + prefix_before(be);
-            SubRec x{r.client, r.filter_id, r.ident, 0};
-            rows[cap - 1 - k] = x;
-          }
-          n_ext += __popcll(be);
-        }
-      }
-    }
+    // Subscriptions that can never merge: one flat coalesced copy into client rows.
+    copy_lists(reinterpret_cast<uint4*>(rows + n_cli), reinterpret_cast<const uint4*>(a.ix.subs),
+               g_off[0][wv], g_pre[0][wv], dt, lane);
+    n_cli += dt;
     // Shared[sub.Filter][client] = sub (topics.go:656-663)
-    {
-      const uint2* __restrict__ src = reinterpret_cast<const uint2*>(a.ix.shr + L.shr_off);
-      uint2* __restrict__ dst = reinterpret_cast<uint2*>(a.shr_rows + sb + n_shr);
-      for (uint32_t i = lane; i < L.shr_cnt; i += 64) dst[i] = src[i];
-      n_shr += L.shr_cnt;
-    }
-    if (gw & kGatherInline) {
-      const uint2* __restrict__ src = reinterpret_cast<const uint2*>(a.ix.inl + L.inl_off);
-      uint2* __restrict__ dst = reinterpret_cast<uint2*>(a.inl_rows + ib + n_inl);
-      for (uint32_t i = lane; i < L.inl_cnt; i += 64) dst[i] = src[i];
-      n_inl += L.inl_cnt;
+    copy_lists(reinterpret_cast<uint2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const uint2*>(a.ix.shr),
+               g_off[1][wv], g_pre[1][wv], st, lane);
+    n_shr += st;
+    // Inline subscriptions in gather order; the last write per id is kept below.
+    copy_lists(reinterpret_cast<uint2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const uint2*>(a.ix.inl),
+               g_off[2][wv], g_pre[2][wv], it, lane);
+    n_inl += it;
+
+    // Subscriptions that may merge with another of the same client, in gather (rank) order.
+    uint64_t mm = __ballot(mn > 0);
+    while (mm) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(mm);
+      mm &= mm - 1;
+      const uint32_t m_cnt = __builtin_amdgcn_readlane(mn, j);
+      const uint32_t m_off = __builtin_amdgcn_readlane(sub_off + dn, j);
+      if (!tab_ready) {
+        for (uint32_t k = lane; k <= T.mask; k += 64) T.key[k] = kTabEmpty;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        tab_ready = true;
+      }
+      const SubRec* __restrict__ ms = a.ix.subs + m_off;
+      for (uint32_t i0 = 0; i0 < m_cnt; i0 += 64) {
+        const uint32_t k = i0 + lane;
+        const bool v = k < m_cnt;
+        SubRec r{0, 0, 0, 0};
+        uint32_t slot = 0;
+        bool is_new = false;
+        if (v) {
+          r = ms[k];
+          r.meta &= ~kMetaMergeBit;
+          slot = tab_insert(T, r.client, &is_new, a.ix.err);
+        }
+        const uint64_t bn = __ballot(v && is_new);
+        if (v && is_new) {  // first (minimum-rank) subscription of this client: the base
+          const uint32_t pos = n_cli + prefix_before(bn);
+          rows[pos] = r;
+          T.row[slot] = pos;
+          T.meta[slot] = r.meta;
+        }
+        n_cli += __popcll(bn);
+        const bool dup = v && !is_new;
+        if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
+          const uint32_t mt = T.meta[slot];
+          const uint32_t q = max(mt & kMetaQos, r.meta & kMetaQos);
+          const uint32_t nm = (mt & ~kMetaQos) | q | (r.meta & kMetaNoLocal);
+          if ((nm & ~kMetaDirty) != (mt & ~kMetaDirty)) T.meta[slot] = nm | kMetaDirty;
+        }
+        const uint64_t be = __ballot(dup && r.ident > 0);
+        if (dup && r.ident > 0) {  // Identifiers[n.Filter] = n.Identifier (id > 0)
+          const uint32_t e = n_ext + prefix_before(be);
+          SubRec x{r.client, r.filter_id, r.ident, 0};
+          rows[cap - 1 - e] = x;
+        }
+        n_ext += __popcll(be);
+      }
     }
   }
 
