@@ -103,7 +103,8 @@ bool is_share_prefix(std::string_view s) {
 // from index d, or — when d is past the last '/' — the last segment alone.
 void Index::path_of(std::string_view filter, int d, std::vector<std::string_view>& out) {
   out.clear();
-  std::vector<std::string_view> segs;
+  thread_local std::vector<std::string_view> segs;
+  segs.clear();
   size_t s = 0;
   for (;;) {
     size_t e = filter.find('/', s);
@@ -130,14 +131,51 @@ static std::string_view segment_at(std::string_view filter, int d) {  // isolate
   }
 }
 
-uint32_t Index::intern_str(std::string_view s) {
-  auto it = str_ids_.find(std::string(s));
-  if (it != str_ids_.end()) return it->second;
-  uint32_t id = (uint32_t)strs_.size();
-  strs_.emplace_back(s);
-  str_ids_.emplace(std::string(s), id);
+uint64_t StrTable::hash(std::string_view s) {
+  uint64_t h = 0xcbf29ce484222325ull ^ s.size();
+  for (unsigned char c : s) h = (h ^ c) * 0x100000001b3ull;
+  return mix64(h);
+}
+
+void StrTable::grow() {
+  slots_.assign(slots_.size() * 2, kNone);
+  const size_t m = slots_.size() - 1;
+  for (uint32_t id = 0; id < hashes_.size(); id++) {
+    size_t i = hashes_[id] & m;
+    while (slots_[i] != kNone) i = (i + 1) & m;
+    slots_[i] = id;
+  }
+}
+
+uint32_t StrTable::find(std::string_view s) const {
+  const uint64_t h = hash(s);
+  const size_t m = slots_.size() - 1;
+  for (size_t i = h & m;; i = (i + 1) & m) {
+    const uint32_t id = slots_[i];
+    if (id == kNone) return kNone;
+    if (hashes_[id] == h && at(id) == s) return id;
+  }
+}
+
+uint32_t StrTable::intern(std::string_view s) {
+  const uint64_t h = hash(s);
+  const size_t m = slots_.size() - 1;
+  size_t i = h & m;
+  for (;; i = (i + 1) & m) {
+    const uint32_t id = slots_[i];
+    if (id == kNone) break;
+    if (hashes_[id] == h && at(id) == s) return id;
+  }
+  const uint32_t id = (uint32_t)hashes_.size();
+  arena_.insert(arena_.end(), s.begin(), s.end());
+  offs_.push_back(arena_.size());
+  hashes_.push_back(h);
+  slots_[i] = id;
+  if (hashes_.size() * 2 > slots_.size()) grow();
   return id;
 }
+
+uint32_t Index::intern_str(std::string_view s) { return strs_.intern(s); }
 
 // ---- construction ----------------------------------------------------------------------------
 Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
@@ -261,6 +299,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   h.key = k;
   h.str = intern_str(seg);
   h.depth = (uint16_t)(nh_[parent].depth + 1);
+  h.seg0 = parent == kRoot ? h.str : nh_[parent].seg0;
   h.live = true;
   max_depth_ = std::max<uint32_t>(max_depth_, h.depth);
 
@@ -334,7 +373,7 @@ void Index::remove_node(uint32_t n) {
 }
 
 uint32_t Index::set(std::string_view filter, int d) {  // topics.go:479-496
-  std::vector<std::string_view> path;
+  thread_local std::vector<std::string_view> path;
   path_of(filter, d, path);
   uint32_t n = kRoot;
   for (std::string_view seg : path) {
@@ -347,7 +386,7 @@ uint32_t Index::set(std::string_view filter, int d) {  // topics.go:479-496
 }
 
 uint32_t Index::seek(std::string_view filter, int d) const {  // topics.go:499-513
-  std::vector<std::string_view> path;
+  thread_local std::vector<std::string_view> path;
   path_of(filter, d, path);
   uint32_t n = kRoot;
   for (std::string_view seg : path) {
@@ -464,6 +503,8 @@ void Index::path_strs(uint32_t n, uint32_t* out, int* len) const {
 // over-approximation: '#' matches any suffix (including none), '+' any one level, and a
 // path may be one level longer than the other only through a trailing '#'.
 bool Index::compatible(uint32_t a, uint32_t b) const {
+  const uint32_t s0 = nh_[a].seg0, s1 = nh_[b].seg0;
+  if (s0 > 1 && s1 > 1 && s0 != s1) return false;  // different literal first levels
   thread_local std::vector<uint32_t> pa, pb;
   pa.resize(nh_[a].depth);
   pb.resize(nh_[b].depth);

@@ -113,9 +113,31 @@ class HashU64 {
   size_t n_ = 0, tombs_ = 0;
 };
 
+// Interned strings: an arena plus an open-addressing table keyed by the bytes (no std::string
+// per lookup).
+class StrTable {
+ public:
+  StrTable() { slots_.assign(1024, kNone); }
+  uint32_t intern(std::string_view s);  // id of s, inserting it if new
+  uint32_t find(std::string_view s) const;  // id or kNone
+  std::string_view at(uint32_t id) const {
+    return std::string_view(arena_.data() + offs_[id], offs_[id + 1] - offs_[id]);
+  }
+  size_t size() const { return offs_.size() - 1; }
+
+ private:
+  static uint64_t hash(std::string_view s);
+  void grow();
+  std::vector<char> arena_;
+  std::vector<uint64_t> offs_{0};
+  std::vector<uint64_t> hashes_;
+  std::vector<uint32_t> slots_;
+};
+
 struct NodeHost {
   SegKey key{0, 0};
   uint32_t str = 0;        // interned segment string id (0 = "+", 1 = "#")
+  uint32_t seg0 = 0;       // str of the path's first segment (quick compatibility reject)
   uint32_t n_children = 0;
   uint32_t child_pos = 0;  // position in the parent's children slab
   uint32_t sub_cap = 0, shr_cap = 0, inl_cap = 0, child_cap = 0;
@@ -203,8 +225,7 @@ class Index {
   uint32_t max_depth_ = 0;
   uint64_t version_ = 0;
 
-  std::unordered_map<std::string, uint32_t> str_ids_;
-  std::vector<std::string> strs_;
+  StrTable strs_;
   std::unordered_map<std::string, uint32_t> long_segs_;  // long segment -> SegInfo index
   std::unordered_map<std::string, uint32_t> group_ids_;
 
