@@ -322,9 +322,14 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
   return x - v;
 }
 
-// Copy the concatenation of up to 64 record lists (list j: `cnt_j` records at src + off[j],
-// exclusive prefix pre[j], pre[64] = total) to dst[0, total): 64 consecutive rows per
-// wave-instruction, four in flight per lane. Each lane keeps a cursor j that only advances.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Copy the concatenation of up to 64 record lists (list j at src + off[j], exclusive prefix
+// pre[j], pre[64] = total) to dst[0, total): 64 consecutive rows per wave-instruction, four
+// loads in flight per lane. Each lane keeps a cursor j that only advances. The rows are
+// written once and never re-read here, so they are stored non-temporally and do not evict
+// the hot subscription lists from L2 / the Infinity Cache.
 template <class V>
 __device__ __forceinline__ void copy_lists(V* __restrict__ dst, const V* __restrict__ src,
                                            const uint32_t* __restrict__ off,
@@ -344,7 +349,7 @@ __device__ __forceinline__ void copy_lists(V* __restrict__ dst, const V* __restr
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t r = r0 + k * 64 + lane;
-      if (r < total) dst[r] = v[k];
+      if (r < total) __builtin_nontemporal_store(v[k], dst + r);
     }
   }
 }
@@ -422,15 +427,15 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     __builtin_amdgcn_wave_barrier();
 
     // Subscriptions that can never merge: one flat coalesced copy into client rows.
-    copy_lists(reinterpret_cast<uint4*>(rows + n_cli), reinterpret_cast<const uint4*>(a.ix.subs),
+    copy_lists(reinterpret_cast<u32x4*>(rows + n_cli), reinterpret_cast<const u32x4*>(a.ix.subs),
                g_off[0][wv], g_pre[0][wv], dt, lane);
     n_cli += dt;
     // Shared[sub.Filter][client] = sub (topics.go:656-663)
-    copy_lists(reinterpret_cast<uint2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const uint2*>(a.ix.shr),
+    copy_lists(reinterpret_cast<u32x2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const u32x2*>(a.ix.shr),
                g_off[1][wv], g_pre[1][wv], st, lane);
     n_shr += st;
     // Inline subscriptions in gather order; the last write per id is kept below.
-    copy_lists(reinterpret_cast<uint2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const uint2*>(a.ix.inl),
+    copy_lists(reinterpret_cast<u32x2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const u32x2*>(a.ix.inl),
                g_off[2][wv], g_pre[2][wv], it, lane);
     n_inl += it;
 
