@@ -66,16 +66,14 @@ def main():
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
+    from mqmatch import dist as D
     from mqmatch import engine as E
     from mqmatch import workload as W
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local_rank = D.env_rank()
+    local = D.device_for(local_rank)
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    backend = D.init(local_rank)
     n_clients = args.clients or max(1, args.subs // 10)
 
     t0 = time.time()
@@ -85,7 +83,7 @@ def main():
     eng = E.Engine(device=local, expected_subs=args.subs)
     eng.subscribe_bulk(w)
     log(f"engine index built in {time.time()-t0:.1f}s: {eng.stats()}")
-    tb, to = W.gen_topics(w, args.topics, seed=W.BASE_SEED + 1000 * rank)
+    tb, to = W.gen_topics(w, args.topics, seed=D.topic_seed(rank))
     n = len(to) - 1
 
     stream = torch.cuda.current_stream()
@@ -104,28 +102,22 @@ def main():
     torch.cuda.synchronize()
     eng.profile(True)
     eng.profile_reset()
-    if world > 1:
-        dist.barrier()
+    D.barrier(backend)
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        r = step()
+        step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier(backend)
     elapsed = time.perf_counter() - t_start
     prof = eng.profile_read()
     eng.profile(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, backend)
     chunks = eng.match_chunks()
     log(f"timed {args.steps} steps in {elapsed:.3f}s; kernels {prof}; chunks/step {chunks}")
 
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
+        D.finalize(backend)
         return
 
     value = n * world * args.steps / elapsed
@@ -192,8 +184,7 @@ def main():
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    D.finalize(backend)
 
 
 if __name__ == "__main__":
