@@ -144,7 +144,7 @@ Device::~Device() {
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_})
+                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_, &gslots_})
     b->release();
 }
 
@@ -233,8 +233,8 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   last_chunks_ = 0;
   if (host) *host = HostMatch{};
   if (!err_.p) {
-    err_.ensure(sizeof(uint32_t));
-    hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
+    err_.ensure(2 * sizeof(uint32_t));
+    hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
   }
   check_err(s);  // faults flagged by the previous batch's kernels
   if (n == 0) return;
@@ -246,9 +246,10 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
   bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
 
+  gslots_.ensure((size_t)n * kGatherCap * sizeof(uint32_t));
   prof.begin(s);
-  launch_walk(false, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, nullptr, s);
-  prof.end("walk_count", s);
+  launch_walk(false, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(), s);
+  prof.end("walk", s);
   hip_check(hipGetLastError(), "k_walk<count>");
   prof.begin(s);
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
@@ -258,15 +259,26 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   h_bpre_.resize(nb + 1);
   hip_check(hipMemcpyAsync(h_bpre_.data(), bpre_.p, (nb + 1) * sizeof(TopicOff), hipMemcpyDeviceToHost, s),
             "D2H block offsets");
+  uint32_t overflow = 0;
+  hip_check(hipMemcpyAsync(&overflow, err_.as<uint32_t>() + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+            "D2H overflow");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   check_err(s);
   const TopicOff tot = h_bpre_[nb];
 
-  gathers_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
-  prof.begin(s);
-  launch_walk(true, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), s);
-  prof.end("walk_fill", s);
-  hip_check(hipGetLastError(), "k_walk<fill>");
+  // A topic with more gathers than its count-pass slots: write all gather lists compactly.
+  const uint32_t* gathers = gslots_.as<uint32_t>();
+  uint32_t gstride = kGatherCap;
+  if (overflow) {
+    hip_check(hipMemsetAsync(err_.as<uint32_t>() + 1, 0, sizeof(uint32_t), s), "hipMemsetAsync");
+    gathers_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
+    prof.begin(s);
+    launch_walk(true, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), s);
+    prof.end("walk_fill", s);
+    hip_check(hipGetLastError(), "k_walk<fill>");
+    gathers = gathers_.as<uint32_t>();
+    gstride = 0;
+  }
 
   // plan output chunks on scan-block boundaries so each chunk's rows fit the budget
   struct Chunk {
@@ -306,7 +318,8 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     a.t1 = std::min<uint64_t>(n, (uint64_t)c.b1 * kScanBlock);
     a.off = offs_.as<TopicOff>();
     a.base = h_bpre_[c.b0];
-    a.gathers = gathers_.as<uint32_t>();
+    a.gathers = gathers;
+    a.gather_stride = gstride;
     a.rows = rows_.as<SubRec>();
     a.shr_rows = shr_rows_.as<ShrRec>();
     a.inl_rows = inl_rows_.as<InlRec>();
@@ -357,8 +370,8 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   *out = mq_msg_result{};
   if (host) *host = HostMsg{};
   if (!err_.p) {
-    err_.ensure(sizeof(uint32_t));
-    hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
+    err_.ensure(2 * sizeof(uint32_t));
+    hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
   }
   check_err(s);
   if (n == 0) return;

@@ -126,7 +126,7 @@ class Device {
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   DevBuf rows_, shr_rows_, inl_rows_, tab_, res_, err_;
-  DevBuf msg_handles_, msg_base_, msg_count_;
+  DevBuf msg_handles_, msg_base_, msg_count_, gslots_;
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;
   uint64_t empty_handle_ = 0;

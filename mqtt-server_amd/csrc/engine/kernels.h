@@ -9,6 +9,7 @@ namespace mq {
 
 constexpr uint32_t kLdsTab = 512;      // LDS merge-table slots per wavefront
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
+constexpr uint32_t kGatherCap = 32;    // per-topic gather slots written by the count pass
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -27,7 +28,7 @@ struct DevIndex {
   uint64_t empty_topic_handle;
   uint32_t empty_topic_live;
   uint32_t pad;
-  uint32_t* err;  // device error word (kErr*), checked by the host after each batch
+  uint32_t* err;  // [0] error bits (kErr*), [1] gather-slot overflow; checked by the host
 };
 
 constexpr uint32_t kErrWalkGuard = 1u;
@@ -51,6 +52,7 @@ struct EmitArgs {
   const TopicOff* off;      // per-topic offsets (n + 1)
   TopicOff base;            // off[t0]: the chunk's output buffers start here
   const uint32_t* gathers;
+  uint32_t gather_stride;   // kGatherCap: per-topic slots of the count pass; 0: compact at off.g
   SubRec* rows;
   ShrRec* shr_rows;
   InlRec* inl_rows;

@@ -21,6 +21,9 @@ namespace mq {
 // ---------------------------------------------------------------------------------------------
 // byte-level helpers over the topic buffer
 // ---------------------------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ uint64_t find_slash(const uint8_t* __restrict__ b, uint64_t s, uint64_t end) {
   while (s < end && b[s] != '/') s++;
   return s;
@@ -29,6 +32,44 @@ __device__ __forceinline__ uint64_t find_slash(const uint8_t* __restrict__ b, ui
 // Start of the segment that ends at `e` (exclusive): one past the previous '/' or b0.
 __device__ __forceinline__ uint64_t seg_start_before(const uint8_t* __restrict__ b, uint64_t b0, uint64_t e) {
   while (e > b0 && b[e - 1] != '/') e--;
+  return e;
+}
+
+// Byte reader with a one-chunk register cache: one 16-byte load serves 16 sequential byte
+// reads. The topic buffer must be readable up to its next 16-byte boundary (include/mqmatch.h).
+struct ByteReader {
+  const uint8_t* base;
+  uint64_t ci;
+  u32x4 c;
+  __device__ __forceinline__ explicit ByteReader(const uint8_t* b) : base(b), ci(~0ull) {}
+  __device__ __forceinline__ uint32_t at(uint64_t i) {
+    const uint64_t k = i >> 4;
+    if (k != ci) {
+      c = *reinterpret_cast<const u32x4*>(base + (k << 4));
+      ci = k;
+    }
+    const uint32_t w = ((uint32_t)i >> 2) & 3;
+    const uint32_t word = w == 0 ? c.x : (w == 1 ? c.y : (w == 2 ? c.z : c.w));
+    return (word >> (((uint32_t)i & 3) * 8)) & 0xffu;
+  }
+};
+
+// Scan the segment that starts at s: returns the position of its terminating '/' (or end) and
+// its key (layout.h) in the same pass.
+__device__ __forceinline__ uint64_t scan_segment(ByteReader& R, uint64_t s, uint64_t end, SegKey* key) {
+  SegKeyBuilder kb;
+  uint64_t i = s;
+  for (; i < end; i++) {
+    const uint32_t ch = R.at(i);
+    if (ch == '/') break;
+    kb.push(ch);
+  }
+  *key = kb.finish();
+  return i;
+}
+
+__device__ __forceinline__ uint64_t seg_start_before(ByteReader& R, uint64_t b0, uint64_t e) {
+  while (e > b0 && R.at(e - 1) != '/') e--;
   return e;
 }
 
@@ -54,6 +95,9 @@ __device__ __forceinline__ uint32_t lookup(const DevIndex& ix, uint32_t parent, 
 // ---------------------------------------------------------------------------------------------
 // k_walk: the match walk (thread per topic)
 // ---------------------------------------------------------------------------------------------
+// FILL=false: count pass; also writes the first kGatherCap gathers of each topic to its slot
+// of `gathers` (stride kGatherCap) and flags a topic with more. FILL=true: writes every gather
+// compactly at off[t].g (run only when some topic overflowed its slot).
 template <bool FILL>
 __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
                                               const uint64_t* __restrict__ to, uint32_t n,
@@ -64,18 +108,19 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
   if (t >= n) return;
   const uint64_t b0 = to[t], b1 = to[t + 1];
   uint32_t ng = 0, rows = 0, shared = 0, inl = 0, merge = 0;
-  uint32_t* gout = FILL ? gathers + off[t].g : nullptr;
+  uint32_t* gout = FILL ? gathers + off[t].g : gathers + (uint64_t)t * kGatherCap;
 
   if (b1 > b0) {  // Subscribers("") matches nothing (topics.go:598-600)
-    const bool dollar = tb[b0] == '$';
+    ByteReader R(tb);
+    const bool dollar = R.at(b0) == '$';
     // gather{Subscriptions,SharedSubscriptions,InlineSubscriptions} of one particle
     auto gather = [&](uint32_t node, bool with_inline) {
       const NodeLists L = ix.lists[node];
       // [MQTT-4.7.1-1]: '$' topics skip subscriptions whose filter starts with '+'/'#' (Q3)
       const bool subs_ok = !(dollar && (L.flags & kFlagSeg0Wild));
-      if (FILL) {
-        gout[ng] = node | (subs_ok ? kGatherSubs : 0u) | (with_inline ? kGatherInline : 0u);
-      } else {
+      const uint32_t gw = node | (subs_ok ? kGatherSubs : 0u) | (with_inline ? kGatherInline : 0u);
+      if (FILL || ng < kGatherCap) gout[ng] = gw;
+      if (!FILL) {
         if (subs_ok) {
           rows += L.n_direct + L.n_merge;
           merge += L.n_merge;
@@ -87,7 +132,8 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
     };
 
     uint32_t node = kRoot;
-    uint64_t s = b0, e = find_slash(tb, b0, b1);
+    SegKey key;
+    uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
     int state = 0;  // 0: literal child next, 1: '+' child next, 2: '#' gather and return
     for (uint64_t guard = 0;; guard++) {
       if (guard > kWalkGuard) {  // never reached on a well-formed image; fail loudly, not hang
@@ -100,14 +146,13 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
         const uint32_t len = (uint32_t)(e - s);
         // A literal "+" segment makes the reference visit the '+' child twice with identical
         // results (topics.go:603); the '+' branch below covers it.
-        if (!(len == 1 && tb[s] == '+')) {
-          const SegKey k = seg_key(tb + s, len);
-          const uint32_t p = lookup(ix, node, k, tb + s, len);
+        if (!(len == 1 && R.at(s) == '+')) {
+          const uint32_t p = lookup(ix, node, key, tb + s, len);
           if (p != kNone) {
             if (has_next) {
               node = p;
               s = e + 1;
-              e = find_slash(tb, s, b1);
+              e = scan_segment(R, s, b1, &key);
               state = 0;
               continue;
             }
@@ -124,7 +169,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
           if (has_next) {
             node = p;
             s = e + 1;
-            e = find_slash(tb, s, b1);
+            e = scan_segment(R, s, b1, &key);
             state = 0;
             continue;
           }
@@ -137,7 +182,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
       // return to the parent: restore its segment window and continue after this branch
       node = nw.parent_flags & kParentMask;
       e = s - 1;
-      s = seg_start_before(tb, b0, e);
+      s = seg_start_before(R, b0, e);
       state = (nw.parent_flags & kFlagPlusKey) ? 2 : 1;
     }
   }
@@ -154,6 +199,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
     }
     c.table = tab;
     cnt[t] = c;
+    if (ng > kGatherCap) atomicOr(ix.err + 1, 1u);
   }
 }
 
@@ -322,9 +368,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
   return x - v;
 }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
 // Copy the concatenation of up to 64 record lists (list j at src + off[j], exclusive prefix
 // pre[j], pre[64] = total) to dst[0, total): 64 consecutive rows per wave-instruction, four
 // loads in flight per lane. Each lane keeps a cursor j that only advances. The rows are
@@ -394,7 +437,8 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     const uint32_t ng = (uint32_t)min<uint64_t>(kGroup, o1.g - g0);
     uint32_t dn = 0, mn = 0, sn = 0, in = 0, sub_off = 0, shr_off = 0, inl_off = 0;
     if (lane < ng) {
-      const uint32_t gw = a.gathers[g0 + lane];
+      const uint32_t gw = a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + (g0 - o0.g) + lane]
+                                          : a.gathers[g0 + lane];
       const NodeLists L = a.ix.lists[gw & kGatherNode];
       if (gw & kGatherSubs) {
         dn = L.n_direct;

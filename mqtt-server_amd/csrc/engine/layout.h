@@ -37,25 +37,31 @@ MQ_HD uint64_t mix64(uint64_t x) {
   return x;
 }
 
-MQ_HD SegKey seg_key(const uint8_t* p, uint32_t len) {
-  SegKey k{0, 0};
-  if (len <= kInlineSegMax) {
-    for (uint32_t i = 0; i < len; i++) {
-      if (i < 8) k.k0 |= (uint64_t)p[i] << (8 * i);
-      else k.k1 |= (uint64_t)p[i] << (8 * (i - 8));
-    }
-    k.k1 |= (uint64_t)len << 56;
-  } else {
-    uint64_t a = 0xcbf29ce484222325ull ^ len, b = 0x84222325cbf29ce4ull + len;
-    for (uint32_t i = 0; i < len; i++) {
-      a = (a ^ p[i]) * 0x100000001b3ull;
-      b = (b + p[i] + 1) * 0x9e3779b97f4a7c15ull;
-      b ^= b >> 29;
-    }
-    k.k0 = mix64(a);
-    k.k1 = (mix64(b) & ~kLongMarker) | kLongMarker;
+constexpr uint64_t kFnvOffset = 0xcbf29ce484222325ull, kFnvPrime = 0x100000001b3ull;
+constexpr uint64_t kHashB0 = 0x84222325cbf29ce4ull, kGolden = 0x9e3779b97f4a7c15ull;
+
+// Incremental form, so the device computes the key in the same pass that finds the '/'.
+struct SegKeyBuilder {
+  uint64_t k0 = 0, k1 = 0, a = kFnvOffset, b = kHashB0;
+  uint32_t len = 0;
+  MQ_HD void push(uint32_t c) {
+    if (len < 8) k0 |= (uint64_t)c << (8 * len);
+    else if (len < kInlineSegMax) k1 |= (uint64_t)c << (8 * (len - 8));
+    a = (a ^ c) * kFnvPrime;
+    b = (b + c + 1) * kGolden;
+    b ^= b >> 29;
+    len++;
   }
-  return k;
+  MQ_HD SegKey finish() const {
+    if (len <= kInlineSegMax) return SegKey{k0, k1 | ((uint64_t)len << 56)};
+    return SegKey{mix64(a ^ ((uint64_t)len * kGolden)), (mix64(b + len) & ~kLongMarker) | kLongMarker};
+  }
+};
+
+MQ_HD SegKey seg_key(const uint8_t* p, uint32_t len) {
+  SegKeyBuilder kb;
+  for (uint32_t i = 0; i < len; i++) kb.push(p[i]);
+  return kb.finish();
 }
 
 MQ_HD bool seg_is_long(const SegKey& k) { return (k.k1 & kLongMarker) == kLongMarker; }

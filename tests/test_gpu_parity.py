@@ -273,3 +273,21 @@ def test_messages_workload_parity(gpu_available):
         for x in h:
             d = fold(d, x)
         assert d == od[i], i
+
+
+def test_gather_slot_overflow(gpu_available):
+    """A topic matching > 32 particles overflows its count-pass gather slots and takes the
+    compact fill pass; mixed with ordinary topics in one batch."""
+    e, o = EngineAdapter(), OracleAdapter()
+    levels = [f"l{i}" for i in range(50)]
+    for d in range(1, 50):
+        f = "/".join(levels[:d]) + "/#"
+        for c in (f"c{d % 7}", "cz"):
+            assert e.subscribe(c, f, identifier=d) == o.subscribe(c, f, identifier=d)
+        e.inline_subscribe(f, d % 5)
+        o.inline_subscribe(f, d % 5)
+    e.subscribe("cq", "l0/+/l2")
+    o.subscribe("cq", "l0/+/l2")
+    topics = ["/".join(levels[:k]) for k in (1, 3, 10, 33, 34, 40, 50)] + ["l0/x/l2", "q"]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
