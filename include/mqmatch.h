@@ -210,6 +210,7 @@ typedef struct mq_stats {
   uint64_t subs, subs_merge, shared, inlines;
   uint64_t retained, retained_live;
   uint64_t device_bytes, upload_bytes_total, syncs;
+  uint64_t partners; /* partner links between may-merge subscriptions */
   uint32_t max_depth, reserved;
 } mq_stats;
 int mq_index_stats(const mq_index* idx, mq_stats* out);

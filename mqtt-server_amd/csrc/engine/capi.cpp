@@ -284,6 +284,7 @@ int mq_index_stats(const mq_index* cidx, mq_stats* out) {
     out->inlines = x.inl.live;
     out->retained = x.retained_len();
     out->max_depth = x.max_depth();
+    out->partners = x.parts.live;
     if (idx->dev) {
       out->device_bytes = idx->dev->device_bytes();
       out->upload_bytes_total = idx->dev->upload_bytes();

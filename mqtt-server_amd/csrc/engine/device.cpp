@@ -137,14 +137,17 @@ Device::Device(int dev) : dev_(dev) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   const char* e = getenv("MQ_CHUNK_ROWS");
   chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : (256ull << 20);  // 4 GiB of 16-B rows
+  const char* ab = getenv("MQ_EMIT_ABLATE");  // diagnosis only: results are wrong when set
+  ablate_ = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0;
 }
 
 Device::~Device() {
   (void)hipSetDevice(dev_);
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
+  subx_.release(); parts_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_, &gslots_})
+                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_, &gslots_, &ovf_})
     b->release();
 }
 
@@ -152,7 +155,8 @@ uint64_t Device::device_bytes() const {
   uint64_t b = edges_.cap * sizeof(EdgeSlot) + walk_.cap * sizeof(NodeWalk) +
                lists_.cap * sizeof(NodeLists) + msg_.cap * sizeof(NodeMsg) +
                seginfo_.cap * sizeof(SegInfo) + segbytes_.cap + subs_.cap * sizeof(SubRec) +
-               shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4;
+               shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4 +
+               subx_.cap * sizeof(SubX) + parts_.cap * 4;
   for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
                           &shr_rows_, &inl_rows_, &tab_, &res_})
     b += x->bytes;
@@ -169,6 +173,8 @@ void Device::sync(Index& ix, hipStream_t s) {
   seginfo_.sync(ix.seginfo, s, &uploaded_);
   segbytes_.sync(ix.segbytes, s, &uploaded_);
   subs_.sync(ix.subs.m, s, &uploaded_);
+  subx_.sync(ix.subx, s, &uploaded_);
+  parts_.sync(ix.parts.m, s, &uploaded_);
   shr_.sync(ix.shr.m, s, &uploaded_);
   inl_.sync(ix.inl.m, s, &uploaded_);
   children_.sync(ix.children.m, s, &uploaded_);
@@ -189,6 +195,8 @@ DevIndex Device::dev_index(const Index& ix) const {
   d.seginfo = seginfo_.d;
   d.segbytes = segbytes_.d;
   d.subs = subs_.d;
+  d.subx = subx_.d;
+  d.parts = parts_.d;
   d.shr = shr_.d;
   d.inl = inl_.d;
   d.children = children_.d;
@@ -300,8 +308,8 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   rows_.ensure(max_rows * sizeof(SubRec));
   shr_rows_.ensure(max_shr * sizeof(ShrRec));
   inl_rows_.ensure(max_inl * sizeof(InlRec));
-  tab_.ensure(max_tab * 3 * sizeof(uint32_t));
   res_.ensure(max_topics * sizeof(mq_topic_result_dev));
+  ovf_.ensure((max_topics + 1) * sizeof(uint32_t));
 
   if (host) {
     host->topics.resize(n);
@@ -310,7 +318,6 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     host->inl.resize(tot.inl);
   }
 
-  std::vector<TopicOff> hoff;
   for (const Chunk& c : chunks) {
     EmitArgs a;
     a.ix = di;
@@ -326,11 +333,32 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     a.tab = tab_.as<uint32_t>();
     a.tab_cap = max_tab;
     a.res = res_.as<mq_topic_result_dev>();
+    a.ablate = ablate_;
+    a.list = nullptr;
+    a.n_list = 0;
+    a.ovf_count = ovf_.as<uint32_t>();
+    a.ovf_list = ovf_.as<uint32_t>() + 1;
+    hip_check(hipMemsetAsync(a.ovf_count, 0, sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
     prof.begin(s);
     launch_emit(a, s);
     prof.end("emit", s);
     hip_check(hipGetLastError(), "k_emit");
     last_chunks_++;
+
+    // Topics whose merge table outgrew LDS: redo them with global tables (sized by the scan).
+    uint32_t n_ovf = 0;
+    hip_check(hipMemcpyAsync(&n_ovf, a.ovf_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H ovf");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (n_ovf) {
+      tab_.ensure(max_tab * 3 * sizeof(uint32_t));
+      a.tab = tab_.as<uint32_t>();
+      a.list = a.ovf_list;
+      a.n_list = n_ovf;
+      prof.begin(s);
+      launch_emit(a, s);
+      prof.end("emit_overflow", s);
+      hip_check(hipGetLastError(), "k_emit<overflow>");
+    }
 
     const TopicOff& lo = h_bpre_[c.b0];
     const TopicOff& hi = h_bpre_[c.b1];
@@ -425,6 +453,7 @@ template struct DevMirror<NodeMsg>;
 template struct DevMirror<SegInfo>;
 template struct DevMirror<uint8_t>;
 template struct DevMirror<SubRec>;
+template struct DevMirror<SubX>;
 template struct DevMirror<ShrRec>;
 template struct DevMirror<InlRec>;
 template struct DevMirror<uint32_t>;

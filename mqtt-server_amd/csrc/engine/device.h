@@ -113,6 +113,7 @@ class Device {
   uint64_t uploaded_ = 0, syncs_ = 0;
   uint32_t last_chunks_ = 0;
   uint64_t chunk_rows_budget_;
+  uint32_t ablate_ = 0;
   DevMirror<EdgeSlot> edges_;
   DevMirror<NodeWalk> walk_;
   DevMirror<NodeLists> lists_;
@@ -120,13 +121,15 @@ class Device {
   DevMirror<SegInfo> seginfo_;
   DevMirror<uint8_t> segbytes_;
   DevMirror<SubRec> subs_;
+  DevMirror<SubX> subx_;
+  DevMirror<uint32_t> parts_;
   DevMirror<ShrRec> shr_;
   DevMirror<InlRec> inl_;
   DevMirror<uint32_t> children_;
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   DevBuf rows_, shr_rows_, inl_rows_, tab_, res_, err_;
-  DevBuf msg_handles_, msg_base_, msg_count_, gslots_;
+  DevBuf msg_handles_, msg_base_, msg_count_, gslots_, ovf_;
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;
   uint64_t empty_handle_ = 0;

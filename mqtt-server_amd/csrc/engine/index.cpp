@@ -202,6 +202,8 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   msg.grow_to(1, NodeMsg{});
   seginfo.grow_to(1, SegInfo{0, 0});
   segbytes.grow_to(1, 0);
+  subx.grow_to(1, SubX{0, 0});
+  parts.m.grow_to(1, 0);
 }
 
 // ---- edge table -------------------------------------------------------------------------------
@@ -407,6 +409,16 @@ void Index::trim(uint32_t n) {  // topics.go:516-522
 }
 
 // ---- subscription lists ----------------------------------------------------------------------------
+// A slot is the SubRec plus its partner descriptor (SubX) and the host-side partner capacity;
+// they always move together, and the (node, client) -> slot map follows.
+void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
+  const SubRec r = subs.m.h[from];
+  subs.m.at_w(to) = r;
+  subx.at_w(to) = subx.h[from];
+  subx_cap_[to] = subx_cap_[from];
+  sub_pos_.put((uint64_t)n << 32 | r.client, to);
+}
+
 void Index::sub_ensure(uint32_t n, uint32_t need) {
   uint32_t cap = nh_[n].sub_cap;
   if (need <= cap) return;
@@ -414,20 +426,12 @@ void Index::sub_ensure(uint32_t n, uint32_t need) {
   while (nc < need) nc *= 2;
   NodeLists& L = lists.at_w(n);
   uint32_t no = subs.alloc(nc), cnt = L.n_direct + L.n_merge;
-  for (uint32_t i = 0; i < cnt; i++) {
-    const SubRec r = subs.m.h[L.sub_off + i];
-    subs.m.at_w(no + i) = r;
-    sub_pos_.put((uint64_t)n << 32 | r.client, no + i);
-  }
+  subx.grow_to(subs.m.size(), SubX{0, 0});
+  subx_cap_.resize(subs.m.size(), 0);
+  for (uint32_t i = 0; i < cnt; i++) move_slot(n, L.sub_off + i, no + i);
   subs.release(L.sub_off, cap);
   L.sub_off = no;
   nh_[n].sub_cap = nc;
-}
-
-static inline void move_sub(SlabPool<SubRec>& subs, HashU64& pos, uint32_t n, uint32_t from, uint32_t to) {
-  const SubRec r = subs.m.h[from];
-  subs.m.at_w(to) = r;
-  pos.put((uint64_t)n << 32 | r.client, to);
 }
 
 uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
@@ -440,10 +444,12 @@ uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
     n_merge_++;
   } else {
     pos = base + L.n_direct;
-    if (L.n_merge) move_sub(subs, sub_pos_, n, pos, base + L.n_direct + L.n_merge);
+    if (L.n_merge) move_slot(n, pos, base + L.n_direct + L.n_merge);
     L.n_direct++;
   }
   subs.m.at_w(pos) = r;
+  subx.at_w(pos) = SubX{0, 0};
+  subx_cap_[pos] = 0;
   sub_pos_.put((uint64_t)n << 32 | r.client, pos);
   subs.live++;
   return pos;
@@ -454,12 +460,12 @@ void Index::sub_remove(uint32_t n, uint32_t pos) {
   uint32_t base = L.sub_off;
   if (pos < base + L.n_direct) {
     uint32_t last_d = base + L.n_direct - 1;
-    if (pos != last_d) move_sub(subs, sub_pos_, n, last_d, pos);
-    if (L.n_merge) move_sub(subs, sub_pos_, n, base + L.n_direct + L.n_merge - 1, last_d);
+    if (pos != last_d) move_slot(n, last_d, pos);
+    if (L.n_merge) move_slot(n, base + L.n_direct + L.n_merge - 1, last_d);
     L.n_direct--;
   } else {
     uint32_t last = base + L.n_direct + L.n_merge - 1;
-    if (pos != last) move_sub(subs, sub_pos_, n, last, pos);
+    if (pos != last) move_slot(n, last, pos);
     L.n_merge--;
     n_merge_--;
   }
@@ -472,9 +478,10 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
   bool is_merge = pos >= base + L.n_direct;
   if (merge == is_merge) return;
   uint32_t other = merge ? base + L.n_direct - 1 : base + L.n_direct;
-  SubRec a = subs.m.h[pos], b = subs.m.h[other];
-  subs.m.at_w(pos) = b;
-  sub_pos_.put((uint64_t)n << 32 | b.client, pos);
+  SubRec a = subs.m.h[pos];
+  const SubX ax = subx.h[pos];
+  const uint32_t acap = subx_cap_[pos];
+  if (other != pos) move_slot(n, other, pos);
   if (merge) {
     a.meta |= 0x1000u;
     L.n_direct--;
@@ -487,7 +494,44 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
     n_merge_--;
   }
   subs.m.at_w(other) = a;
+  subx.at_w(other) = ax;
+  subx_cap_[other] = acap;
   sub_pos_.put((uint64_t)n << 32 | a.client, other);
+}
+
+void Index::part_set(uint32_t pos, const std::vector<uint32_t>& nodes) {
+  uint32_t cap = 1;
+  while (cap < nodes.size()) cap *= 2;
+  const uint32_t off = parts.alloc(cap);
+  for (size_t i = 0; i < nodes.size(); i++) parts.m.at_w(off + i) = nodes[i];
+  subx.at_w(pos) = SubX{off, (uint32_t)nodes.size()};
+  subx_cap_[pos] = cap;
+  parts.live += nodes.size();
+}
+
+void Index::part_add(uint32_t pos, uint32_t node) {
+  SubX& x = subx.at_w(pos);
+  list_push(parts, x.part_off, x.part_cnt, subx_cap_[pos], node);
+}
+
+uint32_t Index::part_remove(uint32_t pos, uint32_t node) {
+  SubX& x = subx.at_w(pos);
+  for (uint32_t i = 0; i < x.part_cnt; i++) {
+    if (parts.m.h[x.part_off + i] != node) continue;
+    parts.m.at_w(x.part_off + i) = parts.m.h[x.part_off + x.part_cnt - 1];
+    x.part_cnt--;
+    parts.live--;
+    break;
+  }
+  return x.part_cnt;
+}
+
+void Index::part_release(uint32_t pos) {
+  SubX& x = subx.at_w(pos);
+  parts.release(x.part_off, subx_cap_[pos]);
+  parts.live -= x.part_cnt;
+  x = SubX{0, 0};
+  subx_cap_[pos] = 0;
 }
 
 void Index::path_strs(uint32_t n, uint32_t* out, int* len) const {
@@ -522,19 +566,6 @@ bool Index::compatible(uint32_t a, uint32_t b) const {
   const std::vector<uint32_t>& lo = la > lb ? pa : pb;
   int llo = std::max(la, lb);
   return llo == m + 1 && lo[m] == 1;
-}
-
-void Index::refresh_merge_flag(uint32_t client, uint32_t node) {
-  auto it = client_nodes_.find(client);
-  bool merge = false;
-  if (it != client_nodes_.end())
-    for (uint32_t m : it->second)
-      if (m != node && compatible(node, m)) {
-        merge = true;
-        break;
-      }
-  uint32_t pos;
-  if (sub_pos_.get((uint64_t)node << 32 | client, &pos)) sub_set_merge(node, pos, merge);
 }
 
 // ---- TopicsIndex operations ----------------------------------------------------------------------
@@ -586,16 +617,25 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
     subs.m.at_w(pos) = rec;
     return 0;
   }
+  // Partners: the client's other subscriptions that could match the same topic (the merge
+  // candidates of gatherSubscriptions / Subscription.Merge, topics.go:641-646).
   std::vector<uint32_t>& mine = client_nodes_[client];
-  bool merge = false;
-  for (uint32_t m : mine) {
-    if (!compatible(n, m)) continue;
-    merge = true;
+  thread_local std::vector<uint32_t> comp;
+  comp.clear();
+  for (uint32_t m : mine)
+    if (compatible(n, m)) comp.push_back(m);
+  if (!comp.empty()) rec.meta |= 0x1000u;
+  pos = sub_add(n, rec, !comp.empty());
+  if (!comp.empty()) part_set(pos, comp);
+  for (uint32_t m : comp) {
     uint32_t mp;
-    if (sub_pos_.get((uint64_t)m << 32 | client, &mp) && !sub_is_merge(mp)) sub_set_merge(m, mp, true);
+    if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
+    if (!sub_is_merge(mp)) {
+      sub_set_merge(m, mp, true);
+      sub_pos_.get((uint64_t)m << 32 | client, &mp);
+    }
+    part_add(mp, n);
   }
-  if (merge) rec.meta |= 0x1000u;
-  sub_add(n, rec, merge);
   mine.push_back(n);
   return 1;
 }
@@ -627,22 +667,24 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
     uint32_t pos;
     uint64_t key = (uint64_t)n << 32 | client;
     if (sub_pos_.get(key, &pos)) {
-      bool was_merge = sub_is_merge(pos);
+      const SubX x = subx.h[pos];
+      std::vector<uint32_t> partners(parts.m.h.begin() + x.part_off, parts.m.h.begin() + x.part_off + x.part_cnt);
+      part_release(pos);
       sub_remove(n, pos);
       sub_pos_.erase(key);
       auto cit = client_nodes_.find(client);
       if (cit != client_nodes_.end()) {
         auto& v = cit->second;
         v.erase(std::find(v.begin(), v.end(), n));
-        if (was_merge) {
-          std::vector<uint32_t> others = v;
-          for (uint32_t m : others) {
-            uint32_t mp;
-            if (sub_pos_.get((uint64_t)m << 32 | client, &mp) && sub_is_merge(mp))
-              refresh_merge_flag(client, m);
-          }
-        }
         if (v.empty()) client_nodes_.erase(cit);
+      }
+      for (uint32_t m : partners) {  // the partners lose this one; unflag those left alone
+        uint32_t mp;
+        if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
+        if (part_remove(mp, n) == 0) {
+          part_release(mp);
+          sub_set_merge(m, mp, false);
+        }
       }
     }
   }

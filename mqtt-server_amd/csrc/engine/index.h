@@ -175,6 +175,8 @@ class Index {
   Mirror<SegInfo> seginfo;
   Mirror<uint8_t> segbytes;
   SlabPool<SubRec> subs;
+  Mirror<SubX> subx;          // parallel to subs: partner list of each subscription slot
+  SlabPool<uint32_t> parts;   // partner node ids
   SlabPool<ShrRec> shr;
   SlabPool<InlRec> inl;
   SlabPool<uint32_t> children;
@@ -211,7 +213,11 @@ class Index {
   void sub_set_merge(uint32_t n, uint32_t pos, bool merge);
   bool compatible(uint32_t a, uint32_t b) const;
   void path_strs(uint32_t n, uint32_t* out, int* len) const;
-  void refresh_merge_flag(uint32_t client, uint32_t node);
+  void move_slot(uint32_t n, uint32_t from, uint32_t to);
+  void part_set(uint32_t pos, const std::vector<uint32_t>& nodes);
+  void part_add(uint32_t pos, uint32_t node);
+  uint32_t part_remove(uint32_t pos, uint32_t node);
+  void part_release(uint32_t pos);
 
   template <class T, class Rec>
   void list_push(SlabPool<T>& pool, uint32_t& off, uint32_t& cnt, uint32_t& cap, const Rec& r);
@@ -244,6 +250,7 @@ class Index {
   };
   std::unordered_map<ShrKey, uint32_t, ShrKeyHash> shr_pos_;
   std::vector<uint32_t> shr_group_;  // group id per shared pool position
+  std::vector<uint32_t> subx_cap_;   // partner slab capacity per subscription slot
   std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
   std::unordered_map<std::string, RetEntry> retained_;
 };

@@ -10,6 +10,8 @@ namespace mq {
 constexpr uint32_t kLdsTab = 512;      // LDS merge-table slots per wavefront
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 32;    // per-topic gather slots written by the count pass
+constexpr uint32_t kGSet = 128;        // LDS set of a topic's gathered nodes (<= kGSet/2 gathers)
+constexpr uint32_t kLdsTabMax = 384;   // entries allowed in an LDS merge table before overflow
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -21,6 +23,8 @@ struct DevIndex {
   const SegInfo* seginfo;
   const uint8_t* segbytes;
   const SubRec* subs;
+  const SubX* subx;
+  const uint32_t* parts;
   const ShrRec* shr;
   const InlRec* inl;
   const uint32_t* children;
@@ -59,6 +63,13 @@ struct EmitArgs {
   uint32_t* tab;            // global merge tables: key | row | meta planes of tab_cap each
   uint64_t tab_cap;
   mq_topic_result_dev* res; // indexed t - t0
+  uint32_t ablate;          // diagnosis only (MQ_EMIT_ABLATE): skip parts of the work; 0 in use
+  // Fast pass (list == nullptr): merge tables in LDS; a topic that would overflow its table is
+  // appended to ovf_list and left for the overflow pass (list = ovf_list, global tables).
+  const uint32_t* list;
+  uint32_t n_list;
+  uint32_t* ovf_list;
+  uint32_t* ovf_count;
 };
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,

@@ -403,11 +403,20 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   __shared__ uint32_t lds_key[4][kLdsTab];
   __shared__ uint32_t lds_row[4][kLdsTab];
   __shared__ uint32_t lds_meta[4][kLdsTab];
+  __shared__ uint32_t gset[4][kGSet];            // nodes gathered with their subscriptions
   __shared__ uint32_t g_off[3][4][kGroup];      // direct-sub / shared / inline list offsets
   __shared__ uint32_t g_pre[3][4][kGroup + 1];  // their exclusive prefixes (+ total)
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t t = a.t0 + blockIdx.x * 4 + wv;
-  if (t >= a.t1) return;  // wave-uniform
+  const uint32_t w = blockIdx.x * 4 + wv;
+  uint32_t t;
+  if (a.list) {
+    if (w >= a.n_list) return;  // wave-uniform
+    t = a.list[w];
+  } else {
+    t = a.t0 + w;
+    if (t >= a.t1) return;  // wave-uniform
+  }
+  const bool global_tab = a.list != nullptr;
 
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
@@ -417,7 +426,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   SubRec* __restrict__ rows = a.rows + rb;
 
   TabRef T;
-  if (tabn) {
+  if (global_tab) {
     const uint64_t tb = o0.tab - a.base.tab;
     T.key = a.tab + tb;
     T.row = a.tab + a.tab_cap + tb;
@@ -430,6 +439,43 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     T.mask = kLdsTab - 1;
   }
   bool tab_ready = false;
+  uint32_t tab_used = 0;
+
+  // Set of the particles whose subscriptions this topic gathers. A may-merge subscription
+  // needs the merge table only if one of its partners (its client's other co-matchable
+  // subscriptions) is in it; otherwise it is its client's only match and is emitted directly.
+  const uint32_t n_g = (uint32_t)(o1.g - o0.g);
+  const bool set_ok = n_g <= kGSet / 2;
+  auto gword = [&](uint32_t i) {
+    return a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + i] : a.gathers[o0.g + i];
+  };
+  if (set_ok) {
+    for (uint32_t k = lane; k < kGSet; k += 64) gset[wv][k] = kTabEmpty;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < n_g) {
+      const uint32_t gw = gword(lane);
+      if (gw & kGatherSubs) {
+        const uint32_t node = gw & kGatherNode;
+        uint32_t sl = hash32(node) & (kGSet - 1);
+        for (uint32_t p = 0; p < kGSet; p++, sl = (sl + 1) & (kGSet - 1)) {
+          const uint32_t old = atomicCAS(&gset[wv][sl], kTabEmpty, node);
+          if (old == kTabEmpty || old == node) break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  auto gathered = [&](uint32_t node) {
+    uint32_t sl = hash32(node) & (kGSet - 1);
+    for (uint32_t p = 0; p < kGSet; p++, sl = (sl + 1) & (kGSet - 1)) {
+      const uint32_t k = gset[wv][sl];
+      if (k == node) return true;
+      if (k == kTabEmpty) return false;
+    }
+    return false;
+  };
 
   uint32_t n_cli = 0, n_ext = 0, n_shr = 0, n_inl = 0;
   for (uint64_t g0 = o0.g; g0 < o1.g; g0 += kGroup) {
@@ -437,8 +483,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     const uint32_t ng = (uint32_t)min<uint64_t>(kGroup, o1.g - g0);
     uint32_t dn = 0, mn = 0, sn = 0, in = 0, sub_off = 0, shr_off = 0, inl_off = 0;
     if (lane < ng) {
-      const uint32_t gw = a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + (g0 - o0.g) + lane]
-                                          : a.gathers[g0 + lane];
+      const uint32_t gw = gword((uint32_t)(g0 - o0.g) + lane);
       const NodeLists L = a.ix.lists[gw & kGatherNode];
       if (gw & kGatherSubs) {
         dn = L.n_direct;
@@ -471,12 +516,14 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     __builtin_amdgcn_wave_barrier();
 
     // Subscriptions that can never merge: one flat coalesced copy into client rows.
-    copy_lists(reinterpret_cast<u32x4*>(rows + n_cli), reinterpret_cast<const u32x4*>(a.ix.subs),
-               g_off[0][wv], g_pre[0][wv], dt, lane);
+    if (!(a.ablate & 1))
+      copy_lists(reinterpret_cast<u32x4*>(rows + n_cli), reinterpret_cast<const u32x4*>(a.ix.subs),
+                 g_off[0][wv], g_pre[0][wv], dt, lane);
     n_cli += dt;
     // Shared[sub.Filter][client] = sub (topics.go:656-663)
-    copy_lists(reinterpret_cast<u32x2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const u32x2*>(a.ix.shr),
-               g_off[1][wv], g_pre[1][wv], st, lane);
+    if (!(a.ablate & 4))
+      copy_lists(reinterpret_cast<u32x2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const u32x2*>(a.ix.shr),
+                 g_off[1][wv], g_pre[1][wv], st, lane);
     n_shr += st;
     // Inline subscriptions in gather order; the last write per id is kept below.
     copy_lists(reinterpret_cast<u32x2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const u32x2*>(a.ix.inl),
@@ -484,38 +531,59 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     n_inl += it;
 
     // Subscriptions that may merge with another of the same client, in gather (rank) order.
-    uint64_t mm = __ballot(mn > 0);
+    uint64_t mm = (a.ablate & 2) ? 0 : __ballot(mn > 0);
     while (mm) {
       const uint32_t j = (uint32_t)__builtin_ctzll(mm);
       mm &= mm - 1;
       const uint32_t m_cnt = __builtin_amdgcn_readlane(mn, j);
       const uint32_t m_off = __builtin_amdgcn_readlane(sub_off + dn, j);
-      if (!tab_ready) {
-        for (uint32_t k = lane; k <= T.mask; k += 64) T.key[k] = kTabEmpty;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        tab_ready = true;
-      }
       const SubRec* __restrict__ ms = a.ix.subs + m_off;
+      const SubX* __restrict__ mx = a.ix.subx + m_off;
       for (uint32_t i0 = 0; i0 < m_cnt; i0 += 64) {
         const uint32_t k = i0 + lane;
         const bool v = k < m_cnt;
         SubRec r{0, 0, 0, 0};
-        uint32_t slot = 0;
-        bool is_new = false;
+        bool shared_client = false;  // another subscription of this client is gathered too
         if (v) {
           r = ms[k];
           r.meta &= ~kMetaMergeBit;
-          slot = tab_insert(T, r.client, &is_new, a.ix.err);
+          if (set_ok) {
+            const SubX x = mx[k];
+            for (uint32_t p = 0; p < x.part_cnt && !shared_client; p++)
+              shared_client = gathered(a.ix.parts[x.part_off + p]);
+          } else {
+            shared_client = true;
+          }
         }
-        const uint64_t bn = __ballot(v && is_new);
-        if (v && is_new) {  // first (minimum-rank) subscription of this client: the base
+        // the client's only match: its merged Subscription is this one (Merge with itself)
+        const uint64_t bd = __ballot(v && !shared_client);
+        if (v && !shared_client) rows[n_cli + prefix_before(bd)] = r;
+        n_cli += __popcll(bd);
+        const uint64_t bt = __ballot(v && shared_client);
+        if (!bt) continue;
+        tab_used += __popcll(bt);
+        if (!global_tab && tab_used > kLdsTabMax) {  // leave the topic to the overflow pass
+          if (lane == 0) a.ovf_list[atomicAdd(a.ovf_count, 1u)] = t;
+          return;
+        }
+        if (!tab_ready) {
+          for (uint32_t q = lane; q <= T.mask; q += 64) T.key[q] = kTabEmpty;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          tab_ready = true;
+        }
+        const bool vt = v && shared_client;
+        uint32_t slot = 0;
+        bool is_new = false;
+        if (vt) slot = tab_insert(T, r.client, &is_new, a.ix.err);
+        const uint64_t bn = __ballot(vt && is_new);
+        if (vt && is_new) {  // first (minimum-rank) subscription of this client: the base
           const uint32_t pos = n_cli + prefix_before(bn);
           rows[pos] = r;
           T.row[slot] = pos;
           T.meta[slot] = r.meta;
         }
         n_cli += __popcll(bn);
-        const bool dup = v && !is_new;
+        const bool dup = vt && !is_new;
         if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
           const uint32_t mt = T.meta[slot];
           const uint32_t q = max(mt & kMetaQos, r.meta & kMetaQos);
@@ -603,8 +671,8 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
 }
 
 void launch_emit(const EmitArgs& a, hipStream_t s) {
-  if (a.t1 <= a.t0) return;
-  const uint32_t waves = a.t1 - a.t0;
+  const uint32_t waves = a.list ? a.n_list : (a.t1 > a.t0 ? a.t1 - a.t0 : 0);
+  if (!waves) return;
   hipLaunchKernelGGL(k_emit, dim3((waves + 3) / 4), dim3(256), 0, s, a);
 }
 

@@ -133,6 +133,13 @@ struct SubRec {  // == mq_client_row
   int32_t ident;
   uint32_t meta;  // qos | nolocal<<8 | rap<<9 | rh<<10 (| kMetaMerge, host-side only)
 };
+// Partner list of a subscription that may merge: the nodes of its client's other
+// subscriptions that could match the same topic. At match time the record needs the merge
+// table only if a partner node is gathered for the topic too.
+struct SubX {
+  uint32_t part_off, part_cnt;
+};
+
 struct ShrRec {  // == mq_shared_row
   uint32_t filter_id;
   uint32_t client;

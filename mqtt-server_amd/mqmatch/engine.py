@@ -57,7 +57,7 @@ class MsgResult(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("nodes", "edges", "edge_capacity", "subs", "subs_merge",
                                            "shared", "inlines", "retained", "retained_live",
-                                           "device_bytes", "upload_bytes_total", "syncs")] + \
+                                           "device_bytes", "upload_bytes_total", "syncs", "partners")] + \
                [("max_depth", C.c_uint32), ("reserved", C.c_uint32)]
 
 

@@ -87,7 +87,25 @@ def test_update_semantics_match_oracle(seed):
         assert eng.retained_len() == orc.retained_len()
         if step % 50 == 0:
             assert eng.stats()["nodes"] == orc.particle_count(), step
-    assert eng.stats()["nodes"] == orc.particle_count()
+    st = eng.stats()
+    assert st["nodes"] == orc.particle_count()
+    assert (st["partners"] == 0) == (st["subs_merge"] == 0)
+
+
+def test_partner_links_symmetric():
+    """Every may-merge subscription has >= 1 partner and links are symmetric: a client with
+    k pairwise co-matchable filters holds k*(k-1) links."""
+    eng = E.Engine()
+    for i, f in enumerate(["a/#", "a/b", "a/+", "x/y"]):
+        eng.subscribe(f, 7, i, 0, 0, 0)
+    st = eng.stats()
+    assert st["subs_merge"] == 3 and st["partners"] == 6
+    eng.unsubscribe("a/#", 7)
+    st = eng.stats()
+    assert st["subs_merge"] == 2 and st["partners"] == 2  # a/b ~ a/+ remain partners
+    eng.unsubscribe("a/+", 7)
+    st = eng.stats()
+    assert st["subs_merge"] == 0 and st["partners"] == 0
 
 
 def test_bulk_subscribe_matches_oracle():
@@ -113,3 +131,4 @@ def test_unsubscribe_everything_empties_trie():
         eng.unsubscribe(f, int(w["client_ids"][i]))
     st = eng.stats()
     assert st["nodes"] == 0 and st["subs"] == 0 and st["shared"] == 0 and st["subs_merge"] == 0
+    assert st["partners"] == 0

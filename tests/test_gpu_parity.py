@@ -291,3 +291,21 @@ def test_gather_slot_overflow(gpu_available):
     topics = ["/".join(levels[:k]) for k in (1, 3, 10, 33, 34, 40, 50)] + ["l0/x/l2", "q"]
     for t, g in zip(topics, e.subscribers_batch(topics)):
         assert g == o.subscribers(t), t
+
+
+def test_merge_table_overflow_pass(gpu_available):
+    """> 384 clients each with two co-matching filters in one topic: the LDS merge table would
+    overflow, so the topic is re-emitted by the global-table pass."""
+    e, o = EngineAdapter(), OracleAdapter()
+    for i in range(600):
+        c = f"m{i}"
+        for f, ident in (("o/#", i % 3), ("o/p", 1 + i % 5), ("o/+", 0)):
+            assert e.subscribe(c, f, identifier=ident, qos=i % 3) == o.subscribe(c, f, identifier=ident, qos=i % 3)
+    for i in range(100):  # partners that are not gathered for "o/p": emitted directly
+        e.subscribe(f"s{i}", "o/q")
+        o.subscribe(f"s{i}", "o/q")
+        e.subscribe(f"s{i}", "o/#")
+        o.subscribe(f"s{i}", "o/#")
+    topics = ["o/p", "o/q", "o", "o/z", "o/p/x"]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
