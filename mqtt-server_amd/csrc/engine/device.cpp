@@ -293,7 +293,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     uint32_t b0, b1;
   };
   std::vector<Chunk> chunks;
-  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_tab = 1, max_topics = 1;
+  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1;
   for (uint32_t b = 0; b < nb;) {
     uint32_t e = b + 1;
     while (e < nb && h_bpre_[e + 1].rows - h_bpre_[b].rows <= chunk_rows_budget_) e++;
@@ -301,7 +301,6 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     max_rows = std::max(max_rows, h_bpre_[e].rows - h_bpre_[b].rows);
     max_shr = std::max(max_shr, h_bpre_[e].shr - h_bpre_[b].shr);
     max_inl = std::max(max_inl, h_bpre_[e].inl - h_bpre_[b].inl);
-    max_tab = std::max(max_tab, h_bpre_[e].tab - h_bpre_[b].tab);
     max_topics = std::max<uint64_t>(max_topics, std::min<uint64_t>(n, (uint64_t)e * kScanBlock) - (uint64_t)b * kScanBlock);
     b = e;
   }
@@ -309,7 +308,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   shr_rows_.ensure(max_shr * sizeof(ShrRec));
   inl_rows_.ensure(max_inl * sizeof(InlRec));
   res_.ensure(max_topics * sizeof(mq_topic_result_dev));
-  ovf_.ensure((max_topics + 1) * sizeof(uint32_t));
+  ovf_.ensure((2 * max_topics + 4) * sizeof(uint32_t));
 
   if (host) {
     host->topics.resize(n);
@@ -330,30 +329,31 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     a.rows = rows_.as<SubRec>();
     a.shr_rows = shr_rows_.as<ShrRec>();
     a.inl_rows = inl_rows_.as<InlRec>();
-    a.tab = tab_.as<uint32_t>();
-    a.tab_cap = max_tab;
+    a.tab = nullptr;
+    a.tab_cap = 0;
     a.res = res_.as<mq_topic_result_dev>();
     a.ablate = ablate_;
     a.list = nullptr;
     a.n_list = 0;
-    a.ovf_count = ovf_.as<uint32_t>();
-    a.ovf_list = ovf_.as<uint32_t>() + 1;
-    hip_check(hipMemsetAsync(a.ovf_count, 0, sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
+    a.ovf = ovf_.as<uint32_t>();
+    hip_check(hipMemsetAsync(a.ovf, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
     prof.begin(s);
     launch_emit(a, s);
     prof.end("emit", s);
     hip_check(hipGetLastError(), "k_emit");
     last_chunks_++;
 
-    // Topics whose merge table outgrew LDS: redo them with global tables (sized by the scan).
-    uint32_t n_ovf = 0;
-    hip_check(hipMemcpyAsync(&n_ovf, a.ovf_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H ovf");
+    // Topics whose merge table outgrew LDS: redo them with global tables sized by the counts
+    // the fast pass measured.
+    uint32_t ov[2] = {0, 0};
+    hip_check(hipMemcpyAsync(ov, a.ovf, sizeof(ov), hipMemcpyDeviceToHost, s), "D2H ovf");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    if (n_ovf) {
-      tab_.ensure(max_tab * 3 * sizeof(uint32_t));
+    if (ov[0]) {
+      tab_.ensure((size_t)ov[1] * 3 * sizeof(uint32_t));
       a.tab = tab_.as<uint32_t>();
-      a.list = a.ovf_list;
-      a.n_list = n_ovf;
+      a.tab_cap = ov[1];
+      a.list = a.ovf + 4;
+      a.n_list = ov[0];
       prof.begin(s);
       launch_emit(a, s);
       prof.end("emit_overflow", s);

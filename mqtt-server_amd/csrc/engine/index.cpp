@@ -202,7 +202,8 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   msg.grow_to(1, NodeMsg{});
   seginfo.grow_to(1, SegInfo{0, 0});
   segbytes.grow_to(1, 0);
-  subx.grow_to(1, SubX{0, 0});
+  subx.grow_to(1, SubX{kNone, kNone});
+  subp_.resize(1, PartList{0, 0, 0});
   parts.m.grow_to(1, 0);
 }
 
@@ -415,8 +416,20 @@ void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
   const SubRec r = subs.m.h[from];
   subs.m.at_w(to) = r;
   subx.at_w(to) = subx.h[from];
-  subx_cap_[to] = subx_cap_[from];
+  subp_[to] = subp_[from];
   sub_pos_.put((uint64_t)n << 32 | r.client, to);
+}
+
+void Index::encode_subx(uint32_t pos) {
+  const PartList& p = subp_[pos];
+  SubX x{kNone, kNone};
+  if (p.cnt > 2) {
+    x = SubX{p.off, kPartIndirect | p.cnt};
+  } else {
+    if (p.cnt > 0) x.a = parts.m.h[p.off];
+    if (p.cnt > 1) x.b = parts.m.h[p.off + 1];
+  }
+  subx.at_w(pos) = x;
 }
 
 void Index::sub_ensure(uint32_t n, uint32_t need) {
@@ -426,8 +439,8 @@ void Index::sub_ensure(uint32_t n, uint32_t need) {
   while (nc < need) nc *= 2;
   NodeLists& L = lists.at_w(n);
   uint32_t no = subs.alloc(nc), cnt = L.n_direct + L.n_merge;
-  subx.grow_to(subs.m.size(), SubX{0, 0});
-  subx_cap_.resize(subs.m.size(), 0);
+  subx.grow_to(subs.m.size(), SubX{kNone, kNone});
+  subp_.resize(subs.m.size(), PartList{0, 0, 0});
   for (uint32_t i = 0; i < cnt; i++) move_slot(n, L.sub_off + i, no + i);
   subs.release(L.sub_off, cap);
   L.sub_off = no;
@@ -448,8 +461,8 @@ uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
     L.n_direct++;
   }
   subs.m.at_w(pos) = r;
-  subx.at_w(pos) = SubX{0, 0};
-  subx_cap_[pos] = 0;
+  subx.at_w(pos) = SubX{kNone, kNone};
+  subp_[pos] = PartList{0, 0, 0};
   sub_pos_.put((uint64_t)n << 32 | r.client, pos);
   subs.live++;
   return pos;
@@ -480,7 +493,7 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
   uint32_t other = merge ? base + L.n_direct - 1 : base + L.n_direct;
   SubRec a = subs.m.h[pos];
   const SubX ax = subx.h[pos];
-  const uint32_t acap = subx_cap_[pos];
+  const PartList ap = subp_[pos];
   if (other != pos) move_slot(n, other, pos);
   if (merge) {
     a.meta |= 0x1000u;
@@ -495,7 +508,7 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
   }
   subs.m.at_w(other) = a;
   subx.at_w(other) = ax;
-  subx_cap_[other] = acap;
+  subp_[other] = ap;
   sub_pos_.put((uint64_t)n << 32 | a.client, other);
 }
 
@@ -504,34 +517,36 @@ void Index::part_set(uint32_t pos, const std::vector<uint32_t>& nodes) {
   while (cap < nodes.size()) cap *= 2;
   const uint32_t off = parts.alloc(cap);
   for (size_t i = 0; i < nodes.size(); i++) parts.m.at_w(off + i) = nodes[i];
-  subx.at_w(pos) = SubX{off, (uint32_t)nodes.size()};
-  subx_cap_[pos] = cap;
+  subp_[pos] = PartList{off, (uint32_t)nodes.size(), cap};
   parts.live += nodes.size();
+  encode_subx(pos);
 }
 
 void Index::part_add(uint32_t pos, uint32_t node) {
-  SubX& x = subx.at_w(pos);
-  list_push(parts, x.part_off, x.part_cnt, subx_cap_[pos], node);
+  PartList& p = subp_[pos];
+  list_push(parts, p.off, p.cnt, p.cap, node);
+  encode_subx(pos);
 }
 
 uint32_t Index::part_remove(uint32_t pos, uint32_t node) {
-  SubX& x = subx.at_w(pos);
-  for (uint32_t i = 0; i < x.part_cnt; i++) {
-    if (parts.m.h[x.part_off + i] != node) continue;
-    parts.m.at_w(x.part_off + i) = parts.m.h[x.part_off + x.part_cnt - 1];
-    x.part_cnt--;
+  PartList& p = subp_[pos];
+  for (uint32_t i = 0; i < p.cnt; i++) {
+    if (parts.m.h[p.off + i] != node) continue;
+    parts.m.at_w(p.off + i) = parts.m.h[p.off + p.cnt - 1];
+    p.cnt--;
     parts.live--;
     break;
   }
-  return x.part_cnt;
+  encode_subx(pos);
+  return p.cnt;
 }
 
 void Index::part_release(uint32_t pos) {
-  SubX& x = subx.at_w(pos);
-  parts.release(x.part_off, subx_cap_[pos]);
-  parts.live -= x.part_cnt;
-  x = SubX{0, 0};
-  subx_cap_[pos] = 0;
+  PartList& p = subp_[pos];
+  parts.release(p.off, p.cap);
+  parts.live -= p.cnt;
+  p = PartList{0, 0, 0};
+  subx.at_w(pos) = SubX{kNone, kNone};
 }
 
 void Index::path_strs(uint32_t n, uint32_t* out, int* len) const {
@@ -667,8 +682,8 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
     uint32_t pos;
     uint64_t key = (uint64_t)n << 32 | client;
     if (sub_pos_.get(key, &pos)) {
-      const SubX x = subx.h[pos];
-      std::vector<uint32_t> partners(parts.m.h.begin() + x.part_off, parts.m.h.begin() + x.part_off + x.part_cnt);
+      const PartList pl = subp_[pos];
+      std::vector<uint32_t> partners(parts.m.h.begin() + pl.off, parts.m.h.begin() + pl.off + pl.cnt);
       part_release(pos);
       sub_remove(n, pos);
       sub_pos_.erase(key);

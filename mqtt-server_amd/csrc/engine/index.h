@@ -175,8 +175,8 @@ class Index {
   Mirror<SegInfo> seginfo;
   Mirror<uint8_t> segbytes;
   SlabPool<SubRec> subs;
-  Mirror<SubX> subx;          // parallel to subs: partner list of each subscription slot
-  SlabPool<uint32_t> parts;   // partner node ids
+  Mirror<SubX> subx;          // parallel to subs: device encoding of each slot's partners
+  SlabPool<uint32_t> parts;   // partner node ids (slab per slot; read by the device if > 2)
   SlabPool<ShrRec> shr;
   SlabPool<InlRec> inl;
   SlabPool<uint32_t> children;
@@ -250,7 +250,11 @@ class Index {
   };
   std::unordered_map<ShrKey, uint32_t, ShrKeyHash> shr_pos_;
   std::vector<uint32_t> shr_group_;  // group id per shared pool position
-  std::vector<uint32_t> subx_cap_;   // partner slab capacity per subscription slot
+  struct PartList {
+    uint32_t off, cnt, cap;
+  };
+  std::vector<PartList> subp_;       // host view of each slot's partner slab
+  void encode_subx(uint32_t pos);
   std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
   std::unordered_map<std::string, RetEntry> retained_;
 };

@@ -9,7 +9,7 @@ namespace mq {
 
 constexpr uint32_t kLdsTab = 512;      // LDS merge-table slots per wavefront
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
-constexpr uint32_t kGatherCap = 32;    // per-topic gather slots written by the count pass
+constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
 constexpr uint32_t kGSet = 128;        // LDS set of a topic's gathered nodes (<= kGSet/2 gathers)
 constexpr uint32_t kLdsTabMax = 384;   // entries allowed in an LDS merge table before overflow
 
@@ -60,16 +60,16 @@ struct EmitArgs {
   SubRec* rows;
   ShrRec* shr_rows;
   InlRec* inl_rows;
-  uint32_t* tab;            // global merge tables: key | row | meta planes of tab_cap each
+  uint32_t* tab;            // overflow pass: merge tables, key | row | meta planes of tab_cap
   uint64_t tab_cap;
   mq_topic_result_dev* res; // indexed t - t0
   uint32_t ablate;          // diagnosis only (MQ_EMIT_ABLATE): skip parts of the work; 0 in use
-  // Fast pass (list == nullptr): merge tables in LDS; a topic that would overflow its table is
-  // appended to ovf_list and left for the overflow pass (list = ovf_list, global tables).
-  const uint32_t* list;
+  // Fast pass (list == nullptr): merge tables in LDS. A topic whose table would outgrow LDS
+  // counts its table-bound records, appends {t, slots} to the overflow list and is left for
+  // the overflow pass (list != nullptr), which claims `slots` of global table per topic.
+  const uint32_t* list;     // overflow pass: pairs {topic, table slots}
   uint32_t n_list;
-  uint32_t* ovf_list;
-  uint32_t* ovf_count;
+  uint32_t* ovf;            // [0] count, [1] total slots, [2] claim counter, [4..] pairs
 };
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,

@@ -411,7 +411,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   uint32_t t;
   if (a.list) {
     if (w >= a.n_list) return;  // wave-uniform
-    t = a.list[w];
+    t = a.list[2 * w];
   } else {
     t = a.t0 + w;
     if (t >= a.t1) return;  // wave-uniform
@@ -422,16 +422,18 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   const uint64_t rb = o0.rows - a.base.rows;
   const uint32_t cap = (uint32_t)(o1.rows - o0.rows);
   const uint64_t sb = o0.shr - a.base.shr, ib = o0.inl - a.base.inl;
-  const uint32_t tabn = (uint32_t)(o1.tab - o0.tab);
   SubRec* __restrict__ rows = a.rows + rb;
 
   TabRef T;
   if (global_tab) {
-    const uint64_t tb = o0.tab - a.base.tab;
+    const uint32_t slots = a.list[2 * w + 1];
+    uint32_t tb = 0;
+    if (lane == 0) tb = atomicAdd(a.ovf + 2, slots);
+    tb = __builtin_amdgcn_readfirstlane(tb);
     T.key = a.tab + tb;
     T.row = a.tab + a.tab_cap + tb;
     T.meta = a.tab + 2 * a.tab_cap + tb;
-    T.mask = tabn - 1;
+    T.mask = slots - 1;
   } else {
     T.key = lds_key[wv];
     T.row = lds_row[wv];
@@ -439,6 +441,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     T.mask = kLdsTab - 1;
   }
   bool tab_ready = false;
+  bool overflowed = false;  // fast pass only: now just counting table-bound records
   uint32_t tab_used = 0;
 
   // Set of the particles whose subscriptions this topic gathers. A may-merge subscription
@@ -516,17 +519,18 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     __builtin_amdgcn_wave_barrier();
 
     // Subscriptions that can never merge: one flat coalesced copy into client rows.
-    if (!(a.ablate & 1))
+    if (!(a.ablate & 1) && !overflowed)
       copy_lists(reinterpret_cast<u32x4*>(rows + n_cli), reinterpret_cast<const u32x4*>(a.ix.subs),
                  g_off[0][wv], g_pre[0][wv], dt, lane);
     n_cli += dt;
     // Shared[sub.Filter][client] = sub (topics.go:656-663)
-    if (!(a.ablate & 4))
+    if (!(a.ablate & 4) && !overflowed)
       copy_lists(reinterpret_cast<u32x2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const u32x2*>(a.ix.shr),
                  g_off[1][wv], g_pre[1][wv], st, lane);
     n_shr += st;
     // Inline subscriptions in gather order; the last write per id is kept below.
-    copy_lists(reinterpret_cast<u32x2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const u32x2*>(a.ix.inl),
+    if (!overflowed)
+      copy_lists(reinterpret_cast<u32x2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const u32x2*>(a.ix.inl),
                g_off[2][wv], g_pre[2][wv], it, lane);
     n_inl += it;
 
@@ -549,22 +553,31 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
           r.meta &= ~kMetaMergeBit;
           if (set_ok) {
             const SubX x = mx[k];
-            for (uint32_t p = 0; p < x.part_cnt && !shared_client; p++)
-              shared_client = gathered(a.ix.parts[x.part_off + p]);
+            if (x.b != kNone && (x.b & kPartIndirect)) {
+              const uint32_t pc = x.b & ~kPartIndirect;
+              for (uint32_t p = 0; p < pc && !shared_client; p++)
+                shared_client = gathered(a.ix.parts[x.a + p]);
+            } else {
+              shared_client = (x.a != kNone && gathered(x.a)) || (x.b != kNone && gathered(x.b));
+            }
           } else {
             shared_client = true;
           }
+        }
+        const uint64_t bt = __ballot(v && shared_client);
+        if (overflowed) {
+          tab_used += __popcll(bt);
+          continue;
         }
         // the client's only match: its merged Subscription is this one (Merge with itself)
         const uint64_t bd = __ballot(v && !shared_client);
         if (v && !shared_client) rows[n_cli + prefix_before(bd)] = r;
         n_cli += __popcll(bd);
-        const uint64_t bt = __ballot(v && shared_client);
         if (!bt) continue;
         tab_used += __popcll(bt);
         if (!global_tab && tab_used > kLdsTabMax) {  // leave the topic to the overflow pass
-          if (lane == 0) a.ovf_list[atomicAdd(a.ovf_count, 1u)] = t;
-          return;
+          overflowed = true;
+          continue;
         }
         if (!tab_ready) {
           for (uint32_t q = lane; q <= T.mask; q += 64) T.key[q] = kTabEmpty;
@@ -599,6 +612,18 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
         n_ext += __popcll(be);
       }
     }
+  }
+
+  if (overflowed) {  // hand the topic to the overflow pass with a table sized for its records
+    if (lane == 0) {
+      uint32_t slots = 1;
+      while (slots < 2 * tab_used) slots <<= 1;
+      const uint32_t i = atomicAdd(a.ovf, 1u);
+      a.ovf[4 + 2 * i] = t;
+      a.ovf[4 + 2 * i + 1] = slots;
+      atomicAdd(a.ovf + 1, slots);
+    }
+    return;
   }
 
   if (tab_ready) {  // write back merged Qos/NoLocal of bases that absorbed later matches

@@ -135,10 +135,12 @@ struct SubRec {  // == mq_client_row
 };
 // Partner list of a subscription that may merge: the nodes of its client's other
 // subscriptions that could match the same topic. At match time the record needs the merge
-// table only if a partner node is gathered for the topic too.
+// table only if a partner node is gathered for the topic too. Device encoding: up to two
+// partners inline {p0|kNone, p1|kNone}; more as {offset into parts, kPartIndirect | count}.
 struct SubX {
-  uint32_t part_off, part_cnt;
+  uint32_t a, b;
 };
+constexpr uint32_t kPartIndirect = 0x80000000u;
 
 struct ShrRec {  // == mq_shared_row
   uint32_t filter_id;
