@@ -1,0 +1,60 @@
+"""Summarise rocprofv3 CSV output (kernel trace / stats / PMC counter collection) into the
+per-kernel tables kept under profiles/.
+
+  python profiles/summarize.py gpurun_out/prof_1m           # kernel_stats + trace summary
+  python profiles/summarize.py gpurun_out/pmc1 gpurun_out/pmc2 --pmc
+
+HBM bytes follow MI355X_MICROARCH.md's HBM/rocprofv3 section: FETCH_SIZE and WRITE_SIZE are
+in KiB, come from separate passes, and FETCH_SIZE reads half the bytes of a wide coalesced
+stream on gfx950, so it is reported both raw and x2 ("corrected") next to WRITE_SIZE.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def kernel_stats(d):
+    out = []
+    for path in glob.glob(os.path.join(d, "*kernel_stats.csv")):
+        for r in csv.DictReader(open(path)):
+            out.append({"kernel": r["Name"].split("(")[0], "calls": int(r["Calls"]),
+                        "avg_us": float(r["AverageNs"]) / 1e3, "total_ms": float(r["TotalDurationNs"]) / 1e6,
+                        "pct": float(r["Percentage"])})
+    return out
+
+
+def pmc(dirs):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    calls = collections.defaultdict(set)
+    for d in dirs:
+        for path in glob.glob(os.path.join(d, "*counter_collection.csv")):
+            for r in csv.DictReader(open(path)):
+                k = r["Kernel_Name"].split("(")[0]
+                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                calls[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
+    out = {}
+    for k, v in agg.items():
+        e = {}
+        for c, x in v.items():
+            n = len(calls[(k, c)])
+            e[c] = {"total": x, "dispatches": n, "per_dispatch": x / max(1, n)}
+        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            nf, nw = len(calls[(k, "FETCH_SIZE")]), len(calls[(k, "WRITE_SIZE")])
+            fetch = v["FETCH_SIZE"] * 1024 / max(1, nf)
+            write = v["WRITE_SIZE"] * 1024 / max(1, nw)
+            e["hbm_bytes_per_dispatch"] = {"fetch_raw": fetch, "fetch_corrected_x2": 2 * fetch,
+                                           "write": write, "total_corrected": 2 * fetch + write}
+        out[k] = e
+    return out
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--pmc" in sys.argv:
+        print(json.dumps(pmc(args), indent=1))
+    else:
+        for d in args:
+            print(json.dumps(kernel_stats(d), indent=1))
