@@ -10,8 +10,9 @@ namespace mq {
 constexpr uint32_t kLdsTab = 512;      // LDS merge-table slots per wavefront
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
-constexpr uint32_t kGSet = 128;        // LDS set of a topic's gathered nodes (<= kGSet/2 gathers)
+constexpr uint32_t kGSet = 256;        // LDS set of a topic's gathered nodes (<= kGSet/2 gathers)
 constexpr uint32_t kLdsTabMax = 384;   // entries allowed in an LDS merge table before overflow
+constexpr uint32_t kTList = 512;       // queued table-bound records per wave (flushed when full)
 
 // Device pointers of the resident index image.
 struct DevIndex {

@@ -404,6 +404,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   __shared__ uint32_t lds_row[4][kLdsTab];
   __shared__ uint32_t lds_meta[4][kLdsTab];
   __shared__ uint32_t gset[4][kGSet];            // nodes gathered with their subscriptions
+  __shared__ uint32_t tlist[4][kTList];          // table-bound records of the current gather
   __shared__ uint32_t g_off[3][4][kGroup];      // direct-sub / shared / inline list offsets
   __shared__ uint32_t g_pre[3][4][kGroup + 1];  // their exclusive prefixes (+ total)
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -543,73 +544,102 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
       const uint32_t m_off = __builtin_amdgcn_readlane(sub_off + dn, j);
       const SubRec* __restrict__ ms = a.ix.subs + m_off;
       const SubX* __restrict__ mx = a.ix.subx + m_off;
-      for (uint32_t i0 = 0; i0 < m_cnt; i0 += 64) {
-        const uint32_t k = i0 + lane;
-        const bool v = k < m_cnt;
-        SubRec r{0, 0, 0, 0};
-        bool shared_client = false;  // another subscription of this client is gathered too
-        if (v) {
-          r = ms[k];
-          r.meta &= ~kMetaMergeBit;
-          if (set_ok) {
-            const SubX x = mx[k];
-            if (x.b != kNone && (x.b & kPartIndirect)) {
-              const uint32_t pc = x.b & ~kPartIndirect;
-              for (uint32_t p = 0; p < pc && !shared_client; p++)
-                shared_client = gathered(a.ix.parts[x.a + p]);
-            } else {
-              shared_client = (x.a != kNone && gathered(x.a)) || (x.b != kNone && gathered(x.b));
-            }
-          } else {
-            shared_client = true;
-          }
-        }
-        const uint64_t bt = __ballot(v && shared_client);
-        if (overflowed) {
-          tab_used += __popcll(bt);
-          continue;
-        }
-        // the client's only match: its merged Subscription is this one (Merge with itself)
-        const uint64_t bd = __ballot(v && !shared_client);
-        if (v && !shared_client) rows[n_cli + prefix_before(bd)] = r;
-        n_cli += __popcll(bd);
-        if (!bt) continue;
-        tab_used += __popcll(bt);
-        if (!global_tab && tab_used > kLdsTabMax) {  // leave the topic to the overflow pass
-          overflowed = true;
-          continue;
-        }
+      uint32_t nt = 0;  // table-bound records of this gather queued in tlist
+      // Table pass: insert the queued records (the rare clients with several matches).
+      auto drain = [&]() {
         if (!tab_ready) {
           for (uint32_t q = lane; q <= T.mask; q += 64) T.key[q] = kTabEmpty;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           tab_ready = true;
         }
-        const bool vt = v && shared_client;
-        uint32_t slot = 0;
-        bool is_new = false;
-        if (vt) slot = tab_insert(T, r.client, &is_new, a.ix.err);
-        const uint64_t bn = __ballot(vt && is_new);
-        if (vt && is_new) {  // first (minimum-rank) subscription of this client: the base
-          const uint32_t pos = n_cli + prefix_before(bn);
-          rows[pos] = r;
-          T.row[slot] = pos;
-          T.meta[slot] = r.meta;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t c0 = 0; c0 < nt; c0 += 64) {
+          const bool vt = c0 + lane < nt;
+          SubRec r{0, 0, 0, 0};
+          uint32_t slot = 0;
+          bool is_new = false;
+          if (vt) {
+            r = ms[tlist[wv][c0 + lane]];
+            r.meta &= ~kMetaMergeBit;
+            slot = tab_insert(T, r.client, &is_new, a.ix.err);
+          }
+          const uint64_t bn = __ballot(vt && is_new);
+          if (vt && is_new) {  // first (minimum-rank) subscription of this client: the base
+            const uint32_t pos = n_cli + prefix_before(bn);
+            rows[pos] = r;
+            T.row[slot] = pos;
+            T.meta[slot] = r.meta;
+          }
+          n_cli += __popcll(bn);
+          const bool dup = vt && !is_new;
+          if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
+            const uint32_t mt = T.meta[slot];
+            const uint32_t q = max(mt & kMetaQos, r.meta & kMetaQos);
+            const uint32_t nm = (mt & ~kMetaQos) | q | (r.meta & kMetaNoLocal);
+            if ((nm & ~kMetaDirty) != (mt & ~kMetaDirty)) T.meta[slot] = nm | kMetaDirty;
+          }
+          const uint64_t be = __ballot(dup && r.ident > 0);
+          if (dup && r.ident > 0) {  // Identifiers[n.Filter] = n.Identifier (id > 0)
+            const uint32_t e = n_ext + prefix_before(be);
+            SubRec x{r.client, r.filter_id, r.ident, 0};
+            rows[cap - 1 - e] = x;
+          }
+          n_ext += __popcll(be);
         }
-        n_cli += __popcll(bn);
-        const bool dup = vt && !is_new;
-        if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
-          const uint32_t mt = T.meta[slot];
-          const uint32_t q = max(mt & kMetaQos, r.meta & kMetaQos);
-          const uint32_t nm = (mt & ~kMetaQos) | q | (r.meta & kMetaNoLocal);
-          if ((nm & ~kMetaDirty) != (mt & ~kMetaDirty)) T.meta[slot] = nm | kMetaDirty;
+        nt = 0;
+      };
+      // Streaming pass, four 64-record chunks in flight: a record none of whose partners is
+      // gathered is its client's only match (its merged Subscription is itself) and is
+      // emitted directly; the others are queued for the table pass. Records of one gather
+      // belong to distinct clients, so their order within the gather does not matter.
+      for (uint32_t i0 = 0;; i0 += 256) {
+        const bool done = i0 >= m_cnt;
+        if ((done || nt + 256 > kTList) && nt && !overflowed) drain();  // the one call site
+        if (done) break;
+        SubRec rr[4];
+        SubX xx[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t k = i0 + u * 64 + lane;
+          if (k < m_cnt) {
+            rr[u] = ms[k];
+            xx[u] = mx[k];
+          }
         }
-        const uint64_t be = __ballot(dup && r.ident > 0);
-        if (dup && r.ident > 0) {  // Identifiers[n.Filter] = n.Identifier (id > 0)
-          const uint32_t e = n_ext + prefix_before(be);
-          SubRec x{r.client, r.filter_id, r.ident, 0};
-          rows[cap - 1 - e] = x;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t k = i0 + u * 64 + lane;
+          const bool v = k < m_cnt;
+          bool shared_client = false;
+          if (v) {
+            if (set_ok) {
+              const SubX x = xx[u];
+              if (x.b != kNone && (x.b & kPartIndirect)) {
+                const uint32_t pc = x.b & ~kPartIndirect;
+                for (uint32_t p = 0; p < pc && !shared_client; p++)
+                  shared_client = gathered(a.ix.parts[x.a + p]);
+              } else {
+                shared_client = (x.a != kNone && gathered(x.a)) || (x.b != kNone && gathered(x.b));
+              }
+            } else {
+              shared_client = true;
+            }
+          }
+          const uint64_t bt = __ballot(v && shared_client);
+          tab_used += __popcll(bt);
+          if (!global_tab && tab_used > kLdsTabMax) overflowed = true;
+          if (overflowed) continue;  // now only counting, for the overflow pass's table
+          const uint64_t bd = __ballot(v && !shared_client);
+          if (v && !shared_client) {
+            u32x4 rv = *reinterpret_cast<const u32x4*>(&rr[u]);
+            rv.w &= ~kMetaMergeBit;
+            __builtin_nontemporal_store(rv, reinterpret_cast<u32x4*>(rows + n_cli + prefix_before(bd)));
+          }
+          n_cli += __popcll(bd);
+          if (v && shared_client) tlist[wv][nt + prefix_before(bt)] = k;
+          nt += __popcll(bt);
         }
-        n_ext += __popcll(be);
       }
     }
   }
