@@ -307,13 +307,6 @@ constexpr uint32_t kTabEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kMetaDirty = 0x80000000u;
 constexpr uint32_t kMetaMergeBit = 0x1000u;
 
-struct TabRef {
-  uint32_t* key;
-  uint32_t* row;
-  uint32_t* meta;
-  uint32_t mask;
-};
-
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -321,34 +314,6 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x *= 0x846ca68bu;
   x ^= x >> 16;
   return x;
-}
-
-// Insert `key` (distinct across the active lanes); returns the slot and whether it was new.
-__device__ __forceinline__ uint32_t tab_insert(const TabRef& T, uint32_t key, bool* is_new,
-                                                uint32_t* err) {
-  uint32_t s = hash32(key) & T.mask;
-  for (uint32_t probes = 0; probes <= T.mask; probes++) {
-    uint32_t k = __hip_atomic_load(T.key + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (k == key) {
-      *is_new = false;
-      return s;
-    }
-    if (k == kTabEmpty) {
-      uint32_t old = atomicCAS(T.key + s, kTabEmpty, key);
-      if (old == kTabEmpty) {
-        *is_new = true;
-        return s;
-      }
-      if (old == key) {
-        *is_new = false;
-        return s;
-      }
-    }
-    s = (s + 1) & T.mask;
-  }
-  atomicOr(err, kErrTableFull);  // sized at <= 1/2 load by the count pass: unreachable
-  *is_new = false;
-  return 0;
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -378,17 +343,21 @@ __device__ __forceinline__ void copy_lists(V* __restrict__ dst, const V* __restr
                                            const uint32_t* __restrict__ off,
                                            const uint32_t* __restrict__ pre, uint32_t total,
                                            uint32_t lane) {
+  // Loads are issued unconditionally (idle lanes re-read the last row) so the four stay in
+  // flight together: a load inside a divergent branch makes the compiler wait for it at the
+  // branch join.
   uint32_t j = 0;
   for (uint32_t r0 = 0; r0 < total; r0 += 256) {
-    V v[4];
+    uint32_t src_i[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const uint32_t r = r0 + k * 64 + lane;
-      if (r < total) {
-        while (pre[j + 1] <= r) j++;
-        v[k] = src[off[j] + (r - pre[j])];
-      }
+      const uint32_t r = min(r0 + k * 64 + lane, total - 1);
+      while (pre[j + 1] <= r) j++;
+      src_i[k] = off[j] + (r - pre[j]);
     }
+    V v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = src[src_i[k]];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t r = r0 + k * 64 + lane;
@@ -425,22 +394,66 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   const uint64_t sb = o0.shr - a.base.shr, ib = o0.inl - a.base.inl;
   SubRec* __restrict__ rows = a.rows + rb;
 
-  TabRef T;
+  // Merge table: LDS on the fast pass, a global slice on the overflow pass. Accesses branch on
+  // the (wave-uniform) kind so each compiles to typed ds_* / global_* instructions.
+  uint32_t* gk = nullptr;
+  uint32_t* gr = nullptr;
+  uint32_t* gm = nullptr;
+  uint32_t tmask = kLdsTab - 1;
   if (global_tab) {
     const uint32_t slots = a.list[2 * w + 1];
     uint32_t tb = 0;
     if (lane == 0) tb = atomicAdd(a.ovf + 2, slots);
     tb = __builtin_amdgcn_readfirstlane(tb);
-    T.key = a.tab + tb;
-    T.row = a.tab + a.tab_cap + tb;
-    T.meta = a.tab + 2 * a.tab_cap + tb;
-    T.mask = slots - 1;
-  } else {
-    T.key = lds_key[wv];
-    T.row = lds_row[wv];
-    T.meta = lds_meta[wv];
-    T.mask = kLdsTab - 1;
+    gk = a.tab + tb;
+    gr = a.tab + a.tab_cap + tb;
+    gm = a.tab + 2 * a.tab_cap + tb;
+    tmask = slots - 1;
   }
+  auto tk_load = [&](uint32_t i) -> uint32_t {
+    return global_tab ? __hip_atomic_load(gk + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : __hip_atomic_load(&lds_key[wv][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto tk_cas = [&](uint32_t i, uint32_t v) -> uint32_t {
+    return global_tab ? atomicCAS(gk + i, kTabEmpty, v) : atomicCAS(&lds_key[wv][i], kTabEmpty, v);
+  };
+  auto tk_store = [&](uint32_t i, uint32_t v) {
+    if (global_tab) gk[i] = v; else lds_key[wv][i] = v;
+  };
+  auto tr_load = [&](uint32_t i) -> uint32_t { return global_tab ? gr[i] : lds_row[wv][i]; };
+  auto tr_store = [&](uint32_t i, uint32_t v) {
+    if (global_tab) gr[i] = v; else lds_row[wv][i] = v;
+  };
+  auto tm_load = [&](uint32_t i) -> uint32_t { return global_tab ? gm[i] : lds_meta[wv][i]; };
+  auto tm_store = [&](uint32_t i, uint32_t v) {
+    if (global_tab) gm[i] = v; else lds_meta[wv][i] = v;
+  };
+  // Insert `key` (distinct across the active lanes); returns the slot and whether it was new.
+  auto tab_insert = [&](uint32_t key, bool* is_new) -> uint32_t {
+    uint32_t sl = hash32(key) & tmask;
+    for (uint32_t probes = 0; probes <= tmask; probes++) {
+      const uint32_t k = tk_load(sl);
+      if (k == key) {
+        *is_new = false;
+        return sl;
+      }
+      if (k == kTabEmpty) {
+        const uint32_t old = tk_cas(sl, key);
+        if (old == kTabEmpty) {
+          *is_new = true;
+          return sl;
+        }
+        if (old == key) {
+          *is_new = false;
+          return sl;
+        }
+      }
+      sl = (sl + 1) & tmask;
+    }
+    atomicOr(a.ix.err, kErrTableFull);  // sized at <= 1/2 load: unreachable
+    *is_new = false;
+    return 0;
+  };
   bool tab_ready = false;
   bool overflowed = false;  // fast pass only: now just counting table-bound records
   uint32_t tab_used = 0;
@@ -548,7 +561,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
       // Table pass: insert the queued records (the rare clients with several matches).
       auto drain = [&]() {
         if (!tab_ready) {
-          for (uint32_t q = lane; q <= T.mask; q += 64) T.key[q] = kTabEmpty;
+          for (uint32_t q = lane; q <= tmask; q += 64) tk_store(q, kTabEmpty);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           tab_ready = true;
         }
@@ -562,22 +575,22 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
           if (vt) {
             r = ms[tlist[wv][c0 + lane]];
             r.meta &= ~kMetaMergeBit;
-            slot = tab_insert(T, r.client, &is_new, a.ix.err);
+            slot = tab_insert(r.client, &is_new);
           }
           const uint64_t bn = __ballot(vt && is_new);
           if (vt && is_new) {  // first (minimum-rank) subscription of this client: the base
             const uint32_t pos = n_cli + prefix_before(bn);
             rows[pos] = r;
-            T.row[slot] = pos;
-            T.meta[slot] = r.meta;
+            tr_store(slot, pos);
+            tm_store(slot, r.meta);
           }
           n_cli += __popcll(bn);
           const bool dup = vt && !is_new;
           if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
-            const uint32_t mt = T.meta[slot];
+            const uint32_t mt = tm_load(slot);
             const uint32_t q = max(mt & kMetaQos, r.meta & kMetaQos);
             const uint32_t nm = (mt & ~kMetaQos) | q | (r.meta & kMetaNoLocal);
-            if ((nm & ~kMetaDirty) != (mt & ~kMetaDirty)) T.meta[slot] = nm | kMetaDirty;
+            if ((nm & ~kMetaDirty) != (mt & ~kMetaDirty)) tm_store(slot, nm | kMetaDirty);
           }
           const uint64_t be = __ballot(dup && r.ident > 0);
           if (dup && r.ident > 0) {  // Identifiers[n.Filter] = n.Identifier (id > 0)
@@ -600,12 +613,10 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
         SubRec rr[4];
         SubX xx[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint32_t k = i0 + u * 64 + lane;
-          if (k < m_cnt) {
-            rr[u] = ms[k];
-            xx[u] = mx[k];
-          }
+        for (int u = 0; u < 4; u++) {  // unconditional loads (see copy_lists)
+          const uint32_t k = min(i0 + u * 64 + lane, m_cnt - 1);
+          rr[u] = ms[k];
+          xx[u] = mx[k];
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -658,10 +669,10 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
 
   if (tab_ready) {  // write back merged Qos/NoLocal of bases that absorbed later matches
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t k = lane; k <= T.mask; k += 64) {
-      if (T.key[k] != kTabEmpty) {
-        const uint32_t m = T.meta[k];
-        if (m & kMetaDirty) rows[T.row[k]].meta = m & ~kMetaDirty;
+    for (uint32_t k = lane; k <= tmask; k += 64) {
+      if (tk_load(k) != kTabEmpty) {
+        const uint32_t m = tm_load(k);
+        if (m & kMetaDirty) rows[tr_load(k)].meta = m & ~kMetaDirty;
       }
     }
   }
