@@ -202,7 +202,7 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   msg.grow_to(1, NodeMsg{});
   seginfo.grow_to(1, SegInfo{0, 0});
   segbytes.grow_to(1, 0);
-  subx.grow_to(1, SubX{kNone, kNone});
+  subx.grow_to(1, SubX{{kNone, kNone, kNone, kNone}});
   subp_.resize(1, PartList{0, 0, 0});
   parts.m.grow_to(1, 0);
 }
@@ -422,12 +422,12 @@ void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
 
 void Index::encode_subx(uint32_t pos) {
   const PartList& p = subp_[pos];
-  SubX x{kNone, kNone};
-  if (p.cnt > 2) {
-    x = SubX{p.off, kPartIndirect | p.cnt};
+  SubX x{{kNone, kNone, kNone, kNone}};
+  if (p.cnt > 4) {
+    x.p[0] = p.off;
+    x.p[1] = kPartIndirect | p.cnt;
   } else {
-    if (p.cnt > 0) x.a = parts.m.h[p.off];
-    if (p.cnt > 1) x.b = parts.m.h[p.off + 1];
+    for (uint32_t i = 0; i < p.cnt; i++) x.p[i] = parts.m.h[p.off + i];
   }
   subx.at_w(pos) = x;
 }
@@ -439,7 +439,7 @@ void Index::sub_ensure(uint32_t n, uint32_t need) {
   while (nc < need) nc *= 2;
   NodeLists& L = lists.at_w(n);
   uint32_t no = subs.alloc(nc), cnt = L.n_direct + L.n_merge;
-  subx.grow_to(subs.m.size(), SubX{kNone, kNone});
+  subx.grow_to(subs.m.size(), SubX{{kNone, kNone, kNone, kNone}});
   subp_.resize(subs.m.size(), PartList{0, 0, 0});
   for (uint32_t i = 0; i < cnt; i++) move_slot(n, L.sub_off + i, no + i);
   subs.release(L.sub_off, cap);
@@ -461,7 +461,7 @@ uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
     L.n_direct++;
   }
   subs.m.at_w(pos) = r;
-  subx.at_w(pos) = SubX{kNone, kNone};
+  subx.at_w(pos) = SubX{{kNone, kNone, kNone, kNone}};
   subp_[pos] = PartList{0, 0, 0};
   sub_pos_.put((uint64_t)n << 32 | r.client, pos);
   subs.live++;
@@ -546,7 +546,7 @@ void Index::part_release(uint32_t pos) {
   parts.release(p.off, p.cap);
   parts.live -= p.cnt;
   p = PartList{0, 0, 0};
-  subx.at_w(pos) = SubX{kNone, kNone};
+  subx.at_w(pos) = SubX{{kNone, kNone, kNone, kNone}};
 }
 
 void Index::path_strs(uint32_t n, uint32_t* out, int* len) const {

@@ -466,7 +466,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   auto gword = [&](uint32_t i) {
     return a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + i] : a.gathers[o0.g + i];
   };
-  if (set_ok) {
+  if (set_ok && !(a.ablate & 16)) {
     for (uint32_t k = lane; k < kGSet; k += 64) gset[wv][k] = kTabEmpty;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -608,7 +608,9 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
       // belong to distinct clients, so their order within the gather does not matter.
       for (uint32_t i0 = 0;; i0 += 256) {
         const bool done = i0 >= m_cnt;
-        if ((done || nt + 256 > kTList) && nt && !overflowed) drain();  // the one call site
+        if ((done || nt + 256 > kTList) && nt && !overflowed) {  // the one call site
+          if (a.ablate & 32) nt = 0; else drain();
+        }
         if (done) break;
         SubRec rr[4];
         SubX xx[4];
@@ -623,15 +625,22 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
           const uint32_t k = i0 + u * 64 + lane;
           const bool v = k < m_cnt;
           bool shared_client = false;
-          if (v) {
+          if (v && !(a.ablate & 8)) {
             if (set_ok) {
               const SubX x = xx[u];
-              if (x.b != kNone && (x.b & kPartIndirect)) {
-                const uint32_t pc = x.b & ~kPartIndirect;
-                for (uint32_t p = 0; p < pc && !shared_client; p++)
-                  shared_client = gathered(a.ix.parts[x.a + p]);
+              if (x.p[1] != kNone && (x.p[1] & kPartIndirect)) {
+                // long partner list: four independent loads per round
+                const uint32_t pc = x.p[1] & ~kPartIndirect;
+                for (uint32_t p0 = 0; p0 < pc && !shared_client; p0 += 4) {
+                  uint32_t q[4];
+#pragma unroll
+                  for (int e = 0; e < 4; e++) q[e] = a.ix.parts[x.p[0] + min(p0 + e, pc - 1)];
+#pragma unroll
+                  for (int e = 0; e < 4; e++) shared_client |= gathered(q[e]);
+                }
               } else {
-                shared_client = (x.a != kNone && gathered(x.a)) || (x.b != kNone && gathered(x.b));
+#pragma unroll
+                for (int e = 0; e < 4; e++) shared_client |= x.p[e] != kNone && gathered(x.p[e]);
               }
             } else {
               shared_client = true;
@@ -642,7 +651,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
           if (!global_tab && tab_used > kLdsTabMax) overflowed = true;
           if (overflowed) continue;  // now only counting, for the overflow pass's table
           const uint64_t bd = __ballot(v && !shared_client);
-          if (v && !shared_client) {
+          if (v && !shared_client && !(a.ablate & 64)) {
             u32x4 rv = *reinterpret_cast<const u32x4*>(&rr[u]);
             rv.w &= ~kMetaMergeBit;
             __builtin_nontemporal_store(rv, reinterpret_cast<u32x4*>(rows + n_cli + prefix_before(bd)));

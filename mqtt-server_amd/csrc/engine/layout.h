@@ -135,10 +135,11 @@ struct SubRec {  // == mq_client_row
 };
 // Partner list of a subscription that may merge: the nodes of its client's other
 // subscriptions that could match the same topic. At match time the record needs the merge
-// table only if a partner node is gathered for the topic too. Device encoding: up to two
-// partners inline {p0|kNone, p1|kNone}; more as {offset into parts, kPartIndirect | count}.
+// table only if a partner node is gathered for the topic too. Device encoding (16 B): up to
+// four partners inline {p0, p1, p2, p3} (kNone-padded); more as
+// {offset into parts, kPartIndirect | count, kNone, kNone}.
 struct SubX {
-  uint32_t a, b;
+  uint32_t p[4];
 };
 constexpr uint32_t kPartIndirect = 0x80000000u;
 
