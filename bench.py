@@ -133,7 +133,8 @@ def main():
             "subs": args.subs, "clients": n_clients, "topics_per_gpu": n,
             "parallelism": f"index replicated on {world} GPU(s), topic batch per GPU",
         },
-        "kernels_ms_per_step": {k: v[1] / max(1, args.steps) for k, v in prof.items()},
+        "kernels_ms_per_step": {k: v[1] / max(1, args.steps) for k, v in prof.items() if v[1] > 0},
+        "counters_per_step": {k: v[0] / max(1, args.steps) for k, v in prof.items() if v[1] == 0},
         "emit_chunks_per_step": chunks,
     }
 

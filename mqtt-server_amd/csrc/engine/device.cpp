@@ -113,6 +113,16 @@ void Profiler::drain() {
   pending_.clear();
 }
 
+void Profiler::count(const char* name, uint64_t n) {
+  if (!on_) return;
+  auto it = std::find_if(totals_.begin(), totals_.end(), [&](const Total& t) { return t.name == name; });
+  if (it == totals_.end()) {
+    totals_.push_back(Total{name, 0, 0});
+    it = totals_.end() - 1;
+  }
+  it->launches += n;
+}
+
 int Profiler::read(mq_kernel_time* out, uint32_t cap) {
   drain();
   uint32_t n = 0;
@@ -274,6 +284,9 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   check_err(s);
   const TopicOff tot = h_bpre_[nb];
 
+  prof.count("topics", n);
+  prof.count("gathers", tot.g);
+  prof.count("reserved_rows", tot.rows);
   // A topic with more gathers than its count-pass slots: write all gather lists compactly.
   const uint32_t* gathers = gslots_.as<uint32_t>();
   uint32_t gstride = kGatherCap;
@@ -348,6 +361,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     uint32_t ov[2] = {0, 0};
     hip_check(hipMemcpyAsync(ov, a.ovf, sizeof(ov), hipMemcpyDeviceToHost, s), "D2H ovf");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    prof.count("overflow_topics", ov[0]);
     if (ov[0]) {
       tab_.ensure((size_t)ov[1] * 3 * sizeof(uint32_t));
       a.tab = tab_.as<uint32_t>();

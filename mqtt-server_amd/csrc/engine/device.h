@@ -59,6 +59,8 @@ class Profiler {
   void begin(hipStream_t s);
   void end(const char* name, hipStream_t s);
   int read(mq_kernel_time* out, uint32_t cap);
+  // Event counters reported next to the kernels (launches = count, total_ms = 0).
+  void count(const char* name, uint64_t n);
   void reset();
 
  private:
