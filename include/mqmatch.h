@@ -175,7 +175,8 @@ int mq_match_batch(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* of
                    mq_match_result** out);
 
 /* Device-resident variant (inputs already in HBM on the index's device, enqueued on
- * `hip_stream`, a hipStream_t or NULL). `out` receives DEVICE pointers owned by the index and
+ * `hip_stream`, a hipStream_t or NULL). d_topic_bytes must be 16-byte aligned and readable up
+ * to the next 16-byte boundary past its end (any hipMalloc / torch allocation is). `out` receives DEVICE pointers owned by the index and
  * valid until its next match call. Batches whose rows exceed the output budget are processed
  * in chunks; then only the last chunk's rows remain resident and out->topics covers that
  * chunk (out->n_topics); mq_match_chunks() reports the chunk count of the last call. */

@@ -24,17 +24,6 @@ namespace mq {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint64_t find_slash(const uint8_t* __restrict__ b, uint64_t s, uint64_t end) {
-  while (s < end && b[s] != '/') s++;
-  return s;
-}
-
-// Start of the segment that ends at `e` (exclusive): one past the previous '/' or b0.
-__device__ __forceinline__ uint64_t seg_start_before(const uint8_t* __restrict__ b, uint64_t b0, uint64_t e) {
-  while (e > b0 && b[e - 1] != '/') e--;
-  return e;
-}
-
 // Byte reader with a one-chunk register cache: one 16-byte load serves 16 sequential byte
 // reads. The topic buffer must be readable up to its next 16-byte boundary (include/mqmatch.h).
 struct ByteReader {
@@ -779,16 +768,20 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
   };
   // len(filter) == 0 || Retained.Len() == 0 (topics.go:535)
   if (b1 > b0 && ix.retained_len != 0) {
+    ByteReader R(fb);
     bool wild = false;
-    for (uint64_t i = b0; i < b1; i++) wild |= (fb[i] == '+') | (fb[i] == '#');
+    for (uint64_t i = b0; i < b1; i++) {
+      const uint32_t ch = R.at(i);
+      wild |= (ch == '+') | (ch == '#');
+    }
     if (!wild) {
       // no wildcard: Retained.Get(filter) (topics.go:539-544)
       uint32_t node = kRoot;
       uint64_t s = b0;
       for (;;) {
-        const uint64_t e = find_slash(fb, s, b1);
-        const uint32_t len = (uint32_t)(e - s);
-        node = lookup(ix, node, seg_key(fb + s, len), fb + s, len);
+        SegKey key;
+        const uint64_t e = scan_segment(R, s, b1, &key);
+        node = lookup(ix, node, key, fb + s, (uint32_t)(e - s));
         if (node == kNone || e >= b1) break;
         s = e + 1;
       }
@@ -798,7 +791,8 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
       }
     } else {
       uint32_t node = kRoot, d = 0, wd = 0;  // wd: level of the segment in the window
-      uint64_t s = b0, e = find_slash(fb, b0, b1);
+      SegKey key;  // key of the window's segment (valid after every forward move)
+      uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
       uint32_t cursor = 0;
       bool resume = false;  // re-entering an enumeration frame after a child returned
       for (uint64_t guard = 0;; guard++) {
@@ -808,8 +802,9 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
         }
         const bool has_next = (wd == d) && (e < b1);
         const uint32_t len = (uint32_t)(e - s);
-        const bool plus = len == 1 && fb[s] == '+';
-        const bool hash = len == 1 && fb[s] == '#';
+        const uint32_t c0 = len == 1 ? R.at(s) : 0;
+        const bool plus = c0 == '+';
+        const bool hash = c0 == '#';
         bool descended = false;
         if (plus || hash) {  // topics.go:547-565
           const NodeMsg nm = ix.msg[node];
@@ -825,7 +820,7 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
               d++;
               if (e < b1) {
                 s = e + 1;
-                e = find_slash(fb, s, b1);
+                e = scan_segment(R, s, b1, &key);
                 wd++;
               }
               descended = true;
@@ -833,13 +828,13 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
             }
           }
         } else if (!resume) {  // literal level (topics.go:568-576)
-          const uint32_t p = lookup(ix, node, seg_key(fb + s, len), fb + s, len);
+          const uint32_t p = lookup(ix, node, key, fb + s, len);
           if (p != kNone) {
             if (has_next) {
               node = p;
               d++;
               s = e + 1;
-              e = find_slash(fb, s, b1);
+              e = scan_segment(R, s, b1, &key);
               wd++;
               descended = true;
             } else {
@@ -856,13 +851,14 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
           resume = false;
           continue;
         }
-        // frame finished: return to the parent frame
+        // frame finished: return to the parent frame (its key is not needed again: a literal
+        // frame is done, an enumeration frame resumes after this child)
         if (d == 0) break;
         const NodeMsg cm = ix.msg[node];
         node = ix.walk[node].parent_flags & kParentMask;
         if (wd == d) {
           e = s - 1;
-          s = seg_start_before(fb, b0, e);
+          s = seg_start_before(R, b0, e);
           wd--;
         }
         d--;
