@@ -1,0 +1,117 @@
+// C++ host mirror of the reference's Go TopicsIndex API (/root/reference/topics.go:306-698),
+// layered on the engine's C-ABI (include/mqmatch.h). It is what the Go cgo shim
+// (mqtt-server_amd/go/topics_gpu.go) does, in the host language available here: same method
+// names and argument meaning, Go-shaped results (maps keyed by client / filter / id), and the
+// host-side SelectShared / MergeSharedSelected. Matching always runs on the GPU engine; an
+// engine error throws mq::host::EngineError.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "mqmatch.h"
+
+namespace mq {
+namespace host {
+
+// packets.Subscription (packets/packets.go:172-182); identifiers is nullopt-as-empty + flag.
+struct Subscription {
+  std::string Filter;
+  int Identifier = 0;
+  bool HasIdentifiers = false;
+  std::map<std::string, int> Identifiers;
+  uint8_t RetainHandling = 0;
+  uint8_t Qos = 0;
+  bool RetainAsPublished = false;
+  bool NoLocal = false;
+
+  // Subscription.Merge (packets/packets.go:254-274)
+  Subscription Merge(const Subscription& n) const {
+    Subscription s = *this;
+    if (!s.HasIdentifiers) {
+      s.HasIdentifiers = true;
+      s.Identifiers = {{s.Filter, s.Identifier}};
+    }
+    if (n.Identifier > 0) s.Identifiers[n.Filter] = n.Identifier;
+    if (n.Qos > s.Qos) s.Qos = n.Qos;
+    if (n.NoLocal) s.NoLocal = true;
+    return s;
+  }
+};
+
+struct InlineSubscription {
+  Subscription Sub;  // the Handler func stays with the embedding application
+};
+
+// Subscribers (topics.go:312-347)
+struct Subscribers {
+  std::map<std::string, std::map<std::string, Subscription>> Shared;
+  std::map<std::string, Subscription> SharedSelected;
+  std::map<std::string, Subscription> Subscriptions;
+  std::map<int, InlineSubscription> InlineSubscriptions;
+
+  // SelectShared: the Go pick is the first entry in random map order; this takes the first
+  // in sorted order, one of the orders Go can produce (topics.go:320-333).
+  void SelectShared() {
+    SharedSelected.clear();
+    for (auto& g : Shared)
+      for (auto& kv : g.second) {
+        auto it = SharedSelected.find(kv.first);
+        const Subscription cls = it == SharedSelected.end() ? kv.second : it->second;
+        SharedSelected[kv.first] = cls.Merge(kv.second);
+        break;
+      }
+  }
+  // MergeSharedSelected (topics.go:338-347)
+  void MergeSharedSelected() {
+    for (auto& kv : SharedSelected) {
+      auto it = Subscriptions.find(kv.first);
+      const Subscription cls = it == Subscriptions.end() ? kv.second : it->second;
+      Subscriptions[kv.first] = cls.Merge(kv.second);
+    }
+  }
+};
+
+struct EngineError : std::runtime_error {
+  int code;
+  EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+class TopicsIndex {
+ public:
+  explicit TopicsIndex(int device = 0);  // NewTopicsIndex (topics.go:356)
+  ~TopicsIndex();
+  TopicsIndex(const TopicsIndex&) = delete;
+  TopicsIndex& operator=(const TopicsIndex&) = delete;
+
+  bool Subscribe(const std::string& client, const Subscription& sub);   // topics.go:401
+  bool Unsubscribe(const std::string& filter, const std::string& client);  // topics.go:423
+  bool InlineSubscribe(const InlineSubscription& sub);                   // topics.go:368
+  bool InlineUnsubscribe(int id, const std::string& filter);             // topics.go:382
+  // RetainMessage (topics.go:453): returns 1 / 0 / -1; `handle` names the packet.
+  int64_t RetainMessage(const std::string& topic, uint64_t handle, uint32_t payload_len,
+                        bool retain);
+  void RetainedDelete(const std::string& topic);  // server.go:1726 (Q12)
+  uint64_t RetainedLen() const;
+  std::vector<uint64_t> Messages(const std::string& filter);  // topics.go:525 (handles)
+  Subscribers Subscribers_(const std::string& topic);          // topics.go:583
+  std::vector<Subscribers> SubscribersBatch(const std::vector<std::string>& topics);
+
+  mq_index* handle() { return idx_; }
+
+ private:
+  uint32_t cid(const std::string& c);
+  uint32_t fid(const std::string& f);
+  mq_index* idx_ = nullptr;
+  std::unordered_map<std::string, uint32_t> client_ids_, filter_ids_;
+  std::vector<std::string> clients_, filters_;
+  std::map<std::pair<uint32_t, uint32_t>, Subscription> stored_;  // (client, filter)
+  std::map<std::pair<int, uint32_t>, InlineSubscription> inline_;  // (id, filter)
+};
+
+}  // namespace host
+}  // namespace mq

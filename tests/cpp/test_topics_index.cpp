@@ -1,0 +1,221 @@
+// The reference's TopicsIndex tests (/root/reference/topics_test.go) restated against the C++
+// host mirror (mqtt-server_amd/csrc/host/topics_index.h) over the GPU engine. White-box checks
+// of index.root.particles are restated through the public API. Run by
+// tests/test_gpu_parity.py::test_cpp_host_mirror (needs a GPU).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "topics_index.h"
+
+using mq::host::InlineSubscription;
+using mq::host::Subscription;
+using mq::host::TopicsIndex;
+
+static int g_fail = 0;
+#define REQUIRE(c)                                                        \
+  do {                                                                    \
+    if (!(c)) {                                                           \
+      std::fprintf(stderr, "%s:%d: REQUIRE(%s) failed\n", __FILE__, __LINE__, #c); \
+      g_fail++;                                                           \
+    }                                                                     \
+  } while (0)
+
+static Subscription S(const std::string& f, uint8_t qos = 0, int id = 0, bool nolocal = false) {
+  Subscription s;
+  s.Filter = f;
+  s.Qos = qos;
+  s.Identifier = id;
+  s.NoLocal = nolocal;
+  return s;
+}
+
+static int ident(const Subscription& s, const std::string& f) {  // Go map zero value
+  auto it = s.Identifiers.find(f);
+  return it == s.Identifiers.end() ? 0 : it->second;
+}
+
+static void TestSubscribe() {  // topics_test.go:170-226
+  TopicsIndex x;
+  REQUIRE(x.Subscribe("cl1", S("a/b/c", 2)));
+  REQUIRE(!x.Subscribe("cl1", S("a/b/c", 1)));
+  REQUIRE(x.Subscribe("cl1", S("A/B/c", 1)));
+  REQUIRE(x.Subscribe("cl1", S("d/+")));
+  REQUIRE(x.Subscribe("cl1", S("d/e/#")));
+  REQUIRE(x.Subscribers_("a/b/c").Subscriptions.at("cl1").Qos == 1);
+}
+
+static void TestUnsubscribe() {  // topics_test.go:254-297
+  TopicsIndex x;
+  x.Subscribe("cl1", S("a/b/c/d", 1));
+  x.Subscribe("cl1", S("a/b/+/d", 1));
+  x.Subscribe("cl1", S("d/e/f", 1));
+  x.Subscribe("cl2", S("d/e/f", 1));
+  x.Subscribe("cl3", S("#", 2));
+  REQUIRE(x.Unsubscribe("a/b/c/d", "cl1"));
+  auto s = x.Subscribers_("a/b/c/d");
+  REQUIRE(s.Subscriptions.size() == 2 && s.Subscriptions.at("cl1").Filter == "a/b/+/d");
+  REQUIRE(x.Unsubscribe("d/e/f", "cl1"));
+  s = x.Subscribers_("d/e/f");
+  REQUIRE(s.Subscriptions.count("cl2") && s.Subscriptions.count("cl3") && !s.Subscriptions.count("cl1"));
+  REQUIRE(!x.Unsubscribe("fdasfdas/dfsfads/sa", "nobody"));
+}
+
+static void TestRetainMessage() {  // topics_test.go:408-443
+  TopicsIndex x;
+  REQUIRE(x.RetainMessage("a/b/c", 1, 5, true) == 1);
+  REQUIRE(x.RetainedLen() == 1);
+  REQUIRE(x.RetainMessage("a/b/d/f", 2, 5, true) == 1);
+  REQUIRE(x.RetainMessage("a/b/d/f", 3, 5, true) == 1);
+  REQUIRE(x.RetainMessage("a/b/c", 4, 0, false) == -1);
+  REQUIRE(x.RetainMessage("a/b/c", 5, 0, false) == 0);
+}
+
+static void TestScanSubscribers() {  // topics_test.go:490-528
+  TopicsIndex x;
+  x.Subscribe("cl1", S("a/b/c", 1, 22));
+  x.Subscribe("cl1", S("a/b/c/d/e/f", 1));
+  x.Subscribe("cl1", S("a/b/c/d/+/f", 2));
+  x.Subscribe("cl2", S("a/#", 0));
+  x.Subscribe("cl2", S("a/b/c", 1));
+  x.Subscribe("cl2", S("a/b/+", 2, 77));
+  x.Subscribe("cl2", S("d/e/f", 2, 7237));
+  x.Subscribe("cl2", S("$SYS/uptime", 2, 3));
+  x.Subscribe("cl3", S("+/b", 1, 234));
+  x.Subscribe("cl4", S("#", 0, 5));
+  x.Subscribe("cl2", S("$SYS/test", 0, 2));
+  auto s = x.Subscribers_("a/b/c").Subscriptions;
+  REQUIRE(s.size() == 3 && s.count("cl1") && s.count("cl2") && s.count("cl4"));
+  REQUIRE(s.at("cl1").Qos == 1 && s.at("cl2").Qos == 2 && s.at("cl4").Qos == 0);
+  REQUIRE(ident(s.at("cl1"), "a/b/c") == 22);
+  REQUIRE(ident(s.at("cl2"), "a/#") == 0);
+  REQUIRE(ident(s.at("cl2"), "a/b/+") == 77);
+  REQUIRE(ident(s.at("cl2"), "a/b/c") == 0);
+  REQUIRE(ident(s.at("cl4"), "#") == 5);
+  s = x.Subscribers_("d/e/f/g").Subscriptions;
+  REQUIRE(s.size() == 1 && s.count("cl4"));
+  REQUIRE(x.Subscribers_("").Subscriptions.empty());
+}
+
+static void TestScanSubscribersShared() {  // topics_test.go:539-566
+  TopicsIndex x;
+  x.Subscribe("cl1", S("$SHARE/tmp/a/b/c", 1, 111));
+  x.Subscribe("cl2", S("$SHARE/tmp/a/b/c", 0, 112));
+  x.Subscribe("cl3", S("$SHARE/tmp2/a/b/c", 0, 113));
+  x.Subscribe("cl2", S("$SHARE/tmp/a/b/+", 0, 10));
+  x.Subscribe("cl3", S("$SHARE/tmp/a/b/+", 1, 200));
+  x.Subscribe("cl4", S("$SHARE/tmp/a/b/+", 0, 201));
+  x.Subscribe("cl5", S("$SHARE/tmp/a/b/c/#", 0));
+  auto s = x.Subscribers_("a/b/c");
+  REQUIRE(s.Shared.size() == 4);
+  s.SelectShared();
+  REQUIRE(s.SharedSelected.size() == 4 || s.SharedSelected.size() == 3);  // one pick per group/filter
+}
+
+static void TestSubscribersFind() {  // topics_test.go:590-625
+  struct Row {
+    const char *f, *t;
+    bool m;
+  } rows[] = {
+      {"a", "a", true}, {"a/", "a", false}, {"a/", "a/", true}, {"/a", "/a", true},
+      {"path/to/my/mqtt", "path/to/my/mqtt", true}, {"path/to/+/mqtt", "path/to/my/mqtt", true},
+      {"+/to/+/mqtt", "path/to/my/mqtt", true}, {"#", "path/to/my/mqtt", true},
+      {"+/+/+/+", "path/to/my/mqtt", true}, {"+/+/+/#", "path/to/my/mqtt", true},
+      {"zen/#", "zen", true}, {"trailing-end/#", "trailing-end/", true},
+      {"+/prefixed", "/prefixed", true}, {"+/+/#", "path/to/my/mqtt", true},
+      {"path/to/", "path/to/my/mqtt", false}, {"#/stuff", "path/to/my/mqtt", false},
+      {"#", "$SYS/info", false}, {"$SYS/#", "$SYS/info", true}, {"+/info", "$SYS/info", false},
+  };
+  for (const Row& r : rows) {
+    TopicsIndex x;
+    x.Subscribe("cl1", S(r.f));
+    const bool got = x.Subscribers_(r.t).Subscriptions.size() == 1;
+    if (got != r.m) std::fprintf(stderr, "find: filter %s topic %s\n", r.f, r.t);
+    REQUIRE(got == r.m);
+  }
+}
+
+static void TestMessagesPattern() {  // topics_test.go:640-685
+  TopicsIndex x;
+  const char* topics[] = {"$SYS/uptime", "$SYS/info", "a/b/c/d", "a/b/c/e", "a/b/d/f",
+                          "q/w/e/r/t/y", "q/x/e/r/t/o", "asdf"};
+  uint64_t h = 1;
+  for (const char* t : topics) x.RetainMessage(t, h++, 5, true);
+  struct Row {
+    const char* f;
+    size_t n;
+  } rows[] = {{"a/b/c/d", 1}, {"$SYS/+", 2}, {"$SYS/#", 2}, {"#", 6}, {"a/b/c/+", 2},
+              {"a/+/c/+", 2}, {"+/+/+/d", 1}, {"q/w/e/#", 1}, {"+/+/+/+", 3}, {"q/#", 2},
+              {"asdf", 1}, {"", 0}, {"#", 6}};
+  for (const Row& r : rows) {
+    const size_t got = x.Messages(r.f).size();
+    if (got != r.n) std::fprintf(stderr, "messages %s: %zu != %zu\n", r.f, got, r.n);
+    REQUIRE(got == r.n);
+  }
+}
+
+static void TestInline() {  // topics_test.go:946-1067
+  TopicsIndex x;
+  InlineSubscription a;
+  a.Sub = S("a/b/c", 0, 1);
+  REQUIRE(x.InlineSubscribe(a));
+  REQUIRE(!x.InlineSubscribe(a));
+  a.Sub.Identifier = 2;
+  REQUIRE(x.InlineSubscribe(a));
+  InlineSubscription b;
+  b.Sub = S("#", 0, 1);
+  x.InlineSubscribe(b);
+  auto s = x.Subscribers_("a/b/c");
+  REQUIRE(s.InlineSubscriptions.size() == 2 && s.InlineSubscriptions.at(1).Sub.Filter == "#");
+  REQUIRE(x.InlineUnsubscribe(1, "a/b/c"));
+  REQUIRE(!x.InlineUnsubscribe(1, "not/exist"));
+}
+
+static void TestPublishToSubscribersIdentifiers() {  // server_test.go:1973-1999
+  TopicsIndex x;
+  REQUIRE(x.Subscribe("cl", S("a/b/+", 0, 2)));
+  REQUIRE(x.Subscribe("cl", S("a/#", 0, 3)));
+  REQUIRE(x.Subscribe("cl", S("d/e/f", 0, 4)));
+  auto sub = x.Subscribers_("a/b/c").Subscriptions.at("cl");
+  std::vector<int> ids;
+  for (auto& kv : sub.Identifiers)
+    if (kv.second > 0) ids.push_back(kv.second);
+  std::sort(ids.begin(), ids.end());
+  REQUIRE((ids == std::vector<int>{2, 3}));  // packets/tpackets.go:1848-1872: 11,2, 11,3
+}
+
+static void TestMergeSharedSelected() {  // topics_test.go:568-588
+  mq::host::Subscribers s;
+  s.SharedSelected["cl1"] = S("$SHARE/tmp/a/b/c", 1, 110);
+  s.SharedSelected["cl2"] = S("$SHARE/tmp2/a/b/c", 1, 111);
+  s.Subscriptions["cl2"] = S("a/b/c", 1, 112);
+  s.MergeSharedSelected();
+  REQUIRE(s.Subscriptions.size() == 2);
+  REQUIRE((s.Subscriptions.at("cl2").Identifiers == std::map<std::string, int>{{"$SHARE/tmp2/a/b/c", 111}, {"a/b/c", 112}}));
+}
+
+int main() {
+  try {
+    TestSubscribe();
+    TestUnsubscribe();
+    TestRetainMessage();
+    TestScanSubscribers();
+    TestScanSubscribersShared();
+    TestSubscribersFind();
+    TestMessagesPattern();
+    TestInline();
+    TestPublishToSubscribersIdentifiers();
+    TestMergeSharedSelected();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "exception: %s\n", e.what());
+    return 2;
+  }
+  if (g_fail) {
+    std::fprintf(stderr, "%d checks failed\n", g_fail);
+    return 1;
+  }
+  std::printf("cpp host mirror: all reference test cases passed\n");
+  return 0;
+}

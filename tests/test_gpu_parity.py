@@ -309,3 +309,13 @@ def test_merge_table_overflow_pass(gpu_available):
     topics = ["o/p", "o/q", "o", "o/z", "o/p/x"]
     for t, g in zip(topics, e.subscribers_batch(topics)):
         assert g == o.subscribers(t), t
+
+
+def test_cpp_host_mirror(gpu_available):
+    """The reference's topics_test.go cases restated in C++ against the C++ host mirror of the
+    Go API (mqtt-server_amd/csrc/host), running on the GPU engine."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "mqtt-server_amd", "build", "test_topics_index")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
