@@ -45,7 +45,7 @@ extern "C" {
 #define MQ_META_NOLOCAL 0x100u      /* merged NoLocal = OR over the client's matches */
 #define MQ_META_RAP 0x200u          /* base RetainAsPublished */
 #define MQ_META_RH_SHIFT 10         /* base RetainHandling, 2 bits */
-#define MQ_META_MERGE 0x1000u       /* internal: subscription may merge with another of its client */
+/* bit 0x1000 is reserved (never set in output rows) */
 
 typedef struct mq_index mq_index;
 

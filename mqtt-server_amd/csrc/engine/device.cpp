@@ -147,17 +147,16 @@ Device::Device(int dev) : dev_(dev) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   const char* e = getenv("MQ_CHUNK_ROWS");
   chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : (256ull << 20);  // 4 GiB of 16-B rows
-  const char* ab = getenv("MQ_EMIT_ABLATE");  // diagnosis only: results are wrong when set
-  ablate_ = ab ? (uint32_t)strtoul(ab, nullptr, 0) : 0;
+  wprof_on_ = getenv("MQ_EMIT_PROF") != nullptr;  // diagnosis only
 }
 
 Device::~Device() {
   (void)hipSetDevice(dev_);
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
-  subx_.release(); parts_.release();
+  npair_.release(); pent_.release(); plist_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_, &gslots_, &ovf_})
+                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_, &gslots_, &ovf_, &wprof_})
     b->release();
 }
 
@@ -166,7 +165,7 @@ uint64_t Device::device_bytes() const {
                lists_.cap * sizeof(NodeLists) + msg_.cap * sizeof(NodeMsg) +
                seginfo_.cap * sizeof(SegInfo) + segbytes_.cap + subs_.cap * sizeof(SubRec) +
                shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4 +
-               subx_.cap * sizeof(SubX) + parts_.cap * 4;
+               npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * 4;
   for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
                           &shr_rows_, &inl_rows_, &tab_, &res_})
     b += x->bytes;
@@ -176,6 +175,7 @@ uint64_t Device::device_bytes() const {
 void Device::sync(Index& ix, hipStream_t s) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   if (ix.version() == synced_version_ && edges_.d) return;
+  ix.flush_pairs();
   edges_.sync(ix.edges, s, &uploaded_);
   walk_.sync(ix.walk, s, &uploaded_);
   lists_.sync(ix.lists, s, &uploaded_);
@@ -183,8 +183,9 @@ void Device::sync(Index& ix, hipStream_t s) {
   seginfo_.sync(ix.seginfo, s, &uploaded_);
   segbytes_.sync(ix.segbytes, s, &uploaded_);
   subs_.sync(ix.subs.m, s, &uploaded_);
-  subx_.sync(ix.subx, s, &uploaded_);
-  parts_.sync(ix.parts.m, s, &uploaded_);
+  npair_.sync(ix.npair, s, &uploaded_);
+  pent_.sync(ix.pent.m, s, &uploaded_);
+  plist_.sync(ix.plist.m, s, &uploaded_);
   shr_.sync(ix.shr.m, s, &uploaded_);
   inl_.sync(ix.inl.m, s, &uploaded_);
   children_.sync(ix.children.m, s, &uploaded_);
@@ -205,8 +206,9 @@ DevIndex Device::dev_index(const Index& ix) const {
   d.seginfo = seginfo_.d;
   d.segbytes = segbytes_.d;
   d.subs = subs_.d;
-  d.subx = subx_.d;
-  d.parts = parts_.d;
+  d.npair = npair_.d;
+  d.pent = pent_.d;
+  d.plist = plist_.d;
   d.shr = shr_.d;
   d.inl = inl_.d;
   d.children = children_.d;
@@ -345,10 +347,17 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     a.tab = nullptr;
     a.tab_cap = 0;
     a.res = res_.as<mq_topic_result_dev>();
-    a.ablate = ablate_;
     a.list = nullptr;
     a.n_list = 0;
     a.ovf = ovf_.as<uint32_t>();
+    a.wprof = nullptr;
+    if (wprof_on_) {
+      if (!wprof_.p) {
+        wprof_.ensure(kWpCount * sizeof(unsigned long long));
+        hip_check(hipMemsetAsync(wprof_.p, 0, kWpCount * sizeof(unsigned long long), s), "memset wprof");
+      }
+      a.wprof = wprof_.as<unsigned long long>();
+    }
     hip_check(hipMemsetAsync(a.ovf, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
     prof.begin(s);
     launch_emit(a, s);
@@ -374,6 +383,16 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       hip_check(hipGetLastError(), "k_emit<overflow>");
     }
 
+    if (wprof_on_) {  // cumulative since the Device was created
+      unsigned long long w[kWpCount];
+      hip_check(hipMemcpyAsync(w, a.wprof, sizeof(w), hipMemcpyDeviceToHost, s), "D2H wprof");
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      fprintf(stderr,
+              "[wprof] waves %llu total %llu setup %llu copy %llu merge %llu drain %llu mrecs %llu "
+              "tabrecs %llu lookups %llu probes %llu chunks %llu\n",
+              w[kWpWaves], w[kWpTotal], w[kWpSetup], w[kWpCopy], w[kWpMerge], w[kWpDrain],
+              w[kWpMergeRecs], w[kWpTabRecs], w[kWpLookups], w[kWpProbes], w[kWpChunks]);
+    }
     const TopicOff& lo = h_bpre_[c.b0];
     const TopicOff& hi = h_bpre_[c.b1];
     const uint32_t nt = a.t1 - a.t0;
@@ -467,7 +486,8 @@ template struct DevMirror<NodeMsg>;
 template struct DevMirror<SegInfo>;
 template struct DevMirror<uint8_t>;
 template struct DevMirror<SubRec>;
-template struct DevMirror<SubX>;
+template struct DevMirror<NodePair>;
+template struct DevMirror<PairEnt>;
 template struct DevMirror<ShrRec>;
 template struct DevMirror<InlRec>;
 template struct DevMirror<uint32_t>;

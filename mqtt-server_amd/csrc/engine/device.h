@@ -115,7 +115,7 @@ class Device {
   uint64_t uploaded_ = 0, syncs_ = 0;
   uint32_t last_chunks_ = 0;
   uint64_t chunk_rows_budget_;
-  uint32_t ablate_ = 0;
+  bool wprof_on_ = false;  // MQ_EMIT_PROF: k_emit wave-phase profile to stderr
   DevMirror<EdgeSlot> edges_;
   DevMirror<NodeWalk> walk_;
   DevMirror<NodeLists> lists_;
@@ -123,15 +123,16 @@ class Device {
   DevMirror<SegInfo> seginfo_;
   DevMirror<uint8_t> segbytes_;
   DevMirror<SubRec> subs_;
-  DevMirror<SubX> subx_;
-  DevMirror<uint32_t> parts_;
+  DevMirror<NodePair> npair_;
+  DevMirror<PairEnt> pent_;
+  DevMirror<uint32_t> plist_;
   DevMirror<ShrRec> shr_;
   DevMirror<InlRec> inl_;
   DevMirror<uint32_t> children_;
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   DevBuf rows_, shr_rows_, inl_rows_, tab_, res_, err_;
-  DevBuf msg_handles_, msg_base_, msg_count_, gslots_, ovf_;
+  DevBuf msg_handles_, msg_base_, msg_count_, gslots_, ovf_, wprof_;
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;
   uint64_t empty_handle_ = 0;

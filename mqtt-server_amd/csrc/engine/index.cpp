@@ -202,9 +202,11 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   msg.grow_to(1, NodeMsg{});
   seginfo.grow_to(1, SegInfo{0, 0});
   segbytes.grow_to(1, 0);
-  subx.grow_to(1, SubX{{kNone, kNone, kNone, kNone}});
   subp_.resize(1, PartList{0, 0, 0});
   parts.m.grow_to(1, 0);
+  npair.grow_to(1, NodePair{0, kNone, 0, 0});
+  pent.m.grow_to(1, PairEnt{kNone, 0, 0, 0});
+  plist.m.grow_to(1, 0);
 }
 
 // ---- edge table -------------------------------------------------------------------------------
@@ -296,6 +298,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
     walk.grow_to(id + 1, NodeWalk{kNone, kNone, 0, kNone});
     lists.grow_to(id + 1, NodeLists{});
     msg.grow_to(id + 1, NodeMsg{});
+    npair.grow_to(id + 1, NodePair{0, kNone, 0, 0});
   }
   NodeHost& h = nh_[id];
   h = NodeHost{};
@@ -367,6 +370,7 @@ void Index::remove_node(uint32_t n) {
   shr.release(lists.h[n].shr_off, h.shr_cap);
   inl.release(lists.h[n].inl_off, h.inl_cap);
   children.release(msg.h[n].child_off, h.child_cap);
+  pairs_release(n);
   walk.at_w(n) = NodeWalk{kNone, kNone, 0, kNone};
   lists.at_w(n) = NodeLists{};
   msg.at_w(n) = NodeMsg{};
@@ -410,26 +414,70 @@ void Index::trim(uint32_t n) {  // topics.go:516-522
 }
 
 // ---- subscription lists ----------------------------------------------------------------------------
-// A slot is the SubRec plus its partner descriptor (SubX) and the host-side partner capacity;
-// they always move together, and the (node, client) -> slot map follows.
+// A slot is the SubRec plus its partner list; they always move together, and the
+// (node, client) -> slot map follows. Any move re-numbers the node's may-merge slots, so the
+// node's pair block goes stale.
 void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
   const SubRec r = subs.m.h[from];
   subs.m.at_w(to) = r;
-  subx.at_w(to) = subx.h[from];
   subp_[to] = subp_[from];
   sub_pos_.put((uint64_t)n << 32 | r.client, to);
+  pairs_dirty(n);
 }
 
-void Index::encode_subx(uint32_t pos) {
-  const PartList& p = subp_[pos];
-  SubX x{{kNone, kNone, kNone, kNone}};
-  if (p.cnt > 4) {
-    x.p[0] = p.off;
-    x.p[1] = kPartIndirect | p.cnt;
-  } else {
-    for (uint32_t i = 0; i < p.cnt; i++) x.p[i] = parts.m.h[p.off + i];
+void Index::pairs_release(uint32_t n) {
+  NodeHost& h = nh_[n];
+  const NodePair& P = npair.h[n];
+  if (P.ent_mask != kNone) {
+    pent.live -= P.n_lists;
+    uint32_t links = 0;
+    for (uint32_t i = 0; i <= P.ent_mask; i++)
+      if (pent.m.h[P.ent_off + i].h != kNone) links += pent.m.h[P.ent_off + i].cnt;
+    plist.live -= links;
+    pent.release(P.ent_off, h.pent_cap);
+    plist.release(P.list_off, h.plist_cap);
   }
-  subx.at_w(pos) = x;
+  h.pent_cap = h.plist_cap = 0;
+  if (P.ent_mask != kNone || P.n_lists) npair.at_w(n) = NodePair{0, kNone, 0, 0};
+}
+
+void Index::flush_pairs() {
+  thread_local std::vector<std::pair<uint32_t, uint32_t>> hk;  // (partner node h, slot k)
+  for (uint32_t n : pair_dirty_) {
+    pair_dirty_flag_[n] = 0;
+    pairs_release(n);
+    if (!nh_[n].live) continue;
+    const NodeLists& L = lists.h[n];
+    hk.clear();
+    for (uint32_t k = 0; k < L.n_merge; k++) {
+      const PartList& p = subp_[L.sub_off + L.n_direct + k];
+      for (uint32_t i = 0; i < p.cnt; i++) hk.emplace_back(parts.m.h[p.off + i], k);
+    }
+    if (hk.empty()) continue;
+    std::sort(hk.begin(), hk.end());
+    uint32_t lists_n = 0;
+    for (size_t i = 0; i < hk.size(); i++) lists_n += i == 0 || hk[i].first != hk[i - 1].first;
+    uint32_t cap = 2, lcap = 1;
+    while (cap < 2 * lists_n) cap <<= 1;
+    while (lcap < hk.size()) lcap <<= 1;
+    const uint32_t eo = pent.alloc(cap), lo = plist.alloc(lcap), mask = cap - 1;
+    for (uint32_t i = 0; i < cap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
+    for (size_t i = 0; i < hk.size(); i++) plist.m.at_w(lo + i) = hk[i].second;
+    for (size_t b = 0; b < hk.size();) {
+      size_t e = b + 1;
+      while (e < hk.size() && hk[e].first == hk[b].first) e++;
+      uint32_t sl = pair_hash(hk[b].first) & mask;
+      while (pent.m.h[eo + sl].h != kNone) sl = (sl + 1) & mask;
+      pent.m.at_w(eo + sl) = PairEnt{hk[b].first, lo + (uint32_t)b, (uint32_t)(e - b), 0};
+      b = e;
+    }
+    pent.live += lists_n;
+    plist.live += hk.size();
+    npair.at_w(n) = NodePair{eo, mask, lo, lists_n};
+    nh_[n].pent_cap = cap;
+    nh_[n].plist_cap = lcap;
+  }
+  pair_dirty_.clear();
 }
 
 void Index::sub_ensure(uint32_t n, uint32_t need) {
@@ -439,7 +487,6 @@ void Index::sub_ensure(uint32_t n, uint32_t need) {
   while (nc < need) nc *= 2;
   NodeLists& L = lists.at_w(n);
   uint32_t no = subs.alloc(nc), cnt = L.n_direct + L.n_merge;
-  subx.grow_to(subs.m.size(), SubX{{kNone, kNone, kNone, kNone}});
   subp_.resize(subs.m.size(), PartList{0, 0, 0});
   for (uint32_t i = 0; i < cnt; i++) move_slot(n, L.sub_off + i, no + i);
   subs.release(L.sub_off, cap);
@@ -455,13 +502,13 @@ uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
     pos = base + L.n_direct + L.n_merge;
     L.n_merge++;
     n_merge_++;
+    pairs_dirty(n);
   } else {
     pos = base + L.n_direct;
     if (L.n_merge) move_slot(n, pos, base + L.n_direct + L.n_merge);
     L.n_direct++;
   }
   subs.m.at_w(pos) = r;
-  subx.at_w(pos) = SubX{{kNone, kNone, kNone, kNone}};
   subp_[pos] = PartList{0, 0, 0};
   sub_pos_.put((uint64_t)n << 32 | r.client, pos);
   subs.live++;
@@ -481,6 +528,7 @@ void Index::sub_remove(uint32_t n, uint32_t pos) {
     if (pos != last) move_slot(n, last, pos);
     L.n_merge--;
     n_merge_--;
+    pairs_dirty(n);
   }
   subs.live--;
 }
@@ -491,23 +539,20 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
   bool is_merge = pos >= base + L.n_direct;
   if (merge == is_merge) return;
   uint32_t other = merge ? base + L.n_direct - 1 : base + L.n_direct;
-  SubRec a = subs.m.h[pos];
-  const SubX ax = subx.h[pos];
+  const SubRec a = subs.m.h[pos];
   const PartList ap = subp_[pos];
   if (other != pos) move_slot(n, other, pos);
   if (merge) {
-    a.meta |= 0x1000u;
     L.n_direct--;
     L.n_merge++;
     n_merge_++;
   } else {
-    a.meta &= ~0x1000u;
     L.n_direct++;
     L.n_merge--;
     n_merge_--;
   }
+  pairs_dirty(n);
   subs.m.at_w(other) = a;
-  subx.at_w(other) = ax;
   subp_[other] = ap;
   sub_pos_.put((uint64_t)n << 32 | a.client, other);
 }
@@ -519,13 +564,11 @@ void Index::part_set(uint32_t pos, const std::vector<uint32_t>& nodes) {
   for (size_t i = 0; i < nodes.size(); i++) parts.m.at_w(off + i) = nodes[i];
   subp_[pos] = PartList{off, (uint32_t)nodes.size(), cap};
   parts.live += nodes.size();
-  encode_subx(pos);
 }
 
 void Index::part_add(uint32_t pos, uint32_t node) {
   PartList& p = subp_[pos];
   list_push(parts, p.off, p.cnt, p.cap, node);
-  encode_subx(pos);
 }
 
 uint32_t Index::part_remove(uint32_t pos, uint32_t node) {
@@ -537,7 +580,6 @@ uint32_t Index::part_remove(uint32_t pos, uint32_t node) {
     parts.live--;
     break;
   }
-  encode_subx(pos);
   return p.cnt;
 }
 
@@ -546,7 +588,6 @@ void Index::part_release(uint32_t pos) {
   parts.release(p.off, p.cap);
   parts.live -= p.cnt;
   p = PartList{0, 0, 0};
-  subx.at_w(pos) = SubX{{kNone, kNone, kNone, kNone}};
 }
 
 void Index::path_strs(uint32_t n, uint32_t* out, int* len) const {
@@ -628,7 +669,6 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
                  ((uint32_t)((flags >> 2) & 3) << kMetaRhShift)};
   uint32_t pos;
   if (sub_pos_.get((uint64_t)n << 32 | client, &pos)) {
-    rec.meta |= subs.m.h[pos].meta & 0x1000u;
     subs.m.at_w(pos) = rec;
     return 0;
   }
@@ -639,17 +679,17 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
   comp.clear();
   for (uint32_t m : mine)
     if (compatible(n, m)) comp.push_back(m);
-  if (!comp.empty()) rec.meta |= 0x1000u;
   pos = sub_add(n, rec, !comp.empty());
   if (!comp.empty()) part_set(pos, comp);
   for (uint32_t m : comp) {
     uint32_t mp;
     if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
-    if (!sub_is_merge(mp)) {
+    if (!sub_is_merge(m, mp)) {
       sub_set_merge(m, mp, true);
       sub_pos_.get((uint64_t)m << 32 | client, &mp);
     }
     part_add(mp, n);
+    pairs_dirty(m);
   }
   mine.push_back(n);
   return 1;
@@ -700,6 +740,7 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
           part_release(mp);
           sub_set_merge(m, mp, false);
         }
+        pairs_dirty(m);
       }
     }
   }

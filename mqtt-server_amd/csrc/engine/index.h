@@ -141,6 +141,7 @@ struct NodeHost {
   uint32_t n_children = 0;
   uint32_t child_pos = 0;  // position in the parent's children slab
   uint32_t sub_cap = 0, shr_cap = 0, inl_cap = 0, child_cap = 0;
+  uint32_t pent_cap = 0, plist_cap = 0;
   uint16_t depth = 0;
   bool live = false;
   bool retain_path = false;
@@ -175,8 +176,10 @@ class Index {
   Mirror<SegInfo> seginfo;
   Mirror<uint8_t> segbytes;
   SlabPool<SubRec> subs;
-  Mirror<SubX> subx;          // parallel to subs: device encoding of each slot's partners
-  SlabPool<uint32_t> parts;   // partner node ids (slab per slot; read by the device if > 2)
+  SlabPool<uint32_t> parts;   // host only: partner node ids of each may-merge slot
+  Mirror<NodePair> npair;     // pair blocks (layout.h), rebuilt by flush_pairs()
+  SlabPool<PairEnt> pent;
+  SlabPool<uint32_t> plist;
   SlabPool<ShrRec> shr;
   SlabPool<InlRec> inl;
   SlabPool<uint32_t> children;
@@ -191,6 +194,10 @@ class Index {
   uint64_t n_subs_merge() const { return n_merge_; }
   uint32_t max_depth() const { return max_depth_; }
   uint64_t version() const { return version_; }
+  // Rebuild the pair blocks of nodes whose may-merge slots or partner lists changed since the
+  // last call (the Device calls this before uploading). O(partner links of those nodes).
+  void flush_pairs();
+  uint64_t pair_links() const { return plist.live; }
 
  private:
   // path of `filter` from isolateParticle depth d on (topics.go:479-496 / 499-513)
@@ -222,7 +229,15 @@ class Index {
   template <class T, class Rec>
   void list_push(SlabPool<T>& pool, uint32_t& off, uint32_t& cnt, uint32_t& cap, const Rec& r);
 
-  bool sub_is_merge(uint32_t pos) const { return (subs.m[pos].meta & 0x1000u) != 0; }
+  bool sub_is_merge(uint32_t n, uint32_t pos) const { return pos >= lists.h[n].sub_off + lists.h[n].n_direct; }
+  void pairs_dirty(uint32_t n) {
+    if (n >= pair_dirty_flag_.size()) pair_dirty_flag_.resize(nh_.size() > n ? nh_.size() : n + 1, 0);
+    if (!pair_dirty_flag_[n]) {
+      pair_dirty_flag_[n] = 1;
+      pair_dirty_.push_back(n);
+    }
+  }
+  void pairs_release(uint32_t n);
   uint32_t sub_count(uint32_t n) const { return lists[n].n_direct + lists[n].n_merge; }
 
   std::vector<NodeHost> nh_;
@@ -253,8 +268,9 @@ class Index {
   struct PartList {
     uint32_t off, cnt, cap;
   };
-  std::vector<PartList> subp_;       // host view of each slot's partner slab
-  void encode_subx(uint32_t pos);
+  std::vector<PartList> subp_;       // each slot's partner slab
+  std::vector<uint32_t> pair_dirty_;  // nodes whose pair block is stale
+  std::vector<uint8_t> pair_dirty_flag_;
   std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
   std::unordered_map<std::string, RetEntry> retained_;
 };

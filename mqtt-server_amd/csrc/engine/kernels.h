@@ -10,9 +10,11 @@ namespace mq {
 constexpr uint32_t kLdsTab = 512;      // LDS merge-table slots per wavefront
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
-constexpr uint32_t kGSet = 256;        // LDS set of a topic's gathered nodes (<= kGSet/2 gathers)
-constexpr uint32_t kLdsTabMax = 384;   // entries allowed in an LDS merge table before overflow
+constexpr uint32_t kLdsTabMax = 384;   // table-bound records allowed in an LDS merge table
 constexpr uint32_t kTList = 512;       // queued table-bound records per wave (flushed when full)
+constexpr uint32_t kPairMax = 128;     // gathers covered by the pair analysis
+constexpr uint32_t kHitMax = 128;      // (g, h) pair hits held per topic
+constexpr uint32_t kBitWin = 2048;     // may-merge slots per table-bound bitmap window
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -24,8 +26,9 @@ struct DevIndex {
   const SegInfo* seginfo;
   const uint8_t* segbytes;
   const SubRec* subs;
-  const SubX* subx;
-  const uint32_t* parts;
+  const NodePair* npair;
+  const PairEnt* pent;
+  const uint32_t* plist;
   const ShrRec* shr;
   const InlRec* inl;
   const uint32_t* children;
@@ -64,13 +67,19 @@ struct EmitArgs {
   uint32_t* tab;            // overflow pass: merge tables, key | row | meta planes of tab_cap
   uint64_t tab_cap;
   mq_topic_result_dev* res; // indexed t - t0
-  uint32_t ablate;          // diagnosis only (MQ_EMIT_ABLATE): skip parts of the work; 0 in use
-  // Fast pass (list == nullptr): merge tables in LDS. A topic whose table would outgrow LDS
-  // counts its table-bound records, appends {t, slots} to the overflow list and is left for
-  // the overflow pass (list != nullptr), which claims `slots` of global table per topic.
+  // Fast pass (list == nullptr): merge tables in LDS. A topic whose table-bound records could
+  // outgrow LDS appends {t, slots} to the overflow list and is left for the overflow pass
+  // (list != nullptr), which claims `slots` of global table per topic.
   const uint32_t* list;     // overflow pass: pairs {topic, table slots}
   uint32_t n_list;
   uint32_t* ovf;            // [0] count, [1] total slots, [2] claim counter, [4..] pairs
+  unsigned long long* wprof;  // diagnosis only (MQ_EMIT_PROF): per-phase wave cycles, kWp* slots
+};
+
+// k_emit wave-profile slots (EmitArgs::wprof).
+enum : int {
+  kWpWaves, kWpTotal, kWpSetup, kWpCopy, kWpMerge, kWpDrain, kWpTail, kWpMergeRecs,
+  kWpTabRecs, kWpLookups, kWpProbes, kWpChunks, kWpCount = 16
 };
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,

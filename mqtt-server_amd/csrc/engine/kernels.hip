@@ -294,7 +294,6 @@ __global__ __launch_bounds__(256) void k_scan_apply(const TopicCount* __restrict
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kTabEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kMetaDirty = 0x80000000u;
-constexpr uint32_t kMetaMergeBit = 0x1000u;
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
@@ -357,14 +356,25 @@ __device__ __forceinline__ void copy_lists(V* __restrict__ dst, const V* __restr
 
 constexpr uint32_t kGroup = 64;  // gathers staged per pass: one per lane
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   __shared__ uint32_t lds_key[4][kLdsTab];
   __shared__ uint32_t lds_row[4][kLdsTab];
   __shared__ uint32_t lds_meta[4][kLdsTab];
-  __shared__ uint32_t gset[4][kGSet];            // nodes gathered with their subscriptions
-  __shared__ uint32_t tlist[4][kTList];          // table-bound records of the current gather
-  __shared__ uint32_t g_off[3][4][kGroup];      // direct-sub / shared / inline list offsets
-  __shared__ uint32_t g_pre[3][4][kGroup + 1];  // their exclusive prefixes (+ total)
+  __shared__ uint32_t gwl[4][kPairMax];          // the topic's gather words (pair analysis)
+  __shared__ uint32_t ghit[4][kPairMax];         // gather has table-bound records
+  __shared__ uint32_t hit_g[4][kHitMax];         // hits: gather index, list offset, list length
+  __shared__ uint32_t hit_off[4][kHitMax];
+  __shared__ uint32_t hit_cnt[4][kHitMax];
+  __shared__ uint32_t bm[4][kBitWin / 32];       // table-bound bitmap of a may-merge window
+  __shared__ uint32_t tlist[4][kTList];          // table-bound records queued for the table
+  __shared__ uint32_t g_off[3][4][kGroup];       // direct-sub / shared / inline list offsets
+  __shared__ uint32_t g_pre[3][4][kGroup + 1];   // their exclusive prefixes (+ total)
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t w = blockIdx.x * 4 + wv;
   uint32_t t;
@@ -376,12 +386,128 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     if (t >= a.t1) return;  // wave-uniform
   }
   const bool global_tab = a.list != nullptr;
+  // Diagnosis only (MQ_EMIT_PROF): per-phase wave cycles and work counts.
+  const bool wp = a.wprof != nullptr;
+  const long long wp_t0 = wp ? clock64() : 0;
+  long long wp_copy = 0, wp_merge = 0, wp_drain = 0, wp_setup = 0;
+  uint32_t wp_mrecs = 0, wp_chunks = 0, wp_look = 0, wp_probe = 0;
+  auto wp_flush = [&](uint32_t tab_recs) {
+    if (!wp) return;
+    const uint32_t lk = wave_sum(wp_look), pr = wave_sum(wp_probe);
+    if (lane == 0) {
+      unsigned long long* q = a.wprof;
+      atomicAdd(q + kWpWaves, 1ull);
+      atomicAdd(q + kWpTotal, (unsigned long long)(clock64() - wp_t0));
+      atomicAdd(q + kWpSetup, (unsigned long long)wp_setup);
+      atomicAdd(q + kWpCopy, (unsigned long long)wp_copy);
+      atomicAdd(q + kWpMerge, (unsigned long long)wp_merge);
+      atomicAdd(q + kWpDrain, (unsigned long long)wp_drain);
+      atomicAdd(q + kWpMergeRecs, (unsigned long long)wp_mrecs);
+      atomicAdd(q + kWpTabRecs, (unsigned long long)tab_recs);
+      atomicAdd(q + kWpLookups, (unsigned long long)lk);
+      atomicAdd(q + kWpProbes, (unsigned long long)pr);
+      atomicAdd(q + kWpChunks, (unsigned long long)wp_chunks);
+    }
+  };
 
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
   const uint32_t cap = (uint32_t)(o1.rows - o0.rows);
   const uint64_t sb = o0.shr - a.base.shr, ib = o0.inl - a.base.inl;
   SubRec* __restrict__ rows = a.rows + rb;
+  const uint32_t n_g = (uint32_t)(o1.g - o0.g);
+  auto gword = [&](uint32_t i) {
+    return a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + i] : a.gathers[o0.g + i];
+  };
+
+  // ---- Pair analysis: which may-merge records need the merge table. For every ordered pair
+  // (g, h) of gathered nodes with subscriptions, g's pair block lists g's may-merge slots whose
+  // client also subscribes at h (layout.h). The union of the hit lists of g is exactly g's
+  // table-bound records; every other record of the topic is its client's only match and is
+  // emitted as is. Beyond kPairMax gathers or kHitMax hits every may-merge record is
+  // table-bound (correct, slower; not seen in the SURVEY.md §8d workloads).
+  bool pair_ok = n_g <= kPairMax;
+  uint32_t n_hit = 0, ub = 0;  // hits; upper bound of the table-bound records
+  if (pair_ok) {
+    for (uint32_t i = lane; i < n_g; i += 64) {
+      gwl[wv][i] = gword(i);
+      ghit[wv][i] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t np = n_g * n_g;
+    uint32_t ub_l = 0;
+    for (uint32_t p0 = 0; p0 < np; p0 += 64) {
+      const uint32_t p = p0 + lane;
+      bool hit = false;
+      uint32_t gi = 0, e_off = 0, e_cnt = 0;
+      if (p < np) {
+        gi = p / n_g;
+        const uint32_t hi = p - gi * n_g;
+        const uint32_t gg = gwl[wv][gi], gh = gwl[wv][hi];
+        if (gi != hi && (gg & gh & kGatherSubs)) {
+          const NodePair P = a.ix.npair[gg & kGatherNode];
+          if (P.ent_mask != kNone) {
+            const uint32_t h = gh & kGatherNode;
+            uint32_t sl = pair_hash(h) & P.ent_mask;
+            if (wp) wp_look++;
+            for (;;) {
+              if (wp) wp_probe++;
+              const PairEnt e = a.ix.pent[P.ent_off + sl];
+              if (e.h == h) {
+                hit = true;
+                e_off = e.off;
+                e_cnt = e.cnt;
+                break;
+              }
+              if (e.h == kNone) break;
+              sl = (sl + 1) & P.ent_mask;
+            }
+          }
+        }
+      }
+      const uint64_t bh = __ballot(hit);
+      if (hit) {
+        const uint32_t x = n_hit + prefix_before(bh);
+        if (x < kHitMax) {
+          hit_g[wv][x] = gi;
+          hit_off[wv][x] = e_off;
+          hit_cnt[wv][x] = e_cnt;
+        }
+        ghit[wv][gi] = 1;
+      }
+      n_hit += __popcll(bh);
+      ub_l += e_cnt;
+    }
+    ub = wave_sum(ub_l);
+    if (n_hit > kHitMax) pair_ok = false;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!pair_ok) {  // every may-merge record is table-bound
+    uint32_t ub_l = 0;
+    for (uint32_t i = lane; i < n_g; i += 64) {
+      const uint32_t gw = gword(i);
+      if (gw & kGatherSubs) ub_l += a.ix.lists[gw & kGatherNode].n_merge;
+    }
+    ub = wave_sum(ub_l);
+  }
+  if (wp) wp_setup = clock64() - wp_t0;
+
+  // A topic whose table would outgrow LDS goes to the overflow pass, which gives it a global
+  // table of >= 2 * ub slots.
+  if (!global_tab && ub > kLdsTabMax) {
+    if (lane == 0) {
+      uint32_t slots = 1;
+      while (slots < 2 * ub) slots <<= 1;
+      const uint32_t i = atomicAdd(a.ovf, 1u);
+      a.ovf[4 + 2 * i] = t;
+      a.ovf[4 + 2 * i + 1] = slots;
+      atomicAdd(a.ovf + 1, slots);
+    }
+    wp_flush(ub);
+    return;
+  }
 
   // Merge table: LDS on the fast pass, a global slice on the overflow pass. Accesses branch on
   // the (wave-uniform) kind so each compiles to typed ds_* / global_* instructions.
@@ -439,61 +565,28 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
       }
       sl = (sl + 1) & tmask;
     }
-    atomicOr(a.ix.err, kErrTableFull);  // sized at <= 1/2 load: unreachable
+    atomicOr(a.ix.err, kErrTableFull);  // sized at <= 3/4 load: unreachable
     *is_new = false;
     return 0;
   };
   bool tab_ready = false;
-  bool overflowed = false;  // fast pass only: now just counting table-bound records
-  uint32_t tab_used = 0;
-
-  // Set of the particles whose subscriptions this topic gathers. A may-merge subscription
-  // needs the merge table only if one of its partners (its client's other co-matchable
-  // subscriptions) is in it; otherwise it is its client's only match and is emitted directly.
-  const uint32_t n_g = (uint32_t)(o1.g - o0.g);
-  const bool set_ok = n_g <= kGSet / 2;
-  auto gword = [&](uint32_t i) {
-    return a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + i] : a.gathers[o0.g + i];
-  };
-  if (set_ok && !(a.ablate & 16)) {
-    for (uint32_t k = lane; k < kGSet; k += 64) gset[wv][k] = kTabEmpty;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane < n_g) {
-      const uint32_t gw = gword(lane);
-      if (gw & kGatherSubs) {
-        const uint32_t node = gw & kGatherNode;
-        uint32_t sl = hash32(node) & (kGSet - 1);
-        for (uint32_t p = 0; p < kGSet; p++, sl = (sl + 1) & (kGSet - 1)) {
-          const uint32_t old = atomicCAS(&gset[wv][sl], kTabEmpty, node);
-          if (old == kTabEmpty || old == node) break;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  auto gathered = [&](uint32_t node) {
-    uint32_t sl = hash32(node) & (kGSet - 1);
-    for (uint32_t p = 0; p < kGSet; p++, sl = (sl + 1) & (kGSet - 1)) {
-      const uint32_t k = gset[wv][sl];
-      if (k == node) return true;
-      if (k == kTabEmpty) return false;
-    }
-    return false;
-  };
+  uint32_t tab_recs = 0;
 
   uint32_t n_cli = 0, n_ext = 0, n_shr = 0, n_inl = 0;
   for (uint64_t g0 = o0.g; g0 < o1.g; g0 += kGroup) {
-    // Stage up to 64 gathers at once (one per lane): the gather word and the node's lists.
+    // Stage up to 64 gathers at once (one per lane): the gather word and the node's lists. A
+    // node without table-bound records this topic is copied whole (direct and may-merge
+    // slots are contiguous); the others copy their direct part and stream the rest below.
+    const uint32_t gbase = (uint32_t)(g0 - o0.g);
     const uint32_t ng = (uint32_t)min<uint64_t>(kGroup, o1.g - g0);
     uint32_t dn = 0, mn = 0, sn = 0, in = 0, sub_off = 0, shr_off = 0, inl_off = 0;
     if (lane < ng) {
-      const uint32_t gw = gword((uint32_t)(g0 - o0.g) + lane);
+      const uint32_t gw = pair_ok ? gwl[wv][gbase + lane] : gword(gbase + lane);
       const NodeLists L = a.ix.lists[gw & kGatherNode];
       if (gw & kGatherSubs) {
-        dn = L.n_direct;
-        mn = L.n_merge;
+        const bool tb = pair_ok ? ghit[wv][gbase + lane] != 0 : L.n_merge != 0;
+        dn = tb ? L.n_direct : L.n_direct + L.n_merge;
+        mn = tb ? L.n_merge : 0;
       }
       sub_off = L.sub_off;
       sn = L.shr_cnt;
@@ -521,34 +614,37 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
-    // Subscriptions that can never merge: one flat coalesced copy into client rows.
-    if (!(a.ablate & 1) && !overflowed)
-      copy_lists(reinterpret_cast<u32x4*>(rows + n_cli), reinterpret_cast<const u32x4*>(a.ix.subs),
-                 g_off[0][wv], g_pre[0][wv], dt, lane);
+    const long long wp_c = wp ? clock64() : 0;
+    // Records that are their client's only match: one flat coalesced copy into client rows.
+    copy_lists(reinterpret_cast<u32x4*>(rows + n_cli), reinterpret_cast<const u32x4*>(a.ix.subs),
+               g_off[0][wv], g_pre[0][wv], dt, lane);
     n_cli += dt;
     // Shared[sub.Filter][client] = sub (topics.go:656-663)
-    if (!(a.ablate & 4) && !overflowed)
-      copy_lists(reinterpret_cast<u32x2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const u32x2*>(a.ix.shr),
-                 g_off[1][wv], g_pre[1][wv], st, lane);
+    copy_lists(reinterpret_cast<u32x2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const u32x2*>(a.ix.shr),
+               g_off[1][wv], g_pre[1][wv], st, lane);
     n_shr += st;
     // Inline subscriptions in gather order; the last write per id is kept below.
-    if (!overflowed)
-      copy_lists(reinterpret_cast<u32x2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const u32x2*>(a.ix.inl),
+    copy_lists(reinterpret_cast<u32x2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const u32x2*>(a.ix.inl),
                g_off[2][wv], g_pre[2][wv], it, lane);
     n_inl += it;
+    if (wp) wp_copy += clock64() - wp_c;
+    const long long wp_m = wp ? clock64() : 0;
 
-    // Subscriptions that may merge with another of the same client, in gather (rank) order.
-    uint64_t mm = (a.ablate & 2) ? 0 : __ballot(mn > 0);
+    // Nodes with table-bound records, in gather (rank) order.
+    uint64_t mm = __ballot(mn > 0);
     while (mm) {
       const uint32_t j = (uint32_t)__builtin_ctzll(mm);
       mm &= mm - 1;
+      const uint32_t gidx = gbase + j;
       const uint32_t m_cnt = __builtin_amdgcn_readlane(mn, j);
       const uint32_t m_off = __builtin_amdgcn_readlane(sub_off + dn, j);
       const SubRec* __restrict__ ms = a.ix.subs + m_off;
-      const SubX* __restrict__ mx = a.ix.subx + m_off;
-      uint32_t nt = 0;  // table-bound records of this gather queued in tlist
-      // Table pass: insert the queued records (the rare clients with several matches).
+      wp_mrecs += m_cnt;
+      uint32_t nt = 0;  // table-bound records queued in tlist
+      // Table pass over the queue (the clients with several matches). Records of one gather
+      // belong to distinct clients, so their order within the gather does not matter.
       auto drain = [&]() {
+        const long long wp_d = wp ? clock64() : 0;
         if (!tab_ready) {
           for (uint32_t q = lane; q <= tmask; q += 64) tk_store(q, kTabEmpty);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -556,6 +652,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        tab_recs += nt;
         for (uint32_t c0 = 0; c0 < nt; c0 += 64) {
           const bool vt = c0 + lane < nt;
           SubRec r{0, 0, 0, 0};
@@ -563,7 +660,6 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
           bool is_new = false;
           if (vt) {
             r = ms[tlist[wv][c0 + lane]];
-            r.meta &= ~kMetaMergeBit;
             slot = tab_insert(r.client, &is_new);
           }
           const uint64_t bn = __ballot(vt && is_new);
@@ -590,79 +686,68 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
           n_ext += __popcll(be);
         }
         nt = 0;
+        if (wp) wp_drain += clock64() - wp_d;
       };
-      // Streaming pass, four 64-record chunks in flight: a record none of whose partners is
-      // gathered is its client's only match (its merged Subscription is itself) and is
-      // emitted directly; the others are queued for the table pass. Records of one gather
-      // belong to distinct clients, so their order within the gather does not matter.
-      for (uint32_t i0 = 0;; i0 += 256) {
-        const bool done = i0 >= m_cnt;
-        if ((done || nt + 256 > kTList) && nt && !overflowed) {  // the one call site
-          if (a.ablate & 32) nt = 0; else drain();
+
+      if (!pair_ok) {  // all of them
+        for (uint32_t i0 = 0; i0 < m_cnt; i0 += 64) {
+          if (i0 + lane < m_cnt) tlist[wv][nt + lane] = i0 + lane;
+          nt += min(64u, m_cnt - i0);
+          if (nt + 64 > kTList) drain();
         }
-        if (done) break;
-        SubRec rr[4];
-        SubX xx[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {  // unconditional loads (see copy_lists)
-          const uint32_t k = min(i0 + u * 64 + lane, m_cnt - 1);
-          rr[u] = ms[k];
-          xx[u] = mx[k];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint32_t k = i0 + u * 64 + lane;
-          const bool v = k < m_cnt;
-          bool shared_client = false;
-          if (v && !(a.ablate & 8)) {
-            if (set_ok) {
-              const SubX x = xx[u];
-              if (x.p[1] != kNone && (x.p[1] & kPartIndirect)) {
-                // long partner list: four independent loads per round
-                const uint32_t pc = x.p[1] & ~kPartIndirect;
-                for (uint32_t p0 = 0; p0 < pc && !shared_client; p0 += 4) {
-                  uint32_t q[4];
-#pragma unroll
-                  for (int e = 0; e < 4; e++) q[e] = a.ix.parts[x.p[0] + min(p0 + e, pc - 1)];
-#pragma unroll
-                  for (int e = 0; e < 4; e++) shared_client |= gathered(q[e]);
-                }
-              } else {
-#pragma unroll
-                for (int e = 0; e < 4; e++) shared_client |= x.p[e] != kNone && gathered(x.p[e]);
+        if (nt) drain();
+        continue;
+      }
+      for (uint32_t w0 = 0; w0 < m_cnt; w0 += kBitWin) {
+        const uint32_t wn = min(kBitWin, m_cnt - w0);
+        // Mark this window's table-bound slots (union of the gather's hit lists) and queue
+        // each once for the table.
+        for (uint32_t q = lane; q < kBitWin / 32; q += 64) bm[wv][q] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t x = 0; x < n_hit; x++) {
+          if (hit_g[wv][x] != gidx) continue;  // wave-uniform
+          const uint32_t off = hit_off[wv][x], cnt = hit_cnt[wv][x];
+          for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
+            bool own = false;
+            uint32_t k = 0;
+            if (c0 + lane < cnt) {
+              k = a.ix.plist[off + c0 + lane] - w0;
+              if (k < wn) {
+                const uint32_t bit = 1u << (k & 31);
+                own = !(atomicOr(&bm[wv][k >> 5], bit) & bit);
               }
-            } else {
-              shared_client = true;
             }
+            const uint64_t bo = __ballot(own);
+            if (own) tlist[wv][nt + prefix_before(bo)] = w0 + k;
+            nt += __popcll(bo);
+            if (nt + 64 > kTList) drain();
           }
-          const uint64_t bt = __ballot(v && shared_client);
-          tab_used += __popcll(bt);
-          if (!global_tab && tab_used > kLdsTabMax) overflowed = true;
-          if (overflowed) continue;  // now only counting, for the overflow pass's table
-          const uint64_t bd = __ballot(v && !shared_client);
-          if (v && !shared_client && !(a.ablate & 64)) {
-            u32x4 rv = *reinterpret_cast<const u32x4*>(&rr[u]);
-            rv.w &= ~kMetaMergeBit;
-            __builtin_nontemporal_store(rv, reinterpret_cast<u32x4*>(rows + n_cli + prefix_before(bd)));
+        }
+        if (nt) drain();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // Stream the window: everything not marked goes straight to client rows. Four
+        // 64-record chunks in flight; loads are unconditional (see copy_lists).
+        for (uint32_t i0 = 0; i0 < wn; i0 += 256) {
+          wp_chunks++;
+          SubRec rr[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) rr[u] = ms[w0 + min(i0 + u * 64 + lane, wn - 1)];
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const uint32_t k = i0 + u * 64 + lane;
+            const bool v = k < wn && !((bm[wv][min(k, wn - 1) >> 5] >> (k & 31)) & 1);
+            const uint64_t bd = __ballot(v);
+            if (v)
+              __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&rr[u]),
+                                          reinterpret_cast<u32x4*>(rows + n_cli + prefix_before(bd)));
+            n_cli += __popcll(bd);
           }
-          n_cli += __popcll(bd);
-          if (v && shared_client) tlist[wv][nt + prefix_before(bt)] = k;
-          nt += __popcll(bt);
         }
       }
     }
-  }
-
-  if (overflowed) {  // hand the topic to the overflow pass with a table sized for its records
-    if (lane == 0) {
-      uint32_t slots = 1;
-      while (slots < 2 * tab_used) slots <<= 1;
-      const uint32_t i = atomicAdd(a.ovf, 1u);
-      a.ovf[4 + 2 * i] = t;
-      a.ovf[4 + 2 * i + 1] = slots;
-      atomicAdd(a.ovf + 1, slots);
-    }
-    return;
+    if (wp) wp_merge += clock64() - wp_m;
   }
 
   if (tab_ready) {  // write back merged Qos/NoLocal of bases that absorbed later matches
@@ -709,6 +794,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     res.reserved = 0;
     a.res[t - a.t0] = res;
   }
+  wp_flush(tab_recs);
 }
 
 }  // namespace mq

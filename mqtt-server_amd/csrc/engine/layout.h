@@ -131,17 +131,35 @@ struct SubRec {  // == mq_client_row
   uint32_t client;
   uint32_t filter_id;
   int32_t ident;
-  uint32_t meta;  // qos | nolocal<<8 | rap<<9 | rh<<10 (| kMetaMerge, host-side only)
+  uint32_t meta;  // qos | nolocal<<8 | rap<<9 | rh<<10
 };
-// Partner list of a subscription that may merge: the nodes of its client's other
-// subscriptions that could match the same topic. At match time the record needs the merge
-// table only if a partner node is gathered for the topic too. Device encoding (16 B): up to
-// four partners inline {p0, p1, p2, p3} (kNone-padded); more as
-// {offset into parts, kPartIndirect | count, kNone, kNone}.
-struct SubX {
-  uint32_t p[4];
+// Pair routing of may-merge subscriptions. A may-merge subscription needs the per-topic merge
+// table only when its client has another subscription gathered for the same topic. For a node
+// g, the pair block maps each partner node h (a node holding another co-matchable
+// subscription of one of g's may-merge clients) to the list of g's may-merge slots, relative
+// k in [0, n_merge), whose client also subscribes at h. A topic probes (g, h) only for pairs
+// of nodes it gathers; the slots on the hit lists are exactly its table-bound records.
+struct NodePair {   // per node (16 B)
+  uint32_t ent_off;   // PairEnt hash table (ent_mask + 1 entries, linear probing)
+  uint32_t ent_mask;  // kNone: the node has no may-merge slots
+  uint32_t list_off;  // the block's slot lists in the pair-list pool
+  uint32_t n_lists;
 };
-constexpr uint32_t kPartIndirect = 0x80000000u;
+struct PairEnt {  // 16 B
+  uint32_t h;     // partner node; kNone = empty
+  uint32_t off;   // absolute offset of the list in the pair-list pool
+  uint32_t cnt;   // slots on the list
+  uint32_t pad;
+};
+
+MQ_HD uint32_t pair_hash(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 
 struct ShrRec {  // == mq_shared_row
   uint32_t filter_id;
