@@ -10,7 +10,7 @@ per GPU, the index replicated on every GPU and each rank matching its own 1M-top
 topics are independent units, so there is no data-path collective ("scaling": "weak"); only
 the timing barrier and a max-over-ranks all-reduce of the elapsed time use the process group.
 
-Rank 0 prints one JSON line with the roofline of the dominant kernel (k_emit; HIP events on
+Rank 0 prints one JSON line with the roofline of the dominant kernel (k_copy; HIP events on
 its launch stream) and the CPU baseline (the oracle restatement of the Go trie, all allotted
 host cores, on a bounded sample of the same batch).
 """
@@ -43,12 +43,12 @@ def host_cores():
 
 
 def read_traffic(path, n_subs):
-    """HBM bytes per k_emit launch from a committed rocprofv3 PMC summary, if present."""
+    """HBM bytes per k_copy launch from a committed rocprofv3 PMC summary, if present."""
     try:
         with open(path) as f:
             d = json.load(f)
         e = d.get(str(n_subs))
-        return None if e is None else float(e["hbm_bytes_per_emit_launch"])
+        return None if e is None else float(e["hbm_bytes_per_copy_launch"])
     except (OSError, ValueError, KeyError):
         return None
 
@@ -121,7 +121,6 @@ def main():
         return
 
     value = n * world * args.steps / elapsed
-    emit_launches, emit_ms = prof.get("emit", (0, 0.0))
     out = {
         "metric": METRIC, "value": value, "unit": "publishes/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
@@ -135,13 +134,30 @@ def main():
         },
         "kernels_ms_per_step": {k: v[1] / max(1, args.steps) for k, v in prof.items() if v[1] > 0},
         "counters_per_step": {k: v[0] / max(1, args.steps) for k, v in prof.items() if v[1] == 0},
-        "emit_chunks_per_step": chunks,
+        "chunks_per_step": chunks,
     }
 
-    # Algorithmic bytes: B = 8L + 4 + 16P + 16S + 16O per topic, with L, P, S, O
-    # from the oracle's exact counters on a sample of this batch; k_emit moves 16S + 16O.
+    # Roofline of the dominant kernel, k_copy. It moves every gathered list into output rows:
+    # per launch it writes copy_bytes (16 B per client row, 8 B per shared / inline row), all of
+    # which must reach HBM (the rows of one step are far larger than every cache). Its reads are
+    # the hot subscription lists, re-read by many topics and served from L2 / the Infinity Cache,
+    # so the HBM-compulsory bytes of a launch are its writes; `traffic` is the
+    # PMC-measured HBM bytes per launch (profiles/pmc_traffic.json) when present.
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-            "traffic": None}
+            "traffic": None, "kernel": "k_copy", "bytes": "output rows written per launch"}
+    copy_launches, copy_ms = prof.get("copy", (0, 0.0))
+    copy_bytes = prof.get("copy_bytes", (0, 0.0))[0]
+    if copy_ms > 0 and copy_launches:
+        launch_ms = copy_ms / copy_launches
+        per_launch = copy_bytes / copy_launches
+        achieved = per_launch / (launch_ms * 1e-3) / 1e9
+        roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS,
+                    traffic=read_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), args.subs))
+        out["copy_avg_launch_ms"] = launch_ms
+        out["copy_bytes_per_launch"] = per_launch
+        # the whole step against the same roofline: all output bytes / step time
+        out["step_output_GBps"] = copy_bytes / max(1, args.steps) / (elapsed / args.steps) / 1e9
+
     cpu = None
     if not args.no_cpu and world == 1:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -162,7 +178,7 @@ def main():
                "sample": f"first {m} topics of the rank-0 batch on the same {args.subs}-subscription "
                          f"index, {cores} threads, Subscribers() per topic (C++ restatement of the "
                          f"Go particle trie, oracle/)"}
-        # oracle counters + parity on a sample
+        # oracle counters (B = 8L + 4 + 16P + 16S + 16O per topic) + parity on a sample
         ns = min(m, 4096)
         dg_o, cnt_o, tot = orc.digest_batch(tb, to[:ns + 1], cores)
         res = eng.match_batch(tb, to[:ns + 1])
@@ -170,18 +186,8 @@ def main():
         out["parity_sample"] = {"topics": ns, "bit_exact": bool((dg_e == dg_o).all())}
         per_topic = {k: v / ns for k, v in tot.items()}
         b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"] + 16 * per_topic["S"] + 16 * per_topic["O"]
-        b_emit = 16 * per_topic["S"] + 16 * per_topic["O"]
-        out["alg_bytes_per_topic"] = {"B": b_topic, "emit": b_emit, "L": per_topic["L"],
-                                      "P": per_topic["P"], "S": per_topic["S"], "O": per_topic["O"],
-                                      "sample_topics": ns}
-        if emit_ms > 0:
-            launch_ms = emit_ms / emit_launches
-            topics_per_launch = n / max(1, chunks)
-            achieved = b_emit * topics_per_launch / (launch_ms * 1e-3) / 1e9
-            roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS)
-            tr = read_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), args.subs)
-            roof["traffic"] = tr
-            out["emit_avg_launch_ms"] = launch_ms
+        out["alg_bytes_per_topic"] = {"B": b_topic, "L": per_topic["L"], "P": per_topic["P"],
+                                      "S": per_topic["S"], "O": per_topic["O"], "sample_topics": ns}
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)

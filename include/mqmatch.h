@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 1
+#define MQ_ABI_VERSION 2
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
@@ -46,6 +46,10 @@ extern "C" {
 #define MQ_META_RAP 0x200u          /* base RetainAsPublished */
 #define MQ_META_RH_SHIFT 10         /* base RetainHandling, 2 bits */
 /* bit 0x1000 is reserved (never set in output rows) */
+/* Row kind of an output row (mq_topic_result): none = client row */
+#define MQ_ROW_IDENT 0x40000000u    /* an Identifiers entry of an earlier client row's client */
+#define MQ_ROW_DROP 0x80000000u     /* absorbed into an earlier client row (identifier 0) */
+#define MQ_ROW_KIND_MASK 0xC0000000u
 
 typedef struct mq_index mq_index;
 
@@ -123,13 +127,9 @@ typedef struct mq_client_row {
 } mq_client_row;
 
 /* Identifiers-map entry other than the base one: a further matching filter of the client
- * with identifier > 0 (packets/packets.go:261-263). */
-typedef struct mq_ident_row {
-  uint32_t client_id;
-  uint32_t filter_id;
-  int32_t identifier;
-  uint32_t reserved;
-} mq_ident_row;
+ * with identifier > 0 (packets/packets.go:261-263). It is an mq_client_row whose meta has
+ * MQ_ROW_IDENT set (its other meta bits are those of that subscription, not merged). */
+typedef mq_client_row mq_ident_row;
 
 /* Subscribers.Shared[filter][client] (topics.go:651-665): the stored subscription's own
  * filter and its client; the group members before the host's SelectShared pick. */
@@ -144,9 +144,12 @@ typedef struct mq_inline_row {
   uint32_t filter_id;
 } mq_inline_row;
 
-/* Per-topic result descriptor. Client and ident rows share one 16-byte row region of
- * `sub_cap` rows starting at `sub_base`: client rows at [sub_base, sub_base + n_client),
- * ident rows at [sub_base + sub_cap - n_ident, sub_base + sub_cap). */
+/* Per-topic result descriptor. Every non-shared subscription the topic gathers leaves one
+ * 16-byte row, in gather (DFS) order, in the region [sub_base, sub_base + sub_cap): a client
+ * row (meta & MQ_ROW_KIND_MASK == 0) for the first-gathered subscription of each client, and
+ * for a client's later matches an ident row (MQ_ROW_IDENT, identifier > 0) or a dropped row
+ * (MQ_ROW_DROP). n_client / n_ident count the client / ident rows. Shared rows are
+ * [shared_base, + n_shared), inline rows [inline_base, + n_inline). */
 typedef struct mq_topic_result {
   uint64_t sub_base;
   uint64_t shared_base;
@@ -163,7 +166,7 @@ typedef struct mq_match_result {
   uint32_t n_topics;
   uint32_t reserved;
   const mq_topic_result* topics; /* n_topics */
-  const mq_client_row* sub_rows; /* client rows; ident rows are read as mq_ident_row */
+  const mq_client_row* sub_rows; /* client, ident and dropped rows (MQ_ROW_*) */
   const mq_shared_row* shared_rows;
   const mq_inline_row* inline_rows;
   uint64_t n_sub_rows, n_shared_rows, n_inline_rows;
@@ -215,6 +218,12 @@ typedef struct mq_stats {
   uint32_t max_depth, reserved;
 } mq_stats;
 int mq_index_stats(const mq_index* idx, mq_stats* out);
+
+/* Diagnostic, host only (no device work): brings the device-bound image up to date and checks
+   its invariants — list bounds, partner links of may-merge subscriptions (symmetric, pointing at
+   the partner's current slot). Returns 0, or MQ_EIO with the first violation in
+   mq_last_error(). */
+int mq_index_check(mq_index* idx);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. */
 typedef struct mq_kernel_time {

@@ -294,6 +294,14 @@ int mq_index_stats(const mq_index* cidx, mq_stats* out) {
   });
 }
 
+int mq_index_check(mq_index* idx) {
+  return guarded(idx, [&]() -> int {
+    std::string why;
+    if (!idx->ix->check(&why)) return fail(MQ_EIO, "index check: " + why);
+    return 0;
+  });
+}
+
 int mq_profile_enable(mq_index* idx, int enable) {
   return guarded(idx, [&] {
     idx->profile = enable != 0;

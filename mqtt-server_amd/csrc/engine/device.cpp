@@ -2,6 +2,7 @@
 #include "device.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -147,16 +148,17 @@ Device::Device(int dev) : dev_(dev) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   const char* e = getenv("MQ_CHUNK_ROWS");
   chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : (256ull << 20);  // 4 GiB of 16-B rows
-  wprof_on_ = getenv("MQ_EMIT_PROF") != nullptr;  // diagnosis only
+  merge_stats_ = getenv("MQ_MERGE_STATS") != nullptr;  // diagnosis only
 }
 
 Device::~Device() {
   (void)hipSetDevice(dev_);
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
-  npair_.release(); pent_.release(); plist_.release();
+  mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                    &shr_rows_, &inl_rows_, &tab_, &res_, &err_, &msg_handles_, &msg_base_, &msg_count_, &gslots_, &ovf_, &wprof_})
+                    &shr_rows_, &inl_rows_, &res_, &err_, &desc_, &tiles_, &msg_handles_, &msg_base_,
+                    &msg_count_, &gslots_, &mstats_})
     b->release();
 }
 
@@ -165,9 +167,10 @@ uint64_t Device::device_bytes() const {
                lists_.cap * sizeof(NodeLists) + msg_.cap * sizeof(NodeMsg) +
                seginfo_.cap * sizeof(SegInfo) + segbytes_.cap + subs_.cap * sizeof(SubRec) +
                shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4 +
+               mref_.cap * sizeof(MergeRef) + mpart_.cap * sizeof(MergePart) +
                npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * 4;
   for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                          &shr_rows_, &inl_rows_, &tab_, &res_})
+                          &shr_rows_, &inl_rows_, &res_, &desc_, &tiles_})
     b += x->bytes;
   return b;
 }
@@ -175,7 +178,7 @@ uint64_t Device::device_bytes() const {
 void Device::sync(Index& ix, hipStream_t s) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   if (ix.version() == synced_version_ && edges_.d) return;
-  ix.flush_pairs();
+  ix.flush_merge();
   edges_.sync(ix.edges, s, &uploaded_);
   walk_.sync(ix.walk, s, &uploaded_);
   lists_.sync(ix.lists, s, &uploaded_);
@@ -183,6 +186,8 @@ void Device::sync(Index& ix, hipStream_t s) {
   seginfo_.sync(ix.seginfo, s, &uploaded_);
   segbytes_.sync(ix.segbytes, s, &uploaded_);
   subs_.sync(ix.subs.m, s, &uploaded_);
+  mref_.sync(ix.mref, s, &uploaded_);
+  mpart_.sync(ix.mpart.m, s, &uploaded_);
   npair_.sync(ix.npair, s, &uploaded_);
   pent_.sync(ix.pent.m, s, &uploaded_);
   plist_.sync(ix.plist.m, s, &uploaded_);
@@ -206,6 +211,8 @@ DevIndex Device::dev_index(const Index& ix) const {
   d.seginfo = seginfo_.d;
   d.segbytes = segbytes_.d;
   d.subs = subs_.d;
+  d.mref = mref_.d;
+  d.mpart = mpart_.d;
   d.npair = npair_.d;
   d.pent = pent_.d;
   d.plist = plist_.d;
@@ -308,22 +315,29 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     uint32_t b0, b1;
   };
   std::vector<Chunk> chunks;
-  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1;
+  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1, max_tiles = 1;
+  auto tiles_of = [](uint64_t rows) { return (rows + kCopyTile - 1) / kCopyTile; };
   for (uint32_t b = 0; b < nb;) {
     uint32_t e = b + 1;
     while (e < nb && h_bpre_[e + 1].rows - h_bpre_[b].rows <= chunk_rows_budget_) e++;
     chunks.push_back(Chunk{b, e});
-    max_rows = std::max(max_rows, h_bpre_[e].rows - h_bpre_[b].rows);
-    max_shr = std::max(max_shr, h_bpre_[e].shr - h_bpre_[b].shr);
-    max_inl = std::max(max_inl, h_bpre_[e].inl - h_bpre_[b].inl);
+    const TopicOff &lo = h_bpre_[b], &hi = h_bpre_[e];
+    max_rows = std::max(max_rows, hi.rows - lo.rows);
+    max_shr = std::max(max_shr, hi.shr - lo.shr);
+    max_inl = std::max(max_inl, hi.inl - lo.inl);
+    max_tiles = std::max(max_tiles, tiles_of(hi.rows - lo.rows) + tiles_of(hi.shr - lo.shr) +
+                                        tiles_of(hi.inl - lo.inl));
     max_topics = std::max<uint64_t>(max_topics, std::min<uint64_t>(n, (uint64_t)e * kScanBlock) - (uint64_t)b * kScanBlock);
     b = e;
   }
+  if (max_rows >= (1ull << 32) || max_shr >= (1ull << 32) || max_inl >= (1ull << 32))
+    throw HipError{hipErrorInvalidValue, "one scan block's output exceeds 2^32 rows"};
   rows_.ensure(max_rows * sizeof(SubRec));
   shr_rows_.ensure(max_shr * sizeof(ShrRec));
   inl_rows_.ensure(max_inl * sizeof(InlRec));
   res_.ensure(max_topics * sizeof(mq_topic_result_dev));
-  ovf_.ensure((2 * max_topics + 4) * sizeof(uint32_t));
+  desc_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
+  tiles_.ensure(max_tiles * sizeof(uint32_t));
 
   if (host) {
     host->topics.resize(n);
@@ -333,68 +347,57 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   }
 
   for (const Chunk& c : chunks) {
+    const TopicOff& lo = h_bpre_[c.b0];
+    const TopicOff& hi = h_bpre_[c.b1];
     EmitArgs a;
     a.ix = di;
     a.t0 = c.b0 * kScanBlock;
     a.t1 = std::min<uint64_t>(n, (uint64_t)c.b1 * kScanBlock);
     a.off = offs_.as<TopicOff>();
-    a.base = h_bpre_[c.b0];
+    a.base = lo;
     a.gathers = gathers;
     a.gather_stride = gstride;
+    a.desc = desc_.as<GDesc>();
+    a.tiles = tiles_.as<uint32_t>();
+    a.total[0] = (uint32_t)(hi.rows - lo.rows);
+    a.total[1] = (uint32_t)(hi.shr - lo.shr);
+    a.total[2] = (uint32_t)(hi.inl - lo.inl);
+    for (int k = 0; k < 3; k++) a.n_tiles[k] = (uint32_t)tiles_of(a.total[k]);
     a.rows = rows_.as<SubRec>();
     a.shr_rows = shr_rows_.as<ShrRec>();
     a.inl_rows = inl_rows_.as<InlRec>();
-    a.tab = nullptr;
-    a.tab_cap = 0;
     a.res = res_.as<mq_topic_result_dev>();
-    a.list = nullptr;
-    a.n_list = 0;
-    a.ovf = ovf_.as<uint32_t>();
-    a.wprof = nullptr;
-    if (wprof_on_) {
-      if (!wprof_.p) {
-        wprof_.ensure(kWpCount * sizeof(unsigned long long));
-        hip_check(hipMemsetAsync(wprof_.p, 0, kWpCount * sizeof(unsigned long long), s), "memset wprof");
+    a.stats = nullptr;
+    if (merge_stats_) {
+      if (!mstats_.p) {
+        mstats_.ensure(4 * sizeof(unsigned long long));
+        hip_check(hipMemsetAsync(mstats_.p, 0, 4 * sizeof(unsigned long long), s), "memset stats");
       }
-      a.wprof = wprof_.as<unsigned long long>();
+      a.stats = mstats_.as<unsigned long long>();
     }
-    hip_check(hipMemsetAsync(a.ovf, 0, 4 * sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
     prof.begin(s);
-    launch_emit(a, s);
-    prof.end("emit", s);
-    hip_check(hipGetLastError(), "k_emit");
+    launch_desc(a, s);
+    prof.end("desc", s);
+    hip_check(hipGetLastError(), "k_desc");
+    prof.begin(s);
+    launch_copy(a, s);
+    prof.end("copy", s);
+    hip_check(hipGetLastError(), "k_copy");
+    prof.begin(s);
+    launch_merge(a, s);
+    prof.end("merge", s);
+    hip_check(hipGetLastError(), "k_merge");
+    prof.count("copy_rows", (uint64_t)a.total[0] + a.total[1] + a.total[2]);
+    prof.count("copy_bytes", 16ull * a.total[0] + 8ull * a.total[1] + 8ull * a.total[2]);
+    prof.count("merge_records", hi.merge - lo.merge);
     last_chunks_++;
-
-    // Topics whose merge table outgrew LDS: redo them with global tables sized by the counts
-    // the fast pass measured.
-    uint32_t ov[2] = {0, 0};
-    hip_check(hipMemcpyAsync(ov, a.ovf, sizeof(ov), hipMemcpyDeviceToHost, s), "D2H ovf");
-    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    prof.count("overflow_topics", ov[0]);
-    if (ov[0]) {
-      tab_.ensure((size_t)ov[1] * 3 * sizeof(uint32_t));
-      a.tab = tab_.as<uint32_t>();
-      a.tab_cap = ov[1];
-      a.list = a.ovf + 4;
-      a.n_list = ov[0];
-      prof.begin(s);
-      launch_emit(a, s);
-      prof.end("emit_overflow", s);
-      hip_check(hipGetLastError(), "k_emit<overflow>");
-    }
-
-    if (wprof_on_) {  // cumulative since the Device was created
-      unsigned long long w[kWpCount];
-      hip_check(hipMemcpyAsync(w, a.wprof, sizeof(w), hipMemcpyDeviceToHost, s), "D2H wprof");
+    if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
+      unsigned long long m[4];
+      hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, s), "D2H stats");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-      fprintf(stderr,
-              "[wprof] waves %llu total %llu setup %llu copy %llu merge %llu drain %llu mrecs %llu "
-              "tabrecs %llu lookups %llu probes %llu chunks %llu\n",
-              w[kWpWaves], w[kWpTotal], w[kWpSetup], w[kWpCopy], w[kWpMerge], w[kWpDrain],
-              w[kWpMergeRecs], w[kWpTabRecs], w[kWpLookups], w[kWpProbes], w[kWpChunks]);
+      fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
     }
-    const TopicOff& lo = h_bpre_[c.b0];
-    const TopicOff& hi = h_bpre_[c.b1];
+
     const uint32_t nt = a.t1 - a.t0;
     if (host) {
       hip_check(hipMemcpyAsync(host->rows.data() + lo.rows, rows_.p, (hi.rows - lo.rows) * sizeof(SubRec),
@@ -486,6 +489,8 @@ template struct DevMirror<NodeMsg>;
 template struct DevMirror<SegInfo>;
 template struct DevMirror<uint8_t>;
 template struct DevMirror<SubRec>;
+template struct DevMirror<MergeRef>;
+template struct DevMirror<MergePart>;
 template struct DevMirror<NodePair>;
 template struct DevMirror<PairEnt>;
 template struct DevMirror<ShrRec>;

@@ -1,5 +1,5 @@
 // Device side of the engine: the HBM-resident mirror of the index image and the batched match
-// pipeline (walk-count -> scan -> walk-fill -> emit per output chunk).
+// pipeline (walk-count -> scan -> [walk-fill] -> per output chunk: desc -> copy -> merge).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -115,7 +115,6 @@ class Device {
   uint64_t uploaded_ = 0, syncs_ = 0;
   uint32_t last_chunks_ = 0;
   uint64_t chunk_rows_budget_;
-  bool wprof_on_ = false;  // MQ_EMIT_PROF: k_emit wave-phase profile to stderr
   DevMirror<EdgeSlot> edges_;
   DevMirror<NodeWalk> walk_;
   DevMirror<NodeLists> lists_;
@@ -123,6 +122,8 @@ class Device {
   DevMirror<SegInfo> seginfo_;
   DevMirror<uint8_t> segbytes_;
   DevMirror<SubRec> subs_;
+  DevMirror<MergeRef> mref_;
+  DevMirror<MergePart> mpart_;
   DevMirror<NodePair> npair_;
   DevMirror<PairEnt> pent_;
   DevMirror<uint32_t> plist_;
@@ -131,8 +132,9 @@ class Device {
   DevMirror<uint32_t> children_;
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
-  DevBuf rows_, shr_rows_, inl_rows_, tab_, res_, err_;
-  DevBuf msg_handles_, msg_base_, msg_count_, gslots_, ovf_, wprof_;
+  DevBuf rows_, shr_rows_, inl_rows_, res_, err_, desc_, tiles_;
+  DevBuf msg_handles_, msg_base_, msg_count_, gslots_, mstats_;
+  bool merge_stats_ = false;  // MQ_MERGE_STATS: k_merge work counters to stderr
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;
   uint64_t empty_handle_ = 0;

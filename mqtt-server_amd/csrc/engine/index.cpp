@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <stdexcept>
 
 namespace mq {
 
@@ -204,6 +205,7 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   segbytes.grow_to(1, 0);
   subp_.resize(1, PartList{0, 0, 0});
   parts.m.grow_to(1, 0);
+  mpart.m.grow_to(1, MergePart{kNone, 0});
   npair.grow_to(1, NodePair{0, kNone, 0, 0});
   pent.m.grow_to(1, PairEnt{kNone, 0, 0, 0});
   plist.m.grow_to(1, 0);
@@ -370,7 +372,7 @@ void Index::remove_node(uint32_t n) {
   shr.release(lists.h[n].shr_off, h.shr_cap);
   inl.release(lists.h[n].inl_off, h.inl_cap);
   children.release(msg.h[n].child_off, h.child_cap);
-  pairs_release(n);
+  merge_release(n);
   walk.at_w(n) = NodeWalk{kNone, kNone, 0, kNone};
   lists.at_w(n) = NodeLists{};
   msg.at_w(n) = NodeMsg{};
@@ -415,18 +417,25 @@ void Index::trim(uint32_t n) {  // topics.go:516-522
 
 // ---- subscription lists ----------------------------------------------------------------------------
 // A slot is the SubRec plus its partner list; they always move together, and the
-// (node, client) -> slot map follows. Any move re-numbers the node's may-merge slots, so the
-// node's pair block goes stale.
+// (node, client) -> slot map follows. A move changes the positions the device partner links
+// name: those of this node's slots and those held by the slot's partners.
 void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
   const SubRec r = subs.m.h[from];
   subs.m.at_w(to) = r;
   subp_[to] = subp_[from];
   sub_pos_.put((uint64_t)n << 32 | r.client, to);
-  pairs_dirty(n);
+  merge_dirty(n);
+  const PartList& p = subp_[to];
+  for (uint32_t i = 0; i < p.cnt; i++) merge_dirty(parts.m.h[p.off + i]);
 }
 
-void Index::pairs_release(uint32_t n) {
+void Index::merge_release(uint32_t n) {
   NodeHost& h = nh_[n];
+  if (h.mpart_cap) {
+    mpart.release(h.mpart_off, h.mpart_cap);
+    mpart.live -= h.mpart_cap;
+  }
+  h.mpart_off = h.mpart_cap = 0;
   const NodePair& P = npair.h[n];
   if (P.ent_mask != kNone) {
     pent.live -= P.n_lists;
@@ -441,27 +450,52 @@ void Index::pairs_release(uint32_t n) {
   if (P.ent_mask != kNone || P.n_lists) npair.at_w(n) = NodePair{0, kNone, 0, 0};
 }
 
-void Index::flush_pairs() {
-  thread_local std::vector<std::pair<uint32_t, uint32_t>> hk;  // (partner node h, slot k)
-  for (uint32_t n : pair_dirty_) {
-    pair_dirty_flag_[n] = 0;
-    pairs_release(n);
+void Index::flush_merge() {
+  if (mref.size() < subs.m.size()) mref.grow_to(subs.m.size(), MergeRef{0, 0});
+  for (uint32_t n : merge_dirty_) {
+    merge_dirty_flag_[n] = 0;
+    merge_release(n);
     if (!nh_[n].live) continue;
     const NodeLists& L = lists.h[n];
+    uint32_t links = 0;
+    for (uint32_t k = 0; k < L.n_merge; k++) links += subp_[L.sub_off + L.n_direct + k].cnt;
+    if (!links) continue;
+    uint32_t cap = 1;
+    while (cap < links) cap <<= 1;
+    const uint32_t off = mpart.alloc(cap);
+    uint32_t at = off;
+    for (uint32_t k = 0; k < L.n_merge; k++) {
+      const uint32_t pos = L.sub_off + L.n_direct + k;
+      const PartList& p = subp_[pos];
+      const uint32_t client = subs.m.h[pos].client;
+      mref.at_w(pos) = MergeRef{at, p.cnt};
+      for (uint32_t i = 0; i < p.cnt; i++) {
+        const uint32_t m = parts.m.h[p.off + i];
+        uint32_t mp = kNone;
+        if (!sub_pos_.get((uint64_t)m << 32 | client, &mp))  // partners are symmetric
+          throw std::logic_error("flush_merge: partner subscription missing");
+        mpart.m.at_w(at++) = MergePart{m, mp};
+      }
+    }
+    nh_[n].mpart_off = off;
+    nh_[n].mpart_cap = cap;
+    mpart.live += cap;
+
+    // pair block: partner node h -> g's slots k whose client also subscribes at h
+    thread_local std::vector<std::pair<uint32_t, uint32_t>> hk;
     hk.clear();
     for (uint32_t k = 0; k < L.n_merge; k++) {
       const PartList& p = subp_[L.sub_off + L.n_direct + k];
       for (uint32_t i = 0; i < p.cnt; i++) hk.emplace_back(parts.m.h[p.off + i], k);
     }
-    if (hk.empty()) continue;
     std::sort(hk.begin(), hk.end());
     uint32_t lists_n = 0;
     for (size_t i = 0; i < hk.size(); i++) lists_n += i == 0 || hk[i].first != hk[i - 1].first;
-    uint32_t cap = 2, lcap = 1;
-    while (cap < 2 * lists_n) cap <<= 1;
+    uint32_t ecap = 2, lcap = 1;
+    while (ecap < 2 * lists_n) ecap <<= 1;
     while (lcap < hk.size()) lcap <<= 1;
-    const uint32_t eo = pent.alloc(cap), lo = plist.alloc(lcap), mask = cap - 1;
-    for (uint32_t i = 0; i < cap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
+    const uint32_t eo = pent.alloc(ecap), lo = plist.alloc(lcap), mask = ecap - 1;
+    for (uint32_t i = 0; i < ecap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
     for (size_t i = 0; i < hk.size(); i++) plist.m.at_w(lo + i) = hk[i].second;
     for (size_t b = 0; b < hk.size();) {
       size_t e = b + 1;
@@ -474,10 +508,63 @@ void Index::flush_pairs() {
     pent.live += lists_n;
     plist.live += hk.size();
     npair.at_w(n) = NodePair{eo, mask, lo, lists_n};
-    nh_[n].pent_cap = cap;
+    nh_[n].pent_cap = ecap;
     nh_[n].plist_cap = lcap;
   }
-  pair_dirty_.clear();
+  merge_dirty_.clear();
+}
+
+bool Index::check(std::string* why) {
+  flush_merge();
+  auto bad = [&](const std::string& m) {
+    *why = m;
+    return false;
+  };
+  for (uint32_t n = 0; n < nh_.size(); n++) {
+    if (!nh_[n].live) continue;
+    const NodeLists& L = lists.h[n];
+    const std::string at = "node " + std::to_string(n);
+    if ((uint64_t)L.sub_off + L.n_direct + L.n_merge > subs.m.size() || L.n_direct + L.n_merge > nh_[n].sub_cap)
+      return bad(at + ": subscription list out of bounds");
+    if ((uint64_t)L.shr_off + L.shr_cnt > shr.m.size() || (uint64_t)L.inl_off + L.inl_cnt > inl.m.size())
+      return bad(at + ": shared/inline list out of bounds");
+    for (uint32_t k = 0; k < L.n_direct + L.n_merge; k++) {
+      const uint32_t pos = L.sub_off + k;
+      const uint32_t client = subs.m.h[pos].client;
+      uint32_t p = kNone;
+      if (!sub_pos_.get((uint64_t)n << 32 | client, &p) || p != pos) return bad(at + ": slot map stale");
+      const PartList& pl = subp_[pos];
+      if (k < L.n_direct) {
+        if (pl.cnt) return bad(at + ": direct slot with partners");
+        continue;
+      }
+      if (!pl.cnt) return bad(at + ": may-merge slot without partners");
+      const MergeRef r = mref.h[pos];
+      if (r.cnt != pl.cnt || (uint64_t)r.off + r.cnt > mpart.m.size()) return bad(at + ": partner ref stale");
+      for (uint32_t e = 0; e < r.cnt; e++) {
+        const MergePart mp = mpart.m.h[r.off + e];
+        if (mp.node != parts.m.h[pl.off + e] || mp.node >= nh_.size() || !nh_[mp.node].live)
+          return bad(at + ": partner node stale");
+        const NodeLists& M = lists.h[mp.node];
+        if (mp.pos < M.sub_off + M.n_direct || mp.pos >= M.sub_off + M.n_direct + M.n_merge)
+          return bad(at + ": partner position outside the partner's may-merge slots");
+        if (subs.m.h[mp.pos].client != client) return bad(at + ": partner position names another client");
+        if (!compatible(n, mp.node)) return bad(at + ": partner not co-matchable");
+        // the pair block of n lists slot k under partner node mp.node
+        const NodePair& P = npair.h[n];
+        if (P.ent_mask == kNone) return bad(at + ": may-merge slots without a pair block");
+        uint32_t sl = pair_hash(mp.node) & P.ent_mask;
+        while (pent.m.h[P.ent_off + sl].h != kNone && pent.m.h[P.ent_off + sl].h != mp.node)
+          sl = (sl + 1) & P.ent_mask;
+        const PairEnt& pe = pent.m.h[P.ent_off + sl];
+        if (pe.h != mp.node) return bad(at + ": pair block misses a partner node");
+        bool listed = false;
+        for (uint32_t i = 0; i < pe.cnt && !listed; i++) listed = plist.m.h[pe.off + i] == k - L.n_direct;
+        if (!listed) return bad(at + ": pair list misses a slot");
+      }
+    }
+  }
+  return true;
 }
 
 void Index::sub_ensure(uint32_t n, uint32_t need) {
@@ -502,7 +589,7 @@ uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
     pos = base + L.n_direct + L.n_merge;
     L.n_merge++;
     n_merge_++;
-    pairs_dirty(n);
+    merge_dirty(n);
   } else {
     pos = base + L.n_direct;
     if (L.n_merge) move_slot(n, pos, base + L.n_direct + L.n_merge);
@@ -528,7 +615,7 @@ void Index::sub_remove(uint32_t n, uint32_t pos) {
     if (pos != last) move_slot(n, last, pos);
     L.n_merge--;
     n_merge_--;
-    pairs_dirty(n);
+    merge_dirty(n);
   }
   subs.live--;
 }
@@ -551,10 +638,11 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
     L.n_merge--;
     n_merge_--;
   }
-  pairs_dirty(n);
+  merge_dirty(n);
   subs.m.at_w(other) = a;
   subp_[other] = ap;
   sub_pos_.put((uint64_t)n << 32 | a.client, other);
+  for (uint32_t i = 0; i < ap.cnt; i++) merge_dirty(parts.m.h[ap.off + i]);
 }
 
 void Index::part_set(uint32_t pos, const std::vector<uint32_t>& nodes) {
@@ -689,7 +777,7 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
       sub_pos_.get((uint64_t)m << 32 | client, &mp);
     }
     part_add(mp, n);
-    pairs_dirty(m);
+    merge_dirty(m);
   }
   mine.push_back(n);
   return 1;
@@ -740,7 +828,7 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
           part_release(mp);
           sub_set_merge(m, mp, false);
         }
-        pairs_dirty(m);
+        merge_dirty(m);
       }
     }
   }

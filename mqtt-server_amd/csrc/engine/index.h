@@ -141,7 +141,8 @@ struct NodeHost {
   uint32_t n_children = 0;
   uint32_t child_pos = 0;  // position in the parent's children slab
   uint32_t sub_cap = 0, shr_cap = 0, inl_cap = 0, child_cap = 0;
-  uint32_t pent_cap = 0, plist_cap = 0;
+  uint32_t mpart_off = 0, mpart_cap = 0;  // the node's slab of device partner links
+  uint32_t pent_cap = 0, plist_cap = 0;    // its pair block slabs
   uint16_t depth = 0;
   bool live = false;
   bool retain_path = false;
@@ -177,7 +178,9 @@ class Index {
   Mirror<uint8_t> segbytes;
   SlabPool<SubRec> subs;
   SlabPool<uint32_t> parts;   // host only: partner node ids of each may-merge slot
-  Mirror<NodePair> npair;     // pair blocks (layout.h), rebuilt by flush_pairs()
+  Mirror<MergeRef> mref;      // device partner links (layout.h), parallel to subs, and
+  SlabPool<MergePart> mpart;  // pair blocks, rebuilt per node by flush_merge()
+  Mirror<NodePair> npair;
   SlabPool<PairEnt> pent;
   SlabPool<uint32_t> plist;
   SlabPool<ShrRec> shr;
@@ -194,10 +197,14 @@ class Index {
   uint64_t n_subs_merge() const { return n_merge_; }
   uint32_t max_depth() const { return max_depth_; }
   uint64_t version() const { return version_; }
-  // Rebuild the pair blocks of nodes whose may-merge slots or partner lists changed since the
-  // last call (the Device calls this before uploading). O(partner links of those nodes).
-  void flush_pairs();
-  uint64_t pair_links() const { return plist.live; }
+  // Rebuild the device partner links of nodes whose may-merge slots, partner lists or
+  // partners' positions changed since the last call (the Device calls this before uploading).
+  // O(partner links of those nodes).
+  void flush_merge();
+  uint64_t merge_links() const { return mpart.live; }
+  // Flush, then verify the device-bound invariants (mq_index_check); false + reason on the
+  // first violation.
+  bool check(std::string* why);
 
  private:
   // path of `filter` from isolateParticle depth d on (topics.go:479-496 / 499-513)
@@ -230,14 +237,14 @@ class Index {
   void list_push(SlabPool<T>& pool, uint32_t& off, uint32_t& cnt, uint32_t& cap, const Rec& r);
 
   bool sub_is_merge(uint32_t n, uint32_t pos) const { return pos >= lists.h[n].sub_off + lists.h[n].n_direct; }
-  void pairs_dirty(uint32_t n) {
-    if (n >= pair_dirty_flag_.size()) pair_dirty_flag_.resize(nh_.size() > n ? nh_.size() : n + 1, 0);
-    if (!pair_dirty_flag_[n]) {
-      pair_dirty_flag_[n] = 1;
-      pair_dirty_.push_back(n);
+  void merge_dirty(uint32_t n) {
+    if (n >= merge_dirty_flag_.size()) merge_dirty_flag_.resize(nh_.size() > n ? nh_.size() : n + 1, 0);
+    if (!merge_dirty_flag_[n]) {
+      merge_dirty_flag_[n] = 1;
+      merge_dirty_.push_back(n);
     }
   }
-  void pairs_release(uint32_t n);
+  void merge_release(uint32_t n);
   uint32_t sub_count(uint32_t n) const { return lists[n].n_direct + lists[n].n_merge; }
 
   std::vector<NodeHost> nh_;
@@ -269,8 +276,8 @@ class Index {
     uint32_t off, cnt, cap;
   };
   std::vector<PartList> subp_;       // each slot's partner slab
-  std::vector<uint32_t> pair_dirty_;  // nodes whose pair block is stale
-  std::vector<uint8_t> pair_dirty_flag_;
+  std::vector<uint32_t> merge_dirty_;  // nodes whose device partner links are stale
+  std::vector<uint8_t> merge_dirty_flag_;
   std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
   std::unordered_map<std::string, RetEntry> retained_;
 };

@@ -7,14 +7,11 @@
 
 namespace mq {
 
-constexpr uint32_t kLdsTab = 512;      // LDS merge-table slots per wavefront
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
-constexpr uint32_t kLdsTabMax = 384;   // table-bound records allowed in an LDS merge table
-constexpr uint32_t kTList = 512;       // queued table-bound records per wave (flushed when full)
-constexpr uint32_t kPairMax = 128;     // gathers covered by the pair analysis
-constexpr uint32_t kHitMax = 128;      // (g, h) pair hits held per topic
-constexpr uint32_t kBitWin = 2048;     // may-merge slots per table-bound bitmap window
+constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves
+constexpr uint32_t kMapSlots = 512;    // per-wave LDS map (gathered merge node -> gather index)
+constexpr uint32_t kPairMax = 128;     // merge gathers covered by the pair analysis
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -26,6 +23,8 @@ struct DevIndex {
   const SegInfo* seginfo;
   const uint8_t* segbytes;
   const SubRec* subs;
+  const MergeRef* mref;
+  const MergePart* mpart;
   const NodePair* npair;
   const PairEnt* pent;
   const uint32_t* plist;
@@ -45,7 +44,7 @@ constexpr uint64_t kWalkGuard = 1ull << 26;
 
 // Exclusive offsets of a topic's outputs (scan of TopicCount).
 struct TopicOff {
-  uint64_t g, rows, shr, inl, tab;
+  uint64_t g, rows, shr, inl, merge;
 };
 
 // Same layout as mq_topic_result (include/mqmatch.h).
@@ -54,6 +53,23 @@ struct mq_topic_result_dev {
   uint32_t sub_cap, n_client, n_ident, n_shared, n_inline, reserved;
 };
 
+// One gather of a topic, flattened for the load-balanced copy (k_desc writes one per gather in
+// compact gather order). Positions are relative to the output chunk and cumulative over its
+// gathers: a topic's rows are the concatenation of its gathers' lists, so the position of a
+// gather's first row is also its destination, and k_copy finds the gather of an output row by
+// a cursor over these records.
+struct GDesc {  // 32 B
+  uint32_t r_pos;  // client-row stream: rows of the chunk before this gather
+  uint32_t r_src;  // subs pool offset of the node's list
+  uint32_t s_pos;  // shared rows
+  uint32_t s_src;
+  uint32_t i_pos;  // inline rows
+  uint32_t i_src;
+  uint32_t word;   // gather word (node | kGatherSubs | kGatherInline)
+  uint32_t pad;
+};
+
+// Per-chunk arguments of k_desc / k_copy / k_merge.
 struct EmitArgs {
   DevIndex ix;
   uint32_t t0, t1;          // topic range of this chunk
@@ -61,32 +77,24 @@ struct EmitArgs {
   TopicOff base;            // off[t0]: the chunk's output buffers start here
   const uint32_t* gathers;
   uint32_t gather_stride;   // kGatherCap: per-topic slots of the count pass; 0: compact at off.g
+  GDesc* desc;              // indexed by absolute gather index
+  uint32_t* tiles;          // k_copy tile -> first gather: [client | shared | inline] tiles
+  uint32_t n_tiles[3];      // tiles per stream
+  uint32_t total[3];        // rows per stream in this chunk
   SubRec* rows;
   ShrRec* shr_rows;
   InlRec* inl_rows;
-  uint32_t* tab;            // overflow pass: merge tables, key | row | meta planes of tab_cap
-  uint64_t tab_cap;
   mq_topic_result_dev* res; // indexed t - t0
-  // Fast pass (list == nullptr): merge tables in LDS. A topic whose table-bound records could
-  // outgrow LDS appends {t, slots} to the overflow list and is left for the overflow pass
-  // (list != nullptr), which claims `slots` of global table per topic.
-  const uint32_t* list;     // overflow pass: pairs {topic, table slots}
-  uint32_t n_list;
-  uint32_t* ovf;            // [0] count, [1] total slots, [2] claim counter, [4..] pairs
-  unsigned long long* wprof;  // diagnosis only (MQ_EMIT_PROF): per-phase wave cycles, kWp* slots
-};
-
-// k_emit wave-profile slots (EmitArgs::wprof).
-enum : int {
-  kWpWaves, kWpTotal, kWpSetup, kWpCopy, kWpMerge, kWpDrain, kWpTail, kWpMergeRecs,
-  kWpTabRecs, kWpLookups, kWpProbes, kWpChunks, kWpCount = 16
+  unsigned long long* stats;  // k_merge: [0] hit lists, [1] records resolved, [2] slow-path topics
 };
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
                  TopicCount* cnt, const TopicOff* off, uint32_t* gathers, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
-void launch_emit(const EmitArgs& a, hipStream_t s);
+void launch_desc(const EmitArgs& a, hipStream_t s);
+void launch_copy(const EmitArgs& a, hipStream_t s);
+void launch_merge(const EmitArgs& a, hipStream_t s);
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
                 uint32_t* count, hipStream_t s);

@@ -6,12 +6,15 @@
 //                   gathers and the rows each topic will emit.
 //   k_scan_*        exclusive scan of the per-topic counts into output offsets.
 //   k_walk<true>    the same walk again, writing the gather list (node + what to gather).
-//   k_emit          one wavefront (64 lanes) per topic: streams the gathered subscription
-//                   lists into the output rows (coalesced 16-byte rows), merges subscriptions of
-//                   clients with several matching filters through a per-wave LDS hash table
+//   k_desc          per output chunk, thread per topic: flattens the gathers into descriptors
+//                   and marks where each k_copy tile starts.
+//   k_copy          load-balanced streaming copy of every gathered list into output rows
+//                   (coalesced 16-byte rows, eight loads in flight per lane).
+//   k_merge         one wavefront (64 lanes) per topic: resolves the subscriptions of clients
+//                   with several matching filters through their partner links
 //                   (gatherSubscriptions + Subscription.Merge, topics.go:631-648,
-//                   packets/packets.go:254-274), copies shared rows and applies the inline
-//                   last-write rule (topics.go:668-676) with ballot/mbcnt compaction.
+//                   packets/packets.go:254-274) and applies the inline last-write rule
+//                   (topics.go:668-676), with ballot/mbcnt compaction.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -181,12 +184,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
     c.rows = rows;
     c.shared = shared;
     c.inlines = inl;
-    uint32_t tab = 0;
-    if (merge > kLdsTab / 2) {
-      tab = 1;
-      while (tab < 2 * merge) tab <<= 1;
-    }
-    c.table = tab;
+    c.merge = merge;
     cnt[t] = c;
     if (ng > kGatherCap) atomicOr(ix.err + 1, 1u);
   }
@@ -200,14 +198,14 @@ __device__ __forceinline__ void add_count(TopicOff& a, const TopicCount& c) {
   a.rows += c.rows;
   a.shr += c.shared;
   a.inl += c.inlines;
-  a.tab += c.table;
+  a.merge += c.merge;
 }
 __device__ __forceinline__ void add_off(TopicOff& a, const TopicOff& b) {
   a.g += b.g;
   a.rows += b.rows;
   a.shr += b.shr;
   a.inl += b.inl;
-  a.tab += b.tab;
+  a.merge += b.merge;
 }
 __device__ __forceinline__ TopicOff shfl_up_off(const TopicOff& v, int d) {
   TopicOff r;
@@ -215,7 +213,7 @@ __device__ __forceinline__ TopicOff shfl_up_off(const TopicOff& v, int d) {
   r.rows = __shfl_up(v.rows, d, 64);
   r.shr = __shfl_up(v.shr, d, 64);
   r.inl = __shfl_up(v.inl, d, 64);
-  r.tab = __shfl_up(v.tab, d, 64);
+  r.merge = __shfl_up(v.merge, d, 64);
   return r;
 }
 
@@ -257,7 +255,7 @@ __global__ __launch_bounds__(256) void k_scan_blocks(const TopicOff* __restrict_
     TopicOff incl = block_scan_incl(v, wt);
     TopicOff c = carry;
     TopicOff ex = incl;
-    ex.g -= v.g; ex.rows -= v.rows; ex.shr -= v.shr; ex.inl -= v.inl; ex.tab -= v.tab;
+    ex.g -= v.g; ex.rows -= v.rows; ex.shr -= v.shr; ex.inl -= v.inl; ex.merge -= v.merge;
     add_off(ex, c);
     if (b < nb) bpre[b] = ex;
     __syncthreads();
@@ -281,7 +279,7 @@ __global__ __launch_bounds__(256) void k_scan_apply(const TopicCount* __restrict
   TopicOff incl = block_scan_incl(v, wt);
   TopicOff ex = bpre[blockIdx.x];
   add_off(ex, incl);
-  ex.g -= v.g; ex.rows -= v.rows; ex.shr -= v.shr; ex.inl -= v.inl; ex.tab -= v.tab;
+  ex.g -= v.g; ex.rows -= v.rows; ex.shr -= v.shr; ex.inl -= v.inl; ex.merge -= v.merge;
   for (int k = 0; k < 4; k++) {
     if (base + k < n) off[base + k] = ex;
     add_count(ex, c[k]);
@@ -290,11 +288,18 @@ __global__ __launch_bounds__(256) void k_scan_apply(const TopicCount* __restrict
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_emit: expand + merge + emit (one wavefront per topic)
+// Emit: every gathered subscription list becomes output rows.
+//   k_desc   thread per topic: flattens the topic's gathers into GDesc records and marks the
+//            k_copy tiles that start inside each gather.
+//   k_copy   load-balanced streaming copy: each wavefront moves kCopyTile consecutive rows of
+//            one stream (direct client rows, shared rows, inline rows) of the whole chunk,
+//            whatever topics and gathers they belong to — 64 consecutive rows per
+//            wave-instruction, eight loads in flight per lane.
+//   k_merge  wavefront per topic: resolves the may-merge records through their partner links
+//            (gatherSubscriptions + Subscription.Merge, topics.go:631-648,
+//            packets/packets.go:254-274), applies the inline last-write rule (topics.go:668-676)
+//            and writes the topic's result record.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kTabEmpty = 0xFFFFFFFFu;
-constexpr uint32_t kMetaDirty = 0x80000000u;
-
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -304,7 +309,6 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   return x;
 }
 
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t prefix_before(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
 }
@@ -321,447 +325,309 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
   return x - v;
 }
 
-// Copy the concatenation of up to 64 record lists (list j at src + off[j], exclusive prefix
-// pre[j], pre[64] = total) to dst[0, total): 64 consecutive rows per wave-instruction, four
-// loads in flight per lane. Each lane keeps a cursor j that only advances. The rows are
-// written once and never re-read here, so they are stored non-temporally and do not evict
-// the hot subscription lists from L2 / the Infinity Cache.
-template <class V>
-__device__ __forceinline__ void copy_lists(V* __restrict__ dst, const V* __restrict__ src,
-                                           const uint32_t* __restrict__ off,
-                                           const uint32_t* __restrict__ pre, uint32_t total,
-                                           uint32_t lane) {
-  // Loads are issued unconditionally (idle lanes re-read the last row) so the four stay in
-  // flight together: a load inside a divergent branch makes the compiler wait for it at the
-  // branch join.
-  uint32_t j = 0;
-  for (uint32_t r0 = 0; r0 < total; r0 += 256) {
-    uint32_t src_i[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t r = min(r0 + k * 64 + lane, total - 1);
-      while (pre[j + 1] <= r) j++;
-      src_i[k] = off[j] + (r - pre[j]);
-    }
-    V v[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) v[k] = src[src_i[k]];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t r = r0 + k * 64 + lane;
-      if (r < total) __builtin_nontemporal_store(v[k], dst + r);
-    }
-  }
-}
-
-constexpr uint32_t kGroup = 64;  // gathers staged per pass: one per lane
-
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
-  __shared__ uint32_t lds_key[4][kLdsTab];
-  __shared__ uint32_t lds_row[4][kLdsTab];
-  __shared__ uint32_t lds_meta[4][kLdsTab];
-  __shared__ uint32_t gwl[4][kPairMax];          // the topic's gather words (pair analysis)
-  __shared__ uint32_t ghit[4][kPairMax];         // gather has table-bound records
-  __shared__ uint32_t hit_g[4][kHitMax];         // hits: gather index, list offset, list length
-  __shared__ uint32_t hit_off[4][kHitMax];
-  __shared__ uint32_t hit_cnt[4][kHitMax];
-  __shared__ uint32_t bm[4][kBitWin / 32];       // table-bound bitmap of a may-merge window
-  __shared__ uint32_t tlist[4][kTList];          // table-bound records queued for the table
-  __shared__ uint32_t g_off[3][4][kGroup];       // direct-sub / shared / inline list offsets
-  __shared__ uint32_t g_pre[3][4][kGroup + 1];   // their exclusive prefixes (+ total)
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t w = blockIdx.x * 4 + wv;
-  uint32_t t;
-  if (a.list) {
-    if (w >= a.n_list) return;  // wave-uniform
-    t = a.list[2 * w];
-  } else {
-    t = a.t0 + w;
-    if (t >= a.t1) return;  // wave-uniform
-  }
-  const bool global_tab = a.list != nullptr;
-  // Diagnosis only (MQ_EMIT_PROF): per-phase wave cycles and work counts.
-  const bool wp = a.wprof != nullptr;
-  const long long wp_t0 = wp ? clock64() : 0;
-  long long wp_copy = 0, wp_merge = 0, wp_drain = 0, wp_setup = 0;
-  uint32_t wp_mrecs = 0, wp_chunks = 0, wp_look = 0, wp_probe = 0;
-  auto wp_flush = [&](uint32_t tab_recs) {
-    if (!wp) return;
-    const uint32_t lk = wave_sum(wp_look), pr = wave_sum(wp_probe);
-    if (lane == 0) {
-      unsigned long long* q = a.wprof;
-      atomicAdd(q + kWpWaves, 1ull);
-      atomicAdd(q + kWpTotal, (unsigned long long)(clock64() - wp_t0));
-      atomicAdd(q + kWpSetup, (unsigned long long)wp_setup);
-      atomicAdd(q + kWpCopy, (unsigned long long)wp_copy);
-      atomicAdd(q + kWpMerge, (unsigned long long)wp_merge);
-      atomicAdd(q + kWpDrain, (unsigned long long)wp_drain);
-      atomicAdd(q + kWpMergeRecs, (unsigned long long)wp_mrecs);
-      atomicAdd(q + kWpTabRecs, (unsigned long long)tab_recs);
-      atomicAdd(q + kWpLookups, (unsigned long long)lk);
-      atomicAdd(q + kWpProbes, (unsigned long long)pr);
-      atomicAdd(q + kWpChunks, (unsigned long long)wp_chunks);
-    }
-  };
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
+__device__ __forceinline__ uint32_t gather_word(const EmitArgs& a, uint32_t t, const TopicOff& o0, uint32_t i) {
+  return a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + i] : a.gathers[o0.g + i];
+}
+
+__global__ __launch_bounds__(256) void k_desc(EmitArgs a) {
+  const uint32_t t = a.t0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.t1) return;
+  const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+  uint32_t rpos = (uint32_t)(o0.rows - a.base.rows);
+  uint32_t spos = (uint32_t)(o0.shr - a.base.shr), ipos = (uint32_t)(o0.inl - a.base.inl);
+  const uint32_t n_g = (uint32_t)(o1.g - o0.g);
+  uint32_t* tile_r = a.tiles;
+  uint32_t* tile_s = a.tiles + a.n_tiles[0];
+  uint32_t* tile_i = tile_s + a.n_tiles[1];
+  for (uint32_t i = 0; i < n_g; i++) {
+    const uint32_t gw = gather_word(a, t, o0, i);
+    const NodeLists L = a.ix.lists[gw & kGatherNode];
+    const uint32_t rn = (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
+    const uint32_t in = (gw & kGatherInline) ? L.inl_cnt : 0u;
+    const uint32_t g = (uint32_t)(o0.g + i);
+    GDesc d;
+    d.r_pos = rpos;
+    d.r_src = L.sub_off;
+    d.s_pos = spos;
+    d.s_src = L.shr_off;
+    d.i_pos = ipos;
+    d.i_src = L.inl_off;
+    d.word = gw;
+    d.pad = 0;
+    a.desc[g] = d;
+    // the k_copy tiles whose first row falls inside this gather start their cursor here
+    for (uint32_t k = (rpos + kCopyTile - 1) / kCopyTile; k * kCopyTile < rpos + rn; k++) tile_r[k] = g;
+    for (uint32_t k = (spos + kCopyTile - 1) / kCopyTile; k * kCopyTile < spos + L.shr_cnt; k++) tile_s[k] = g;
+    for (uint32_t k = (ipos + kCopyTile - 1) / kCopyTile; k * kCopyTile < ipos + in; k++) tile_i[k] = g;
+    rpos += rn;
+    spos += L.shr_cnt;
+    ipos += in;
+  }
+}
+
+// Stream S of one tile: rows [x0, x1) of the chunk's stream S (0: client rows, 1: shared rows,
+// 2: inline rows), starting at gather j.
+template <int S, class V>
+__device__ __forceinline__ void copy_tile(const EmitArgs& a, const V* __restrict__ src, V* __restrict__ dst,
+                                          uint32_t x0, uint32_t x1, uint32_t j, uint32_t lane) {
+  constexpr int U = 8;
+  const uint32_t jend = (uint32_t)a.off[a.t1].g;
+  auto pos_of = [&](uint32_t g) -> uint32_t {
+    return S == 0 ? a.desc[g].r_pos : (S == 1 ? a.desc[g].s_pos : a.desc[g].i_pos);
+  };
+  auto src_of = [&](uint32_t g) -> uint32_t {
+    return S == 0 ? a.desc[g].r_src : (S == 1 ? a.desc[g].s_src : a.desc[g].i_src);
+  };
+  uint32_t cur = pos_of(j);
+  uint32_t nxt = j + 1 < jend ? pos_of(j + 1) : 0xFFFFFFFFu;
+  uint32_t sb = src_of(j) - cur;  // source index = sb + row
+  for (uint32_t r0 = x0; r0 < x1; r0 += 64 * U) {
+    uint32_t si[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t x = min(r0 + u * 64 + lane, x1 - 1);
+      while (x >= nxt) {  // advance this lane's cursor to the gather holding row x
+        j++;
+        cur = nxt;
+        nxt = j + 1 < jend ? pos_of(j + 1) : 0xFFFFFFFFu;
+        sb = src_of(j) - cur;
+      }
+      si[u] = sb + x;
+    }
+    V v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = src[si[u]];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t x = r0 + u * 64 + lane;
+      if (x < x1) __builtin_nontemporal_store(v[u], dst + x);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t j = a.tiles[min(w, a.n_tiles[0] + a.n_tiles[1] + a.n_tiles[2] - 1)];
+  if (w < a.n_tiles[0]) {
+    const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[0]);
+    copy_tile<0>(a, reinterpret_cast<const u32x4*>(a.ix.subs), reinterpret_cast<u32x4*>(a.rows), x0, x1, j, lane);
+    return;
+  }
+  w -= a.n_tiles[0];
+  if (w < a.n_tiles[1]) {
+    const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[1]);
+    copy_tile<1>(a, reinterpret_cast<const u32x2*>(a.ix.shr), reinterpret_cast<u32x2*>(a.shr_rows), x0, x1, j, lane);
+    return;
+  }
+  w -= a.n_tiles[1];
+  if (w < a.n_tiles[2]) {
+    const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[2]);
+    copy_tile<2>(a, reinterpret_cast<const u32x2*>(a.ix.inl), reinterpret_cast<u32x2*>(a.inl_rows), x0, x1, j, lane);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
+  __shared__ uint32_t map_key[4][kMapSlots];  // gathered node with may-merge records
+  __shared__ uint32_t map_val[4][kMapSlots];  // its gather index (= DFS rank order)
+  __shared__ uint32_t mg_node[4][kPairMax];   // the topic's merge gathers, in gather order:
+  __shared__ uint32_t mg_gi[4][kPairMax];     //   node, gather index,
+  __shared__ uint32_t mg_moff[4][kPairMax];   //   subs pool offset of its may-merge slots,
+  __shared__ uint32_t mg_row[4][kPairMax];    //   output row of its first may-merge slot
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t t = a.t0 + blockIdx.x * 4 + wv;
+  if (t >= a.t1) return;  // wave-uniform
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
   const uint32_t cap = (uint32_t)(o1.rows - o0.rows);
-  const uint64_t sb = o0.shr - a.base.shr, ib = o0.inl - a.base.inl;
-  SubRec* __restrict__ rows = a.rows + rb;
+  const uint64_t ib = o0.inl - a.base.inl;
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
-  auto gword = [&](uint32_t i) {
-    return a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + i] : a.gathers[o0.g + i];
-  };
+  const GDesc* __restrict__ gd = a.desc + o0.g;
+  SubRec* __restrict__ crow = a.rows;  // chunk-relative rows (GDesc positions)
+  uint32_t n_nonbase = 0, n_ext = 0;
+  uint32_t st_hits = 0, st_recs = 0, st_slow = 0;
 
-  // ---- Pair analysis: which may-merge records need the merge table. For every ordered pair
-  // (g, h) of gathered nodes with subscriptions, g's pair block lists g's may-merge slots whose
-  // client also subscribes at h (layout.h). The union of the hit lists of g is exactly g's
-  // table-bound records; every other record of the topic is its client's only match and is
-  // emitted as is. Beyond kPairMax gathers or kHitMax hits every may-merge record is
-  // table-bound (correct, slower; not seen in the SURVEY.md §8d workloads).
-  bool pair_ok = n_g <= kPairMax;
-  uint32_t n_hit = 0, ub = 0;  // hits; upper bound of the table-bound records
-  if (pair_ok) {
-    for (uint32_t i = lane; i < n_g; i += 64) {
-      gwl[wv][i] = gword(i);
-      ghit[wv][i] = 0;
+  if (o1.merge > o0.merge) {  // the topic gathers may-merge records
+    // Map every gathered node that holds may-merge records (and whose subscriptions are
+    // gathered, Q3) to its gather index, and list them in gather order. Nodes are distinct
+    // within a topic.
+    for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
+    wave_sync_lds();
+    uint32_t n_map = 0;
+    for (uint32_t i0 = 0; i0 < n_g; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      bool ins = false;
+      uint32_t node = 0, moff = 0, mrow = 0;
+      if (i < n_g) {
+        const GDesc d = gd[i];
+        node = d.word & kGatherNode;
+        if (d.word & kGatherSubs) {
+          const NodeLists L = a.ix.lists[node];
+          ins = L.n_merge > 0;
+          moff = L.sub_off + L.n_direct;
+          mrow = d.r_pos + L.n_direct;
+        }
+      }
+      const uint64_t bi = __ballot(ins);
+      const uint32_t x = n_map + prefix_before(bi);
+      if (ins && x < kMapSlots / 2) {
+        uint32_t sl = hash32(node) & (kMapSlots - 1);
+        while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
+        map_val[wv][sl] = i;
+      }
+      if (ins && x < kPairMax) {
+        mg_node[wv][x] = node;
+        mg_gi[wv][x] = i;
+        mg_moff[wv][x] = moff;
+        mg_row[wv][x] = mrow;
+      }
+      n_map += __popcll(bi);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t np = n_g * n_g;
-    uint32_t ub_l = 0;
-    for (uint32_t p0 = 0; p0 < np; p0 += 64) {
-      const uint32_t p = p0 + lane;
-      bool hit = false;
-      uint32_t gi = 0, e_off = 0, e_cnt = 0;
-      if (p < np) {
-        gi = p / n_g;
-        const uint32_t hi = p - gi * n_g;
-        const uint32_t gg = gwl[wv][gi], gh = gwl[wv][hi];
-        if (gi != hi && (gg & gh & kGatherSubs)) {
-          const NodePair P = a.ix.npair[gg & kGatherNode];
-          if (P.ent_mask != kNone) {
-            const uint32_t h = gh & kGatherNode;
-            uint32_t sl = pair_hash(h) & P.ent_mask;
-            if (wp) wp_look++;
-            for (;;) {
-              if (wp) wp_probe++;
-              const PairEnt e = a.ix.pent[P.ent_off + sl];
-              if (e.h == h) {
-                hit = true;
-                e_off = e.off;
-                e_cnt = e.cnt;
-                break;
+    wave_sync_lds();
+    const bool scan_all = n_map > kMapSlots / 2;  // beyond the map: look partners up linearly
+    auto gathered = [&](uint32_t h) -> uint32_t {  // gather index of node h, or kNone
+      if (!scan_all) {
+        uint32_t sl = hash32(h) & (kMapSlots - 1);
+        for (;;) {
+          const uint32_t k = map_key[wv][sl];
+          if (k == h) return map_val[wv][sl];
+          if (k == kNone) return kNone;
+          sl = (sl + 1) & (kMapSlots - 1);
+        }
+      }
+      for (uint32_t i = 0; i < n_g; i++) {
+        const uint32_t gw = gd[i].word;
+        if ((gw & kGatherNode) == h && (gw & kGatherSubs)) return i;
+      }
+      return kNone;
+    };
+
+    // Resolve one record whose client may have other matches for this topic: its partners that
+    // are gathered decide it (layout.h, MergeRef). An earlier one makes it a non-base entry:
+    // an Identifiers row when its identifier is > 0 (Subscription.Merge,
+    // packets/packets.go:261-263), else dropped. Otherwise it is the base and takes the
+    // partners' max Qos and OR'd NoLocal (packets/packets.go:265-271). A record may be reached
+    // through several hit lists; every visit writes the same row, and only the visit through
+    // its first gathered partner (`via`, or any when via == kNone) counts it.
+    auto resolve = [&](bool active, uint32_t pos, uint32_t row, uint32_t gi, uint32_t via) {
+      bool counted = false, nonbase = false;
+      int32_t ident = 0;
+      if (active) {
+        const SubRec rec = a.ix.subs[pos];
+        const MergeRef mr = a.ix.mref[pos];
+        bool bound = false, base = true;
+        uint32_t first = kNone;
+        uint32_t q = rec.meta & kMetaQos, nl = rec.meta & kMetaNoLocal;
+        for (uint32_t e = 0; e < mr.cnt; e++) {
+          const MergePart p = a.ix.mpart[mr.off + e];
+          const uint32_t gh = gathered(p.node);
+          if (gh == kNone) continue;
+          if (!bound) first = p.node;
+          bound = true;
+          if (gh < gi) {
+            base = false;
+            break;
+          }
+          const uint32_t pm = a.ix.subs[p.pos].meta;
+          q = max(q, pm & kMetaQos);
+          nl |= pm & kMetaNoLocal;
+        }
+        if (bound) {
+          counted = via == kNone || via == first;
+          nonbase = !base;
+          ident = rec.ident;
+          if (base) {
+            const uint32_t m = (rec.meta & ~(kMetaQos | kMetaNoLocal)) | q | nl;
+            if (m != rec.meta) crow[row].meta = m;
+          } else {
+            crow[row].meta = rec.meta | (rec.ident > 0 ? kRowIdent : kRowDrop);
+          }
+        }
+      }
+      const uint64_t bn = __ballot(counted && nonbase);
+      const uint64_t bx = __ballot(counted && nonbase && ident > 0);
+      n_nonbase += __popcll(bn);
+      n_ext += __popcll(bx);
+    };
+
+    if (n_map <= kPairMax) {
+      // Pair analysis over ordered pairs (g, h) of merge gathers: g's pair block lists the slots
+      // whose client also subscribes at h. Every hit list is resolved by the whole wave.
+      const uint32_t np = n_map * n_map;
+      for (uint32_t p0 = 0; p0 < np; p0 += 64) {
+        const uint32_t p = p0 + lane;
+        bool hit = false;
+        uint32_t ga = 0, e_off = 0, e_cnt = 0, hn = 0;
+        if (p < np) {
+          ga = p / n_map;
+          const uint32_t hb = p - ga * n_map;
+          if (ga != hb) {
+            const NodePair P = a.ix.npair[mg_node[wv][ga]];
+            if (P.ent_mask != kNone) {
+              hn = mg_node[wv][hb];
+              uint32_t sl = pair_hash(hn) & P.ent_mask;
+              for (uint32_t probes = 0; probes <= P.ent_mask; probes++) {
+                const PairEnt e = a.ix.pent[P.ent_off + sl];
+                if (e.h == hn) {
+                  hit = true;
+                  e_off = e.off;
+                  e_cnt = e.cnt;
+                  break;
+                }
+                if (e.h == kNone) break;
+                sl = (sl + 1) & P.ent_mask;
               }
-              if (e.h == kNone) break;
-              sl = (sl + 1) & P.ent_mask;
             }
           }
         }
-      }
-      const uint64_t bh = __ballot(hit);
-      if (hit) {
-        const uint32_t x = n_hit + prefix_before(bh);
-        if (x < kHitMax) {
-          hit_g[wv][x] = gi;
-          hit_off[wv][x] = e_off;
-          hit_cnt[wv][x] = e_cnt;
-        }
-        ghit[wv][gi] = 1;
-      }
-      n_hit += __popcll(bh);
-      ub_l += e_cnt;
-    }
-    ub = wave_sum(ub_l);
-    if (n_hit > kHitMax) pair_ok = false;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (!pair_ok) {  // every may-merge record is table-bound
-    uint32_t ub_l = 0;
-    for (uint32_t i = lane; i < n_g; i += 64) {
-      const uint32_t gw = gword(i);
-      if (gw & kGatherSubs) ub_l += a.ix.lists[gw & kGatherNode].n_merge;
-    }
-    ub = wave_sum(ub_l);
-  }
-  if (wp) wp_setup = clock64() - wp_t0;
-
-  // A topic whose table would outgrow LDS goes to the overflow pass, which gives it a global
-  // table of >= 2 * ub slots.
-  if (!global_tab && ub > kLdsTabMax) {
-    if (lane == 0) {
-      uint32_t slots = 1;
-      while (slots < 2 * ub) slots <<= 1;
-      const uint32_t i = atomicAdd(a.ovf, 1u);
-      a.ovf[4 + 2 * i] = t;
-      a.ovf[4 + 2 * i + 1] = slots;
-      atomicAdd(a.ovf + 1, slots);
-    }
-    wp_flush(ub);
-    return;
-  }
-
-  // Merge table: LDS on the fast pass, a global slice on the overflow pass. Accesses branch on
-  // the (wave-uniform) kind so each compiles to typed ds_* / global_* instructions.
-  uint32_t* gk = nullptr;
-  uint32_t* gr = nullptr;
-  uint32_t* gm = nullptr;
-  uint32_t tmask = kLdsTab - 1;
-  if (global_tab) {
-    const uint32_t slots = a.list[2 * w + 1];
-    uint32_t tb = 0;
-    if (lane == 0) tb = atomicAdd(a.ovf + 2, slots);
-    tb = __builtin_amdgcn_readfirstlane(tb);
-    gk = a.tab + tb;
-    gr = a.tab + a.tab_cap + tb;
-    gm = a.tab + 2 * a.tab_cap + tb;
-    tmask = slots - 1;
-  }
-  auto tk_load = [&](uint32_t i) -> uint32_t {
-    return global_tab ? __hip_atomic_load(gk + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : __hip_atomic_load(&lds_key[wv][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-  auto tk_cas = [&](uint32_t i, uint32_t v) -> uint32_t {
-    return global_tab ? atomicCAS(gk + i, kTabEmpty, v) : atomicCAS(&lds_key[wv][i], kTabEmpty, v);
-  };
-  auto tk_store = [&](uint32_t i, uint32_t v) {
-    if (global_tab) gk[i] = v; else lds_key[wv][i] = v;
-  };
-  auto tr_load = [&](uint32_t i) -> uint32_t { return global_tab ? gr[i] : lds_row[wv][i]; };
-  auto tr_store = [&](uint32_t i, uint32_t v) {
-    if (global_tab) gr[i] = v; else lds_row[wv][i] = v;
-  };
-  auto tm_load = [&](uint32_t i) -> uint32_t { return global_tab ? gm[i] : lds_meta[wv][i]; };
-  auto tm_store = [&](uint32_t i, uint32_t v) {
-    if (global_tab) gm[i] = v; else lds_meta[wv][i] = v;
-  };
-  // Insert `key` (distinct across the active lanes); returns the slot and whether it was new.
-  auto tab_insert = [&](uint32_t key, bool* is_new) -> uint32_t {
-    uint32_t sl = hash32(key) & tmask;
-    for (uint32_t probes = 0; probes <= tmask; probes++) {
-      const uint32_t k = tk_load(sl);
-      if (k == key) {
-        *is_new = false;
-        return sl;
-      }
-      if (k == kTabEmpty) {
-        const uint32_t old = tk_cas(sl, key);
-        if (old == kTabEmpty) {
-          *is_new = true;
-          return sl;
-        }
-        if (old == key) {
-          *is_new = false;
-          return sl;
-        }
-      }
-      sl = (sl + 1) & tmask;
-    }
-    atomicOr(a.ix.err, kErrTableFull);  // sized at <= 3/4 load: unreachable
-    *is_new = false;
-    return 0;
-  };
-  bool tab_ready = false;
-  uint32_t tab_recs = 0;
-
-  uint32_t n_cli = 0, n_ext = 0, n_shr = 0, n_inl = 0;
-  for (uint64_t g0 = o0.g; g0 < o1.g; g0 += kGroup) {
-    // Stage up to 64 gathers at once (one per lane): the gather word and the node's lists. A
-    // node without table-bound records this topic is copied whole (direct and may-merge
-    // slots are contiguous); the others copy their direct part and stream the rest below.
-    const uint32_t gbase = (uint32_t)(g0 - o0.g);
-    const uint32_t ng = (uint32_t)min<uint64_t>(kGroup, o1.g - g0);
-    uint32_t dn = 0, mn = 0, sn = 0, in = 0, sub_off = 0, shr_off = 0, inl_off = 0;
-    if (lane < ng) {
-      const uint32_t gw = pair_ok ? gwl[wv][gbase + lane] : gword(gbase + lane);
-      const NodeLists L = a.ix.lists[gw & kGatherNode];
-      if (gw & kGatherSubs) {
-        const bool tb = pair_ok ? ghit[wv][gbase + lane] != 0 : L.n_merge != 0;
-        dn = tb ? L.n_direct : L.n_direct + L.n_merge;
-        mn = tb ? L.n_merge : 0;
-      }
-      sub_off = L.sub_off;
-      sn = L.shr_cnt;
-      shr_off = L.shr_off;
-      if (gw & kGatherInline) {
-        in = L.inl_cnt;
-        inl_off = L.inl_off;
-      }
-    }
-    uint32_t dt, st, it;
-    const uint32_t dp = wave_excl_scan(dn, lane, &dt);
-    const uint32_t sp = wave_excl_scan(sn, lane, &st);
-    const uint32_t ip = wave_excl_scan(in, lane, &it);
-    g_off[0][wv][lane] = sub_off;
-    g_off[1][wv][lane] = shr_off;
-    g_off[2][wv][lane] = inl_off;
-    g_pre[0][wv][lane] = dp;
-    g_pre[1][wv][lane] = sp;
-    g_pre[2][wv][lane] = ip;
-    if (lane == 0) {
-      g_pre[0][wv][kGroup] = dt;
-      g_pre[1][wv][kGroup] = st;
-      g_pre[2][wv][kGroup] = it;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-
-    const long long wp_c = wp ? clock64() : 0;
-    // Records that are their client's only match: one flat coalesced copy into client rows.
-    copy_lists(reinterpret_cast<u32x4*>(rows + n_cli), reinterpret_cast<const u32x4*>(a.ix.subs),
-               g_off[0][wv], g_pre[0][wv], dt, lane);
-    n_cli += dt;
-    // Shared[sub.Filter][client] = sub (topics.go:656-663)
-    copy_lists(reinterpret_cast<u32x2*>(a.shr_rows + sb + n_shr), reinterpret_cast<const u32x2*>(a.ix.shr),
-               g_off[1][wv], g_pre[1][wv], st, lane);
-    n_shr += st;
-    // Inline subscriptions in gather order; the last write per id is kept below.
-    copy_lists(reinterpret_cast<u32x2*>(a.inl_rows + ib + n_inl), reinterpret_cast<const u32x2*>(a.ix.inl),
-               g_off[2][wv], g_pre[2][wv], it, lane);
-    n_inl += it;
-    if (wp) wp_copy += clock64() - wp_c;
-    const long long wp_m = wp ? clock64() : 0;
-
-    // Nodes with table-bound records, in gather (rank) order.
-    uint64_t mm = __ballot(mn > 0);
-    while (mm) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(mm);
-      mm &= mm - 1;
-      const uint32_t gidx = gbase + j;
-      const uint32_t m_cnt = __builtin_amdgcn_readlane(mn, j);
-      const uint32_t m_off = __builtin_amdgcn_readlane(sub_off + dn, j);
-      const SubRec* __restrict__ ms = a.ix.subs + m_off;
-      wp_mrecs += m_cnt;
-      uint32_t nt = 0;  // table-bound records queued in tlist
-      // Table pass over the queue (the clients with several matches). Records of one gather
-      // belong to distinct clients, so their order within the gather does not matter.
-      auto drain = [&]() {
-        const long long wp_d = wp ? clock64() : 0;
-        if (!tab_ready) {
-          for (uint32_t q = lane; q <= tmask; q += 64) tk_store(q, kTabEmpty);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          tab_ready = true;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        tab_recs += nt;
-        for (uint32_t c0 = 0; c0 < nt; c0 += 64) {
-          const bool vt = c0 + lane < nt;
-          SubRec r{0, 0, 0, 0};
-          uint32_t slot = 0;
-          bool is_new = false;
-          if (vt) {
-            r = ms[tlist[wv][c0 + lane]];
-            slot = tab_insert(r.client, &is_new);
-          }
-          const uint64_t bn = __ballot(vt && is_new);
-          if (vt && is_new) {  // first (minimum-rank) subscription of this client: the base
-            const uint32_t pos = n_cli + prefix_before(bn);
-            rows[pos] = r;
-            tr_store(slot, pos);
-            tm_store(slot, r.meta);
-          }
-          n_cli += __popcll(bn);
-          const bool dup = vt && !is_new;
-          if (dup) {  // Subscription.Merge: max Qos, OR NoLocal (packets/packets.go:264-271)
-            const uint32_t mt = tm_load(slot);
-            const uint32_t q = max(mt & kMetaQos, r.meta & kMetaQos);
-            const uint32_t nm = (mt & ~kMetaQos) | q | (r.meta & kMetaNoLocal);
-            if ((nm & ~kMetaDirty) != (mt & ~kMetaDirty)) tm_store(slot, nm | kMetaDirty);
-          }
-          const uint64_t be = __ballot(dup && r.ident > 0);
-          if (dup && r.ident > 0) {  // Identifiers[n.Filter] = n.Identifier (id > 0)
-            const uint32_t e = n_ext + prefix_before(be);
-            SubRec x{r.client, r.filter_id, r.ident, 0};
-            rows[cap - 1 - e] = x;
-          }
-          n_ext += __popcll(be);
-        }
-        nt = 0;
-        if (wp) wp_drain += clock64() - wp_d;
-      };
-
-      if (!pair_ok) {  // all of them
-        for (uint32_t i0 = 0; i0 < m_cnt; i0 += 64) {
-          if (i0 + lane < m_cnt) tlist[wv][nt + lane] = i0 + lane;
-          nt += min(64u, m_cnt - i0);
-          if (nt + 64 > kTList) drain();
-        }
-        if (nt) drain();
-        continue;
-      }
-      for (uint32_t w0 = 0; w0 < m_cnt; w0 += kBitWin) {
-        const uint32_t wn = min(kBitWin, m_cnt - w0);
-        // Mark this window's table-bound slots (union of the gather's hit lists) and queue
-        // each once for the table.
-        for (uint32_t q = lane; q < kBitWin / 32; q += 64) bm[wv][q] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t x = 0; x < n_hit; x++) {
-          if (hit_g[wv][x] != gidx) continue;  // wave-uniform
-          const uint32_t off = hit_off[wv][x], cnt = hit_cnt[wv][x];
+        uint64_t bh = __ballot(hit);
+        st_hits += __popcll(bh);
+        while (bh) {
+          const uint32_t src = (uint32_t)__builtin_ctzll(bh);
+          bh &= bh - 1;
+          const uint32_t xa = __builtin_amdgcn_readlane(ga, src);
+          const uint32_t off = __builtin_amdgcn_readlane(e_off, src);
+          const uint32_t cnt = __builtin_amdgcn_readlane(e_cnt, src);
+          const uint32_t via = __builtin_amdgcn_readlane(hn, src);
+          const uint32_t moff = mg_moff[wv][xa], mrow = mg_row[wv][xa], gi = mg_gi[wv][xa];
           for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
-            bool own = false;
-            uint32_t k = 0;
-            if (c0 + lane < cnt) {
-              k = a.ix.plist[off + c0 + lane] - w0;
-              if (k < wn) {
-                const uint32_t bit = 1u << (k & 31);
-                own = !(atomicOr(&bm[wv][k >> 5], bit) & bit);
-              }
-            }
-            const uint64_t bo = __ballot(own);
-            if (own) tlist[wv][nt + prefix_before(bo)] = w0 + k;
-            nt += __popcll(bo);
-            if (nt + 64 > kTList) drain();
-          }
-        }
-        if (nt) drain();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        // Stream the window: everything not marked goes straight to client rows. Four
-        // 64-record chunks in flight; loads are unconditional (see copy_lists).
-        for (uint32_t i0 = 0; i0 < wn; i0 += 256) {
-          wp_chunks++;
-          SubRec rr[4];
-#pragma unroll
-          for (int u = 0; u < 4; u++) rr[u] = ms[w0 + min(i0 + u * 64 + lane, wn - 1)];
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            const uint32_t k = i0 + u * 64 + lane;
-            const bool v = k < wn && !((bm[wv][min(k, wn - 1) >> 5] >> (k & 31)) & 1);
-            const uint64_t bd = __ballot(v);
-            if (v)
-              __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(&rr[u]),
-                                          reinterpret_cast<u32x4*>(rows + n_cli + prefix_before(bd)));
-            n_cli += __popcll(bd);
+            const bool act = c0 + lane < cnt;
+            const uint32_t k = act ? a.ix.plist[off + c0 + lane] : 0u;
+            resolve(act, moff + k, mrow + k, gi, via);
+            st_recs += min(64u, cnt - c0);
           }
         }
       }
-    }
-    if (wp) wp_merge += clock64() - wp_m;
-  }
-
-  if (tab_ready) {  // write back merged Qos/NoLocal of bases that absorbed later matches
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t k = lane; k <= tmask; k += 64) {
-      if (tk_load(k) != kTabEmpty) {
-        const uint32_t m = tm_load(k);
-        if (m & kMetaDirty) rows[tr_load(k)].meta = m & ~kMetaDirty;
+    } else {
+      // Too many merge gathers for the pair analysis: resolve every may-merge record.
+      st_slow = 1;
+      for (uint32_t i = 0; i < n_g; i++) {
+        const GDesc d = gd[i];
+        if (!(d.word & kGatherSubs)) continue;
+        const NodeLists L = a.ix.lists[d.word & kGatherNode];
+        for (uint32_t c0 = 0; c0 < L.n_merge; c0 += 64) {
+          const bool act = c0 + lane < L.n_merge;
+          resolve(act, L.sub_off + L.n_direct + c0 + lane, d.r_pos + L.n_direct + c0 + lane, i, kNone);
+          st_recs += min(64u, L.n_merge - c0);
+        }
       }
     }
   }
 
-  if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t n_inl = (uint32_t)(o1.inl - o0.inl);
+  if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675); rows from k_copy
     InlRec* __restrict__ ir = a.inl_rows + ib;
     uint32_t kept = 0;
     for (uint32_t i0 = 0; i0 < n_inl; i0 += 64) {
@@ -784,17 +650,21 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   if (lane == 0) {
     mq_topic_result_dev res;
     res.sub_base = rb;
-    res.shared_base = sb;
+    res.shared_base = o0.shr - a.base.shr;
     res.inline_base = ib;
     res.sub_cap = cap;
-    res.n_client = n_cli;
+    res.n_client = cap - n_nonbase;
     res.n_ident = n_ext;
-    res.n_shared = n_shr;
+    res.n_shared = (uint32_t)(o1.shr - o0.shr);
     res.n_inline = n_inl;
     res.reserved = 0;
     a.res[t - a.t0] = res;
+    if (a.stats && (st_hits | st_recs | st_slow)) {  // diagnosis only (MQ_MERGE_STATS)
+      atomicAdd(a.stats + 0, (unsigned long long)st_hits);
+      atomicAdd(a.stats + 1, (unsigned long long)st_recs);
+      atomicAdd(a.stats + 2, (unsigned long long)st_slow);
+    }
   }
-  wp_flush(tab_recs);
 }
 
 }  // namespace mq
@@ -820,10 +690,22 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
   hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(256), 0, s, cnt, n, bpre, off);
 }
 
-void launch_emit(const EmitArgs& a, hipStream_t s) {
-  const uint32_t waves = a.list ? a.n_list : (a.t1 > a.t0 ? a.t1 - a.t0 : 0);
+void launch_desc(const EmitArgs& a, hipStream_t s) {
+  const uint32_t n = a.t1 - a.t0;
+  if (!n) return;
+  hipLaunchKernelGGL(k_desc, dim3((n + 255) / 256), dim3(256), 0, s, a);
+}
+
+void launch_copy(const EmitArgs& a, hipStream_t s) {
+  const uint32_t waves = a.n_tiles[0] + a.n_tiles[1] + a.n_tiles[2];
   if (!waves) return;
-  hipLaunchKernelGGL(k_emit, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_copy, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+}
+
+void launch_merge(const EmitArgs& a, hipStream_t s) {
+  const uint32_t waves = a.t1 - a.t0;
+  if (!waves) return;
+  hipLaunchKernelGGL(k_merge, dim3((waves + 3) / 4), dim3(256), 0, s, a);
 }
 
 

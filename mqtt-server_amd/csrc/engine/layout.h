@@ -131,14 +131,29 @@ struct SubRec {  // == mq_client_row
   uint32_t client;
   uint32_t filter_id;
   int32_t ident;
-  uint32_t meta;  // qos | nolocal<<8 | rap<<9 | rh<<10
+  uint32_t meta;  // qos | nolocal<<8 | rap<<9 | rh<<10 | row kind (output rows only)
 };
-// Pair routing of may-merge subscriptions. A may-merge subscription needs the per-topic merge
-// table only when its client has another subscription gathered for the same topic. For a node
-// g, the pair block maps each partner node h (a node holding another co-matchable
-// subscription of one of g's may-merge clients) to the list of g's may-merge slots, relative
-// k in [0, n_merge), whose client also subscribes at h. A topic probes (g, h) only for pairs
-// of nodes it gathers; the slots on the hit lists are exactly its table-bound records.
+// Partner links of may-merge subscriptions. A may-merge subscription (client c at node g)
+// has partners: the other non-shared subscriptions of c whose filters can match one topic
+// together with g's (Index::compatible). For the slot at subs pool position pos,
+// mref[pos] = {off, cnt} names its partners mpart[off, off + cnt), each the partner's node and
+// pool position. For a topic, the partners that are gathered decide the record alone:
+// none -> a plain client row; all gathered later -> the merge base (client row with the
+// partners' max Qos and OR'd NoLocal); one gathered earlier -> a non-base entry (an ident row
+// when its identifier is > 0). That is gatherSubscriptions + Subscription.Merge
+// (topics.go:631-648, packets/packets.go:254-274) without a per-topic table.
+struct MergeRef {  // 8 B, parallel to the subs pool
+  uint32_t off, cnt;
+};
+struct MergePart {  // 8 B
+  uint32_t node, pos;
+};
+// Pair blocks find a topic's merging records without touching the others. For a node g, the
+// block maps each partner node h (a node holding a partner of one of g's may-merge
+// subscriptions) to the list of g's may-merge slots, relative k in [0, n_merge), whose client
+// also subscribes at h. A topic probes (g, h) only for pairs of nodes it gathers; the slots on
+// the hit lists are exactly the records whose client has another match for the topic. Every
+// other record is its client's only match and stays a plain client row.
 struct NodePair {   // per node (16 B)
   uint32_t ent_off;   // PairEnt hash table (ent_mask + 1 entries, linear probing)
   uint32_t ent_mask;  // kNone: the node has no may-merge slots
@@ -174,6 +189,8 @@ constexpr uint32_t kMetaQos = 0x3u;
 constexpr uint32_t kMetaNoLocal = 0x100u;
 constexpr uint32_t kMetaRap = 0x200u;
 constexpr uint32_t kMetaRhShift = 10;
+constexpr uint32_t kRowIdent = 1u << 30;  // == MQ_ROW_IDENT
+constexpr uint32_t kRowDrop = 1u << 31;   // == MQ_ROW_DROP
 
 // Gather word written by the walk: node | kGatherSubs | kGatherInline.
 constexpr uint32_t kGatherNode = 0x3FFFFFFFu;
@@ -181,8 +198,9 @@ constexpr uint32_t kGatherSubs = 1u << 30;    // gather non-shared subscriptions
 constexpr uint32_t kGatherInline = 1u << 31;  // gather inline subscriptions
 
 // Per-topic counts from the walk (count pass), exclusive-scanned into offsets.
+// rows = non-shared records of the gathers (one output row each); merge = the may-merge ones.
 struct TopicCount {
-  uint32_t gathers, rows, shared, inlines, table;
+  uint32_t gathers, rows, shared, inlines, merge;
 };
 
 }  // namespace mq

@@ -113,19 +113,20 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::st
   for (size_t t = 0; t < topics.size(); t++) {
     const mq_topic_result& tr = r->topics[t];
     Subscribers& s = out[t];
-    for (uint32_t i = 0; i < tr.n_client; i++) {  // client rows: merged Subscription
+    // rows in gather order: a client's client row precedes its ident rows
+    for (uint32_t i = 0; i < tr.sub_cap; i++) {
       const mq_client_row& row = r->sub_rows[tr.sub_base + i];
-      Subscription sub = stored_.at({row.client_id, row.filter_id});
-      sub.Qos = row.meta & MQ_META_QOS_MASK;
-      sub.NoLocal = (row.meta & MQ_META_NOLOCAL) != 0;
-      sub.HasIdentifiers = true;
-      sub.Identifiers = {{sub.Filter, sub.Identifier}};
-      s.Subscriptions[clients_[row.client_id]] = sub;
-    }
-    const uint64_t end = tr.sub_base + tr.sub_cap;
-    for (uint32_t i = 0; i < tr.n_ident; i++) {  // ident rows: further Identifiers entries
-      const mq_ident_row& row = reinterpret_cast<const mq_ident_row&>(r->sub_rows[end - 1 - i]);
-      s.Subscriptions[clients_[row.client_id]].Identifiers[filters_[row.filter_id]] = row.identifier;
+      const uint32_t kind = row.meta & MQ_ROW_KIND_MASK;
+      if (kind == 0) {  // client row: merged Subscription
+        Subscription sub = stored_.at({row.client_id, row.filter_id});
+        sub.Qos = row.meta & MQ_META_QOS_MASK;
+        sub.NoLocal = (row.meta & MQ_META_NOLOCAL) != 0;
+        sub.HasIdentifiers = true;
+        sub.Identifiers = {{sub.Filter, sub.Identifier}};
+        s.Subscriptions[clients_[row.client_id]] = sub;
+      } else if (kind == MQ_ROW_IDENT) {  // further Identifiers entry
+        s.Subscriptions[clients_[row.client_id]].Identifiers[filters_[row.filter_id]] = row.identifier;
+      }
     }
     for (uint32_t i = 0; i < tr.n_shared; i++) {
       const mq_shared_row& row = r->shared_rows[tr.shared_base + i];

@@ -241,17 +241,19 @@ func (x *TopicsIndex) SubscribersBatch(topics []string) []*Subscribers {
 			Subscriptions:       map[string]packets.Subscription{},
 			InlineSubscriptions: map[int]InlineSubscription{},
 		}
-		for _, cr := range rows[t.sub_base : t.sub_base+C.uint64_t(t.n_client)] {
-			base := x.stored[subKey{uint32(cr.client_id), uint32(cr.filter_id)}]
-			base.Qos = byte(cr.meta & C.MQ_META_QOS_MASK)
-			base.NoLocal = cr.meta&C.MQ_META_NOLOCAL != 0
-			base.Identifiers = map[string]int{base.Filter: base.Identifier}
-			s.Subscriptions[x.clients.strs[cr.client_id]] = base
-		}
-		end := t.sub_base + C.uint64_t(t.sub_cap)
-		for _, ir := range rows[end-C.uint64_t(t.n_ident) : end] {
-			sub := s.Subscriptions[x.clients.strs[ir.client_id]]
-			sub.Identifiers[x.filters.strs[ir.filter_id]] = int(ir.identifier)
+		// rows in gather order: a client's client row precedes its ident rows
+		for _, cr := range rows[t.sub_base : t.sub_base+C.uint64_t(t.sub_cap)] {
+			switch cr.meta & C.MQ_ROW_KIND_MASK {
+			case 0: // client row: the merged Subscription
+				base := x.stored[subKey{uint32(cr.client_id), uint32(cr.filter_id)}]
+				base.Qos = byte(cr.meta & C.MQ_META_QOS_MASK)
+				base.NoLocal = cr.meta&C.MQ_META_NOLOCAL != 0
+				base.Identifiers = map[string]int{base.Filter: base.Identifier}
+				s.Subscriptions[x.clients.strs[cr.client_id]] = base
+			case C.MQ_ROW_IDENT: // a further Identifiers entry of that client
+				sub := s.Subscriptions[x.clients.strs[cr.client_id]]
+				sub.Identifiers[x.filters.strs[cr.filter_id]] = int(cr.identifier)
+			}
 		}
 		for _, sr := range shared[t.shared_base : t.shared_base+C.uint64_t(t.n_shared)] {
 			f, c := x.filters.strs[sr.filter_id], x.clients.strs[sr.client_id]

@@ -72,7 +72,7 @@ EXPORTS = [
     "mq_retained_delete", "mq_retained_len", "mq_subscribe_bulk", "mq_retain_bulk",
     "mq_match_batch", "mq_match_device", "mq_match_chunks", "mq_messages_batch",
     "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
-    "mq_profile_read", "mq_profile_reset",
+    "mq_profile_read", "mq_profile_reset", "mq_index_check",
 ]
 
 _LIB = None
@@ -117,6 +117,7 @@ def lib():
         "mq_result_free": (None, [vp]),
         "mq_sync": (C.c_int, [vp, vp]),
         "mq_index_stats": (C.c_int, [vp, C.POINTER(Stats)]),
+        "mq_index_check": (C.c_int, [vp]),
         "mq_profile_enable": (C.c_int, [vp, C.c_int]),
         "mq_profile_read": (C.c_int, [vp, C.POINTER(KernelTime), C.c_uint32]),
         "mq_profile_reset": (C.c_int, [vp]),
@@ -298,6 +299,10 @@ class Engine:
     def sync(self, stream=None):
         _check(lib().mq_sync(self.h, stream), "mq_sync")
 
+    def check(self):
+        """mq_index_check: host-side invariants of the device-bound image (raises on violation)."""
+        _check(lib().mq_index_check(self.h), "mq_index_check")
+
     def stats(self):
         s = Stats()
         _check(lib().mq_index_stats(self.h, C.byref(s)), "mq_index_stats")
@@ -384,13 +389,20 @@ class Engine:
         _check(lib().mq_profile_reset(self.h), "mq_profile_reset")
 
 
+ROW_IDENT = 0x40000000  # MQ_ROW_IDENT (include/mqmatch.h)
+ROW_DROP = 0x80000000   # MQ_ROW_DROP
+ROW_KIND_MASK = 0xC0000000
+
+
 def topic_rows(res, t):
-    """Row views of topic t from a match_batch() dict."""
+    """Row views of topic t from a match_batch() dict: (client rows, ident rows, shared rows,
+    inline rows). Client and ident rows are picked out of the topic's row region by kind."""
     b, cap = int(res["sub_base"][t]), int(res["sub_cap"][t])
-    nc, ni = int(res["n_client"][t]), int(res["n_ident"][t])
     sb, ns = int(res["shared_base"][t]), int(res["n_shared"][t])
     ib, nl = int(res["inline_base"][t]), int(res["n_inline"][t])
-    return (res["rows"][b:b + nc], res["rows"][b + cap - ni:b + cap],
+    region = res["rows"][b:b + cap]
+    kind = region[:, 3] & ROW_KIND_MASK
+    return (region[kind == 0], region[kind == ROW_IDENT],
             res["shared"][sb:sb + ns], res["inline"][ib:ib + nl])
 
 

@@ -51,18 +51,26 @@ def engine_digests(res):
     rows = res["rows"].astype(np.uint64)
     base, cap = res["sub_base"].astype(np.int64), res["sub_cap"].astype(np.int64)
     nc, ni = res["n_client"].astype(np.int64), res["n_ident"].astype(np.int64)
-    ci = _ranges(base, nc)
-    ii = _ranges(base + cap - ni, ni)
+    # every gathered record leaves one row in [base, base + cap): client rows (kind 0), ident
+    # rows (MQ_ROW_IDENT) and dropped rows (MQ_ROW_DROP), in gather order
+    ri = _ranges(base, cap)
+    kind = rows[ri, 3] >> np.uint64(30)
+    zero = np.uint64(0)
+    hc = np.where(kind == 0, row_hash(1, rows[ri, 0], rows[ri, 1], rows[ri, 2], rows[ri, 3]), zero)
+    hi = np.where(kind == 1, row_hash(2, rows[ri, 0], rows[ri, 1], rows[ri, 2], 0), zero)
+    k_c = _seg_sums((kind == 0).astype(np.uint64), cap)
+    k_i = _seg_sums((kind == 1).astype(np.uint64), cap)
+    assert (k_c == nc.astype(np.uint64)).all() and (k_i == ni.astype(np.uint64)).all(), \
+        "row kinds disagree with n_client / n_ident"
     si = _ranges(res["shared_base"].astype(np.int64), res["n_shared"].astype(np.int64))
     li = _ranges(res["inline_base"].astype(np.int64), res["n_inline"].astype(np.int64))
-    hc = row_hash(1, rows[ci, 0], rows[ci, 1], rows[ci, 2], rows[ci, 3])
-    hi = row_hash(2, rows[ii, 0], rows[ii, 1], rows[ii, 2], 0)
     sh = res["shared"].astype(np.uint64)
     hs = row_hash(3, sh[si, 0], sh[si, 1], 0, 0)
     il = res["inline"].astype(np.uint64)
     hl = row_hash(4, il[li, 0], il[li, 1], 0, 0)
     d = np.full(n, SEED, np.uint64)
     counts = np.stack([nc, ni, res["n_shared"].astype(np.int64), res["n_inline"].astype(np.int64)], 1)
-    for k, h in enumerate((hc, hi, hs, hl)):
-        d = fold(fold(d, counts[:, k].astype(np.uint64)), _seg_sums(h, counts[:, k]))
+    sums = (_seg_sums(hc, cap), _seg_sums(hi, cap), _seg_sums(hs, counts[:, 2]), _seg_sums(hl, counts[:, 3]))
+    for k in range(4):
+        d = fold(fold(d, counts[:, k].astype(np.uint64)), sums[k])
     return d, counts.astype(np.uint32)

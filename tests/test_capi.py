@@ -27,7 +27,7 @@ def test_library_exports_all_symbols():
     L = E.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.mq_abi_version() == 1
+    assert L.mq_abi_version() == 2
 
 
 def test_errors_are_reported():
@@ -87,6 +87,7 @@ def test_update_semantics_match_oracle(seed):
         assert eng.retained_len() == orc.retained_len()
         if step % 50 == 0:
             assert eng.stats()["nodes"] == orc.particle_count(), step
+            eng.check()
     st = eng.stats()
     assert st["nodes"] == orc.particle_count()
     assert (st["partners"] == 0) == (st["subs_merge"] == 0)
@@ -100,7 +101,9 @@ def test_partner_links_symmetric():
         eng.subscribe(f, 7, i, 0, 0, 0)
     st = eng.stats()
     assert st["subs_merge"] == 3 and st["partners"] == 6
+    eng.check()
     eng.unsubscribe("a/#", 7)
+    eng.check()
     st = eng.stats()
     assert st["subs_merge"] == 2 and st["partners"] == 2  # a/b ~ a/+ remain partners
     eng.unsubscribe("a/+", 7)
@@ -119,6 +122,28 @@ def test_bulk_subscribe_matches_oracle():
     st = eng.stats()
     assert st["nodes"] == orc.particle_count()
     assert st["subs"] + st["shared"] == int(a.sum())
+    eng.check()
+
+
+def test_partner_links_survive_churn():
+    """Random unsubscribe / resubscribe churn on a workload index: after every round the
+    device partner links name each partner's current slot (mq_index_check)."""
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(20000, 600, seed=9)  # ~33 filters per client: many partners
+    eng = E.Engine()
+    eng.subscribe_bulk(w)
+    eng.check()
+    fs = W.strings(w["bytes"], w["offs"])
+    r = random.Random(10)
+    for _ in range(4):
+        for _ in range(1500):
+            i = r.randrange(len(fs))
+            if r.random() < 0.5:
+                eng.unsubscribe(fs[i], int(w["client_ids"][i]))
+            else:
+                eng.subscribe(fs[i], r.randrange(600), int(w["filter_ids"][i]), 1, 0, 3)
+        eng.check()
+    assert eng.stats()["subs_merge"] > 0
 
 
 def test_unsubscribe_everything_empties_trie():

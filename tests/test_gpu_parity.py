@@ -293,9 +293,9 @@ def test_gather_slot_overflow(gpu_available):
         assert g == o.subscribers(t), t
 
 
-def test_merge_table_overflow_pass(gpu_available):
-    """> 384 clients each with two co-matching filters in one topic: the LDS merge table would
-    overflow, so the topic is re-emitted by the global-table pass."""
+def test_many_merging_clients(gpu_available):
+    """600 clients each with three co-matching filters in one topic (bases, max Qos, ident rows),
+    next to clients whose partners are not gathered for the topic (plain rows)."""
     e, o = EngineAdapter(), OracleAdapter()
     for i in range(600):
         c = f"m{i}"
@@ -307,6 +307,25 @@ def test_merge_table_overflow_pass(gpu_available):
         e.subscribe(f"s{i}", "o/#")
         o.subscribe(f"s{i}", "o/#")
     topics = ["o/p", "o/q", "o", "o/z", "o/p/x"]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
+
+
+def test_partner_map_fallback(gpu_available):
+    """Topics gathering 256 (LDS map) and 512 (> map capacity: linear partner lookup) nodes
+    that all hold may-merge subscriptions: every literal/'+' path of depth 8 and 9."""
+    import itertools
+    e, o = EngineAdapter(), OracleAdapter()
+    for depth in (8, 9):
+        paths = ["/".join(f"a{i}" if b == 0 else "+" for i, b in enumerate(bits))
+                 for bits in itertools.product((0, 1), repeat=depth)]
+        for k, f in enumerate(paths):  # client k holds paths k and k + 1: partners pairwise
+            for g in (f, paths[(k + 1) % len(paths)]):
+                c = f"d{depth}c{k}"
+                kw = dict(qos=(k + len(g)) % 3, identifier=(k % 4) * 7, no_local=k % 5 == 0)
+                assert e.subscribe(c, g, **kw) == o.subscribe(c, g, **kw)
+    topics = ["/".join(f"a{i}" for i in range(9)), "/".join(f"a{i}" for i in range(8)),
+              "/".join(f"a{i}" for i in range(8)) + "/x", "a0/a1"]
     for t, g in zip(topics, e.subscribers_batch(topics)):
         assert g == o.subscribers(t), t
 
