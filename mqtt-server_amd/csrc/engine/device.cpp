@@ -156,10 +156,16 @@ Device::~Device() {
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
-  for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                    &shr_rows_, &inl_rows_, &res_, &err_, &desc_, &tiles_, &msg_handles_, &msg_base_,
-                    &msg_count_, &gslots_, &mstats_})
+  for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &desc_,
+                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_})
     b->release();
+  for (int k = 0; k < 2; k++) {
+    for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &tiles_[k]}) b->release();
+    if (copy_done_[k]) (void)hipEventDestroy(copy_done_[k]);
+    if (merge_done_[k]) (void)hipEventDestroy(merge_done_[k]);
+  }
+  if (side_done_) (void)hipEventDestroy(side_done_);
+  if (side_) (void)hipStreamDestroy(side_);
 }
 
 uint64_t Device::device_bytes() const {
@@ -168,10 +174,11 @@ uint64_t Device::device_bytes() const {
                seginfo_.cap * sizeof(SegInfo) + segbytes_.cap + subs_.cap * sizeof(SubRec) +
                shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4 +
                mref_.cap * sizeof(MergeRef) + mpart_.cap * sizeof(MergePart) +
-               npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * 4;
-  for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &rows_,
-                          &shr_rows_, &inl_rows_, &res_, &desc_, &tiles_})
+               npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * sizeof(PairSlot);
+  for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &desc_})
     b += x->bytes;
+  for (int k = 0; k < 2; k++)
+    for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &tiles_[k]}) b += x->bytes;
   return b;
 }
 
@@ -332,12 +339,23 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   }
   if (max_rows >= (1ull << 32) || max_shr >= (1ull << 32) || max_inl >= (1ull << 32))
     throw HipError{hipErrorInvalidValue, "one scan block's output exceeds 2^32 rows"};
-  rows_.ensure(max_rows * sizeof(SubRec));
-  shr_rows_.ensure(max_shr * sizeof(ShrRec));
-  inl_rows_.ensure(max_inl * sizeof(InlRec));
-  res_.ensure(max_topics * sizeof(mq_topic_result_dev));
+  const size_t nbuf = chunks.size() > 1 ? 2 : 1;
+  for (size_t k = 0; k < nbuf; k++) {
+    rows_[k].ensure(max_rows * sizeof(SubRec));
+    shr_rows_[k].ensure(max_shr * sizeof(ShrRec));
+    inl_rows_[k].ensure(max_inl * sizeof(InlRec));
+    res_[k].ensure(max_topics * sizeof(mq_topic_result_dev));
+    tiles_[k].ensure(max_tiles * sizeof(uint32_t));
+  }
   desc_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
-  tiles_.ensure(max_tiles * sizeof(uint32_t));
+  if (!side_) {
+    hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate");
+    for (int k = 0; k < 2; k++) {
+      hip_check(hipEventCreateWithFlags(&copy_done_[k], hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&merge_done_[k], hipEventDisableTiming), "hipEventCreate");
+    }
+    hip_check(hipEventCreateWithFlags(&side_done_, hipEventDisableTiming), "hipEventCreate");
+  }
 
   if (host) {
     host->topics.resize(n);
@@ -346,7 +364,11 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     host->inl.resize(tot.inl);
   }
 
-  for (const Chunk& c : chunks) {
+  // Per chunk: k_desc + k_copy on the launch stream, then k_merge (and, for host results, the
+  // D2H copies) on the side stream. Chunk i + 2 reuses chunk i's buffers after its merge.
+  for (size_t ci = 0; ci < chunks.size(); ci++) {
+    const Chunk& c = chunks[ci];
+    const size_t b = ci % nbuf;
     const TopicOff& lo = h_bpre_[c.b0];
     const TopicOff& hi = h_bpre_[c.b1];
     EmitArgs a;
@@ -358,15 +380,15 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     a.gathers = gathers;
     a.gather_stride = gstride;
     a.desc = desc_.as<GDesc>();
-    a.tiles = tiles_.as<uint32_t>();
+    a.tiles = tiles_[b].as<uint32_t>();
     a.total[0] = (uint32_t)(hi.rows - lo.rows);
     a.total[1] = (uint32_t)(hi.shr - lo.shr);
     a.total[2] = (uint32_t)(hi.inl - lo.inl);
     for (int k = 0; k < 3; k++) a.n_tiles[k] = (uint32_t)tiles_of(a.total[k]);
-    a.rows = rows_.as<SubRec>();
-    a.shr_rows = shr_rows_.as<ShrRec>();
-    a.inl_rows = inl_rows_.as<InlRec>();
-    a.res = res_.as<mq_topic_result_dev>();
+    a.rows = rows_[b].as<SubRec>();
+    a.shr_rows = shr_rows_[b].as<ShrRec>();
+    a.inl_rows = inl_rows_[b].as<InlRec>();
+    a.res = res_[b].as<mq_topic_result_dev>();
     a.stats = nullptr;
     if (merge_stats_) {
       if (!mstats_.p) {
@@ -375,6 +397,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       }
       a.stats = mstats_.as<unsigned long long>();
     }
+    if (ci >= nbuf) hip_check(hipStreamWaitEvent(s, merge_done_[b], 0), "hipStreamWaitEvent");
     prof.begin(s);
     launch_desc(a, s);
     prof.end("desc", s);
@@ -383,47 +406,60 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     launch_copy(a, s);
     prof.end("copy", s);
     hip_check(hipGetLastError(), "k_copy");
-    prof.begin(s);
-    launch_merge(a, s);
-    prof.end("merge", s);
+    hip_check(hipEventRecord(copy_done_[b], s), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
+    prof.begin(side_);
+    launch_merge(a, side_);
+    prof.end("merge", side_);
     hip_check(hipGetLastError(), "k_merge");
     prof.count("copy_rows", (uint64_t)a.total[0] + a.total[1] + a.total[2]);
     prof.count("copy_bytes", 16ull * a.total[0] + 8ull * a.total[1] + 8ull * a.total[2]);
     prof.count("merge_records", hi.merge - lo.merge);
     last_chunks_++;
-    if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
-      unsigned long long m[4];
-      hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, s), "D2H stats");
-      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-      fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
-    }
 
     const uint32_t nt = a.t1 - a.t0;
     if (host) {
-      hip_check(hipMemcpyAsync(host->rows.data() + lo.rows, rows_.p, (hi.rows - lo.rows) * sizeof(SubRec),
-                               hipMemcpyDeviceToHost, s), "D2H rows");
-      hip_check(hipMemcpyAsync(host->shr.data() + lo.shr, shr_rows_.p, (hi.shr - lo.shr) * sizeof(ShrRec),
-                               hipMemcpyDeviceToHost, s), "D2H shared rows");
-      hip_check(hipMemcpyAsync(host->inl.data() + lo.inl, inl_rows_.p, (hi.inl - lo.inl) * sizeof(InlRec),
-                               hipMemcpyDeviceToHost, s), "D2H inline rows");
-      hip_check(hipMemcpyAsync(host->topics.data() + a.t0, res_.p, nt * sizeof(mq_topic_result),
-                               hipMemcpyDeviceToHost, s), "D2H topic results");
-      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-      for (uint32_t i = 0; i < nt; i++) {
-        mq_topic_result& r = host->topics[a.t0 + i];
+      hip_check(hipMemcpyAsync(host->rows.data() + lo.rows, a.rows, (hi.rows - lo.rows) * sizeof(SubRec),
+                               hipMemcpyDeviceToHost, side_), "D2H rows");
+      hip_check(hipMemcpyAsync(host->shr.data() + lo.shr, a.shr_rows, (hi.shr - lo.shr) * sizeof(ShrRec),
+                               hipMemcpyDeviceToHost, side_), "D2H shared rows");
+      hip_check(hipMemcpyAsync(host->inl.data() + lo.inl, a.inl_rows, (hi.inl - lo.inl) * sizeof(InlRec),
+                               hipMemcpyDeviceToHost, side_), "D2H inline rows");
+      hip_check(hipMemcpyAsync(host->topics.data() + a.t0, a.res, nt * sizeof(mq_topic_result),
+                               hipMemcpyDeviceToHost, side_), "D2H topic results");
+    }
+    hip_check(hipEventRecord(merge_done_[b], side_), "hipEventRecord");
+    if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
+      unsigned long long m[4];
+      hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, side_), "D2H stats");
+      hip_check(hipStreamSynchronize(side_), "hipStreamSynchronize");
+      fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
+    }
+    out->n_topics = nt;
+    out->topics = reinterpret_cast<const mq_topic_result*>(a.res);
+    out->sub_rows = reinterpret_cast<const mq_client_row*>(a.rows);
+    out->shared_rows = reinterpret_cast<const mq_shared_row*>(a.shr_rows);
+    out->inline_rows = reinterpret_cast<const mq_inline_row*>(a.inl_rows);
+    out->n_sub_rows = hi.rows - lo.rows;
+    out->n_shared_rows = hi.shr - lo.shr;
+    out->n_inline_rows = hi.inl - lo.inl;
+  }
+  // the launch stream completes only after the side stream's work of this batch
+  hip_check(hipEventRecord(side_done_, side_), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(s, side_done_, 0), "hipStreamWaitEvent");
+  if (host) {
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    for (const Chunk& c : chunks) {
+      const TopicOff& lo = h_bpre_[c.b0];
+      const uint32_t t0 = c.b0 * kScanBlock, t1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)c.b1 * kScanBlock);
+      for (uint32_t t = t0; t < t1; t++) {
+        mq_topic_result& r = host->topics[t];
         r.sub_base += lo.rows;
         r.shared_base += lo.shr;
         r.inline_base += lo.inl;
       }
     }
-    out->n_topics = nt;
-    out->topics = res_.as<mq_topic_result>();
-    out->sub_rows = rows_.as<mq_client_row>();
-    out->shared_rows = shr_rows_.as<mq_shared_row>();
-    out->inline_rows = inl_rows_.as<mq_inline_row>();
-    out->n_sub_rows = hi.rows - lo.rows;
-    out->n_shared_rows = hi.shr - lo.shr;
-    out->n_inline_rows = hi.inl - lo.inl;
+    check_err(s);
   }
 }
 
@@ -493,6 +529,7 @@ template struct DevMirror<MergeRef>;
 template struct DevMirror<MergePart>;
 template struct DevMirror<NodePair>;
 template struct DevMirror<PairEnt>;
+template struct DevMirror<PairSlot>;
 template struct DevMirror<ShrRec>;
 template struct DevMirror<InlRec>;
 template struct DevMirror<uint32_t>;

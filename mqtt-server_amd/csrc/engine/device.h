@@ -126,13 +126,18 @@ class Device {
   DevMirror<MergePart> mpart_;
   DevMirror<NodePair> npair_;
   DevMirror<PairEnt> pent_;
-  DevMirror<uint32_t> plist_;
+  DevMirror<PairSlot> plist_;
   DevMirror<ShrRec> shr_;
   DevMirror<InlRec> inl_;
   DevMirror<uint32_t> children_;
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
-  DevBuf rows_, shr_rows_, inl_rows_, res_, err_, desc_, tiles_;
+  // Output chunks alternate between two buffer sets so that k_merge of chunk i (side stream)
+  // overlaps k_desc/k_copy of chunk i + 1 (launch stream).
+  DevBuf rows_[2], shr_rows_[2], inl_rows_[2], res_[2], tiles_[2];
+  DevBuf err_, desc_;
+  hipStream_t side_ = nullptr;
+  hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_, mstats_;
   bool merge_stats_ = false;  // MQ_MERGE_STATS: k_merge work counters to stderr
   std::vector<TopicOff> h_bpre_;

@@ -208,7 +208,7 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   mpart.m.grow_to(1, MergePart{kNone, 0});
   npair.grow_to(1, NodePair{0, kNone, 0, 0});
   pent.m.grow_to(1, PairEnt{kNone, 0, 0, 0});
-  plist.m.grow_to(1, 0);
+  plist.m.grow_to(1, PairSlot{0, 0, 0, 0});
 }
 
 // ---- edge table -------------------------------------------------------------------------------
@@ -474,7 +474,7 @@ void Index::flush_merge() {
         uint32_t mp = kNone;
         if (!sub_pos_.get((uint64_t)m << 32 | client, &mp))  // partners are symmetric
           throw std::logic_error("flush_merge: partner subscription missing");
-        mpart.m.at_w(at++) = MergePart{m, mp};
+        mpart.m.at_w(at++) = MergePart{m, subs.m.h[mp].meta & (kMetaQos | kMetaNoLocal)};
       }
     }
     nh_[n].mpart_off = off;
@@ -496,7 +496,10 @@ void Index::flush_merge() {
     while (lcap < hk.size()) lcap <<= 1;
     const uint32_t eo = pent.alloc(ecap), lo = plist.alloc(lcap), mask = ecap - 1;
     for (uint32_t i = 0; i < ecap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
-    for (size_t i = 0; i < hk.size(); i++) plist.m.at_w(lo + i) = hk[i].second;
+    for (size_t i = 0; i < hk.size(); i++) {
+      const MergeRef r = mref.h[L.sub_off + L.n_direct + hk[i].second];
+      plist.m.at_w(lo + i) = PairSlot{hk[i].second, r.off, r.cnt, 0};
+    }
     for (size_t b = 0; b < hk.size();) {
       size_t e = b + 1;
       while (e < hk.size() && hk[e].first == hk[b].first) e++;
@@ -545,10 +548,12 @@ bool Index::check(std::string* why) {
         const MergePart mp = mpart.m.h[r.off + e];
         if (mp.node != parts.m.h[pl.off + e] || mp.node >= nh_.size() || !nh_[mp.node].live)
           return bad(at + ": partner node stale");
+        uint32_t ppos = kNone;
+        if (!sub_pos_.get((uint64_t)mp.node << 32 | client, &ppos)) return bad(at + ": partner missing");
         const NodeLists& M = lists.h[mp.node];
-        if (mp.pos < M.sub_off + M.n_direct || mp.pos >= M.sub_off + M.n_direct + M.n_merge)
-          return bad(at + ": partner position outside the partner's may-merge slots");
-        if (subs.m.h[mp.pos].client != client) return bad(at + ": partner position names another client");
+        if (ppos < M.sub_off + M.n_direct || ppos >= M.sub_off + M.n_direct + M.n_merge)
+          return bad(at + ": partner outside the partner's may-merge slots");
+        if (mp.meta != (subs.m.h[ppos].meta & (kMetaQos | kMetaNoLocal))) return bad(at + ": partner meta stale");
         if (!compatible(n, mp.node)) return bad(at + ": partner not co-matchable");
         // the pair block of n lists slot k under partner node mp.node
         const NodePair& P = npair.h[n];
@@ -559,7 +564,10 @@ bool Index::check(std::string* why) {
         const PairEnt& pe = pent.m.h[P.ent_off + sl];
         if (pe.h != mp.node) return bad(at + ": pair block misses a partner node");
         bool listed = false;
-        for (uint32_t i = 0; i < pe.cnt && !listed; i++) listed = plist.m.h[pe.off + i] == k - L.n_direct;
+        for (uint32_t i = 0; i < pe.cnt && !listed; i++) {
+          const PairSlot& ps = plist.m.h[pe.off + i];
+          listed = ps.k == k - L.n_direct && ps.mp_off == r.off && ps.mp_cnt == r.cnt;
+        }
         if (!listed) return bad(at + ": pair list misses a slot");
       }
     }
@@ -758,6 +766,8 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
   uint32_t pos;
   if (sub_pos_.get((uint64_t)n << 32 | client, &pos)) {
     subs.m.at_w(pos) = rec;
+    const PartList& p = subp_[pos];  // the partners' links carry this subscription's meta
+    for (uint32_t i = 0; i < p.cnt; i++) merge_dirty(parts.m.h[p.off + i]);
     return 0;
   }
   // Partners: the client's other subscriptions that could match the same topic (the merge

@@ -182,7 +182,7 @@ class Index {
   SlabPool<MergePart> mpart;  // pair blocks, rebuilt per node by flush_merge()
   Mirror<NodePair> npair;
   SlabPool<PairEnt> pent;
-  SlabPool<uint32_t> plist;
+  SlabPool<PairSlot> plist;
   SlabPool<ShrRec> shr;
   SlabPool<InlRec> inl;
   SlabPool<uint32_t> children;

@@ -10,8 +10,9 @@ namespace mq {
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
 constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves
-constexpr uint32_t kMapSlots = 512;    // per-wave LDS map (gathered merge node -> gather index)
+constexpr uint32_t kMapSlots = 256;    // per-wave LDS map (gathered merge node -> gather index)
 constexpr uint32_t kPairMax = 128;     // merge gathers covered by the pair analysis
+constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -27,7 +28,7 @@ struct DevIndex {
   const MergePart* mpart;
   const NodePair* npair;
   const PairEnt* pent;
-  const uint32_t* plist;
+  const PairSlot* plist;
   const ShrRec* shr;
   const InlRec* inl;
   const uint32_t* children;

@@ -440,12 +440,16 @@ __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
-  __shared__ uint32_t map_key[4][kMapSlots];  // gathered node with may-merge records
-  __shared__ uint32_t map_val[4][kMapSlots];  // its gather index (= DFS rank order)
-  __shared__ uint32_t mg_node[4][kPairMax];   // the topic's merge gathers, in gather order:
-  __shared__ uint32_t mg_gi[4][kPairMax];     //   node, gather index,
-  __shared__ uint32_t mg_moff[4][kPairMax];   //   subs pool offset of its may-merge slots,
-  __shared__ uint32_t mg_row[4][kPairMax];    //   output row of its first may-merge slot
+  __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records
+  __shared__ uint32_t map_val[4][kMapSlots];   // its gather index (= DFS rank order)
+  __shared__ uint32_t mg_node[4][kPairMax];    // the topic's merge gathers, in gather order:
+  __shared__ uint32_t mg_gi[4][kPairMax];      //   node, gather index,
+  __shared__ uint32_t mg_moff[4][kPairMax];    //   subs pool offset of its may-merge slots,
+  __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first may-merge slot
+  __shared__ uint32_t h_ga[4][kHitMax];        // staged hit lists: merge gather of g,
+  __shared__ uint32_t h_off[4][kHitMax];       //   pair-list offset,
+  __shared__ uint32_t h_via[4][kHitMax];       //   partner node h,
+  __shared__ uint32_t h_pre[4][kHitMax + 1];   //   exclusive prefix of their lengths (+ total)
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t t = a.t0 + blockIdx.x * 4 + wv;
   if (t >= a.t1) return;  // wave-uniform
@@ -482,12 +486,10 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
       }
       const uint64_t bi = __ballot(ins);
       const uint32_t x = n_map + prefix_before(bi);
-      if (ins && x < kMapSlots / 2) {
+      if (ins && x < kPairMax) {
         uint32_t sl = hash32(node) & (kMapSlots - 1);
         while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
         map_val[wv][sl] = i;
-      }
-      if (ins && x < kPairMax) {
         mg_node[wv][x] = node;
         mg_gi[wv][x] = i;
         mg_moff[wv][x] = moff;
@@ -496,9 +498,9 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
       n_map += __popcll(bi);
     }
     wave_sync_lds();
-    const bool scan_all = n_map > kMapSlots / 2;  // beyond the map: look partners up linearly
+    const bool slow = n_map > kPairMax;  // beyond the map: look partners up linearly
     auto gathered = [&](uint32_t h) -> uint32_t {  // gather index of node h, or kNone
-      if (!scan_all) {
+      if (!slow) {
         uint32_t sl = hash32(h) & (kMapSlots - 1);
         for (;;) {
           const uint32_t k = map_key[wv][sl];
@@ -515,23 +517,23 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
     };
 
     // Resolve one record whose client may have other matches for this topic: its partners that
-    // are gathered decide it (layout.h, MergeRef). An earlier one makes it a non-base entry:
+    // are gathered decide it (layout.h, MergePart). An earlier one makes it a non-base entry:
     // an Identifiers row when its identifier is > 0 (Subscription.Merge,
     // packets/packets.go:261-263), else dropped. Otherwise it is the base and takes the
     // partners' max Qos and OR'd NoLocal (packets/packets.go:265-271). A record may be reached
     // through several hit lists; every visit writes the same row, and only the visit through
     // its first gathered partner (`via`, or any when via == kNone) counts it.
-    auto resolve = [&](bool active, uint32_t pos, uint32_t row, uint32_t gi, uint32_t via) {
+    auto resolve = [&](bool active, uint32_t pos, uint32_t row, uint32_t gi, uint32_t via,
+                       uint32_t mp_off, uint32_t mp_cnt) {
       bool counted = false, nonbase = false;
       int32_t ident = 0;
       if (active) {
         const SubRec rec = a.ix.subs[pos];
-        const MergeRef mr = a.ix.mref[pos];
         bool bound = false, base = true;
         uint32_t first = kNone;
         uint32_t q = rec.meta & kMetaQos, nl = rec.meta & kMetaNoLocal;
-        for (uint32_t e = 0; e < mr.cnt; e++) {
-          const MergePart p = a.ix.mpart[mr.off + e];
+        for (uint32_t e = 0; e < mp_cnt; e++) {
+          const MergePart p = a.ix.mpart[mp_off + e];
           const uint32_t gh = gathered(p.node);
           if (gh == kNone) continue;
           if (!bound) first = p.node;
@@ -540,9 +542,8 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
             base = false;
             break;
           }
-          const uint32_t pm = a.ix.subs[p.pos].meta;
-          q = max(q, pm & kMetaQos);
-          nl |= pm & kMetaNoLocal;
+          q = max(q, p.meta & kMetaQos);
+          nl |= p.meta & kMetaNoLocal;
         }
         if (bound) {
           counted = via == kNone || via == first;
@@ -562,9 +563,29 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
       n_ext += __popcll(bx);
     };
 
-    if (n_map <= kPairMax) {
+    if (!slow) {
       // Pair analysis over ordered pairs (g, h) of merge gathers: g's pair block lists the slots
-      // whose client also subscribes at h. Every hit list is resolved by the whole wave.
+      // whose client also subscribes at h. Hit lists are staged in LDS and their concatenation
+      // is resolved 64 records per wave-instruction.
+      uint32_t n_hit = 0, tot = 0;
+      auto flush_hits = [&]() {
+        if (lane == 0) h_pre[wv][n_hit] = tot;
+        wave_sync_lds();
+        uint32_t jj = 0;
+        for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
+          const uint32_t r = r0 + lane;
+          const uint32_t rc = min(r, tot - 1);
+          while (h_pre[wv][jj + 1] <= rc) jj++;
+          const uint32_t xa = h_ga[wv][jj];
+          const PairSlot e = a.ix.plist[h_off[wv][jj] + (rc - h_pre[wv][jj])];
+          resolve(r < tot, mg_moff[wv][xa] + e.k, mg_row[wv][xa] + e.k, mg_gi[wv][xa], h_via[wv][jj],
+                  e.mp_off, e.mp_cnt);
+        }
+        st_recs += tot;
+        n_hit = 0;
+        tot = 0;
+        wave_sync_lds();
+      };
       const uint32_t np = n_map * n_map;
       for (uint32_t p0 = 0; p0 < np; p0 += 64) {
         const uint32_t p = p0 + lane;
@@ -592,24 +613,23 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
             }
           }
         }
-        uint64_t bh = __ballot(hit);
-        st_hits += __popcll(bh);
-        while (bh) {
-          const uint32_t src = (uint32_t)__builtin_ctzll(bh);
-          bh &= bh - 1;
-          const uint32_t xa = __builtin_amdgcn_readlane(ga, src);
-          const uint32_t off = __builtin_amdgcn_readlane(e_off, src);
-          const uint32_t cnt = __builtin_amdgcn_readlane(e_cnt, src);
-          const uint32_t via = __builtin_amdgcn_readlane(hn, src);
-          const uint32_t moff = mg_moff[wv][xa], mrow = mg_row[wv][xa], gi = mg_gi[wv][xa];
-          for (uint32_t c0 = 0; c0 < cnt; c0 += 64) {
-            const bool act = c0 + lane < cnt;
-            const uint32_t k = act ? a.ix.plist[off + c0 + lane] : 0u;
-            resolve(act, moff + k, mrow + k, gi, via);
-            st_recs += min(64u, cnt - c0);
-          }
+        const uint64_t bh = __ballot(hit);
+        const uint32_t nh = __popcll(bh);
+        st_hits += nh;
+        if (n_hit + nh > kHitMax) flush_hits();
+        uint32_t ct;
+        const uint32_t cp = wave_excl_scan(hit ? e_cnt : 0u, lane, &ct);
+        if (hit) {
+          const uint32_t x = n_hit + prefix_before(bh);
+          h_ga[wv][x] = ga;
+          h_off[wv][x] = e_off;
+          h_via[wv][x] = hn;
+          h_pre[wv][x] = tot + cp;
         }
+        n_hit += nh;
+        tot += ct;
       }
+      if (n_hit) flush_hits();
     } else {
       // Too many merge gathers for the pair analysis: resolve every may-merge record.
       st_slow = 1;
@@ -619,7 +639,9 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
         const NodeLists L = a.ix.lists[d.word & kGatherNode];
         for (uint32_t c0 = 0; c0 < L.n_merge; c0 += 64) {
           const bool act = c0 + lane < L.n_merge;
-          resolve(act, L.sub_off + L.n_direct + c0 + lane, d.r_pos + L.n_direct + c0 + lane, i, kNone);
+          const uint32_t pos = L.sub_off + L.n_direct + min(c0 + lane, L.n_merge - 1);
+          const MergeRef mr = a.ix.mref[pos];
+          resolve(act, pos, d.r_pos + L.n_direct + c0 + lane, i, kNone, mr.off, mr.cnt);
           st_recs += min(64u, L.n_merge - c0);
         }
       }

@@ -135,18 +135,19 @@ struct SubRec {  // == mq_client_row
 };
 // Partner links of may-merge subscriptions. A may-merge subscription (client c at node g)
 // has partners: the other non-shared subscriptions of c whose filters can match one topic
-// together with g's (Index::compatible). For the slot at subs pool position pos,
-// mref[pos] = {off, cnt} names its partners mpart[off, off + cnt), each the partner's node and
-// pool position. For a topic, the partners that are gathered decide the record alone:
-// none -> a plain client row; all gathered later -> the merge base (client row with the
-// partners' max Qos and OR'd NoLocal); one gathered earlier -> a non-base entry (an ident row
-// when its identifier is > 0). That is gatherSubscriptions + Subscription.Merge
-// (topics.go:631-648, packets/packets.go:254-274) without a per-topic table.
+// together with g's (Index::compatible). For a topic, the partners that are gathered decide
+// the record alone: none -> a plain client row; all gathered later -> the merge base (client
+// row with the partners' max Qos and OR'd NoLocal); one gathered earlier -> a non-base entry
+// (an ident row when its identifier is > 0, else dropped). That is gatherSubscriptions +
+// Subscription.Merge (topics.go:631-648, packets/packets.go:254-274) without a per-topic
+// table. The links of one slot are MergePart records mpart[off, off + cnt); mref[pos] names
+// them for the slot at subs pool position pos, PairSlot for the slots on pair lists.
 struct MergeRef {  // 8 B, parallel to the subs pool
   uint32_t off, cnt;
 };
 struct MergePart {  // 8 B
-  uint32_t node, pos;
+  uint32_t node;  // the partner's node
+  uint32_t meta;  // the partner's Qos | NoLocal (the bits Subscription.Merge takes from it)
 };
 // Pair blocks find a topic's merging records without touching the others. For a node g, the
 // block maps each partner node h (a node holding a partner of one of g's may-merge
@@ -164,6 +165,12 @@ struct PairEnt {  // 16 B
   uint32_t h;     // partner node; kNone = empty
   uint32_t off;   // absolute offset of the list in the pair-list pool
   uint32_t cnt;   // slots on the list
+  uint32_t pad;
+};
+struct PairSlot {  // 16 B: one slot on a pair list, with its partner links
+  uint32_t k;       // may-merge slot of g, relative to g's may-merge slots
+  uint32_t mp_off;  // its MergePart records
+  uint32_t mp_cnt;
   uint32_t pad;
 };
 

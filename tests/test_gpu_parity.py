@@ -312,11 +312,11 @@ def test_many_merging_clients(gpu_available):
 
 
 def test_partner_map_fallback(gpu_available):
-    """Topics gathering 256 (LDS map) and 512 (> map capacity: linear partner lookup) nodes
-    that all hold may-merge subscriptions: every literal/'+' path of depth 8 and 9."""
+    """Topics gathering 128 (the pair analysis' limit), 256 and 512 (linear partner lookup)
+    nodes that all hold may-merge subscriptions: every literal/'+' path of depth 7, 8 and 9."""
     import itertools
     e, o = EngineAdapter(), OracleAdapter()
-    for depth in (8, 9):
+    for depth in (7, 8, 9):
         paths = ["/".join(f"a{i}" if b == 0 else "+" for i, b in enumerate(bits))
                  for bits in itertools.product((0, 1), repeat=depth)]
         for k, f in enumerate(paths):  # client k holds paths k and k + 1: partners pairwise
@@ -325,7 +325,25 @@ def test_partner_map_fallback(gpu_available):
                 kw = dict(qos=(k + len(g)) % 3, identifier=(k % 4) * 7, no_local=k % 5 == 0)
                 assert e.subscribe(c, g, **kw) == o.subscribe(c, g, **kw)
     topics = ["/".join(f"a{i}" for i in range(9)), "/".join(f"a{i}" for i in range(8)),
-              "/".join(f"a{i}" for i in range(8)) + "/x", "a0/a1"]
+              "/".join(f"a{i}" for i in range(7)), "/".join(f"a{i}" for i in range(8)) + "/x", "a0/a1"]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
+
+
+def test_many_pair_hits(gpu_available):
+    """A topic whose merge gathers are pairwise partners through many clients: hundreds of
+    (g, h) hit lists, staged and resolved in several flushes."""
+    e, o = EngineAdapter(), OracleAdapter()
+    r = random.Random(77)
+    fs = ["#", "a/#", "+/#", "a/b/#", "a/+/#", "+/b/#", "+/+/#", "a/b/c/#", "a/b/+/#", "+/b/c/#",
+          "a/+/c/#", "+/+/c/#", "a/b/c/d", "a/b/c/+", "a/+/c/d", "+/b/c/d", "+/+/+/+", "a/b/+/d",
+          "+/+/c/d", "a/+/+/d", "a/b/c/d/#"]
+    for c in range(40):
+        mine = fs if c < 3 else r.sample(fs, r.randint(2, 8))
+        for f in mine:
+            kw = dict(qos=r.randint(0, 2), identifier=r.choice([0, 0, 4, 11]), no_local=r.random() < 0.3)
+            assert e.subscribe(f"p{c}", f, **kw) == o.subscribe(f"p{c}", f, **kw)
+    topics = ["a/b/c/d", "a/b/c", "a/x/c/d", "$SYS/b/c/d", "a/b/c/d/e", "q"]
     for t, g in zip(topics, e.subscribers_batch(topics)):
         assert g == o.subscribers(t), t
 
