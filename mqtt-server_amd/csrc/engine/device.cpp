@@ -148,7 +148,26 @@ Device::Device(int dev) : dev_(dev) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   const char* e = getenv("MQ_CHUNK_ROWS");
   chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : (256ull << 20);  // 4 GiB of 16-B rows
-  merge_stats_ = getenv("MQ_MERGE_STATS") != nullptr;  // diagnosis only
+  const char* ms = getenv("MQ_MERGE_STATS");  // diagnosis only
+  merge_stats_ = ms != nullptr;
+  if (ms && *ms) tstat_path_ = ms;
+  int cus = 0;
+  hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_), "hipDeviceGetAttribute");
+  n_cus_ = (uint32_t)std::max(1, cus);
+  read_knobs();
+}
+
+// Tuning and diagnosis knobs, re-read per batch (development only; the defaults are the product).
+void Device::read_knobs() {
+  auto knob = [](const char* name, uint32_t def) {
+    const char* v = getenv(name);
+    return v ? (uint32_t)atoi(v) : def;
+  };
+  serial_ = getenv("MQ_SERIAL") != nullptr;                      // k_merge on the launch stream
+  // 0: one wavefront per tile / topic; else a persistent grid of that many workgroups per CU
+  copy_blocks_ = n_cus_ * knob("MQ_COPY_BLOCKS_PER_CU", kCopyBlocksPerCU);
+  merge_blocks_ = n_cus_ * knob("MQ_MERGE_BLOCKS_PER_CU", kMergeBlocksPerCU);
+  merge_diag_ = knob("MQ_MERGE_DIAG", 0);
 }
 
 Device::~Device() {
@@ -157,10 +176,10 @@ Device::~Device() {
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &desc_,
-                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_})
+                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_, &tstat_, &tiles_, &plan_})
     b->release();
   for (int k = 0; k < 2; k++) {
-    for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &tiles_[k]}) b->release();
+    for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k]}) b->release();
     if (copy_done_[k]) (void)hipEventDestroy(copy_done_[k]);
     if (merge_done_[k]) (void)hipEventDestroy(merge_done_[k]);
   }
@@ -175,10 +194,10 @@ uint64_t Device::device_bytes() const {
                shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4 +
                mref_.cap * sizeof(MergeRef) + mpart_.cap * sizeof(MergePart) +
                npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * sizeof(PairSlot);
-  for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &desc_})
+  for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &desc_, &tiles_})
     b += x->bytes;
   for (int k = 0; k < 2; k++)
-    for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &tiles_[k]}) b += x->bytes;
+    for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k]}) b += x->bytes;
   return b;
 }
 
@@ -262,6 +281,7 @@ void Device::stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hip
 void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                    HostMatch* host, mq_match_result* out) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
+  read_knobs();
   sync(ix, s);
   memset(out, 0, sizeof(*out));
   last_chunks_ = 0;
@@ -322,22 +342,33 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     uint32_t b0, b1;
   };
   std::vector<Chunk> chunks;
-  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1, max_tiles = 1;
+  std::vector<ChunkPlan> plan;
+  std::vector<uint32_t> chunk_of_block(nb);
+  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1, total_tiles = 0;
   auto tiles_of = [](uint64_t rows) { return (rows + kCopyTile - 1) / kCopyTile; };
   for (uint32_t b = 0; b < nb;) {
     uint32_t e = b + 1;
     while (e < nb && h_bpre_[e + 1].rows - h_bpre_[b].rows <= chunk_rows_budget_) e++;
-    chunks.push_back(Chunk{b, e});
     const TopicOff &lo = h_bpre_[b], &hi = h_bpre_[e];
+    for (uint32_t k = b; k < e; k++) chunk_of_block[k] = (uint32_t)chunks.size();
+    chunks.push_back(Chunk{b, e});
+    ChunkPlan p;
+    p.rows = lo.rows;
+    p.shr = lo.shr;
+    p.inl = lo.inl;
+    p.tile_off = (uint32_t)total_tiles;
+    p.n_tiles0 = (uint32_t)tiles_of(hi.rows - lo.rows);
+    p.n_tiles1 = (uint32_t)tiles_of(hi.shr - lo.shr);
+    p.pad = 0;
+    plan.push_back(p);
     max_rows = std::max(max_rows, hi.rows - lo.rows);
     max_shr = std::max(max_shr, hi.shr - lo.shr);
     max_inl = std::max(max_inl, hi.inl - lo.inl);
-    max_tiles = std::max(max_tiles, tiles_of(hi.rows - lo.rows) + tiles_of(hi.shr - lo.shr) +
-                                        tiles_of(hi.inl - lo.inl));
+    total_tiles += tiles_of(hi.rows - lo.rows) + tiles_of(hi.shr - lo.shr) + tiles_of(hi.inl - lo.inl);
     max_topics = std::max<uint64_t>(max_topics, std::min<uint64_t>(n, (uint64_t)e * kScanBlock) - (uint64_t)b * kScanBlock);
     b = e;
   }
-  if (max_rows >= (1ull << 32) || max_shr >= (1ull << 32) || max_inl >= (1ull << 32))
+  if (max_rows >= (1ull << 32) || max_shr >= (1ull << 32) || max_inl >= (1ull << 32) || total_tiles >= (1ull << 32))
     throw HipError{hipErrorInvalidValue, "one scan block's output exceeds 2^32 rows"};
   const size_t nbuf = chunks.size() > 1 ? 2 : 1;
   for (size_t k = 0; k < nbuf; k++) {
@@ -345,9 +376,14 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     shr_rows_[k].ensure(max_shr * sizeof(ShrRec));
     inl_rows_[k].ensure(max_inl * sizeof(InlRec));
     res_[k].ensure(max_topics * sizeof(mq_topic_result_dev));
-    tiles_[k].ensure(max_tiles * sizeof(uint32_t));
   }
   desc_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
+  tiles_.ensure(std::max<uint64_t>(total_tiles, 1) * sizeof(uint32_t));
+  plan_.ensure(plan.size() * sizeof(ChunkPlan) + nb * sizeof(uint32_t));
+  h_plan_.resize(plan.size() * sizeof(ChunkPlan) + nb * sizeof(uint32_t));
+  memcpy(h_plan_.data(), plan.data(), plan.size() * sizeof(ChunkPlan));
+  memcpy(h_plan_.data() + plan.size() * sizeof(ChunkPlan), chunk_of_block.data(), nb * sizeof(uint32_t));
+  hip_check(hipMemcpyAsync(plan_.p, h_plan_.data(), h_plan_.size(), hipMemcpyHostToDevice, s), "H2D chunk plan");
   if (!side_) {
     hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate");
     for (int k = 0; k < 2; k++) {
@@ -356,6 +392,22 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     }
     hip_check(hipEventCreateWithFlags(&side_done_, hipEventDisableTiming), "hipEventCreate");
   }
+
+  // every topic's gathers become GDesc records and k_copy tile starts, in one launch
+  DescArgs da;
+  da.ix = di;
+  da.n = n;
+  da.gather_stride = gstride;
+  da.off = offs_.as<TopicOff>();
+  da.gathers = gathers;
+  da.plan = reinterpret_cast<const ChunkPlan*>(plan_.p);
+  da.chunk_of_block = reinterpret_cast<const uint32_t*>(plan_.as<uint8_t>() + plan.size() * sizeof(ChunkPlan));
+  da.desc = desc_.as<GDesc>();
+  da.tiles = tiles_.as<uint32_t>();
+  prof.begin(s);
+  launch_desc(da, s);
+  prof.end("desc", s);
+  hip_check(hipGetLastError(), "k_desc");
 
   if (host) {
     host->topics.resize(n);
@@ -366,6 +418,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
 
   // Per chunk: k_desc + k_copy on the launch stream, then k_merge (and, for host results, the
   // D2H copies) on the side stream. Chunk i + 2 reuses chunk i's buffers after its merge.
+  hipStream_t cs = s;  // k_copy stream
   for (size_t ci = 0; ci < chunks.size(); ci++) {
     const Chunk& c = chunks[ci];
     const size_t b = ci % nbuf;
@@ -377,10 +430,8 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     a.t1 = std::min<uint64_t>(n, (uint64_t)c.b1 * kScanBlock);
     a.off = offs_.as<TopicOff>();
     a.base = lo;
-    a.gathers = gathers;
-    a.gather_stride = gstride;
     a.desc = desc_.as<GDesc>();
-    a.tiles = tiles_[b].as<uint32_t>();
+    a.tiles = tiles_.as<uint32_t>() + plan[ci].tile_off;
     a.total[0] = (uint32_t)(hi.rows - lo.rows);
     a.total[1] = (uint32_t)(hi.shr - lo.shr);
     a.total[2] = (uint32_t)(hi.inl - lo.inl);
@@ -390,6 +441,12 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     a.inl_rows = inl_rows_[b].as<InlRec>();
     a.res = res_[b].as<mq_topic_result_dev>();
     a.stats = nullptr;
+    a.tstat = nullptr;
+    a.diag = merge_diag_;
+    if (!tstat_path_.empty()) {
+      if (ci == 0) tstat_.ensure((size_t)n * kTStat * sizeof(uint32_t));
+      a.tstat = tstat_.as<uint32_t>();
+    }
     if (merge_stats_) {
       if (!mstats_.p) {
         mstats_.ensure(4 * sizeof(unsigned long long));
@@ -397,20 +454,19 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       }
       a.stats = mstats_.as<unsigned long long>();
     }
-    if (ci >= nbuf) hip_check(hipStreamWaitEvent(s, merge_done_[b], 0), "hipStreamWaitEvent");
-    prof.begin(s);
-    launch_desc(a, s);
-    prof.end("desc", s);
-    hip_check(hipGetLastError(), "k_desc");
-    prof.begin(s);
-    launch_copy(a, s);
-    prof.end("copy", s);
+    if (ci >= nbuf) hip_check(hipStreamWaitEvent(cs, merge_done_[b], 0), "hipStreamWaitEvent");
+    prof.begin(cs);
+    launch_copy(a, copy_blocks_, cs);
+    prof.end("copy", cs);
     hip_check(hipGetLastError(), "k_copy");
-    hip_check(hipEventRecord(copy_done_[b], s), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
-    prof.begin(side_);
-    launch_merge(a, side_);
-    prof.end("merge", side_);
+    hipStream_t ms = serial_ ? cs : side_;
+    if (!serial_) {
+      hip_check(hipEventRecord(copy_done_[b], cs), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
+    }
+    prof.begin(ms);
+    launch_merge(a, merge_blocks_, ms);
+    prof.end("merge", ms);
     hip_check(hipGetLastError(), "k_merge");
     prof.count("copy_rows", (uint64_t)a.total[0] + a.total[1] + a.total[2]);
     prof.count("copy_bytes", 16ull * a.total[0] + 8ull * a.total[1] + 8ull * a.total[2]);
@@ -420,19 +476,19 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     const uint32_t nt = a.t1 - a.t0;
     if (host) {
       hip_check(hipMemcpyAsync(host->rows.data() + lo.rows, a.rows, (hi.rows - lo.rows) * sizeof(SubRec),
-                               hipMemcpyDeviceToHost, side_), "D2H rows");
+                               hipMemcpyDeviceToHost, ms), "D2H rows");
       hip_check(hipMemcpyAsync(host->shr.data() + lo.shr, a.shr_rows, (hi.shr - lo.shr) * sizeof(ShrRec),
-                               hipMemcpyDeviceToHost, side_), "D2H shared rows");
+                               hipMemcpyDeviceToHost, ms), "D2H shared rows");
       hip_check(hipMemcpyAsync(host->inl.data() + lo.inl, a.inl_rows, (hi.inl - lo.inl) * sizeof(InlRec),
-                               hipMemcpyDeviceToHost, side_), "D2H inline rows");
+                               hipMemcpyDeviceToHost, ms), "D2H inline rows");
       hip_check(hipMemcpyAsync(host->topics.data() + a.t0, a.res, nt * sizeof(mq_topic_result),
-                               hipMemcpyDeviceToHost, side_), "D2H topic results");
+                               hipMemcpyDeviceToHost, ms), "D2H topic results");
     }
-    hip_check(hipEventRecord(merge_done_[b], side_), "hipEventRecord");
+    hip_check(hipEventRecord(merge_done_[b], ms), "hipEventRecord");
     if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
       unsigned long long m[4];
-      hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, side_), "D2H stats");
-      hip_check(hipStreamSynchronize(side_), "hipStreamSynchronize");
+      hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, ms), "D2H stats");
+      hip_check(hipStreamSynchronize(ms), "hipStreamSynchronize");
       fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
     }
     out->n_topics = nt;
@@ -447,6 +503,15 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   // the launch stream completes only after the side stream's work of this batch
   hip_check(hipEventRecord(side_done_, side_), "hipEventRecord");
   hip_check(hipStreamWaitEvent(s, side_done_, 0), "hipStreamWaitEvent");
+  if (!tstat_path_.empty()) {  // diagnosis only: per-topic k_merge counters of this batch
+    std::vector<uint32_t> h((size_t)n * kTStat);
+    hip_check(hipMemcpyAsync(h.data(), tstat_.p, h.size() * 4, hipMemcpyDeviceToHost, s), "D2H tstat");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (FILE* f = fopen(tstat_path_.c_str(), "wb")) {
+      fwrite(h.data(), 4, h.size(), f);
+      fclose(f);
+    }
+  }
   if (host) {
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     for (const Chunk& c : chunks) {

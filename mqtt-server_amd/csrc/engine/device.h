@@ -108,6 +108,7 @@ class Device {
 
  private:
   DevIndex dev_index(const Index& ix) const;
+  void read_knobs();
   void check_err(hipStream_t s);
 
   int dev_;
@@ -134,12 +135,19 @@ class Device {
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   // Output chunks alternate between two buffer sets so that k_merge of chunk i (side stream)
   // overlaps k_desc/k_copy of chunk i + 1 (launch stream).
-  DevBuf rows_[2], shr_rows_[2], inl_rows_[2], res_[2], tiles_[2];
+  DevBuf rows_[2], shr_rows_[2], inl_rows_[2], res_[2];
+  DevBuf tiles_, plan_;  // the batch's k_copy tile table; chunk plans + block -> chunk map
+  std::vector<uint8_t> h_plan_;
   DevBuf err_, desc_;
   hipStream_t side_ = nullptr;
   hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_, mstats_;
   bool merge_stats_ = false;  // MQ_MERGE_STATS: k_merge work counters to stderr
+  std::string tstat_path_;    // MQ_MERGE_STATS=<path>: per-topic k_merge counters (kTStat u32 each)
+  uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
+  uint32_t n_cus_ = 1, merge_diag_ = 0;
+  bool serial_ = false;       // MQ_SERIAL: k_merge on the launch stream (isolated kernel times)
+  DevBuf tstat_;
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;
   uint64_t empty_handle_ = 0;

@@ -492,7 +492,7 @@ void Index::flush_merge() {
     uint32_t lists_n = 0;
     for (size_t i = 0; i < hk.size(); i++) lists_n += i == 0 || hk[i].first != hk[i - 1].first;
     uint32_t ecap = 2, lcap = 1;
-    while (ecap < 2 * lists_n) ecap <<= 1;
+    while (ecap < 4 * lists_n) ecap <<= 1;  // load <= 1/4: k_merge probes four slots per load round
     while (lcap < hk.size()) lcap <<= 1;
     const uint32_t eo = pent.alloc(ecap), lo = plist.alloc(lcap), mask = ecap - 1;
     for (uint32_t i = 0; i < ecap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};

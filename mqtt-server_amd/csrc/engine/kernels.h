@@ -9,10 +9,13 @@ namespace mq {
 
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
-constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves
-constexpr uint32_t kMapSlots = 256;    // per-wave LDS map (gathered merge node -> gather index)
-constexpr uint32_t kPairMax = 128;     // merge gathers covered by the pair analysis
+constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves per tile
+constexpr uint32_t kCopyBlocksPerCU = 8;   // persistent k_copy: 256-thread workgroups per CU
+constexpr uint32_t kMergeBlocksPerCU = 8;  // persistent k_merge beside it (side stream)
+constexpr uint32_t kMapSlots = 128;    // per-wave LDS map (gathered merge node -> gather index)
+constexpr uint32_t kPairMax = 64;     // merge gathers covered by the pair analysis
 constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
+constexpr uint32_t kPartBatch = 8;     // partner links loaded together per record
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -67,8 +70,9 @@ struct GDesc {  // 32 B
   uint32_t i_pos;  // inline rows
   uint32_t i_src;
   uint32_t word;   // gather word (node | kGatherSubs | kGatherInline)
-  uint32_t pad;
+  uint32_t mdir;   // n_direct of the node | kDescMerge when its may-merge records are gathered
 };
+constexpr uint32_t kDescMerge = 1u << 31;
 
 // Per-chunk arguments of k_desc / k_copy / k_merge.
 struct EmitArgs {
@@ -76,10 +80,8 @@ struct EmitArgs {
   uint32_t t0, t1;          // topic range of this chunk
   const TopicOff* off;      // per-topic offsets (n + 1)
   TopicOff base;            // off[t0]: the chunk's output buffers start here
-  const uint32_t* gathers;
-  uint32_t gather_stride;   // kGatherCap: per-topic slots of the count pass; 0: compact at off.g
   GDesc* desc;              // indexed by absolute gather index
-  uint32_t* tiles;          // k_copy tile -> first gather: [client | shared | inline] tiles
+  const uint32_t* tiles;    // k_copy tile -> first gather: [client | shared | inline] tiles
   uint32_t n_tiles[3];      // tiles per stream
   uint32_t total[3];        // rows per stream in this chunk
   SubRec* rows;
@@ -87,15 +89,39 @@ struct EmitArgs {
   InlRec* inl_rows;
   mq_topic_result_dev* res; // indexed t - t0
   unsigned long long* stats;  // k_merge: [0] hit lists, [1] records resolved, [2] slow-path topics
+  uint32_t diag;              // diagnosis knobs (MQ_MERGE_DIAG): 1 = no row writes, 2 = no flush
+  uint32_t* tstat;            // diagnosis (MQ_MERGE_STATS=path): kTStat words per topic, index t
+};
+constexpr uint32_t kTStat = 8;
+
+// Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile
+// table sits in the batch's tile array.
+struct ChunkPlan {  // 32 B
+  uint64_t rows, shr, inl;  // off[first topic of the chunk]
+  uint32_t tile_off;        // its tiles: [client | shared | inline] from tiles + tile_off
+  uint32_t n_tiles0, n_tiles1, pad;
+};
+
+// One k_desc launch over every topic of the batch.
+struct DescArgs {
+  DevIndex ix;
+  uint32_t n;
+  uint32_t gather_stride;
+  const TopicOff* off;
+  const uint32_t* gathers;
+  const uint32_t* chunk_of_block;  // scan block -> chunk
+  const ChunkPlan* plan;
+  GDesc* desc;
+  uint32_t* tiles;
 };
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
                  TopicCount* cnt, const TopicOff* off, uint32_t* gathers, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
-void launch_desc(const EmitArgs& a, hipStream_t s);
-void launch_copy(const EmitArgs& a, hipStream_t s);
-void launch_merge(const EmitArgs& a, hipStream_t s);
+void launch_desc(const DescArgs& a, hipStream_t s);
+void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
+void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
                 uint32_t* count, hipStream_t s);

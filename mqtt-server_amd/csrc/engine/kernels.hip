@@ -19,6 +19,8 @@
 
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace mq {
 
 // ---------------------------------------------------------------------------------------------
@@ -337,26 +339,24 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t gather_word(const EmitArgs& a, uint32_t t, const TopicOff& o0, uint32_t i) {
-  return a.gather_stride ? a.gathers[(uint64_t)t * a.gather_stride + i] : a.gathers[o0.g + i];
-}
-
-__global__ __launch_bounds__(256) void k_desc(EmitArgs a) {
-  const uint32_t t = a.t0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.t1) return;
+__global__ __launch_bounds__(256) void k_desc(DescArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.n) return;
+  const ChunkPlan cp = a.plan[a.chunk_of_block[t / kScanBlock]];
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
-  uint32_t rpos = (uint32_t)(o0.rows - a.base.rows);
-  uint32_t spos = (uint32_t)(o0.shr - a.base.shr), ipos = (uint32_t)(o0.inl - a.base.inl);
+  uint32_t rpos = (uint32_t)(o0.rows - cp.rows);
+  uint32_t spos = (uint32_t)(o0.shr - cp.shr), ipos = (uint32_t)(o0.inl - cp.inl);
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
-  uint32_t* tile_r = a.tiles;
-  uint32_t* tile_s = a.tiles + a.n_tiles[0];
-  uint32_t* tile_i = tile_s + a.n_tiles[1];
+  uint32_t* tile_r = a.tiles + cp.tile_off;
+  uint32_t* tile_s = tile_r + cp.n_tiles0;
+  uint32_t* tile_i = tile_s + cp.n_tiles1;
+  const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
   for (uint32_t i = 0; i < n_g; i++) {
-    const uint32_t gw = gather_word(a, t, o0, i);
+    const uint32_t gw = gw_src[i];
     const NodeLists L = a.ix.lists[gw & kGatherNode];
     const uint32_t rn = (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
     const uint32_t in = (gw & kGatherInline) ? L.inl_cnt : 0u;
-    const uint32_t g = (uint32_t)(o0.g + i);
+    const uint64_t g = o0.g + i;
     GDesc d;
     d.r_pos = rpos;
     d.r_src = L.sub_off;
@@ -365,12 +365,12 @@ __global__ __launch_bounds__(256) void k_desc(EmitArgs a) {
     d.i_pos = ipos;
     d.i_src = L.inl_off;
     d.word = gw;
-    d.pad = 0;
+    d.mdir = L.n_direct | ((gw & kGatherSubs) && L.n_merge ? kDescMerge : 0u);
     a.desc[g] = d;
     // the k_copy tiles whose first row falls inside this gather start their cursor here
-    for (uint32_t k = (rpos + kCopyTile - 1) / kCopyTile; k * kCopyTile < rpos + rn; k++) tile_r[k] = g;
-    for (uint32_t k = (spos + kCopyTile - 1) / kCopyTile; k * kCopyTile < spos + L.shr_cnt; k++) tile_s[k] = g;
-    for (uint32_t k = (ipos + kCopyTile - 1) / kCopyTile; k * kCopyTile < ipos + in; k++) tile_i[k] = g;
+    for (uint32_t k = (rpos + kCopyTile - 1) / kCopyTile; k * kCopyTile < rpos + rn; k++) tile_r[k] = (uint32_t)g;
+    for (uint32_t k = (spos + kCopyTile - 1) / kCopyTile; k * kCopyTile < spos + L.shr_cnt; k++) tile_s[k] = (uint32_t)g;
+    for (uint32_t k = (ipos + kCopyTile - 1) / kCopyTile; k * kCopyTile < ipos + in; k++) tile_i[k] = (uint32_t)g;
     rpos += rn;
     spos += L.shr_cnt;
     ipos += in;
@@ -378,11 +378,18 @@ __global__ __launch_bounds__(256) void k_desc(EmitArgs a) {
 }
 
 // Stream S of one tile: rows [x0, x1) of the chunk's stream S (0: client rows, 1: shared rows,
-// 2: inline rows), starting at gather j.
+// 2: inline rows), starting at gather j. The gathers' (position, source) pairs are read as a
+// register window of 64 consecutive GDesc records (one coalesced load: lane k holds gather
+// wb + k) plus the start of gather wb + 64. Each lane keeps its own gather cursor and reads the
+// window with ds_bpermute in wave-uniform loops (every lane executes every bpermute), so the
+// inner loop issues no dependent global loads. The window slides to lane 0's gather (the lowest
+// row) when a lane's row lies past it; rows past a window that cannot slide (more than 64
+// gathers, empty ones included, between lane 0 and the lane) are found by a global scan.
 template <int S, class V>
 __device__ __forceinline__ void copy_tile(const EmitArgs& a, const V* __restrict__ src, V* __restrict__ dst,
                                           uint32_t x0, uint32_t x1, uint32_t j, uint32_t lane) {
   constexpr int U = 8;
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
   const uint32_t jend = (uint32_t)a.off[a.t1].g;
   auto pos_of = [&](uint32_t g) -> uint32_t {
     return S == 0 ? a.desc[g].r_pos : (S == 1 ? a.desc[g].s_pos : a.desc[g].i_pos);
@@ -390,20 +397,66 @@ __device__ __forceinline__ void copy_tile(const EmitArgs& a, const V* __restrict
   auto src_of = [&](uint32_t g) -> uint32_t {
     return S == 0 ? a.desc[g].r_src : (S == 1 ? a.desc[g].s_src : a.desc[g].i_src);
   };
-  uint32_t cur = pos_of(j);
-  uint32_t nxt = j + 1 < jend ? pos_of(j + 1) : 0xFFFFFFFFu;
-  uint32_t sb = src_of(j) - cur;  // source index = sb + row
+  uint32_t wb = j, wpos = kInf, wsrc = 0, wsent = kInf;
+  auto load_window = [&]() {
+    const uint32_t g = wb + lane;
+    wpos = g < jend ? pos_of(g) : kInf;
+    wsrc = g < jend ? src_of(g) : 0u;
+    wsent = wb + 64 < jend ? pos_of(wb + 64) : kInf;
+  };
+  // start of gather ga + 1 for an in-window ga (kInf when ga is past the window: unknown)
+  auto next_of = [&](uint32_t ga) -> uint32_t {
+    const uint32_t k = ga - wb;
+    const uint32_t v = __shfl(wpos, (int)min(k + 1, 63u), 64);
+    return k < 63 ? v : (k == 63 ? wsent : kInf);
+  };
+  load_window();
+  uint32_t ga = j;  // this lane's gather (absolute index)
+  uint32_t nxt = next_of(ga);
+  uint32_t sb = __shfl(wsrc, 0, 64) - __shfl(wpos, 0, 64);  // source index = sb + row
   for (uint32_t r0 = x0; r0 < x1; r0 += 64 * U) {
     uint32_t si[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t x = min(r0 + u * 64 + lane, x1 - 1);
-      while (x >= nxt) {  // advance this lane's cursor to the gather holding row x
-        j++;
-        cur = nxt;
-        nxt = j + 1 < jend ? pos_of(j + 1) : 0xFFFFFFFFu;
-        sb = src_of(j) - cur;
+      bool moved = false, slow = false;
+      uint32_t sb_slow = 0;
+      for (;;) {
+        const bool adv = ga - wb < 64 && x >= nxt;
+        if (__any(adv)) {
+          if (adv) {
+            ga++;
+            moved = true;
+          }
+          nxt = next_of(ga);
+          continue;
+        }
+        const bool out = ga - wb >= 64 || (ga - wb == 63 && x >= wsent);
+        if (!__any(out)) break;
+        const uint32_t nb = __shfl(ga, 0, 64);  // lane 0 holds the lowest row
+        if (nb != wb) {
+          wb = nb;
+          load_window();
+          nxt = next_of(ga);
+          moved = true;
+          continue;
+        }
+        if (out) {  // the window cannot reach this lane's row: scan the records
+          uint32_t n2 = ga + 1 < jend ? pos_of(ga + 1) : kInf;
+          while (x >= n2) {
+            ga++;
+            n2 = ga + 1 < jend ? pos_of(ga + 1) : kInf;
+          }
+          sb_slow = src_of(ga) - pos_of(ga);
+          slow = true;
+          nxt = kInf;
+        }
+        break;
       }
+      const uint32_t k = min(ga - wb, 63u);
+      const uint32_t sp = __shfl(wpos, (int)k, 64), ss = __shfl(wsrc, (int)k, 64);
+      if (slow) sb = sb_slow;
+      else if (moved) sb = ss - sp;
       si[u] = sb + x;
     }
     V v[U];
@@ -417,23 +470,26 @@ __device__ __forceinline__ void copy_tile(const EmitArgs& a, const V* __restrict
   }
 }
 
+// Persistent: a.copy_waves wavefronts stride over the chunk's tiles, so the copy holds only the
+// wave slots it needs to keep HBM busy and k_merge (side stream) gets the rest of every CU.
 __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t j = a.tiles[min(w, a.n_tiles[0] + a.n_tiles[1] + a.n_tiles[2] - 1)];
-  if (w < a.n_tiles[0]) {
-    const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[0]);
-    copy_tile<0>(a, reinterpret_cast<const u32x4*>(a.ix.subs), reinterpret_cast<u32x4*>(a.rows), x0, x1, j, lane);
-    return;
-  }
-  w -= a.n_tiles[0];
-  if (w < a.n_tiles[1]) {
-    const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[1]);
-    copy_tile<1>(a, reinterpret_cast<const u32x2*>(a.ix.shr), reinterpret_cast<u32x2*>(a.shr_rows), x0, x1, j, lane);
-    return;
-  }
-  w -= a.n_tiles[1];
-  if (w < a.n_tiles[2]) {
+  const uint32_t n_all = a.n_tiles[0] + a.n_tiles[1] + a.n_tiles[2];
+  for (uint32_t w0 = blockIdx.x * 4 + (threadIdx.x >> 6); w0 < n_all; w0 += gridDim.x * 4) {
+    uint32_t w = w0;
+    const uint32_t j = a.tiles[w];
+    if (w < a.n_tiles[0]) {
+      const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[0]);
+      copy_tile<0>(a, reinterpret_cast<const u32x4*>(a.ix.subs), reinterpret_cast<u32x4*>(a.rows), x0, x1, j, lane);
+      continue;
+    }
+    w -= a.n_tiles[0];
+    if (w < a.n_tiles[1]) {
+      const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[1]);
+      copy_tile<1>(a, reinterpret_cast<const u32x2*>(a.ix.shr), reinterpret_cast<u32x2*>(a.shr_rows), x0, x1, j, lane);
+      continue;
+    }
+    w -= a.n_tiles[1];
     const uint32_t x0 = w * kCopyTile, x1 = min(x0 + kCopyTile, a.total[2]);
     copy_tile<2>(a, reinterpret_cast<const u32x2*>(a.ix.inl), reinterpret_cast<u32x2*>(a.inl_rows), x0, x1, j, lane);
   }
@@ -445,14 +501,16 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
   __shared__ uint32_t mg_node[4][kPairMax];    // the topic's merge gathers, in gather order:
   __shared__ uint32_t mg_gi[4][kPairMax];      //   node, gather index,
   __shared__ uint32_t mg_moff[4][kPairMax];    //   subs pool offset of its may-merge slots,
-  __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first may-merge slot
+  __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first may-merge slot,
+  __shared__ uint32_t mg_eoff[4][kPairMax];    //   its pair-block hash table (NodePair)
+  __shared__ uint32_t mg_emask[4][kPairMax];
   __shared__ uint32_t h_ga[4][kHitMax];        // staged hit lists: merge gather of g,
   __shared__ uint32_t h_off[4][kHitMax];       //   pair-list offset,
   __shared__ uint32_t h_via[4][kHitMax];       //   partner node h,
   __shared__ uint32_t h_pre[4][kHitMax + 1];   //   exclusive prefix of their lengths (+ total)
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t t = a.t0 + blockIdx.x * 4 + wv;
-  if (t >= a.t1) return;  // wave-uniform
+  // persistent: a.merge grid's waves stride over the chunk's topics (wave-uniform loop)
+  for (uint32_t t = a.t0 + blockIdx.x * 4 + wv; t < a.t1; t += gridDim.x * 4) {
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
   const uint32_t cap = (uint32_t)(o1.rows - o0.rows);
@@ -461,7 +519,9 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
   const GDesc* __restrict__ gd = a.desc + o0.g;
   SubRec* __restrict__ crow = a.rows;  // chunk-relative rows (GDesc positions)
   uint32_t n_nonbase = 0, n_ext = 0;
-  uint32_t st_hits = 0, st_recs = 0, st_slow = 0;
+  uint32_t st_hits = 0, st_recs = 0, st_slow = 0, st_map = 0;
+  const uint64_t c_start = a.tstat ? clock64() : 0;
+  uint64_t c_map = c_start, c_pair = c_start, c_flush = 0;
 
   if (o1.merge > o0.merge) {  // the topic gathers may-merge records
     // Map every gathered node that holds may-merge records (and whose subscriptions are
@@ -474,15 +534,15 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
       const uint32_t i = i0 + lane;
       bool ins = false;
       uint32_t node = 0, moff = 0, mrow = 0;
+      NodePair P{0, kNone, 0, 0};
       if (i < n_g) {
         const GDesc d = gd[i];
         node = d.word & kGatherNode;
-        if (d.word & kGatherSubs) {
-          const NodeLists L = a.ix.lists[node];
-          ins = L.n_merge > 0;
-          moff = L.sub_off + L.n_direct;
-          mrow = d.r_pos + L.n_direct;
-        }
+        ins = (d.mdir & kDescMerge) != 0;
+        const uint32_t nd = d.mdir & ~kDescMerge;
+        moff = d.r_src + nd;
+        mrow = d.r_pos + nd;
+        if (ins) P = a.ix.npair[node];
       }
       const uint64_t bi = __ballot(ins);
       const uint32_t x = n_map + prefix_before(bi);
@@ -494,10 +554,14 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
         mg_gi[wv][x] = i;
         mg_moff[wv][x] = moff;
         mg_row[wv][x] = mrow;
+        mg_eoff[wv][x] = P.ent_off;
+        mg_emask[wv][x] = P.ent_mask;
       }
       n_map += __popcll(bi);
     }
     wave_sync_lds();
+    st_map = n_map;
+    if (a.tstat) c_map = clock64();
     const bool slow = n_map > kPairMax;  // beyond the map: look partners up linearly
     auto gathered = [&](uint32_t h) -> uint32_t {  // gather index of node h, or kNone
       if (!slow) {
@@ -532,24 +596,33 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
         bool bound = false, base = true;
         uint32_t first = kNone;
         uint32_t q = rec.meta & kMetaQos, nl = rec.meta & kMetaNoLocal;
-        for (uint32_t e = 0; e < mp_cnt; e++) {
-          const MergePart p = a.ix.mpart[mp_off + e];
-          const uint32_t gh = gathered(p.node);
-          if (gh == kNone) continue;
-          if (!bound) first = p.node;
-          bound = true;
-          if (gh < gi) {
-            base = false;
-            break;
+        // partner links in batches of kPartBatch independent loads (one latency per batch)
+        for (uint32_t e0 = 0; e0 < mp_cnt && base; e0 += kPartBatch) {
+          MergePart pb[kPartBatch];
+#pragma unroll
+          for (uint32_t u = 0; u < kPartBatch; u++)
+            pb[u] = e0 + u < mp_cnt ? a.ix.mpart[mp_off + e0 + u] : MergePart{kNone, 0};
+#pragma unroll
+          for (uint32_t u = 0; u < kPartBatch; u++) {
+            if (!base || pb[u].node == kNone) continue;
+            const uint32_t gh = gathered(pb[u].node);
+            if (gh == kNone) continue;
+            if (!bound) first = pb[u].node;
+            bound = true;
+            if (gh < gi) {
+              base = false;
+              continue;
+            }
+            q = max(q, pb[u].meta & kMetaQos);
+            nl |= pb[u].meta & kMetaNoLocal;
           }
-          q = max(q, p.meta & kMetaQos);
-          nl |= p.meta & kMetaNoLocal;
         }
         if (bound) {
           counted = via == kNone || via == first;
           nonbase = !base;
           ident = rec.ident;
-          if (base) {
+          if (a.diag & 1) {
+          } else if (base) {
             const uint32_t m = (rec.meta & ~(kMetaQos | kMetaNoLocal)) | q | nl;
             if (m != rec.meta) crow[row].meta = m;
           } else {
@@ -569,13 +642,19 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
       // is resolved 64 records per wave-instruction.
       uint32_t n_hit = 0, tot = 0;
       auto flush_hits = [&]() {
+        const uint64_t cf0 = a.tstat ? clock64() : 0;
         if (lane == 0) h_pre[wv][n_hit] = tot;
         wave_sync_lds();
-        uint32_t jj = 0;
+        if (a.diag & 2) tot = 0;
         for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
           const uint32_t r = r0 + lane;
           const uint32_t rc = min(r, tot - 1);
-          while (h_pre[wv][jj + 1] <= rc) jj++;
+          uint32_t lo = 0, hi = n_hit;  // h_pre[lo] <= rc < h_pre[hi] (lists are non-empty)
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (h_pre[wv][mid] <= rc) lo = mid; else hi = mid;
+          }
+          const uint32_t jj = lo;
           const uint32_t xa = h_ga[wv][jj];
           const PairSlot e = a.ix.plist[h_off[wv][jj] + (rc - h_pre[wv][jj])];
           resolve(r < tot, mg_moff[wv][xa] + e.k, mg_row[wv][xa] + e.k, mg_gi[wv][xa], h_via[wv][jj],
@@ -585,6 +664,7 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
         n_hit = 0;
         tot = 0;
         wave_sync_lds();
+        if (a.tstat) c_flush += clock64() - cf0;
       };
       const uint32_t np = n_map * n_map;
       for (uint32_t p0 = 0; p0 < np; p0 += 64) {
@@ -595,20 +675,30 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
           ga = p / n_map;
           const uint32_t hb = p - ga * n_map;
           if (ga != hb) {
-            const NodePair P = a.ix.npair[mg_node[wv][ga]];
-            if (P.ent_mask != kNone) {
+            const uint32_t ent_mask = mg_emask[wv][ga], ent_off = mg_eoff[wv][ga];
+            if (ent_mask != kNone) {
               hn = mg_node[wv][hb];
-              uint32_t sl = pair_hash(hn) & P.ent_mask;
-              for (uint32_t probes = 0; probes <= P.ent_mask; probes++) {
-                const PairEnt e = a.ix.pent[P.ent_off + sl];
-                if (e.h == hn) {
-                  hit = true;
-                  e_off = e.off;
-                  e_cnt = e.cnt;
-                  break;
+              // linear probing, four slots per round: one load latency covers most probes
+              uint32_t sl = pair_hash(hn) & ent_mask;
+              for (uint32_t probes = 0; probes <= ent_mask; probes += 4) {
+                PairEnt pe[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) pe[u] = a.ix.pent[ent_off + ((sl + u) & ent_mask)];
+                bool stop = false;
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) {
+                  if (stop) continue;
+                  if (pe[u].h == hn) {
+                    hit = true;
+                    e_off = pe[u].off;
+                    e_cnt = pe[u].cnt;
+                    stop = true;
+                  } else if (pe[u].h == kNone) {
+                    stop = true;
+                  }
                 }
-                if (e.h == kNone) break;
-                sl = (sl + 1) & P.ent_mask;
+                if (stop) break;
+                sl = (sl + 4) & ent_mask;
               }
             }
           }
@@ -648,7 +738,9 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
     }
   }
 
+  if (a.tstat) c_pair = clock64();
   uint32_t n_inl = (uint32_t)(o1.inl - o0.inl);
+  const uint32_t st_inl = n_inl;
   if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675); rows from k_copy
     InlRec* __restrict__ ir = a.inl_rows + ib;
     uint32_t kept = 0;
@@ -681,12 +773,26 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
     res.n_inline = n_inl;
     res.reserved = 0;
     a.res[t - a.t0] = res;
+    if (a.tstat) {
+      const uint64_t c_end = clock64();
+      uint32_t* ts = a.tstat + (uint64_t)t * kTStat;
+      ts[0] = (uint32_t)min<uint64_t>(c_end - c_start, 0xFFFFFFFFull);
+      ts[1] = (uint32_t)min<uint64_t>(c_map - c_start, 0xFFFFFFFFull);
+      ts[2] = (uint32_t)min<uint64_t>(c_pair - c_map, 0xFFFFFFFFull);
+      ts[3] = n_g;
+      ts[4] = st_map;
+      ts[5] = st_hits;
+      ts[6] = st_recs | (st_slow << 31);
+      ts[7] = (uint32_t)min<uint64_t>(c_flush, 0xFFFFFFFFull);
+      (void)st_inl;
+    }
     if (a.stats && (st_hits | st_recs | st_slow)) {  // diagnosis only (MQ_MERGE_STATS)
       atomicAdd(a.stats + 0, (unsigned long long)st_hits);
       atomicAdd(a.stats + 1, (unsigned long long)st_recs);
       atomicAdd(a.stats + 2, (unsigned long long)st_slow);
     }
   }
+  }  // topic loop
 }
 
 }  // namespace mq
@@ -712,22 +818,23 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
   hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(256), 0, s, cnt, n, bpre, off);
 }
 
-void launch_desc(const EmitArgs& a, hipStream_t s) {
-  const uint32_t n = a.t1 - a.t0;
-  if (!n) return;
-  hipLaunchKernelGGL(k_desc, dim3((n + 255) / 256), dim3(256), 0, s, a);
+void launch_desc(const DescArgs& a, hipStream_t s) {
+  if (!a.n) return;
+  hipLaunchKernelGGL(k_desc, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 
-void launch_copy(const EmitArgs& a, hipStream_t s) {
+void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
   const uint32_t waves = a.n_tiles[0] + a.n_tiles[1] + a.n_tiles[2];
   if (!waves) return;
-  hipLaunchKernelGGL(k_copy, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
+  hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, a);
 }
 
-void launch_merge(const EmitArgs& a, hipStream_t s) {
+void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
   const uint32_t waves = a.t1 - a.t0;
   if (!waves) return;
-  hipLaunchKernelGGL(k_merge, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
+  hipLaunchKernelGGL(k_merge, dim3(blocks), dim3(256), 0, s, a);
 }
 
 
