@@ -168,6 +168,7 @@ void Device::read_knobs() {
   copy_blocks_ = n_cus_ * knob("MQ_COPY_BLOCKS_PER_CU", kCopyBlocksPerCU);
   merge_blocks_ = n_cus_ * knob("MQ_MERGE_BLOCKS_PER_CU", kMergeBlocksPerCU);
   merge_diag_ = knob("MQ_MERGE_DIAG", 0);
+  subbatch_topics_ = knob("MQ_SUBBATCH_TOPICS", kSubBatchTopics);  // topics per pipelined sub-batch
 }
 
 Device::~Device() {
@@ -175,8 +176,8 @@ Device::~Device() {
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
-  for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &desc_,
-                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_, &tstat_, &tiles_, &plan_})
+  for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
+                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_, &tstat_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k]}) b->release();
@@ -185,6 +186,17 @@ Device::~Device() {
   }
   if (side_done_) (void)hipEventDestroy(side_done_);
   if (side_) (void)hipStreamDestroy(side_);
+  if (wstream_) (void)hipStreamDestroy(wstream_);
+  if (ev_in_) (void)hipEventDestroy(ev_in_);
+  for (hipEvent_t e : ev_scan_) (void)hipEventDestroy(e);
+  for (int k = 0; k < 2; k++) {
+    if (sb_done_[k]) (void)hipEventDestroy(sb_done_[k]);
+    desc_[k].release();
+    tiles_[k].release();
+  }
+  plan_.release();
+  if (h_plan_) (void)hipHostFree(h_plan_);
+  if (h_pin_) (void)hipHostFree(h_pin_);
 }
 
 uint64_t Device::device_bytes() const {
@@ -194,7 +206,8 @@ uint64_t Device::device_bytes() const {
                shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4 +
                mref_.cap * sizeof(MergeRef) + mpart_.cap * sizeof(MergePart) +
                npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * sizeof(PairSlot);
-  for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &desc_, &tiles_})
+  for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &desc_[0], &desc_[1],
+                          &tiles_[0], &tiles_[1]})
     b += x->bytes;
   for (int k = 0; k < 2; k++)
     for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k]}) b += x->bytes;
@@ -278,6 +291,41 @@ void Device::stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hip
   *d_to = in_offs_.as<uint64_t>();
 }
 
+// Grow a scratch buffer between launches of one batch: earlier launches may still read the old
+// allocation, so the device drains first (rare: buffers only grow).
+static void grow(DevBuf& b, size_t bytes) {
+  if (bytes <= b.bytes && b.p) return;
+  if (b.p) hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(grow)");
+  b.ensure(bytes);
+}
+
+void Device::ensure_streams() {
+  if (side_) return;
+  hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate");
+  hip_check(hipStreamCreateWithFlags(&wstream_, hipStreamNonBlocking), "hipStreamCreate");
+  for (int k = 0; k < 2; k++) {
+    hip_check(hipEventCreateWithFlags(&copy_done_[k], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&merge_done_[k], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&sb_done_[k], hipEventDisableTiming), "hipEventCreate");
+  }
+  hip_check(hipEventCreateWithFlags(&side_done_, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
+}
+
+void Device::pinned(size_t bytes) {
+  if (bytes <= h_pin_bytes_) return;
+  if (h_pin_) {
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(pinned)");
+    (void)hipHostFree(h_pin_);
+  }
+  h_pin_bytes_ = std::max<size_t>(bytes, 1 << 16);
+  hip_check(hipHostMalloc(&h_pin_, h_pin_bytes_, hipHostMallocDefault), "hipHostMalloc");
+}
+
+// The batch is cut into scan-block aligned sub-batches. Walk + scan of every sub-batch are queued
+// up front on the walk stream; the host plans sub-batch b's output chunks as soon as its scan
+// lands and queues k_desc/k_copy (launch stream) and k_merge (side stream), so the walks of the
+// later sub-batches run under the copies of the earlier ones.
 void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                    HostMatch* host, mq_match_result* out) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
@@ -292,213 +340,271 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   }
   check_err(s);  // faults flagged by the previous batch's kernels
   if (n == 0) return;
+  ensure_streams();
   const DevIndex di = dev_index(ix);
-  const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
 
-  counts_.ensure((size_t)n * sizeof(TopicCount));
-  offs_.ensure((size_t)(n + 1) * sizeof(TopicOff));
-  bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
-  bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
-
-  gslots_.ensure((size_t)n * kGatherCap * sizeof(uint32_t));
-  prof.begin(s);
-  launch_walk(false, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(), s);
-  prof.end("walk", s);
-  hip_check(hipGetLastError(), "k_walk<count>");
-  prof.begin(s);
-  launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
-  prof.end("scan", s);
-  hip_check(hipGetLastError(), "k_scan");
-
-  h_bpre_.resize(nb + 1);
-  hip_check(hipMemcpyAsync(h_bpre_.data(), bpre_.p, (nb + 1) * sizeof(TopicOff), hipMemcpyDeviceToHost, s),
-            "D2H block offsets");
-  uint32_t overflow = 0;
-  hip_check(hipMemcpyAsync(&overflow, err_.as<uint32_t>() + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
-            "D2H overflow");
-  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-  check_err(s);
-  const TopicOff tot = h_bpre_[nb];
-
-  prof.count("topics", n);
-  prof.count("gathers", tot.g);
-  prof.count("reserved_rows", tot.rows);
-  // A topic with more gathers than its count-pass slots: write all gather lists compactly.
-  const uint32_t* gathers = gslots_.as<uint32_t>();
-  uint32_t gstride = kGatherCap;
-  if (overflow) {
-    hip_check(hipMemsetAsync(err_.as<uint32_t>() + 1, 0, sizeof(uint32_t), s), "hipMemsetAsync");
-    gathers_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
-    prof.begin(s);
-    launch_walk(true, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), s);
-    prof.end("walk_fill", s);
-    hip_check(hipGetLastError(), "k_walk<fill>");
-    gathers = gathers_.as<uint32_t>();
-    gstride = 0;
-  }
-
-  // plan output chunks on scan-block boundaries so each chunk's rows fit the budget
-  struct Chunk {
-    uint32_t b0, b1;
+  struct Sub {
+    uint32_t t0, n, nb, blk0;  // first topic, topics, scan blocks, first scan block of the batch
   };
-  std::vector<Chunk> chunks;
-  std::vector<ChunkPlan> plan;
-  std::vector<uint32_t> chunk_of_block(nb);
-  uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1, total_tiles = 0;
-  auto tiles_of = [](uint64_t rows) { return (rows + kCopyTile - 1) / kCopyTile; };
-  for (uint32_t b = 0; b < nb;) {
-    uint32_t e = b + 1;
-    while (e < nb && h_bpre_[e + 1].rows - h_bpre_[b].rows <= chunk_rows_budget_) e++;
-    const TopicOff &lo = h_bpre_[b], &hi = h_bpre_[e];
-    for (uint32_t k = b; k < e; k++) chunk_of_block[k] = (uint32_t)chunks.size();
-    chunks.push_back(Chunk{b, e});
-    ChunkPlan p;
-    p.rows = lo.rows;
-    p.shr = lo.shr;
-    p.inl = lo.inl;
-    p.tile_off = (uint32_t)total_tiles;
-    p.n_tiles0 = (uint32_t)tiles_of(hi.rows - lo.rows);
-    p.n_tiles1 = (uint32_t)tiles_of(hi.shr - lo.shr);
-    p.pad = 0;
-    plan.push_back(p);
-    max_rows = std::max(max_rows, hi.rows - lo.rows);
-    max_shr = std::max(max_shr, hi.shr - lo.shr);
-    max_inl = std::max(max_inl, hi.inl - lo.inl);
-    total_tiles += tiles_of(hi.rows - lo.rows) + tiles_of(hi.shr - lo.shr) + tiles_of(hi.inl - lo.inl);
-    max_topics = std::max<uint64_t>(max_topics, std::min<uint64_t>(n, (uint64_t)e * kScanBlock) - (uint64_t)b * kScanBlock);
-    b = e;
+  const uint32_t sbt = std::max(kScanBlock, subbatch_topics_ / kScanBlock * kScanBlock);
+  const uint32_t S = (n + sbt - 1) / sbt;
+  std::vector<Sub> sub(S);
+  uint32_t nb_all = 0;
+  for (uint32_t b = 0; b < S; b++) {
+    sub[b].t0 = b * sbt;
+    sub[b].n = std::min(n - b * sbt, sbt);
+    sub[b].nb = (sub[b].n + kScanBlock - 1) / kScanBlock;
+    sub[b].blk0 = nb_all;
+    nb_all += sub[b].nb;
   }
-  if (max_rows >= (1ull << 32) || max_shr >= (1ull << 32) || max_inl >= (1ull << 32) || total_tiles >= (1ull << 32))
-    throw HipError{hipErrorInvalidValue, "one scan block's output exceeds 2^32 rows"};
-  const size_t nbuf = chunks.size() > 1 ? 2 : 1;
-  for (size_t k = 0; k < nbuf; k++) {
-    rows_[k].ensure(max_rows * sizeof(SubRec));
-    shr_rows_[k].ensure(max_shr * sizeof(ShrRec));
-    inl_rows_[k].ensure(max_inl * sizeof(InlRec));
-    res_[k].ensure(max_topics * sizeof(mq_topic_result_dev));
-  }
-  desc_.ensure(std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
-  tiles_.ensure(std::max<uint64_t>(total_tiles, 1) * sizeof(uint32_t));
-  plan_.ensure(plan.size() * sizeof(ChunkPlan) + nb * sizeof(uint32_t));
-  h_plan_.resize(plan.size() * sizeof(ChunkPlan) + nb * sizeof(uint32_t));
-  memcpy(h_plan_.data(), plan.data(), plan.size() * sizeof(ChunkPlan));
-  memcpy(h_plan_.data() + plan.size() * sizeof(ChunkPlan), chunk_of_block.data(), nb * sizeof(uint32_t));
-  hip_check(hipMemcpyAsync(plan_.p, h_plan_.data(), h_plan_.size(), hipMemcpyHostToDevice, s), "H2D chunk plan");
-  if (!side_) {
-    hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate");
-    for (int k = 0; k < 2; k++) {
-      hip_check(hipEventCreateWithFlags(&copy_done_[k], hipEventDisableTiming), "hipEventCreate");
-      hip_check(hipEventCreateWithFlags(&merge_done_[k], hipEventDisableTiming), "hipEventCreate");
+  // sub-batch b: offsets at offs_ + t0 + b (n + 1 entries), block sums at blk0 + b (nb + 1)
+  grow(counts_, (size_t)n * sizeof(TopicCount));
+  grow(offs_, (size_t)(n + S) * sizeof(TopicOff));
+  grow(bsum_, (size_t)(nb_all + S) * sizeof(TopicOff));
+  grow(bpre_, (size_t)(nb_all + S) * sizeof(TopicOff));
+  grow(gslots_, (size_t)n * kGatherCap * sizeof(uint32_t));
+  grow(ovf_, (size_t)S * sizeof(uint32_t));
+  pinned((size_t)(nb_all + S) * sizeof(TopicOff) + S * sizeof(uint32_t));
+  const size_t plan_bytes = (size_t)nb_all * (sizeof(ChunkPlan) + sizeof(uint32_t));  // <= one chunk per block
+  grow(plan_, plan_bytes);
+  if (plan_bytes > h_plan_bytes_) {
+    if (h_plan_) {
+      hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(plan)");
+      (void)hipHostFree(h_plan_);
     }
-    hip_check(hipEventCreateWithFlags(&side_done_, hipEventDisableTiming), "hipEventCreate");
+    h_plan_bytes_ = std::max<size_t>(plan_bytes, 1 << 16);
+    hip_check(hipHostMalloc(&h_plan_, h_plan_bytes_, hipHostMallocDefault), "hipHostMalloc");
+  }
+  TopicOff* h_bpre = static_cast<TopicOff*>(h_pin_);
+  uint32_t* h_ovf = reinterpret_cast<uint32_t*>(h_bpre + nb_all + S);
+  while (ev_scan_.size() < S) {
+    hipEvent_t e;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    ev_scan_.push_back(e);
+  }
+  hip_check(hipMemsetAsync(ovf_.p, 0, S * sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
+  hip_check(hipEventRecord(ev_in_, s), "hipEventRecord");  // inputs + the previous batch are done
+  hip_check(hipStreamWaitEvent(wstream_, ev_in_, 0), "hipStreamWaitEvent");
+  for (uint32_t b = 0; b < S; b++) {
+    const Sub& q = sub[b];
+    TopicOff* off_b = offs_.as<TopicOff>() + q.t0 + b;
+    prof.begin(wstream_);
+    launch_walk(false, d_tb, d_to + q.t0, q.n, di, counts_.as<TopicCount>() + q.t0, nullptr,
+                gslots_.as<uint32_t>() + (size_t)q.t0 * kGatherCap, ovf_.as<uint32_t>() + b, wstream_);
+    prof.end("walk", wstream_);
+    hip_check(hipGetLastError(), "k_walk<count>");
+    prof.begin(wstream_);
+    launch_scan(counts_.as<TopicCount>() + q.t0, q.n, bsum_.as<TopicOff>() + q.blk0 + b,
+                bpre_.as<TopicOff>() + q.blk0 + b, off_b, wstream_);
+    prof.end("scan", wstream_);
+    hip_check(hipGetLastError(), "k_scan");
+    hip_check(hipMemcpyAsync(h_bpre + q.blk0 + b, bpre_.as<TopicOff>() + q.blk0 + b, (q.nb + 1) * sizeof(TopicOff),
+                             hipMemcpyDeviceToHost, wstream_), "D2H block offsets");
+    hip_check(hipMemcpyAsync(h_ovf + b, ovf_.as<uint32_t>() + b, sizeof(uint32_t), hipMemcpyDeviceToHost, wstream_),
+              "D2H overflow");
+    hip_check(hipEventRecord(ev_scan_[b], wstream_), "hipEventRecord");
   }
 
-  // every topic's gathers become GDesc records and k_copy tile starts, in one launch
-  DescArgs da;
-  da.ix = di;
-  da.n = n;
-  da.gather_stride = gstride;
-  da.off = offs_.as<TopicOff>();
-  da.gathers = gathers;
-  da.plan = reinterpret_cast<const ChunkPlan*>(plan_.p);
-  da.chunk_of_block = reinterpret_cast<const uint32_t*>(plan_.as<uint8_t>() + plan.size() * sizeof(ChunkPlan));
-  da.desc = desc_.as<GDesc>();
-  da.tiles = tiles_.as<uint32_t>();
-  prof.begin(s);
-  launch_desc(da, s);
-  prof.end("desc", s);
-  hip_check(hipGetLastError(), "k_desc");
-
+  // host results need every sub-batch's totals first (global row offsets)
+  std::vector<TopicOff> base(S + 1, TopicOff{0, 0, 0, 0, 0});
   if (host) {
+    hip_check(hipStreamSynchronize(wstream_), "hipStreamSynchronize");
+    for (uint32_t b = 0; b < S; b++) {
+      base[b + 1] = base[b];
+      const TopicOff& t = h_bpre[sub[b].blk0 + b + sub[b].nb];
+      base[b + 1].rows += t.rows;
+      base[b + 1].shr += t.shr;
+      base[b + 1].inl += t.inl;
+    }
     host->topics.resize(n);
-    host->rows.resize(tot.rows);
-    host->shr.resize(tot.shr);
-    host->inl.resize(tot.inl);
+    host->rows.resize(base[S].rows);
+    host->shr.resize(base[S].shr);
+    host->inl.resize(base[S].inl);
   }
 
-  // Per chunk: k_desc + k_copy on the launch stream, then k_merge (and, for host results, the
-  // D2H copies) on the side stream. Chunk i + 2 reuses chunk i's buffers after its merge.
-  hipStream_t cs = s;  // k_copy stream
-  for (size_t ci = 0; ci < chunks.size(); ci++) {
-    const Chunk& c = chunks[ci];
-    const size_t b = ci % nbuf;
-    const TopicOff& lo = h_bpre_[c.b0];
-    const TopicOff& hi = h_bpre_[c.b1];
-    EmitArgs a;
-    a.ix = di;
-    a.t0 = c.b0 * kScanBlock;
-    a.t1 = std::min<uint64_t>(n, (uint64_t)c.b1 * kScanBlock);
-    a.off = offs_.as<TopicOff>();
-    a.base = lo;
-    a.desc = desc_.as<GDesc>();
-    a.tiles = tiles_.as<uint32_t>() + plan[ci].tile_off;
-    a.total[0] = (uint32_t)(hi.rows - lo.rows);
-    a.total[1] = (uint32_t)(hi.shr - lo.shr);
-    a.total[2] = (uint32_t)(hi.inl - lo.inl);
-    for (int k = 0; k < 3; k++) a.n_tiles[k] = (uint32_t)tiles_of(a.total[k]);
-    a.rows = rows_[b].as<SubRec>();
-    a.shr_rows = shr_rows_[b].as<ShrRec>();
-    a.inl_rows = inl_rows_[b].as<InlRec>();
-    a.res = res_[b].as<mq_topic_result_dev>();
-    a.stats = nullptr;
-    a.tstat = nullptr;
-    a.diag = merge_diag_;
-    if (!tstat_path_.empty()) {
-      if (ci == 0) tstat_.ensure((size_t)n * kTStat * sizeof(uint32_t));
-      a.tstat = tstat_.as<uint32_t>();
-    }
-    if (merge_stats_) {
-      if (!mstats_.p) {
-        mstats_.ensure(4 * sizeof(unsigned long long));
-        hip_check(hipMemsetAsync(mstats_.p, 0, 4 * sizeof(unsigned long long), s), "memset stats");
-      }
-      a.stats = mstats_.as<unsigned long long>();
-    }
-    if (ci >= nbuf) hip_check(hipStreamWaitEvent(cs, merge_done_[b], 0), "hipStreamWaitEvent");
-    prof.begin(cs);
-    launch_copy(a, copy_blocks_, cs);
-    prof.end("copy", cs);
-    hip_check(hipGetLastError(), "k_copy");
-    hipStream_t ms = serial_ ? cs : side_;
-    if (!serial_) {
-      hip_check(hipEventRecord(copy_done_[b], cs), "hipEventRecord");
-      hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
-    }
-    prof.begin(ms);
-    launch_merge(a, merge_blocks_, ms);
-    prof.end("merge", ms);
-    hip_check(hipGetLastError(), "k_merge");
-    prof.count("copy_rows", (uint64_t)a.total[0] + a.total[1] + a.total[2]);
-    prof.count("copy_bytes", 16ull * a.total[0] + 8ull * a.total[1] + 8ull * a.total[2]);
-    prof.count("merge_records", hi.merge - lo.merge);
-    last_chunks_++;
+  struct Chunk {
+    uint32_t sb, b0, b1;  // sub-batch, scan-block range within it
+  };
+  std::vector<Chunk> done;
+  auto tiles_of = [](uint64_t rows) { return (rows + kCopyTile - 1) / kCopyTile; };
+  size_t ci = 0;
+  for (uint32_t sb = 0; sb < S; sb++) {
+    const Sub& q = sub[sb];
+    const uint32_t p = sb & 1;
+    hip_check(hipEventSynchronize(ev_scan_[sb]), "hipEventSynchronize");
+    const TopicOff* hb = h_bpre + q.blk0 + sb;
+    const TopicOff tot = hb[q.nb];
+    const TopicOff* off_b = offs_.as<TopicOff>() + q.t0 + sb;
+    prof.count("topics", q.n);
+    prof.count("gathers", tot.g);
+    prof.count("reserved_rows", tot.rows);
+    hip_check(hipStreamWaitEvent(s, ev_scan_[sb], 0), "hipStreamWaitEvent");
+    // sub-batch sb reuses the desc / tile / plan buffers of sb - 2 once its merges are done
+    if (sb >= 2) hip_check(hipStreamWaitEvent(s, sb_done_[p], 0), "hipStreamWaitEvent");
 
-    const uint32_t nt = a.t1 - a.t0;
-    if (host) {
-      hip_check(hipMemcpyAsync(host->rows.data() + lo.rows, a.rows, (hi.rows - lo.rows) * sizeof(SubRec),
-                               hipMemcpyDeviceToHost, ms), "D2H rows");
-      hip_check(hipMemcpyAsync(host->shr.data() + lo.shr, a.shr_rows, (hi.shr - lo.shr) * sizeof(ShrRec),
-                               hipMemcpyDeviceToHost, ms), "D2H shared rows");
-      hip_check(hipMemcpyAsync(host->inl.data() + lo.inl, a.inl_rows, (hi.inl - lo.inl) * sizeof(InlRec),
-                               hipMemcpyDeviceToHost, ms), "D2H inline rows");
-      hip_check(hipMemcpyAsync(host->topics.data() + a.t0, a.res, nt * sizeof(mq_topic_result),
-                               hipMemcpyDeviceToHost, ms), "D2H topic results");
+    // A topic with more gathers than its count-pass slots: write all gather lists compactly.
+    const uint32_t* gathers = gslots_.as<uint32_t>() + (size_t)q.t0 * kGatherCap;
+    uint32_t gstride = kGatherCap;
+    if (h_ovf[sb]) {
+      grow(gathers_, std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
+      prof.begin(s);
+      launch_walk(true, d_tb, d_to + q.t0, q.n, di, nullptr, off_b, gathers_.as<uint32_t>(), nullptr, s);
+      prof.end("walk_fill", s);
+      hip_check(hipGetLastError(), "k_walk<fill>");
+      gathers = gathers_.as<uint32_t>();
+      gstride = 0;
     }
-    hip_check(hipEventRecord(merge_done_[b], ms), "hipEventRecord");
-    if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
-      unsigned long long m[4];
-      hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, ms), "D2H stats");
-      hip_check(hipStreamSynchronize(ms), "hipStreamSynchronize");
-      fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
+
+    // plan output chunks on scan-block boundaries so each chunk's rows fit the budget
+    std::vector<Chunk> chunks;
+    std::vector<ChunkPlan> plan;
+    std::vector<uint32_t> chunk_of_block(q.nb);
+    uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1, total_tiles = 0;
+    for (uint32_t b = 0; b < q.nb;) {
+      uint32_t e = b + 1;
+      while (e < q.nb && hb[e + 1].rows - hb[b].rows <= chunk_rows_budget_) e++;
+      const TopicOff &lo = hb[b], &hi = hb[e];
+      for (uint32_t k = b; k < e; k++) chunk_of_block[k] = (uint32_t)chunks.size();
+      chunks.push_back(Chunk{sb, b, e});
+      ChunkPlan cp;
+      cp.rows = lo.rows;
+      cp.shr = lo.shr;
+      cp.inl = lo.inl;
+      cp.tile_off = (uint32_t)total_tiles;
+      cp.n_tiles0 = (uint32_t)tiles_of(hi.rows - lo.rows);
+      cp.n_tiles1 = (uint32_t)tiles_of(hi.shr - lo.shr);
+      cp.pad = 0;
+      plan.push_back(cp);
+      max_rows = std::max(max_rows, hi.rows - lo.rows);
+      max_shr = std::max(max_shr, hi.shr - lo.shr);
+      max_inl = std::max(max_inl, hi.inl - lo.inl);
+      total_tiles += tiles_of(hi.rows - lo.rows) + tiles_of(hi.shr - lo.shr) + tiles_of(hi.inl - lo.inl);
+      max_topics = std::max<uint64_t>(max_topics, std::min<uint64_t>(q.n, (uint64_t)e * kScanBlock) - (uint64_t)b * kScanBlock);
+      b = e;
     }
-    out->n_topics = nt;
-    out->topics = reinterpret_cast<const mq_topic_result*>(a.res);
-    out->sub_rows = reinterpret_cast<const mq_client_row*>(a.rows);
-    out->shared_rows = reinterpret_cast<const mq_shared_row*>(a.shr_rows);
-    out->inline_rows = reinterpret_cast<const mq_inline_row*>(a.inl_rows);
-    out->n_sub_rows = hi.rows - lo.rows;
-    out->n_shared_rows = hi.shr - lo.shr;
-    out->n_inline_rows = hi.inl - lo.inl;
+    if (max_rows >= (1ull << 32) || max_shr >= (1ull << 32) || max_inl >= (1ull << 32) || total_tiles >= (1ull << 32))
+      throw HipError{hipErrorInvalidValue, "one scan block's output exceeds 2^32 rows"};
+    for (size_t k = 0; k < 2; k++) {
+      grow(rows_[k], max_rows * sizeof(SubRec));
+      grow(shr_rows_[k], max_shr * sizeof(ShrRec));
+      grow(inl_rows_[k], max_inl * sizeof(InlRec));
+      grow(res_[k], max_topics * sizeof(mq_topic_result_dev));
+    }
+    grow(desc_[p], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
+    grow(tiles_[p], std::max<uint64_t>(total_tiles, 1) * sizeof(uint32_t));
+    // plans of every sub-batch have their own slots (the host runs ahead of the launch stream,
+    // so a pinned slot must not be rewritten before its H2D copy has run)
+    ChunkPlan* hp = static_cast<ChunkPlan*>(h_plan_) + q.blk0;
+    uint32_t* hc = reinterpret_cast<uint32_t*>(static_cast<ChunkPlan*>(h_plan_) + nb_all) + q.blk0;
+    ChunkPlan* dp = plan_.as<ChunkPlan>() + q.blk0;
+    uint32_t* dc = reinterpret_cast<uint32_t*>(plan_.as<ChunkPlan>() + nb_all) + q.blk0;
+    memcpy(hp, plan.data(), plan.size() * sizeof(ChunkPlan));
+    memcpy(hc, chunk_of_block.data(), q.nb * sizeof(uint32_t));
+    hip_check(hipMemcpyAsync(dp, hp, plan.size() * sizeof(ChunkPlan), hipMemcpyHostToDevice, s), "H2D chunk plan");
+    hip_check(hipMemcpyAsync(dc, hc, q.nb * sizeof(uint32_t), hipMemcpyHostToDevice, s), "H2D chunk map");
+
+    // every topic's gathers become GDesc records and k_copy tile starts, in one launch
+    DescArgs da;
+    da.ix = di;
+    da.n = q.n;
+    da.gather_stride = gstride;
+    da.off = off_b;
+    da.gathers = gathers;
+    da.plan = dp;
+    da.chunk_of_block = dc;
+    da.desc = desc_[p].as<GDesc>();
+    da.tiles = tiles_[p].as<uint32_t>();
+    prof.begin(s);
+    launch_desc(da, s);
+    prof.end("desc", s);
+    hip_check(hipGetLastError(), "k_desc");
+
+    // Per chunk: k_copy on the launch stream, then k_merge (and, for host results, the D2H
+    // copies) on the side stream. Chunk i + 2 reuses chunk i's buffers after its merge.
+    hipStream_t ms = serial_ ? s : side_;
+    for (size_t cj = 0; cj < chunks.size(); cj++, ci++) {
+      const Chunk& c = chunks[cj];
+      const size_t b = ci & 1;
+      const TopicOff& lo = hb[c.b0];
+      const TopicOff& hi = hb[c.b1];
+      EmitArgs a;
+      a.ix = di;
+      a.t0 = c.b0 * kScanBlock;
+      a.t1 = std::min<uint64_t>(q.n, (uint64_t)c.b1 * kScanBlock);
+      a.off = off_b;
+      a.base = lo;
+      a.desc = desc_[p].as<GDesc>();
+      a.tiles = tiles_[p].as<uint32_t>() + plan[cj].tile_off;
+      a.total[0] = (uint32_t)(hi.rows - lo.rows);
+      a.total[1] = (uint32_t)(hi.shr - lo.shr);
+      a.total[2] = (uint32_t)(hi.inl - lo.inl);
+      for (int k = 0; k < 3; k++) a.n_tiles[k] = (uint32_t)tiles_of(a.total[k]);
+      a.rows = rows_[b].as<SubRec>();
+      a.shr_rows = shr_rows_[b].as<ShrRec>();
+      a.inl_rows = inl_rows_[b].as<InlRec>();
+      a.res = res_[b].as<mq_topic_result_dev>();
+      a.stats = nullptr;
+      a.tstat = nullptr;
+      a.diag = merge_diag_;
+      if (!tstat_path_.empty()) {
+        if (ci == 0) grow(tstat_, (size_t)n * kTStat * sizeof(uint32_t));
+        a.tstat = tstat_.as<uint32_t>() + (size_t)q.t0 * kTStat;
+      }
+      if (merge_stats_) {
+        if (!mstats_.p) {
+          mstats_.ensure(4 * sizeof(unsigned long long));
+          hip_check(hipMemsetAsync(mstats_.p, 0, 4 * sizeof(unsigned long long), s), "memset stats");
+        }
+        a.stats = mstats_.as<unsigned long long>();
+      }
+      if (ci >= 2) hip_check(hipStreamWaitEvent(s, merge_done_[b], 0), "hipStreamWaitEvent");
+      prof.begin(s);
+      launch_copy(a, copy_blocks_, s);
+      prof.end("copy", s);
+      hip_check(hipGetLastError(), "k_copy");
+      if (!serial_) {
+        hip_check(hipEventRecord(copy_done_[b], s), "hipEventRecord");
+        hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
+      }
+      prof.begin(ms);
+      launch_merge(a, merge_blocks_, ms);
+      prof.end("merge", ms);
+      hip_check(hipGetLastError(), "k_merge");
+      prof.count("copy_rows", (uint64_t)a.total[0] + a.total[1] + a.total[2]);
+      prof.count("copy_bytes", 16ull * a.total[0] + 8ull * a.total[1] + 8ull * a.total[2]);
+      prof.count("merge_records", hi.merge - lo.merge);
+      last_chunks_++;
+
+      const uint32_t nt = a.t1 - a.t0;
+      if (host) {
+        const TopicOff& g = base[sb];
+        hip_check(hipMemcpyAsync(host->rows.data() + g.rows + lo.rows, a.rows, (hi.rows - lo.rows) * sizeof(SubRec),
+                                 hipMemcpyDeviceToHost, ms), "D2H rows");
+        hip_check(hipMemcpyAsync(host->shr.data() + g.shr + lo.shr, a.shr_rows, (hi.shr - lo.shr) * sizeof(ShrRec),
+                                 hipMemcpyDeviceToHost, ms), "D2H shared rows");
+        hip_check(hipMemcpyAsync(host->inl.data() + g.inl + lo.inl, a.inl_rows, (hi.inl - lo.inl) * sizeof(InlRec),
+                                 hipMemcpyDeviceToHost, ms), "D2H inline rows");
+        hip_check(hipMemcpyAsync(host->topics.data() + q.t0 + a.t0, a.res, nt * sizeof(mq_topic_result),
+                                 hipMemcpyDeviceToHost, ms), "D2H topic results");
+      }
+      hip_check(hipEventRecord(merge_done_[b], ms), "hipEventRecord");
+      if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
+        unsigned long long m[4];
+        hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, ms), "D2H stats");
+        hip_check(hipStreamSynchronize(ms), "hipStreamSynchronize");
+        fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
+      }
+      out->n_topics = nt;
+      out->topics = reinterpret_cast<const mq_topic_result*>(a.res);
+      out->sub_rows = reinterpret_cast<const mq_client_row*>(a.rows);
+      out->shared_rows = reinterpret_cast<const mq_shared_row*>(a.shr_rows);
+      out->inline_rows = reinterpret_cast<const mq_inline_row*>(a.inl_rows);
+      out->n_sub_rows = hi.rows - lo.rows;
+      out->n_shared_rows = hi.shr - lo.shr;
+      out->n_inline_rows = hi.inl - lo.inl;
+      done.push_back(c);
+    }
+    hip_check(hipEventRecord(sb_done_[p], ms), "hipEventRecord");
   }
   // the launch stream completes only after the side stream's work of this batch
   hip_check(hipEventRecord(side_done_, side_), "hipEventRecord");
@@ -514,14 +620,16 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   }
   if (host) {
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    for (const Chunk& c : chunks) {
-      const TopicOff& lo = h_bpre_[c.b0];
-      const uint32_t t0 = c.b0 * kScanBlock, t1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)c.b1 * kScanBlock);
+    for (const Chunk& c : done) {
+      const Sub& q = sub[c.sb];
+      const TopicOff& lo = h_bpre[q.blk0 + c.sb + c.b0];
+      const TopicOff& g = base[c.sb];
+      const uint32_t t0 = c.b0 * kScanBlock, t1 = (uint32_t)std::min<uint64_t>(q.n, (uint64_t)c.b1 * kScanBlock);
       for (uint32_t t = t0; t < t1; t++) {
-        mq_topic_result& r = host->topics[t];
-        r.sub_base += lo.rows;
-        r.shared_base += lo.shr;
-        r.inline_base += lo.inl;
+        mq_topic_result& r = host->topics[q.t0 + t];
+        r.sub_base += g.rows + lo.rows;
+        r.shared_base += g.shr + lo.shr;
+        r.inline_base += g.inl + lo.inl;
       }
     }
     check_err(s);

@@ -136,9 +136,22 @@ class Device {
   // Output chunks alternate between two buffer sets so that k_merge of chunk i (side stream)
   // overlaps k_desc/k_copy of chunk i + 1 (launch stream).
   DevBuf rows_[2], shr_rows_[2], inl_rows_[2], res_[2];
-  DevBuf tiles_, plan_;  // the batch's k_copy tile table; chunk plans + block -> chunk map
-  std::vector<uint8_t> h_plan_;
-  DevBuf err_, desc_;
+  // per sub-batch parity: gather records and k_copy tile table
+  DevBuf desc_[2], tiles_[2];
+  // chunk plans + block -> chunk maps of every sub-batch ([nb_all] plans, then [nb_all] u32)
+  DevBuf plan_;
+  void* h_plan_ = nullptr;  // their pinned staging
+  size_t h_plan_bytes_ = 0;
+  void* h_pin_ = nullptr;  // pinned: block offsets + overflow flags of every sub-batch
+  size_t h_pin_bytes_ = 0;
+  DevBuf ovf_;             // per sub-batch gather-slot overflow flags
+  hipStream_t wstream_ = nullptr;  // walk + scan of the sub-batches
+  hipEvent_t ev_in_ = nullptr, sb_done_[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev_scan_;
+  uint32_t subbatch_topics_ = kSubBatchTopics;
+  void ensure_streams();
+  void pinned(size_t bytes);
+  DevBuf err_;
   hipStream_t side_ = nullptr;
   hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_, mstats_;

@@ -9,6 +9,7 @@ namespace mq {
 
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
+constexpr uint32_t kSubBatchTopics = 1u << 22;  // topics per pipelined sub-batch (Device::match)
 constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves per tile
 constexpr uint32_t kCopyBlocksPerCU = 8;   // persistent k_copy: 256-thread workgroups per CU
 constexpr uint32_t kMergeBlocksPerCU = 8;  // persistent k_merge beside it (side stream)
@@ -116,7 +117,7 @@ struct DescArgs {
 };
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
-                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, hipStream_t s);
+                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_desc(const DescArgs& a, hipStream_t s);

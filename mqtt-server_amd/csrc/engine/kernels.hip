@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
                                               const uint64_t* __restrict__ to, uint32_t n,
                                               DevIndex ix, TopicCount* __restrict__ cnt,
                                               const TopicOff* __restrict__ off,
-                                              uint32_t* __restrict__ gathers) {
+                                              uint32_t* __restrict__ gathers, uint32_t* __restrict__ ovf) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const uint64_t b0 = to[t], b1 = to[t + 1];
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
     c.inlines = inl;
     c.merge = merge;
     cnt[t] = c;
-    if (ng > kGatherCap) atomicOr(ix.err + 1, 1u);
+    if (ng > kGatherCap) atomicOr(ovf, 1u);
   }
 }
 
@@ -800,13 +800,13 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
 namespace mq {
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
-                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, hipStream_t s) {
+                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf, hipStream_t s) {
   if (!n) return;
   dim3 grid((n + 255) / 256);
   if (fill)
-    hipLaunchKernelGGL(k_walk<true>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers);
+    hipLaunchKernelGGL(k_walk<true>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf);
   else
-    hipLaunchKernelGGL(k_walk<false>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers);
+    hipLaunchKernelGGL(k_walk<false>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf);
 }
 
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,

@@ -196,6 +196,36 @@ def test_chunked_outputs(gpu_available, monkeypatch):
     assert eng.match_chunks() > 1
 
 
+def test_subbatch_pipeline(gpu_available, monkeypatch):
+    """Batches cut into pipelined sub-batches (walk of sub-batch b + 1 under the copies of b),
+    each with several output chunks: results identical to the oracle."""
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(50000, 5000, seed=43)
+    tb, to = W.gen_topics(w, 30000, seed=44)
+    monkeypatch.setenv("MQ_SUBBATCH_TOPICS", "4096")
+    monkeypatch.setenv("MQ_CHUNK_ROWS", "300000")
+    _digest_parity(eng, orc, tb, to)
+    assert eng.match_chunks() >= 8
+    monkeypatch.setenv("MQ_SUBBATCH_TOPICS", "1024")  # one scan block per sub-batch
+    _digest_parity(eng, orc, tb, to[:5001])
+
+
+def test_subbatch_gather_overflow(gpu_available, monkeypatch):
+    """Gather-slot overflow (compact fill pass) in some sub-batches only."""
+    monkeypatch.setenv("MQ_SUBBATCH_TOPICS", "1024")
+    e, o = EngineAdapter(), OracleAdapter()
+    levels = [f"l{i}" for i in range(80)]
+    for d in range(1, 80):
+        f = "/".join(levels[:d]) + "/#"
+        assert e.subscribe(f"c{d % 7}", f, identifier=d) == o.subscribe(f"c{d % 7}", f, identifier=d)
+    deep = "/".join(levels)
+    topics = [f"l0/x{i}" for i in range(3000)] + [deep] * 3 + ["/".join(levels[:5])] * 2000
+    got = e.subscribers_batch(topics)
+    for t in (topics[0], deep, topics[-1]):
+        assert got[topics.index(t)] == o.subscribers(t), t
+    assert got[3000] == got[3002]
+
+
 def test_match_device_stream(gpu_available):
     """mq_match_device on torch-owned device buffers and a torch stream."""
     import torch
