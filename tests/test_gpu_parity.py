@@ -143,7 +143,8 @@ def _digest_parity(eng, orc, tb, to):
     return cnt
 
 
-@pytest.mark.parametrize("n_subs,n_clients,n_topics", [(10000, 1000, 20000), (200000, 20000, 20000)])
+@pytest.mark.parametrize("n_subs,n_clients,n_topics", [(10000, 1000, 20000), (200000, 20000, 20000),
+                                                     (1000000, 100000, 6000)])
 def test_workload_digest_parity(n_subs, n_clients, n_topics, gpu_available):
     from mqmatch import workload as W
     w, eng, orc = _workload_pair(n_subs, n_clients, seed=11)
@@ -224,6 +225,25 @@ def test_subbatch_gather_overflow(gpu_available, monkeypatch):
     for t in (topics[0], deep, topics[-1]):
         assert got[topics.index(t)] == o.subscribers(t), t
     assert got[3000] == got[3002]
+
+
+def test_hot_lists(gpu_available):
+    """Lists of >= 1024 subscriptions (root '#', 'a/#') take the node-major copy (k_hot); some of
+    their clients also hold co-matching filters (merge bases / ident rows inside hot lists)."""
+    e, o = EngineAdapter(), OracleAdapter()
+    for i in range(3000):
+        c = f"h{i}"
+        assert e.subscribe(c, "#", qos=i % 3, identifier=i % 5) == o.subscribe(c, "#", qos=i % 3, identifier=i % 5)
+        if i % 2:
+            assert e.subscribe(c, "a/#", identifier=i % 7) == o.subscribe(c, "a/#", identifier=i % 7)
+        if i % 5 == 0:
+            assert e.subscribe(c, "a/+/c", qos=2) == o.subscribe(c, "a/+/c", qos=2)
+    for i in range(1500):
+        c = f"k{i}"
+        assert e.subscribe(c, "a/b/c") == o.subscribe(c, "a/b/c")
+    topics = (["a/b/c", "a/x", "b", "$SYS/x", "a", "a/b/c/d"] * 50)[:300]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
 
 
 def test_match_device_stream(gpu_available):
