@@ -1,7 +1,7 @@
 # Parity, then interleaved knob sweep (tools/tune.py) at 1M and 10M.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-D=gpurun_out/tune12
+D=gpurun_out/tune13
 mkdir -p $D
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $D/pytest_gpu.log 2>&1 || exit 1
 C="MQ_COPY_BLOCKS_PER_CU=8; MQ_COPY_BLOCKS_PER_CU=0; MQ_SERIAL=1"

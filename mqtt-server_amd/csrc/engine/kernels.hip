@@ -30,40 +30,98 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Byte reader with a one-chunk register cache: one 16-byte load serves 16 sequential byte
-// reads. The topic buffer must be readable up to its next 16-byte boundary (include/mqmatch.h).
+// reads. The topic buffer must be readable up to its next 16-byte boundary (include/mqmatch.h):
+// every chunk this reader loads holds at least one byte of the buffer.
 struct ByteReader {
   const uint8_t* base;
   uint64_t ci;
   u32x4 c;
   __device__ __forceinline__ explicit ByteReader(const uint8_t* b) : base(b), ci(~0ull) {}
-  __device__ __forceinline__ uint32_t at(uint64_t i) {
-    const uint64_t k = i >> 4;
+  __device__ __forceinline__ u32x4 chunk(uint64_t k) {
     if (k != ci) {
       c = *reinterpret_cast<const u32x4*>(base + (k << 4));
       ci = k;
     }
+    return c;
+  }
+  __device__ __forceinline__ uint32_t at(uint64_t i) {
+    const u32x4 v = chunk(i >> 4);
     const uint32_t w = ((uint32_t)i >> 2) & 3;
-    const uint32_t word = w == 0 ? c.x : (w == 1 ? c.y : (w == 2 ? c.z : c.w));
+    const uint32_t word = w == 0 ? v.x : (w == 1 ? v.y : (w == 2 ? v.z : v.w));
     return (word >> (((uint32_t)i & 3) * 8)) & 0xffu;
   }
 };
 
-// Scan the segment that starts at s: returns the position of its terminating '/' (or end) and
-// its key (layout.h) in the same pass.
-__device__ __forceinline__ uint64_t scan_segment(ByteReader& R, uint64_t s, uint64_t end, SegKey* key) {
-  SegKeyBuilder kb;
-  uint64_t i = s;
-  for (; i < end; i++) {
-    const uint32_t ch = R.at(i);
-    if (ch == '/') break;
-    kb.push(ch);
-  }
-  *key = kb.finish();
-  return i;
+// SWAR segment scanning: a 16-byte chunk is searched for '/' with exact per-byte zero tests, so
+// the walk does per-chunk rather than per-byte work; only segments longer than 15 bytes (hashed
+// keys) are read byte by byte.
+__device__ __forceinline__ uint32_t slash_nibble(uint32_t w) {  // bit i: byte i of w is '/'
+  const uint32_t x = w ^ 0x2F2F2F2Fu;
+  const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 where byte == 0
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+__device__ __forceinline__ uint32_t slash_mask(const u32x4& c) {  // bit i: byte i of the chunk is '/'
+  return slash_nibble(c.x) | (slash_nibble(c.y) << 4) | (slash_nibble(c.z) << 8) | (slash_nibble(c.w) << 12);
 }
 
+// First '/' in [s, end), or end. Bytes past `end` belong to the next topic.
+__device__ __forceinline__ uint64_t find_slash(ByteReader& R, uint64_t s, uint64_t end) {
+  if (s >= end) return end;
+  uint64_t k = s >> 4;
+  uint32_t m = slash_mask(R.chunk(k)) & (0xFFFFu << (s & 15));
+  for (;;) {
+    if (m) return min((k << 4) + (uint64_t)(__ffs(m) - 1), end);
+    k++;
+    if ((k << 4) >= end) return end;
+    m = slash_mask(R.chunk(k));
+  }
+}
+
+// Start of the segment that ends at e: one past the last '/' in [b0, e), or b0.
 __device__ __forceinline__ uint64_t seg_start_before(ByteReader& R, uint64_t b0, uint64_t e) {
-  while (e > b0 && R.at(e - 1) != '/') e--;
+  if (e <= b0) return b0;
+  uint64_t k = (e - 1) >> 4;
+  const uint32_t top = (uint32_t)((e - 1) & 15);
+  uint32_t m = slash_mask(R.chunk(k)) & (top == 15 ? 0xFFFFu : ((2u << top) - 1u));
+  for (;;) {
+    if (m) return max((k << 4) + (uint64_t)(31 - __clz(m)) + 1, b0);
+    if ((k << 4) <= b0) return b0;
+    k--;
+    m = slash_mask(R.chunk(k));
+  }
+}
+
+// Key (layout.h) of the segment [s, e): inline segments (<= 15 bytes) are cut out of at most two
+// chunks with funnel shifts; longer ones take the byte-wise hash of SegKeyBuilder.
+__device__ __forceinline__ SegKey key_of(ByteReader& R, uint64_t s, uint64_t e) {
+  const uint32_t len = (uint32_t)(e - s);
+  if (len > kInlineSegMax) {
+    SegKeyBuilder kb;
+    for (uint64_t i = s; i < e; i++) kb.push(R.at(i));
+    return kb.finish();
+  }
+  if (len == 0) return SegKey{0, 0};
+  const uint64_t k = s >> 4;
+  const u32x4 c0 = R.chunk(k);
+  const u32x4 c1 = ((e - 1) >> 4) != k ? R.chunk(k + 1) : u32x4{0u, 0u, 0u, 0u};
+  const uint64_t q0 = c0.x | (uint64_t)c0.y << 32, q1 = c0.z | (uint64_t)c0.w << 32;
+  const uint64_t q2 = c1.x | (uint64_t)c1.y << 32, q3 = c1.z | (uint64_t)c1.w << 32;
+  const uint32_t o = (uint32_t)(s & 15);
+  const uint64_t a = o >= 8 ? q1 : q0, b = o >= 8 ? q2 : q1, c = o >= 8 ? q3 : q2;
+  const uint32_t sh = (o & 7) * 8;
+  uint64_t v0 = sh ? (a >> sh) | (b << (64 - sh)) : a;
+  uint64_t v1 = sh ? (b >> sh) | (c << (64 - sh)) : b;
+  if (len < 8) v0 &= (1ull << (8 * len)) - 1;
+  const uint32_t lb = len > 8 ? len - 8 : 0;  // <= 7 bytes in k1
+  v1 = lb ? v1 & ((1ull << (8 * lb)) - 1) : 0ull;
+  return SegKey{v0, v1 | ((uint64_t)len << 56)};
+}
+
+// Scan the segment that starts at s: returns the position of its terminating '/' (or end) and
+// its key (layout.h).
+__device__ __forceinline__ uint64_t scan_segment(ByteReader& R, uint64_t s, uint64_t end, SegKey* key) {
+  const uint64_t e = find_slash(R, s, end);
+  *key = key_of(R, s, e);
   return e;
 }
 
