@@ -188,6 +188,17 @@ def main():
         b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"] + 16 * per_topic["S"] + 16 * per_topic["O"]
         out["alg_bytes_per_topic"] = {"B": b_topic, "L": per_topic["L"], "P": per_topic["P"],
                                       "S": per_topic["S"], "O": per_topic["O"], "sample_topics": ns}
+        # End-to-end through the host-buffer boundary (mq_match_batch: H2D of the topics, the
+        # kernels, D2H of every result row into host memory) on a bounded sample: PCIe-bound,
+        # reported beside `value`, never as it.
+        ne = min(n, 20000)
+        eng.match_batch_rows(tb, to[:ne + 1])
+        t0 = time.perf_counter()
+        rows = eng.match_batch_rows(tb, to[:ne + 1])
+        dt = time.perf_counter() - t0
+        out["end_to_end"] = {"value": ne / dt, "unit": "publishes/s", "sample_topics": ne,
+                             "result_bytes": 16 * rows[0] + 8 * rows[1] + 8 * rows[2],
+                             "GBps_to_host": (16 * rows[0] + 8 * rows[1] + 8 * rows[2]) / dt / 1e9}
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)

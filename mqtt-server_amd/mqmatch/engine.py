@@ -308,6 +308,18 @@ class Engine:
         _check(lib().mq_index_stats(self.h, C.byref(s)), "mq_index_stats")
         return {n: getattr(s, n) for n, _ in Stats._fields_ if n != "reserved"}
 
+    def match_batch_rows(self, bytes_, offs):
+        """mq_match_batch with its results left in the library's host buffers (freed here):
+        the end-to-end path (H2D topics, kernels, D2H of every row). Returns the row counts."""
+        n = len(offs) - 1
+        rp = C.POINTER(MatchResult)()
+        _check(lib().mq_match_batch(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)),
+               "mq_match_batch")
+        r = rp.contents
+        counts = (int(r.n_sub_rows), int(r.n_shared_rows), int(r.n_inline_rows))
+        lib().mq_result_free(rp)
+        return counts
+
     def match_batch(self, bytes_, offs):
         """mq_match_batch -> dict of numpy arrays (host copies)."""
         n = len(offs) - 1
