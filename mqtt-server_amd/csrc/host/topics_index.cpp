@@ -36,6 +36,7 @@ uint32_t TopicsIndex::fid(const std::string& f) {
 }
 
 bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) {
+  std::lock_guard<std::mutex> lk(mu_);
   const uint32_t c = cid(client), f = fid(sub.Filter);
   const uint8_t flags = (sub.NoLocal ? MQ_SUB_NOLOCAL : 0) | (sub.RetainAsPublished ? MQ_SUB_RAP : 0) |
                         (uint8_t)((sub.RetainHandling & 3) << MQ_SUB_RH_SHIFT);
@@ -50,12 +51,14 @@ bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) 
 }
 
 bool TopicsIndex::Unsubscribe(const std::string& filter, const std::string& client) {
+  std::lock_guard<std::mutex> lk(mu_);
   const int rc = mq_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), cid(client));
   check(rc, "mq_unsubscribe");
   return rc == 1;
 }
 
 bool TopicsIndex::InlineSubscribe(const InlineSubscription& sub) {
+  std::lock_guard<std::mutex> lk(mu_);
   const uint32_t f = fid(sub.Sub.Filter);
   const int rc = mq_inline_subscribe(idx_, sub.Sub.Filter.data(), (uint32_t)sub.Sub.Filter.size(),
                                      sub.Sub.Identifier, f);
@@ -65,6 +68,7 @@ bool TopicsIndex::InlineSubscribe(const InlineSubscription& sub) {
 }
 
 bool TopicsIndex::InlineUnsubscribe(int id, const std::string& filter) {
+  std::lock_guard<std::mutex> lk(mu_);
   const int rc = mq_inline_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), id);
   check(rc, "mq_inline_unsubscribe");
   return rc == 1;
@@ -99,6 +103,7 @@ std::vector<uint64_t> TopicsIndex::Messages(const std::string& filter) {
 Subscribers TopicsIndex::Subscribers_(const std::string& topic) { return SubscribersBatch({topic})[0]; }
 
 std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::string>& topics) {
+  std::lock_guard<std::mutex> lk(mu_);
   std::string bytes;
   std::vector<uint64_t> offs(1, 0);
   for (const std::string& t : topics) {

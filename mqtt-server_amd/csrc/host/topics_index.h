@@ -8,6 +8,7 @@
 
 #include <cstdint>
 #include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -107,6 +108,7 @@ class TopicsIndex {
   uint32_t cid(const std::string& c);
   uint32_t fid(const std::string& f);
   mq_index* idx_ = nullptr;
+  mutable std::mutex mu_;  // the host tables; every public method is thread-safe
   std::unordered_map<std::string, uint32_t> client_ids_, filter_ids_;
   std::vector<std::string> clients_, filters_;
   std::map<std::pair<uint32_t, uint32_t>, Subscription> stored_;  // (client, filter)

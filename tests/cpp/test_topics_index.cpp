@@ -8,7 +8,12 @@
 #include <string>
 #include <vector>
 
+#include "publish_batcher.h"
 #include "topics_index.h"
+
+#include <future>
+#include <random>
+#include <thread>
 
 using mq::host::InlineSubscription;
 using mq::host::Subscription;
@@ -196,6 +201,84 @@ static void TestMergeSharedSelected() {  // topics_test.go:568-588
   REQUIRE((s.Subscriptions.at("cl2").Identifiers == std::map<std::string, int>{{"$SHARE/tmp2/a/b/c", 111}, {"a/b/c", 112}}));
 }
 
+static bool same_sub(const Subscription& a, const Subscription& b) {
+  return a.Filter == b.Filter && a.Identifier == b.Identifier && a.HasIdentifiers == b.HasIdentifiers &&
+         a.Identifiers == b.Identifiers && a.RetainHandling == b.RetainHandling && a.Qos == b.Qos &&
+         a.RetainAsPublished == b.RetainAsPublished && a.NoLocal == b.NoLocal;
+}
+
+template <class M>
+static bool same_map(const M& a, const M& b) {
+  if (a.size() != b.size()) return false;
+  for (auto ia = a.begin(), ib = b.begin(); ia != a.end(); ++ia, ++ib)
+    if (ia->first != ib->first || !same_sub(ia->second, ib->second)) return false;
+  return true;
+}
+
+static bool same(const mq::host::Subscribers& a, const mq::host::Subscribers& b) {
+  if (!same_map(a.Subscriptions, b.Subscriptions) || a.Shared.size() != b.Shared.size() ||
+      a.InlineSubscriptions.size() != b.InlineSubscriptions.size())
+    return false;
+  for (auto ia = a.Shared.begin(), ib = b.Shared.begin(); ia != a.Shared.end(); ++ia, ++ib)
+    if (ia->first != ib->first || !same_map(ia->second, ib->second)) return false;
+  for (auto ia = a.InlineSubscriptions.begin(), ib = b.InlineSubscriptions.begin(); ia != a.InlineSubscriptions.end();
+       ++ia, ++ib)
+    if (ia->first != ib->first || !same_sub(ia->second.Sub, ib->second.Sub)) return false;
+  return true;
+}
+
+// The publish batching stage: 8 producer threads submit topics concurrently; every future holds
+// exactly what Subscribers(topic) returns, and the stage really batched them.
+static void TestPublishBatcher() {
+  TopicsIndex ix;
+  std::mt19937 r(7);
+  const char* segs[] = {"a", "b", "c", "d", "+", "#"};
+  std::vector<std::string> filters;
+  for (int i = 0; i < 400; i++) {
+    std::string f;
+    const int n = 1 + (int)(r() % 4);
+    for (int k = 0; k < n; k++) {
+      std::string sg = segs[r() % (k + 1 == n ? 6 : 5)];
+      f += (k ? "/" : "") + sg;
+    }
+    if (i % 10 == 0) f = "$share/g" + std::to_string(i % 3) + "/" + f;
+    ix.Subscribe("c" + std::to_string(r() % 50), S(f, (uint8_t)(r() % 3), (int)(r() % 4)));
+  }
+  InlineSubscription in;
+  in.Sub.Filter = "a/#";
+  in.Sub.Identifier = 9;
+  ix.InlineSubscribe(in);
+  std::vector<std::string> topics;
+  for (int i = 0; i < 64; i++) {
+    std::string t;
+    const int n = 1 + (int)(r() % 4);
+    for (int k = 0; k < n; k++) t += (k ? "/" : "") + std::string(segs[r() % 4]);
+    topics.push_back(t);
+  }
+  std::vector<std::vector<std::future<mq::host::Subscribers>>> futs(8);
+  {
+    mq::host::PublishBatcher b(ix, 4096, std::chrono::microseconds(2000));
+    std::vector<std::thread> th;
+    for (int w = 0; w < 8; w++)
+      th.emplace_back([&, w] {
+        for (int i = 0; i < 500; i++) futs[w].push_back(b.Submit(topics[(w * 7 + i) % topics.size()]));
+      });
+    for (auto& t : th) t.join();
+    for (auto& fv : futs)
+      for (auto& f : fv) f.wait();
+    const auto st = b.stats();
+    REQUIRE(st.topics == 4000);
+    REQUIRE(st.batches < st.topics);  // publishes were matched in batches
+    std::printf("publish batcher: %llu topics in %llu batches (largest %llu)\n",
+                (unsigned long long)st.topics, (unsigned long long)st.batches, (unsigned long long)st.largest);
+  }
+  for (int w = 0; w < 8; w++)
+    for (int i = 0; i < 500; i++) {
+      const std::string& t = topics[(w * 7 + i) % topics.size()];
+      REQUIRE(same(futs[w][i].get(), ix.Subscribers_(t)));
+    }
+}
+
 int main() {
   try {
     TestSubscribe();
@@ -208,6 +291,7 @@ int main() {
     TestInline();
     TestPublishToSubscribersIdentifiers();
     TestMergeSharedSelected();
+    TestPublishBatcher();
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 2;
