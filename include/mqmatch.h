@@ -185,6 +185,17 @@ int mq_match_batch(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* of
  * chunk (out->n_topics); mq_match_chunks() reports the chunk count of the last call. */
 int mq_match_device(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t* d_offsets,
                     uint32_t n, void* hip_stream, mq_match_result* out);
+/* Device-resident results of every chunk: like mq_match_device, and for each output chunk, once
+ * its kernels are queued, fn(user, chunk, first_topic, chunk_stream) is called on the calling
+ * thread. `chunk` holds device pointers (row offsets relative to the chunk) of topics
+ * [first_topic, first_topic + chunk->n_topics); they stay valid for work the consumer enqueues
+ * on `chunk_stream` before returning (e.g. a device-side fan-out or a D2H copy): the buffers are
+ * reused only after that work. Replaces the reference's per-topic Subscribers() for GPU-side
+ * consumers (topics.go:583). C consumers only: the Go shim uses mq_match_batch (no callbacks
+ * into Go). */
+typedef void (*mq_chunk_fn)(void* user, const mq_match_result* chunk, uint32_t first_topic, void* chunk_stream);
+int mq_match_device_chunks(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t* d_offsets, uint32_t n,
+                           void* hip_stream, mq_chunk_fn fn, void* user);
 uint32_t mq_match_chunks(const mq_index* idx);
 
 /* ---- batched reverse retained scan: TopicsIndex.Messages (topics.go:525-579) ---- */

@@ -206,6 +206,16 @@ int mq_match_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, ui
   });
 }
 
+int mq_match_device_chunks(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
+                           mq_chunk_fn fn, void* user) {
+  if (n && !d_to) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    mq_match_result last;
+    idx->device().match(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, nullptr, &last, fn, user);
+    return 0;
+  });
+}
+
 uint32_t mq_match_chunks(const mq_index* idx) {
   return idx && idx->dev ? idx->dev->last_chunks() : 0;
 }

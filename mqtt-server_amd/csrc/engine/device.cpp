@@ -327,7 +327,7 @@ void Device::pinned(size_t bytes) {
 // lands and queues k_desc/k_copy (launch stream) and k_merge (side stream), so the walks of the
 // later sub-batches run under the copies of the earlier ones.
 void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                   HostMatch* host, mq_match_result* out) {
+                   HostMatch* host, mq_match_result* out, mq_chunk_fn fn, void* user) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   read_knobs();
   sync(ix, s);
@@ -587,6 +587,17 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipMemcpyAsync(host->topics.data() + q.t0 + a.t0, a.res, nt * sizeof(mq_topic_result),
                                  hipMemcpyDeviceToHost, ms), "D2H topic results");
       }
+      mq_match_result cr;
+      memset(&cr, 0, sizeof(cr));
+      cr.n_topics = nt;
+      cr.topics = reinterpret_cast<const mq_topic_result*>(a.res);
+      cr.sub_rows = reinterpret_cast<const mq_client_row*>(a.rows);
+      cr.shared_rows = reinterpret_cast<const mq_shared_row*>(a.shr_rows);
+      cr.inline_rows = reinterpret_cast<const mq_inline_row*>(a.inl_rows);
+      cr.n_sub_rows = hi.rows - lo.rows;
+      cr.n_shared_rows = hi.shr - lo.shr;
+      cr.n_inline_rows = hi.inl - lo.inl;
+      if (fn) fn(user, &cr, q.t0 + a.t0, ms);  // the consumer's work precedes the buffer's reuse
       hip_check(hipEventRecord(merge_done_[b], ms), "hipEventRecord");
       if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
         unsigned long long m[4];
@@ -594,14 +605,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipStreamSynchronize(ms), "hipStreamSynchronize");
         fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
       }
-      out->n_topics = nt;
-      out->topics = reinterpret_cast<const mq_topic_result*>(a.res);
-      out->sub_rows = reinterpret_cast<const mq_client_row*>(a.rows);
-      out->shared_rows = reinterpret_cast<const mq_shared_row*>(a.shr_rows);
-      out->inline_rows = reinterpret_cast<const mq_inline_row*>(a.inl_rows);
-      out->n_sub_rows = hi.rows - lo.rows;
-      out->n_shared_rows = hi.shr - lo.shr;
-      out->n_inline_rows = hi.inl - lo.inl;
+      *out = cr;
       done.push_back(c);
     }
     hip_check(hipEventRecord(sb_done_[p], ms), "hipEventRecord");

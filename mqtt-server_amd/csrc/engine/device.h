@@ -91,8 +91,10 @@ class Device {
   void sync(Index& ix, hipStream_t s);
   // Match n topics resident on the device. Fills `out` with device pointers of the last chunk;
   // when `host` is set every chunk's rows are also copied into it (global offsets).
+  // fn (optional): per-chunk consumer (mq_match_device_chunks), called before the chunk's
+  // buffers are released for reuse.
   void match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-             HostMatch* host, mq_match_result* out);
+             HostMatch* host, mq_match_result* out, mq_chunk_fn fn = nullptr, void* user = nullptr);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
                 HostMsg* host, mq_msg_result* out);

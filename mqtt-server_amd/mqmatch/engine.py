@@ -72,8 +72,10 @@ EXPORTS = [
     "mq_retained_delete", "mq_retained_len", "mq_subscribe_bulk", "mq_retain_bulk",
     "mq_match_batch", "mq_match_device", "mq_match_chunks", "mq_messages_batch",
     "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
-    "mq_profile_read", "mq_profile_reset", "mq_index_check",
+    "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
 ]
+
+CHUNK_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(MatchResult), C.c_uint32, C.c_void_p)
 
 _LIB = None
 
@@ -112,6 +114,7 @@ def lib():
         "mq_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MatchResult))]),
         "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
         "mq_match_chunks": (C.c_uint32, [vp]),
+        "mq_match_device_chunks": (C.c_int, [vp, vp, vp, C.c_uint32, vp, CHUNK_FN, vp]),
         "mq_messages_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MsgResult))]),
         "mq_messages_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MsgResult)]),
         "mq_result_free": (None, [vp]),
@@ -385,6 +388,13 @@ class Engine:
                                      C.c_void_p(stream) if stream else None, C.byref(r)),
                "mq_match_device")
         return r
+
+    def match_device_chunks(self, d_bytes, d_offs, n, stream, fn):
+        """mq_match_device_chunks: fn(chunk: MatchResult, first_topic, chunk_stream) per chunk."""
+        cb = CHUNK_FN(lambda user, chunk, first, cs: fn(chunk.contents, int(first), cs))
+        _check(lib().mq_match_device_chunks(self.h, C.c_void_p(d_bytes), C.c_void_p(d_offs), n,
+                                            C.c_void_p(stream) if stream else None, cb, None),
+               "mq_match_device_chunks")
 
     def match_chunks(self):
         return int(lib().mq_match_chunks(self.h))

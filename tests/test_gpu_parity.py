@@ -246,6 +246,48 @@ def test_hot_lists(gpu_available):
         assert g == o.subscribers(t), t
 
 
+def test_match_device_chunks_consumer(gpu_available, monkeypatch):
+    """mq_match_device_chunks: a consumer copying every chunk to the host on the chunk stream
+    sees exactly mq_match_batch's rows and per-topic records."""
+    import ctypes as C
+    import torch
+    from mqmatch import workload as W
+    monkeypatch.setenv("MQ_CHUNK_ROWS", "150000")
+    w, eng, orc = _workload_pair(50000, 5000, seed=45)
+    tb, to = W.gen_topics(w, 20000, seed=46)
+    n = len(to) - 1
+    host = eng.match_batch(tb, to)
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+    hip.hipMemcpyAsync.restype = C.c_int
+    rows = np.zeros((len(host["rows"]), 4), np.uint32)
+    topics = np.zeros((n, 12), np.uint32)
+    bases = []
+
+    def consume(chunk, first, stream):
+        r0 = sum(c for _, _, c in bases)
+        if chunk.n_sub_rows:
+            assert hip.hipMemcpyAsync(rows[r0:].ctypes.data, chunk.sub_rows, chunk.n_sub_rows * 16, 2, stream) == 0
+        assert hip.hipMemcpyAsync(topics[first:].ctypes.data, chunk.topics, chunk.n_topics * 48, 2, stream) == 0
+        bases.append((first, chunk.n_topics, chunk.n_sub_rows))
+
+    d_tb = torch.from_numpy(tb).cuda()
+    d_to = torch.from_numpy(to.view(np.int64)).cuda()
+    s = torch.cuda.Stream()
+    eng.match_device_chunks(d_tb.data_ptr(), d_to.data_ptr(), n, s.cuda_stream, consume)
+    torch.cuda.synchronize()
+    assert len(bases) == eng.match_chunks() > 2
+    assert (rows == host["rows"]).all()
+    sub_base = topics[:, 0].astype(np.uint64) | (topics[:, 1].astype(np.uint64) << np.uint64(32))
+    r0 = 0
+    for first, nt, nr in bases:
+        sub_base[first:first + nt] += np.uint64(r0)
+        r0 += nr
+    assert (sub_base == host["sub_base"]).all()
+    assert (topics[:, 6] == host["sub_cap"]).all() and (topics[:, 7] == host["n_client"]).all()
+    assert (topics[:, 8] == host["n_ident"]).all() and (topics[:, 10] == host["n_inline"]).all()
+
+
 def test_match_device_stream(gpu_available):
     """mq_match_device on torch-owned device buffers and a torch stream."""
     import torch
