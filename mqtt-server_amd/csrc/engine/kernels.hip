@@ -511,10 +511,12 @@ __device__ __forceinline__ void copy_tile(const EmitArgs& a, const V* __restrict
         }
         break;
       }
-      const uint32_t k = min(ga - wb, 63u);
-      const uint32_t sp = __shfl(wpos, (int)k, 64), ss = __shfl(wsrc, (int)k, 64);
-      if (slow) sb = sb_slow;
-      else if (moved) sb = ss - sp;
+      if (__any(moved || slow)) {  // usually no lane changed gather: keep sb without bpermutes
+        const uint32_t k = min(ga - wb, 63u);
+        const uint32_t sp = __shfl(wpos, (int)k, 64), ss = __shfl(wsrc, (int)k, 64);
+        if (slow) sb = sb_slow;
+        else if (moved) sb = ss - sp;
+      }
       si[u] = sb + x;
     }
     V v[U];
