@@ -1,0 +1,114 @@
+"""Secondary benchmark: the retained-message reverse match (Messages, topics.go:525-579) —
+BASELINE.json config 5 ("100M retained topics x 100k wildcard subscribe filters"), scaled by
+--retained (default 10M retained topics, 10 % of config 5; the 100M-topic host image does not
+fit the build container). A step is mq_messages_device over a batch of --filters filters already
+in HBM (k_msg count pass, scan, k_msg fill pass writing every retained handle).
+
+Prints one JSON line like bench.py's: throughput, output handles per filter, the k_msg roofline
+(algorithmic bytes B = 8·L + 4 + 16·P + 16·O per filter, SURVEY.md §8d, from the oracle's exact
+counters on a sample, over the two k_msg launches' HIP-event time) and the CPU baseline (the
+oracle's Messages on 16 host threads over a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mqtt-server_amd"))
+HBM_PEAK_GBS = 8000.0
+
+
+def log(msg):
+    print(f"[bench_messages {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--retained", type=int, default=10_000_000)
+    ap.add_argument("--sys", type=int, default=1000, help="$SYS/... retained topics (Q4)")
+    ap.add_argument("--filters", type=int, default=100_000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    rb, ro, hd, rh = W.gen_retained(args.retained, n_sys=args.sys, seed=W.BASE_SEED + 3)
+    fb, fo = W.gen_msg_filters(rh, args.filters, seed=W.BASE_SEED + 4)
+    n = len(fo) - 1
+    log(f"generated {len(ro) - 1} retained topics, {n} filters in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    eng = E.Engine(device=0)
+    eng.retain_bulk(rb, ro, hd)
+    log(f"engine index built in {time.time() - t0:.1f}s: {eng.stats()}")
+    stream = torch.cuda.current_stream()
+    d_fb = torch.from_numpy(np.concatenate([fb, np.zeros(16, np.uint8)])).to("cuda:0")
+    d_fo = torch.from_numpy(fo.view(np.int64)).to("cuda:0")
+    eng.sync(stream.cuda_stream)
+    torch.cuda.synchronize()
+
+    def step():
+        return eng.messages_device(d_fb.data_ptr(), d_fo.data_ptr(), n, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        r = step()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    eng.profile_reset()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        r = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    prof = eng.profile_read()
+    eng.profile(False)
+    handles = int(r.n_handles)
+    out = {
+        "metric": "Messages filters/sec (retained reverse match)", "value": n * args.steps / elapsed,
+        "unit": "filters/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "dtype": "u64",
+        "data": "synthetic (SURVEY.md §8d generator, retained seed +3)",
+        "config": {"workload": f"config 5 scaled: {len(ro) - 1} retained topics ({args.sys} $SYS), "
+                               f"{n} wildcard filters per step", "retained": len(ro) - 1, "filters": n},
+        "handles_per_step": handles, "handles_per_filter": handles / max(1, n),
+        "kernels_ms_per_step": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
+    }
+    cpu = None
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as O
+        orc = O.OracleIndex()
+        orc.retain_bulk(rb, ro, hd)
+        ns = min(n, 4096)
+        dg, cnt, tot = orc.messages_digest_batch(fb, fo[:ns + 1], nthreads=16)
+        base, count, hs = eng.messages_batch(fb, fo[:ns + 1])
+        out["parity_sample"] = {"filters": ns, "counts_equal": bool((count == cnt).all())}
+        per = {k: v / ns for k, v in tot.items()}
+        b = 8 * per["L"] + 4 + 16 * per["P"] + 16 * per["O"]
+        out["alg_bytes_per_filter"] = {"B": b, **per, "sample_filters": ns}
+        kms = sum(v[1] for k, v in prof.items() if k.startswith("msg")) / args.steps
+        if kms > 0:
+            ach = b * n / (kms * 1e-3) / 1e9
+            out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "k_msg (count + fill)"}
+        cal = min(n, 2048)
+        secs, _ = orc.bench_messages(fb, fo[:cal + 1], 16)
+        m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
+        secs, _ = orc.bench_messages(fb, fo[:m + 1], 16)
+        cpu = {"value": m / secs, "unit": "filters/s", "cores": 16, "kind": "port",
+               "sample": f"first {m} filters, 16 threads, Messages() per filter (oracle/)"}
+    out["cpu_baseline"] = cpu
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

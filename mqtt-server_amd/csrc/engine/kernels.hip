@@ -899,12 +899,17 @@ void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
 
 
 // ---------------------------------------------------------------------------------------------
-// k_msg: Messages(filter), the reverse retained scan (topics.go:525-579). One thread per filter.
-// The recursion is a depth-first walk without a stack: a frame is (node, level d); a '+'/'#'
-// level enumerates the node's children slab and, after returning from child c, resumes at
-// c's slab position + 1 (NodeMsg.child_pos). Levels past the last segment repeat it
-// (isolateParticle, topics.go:679-698), which is how a trailing '#' covers the subtree.
-// FILL=false counts the packets per filter; FILL=true writes their handles.
+// k_msg: Messages(filter), the reverse retained scan (topics.go:525-579). One wavefront per
+// filter. The literal prefix of the filter is walked first (all lanes alike) down to its first
+// '+'/'#' level, whose children are the units of parallel work: lane k takes child k of that
+// enumeration frame (and k + 64, ...), applies the frame's per-child rule (Q4 $SYS skip at level
+// 0, emit at the last level, descend otherwise) and walks the child's subtree depth-first
+// without a stack — a frame is (node, level d); a '+'/'#' level enumerates the node's children
+// slab and, after returning from child c, resumes at c's slab position + 1 (NodeMsg.child_pos);
+// levels past the last segment repeat it (isolateParticle, topics.go:679-698), which is how a
+// trailing '#' covers the subtree. A lane stops when it returns to the enumeration frame.
+// FILL=false counts the packets per filter; FILL=true counts each child's packets again, takes
+// a wave prefix sum and writes them at the filter's offset, children in slab order.
 // ---------------------------------------------------------------------------------------------
 template <bool FILL>
 __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
@@ -914,121 +919,189 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
                                              uint64_t* __restrict__ handles,
                                              uint64_t* __restrict__ base_out,
                                              uint32_t* __restrict__ count_out) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n) return;  // wave-uniform
   const uint64_t b0 = fo[t], b1 = fo[t + 1];
-  uint32_t c = 0;
+  uint32_t total = 0;  // packets of this filter (wave-uniform)
   uint64_t* out = FILL ? handles + off[t].rows : nullptr;
-  auto emit = [&](uint64_t h) {
-    if (FILL) out[c] = h;
-    c++;
-  };
   // len(filter) == 0 || Retained.Len() == 0 (topics.go:535)
   if (b1 > b0 && ix.retained_len != 0) {
     ByteReader R(fb);
-    bool wild = false;
-    for (uint64_t i = b0; i < b1; i++) {
-      const uint32_t ch = R.at(i);
-      wild |= (ch == '+') | (ch == '#');
+    bool w = false;
+    for (uint64_t i = b0 + lane; i < b1; i += 64) {
+      const uint32_t ch = fb[i];
+      w |= (ch == '+') | (ch == '#');
     }
+    const bool wild = __any(w);
+    // the literal prefix, down to the first '+'/'#' level (all lanes alike)
+    uint32_t node = kRoot, d = 0;
+    SegKey key;
+    uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
+    bool frame = false;  // an enumeration frame was reached at (node, d)
     if (!wild) {
       // no wildcard: Retained.Get(filter) (topics.go:539-544)
-      uint32_t node = kRoot;
-      uint64_t s = b0;
       for (;;) {
-        SegKey key;
-        const uint64_t e = scan_segment(R, s, b1, &key);
         node = lookup(ix, node, key, fb + s, (uint32_t)(e - s));
         if (node == kNone || e >= b1) break;
         s = e + 1;
+        e = scan_segment(R, s, b1, &key);
       }
-      if (node != kNone) {
-        const NodeMsg m = ix.msg[node];
-        if (m.flags & kRetainLive) emit(m.handle);
+      if (node != kNone && (ix.msg[node].flags & kRetainLive)) {
+        if (FILL && lane == 0) out[0] = ix.msg[node].handle;
+        total = 1;
       }
     } else {
-      uint32_t node = kRoot, d = 0, wd = 0;  // wd: level of the segment in the window
-      SegKey key;  // key of the window's segment (valid after every forward move)
-      uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
-      uint32_t cursor = 0;
-      bool resume = false;  // re-entering an enumeration frame after a child returned
-      for (uint64_t guard = 0;; guard++) {
-        if (guard > kWalkGuard * 64) {
-          atomicOr(ix.err, kErrWalkGuard);
-          break;
-        }
-        const bool has_next = (wd == d) && (e < b1);
+      for (;;) {
         const uint32_t len = (uint32_t)(e - s);
         const uint32_t c0 = len == 1 ? R.at(s) : 0;
-        const bool plus = c0 == '+';
-        const bool hash = c0 == '#';
-        bool descended = false;
-        if (plus || hash) {  // topics.go:547-565
-          const NodeMsg nm = ix.msg[node];
-          if (!resume) cursor = 0;
-          while (cursor < nm.child_cnt) {
-            const uint32_t ch = ix.children[nm.child_off + cursor];
-            cursor++;
-            const NodeMsg cm = ix.msg[ch];
-            if (d == 0 && cm.key_sys) continue;  // only the exact $SYS particle, level 0 (Q4)
-            if (!has_next && (cm.flags & kRetainPath) && (cm.flags & kRetainLive)) emit(cm.handle);
-            if (has_next || hash) {
-              node = ch;
-              d++;
-              if (e < b1) {
+        if (c0 == '+' || c0 == '#') {
+          frame = true;
+          break;
+        }
+        const uint32_t p = lookup(ix, node, key, fb + s, len);  // literal level (topics.go:568-576)
+        if (p == kNone) break;
+        if (e < b1) {
+          node = p;
+          d++;
+          s = e + 1;
+          e = scan_segment(R, s, b1, &key);
+          continue;
+        }
+        const NodeMsg m = ix.msg[p];
+        uint64_t h = 0;
+        bool hit = false;
+        if (m.flags & kRetainPath) {
+          hit = (m.flags & kRetainLive) != 0;
+          h = m.handle;
+        } else if (ix.empty_topic_live) {
+          hit = true;
+          h = ix.empty_topic_handle;  // Retained.Get("") on a particle without a path (Q6)
+        }
+        if (hit) {
+          if (FILL && lane == 0) out[0] = h;
+          total = 1;
+        }
+        break;
+      }
+    }
+    if (frame) {  // topics.go:547-565 at (node, d), segment [s, e)
+      const uint32_t fd = d;
+      const uint64_t fs = s, fe = e;
+      const SegKey fkey = key;
+      const bool has_next = fe < b1;
+      const bool hash = R.at(fs) == '#';
+      const NodeMsg nm = ix.msg[node];
+      // packets under child k of the frame (its own and its subtree's); write: store them at dst
+      auto child = [&](uint32_t k, bool write, uint64_t* dst) -> uint32_t {
+        uint32_t c = 0;
+        auto emit = [&](uint64_t h) {
+          if (write) dst[c] = h;
+          c++;
+        };
+        const uint32_t ch0 = ix.children[nm.child_off + k];
+        const NodeMsg cm0 = ix.msg[ch0];
+        if (fd == 0 && cm0.key_sys) return 0u;  // only the exact $SYS particle, level 0 (Q4)
+        if (!has_next && (cm0.flags & kRetainPath) && (cm0.flags & kRetainLive)) emit(cm0.handle);
+        if (!(has_next || hash)) return c;
+        uint32_t node = ch0, d = fd + 1, wd = fd;  // wd: level of the segment in the window
+        uint64_t s = fs, e = fe;
+        SegKey key = fkey;
+        if (e < b1) {
+          s = e + 1;
+          e = scan_segment(R, s, b1, &key);
+          wd++;
+        }
+        uint32_t cursor = 0;
+        bool resume = false;  // re-entering an enumeration frame after a child returned
+        for (uint64_t guard = 0;; guard++) {
+          if (guard > kWalkGuard * 64) {
+            atomicOr(ix.err, kErrWalkGuard);
+            break;
+          }
+          const bool has_nx = (wd == d) && (e < b1);
+          const uint32_t len = (uint32_t)(e - s);
+          const uint32_t c0 = len == 1 ? R.at(s) : 0;
+          const bool plus = c0 == '+';
+          const bool hsh = c0 == '#';
+          bool descended = false;
+          if (plus || hsh) {  // topics.go:547-565
+            const NodeMsg xm = ix.msg[node];
+            if (!resume) cursor = 0;
+            while (cursor < xm.child_cnt) {
+              const uint32_t ch = ix.children[xm.child_off + cursor];
+              cursor++;
+              const NodeMsg cm = ix.msg[ch];
+              if (!has_nx && (cm.flags & kRetainPath) && (cm.flags & kRetainLive)) emit(cm.handle);
+              if (has_nx || hsh) {
+                node = ch;
+                d++;
+                if (e < b1) {
+                  s = e + 1;
+                  e = scan_segment(R, s, b1, &key);
+                  wd++;
+                }
+                descended = true;
+                break;
+              }
+            }
+          } else if (!resume) {  // literal level (topics.go:568-576)
+            const uint32_t p = lookup(ix, node, key, fb + s, len);
+            if (p != kNone) {
+              if (has_nx) {
+                node = p;
+                d++;
                 s = e + 1;
                 e = scan_segment(R, s, b1, &key);
                 wd++;
-              }
-              descended = true;
-              break;
-            }
-          }
-        } else if (!resume) {  // literal level (topics.go:568-576)
-          const uint32_t p = lookup(ix, node, key, fb + s, len);
-          if (p != kNone) {
-            if (has_next) {
-              node = p;
-              d++;
-              s = e + 1;
-              e = scan_segment(R, s, b1, &key);
-              wd++;
-              descended = true;
-            } else {
-              const NodeMsg m = ix.msg[p];
-              if (m.flags & kRetainPath) {
-                if (m.flags & kRetainLive) emit(m.handle);
-              } else if (ix.empty_topic_live) {
-                emit(ix.empty_topic_handle);  // Retained.Get("") on a particle without a path (Q6)
+                descended = true;
+              } else {
+                const NodeMsg m = ix.msg[p];
+                if (m.flags & kRetainPath) {
+                  if (m.flags & kRetainLive) emit(m.handle);
+                } else if (ix.empty_topic_live) {
+                  emit(ix.empty_topic_handle);  // Q6
+                }
               }
             }
           }
+          if (descended) {
+            resume = false;
+            continue;
+          }
+          // frame finished: return to the parent frame; the child of the wave's enumeration
+          // frame is done when we would return into it
+          if (d == fd + 1) break;
+          const NodeMsg cm = ix.msg[node];
+          node = ix.walk[node].parent_flags & kParentMask;
+          if (wd == d) {
+            e = s - 1;
+            s = seg_start_before(R, b0, e);
+            wd--;
+          }
+          d--;
+          cursor = cm.child_pos + 1;
+          resume = true;
         }
-        if (descended) {
-          resume = false;
-          continue;
-        }
-        // frame finished: return to the parent frame (its key is not needed again: a literal
-        // frame is done, an enumeration frame resumes after this child)
-        if (d == 0) break;
-        const NodeMsg cm = ix.msg[node];
-        node = ix.walk[node].parent_flags & kParentMask;
-        if (wd == d) {
-          e = s - 1;
-          s = seg_start_before(R, b0, e);
-          wd--;
-        }
-        d--;
-        cursor = cm.child_pos + 1;
-        resume = true;
+        return c;
+      };
+      for (uint32_t k0 = 0; k0 < nm.child_cnt; k0 += 64) {  // wave-uniform
+        const uint32_t k = k0 + lane;
+        const uint32_t ck = k < nm.child_cnt ? child(k, false, nullptr) : 0u;
+        uint32_t sum;
+        const uint32_t pre = wave_excl_scan(ck, lane, &sum);
+        if (FILL && ck) child(k, true, out + total + pre);
+        total += sum;
       }
     }
   }
-  if (!FILL) {
-    cnt[t] = TopicCount{0, c, 0, 0, 0};
-  } else {
-    base_out[t] = off[t].rows;
-    count_out[t] = c;
+  if (lane == 0) {
+    if (!FILL) {
+      cnt[t] = TopicCount{0, total, 0, 0, 0};
+    } else {
+      base_out[t] = off[t].rows;
+      count_out[t] = total;
+    }
   }
 }
 
@@ -1036,7 +1109,7 @@ void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, co
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
                 uint32_t* count, hipStream_t s) {
   if (!n) return;
-  dim3 grid((n + 255) / 256);
+  dim3 grid((n + 3) / 4);  // one wavefront per filter
   if (fill)
     hipLaunchKernelGGL(k_msg<true>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count);
   else

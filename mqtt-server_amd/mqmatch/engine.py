@@ -355,7 +355,7 @@ class Engine:
         return out
 
     def messages_batch(self, bytes_, offs):
-        """mq_messages_batch -> list of sorted handle arrays, one per filter."""
+        """mq_messages_batch -> (base, count, handles): filter i has handles[base[i] : base[i] + count[i]]."""
         n = len(offs) - 1
         rp = C.POINTER(MsgResult)()
         _check(lib().mq_messages_batch(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)),
