@@ -42,9 +42,9 @@ struct MatchHolder {
 };
 struct MsgHolder {
   mq_msg_result pub;
-  std::vector<uint64_t> base;
-  std::vector<uint32_t> count;
-  std::vector<uint64_t> handles;
+  PinnedVec<uint64_t> base;
+  PinnedVec<uint32_t> count;
+  PinnedVec<uint64_t> handles;
 };
 std::mutex g_res_mu;
 std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages

@@ -5,11 +5,58 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
 
 namespace mq {
 
 void hip_check(hipError_t e, const char* where) {
   if (e != hipSuccess) throw HipError{e, std::string(where) + ": " + hipGetErrorString(e)};
+}
+
+// ---- pooled pinned host memory (PinnedAlloc) ------------------------------------------------------
+namespace {
+std::mutex g_pin_mu;
+std::multimap<size_t, void*> g_pin_free;  // capacity -> block
+size_t g_pin_pooled = 0;
+constexpr size_t kPinMin = 64 << 10, kPinPoolCap = 32ull << 30;
+size_t pin_cap(size_t bytes) {
+  size_t c = kPinMin;
+  while (c < bytes) c <<= 1;
+  return c;
+}
+}  // namespace
+
+void* pinned_alloc(size_t bytes) {
+  const size_t cap = pin_cap(bytes);
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_free.find(cap);
+    if (it != g_pin_free.end()) {
+      void* p = it->second;
+      g_pin_free.erase(it);
+      g_pin_pooled -= cap;
+      return p;
+    }
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess || !p) throw std::bad_alloc();
+  return p;
+}
+
+void pinned_free(void* p, size_t bytes) {
+  if (!p) return;
+  const size_t cap = pin_cap(bytes);
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (g_pin_pooled + cap <= kPinPoolCap) {
+      g_pin_free.emplace(cap, p);
+      g_pin_pooled += cap;
+      return;
+    }
+  }
+  (void)hipHostFree(p);
 }
 
 void DevBuf::ensure(size_t b) {
