@@ -908,8 +908,8 @@ void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
 // slab and, after returning from child c, resumes at c's slab position + 1 (NodeMsg.child_pos);
 // levels past the last segment repeat it (isolateParticle, topics.go:679-698), which is how a
 // trailing '#' covers the subtree. A lane stops when it returns to the enumeration frame.
-// FILL=false counts the packets per filter; FILL=true counts each child's packets again, takes
-// a wave prefix sum and writes them at the filter's offset, children in slab order.
+// FILL=false counts the packets per filter; FILL=true walks again and appends them at the
+// filter's offset through a per-wave LDS cursor (Messages' order is Go map order, i.e. none).
 // ---------------------------------------------------------------------------------------------
 template <bool FILL>
 __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
@@ -919,8 +919,9 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
                                              uint64_t* __restrict__ handles,
                                              uint64_t* __restrict__ base_out,
                                              uint32_t* __restrict__ count_out) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ uint32_t cursor[4];  // FILL: next free slot of the wave's filter
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t t = blockIdx.x * 4 + wv;
   if (t >= n) return;  // wave-uniform
   const uint64_t b0 = fo[t], b1 = fo[t + 1];
   uint32_t total = 0;  // packets of this filter (wave-uniform)
@@ -992,11 +993,11 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
       const bool has_next = fe < b1;
       const bool hash = R.at(fs) == '#';
       const NodeMsg nm = ix.msg[node];
-      // packets under child k of the frame (its own and its subtree's); write: store them at dst
-      auto child = [&](uint32_t k, bool write, uint64_t* dst) -> uint32_t {
+      // packets under child k of the frame (its own and its subtree's), counted or appended
+      auto child = [&](uint32_t k) -> uint32_t {
         uint32_t c = 0;
         auto emit = [&](uint64_t h) {
-          if (write) dst[c] = h;
+          if (FILL) out[atomicAdd(&cursor[wv], 1u)] = h;
           c++;
         };
         const uint32_t ch0 = ix.children[nm.child_off + k];
@@ -1085,13 +1086,11 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
         }
         return c;
       };
+      if (FILL && lane == 0) cursor[wv] = total;
+      wave_sync_lds();
       for (uint32_t k0 = 0; k0 < nm.child_cnt; k0 += 64) {  // wave-uniform
         const uint32_t k = k0 + lane;
-        const uint32_t ck = k < nm.child_cnt ? child(k, false, nullptr) : 0u;
-        uint32_t sum;
-        const uint32_t pre = wave_excl_scan(ck, lane, &sum);
-        if (FILL && ck) child(k, true, out + total + pre);
-        total += sum;
+        total += wave_sum(k < nm.child_cnt ? child(k) : 0u);
       }
     }
   }
