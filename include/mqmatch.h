@@ -213,6 +213,24 @@ int mq_messages_batch(mq_index* idx, const uint8_t* filter_bytes, const uint64_t
 int mq_messages_device(mq_index* idx, const uint8_t* d_filter_bytes, const uint64_t* d_offsets,
                        uint32_t n, void* hip_stream, mq_msg_result* out);
 
+/* Batched auth.MatchTopic (hooks/auth/ledger.go:90-118): the ACL ledger's
+ * filter/topic test that the fan-out runs per recipient (server.go:1029 -> Ledger.ACLOk ->
+ * RString.FilterMatches). Pairs index two string tables (filters, topics: bytes + u64 offsets)
+ * so one publish topic can be tested against many ACL filters. Per pair: matched (0/1) and the
+ * captured elements ('+' parts, the '#' remainder) as (start, len) spans into the pair's topic,
+ * including those captured before a failed match, as the reference returns them. */
+typedef struct mq_acl_result {
+  uint64_t n_pairs;
+  const uint8_t* matched;
+  const uint32_t* n_elems;
+  const uint64_t* elem_base;  /* pair p's spans: elems[2 * elem_base[p] .. + 2 * n_elems[p]) */
+  const uint32_t* elems;
+} mq_acl_result;
+int mq_acl_match_batch(mq_index* idx, const uint8_t* filter_bytes, const uint64_t* filter_offs, uint32_t n_filters,
+                       const uint8_t* topic_bytes, const uint64_t* topic_offs, uint32_t n_topics,
+                       const uint32_t* pair_filter, const uint32_t* pair_topic, uint64_t n_pairs,
+                       mq_acl_result** out);
+
 void mq_result_free(void* result);
 
 /* ---- device image, statistics and profiling ---- */

@@ -46,8 +46,12 @@ struct MsgHolder {
   PinnedVec<uint32_t> count;
   PinnedVec<uint64_t> handles;
 };
+struct AclHolder {
+  mq_acl_result pub;
+  HostAcl data;
+};
 std::mutex g_res_mu;
-std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages
+std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages, 3 = acl
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -258,6 +262,28 @@ int mq_messages_device(mq_index* idx, const uint8_t* d_fb, const uint64_t* d_fo,
   });
 }
 
+int mq_acl_match_batch(mq_index* idx, const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb,
+                       const uint64_t* to, uint32_t nt, const uint32_t* pf, const uint32_t* pt, uint64_t n_pairs,
+                       mq_acl_result** out) {
+  if (!out || !fo || !to || (n_pairs && (!pf || !pt)) || (fo[nf] && !fb) || (to[nt] && !tb))
+    return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    std::unique_ptr<AclHolder> h(new AclHolder());
+    idx->device().acl(fb, fo, nf, tb, to, nt, pf, pt, n_pairs, &h->data);
+    mq_acl_result& r = h->pub;
+    r.n_pairs = n_pairs;
+    r.matched = h->data.matched.data();
+    r.n_elems = h->data.n_elems.data();
+    r.elem_base = h->data.elem_base.data();
+    r.elems = h->data.elems.data();
+    *out = &h->pub;
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    g_results[&h->pub] = 3;
+    h.release();
+    return 0;
+  });
+}
+
 void mq_result_free(void* r) {
   if (!r) return;
   int kind = 0;
@@ -270,6 +296,7 @@ void mq_result_free(void* r) {
   }
   if (kind == 1) delete reinterpret_cast<MatchHolder*>(r);
   if (kind == 2) delete reinterpret_cast<MsgHolder*>(r);
+  if (kind == 3) delete reinterpret_cast<AclHolder*>(r);
 }
 
 int mq_sync(mq_index* idx, void* stream) {

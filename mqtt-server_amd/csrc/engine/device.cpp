@@ -224,7 +224,7 @@ Device::~Device() {
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
-                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_, &tstat_})
+                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_, &tstat_, &acl_buf_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k]}) b->release();
@@ -685,6 +685,72 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     }
     check_err(s);
   }
+}
+
+void Device::acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb, const uint64_t* to,
+                 uint32_t nt, const uint32_t* pf, const uint32_t* pt, uint64_t n_pairs, HostAcl* out) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  *out = HostAcl{};
+  out->matched.resize(n_pairs);
+  out->n_elems.resize(n_pairs);
+  out->elem_base.resize(n_pairs);
+  if (!n_pairs) return;
+  // capacity of a pair = '+' / '#' parts of its filter (each captures at most one element)
+  std::vector<uint32_t> cap(nf, 0);
+  for (uint32_t f = 0; f < nf; f++) {
+    uint64_t b = fo[f];
+    for (uint64_t i = fo[f]; i <= fo[f + 1]; i++) {
+      if (i == fo[f + 1] || fb[i] == '/') {
+        if (i - b == 1 && (fb[b] == '+' || fb[b] == '#')) cap[f]++;
+        b = i + 1;
+      }
+    }
+  }
+  uint64_t total = 0;
+  for (uint64_t p = 0; p < n_pairs; p++) {
+    if (pf[p] >= nf || pt[p] >= nt) throw HipError{hipErrorInvalidValue, "pair index out of range"};
+    out->elem_base[p] = total;
+    total += cap[pf[p]];
+  }
+  out->elems.resize(2 * std::max<uint64_t>(total, 1));
+  auto up = [](uint64_t x) { return (x + 255) & ~255ull; };  // 256-byte aligned sub-buffers
+  const uint64_t fbytes = fo[nf], tbytes = to[nt];
+  const uint64_t o_fb = 0, o_fo = up(o_fb + fbytes + 16), o_tb = up(o_fo + 8 * (nf + 1)),
+                 o_to = up(o_tb + tbytes + 16), o_pf = up(o_to + 8 * (nt + 1)), o_pt = up(o_pf + 4 * n_pairs),
+                 o_eb = up(o_pt + 4 * n_pairs), o_m = up(o_eb + 8 * n_pairs), o_ne = up(o_m + n_pairs),
+                 o_el = up(o_ne + 4 * n_pairs), o_end = up(o_el + 8 * std::max<uint64_t>(total, 1));
+  acl_buf_.ensure(o_end);
+  uint8_t* d = acl_buf_.as<uint8_t>();
+  hipStream_t s = nullptr;
+  hip_check(hipMemsetAsync(d, 0, o_fo, s), "memset");
+  hip_check(hipMemsetAsync(d + o_tb, 0, o_to - o_tb, s), "memset");
+  if (fbytes) hip_check(hipMemcpyAsync(d + o_fb, fb, fbytes, hipMemcpyHostToDevice, s), "H2D");
+  hip_check(hipMemcpyAsync(d + o_fo, fo, 8 * (nf + 1), hipMemcpyHostToDevice, s), "H2D");
+  if (tbytes) hip_check(hipMemcpyAsync(d + o_tb, tb, tbytes, hipMemcpyHostToDevice, s), "H2D");
+  hip_check(hipMemcpyAsync(d + o_to, to, 8 * (nt + 1), hipMemcpyHostToDevice, s), "H2D");
+  hip_check(hipMemcpyAsync(d + o_pf, pf, 4 * n_pairs, hipMemcpyHostToDevice, s), "H2D");
+  hip_check(hipMemcpyAsync(d + o_pt, pt, 4 * n_pairs, hipMemcpyHostToDevice, s), "H2D");
+  hip_check(hipMemcpyAsync(d + o_eb, out->elem_base.data(), 8 * n_pairs, hipMemcpyHostToDevice, s), "H2D");
+  AclArgs a;
+  a.filter_bytes = d + o_fb;
+  a.filter_offs = reinterpret_cast<const uint64_t*>(d + o_fo);
+  a.topic_bytes = d + o_tb;
+  a.topic_offs = reinterpret_cast<const uint64_t*>(d + o_to);
+  a.pair_filter = reinterpret_cast<const uint32_t*>(d + o_pf);
+  a.pair_topic = reinterpret_cast<const uint32_t*>(d + o_pt);
+  a.elem_base = reinterpret_cast<const uint64_t*>(d + o_eb);
+  a.n_pairs = n_pairs;
+  a.matched = d + o_m;
+  a.n_elems = reinterpret_cast<uint32_t*>(d + o_ne);
+  a.elems = reinterpret_cast<uint32_t*>(d + o_el);
+  prof.begin(s);
+  launch_acl(a, s);
+  prof.end("acl", s);
+  hip_check(hipGetLastError(), "k_acl");
+  hip_check(hipMemcpyAsync(out->matched.data(), d + o_m, n_pairs, hipMemcpyDeviceToHost, s), "D2H");
+  hip_check(hipMemcpyAsync(out->n_elems.data(), d + o_ne, 4 * n_pairs, hipMemcpyDeviceToHost, s), "D2H");
+  if (total) hip_check(hipMemcpyAsync(out->elems.data(), d + o_el, 8 * total, hipMemcpyDeviceToHost, s), "D2H");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
 void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,

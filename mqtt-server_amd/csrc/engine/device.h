@@ -73,6 +73,14 @@ struct HostMsg {
   PinnedVec<uint64_t> handles;
 };
 
+// Host-side destination of a batched MatchTopic (mq_acl_match_batch).
+struct HostAcl {
+  PinnedVec<uint8_t> matched;
+  PinnedVec<uint32_t> n_elems;
+  PinnedVec<uint64_t> elem_base;
+  PinnedVec<uint32_t> elems;
+};
+
 // Host-side destination of a batch's results (mq_match_batch).
 struct HostMatch {
   PinnedVec<mq_topic_result> topics;
@@ -127,6 +135,9 @@ class Device {
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
                 HostMsg* host, mq_msg_result* out);
+  // auth.MatchTopic over (filter, topic) pairs of two host string tables (k_acl).
+  void acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb, const uint64_t* to,
+           uint32_t nt, const uint32_t* pf, const uint32_t* pt, uint64_t n_pairs, HostAcl* out);
   // Copy host topics to the device input buffers and return their device pointers.
   void stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hipStream_t s,
                     const uint8_t** d_tb, const uint64_t** d_to);
@@ -192,6 +203,7 @@ class Device {
   uint32_t n_cus_ = 1, merge_diag_ = 0;
   bool serial_ = false;       // MQ_SERIAL: k_merge on the launch stream (isolated kernel times)
   DevBuf tstat_;
+  DevBuf acl_buf_;  // k_acl inputs and outputs
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;
   uint64_t empty_handle_ = 0;

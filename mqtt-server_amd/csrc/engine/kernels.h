@@ -116,6 +116,22 @@ struct DescArgs {
   uint32_t* tiles;
 };
 
+// Batched auth.MatchTopic (k_acl).
+struct AclArgs {
+  const uint8_t* filter_bytes;
+  const uint64_t* filter_offs;
+  const uint8_t* topic_bytes;
+  const uint64_t* topic_offs;
+  const uint32_t* pair_filter;
+  const uint32_t* pair_topic;
+  const uint64_t* elem_base;  // per pair: first (start, len) slot in elems
+  uint64_t n_pairs;
+  uint8_t* matched;
+  uint32_t* n_elems;
+  uint32_t* elems;
+};
+void launch_acl(const AclArgs& a, hipStream_t s);
+
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
                  TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,

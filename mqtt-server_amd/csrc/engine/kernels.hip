@@ -1104,6 +1104,66 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_acl: auth.MatchTopic (hooks/auth/ledger.go:90-118) for (filter, topic) pairs — the ACL test
+// the fan-out runs per recipient (server.go:1029 -> Ledger.ACLOk -> FilterMatches). One thread
+// per pair; filter and topic are split on '/' as strings.Split does (an empty string is one empty
+// part); '+' captures the topic part, '#' captures the rest of the topic (when a part exists at
+// its position) and matches; a filter that runs out first matches (the reference's prefix rule).
+// Captured elements are (start, len) spans into the topic, written from elem_base[pair].
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_acl(AclArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_pairs) return;
+  const uint32_t f = a.pair_filter[i], t = a.pair_topic[i];
+  const uint64_t fb0 = a.filter_offs[f], fb1 = a.filter_offs[f + 1];
+  const uint64_t tb0 = a.topic_offs[t], tb1 = a.topic_offs[t + 1];
+  ByteReader RF(a.filter_bytes), RT(a.topic_bytes);
+  uint32_t* el = a.elems + 2 * a.elem_base[i];
+  uint32_t n_el = 0;
+  bool matched = true;
+  uint64_t fs = fb0, ts = tb0;
+  bool topic_left = true;  // a topic part exists at this index
+  for (;;) {
+    const uint64_t fe = find_slash(RF, fs, fb1);
+    if (!topic_left) {  // ledger.go:95-98
+      matched = false;
+      break;
+    }
+    const uint64_t te = find_slash(RT, ts, tb1);
+    const uint64_t flen = fe - fs;
+    const uint32_t c0 = flen == 1 ? RF.at(fs) : 0u;
+    if (c0 == '+') {  // ledger.go:100-103
+      el[2 * n_el] = (uint32_t)(ts - tb0);
+      el[2 * n_el + 1] = (uint32_t)(te - ts);
+      n_el++;
+    } else if (c0 == '#') {  // ledger.go:105-109
+      el[2 * n_el] = (uint32_t)(ts - tb0);
+      el[2 * n_el + 1] = (uint32_t)(tb1 - ts);
+      n_el++;
+      break;
+    } else {  // ledger.go:111-114
+      bool eq = flen == te - ts;
+      for (uint64_t k = 0; eq && k < flen; k++) eq = RF.at(fs + k) == RT.at(ts + k);
+      if (!eq) {
+        matched = false;
+        break;
+      }
+    }
+    if (fe >= fb1) break;  // the filter's parts are used up: ledger.go:117
+    fs = fe + 1;
+    topic_left = te < tb1;
+    ts = topic_left ? te + 1 : tb1;
+  }
+  a.matched[i] = matched ? 1 : 0;
+  a.n_elems[i] = n_el;
+}
+
+void launch_acl(const AclArgs& a, hipStream_t s) {
+  if (!a.n_pairs) return;
+  hipLaunchKernelGGL(k_acl, dim3((uint32_t)((a.n_pairs + 255) / 256)), dim3(256), 0, s, a);
+}
+
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
                 uint32_t* count, hipStream_t s) {

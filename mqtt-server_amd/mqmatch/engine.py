@@ -54,6 +54,11 @@ class MsgResult(C.Structure):
                 ("count", C.c_void_p), ("handles", C.c_void_p), ("n_handles", C.c_uint64)]
 
 
+class AclResult(C.Structure):
+    _fields_ = [("n_pairs", C.c_uint64), ("matched", C.c_void_p), ("n_elems", C.c_void_p),
+                ("elem_base", C.c_void_p), ("elems", C.c_void_p)]
+
+
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("nodes", "edges", "edge_capacity", "subs", "subs_merge",
                                            "shared", "inlines", "retained", "retained_live",
@@ -73,6 +78,7 @@ EXPORTS = [
     "mq_match_batch", "mq_match_device", "mq_match_chunks", "mq_messages_batch",
     "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
     "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
+    "mq_acl_match_batch",
 ]
 
 CHUNK_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(MatchResult), C.c_uint32, C.c_void_p)
@@ -115,6 +121,8 @@ def lib():
         "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
         "mq_match_chunks": (C.c_uint32, [vp]),
         "mq_match_device_chunks": (C.c_int, [vp, vp, vp, C.c_uint32, vp, CHUNK_FN, vp]),
+        "mq_acl_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, _u8p, _u64p, C.c_uint32, _u32p, _u32p,
+                                         C.c_uint64, C.POINTER(C.POINTER(AclResult))]),
         "mq_messages_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MsgResult))]),
         "mq_messages_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MsgResult)]),
         "mq_result_free": (None, [vp]),
@@ -398,6 +406,41 @@ class Engine:
 
     def match_chunks(self):
         return int(lib().mq_match_chunks(self.h))
+
+    def acl_match_batch(self, filters, topics, pair_filter, pair_topic):
+        """mq_acl_match_batch (auth.MatchTopic, hooks/auth/ledger.go:90-118) over pairs of the two
+        string lists -> list of (elements, matched) per pair, as the reference returns them."""
+        fb, fo = pack_strings(filters)
+        tb, to = pack_strings(topics)
+        pf = np.ascontiguousarray(pair_filter, np.uint32)
+        pt = np.ascontiguousarray(pair_topic, np.uint32)
+        n = len(pf)
+        rp = C.POINTER(AclResult)()
+        _check(lib().mq_acl_match_batch(self.h, _p(fb, _u8p), _p(fo, _u64p), len(filters), _p(tb, _u8p),
+                                        _p(to, _u64p), len(topics), _p(pf, _u32p), _p(pt, _u32p), n,
+                                        C.byref(rp)), "mq_acl_match_batch")
+        try:
+            r = rp.contents
+            def arr(ptr, count, dtype):
+                if count == 0 or not ptr:
+                    return np.zeros(0, dtype)
+                buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+                return np.frombuffer(buf, dtype).copy()
+            matched = arr(r.matched, n, np.uint8)
+            n_el = arr(r.n_elems, n, np.uint32)
+            base = arr(r.elem_base, n, np.uint64)
+            total = int((base[-1] + n_el[-1])) if n else 0
+            spans = arr(r.elems, 2 * max(total, 1), np.uint32)
+        finally:
+            lib().mq_result_free(rp)
+        raw = [_b(t) for t in topics]
+        out = []
+        for i in range(n):
+            t = raw[int(pt[i])]
+            els = [t[spans[2 * (int(base[i]) + k)]:spans[2 * (int(base[i]) + k)] + spans[2 * (int(base[i]) + k) + 1]]
+                   .decode("utf-8", "surrogateescape") for k in range(int(n_el[i]))]
+            out.append((els, bool(matched[i])))
+        return out
 
     def profile(self, enable=True):
         _check(lib().mq_profile_enable(self.h, 1 if enable else 0), "mq_profile_enable")

@@ -65,6 +65,7 @@ def lib():
     L.orc_isolate_particle.argtypes = [C.c_char_p, C.c_uint32, C.c_int, _u32p, _u32p]
     L.orc_is_valid_filter.argtypes = [C.c_char_p, C.c_uint32, C.c_int]
     L.orc_is_shared_filter.argtypes = [C.c_char_p, C.c_uint32]
+    L.orc_match_topic.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, _u32p, C.c_uint32, _u32p]
     L.orc_equal_fold_ascii.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32]
     L.orc_path_exists.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int]
     L.orc_node_counts.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int, _i64p]
@@ -93,6 +94,17 @@ def isolate_particle(f, d):
 def is_valid_filter(f, for_publish):
     fb = _b(f)
     return bool(lib().orc_is_valid_filter(fb, len(fb), 1 if for_publish else 0))
+
+
+def match_topic(filter, topic):
+    """auth.MatchTopic (hooks/auth/ledger.go:90-118) -> (elements, matched)."""
+    fb, tb = _b(filter), _b(topic)
+    cap = len(fb) + 1
+    el = np.zeros(2 * cap, np.uint32)
+    n = C.c_uint32()
+    m = lib().orc_match_topic(fb, len(fb), tb, len(tb), _ptr(el, _u32p), cap, C.byref(n))
+    elems = [tb[el[2 * i]:el[2 * i] + el[2 * i + 1]].decode("utf-8", "surrogateescape") for i in range(n.value)]
+    return elems, bool(m)
 
 
 def is_shared_filter(f):

@@ -371,6 +371,18 @@ int orc_isolate_particle(const char* f, uint32_t flen, int d, uint32_t* start, u
 int orc_is_valid_filter(const char* f, uint32_t flen, int for_publish) {
   return is_valid_filter(std::string_view(f, flen), for_publish != 0) ? 1 : 0;
 }
+// auth.MatchTopic: returns matched; elems (cap pairs of start, len in the topic) and *n_elems
+int orc_match_topic(const char* f, uint32_t flen, const char* t, uint32_t tlen, uint32_t* elems, uint32_t cap,
+                    uint32_t* n_elems) {
+  std::vector<std::pair<uint32_t, uint32_t>> el;
+  const bool m = match_topic(std::string_view(f, flen), std::string_view(t, tlen), &el);
+  *n_elems = (uint32_t)el.size();
+  for (size_t i = 0; i < el.size() && i < cap; i++) {
+    elems[2 * i] = el[i].first;
+    elems[2 * i + 1] = el[i].second;
+  }
+  return m ? 1 : 0;
+}
 int orc_is_shared_filter(const char* f, uint32_t flen) {
   return is_shared_filter(std::string_view(f, flen)) ? 1 : 0;
 }

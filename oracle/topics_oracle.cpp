@@ -102,6 +102,45 @@ bool is_shared_filter(std::string_view filter) {  // topics.go:701-704
   return equal_fold_ascii(isolate_particle(filter, 0, &hn), kSharePrefix);
 }
 
+static std::vector<std::string_view> split_slash(std::string_view s) {  // strings.Split(s, "/")
+  std::vector<std::string_view> out;
+  size_t b = 0;
+  for (;;) {
+    const size_t e = s.find('/', b);
+    if (e == std::string_view::npos) {
+      out.push_back(s.substr(b));
+      return out;
+    }
+    out.push_back(s.substr(b, e - b));
+    b = e + 1;
+  }
+}
+
+bool match_topic(std::string_view filter, std::string_view topic,  // hooks/auth/ledger.go:90-118
+                 std::vector<std::pair<uint32_t, uint32_t>>* elements) {
+  const std::vector<std::string_view> fp = split_slash(filter), tp = split_slash(topic);
+  if (elements) elements->clear();
+  auto span = [&](std::string_view v) {
+    return std::make_pair((uint32_t)(v.data() - topic.data()), (uint32_t)v.size());
+  };
+  for (size_t i = 0; i < fp.size(); i++) {
+    if (i >= tp.size()) return false;  // ledger.go:95-98
+    if (fp[i] == "+") {                // ledger.go:100-103
+      if (elements) elements->push_back(span(tp[i]));
+      continue;
+    }
+    if (fp[i] == "#") {  // ledger.go:105-109: the rest of the topic, joined
+      if (elements) {
+        const uint32_t b = (uint32_t)(tp[i].data() - topic.data());
+        elements->push_back(std::make_pair(b, (uint32_t)topic.size() - b));
+      }
+      return true;
+    }
+    if (fp[i] != tp[i]) return false;  // ledger.go:111-114
+  }
+  return true;  // ledger.go:117
+}
+
 bool is_valid_filter(std::string_view filter, bool for_publish) {  // topics.go:707-745
   if (!for_publish && filter.empty()) return false;
   if (for_publish) {

@@ -105,6 +105,11 @@ bool equal_fold_ascii(std::string_view s, std::string_view ascii_target);
 // IsSharedFilter / IsValidFilter (topics.go:700-745).
 bool is_shared_filter(std::string_view filter);
 bool is_valid_filter(std::string_view filter, bool for_publish);
+// auth.MatchTopic (hooks/auth/ledger.go:90-118): the ACL ledger's filter/topic test, with its
+// captured '+' / '#' elements (spans into the topic). Not the TopicsIndex rules: a filter
+// shorter than the topic matches it, and '#' needs at least one topic level at its position.
+bool match_topic(std::string_view filter, std::string_view topic,
+                 std::vector<std::pair<uint32_t, uint32_t>>* elements);
 
 class TopicsIndex {
  public:

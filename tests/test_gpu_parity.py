@@ -448,3 +448,24 @@ def test_cpp_host_mirror(gpu_available):
                        "mqtt-server_amd", "build", "test_topics_index")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_acl_match_topic_batch(gpu_available):
+    """Batched auth.MatchTopic (hooks/auth/ledger.go:90-118) on the GPU: the reference's own cases
+    (ledger_test.go:461-493) and random filter/topic pairs, against the oracle's restatement."""
+    from mqmatch import engine as E
+    eng = E.Engine()
+    kat = [("a/+/c/+", "a/b/c/d"), ("a/+/+/+", "a/b/c/d"), ("stuff/#", "stuff/things/yeah"),
+           ("a/+/#/+", "a/b/c/d/as/dds"), ("test", "test"), ("things/stuff//", "things/stuff/"), ("t", "t2"),
+           (" ", "  ")]
+    r = random.Random(71)
+    segs = ["a", "b", "c", "", "+", "#", "longersegment-abcdefgh", "ü"]
+    filters = [k[0] for k in kat] + ["/".join(r.choice(segs) for _ in range(r.randint(1, 5))) for _ in range(300)]
+    topics = [k[1] for k in kat] + ["/".join(r.choice(segs[:4] + segs[6:]) for _ in range(r.randint(1, 6)))
+                                    for _ in range(200)] + [""]
+    pf = list(range(len(kat))) + [r.randrange(len(filters)) for _ in range(20000)]
+    pt = list(range(len(kat))) + [r.randrange(len(topics)) for _ in range(20000)]
+    got = eng.acl_match_batch(filters, topics, pf, pt)
+    for f, t, g in zip(pf, pt, got):
+        assert g == O.match_topic(filters[f], topics[t]), (filters[f], topics[t])
+    assert sum(m for _, m in got) > 1000

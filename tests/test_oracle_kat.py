@@ -115,3 +115,12 @@ def test_retained_expiry_keeps_path():
     assert ix.messages("a/+") == [] and ix.messages("a/b") == []
     ix.unsubscribe("a/b", "c")
     assert ix.path_exists("a/b")  # retainPath still set
+
+
+def test_match_topic():  # hooks/auth/ledger_test.go:461-493 (auth.MatchTopic)
+    cases = [("a/+/c/+", "a/b/c/d", ["b", "d"], True), ("a/+/+/+", "a/b/c/d", ["b", "c", "d"], True),
+             ("stuff/#", "stuff/things/yeah", ["things/yeah"], True),
+             ("a/+/#/+", "a/b/c/d/as/dds", ["b", "c/d/as/dds"], True), ("test", "test", [], True),
+             ("things/stuff//", "things/stuff/", [], False), ("t", "t2", [], False), (" ", "  ", [], False)]
+    for f, t, el, m in cases:
+        assert O.match_topic(f, t) == (el, m), (f, t)
