@@ -193,8 +193,6 @@ void Profiler::reset() {
 // ---- device --------------------------------------------------------------------------------------
 Device::Device(int dev) : dev_(dev) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
-  const char* e = getenv("MQ_CHUNK_ROWS");
-  chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : (256ull << 20);  // 4 GiB of 16-B rows
   const char* ms = getenv("MQ_MERGE_STATS");  // diagnosis only
   merge_stats_ = ms != nullptr;
   if (ms && *ms) tstat_path_ = ms;
@@ -211,6 +209,9 @@ void Device::read_knobs() {
     return v ? (uint32_t)atoi(v) : def;
   };
   serial_ = getenv("MQ_SERIAL") != nullptr;                      // k_merge on the launch stream
+  const char* e = getenv("MQ_CHUNK_ROWS");  // output chunk budget (tests use small ones)
+  chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : kChunkRows;
+  chunk_tail_ = knob("MQ_CHUNK_TAIL", kChunkTail);
   // 0: one wavefront per tile / topic; else a persistent grid of that many workgroups per CU
   copy_blocks_ = n_cus_ * knob("MQ_COPY_BLOCKS_PER_CU", kCopyBlocksPerCU);
   merge_blocks_ = n_cus_ * knob("MQ_MERGE_BLOCKS_PER_CU", kMergeBlocksPerCU);
@@ -502,14 +503,23 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       gstride = 0;
     }
 
-    // plan output chunks on scan-block boundaries so each chunk's rows fit the budget
+    // Plan output chunks on scan-block boundaries, each within the row budget. The merge of the
+    // last chunk runs alone after every copy, so the rows are cut into equal main chunks plus a
+    // last one of about budget / chunk_tail rows: the exposed tail is that small chunk's merge.
     std::vector<Chunk> chunks;
     std::vector<ChunkPlan> plan;
     std::vector<uint32_t> chunk_of_block(q.nb);
     uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1, total_tiles = 0;
+    uint64_t target = chunk_rows_budget_;
+    if (tot.rows > chunk_rows_budget_ && chunk_tail_ > 1) {
+      const uint64_t main_rows = tot.rows - chunk_rows_budget_ / chunk_tail_;
+      const uint64_t n_main = (main_rows + chunk_rows_budget_ - 1) / chunk_rows_budget_;
+      target = (main_rows + n_main - 1) / n_main;
+    }
     for (uint32_t b = 0; b < q.nb;) {
       uint32_t e = b + 1;
-      while (e < q.nb && hb[e + 1].rows - hb[b].rows <= chunk_rows_budget_) e++;
+      const uint64_t cap = tot.rows - hb[b].rows <= chunk_rows_budget_ ? chunk_rows_budget_ : target;
+      while (e < q.nb && hb[e + 1].rows - hb[b].rows <= cap) e++;
       const TopicOff &lo = hb[b], &hi = hb[e];
       for (uint32_t k = b; k < e; k++) chunk_of_block[k] = (uint32_t)chunks.size();
       chunks.push_back(Chunk{sb, b, e});
