@@ -42,14 +42,17 @@ def host_cores():
     return max(1, min(n, 16))  # the GPU box allots 16 host cores per GPU
 
 
-def read_traffic(path, n_subs):
-    """HBM bytes per k_copy launch from a committed rocprofv3 PMC summary, if present."""
+def read_traffic(path, n_subs, write_bytes_per_launch):
+    """HBM bytes per k_copy launch (FETCH_SIZE x2 + WRITE_SIZE) from a committed rocprofv3 PMC
+    summary of the same configuration, if present: the entry is used only when its WRITE_SIZE per
+    launch is within 5 % of this run's algorithmic bytes per launch (same chunking)."""
     try:
         with open(path) as f:
-            d = json.load(f)
-        e = d.get(str(n_subs))
-        return None if e is None else float(e["hbm_bytes_per_copy_launch"])
-    except (OSError, ValueError, KeyError):
+            e = json.load(f).get(str(n_subs))
+        if e is None or abs(float(e["write"]) - write_bytes_per_launch) > 0.05 * write_bytes_per_launch:
+            return None
+        return float(e["hbm_bytes_per_copy_launch"])
+    except (OSError, ValueError, KeyError, TypeError):
         return None
 
 
@@ -152,7 +155,7 @@ def main():
         per_launch = copy_bytes / copy_launches
         achieved = per_launch / (launch_ms * 1e-3) / 1e9
         roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS,
-                    traffic=read_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), args.subs))
+                    traffic=read_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), args.subs, per_launch))
         out["copy_avg_launch_ms"] = launch_ms
         out["copy_bytes_per_launch"] = per_launch
         # the whole step against the same roofline: all output bytes / step time
