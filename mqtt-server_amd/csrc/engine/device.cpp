@@ -212,6 +212,7 @@ void Device::read_knobs() {
   const char* e = getenv("MQ_CHUNK_ROWS");  // output chunk budget (tests use small ones)
   chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : kChunkRows;
   chunk_tail_ = knob("MQ_CHUNK_TAIL", kChunkTail);
+  chunk_min_ = knob("MQ_CHUNK_MIN", kChunkMin);
   // 0: one wavefront per tile / topic; else a persistent grid of that many workgroups per CU
   copy_blocks_ = n_cus_ * knob("MQ_COPY_BLOCKS_PER_CU", kCopyBlocksPerCU);
   merge_blocks_ = n_cus_ * knob("MQ_MERGE_BLOCKS_PER_CU", kMergeBlocksPerCU);
@@ -510,15 +511,20 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     std::vector<ChunkPlan> plan;
     std::vector<uint32_t> chunk_of_block(q.nb);
     uint64_t max_rows = 1, max_shr = 1, max_inl = 1, max_topics = 1, total_tiles = 0;
-    uint64_t target = chunk_rows_budget_;
-    if (tot.rows > chunk_rows_budget_ && chunk_tail_ > 1) {
-      const uint64_t main_rows = tot.rows - chunk_rows_budget_ / chunk_tail_;
-      const uint64_t n_main = (main_rows + chunk_rows_budget_ - 1) / chunk_rows_budget_;
+    // at least chunk_min_ chunks (so merges overlap copies) unless chunks would get small
+    uint64_t target = std::min<uint64_t>(chunk_rows_budget_,
+                                         std::max<uint64_t>(tot.rows / std::max(1u, chunk_min_) + 1, kChunkRowsMin));
+    if (tot.rows > target && chunk_tail_ > 1) {
+      const uint64_t main_rows = tot.rows - target / chunk_tail_;
+      const uint64_t n_main = (main_rows + target - 1) / target;
       target = (main_rows + n_main - 1) / n_main;
     }
     for (uint32_t b = 0; b < q.nb;) {
       uint32_t e = b + 1;
-      const uint64_t cap = tot.rows - hb[b].rows <= chunk_rows_budget_ ? chunk_rows_budget_ : target;
+      const uint64_t remaining = tot.rows - hb[b].rows;
+      const uint64_t cap = chunk_tail_ > 1 && remaining <= target + target / chunk_tail_
+                               ? std::min<uint64_t>(remaining, chunk_rows_budget_)
+                               : target;
       while (e < q.nb && hb[e + 1].rows - hb[b].rows <= cap) e++;
       const TopicOff &lo = hb[b], &hi = hb[e];
       for (uint32_t k = b; k < e; k++) chunk_of_block[k] = (uint32_t)chunks.size();

@@ -10,6 +10,8 @@ namespace mq {
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
 constexpr uint64_t kChunkRows = 0xF0000000ull;  // output rows per chunk (60 GiB of 16-B rows; u32 row indices)
+constexpr uint32_t kChunkMin = 2;               // a large batch is cut into at least this many chunks
+constexpr uint64_t kChunkRowsMin = 64ull << 20;  // ... unless they would hold fewer rows than this
 constexpr uint32_t kChunkTail = 0;               // > 1: last chunk ~ kChunkRows / kChunkTail rows (measured: no gain)
 constexpr uint32_t kSubBatchTopics = 1u << 22;  // topics per pipelined sub-batch (Device::match)
 constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves per tile
