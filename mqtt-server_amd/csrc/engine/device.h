@@ -158,8 +158,8 @@ class Device {
   uint64_t uploaded_ = 0, syncs_ = 0;
   uint32_t last_chunks_ = 0;
   uint64_t chunk_rows_budget_;
-  uint32_t chunk_tail_ = 0;
-  uint32_t chunk_min_ = 2;  // chunks a large batch is cut into at least (MQ_CHUNK_MIN)  // last chunk ~ budget / chunk_tail_ (0, 1: plain budget cuts)
+  uint32_t chunk_tail_ = 0;  // > 1: last chunk ~ target / chunk_tail_ (MQ_CHUNK_TAIL)
+  uint32_t chunk_min_ = 2;   // chunks a large batch is cut into at least (MQ_CHUNK_MIN)
   DevMirror<EdgeSlot> edges_;
   DevMirror<NodeWalk> walk_;
   DevMirror<NodeLists> lists_;
