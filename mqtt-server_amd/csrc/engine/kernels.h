@@ -16,7 +16,7 @@ constexpr uint32_t kChunkTail = 0;               // > 1: last chunk ~ kChunkRows
 constexpr uint32_t kSubBatchTopics = 1u << 22;  // topics per pipelined sub-batch (Device::match)
 constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves per tile
 constexpr uint32_t kCopyBlocksPerCU = 8;   // persistent k_copy: 256-thread workgroups per CU
-constexpr uint32_t kMergeBlocksPerCU = 8;  // persistent k_merge beside it (side stream)
+constexpr uint32_t kMergeBlocksPerCU = 0;  // persistent k_merge beside it (side stream)
 constexpr uint32_t kMapSlots = 128;    // per-wave LDS map (gathered merge node -> gather index)
 constexpr uint32_t kPairMax = 64;     // merge gathers covered by the pair analysis
 constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
