@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 2
+#define MQ_ABI_VERSION 3
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
