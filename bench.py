@@ -62,7 +62,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--subs", type=int, default=10_000_000)
-    ap.add_argument("--clients", type=int, default=0, help="default: subs/10 (SURVEY.md §8d)")
+    ap.add_argument("--clients", type=int, default=0, help="default: subs/10 (mqtt mix), subs (iot mix)")
+    ap.add_argument("--mix", choices=["mqtt", "iot"], default="mqtt",
+                    help="mqtt: config-2/3 mix (the metric's); iot: config-4 IoT fan-in (exact device filters + 1%% dashboards)")
     ap.add_argument("--topics", type=int, default=1_000_000, help="publish topics per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -77,16 +79,17 @@ def main():
     local = D.device_for(local_rank)
     torch.cuda.set_device(local)
     backend = D.init(local_rank)
-    n_clients = args.clients or max(1, args.subs // 10)
+    mix = W.MIX_IOT if args.mix == "iot" else W.MIX_MQTT
+    n_clients = args.clients or (args.subs if args.mix == "iot" else max(1, args.subs // 10))
 
     t0 = time.time()
-    w = W.gen_subscriptions(args.subs, n_clients, seed=W.BASE_SEED)
+    w = W.gen_subscriptions(args.subs, n_clients, seed=W.BASE_SEED, mix=mix)
     log(f"generated {args.subs} subscriptions ({w['n_unique_filters']} distinct filters) in {time.time()-t0:.1f}s")
     t0 = time.time()
     eng = E.Engine(device=local, expected_subs=args.subs)
     eng.subscribe_bulk(w)
     log(f"engine index built in {time.time()-t0:.1f}s: {eng.stats()}")
-    tb, to = W.gen_topics(w, args.topics, seed=D.topic_seed(rank))
+    tb, to = W.gen_topics(w, args.topics, seed=D.topic_seed(rank), mix=mix)
     n = len(to) - 1
 
     stream = torch.cuda.current_stream()
@@ -118,6 +121,12 @@ def main():
     elapsed = D.max_over_ranks(elapsed, backend)
     chunks = eng.match_chunks()
     log(f"timed {args.steps} steps in {elapsed:.3f}s; kernels {prof}; chunks/step {chunks}")
+    try:
+        with open("/proc/self/status") as f:
+            hwm = [l.split()[1] for l in f if l.startswith("VmHWM")]
+        log(f"peak host memory of this rank: {int(hwm[0]) / 2**20:.1f} GiB")
+    except (OSError, IndexError, ValueError):
+        pass
 
     if rank != 0:
         D.finalize(backend)
@@ -130,8 +139,12 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (SURVEY.md §8d generator, seed 0x6D716D61)",
         "config": {
-            "workload": f"config-3 mix: {args.subs} subscriptions (depth 4-8, 30% '+', 10% '#', "
-                        f"5% $share, 0.1% top-level wildcards), {n} publish topics per GPU per step",
+            "workload": (f"config-3 mix: {args.subs} subscriptions (depth 4-8, 30% '+', 10% '#', "
+                         f"5% $share, 0.1% top-level wildcards), {n} publish topics per GPU per step")
+                        if args.mix == "mqtt" else
+                        (f"config-4 IoT fan-in: {args.subs} subscriptions (exact dev/r/s/d/telemetry filters, "
+                         f"one client each, 1% dashboards dev/r/+/+/telemetry | dev/r/s/#), {n} device topics "
+                         f"per GPU per step"),
             "subs": args.subs, "clients": n_clients, "topics_per_gpu": n,
             "parallelism": f"index replicated on {world} GPU(s), topic batch per GPU",
         },

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 R=$GRAFT_REPO_ROOT
-D=$R/gpurun_out/final2
+D=$R/gpurun_out/final3
 mkdir -p $D
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $D/pytest_gpu.log 2>&1 || exit 1
 timeout -k 10 500 python bench.py --steps 10 --warmup 2 --cpu-seconds 10 > $D/bench_10m.json 2> $D/bench_10m.err || exit 1
