@@ -29,6 +29,19 @@ METRIC = "matched publishes/sec (whole node) at 10M subs; HBM GB/s fraction of p
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def heartbeat(period=30.0):
+    """Log a line every `period` s from a daemon thread, so that long host phases (generating or
+    building a 50M-100M entry index) are not mistaken for a hung run."""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            log(f"... working ({time.time() - t0:.0f}s)")
+    threading.Thread(target=run, daemon=True).start()
+
+
 def log(msg):
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -69,6 +82,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    heartbeat()
 
     import torch
     from mqmatch import dist as D

@@ -22,6 +22,19 @@ sys.path.insert(0, os.path.join(REPO, "mqtt-server_amd"))
 HBM_PEAK_GBS = 8000.0
 
 
+def heartbeat(period=30.0):
+    """Log a line every `period` s from a daemon thread, so that long host phases (generating or
+    building a 50M-100M entry index) are not mistaken for a hung run."""
+    import threading
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period)
+            log(f"... working ({time.time() - t0:.0f}s)")
+    threading.Thread(target=run, daemon=True).start()
+
+
 def log(msg):
     print(f"[bench_messages {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -36,6 +49,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    heartbeat()
     import torch
     from mqmatch import engine as E
     from mqmatch import workload as W
@@ -107,6 +121,12 @@ def main():
         cpu = {"value": m / secs, "unit": "filters/s", "cores": 16, "kind": "port",
                "sample": f"first {m} filters, 16 threads, Messages() per filter (oracle/)"}
     out["cpu_baseline"] = cpu
+    try:
+        with open("/proc/self/status") as f:
+            hwm = [l.split()[1] for l in f if l.startswith("VmHWM")]
+        log(f"peak host memory: {int(hwm[0]) / 2**20:.1f} GiB")
+    except (OSError, IndexError, ValueError):
+        pass
     print(json.dumps(out), flush=True)
 
 

@@ -252,7 +252,7 @@ uint64_t Device::device_bytes() const {
   uint64_t b = edges_.cap * sizeof(EdgeSlot) + walk_.cap * sizeof(NodeWalk) +
                lists_.cap * sizeof(NodeLists) + msg_.cap * sizeof(NodeMsg) +
                seginfo_.cap * sizeof(SegInfo) + segbytes_.cap + subs_.cap * sizeof(SubRec) +
-               shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * 4 +
+               shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * sizeof(ChildRec) +
                mref_.cap * sizeof(MergeRef) + mpart_.cap * sizeof(MergePart) +
                npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * sizeof(PairSlot);
   for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &desc_[0], &desc_[1],
@@ -839,5 +839,6 @@ template struct DevMirror<PairSlot>;
 template struct DevMirror<ShrRec>;
 template struct DevMirror<InlRec>;
 template struct DevMirror<uint32_t>;
+template struct DevMirror<ChildRec>;
 
 }  // namespace mq

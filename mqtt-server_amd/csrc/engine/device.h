@@ -174,7 +174,7 @@ class Device {
   DevMirror<PairSlot> plist_;
   DevMirror<ShrRec> shr_;
   DevMirror<InlRec> inl_;
-  DevMirror<uint32_t> children_;
+  DevMirror<ChildRec> children_;
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   // Output chunks alternate between two buffer sets so that k_merge of chunk i (side stream)

@@ -337,7 +337,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   L.flags = flags & kFlagSeg0Wild;
   lists.at_w(id) = L;
   NodeMsg M{};
-  M.depth = h.depth;
+  M.parent = parent;
   M.key_sys = (parent == kRoot && seg == "$SYS") ? 1u : 0u;
   msg.at_w(id) = M;
 
@@ -347,10 +347,20 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   NodeMsg& pm = msg.at_w(parent);
   h.child_pos = pm.child_cnt;
   msg.h[id].child_pos = pm.child_cnt;
-  list_push(children, pm.child_off, pm.child_cnt, nh_[parent].child_cap, id);
+  list_push(children, pm.child_off, pm.child_cnt, nh_[parent].child_cap,
+            ChildRec{id, 0, 0, M.key_sys ? kChildSys : 0u, 0});
+  child_rec_sync(parent);  // the parent's slab may have moved
   nh_[parent].n_children++;
   n_live_nodes_++;
   return id;
+}
+
+void Index::child_rec_sync(uint32_t n) {
+  if (n == kRoot) return;
+  const NodeMsg& M = msg.h[n];
+  const uint32_t p = M.parent;
+  children.m.at_w(msg.h[p].child_off + M.child_pos) =
+      ChildRec{n, M.child_off, M.child_cnt, M.flags | (M.key_sys ? kChildSys : 0u), M.handle};
 }
 
 void Index::remove_node(uint32_t n) {
@@ -360,12 +370,13 @@ void Index::remove_node(uint32_t n) {
   if (h.str == 0) walk.at_w(p).plus_child = kNone;
   if (h.str == 1) walk.at_w(p).hash_child = kNone;
   NodeMsg& pm = msg.at_w(p);
-  uint32_t last = children.m.h[pm.child_off + pm.child_cnt - 1];
+  const ChildRec last = children.m.h[pm.child_off + pm.child_cnt - 1];
   children.m.at_w(pm.child_off + h.child_pos) = last;
-  nh_[last].child_pos = h.child_pos;
-  msg.at_w(last).child_pos = h.child_pos;
+  nh_[last.node].child_pos = h.child_pos;
+  msg.at_w(last.node).child_pos = h.child_pos;
   pm.child_cnt--;
   children.live--;
+  child_rec_sync(p);
   nh_[p].n_children--;
   // release the node's (empty) slabs
   subs.release(lists.h[n].sub_off, h.sub_cap);
@@ -901,6 +912,7 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
     NodeMsg& M = msg.at_w(n);
     M.flags = path ? (kRetainPath | kRetainLive) : 0;
     M.handle = path ? handle : 0;
+    child_rec_sync(n);
     retained_[t] = RetEntry{handle, payload_len, retain};
     if (topic.empty()) {
       empty_topic_live = true;
@@ -915,6 +927,7 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
   NodeMsg& M = msg.at_w(n);
   M.flags = 0;
   M.handle = 0;
+  child_rec_sync(n);
   if (it != retained_.end()) retained_.erase(it);
   if (topic.empty()) empty_topic_live = false;
   trim(n);
@@ -935,6 +948,7 @@ int Index::retained_delete(std::string_view topic) {
   if (n != kNone && nh_[n].retain_path) {
     NodeMsg& M = msg.at_w(n);
     M.flags &= ~kRetainLive;
+    child_rec_sync(n);
   }
   return 1;
 }

@@ -185,7 +185,7 @@ class Index {
   SlabPool<PairSlot> plist;
   SlabPool<ShrRec> shr;
   SlabPool<InlRec> inl;
-  SlabPool<uint32_t> children;
+  SlabPool<ChildRec> children;  // per node: its children (NodeMsg.child_off/child_cnt)
   // Retained packet stored on topic "" (retainPath "" is "no path", Q6): literal-final
   // lookups of particles without a retain path read this entry (topics.go:573).
   bool empty_topic_live = false;
@@ -215,6 +215,8 @@ class Index {
   uint32_t find_child(uint32_t parent, const SegKey& k, std::string_view seg) const;
   uint32_t new_node(uint32_t parent, std::string_view seg, const SegKey& k);
   void remove_node(uint32_t n);
+  // Refresh n's entry in its parent's children slab from msg[n] (after any NodeMsg change).
+  void child_rec_sync(uint32_t n);
   void edge_insert(uint32_t parent, const SegKey& k, uint32_t child);
   void edge_erase(uint32_t parent, const SegKey& k, uint32_t child);
   void edge_rehash(size_t cap);

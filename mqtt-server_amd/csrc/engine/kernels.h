@@ -39,7 +39,7 @@ struct DevIndex {
   const PairSlot* plist;
   const ShrRec* shr;
   const InlRec* inl;
-  const uint32_t* children;
+  const ChildRec* children;
   uint64_t retained_len;
   uint64_t empty_topic_handle;
   uint32_t empty_topic_live;

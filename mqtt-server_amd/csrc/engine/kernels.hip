@@ -905,7 +905,9 @@ void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
 // enumeration frame (and k + 64, ...), applies the frame's per-child rule (Q4 $SYS skip at level
 // 0, emit at the last level, descend otherwise) and walks the child's subtree depth-first
 // without a stack — a frame is (node, level d); a '+'/'#' level enumerates the node's children
-// slab and, after returning from child c, resumes at c's slab position + 1 (NodeMsg.child_pos);
+// slab (ChildRec: each child's retained state and own slab, read sequentially; childless
+// children are never entered) and, after returning from child c, resumes at c's slab position
+// + 1 (NodeMsg.child_pos, NodeMsg.parent);
 // levels past the last segment repeat it (isolateParticle, topics.go:679-698), which is how a
 // trailing '#' covers the subtree. A lane stops when it returns to the enumeration frame.
 // FILL=false counts the packets per filter; FILL=true walks again and appends them at the
@@ -1000,12 +1002,13 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
           if (FILL) out[atomicAdd(&cursor[wv], 1u)] = h;
           c++;
         };
-        const uint32_t ch0 = ix.children[nm.child_off + k];
-        const NodeMsg cm0 = ix.msg[ch0];
-        if (fd == 0 && cm0.key_sys) return 0u;  // only the exact $SYS particle, level 0 (Q4)
-        if (!has_next && (cm0.flags & kRetainPath) && (cm0.flags & kRetainLive)) emit(cm0.handle);
-        if (!(has_next || hash)) return c;
-        uint32_t node = ch0, d = fd + 1, wd = fd;  // wd: level of the segment in the window
+        const ChildRec r0 = ix.children[nm.child_off + k];
+        if (fd == 0 && (r0.flags & kChildSys)) return 0u;  // only the exact $SYS particle, level 0 (Q4)
+        if (!has_next && (r0.flags & kRetainPath) && (r0.flags & kRetainLive)) emit(r0.handle);
+        // a childless particle has nothing below it for any further level: not entered
+        if (!(has_next || hash) || r0.child_cnt == 0) return c;
+        uint32_t node = r0.node, d = fd + 1, wd = fd;  // wd: level of the segment in the window
+        uint32_t coff = r0.child_off, ccnt = r0.child_cnt;  // node's children slab
         uint64_t s = fs, e = fe;
         SegKey key = fkey;
         if (e < b1) {
@@ -1026,16 +1029,16 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
           const bool plus = c0 == '+';
           const bool hsh = c0 == '#';
           bool descended = false;
-          if (plus || hsh) {  // topics.go:547-565
-            const NodeMsg xm = ix.msg[node];
+          if (plus || hsh) {  // topics.go:547-565: the slab copy holds what each child needs
             if (!resume) cursor = 0;
-            while (cursor < xm.child_cnt) {
-              const uint32_t ch = ix.children[xm.child_off + cursor];
+            while (cursor < ccnt) {
+              const ChildRec cr = ix.children[coff + cursor];
               cursor++;
-              const NodeMsg cm = ix.msg[ch];
-              if (!has_nx && (cm.flags & kRetainPath) && (cm.flags & kRetainLive)) emit(cm.handle);
-              if (has_nx || hsh) {
-                node = ch;
+              if (!has_nx && (cr.flags & kRetainPath) && (cr.flags & kRetainLive)) emit(cr.handle);
+              if ((has_nx || hsh) && cr.child_cnt != 0) {
+                node = cr.node;
+                coff = cr.child_off;
+                ccnt = cr.child_cnt;
                 d++;
                 if (e < b1) {
                   s = e + 1;
@@ -1049,20 +1052,22 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
           } else if (!resume) {  // literal level (topics.go:568-576)
             const uint32_t p = lookup(ix, node, key, fb + s, len);
             if (p != kNone) {
+              const NodeMsg m = ix.msg[p];
               if (has_nx) {
-                node = p;
-                d++;
-                s = e + 1;
-                e = scan_segment(R, s, b1, &key);
-                wd++;
-                descended = true;
-              } else {
-                const NodeMsg m = ix.msg[p];
-                if (m.flags & kRetainPath) {
-                  if (m.flags & kRetainLive) emit(m.handle);
-                } else if (ix.empty_topic_live) {
-                  emit(ix.empty_topic_handle);  // Q6
+                if (m.child_cnt != 0) {
+                  node = p;
+                  coff = m.child_off;
+                  ccnt = m.child_cnt;
+                  d++;
+                  s = e + 1;
+                  e = scan_segment(R, s, b1, &key);
+                  wd++;
+                  descended = true;
                 }
+              } else if (m.flags & kRetainPath) {
+                if (m.flags & kRetainLive) emit(m.handle);
+              } else if (ix.empty_topic_live) {
+                emit(ix.empty_topic_handle);  // Q6
               }
             }
           }
@@ -1074,7 +1079,10 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
           // frame is done when we would return into it
           if (d == fd + 1) break;
           const NodeMsg cm = ix.msg[node];
-          node = ix.walk[node].parent_flags & kParentMask;
+          node = cm.parent;
+          const NodeMsg pm = ix.msg[node];
+          coff = pm.child_off;
+          ccnt = pm.child_cnt;
           if (wd == d) {
             e = s - 1;
             s = seg_start_before(R, b0, e);

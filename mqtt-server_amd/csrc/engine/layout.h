@@ -111,14 +111,26 @@ struct NodeLists {
 // Retained-message state and children of a node, for Messages (32 B).
 constexpr uint32_t kRetainPath = 1u;  // particle.retainPath != "" (topics.go:755)
 constexpr uint32_t kRetainLive = 2u;  // Retained map holds the path (Q12 decouples the two)
+constexpr uint32_t kChildSys = 4u;    // ChildRec: key == "$SYS" under the root (topics.go:549)
 struct NodeMsg {
-  uint32_t child_off, child_cnt;  // children slab (u32 node ids) for '+'/'#' enumeration
+  uint32_t child_off, child_cnt;  // children slab (ChildRec) for '+'/'#' enumeration
   uint32_t flags;                 // kRetainPath | kRetainLive
-  uint32_t depth;
+  uint32_t parent;                // parent node (the stackless Messages walk returns through it)
   uint64_t handle;                // retained packet handle when kRetainLive
   uint32_t key_sys;               // key == "$SYS" under the root (topics.go:549)
   uint32_t child_pos;             // position in the parent's children slab
 };
+
+// Entry of a node's children slab (24 B): the child and a copy of the NodeMsg fields a '+'/'#'
+// enumeration needs, so that enumerating children reads the slab sequentially instead of one
+// random NodeMsg per child (Index::child_rec_sync keeps the copy current).
+struct ChildRec {
+  uint32_t node;
+  uint32_t child_off, child_cnt;  // the child's own children slab
+  uint32_t flags;                 // kRetainPath | kRetainLive | kChildSys
+  uint64_t handle;
+};
+static_assert(sizeof(ChildRec) == 24, "ChildRec layout");
 
 struct SegInfo {  // long segment bytes in the segment pool
   uint32_t off, len;
