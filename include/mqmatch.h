@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 3
+#define MQ_ABI_VERSION 4
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
@@ -53,9 +53,16 @@ extern "C" {
 
 typedef struct mq_index mq_index;
 
+/* mq_config.flags. MQ_CFG_SELECT_SHARED: SelectShared runs on the device (k_pick) and every
+ * match result's shared rows hold only the picked member of each shared filter (its client
+ * with the smallest id) — for brokers whose hooks do not implement OnSelectSubscribers
+ * (server.go:1001-1006), where the Go pick is the first member in random map order
+ * (topics.go:320-333). The shim then builds SharedSelected from these rows directly. */
+#define MQ_CFG_SELECT_SHARED 1u
+
 typedef struct mq_config {
   int32_t device;          /* HIP device ordinal; the device is first touched by mq_sync/match */
-  uint32_t flags;          /* reserved, 0 */
+  uint32_t flags;          /* MQ_CFG_* */
   uint64_t expected_subs;  /* capacity hint (0 = default) */
   uint64_t expected_nodes; /* capacity hint (0 = default) */
 } mq_config;
@@ -197,6 +204,16 @@ typedef void (*mq_chunk_fn)(void* user, const mq_match_result* chunk, uint32_t f
 int mq_match_device_chunks(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t* d_offsets, uint32_t n,
                            void* hip_stream, mq_chunk_fn fn, void* user);
 uint32_t mq_match_chunks(const mq_index* idx);
+
+/* SelectShared on the device (topics.go:320-333) for device results (a chunk
+ * handed to an mq_chunk_fn, or mq_match_device's output), enqueued on hip_stream: for every
+ * topic t, one member (smallest client id) of each shared filter among its shared rows is
+ * written to d_selected[topics[t].shared_base + k], k < d_n_selected[t]. d_selected holds
+ * n_shared_rows rows, d_n_selected n_topics u32. The chunk is not modified. Replaces the
+ * host's SelectShared when no OnSelectSubscribers hook picks (server.go:1001-1006). It takes
+ * no handle lock, so an mq_chunk_fn may call it on its chunk; a match must have run first. */
+int mq_select_shared_device(mq_index* idx, const mq_match_result* chunk, void* hip_stream,
+                            mq_shared_row* d_selected, uint32_t* d_n_selected);
 
 /* ---- batched reverse retained scan: TopicsIndex.Messages (topics.go:525-579) ---- */
 typedef struct mq_msg_result {

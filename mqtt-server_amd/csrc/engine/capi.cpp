@@ -27,6 +27,7 @@ struct mq_index {
     if (!dev) {
       dev.reset(new Device(cfg.device));
       dev->prof.enable(profile);
+      dev->set_select_shared((cfg.flags & MQ_CFG_SELECT_SHARED) != 0);
     }
     return *dev;
   }
@@ -218,6 +219,22 @@ int mq_match_device_chunks(mq_index* idx, const uint8_t* d_tb, const uint64_t* d
     idx->device().match(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, nullptr, &last, fn, user);
     return 0;
   });
+}
+
+int mq_select_shared_device(mq_index* idx, const mq_match_result* chunk, void* stream,
+                            mq_shared_row* d_sel, uint32_t* d_n) {
+  if (!chunk || (chunk->n_topics && (!chunk->topics || !d_n)) || (chunk->n_shared_rows && (!chunk->shared_rows || !d_sel)))
+    return fail(MQ_EINVAL, "null argument");
+  if (!idx) return fail(MQ_EINVAL, "null index");
+  // No handle lock: this is called from inside mq_match_device_chunks' consumer, which runs
+  // under it. It reads only the chunk and the device's guard flag, set up by that match.
+  if (!idx->dev) return fail(MQ_EINVAL, "no match has run on this index");
+  try {
+    idx->dev->select_shared(*chunk, (hipStream_t)stream, reinterpret_cast<ShrRec*>(d_sel), d_n);
+    return 0;
+  } catch (const HipError& e) {
+    return fail(MQ_EIO, e.where);
+  }
 }
 
 uint32_t mq_match_chunks(const mq_index* idx) {

@@ -229,7 +229,7 @@ Device::~Device() {
                     &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_, &tstat_, &acl_buf_})
     b->release();
   for (int k = 0; k < 2; k++) {
-    for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k]}) b->release();
+    for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
     if (copy_done_[k]) (void)hipEventDestroy(copy_done_[k]);
     if (merge_done_[k]) (void)hipEventDestroy(merge_done_[k]);
   }
@@ -259,7 +259,7 @@ uint64_t Device::device_bytes() const {
                           &tiles_[0], &tiles_[1]})
     b += x->bytes;
   for (int k = 0; k < 2; k++)
-    for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k]}) b += x->bytes;
+    for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b += x->bytes;
   return b;
 }
 
@@ -323,8 +323,23 @@ void Device::check_err(hipStream_t s) {
     hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
     throw HipError{hipErrorUnknown, std::string("device guard tripped: ") +
                                         ((e & kErrWalkGuard) ? "walk iteration bound " : "") +
-                                        ((e & kErrTableFull) ? "merge table full" : "")};
+                                        ((e & kErrTableFull) ? "merge table full " : "") +
+                                        ((e & kErrPickGuard) ? "shared pick partitions" : "")};
   }
+}
+
+void Device::select_shared(const mq_match_result& r, hipStream_t s, ShrRec* d_sel, uint32_t* d_n) {
+  if (!err_.p) throw HipError{hipErrorNotReady, "select_shared before any match"};
+  PickArgs pa;
+  pa.res = reinterpret_cast<const mq_topic_result_dev*>(r.topics);
+  pa.rows = reinterpret_cast<const ShrRec*>(r.shared_rows);
+  pa.sel = d_sel;
+  pa.n_out = d_n;
+  pa.n_out_stride = 1;
+  pa.n = r.n_topics;
+  pa.err = err_.as<uint32_t>();
+  launch_pick(pa, s);
+  hip_check(hipGetLastError(), "k_pick");  // the guard flag is reported by the next match
 }
 
 void Device::stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hipStream_t s,
@@ -633,17 +648,34 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       launch_merge(a, merge_blocks_, ms);
       prof.end("merge", ms);
       hip_check(hipGetLastError(), "k_merge");
+      const uint32_t nt = a.t1 - a.t0;
+      const ShrRec* shr_out = a.shr_rows;
+      if (select_shared_) {  // SelectShared on the device: the chunk's shared rows become the picks
+        grow(sel_rows_[b], shr_rows_[b].bytes);
+        PickArgs pa;
+        pa.res = a.res;
+        pa.rows = a.shr_rows;
+        pa.sel = sel_rows_[b].as<ShrRec>();
+        pa.n_out = &a.res[0].n_shared;
+        pa.n_out_stride = sizeof(mq_topic_result_dev) / sizeof(uint32_t);
+        pa.n = nt;
+        pa.err = err_.as<uint32_t>();
+        prof.begin(ms);
+        launch_pick(pa, ms);
+        prof.end("pick", ms);
+        hip_check(hipGetLastError(), "k_pick");
+        shr_out = pa.sel;
+      }
       prof.count("copy_rows", (uint64_t)a.total[0] + a.total[1] + a.total[2]);
       prof.count("copy_bytes", 16ull * a.total[0] + 8ull * a.total[1] + 8ull * a.total[2]);
       prof.count("merge_records", hi.merge - lo.merge);
       last_chunks_++;
 
-      const uint32_t nt = a.t1 - a.t0;
       if (host) {
         const TopicOff& g = base[sb];
         hip_check(hipMemcpyAsync(host->rows.data() + g.rows + lo.rows, a.rows, (hi.rows - lo.rows) * sizeof(SubRec),
                                  hipMemcpyDeviceToHost, ms), "D2H rows");
-        hip_check(hipMemcpyAsync(host->shr.data() + g.shr + lo.shr, a.shr_rows, (hi.shr - lo.shr) * sizeof(ShrRec),
+        hip_check(hipMemcpyAsync(host->shr.data() + g.shr + lo.shr, shr_out, (hi.shr - lo.shr) * sizeof(ShrRec),
                                  hipMemcpyDeviceToHost, ms), "D2H shared rows");
         hip_check(hipMemcpyAsync(host->inl.data() + g.inl + lo.inl, a.inl_rows, (hi.inl - lo.inl) * sizeof(InlRec),
                                  hipMemcpyDeviceToHost, ms), "D2H inline rows");
@@ -655,7 +687,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       cr.n_topics = nt;
       cr.topics = reinterpret_cast<const mq_topic_result*>(a.res);
       cr.sub_rows = reinterpret_cast<const mq_client_row*>(a.rows);
-      cr.shared_rows = reinterpret_cast<const mq_shared_row*>(a.shr_rows);
+      cr.shared_rows = reinterpret_cast<const mq_shared_row*>(shr_out);
       cr.inline_rows = reinterpret_cast<const mq_inline_row*>(a.inl_rows);
       cr.n_sub_rows = hi.rows - lo.rows;
       cr.n_shared_rows = hi.shr - lo.shr;

@@ -142,6 +142,12 @@ class Device {
   void stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hipStream_t s,
                     const uint8_t** d_tb, const uint64_t** d_to);
 
+  // SelectShared on the device (k_pick) for a chunk of device results: picked rows to d_sel at
+  // each topic's shared_base, picked counts to d_n (mq_select_shared_device).
+  void select_shared(const mq_match_result& r, hipStream_t s, ShrRec* d_sel, uint32_t* d_n);
+  // MQ_CFG_SELECT_SHARED: match results carry only the picked member of each shared filter.
+  void set_select_shared(bool on) { select_shared_ = on; }
+
   uint32_t last_chunks() const { return last_chunks_; }
   uint64_t device_bytes() const;
   uint64_t upload_bytes() const { return uploaded_; }
@@ -180,6 +186,8 @@ class Device {
   // Output chunks alternate between two buffer sets so that k_merge of chunk i (side stream)
   // overlaps k_desc/k_copy of chunk i + 1 (launch stream).
   DevBuf rows_[2], shr_rows_[2], inl_rows_[2], res_[2];
+  DevBuf sel_rows_[2];          // k_pick output (MQ_CFG_SELECT_SHARED)
+  bool select_shared_ = false;
   // per sub-batch parity: gather records and k_copy tile table
   DevBuf desc_[2], tiles_[2];
   // chunk plans + block -> chunk maps of every sub-batch ([nb_all] plans, then [nb_all] u32)

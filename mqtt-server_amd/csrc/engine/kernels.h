@@ -49,6 +49,7 @@ struct DevIndex {
 
 constexpr uint32_t kErrWalkGuard = 1u;
 constexpr uint32_t kErrTableFull = 2u;
+constexpr uint32_t kErrPickGuard = 4u;  // k_pick: hash partitions exhausted
 constexpr uint64_t kWalkGuard = 1ull << 26;
 
 // Exclusive offsets of a topic's outputs (scan of TopicCount).
@@ -135,6 +136,18 @@ struct AclArgs {
   uint32_t* elems;
 };
 void launch_acl(const AclArgs& a, hipStream_t s);
+
+// SelectShared on the device (k_pick): per topic, one member of every shared filter.
+struct PickArgs {
+  const mq_topic_result_dev* res;  // n topic results (shared_base / n_shared read)
+  const ShrRec* rows;              // the chunk's shared rows
+  ShrRec* sel;                     // picked rows of topic t at [shared_base, + picked)
+  uint32_t* n_out;                 // picked count of topic t at n_out[t * n_out_stride]
+  uint32_t n_out_stride;
+  uint32_t n;
+  uint32_t* err;                   // kErrPickGuard
+};
+void launch_pick(const PickArgs& a, hipStream_t s);
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
                  TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf, hipStream_t s);

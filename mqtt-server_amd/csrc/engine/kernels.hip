@@ -1172,6 +1172,100 @@ void launch_acl(const AclArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_acl, dim3((uint32_t)((a.n_pairs + 255) / 256)), dim3(256), 0, s, a);
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_pick — SelectShared on the device (topics.go:320-333). Go keeps the first
+// member of each Shared[filter] map in random iteration order, so any one member is a conformant
+// pick; this one is deterministic: the member with the smallest client id. One wavefront per
+// topic: the topic's shared rows are inserted into a per-wave LDS hash table keyed by filter id
+// (atomicMin of the client per slot), then streamed again in row order and each filter's picked
+// row is compacted by ballot/mbcnt into `sel` at the topic's shared_base. A topic with more
+// distinct filters than the table holds is re-run in hash partitions (2, 4, ... passes over its
+// rows), each pass with the table to itself. (filter, client) pairs are unique within a topic
+// (a filter lives at one node, keyed there by (group, client)), so exactly one row wins.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kPickSlots = 1024;       // per wave: 8 KB of LDS
+constexpr uint32_t kPickProbe = 256;        // probe bound before a pass is split
+constexpr uint32_t kPickMaxParts = 1u << 16;
+
+__global__ __launch_bounds__(256) void k_pick(PickArgs a) {
+  __shared__ uint32_t keys[4][kPickSlots];  // filter id + 1 (0 = empty)
+  __shared__ uint32_t vals[4][kPickSlots];  // smallest client id seen
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * 4 + w;
+  if (t >= a.n) return;  // whole wavefront
+  uint32_t* K = keys[w];
+  uint32_t* V = vals[w];
+  const uint64_t base = a.res[t].shared_base;
+  const uint32_t cnt = a.res[t].n_shared;
+  const ShrRec* rows = a.rows + base;
+  uint32_t picked = 0;
+  uint32_t parts = 1;
+  for (uint32_t part = 0; cnt && part < parts;) {
+    for (uint32_t i = lane; i < kPickSlots; i += 64) {
+      K[i] = 0;
+      V[i] = 0xFFFFFFFFu;
+    }
+    wave_sync_lds();
+    bool full = false;
+    for (uint32_t r = lane; r < cnt; r += 64) {
+      const ShrRec rec = rows[r];
+      if (parts > 1 && hash32(rec.filter_id ^ 0x5bd1e995u) % parts != part) continue;
+      const uint32_t key = rec.filter_id + 1;
+      uint32_t slot = hash32(rec.filter_id) & (kPickSlots - 1);
+      uint32_t probe = 0;
+      for (;; probe++) {
+        if (probe == kPickProbe) {
+          full = true;
+          break;
+        }
+        const uint32_t old = atomicCAS(&K[slot], 0u, key);
+        if (old == 0u || old == key) {
+          atomicMin(&V[slot], rec.client);
+          break;
+        }
+        slot = (slot + 1) & (kPickSlots - 1);
+      }
+    }
+    wave_sync_lds();
+    if (__any(full)) {  // too many filters for one table: start over in twice as many partitions
+      if (parts >= kPickMaxParts) {
+        if (lane == 0) atomicOr(a.err, kErrPickGuard);
+        picked = 0;
+        break;
+      }
+      parts *= 2;
+      part = 0;
+      picked = 0;
+      continue;
+    }
+    for (uint32_t rb = 0; rb < cnt; rb += 64) {
+      const uint32_t r = rb + lane;
+      bool take = false;
+      ShrRec rec{0, 0};
+      if (r < cnt) {
+        rec = rows[r];
+        if (parts == 1 || hash32(rec.filter_id ^ 0x5bd1e995u) % parts == part) {
+          const uint32_t key = rec.filter_id + 1;
+          uint32_t slot = hash32(rec.filter_id) & (kPickSlots - 1);
+          while (K[slot] != key) slot = (slot + 1) & (kPickSlots - 1);  // inserted above
+          take = V[slot] == rec.client;
+        }
+      }
+      const uint64_t m = __ballot(take);
+      if (take) a.sel[base + picked + prefix_before(m)] = rec;
+      picked += (uint32_t)__popcll(m);
+    }
+    wave_sync_lds();  // the next pass clears the table
+    part++;
+  }
+  if (lane == 0) a.n_out[(uint64_t)t * a.n_out_stride] = picked;
+}
+
+void launch_pick(const PickArgs& a, hipStream_t s) {
+  if (!a.n) return;
+  hipLaunchKernelGGL(k_pick, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
+}
+
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
                 uint32_t* count, hipStream_t s) {

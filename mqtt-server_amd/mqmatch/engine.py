@@ -78,8 +78,10 @@ EXPORTS = [
     "mq_match_batch", "mq_match_device", "mq_match_chunks", "mq_messages_batch",
     "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
     "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
-    "mq_acl_match_batch",
+    "mq_acl_match_batch", "mq_select_shared_device",
 ]
+
+CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
 
 CHUNK_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(MatchResult), C.c_uint32, C.c_void_p)
 
@@ -120,6 +122,7 @@ def lib():
         "mq_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MatchResult))]),
         "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
         "mq_match_chunks": (C.c_uint32, [vp]),
+        "mq_select_shared_device": (C.c_int, [vp, C.POINTER(MatchResult), vp, vp, vp]),
         "mq_match_device_chunks": (C.c_int, [vp, vp, vp, C.c_uint32, vp, CHUNK_FN, vp]),
         "mq_acl_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, _u8p, _u64p, C.c_uint32, _u32p, _u32p,
                                          C.c_uint64, C.POINTER(C.POINTER(AclResult))]),
@@ -242,9 +245,11 @@ def is_share_prefix(seg: str) -> bool:
 class Engine:
     """Thin object wrapper over one mq_index handle (id-level C-ABI)."""
 
-    def __init__(self, device=0, expected_subs=0, expected_nodes=0):
+    def __init__(self, device=0, expected_subs=0, expected_nodes=0, select_shared=False):
+        """select_shared: MQ_CFG_SELECT_SHARED (results carry one picked member per shared
+        filter; SelectShared ran on the device)."""
         L = lib()
-        cfg = MqConfig(device, 0, expected_subs, expected_nodes)
+        cfg = MqConfig(device, CFG_SELECT_SHARED if select_shared else 0, expected_subs, expected_nodes)
         h = C.c_void_p()
         _check(L.mq_index_create(C.byref(cfg), C.byref(h)), "mq_index_create")
         self.h = h
@@ -404,6 +409,13 @@ class Engine:
                                             C.c_void_p(stream) if stream else None, cb, None),
                "mq_match_device_chunks")
 
+    def select_shared_device(self, chunk, stream, d_selected, d_n_selected):
+        """mq_select_shared_device on a device MatchResult (SelectShared, topics.go:320-333):
+        picked rows to d_selected at each topic's shared_base, counts to d_n_selected."""
+        _check(lib().mq_select_shared_device(self.h, C.byref(chunk), C.c_void_p(stream) if stream else None,
+                                             C.c_void_p(d_selected), C.c_void_p(d_n_selected)),
+               "mq_select_shared_device")
+
     def match_chunks(self):
         return int(lib().mq_match_chunks(self.h))
 
@@ -474,8 +486,10 @@ def topic_rows(res, t):
 class TopicsIndex:
     """Mirror of the Go TopicsIndex (topics.go:349-698) over the engine's C-ABI."""
 
-    def __init__(self, device=0):
-        self.engine = Engine(device)
+    def __init__(self, device=0, select_shared=False):
+        """select_shared: SelectShared on the device (MQ_CFG_SELECT_SHARED) — each Shared[filter]
+        holds only its picked member, for a broker with no OnSelectSubscribers hook."""
+        self.engine = Engine(device, select_shared=select_shared)
         self.client_ids: Dict[str, int] = {}
         self.clients: List[str] = []
         self.filter_ids: Dict[str, int] = {}
