@@ -1186,74 +1186,105 @@ void launch_acl(const AclArgs& a, hipStream_t s) {
 constexpr uint32_t kPickSlots = 1024;       // per wave: 8 KB of LDS
 constexpr uint32_t kPickProbe = 256;        // probe bound before a pass is split
 constexpr uint32_t kPickMaxParts = 1u << 16;
+constexpr uint32_t kPickBatch = 16;         // rows per lane in flight (1024 per wave)
 
-__global__ __launch_bounds__(256) void k_pick(PickArgs a) {
-  __shared__ uint32_t keys[4][kPickSlots];  // filter id + 1 (0 = empty)
-  __shared__ uint32_t vals[4][kPickSlots];  // smallest client id seen
-  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t t = blockIdx.x * 4 + w;
-  if (t >= a.n) return;  // whole wavefront
-  uint32_t* K = keys[w];
-  uint32_t* V = vals[w];
+__device__ __forceinline__ bool pick_in_part(uint32_t filter_id, uint32_t parts, uint32_t part) {
+  return parts == 1 || hash32(filter_id ^ 0x5bd1e995u) % parts == part;
+}
+
+// One wavefront per workgroup: a topic's table is released as soon as its own wave ends.
+__global__ __launch_bounds__(64) void k_pick(PickArgs a) {
+  __shared__ uint32_t K[kPickSlots];  // filter id + 1 (0 = empty)
+  __shared__ uint32_t V[kPickSlots];  // smallest client id seen
+  const uint32_t lane = threadIdx.x;
+  const uint32_t t = blockIdx.x;
   const uint64_t base = a.res[t].shared_base;
   const uint32_t cnt = a.res[t].n_shared;
   const ShrRec* rows = a.rows + base;
+  constexpr uint32_t kSpan = 64 * kPickBatch;
+  const bool resident = cnt <= kSpan;  // the mark pass reuses the rows held in registers
+  ShrRec buf[kPickBatch];
   uint32_t picked = 0;
   uint32_t parts = 1;
+  // table size: a power of two >= 2 * rows (64 .. kPickSlots), so small topics clear little
+  uint32_t tsize = 64;
+  while (tsize < kPickSlots && tsize < 2 * cnt) tsize *= 2;
   for (uint32_t part = 0; cnt && part < parts;) {
-    for (uint32_t i = lane; i < kPickSlots; i += 64) {
+    const uint32_t tmask = tsize - 1;
+    for (uint32_t i = lane; i < tsize; i += 64) {
       K[i] = 0;
       V[i] = 0xFFFFFFFFu;
     }
     wave_sync_lds();
     bool full = false;
-    for (uint32_t r = lane; r < cnt; r += 64) {
-      const ShrRec rec = rows[r];
-      if (parts > 1 && hash32(rec.filter_id ^ 0x5bd1e995u) % parts != part) continue;
-      const uint32_t key = rec.filter_id + 1;
-      uint32_t slot = hash32(rec.filter_id) & (kPickSlots - 1);
-      uint32_t probe = 0;
-      for (;; probe++) {
-        if (probe == kPickProbe) {
-          full = true;
-          break;
+    for (uint32_t rb = 0; rb < cnt; rb += kSpan) {
+#pragma unroll
+      for (uint32_t j = 0; j < kPickBatch; j++) {  // all loads issued before any use
+        const uint32_t r = rb + j * 64 + lane;
+        buf[j] = r < cnt ? rows[r] : ShrRec{0, 0};
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kPickBatch; j++) {
+        const uint32_t r = rb + j * 64 + lane;
+        if (r >= cnt || !pick_in_part(buf[j].filter_id, parts, part)) continue;
+        const uint32_t key = buf[j].filter_id + 1;
+        uint32_t slot = hash32(buf[j].filter_id) & tmask;
+        for (uint32_t probe = 0;; probe++) {
+          if (probe == kPickProbe || probe == tsize) {
+            full = true;
+            break;
+          }
+          // plain LDS reads first: a filter's later members mostly find their slot claimed
+          // and the client beaten, and skip the atomics (same-slot atomics serialise)
+          uint32_t k = K[slot];
+          if (k == 0u) {
+            k = atomicCAS(&K[slot], 0u, key);
+            if (k == 0u) k = key;
+          }
+          if (k == key) {
+            if (buf[j].client < V[slot]) atomicMin(&V[slot], buf[j].client);
+            break;
+          }
+          slot = (slot + 1) & tmask;
         }
-        const uint32_t old = atomicCAS(&K[slot], 0u, key);
-        if (old == 0u || old == key) {
-          atomicMin(&V[slot], rec.client);
-          break;
-        }
-        slot = (slot + 1) & (kPickSlots - 1);
       }
     }
     wave_sync_lds();
-    if (__any(full)) {  // too many filters for one table: start over in twice as many partitions
+    if (__any(full)) {  // too many filters for the table: grow it, then split into partitions
       if (parts >= kPickMaxParts) {
         if (lane == 0) atomicOr(a.err, kErrPickGuard);
         picked = 0;
         break;
       }
-      parts *= 2;
+      if (tsize < kPickSlots) tsize = kPickSlots;
+      else parts *= 2;
       part = 0;
       picked = 0;
       continue;
     }
-    for (uint32_t rb = 0; rb < cnt; rb += 64) {
-      const uint32_t r = rb + lane;
-      bool take = false;
-      ShrRec rec{0, 0};
-      if (r < cnt) {
-        rec = rows[r];
-        if (parts == 1 || hash32(rec.filter_id ^ 0x5bd1e995u) % parts == part) {
-          const uint32_t key = rec.filter_id + 1;
-          uint32_t slot = hash32(rec.filter_id) & (kPickSlots - 1);
-          while (K[slot] != key) slot = (slot + 1) & (kPickSlots - 1);  // inserted above
-          take = V[slot] == rec.client;
+    for (uint32_t rb = 0; rb < cnt; rb += kSpan) {
+      if (!resident) {
+#pragma unroll
+        for (uint32_t j = 0; j < kPickBatch; j++) {
+          const uint32_t r = rb + j * 64 + lane;
+          buf[j] = r < cnt ? rows[r] : ShrRec{0, 0};
         }
       }
-      const uint64_t m = __ballot(take);
-      if (take) a.sel[base + picked + prefix_before(m)] = rec;
-      picked += (uint32_t)__popcll(m);
+#pragma unroll
+      for (uint32_t j = 0; j < kPickBatch; j++) {
+        if (rb + j * 64 >= cnt) break;  // wave-uniform
+        const uint32_t r = rb + j * 64 + lane;
+        bool take = false;
+        if (r < cnt && pick_in_part(buf[j].filter_id, parts, part)) {
+          const uint32_t key = buf[j].filter_id + 1;
+          uint32_t slot = hash32(buf[j].filter_id) & tmask;
+          while (K[slot] != key) slot = (slot + 1) & tmask;  // inserted above
+          take = V[slot] == buf[j].client;
+        }
+        const uint64_t m = __ballot(take);
+        if (take) a.sel[base + picked + prefix_before(m)] = buf[j];
+        picked += (uint32_t)__popcll(m);
+      }
     }
     wave_sync_lds();  // the next pass clears the table
     part++;
@@ -1263,7 +1294,7 @@ __global__ __launch_bounds__(256) void k_pick(PickArgs a) {
 
 void launch_pick(const PickArgs& a, hipStream_t s) {
   if (!a.n) return;
-  hipLaunchKernelGGL(k_pick, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_pick, dim3(a.n), dim3(64), 0, s, a);
 }
 
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
