@@ -218,6 +218,8 @@ void Device::read_knobs() {
   merge_blocks_ = n_cus_ * knob("MQ_MERGE_BLOCKS_PER_CU", kMergeBlocksPerCU);
   merge_diag_ = knob("MQ_MERGE_DIAG", 0);
   subbatch_topics_ = knob("MQ_SUBBATCH_TOPICS", kSubBatchTopics);  // topics per pipelined sub-batch
+  const char* sb = getenv("MQ_MSG_SPEC_MB");  // Messages speculative-count scratch (0: two walks)
+  msg_spec_bytes_ = (sb ? strtoull(sb, nullptr, 10) : kMsgSpecMB) << 20;
 }
 
 Device::~Device() {
@@ -226,7 +228,7 @@ Device::~Device() {
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
-                    &msg_handles_, &msg_base_, &msg_count_, &gslots_, &mstats_, &tstat_, &acl_buf_})
+                    &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &mstats_, &tstat_, &acl_buf_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
@@ -819,8 +821,17 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   offs_.ensure((size_t)(n + 1) * sizeof(TopicOff));
   bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
   bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+  // Speculative count: the count pass also writes each filter's first `cap` handles to scratch,
+  // so that only filters with more (or counted through below_live) are walked a second time.
+  uint32_t cap = (uint32_t)std::min<uint64_t>(kMsgSpecCap, msg_spec_bytes_ / ((uint64_t)n * sizeof(uint64_t)));
+  if (cap < 64) cap = 0;
+  uint64_t* spec = nullptr;
+  if (cap) {
+    msg_spec_.ensure((size_t)n * cap * sizeof(uint64_t));
+    spec = msg_spec_.as<uint64_t>();
+  }
   prof.begin(s);
-  launch_msg(false, d_fb, d_fo, n, di, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, s);
+  launch_msg(false, d_fb, d_fo, n, di, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, spec, cap, s);
   prof.end("msg_count", s);
   hip_check(hipGetLastError(), "k_msg<count>");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
@@ -832,9 +843,16 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   msg_handles_.ensure(std::max<uint64_t>(tot.rows, 1) * sizeof(uint64_t));
   msg_base_.ensure((size_t)n * sizeof(uint64_t));
   msg_count_.ensure((size_t)n * sizeof(uint32_t));
+  if (cap) {
+    prof.begin(s);
+    launch_msg_place(n, counts_.as<TopicCount>(), offs_.as<TopicOff>(), spec, cap, msg_handles_.as<uint64_t>(),
+                     msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), s);
+    prof.end("msg_place", s);
+    hip_check(hipGetLastError(), "k_msg_place");
+  }
   prof.begin(s);
-  launch_msg(true, d_fb, d_fo, n, di, nullptr, offs_.as<TopicOff>(), msg_handles_.as<uint64_t>(),
-             msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), s);
+  launch_msg(true, d_fb, d_fo, n, di, counts_.as<TopicCount>(), offs_.as<TopicOff>(), msg_handles_.as<uint64_t>(),
+             msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), spec, cap, s);
   prof.end("msg_fill", s);
   hip_check(hipGetLastError(), "k_msg<fill>");
   out->n_filters = n;

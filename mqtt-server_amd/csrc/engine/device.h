@@ -207,6 +207,8 @@ class Device {
   hipStream_t side_ = nullptr;
   hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_, mstats_;
+  DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter
+  uint64_t msg_spec_bytes_ = 0;  // its budget (MQ_MSG_SPEC_MB)
   bool merge_stats_ = false;  // MQ_MERGE_STATS: k_merge work counters to stderr
   std::string tstat_path_;    // MQ_MERGE_STATS=<path>: per-topic k_merge counters (kTStat u32 each)
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)

@@ -338,7 +338,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   lists.at_w(id) = L;
   NodeMsg M{};
   M.parent = parent;
-  M.key_sys = (parent == kRoot && seg == "$SYS") ? 1u : 0u;
+  M.flags = (parent == kRoot && seg == "$SYS") ? kChildSys : 0u;
   msg.at_w(id) = M;
 
   edge_insert(parent, k, id);
@@ -348,11 +348,19 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   h.child_pos = pm.child_cnt;
   msg.h[id].child_pos = pm.child_cnt;
   list_push(children, pm.child_off, pm.child_cnt, nh_[parent].child_cap,
-            ChildRec{id, 0, 0, M.key_sys ? kChildSys : 0u, 0});
+            ChildRec{id, 0, 0, M.flags, 0});
   child_rec_sync(parent);  // the parent's slab may have moved
   nh_[parent].n_children++;
   n_live_nodes_++;
   return id;
+}
+
+// A live retained topic at n counts in below_live of every strict ancestor (root included).
+void Index::add_below_live(uint32_t n, int delta) {
+  for (uint32_t a = n; a != kRoot;) {
+    a = msg.h[a].parent;
+    msg.at_w(a).below_live += (uint32_t)delta;
+  }
 }
 
 void Index::child_rec_sync(uint32_t n) {
@@ -360,7 +368,7 @@ void Index::child_rec_sync(uint32_t n) {
   const NodeMsg& M = msg.h[n];
   const uint32_t p = M.parent;
   children.m.at_w(msg.h[p].child_off + M.child_pos) =
-      ChildRec{n, M.child_off, M.child_cnt, M.flags | (M.key_sys ? kChildSys : 0u), M.handle};
+      ChildRec{n, M.child_off, M.child_cnt, M.flags, M.handle};
 }
 
 void Index::remove_node(uint32_t n) {
@@ -582,6 +590,19 @@ bool Index::check(std::string* why) {
         if (!listed) return bad(at + ": pair list misses a slot");
       }
     }
+  }
+  {  // below_live == live retained particles strictly below, recomputed bottom-up
+    std::vector<uint32_t> below(nh_.size(), 0);
+    for (uint32_t n = 0; n < nh_.size(); n++) {
+      if (!nh_[n].live || n == kRoot || !(msg.h[n].flags & kRetainLive)) continue;
+      for (uint32_t a = n; a != kRoot;) {
+        a = msg.h[a].parent;
+        below[a]++;
+      }
+    }
+    for (uint32_t n = 0; n < nh_.size(); n++)
+      if ((nh_[n].live || n == kRoot) && below[n] != msg.h[n].below_live)
+        return bad("node " + std::to_string(n) + ": below_live stale");
   }
   return true;
 }
@@ -910,9 +931,11 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
     bool path = !topic.empty();  // retainPath = pk.TopicName; "" means no path
     nh_[n].retain_path = path;
     NodeMsg& M = msg.at_w(n);
-    M.flags = path ? (kRetainPath | kRetainLive) : 0;
+    const bool was_live = M.flags & kRetainLive;
+    M.flags = (M.flags & kChildSys) | (path ? (kRetainPath | kRetainLive) : 0);
     M.handle = path ? handle : 0;
     child_rec_sync(n);
+    if (path && !was_live) add_below_live(n, 1);
     retained_[t] = RetEntry{handle, payload_len, retain};
     if (topic.empty()) {
       empty_topic_live = true;
@@ -925,9 +948,11 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
   if (it != retained_.end() && it->second.payload_len > 0 && it->second.retain) out = -1;
   nh_[n].retain_path = false;
   NodeMsg& M = msg.at_w(n);
-  M.flags = 0;
+  const bool was_live = M.flags & kRetainLive;
+  M.flags &= kChildSys;
   M.handle = 0;
   child_rec_sync(n);
+  if (was_live) add_below_live(n, -1);
   if (it != retained_.end()) retained_.erase(it);
   if (topic.empty()) empty_topic_live = false;
   trim(n);
@@ -947,8 +972,10 @@ int Index::retained_delete(std::string_view topic) {
   uint32_t n = seek(topic, 0);
   if (n != kNone && nh_[n].retain_path) {
     NodeMsg& M = msg.at_w(n);
+    const bool was_live = M.flags & kRetainLive;
     M.flags &= ~kRetainLive;
     child_rec_sync(n);
+    if (was_live) add_below_live(n, -1);
   }
   return 1;
 }

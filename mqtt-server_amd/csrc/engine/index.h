@@ -217,6 +217,7 @@ class Index {
   void remove_node(uint32_t n);
   // Refresh n's entry in its parent's children slab from msg[n] (after any NodeMsg change).
   void child_rec_sync(uint32_t n);
+  void add_below_live(uint32_t n, int delta);
   void edge_insert(uint32_t parent, const SegKey& k, uint32_t child);
   void edge_erase(uint32_t parent, const SegKey& k, uint32_t child);
   void edge_rehash(size_t cap);

@@ -14,6 +14,8 @@ constexpr uint32_t kChunkMin = 2;               // a large batch is cut into at 
 constexpr uint64_t kChunkRowsMin = 64ull << 20;  // ... unless they would hold fewer rows than this
 constexpr uint32_t kChunkTail = 0;               // > 1: last chunk ~ kChunkRows / kChunkTail rows (measured: no gain)
 constexpr uint32_t kSubBatchTopics = 1u << 22;  // topics per pipelined sub-batch (Device::match)
+constexpr uint64_t kMsgSpecMB = 16384;  // Messages: speculative-count scratch budget (MiB)
+constexpr uint32_t kMsgSpecCap = 32768;  // ... and at most this many handles per filter
 constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves per tile
 constexpr uint32_t kCopyBlocksPerCU = 8;   // persistent k_copy: 256-thread workgroups per CU
 constexpr uint32_t kMergeBlocksPerCU = 0;  // persistent k_merge beside it (side stream)
@@ -156,8 +158,13 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
 void launch_desc(const DescArgs& a, hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
 void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
+// k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
+// first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
+// fill pass must still walk; the fill pass then walks only those.
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
-                uint32_t* count, hipStream_t s);
+                uint32_t* count, uint64_t* spec, uint32_t spec_cap, hipStream_t s);
+void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
+                      uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
 
 }  // namespace mq

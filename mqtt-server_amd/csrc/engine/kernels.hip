@@ -920,14 +920,20 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
                                              const TopicOff* __restrict__ off,
                                              uint64_t* __restrict__ handles,
                                              uint64_t* __restrict__ base_out,
-                                             uint32_t* __restrict__ count_out) {
-  __shared__ uint32_t cursor[4];  // FILL: next free slot of the wave's filter
+                                             uint32_t* __restrict__ count_out,
+                                             uint64_t* __restrict__ spec, uint32_t spec_cap) {
+  __shared__ uint32_t cursor[4];  // FILL / speculative count: next free slot of the filter
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t t = blockIdx.x * 4 + wv;
   if (t >= n) return;  // wave-uniform
+  // FILL after a speculative count: only the filters k_msg_place could not place are walked
+  if (FILL && spec && cnt[t].gathers == 0) return;
   const uint64_t b0 = fo[t], b1 = fo[t + 1];
   uint32_t total = 0;  // packets of this filter (wave-uniform)
   uint64_t* out = FILL ? handles + off[t].rows : nullptr;
+  // speculative count: the handles also go to the filter's scratch slots (first spec_cap)
+  uint64_t* sp = (!FILL && spec) ? spec + (uint64_t)t * spec_cap : nullptr;
+  bool partial = false;  // a count shortcut (below_live) left the scratch incomplete
   // len(filter) == 0 || Retained.Len() == 0 (topics.go:535)
   if (b1 > b0 && ix.retained_len != 0) {
     ByteReader R(fb);
@@ -952,6 +958,7 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
       }
       if (node != kNone && (ix.msg[node].flags & kRetainLive)) {
         if (FILL && lane == 0) out[0] = ix.msg[node].handle;
+        if (sp && lane == 0 && spec_cap) sp[0] = ix.msg[node].handle;
         total = 1;
       }
     } else {
@@ -983,6 +990,7 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
         }
         if (hit) {
           if (FILL && lane == 0) out[0] = h;
+          if (sp && lane == 0 && spec_cap) sp[0] = h;
           total = 1;
         }
         break;
@@ -999,7 +1007,12 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
       auto child = [&](uint32_t k) -> uint32_t {
         uint32_t c = 0;
         auto emit = [&](uint64_t h) {
-          if (FILL) out[atomicAdd(&cursor[wv], 1u)] = h;
+          if (FILL) {
+            out[atomicAdd(&cursor[wv], 1u)] = h;
+          } else if (sp) {
+            const uint32_t q = atomicAdd(&cursor[wv], 1u);
+            if (q < spec_cap) sp[q] = h;
+          }
           c++;
         };
         const ChildRec r0 = ix.children[nm.child_off + k];
@@ -1007,6 +1020,11 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
         if (!has_next && (r0.flags & kRetainPath) && (r0.flags & kRetainLive)) emit(r0.handle);
         // a childless particle has nothing below it for any further level: not entered
         if (!(has_next || hash) || r0.child_cnt == 0) return c;
+        // count pass, '#' frame: every live retained topic below the child, from its aggregate
+        if (!FILL && hash) {
+          partial = true;
+          return c + ix.msg[r0.node].below_live;
+        }
         uint32_t node = r0.node, d = fd + 1, wd = fd;  // wd: level of the segment in the window
         uint32_t coff = r0.child_off, ccnt = r0.child_cnt;  // node's children slab
         uint64_t s = fs, e = fe;
@@ -1029,7 +1047,10 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
           const bool plus = c0 == '+';
           const bool hsh = c0 == '#';
           bool descended = false;
-          if (plus || hsh) {  // topics.go:547-565: the slab copy holds what each child needs
+          if (!FILL && hsh) {  // count pass: the subtree's live retained topics (below_live)
+            c += ix.msg[node].below_live;
+            partial = true;
+          } else if (plus || hsh) {  // topics.go:547-565: the slab copy holds what each child needs
             if (!resume) cursor = 0;
             while (cursor < ccnt) {
               const ChildRec cr = ix.children[coff + cursor];
@@ -1094,17 +1115,23 @@ __global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
         }
         return c;
       };
-      if (FILL && lane == 0) cursor[wv] = total;
+      if ((FILL || sp) && lane == 0) cursor[wv] = total;
       wave_sync_lds();
+      if (!FILL && hash && fd > 0) {
+        // count pass, '#' below level 0 (no $SYS exclusion): the frame's aggregate
+        total += nm.below_live;
+        partial = true;
+      } else
       for (uint32_t k0 = 0; k0 < nm.child_cnt; k0 += 64) {  // wave-uniform
         const uint32_t k = k0 + lane;
         total += wave_sum(k < nm.child_cnt ? child(k) : 0u);
       }
     }
   }
+  const bool walk_again = __any(partial) || total > spec_cap;  // for the FILL pass
   if (lane == 0) {
     if (!FILL) {
-      cnt[t] = TopicCount{0, total, 0, 0, 0};
+      cnt[t] = TopicCount{(sp && !walk_again) ? 0u : 1u, total, 0, 0, 0};
     } else {
       base_out[t] = off[t].rows;
       count_out[t] = total;
@@ -1299,13 +1326,46 @@ void launch_pick(const PickArgs& a, hipStream_t s) {
 
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
-                uint32_t* count, hipStream_t s) {
+                uint32_t* count, uint64_t* spec, uint32_t spec_cap, hipStream_t s) {
   if (!n) return;
   dim3 grid((n + 3) / 4);  // one wavefront per filter
   if (fill)
-    hipLaunchKernelGGL(k_msg<true>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count);
+    hipLaunchKernelGGL(k_msg<true>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count,
+                       spec, spec_cap);
   else
-    hipLaunchKernelGGL(k_msg<false>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count);
+    hipLaunchKernelGGL(k_msg<false>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count,
+                       spec, spec_cap);
+}
+
+// k_msg_place: after a speculative count, every filter whose handles all sit in its scratch
+// slots is moved to its output range (one wavefront per filter, coalesced 8-byte rows); the
+// others (more than spec_cap handles, or counted through a below_live shortcut) are left to
+// k_msg<true>, which walks only them.
+__global__ __launch_bounds__(256) void k_msg_place(uint32_t n, const TopicCount* __restrict__ cnt,
+                                                   const TopicOff* __restrict__ off,
+                                                   const uint64_t* __restrict__ spec, uint32_t spec_cap,
+                                                   uint64_t* __restrict__ handles,
+                                                   uint64_t* __restrict__ base_out,
+                                                   uint32_t* __restrict__ count_out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n) return;
+  const TopicCount c = cnt[t];
+  if (c.gathers != 0) return;  // walked again by the FILL pass
+  const uint64_t o = off[t].rows;
+  const uint64_t* src = spec + (uint64_t)t * spec_cap;
+  for (uint32_t i = lane; i < c.rows; i += 64) handles[o + i] = src[i];
+  if (lane == 0) {
+    base_out[t] = o;
+    count_out[t] = c.rows;
+  }
+}
+
+void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
+                      uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_msg_place, dim3((n + 3) / 4), dim3(256), 0, s, n, cnt, off, spec, spec_cap, handles,
+                     base, count);
 }
 
 }  // namespace mq

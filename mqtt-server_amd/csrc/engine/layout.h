@@ -111,13 +111,14 @@ struct NodeLists {
 // Retained-message state and children of a node, for Messages (32 B).
 constexpr uint32_t kRetainPath = 1u;  // particle.retainPath != "" (topics.go:755)
 constexpr uint32_t kRetainLive = 2u;  // Retained map holds the path (Q12 decouples the two)
-constexpr uint32_t kChildSys = 4u;    // ChildRec: key == "$SYS" under the root (topics.go:549)
+constexpr uint32_t kChildSys = 4u;    // key == "$SYS" under the root (topics.go:549)
 struct NodeMsg {
   uint32_t child_off, child_cnt;  // children slab (ChildRec) for '+'/'#' enumeration
-  uint32_t flags;                 // kRetainPath | kRetainLive
+  uint32_t flags;                 // kRetainPath | kRetainLive | kChildSys
   uint32_t parent;                // parent node (the stackless Messages walk returns through it)
   uint64_t handle;                // retained packet handle when kRetainLive
-  uint32_t key_sys;               // key == "$SYS" under the root (topics.go:549)
+  uint32_t below_live;            // live retained topics strictly below this particle: a '#'
+                                  // frame's Messages count without walking the subtree
   uint32_t child_pos;             // position in the parent's children slab
 };
 

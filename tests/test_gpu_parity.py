@@ -347,9 +347,15 @@ def test_messages_empty_topic_retained(gpu_available):
         assert e.messages(f) == o.messages(f), f
 
 
-def test_messages_workload_parity(gpu_available):
+@pytest.mark.parametrize("spec_mb", [None, "0", "3"])
+def test_messages_workload_parity(spec_mb, gpu_available, monkeypatch):
+    """Messages on a config-5-shaped workload. spec_mb: the speculative count's scratch budget
+    (default: one walk for most filters; "0": count and fill walks; "3": a few hundred slots per
+    filter, so that many filters overflow their scratch and are walked again)."""
     from mqmatch import workload as W
     from mqmatch import engine as E
+    if spec_mb is not None:
+        monkeypatch.setenv("MQ_MSG_SPEC_MB", spec_mb)
     rb, ro, hd, rh = W.gen_retained(100000, n_sys=1000, seed=61)
     fb, fo = W.gen_msg_filters(rh, 5000, seed=62)
     eng, orc = E.Engine(), O.OracleIndex()
