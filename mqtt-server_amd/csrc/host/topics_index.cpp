@@ -10,8 +10,8 @@ static void check(int rc, const char* what) {
   if (rc < 0) throw EngineError(rc, std::string(what) + ": " + mq_last_error());
 }
 
-TopicsIndex::TopicsIndex(int device) {
-  mq_config cfg{device, 0, 0, 0};
+TopicsIndex::TopicsIndex(int device, bool select_shared) {
+  mq_config cfg{device, select_shared ? MQ_CFG_SELECT_SHARED : 0u, 0, 0};
   check(mq_index_create(&cfg, &idx_), "mq_index_create");
 }
 

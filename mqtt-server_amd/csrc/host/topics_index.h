@@ -84,7 +84,10 @@ struct EngineError : std::runtime_error {
 
 class TopicsIndex {
  public:
-  explicit TopicsIndex(int device = 0);  // NewTopicsIndex (topics.go:356)
+  // NewTopicsIndex (topics.go:356). select_shared: SelectShared on the device
+  // (MQ_CFG_SELECT_SHARED) — each Shared[filter] holds only its picked member, for brokers
+  // without an OnSelectSubscribers hook (server.go:1001-1006).
+  explicit TopicsIndex(int device = 0, bool select_shared = false);
   ~TopicsIndex();
   TopicsIndex(const TopicsIndex&) = delete;
   TopicsIndex& operator=(const TopicsIndex&) = delete;

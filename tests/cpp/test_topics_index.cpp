@@ -119,6 +119,27 @@ static void TestScanSubscribersShared() {  // topics_test.go:539-566
   REQUIRE(s.SharedSelected.size() == 4 || s.SharedSelected.size() == 3);  // one pick per group/filter
 }
 
+// The same subscriptions with SelectShared on the device: one member (the smallest client id)
+// per shared filter; the broker flow then picks it (topics.go:320-347).
+static void TestScanSubscribersSharedSelected() {
+  TopicsIndex x(0, true);
+  x.Subscribe("cl1", S("$SHARE/tmp/a/b/c", 1, 111));
+  x.Subscribe("cl2", S("$SHARE/tmp/a/b/c", 0, 112));
+  x.Subscribe("cl3", S("$SHARE/tmp2/a/b/c", 0, 113));
+  x.Subscribe("cl2", S("$SHARE/tmp/a/b/+", 0, 10));
+  x.Subscribe("cl3", S("$SHARE/tmp/a/b/+", 1, 200));
+  x.Subscribe("cl4", S("$SHARE/tmp/a/b/+", 0, 201));
+  x.Subscribe("cl5", S("$SHARE/tmp/a/b/c/#", 0));
+  auto s = x.Subscribers_("a/b/c");
+  REQUIRE(s.Shared.size() == 4);
+  for (const auto& f : s.Shared) REQUIRE(f.second.size() == 1);
+  REQUIRE(s.Shared.at("$SHARE/tmp/a/b/c").count("cl1"));  // client ids interned in order
+  REQUIRE(s.Shared.at("$SHARE/tmp/a/b/+").count("cl2"));
+  s.SelectShared();
+  s.MergeSharedSelected();
+  REQUIRE(s.SharedSelected.size() == 4 && s.Subscriptions.size() == 4);
+}
+
 static void TestSubscribersFind() {  // topics_test.go:590-625
   struct Row {
     const char *f, *t;
@@ -286,6 +307,7 @@ int main() {
     TestRetainMessage();
     TestScanSubscribers();
     TestScanSubscribersShared();
+    TestScanSubscribersSharedSelected();
     TestSubscribersFind();
     TestMessagesPattern();
     TestInline();
