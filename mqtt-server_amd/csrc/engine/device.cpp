@@ -821,6 +821,11 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   offs_.ensure((size_t)(n + 1) * sizeof(TopicOff));
   bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
   bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+  // k_msg register budget: on a large retained index the walk waits on HBM far more often, and
+  // 6 waves per SIMD (with spills) beat 4 (10M retained: 54.8 -> 50.2 ms per 100k filters); on
+  // a small, cache-resident one the spills cost more (1M: 8.7 vs 9.2 ms). MQ_MSG_WPE overrides.
+  msg_wpe_ = ix.retained_len() >= kMsgWpeMinRetained ? kMsgWavesPerEU : 1u;
+  if (const char* w = getenv("MQ_MSG_WPE")) msg_wpe_ = (uint32_t)atoi(w);  // read per batch (tuning)
   // Speculative count: the count pass also writes each filter's first `cap` handles to scratch,
   // so that only filters with more (or counted through below_live) are walked a second time.
   uint32_t cap = (uint32_t)std::min<uint64_t>(kMsgSpecCap, msg_spec_bytes_ / ((uint64_t)n * sizeof(uint64_t)));
@@ -831,7 +836,8 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
     spec = msg_spec_.as<uint64_t>();
   }
   prof.begin(s);
-  launch_msg(false, d_fb, d_fo, n, di, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, spec, cap, s);
+  launch_msg(false, d_fb, d_fo, n, di, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, spec, cap,
+             msg_wpe_, s);
   prof.end("msg_count", s);
   hip_check(hipGetLastError(), "k_msg<count>");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
@@ -852,7 +858,7 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   }
   prof.begin(s);
   launch_msg(true, d_fb, d_fo, n, di, counts_.as<TopicCount>(), offs_.as<TopicOff>(), msg_handles_.as<uint64_t>(),
-             msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), spec, cap, s);
+             msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), spec, cap, msg_wpe_, s);
   prof.end("msg_fill", s);
   hip_check(hipGetLastError(), "k_msg<fill>");
   out->n_filters = n;

@@ -209,6 +209,7 @@ class Device {
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_, mstats_;
   DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter
   uint64_t msg_spec_bytes_ = 0;  // its budget (MQ_MSG_SPEC_MB)
+  uint32_t msg_wpe_ = 1;         // k_msg variant (MQ_MSG_WPE)
   bool merge_stats_ = false;  // MQ_MERGE_STATS: k_merge work counters to stderr
   std::string tstat_path_;    // MQ_MERGE_STATS=<path>: per-topic k_merge counters (kTStat u32 each)
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)

@@ -16,6 +16,8 @@ constexpr uint32_t kChunkTail = 0;               // > 1: last chunk ~ kChunkRows
 constexpr uint32_t kSubBatchTopics = 1u << 22;  // topics per pipelined sub-batch (Device::match)
 constexpr uint64_t kMsgSpecMB = 16384;  // Messages: speculative-count scratch budget (MiB)
 constexpr uint32_t kMsgSpecCap = 32768;  // ... and at most this many handles per filter
+constexpr uint32_t kMsgWavesPerEU = 6;   // k_msg register budget: 1 (none), 6 or 8 waves per SIMD
+constexpr uint64_t kMsgWpeMinRetained = 4000000;  // ... used from this many retained topics on
 constexpr uint32_t kCopyTile = 4096;   // rows one k_copy wavefront moves per tile
 constexpr uint32_t kCopyBlocksPerCU = 8;   // persistent k_copy: 256-thread workgroups per CU
 constexpr uint32_t kMergeBlocksPerCU = 0;  // persistent k_merge beside it (side stream)
@@ -163,7 +165,7 @@ void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
 // fill pass must still walk; the fill pass then walks only those.
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
-                uint32_t* count, uint64_t* spec, uint32_t spec_cap, hipStream_t s);
+                uint32_t* count, uint64_t* spec, uint32_t spec_cap, uint32_t wpe, hipStream_t s);
 void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
                       uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
 

@@ -913,8 +913,11 @@ void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
 // FILL=false counts the packets per filter; FILL=true walks again and appends them at the
 // filter's offset through a per-wave LDS cursor (Messages' order is Go map order, i.e. none).
 // ---------------------------------------------------------------------------------------------
-template <bool FILL>
-__global__ __launch_bounds__(256) void k_msg(const uint8_t* __restrict__ fb,
+// WPE: minimum waves per SIMD asked of the register allocator (1 = no constraint). The walk
+// needs ~127 VGPRs (4 waves per SIMD); fewer registers with some spills buy occupancy for
+// this latency-bound kernel (MQ_MSG_WPE picks the variant).
+template <bool FILL, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_msg(const uint8_t* __restrict__ fb,
                                              const uint64_t* __restrict__ fo, uint32_t n,
                                              DevIndex ix, TopicCount* __restrict__ cnt,
                                              const TopicOff* __restrict__ off,
@@ -1324,17 +1327,29 @@ void launch_pick(const PickArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_pick, dim3(a.n), dim3(64), 0, s, a);
 }
 
-void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
-                TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
-                uint32_t* count, uint64_t* spec, uint32_t spec_cap, hipStream_t s) {
-  if (!n) return;
+template <int WPE>
+static void launch_msg_wpe(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                           TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
+                           uint32_t* count, uint64_t* spec, uint32_t spec_cap, hipStream_t s) {
   dim3 grid((n + 3) / 4);  // one wavefront per filter
   if (fill)
-    hipLaunchKernelGGL(k_msg<true>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count,
+    hipLaunchKernelGGL((k_msg<true, WPE>), grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count,
                        spec, spec_cap);
   else
-    hipLaunchKernelGGL(k_msg<false>, grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count,
-                       spec, spec_cap);
+    hipLaunchKernelGGL((k_msg<false, WPE>), grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base,
+                       count, spec, spec_cap);
+}
+
+void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
+                uint32_t* count, uint64_t* spec, uint32_t spec_cap, uint32_t wpe, hipStream_t s) {
+  if (!n) return;
+  if (wpe >= 8)
+    launch_msg_wpe<8>(fill, fb, fo, n, ix, cnt, off, handles, base, count, spec, spec_cap, s);
+  else if (wpe >= 6)
+    launch_msg_wpe<6>(fill, fb, fo, n, ix, cnt, off, handles, base, count, spec, spec_cap, s);
+  else
+    launch_msg_wpe<1>(fill, fb, fo, n, ix, cnt, off, handles, base, count, spec, spec_cap, s);
 }
 
 // k_msg_place: after a speculative count, every filter whose handles all sit in its scratch
