@@ -47,6 +47,16 @@ def log(msg):
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def _device_view(ptr, nbytes):
+    """A torch uint8 tensor over library-owned device memory (__cuda_array_interface__)."""
+    import torch
+
+    class _Buf:
+        __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (int(ptr), False),
+                                    "version": 3, "strides": None}
+    return torch.as_tensor(_Buf(), device="cuda")
+
+
 def host_cores():
     try:
         n = len(os.sched_getaffinity(0))
@@ -83,6 +93,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--select-shared", action="store_true",
                     help="MQ_CFG_SELECT_SHARED: SelectShared on the device (k_pick) in every step")
+    ap.add_argument("--format", choices=["spans", "rows"], default="spans",
+                    help="spans: mq_match_spans_device (gathered lists named, merges patched); rows: "
+                         "mq_match_device_chunks with every row materialised and each chunk consumed "
+                         "by a device-side checksum")
     args = ap.parse_args()
     heartbeat()
 
@@ -116,8 +130,25 @@ def main():
     torch.cuda.synchronize()
     log(f"device image uploaded in {time.time()-t0:.1f}s")
 
-    def step():
-        return eng.match_device(d_tb.data_ptr(), d_to.data_ptr(), n, stream.cuda_stream)
+    consumed = []
+
+    def consume(chunk, first, cstream):
+        # rows format: every chunk is read on its stream before its buffers are reused (a
+        # device-side checksum standing in for a fan-out), so the step delivers every row
+        nb = int(chunk.n_sub_rows) * 16
+        if nb:
+            t = torch.cuda.ExternalStream(cstream)
+            with torch.cuda.stream(t):
+                v = _device_view(chunk.sub_rows, nb)
+                consumed.append(v.view(torch.int64).sum())
+
+    if args.format == "spans":
+        def step():
+            return eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, stream.cuda_stream)
+    else:
+        def step():
+            consumed.clear()
+            eng.match_device_chunks(d_tb.data_ptr(), d_to.data_ptr(), n, stream.cuda_stream, consume)
 
     for _ in range(args.warmup):
         step()
@@ -164,6 +195,7 @@ def main():
             "subs": args.subs, "clients": n_clients, "topics_per_gpu": n,
             "parallelism": f"index replicated on {world} GPU(s), topic batch per GPU",
             "select_shared": bool(args.select_shared),
+            "format": args.format,
         },
         "kernels_ms_per_step": {k: v[1] / max(1, args.steps) for k, v in prof.items() if v[1] > 0},
         "counters_per_step": {k: v[0] / max(1, args.steps) for k, v in prof.items() if v[1] == 0},
@@ -215,9 +247,9 @@ def main():
         ns = min(m, 4096)
         dg_o, cnt_o, tot = orc.digest_batch(tb, to[:ns + 1], cores)
         if not args.select_shared:  # picked shared rows are checked by tests/test_gpu_select.py
-            res = eng.match_batch(tb, to[:ns + 1])
+            res = eng.match_batch_spans(tb, to[:ns + 1]) if args.format == "spans" else eng.match_batch(tb, to[:ns + 1])
             dg_e, _ = engine_digests(res)
-            out["parity_sample"] = {"topics": ns, "bit_exact": bool((dg_e == dg_o).all())}
+            out["parity_sample"] = {"topics": ns, "format": args.format, "bit_exact": bool((dg_e == dg_o).all())}
         per_topic = {k: v / ns for k, v in tot.items()}
         b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"] + 16 * per_topic["S"] + 16 * per_topic["O"]
         out["alg_bytes_per_topic"] = {"B": b_topic, "L": per_topic["L"], "P": per_topic["P"],

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 4
+#define MQ_ABI_VERSION 5
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
@@ -34,6 +34,7 @@ extern "C" {
 #define MQ_ENODEV (-19)
 #define MQ_EIO (-5)
 #define MQ_ERANGE (-34)
+#define MQ_ESTALE (-116)
 
 /* packets.Subscription flag bits (packets/packets.go:172-182) for mq_subscribe() */
 #define MQ_SUB_NOLOCAL 0x1u         /* NoLocal */
@@ -215,6 +216,80 @@ uint32_t mq_match_chunks(const mq_index* idx);
 int mq_select_shared_device(mq_index* idx, const mq_match_result* chunk, void* hip_stream,
                             mq_shared_row* d_selected, uint32_t* d_n_selected);
 
+/* ---- span format: Subscribers without copying the gathered lists (ABI v5) ----
+ *
+ * The row format above copies every gathered subscription of every topic into output rows; at
+ * 10M subscriptions a topic gathers ~15k of them (the root '#', '+/...', 'x/#' lists, the same
+ * for most topics), 245 KB per topic. The span format names them instead. A topic's result is
+ *   - one mq_span per gathered particle, in gather (DFS) order: its non-shared records
+ *     sub_pool[sub_off, + n_sub) (n_sub = 0 when the '$' rule drops them, Q3) and its shared
+ *     members shared_pool[shr_off, + n_shr);
+ *   - mq_patch records for the records whose row differs from the pool record: the merge base
+ *     of a client with several matches (merged Qos / NoLocal), or a later match of the client
+ *     (MQ_ROW_IDENT / MQ_ROW_DROP). `row` is the record's position in the concatenation of the
+ *     topic's spans' sub ranges (0 .. n_rows-1); each row is patched at most once; patches are
+ *     in no particular order;
+ *   - the inline rows, last-write applied (as in the row format).
+ * Expanding spans and applying patches gives exactly the row format's rows (mq_spans_expand).
+ * With MQ_CFG_SELECT_SHARED the picked shared members are materialised (picked_rows at
+ * picked_base, n_shared of them) and flags has MQ_SPANS_PICKED. */
+typedef struct mq_span {
+  uint32_t sub_off, n_sub; /* records sub_pool[sub_off, + n_sub) */
+  uint32_t shr_off, n_shr; /* members shared_pool[shr_off, + n_shr) */
+} mq_span;
+
+typedef struct mq_patch {
+  uint32_t row;  /* topic-relative record row */
+  uint32_t meta; /* replaces the pool record's meta (MQ_META_*, MQ_ROW_*) */
+} mq_patch;
+
+typedef struct mq_topic_spans {
+  uint64_t span_base, patch_base, inline_base, picked_base;
+  uint32_t n_spans, n_patches, n_inline;
+  uint32_t n_rows;   /* gathered non-shared records (client + ident + dropped rows) */
+  uint32_t n_client, n_ident;
+  uint32_t n_shared; /* shared members (picked members with MQ_SPANS_PICKED) */
+  uint32_t reserved;
+} mq_topic_spans;
+
+#define MQ_SPANS_PICKED 1u
+
+typedef struct mq_span_result {
+  uint32_t n_topics;
+  uint32_t flags; /* MQ_SPANS_PICKED */
+  const mq_topic_spans* topics;
+  const mq_span* spans;
+  const mq_patch* patches;
+  const mq_inline_row* inline_rows;
+  const mq_shared_row* picked_rows;
+  const mq_client_row* sub_pool;    /* the index's subscription records */
+  const mq_shared_row* shared_pool; /* the index's shared members */
+  uint64_t n_spans, n_patches, n_inline_rows, n_picked_rows;
+  uint64_t sub_pool_len, shared_pool_len;
+} mq_span_result;
+
+/* Span-format Subscribers for a batch of host topics (as mq_match_batch). The result's arrays
+ * are host copies; its pools point at the index's host image, which the result pins: updates
+ * issued while it is held wait until mq_result_free (as the reference's writers wait for the
+ * per-node read locks a gather holds, topics.go:270-277), so free it before updating from the
+ * same thread. */
+int mq_match_spans(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets, uint32_t n,
+                   mq_span_result** out);
+/* Device-resident span format (inputs in HBM, enqueued on hip_stream, as mq_match_device). All
+ * pointers in *out are DEVICE pointers owned by the index, valid until its next update or match
+ * call. The whole batch is one result (no chunks); the call returns after the batch's kernels
+ * have completed, with their guard flags checked (MQ_EIO when one tripped). */
+int mq_match_spans_device(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t* d_offsets,
+                          uint32_t n, void* hip_stream, mq_span_result* out);
+/* Materialise the rows of topics [first, first + count) of a HOST span result (mq_match_spans):
+ * their sub rows (n_rows each, patches applied: exactly the row format's rows) and shared rows,
+ * concatenated in topic order. Returns 0, or MQ_ERANGE when a capacity is too small; the
+ * numbers of rows written go to *n_rows / *n_shared (nullable). Thread-safe for disjoint
+ * outputs. */
+int mq_spans_expand(const mq_span_result* r, uint32_t first, uint32_t count, mq_client_row* rows,
+                    uint64_t rows_cap, mq_shared_row* shared, uint64_t shared_cap, uint64_t* n_rows,
+                    uint64_t* n_shared);
+
 /* ---- batched reverse retained scan: TopicsIndex.Messages (topics.go:525-579) ---- */
 typedef struct mq_msg_result {
   uint32_t n_filters;
@@ -270,6 +345,15 @@ int mq_index_stats(const mq_index* idx, mq_stats* out);
    the partner's current slot). Returns 0, or MQ_EIO with the first violation in
    mq_last_error(). */
 int mq_index_check(mq_index* idx);
+
+/* Engine options (tuning; the defaults are the product). Returns 0 or MQ_EINVAL. */
+#define MQ_OPT_CHUNK_ROWS 1      /* row format: output rows per chunk (default 0xF0000000) */
+#define MQ_OPT_SUBBATCH_TOPICS 2 /* row format: topics per pipelined sub-batch */
+#define MQ_OPT_MSG_SPEC_MB 3     /* Messages: speculative-count scratch budget (MiB; 0: two walks) */
+#define MQ_OPT_MSG_WAVES 4       /* Messages: k_msg waves per SIMD (1, 6, 8; 0: by index size) */
+#define MQ_OPT_SERIAL 5          /* 1: no side-stream overlap (isolated kernel timings) */
+#define MQ_OPT_PATCH_CAP 6       /* span format: initial patch pool capacity (patches) */
+int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. */
 typedef struct mq_kernel_time {

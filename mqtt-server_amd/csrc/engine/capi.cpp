@@ -3,12 +3,15 @@
 // and HIP failures into negative errno codes with a thread-local message.
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <cstring>
 #include <new>
 #include <string>
 #include <unordered_map>
+#include <utility>
+#include <vector>
 
 #include "device.h"
 #include "index.h"
@@ -16,18 +19,30 @@
 
 using namespace mq;
 
-struct mq_index {
+// The handle's lock. `views` counts host span results that pin the host image (their pools
+// point into it); updates wait until they are freed. Results hold a reference, so freeing one
+// after mq_index_destroy is safe.
+struct IndexLock {
   std::mutex mu;
+  std::condition_variable cv;
+  uint64_t views = 0;
+};
+
+struct mq_index {
+  std::shared_ptr<IndexLock> lk = std::make_shared<IndexLock>();
   mq_config cfg;
   std::unique_ptr<Index> ix;
   std::unique_ptr<Device> dev;
   bool profile = false;
+
+  std::vector<std::pair<uint32_t, uint64_t>> options;  // mq_set_option, in call order
 
   Device& device() {
     if (!dev) {
       dev.reset(new Device(cfg.device));
       dev->prof.enable(profile);
       dev->set_select_shared((cfg.flags & MQ_CFG_SELECT_SHARED) != 0);
+      for (auto& o : options) dev->set_option(o.first, o.second);
     }
     return *dev;
   }
@@ -41,6 +56,11 @@ struct MatchHolder {
   mq_match_result pub;  // first member: the pointer handed out
   HostMatch data;
 };
+struct SpanHolder {
+  mq_span_result pub;
+  HostSpans data;
+  std::shared_ptr<IndexLock> lk;  // the pinned index's lock (views)
+};
 struct MsgHolder {
   mq_msg_result pub;
   PinnedVec<uint64_t> base;
@@ -52,18 +72,22 @@ struct AclHolder {
   HostAcl data;
 };
 std::mutex g_res_mu;
-std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages, 3 = acl
+std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages, 3 = acl, 4 = spans
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
 
+// Runs f under the handle's lock; an update (writes the host image) first waits for the host
+// span results that pin it to be freed.
 template <class F>
-int guarded(mq_index* idx, F&& f) {
+int guarded(mq_index* idx, F&& f, bool update = false) {
   if (!idx) return fail(MQ_EINVAL, "null index");
   try {
-    std::lock_guard<std::mutex> lk(idx->mu);
+    IndexLock& L = *idx->lk;
+    std::unique_lock<std::mutex> lk(L.mu);
+    if (update) L.cv.wait(lk, [&] { return L.views == 0; });
     return f();
   } catch (const HipError& e) {
     return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
@@ -104,12 +128,12 @@ int mq_subscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t clie
   if (qos > 2) return fail(MQ_EINVAL, "qos > 2");
   return guarded(idx, [&] {
     return idx->ix->subscribe(std::string_view(filter, flen), client_id, filter_id, qos, flags, identifier);
-  });
+  }, true);
 }
 
 int mq_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t client_id) {
   if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
-  return guarded(idx, [&] { return idx->ix->unsubscribe(std::string_view(filter, flen), client_id); });
+  return guarded(idx, [&] { return idx->ix->unsubscribe(std::string_view(filter, flen), client_id); }, true);
 }
 
 int mq_inline_subscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier,
@@ -117,12 +141,12 @@ int mq_inline_subscribe(mq_index* idx, const char* filter, uint32_t flen, int32_
   if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
   return guarded(idx, [&] {
     return idx->ix->inline_subscribe(std::string_view(filter, flen), identifier, filter_id);
-  });
+  }, true);
 }
 
 int mq_inline_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier) {
   if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
-  return guarded(idx, [&] { return idx->ix->inline_unsubscribe(std::string_view(filter, flen), identifier); });
+  return guarded(idx, [&] { return idx->ix->inline_unsubscribe(std::string_view(filter, flen), identifier); }, true);
 }
 
 int mq_retain_message(mq_index* idx, const char* topic, uint32_t tlen, uint64_t handle,
@@ -132,17 +156,17 @@ int mq_retain_message(mq_index* idx, const char* topic, uint32_t tlen, uint64_t 
     int64_t r = idx->ix->retain_message(std::string_view(topic, tlen), handle, payload_len, retain != 0);
     if (out) *out = r;
     return 0;
-  });
+  }, true);
 }
 
 int mq_retained_delete(mq_index* idx, const char* topic, uint32_t tlen) {
   if (bad_str(topic, tlen)) return fail(MQ_EINVAL, "null topic");
-  return guarded(idx, [&] { return idx->ix->retained_delete(std::string_view(topic, tlen)); });
+  return guarded(idx, [&] { return idx->ix->retained_delete(std::string_view(topic, tlen)); }, true);
 }
 
 uint64_t mq_retained_len(const mq_index* idx) {
   if (!idx) return 0;
-  std::lock_guard<std::mutex> lk(const_cast<mq_index*>(idx)->mu);
+  std::lock_guard<std::mutex> lk(idx->lk->mu);
   return idx->ix->retained_len();
 }
 
@@ -159,7 +183,7 @@ int mq_subscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs,
       if (out_new) out_new[i] = (uint8_t)r;
     }
     return 0;
-  });
+  }, true);
 }
 
 int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint64_t* handles,
@@ -170,7 +194,7 @@ int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, co
       idx->ix->retain_message(std::string_view((const char*)bytes + offs[i], offs[i + 1] - offs[i]),
                               handles[i], 1, true);
     return 0;
-  });
+  }, true);
 }
 
 int mq_match_batch(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_match_result** out) {
@@ -200,6 +224,89 @@ int mq_match_batch(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
     h.release();
     return 0;
   });
+}
+
+int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_span_result** out) {
+  if (!out || (n && (!to || (!tb && to[n] != 0)))) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    Device& d = idx->device();
+    std::unique_ptr<SpanHolder> h(new SpanHolder());
+    const uint8_t* dtb = nullptr;
+    const uint64_t* dto = nullptr;
+    if (n) d.stage_inputs(tb, to, n, nullptr, &dtb, &dto);
+    mq_span_result dev_out;
+    d.match_spans(*idx->ix, dtb, dto, n, nullptr, &h->data, &dev_out);
+    mq_span_result& r = h->pub;
+    r = dev_out;  // counts and flags; pointers replaced by the host copies and host pools
+    r.topics = reinterpret_cast<const mq_topic_spans*>(h->data.topics.data());
+    r.spans = reinterpret_cast<const mq_span*>(h->data.spans.data());
+    r.patches = reinterpret_cast<const mq_patch*>(h->data.patches.data());
+    r.inline_rows = reinterpret_cast<const mq_inline_row*>(h->data.inl.data());
+    r.picked_rows = reinterpret_cast<const mq_shared_row*>(h->data.picked.data());
+    r.sub_pool = reinterpret_cast<const mq_client_row*>(idx->ix->subs.m.h.data());
+    r.shared_pool = reinterpret_cast<const mq_shared_row*>(idx->ix->shr.m.h.data());
+    r.sub_pool_len = idx->ix->subs.m.size();
+    r.shared_pool_len = idx->ix->shr.m.size();
+    h->lk = idx->lk;
+    idx->lk->views++;  // under the handle lock: the pools stay put until mq_result_free
+    *out = &h->pub;
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    g_results[&h->pub] = 4;
+    h.release();
+    return 0;
+  });
+}
+
+int mq_match_spans_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
+                          mq_span_result* out) {
+  if (!out || (n && !d_to)) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    idx->device().match_spans(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, nullptr, out);
+    return 0;
+  });
+}
+
+int mq_spans_expand(const mq_span_result* r, uint32_t first, uint32_t count, mq_client_row* rows,
+                    uint64_t rows_cap, mq_shared_row* shared, uint64_t shared_cap, uint64_t* n_rows,
+                    uint64_t* n_shared) {
+  if (!r || (uint64_t)first + count > r->n_topics) return fail(MQ_EINVAL, "topic range out of bounds");
+  {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    auto it = g_results.find((void*)r);
+    if (it == g_results.end() || it->second != 4) return fail(MQ_EINVAL, "not a host span result (mq_match_spans)");
+  }
+  const bool picked = (r->flags & MQ_SPANS_PICKED) != 0;
+  uint64_t nr = 0, ns = 0;
+  for (uint32_t t = first; t < first + count; t++) {
+    const mq_topic_spans& ts = r->topics[t];
+    if (nr + ts.n_rows > rows_cap || ns + ts.n_shared > shared_cap) return fail(MQ_ERANGE, "output capacity");
+    if ((ts.n_rows && !rows) || (ts.n_shared && !shared)) return fail(MQ_EINVAL, "null output");
+    mq_client_row* out = rows + nr;
+    uint64_t w = 0;
+    for (uint32_t k = 0; k < ts.n_spans; k++) {
+      const mq_span& sp = r->spans[ts.span_base + k];
+      if (sp.n_sub) memcpy(out + w, r->sub_pool + sp.sub_off, (size_t)sp.n_sub * sizeof(mq_client_row));
+      w += sp.n_sub;
+      if (!picked && sp.n_shr) {
+        memcpy(shared + ns, r->shared_pool + sp.shr_off, (size_t)sp.n_shr * sizeof(mq_shared_row));
+        ns += sp.n_shr;
+      }
+    }
+    if (w != ts.n_rows) return fail(MQ_EIO, "spans disagree with n_rows");
+    for (uint32_t k = 0; k < ts.n_patches; k++) {
+      const mq_patch& p = r->patches[ts.patch_base + k];
+      if (p.row >= ts.n_rows) return fail(MQ_EIO, "patch row out of range");
+      out[p.row].meta = p.meta;
+    }
+    if (picked && ts.n_shared) {
+      memcpy(shared + ns, r->picked_rows + ts.picked_base, (size_t)ts.n_shared * sizeof(mq_shared_row));
+      ns += ts.n_shared;
+    }
+    nr += ts.n_rows;
+  }
+  if (n_rows) *n_rows = nr;
+  if (n_shared) *n_shared = ns;
+  return 0;
 }
 
 int mq_match_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
@@ -314,6 +421,16 @@ void mq_result_free(void* r) {
   if (kind == 1) delete reinterpret_cast<MatchHolder*>(r);
   if (kind == 2) delete reinterpret_cast<MsgHolder*>(r);
   if (kind == 3) delete reinterpret_cast<AclHolder*>(r);
+  if (kind == 4) {
+    SpanHolder* h = reinterpret_cast<SpanHolder*>(r);
+    std::shared_ptr<IndexLock> lk = h->lk;
+    delete h;
+    {
+      std::lock_guard<std::mutex> g(lk->mu);
+      lk->views--;
+    }
+    lk->cv.notify_all();
+  }
 }
 
 int mq_sync(mq_index* idx, void* stream) {
@@ -352,6 +469,15 @@ int mq_index_check(mq_index* idx) {
   return guarded(idx, [&]() -> int {
     std::string why;
     if (!idx->ix->check(&why)) return fail(MQ_EIO, "index check: " + why);
+    return 0;
+  });
+}
+
+int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_PATCH_CAP) return fail(MQ_EINVAL, "unknown option");
+  return guarded(idx, [&] {
+    idx->options.emplace_back(option, value);  // applied when the device is first touched
+    if (idx->dev) idx->dev->set_option(option, value);
     return 0;
   });
 }

@@ -193,33 +193,27 @@ void Profiler::reset() {
 // ---- device --------------------------------------------------------------------------------------
 Device::Device(int dev) : dev_(dev) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
-  const char* ms = getenv("MQ_MERGE_STATS");  // diagnosis only
-  merge_stats_ = ms != nullptr;
-  if (ms && *ms) tstat_path_ = ms;
   int cus = 0;
   hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_), "hipDeviceGetAttribute");
   n_cus_ = (uint32_t)std::max(1, cus);
-  read_knobs();
+  chunk_rows_budget_ = kChunkRows;
+  chunk_tail_ = kChunkTail;
+  chunk_min_ = kChunkMin;
+  copy_blocks_ = n_cus_ * kCopyBlocksPerCU;    // persistent grid of that many workgroups per CU
+  merge_blocks_ = n_cus_ * kMergeBlocksPerCU;  // 0: one wavefront per topic
+  msg_spec_bytes_ = kMsgSpecMB << 20;
 }
 
-// Tuning and diagnosis knobs, re-read per batch (development only; the defaults are the product).
-void Device::read_knobs() {
-  auto knob = [](const char* name, uint32_t def) {
-    const char* v = getenv(name);
-    return v ? (uint32_t)atoi(v) : def;
-  };
-  serial_ = getenv("MQ_SERIAL") != nullptr;                      // k_merge on the launch stream
-  const char* e = getenv("MQ_CHUNK_ROWS");  // output chunk budget (tests use small ones)
-  chunk_rows_budget_ = e ? strtoull(e, nullptr, 10) : kChunkRows;
-  chunk_tail_ = knob("MQ_CHUNK_TAIL", kChunkTail);
-  chunk_min_ = knob("MQ_CHUNK_MIN", kChunkMin);
-  // 0: one wavefront per tile / topic; else a persistent grid of that many workgroups per CU
-  copy_blocks_ = n_cus_ * knob("MQ_COPY_BLOCKS_PER_CU", kCopyBlocksPerCU);
-  merge_blocks_ = n_cus_ * knob("MQ_MERGE_BLOCKS_PER_CU", kMergeBlocksPerCU);
-  merge_diag_ = knob("MQ_MERGE_DIAG", 0);
-  subbatch_topics_ = knob("MQ_SUBBATCH_TOPICS", kSubBatchTopics);  // topics per pipelined sub-batch
-  const char* sb = getenv("MQ_MSG_SPEC_MB");  // Messages speculative-count scratch (0: two walks)
-  msg_spec_bytes_ = (sb ? strtoull(sb, nullptr, 10) : kMsgSpecMB) << 20;
+bool Device::set_option(uint32_t opt, uint64_t v) {
+  switch (opt) {
+    case MQ_OPT_CHUNK_ROWS: chunk_rows_budget_ = v ? std::min<uint64_t>(v, kChunkRows) : kChunkRows; return true;
+    case MQ_OPT_SUBBATCH_TOPICS: subbatch_topics_ = v ? (uint32_t)std::min<uint64_t>(v, 1u << 30) : kSubBatchTopics; return true;
+    case MQ_OPT_MSG_SPEC_MB: msg_spec_bytes_ = v << 20; return true;
+    case MQ_OPT_MSG_WAVES: msg_wpe_opt_ = (uint32_t)v; return true;
+    case MQ_OPT_SERIAL: serial_ = v != 0; return true;
+    case MQ_OPT_PATCH_CAP: patch_cap_init_ = std::max<uint64_t>(v, 64); return true;
+    default: return false;
+  }
 }
 
 Device::~Device() {
@@ -228,7 +222,8 @@ Device::~Device() {
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
   mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
-                    &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &mstats_, &tstat_, &acl_buf_})
+                    &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &acl_buf_, &sp_res_,
+                    &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
@@ -258,7 +253,7 @@ uint64_t Device::device_bytes() const {
                mref_.cap * sizeof(MergeRef) + mpart_.cap * sizeof(MergePart) +
                npair_.cap * sizeof(NodePair) + pent_.cap * sizeof(PairEnt) + plist_.cap * sizeof(PairSlot);
   for (const DevBuf* x : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &desc_[0], &desc_[1],
-                          &tiles_[0], &tiles_[1]})
+                          &tiles_[0], &tiles_[1], &sp_res_, &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_})
     b += x->bytes;
   for (int k = 0; k < 2; k++)
     for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b += x->bytes;
@@ -326,7 +321,8 @@ void Device::check_err(hipStream_t s) {
     throw HipError{hipErrorUnknown, std::string("device guard tripped: ") +
                                         ((e & kErrWalkGuard) ? "walk iteration bound " : "") +
                                         ((e & kErrTableFull) ? "merge table full " : "") +
-                                        ((e & kErrPickGuard) ? "shared pick partitions" : "")};
+                                        ((e & kErrPickGuard) ? "shared pick partitions " : "") +
+                                        ((e & kErrDeepRank) ? "cross-shard merge deeper than 32 levels" : "")};
   }
 }
 
@@ -335,6 +331,9 @@ void Device::select_shared(const mq_match_result& r, hipStream_t s, ShrRec* d_se
   PickArgs pa;
   pa.res = reinterpret_cast<const mq_topic_result_dev*>(r.topics);
   pa.rows = reinterpret_cast<const ShrRec*>(r.shared_rows);
+  pa.sres = nullptr;
+  pa.spans = nullptr;
+  pa.pool = nullptr;
   pa.sel = d_sel;
   pa.n_out = d_n;
   pa.n_out_stride = 1;
@@ -395,7 +394,6 @@ void Device::pinned(size_t bytes) {
 void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                    HostMatch* host, mq_match_result* out, mq_chunk_fn fn, void* user) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
-  read_knobs();
   sync(ix, s);
   memset(out, 0, sizeof(*out));
   last_chunks_ = 0;
@@ -594,8 +592,10 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     da.chunk_of_block = dc;
     da.desc = desc_[p].as<GDesc>();
     da.tiles = tiles_[p].as<uint32_t>();
+    da.spans = nullptr;
+    da.inl_out = nullptr;
     prof.begin(s);
-    launch_desc(da, s);
+    launch_desc(da, false, s);
     prof.end("desc", s);
     hip_check(hipGetLastError(), "k_desc");
 
@@ -623,20 +623,10 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       a.shr_rows = shr_rows_[b].as<ShrRec>();
       a.inl_rows = inl_rows_[b].as<InlRec>();
       a.res = res_[b].as<mq_topic_result_dev>();
-      a.stats = nullptr;
-      a.tstat = nullptr;
-      a.diag = merge_diag_;
-      if (!tstat_path_.empty()) {
-        if (ci == 0) grow(tstat_, (size_t)n * kTStat * sizeof(uint32_t));
-        a.tstat = tstat_.as<uint32_t>() + (size_t)q.t0 * kTStat;
-      }
-      if (merge_stats_) {
-        if (!mstats_.p) {
-          mstats_.ensure(4 * sizeof(unsigned long long));
-          hip_check(hipMemsetAsync(mstats_.p, 0, 4 * sizeof(unsigned long long), s), "memset stats");
-        }
-        a.stats = mstats_.as<unsigned long long>();
-      }
+      a.sres = nullptr;
+      a.patches = nullptr;
+      a.pcount = nullptr;
+      a.pcap = 0;
       if (ci >= 2) hip_check(hipStreamWaitEvent(s, merge_done_[b], 0), "hipStreamWaitEvent");
       prof.begin(s);
       launch_copy(a, copy_blocks_, s);
@@ -647,7 +637,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
       }
       prof.begin(ms);
-      launch_merge(a, merge_blocks_, ms);
+      launch_merge(a, false, merge_blocks_, ms);
       prof.end("merge", ms);
       hip_check(hipGetLastError(), "k_merge");
       const uint32_t nt = a.t1 - a.t0;
@@ -657,6 +647,9 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         PickArgs pa;
         pa.res = a.res;
         pa.rows = a.shr_rows;
+        pa.sres = nullptr;
+        pa.spans = nullptr;
+        pa.pool = nullptr;
         pa.sel = sel_rows_[b].as<ShrRec>();
         pa.n_out = &a.res[0].n_shared;
         pa.n_out_stride = sizeof(mq_topic_result_dev) / sizeof(uint32_t);
@@ -696,12 +689,6 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       cr.n_inline_rows = hi.inl - lo.inl;
       if (fn) fn(user, &cr, q.t0 + a.t0, ms);  // the consumer's work precedes the buffer's reuse
       hip_check(hipEventRecord(merge_done_[b], ms), "hipEventRecord");
-      if (merge_stats_) {  // diagnosis only: cumulative since the Device was created
-        unsigned long long m[4];
-        hip_check(hipMemcpyAsync(m, a.stats, sizeof(m), hipMemcpyDeviceToHost, ms), "D2H stats");
-        hip_check(hipStreamSynchronize(ms), "hipStreamSynchronize");
-        fprintf(stderr, "[merge] hit lists %llu records resolved %llu slow-path topics %llu\n", m[0], m[1], m[2]);
-      }
       *out = cr;
       done.push_back(c);
     }
@@ -710,15 +697,6 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   // the launch stream completes only after the side stream's work of this batch
   hip_check(hipEventRecord(side_done_, side_), "hipEventRecord");
   hip_check(hipStreamWaitEvent(s, side_done_, 0), "hipStreamWaitEvent");
-  if (!tstat_path_.empty()) {  // diagnosis only: per-topic k_merge counters of this batch
-    std::vector<uint32_t> h((size_t)n * kTStat);
-    hip_check(hipMemcpyAsync(h.data(), tstat_.p, h.size() * 4, hipMemcpyDeviceToHost, s), "D2H tstat");
-    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    if (FILE* f = fopen(tstat_path_.c_str(), "wb")) {
-      fwrite(h.data(), 4, h.size(), f);
-      fclose(f);
-    }
-  }
   if (host) {
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     for (const Chunk& c : done) {
@@ -735,6 +713,186 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     }
     check_err(s);
   }
+}
+
+TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+                           const uint32_t** gathers, uint32_t* gstride) {
+  const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+  grow(counts_, (size_t)n * sizeof(TopicCount));
+  grow(offs_, (size_t)(n + 1) * sizeof(TopicOff));
+  grow(bsum_, (size_t)(nb + 1) * sizeof(TopicOff));
+  grow(bpre_, (size_t)(nb + 1) * sizeof(TopicOff));
+  grow(gslots_, (size_t)n * kGatherCap * sizeof(uint32_t));
+  grow(ovf_, sizeof(uint32_t));
+  pinned(sizeof(TopicOff) + sizeof(uint32_t));
+  TopicOff* h_tot = static_cast<TopicOff*>(h_pin_);
+  uint32_t* h_ovf = reinterpret_cast<uint32_t*>(h_tot + 1);
+  hip_check(hipMemsetAsync(ovf_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
+  prof.begin(s);
+  launch_walk(false, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(), ovf_.as<uint32_t>(), s);
+  prof.end("walk", s);
+  hip_check(hipGetLastError(), "k_walk<count>");
+  prof.begin(s);
+  launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
+  prof.end("scan", s);
+  hip_check(hipGetLastError(), "k_scan");
+  hip_check(hipMemcpyAsync(h_tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H totals");
+  hip_check(hipMemcpyAsync(h_ovf, ovf_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H overflow");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  const TopicOff tot = *h_tot;
+  *gathers = gslots_.as<uint32_t>();
+  *gstride = kGatherCap;
+  if (*h_ovf) {  // a topic with more gathers than its count-pass slots: write all lists compactly
+    grow(gathers_, std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
+    prof.begin(s);
+    launch_walk(true, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), nullptr, s);
+    prof.end("walk_fill", s);
+    hip_check(hipGetLastError(), "k_walk<fill>");
+    *gathers = gathers_.as<uint32_t>();
+    *gstride = 0;
+  }
+  prof.count("topics", n);
+  prof.count("gathers", tot.g);
+  prof.count("reserved_rows", tot.rows);
+  return tot;
+}
+
+// Span format: walk + scan, then k_desc writes each topic's spans (and copies its inline rows)
+// and k_merge resolves the co-matching records into patches; nothing is copied per row. The
+// patch pool grows when a batch reserves more than it holds (the batch's k_merge then runs
+// again); the call ends with the stream synchronised and the guard flags checked.
+void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+                         HostSpans* host, mq_span_result* out) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  sync(ix, s);
+  memset(out, 0, sizeof(*out));
+  if (host) *host = HostSpans{};
+  if (!err_.p) {
+    err_.ensure(2 * sizeof(uint32_t));
+    hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
+  }
+  check_err(s);  // faults flagged by an earlier row-format batch
+  const DevIndex di = dev_index(ix);
+  out->sub_pool = reinterpret_cast<const mq_client_row*>(di.subs);
+  out->shared_pool = reinterpret_cast<const mq_shared_row*>(di.shr);
+  out->sub_pool_len = ix.subs.m.size();
+  out->shared_pool_len = ix.shr.m.size();
+  out->flags = select_shared_ ? MQ_SPANS_PICKED : 0u;
+  if (n == 0) return;
+  ensure_streams();
+
+  const uint32_t* gathers = nullptr;
+  uint32_t gstride = 0;
+  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride);
+  grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
+  grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
+  grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
+  grow(sp_res_, (size_t)n * sizeof(TopicSpansDev));
+  if (select_shared_) grow(sp_picked_, std::max<uint64_t>(tot.shr, 1) * sizeof(ShrRec));
+  if (!sp_pcount_.p) sp_pcount_.ensure(sizeof(unsigned long long));
+  if (patch_cap_ < patch_cap_init_) {
+    grow(sp_patches_, patch_cap_init_ * sizeof(PatchRec));
+    patch_cap_ = patch_cap_init_;
+  }
+
+  DescArgs da;
+  da.ix = di;
+  da.n = n;
+  da.gather_stride = gstride;
+  da.off = offs_.as<TopicOff>();
+  da.gathers = gathers;
+  da.chunk_of_block = nullptr;
+  da.plan = nullptr;
+  da.desc = desc_[0].as<GDesc>();
+  da.tiles = nullptr;
+  da.spans = sp_spans_.as<SpanRec>();
+  da.inl_out = sp_inl_.as<InlRec>();
+  prof.begin(s);
+  launch_desc(da, true, s);
+  prof.end("desc", s);
+  hip_check(hipGetLastError(), "k_desc<spans>");
+
+  EmitArgs a;
+  memset(&a, 0, sizeof(a));
+  a.ix = di;
+  a.t0 = 0;
+  a.t1 = n;
+  a.off = offs_.as<TopicOff>();
+  a.base = TopicOff{0, 0, 0, 0, 0};
+  a.desc = desc_[0].as<GDesc>();
+  a.inl_rows = sp_inl_.as<InlRec>();
+  a.sres = sp_res_.as<TopicSpansDev>();
+  a.pcount = sp_pcount_.as<unsigned long long>();
+  pinned(sizeof(unsigned long long) + 2 * sizeof(uint32_t));
+  unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);
+  uint32_t* h_err = reinterpret_cast<uint32_t*>(h_pc + 1);
+  for (int attempt = 0;; attempt++) {
+    a.patches = sp_patches_.as<PatchRec>();
+    a.pcap = patch_cap_;
+    hip_check(hipMemsetAsync(a.pcount, 0, sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
+    prof.begin(s);
+    launch_merge(a, true, merge_blocks_, s);
+    prof.end("merge", s);
+    hip_check(hipGetLastError(), "k_merge<spans>");
+    hip_check(hipMemcpyAsync(h_pc, a.pcount, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H pcount");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (*h_pc <= patch_cap_) break;
+    if (attempt) throw HipError{hipErrorUnknown, "k_merge<spans>: patch reservations changed between runs"};
+    const uint64_t want = *h_pc + *h_pc / 4 + 1024;  // every patch range of this batch, with slack
+    sp_patches_.release();
+    sp_patches_.ensure(want * sizeof(PatchRec));
+    patch_cap_ = want;
+  }
+  const uint64_t n_patches = *h_pc;
+  if (select_shared_) {  // SelectShared on the device: picked members at each topic's picked_base
+    PickArgs pa;
+    pa.res = nullptr;
+    pa.rows = nullptr;
+    pa.sres = a.sres;
+    pa.spans = sp_spans_.as<SpanRec>();
+    pa.pool = di.shr;
+    pa.sel = sp_picked_.as<ShrRec>();
+    pa.n_out = &a.sres[0].n_shared;
+    pa.n_out_stride = sizeof(TopicSpansDev) / sizeof(uint32_t);
+    pa.n = n;
+    pa.err = err_.as<uint32_t>();
+    prof.begin(s);
+    launch_pick(pa, s);
+    prof.end("pick", s);
+    hip_check(hipGetLastError(), "k_pick<spans>");
+  }
+  prof.count("patches", n_patches);
+  out->n_topics = n;
+  out->topics = reinterpret_cast<const mq_topic_spans*>(a.sres);
+  out->spans = reinterpret_cast<const mq_span*>(sp_spans_.p);
+  out->patches = reinterpret_cast<const mq_patch*>(sp_patches_.p);
+  out->inline_rows = reinterpret_cast<const mq_inline_row*>(sp_inl_.p);
+  out->picked_rows = select_shared_ ? reinterpret_cast<const mq_shared_row*>(sp_picked_.p) : nullptr;
+  out->n_spans = tot.g;
+  out->n_patches = n_patches;
+  out->n_inline_rows = tot.inl;
+  out->n_picked_rows = select_shared_ ? tot.shr : 0;
+  if (host) {
+    host->topics.resize(n);
+    host->spans.resize(tot.g);
+    host->patches.resize(n_patches);
+    host->inl.resize(tot.inl);
+    host->picked.resize(out->n_picked_rows);
+    hip_check(hipMemcpyAsync(host->topics.data(), a.sres, n * sizeof(TopicSpansDev), hipMemcpyDeviceToHost, s), "D2H");
+    if (tot.g)
+      hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, s), "D2H");
+    if (n_patches)
+      hip_check(hipMemcpyAsync(host->patches.data(), sp_patches_.p, n_patches * sizeof(PatchRec),
+                               hipMemcpyDeviceToHost, s), "D2H");
+    if (tot.inl)
+      hip_check(hipMemcpyAsync(host->inl.data(), sp_inl_.p, tot.inl * sizeof(InlRec), hipMemcpyDeviceToHost, s), "D2H");
+    if (out->n_picked_rows)
+      hip_check(hipMemcpyAsync(host->picked.data(), sp_picked_.p, out->n_picked_rows * sizeof(ShrRec),
+                               hipMemcpyDeviceToHost, s), "D2H");
+  }
+  hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (*h_err) check_err(s);  // throws with the tripped guard's name
 }
 
 void Device::acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb, const uint64_t* to,
@@ -824,8 +982,7 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   // k_msg register budget: on a large retained index the walk waits on HBM far more often, and
   // 6 waves per SIMD (with spills) beat 4 (10M retained: 54.8 -> 50.2 ms per 100k filters); on
   // a small, cache-resident one the spills cost more (1M: 8.7 vs 9.2 ms). MQ_MSG_WPE overrides.
-  msg_wpe_ = ix.retained_len() >= kMsgWpeMinRetained ? kMsgWavesPerEU : 1u;
-  if (const char* w = getenv("MQ_MSG_WPE")) msg_wpe_ = (uint32_t)atoi(w);  // read per batch (tuning)
+  const uint32_t msg_wpe = msg_wpe_opt_ ? msg_wpe_opt_ : (ix.retained_len() >= kMsgWpeMinRetained ? kMsgWavesPerEU : 1u);
   // Speculative count: the count pass also writes each filter's first `cap` handles to scratch,
   // so that only filters with more (or counted through below_live) are walked a second time.
   uint32_t cap = (uint32_t)std::min<uint64_t>(kMsgSpecCap, msg_spec_bytes_ / ((uint64_t)n * sizeof(uint64_t)));
@@ -837,7 +994,7 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   }
   prof.begin(s);
   launch_msg(false, d_fb, d_fo, n, di, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, spec, cap,
-             msg_wpe_, s);
+             msg_wpe, s);
   prof.end("msg_count", s);
   hip_check(hipGetLastError(), "k_msg<count>");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
@@ -858,7 +1015,7 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   }
   prof.begin(s);
   launch_msg(true, d_fb, d_fo, n, di, counts_.as<TopicCount>(), offs_.as<TopicOff>(), msg_handles_.as<uint64_t>(),
-             msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), spec, cap, msg_wpe_, s);
+             msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), spec, cap, msg_wpe, s);
   prof.end("msg_fill", s);
   hip_check(hipGetLastError(), "k_msg<fill>");
   out->n_filters = n;

@@ -81,6 +81,15 @@ struct HostAcl {
   PinnedVec<uint32_t> elems;
 };
 
+// Host-side destination of a span-format batch (mq_match_spans).
+struct HostSpans {
+  PinnedVec<TopicSpansDev> topics;
+  PinnedVec<SpanRec> spans;
+  PinnedVec<PatchRec> patches;
+  PinnedVec<InlRec> inl;
+  PinnedVec<ShrRec> picked;
+};
+
 // Host-side destination of a batch's results (mq_match_batch).
 struct HostMatch {
   PinnedVec<mq_topic_result> topics;
@@ -132,6 +141,11 @@ class Device {
   // buffers are released for reuse.
   void match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
              HostMatch* host, mq_match_result* out, mq_chunk_fn fn = nullptr, void* user = nullptr);
+  // Span format (mq_match_spans*): spans + patches + inline rows of n topics on the device; the
+  // call returns after the kernels completed and their guard flags were checked. `host`: also
+  // copies every array into it (out's pointers then still name the device arrays).
+  void match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+                   HostSpans* host, mq_span_result* out);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
                 HostMsg* host, mq_msg_result* out);
@@ -147,6 +161,9 @@ class Device {
   void select_shared(const mq_match_result& r, hipStream_t s, ShrRec* d_sel, uint32_t* d_n);
   // MQ_CFG_SELECT_SHARED: match results carry only the picked member of each shared filter.
   void set_select_shared(bool on) { select_shared_ = on; }
+  bool select_shared() const { return select_shared_; }
+  // mq_set_option (MQ_OPT_*); false for an unknown option.
+  bool set_option(uint32_t opt, uint64_t value);
 
   uint32_t last_chunks() const { return last_chunks_; }
   uint64_t device_bytes() const;
@@ -156,8 +173,10 @@ class Device {
 
  private:
   DevIndex dev_index(const Index& ix) const;
-  void read_knobs();
   void check_err(hipStream_t s);
+  // walk (count) + scan of n topics; returns the batch totals (synchronises s)
+  TopicOff walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+                     const uint32_t** gathers, uint32_t* gstride);
 
   int dev_;
   uint64_t synced_version_ = ~0ull;
@@ -206,16 +225,17 @@ class Device {
   DevBuf err_;
   hipStream_t side_ = nullptr;
   hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
-  DevBuf msg_handles_, msg_base_, msg_count_, gslots_, mstats_;
+  DevBuf msg_handles_, msg_base_, msg_count_, gslots_;
+  // span format outputs
+  DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;
+  uint64_t patch_cap_ = 0;           // patches sp_patches_ holds
+  uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter
   uint64_t msg_spec_bytes_ = 0;  // its budget (MQ_MSG_SPEC_MB)
-  uint32_t msg_wpe_ = 1;         // k_msg variant (MQ_MSG_WPE)
-  bool merge_stats_ = false;  // MQ_MERGE_STATS: k_merge work counters to stderr
-  std::string tstat_path_;    // MQ_MERGE_STATS=<path>: per-topic k_merge counters (kTStat u32 each)
+  uint32_t msg_wpe_opt_ = 0;     // k_msg variant (MQ_OPT_MSG_WAVES; 0: by index size)
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
-  uint32_t n_cus_ = 1, merge_diag_ = 0;
-  bool serial_ = false;       // MQ_SERIAL: k_merge on the launch stream (isolated kernel times)
-  DevBuf tstat_;
+  uint32_t n_cus_ = 1;
+  bool serial_ = false;       // MQ_OPT_SERIAL: k_merge on the launch stream (isolated kernel times)
   DevBuf acl_buf_;  // k_acl inputs and outputs
   std::vector<TopicOff> h_bpre_;
   uint64_t retained_len_ = 0;

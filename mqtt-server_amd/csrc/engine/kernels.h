@@ -54,6 +54,7 @@ struct DevIndex {
 constexpr uint32_t kErrWalkGuard = 1u;
 constexpr uint32_t kErrTableFull = 2u;
 constexpr uint32_t kErrPickGuard = 4u;  // k_pick: hash partitions exhausted
+constexpr uint32_t kErrDeepRank = 8u;   // sharded merge: two ranks tie beyond the rank key's 32 levels
 constexpr uint64_t kWalkGuard = 1ull << 26;
 
 // Exclusive offsets of a topic's outputs (scan of TopicCount).
@@ -84,7 +85,22 @@ struct GDesc {  // 32 B
 };
 constexpr uint32_t kDescMerge = 1u << 31;
 
-// Per-chunk arguments of k_desc / k_copy / k_merge.
+// Span-format records (include/mqmatch.h mq_span / mq_patch / mq_topic_spans).
+struct SpanRec {  // one gathered particle: subs[sub_off, + n_sub), shr[shr_off, + n_shr)
+  uint32_t sub_off, n_sub, shr_off, n_shr;
+};
+struct PatchRec {  // topic-relative record row -> replacement meta (merge base / ident / drop)
+  uint32_t row, meta;
+};
+struct TopicSpansDev {  // == mq_topic_spans
+  uint64_t span_base, patch_base, inline_base, picked_base;
+  uint32_t n_spans, n_patches, n_inline, n_rows;
+  uint32_t n_client, n_ident, n_shared, reserved;
+};
+static_assert(sizeof(TopicSpansDev) == 64, "mq_topic_spans layout");
+
+// Per-chunk arguments of k_desc / k_copy / k_merge. In the span format (k_merge<true>) the
+// whole batch is one chunk, GDesc row positions are topic-relative and k_merge emits patches.
 struct EmitArgs {
   DevIndex ix;
   uint32_t t0, t1;          // topic range of this chunk
@@ -97,12 +113,13 @@ struct EmitArgs {
   SubRec* rows;
   ShrRec* shr_rows;
   InlRec* inl_rows;
-  mq_topic_result_dev* res; // indexed t - t0
-  unsigned long long* stats;  // k_merge: [0] hit lists, [1] records resolved, [2] slow-path topics
-  uint32_t diag;              // diagnosis knobs (MQ_MERGE_DIAG): 1 = no row writes, 2 = no flush
-  uint32_t* tstat;            // diagnosis (MQ_MERGE_STATS=path): kTStat words per topic, index t
+  mq_topic_result_dev* res; // indexed t - t0 (row format)
+  // span format
+  TopicSpansDev* sres;            // indexed t
+  PatchRec* patches;              // patch pool; topics reserve ranges with atomicAdd on *pcount
+  unsigned long long* pcount;     // patches reserved (may exceed pcap: the host then grows the pool)
+  uint64_t pcap;
 };
-constexpr uint32_t kTStat = 8;
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile
 // table sits in the batch's tile array.
@@ -123,6 +140,9 @@ struct DescArgs {
   const ChunkPlan* plan;
   GDesc* desc;
   uint32_t* tiles;
+  // span format: one SpanRec per gather, inline rows copied to inl_out at off[t].inl
+  SpanRec* spans;
+  InlRec* inl_out;
 };
 
 // Batched auth.MatchTopic (k_acl).
@@ -143,23 +163,26 @@ void launch_acl(const AclArgs& a, hipStream_t s);
 
 // SelectShared on the device (k_pick): per topic, one member of every shared filter.
 struct PickArgs {
-  const mq_topic_result_dev* res;  // n topic results (shared_base / n_shared read)
+  const mq_topic_result_dev* res;  // row format: n topic results (shared_base / n_shared read)
   const ShrRec* rows;              // the chunk's shared rows
+  const TopicSpansDev* sres;       // span format: topics (span_base / n_spans / picked_base)
+  const SpanRec* spans;            //   their spans, whose shared ranges index
+  const ShrRec* pool;              //   the shared pool
   ShrRec* sel;                     // picked rows of topic t at [shared_base, + picked)
   uint32_t* n_out;                 // picked count of topic t at n_out[t * n_out_stride]
   uint32_t n_out_stride;
   uint32_t n;
   uint32_t* err;                   // kErrPickGuard
 };
-void launch_pick(const PickArgs& a, hipStream_t s);
+void launch_pick(const PickArgs& a, hipStream_t s);  // a.sres != null: span format
 
 void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
                  TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
-void launch_desc(const DescArgs& a, hipStream_t s);
+void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
-void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
+void launch_merge(const EmitArgs& a, bool spans, uint32_t max_blocks, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
 // first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
 // fill pass must still walk; the fill pass then walks only those.

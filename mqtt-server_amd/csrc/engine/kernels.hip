@@ -397,17 +397,24 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// SPANS=false (row format): positions are relative to the topic's output chunk and the k_copy
+// tiles starting in each gather are marked. SPANS=true: positions are topic-relative (k_merge
+// patches name a topic's rows), every gather also becomes a SpanRec at its gather index, and
+// the gathered inline rows are copied to off[t].inl for k_merge's last-write pass.
+template <bool SPANS>
 __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= a.n) return;
-  const ChunkPlan cp = a.plan[a.chunk_of_block[t / kScanBlock]];
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
-  uint32_t rpos = (uint32_t)(o0.rows - cp.rows);
-  uint32_t spos = (uint32_t)(o0.shr - cp.shr), ipos = (uint32_t)(o0.inl - cp.inl);
+  ChunkPlan cp{0, 0, 0, 0, 0, 0, 0};
+  if (!SPANS) cp = a.plan[a.chunk_of_block[t / kScanBlock]];
+  uint32_t rpos = SPANS ? 0u : (uint32_t)(o0.rows - cp.rows);
+  uint32_t spos = (uint32_t)(o0.shr - cp.shr);
+  uint64_t ipos = o0.inl - cp.inl;
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
-  uint32_t* tile_r = a.tiles + cp.tile_off;
-  uint32_t* tile_s = tile_r + cp.n_tiles0;
-  uint32_t* tile_i = tile_s + cp.n_tiles1;
+  uint32_t* tile_r = SPANS ? nullptr : a.tiles + cp.tile_off;
+  uint32_t* tile_s = SPANS ? nullptr : tile_r + cp.n_tiles0;
+  uint32_t* tile_i = SPANS ? nullptr : tile_s + cp.n_tiles1;
   const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
   for (uint32_t i = 0; i < n_g; i++) {
     const uint32_t gw = gw_src[i];
@@ -420,15 +427,20 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     d.r_src = L.sub_off;
     d.s_pos = spos;
     d.s_src = L.shr_off;
-    d.i_pos = ipos;
+    d.i_pos = (uint32_t)ipos;
     d.i_src = L.inl_off;
     d.word = gw;
     d.mdir = L.n_direct | ((gw & kGatherSubs) && L.n_merge ? kDescMerge : 0u);
     a.desc[g] = d;
-    // the k_copy tiles whose first row falls inside this gather start their cursor here
-    for (uint32_t k = (rpos + kCopyTile - 1) / kCopyTile; k * kCopyTile < rpos + rn; k++) tile_r[k] = (uint32_t)g;
-    for (uint32_t k = (spos + kCopyTile - 1) / kCopyTile; k * kCopyTile < spos + L.shr_cnt; k++) tile_s[k] = (uint32_t)g;
-    for (uint32_t k = (ipos + kCopyTile - 1) / kCopyTile; k * kCopyTile < ipos + in; k++) tile_i[k] = (uint32_t)g;
+    if (SPANS) {
+      a.spans[g] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
+      for (uint32_t k = 0; k < in; k++) a.inl_out[ipos + k] = a.ix.inl[L.inl_off + k];
+    } else {
+      // the k_copy tiles whose first row falls inside this gather start their cursor here
+      for (uint32_t k = (rpos + kCopyTile - 1) / kCopyTile; k * kCopyTile < rpos + rn; k++) tile_r[k] = (uint32_t)g;
+      for (uint32_t k = (spos + kCopyTile - 1) / kCopyTile; k * kCopyTile < spos + L.shr_cnt; k++) tile_s[k] = (uint32_t)g;
+      for (uint64_t k = (ipos + kCopyTile - 1) / kCopyTile; k * kCopyTile < ipos + in; k++) tile_i[k] = (uint32_t)g;
+    }
     rpos += rn;
     spos += L.shr_cnt;
     ipos += in;
@@ -555,6 +567,14 @@ __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
   }
 }
 
+// SPANS=false: the records were copied to the chunk's rows by k_copy and are rewritten in
+// place. SPANS=true: nothing was copied; each record whose row changes leaves a PatchRec (its
+// topic-relative row, the new meta) in a range the topic reserves with one atomicAdd on
+// a.pcount, sized by the records its hit lists hold (the reservation is made before any record
+// is resolved: when the hit lists do not fit in LDS the pair analysis runs twice, counting,
+// then resolving). A reservation past a.pcap writes nothing; the host reads *pcount, grows the
+// pool and runs the batch's k_merge again.
+template <bool SPANS>
 __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
   __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records
   __shared__ uint32_t map_val[4][kMapSlots];   // its gather index (= DFS rank order)
@@ -577,11 +597,25 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
   const uint64_t ib = o0.inl - a.base.inl;
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
   const GDesc* __restrict__ gd = a.desc + o0.g;
-  SubRec* __restrict__ crow = a.rows;  // chunk-relative rows (GDesc positions)
+  SubRec* __restrict__ crow = a.rows;  // chunk-relative rows (GDesc positions), row format
   uint32_t n_nonbase = 0, n_ext = 0;
-  uint32_t st_hits = 0, st_recs = 0, st_slow = 0, st_map = 0;
-  const uint64_t c_start = a.tstat ? clock64() : 0;
-  uint64_t c_map = c_start, c_pair = c_start, c_flush = 0;
+  uint64_t pbase = 0;    // span format: the topic's patch range [pbase, pbase + reserved)
+  uint32_t n_patch = 0;
+  bool pfit = true;      // the reservation fits the pool
+
+  // reserve n patch slots for this topic (wave-uniform)
+  auto reserve = [&](uint64_t n) {
+    unsigned long long b = 0;
+    if (lane == 0 && n) b = atomicAdd(a.pcount, (unsigned long long)n);
+    pbase = __shfl((unsigned long long)b, 0, 64);
+    pfit = pbase + n <= a.pcap;
+  };
+  // one patch per lane that wants one, compacted by ballot (wave-uniform)
+  auto emit_patch = [&](bool want, uint32_t row, uint32_t meta) {
+    const uint64_t m = __ballot(want);
+    if (want && pfit) a.patches[pbase + n_patch + prefix_before(m)] = PatchRec{row, meta};
+    n_patch += (uint32_t)__popcll(m);
+  };
 
   if (o1.merge > o0.merge) {  // the topic gathers may-merge records
     // Map every gathered node that holds may-merge records (and whose subscriptions are
@@ -620,8 +654,6 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
       n_map += __popcll(bi);
     }
     wave_sync_lds();
-    st_map = n_map;
-    if (a.tstat) c_map = clock64();
     const bool slow = n_map > kPairMax;  // beyond the map: look partners up linearly
     auto gathered = [&](uint32_t h) -> uint32_t {  // gather index of node h, or kNone
       if (!slow) {
@@ -645,11 +677,13 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
     // an Identifiers row when its identifier is > 0 (Subscription.Merge,
     // packets/packets.go:261-263), else dropped. Otherwise it is the base and takes the
     // partners' max Qos and OR'd NoLocal (packets/packets.go:265-271). A record may be reached
-    // through several hit lists; every visit writes the same row, and only the visit through
-    // its first gathered partner (`via`, or any when via == kNone) counts it.
+    // through several hit lists; only the visit through its first gathered partner (`via`, or
+    // any when via == kNone) counts it, and only that visit leaves a patch (the row format
+    // writes the same row on every visit). Called by all lanes (wave-uniform).
     auto resolve = [&](bool active, uint32_t pos, uint32_t row, uint32_t gi, uint32_t via,
                        uint32_t mp_off, uint32_t mp_cnt) {
-      bool counted = false, nonbase = false;
+      bool counted = false, nonbase = false, want = false;
+      uint32_t pmeta = 0;
       int32_t ident = 0;
       if (active) {
         const SubRec rec = a.ix.subs[pos];
@@ -681,15 +715,16 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
           counted = via == kNone || via == first;
           nonbase = !base;
           ident = rec.ident;
-          if (a.diag & 1) {
-          } else if (base) {
-            const uint32_t m = (rec.meta & ~(kMetaQos | kMetaNoLocal)) | q | nl;
-            if (m != rec.meta) crow[row].meta = m;
-          } else {
-            crow[row].meta = rec.meta | (rec.ident > 0 ? kRowIdent : kRowDrop);
+          pmeta = base ? (rec.meta & ~(kMetaQos | kMetaNoLocal)) | q | nl
+                       : rec.meta | (rec.ident > 0 ? kRowIdent : kRowDrop);
+          if (SPANS) {
+            want = counted && pmeta != rec.meta;
+          } else if (pmeta != rec.meta) {
+            crow[row].meta = pmeta;
           }
         }
       }
+      if (SPANS) emit_patch(want, row, pmeta);
       const uint64_t bn = __ballot(counted && nonbase);
       const uint64_t bx = __ballot(counted && nonbase && ident > 0);
       n_nonbase += __popcll(bn);
@@ -702,10 +737,8 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
       // is resolved 64 records per wave-instruction.
       uint32_t n_hit = 0, tot = 0;
       auto flush_hits = [&]() {
-        const uint64_t cf0 = a.tstat ? clock64() : 0;
         if (lane == 0) h_pre[wv][n_hit] = tot;
         wave_sync_lds();
-        if (a.diag & 2) tot = 0;
         for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
           const uint32_t r = r0 + lane;
           const uint32_t rc = min(r, tot - 1);
@@ -720,69 +753,96 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
           resolve(r < tot, mg_moff[wv][xa] + e.k, mg_row[wv][xa] + e.k, mg_gi[wv][xa], h_via[wv][jj],
                   e.mp_off, e.mp_cnt);
         }
-        st_recs += tot;
         n_hit = 0;
         tot = 0;
         wave_sync_lds();
-        if (a.tstat) c_flush += clock64() - cf0;
       };
-      const uint32_t np = n_map * n_map;
-      for (uint32_t p0 = 0; p0 < np; p0 += 64) {
-        const uint32_t p = p0 + lane;
-        bool hit = false;
-        uint32_t ga = 0, e_off = 0, e_cnt = 0, hn = 0;
-        if (p < np) {
-          ga = p / n_map;
-          const uint32_t hb = p - ga * n_map;
-          if (ga != hb) {
-            const uint32_t ent_mask = mg_emask[wv][ga], ent_off = mg_eoff[wv][ga];
-            if (ent_mask != kNone) {
-              hn = mg_node[wv][hb];
-              // linear probing, four slots per round: one load latency covers most probes
-              uint32_t sl = pair_hash(hn) & ent_mask;
-              for (uint32_t probes = 0; probes <= ent_mask; probes += 4) {
-                PairEnt pe[4];
+      // counting = true: stage hit lists while they fit and add up every list's length
+      // (tot_all); stop staging at the first batch that does not fit (staged_all = false).
+      // counting = false: stage and resolve (flush) as the lists come.
+      uint64_t tot_all = 0;
+      bool staged_all = true;
+      auto pairs = [&](bool counting) {
+        const uint32_t np = n_map * n_map;
+        for (uint32_t p0 = 0; p0 < np; p0 += 64) {
+          const uint32_t p = p0 + lane;
+          bool hit = false;
+          uint32_t ga = 0, e_off = 0, e_cnt = 0, hn = 0;
+          if (p < np) {
+            ga = p / n_map;
+            const uint32_t hb = p - ga * n_map;
+            if (ga != hb) {
+              const uint32_t ent_mask = mg_emask[wv][ga], ent_off = mg_eoff[wv][ga];
+              if (ent_mask != kNone) {
+                hn = mg_node[wv][hb];
+                // linear probing, four slots per round: one load latency covers most probes
+                uint32_t sl = pair_hash(hn) & ent_mask;
+                for (uint32_t probes = 0; probes <= ent_mask; probes += 4) {
+                  PairEnt pe[4];
 #pragma unroll
-                for (uint32_t u = 0; u < 4; u++) pe[u] = a.ix.pent[ent_off + ((sl + u) & ent_mask)];
-                bool stop = false;
+                  for (uint32_t u = 0; u < 4; u++) pe[u] = a.ix.pent[ent_off + ((sl + u) & ent_mask)];
+                  bool stop = false;
 #pragma unroll
-                for (uint32_t u = 0; u < 4; u++) {
-                  if (stop) continue;
-                  if (pe[u].h == hn) {
-                    hit = true;
-                    e_off = pe[u].off;
-                    e_cnt = pe[u].cnt;
-                    stop = true;
-                  } else if (pe[u].h == kNone) {
-                    stop = true;
+                  for (uint32_t u = 0; u < 4; u++) {
+                    if (stop) continue;
+                    if (pe[u].h == hn) {
+                      hit = true;
+                      e_off = pe[u].off;
+                      e_cnt = pe[u].cnt;
+                      stop = true;
+                    } else if (pe[u].h == kNone) {
+                      stop = true;
+                    }
                   }
+                  if (stop) break;
+                  sl = (sl + 4) & ent_mask;
                 }
-                if (stop) break;
-                sl = (sl + 4) & ent_mask;
               }
             }
           }
+          const uint64_t bh = __ballot(hit);
+          const uint32_t nh = __popcll(bh);
+          uint32_t ct;
+          const uint32_t cp = wave_excl_scan(hit ? e_cnt : 0u, lane, &ct);
+          if (counting) {
+            tot_all += ct;
+            if (!staged_all || n_hit + nh > kHitMax) {  // wave-uniform
+              staged_all = false;
+              continue;
+            }
+          } else if (n_hit + nh > kHitMax) {
+            flush_hits();
+          }
+          if (hit) {
+            const uint32_t x = n_hit + prefix_before(bh);
+            h_ga[wv][x] = ga;
+            h_off[wv][x] = e_off;
+            h_via[wv][x] = hn;
+            h_pre[wv][x] = tot + cp;
+          }
+          n_hit += nh;
+          tot += ct;
         }
-        const uint64_t bh = __ballot(hit);
-        const uint32_t nh = __popcll(bh);
-        st_hits += nh;
-        if (n_hit + nh > kHitMax) flush_hits();
-        uint32_t ct;
-        const uint32_t cp = wave_excl_scan(hit ? e_cnt : 0u, lane, &ct);
-        if (hit) {
-          const uint32_t x = n_hit + prefix_before(bh);
-          h_ga[wv][x] = ga;
-          h_off[wv][x] = e_off;
-          h_via[wv][x] = hn;
-          h_pre[wv][x] = tot + cp;
+      };
+      if (SPANS) {
+        pairs(true);
+        reserve(tot_all);
+        if (staged_all) {
+          if (n_hit) flush_hits();
+        } else {  // rare: more hit lists than LDS holds; probe again, resolving as they come
+          n_hit = 0;
+          tot = 0;
+          wave_sync_lds();
+          pairs(false);
+          if (n_hit) flush_hits();
         }
-        n_hit += nh;
-        tot += ct;
+      } else {
+        pairs(false);
+        if (n_hit) flush_hits();
       }
-      if (n_hit) flush_hits();
     } else {
       // Too many merge gathers for the pair analysis: resolve every may-merge record.
-      st_slow = 1;
+      if (SPANS) reserve(o1.merge - o0.merge);
       for (uint32_t i = 0; i < n_g; i++) {
         const GDesc d = gd[i];
         if (!(d.word & kGatherSubs)) continue;
@@ -792,16 +852,13 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
           const uint32_t pos = L.sub_off + L.n_direct + min(c0 + lane, L.n_merge - 1);
           const MergeRef mr = a.ix.mref[pos];
           resolve(act, pos, d.r_pos + L.n_direct + c0 + lane, i, kNone, mr.off, mr.cnt);
-          st_recs += min(64u, L.n_merge - c0);
         }
       }
     }
   }
 
-  if (a.tstat) c_pair = clock64();
   uint32_t n_inl = (uint32_t)(o1.inl - o0.inl);
-  const uint32_t st_inl = n_inl;
-  if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675); rows from k_copy
+  if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675)
     InlRec* __restrict__ ir = a.inl_rows + ib;
     uint32_t kept = 0;
     for (uint32_t i0 = 0; i0 < n_inl; i0 += 64) {
@@ -822,34 +879,33 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
   }
 
   if (lane == 0) {
-    mq_topic_result_dev res;
-    res.sub_base = rb;
-    res.shared_base = o0.shr - a.base.shr;
-    res.inline_base = ib;
-    res.sub_cap = cap;
-    res.n_client = cap - n_nonbase;
-    res.n_ident = n_ext;
-    res.n_shared = (uint32_t)(o1.shr - o0.shr);
-    res.n_inline = n_inl;
-    res.reserved = 0;
-    a.res[t - a.t0] = res;
-    if (a.tstat) {
-      const uint64_t c_end = clock64();
-      uint32_t* ts = a.tstat + (uint64_t)t * kTStat;
-      ts[0] = (uint32_t)min<uint64_t>(c_end - c_start, 0xFFFFFFFFull);
-      ts[1] = (uint32_t)min<uint64_t>(c_map - c_start, 0xFFFFFFFFull);
-      ts[2] = (uint32_t)min<uint64_t>(c_pair - c_map, 0xFFFFFFFFull);
-      ts[3] = n_g;
-      ts[4] = st_map;
-      ts[5] = st_hits;
-      ts[6] = st_recs | (st_slow << 31);
-      ts[7] = (uint32_t)min<uint64_t>(c_flush, 0xFFFFFFFFull);
-      (void)st_inl;
-    }
-    if (a.stats && (st_hits | st_recs | st_slow)) {  // diagnosis only (MQ_MERGE_STATS)
-      atomicAdd(a.stats + 0, (unsigned long long)st_hits);
-      atomicAdd(a.stats + 1, (unsigned long long)st_recs);
-      atomicAdd(a.stats + 2, (unsigned long long)st_slow);
+    if (SPANS) {
+      TopicSpansDev res;
+      res.span_base = o0.g;
+      res.patch_base = pbase;
+      res.inline_base = ib;
+      res.picked_base = o0.shr;
+      res.n_spans = n_g;
+      res.n_patches = n_patch;
+      res.n_inline = n_inl;
+      res.n_rows = cap;
+      res.n_client = cap - n_nonbase;
+      res.n_ident = n_ext;
+      res.n_shared = (uint32_t)(o1.shr - o0.shr);
+      res.reserved = 0;
+      a.sres[t] = res;
+    } else {
+      mq_topic_result_dev res;
+      res.sub_base = rb;
+      res.shared_base = o0.shr - a.base.shr;
+      res.inline_base = ib;
+      res.sub_cap = cap;
+      res.n_client = cap - n_nonbase;
+      res.n_ident = n_ext;
+      res.n_shared = (uint32_t)(o1.shr - o0.shr);
+      res.n_inline = n_inl;
+      res.reserved = 0;
+      a.res[t - a.t0] = res;
     }
   }
   }  // topic loop
@@ -878,9 +934,12 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
   hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(256), 0, s, cnt, n, bpre, off);
 }
 
-void launch_desc(const DescArgs& a, hipStream_t s) {
+void launch_desc(const DescArgs& a, bool spans, hipStream_t s) {
   if (!a.n) return;
-  hipLaunchKernelGGL(k_desc, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+  if (spans)
+    hipLaunchKernelGGL(k_desc<true>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_desc<false>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
@@ -890,11 +949,14 @@ void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
   hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, a);
 }
 
-void launch_merge(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
+void launch_merge(const EmitArgs& a, bool spans, uint32_t max_blocks, hipStream_t s) {
   const uint32_t waves = a.t1 - a.t0;
   if (!waves) return;
   const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
-  hipLaunchKernelGGL(k_merge, dim3(blocks), dim3(256), 0, s, a);
+  if (spans)
+    hipLaunchKernelGGL(k_merge<true>, dim3(blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_merge<false>, dim3(blocks), dim3(256), 0, s, a);
 }
 
 
@@ -1223,16 +1285,39 @@ __device__ __forceinline__ bool pick_in_part(uint32_t filter_id, uint32_t parts,
 }
 
 // One wavefront per workgroup: a topic's table is released as soon as its own wave ends.
+// Row format: the topic's shared rows are one contiguous segment; span format: one segment per
+// span (the shared-pool ranges of its gathered particles), picks written at picked_base.
+template <bool SPANS>
 __global__ __launch_bounds__(64) void k_pick(PickArgs a) {
   __shared__ uint32_t K[kPickSlots];  // filter id + 1 (0 = empty)
   __shared__ uint32_t V[kPickSlots];  // smallest client id seen
   const uint32_t lane = threadIdx.x;
   const uint32_t t = blockIdx.x;
-  const uint64_t base = a.res[t].shared_base;
-  const uint32_t cnt = a.res[t].n_shared;
-  const ShrRec* rows = a.rows + base;
+  uint64_t base, span_base = 0;
+  uint32_t cnt, n_seg = 1;
+  if (SPANS) {
+    const TopicSpansDev& r = a.sres[t];
+    base = r.picked_base;
+    cnt = r.n_shared;
+    span_base = r.span_base;
+    n_seg = r.n_spans;
+  } else {
+    base = a.res[t].shared_base;
+    cnt = a.res[t].n_shared;
+  }
+  // segment k of the topic's shared rows (wave-uniform)
+  auto segment = [&](uint32_t k, const ShrRec** p, uint32_t* c) {
+    if (SPANS) {
+      const SpanRec sp = a.spans[span_base + k];
+      *p = a.pool + sp.shr_off;
+      *c = sp.n_shr;
+    } else {
+      *p = a.rows + base;
+      *c = cnt;
+    }
+  };
   constexpr uint32_t kSpan = 64 * kPickBatch;
-  const bool resident = cnt <= kSpan;  // the mark pass reuses the rows held in registers
+  const bool resident = !SPANS && cnt <= kSpan;  // the mark pass reuses the rows held in registers
   ShrRec buf[kPickBatch];
   uint32_t picked = 0;
   uint32_t parts = 1;
@@ -1247,35 +1332,40 @@ __global__ __launch_bounds__(64) void k_pick(PickArgs a) {
     }
     wave_sync_lds();
     bool full = false;
-    for (uint32_t rb = 0; rb < cnt; rb += kSpan) {
+    for (uint32_t sg = 0; sg < n_seg; sg++) {
+      const ShrRec* rows;
+      uint32_t sc;
+      segment(sg, &rows, &sc);
+      for (uint32_t rb = 0; rb < sc; rb += kSpan) {
 #pragma unroll
-      for (uint32_t j = 0; j < kPickBatch; j++) {  // all loads issued before any use
-        const uint32_t r = rb + j * 64 + lane;
-        buf[j] = r < cnt ? rows[r] : ShrRec{0, 0};
-      }
+        for (uint32_t j = 0; j < kPickBatch; j++) {  // all loads issued before any use
+          const uint32_t r = rb + j * 64 + lane;
+          buf[j] = r < sc ? rows[r] : ShrRec{0, 0};
+        }
 #pragma unroll
-      for (uint32_t j = 0; j < kPickBatch; j++) {
-        const uint32_t r = rb + j * 64 + lane;
-        if (r >= cnt || !pick_in_part(buf[j].filter_id, parts, part)) continue;
-        const uint32_t key = buf[j].filter_id + 1;
-        uint32_t slot = hash32(buf[j].filter_id) & tmask;
-        for (uint32_t probe = 0;; probe++) {
-          if (probe == kPickProbe || probe == tsize) {
-            full = true;
-            break;
+        for (uint32_t j = 0; j < kPickBatch; j++) {
+          const uint32_t r = rb + j * 64 + lane;
+          if (r >= sc || !pick_in_part(buf[j].filter_id, parts, part)) continue;
+          const uint32_t key = buf[j].filter_id + 1;
+          uint32_t slot = hash32(buf[j].filter_id) & tmask;
+          for (uint32_t probe = 0;; probe++) {
+            if (probe == kPickProbe || probe == tsize) {
+              full = true;
+              break;
+            }
+            // plain LDS reads first: a filter's later members mostly find their slot claimed
+            // and the client beaten, and skip the atomics (same-slot atomics serialise)
+            uint32_t k = K[slot];
+            if (k == 0u) {
+              k = atomicCAS(&K[slot], 0u, key);
+              if (k == 0u) k = key;
+            }
+            if (k == key) {
+              if (buf[j].client < V[slot]) atomicMin(&V[slot], buf[j].client);
+              break;
+            }
+            slot = (slot + 1) & tmask;
           }
-          // plain LDS reads first: a filter's later members mostly find their slot claimed
-          // and the client beaten, and skip the atomics (same-slot atomics serialise)
-          uint32_t k = K[slot];
-          if (k == 0u) {
-            k = atomicCAS(&K[slot], 0u, key);
-            if (k == 0u) k = key;
-          }
-          if (k == key) {
-            if (buf[j].client < V[slot]) atomicMin(&V[slot], buf[j].client);
-            break;
-          }
-          slot = (slot + 1) & tmask;
         }
       }
     }
@@ -1292,28 +1382,33 @@ __global__ __launch_bounds__(64) void k_pick(PickArgs a) {
       picked = 0;
       continue;
     }
-    for (uint32_t rb = 0; rb < cnt; rb += kSpan) {
-      if (!resident) {
+    for (uint32_t sg = 0; sg < n_seg; sg++) {
+      const ShrRec* rows;
+      uint32_t sc;
+      segment(sg, &rows, &sc);
+      for (uint32_t rb = 0; rb < sc; rb += kSpan) {
+        if (!resident) {
+#pragma unroll
+          for (uint32_t j = 0; j < kPickBatch; j++) {
+            const uint32_t r = rb + j * 64 + lane;
+            buf[j] = r < sc ? rows[r] : ShrRec{0, 0};
+          }
+        }
 #pragma unroll
         for (uint32_t j = 0; j < kPickBatch; j++) {
+          if (rb + j * 64 >= sc) break;  // wave-uniform
           const uint32_t r = rb + j * 64 + lane;
-          buf[j] = r < cnt ? rows[r] : ShrRec{0, 0};
+          bool take = false;
+          if (r < sc && pick_in_part(buf[j].filter_id, parts, part)) {
+            const uint32_t key = buf[j].filter_id + 1;
+            uint32_t slot = hash32(buf[j].filter_id) & tmask;
+            while (K[slot] != key) slot = (slot + 1) & tmask;  // inserted above
+            take = V[slot] == buf[j].client;
+          }
+          const uint64_t m = __ballot(take);
+          if (take) a.sel[base + picked + prefix_before(m)] = buf[j];
+          picked += (uint32_t)__popcll(m);
         }
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < kPickBatch; j++) {
-        if (rb + j * 64 >= cnt) break;  // wave-uniform
-        const uint32_t r = rb + j * 64 + lane;
-        bool take = false;
-        if (r < cnt && pick_in_part(buf[j].filter_id, parts, part)) {
-          const uint32_t key = buf[j].filter_id + 1;
-          uint32_t slot = hash32(buf[j].filter_id) & tmask;
-          while (K[slot] != key) slot = (slot + 1) & tmask;  // inserted above
-          take = V[slot] == buf[j].client;
-        }
-        const uint64_t m = __ballot(take);
-        if (take) a.sel[base + picked + prefix_before(m)] = buf[j];
-        picked += (uint32_t)__popcll(m);
       }
     }
     wave_sync_lds();  // the next pass clears the table
@@ -1324,7 +1419,10 @@ __global__ __launch_bounds__(64) void k_pick(PickArgs a) {
 
 void launch_pick(const PickArgs& a, hipStream_t s) {
   if (!a.n) return;
-  hipLaunchKernelGGL(k_pick, dim3(a.n), dim3(64), 0, s, a);
+  if (a.sres)
+    hipLaunchKernelGGL(k_pick<true>, dim3(a.n), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_pick<false>, dim3(a.n), dim3(64), 0, s, a);
 }
 
 template <int WPE>

@@ -102,6 +102,9 @@ std::vector<uint64_t> TopicsIndex::Messages(const std::string& filter) {
 
 Subscribers TopicsIndex::Subscribers_(const std::string& topic) { return SubscribersBatch({topic})[0]; }
 
+// One mq_match_spans call for the batch; each topic's Subscribers is rebuilt straight from its
+// spans (the index's records, pinned by the result) with the topic's patches applied — no row
+// copies (include/mqmatch.h, span format).
 std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::string>& topics) {
   std::lock_guard<std::mutex> lk(mu_);
   std::string bytes;
@@ -111,34 +114,49 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::st
     offs.push_back(bytes.size());
   }
   bytes.resize(bytes.size() + 16, '\0');  // readable padding (include/mqmatch.h)
-  mq_match_result* r = nullptr;
-  check(mq_match_batch(idx_, (const uint8_t*)bytes.data(), offs.data(), (uint32_t)topics.size(), &r),
-        "mq_match_batch");
+  mq_span_result* r = nullptr;
+  check(mq_match_spans(idx_, (const uint8_t*)bytes.data(), offs.data(), (uint32_t)topics.size(), &r),
+        "mq_match_spans");
   std::vector<Subscribers> out(topics.size());
+  std::unordered_map<uint32_t, uint32_t> patched;  // topic row -> meta
   for (size_t t = 0; t < topics.size(); t++) {
-    const mq_topic_result& tr = r->topics[t];
+    const mq_topic_spans& ts = r->topics[t];
     Subscribers& s = out[t];
-    // rows in gather order: a client's client row precedes its ident rows
-    for (uint32_t i = 0; i < tr.sub_cap; i++) {
-      const mq_client_row& row = r->sub_rows[tr.sub_base + i];
-      const uint32_t kind = row.meta & MQ_ROW_KIND_MASK;
-      if (kind == 0) {  // client row: merged Subscription
-        Subscription sub = stored_.at({row.client_id, row.filter_id});
-        sub.Qos = row.meta & MQ_META_QOS_MASK;
-        sub.NoLocal = (row.meta & MQ_META_NOLOCAL) != 0;
-        sub.HasIdentifiers = true;
-        sub.Identifiers = {{sub.Filter, sub.Identifier}};
-        s.Subscriptions[clients_[row.client_id]] = sub;
-      } else if (kind == MQ_ROW_IDENT) {  // further Identifiers entry
-        s.Subscriptions[clients_[row.client_id]].Identifiers[filters_[row.filter_id]] = row.identifier;
+    patched.clear();
+    for (uint32_t k = 0; k < ts.n_patches; k++) patched[r->patches[ts.patch_base + k].row] = r->patches[ts.patch_base + k].meta;
+    // records in gather order: a client's client row precedes its ident rows
+    uint32_t rowi = 0;
+    for (uint32_t k = 0; k < ts.n_spans; k++) {
+      const mq_span& sp = r->spans[ts.span_base + k];
+      for (uint32_t i = 0; i < sp.n_sub; i++, rowi++) {
+        mq_client_row row = r->sub_pool[sp.sub_off + i];
+        auto pit = patched.find(rowi);
+        if (pit != patched.end()) row.meta = pit->second;
+        const uint32_t kind = row.meta & MQ_ROW_KIND_MASK;
+        if (kind == 0) {  // client row: merged Subscription
+          Subscription sub = stored_.at({row.client_id, row.filter_id});
+          sub.Qos = row.meta & MQ_META_QOS_MASK;
+          sub.NoLocal = (row.meta & MQ_META_NOLOCAL) != 0;
+          sub.HasIdentifiers = true;
+          sub.Identifiers = {{sub.Filter, sub.Identifier}};
+          s.Subscriptions[clients_[row.client_id]] = sub;
+        } else if (kind == MQ_ROW_IDENT) {  // further Identifiers entry
+          s.Subscriptions[clients_[row.client_id]].Identifiers[filters_[row.filter_id]] = row.identifier;
+        }
       }
+      if (!(r->flags & MQ_SPANS_PICKED))
+        for (uint32_t i = 0; i < sp.n_shr; i++) {
+          const mq_shared_row& row = r->shared_pool[sp.shr_off + i];
+          s.Shared[filters_[row.filter_id]][clients_[row.client_id]] = stored_.at({row.client_id, row.filter_id});
+        }
     }
-    for (uint32_t i = 0; i < tr.n_shared; i++) {
-      const mq_shared_row& row = r->shared_rows[tr.shared_base + i];
-      s.Shared[filters_[row.filter_id]][clients_[row.client_id]] = stored_.at({row.client_id, row.filter_id});
-    }
-    for (uint32_t i = 0; i < tr.n_inline; i++) {
-      const mq_inline_row& row = r->inline_rows[tr.inline_base + i];
+    if (r->flags & MQ_SPANS_PICKED)
+      for (uint32_t i = 0; i < ts.n_shared; i++) {
+        const mq_shared_row& row = r->picked_rows[ts.picked_base + i];
+        s.Shared[filters_[row.filter_id]][clients_[row.client_id]] = stored_.at({row.client_id, row.filter_id});
+      }
+    for (uint32_t i = 0; i < ts.n_inline; i++) {
+      const mq_inline_row& row = r->inline_rows[ts.inline_base + i];
       s.InlineSubscriptions[row.identifier] = inline_.at({row.identifier, row.filter_id});
     }
   }

@@ -49,6 +49,27 @@ class MatchResult(C.Structure):
                 ("n_shared_rows", C.c_uint64), ("n_inline_rows", C.c_uint64)]
 
 
+class TopicSpans(C.Structure):
+    _fields_ = [("span_base", C.c_uint64), ("patch_base", C.c_uint64), ("inline_base", C.c_uint64),
+                ("picked_base", C.c_uint64), ("n_spans", C.c_uint32), ("n_patches", C.c_uint32),
+                ("n_inline", C.c_uint32), ("n_rows", C.c_uint32), ("n_client", C.c_uint32),
+                ("n_ident", C.c_uint32), ("n_shared", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class SpanResult(C.Structure):
+    _fields_ = [("n_topics", C.c_uint32), ("flags", C.c_uint32), ("topics", C.c_void_p), ("spans", C.c_void_p),
+                ("patches", C.c_void_p), ("inline_rows", C.c_void_p), ("picked_rows", C.c_void_p),
+                ("sub_pool", C.c_void_p), ("shared_pool", C.c_void_p), ("n_spans", C.c_uint64),
+                ("n_patches", C.c_uint64), ("n_inline_rows", C.c_uint64), ("n_picked_rows", C.c_uint64),
+                ("sub_pool_len", C.c_uint64), ("shared_pool_len", C.c_uint64)]
+
+
+SPANS_PICKED = 1  # MQ_SPANS_PICKED
+
+# mq_set_option (include/mqmatch.h MQ_OPT_*)
+OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP = 1, 2, 3, 4, 5, 6
+
+
 class MsgResult(C.Structure):
     _fields_ = [("n_filters", C.c_uint32), ("reserved", C.c_uint32), ("base", C.c_void_p),
                 ("count", C.c_void_p), ("handles", C.c_void_p), ("n_handles", C.c_uint64)]
@@ -78,7 +99,8 @@ EXPORTS = [
     "mq_match_batch", "mq_match_device", "mq_match_chunks", "mq_messages_batch",
     "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
     "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
-    "mq_acl_match_batch", "mq_select_shared_device",
+    "mq_acl_match_batch", "mq_select_shared_device", "mq_match_spans", "mq_match_spans_device",
+    "mq_spans_expand", "mq_set_option",
 ]
 
 CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
@@ -121,6 +143,11 @@ def lib():
         "mq_retain_bulk": (C.c_int, [vp, _u8p, _u64p, _u64p, C.c_uint64]),
         "mq_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MatchResult))]),
         "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
+        "mq_match_spans": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(SpanResult))]),
+        "mq_match_spans_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(SpanResult)]),
+        "mq_spans_expand": (C.c_int, [C.POINTER(SpanResult), C.c_uint32, C.c_uint32, vp, C.c_uint64, vp,
+                                      C.c_uint64, _u64p, _u64p]),
+        "mq_set_option": (C.c_int, [vp, C.c_uint32, C.c_uint64]),
         "mq_match_chunks": (C.c_uint32, [vp]),
         "mq_select_shared_device": (C.c_int, [vp, C.POINTER(MatchResult), vp, vp, vp]),
         "mq_match_device_chunks": (C.c_int, [vp, vp, vp, C.c_uint32, vp, CHUNK_FN, vp]),
@@ -324,6 +351,56 @@ class Engine:
         _check(lib().mq_index_stats(self.h, C.byref(s)), "mq_index_stats")
         return {n: getattr(s, n) for n, _ in Stats._fields_ if n != "reserved"}
 
+    def set_option(self, option, value):
+        """mq_set_option (MQ_OPT_*)."""
+        _check(lib().mq_set_option(self.h, option, int(value)), "mq_set_option")
+
+    def match_spans(self, bytes_, offs):
+        """mq_match_spans -> dict of numpy copies of the span-format result (topics as a
+        structured array, spans [n,4], patches [n,2], inline rows, picked rows, flags)."""
+        n = len(offs) - 1
+        rp = C.POINTER(SpanResult)()
+        _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
+        try:
+            return _span_arrays(rp.contents, n)
+        finally:
+            lib().mq_result_free(rp)
+
+    def match_batch_spans(self, bytes_, offs):
+        """mq_match_spans, expanded on the host by mq_spans_expand into exactly match_batch()'s
+        dict (rows region per topic = its spans' records with the patches applied)."""
+        n = len(offs) - 1
+        rp = C.POINTER(SpanResult)()
+        _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
+        try:
+            r = rp.contents
+            a = _span_arrays(r, n)
+            t = a["topics"]
+            n_rows, n_shared = t["n_rows"].astype(np.uint64), t["n_shared"].astype(np.uint64)
+            rows = np.zeros((max(int(n_rows.sum()), 1), 4), np.uint32)
+            shared = np.zeros((max(int(n_shared.sum()), 1), 2), np.uint32)
+            nr, ns = C.c_uint64(), C.c_uint64()
+            _check(lib().mq_spans_expand(rp, 0, n, rows.ctypes.data, len(rows), shared.ctypes.data, len(shared),
+                                         C.byref(nr), C.byref(ns)), "mq_spans_expand")
+        finally:
+            lib().mq_result_free(rp)
+        excl = lambda c: np.concatenate(([0], np.cumsum(c)[:-1])).astype(np.uint64) if len(c) else np.zeros(0, np.uint64)
+        return {
+            "sub_base": excl(n_rows), "shared_base": excl(n_shared), "inline_base": t["inline_base"].copy(),
+            "sub_cap": t["n_rows"].copy(), "n_client": t["n_client"].copy(), "n_ident": t["n_ident"].copy(),
+            "n_shared": t["n_shared"].copy(), "n_inline": t["n_inline"].copy(),
+            "rows": rows[:int(nr.value)], "shared": shared[:int(ns.value)], "inline": a["inline"],
+            "n_patches": int(t["n_patches"].sum()), "n_spans": int(t["n_spans"].sum()),
+        }
+
+    def match_spans_device(self, d_bytes, d_offs, n, stream=None):
+        """mq_match_spans_device on device pointers (ints); returns the SpanResult struct."""
+        r = SpanResult()
+        _check(lib().mq_match_spans_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_offs), n,
+                                           C.c_void_p(stream) if stream else None, C.byref(r)),
+               "mq_match_spans_device")
+        return r
+
     def match_batch_rows(self, bytes_, offs):
         """mq_match_batch with its results left in the library's host buffers (freed here):
         the end-to-end path (H2D topics, kernels, D2H of every row). Returns the row counts."""
@@ -466,6 +543,31 @@ class Engine:
         _check(lib().mq_profile_reset(self.h), "mq_profile_reset")
 
 
+_TOPIC_SPANS_DT = np.dtype([("span_base", np.uint64), ("patch_base", np.uint64), ("inline_base", np.uint64),
+                            ("picked_base", np.uint64), ("n_spans", np.uint32), ("n_patches", np.uint32),
+                            ("n_inline", np.uint32), ("n_rows", np.uint32), ("n_client", np.uint32),
+                            ("n_ident", np.uint32), ("n_shared", np.uint32), ("reserved", np.uint32)])
+
+
+def _span_arrays(r, n):
+    """numpy copies of a host SpanResult's arrays."""
+    def arr(ptr, count, dtype, width=None):
+        shape = (count,) if width is None else (count, width)
+        if count == 0 or not ptr:
+            return np.zeros(shape, dtype)
+        nbytes = count * np.dtype(dtype).itemsize * (width or 1)
+        buf = (C.c_char * nbytes).from_address(ptr)
+        return np.frombuffer(buf, dtype).reshape(shape).copy()
+    return {
+        "topics": arr(r.topics, n, _TOPIC_SPANS_DT),
+        "spans": arr(r.spans, int(r.n_spans), np.uint32, 4),
+        "patches": arr(r.patches, int(r.n_patches), np.uint32, 2),
+        "inline": arr(r.inline_rows, int(r.n_inline_rows), np.uint32, 2),
+        "picked": arr(r.picked_rows, int(r.n_picked_rows), np.uint32, 2),
+        "flags": int(r.flags),
+    }
+
+
 ROW_IDENT = 0x40000000  # MQ_ROW_IDENT (include/mqmatch.h)
 ROW_DROP = 0x80000000   # MQ_ROW_DROP
 ROW_KIND_MASK = 0xC0000000
@@ -486,9 +588,13 @@ def topic_rows(res, t):
 class TopicsIndex:
     """Mirror of the Go TopicsIndex (topics.go:349-698) over the engine's C-ABI."""
 
-    def __init__(self, device=0, select_shared=False):
+    def __init__(self, device=0, select_shared=False, fmt="spans"):
         """select_shared: SelectShared on the device (MQ_CFG_SELECT_SHARED) — each Shared[filter]
-        holds only its picked member, for a broker with no OnSelectSubscribers hook."""
+        holds only its picked member, for a broker with no OnSelectSubscribers hook.
+        fmt: "spans" (mq_match_spans + mq_spans_expand, the default) or "rows" (mq_match_batch)."""
+        if fmt not in ("spans", "rows"):
+            raise ValueError(fmt)
+        self.fmt = fmt
         self.engine = Engine(device, select_shared=select_shared)
         self.client_ids: Dict[str, int] = {}
         self.clients: List[str] = []
@@ -553,7 +659,10 @@ class TopicsIndex:
     def subscribers_batch(self, topics) -> List[Subscribers]:
         """The batching stage's entry point: one engine call for many topics."""
         raw, offs = pack_strings(topics)
-        res = self.engine.match_batch(raw, offs)
+        if self.fmt == "spans":
+            res = self.engine.match_batch_spans(raw, offs)
+        else:
+            res = self.engine.match_batch(raw, offs)
         return [self._rebuild(res, t) for t in range(len(topics))]
 
     def _rebuild(self, res, t) -> Subscribers:

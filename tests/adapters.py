@@ -73,10 +73,10 @@ def canonical(subs):
 class EngineAdapter:
     name = "engine"
 
-    def __init__(self):
+    def __init__(self, fmt="spans"):
         from mqmatch import engine as E
         self.E = E
-        self.x = E.TopicsIndex(0)
+        self.x = E.TopicsIndex(0, fmt=fmt)
         self._h = 0
 
     def subscribe(self, client, filter, qos=0, identifier=0, no_local=False, rap=False, rh=0):

@@ -27,7 +27,7 @@ def test_library_exports_all_symbols():
     L = E.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.mq_abi_version() == 4
+    assert L.mq_abi_version() == 5
 
 
 def test_errors_are_reported():
@@ -157,3 +157,13 @@ def test_unsubscribe_everything_empties_trie():
     st = eng.stats()
     assert st["nodes"] == 0 and st["subs"] == 0 and st["shared"] == 0 and st["subs_merge"] == 0
     assert st["partners"] == 0
+
+
+def test_options_without_device():
+    """mq_set_option is accepted before the device exists (applied when it is first touched) and
+    rejects unknown options."""
+    eng = E.Engine()
+    eng.set_option(E.OPT_CHUNK_ROWS, 1 << 20)
+    eng.set_option(E.OPT_PATCH_CAP, 1024)
+    with pytest.raises(E.EngineError):
+        eng.set_option(99, 1)

@@ -6,6 +6,7 @@ reference's tests and quirk register (SURVEY.md App. A): empty topics, '$' topic
 levels, literal '+'/'#' topic levels, long (hashed) segments, deep topics, Unicode $share,
 inline last-write, incremental updates between batches, chunked outputs.
 """
+import functools
 import os
 import random
 
@@ -20,9 +21,13 @@ import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+FORMATS = ["spans", "rows"]  # mq_match_spans (+ mq_spans_expand) and mq_match_batch
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("kat", KATS + MESSAGE_KATS, ids=lambda f: f.__name__)
-def test_engine_kat(kat, gpu_available):
-    kat(EngineAdapter)
+def test_engine_kat(kat, fmt, gpu_available):
+    kat(functools.partial(EngineAdapter, fmt))
 
 
 SEGS = ["a", "b", "c", "", "+", "#", "$SYS", "$share", "$SHARE", "$ſhare", "g", "sport",
@@ -35,8 +40,8 @@ def rand_filter(r, segs=SEGS):
     return "/".join(r.choice(segs) for _ in range(r.randint(1, 5)))
 
 
-def build_pair(r, n_subs, n_clients, n_inline=0):
-    e, o = EngineAdapter(), OracleAdapter()
+def build_pair(r, n_subs, n_clients, n_inline=0, fmt="spans"):
+    e, o = EngineAdapter(fmt), OracleAdapter()
     for _ in range(n_subs):
         f = rand_filter(r)
         c = f"c{r.randrange(n_clients)}"
@@ -49,10 +54,11 @@ def build_pair(r, n_subs, n_clients, n_inline=0):
     return e, o
 
 
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("seed", range(8))
-def test_random_small_parity(seed, gpu_available):
+def test_random_small_parity(seed, fmt, gpu_available):
     r = random.Random(1000 + seed)
-    e, o = build_pair(r, 300, 12, n_inline=40)
+    e, o = build_pair(r, 300, 12, n_inline=40, fmt=fmt)
     topics = ["/".join(r.choice(TSEGS) for _ in range(r.randint(1, 6))) for _ in range(400)]
     topics += ["", "a", "a/", "/", "//", "$SYS", "a/+", "+", "#", "a/#", "+/+", "a/b/c/+/#"]
     got = e.subscribers_batch(topics)
@@ -134,12 +140,17 @@ def _workload_pair(n_subs, n_clients, seed):
     return w, eng, orc
 
 
-def _digest_parity(eng, orc, tb, to):
-    res = eng.match_batch(tb, to)
-    dg, cnt = engine_digests(res)
-    od, ocnt, _ = orc.digest_batch(tb, to, nthreads=os.cpu_count() or 8)
-    bad = np.nonzero(dg != od)[0]
-    assert len(bad) == 0, f"{len(bad)} topics differ, first {bad[:5]}, counts {cnt[bad[:3]]} vs {ocnt[bad[:3]]}"
+def _digest_parity(eng, orc, tb, to, fmts=("rows", "spans")):
+    """Per-topic digests of the engine in each result format against the oracle's."""
+    od, ocnt, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+    for fmt in fmts:
+        res = eng.match_batch_spans(tb, to) if fmt == "spans" else eng.match_batch(tb, to)
+        dg, cnt = engine_digests(res)
+        bad = np.nonzero(dg != od)[0]
+        assert len(bad) == 0, (f"{fmt}: {len(bad)} topics differ, first {bad[:5]}, counts {cnt[bad[:3]]} vs "
+                               f"{ocnt[bad[:3]]}")
+        if fmt == "spans":  # the patches name a small part of the rows; each row at most once
+            assert res["n_patches"] <= int(res["sub_cap"].sum())
     return cnt
 
 
@@ -188,33 +199,35 @@ def test_incremental_updates_between_batches(gpu_available):
     assert st["upload_bytes_total"] > 0
 
 
-def test_chunked_outputs(gpu_available, monkeypatch):
+def test_chunked_outputs(gpu_available):
+    from mqmatch import engine as E
     from mqmatch import workload as W
-    monkeypatch.setenv("MQ_CHUNK_ROWS", "200000")
     w, eng, orc = _workload_pair(50000, 5000, seed=41)
+    eng.set_option(E.OPT_CHUNK_ROWS, 200000)
     tb, to = W.gen_topics(w, 30000, seed=42)
-    _digest_parity(eng, orc, tb, to)
+    _digest_parity(eng, orc, tb, to, fmts=("rows",))
     assert eng.match_chunks() > 1
 
 
-def test_subbatch_pipeline(gpu_available, monkeypatch):
+def test_subbatch_pipeline(gpu_available):
     """Batches cut into pipelined sub-batches (walk of sub-batch b + 1 under the copies of b),
     each with several output chunks: results identical to the oracle."""
+    from mqmatch import engine as E
     from mqmatch import workload as W
     w, eng, orc = _workload_pair(50000, 5000, seed=43)
     tb, to = W.gen_topics(w, 30000, seed=44)
-    monkeypatch.setenv("MQ_SUBBATCH_TOPICS", "4096")
-    monkeypatch.setenv("MQ_CHUNK_ROWS", "300000")
-    _digest_parity(eng, orc, tb, to)
+    eng.set_option(E.OPT_SUBBATCH_TOPICS, 4096)
+    eng.set_option(E.OPT_CHUNK_ROWS, 300000)
+    _digest_parity(eng, orc, tb, to, fmts=("rows",))
     assert eng.match_chunks() >= 8
-    monkeypatch.setenv("MQ_SUBBATCH_TOPICS", "1024")  # one scan block per sub-batch
-    _digest_parity(eng, orc, tb, to[:5001])
+    eng.set_option(E.OPT_SUBBATCH_TOPICS, 1024)  # one scan block per sub-batch
+    _digest_parity(eng, orc, tb, to[:5001], fmts=("rows",))
 
 
-def test_subbatch_gather_overflow(gpu_available, monkeypatch):
+def test_subbatch_gather_overflow(gpu_available):
     """Gather-slot overflow (compact fill pass) in some sub-batches only."""
-    monkeypatch.setenv("MQ_SUBBATCH_TOPICS", "1024")
-    e, o = EngineAdapter(), OracleAdapter()
+    e, o = EngineAdapter("rows"), OracleAdapter()
+    e.x.engine.set_option(e.E.OPT_SUBBATCH_TOPICS, 1024)
     levels = [f"l{i}" for i in range(80)]
     for d in range(1, 80):
         f = "/".join(levels[:d]) + "/#"
@@ -227,10 +240,12 @@ def test_subbatch_gather_overflow(gpu_available, monkeypatch):
     assert got[3000] == got[3002]
 
 
-def test_hot_lists(gpu_available):
-    """Lists of >= 1024 subscriptions (root '#', 'a/#') take the node-major copy (k_hot); some of
-    their clients also hold co-matching filters (merge bases / ident rows inside hot lists)."""
-    e, o = EngineAdapter(), OracleAdapter()
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_long_lists_with_merges(fmt, gpu_available):
+    """Lists of thousands of subscriptions (root '#', 'a/#': one span each, or many k_copy tiles
+    over one list) in which some clients hold co-matching filters, so merge bases and ident rows
+    sit inside long lists."""
+    e, o = EngineAdapter(fmt), OracleAdapter()
     for i in range(3000):
         c = f"h{i}"
         assert e.subscribe(c, "#", qos=i % 3, identifier=i % 5) == o.subscribe(c, "#", qos=i % 3, identifier=i % 5)
@@ -246,14 +261,15 @@ def test_hot_lists(gpu_available):
         assert g == o.subscribers(t), t
 
 
-def test_match_device_chunks_consumer(gpu_available, monkeypatch):
+def test_match_device_chunks_consumer(gpu_available):
     """mq_match_device_chunks: a consumer copying every chunk to the host on the chunk stream
     sees exactly mq_match_batch's rows and per-topic records."""
     import ctypes as C
     import torch
+    from mqmatch import engine as E
     from mqmatch import workload as W
-    monkeypatch.setenv("MQ_CHUNK_ROWS", "150000")
     w, eng, orc = _workload_pair(50000, 5000, seed=45)
+    eng.set_option(E.OPT_CHUNK_ROWS, 150000)
     tb, to = W.gen_topics(w, 20000, seed=46)
     n = len(to) - 1
     host = eng.match_batch(tb, to)
@@ -304,6 +320,86 @@ def test_match_device_stream(gpu_available):
     assert r.n_topics == len(to) - 1 and r.n_sub_rows == len(host["rows"])
 
 
+def test_spans_patch_pool_growth(gpu_available):
+    """A patch pool far smaller than a batch needs: the batch's reservations exceed it, the pool
+    grows and k_merge runs again; the result is unchanged."""
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(60000, 3000, seed=47)
+    eng.set_option(E.OPT_PATCH_CAP, 64)
+    tb, to = W.gen_topics(w, 8000, seed=48)
+    _digest_parity(eng, orc, tb, to, fmts=("spans",))
+    _digest_parity(eng, orc, tb, to, fmts=("spans",))  # the grown pool is kept
+
+
+def test_spans_format_shape(gpu_available):
+    """The span format itself: spans in gather order cover exactly n_rows records, patch rows are
+    in range and unique per topic, and a topic without co-matching records has no patches."""
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(40000, 4000, seed=49)
+    tb, to = W.gen_topics(w, 3000, seed=50)
+    a = eng.match_spans(tb, to)
+    t, spans, patches = a["topics"], a["spans"], a["patches"]
+    for i in range(len(t)):
+        sp = spans[int(t["span_base"][i]):int(t["span_base"][i]) + int(t["n_spans"][i])]
+        assert int(sp[:, 1].sum()) == int(t["n_rows"][i])
+        assert int(sp[:, 3].sum()) == int(t["n_shared"][i])
+        pr = patches[int(t["patch_base"][i]):int(t["patch_base"][i]) + int(t["n_patches"][i]), 0]
+        assert len(set(pr.tolist())) == len(pr) and (pr < max(1, int(t["n_rows"][i]))).all()
+        if int(t["n_client"][i]) == int(t["n_rows"][i]):
+            assert all((patches[int(t["patch_base"][i]) + k, 1] & 0xC0000000) == 0 for k in range(len(pr)))
+    rows_bytes = 16 * int(t["n_rows"].sum())
+    span_bytes = 64 * len(t) + 16 * len(spans) + 8 * len(patches)
+    assert span_bytes * 4 < rows_bytes  # the point of the format
+
+
+def test_spans_device_matches_host(gpu_available):
+    """mq_match_spans_device on torch buffers: the same per-topic records as mq_match_spans."""
+    import ctypes as C
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(20000, 2000, seed=53)
+    tb, to = W.gen_topics(w, 4096, seed=54)
+    host = eng.match_spans(tb, to)
+    d_tb = torch.from_numpy(tb).cuda()
+    d_to = torch.from_numpy(to.view(np.int64)).cuda()
+    s = torch.cuda.Stream()
+    r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), len(to) - 1, s.cuda_stream)
+    n = len(to) - 1
+    top = torch.empty(n * 16, dtype=torch.int32, device="cuda")
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipMemcpy(top.data_ptr(), r.topics, n * 64, 3) == 0
+    got = top.cpu().numpy().view(E._TOPIC_SPANS_DT)
+    for k in ("span_base", "n_spans", "n_rows", "n_client", "n_ident", "n_shared", "n_inline", "n_patches"):
+        assert (got[k] == host["topics"][k]).all(), k
+    assert r.n_spans == len(host["spans"]) and r.n_patches >= int(host["topics"]["n_patches"].sum())
+
+
+def test_spans_result_pins_host_image(gpu_available):
+    """A host span result pins the pools it points into: an update from another thread waits
+    until the result is freed."""
+    import ctypes as C
+    import threading
+    import time
+    from mqmatch import engine as E
+    eng = E.Engine()
+    for c in range(50):
+        eng.subscribe("a/+", c, 0, 1, 0, 0)
+    tb, to = E.pack_strings(["a/b"])
+    rp = C.POINTER(E.SpanResult)()
+    assert E.lib().mq_match_spans(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), 1, C.byref(rp)) == 0
+    done = []
+    th = threading.Thread(target=lambda: done.append(eng.subscribe("a/b", 999, 1, 0, 0, 0)))
+    th.start()
+    time.sleep(0.5)
+    assert not done  # waiting for the view
+    E.lib().mq_result_free(rp)
+    th.join(timeout=30)
+    assert done == [1]
+
+
 MSEGS = ["a", "b", "c", "", "$SYS", "$share", "g", "x", "averyveryverylongsegment", "ü", "$x"]
 
 
@@ -347,18 +443,18 @@ def test_messages_empty_topic_retained(gpu_available):
         assert e.messages(f) == o.messages(f), f
 
 
-@pytest.mark.parametrize("spec_mb", [None, "0", "3"])
-def test_messages_workload_parity(spec_mb, gpu_available, monkeypatch):
+@pytest.mark.parametrize("spec_mb", [None, 0, 3])
+def test_messages_workload_parity(spec_mb, gpu_available):
     """Messages on a config-5-shaped workload. spec_mb: the speculative count's scratch budget
     (default: one walk for most filters; "0": count and fill walks; "3": a few hundred slots per
     filter, so that many filters overflow their scratch and are walked again)."""
     from mqmatch import workload as W
     from mqmatch import engine as E
-    if spec_mb is not None:
-        monkeypatch.setenv("MQ_MSG_SPEC_MB", spec_mb)
     rb, ro, hd, rh = W.gen_retained(100000, n_sys=1000, seed=61)
     fb, fo = W.gen_msg_filters(rh, 5000, seed=62)
     eng, orc = E.Engine(), O.OracleIndex()
+    if spec_mb is not None:
+        eng.set_option(E.OPT_MSG_SPEC_MB, spec_mb)
     eng.retain_bulk(rb, ro, hd)
     orc.retain_bulk(rb, ro, hd)
     base, count, hs = eng.messages_batch(fb, fo)
@@ -373,10 +469,11 @@ def test_messages_workload_parity(spec_mb, gpu_available, monkeypatch):
         assert d == od[i], i
 
 
-def test_gather_slot_overflow(gpu_available):
-    """A topic matching > 32 particles overflows its count-pass gather slots and takes the
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_gather_slot_overflow(fmt, gpu_available):
+    """A topic matching > 64 particles overflows its count-pass gather slots and takes the
     compact fill pass; mixed with ordinary topics in one batch."""
-    e, o = EngineAdapter(), OracleAdapter()
+    e, o = EngineAdapter(fmt), OracleAdapter()
     levels = [f"l{i}" for i in range(50)]
     for d in range(1, 50):
         f = "/".join(levels[:d]) + "/#"
@@ -391,10 +488,11 @@ def test_gather_slot_overflow(gpu_available):
         assert g == o.subscribers(t), t
 
 
-def test_many_merging_clients(gpu_available):
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_many_merging_clients(fmt, gpu_available):
     """600 clients each with three co-matching filters in one topic (bases, max Qos, ident rows),
     next to clients whose partners are not gathered for the topic (plain rows)."""
-    e, o = EngineAdapter(), OracleAdapter()
+    e, o = EngineAdapter(fmt), OracleAdapter()
     for i in range(600):
         c = f"m{i}"
         for f, ident in (("o/#", i % 3), ("o/p", 1 + i % 5), ("o/+", 0)):
@@ -409,11 +507,12 @@ def test_many_merging_clients(gpu_available):
         assert g == o.subscribers(t), t
 
 
-def test_partner_map_fallback(gpu_available):
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_partner_map_fallback(fmt, gpu_available):
     """Topics gathering 128 (the pair analysis' limit), 256 and 512 (linear partner lookup)
     nodes that all hold may-merge subscriptions: every literal/'+' path of depth 7, 8 and 9."""
     import itertools
-    e, o = EngineAdapter(), OracleAdapter()
+    e, o = EngineAdapter(fmt), OracleAdapter()
     for depth in (7, 8, 9):
         paths = ["/".join(f"a{i}" if b == 0 else "+" for i, b in enumerate(bits))
                  for bits in itertools.product((0, 1), repeat=depth)]
@@ -428,10 +527,12 @@ def test_partner_map_fallback(gpu_available):
         assert g == o.subscribers(t), t
 
 
-def test_many_pair_hits(gpu_available):
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_many_pair_hits(fmt, gpu_available):
     """A topic whose merge gathers are pairwise partners through many clients: hundreds of
-    (g, h) hit lists, staged and resolved in several flushes."""
-    e, o = EngineAdapter(), OracleAdapter()
+    (g, h) hit lists, staged and resolved in several flushes (span format: more lists than LDS
+    holds, so the pair analysis counts first, reserves the patches, then resolves)."""
+    e, o = EngineAdapter(fmt), OracleAdapter()
     r = random.Random(77)
     fs = ["#", "a/#", "+/#", "a/b/#", "a/+/#", "+/b/#", "+/+/#", "a/b/c/#", "a/b/+/#", "+/b/c/#",
           "a/+/c/#", "+/+/c/#", "a/b/c/d", "a/b/c/+", "a/+/c/d", "+/b/c/d", "+/+/+/+", "a/b/+/d",

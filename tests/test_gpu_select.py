@@ -41,9 +41,10 @@ def _pair(w):
     return full, sel
 
 
-def _check_batch(full, sel, tb, to):
-    a, b = full.match_batch(tb, to), sel.match_batch(tb, to)
-    for k in ("sub_base", "sub_cap", "n_client", "n_ident", "n_inline", "shared_base"):
+def _check_batch(full, sel, tb, to, fmt="rows"):
+    a = full.match_batch(tb, to)
+    b = sel.match_batch_spans(tb, to) if fmt == "spans" else sel.match_batch(tb, to)
+    for k in ("sub_base", "sub_cap", "n_client", "n_ident", "n_inline") + (("shared_base",) if fmt == "rows" else ()):
         assert (a[k] == b[k]).all(), k
     assert (a["rows"] == b["rows"]).all() and (a["inline"] == b["inline"]).all()
     n_picked = 0
@@ -53,16 +54,18 @@ def _check_batch(full, sel, tb, to):
     return a, b, n_picked
 
 
-def test_select_shared_workload(gpu_available):
+@pytest.mark.parametrize("fmt", ["rows", "spans"])
+def test_select_shared_workload(fmt, gpu_available):
     from mqmatch import workload as W
     w = W.gen_subscriptions(60000, 3000, seed=71)
     full, sel = _pair(w)
     tb, to = W.gen_topics(w, 8000, seed=72)
-    a, b, n_picked = _check_batch(full, sel, tb, to)
+    a, b, n_picked = _check_batch(full, sel, tb, to, fmt)
     assert n_picked > 0 and n_picked < int(a["n_shared"].sum())
 
 
-def test_select_shared_many_filters_per_topic(gpu_available):
+@pytest.mark.parametrize("fmt", ["rows", "spans"])
+def test_select_shared_many_filters_per_topic(fmt, gpu_available):
     """More distinct shared filters in one topic than k_pick's LDS table holds: the topic is
     re-run in hash partitions."""
     from mqmatch import engine as E
@@ -80,7 +83,7 @@ def test_select_shared_many_filters_per_topic(gpu_available):
         e.subscribe("a/b", 5, fid, qos=2)
     topics = ["a/b", "a/c", "x", "a", "a/b/c", "$SYS/a"]
     tb, to = E.pack_strings(topics)
-    a, b, n_picked = _check_batch(full, sel, tb, to)
+    a, b, n_picked = _check_batch(full, sel, tb, to, fmt)
     assert int(b["n_shared"][0]) == 9000 and n_picked == 9000 + 6000 + 3000 * 4
 
 
@@ -115,14 +118,15 @@ def test_select_shared_vs_oracle_and_server_flow(gpu_available):
             next(iter(m)) for m in got.shared.values()}, t
 
 
-def test_select_shared_device_api(gpu_available, monkeypatch):
+def test_select_shared_device_api(gpu_available):
     """mq_select_shared_device on each chunk inside a chunk consumer (torch-owned output
     buffers, the chunk stream) equals the MQ_CFG_SELECT_SHARED batch results."""
     import torch
+    from mqmatch import engine as E
     from mqmatch import workload as W
-    monkeypatch.setenv("MQ_CHUNK_ROWS", "150000")
     w = W.gen_subscriptions(50000, 5000, seed=75)
     full, sel = _pair(w)
+    full.set_option(E.OPT_CHUNK_ROWS, 150000)
     tb, to = W.gen_topics(w, 20000, seed=76)
     n = len(to) - 1
     want = sel.match_batch(tb, to)
