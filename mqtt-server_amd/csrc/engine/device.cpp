@@ -212,6 +212,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_MSG_WAVES: msg_wpe_opt_ = (uint32_t)v; return true;
     case MQ_OPT_SERIAL: serial_ = v != 0; return true;
     case MQ_OPT_PATCH_CAP: patch_cap_init_ = std::max<uint64_t>(v, 64); return true;
+    case MQ_OPT_MERGE_WAVES: merge_wpe_ = (uint32_t)v; return true;
     default: return false;
   }
 }
@@ -637,7 +638,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
       }
       prof.begin(ms);
-      launch_merge(a, false, merge_blocks_, ms);
+      launch_merge(a, false, merge_wpe_, merge_blocks_, ms);
       prof.end("merge", ms);
       hip_check(hipGetLastError(), "k_merge");
       const uint32_t nt = a.t1 - a.t0;
@@ -831,7 +832,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     a.pcap = patch_cap_;
     hip_check(hipMemsetAsync(a.pcount, 0, sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
     prof.begin(s);
-    launch_merge(a, true, merge_blocks_, s);
+    launch_merge(a, true, merge_wpe_, merge_blocks_, s);
     prof.end("merge", s);
     hip_check(hipGetLastError(), "k_merge<spans>");
     hip_check(hipMemcpyAsync(h_pc, a.pcount, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H pcount");

@@ -517,7 +517,8 @@ void Index::flush_merge() {
     for (uint32_t i = 0; i < ecap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
     for (size_t i = 0; i < hk.size(); i++) {
       const MergeRef r = mref.h[L.sub_off + L.n_direct + hk[i].second];
-      plist.m.at_w(lo + i) = PairSlot{hk[i].second, r.off, r.cnt, 0};
+      const SubRec& rec = subs.m.h[L.sub_off + L.n_direct + hk[i].second];
+      plist.m.at_w(lo + i) = PairSlot{hk[i].second, r.off, r.cnt, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u)};
     }
     for (size_t b = 0; b < hk.size();) {
       size_t e = b + 1;
@@ -583,9 +584,11 @@ bool Index::check(std::string* why) {
         const PairEnt& pe = pent.m.h[P.ent_off + sl];
         if (pe.h != mp.node) return bad(at + ": pair block misses a partner node");
         bool listed = false;
+        const SubRec& rec = subs.m.h[pos];
+        const uint32_t want_meta = rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u);
         for (uint32_t i = 0; i < pe.cnt && !listed; i++) {
           const PairSlot& ps = plist.m.h[pe.off + i];
-          listed = ps.k == k - L.n_direct && ps.mp_off == r.off && ps.mp_cnt == r.cnt;
+          listed = ps.k == k - L.n_direct && ps.mp_off == r.off && ps.mp_cnt == r.cnt && ps.meta == want_meta;
         }
         if (!listed) return bad(at + ": pair list misses a slot");
       }
@@ -798,8 +801,9 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
   uint32_t pos;
   if (sub_pos_.get((uint64_t)n << 32 | client, &pos)) {
     subs.m.at_w(pos) = rec;
-    const PartList& p = subp_[pos];  // the partners' links carry this subscription's meta
+    const PartList& p = subp_[pos];  // the partners' links carry this subscription's meta,
     for (uint32_t i = 0; i < p.cnt; i++) merge_dirty(parts.m.h[p.off + i]);
+    if (sub_is_merge(n, pos)) merge_dirty(n);  // and n's pair slots copy it
     return 0;
   }
   // Partners: the client's other subscriptions that could match the same topic (the merge

@@ -25,6 +25,7 @@ constexpr uint32_t kMapSlots = 128;    // per-wave LDS map (gathered merge node 
 constexpr uint32_t kPairMax = 64;     // merge gathers covered by the pair analysis
 constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
 constexpr uint32_t kPartBatch = 8;     // partner links loaded together per record
+constexpr uint32_t kMergeWavesPerEU = 1;  // k_merge register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -182,7 +183,7 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
-void launch_merge(const EmitArgs& a, bool spans, uint32_t max_blocks, hipStream_t s);
+void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
 // first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
 // fill pass must still walk; the fill pass then walks only those.

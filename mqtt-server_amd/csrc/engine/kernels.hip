@@ -431,6 +431,11 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     d.i_src = L.inl_off;
     d.word = gw;
     d.mdir = L.n_direct | ((gw & kGatherSubs) && L.n_merge ? kDescMerge : 0u);
+    if (SPANS && (d.mdir & kDescMerge)) {  // k_merge reads the pair block's header from here
+      const NodePair P = a.ix.npair[gw & kGatherNode];
+      d.s_pos = P.ent_off;
+      d.s_src = P.ent_mask;
+    }
     a.desc[g] = d;
     if (SPANS) {
       a.spans[g] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
@@ -574,13 +579,14 @@ __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
 // is resolved: when the hit lists do not fit in LDS the pair analysis runs twice, counting,
 // then resolving). A reservation past a.pcap writes nothing; the host reads *pcount, grows the
 // pool and runs the batch's k_merge again.
-template <bool SPANS>
-__global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
+// WPE: minimum waves per SIMD asked of the register allocator (1 = no constraint; the kernel is
+// latency-bound, so occupancy can pay for a few spills). MQ_OPT_MERGE_WAVES picks the variant.
+template <bool SPANS, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
   __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records
   __shared__ uint32_t map_val[4][kMapSlots];   // its gather index (= DFS rank order)
   __shared__ uint32_t mg_node[4][kPairMax];    // the topic's merge gathers, in gather order:
   __shared__ uint32_t mg_gi[4][kPairMax];      //   node, gather index,
-  __shared__ uint32_t mg_moff[4][kPairMax];    //   subs pool offset of its may-merge slots,
   __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first may-merge slot,
   __shared__ uint32_t mg_eoff[4][kPairMax];    //   its pair-block hash table (NodePair)
   __shared__ uint32_t mg_emask[4][kPairMax];
@@ -627,16 +633,18 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
     for (uint32_t i0 = 0; i0 < n_g; i0 += 64) {
       const uint32_t i = i0 + lane;
       bool ins = false;
-      uint32_t node = 0, moff = 0, mrow = 0;
+      uint32_t node = 0, mrow = 0;
       NodePair P{0, kNone, 0, 0};
       if (i < n_g) {
         const GDesc d = gd[i];
         node = d.word & kGatherNode;
         ins = (d.mdir & kDescMerge) != 0;
         const uint32_t nd = d.mdir & ~kDescMerge;
-        moff = d.r_src + nd;
         mrow = d.r_pos + nd;
-        if (ins) P = a.ix.npair[node];
+        if (ins) {
+          if (SPANS) P = NodePair{d.s_pos, d.s_src, 0, 0};  // folded in by k_desc<true>
+          else P = a.ix.npair[node];
+        }
       }
       const uint64_t bi = __ballot(ins);
       const uint32_t x = n_map + prefix_before(bi);
@@ -646,7 +654,6 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
         map_val[wv][sl] = i;
         mg_node[wv][x] = node;
         mg_gi[wv][x] = i;
-        mg_moff[wv][x] = moff;
         mg_row[wv][x] = mrow;
         mg_eoff[wv][x] = P.ent_off;
         mg_emask[wv][x] = P.ent_mask;
@@ -680,16 +687,17 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
     // through several hit lists; only the visit through its first gathered partner (`via`, or
     // any when via == kNone) counts it, and only that visit leaves a patch (the row format
     // writes the same row on every visit). Called by all lanes (wave-uniform).
-    auto resolve = [&](bool active, uint32_t pos, uint32_t row, uint32_t gi, uint32_t via,
+    // mw: the record's meta | kSlotIdentPos when its identifier is > 0 (PairSlot.meta).
+    auto resolve = [&](bool active, uint32_t mw, uint32_t row, uint32_t gi, uint32_t via,
                        uint32_t mp_off, uint32_t mp_cnt) {
       bool counted = false, nonbase = false, want = false;
       uint32_t pmeta = 0;
-      int32_t ident = 0;
       if (active) {
-        const SubRec rec = a.ix.subs[pos];
+        const uint32_t rmeta = mw & ~kSlotIdentPos;
+        const bool idpos = (mw & kSlotIdentPos) != 0;
         bool bound = false, base = true;
         uint32_t first = kNone;
-        uint32_t q = rec.meta & kMetaQos, nl = rec.meta & kMetaNoLocal;
+        uint32_t q = rmeta & kMetaQos, nl = rmeta & kMetaNoLocal;
         // partner links in batches of kPartBatch independent loads (one latency per batch)
         for (uint32_t e0 = 0; e0 < mp_cnt && base; e0 += kPartBatch) {
           MergePart pb[kPartBatch];
@@ -714,19 +722,17 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
         if (bound) {
           counted = via == kNone || via == first;
           nonbase = !base;
-          ident = rec.ident;
-          pmeta = base ? (rec.meta & ~(kMetaQos | kMetaNoLocal)) | q | nl
-                       : rec.meta | (rec.ident > 0 ? kRowIdent : kRowDrop);
+          pmeta = base ? (rmeta & ~(kMetaQos | kMetaNoLocal)) | q | nl : rmeta | (idpos ? kRowIdent : kRowDrop);
           if (SPANS) {
-            want = counted && pmeta != rec.meta;
-          } else if (pmeta != rec.meta) {
+            want = counted && pmeta != rmeta;
+          } else if (pmeta != rmeta) {
             crow[row].meta = pmeta;
           }
         }
       }
       if (SPANS) emit_patch(want, row, pmeta);
       const uint64_t bn = __ballot(counted && nonbase);
-      const uint64_t bx = __ballot(counted && nonbase && ident > 0);
+      const uint64_t bx = __ballot(counted && nonbase && (pmeta & kRowIdent));
       n_nonbase += __popcll(bn);
       n_ext += __popcll(bx);
     };
@@ -750,8 +756,7 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
           const uint32_t jj = lo;
           const uint32_t xa = h_ga[wv][jj];
           const PairSlot e = a.ix.plist[h_off[wv][jj] + (rc - h_pre[wv][jj])];
-          resolve(r < tot, mg_moff[wv][xa] + e.k, mg_row[wv][xa] + e.k, mg_gi[wv][xa], h_via[wv][jj],
-                  e.mp_off, e.mp_cnt);
+          resolve(r < tot, e.meta, mg_row[wv][xa] + e.k, mg_gi[wv][xa], h_via[wv][jj], e.mp_off, e.mp_cnt);
         }
         n_hit = 0;
         tot = 0;
@@ -851,7 +856,9 @@ __global__ __launch_bounds__(256) void k_merge(EmitArgs a) {
           const bool act = c0 + lane < L.n_merge;
           const uint32_t pos = L.sub_off + L.n_direct + min(c0 + lane, L.n_merge - 1);
           const MergeRef mr = a.ix.mref[pos];
-          resolve(act, pos, d.r_pos + L.n_direct + c0 + lane, i, kNone, mr.off, mr.cnt);
+          const SubRec rec = a.ix.subs[pos];
+          resolve(act, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u), d.r_pos + L.n_direct + c0 + lane, i, kNone,
+                  mr.off, mr.cnt);
         }
       }
     }
@@ -949,14 +956,19 @@ void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
   hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, a);
 }
 
-void launch_merge(const EmitArgs& a, bool spans, uint32_t max_blocks, hipStream_t s) {
+void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_blocks, hipStream_t s) {
   const uint32_t waves = a.t1 - a.t0;
   if (!waves) return;
   const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
-  if (spans)
-    hipLaunchKernelGGL(k_merge<true>, dim3(blocks), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(k_merge<false>, dim3(blocks), dim3(256), 0, s, a);
+  if (spans) {
+    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, 8>), dim3(blocks), dim3(256), 0, s, a);
+    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, 6>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, 1>), dim3(blocks), dim3(256), 0, s, a);
+  } else {
+    if (wpe >= 8) hipLaunchKernelGGL((k_merge<false, 8>), dim3(blocks), dim3(256), 0, s, a);
+    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<false, 6>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_merge<false, 1>), dim3(blocks), dim3(256), 0, s, a);
+  }
 }
 
 

@@ -184,8 +184,10 @@ struct PairSlot {  // 16 B: one slot on a pair list, with its partner links
   uint32_t k;       // may-merge slot of g, relative to g's may-merge slots
   uint32_t mp_off;  // its MergePart records
   uint32_t mp_cnt;
-  uint32_t pad;
+  uint32_t meta;    // the slot's SubRec meta | kSlotIdentPos (its identifier is > 0): resolving
+                    // the slot needs no load of the record itself
 };
+constexpr uint32_t kSlotIdentPos = 0x1000u;  // the reserved meta bit (include/mqmatch.h)
 
 MQ_HD uint32_t pair_hash(uint32_t x) {
   x ^= x >> 16;

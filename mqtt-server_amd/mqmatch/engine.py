@@ -67,7 +67,8 @@ class SpanResult(C.Structure):
 SPANS_PICKED = 1  # MQ_SPANS_PICKED
 
 # mq_set_option (include/mqmatch.h MQ_OPT_*)
-OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP = 1, 2, 3, 4, 5, 6
+OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP, OPT_MERGE_WAVES = \
+    1, 2, 3, 4, 5, 6, 7
 
 
 class MsgResult(C.Structure):
