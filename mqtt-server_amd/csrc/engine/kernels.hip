@@ -391,6 +391,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+// Index of the calling wavefront in its workgroup, as a wave-uniform (scalar) value: the
+// compiler cannot prove threadIdx.x >> 6 uniform, and per-wave work indexed by it would
+// otherwise run as vector code under exec masks.
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -552,7 +557,7 @@ __device__ __forceinline__ void copy_tile(const EmitArgs& a, const V* __restrict
 __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t n_all = a.n_tiles[0] + a.n_tiles[1] + a.n_tiles[2];
-  for (uint32_t w0 = blockIdx.x * 4 + (threadIdx.x >> 6); w0 < n_all; w0 += gridDim.x * 4) {
+  for (uint32_t w0 = blockIdx.x * 4 + wave_id(); w0 < n_all; w0 += gridDim.x * 4) {
     uint32_t w = w0;
     const uint32_t j = a.tiles[w];
     if (w < a.n_tiles[0]) {
@@ -594,7 +599,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ uint32_t h_off[4][kHitMax];       //   pair-list offset,
   __shared__ uint32_t h_via[4][kHitMax];       //   partner node h,
   __shared__ uint32_t h_pre[4][kHitMax + 1];   //   exclusive prefix of their lengths (+ total)
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t wv = wave_id(), lane = threadIdx.x & 63;
   // persistent: a.merge grid's waves stride over the chunk's topics (wave-uniform loop)
   for (uint32_t t = a.t0 + blockIdx.x * 4 + wv; t < a.t1; t += gridDim.x * 4) {
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
@@ -1000,7 +1005,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                              uint32_t* __restrict__ count_out,
                                              uint64_t* __restrict__ spec, uint32_t spec_cap) {
   __shared__ uint32_t cursor[4];  // FILL / speculative count: next free slot of the filter
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63, wv = wave_id();
   const uint32_t t = blockIdx.x * 4 + wv;
   if (t >= n) return;  // wave-uniform
   // FILL after a speculative count: only the filters k_msg_place could not place are walked
@@ -1473,7 +1478,7 @@ __global__ __launch_bounds__(256) void k_msg_place(uint32_t n, const TopicCount*
                                                    uint64_t* __restrict__ base_out,
                                                    uint32_t* __restrict__ count_out) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t t = blockIdx.x * 4 + wave_id();
   if (t >= n) return;
   const TopicCount c = cnt[t];
   if (c.gathers != 0) return;  // walked again by the FILL pass
