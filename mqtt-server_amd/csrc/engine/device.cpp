@@ -224,7 +224,7 @@ Device::~Device() {
   mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
                     &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &acl_buf_, &sp_res_,
-                    &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_})
+                    &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_, &sp_compact_, &sp_roff_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
@@ -627,7 +627,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       a.sres = nullptr;
       a.patches = nullptr;
       a.pcount = nullptr;
-      a.pcap = 0;
+      a.rcap = 0;
       if (ci >= 2) hip_check(hipStreamWaitEvent(s, merge_done_[b], 0), "hipStreamWaitEvent");
       prof.begin(s);
       launch_copy(a, copy_blocks_, s);
@@ -790,10 +790,11 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
   grow(sp_res_, (size_t)n * sizeof(TopicSpansDev));
   if (select_shared_) grow(sp_picked_, std::max<uint64_t>(tot.shr, 1) * sizeof(ShrRec));
-  if (!sp_pcount_.p) sp_pcount_.ensure(sizeof(unsigned long long));
-  if (patch_cap_ < patch_cap_init_) {
-    grow(sp_patches_, patch_cap_init_ * sizeof(PatchRec));
-    patch_cap_ = patch_cap_init_;
+  if (!sp_pcount_.p) sp_pcount_.ensure(kPatchRegions * sizeof(unsigned long long));
+  if (rcap_ * kPatchRegions < patch_cap_init_) {
+    rcap_ = std::max<uint64_t>((patch_cap_init_ + kPatchRegions - 1) / kPatchRegions, 16);
+    sp_patches_.release();
+    sp_patches_.ensure(rcap_ * kPatchRegions * sizeof(PatchRec));
   }
 
   DescArgs da;
@@ -824,27 +825,35 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   a.inl_rows = sp_inl_.as<InlRec>();
   a.sres = sp_res_.as<TopicSpansDev>();
   a.pcount = sp_pcount_.as<unsigned long long>();
-  pinned(sizeof(unsigned long long) + 2 * sizeof(uint32_t));
-  unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);
-  uint32_t* h_err = reinterpret_cast<uint32_t*>(h_pc + 1);
+  pinned((2 * kPatchRegions + 1) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
+  unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
+  uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
+  uint32_t* h_err = reinterpret_cast<uint32_t*>(h_roff + kPatchRegions + 1);
+  uint64_t n_patches = 0, max_region = 0;
   for (int attempt = 0;; attempt++) {
     a.patches = sp_patches_.as<PatchRec>();
-    a.pcap = patch_cap_;
-    hip_check(hipMemsetAsync(a.pcount, 0, sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
+    a.rcap = rcap_;
+    hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
     prof.begin(s);
     launch_merge(a, true, merge_wpe_, merge_blocks_, s);
     prof.end("merge", s);
     hip_check(hipGetLastError(), "k_merge<spans>");
-    hip_check(hipMemcpyAsync(h_pc, a.pcount, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H pcount");
+    hip_check(hipMemcpyAsync(h_pc, a.pcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
+              "D2H pcount");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    if (*h_pc <= patch_cap_) break;
+    n_patches = max_region = 0;
+    for (uint32_t r = 0; r < kPatchRegions; r++) {
+      h_roff[r] = n_patches;
+      n_patches += h_pc[r];
+      max_region = std::max<uint64_t>(max_region, h_pc[r]);
+    }
+    h_roff[kPatchRegions] = n_patches;
+    if (max_region <= rcap_) break;
     if (attempt) throw HipError{hipErrorUnknown, "k_merge<spans>: patch reservations changed between runs"};
-    const uint64_t want = *h_pc + *h_pc / 4 + 1024;  // every patch range of this batch, with slack
+    rcap_ = max_region + max_region / 4 + 64;  // every region of this batch, with slack
     sp_patches_.release();
-    sp_patches_.ensure(want * sizeof(PatchRec));
-    patch_cap_ = want;
+    sp_patches_.ensure(rcap_ * kPatchRegions * sizeof(PatchRec));
   }
-  const uint64_t n_patches = *h_pc;
   if (select_shared_) {  // SelectShared on the device: picked members at each topic's picked_base
     PickArgs pa;
     pa.res = nullptr;
@@ -870,7 +879,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   out->inline_rows = reinterpret_cast<const mq_inline_row*>(sp_inl_.p);
   out->picked_rows = select_shared_ ? reinterpret_cast<const mq_shared_row*>(sp_picked_.p) : nullptr;
   out->n_spans = tot.g;
-  out->n_patches = n_patches;
+  out->n_patches = rcap_ * kPatchRegions;  // the pool's extent: topic ranges sit in regions
   out->n_inline_rows = tot.inl;
   out->n_picked_rows = select_shared_ ? tot.shr : 0;
   if (host) {
@@ -882,9 +891,16 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     hip_check(hipMemcpyAsync(host->topics.data(), a.sres, n * sizeof(TopicSpansDev), hipMemcpyDeviceToHost, s), "D2H");
     if (tot.g)
       hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, s), "D2H");
-    if (n_patches)
-      hip_check(hipMemcpyAsync(host->patches.data(), sp_patches_.p, n_patches * sizeof(PatchRec),
+    if (n_patches) {  // the regions' used parts, packed; patch_base is remapped below
+      grow(sp_compact_, n_patches * sizeof(PatchRec));
+      grow(sp_roff_, kPatchRegions * sizeof(uint64_t));
+      hip_check(hipMemcpyAsync(sp_roff_.p, h_roff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D");
+      launch_patch_compact(sp_patches_.as<PatchRec>(), rcap_, a.pcount, sp_roff_.as<uint64_t>(),
+                           sp_compact_.as<PatchRec>(), s);
+      hip_check(hipGetLastError(), "k_patch_compact");
+      hip_check(hipMemcpyAsync(host->patches.data(), sp_compact_.p, n_patches * sizeof(PatchRec),
                                hipMemcpyDeviceToHost, s), "D2H");
+    }
     if (tot.inl)
       hip_check(hipMemcpyAsync(host->inl.data(), sp_inl_.p, tot.inl * sizeof(InlRec), hipMemcpyDeviceToHost, s), "D2H");
     if (out->n_picked_rows)
@@ -894,6 +910,9 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   if (*h_err) check_err(s);  // throws with the tripped guard's name
+  if (host)
+    for (TopicSpansDev& t : host->topics)
+      if (t.n_patches) t.patch_base = h_roff[t.patch_base / rcap_] + t.patch_base % rcap_;
 }
 
 void Device::acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb, const uint64_t* to,

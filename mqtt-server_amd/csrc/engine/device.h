@@ -228,7 +228,8 @@ class Device {
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_;
   // span format outputs
   DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;
-  uint64_t patch_cap_ = 0;           // patches sp_patches_ holds
+  DevBuf sp_compact_, sp_roff_;      // host results: the patch regions packed
+  uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
   uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter
   uint64_t msg_spec_bytes_ = 0;  // its budget (MQ_MSG_SPEC_MB)

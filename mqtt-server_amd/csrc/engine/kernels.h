@@ -25,6 +25,7 @@ constexpr uint32_t kMapSlots = 128;    // per-wave LDS map (gathered merge node 
 constexpr uint32_t kPairMax = 64;     // merge gathers covered by the pair analysis
 constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
 constexpr uint32_t kPartBatch = 8;     // partner links loaded together per record
+constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 constexpr uint32_t kMergeWavesPerEU = 1;  // k_merge register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.
@@ -117,9 +118,9 @@ struct EmitArgs {
   mq_topic_result_dev* res; // indexed t - t0 (row format)
   // span format
   TopicSpansDev* sres;            // indexed t
-  PatchRec* patches;              // patch pool; topics reserve ranges with atomicAdd on *pcount
-  unsigned long long* pcount;     // patches reserved (may exceed pcap: the host then grows the pool)
-  uint64_t pcap;
+  PatchRec* patches;              // patch pool: kPatchRegions regions of rcap patches; topic t
+  unsigned long long* pcount;     //   reserves in region t % kPatchRegions with atomicAdd on
+  uint64_t rcap;                  //   pcount[region] (may exceed rcap: the host grows the pool)
 };
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile
@@ -190,6 +191,10 @@ void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_bloc
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
                 uint32_t* count, uint64_t* spec, uint32_t spec_cap, uint32_t wpe, hipStream_t s);
+// Pack the used prefix of every patch region (pcount[r] patches of region r) into `out` at
+// roff[r] (span format, host results).
+void launch_patch_compact(const PatchRec* pool, uint64_t rcap, const unsigned long long* pcount,
+                          const uint64_t* roff, PatchRec* out, hipStream_t s);
 void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
                       uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
 

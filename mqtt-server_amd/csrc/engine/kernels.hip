@@ -579,11 +579,12 @@ __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
 
 // SPANS=false: the records were copied to the chunk's rows by k_copy and are rewritten in
 // place. SPANS=true: nothing was copied; each record whose row changes leaves a PatchRec (its
-// topic-relative row, the new meta) in a range the topic reserves with one atomicAdd on
-// a.pcount, sized by the records its hit lists hold (the reservation is made before any record
-// is resolved: when the hit lists do not fit in LDS the pair analysis runs twice, counting,
-// then resolving). A reservation past a.pcap writes nothing; the host reads *pcount, grows the
-// pool and runs the batch's k_merge again.
+// topic-relative row, the new meta) in a range the topic reserves with one atomicAdd on its
+// region's counter (a.pcount[t % kPatchRegions]: one shared counter serialised a million
+// same-address atomics per batch), sized by the records its hit lists hold (the reservation is
+// made before any record is resolved: when the hit lists do not fit in LDS the pair analysis
+// runs twice, counting, then resolving). A reservation past the region's a.rcap writes
+// nothing; the host reads the counters, grows the pool and runs the batch's k_merge again.
 // WPE: minimum waves per SIMD asked of the register allocator (1 = no constraint; the kernel is
 // latency-bound, so occupancy can pay for a few spills). MQ_OPT_MERGE_WAVES picks the variant.
 template <bool SPANS, int WPE>
@@ -614,12 +615,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t n_patch = 0;
   bool pfit = true;      // the reservation fits the pool
 
-  // reserve n patch slots for this topic (wave-uniform)
+  // reserve n patch slots for this topic in its region (wave-uniform)
   auto reserve = [&](uint64_t n) {
+    const uint32_t region = t & (kPatchRegions - 1);
     unsigned long long b = 0;
-    if (lane == 0 && n) b = atomicAdd(a.pcount, (unsigned long long)n);
-    pbase = __shfl((unsigned long long)b, 0, 64);
-    pfit = pbase + n <= a.pcap;
+    if (lane == 0 && n) b = atomicAdd(a.pcount + region, (unsigned long long)n);
+    b = __shfl((unsigned long long)b, 0, 64);
+    pfit = b + n <= a.rcap;
+    pbase = (uint64_t)region * a.rcap + b;
   };
   // one patch per lane that wants one, compacted by ballot (wave-uniform)
   auto emit_patch = [&](bool want, uint32_t row, uint32_t meta) {
@@ -1440,6 +1443,21 @@ void launch_pick(const PickArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_pick<true>, dim3(a.n), dim3(64), 0, s, a);
   else
     hipLaunchKernelGGL(k_pick<false>, dim3(a.n), dim3(64), 0, s, a);
+}
+
+__global__ __launch_bounds__(256) void k_patch_compact(const PatchRec* __restrict__ pool, uint64_t rcap,
+                                                      const unsigned long long* __restrict__ pcount,
+                                                      const uint64_t* __restrict__ roff, PatchRec* __restrict__ out) {
+  const uint32_t r = blockIdx.x;
+  const uint64_t n = pcount[r];
+  const PatchRec* src = pool + (uint64_t)r * rcap;
+  PatchRec* dst = out + roff[r];
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+void launch_patch_compact(const PatchRec* pool, uint64_t rcap, const unsigned long long* pcount,
+                          const uint64_t* roff, PatchRec* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_patch_compact, dim3(kPatchRegions), dim3(256), 0, s, pool, rcap, pcount, roff, out);
 }
 
 template <int WPE>
