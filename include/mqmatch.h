@@ -264,7 +264,10 @@ typedef struct mq_span_result {
   const mq_shared_row* picked_rows;
   const mq_client_row* sub_pool;    /* the index's subscription records */
   const mq_shared_row* shared_pool; /* the index's shared members */
-  uint64_t n_spans, n_patches, n_inline_rows, n_picked_rows;
+  uint64_t n_spans;
+  uint64_t n_patches; /* host result: patches, packed; device result: the patch pool's extent
+                         (topic ranges lie in per-region parts of it, with unused gaps) */
+  uint64_t n_inline_rows, n_picked_rows;
   uint64_t sub_pool_len, shared_pool_len;
 } mq_span_result;
 

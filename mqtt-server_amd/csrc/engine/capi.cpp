@@ -243,6 +243,7 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
     r.patches = reinterpret_cast<const mq_patch*>(h->data.patches.data());
     r.inline_rows = reinterpret_cast<const mq_inline_row*>(h->data.inl.data());
     r.picked_rows = reinterpret_cast<const mq_shared_row*>(h->data.picked.data());
+    r.n_patches = h->data.patches.size();  // packed (the device pool has per-region gaps)
     r.sub_pool = reinterpret_cast<const mq_client_row*>(idx->ix->subs.m.h.data());
     r.shared_pool = reinterpret_cast<const mq_shared_row*>(idx->ix->shr.m.h.data());
     r.sub_pool_len = idx->ix->subs.m.size();

@@ -1,7 +1,7 @@
 # Round 2: patch regions (one counter per region) — GPU suite, k_merge variants, PMC pass.
 # PMC pass of instruction counters on the 1M span-format run.
 set -o pipefail
-D=gpurun_out/r2_tune3
+D=gpurun_out/r2_tune4
 mkdir -p $D
 export TMPDIR=/tmp
 rocprofv3 -L > $D/counters.txt 2>&1 || true
