@@ -58,11 +58,28 @@ def _device_view(ptr, nbytes):
 
 
 def host_cores():
+    """Host threads for the CPU baseline: every core this process may use (the GOMAXPROCS
+    analogue), capped by OMP_NUM_THREADS where the machine sets a per-job share (the GPU box
+    allots 16 host threads per GPU and sets it to 16)."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(n, 16))  # the GPU box allots 16 host cores per GPU
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    if cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def read_traffic(path, n_subs, write_bytes_per_launch):
@@ -77,6 +94,53 @@ def read_traffic(path, n_subs, write_bytes_per_launch):
         return float(e["hbm_bytes_per_copy_launch"])
     except (OSError, ValueError, KeyError, TypeError):
         return None
+
+
+def spans_roofline(prof, work, steps, n):
+    """Roofline of the span format's dominant kernel, k_merge. Its algorithmic bytes per launch
+     are what it must read and write for the launch's topics: 40 B of offsets and a
+    64 B result record per topic, the 32 B GDesc of every gather, 16 B per pair-table entry
+    probed, 16 B per pair slot resolved, 8 B per partner link, 8 B per patch — priced from the
+    work counters of an extra step (the same batch, so the same work) — over the launch's mean
+    time from HIP events in the timed region. Latency-bound (dependent probes of hash tables and
+    lists), so the HBM fraction is low by nature; the step's other kernels are walk and desc."""
+    launches, ms = prof.get("merge", (0, 0.0))
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+            "traffic": None, "kernel": "k_merge<spans>",
+            "bytes": "offsets + result + GDesc + pair entries + pair slots + partner links + patches"}
+    if not launches or ms <= 0:
+        return roof
+    g = lambda k: work.get(k, (0, 0.0))[0]
+    per_launch = (104 * n + 32 * g("gathers") + 16 * g("merge_pair_entries") + 16 * g("merge_records")
+                  + 8 * g("merge_links") + 8 * g("patches"))
+    launch_ms = ms / launches
+    achieved = per_launch / (launch_ms * 1e-3) / 1e9
+    roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, launch_ms=launch_ms, bytes_per_launch=per_launch)
+    return roof
+
+
+def rows_roofline(prof, args, elapsed, out):
+    """Roofline of the row format's dominant kernel, k_copy. It moves every gathered list into
+    output rows: per launch it writes copy_bytes (16 B per client row, 8 B per shared / inline
+    row), all of which must reach HBM (the rows of one step are far larger than every cache).
+    Its reads are the hot subscription lists, re-read by many topics and served from L2 / the
+    Infinity Cache, so the HBM-compulsory bytes of a launch are its writes (DESIGN.md §5);
+    `traffic` is the PMC-measured HBM bytes per launch (profiles/pmc_traffic.json) when present."""
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+            "traffic": None, "kernel": "k_copy", "bytes": "output rows written per launch"}
+    copy_launches, copy_ms = prof.get("copy", (0, 0.0))
+    copy_bytes = prof.get("copy_bytes", (0, 0.0))[0]
+    if copy_ms > 0 and copy_launches:
+        launch_ms = copy_ms / copy_launches
+        per_launch = copy_bytes / copy_launches
+        achieved = per_launch / (launch_ms * 1e-3) / 1e9
+        roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS,
+                    traffic=read_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), args.subs, per_launch))
+        out["copy_avg_launch_ms"] = launch_ms
+        out["copy_bytes_per_launch"] = per_launch
+        # the whole step against the same roofline: all output bytes / step time
+        out["step_output_GBps"] = copy_bytes / max(1, args.steps) / (elapsed / args.steps) / 1e9
+    return roof
 
 
 def main():
@@ -202,27 +266,18 @@ def main():
         "chunks_per_step": chunks,
     }
 
-    # Roofline of the dominant kernel, k_copy. It moves every gathered list into output rows:
-    # per launch it writes copy_bytes (16 B per client row, 8 B per shared / inline row), all of
-    # which must reach HBM (the rows of one step are far larger than every cache). Its reads are
-    # the hot subscription lists, re-read by many topics and served from L2 / the Infinity Cache,
-    # so the HBM-compulsory bytes of a launch are its writes; `traffic` is the
-    # PMC-measured HBM bytes per launch (profiles/pmc_traffic.json) when present.
-    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-            "traffic": None, "kernel": "k_copy", "bytes": "output rows written per launch"}
-    copy_launches, copy_ms = prof.get("copy", (0, 0.0))
-    copy_bytes = prof.get("copy_bytes", (0, 0.0))[0]
-    if copy_ms > 0 and copy_launches:
-        launch_ms = copy_ms / copy_launches
-        per_launch = copy_bytes / copy_launches
-        achieved = per_launch / (launch_ms * 1e-3) / 1e9
-        roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS,
-                    traffic=read_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), args.subs, per_launch))
-        out["copy_avg_launch_ms"] = launch_ms
-        out["copy_bytes_per_launch"] = per_launch
-        # the whole step against the same roofline: all output bytes / step time
-        out["step_output_GBps"] = copy_bytes / max(1, args.steps) / (elapsed / args.steps) / 1e9
-
+    if args.format == "spans":
+        # One extra, untimed step with k_merge's work counters (MQ_PROF_WORK costs atomics).
+        eng.profile(True, work=True)
+        eng.profile_reset()
+        step()
+        torch.cuda.synchronize()
+        work = eng.profile_read()
+        eng.profile(False)
+        out["roofline"] = spans_roofline(prof, work, args.steps, n)
+        out["merge_work_per_topic"] = {k[6:]: work[k][0] / n for k in work if k.startswith("merge_") and k != "merge_topics"}
+    else:
+        out["roofline"] = rows_roofline(prof, args, elapsed, out)
     cpu = None
     if not args.no_cpu and world == 1:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -234,15 +289,31 @@ def main():
         orc.subscribe_bulk(w)
         log(f"oracle index built in {time.time()-t0:.1f}s")
         cores = host_cores()
-        # calibrate, then time a sample of about --cpu-seconds of CPU work
+        # The baseline is the fast restatement (oracle/topics_fast.h: the Go trie's algorithm with
+        # client ids interned at build time and flat per-thread result tables; digest-equal to the
+        # oracle): calibrate, then time a sample of about --cpu-seconds of CPU work.
+        t0 = time.time()
+        fast = orc.fast()
+        log(f"fast CPU restatement built in {time.time()-t0:.1f}s")
         cal = min(n, 256 * cores)
-        secs, _ = orc.bench_subscribers(tb, to[:cal + 1], cores)
+        secs, _ = fast.bench_subscribers(tb, to[:cal + 1], cores)
         m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
-        secs, _ = orc.bench_subscribers(tb, to[:m + 1], cores)
+        secs, _ = fast.bench_subscribers(tb, to[:m + 1], cores)
         cpu = {"value": m / secs, "unit": "publishes/s", "cores": cores, "kind": "port",
-               "sample": f"first {m} topics of the rank-0 batch on the same {args.subs}-subscription "
-                         f"index, {cores} threads, Subscribers() per topic (C++ restatement of the "
-                         f"Go particle trie, oracle/)"}
+               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+               "sample": f"first {m} topics of the rank-0 batch on the same {args.subs}-subscription index, "
+                         f"{cores} threads (std::thread, shared frozen index), Subscribers() per topic: the "
+                         f"fast CPU restatement of the Go particle trie (oracle/topics_fast.cpp: interned "
+                         f"client ids, flat per-thread result tables; digest-equal to the oracle)"}
+        # the literal restatement (per-call ordered result maps, as the oracle checks with)
+        lit_cal = min(n, 16 * cores)
+        lsecs, _ = orc.bench_subscribers(tb, to[:lit_cal + 1], cores)
+        lm = int(min(n, max(lit_cal, lit_cal * min(5.0, args.cpu_seconds / 3) / max(lsecs, 1e-6))))
+        lsecs, _ = orc.bench_subscribers(tb, to[:lm + 1], cores)
+        out["cpu_baseline_literal"] = {"value": lm / lsecs, "unit": "publishes/s", "cores": cores,
+                                       "sample": f"first {lm} topics; oracle/topics_oracle.cpp (ordered "
+                                                 f"std::map results, string keys, map copy per gather)"}
+        del fast
         # oracle counters (B = 8L + 4 + 16P + 16S + 16O per topic) + parity on a sample
         ns = min(m, 4096)
         dg_o, cnt_o, tot = orc.digest_batch(tb, to[:ns + 1], cores)
@@ -254,18 +325,32 @@ def main():
         b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"] + 16 * per_topic["S"] + 16 * per_topic["O"]
         out["alg_bytes_per_topic"] = {"B": b_topic, "L": per_topic["L"], "P": per_topic["P"],
                                       "S": per_topic["S"], "O": per_topic["O"], "sample_topics": ns}
-        # End-to-end through the host-buffer boundary (mq_match_batch: H2D of the topics, the
-        # kernels, D2H of every result row into host memory) on a bounded sample: PCIe-bound,
-        # reported beside `value`, never as it.
-        ne = min(n, 20000)
-        eng.match_batch_rows(tb, to[:ne + 1])
-        t0 = time.perf_counter()
-        rows = eng.match_batch_rows(tb, to[:ne + 1])
-        dt = time.perf_counter() - t0
-        out["end_to_end"] = {"value": ne / dt, "unit": "publishes/s", "sample_topics": ne,
-                             "result_bytes": 16 * rows[0] + 8 * rows[1] + 8 * rows[2],
-                             "GBps_to_host": (16 * rows[0] + 8 * rows[1] + 8 * rows[2]) / dt / 1e9}
-    out["roofline"] = roof
+        # End-to-end through the host-buffer boundary on a bounded sample (H2D of the topics, the
+        # kernels, D2H of the results into host memory), reported beside `value`, never as it
+        # (DESIGN.md §5). Span format: mq_match_spans, and separately with every row expanded
+        # on the host (mq_spans_expand, one thread); row format: mq_match_batch (PCIe-bound).
+        if args.format == "spans":
+            ne = min(n, 200000)
+            eng.match_spans_host(tb, to[:ne + 1])
+            t0 = time.perf_counter()
+            nbytes, _ = eng.match_spans_host(tb, to[:ne + 1])
+            dt = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            _, nrows = eng.match_spans_host(tb, to[:ne + 1], expand=True)
+            dtx = time.perf_counter() - t0
+            out["end_to_end"] = {"value": ne / dt, "unit": "publishes/s", "sample_topics": ne,
+                                 "result_bytes": nbytes, "GBps_to_host": nbytes / dt / 1e9,
+                                 "expanded": {"value": ne / dtx, "rows": nrows, "host_threads": 1,
+                                              "rows_GBps": 16 * nrows / dtx / 1e9}}
+        else:
+            ne = min(n, 20000)
+            eng.match_batch_rows(tb, to[:ne + 1])
+            t0 = time.perf_counter()
+            rows = eng.match_batch_rows(tb, to[:ne + 1])
+            dt = time.perf_counter() - t0
+            out["end_to_end"] = {"value": ne / dt, "unit": "publishes/s", "sample_topics": ne,
+                                 "result_bytes": 16 * rows[0] + 8 * rows[1] + 8 * rows[2],
+                                 "GBps_to_host": (16 * rows[0] + 8 * rows[1] + 8 * rows[2]) / dt / 1e9}
     out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)
     D.finalize(backend)

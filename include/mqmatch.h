@@ -359,7 +359,13 @@ int mq_index_check(mq_index* idx);
 #define MQ_OPT_MERGE_WAVES 7     /* k_merge waves per SIMD the registers are budgeted for (1, 6, 8) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
-/* Kernel timing by HIP events recorded on the launch stream around each kernel. */
+/* Kernel timing by HIP events recorded on the launch stream around each kernel. enable: 0 off,
+ * MQ_PROF_TIMES kernel times, MQ_PROF_WORK also the span format's k_merge work counters
+ * (pair-table loads, resolved records, partner links; entries "merge_*" with launches = count
+ * and total_ms = 0), from which bench.py prices k_merge's algorithmic bytes. The counters cost
+ * atomics: enable them for a measurement pass, not in a timed one. */
+#define MQ_PROF_TIMES 1
+#define MQ_PROF_WORK 2
 typedef struct mq_kernel_time {
   char name[32];
   uint64_t launches;

@@ -33,14 +33,14 @@ struct mq_index {
   mq_config cfg;
   std::unique_ptr<Index> ix;
   std::unique_ptr<Device> dev;
-  bool profile = false;
+  int profile = 0;  // MQ_PROF_*
 
   std::vector<std::pair<uint32_t, uint64_t>> options;  // mq_set_option, in call order
 
   Device& device() {
     if (!dev) {
       dev.reset(new Device(cfg.device));
-      dev->prof.enable(profile);
+      dev->prof.enable(profile != 0, (profile & MQ_PROF_WORK) != 0);
       dev->set_select_shared((cfg.flags & MQ_CFG_SELECT_SHARED) != 0);
       for (auto& o : options) dev->set_option(o.first, o.second);
     }
@@ -485,8 +485,8 @@ int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
 
 int mq_profile_enable(mq_index* idx, int enable) {
   return guarded(idx, [&] {
-    idx->profile = enable != 0;
-    if (idx->dev) idx->dev->prof.enable(idx->profile);
+    idx->profile = enable;
+    if (idx->dev) idx->dev->prof.enable(enable != 0, (enable & MQ_PROF_WORK) != 0);
     return 0;
   });
 }

@@ -628,6 +628,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       a.patches = nullptr;
       a.pcount = nullptr;
       a.rcap = 0;
+      a.work = nullptr;
       if (ci >= 2) hip_check(hipStreamWaitEvent(s, merge_done_[b], 0), "hipStreamWaitEvent");
       prof.begin(s);
       launch_copy(a, copy_blocks_, s);
@@ -825,6 +826,11 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   a.inl_rows = sp_inl_.as<InlRec>();
   a.sres = sp_res_.as<TopicSpansDev>();
   a.pcount = sp_pcount_.as<unsigned long long>();
+  a.work = nullptr;
+  if (prof.work()) {
+    grow(sp_work_, kPatchRegions * kWork * sizeof(unsigned long long));
+    a.work = sp_work_.as<unsigned long long>();
+  }
   pinned((2 * kPatchRegions + 1) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
   unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
@@ -834,6 +840,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     a.patches = sp_patches_.as<PatchRec>();
     a.rcap = rcap_;
     hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
+    if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
     prof.begin(s);
     launch_merge(a, true, merge_wpe_, merge_blocks_, s);
     prof.end("merge", s);
@@ -872,6 +879,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     hip_check(hipGetLastError(), "k_pick<spans>");
   }
   prof.count("patches", n_patches);
+  prof.count("spans", tot.g);
   out->n_topics = n;
   out->topics = reinterpret_cast<const mq_topic_spans*>(a.sres);
   out->spans = reinterpret_cast<const mq_span*>(sp_spans_.p);
@@ -882,6 +890,18 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   out->n_patches = rcap_ * kPatchRegions;  // the pool's extent: topic ranges sit in regions
   out->n_inline_rows = tot.inl;
   out->n_picked_rows = select_shared_ ? tot.shr : 0;
+  if (a.work) {  // MQ_PROF_WORK: k_merge's work, for its algorithmic bytes (bench.py)
+    std::vector<unsigned long long> w(kPatchRegions * kWork);
+    hip_check(hipMemcpyAsync(w.data(), a.work, w.size() * sizeof(w[0]), hipMemcpyDeviceToHost, s), "D2H work");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    uint64_t sum[kWork] = {0, 0, 0, 0};
+    for (uint32_t r = 0; r < kPatchRegions; r++)
+      for (uint32_t k = 0; k < kWork; k++) sum[k] += w[r * kWork + k];
+    prof.count("merge_pair_entries", sum[0]);
+    prof.count("merge_records", sum[1]);
+    prof.count("merge_links", sum[2]);
+    prof.count("merge_topics", n);
+  }
   if (host) {
     host->topics.resize(n);
     host->spans.resize(tot.g);

@@ -100,8 +100,12 @@ struct HostMatch {
 
 class Profiler {
  public:
-  void enable(bool on) { on_ = on; }
+  void enable(bool on, bool work = false) {
+    on_ = on;
+    work_ = on && work;
+  }
   bool on() const { return on_; }
+  bool work() const { return work_; }  // MQ_PROF_WORK: kernel work counters
   void begin(hipStream_t s);
   void end(const char* name, hipStream_t s);
   int read(mq_kernel_time* out, uint32_t cap);
@@ -120,7 +124,7 @@ class Profiler {
     double ms = 0;
   };
   void drain();
-  bool on_ = false;
+  bool on_ = false, work_ = false;
   hipEvent_t cur_ = nullptr;
   std::vector<Pending> pending_;
   std::vector<hipEvent_t> free_;
@@ -229,6 +233,7 @@ class Device {
   // span format outputs
   DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;
   DevBuf sp_compact_, sp_roff_;      // host results: the patch regions packed
+  DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
   uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter

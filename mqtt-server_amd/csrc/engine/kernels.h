@@ -26,6 +26,9 @@ constexpr uint32_t kPairMax = 64;     // merge gathers covered by the pair analy
 constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
 constexpr uint32_t kPartBatch = 8;     // partner links loaded together per record
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
+// k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
+// resolved (pair slots read), partner links loaded
+constexpr uint32_t kWork = 4;
 constexpr uint32_t kMergeWavesPerEU = 1;  // k_merge register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.
@@ -121,6 +124,7 @@ struct EmitArgs {
   PatchRec* patches;              // patch pool: kPatchRegions regions of rcap patches; topic t
   unsigned long long* pcount;     //   reserves in region t % kPatchRegions with atomicAdd on
   uint64_t rcap;                  //   pcount[region] (may exceed rcap: the host grows the pool)
+  unsigned long long* work;       // MQ_PROF_WORK: per region kWork counters (null: off)
 };
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile

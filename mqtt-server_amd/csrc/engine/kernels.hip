@@ -614,6 +614,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint64_t pbase = 0;    // span format: the topic's patch range [pbase, pbase + reserved)
   uint32_t n_patch = 0;
   bool pfit = true;      // the reservation fits the pool
+  uint32_t w_ent = 0, w_rec = 0, w_link = 0;  // this lane's work (MQ_PROF_WORK)
 
   // reserve n patch slots for this topic in its region (wave-uniform)
   auto reserve = [&](uint64_t n) {
@@ -712,6 +713,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (uint32_t u = 0; u < kPartBatch; u++)
             pb[u] = e0 + u < mp_cnt ? a.ix.mpart[mp_off + e0 + u] : MergePart{kNone, 0};
+          w_link += min(kPartBatch, mp_cnt - e0);
 #pragma unroll
           for (uint32_t u = 0; u < kPartBatch; u++) {
             if (!base || pb[u].node == kNone) continue;
@@ -764,6 +766,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const uint32_t jj = lo;
           const uint32_t xa = h_ga[wv][jj];
           const PairSlot e = a.ix.plist[h_off[wv][jj] + (rc - h_pre[wv][jj])];
+          w_rec += r < tot;
           resolve(r < tot, e.meta, mg_row[wv][xa] + e.k, mg_gi[wv][xa], h_via[wv][jj], e.mp_off, e.mp_cnt);
         }
         n_hit = 0;
@@ -794,6 +797,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                   PairEnt pe[4];
 #pragma unroll
                   for (uint32_t u = 0; u < 4; u++) pe[u] = a.ix.pent[ent_off + ((sl + u) & ent_mask)];
+                  w_ent += 4;
                   bool stop = false;
 #pragma unroll
                   for (uint32_t u = 0; u < 4; u++) {
@@ -865,6 +869,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const uint32_t pos = L.sub_off + L.n_direct + min(c0 + lane, L.n_merge - 1);
           const MergeRef mr = a.ix.mref[pos];
           const SubRec rec = a.ix.subs[pos];
+          w_rec += act;
           resolve(act, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u), d.r_pos + L.n_direct + c0 + lane, i, kNone,
                   mr.off, mr.cnt);
         }
@@ -891,6 +896,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       kept += __popcll(bk);
     }
     n_inl = kept;
+  }
+
+  if (SPANS && a.work) {  // MQ_PROF_WORK: one set of atomics per topic, spread over the regions
+    const uint32_t e = wave_sum(w_ent), rr = wave_sum(w_rec), l = wave_sum(w_link);
+    unsigned long long* wc = a.work + (uint64_t)(t & (kPatchRegions - 1)) * kWork;
+    if (lane == 0 && (e | rr | l)) {
+      atomicAdd(wc + 0, (unsigned long long)e);
+      atomicAdd(wc + 1, (unsigned long long)rr);
+      atomicAdd(wc + 2, (unsigned long long)l);
+    }
   }
 
   if (lane == 0) {

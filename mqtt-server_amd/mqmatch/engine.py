@@ -65,6 +65,7 @@ class SpanResult(C.Structure):
 
 
 SPANS_PICKED = 1  # MQ_SPANS_PICKED
+PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 
 # mq_set_option (include/mqmatch.h MQ_OPT_*)
 OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP, OPT_MERGE_WAVES = \
@@ -394,6 +395,37 @@ class Engine:
             "n_patches": int(t["n_patches"].sum()), "n_spans": int(t["n_spans"].sum()),
         }
 
+    def match_spans_host(self, bytes_, offs, expand=False, block=1024):
+        """mq_match_spans with its results left in the library's host buffers (the end-to-end
+        path: H2D topics, kernels, D2H of the span-format arrays). expand=True also materialises
+        every topic's rows with mq_spans_expand, `block` topics per call into one reused buffer
+        (what a consumer that wants rows pays). Returns (result bytes, rows expanded)."""
+        n = len(offs) - 1
+        rp = C.POINTER(SpanResult)()
+        _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
+        try:
+            r = rp.contents
+            nbytes = 64 * n + 16 * r.n_spans + 8 * r.n_patches + 8 * r.n_inline_rows + 8 * r.n_picked_rows
+            done = 0
+            if expand and n:
+                buf = (C.c_char * (n * 64)).from_address(r.topics)
+                top = np.frombuffer(buf, _TOPIC_SPANS_DT)
+                csum = np.concatenate(([0], np.cumsum(top["n_rows"].astype(np.uint64))))
+                ssum = np.concatenate(([0], np.cumsum(top["n_shared"].astype(np.uint64))))
+                starts = list(range(0, n, block))
+                cap_r = max(int(max(csum[min(b + block, n)] - csum[b] for b in starts)), 1)
+                cap_s = max(int(max(ssum[min(b + block, n)] - ssum[b] for b in starts)), 1)
+                rows = np.empty((cap_r, 4), np.uint32)
+                shared = np.empty((cap_s, 2), np.uint32)
+                nr, ns = C.c_uint64(), C.c_uint64()
+                for b in starts:
+                    _check(lib().mq_spans_expand(rp, b, min(block, n - b), rows.ctypes.data, cap_r, shared.ctypes.data,
+                                                 cap_s, C.byref(nr), C.byref(ns)), "mq_spans_expand")
+                    done += int(nr.value)
+        finally:
+            lib().mq_result_free(rp)
+        return int(nbytes), done
+
     def match_spans_device(self, d_bytes, d_offs, n, stream=None):
         """mq_match_spans_device on device pointers (ints); returns the SpanResult struct."""
         r = SpanResult()
@@ -532,8 +564,10 @@ class Engine:
             out.append((els, bool(matched[i])))
         return out
 
-    def profile(self, enable=True):
-        _check(lib().mq_profile_enable(self.h, 1 if enable else 0), "mq_profile_enable")
+    def profile(self, enable=True, work=False):
+        """mq_profile_enable: kernel times (HIP events); work=True adds k_merge's work counters."""
+        mode = (PROF_TIMES | (PROF_WORK if work else 0)) if enable else 0
+        _check(lib().mq_profile_enable(self.h, mode), "mq_profile_enable")
 
     def profile_read(self):
         arr = (KernelTime * 32)()

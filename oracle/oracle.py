@@ -70,6 +70,12 @@ def lib():
     L.orc_path_exists.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int]
     L.orc_node_counts.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int, _i64p]
     L.orc_node_counts.restype = C.c_int64
+    L.orc_fast_build.argtypes = [C.c_void_p]
+    L.orc_fast_build.restype = C.c_void_p
+    L.orc_fast_free.argtypes = [C.c_void_p]
+    L.orc_fast_digest_batch.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint32, _u64p, _u32p]
+    L.orc_fast_bench.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint32, _u64p]
+    L.orc_fast_bench.restype = C.c_double
     L.orc_root_children.argtypes = [C.c_void_p]
     L.orc_root_children.restype = C.c_uint64
     _LIB = L
@@ -250,9 +256,47 @@ class OracleIndex:
                                            nthreads, C.byref(sink))
         return float(secs), int(sink.value)
 
+    def fast(self):
+        """FastIndex snapshot of this index (topics_fast.h): the CPU baseline's restatement."""
+        return FastIndex(self)
+
     def bench_messages(self, bytes_, offs, nthreads):
         n = len(offs) - 1
         sink = C.c_uint64()
         secs = lib().orc_bench_messages(self.h, _ptr(bytes_, _u8p), _ptr(offs, _u64p), n,
                                         nthreads, C.byref(sink))
+        return float(secs), int(sink.value)
+
+
+class FastIndex:
+    """The fast CPU restatement (oracle/topics_fast.h) over a frozen OracleIndex: flat result
+    tables per thread, interned client ids. bench.py's cpu_baseline; digest-checked against the
+    oracle in tests/test_oracle_kat.py."""
+
+    def __init__(self, orc):
+        self.h = lib().orc_fast_build(orc.h)
+
+    def close(self):
+        if self.h:
+            lib().orc_fast_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def digest_batch(self, bytes_, offs, nthreads=8):
+        n = len(offs) - 1
+        dig = np.zeros(n, np.uint64)
+        cnt = np.zeros(n * 4, np.uint32)
+        lib().orc_fast_digest_batch(self.h, _ptr(bytes_, _u8p), _ptr(offs, _u64p), n, nthreads,
+                                    _ptr(dig, _u64p), _ptr(cnt, _u32p))
+        return dig, cnt.reshape(n, 4)
+
+    def bench_subscribers(self, bytes_, offs, nthreads):
+        n = len(offs) - 1
+        sink = C.c_uint64()
+        secs = lib().orc_fast_bench(self.h, _ptr(bytes_, _u8p), _ptr(offs, _u64p), n, nthreads, C.byref(sink))
         return float(secs), int(sink.value)

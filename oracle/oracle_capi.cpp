@@ -8,10 +8,12 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "topics_fast.h"
 #include "topics_oracle.h"
 
 using namespace oracle;
@@ -351,6 +353,60 @@ double orc_bench_messages(void* hp, const uint8_t* bytes, const uint64_t* offs, 
       uint64_t local = 0;
       for (uint64_t i = t; i < n; i += nthreads)
         local += h->idx.messages(std::string((const char*)bytes + offs[i], offs[i + 1] - offs[i])).size();
+      acc += local;
+    });
+  }
+  for (auto& x : th) x.join();
+  auto t1 = std::chrono::steady_clock::now();
+  if (sink) *sink = acc.load();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// ---- the fast CPU restatement (topics_fast.h): bench.py's cpu_baseline, checked against the
+// oracle's digests in the tests ----
+void* orc_fast_build(void* hp) {
+  Handle* h = (Handle*)hp;
+  return fast_build(h->idx, h->client_ids, h->filter_ids);
+}
+void orc_fast_free(void* fp) { fast_free((FastIndex*)fp); }
+
+int orc_fast_digest_batch(void* fp, const uint8_t* bytes, const uint64_t* offs, uint64_t n, uint32_t nthreads,
+                          uint64_t* digests, uint32_t* row_counts) {
+  const FastIndex& f = *(FastIndex*)fp;
+  if (nthreads == 0) nthreads = 1;
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nthreads; t++) {
+    th.emplace_back([&, t] {
+      std::unique_ptr<FastScratch, void (*)(FastScratch*)> s(fast_scratch(f), fast_scratch_free);
+      for (uint64_t i = t; i < n; i += nthreads) {
+        uint64_t cnt[4];
+        fast_subscribers(f, *s, (const char*)bytes + offs[i], (uint32_t)(offs[i + 1] - offs[i]), &digests[i], cnt);
+        if (row_counts)
+          for (int k = 0; k < 4; k++) row_counts[i * 4 + k] = (uint32_t)cnt[k];
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  return 0;
+}
+
+// CPU baseline: `nthreads` std::threads each run Subscribers(topic) on the shared frozen index
+// (topics.go:583 takes no writer lock). Scratch tables are set up before the clock starts.
+double orc_fast_bench(void* fp, const uint8_t* bytes, const uint64_t* offs, uint64_t n, uint32_t nthreads,
+                      uint64_t* sink) {
+  const FastIndex& f = *(FastIndex*)fp;
+  if (nthreads == 0) nthreads = 1;
+  std::vector<std::unique_ptr<FastScratch, void (*)(FastScratch*)>> sc;
+  for (uint32_t t = 0; t < nthreads; t++) sc.emplace_back(fast_scratch(f), fast_scratch_free);
+  std::atomic<uint64_t> acc{0};
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nthreads; t++) {
+    th.emplace_back([&, t] {
+      uint64_t local = 0;
+      for (uint64_t i = t; i < n; i += nthreads)
+        local += fast_subscribers(f, *sc[t], (const char*)bytes + offs[i], (uint32_t)(offs[i + 1] - offs[i]), nullptr,
+                                  nullptr);
       acc += local;
     });
   }

@@ -124,3 +124,30 @@ def test_match_topic():  # hooks/auth/ledger_test.go:461-493 (auth.MatchTopic, S
              ("things/stuff//", "things/stuff/", [], False), ("t", "t2", [], False), (" ", "  ", [], False)]
     for f, t, el, m in cases:
         assert O.match_topic(f, t) == (el, m), (f, t)
+
+
+def test_fast_baseline_matches_oracle():
+    """The CPU baseline's fast restatement (oracle/topics_fast.h) gives the oracle's digests on a
+    workload batch, including '$' topics, shared and inline subscriptions."""
+    import random
+    import numpy as np
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(30000, 3000, seed=91)
+    orc = O.OracleIndex()
+    orc.subscribe_bulk(w)
+    r = random.Random(92)
+    for i in range(200):  # inline subscriptions with repeated ids (last write wins)
+        f = "/".join(r.choice(["a", "+", "#", "b"]) for _ in range(r.randint(1, 3)))
+        orc.inline_subscribe(f, r.randint(1, 20))
+    tb, to = W.gen_topics(w, 4000, seed=93)
+    extra = ["a", "a/b", "b/a/x", "$SYS/a", "", "a/+"]
+    topics = W.strings(tb, to) + extra
+    raw = [t.encode("utf-8", "surrogateescape") for t in topics]
+    offs = np.zeros(len(raw) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in raw])
+    b = np.frombuffer(b"".join(raw) + b"\0" * 16, np.uint8).copy()
+    od, ocnt, _ = orc.digest_batch(b, offs, nthreads=4)
+    fd, fcnt = orc.fast().digest_batch(b, offs, nthreads=4)
+    assert (fcnt == ocnt).all()
+    assert (fd == od).all(), np.nonzero(fd != od)[0][:5]
+    assert ocnt[:, 0].sum() > len(topics) and ocnt[:, 3].sum() > 0
