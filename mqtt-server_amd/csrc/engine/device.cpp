@@ -212,7 +212,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_MSG_WAVES: msg_wpe_opt_ = (uint32_t)v; return true;
     case MQ_OPT_SERIAL: serial_ = v != 0; return true;
     case MQ_OPT_PATCH_CAP: patch_cap_init_ = std::max<uint64_t>(v, 64); return true;
-    case MQ_OPT_MERGE_WAVES: merge_wpe_ = (uint32_t)v; return true;
+    case MQ_OPT_MERGE_WAVES: merge_wpe_opt_ = (uint32_t)v; return true;
     default: return false;
   }
 }
@@ -639,7 +639,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
       }
       prof.begin(ms);
-      launch_merge(a, false, merge_wpe_, merge_blocks_, ms);
+      launch_merge(a, false, merge_wpe_opt_ ? merge_wpe_opt_ : 1u, merge_blocks_, ms);
       prof.end("merge", ms);
       hip_check(hipGetLastError(), "k_merge");
       const uint32_t nt = a.t1 - a.t0;
@@ -836,13 +836,17 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
   uint32_t* h_err = reinterpret_cast<uint32_t*>(h_roff + kPatchRegions + 1);
   uint64_t n_patches = 0, max_region = 0;
+  // k_merge register budget: on a large index the merge waits on memory more often and 6 waves
+  // per SIMD beat the unconstrained 5 (10M subscriptions: 7.7 -> 5.7 ms per 1M topics); on a
+  // small one the spills cost more (1M: 1.8 vs 2.4 ms). MQ_OPT_MERGE_WAVES overrides.
+  const uint32_t merge_wpe = merge_wpe_opt_ ? merge_wpe_opt_ : (ix.subs.live >= kMergeWpeMinSubs ? kMergeWavesPerEU : 1u);
   for (int attempt = 0;; attempt++) {
     a.patches = sp_patches_.as<PatchRec>();
     a.rcap = rcap_;
     hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
     if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
     prof.begin(s);
-    launch_merge(a, true, merge_wpe_, merge_blocks_, s);
+    launch_merge(a, true, merge_wpe, merge_blocks_, s);
     prof.end("merge", s);
     hip_check(hipGetLastError(), "k_merge<spans>");
     hip_check(hipMemcpyAsync(h_pc, a.pcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),

@@ -239,7 +239,7 @@ class Device {
   DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter
   uint64_t msg_spec_bytes_ = 0;  // its budget (MQ_MSG_SPEC_MB)
   uint32_t msg_wpe_opt_ = 0;     // k_msg variant (MQ_OPT_MSG_WAVES; 0: by index size)
-  uint32_t merge_wpe_ = kMergeWavesPerEU;  // k_merge variant (MQ_OPT_MERGE_WAVES)
+  uint32_t merge_wpe_opt_ = 0;   // k_merge variant (MQ_OPT_MERGE_WAVES; 0: by index size)
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
   uint32_t n_cus_ = 1;
   bool serial_ = false;       // MQ_OPT_SERIAL: k_merge on the launch stream (isolated kernel times)

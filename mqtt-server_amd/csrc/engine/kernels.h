@@ -29,7 +29,8 @@ constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (on
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded
 constexpr uint32_t kWork = 4;
-constexpr uint32_t kMergeWavesPerEU = 1;  // k_merge register budget: 1 (none), 6 or 8 waves per SIMD
+constexpr uint32_t kMergeWavesPerEU = 6;  // k_merge register budget: 1 (none), 6 or 8 waves per SIMD
+constexpr uint64_t kMergeWpeMinSubs = 4000000;  // ... used from this many subscriptions on
 
 // Device pointers of the resident index image.
 struct DevIndex {

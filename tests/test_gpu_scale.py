@@ -1,0 +1,63 @@
+"""Parity at the benchmark's own scale: the headline configuration
+(10M subscriptions, config-3 mix, SURVEY.md §8d generator) and the IoT fan-in mix at 5M
+subscriptions, through the C-ABI in both result formats, digest-equal to the oracle on a
+4096-topic (IoT: 20000-topic) sample of the bench's own batch. Besides the sample, every topic
+of a 1M-topic batch is checked for size-independent properties of the span format (counts add
+up, patches in range, no patches where no client has two matches)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from digest import engine_digests
+
+pytestmark = pytest.mark.gpu
+
+
+def _parity(eng, orc, tb, to, fmts=("spans", "rows")):
+    od, ocnt, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+    for fmt in fmts:
+        res = eng.match_batch_spans(tb, to) if fmt == "spans" else eng.match_batch(tb, to)
+        dg, cnt = engine_digests(res)
+        bad = np.nonzero(dg != od)[0]
+        assert len(bad) == 0, f"{fmt}: {len(bad)} of {len(dg)} topics differ, first {bad[:5]}"
+        assert (cnt == ocnt).all()
+    return ocnt
+
+
+def test_headline_10m_subscriptions(gpu_available):
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(10_000_000, 1_000_000, seed=W.BASE_SEED)  # bench.py's index
+    eng = E.Engine(expected_subs=10_000_000)
+    new = eng.subscribe_bulk(w)
+    orc = O.OracleIndex()
+    assert (orc.subscribe_bulk(w) == new).all()
+    tb, to = W.gen_topics(w, 1_000_000, seed=W.BASE_SEED)  # bench.py's rank-0 batch
+    cnt = _parity(eng, orc, tb, to[:4097])
+    assert cnt[:, 0].mean() > 1000  # the workload really fans out
+    del orc
+    # every topic of the full batch: span-format invariants, independent of the oracle
+    a = eng.match_spans(tb, to)
+    t = a["topics"]
+    assert (t["n_client"] + (t["n_rows"] - t["n_client"]) == t["n_rows"]).all()
+    assert (t["n_ident"] <= t["n_rows"] - t["n_client"]).all()
+    assert int(t["n_spans"].sum()) == len(a["spans"]) and int(t["n_patches"].sum()) == len(a["patches"])
+    sp = a["spans"]
+    rows_per_topic = np.add.reduceat(sp[:, 1].astype(np.int64), t["span_base"].astype(np.int64))
+    assert (rows_per_topic == t["n_rows"]).all()
+    no_merge = t["n_client"] == t["n_rows"]
+    assert (t["n_patches"][no_merge] <= t["n_rows"][no_merge]).all()
+
+
+def test_iot_5m_subscriptions(gpu_available):
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(5_000_000, 5_000_000, seed=W.BASE_SEED, mix=W.MIX_IOT)
+    eng = E.Engine(expected_subs=5_000_000)
+    new = eng.subscribe_bulk(w)
+    orc = O.OracleIndex()
+    assert (orc.subscribe_bulk(w) == new).all()
+    tb, to = W.gen_topics(w, 20000, seed=W.BASE_SEED, mix=W.MIX_IOT)
+    _parity(eng, orc, tb, to)
