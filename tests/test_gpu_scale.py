@@ -41,14 +41,18 @@ def test_headline_10m_subscriptions(gpu_available):
     # every topic of the full batch: span-format invariants, independent of the oracle
     a = eng.match_spans(tb, to)
     t = a["topics"]
-    assert (t["n_client"] + (t["n_rows"] - t["n_client"]) == t["n_rows"]).all()
-    assert (t["n_ident"] <= t["n_rows"] - t["n_client"]).all()
+    assert (t["n_client"] <= t["n_rows"]).all() and (t["n_ident"] <= t["n_rows"] - t["n_client"]).all()
     assert int(t["n_spans"].sum()) == len(a["spans"]) and int(t["n_patches"].sum()) == len(a["patches"])
-    sp = a["spans"]
-    rows_per_topic = np.add.reduceat(sp[:, 1].astype(np.int64), t["span_base"].astype(np.int64))
-    assert (rows_per_topic == t["n_rows"]).all()
+    sb, ns = t["span_base"].astype(np.int64), t["n_spans"].astype(np.int64)
+    cs = np.concatenate(([0], np.cumsum(a["spans"][:, 1].astype(np.int64))))
+    assert (cs[sb + ns] - cs[sb] == t["n_rows"]).all()  # spans cover exactly the gathered records
+    cs = np.concatenate(([0], np.cumsum(a["spans"][:, 3].astype(np.int64))))
+    assert (cs[sb + ns] - cs[sb] == t["n_shared"]).all()
+    # a patch changes a row; a topic whose records all belong to distinct clients needs none but
+    # merge-base Qos/NoLocal rewrites, which exist only where n_client < n_rows
     no_merge = t["n_client"] == t["n_rows"]
-    assert (t["n_patches"][no_merge] <= t["n_rows"][no_merge]).all()
+    assert (t["n_patches"][no_merge] == 0).all()
+    assert int((t["n_rows"] - t["n_client"]).sum()) <= int(t["n_patches"].sum())
 
 
 def test_iot_5m_subscriptions(gpu_available):
