@@ -112,7 +112,7 @@ def spans_roofline(prof, work, steps, n):
         return roof
     g = lambda k: work.get(k, (0, 0.0))[0]
     per_launch = (104 * n + 32 * g("gathers") + 16 * g("merge_pair_entries") + 16 * g("merge_records")
-                  + 8 * g("merge_links") + 8 * g("patches"))
+                  + 8 * g("merge_links") + 8 * g("merge_patches"))
     launch_ms = ms / launches
     achieved = per_launch / (launch_ms * 1e-3) / 1e9
     roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, launch_ms=launch_ms, bytes_per_launch=per_launch)

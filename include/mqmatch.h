@@ -66,6 +66,19 @@ typedef struct mq_config {
   uint32_t flags;          /* MQ_CFG_* */
   uint64_t expected_subs;  /* capacity hint (0 = default) */
   uint64_t expected_nodes; /* capacity hint (0 = default) */
+  /* Sharded index: this handle holds shard shard_index of
+   * shard_count (<= 16; 0 or 1: not sharded). Subscriptions are owned by a hash of the filter
+   * (shared: of the group and path), inline subscriptions by identifier, retained messages by
+   * topic. Every update must be issued to every shard's handle: each applies what it owns and
+   * records the others' subscriptions of its clients as cross-shard merge partners. Return
+   * values are the shard's part of the reference's: the owner answers Subscribe /
+   * InlineSubscribe / RetainMessage (the others return 0; sum or OR them), Unsubscribe /
+   * InlineUnsubscribe return whether the particle exists on this shard (OR them, Q10). Filter
+   * ids must be < 2^31. A batch runs as mq_match_spans_begin on every shard, an exchange of the
+   * exported lists, and mq_match_spans_end; the topic's Subscribers are the union of the
+   * shards' results (disjoint: each shard emits its own subscriptions, merged exactly). */
+  uint32_t shard_index;
+  uint32_t shard_count;
 } mq_config;
 
 /* ---- lifecycle: NewTopicsIndex (topics.go:356-364) ---- */
@@ -293,6 +306,41 @@ int mq_spans_expand(const mq_span_result* r, uint32_t first, uint32_t count, mq_
                     uint64_t rows_cap, mq_shared_row* shared, uint64_t shared_cap, uint64_t* n_rows,
                     uint64_t* n_shared);
 
+/* ---- sharded batches (mq_config.shard_count > 1) ----
+ * A topic's client merge (Subscription.Merge over the client's matches, in DFS order) can span
+ * shards. mq_match_spans_begin walks the batch and exports, per topic, this shard's gathered
+ * particles that hold a subscription whose client has a co-matchable filter on another shard:
+ * the filter id and its DFS rank key (two bits per level, 32 levels).
+ * The caller gathers every other shard's export (e.g. an all-gather over RCCL) and passes them
+ * to mq_match_spans_end, which resolves this shard's records exactly against them. A cross-shard
+ * tie beyond the key's 32 levels fails the batch loudly (MQ_EIO). */
+typedef struct mq_xent {
+  uint32_t filter_id;
+  uint32_t deep; /* deeper than the rank key's 32 levels */
+  uint64_t rank;
+} mq_xent;
+
+typedef struct mq_xlist {
+  uint32_t n_topics;
+  uint32_t shard;
+  const uint32_t* counts; /* n_topics: entries per topic (DEVICE memory) */
+  const mq_xent* ents;    /* the topics' entries in topic order (DEVICE memory) */
+  uint64_t n_ents;
+} mq_xlist;
+
+/* Begin a span-format batch (inputs in HBM as mq_match_spans_device). *exported holds device
+ * pointers owned by the index, valid until mq_match_spans_end; an index that is not sharded
+ * exports nothing (n_ents = 0, null pointers). No update may run until the batch ends. */
+int mq_match_spans_begin(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t* d_offsets, uint32_t n,
+                         void* hip_stream, mq_xlist* exported);
+/* End it with the other shards' exports (n_foreign <= 15 lists in device memory readable by
+ * this index's device; 0 for an index that is not sharded): results as mq_match_spans_device. */
+int mq_match_spans_end(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, void* hip_stream,
+                       mq_span_result* out);
+/* The same with the results copied to host memory (as mq_match_spans: the result pins the
+ * host image until mq_result_free). */
+int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, mq_span_result** out);
+
 /* ---- batched reverse retained scan: TopicsIndex.Messages (topics.go:525-579) ---- */
 typedef struct mq_msg_result {
   uint32_t n_filters;
@@ -339,6 +387,7 @@ typedef struct mq_stats {
   uint64_t retained, retained_live;
   uint64_t device_bytes, upload_bytes_total, syncs;
   uint64_t partners; /* partner links between may-merge subscriptions */
+  uint64_t foreign;  /* sharded: other shards' subscriptions recorded as merge partners */
   uint32_t max_depth, reserved;
 } mq_stats;
 int mq_index_stats(const mq_index* idx, mq_stats* out);

@@ -111,8 +111,13 @@ int mq_index_create(const mq_config* cfg, mq_index** out) {
   if (!out) return fail(MQ_EINVAL, "null out");
   try {
     mq_index* idx = new mq_index();
-    idx->cfg = cfg ? *cfg : mq_config{0, 0, 0, 0};
+    idx->cfg = cfg ? *cfg : mq_config{0, 0, 0, 0, 0, 0};
+    if (idx->cfg.shard_count > kMaxShards || (idx->cfg.shard_count > 1 && idx->cfg.shard_index >= idx->cfg.shard_count)) {
+      delete idx;
+      return fail(MQ_EINVAL, "bad shard_index / shard_count");
+    }
     idx->ix.reset(new Index(idx->cfg.expected_subs, idx->cfg.expected_nodes));
+    if (idx->cfg.shard_count > 1) idx->ix->set_shard(idx->cfg.shard_index, idx->cfg.shard_count);
     *out = idx;
     return 0;
   } catch (const std::bad_alloc&) {
@@ -226,6 +231,33 @@ int mq_match_batch(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
   });
 }
 
+namespace {
+// A host span result: the device arrays copied into h->data, the pools pointing at the host
+// image, which the result pins (views) until mq_result_free. Under the handle lock.
+int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_span_result& dev_out,
+                       mq_span_result** out) {
+  mq_span_result& r = h->pub;
+  r = dev_out;  // counts and flags; pointers replaced by the host copies and host pools
+  r.topics = reinterpret_cast<const mq_topic_spans*>(h->data.topics.data());
+  r.spans = reinterpret_cast<const mq_span*>(h->data.spans.data());
+  r.patches = reinterpret_cast<const mq_patch*>(h->data.patches.data());
+  r.inline_rows = reinterpret_cast<const mq_inline_row*>(h->data.inl.data());
+  r.picked_rows = reinterpret_cast<const mq_shared_row*>(h->data.picked.data());
+  r.n_patches = h->data.patches.size();  // packed (the device pool has per-region gaps)
+  r.sub_pool = reinterpret_cast<const mq_client_row*>(idx->ix->subs.m.h.data());
+  r.shared_pool = reinterpret_cast<const mq_shared_row*>(idx->ix->shr.m.h.data());
+  r.sub_pool_len = idx->ix->subs.m.size();
+  r.shared_pool_len = idx->ix->shr.m.size();
+  h->lk = idx->lk;
+  idx->lk->views++;  // the pools stay put until mq_result_free
+  *out = &h->pub;
+  std::lock_guard<std::mutex> lk(g_res_mu);
+  g_results[&h->pub] = 4;
+  h.release();
+  return 0;
+}
+}  // namespace
+
 int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_span_result** out) {
   if (!out || (n && (!to || (!tb && to[n] != 0)))) return fail(MQ_EINVAL, "null argument");
   return guarded(idx, [&] {
@@ -236,25 +268,17 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
     if (n) d.stage_inputs(tb, to, n, nullptr, &dtb, &dto);
     mq_span_result dev_out;
     d.match_spans(*idx->ix, dtb, dto, n, nullptr, &h->data, &dev_out);
-    mq_span_result& r = h->pub;
-    r = dev_out;  // counts and flags; pointers replaced by the host copies and host pools
-    r.topics = reinterpret_cast<const mq_topic_spans*>(h->data.topics.data());
-    r.spans = reinterpret_cast<const mq_span*>(h->data.spans.data());
-    r.patches = reinterpret_cast<const mq_patch*>(h->data.patches.data());
-    r.inline_rows = reinterpret_cast<const mq_inline_row*>(h->data.inl.data());
-    r.picked_rows = reinterpret_cast<const mq_shared_row*>(h->data.picked.data());
-    r.n_patches = h->data.patches.size();  // packed (the device pool has per-region gaps)
-    r.sub_pool = reinterpret_cast<const mq_client_row*>(idx->ix->subs.m.h.data());
-    r.shared_pool = reinterpret_cast<const mq_shared_row*>(idx->ix->shr.m.h.data());
-    r.sub_pool_len = idx->ix->subs.m.size();
-    r.shared_pool_len = idx->ix->shr.m.size();
-    h->lk = idx->lk;
-    idx->lk->views++;  // under the handle lock: the pools stay put until mq_result_free
-    *out = &h->pub;
-    std::lock_guard<std::mutex> lk(g_res_mu);
-    g_results[&h->pub] = 4;
-    h.release();
-    return 0;
+    return publish_host_spans(idx, std::move(h), dev_out, out);
+  });
+}
+
+int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, mq_span_result** out) {
+  if (!out || (n_foreign && !foreign)) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    std::unique_ptr<SpanHolder> h(new SpanHolder());
+    mq_span_result dev_out;
+    idx->device().spans_end(*idx->ix, foreign, n_foreign, nullptr, &h->data, &dev_out);
+    return publish_host_spans(idx, std::move(h), dev_out, out);
   });
 }
 
@@ -263,6 +287,23 @@ int mq_match_spans_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_
   if (!out || (n && !d_to)) return fail(MQ_EINVAL, "null argument");
   return guarded(idx, [&] {
     idx->device().match_spans(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, nullptr, out);
+    return 0;
+  });
+}
+
+int mq_match_spans_begin(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
+                         mq_xlist* exported) {
+  if (!exported || (n && !d_to)) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    idx->device().spans_begin(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, exported);
+    return 0;
+  });
+}
+
+int mq_match_spans_end(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, void* stream, mq_span_result* out) {
+  if (!out || (n_foreign && !foreign)) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    idx->device().spans_end(*idx->ix, foreign, n_foreign, (hipStream_t)stream, nullptr, out);
     return 0;
   });
 }
@@ -457,6 +498,7 @@ int mq_index_stats(const mq_index* cidx, mq_stats* out) {
     out->retained = x.retained_len();
     out->max_depth = x.max_depth();
     out->partners = x.parts.live;
+    out->foreign = x.foreign_subs();
     if (idx->dev) {
       out->device_bytes = idx->dev->device_bytes();
       out->upload_bytes_total = idx->dev->upload_bytes();

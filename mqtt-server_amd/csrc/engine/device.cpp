@@ -221,10 +221,11 @@ Device::~Device() {
   (void)hipSetDevice(dev_);
   edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
   segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
-  mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release();
+  mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release(); xinfo_.release();
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
                     &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &acl_buf_, &sp_res_,
-                    &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_, &sp_compact_, &sp_roff_})
+                    &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_, &sp_compact_, &sp_roff_,
+                    &sp_work_, &x_off_, &x_ents_, &x_cnt_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
@@ -236,6 +237,7 @@ Device::~Device() {
   if (wstream_) (void)hipStreamDestroy(wstream_);
   if (ev_in_) (void)hipEventDestroy(ev_in_);
   for (hipEvent_t e : ev_scan_) (void)hipEventDestroy(e);
+  for (DevBuf& b : x_foff_) b.release();
   for (int k = 0; k < 2; k++) {
     if (sb_done_[k]) (void)hipEventDestroy(sb_done_[k]);
     desc_[k].release();
@@ -280,6 +282,7 @@ void Device::sync(Index& ix, hipStream_t s) {
   shr_.sync(ix.shr.m, s, &uploaded_);
   inl_.sync(ix.inl.m, s, &uploaded_);
   children_.sync(ix.children.m, s, &uploaded_);
+  if (ix.sharded()) xinfo_.sync(ix.xinfo, s, &uploaded_);
   retained_len_ = ix.retained_len();
   empty_live_ = ix.empty_topic_live;
   empty_handle_ = ix.empty_topic_handle;
@@ -305,6 +308,7 @@ DevIndex Device::dev_index(const Index& ix) const {
   d.shr = shr_.d;
   d.inl = inl_.d;
   d.children = children_.d;
+  d.xinfo = ix.sharded() ? xinfo_.d : nullptr;
   d.retained_len = retained_len_;
   d.empty_topic_handle = empty_handle_;
   d.empty_topic_live = empty_live_ ? 1u : 0u;
@@ -765,27 +769,36 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
 // again); the call ends with the stream synchronised and the guard flags checked.
 void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                          HostSpans* host, mq_span_result* out) {
+  mq_xlist x;
+  spans_begin(ix, d_tb, d_to, n, s, &x);
+  spans_end(ix, nullptr, 0, s, host, out);
+}
+
+void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+                         mq_xlist* x) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   sync(ix, s);
-  memset(out, 0, sizeof(*out));
-  if (host) *host = HostSpans{};
+  memset(x, 0, sizeof(*x));
+  x->n_topics = n;
+  x->shard = ix.shard();
+  sb_ = SpanBatch{};
   if (!err_.p) {
     err_.ensure(2 * sizeof(uint32_t));
     hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
   }
   check_err(s);  // faults flagged by an earlier row-format batch
   const DevIndex di = dev_index(ix);
-  out->sub_pool = reinterpret_cast<const mq_client_row*>(di.subs);
-  out->shared_pool = reinterpret_cast<const mq_shared_row*>(di.shr);
-  out->sub_pool_len = ix.subs.m.size();
-  out->shared_pool_len = ix.shr.m.size();
-  out->flags = select_shared_ ? MQ_SPANS_PICKED : 0u;
+  sb_.pending = true;
+  sb_.n = n;
+  sb_.version = ix.version();
+  sb_.di = di;
   if (n == 0) return;
   ensure_streams();
 
   const uint32_t* gathers = nullptr;
   uint32_t gstride = 0;
   const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride);
+  sb_.tot = tot;
   grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
   grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
   grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
@@ -815,8 +828,64 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   prof.end("desc", s);
   hip_check(hipGetLastError(), "k_desc<spans>");
 
+  if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
+    const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+    grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
+    grow(x_cnt_, (size_t)n * sizeof(uint32_t));
+    prof.begin(s);
+    launch_xlist(true, di, n, offs_.as<TopicOff>(), desc_[0].as<GDesc>(), counts_.as<TopicCount>(), nullptr, nullptr,
+                 nullptr, s);
+    launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
+    TopicOff* h_tot = static_cast<TopicOff*>(h_pin_);
+    hip_check(hipMemcpyAsync(h_tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    const uint64_t n_ents = h_tot->g;
+    grow(x_ents_, std::max<uint64_t>(n_ents, 1) * sizeof(XEnt));
+    launch_xlist(false, di, n, offs_.as<TopicOff>(), desc_[0].as<GDesc>(), nullptr, x_off_.as<TopicOff>(),
+                 x_ents_.as<XEnt>(), x_cnt_.as<uint32_t>(), s);
+    prof.end("xlist", s);
+    hip_check(hipGetLastError(), "k_xlist");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    x->counts = x_cnt_.as<uint32_t>();
+    x->ents = reinterpret_cast<const mq_xent*>(x_ents_.p);
+    x->n_ents = n_ents;
+    prof.count("xents", n_ents);
+  }
+}
+
+void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host,
+                       mq_span_result* out) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  memset(out, 0, sizeof(*out));
+  if (host) *host = HostSpans{};
+  if (!sb_.pending) throw HipError{hipErrorInvalidValue, "spans_end without spans_begin"};
+  sb_.pending = false;
+  if (ix.version() != sb_.version) throw HipError{hipErrorInvalidValue, "index updated between spans_begin and spans_end"};
+  const DevIndex di = sb_.di;
+  const uint32_t n = sb_.n;
+  const TopicOff tot = sb_.tot;
+  out->sub_pool = reinterpret_cast<const mq_client_row*>(di.subs);
+  out->shared_pool = reinterpret_cast<const mq_shared_row*>(di.shr);
+  out->sub_pool_len = ix.subs.m.size();
+  out->shared_pool_len = ix.shr.m.size();
+  out->flags = select_shared_ ? MQ_SPANS_PICKED : 0u;
+  if (nf > kMaxShards - 1) throw HipError{hipErrorInvalidValue, "more foreign lists than kMaxShards - 1"};
+  if (nf && !ix.sharded()) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
+  if (n == 0) return;
+
   EmitArgs a;
   memset(&a, 0, sizeof(a));
+  a.n_xf = nf;
+  for (uint32_t f = 0; f < nf; f++) {  // import: per-topic offsets of each foreign list
+    if (xf[f].n_topics != n || (xf[f].n_ents && (!xf[f].counts || !xf[f].ents)))
+      throw HipError{hipErrorInvalidValue, "foreign list does not match the batch"};
+    grow(x_foff_[f], (size_t)(n + 1) * sizeof(TopicOff));
+    launch_counts(xf[f].counts, n, counts_.as<TopicCount>(), s);
+    launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), x_foff_[f].as<TopicOff>(), s);
+    hip_check(hipGetLastError(), "import");
+    a.xoff[f] = x_foff_[f].as<TopicOff>();
+    a.xent[f] = reinterpret_cast<const XEnt*>(xf[f].ents);
+  }
   a.ix = di;
   a.t0 = 0;
   a.t1 = n;
@@ -882,7 +951,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     prof.end("pick", s);
     hip_check(hipGetLastError(), "k_pick<spans>");
   }
-  prof.count("patches", n_patches);
+  prof.count("patch_slots", n_patches);  // reserved; the written ones: merge_patches (MQ_PROF_WORK)
   prof.count("spans", tot.g);
   out->n_topics = n;
   out->topics = reinterpret_cast<const mq_topic_spans*>(a.sres);
@@ -904,6 +973,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     prof.count("merge_pair_entries", sum[0]);
     prof.count("merge_records", sum[1]);
     prof.count("merge_links", sum[2]);
+    prof.count("merge_patches", sum[3]);
     prof.count("merge_topics", n);
   }
   if (host) {

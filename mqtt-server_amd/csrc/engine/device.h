@@ -150,6 +150,11 @@ class Device {
   // copies every array into it (out's pointers then still name the device arrays).
   void match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                    HostSpans* host, mq_span_result* out);
+  // The same in two phases, for a sharded index: begin walks the batch and
+  // exports the topics' gathered cross-shard nodes (device pointers in *x, valid until end);
+  // the caller exchanges the lists between the shards; end merges with the other shards' lists.
+  void spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x);
+  void spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
                 HostMsg* host, mq_msg_result* out);
@@ -204,6 +209,7 @@ class Device {
   DevMirror<ShrRec> shr_;
   DevMirror<InlRec> inl_;
   DevMirror<ChildRec> children_;
+  DevMirror<XInfo> xinfo_;
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   // Output chunks alternate between two buffer sets so that k_merge of chunk i (side stream)
@@ -234,6 +240,15 @@ class Device {
   DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;
   DevBuf sp_compact_, sp_roff_;      // host results: the patch regions packed
   DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
+  // sharded: the exported list (offsets, entries, counts) and the imported lists' offsets
+  DevBuf x_off_, x_ents_, x_cnt_, x_foff_[kMaxShards - 1];
+  struct SpanBatch {               // between spans_begin and spans_end
+    bool pending = false;
+    uint32_t n = 0;
+    uint64_t version = 0;
+    TopicOff tot{0, 0, 0, 0, 0};
+    DevIndex di{};
+  } sb_;
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
   uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter

@@ -178,6 +178,47 @@ uint32_t StrTable::intern(std::string_view s) {
 
 uint32_t Index::intern_str(std::string_view s) { return strs_.intern(s); }
 
+// ---- sharding ------------------------------------------------------------------
+uint32_t Index::shard_hash(std::string_view key) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (unsigned char c : key) h = (h ^ c) * 0x100000001b3ull;
+  return (uint32_t)(mix64(h ^ key.size()) >> 32);
+}
+
+void Index::set_shard(uint32_t shard, uint32_t n_shards) {
+  shard_ = shard;
+  n_shards_ = n_shards ? n_shards : 1;
+  if (n_shards_ > 1) {
+    xinfo.grow_to(nh_.size(), XInfo{kNone, 0, 0});
+    for (uint32_t n = 1; n < nh_.size(); n++)
+      if (nh_[n].live) set_rank(n, walk.h[n].parent_flags & kParentMask, strs_.at(nh_[n].str));
+  }
+}
+
+// rank key of node n from its parent's (layout.h XInfo)
+void Index::set_rank(uint32_t n, uint32_t parent, std::string_view seg) {
+  const XInfo& P = xinfo.h[parent];
+  XInfo x{kNone, P.deep, P.rank};
+  const uint32_t d = nh_[n].depth;  // 1-based
+  const uint64_t code = seg == "+" ? 2 : (seg == "#" ? 3 : 1);
+  if (d <= 32) x.rank |= code << (64 - 2 * d);
+  else x.deep = 1;
+  xinfo.at_w(n) = x;
+}
+
+// Qos | NoLocal of partner `p` (a node of this shard, or kForeign | fid) of `client`'s slot
+uint32_t Index::partner_meta(uint32_t p, uint32_t client) const {
+  uint32_t i = kNone;
+  if (p & kForeign) {
+    if (!fsub_pos_.get((uint64_t)(p & ~kForeign) << 32 | client, &i))
+      throw std::logic_error("partner_meta: foreign partner missing");
+    return fsubs_[i].meta;
+  }
+  if (!sub_pos_.get((uint64_t)p << 32 | client, &i))  // partners are symmetric
+    throw std::logic_error("flush_merge: partner subscription missing");
+  return subs.m.h[i].meta & (kMetaQos | kMetaNoLocal);
+}
+
 // ---- construction ----------------------------------------------------------------------------
 Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   intern_str("+");
@@ -341,6 +382,10 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   M.flags = (parent == kRoot && seg == "$SYS") ? kChildSys : 0u;
   msg.at_w(id) = M;
 
+  if (sharded()) {
+    xinfo.grow_to(id + 1, XInfo{kNone, 0, 0});
+    set_rank(id, parent, seg);
+  }
   edge_insert(parent, k, id);
   if (h.str == 0) walk.at_w(parent).plus_child = id;
   if (h.str == 1) walk.at_w(parent).hash_child = id;
@@ -395,6 +440,7 @@ void Index::remove_node(uint32_t n) {
   walk.at_w(n) = NodeWalk{kNone, kNone, 0, kNone};
   lists.at_w(n) = NodeLists{};
   msg.at_w(n) = NodeMsg{};
+  if (sharded()) xinfo.at_w(n) = XInfo{kNone, 0, 0};
   h = NodeHost{};
   free_nodes_.push_back(n);
   n_live_nodes_--;
@@ -445,7 +491,7 @@ void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
   sub_pos_.put((uint64_t)n << 32 | r.client, to);
   merge_dirty(n);
   const PartList& p = subp_[to];
-  for (uint32_t i = 0; i < p.cnt; i++) merge_dirty(parts.m.h[p.off + i]);
+  for (uint32_t i = 0; i < p.cnt; i++) touch_partner(parts.m.h[p.off + i]);
 }
 
 void Index::merge_release(uint32_t n) {
@@ -476,8 +522,19 @@ void Index::flush_merge() {
     merge_release(n);
     if (!nh_[n].live) continue;
     const NodeLists& L = lists.h[n];
-    uint32_t links = 0;
-    for (uint32_t k = 0; k < L.n_merge; k++) links += subp_[L.sub_off + L.n_direct + k].cnt;
+    uint32_t links = 0, xs = 0;
+    for (uint32_t k = 0; k < L.n_merge; k++) {
+      const PartList& p = subp_[L.sub_off + L.n_direct + k];
+      links += p.cnt;
+      bool x = false;
+      for (uint32_t i = 0; i < p.cnt && !x; i++) x = (parts.m.h[p.off + i] & kForeign) != 0;
+      xs += x;
+    }
+    if ((xs != 0) != ((L.flags & kFlagXNode) != 0)) {
+      NodeLists& W = lists.at_w(n);
+      W.flags = xs ? (W.flags | kFlagXNode) : (W.flags & ~kFlagXNode);
+    }
+    nh_[n].x_slots = xs;
     if (!links) continue;
     uint32_t cap = 1;
     while (cap < links) cap <<= 1;
@@ -490,10 +547,7 @@ void Index::flush_merge() {
       mref.at_w(pos) = MergeRef{at, p.cnt};
       for (uint32_t i = 0; i < p.cnt; i++) {
         const uint32_t m = parts.m.h[p.off + i];
-        uint32_t mp = kNone;
-        if (!sub_pos_.get((uint64_t)m << 32 | client, &mp))  // partners are symmetric
-          throw std::logic_error("flush_merge: partner subscription missing");
-        mpart.m.at_w(at++) = MergePart{m, subs.m.h[mp].meta & (kMetaQos | kMetaNoLocal)};
+        mpart.m.at_w(at++) = MergePart{m, partner_meta(m, client)};
       }
     }
     nh_[n].mpart_off = off;
@@ -566,8 +620,16 @@ bool Index::check(std::string* why) {
       if (r.cnt != pl.cnt || (uint64_t)r.off + r.cnt > mpart.m.size()) return bad(at + ": partner ref stale");
       for (uint32_t e = 0; e < r.cnt; e++) {
         const MergePart mp = mpart.m.h[r.off + e];
-        if (mp.node != parts.m.h[pl.off + e] || mp.node >= nh_.size() || !nh_[mp.node].live)
-          return bad(at + ": partner node stale");
+        if (mp.node != parts.m.h[pl.off + e]) return bad(at + ": partner link stale");
+        if (mp.node & kForeign) {  // another shard's subscription of the client
+          uint32_t fi = kNone;
+          if (!fsub_pos_.get((uint64_t)(mp.node & ~kForeign) << 32 | client, &fi)) return bad(at + ": foreign partner missing");
+          if (mp.meta != fsubs_[fi].meta) return bad(at + ": foreign partner meta stale");
+          if (!compatible_foreign(n, fsubs_[fi])) return bad(at + ": foreign partner not co-matchable");
+          if (!(L.flags & kFlagXNode)) return bad(at + ": foreign partner but no X flag");
+          continue;
+        }
+        if (mp.node >= nh_.size() || !nh_[mp.node].live) return bad(at + ": partner node stale");
         uint32_t ppos = kNone;
         if (!sub_pos_.get((uint64_t)mp.node << 32 | client, &ppos)) return bad(at + ": partner missing");
         const NodeLists& M = lists.h[mp.node];
@@ -685,7 +747,7 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
   subs.m.at_w(other) = a;
   subp_[other] = ap;
   sub_pos_.put((uint64_t)n << 32 | a.client, other);
-  for (uint32_t i = 0; i < ap.cnt; i++) merge_dirty(parts.m.h[ap.off + i]);
+  for (uint32_t i = 0; i < ap.cnt; i++) touch_partner(parts.m.h[ap.off + i]);
 }
 
 void Index::part_set(uint32_t pos, const std::vector<uint32_t>& nodes) {
@@ -733,6 +795,19 @@ void Index::path_strs(uint32_t n, uint32_t* out, int* len) const {
 // Could one publish topic match both node paths a and b (A.2 rules A/B/C)? A sound
 // over-approximation: '#' matches any suffix (including none), '+' any one level, and a
 // path may be one level longer than the other only through a trailing '#'.
+bool Index::compatible_strs(const uint32_t* pa, int la, const uint32_t* pb, int lb) {
+  const int m = std::min(la, lb);
+  for (int i = 0; i < m; i++) {
+    const uint32_t x = pa[i], y = pb[i];
+    if (x == 1 || y == 1) return true;  // '#'
+    if (x == 0 || y == 0) continue;     // '+'
+    if (x != y) return false;
+  }
+  if (la == lb) return true;
+  const uint32_t* lo = la > lb ? pa : pb;
+  return std::max(la, lb) == m + 1 && lo[m] == 1;
+}
+
 bool Index::compatible(uint32_t a, uint32_t b) const {
   const uint32_t s0 = nh_[a].seg0, s1 = nh_[b].seg0;
   if (s0 > 1 && s1 > 1 && s0 != s1) return false;  // different literal first levels
@@ -742,26 +817,132 @@ bool Index::compatible(uint32_t a, uint32_t b) const {
   int la, lb;
   path_strs(a, pa.data(), &la);
   path_strs(b, pb.data(), &lb);
-  int m = std::min(la, lb);
-  for (int i = 0; i < m; i++) {
-    uint32_t x = pa[i], y = pb[i];
-    if (x == 1 || y == 1) return true;  // '#'
-    if (x == 0 || y == 0) continue;     // '+'
-    if (x != y) return false;
+  return compatible_strs(pa.data(), la, pb.data(), lb);
+}
+
+bool Index::compatible_foreign(uint32_t a, const ForeignSub& f) const {
+  const uint32_t s0 = nh_[a].seg0, s1 = fpaths_[f.path_off];
+  if (s0 > 1 && s1 > 1 && s0 != s1) return false;
+  thread_local std::vector<uint32_t> pa;
+  pa.resize(nh_[a].depth);
+  int la;
+  path_strs(a, pa.data(), &la);
+  return compatible_strs(pa.data(), la, fpaths_.data() + f.path_off, (int)f.depth);
+}
+
+// A non-shared subscription owned by another shard (sharded index): recorded as a foreign
+// partner of this shard's co-matchable subscriptions of the same client.
+int Index::foreign_subscribe(std::string_view filter, uint32_t client, uint32_t fid, uint32_t meta) {
+  if (fid & kForeign) throw std::invalid_argument("sharded index: filter ids must be < 2^31");
+  const uint32_t sid = ffilt_.intern(filter);
+  if (sid >= ffid_.size()) ffid_.resize(sid + 1, kNone);
+  ffid_[sid] = fid;
+  uint32_t i = kNone;
+  const uint64_t key = (uint64_t)fid << 32 | client;
+  auto cn = client_nodes_.find(client);
+  if (fsub_pos_.get(key, &i)) {  // re-Subscribe: the partners' links carry its meta
+    if (fsubs_[i].meta != meta && cn != client_nodes_.end())
+      for (uint32_t m : cn->second) merge_dirty(m);
+    fsubs_[i].meta = meta;
+    return 0;
   }
-  if (la == lb) return true;
-  const std::vector<uint32_t>& lo = la > lb ? pa : pb;
-  int llo = std::max(la, lb);
-  return llo == m + 1 && lo[m] == 1;
+  thread_local std::vector<std::string_view> path;
+  path_of(filter, 0, path);
+  ForeignSub f{client, fid, meta, (uint32_t)fpaths_.size(), (uint32_t)path.size()};
+  for (std::string_view seg : path) fpaths_.push_back(intern_str(seg));
+  if (!fsub_free_.empty()) {
+    i = fsub_free_.back();
+    fsub_free_.pop_back();
+    fsubs_[i] = f;
+  } else {
+    i = (uint32_t)fsubs_.size();
+    fsubs_.push_back(f);
+  }
+  fsub_pos_.put(key, i);
+  client_foreign_[client].push_back(i);
+  if (cn != client_nodes_.end())
+    for (uint32_t m : cn->second) {
+      if (!compatible_foreign(m, f)) continue;
+      uint32_t mp;
+      if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
+      if (!sub_is_merge(m, mp)) {
+        sub_set_merge(m, mp, true);
+        sub_pos_.get((uint64_t)m << 32 | client, &mp);
+      }
+      part_add(mp, kForeign | fid);
+      merge_dirty(m);
+    }
+  return 0;
+}
+
+void Index::foreign_unsubscribe(uint32_t client, uint32_t fid) {
+  uint32_t i = kNone;
+  const uint64_t key = (uint64_t)fid << 32 | client;
+  if (!fsub_pos_.get(key, &i)) return;
+  auto cn = client_nodes_.find(client);
+  if (cn != client_nodes_.end())
+    for (uint32_t m : cn->second) {
+      uint32_t mp;
+      if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
+      const PartList& p = subp_[mp];
+      bool linked = false;
+      for (uint32_t k = 0; k < p.cnt && !linked; k++) linked = parts.m.h[p.off + k] == (kForeign | fid);
+      if (!linked) continue;
+      if (part_remove(mp, kForeign | fid) == 0) {
+        part_release(mp);
+        sub_set_merge(m, mp, false);
+      }
+      merge_dirty(m);
+    }
+  fsub_pos_.erase(key);
+  auto cf = client_foreign_.find(client);
+  if (cf != client_foreign_.end()) {
+    auto& v = cf->second;
+    v.erase(std::find(v.begin(), v.end(), i));
+    if (v.empty()) client_foreign_.erase(cf);
+  }
+  fsubs_[i].depth = 0;
+  fsub_free_.push_back(i);
 }
 
 // ---- TopicsIndex operations ----------------------------------------------------------------------
 
 // topics.go:401-419
+// Owner shard of a subscription. A shared one is keyed by (particle, group, client)
+// (topics.go:406-411): its owner hashes the group and the particle's path — "$share/g/a" and
+// "$SHARE/g/a" are one key, and so are "$share/g" and "$share/g/g" (Q13: a short filter's
+// particle is its last segment, isolateParticle beyond range). Others hash the filter.
+static std::string shard_key(std::string_view filter, bool share) {
+  if (!share) return std::string(filter);
+  std::string k(segment_at(filter, 1));
+  k.push_back('\0');
+  std::vector<std::string_view> path;
+  size_t s = 0;
+  std::vector<std::string_view> segs;
+  for (;;) {
+    const size_t e = filter.find('/', s);
+    segs.push_back(filter.substr(s, e == std::string_view::npos ? std::string_view::npos : e - s));
+    if (e == std::string_view::npos) break;
+    s = e + 1;
+  }
+  if (segs.size() > 2) path.assign(segs.begin() + 2, segs.end());
+  else path.push_back(segs.back());
+  for (std::string_view p : path) {
+    k.append(p.data(), p.size());
+    k.push_back('/');
+  }
+  return k;
+}
+
 int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_id, uint8_t qos,
                      uint8_t flags, int32_t ident) {
   version_++;
-  if (is_share_prefix(segment_at(filter, 0))) {
+  const bool share = is_share_prefix(segment_at(filter, 0));
+  if (sharded() && shard_hash(shard_key(filter, share)) % n_shards_ != shard_) {
+    if (share) return 0;  // the owner answers
+    return foreign_subscribe(filter, client, filter_id, (uint32_t)(qos & 3) | ((flags & 1) ? kMetaNoLocal : 0));
+  }
+  if (share) {
     std::string group(segment_at(filter, 1));
     auto git = group_ids_.find(group);
     uint32_t gid;
@@ -802,19 +983,29 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
   if (sub_pos_.get((uint64_t)n << 32 | client, &pos)) {
     subs.m.at_w(pos) = rec;
     const PartList& p = subp_[pos];  // the partners' links carry this subscription's meta,
-    for (uint32_t i = 0; i < p.cnt; i++) merge_dirty(parts.m.h[p.off + i]);
+    for (uint32_t i = 0; i < p.cnt; i++) touch_partner(parts.m.h[p.off + i]);
     if (sub_is_merge(n, pos)) merge_dirty(n);  // and n's pair slots copy it
     return 0;
   }
   // Partners: the client's other subscriptions that could match the same topic (the merge
-  // candidates of gatherSubscriptions / Subscription.Merge, topics.go:641-646).
+  // candidates of gatherSubscriptions / Subscription.Merge, topics.go:641-646), on this shard
+  // and (sharded index) on the others.
+  if (sharded() && xinfo.h[n].fid == kNone) {
+    if (filter_id & kForeign) throw std::invalid_argument("sharded index: filter ids must be < 2^31");
+    xinfo.at_w(n).fid = filter_id;
+  }
   std::vector<uint32_t>& mine = client_nodes_[client];
-  thread_local std::vector<uint32_t> comp;
+  thread_local std::vector<uint32_t> comp, all;
   comp.clear();
   for (uint32_t m : mine)
     if (compatible(n, m)) comp.push_back(m);
-  pos = sub_add(n, rec, !comp.empty());
-  if (!comp.empty()) part_set(pos, comp);
+  all = comp;
+  auto cf = client_foreign_.find(client);
+  if (cf != client_foreign_.end())
+    for (uint32_t i : cf->second)
+      if (compatible_foreign(n, fsubs_[i])) all.push_back(kForeign | fsubs_[i].fid);
+  pos = sub_add(n, rec, !all.empty());
+  if (!all.empty()) part_set(pos, all);
   for (uint32_t m : comp) {
     uint32_t mp;
     if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
@@ -833,6 +1024,13 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
 int Index::unsubscribe(std::string_view filter, uint32_t client) {
   version_++;
   bool share = is_share_prefix(segment_at(filter, 0));
+  if (sharded() && shard_hash(shard_key(filter, share)) % n_shards_ != shard_) {
+    if (!share) {  // the owner drops the subscription; here it stops being a foreign partner
+      const uint32_t sid = ffilt_.find(filter);
+      if (sid != kNone && sid < ffid_.size()) foreign_unsubscribe(client, ffid_[sid]);
+    }
+    return seek(filter, share ? 2 : 0) != kNone ? 1 : 0;  // this shard's part of "particle exists"
+  }
   uint32_t n = seek(filter, share ? 2 : 0);
   if (n == kNone) return 0;
   if (share) {
@@ -868,6 +1066,7 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
         if (v.empty()) client_nodes_.erase(cit);
       }
       for (uint32_t m : partners) {  // the partners lose this one; unflag those left alone
+        if (m & kForeign) continue;  // another shard's subscription: no link back on this shard
         uint32_t mp;
         if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
         if (part_remove(mp, n) == 0) {
@@ -883,8 +1082,13 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
 }
 
 // topics.go:368-378
+static std::string_view inline_key(const int32_t& ident) {
+  return std::string_view(reinterpret_cast<const char*>(&ident), sizeof(ident));
+}
+
 int Index::inline_subscribe(std::string_view filter, int32_t ident, uint32_t filter_id) {
   version_++;
+  if (sharded() && shard_hash(inline_key(ident)) % n_shards_ != shard_) return 0;  // by identifier
   uint32_t n = set(filter, 0);
   uint64_t key = (uint64_t)n << 32 | (uint32_t)ident;
   InlRec rec{ident, filter_id};
@@ -908,6 +1112,7 @@ int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
   version_++;
   uint32_t n = seek(filter, 0);
   if (n == kNone) return 0;
+  if (sharded() && shard_hash(inline_key(ident)) % n_shards_ != shard_) return 1;  // exists here
   uint64_t key = (uint64_t)n << 32 | (uint32_t)ident;
   uint32_t pos;
   if (inl_pos_.get(key, &pos)) {
@@ -929,6 +1134,7 @@ int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
 int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
                               bool retain) {
   version_++;
+  if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;  // retained: by topic
   uint32_t n = set(topic, 0);
   std::string t(topic);
   if (payload_len > 0) {
@@ -966,6 +1172,7 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
 // Retained.Delete (server.go:1726): the map entry only; the particle keeps retainPath (Q12).
 int Index::retained_delete(std::string_view topic) {
   version_++;
+  if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;
   auto it = retained_.find(std::string(topic));
   if (it == retained_.end()) return 0;
   retained_.erase(it);

@@ -143,6 +143,7 @@ struct NodeHost {
   uint32_t sub_cap = 0, shr_cap = 0, inl_cap = 0, child_cap = 0;
   uint32_t mpart_off = 0, mpart_cap = 0;  // the node's slab of device partner links
   uint32_t pent_cap = 0, plist_cap = 0;    // its pair block slabs
+  uint32_t x_slots = 0;                    // sharded: may-merge slots with a foreign partner
   uint16_t depth = 0;
   bool live = false;
   bool retain_path = false;
@@ -154,9 +155,29 @@ struct RetEntry {
   bool retain;
 };
 
+// A subscription held by another shard, as this shard sees it (sharded index): what its
+// partner links need — the filter's path, for co-matchability with this shard's filters.
+struct ForeignSub {
+  uint32_t client, fid, meta;  // meta: Qos | NoLocal (the bits Subscription.Merge takes)
+  uint32_t path_off, depth;    // segment string ids in Index::fpaths_ (depth 0: a free entry)
+};
+
 class Index {
  public:
   explicit Index(uint64_t expected_subs = 0, uint64_t expected_nodes = 0);
+
+  // Sharded index: this index holds shard `shard` of `n_shards`. Every update is
+  // issued to every shard; each applies the part it owns — non-shared and shared subscriptions
+  // by a hash of the full filter, inline subscriptions by identifier, retained messages by
+  // topic — and records the other shards' non-shared subscriptions of its clients as foreign
+  // partners (cross-shard merges). Returns the shard's own answer: the reference's return value
+  // is the owner's (Subscribe, InlineSubscribe, RetainMessage: others return 0) or the OR over
+  // shards (Unsubscribe / InlineUnsubscribe: particle exists, Q10). Call before any update.
+  void set_shard(uint32_t shard, uint32_t n_shards);
+  uint32_t shard() const { return shard_; }
+  uint32_t n_shards() const { return n_shards_; }
+  bool sharded() const { return n_shards_ > 1; }
+  static uint32_t shard_hash(std::string_view key);  // owner = shard_hash(key) % n_shards
 
   // TopicsIndex API (topics.go:368-476); semantics and return values as the reference.
   int subscribe(std::string_view filter, uint32_t client, uint32_t filter_id, uint8_t qos,
@@ -186,6 +207,7 @@ class Index {
   SlabPool<ShrRec> shr;
   SlabPool<InlRec> inl;
   SlabPool<ChildRec> children;  // per node: its children (NodeMsg.child_off/child_cnt)
+  Mirror<XInfo> xinfo;          // sharded only (empty otherwise): per node fid + rank key
   // Retained packet stored on topic "" (retainPath "" is "no path", Q6): literal-final
   // lookups of particles without a retain path read this entry (topics.go:573).
   bool empty_topic_live = false;
@@ -202,6 +224,7 @@ class Index {
   // O(partner links of those nodes).
   void flush_merge();
   uint64_t merge_links() const { return mpart.live; }
+  uint64_t foreign_subs() const { return fsub_pos_.size(); }
   // Flush, then verify the device-bound invariants (mq_index_check); false + reason on the
   // first violation.
   bool check(std::string* why);
@@ -229,7 +252,17 @@ class Index {
   void sub_remove(uint32_t n, uint32_t pos);
   void sub_set_merge(uint32_t n, uint32_t pos, bool merge);
   bool compatible(uint32_t a, uint32_t b) const;
+  bool compatible_foreign(uint32_t a, const ForeignSub& f) const;
+  static bool compatible_strs(const uint32_t* pa, int la, const uint32_t* pb, int lb);
   void path_strs(uint32_t n, uint32_t* out, int* len) const;
+  // sharded: a non-shared subscription owned by another shard (Subscribe / Unsubscribe)
+  int foreign_subscribe(std::string_view filter, uint32_t client, uint32_t fid, uint32_t meta);
+  void foreign_unsubscribe(uint32_t client, uint32_t fid);
+  uint32_t partner_meta(uint32_t partner, uint32_t client) const;  // Qos | NoLocal of a partner
+  void touch_partner(uint32_t p) {
+    if (!(p & kForeign)) merge_dirty(p);
+  }
+  void set_rank(uint32_t n, uint32_t parent, std::string_view seg);
   void move_slot(uint32_t n, uint32_t from, uint32_t to);
   void part_set(uint32_t pos, const std::vector<uint32_t>& nodes);
   void part_add(uint32_t pos, uint32_t node);
@@ -283,6 +316,15 @@ class Index {
   std::vector<uint8_t> merge_dirty_flag_;
   std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
   std::unordered_map<std::string, RetEntry> retained_;
+  // sharding
+  uint32_t shard_ = 0, n_shards_ = 1;
+  std::vector<ForeignSub> fsubs_;
+  std::vector<uint32_t> fsub_free_;
+  HashU64 fsub_pos_{64};  // (fid << 32 | client) -> fsubs_ index
+  std::unordered_map<uint32_t, std::vector<uint32_t>> client_foreign_;  // client -> fsubs_ indices
+  std::vector<uint32_t> fpaths_;                                         // foreign filters' segment ids
+  StrTable ffilt_;                   // foreign non-shared filter strings -> ffid_ index
+  std::vector<uint32_t> ffid_;       // their caller filter ids
 };
 
 // strings.EqualFold(s, "$SHARE") under Go's Unicode simple folding (Q9: U+017F ~ 's').

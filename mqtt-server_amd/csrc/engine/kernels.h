@@ -27,7 +27,7 @@ constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
 constexpr uint32_t kPartBatch = 8;     // partner links loaded together per record
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
-// resolved (pair slots read), partner links loaded
+// resolved (pair slots read), partner links loaded, patches written
 constexpr uint32_t kWork = 4;
 constexpr uint32_t kMergeWavesPerEU = 6;  // k_merge register budget: 1 (none), 6 or 8 waves per SIMD
 constexpr uint64_t kMergeWpeMinSubs = 4000000;  // ... used from this many subscriptions on
@@ -50,6 +50,7 @@ struct DevIndex {
   const ShrRec* shr;
   const InlRec* inl;
   const ChildRec* children;
+  const XInfo* xinfo;  // sharded index only (else null): per node filter id + rank key
   uint64_t retained_len;
   uint64_t empty_topic_handle;
   uint32_t empty_topic_live;
@@ -90,6 +91,10 @@ struct GDesc {  // 32 B
   uint32_t mdir;   // n_direct of the node | kDescMerge when its may-merge records are gathered
 };
 constexpr uint32_t kDescMerge = 1u << 31;
+// Span format, sharded index: k_desc folds a merge gather's rank key (XInfo.rank) into the
+// GDesc's i_pos (low) / i_src (high) words, which the span format does not otherwise use.
+
+constexpr uint32_t kMaxShards = 16;  // sharded index: shards a batch's exchange can join
 
 // Span-format records (include/mqmatch.h mq_span / mq_patch / mq_topic_spans).
 struct SpanRec {  // one gathered particle: subs[sub_off, + n_sub), shr[shr_off, + n_shr)
@@ -126,6 +131,10 @@ struct EmitArgs {
   unsigned long long* pcount;     //   reserves in region t % kPatchRegions with atomicAdd on
   uint64_t rcap;                  //   pcount[region] (may exceed rcap: the host grows the pool)
   unsigned long long* work;       // MQ_PROF_WORK: per region kWork counters (null: off)
+  // sharded index: the other shards' exported cross-shard nodes of every topic (k_xlist)
+  uint32_t n_xf;
+  const TopicOff* xoff[kMaxShards - 1];  // per foreign shard: per-topic offsets (.g) into
+  const XEnt* xent[kMaxShards - 1];      //   its entries
 };
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile
@@ -196,6 +205,13 @@ void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_bloc
 void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                 TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
                 uint32_t* count, uint64_t* spec, uint32_t spec_cap, uint32_t wpe, hipStream_t s);
+// Sharded index: the topics' gathered cross-shard nodes (kFlagXNode, subscriptions gathered).
+// count = true: TopicCount.gathers = their number per topic; else written as XEnt at
+// off[t].g with their number in counts[t] (the exported list, mq_xlist).
+void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const GDesc* desc,
+                  TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts, hipStream_t s);
+// TopicCount.gathers = counts[t] (an imported list's counts, for launch_scan)
+void launch_counts(const uint32_t* counts, uint32_t n, TopicCount* cnt, hipStream_t s);
 // Pack the used prefix of every patch region (pcount[r] patches of region r) into `out` at
 // roff[r] (span format, host results).
 void launch_patch_compact(const PatchRec* pool, uint64_t rcap, const unsigned long long* pcount,

@@ -436,10 +436,19 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     d.i_src = L.inl_off;
     d.word = gw;
     d.mdir = L.n_direct | ((gw & kGatherSubs) && L.n_merge ? kDescMerge : 0u);
-    if (SPANS && (d.mdir & kDescMerge)) {  // k_merge reads the pair block's header from here
-      const NodePair P = a.ix.npair[gw & kGatherNode];
-      d.s_pos = P.ent_off;
-      d.s_src = P.ent_mask;
+    if (SPANS) {  // k_merge reads the pair block's header (and the rank key) from here
+      d.i_pos = 0;
+      d.i_src = 0;
+      if (d.mdir & kDescMerge) {
+        const NodePair P = a.ix.npair[gw & kGatherNode];
+        d.s_pos = P.ent_off;
+        d.s_src = P.ent_mask;
+        if (a.ix.xinfo) {
+          const uint64_t rk = a.ix.xinfo[gw & kGatherNode].rank;
+          d.i_pos = (uint32_t)rk;
+          d.i_src = (uint32_t)(rk >> 32);
+        }
+      }
     }
     a.desc[g] = d;
     if (SPANS) {
@@ -577,6 +586,12 @@ __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
   }
 }
 
+// Rank key of a span-format merge gather of a sharded index (k_desc<true>; else 0).
+template <bool XS>
+__device__ __forceinline__ uint64_t gdesc_rank(const GDesc& d) {
+  return XS ? ((uint64_t)d.i_src << 32 | d.i_pos) : 0ull;
+}
+
 // SPANS=false: the records were copied to the chunk's rows by k_copy and are rewritten in
 // place. SPANS=true: nothing was copied; each record whose row changes leaves a PatchRec (its
 // topic-relative row, the new meta) in a range the topic reserves with one atomicAdd on its
@@ -587,12 +602,17 @@ __global__ __launch_bounds__(256) void k_copy(EmitArgs a) {
 // nothing; the host reads the counters, grows the pool and runs the batch's k_merge again.
 // WPE: minimum waves per SIMD asked of the register allocator (1 = no constraint; the kernel is
 // latency-bound, so occupancy can pay for a few spills). MQ_OPT_MERGE_WAVES picks the variant.
-template <bool SPANS, int WPE>
+// XS (span format of a sharded index): the other shards' exported nodes join the topic's map
+// and DFS order compares rank keys first (SPANS must be true).
+template <bool SPANS, bool XS, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
-  __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records
-  __shared__ uint32_t map_val[4][kMapSlots];   // its gather index (= DFS rank order)
-  __shared__ uint32_t mg_node[4][kPairMax];    // the topic's merge gathers, in gather order:
-  __shared__ uint32_t mg_gi[4][kPairMax];      //   node, gather index,
+  constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
+  __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records (or
+                                               //   kForeign | fid: another shard's, XS)
+  __shared__ uint32_t map_val[4][kMapSlots];   // its entry below
+  __shared__ uint32_t mg_node[4][kEnt];        // entries: the topic's merge gathers in gather
+  __shared__ uint32_t mg_gi[4][kEnt];          //   order (node, gather index), then (XS) the
+  __shared__ uint64_t mg_rank[4][XS ? kEnt : 1];  // other shards' (kForeign | fid, kNone, rank)
   __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first may-merge slot,
   __shared__ uint32_t mg_eoff[4][kPairMax];    //   its pair-block hash table (NodePair)
   __shared__ uint32_t mg_emask[4][kPairMax];
@@ -601,6 +621,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ uint32_t h_via[4][kHitMax];       //   partner node h,
   __shared__ uint32_t h_pre[4][kHitMax + 1];   //   exclusive prefix of their lengths (+ total)
   const uint32_t wv = wave_id(), lane = threadIdx.x & 63;
+  auto rank_of = [](const GDesc& d) { return gdesc_rank<XS>(d); };
   // persistent: a.merge grid's waves stride over the chunk's topics (wave-uniform loop)
   for (uint32_t t = a.t0 + blockIdx.x * 4 + wv; t < a.t1; t += gridDim.x * 4) {
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
@@ -660,32 +681,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (ins && x < kPairMax) {
         uint32_t sl = hash32(node) & (kMapSlots - 1);
         while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
-        map_val[wv][sl] = i;
+        map_val[wv][sl] = x;
         mg_node[wv][x] = node;
         mg_gi[wv][x] = i;
+        if (XS) mg_rank[wv][x] = rank_of(gd[i]);
         mg_row[wv][x] = mrow;
         mg_eoff[wv][x] = P.ent_off;
         mg_emask[wv][x] = P.ent_mask;
       }
       n_map += __popcll(bi);
     }
+    // sharded index: the other shards' gathered cross-shard nodes join the map as entries
+    // n_map.. (their partner links name them kForeign | fid; their rank keys order them)
+    uint32_t n_ent = n_map;
+    for (uint32_t f = 0; XS && f < a.n_xf; f++) {
+      const uint64_t x0 = a.xoff[f][t].g, x1 = a.xoff[f][t + 1].g;
+      for (uint64_t k0 = x0; k0 < x1; k0 += 64) {
+        const uint64_t k = k0 + lane;
+        const uint32_t x = n_ent + (uint32_t)(k - x0);
+        if (k < x1 && x < kEnt && n_map <= kPairMax) {
+          const XEnt e = a.xent[f][k];
+          const uint32_t key = kForeign | e.fid;
+          uint32_t sl = hash32(key) & (kMapSlots - 1);
+          while (atomicCAS(&map_key[wv][sl], kNone, key) != kNone) sl = (sl + 1) & (kMapSlots - 1);
+          map_val[wv][sl] = x;
+          mg_node[wv][x] = key;
+          mg_gi[wv][x] = kNone;
+          if (XS) mg_rank[wv][x] = e.rank;
+        }
+      }
+      n_ent += (uint32_t)(x1 - x0);
+    }
     wave_sync_lds();
-    const bool slow = n_map > kPairMax;  // beyond the map: look partners up linearly
-    auto gathered = [&](uint32_t h) -> uint32_t {  // gather index of node h, or kNone
+    const bool slow = n_map > kPairMax || n_ent > kEnt;  // beyond the map: linear lookups
+    // Is node h (or kForeign | fid) gathered for this topic? Its DFS position: rank key, then
+    // gather index (kNone for another shard's node).
+    auto gathered = [&](uint32_t h, uint64_t* rk, uint32_t* gi) -> bool {
       if (!slow) {
         uint32_t sl = hash32(h) & (kMapSlots - 1);
         for (;;) {
           const uint32_t k = map_key[wv][sl];
-          if (k == h) return map_val[wv][sl];
-          if (k == kNone) return kNone;
+          if (k == h) {
+            const uint32_t y = map_val[wv][sl];
+            *rk = XS ? mg_rank[wv][y] : 0ull;
+            *gi = mg_gi[wv][y];
+            return true;
+          }
+          if (k == kNone) return false;
           sl = (sl + 1) & (kMapSlots - 1);
         }
       }
-      for (uint32_t i = 0; i < n_g; i++) {
-        const uint32_t gw = gd[i].word;
-        if ((gw & kGatherNode) == h && (gw & kGatherSubs)) return i;
+      if (XS && (h & kForeign)) {
+        for (uint32_t f = 0; f < a.n_xf; f++)
+          for (uint64_t k = a.xoff[f][t].g; k < a.xoff[f][t + 1].g; k++)
+            if ((kForeign | a.xent[f][k].fid) == h) {
+              *rk = a.xent[f][k].rank;
+              *gi = kNone;
+              return true;
+            }
+        return false;
       }
-      return kNone;
+      for (uint32_t i = 0; i < n_g; i++) {
+        const GDesc d = gd[i];
+        if ((d.word & kGatherNode) == h && (d.word & kGatherSubs)) {
+          *rk = rank_of(d);
+          *gi = i;
+          return true;
+        }
+      }
+      return false;
+    };
+    // does the gathered node at (rh, gh) come before the record's own (rg, gg) in DFS order?
+    auto before = [&](uint64_t rh, uint32_t gh, uint64_t rg, uint32_t gg) -> bool {
+      if (!XS) return gh < gg;
+      if (rh != rg) return rh < rg;
+      if (gh != kNone) return gh < gg;  // both on this shard: gather order is DFS order
+      atomicOr(a.ix.err, kErrDeepRank);  // another shard's node tied beyond the key's 32 levels
+      return false;
     };
 
     // Resolve one record whose client may have other matches for this topic: its partners that
@@ -696,8 +768,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // through several hit lists; only the visit through its first gathered partner (`via`, or
     // any when via == kNone) counts it, and only that visit leaves a patch (the row format
     // writes the same row on every visit). Called by all lanes (wave-uniform).
-    // mw: the record's meta | kSlotIdentPos when its identifier is > 0 (PairSlot.meta).
-    auto resolve = [&](bool active, uint32_t mw, uint32_t row, uint32_t gi, uint32_t via,
+    // mw: the record's meta | kSlotIdentPos when its identifier is > 0 (PairSlot.meta); (rg, gi):
+    // its gather's rank key and gather index.
+    auto resolve = [&](bool active, uint32_t mw, uint32_t row, uint64_t rg, uint32_t gi, uint32_t via,
                        uint32_t mp_off, uint32_t mp_cnt) {
       bool counted = false, nonbase = false, want = false;
       uint32_t pmeta = 0;
@@ -717,11 +790,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (uint32_t u = 0; u < kPartBatch; u++) {
             if (!base || pb[u].node == kNone) continue;
-            const uint32_t gh = gathered(pb[u].node);
-            if (gh == kNone) continue;
+            uint64_t rh;
+            uint32_t gh;
+            if (!gathered(pb[u].node, &rh, &gh)) continue;
             if (!bound) first = pb[u].node;
             bound = true;
-            if (gh < gi) {
+            if (before(rh, gh, rg, gi)) {
               base = false;
               continue;
             }
@@ -767,7 +841,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const uint32_t xa = h_ga[wv][jj];
           const PairSlot e = a.ix.plist[h_off[wv][jj] + (rc - h_pre[wv][jj])];
           w_rec += r < tot;
-          resolve(r < tot, e.meta, mg_row[wv][xa] + e.k, mg_gi[wv][xa], h_via[wv][jj], e.mp_off, e.mp_cnt);
+          resolve(r < tot, e.meta, mg_row[wv][xa] + e.k, XS ? mg_rank[wv][xa] : 0ull, mg_gi[wv][xa], h_via[wv][jj],
+                  e.mp_off, e.mp_cnt);
         }
         n_hit = 0;
         tot = 0;
@@ -779,14 +854,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       uint64_t tot_all = 0;
       bool staged_all = true;
       auto pairs = [&](bool counting) {
-        const uint32_t np = n_map * n_map;
+        const uint32_t np = n_map * n_ent;  // (g: a merge gather here, h: any entry)
         for (uint32_t p0 = 0; p0 < np; p0 += 64) {
           const uint32_t p = p0 + lane;
           bool hit = false;
           uint32_t ga = 0, e_off = 0, e_cnt = 0, hn = 0;
           if (p < np) {
-            ga = p / n_map;
-            const uint32_t hb = p - ga * n_map;
+            ga = p / n_ent;
+            const uint32_t hb = p - ga * n_ent;
             if (ga != hb) {
               const uint32_t ent_mask = mg_emask[wv][ga], ent_off = mg_eoff[wv][ga];
               if (ent_mask != kNone) {
@@ -870,8 +945,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const MergeRef mr = a.ix.mref[pos];
           const SubRec rec = a.ix.subs[pos];
           w_rec += act;
-          resolve(act, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u), d.r_pos + L.n_direct + c0 + lane, i, kNone,
-                  mr.off, mr.cnt);
+          resolve(act, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u), d.r_pos + L.n_direct + c0 + lane, rank_of(d),
+                  i, kNone, mr.off, mr.cnt);
         }
       }
     }
@@ -905,6 +980,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       atomicAdd(wc + 0, (unsigned long long)e);
       atomicAdd(wc + 1, (unsigned long long)rr);
       atomicAdd(wc + 2, (unsigned long long)l);
+      atomicAdd(wc + 3, (unsigned long long)n_patch);
     }
   }
 
@@ -983,17 +1059,19 @@ void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_bloc
   const uint32_t waves = a.t1 - a.t0;
   if (!waves) return;
   const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
-  if (spans) {
-    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, 8>), dim3(blocks), dim3(256), 0, s, a);
-    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, 6>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_merge<true, 1>), dim3(blocks), dim3(256), 0, s, a);
+  const dim3 g(blocks), b(256);
+  if (spans && a.ix.xinfo) {  // sharded index
+    hipLaunchKernelGGL((k_merge<true, true, 1>), g, b, 0, s, a);
+  } else if (spans) {
+    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8>), g, b, 0, s, a);
+    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, false, 1>), g, b, 0, s, a);
   } else {
-    if (wpe >= 8) hipLaunchKernelGGL((k_merge<false, 8>), dim3(blocks), dim3(256), 0, s, a);
-    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<false, 6>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_merge<false, 1>), dim3(blocks), dim3(256), 0, s, a);
+    if (wpe >= 8) hipLaunchKernelGGL((k_merge<false, false, 8>), g, b, 0, s, a);
+    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<false, false, 6>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<false, false, 1>), g, b, 0, s, a);
   }
 }
-
 
 // ---------------------------------------------------------------------------------------------
 // k_msg: Messages(filter), the reverse retained scan (topics.go:525-579). One wavefront per
@@ -1458,6 +1536,51 @@ void launch_pick(const PickArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_pick<true>, dim3(a.n), dim3(64), 0, s, a);
   else
     hipLaunchKernelGGL(k_pick<false>, dim3(a.n), dim3(64), 0, s, a);
+}
+
+// Sharded index: each topic's gathered cross-shard nodes (the exported list).
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_xlist(DevIndex ix, uint32_t n, const TopicOff* __restrict__ off,
+                                               const GDesc* __restrict__ desc, TopicCount* __restrict__ cnt,
+                                               const TopicOff* __restrict__ xoff, XEnt* __restrict__ ents,
+                                               uint32_t* __restrict__ counts) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t g0 = off[t].g, g1 = off[t + 1].g;
+  uint32_t k = 0;
+  XEnt* out = COUNT ? nullptr : ents + xoff[t].g;
+  for (uint64_t g = g0; g < g1; g++) {
+    const uint32_t gw = desc[g].word;
+    if (!(gw & kGatherSubs)) continue;
+    const uint32_t node = gw & kGatherNode;
+    if (!(ix.lists[node].flags & kFlagXNode)) continue;
+    if (!COUNT) {
+      const XInfo x = ix.xinfo[node];
+      out[k] = XEnt{x.fid, x.deep, x.rank};
+    }
+    k++;
+  }
+  if (COUNT) cnt[t] = TopicCount{k, 0, 0, 0, 0};
+  else counts[t] = k;
+}
+
+void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const GDesc* desc,
+                  TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts, hipStream_t s) {
+  if (!n) return;
+  if (count)
+    hipLaunchKernelGGL(k_xlist<true>, dim3((n + 255) / 256), dim3(256), 0, s, ix, n, off, desc, cnt, xoff, ents, counts);
+  else
+    hipLaunchKernelGGL(k_xlist<false>, dim3((n + 255) / 256), dim3(256), 0, s, ix, n, off, desc, cnt, xoff, ents, counts);
+}
+
+__global__ __launch_bounds__(256) void k_counts(const uint32_t* __restrict__ counts, uint32_t n,
+                                                TopicCount* __restrict__ cnt) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) cnt[t] = TopicCount{counts[t], 0, 0, 0, 0};
+}
+
+void launch_counts(const uint32_t* counts, uint32_t n, TopicCount* cnt, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_counts, dim3((n + 255) / 256), dim3(256), 0, s, counts, n, cnt);
 }
 
 __global__ __launch_bounds__(256) void k_patch_compact(const PatchRec* __restrict__ pool, uint64_t rcap,

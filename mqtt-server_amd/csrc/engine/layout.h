@@ -88,6 +88,8 @@ struct EdgeSlot {  // 32 B
 // Walk record, read by the match walk (16 B).
 constexpr uint32_t kParentMask = 0x3FFFFFFFu;
 constexpr uint32_t kFlagSeg0Wild = 1u << 30;  // path segment 0 starts with '+'/'#' (Q3 rule)
+constexpr uint32_t kFlagXNode = 1u << 28;     // NodeLists.flags, sharded index: a subscription here
+                                              // has a co-matchable filter on another shard
 constexpr uint32_t kFlagPlusKey = 1u << 31;   // this node's key is "+"
 
 struct NodeWalk {
@@ -132,6 +134,24 @@ struct ChildRec {
   uint64_t handle;
 };
 static_assert(sizeof(ChildRec) == 24, "ChildRec layout");
+
+// Sharded index: a node's filter id and DFS rank key, exported per batch for the
+// node's cross-shard co-matches. rank = code(path) of SURVEY.md App. A.3, two bits per level
+// (kappa + 1: literal 1, '+' 2, '#' 3) from the top, zero-padded, so a proper prefix sorts first;
+// paths deeper than 32 levels keep their 32-level code and set `deep`.
+struct XInfo {  // 16 B
+  uint32_t fid;   // filter id of the node's non-shared subscriptions (kNone: none yet)
+  uint32_t deep;  // 1: deeper than the rank key's 32 levels
+  uint64_t rank;
+};
+constexpr uint32_t kForeign = 1u << 31;  // partner id of a filter held by another shard: kForeign | fid
+
+// One exported cross-shard node of a topic (mq_xent).
+struct XEnt {  // 16 B
+  uint32_t fid;
+  uint32_t deep;
+  uint64_t rank;
+};
 
 struct SegInfo {  // long segment bytes in the segment pool
   uint32_t off, len;

@@ -11,7 +11,7 @@ static void check(int rc, const char* what) {
 }
 
 TopicsIndex::TopicsIndex(int device, bool select_shared) {
-  mq_config cfg{device, select_shared ? MQ_CFG_SELECT_SHARED : 0u, 0, 0};
+  mq_config cfg{device, select_shared ? MQ_CFG_SELECT_SHARED : 0u, 0, 0, 0, 0};
   check(mq_index_create(&cfg, &idx_), "mq_index_create");
 }
 

@@ -1,8 +1,12 @@
 """Multi-process plumbing for the engine: one process per GPU.
 
-Publish topics are independent units, so the batch is partitioned across ranks and every rank
-holds a full replica of the index: no data-path collective. The process group carries only
-the timing barrier, the max-over-ranks elapsed time and (in tests) result checksums.
+Two modes:
+  - replicated: publish topics are independent units, so the batch is partitioned across ranks
+    and every rank holds a full replica of the index: no data-path collective; the process
+    group carries only the timing barrier, the max-over-ranks elapsed time and test checksums;
+  - sharded (north star, §8e(ii)): subscriptions are sharded by filter hash, every rank matches
+    the full batch, and the ranks all-gather each topic's cross-shard nodes (exchange_xlists,
+    RCCL all-gather over xGMI) so that every shard resolves its client merges exactly.
 
 Backend: "nccl" (RCCL over xGMI) on GPUs; `MQ_DIST_BACKEND=gloo` rehearses the same code on
 CPU or with several ranks sharing one GPU (RCCL refuses duplicate GPUs in a communicator).
@@ -88,6 +92,52 @@ def gather_u64(arr, backend):
     outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(outs, t)
     return [o.cpu().numpy().view(np.uint64) for o in outs]
+
+
+def _device_view(ptr, nbytes):
+    """A torch uint8 CUDA tensor over engine-owned device memory (__cuda_array_interface__)."""
+    import torch
+
+    class _Buf:
+        __cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(ptr or 0), False),
+                                    "version": 3, "strides": None}
+    return torch.as_tensor(_Buf(), device="cuda")
+
+
+def exchange_xlists(x, backend):
+    """All-gather every rank's exported list (mq_xlist from Engine.match_spans_begin): returns
+    the other ranks' lists as XList structs over device tensors, and the tensors (keep them
+    alive until mq_match_spans_end). nccl: two all-gathers of device buffers (counts, entries
+    padded to the largest rank's) plus one of the entry counts; gloo: the same through host
+    memory."""
+    import torch
+    import torch.distributed as dist
+    from .engine import XList
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n = int(x.n_topics)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    counts = _device_view(x.counts, 4 * n).view(torch.int32) if n else torch.zeros(0, dtype=torch.int32, device=dev)
+    ents = _device_view(x.ents, 16 * int(x.n_ents)) if x.n_ents else torch.zeros(0, dtype=torch.uint8, device=dev)
+    on = dev if backend == "nccl" else torch.device("cpu")
+    ne = torch.tensor([int(x.n_ents)], dtype=torch.int64, device=on)
+    ne_all = torch.empty(world, dtype=torch.int64, device=on)
+    dist.all_gather_into_tensor(ne_all, ne)
+    ne_host = ne_all.cpu().tolist()
+    maxe = max(1, max(ne_host))
+    c_all = torch.empty(world * n, dtype=torch.int32, device=on)
+    dist.all_gather_into_tensor(c_all, counts.to(on))
+    pad = torch.zeros(16 * maxe, dtype=torch.uint8, device=on)
+    pad[:ents.numel()] = ents.to(on)
+    e_all = torch.empty(world * 16 * maxe, dtype=torch.uint8, device=on)
+    dist.all_gather_into_tensor(e_all, pad)
+    if on.type != "cuda":
+        c_all, e_all = c_all.to(dev), e_all.to(dev)
+    out = []
+    for r in range(world):
+        if r == rank:
+            continue
+        out.append(XList(n, r, c_all[r * n:].data_ptr() if n else None, e_all[r * 16 * maxe:].data_ptr(), ne_host[r]))
+    return out, (c_all, e_all)
 
 
 def finalize(backend):

@@ -33,7 +33,13 @@ _i64p = C.POINTER(C.c_int64)
 
 class MqConfig(C.Structure):
     _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("expected_subs", C.c_uint64),
-                ("expected_nodes", C.c_uint64)]
+                ("expected_nodes", C.c_uint64), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32)]
+
+
+class XList(C.Structure):
+    """mq_xlist: a shard's exported cross-shard nodes per topic (device pointers)."""
+    _fields_ = [("n_topics", C.c_uint32), ("shard", C.c_uint32), ("counts", C.c_void_p), ("ents", C.c_void_p),
+                ("n_ents", C.c_uint64)]
 
 
 class TopicResult(C.Structure):
@@ -85,7 +91,8 @@ class AclResult(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("nodes", "edges", "edge_capacity", "subs", "subs_merge",
                                            "shared", "inlines", "retained", "retained_live",
-                                           "device_bytes", "upload_bytes_total", "syncs", "partners")] + \
+                                           "device_bytes", "upload_bytes_total", "syncs", "partners",
+                                           "foreign")] + \
                [("max_depth", C.c_uint32), ("reserved", C.c_uint32)]
 
 
@@ -102,7 +109,8 @@ EXPORTS = [
     "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
     "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
     "mq_acl_match_batch", "mq_select_shared_device", "mq_match_spans", "mq_match_spans_device",
-    "mq_spans_expand", "mq_set_option",
+    "mq_spans_expand", "mq_set_option", "mq_match_spans_begin", "mq_match_spans_end",
+    "mq_match_spans_end_host",
 ]
 
 CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
@@ -150,6 +158,9 @@ def lib():
         "mq_spans_expand": (C.c_int, [C.POINTER(SpanResult), C.c_uint32, C.c_uint32, vp, C.c_uint64, vp,
                                       C.c_uint64, _u64p, _u64p]),
         "mq_set_option": (C.c_int, [vp, C.c_uint32, C.c_uint64]),
+        "mq_match_spans_begin": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(XList)]),
+        "mq_match_spans_end": (C.c_int, [vp, C.POINTER(XList), C.c_uint32, vp, C.POINTER(SpanResult)]),
+        "mq_match_spans_end_host": (C.c_int, [vp, C.POINTER(XList), C.c_uint32, C.POINTER(C.POINTER(SpanResult))]),
         "mq_match_chunks": (C.c_uint32, [vp]),
         "mq_select_shared_device": (C.c_int, [vp, C.POINTER(MatchResult), vp, vp, vp]),
         "mq_match_device_chunks": (C.c_int, [vp, vp, vp, C.c_uint32, vp, CHUNK_FN, vp]),
@@ -274,11 +285,12 @@ def is_share_prefix(seg: str) -> bool:
 class Engine:
     """Thin object wrapper over one mq_index handle (id-level C-ABI)."""
 
-    def __init__(self, device=0, expected_subs=0, expected_nodes=0, select_shared=False):
+    def __init__(self, device=0, expected_subs=0, expected_nodes=0, select_shared=False, shard=0, n_shards=1):
         """select_shared: MQ_CFG_SELECT_SHARED (results carry one picked member per shared
-        filter; SelectShared ran on the device)."""
+        filter; SelectShared ran on the device). shard / n_shards: a sharded index (mq_config)."""
         L = lib()
-        cfg = MqConfig(device, CFG_SELECT_SHARED if select_shared else 0, expected_subs, expected_nodes)
+        cfg = MqConfig(device, CFG_SELECT_SHARED if select_shared else 0, expected_subs, expected_nodes,
+                       shard, n_shards)
         h = C.c_void_p()
         _check(L.mq_index_create(C.byref(cfg), C.byref(h)), "mq_index_create")
         self.h = h
@@ -374,26 +386,14 @@ class Engine:
         n = len(offs) - 1
         rp = C.POINTER(SpanResult)()
         _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
-        try:
-            r = rp.contents
-            a = _span_arrays(r, n)
-            t = a["topics"]
-            n_rows, n_shared = t["n_rows"].astype(np.uint64), t["n_shared"].astype(np.uint64)
-            rows = np.zeros((max(int(n_rows.sum()), 1), 4), np.uint32)
-            shared = np.zeros((max(int(n_shared.sum()), 1), 2), np.uint32)
-            nr, ns = C.c_uint64(), C.c_uint64()
-            _check(lib().mq_spans_expand(rp, 0, n, rows.ctypes.data, len(rows), shared.ctypes.data, len(shared),
-                                         C.byref(nr), C.byref(ns)), "mq_spans_expand")
-        finally:
-            lib().mq_result_free(rp)
-        excl = lambda c: np.concatenate(([0], np.cumsum(c)[:-1])).astype(np.uint64) if len(c) else np.zeros(0, np.uint64)
-        return {
-            "sub_base": excl(n_rows), "shared_base": excl(n_shared), "inline_base": t["inline_base"].copy(),
-            "sub_cap": t["n_rows"].copy(), "n_client": t["n_client"].copy(), "n_ident": t["n_ident"].copy(),
-            "n_shared": t["n_shared"].copy(), "n_inline": t["n_inline"].copy(),
-            "rows": rows[:int(nr.value)], "shared": shared[:int(ns.value)], "inline": a["inline"],
-            "n_patches": int(t["n_patches"].sum()), "n_spans": int(t["n_spans"].sum()),
-        }
+        return _expand_host_spans(rp, n)
+
+    def match_spans_end_expanded(self, foreign, n):
+        """mq_match_spans_end_host with the other shards' XLists, expanded like match_batch_spans."""
+        arr = (XList * max(1, len(foreign)))(*foreign)
+        rp = C.POINTER(SpanResult)()
+        _check(lib().mq_match_spans_end_host(self.h, arr, len(foreign), C.byref(rp)), "mq_match_spans_end_host")
+        return _expand_host_spans(rp, n)
 
     def match_spans_host(self, bytes_, offs, expand=False, block=1024):
         """mq_match_spans with its results left in the library's host buffers (the end-to-end
@@ -425,6 +425,22 @@ class Engine:
         finally:
             lib().mq_result_free(rp)
         return int(nbytes), done
+
+    def match_spans_begin(self, d_bytes, d_offs, n, stream=None):
+        """mq_match_spans_begin -> XList (this shard's export; device pointers)."""
+        x = XList()
+        _check(lib().mq_match_spans_begin(self.h, C.c_void_p(d_bytes), C.c_void_p(d_offs), n,
+                                          C.c_void_p(stream) if stream else None, C.byref(x)),
+               "mq_match_spans_begin")
+        return x
+
+    def match_spans_end(self, foreign, stream=None):
+        """mq_match_spans_end with the other shards' XLists -> SpanResult (device pointers)."""
+        arr = (XList * max(1, len(foreign)))(*foreign)
+        r = SpanResult()
+        _check(lib().mq_match_spans_end(self.h, arr, len(foreign), C.c_void_p(stream) if stream else None,
+                                        C.byref(r)), "mq_match_spans_end")
+        return r
 
     def match_spans_device(self, d_bytes, d_offs, n, stream=None):
         """mq_match_spans_device on device pointers (ints); returns the SpanResult struct."""
@@ -600,6 +616,30 @@ def _span_arrays(r, n):
         "inline": arr(r.inline_rows, int(r.n_inline_rows), np.uint32, 2),
         "picked": arr(r.picked_rows, int(r.n_picked_rows), np.uint32, 2),
         "flags": int(r.flags),
+    }
+
+
+def _expand_host_spans(rp, n):
+    """Expand a host SpanResult (then freed) into match_batch()'s dict via mq_spans_expand."""
+    try:
+        r = rp.contents
+        a = _span_arrays(r, n)
+        t = a["topics"]
+        n_rows, n_shared = t["n_rows"].astype(np.uint64), t["n_shared"].astype(np.uint64)
+        rows = np.zeros((max(int(n_rows.sum()), 1), 4), np.uint32)
+        shared = np.zeros((max(int(n_shared.sum()), 1), 2), np.uint32)
+        nr, ns = C.c_uint64(), C.c_uint64()
+        _check(lib().mq_spans_expand(rp, 0, n, rows.ctypes.data, len(rows), shared.ctypes.data, len(shared),
+                                     C.byref(nr), C.byref(ns)), "mq_spans_expand")
+    finally:
+        lib().mq_result_free(rp)
+    excl = lambda c: np.concatenate(([0], np.cumsum(c)[:-1])).astype(np.uint64) if len(c) else np.zeros(0, np.uint64)
+    return {
+        "sub_base": excl(n_rows), "shared_base": excl(n_shared), "inline_base": t["inline_base"].copy(),
+        "sub_cap": t["n_rows"].copy(), "n_client": t["n_client"].copy(), "n_ident": t["n_ident"].copy(),
+        "n_shared": t["n_shared"].copy(), "n_inline": t["n_inline"].copy(),
+        "rows": rows[:int(nr.value)], "shared": shared[:int(ns.value)], "inline": a["inline"],
+        "n_patches": int(t["n_patches"].sum()), "n_spans": int(t["n_spans"].sum()),
     }
 
 

@@ -47,6 +47,21 @@ def _seg_sums(h, counts):
 
 def engine_digests(res):
     """res: Engine.match_batch() dict -> (digests u64[n], counts u32[n,4])."""
+    counts, sums = engine_digest_parts(res)
+    return fold_parts(counts, sums), counts.astype(np.uint32)
+
+
+def fold_parts(counts, sums):
+    """Per-topic digest from per-category row counts and wrapping sums of row hashes (the parts
+    of disjoint results, e.g. the shards of a sharded index, add up)."""
+    d = np.full(len(counts), SEED, np.uint64)
+    for k in range(4):
+        d = fold(fold(d, counts[:, k].astype(np.uint64)), sums[:, k].astype(np.uint64))
+    return d
+
+
+def engine_digest_parts(res):
+    """res: Engine.match_batch() dict -> (counts i64[n,4], sums u64[n,4]) per row category."""
     n = len(res["n_client"])
     rows = res["rows"].astype(np.uint64)
     base, cap = res["sub_base"].astype(np.int64), res["sub_cap"].astype(np.int64)
@@ -68,9 +83,7 @@ def engine_digests(res):
     hs = row_hash(3, sh[si, 0], sh[si, 1], 0, 0)
     il = res["inline"].astype(np.uint64)
     hl = row_hash(4, il[li, 0], il[li, 1], 0, 0)
-    d = np.full(n, SEED, np.uint64)
     counts = np.stack([nc, ni, res["n_shared"].astype(np.int64), res["n_inline"].astype(np.int64)], 1)
-    sums = (_seg_sums(hc, cap), _seg_sums(hi, cap), _seg_sums(hs, counts[:, 2]), _seg_sums(hl, counts[:, 3]))
-    for k in range(4):
-        d = fold(fold(d, counts[:, k].astype(np.uint64)), sums[k])
-    return d, counts.astype(np.uint32)
+    sums = np.stack([_seg_sums(hc, cap), _seg_sums(hi, cap), _seg_sums(hs, counts[:, 2]), _seg_sums(hl, counts[:, 3])],
+                    1).astype(np.uint64)
+    return counts, sums
