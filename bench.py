@@ -143,6 +143,103 @@ def rows_roofline(prof, args, elapsed, out):
     return roof
 
 
+def run_sharded(args, mix, n_clients, rank, world, local, backend):
+    """North-star sharded mode. A step is one batch of
+    --topics publish topics matched by the whole node: every shard walks the full batch
+    (mq_match_spans_begin), the shards all-gather their exported cross-shard node lists (RCCL
+    all-gather over xGMI via torch.distributed; --sim-shards: through device memory on one GPU),
+    and each shard resolves its own subscriptions exactly (mq_match_spans_end). The topic's
+    Subscribers are the union of the shards' disjoint results. Total work per step is fixed as
+    shards are added ("scaling": "strong")."""
+    import numpy as np
+    import torch
+    from mqmatch import dist as D
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    sim = args.sim_shards if world == 1 else 0
+    n_shards = sim or world
+    t0 = time.time()
+    w = W.gen_subscriptions(args.subs, n_clients, seed=W.BASE_SEED, mix=mix)
+    log(f"generated {args.subs} subscriptions in {time.time()-t0:.1f}s")
+    t0 = time.time()
+    mine = range(n_shards) if sim else [rank]
+    engs = [E.Engine(device=local, expected_subs=args.subs // n_shards, shard=k, n_shards=n_shards) for k in mine]
+    for e in engs:
+        e.subscribe_bulk(w)
+    log(f"{len(engs)} shard index(es) built in {time.time()-t0:.1f}s: {[e.stats() for e in engs]}")
+    tb, to = W.gen_topics(w, args.topics, seed=D.topic_seed(0), mix=mix)  # the same batch on every shard
+    n = len(to) - 1
+    stream = torch.cuda.current_stream()
+    d_tb = torch.from_numpy(tb).to(f"cuda:{local}")
+    d_to = torch.from_numpy(to.view(np.int64)).to(f"cuda:{local}")
+    for e in engs:
+        e.sync(stream.cuda_stream)
+    torch.cuda.synchronize()
+    ents = []
+
+    def step():
+        xs = [e.match_spans_begin(d_tb.data_ptr(), d_to.data_ptr(), n, stream.cuda_stream) for e in engs]
+        ents.append(sum(int(x.n_ents) for x in xs))
+        if sim:
+            for k, e in enumerate(engs):
+                e.match_spans_end([x for j, x in enumerate(xs) if j != k], stream.cuda_stream)
+        else:
+            foreign, keep = D.exchange_xlists(xs[0], backend) if backend else ([], None)
+            engs[0].match_spans_end(foreign, stream.cuda_stream)
+            del keep
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    for e in engs:
+        e.profile(True)
+        e.profile_reset()
+    ents.clear()
+    D.barrier(backend)
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    D.barrier(backend)
+    elapsed = D.max_over_ranks(time.perf_counter() - t_start, backend)
+    profs = [e.profile_read() for e in engs]
+    ents_step = D.sum_over_ranks(sum(ents) / max(1, args.steps), backend)
+    if rank != 0:
+        D.finalize(backend)
+        return
+    kern = {}
+    for p in profs:
+        for k, v in p.items():
+            if v[1] > 0:
+                kern[k] = kern.get(k, 0.0) + v[1] / max(1, args.steps) / len(profs)
+    ms = 1000.0 * elapsed / args.steps
+    out = {
+        "metric": METRIC, "value": n / (elapsed / args.steps), "unit": "publishes/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (SURVEY.md §8d generator, seed 0x6D716D61)",
+        "config": {"workload": f"config-3 mix: {args.subs} subscriptions sharded by filter hash over {n_shards} shards, "
+                               f"{n} publish topics per step matched by every shard",
+                   "subs": args.subs, "clients": n_clients, "topics_per_step": n, "shards": n_shards,
+                   "parallelism": (f"{n_shards} shards simulated on one GPU (run in turn; exchange through device "
+                                   f"memory)" if sim else f"one shard per GPU, RCCL all-gather of the cross-shard lists"),
+                   "format": "spans"},
+        "kernels_ms_per_step_per_shard": kern,
+        "exchange": {"entries_per_topic": ents_step / n,
+                     "bytes_per_topic_exported": 16.0 * ents_step / n + 4.0 * n_shards,
+                     "note": "each shard exports 4 B of count + 16 B per cross-shard node per topic; an all-gather "
+                             "delivers every other shard's export to each shard"},
+        "roofline": None, "cpu_baseline": None,
+    }
+    if sim:
+        out["note"] = ("simulated shards run one after another on one GPU: ms_per_step is the sum of the shards' "
+                       "work, so a node with one shard per GPU would run a step in about ms_per_step / shards "
+                       "plus the exchange")
+    print(json.dumps(out), flush=True)
+    D.finalize(backend)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +254,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--select-shared", action="store_true",
                     help="MQ_CFG_SELECT_SHARED: SelectShared on the device (k_pick) in every step")
+    ap.add_argument("--shard", choices=["none", "filter"], default="none",
+                    help="filter: the north-star sharded mode (SURVEY.md §8e(ii)) — subscriptions sharded by "
+                         "filter hash over the ranks, every rank matching the same full batch, the ranks' "
+                         "cross-shard node lists all-gathered over RCCL each step (DESIGN.md §6)")
+    ap.add_argument("--sim-shards", type=int, default=0,
+                    help="one GPU: hold this many shards in one process and run the sharded step on them in "
+                         "turn (exchange through device memory): per-shard work and exchange volume")
     ap.add_argument("--format", choices=["spans", "rows"], default="spans",
                     help="spans: mq_match_spans_device (gathered lists named, merges patched); rows: "
                          "mq_match_device_chunks with every row materialised and each chunk consumed "
@@ -170,11 +274,15 @@ def main():
     from mqmatch import workload as W
 
     rank, world, local_rank = D.env_rank()
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     local = D.device_for(local_rank)
     torch.cuda.set_device(local)
     backend = D.init(local_rank)
     mix = W.MIX_IOT if args.mix == "iot" else W.MIX_MQTT
     n_clients = args.clients or (args.subs if args.mix == "iot" else max(1, args.subs // 10))
+    if args.shard == "filter" or args.sim_shards > 1:
+        return run_sharded(args, mix, n_clients, rank, world, local, backend)
 
     t0 = time.time()
     w = W.gen_subscriptions(args.subs, n_clients, seed=W.BASE_SEED, mix=mix)
