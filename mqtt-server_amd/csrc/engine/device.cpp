@@ -225,7 +225,7 @@ Device::~Device() {
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
                     &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &acl_buf_, &sp_res_,
                     &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_, &sp_compact_, &sp_roff_,
-                    &sp_work_, &x_off_, &x_ents_, &x_cnt_})
+                    &sp_work_, &x_off_, &x_ents_, &x_cnt_, &x_src_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
@@ -876,6 +876,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   EmitArgs a;
   memset(&a, 0, sizeof(a));
   a.n_xf = nf;
+  XSrc h_src[kMaxShards - 1];
   for (uint32_t f = 0; f < nf; f++) {  // import: per-topic offsets of each foreign list
     if (xf[f].n_topics != n || (xf[f].n_ents && (!xf[f].counts || !xf[f].ents)))
       throw HipError{hipErrorInvalidValue, "foreign list does not match the batch"};
@@ -883,8 +884,13 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     launch_counts(xf[f].counts, n, counts_.as<TopicCount>(), s);
     launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), x_foff_[f].as<TopicOff>(), s);
     hip_check(hipGetLastError(), "import");
-    a.xoff[f] = x_foff_[f].as<TopicOff>();
-    a.xent[f] = reinterpret_cast<const XEnt*>(xf[f].ents);
+    h_src[f] = XSrc{x_foff_[f].as<TopicOff>(), reinterpret_cast<const XEnt*>(xf[f].ents)};
+  }
+  if (nf) {
+    grow(x_src_, sizeof(h_src));
+    hip_check(hipMemcpyAsync(x_src_.p, h_src, nf * sizeof(XSrc), hipMemcpyHostToDevice, s), "H2D xsrc");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");  // h_src is on the stack
+    a.xsrc = x_src_.as<XSrc>();
   }
   a.ix = di;
   a.t0 = 0;

@@ -241,7 +241,7 @@ class Device {
   DevBuf sp_compact_, sp_roff_;      // host results: the patch regions packed
   DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
   // sharded: the exported list (offsets, entries, counts) and the imported lists' offsets
-  DevBuf x_off_, x_ents_, x_cnt_, x_foff_[kMaxShards - 1];
+  DevBuf x_off_, x_ents_, x_cnt_, x_src_, x_foff_[kMaxShards - 1];
   struct SpanBatch {               // between spans_begin and spans_end
     bool pending = false;
     uint32_t n = 0;

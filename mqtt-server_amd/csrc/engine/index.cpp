@@ -1130,41 +1130,46 @@ int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
   return 1;
 }
 
-// topics.go:453-476
+// topics.go:453-476. The Retained map (packets.Packets, topics.go:351) is kept on the particles:
+// a non-empty topic's particle is unique (its path spells the topic), so the map entry is the
+// particle's kRetainLive bit (with the packet's Retain flag, which the -1 answer reads) and the
+// entry of topic "" (retainPath "" is no path, Q6) is kept apart.
 int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
                               bool retain) {
   version_++;
   if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;  // retained: by topic
-  uint32_t n = set(topic, 0);
-  std::string t(topic);
+  const uint32_t n = set(topic, 0);
+  const bool path = !topic.empty();  // retainPath = pk.TopicName; "" means no path
+  NodeMsg& M = msg.at_w(n);
+  const bool node_live = (M.flags & kRetainLive) != 0;
   if (payload_len > 0) {
-    bool path = !topic.empty();  // retainPath = pk.TopicName; "" means no path
     nh_[n].retain_path = path;
-    NodeMsg& M = msg.at_w(n);
-    const bool was_live = M.flags & kRetainLive;
-    M.flags = (M.flags & kChildSys) | (path ? (kRetainPath | kRetainLive) : 0);
+    M.flags = (M.flags & kChildSys) | (path ? (kRetainPath | kRetainLive | (retain ? kRetainFlag : 0u)) : 0u);
     M.handle = path ? handle : 0;
     child_rec_sync(n);
-    if (path && !was_live) add_below_live(n, 1);
-    retained_[t] = RetEntry{handle, payload_len, retain};
-    if (topic.empty()) {
+    if (path && !node_live) {
+      add_below_live(n, 1);
+      n_retained_++;
+    }
+    if (!path) {
+      if (!empty_topic_live) n_retained_++;
       empty_topic_live = true;
       empty_topic_handle = handle;
+      empty_topic_retain = retain;
     }
     return 1;
   }
-  int64_t out = 0;
-  auto it = retained_.find(t);
-  if (it != retained_.end() && it->second.payload_len > 0 && it->second.retain) out = -1;
+  // -1: the replaced entry had a payload (every stored one has) and its Retain flag
+  const bool was_live = path ? node_live : empty_topic_live;
+  const bool was_retain = path ? (M.flags & kRetainFlag) != 0 : empty_topic_retain;
+  const int64_t out = was_live && was_retain ? -1 : 0;
   nh_[n].retain_path = false;
-  NodeMsg& M = msg.at_w(n);
-  const bool was_live = M.flags & kRetainLive;
   M.flags &= kChildSys;
   M.handle = 0;
   child_rec_sync(n);
-  if (was_live) add_below_live(n, -1);
-  if (it != retained_.end()) retained_.erase(it);
-  if (topic.empty()) empty_topic_live = false;
+  if (node_live) add_below_live(n, -1);
+  if (was_live) n_retained_--;
+  if (!path) empty_topic_live = false;
   trim(n);
   return out;
 }
@@ -1173,21 +1178,18 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
 int Index::retained_delete(std::string_view topic) {
   version_++;
   if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;
-  auto it = retained_.find(std::string(topic));
-  if (it == retained_.end()) return 0;
-  retained_.erase(it);
   if (topic.empty()) {
+    if (!empty_topic_live) return 0;
     empty_topic_live = false;
+    n_retained_--;
     return 1;
   }
-  uint32_t n = seek(topic, 0);
-  if (n != kNone && nh_[n].retain_path) {
-    NodeMsg& M = msg.at_w(n);
-    const bool was_live = M.flags & kRetainLive;
-    M.flags &= ~kRetainLive;
-    child_rec_sync(n);
-    if (was_live) add_below_live(n, -1);
-  }
+  const uint32_t n = seek(topic, 0);
+  if (n == kNone || !(msg.h[n].flags & kRetainLive)) return 0;
+  msg.at_w(n).flags &= ~(kRetainLive | kRetainFlag);
+  child_rec_sync(n);
+  add_below_live(n, -1);
+  n_retained_--;
   return 1;
 }
 

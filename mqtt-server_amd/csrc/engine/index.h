@@ -149,12 +149,6 @@ struct NodeHost {
   bool retain_path = false;
 };
 
-struct RetEntry {
-  uint64_t handle;
-  uint32_t payload_len;
-  bool retain;
-};
-
 // A subscription held by another shard, as this shard sees it (sharded index): what its
 // partner links need — the filter's path, for co-matchability with this shard's filters.
 struct ForeignSub {
@@ -188,7 +182,7 @@ class Index {
   int64_t retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
                          bool retain);
   int retained_delete(std::string_view topic);
-  uint64_t retained_len() const { return retained_.size(); }
+  uint64_t retained_len() const { return n_retained_; }
 
   // Device image (layout.h); the Device uploads dirty pages of these.
   Mirror<EdgeSlot> edges;
@@ -211,6 +205,7 @@ class Index {
   // Retained packet stored on topic "" (retainPath "" is "no path", Q6): literal-final
   // lookups of particles without a retain path read this entry (topics.go:573).
   bool empty_topic_live = false;
+  bool empty_topic_retain = false;
   uint64_t empty_topic_handle = 0;
 
   uint64_t edge_mask() const { return edges.size() - 1; }
@@ -315,7 +310,7 @@ class Index {
   std::vector<uint32_t> merge_dirty_;  // nodes whose device partner links are stale
   std::vector<uint8_t> merge_dirty_flag_;
   std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
-  std::unordered_map<std::string, RetEntry> retained_;
+  uint64_t n_retained_ = 0;  // live Retained entries (topic "" included)
   // sharding
   uint32_t shard_ = 0, n_shards_ = 1;
   std::vector<ForeignSub> fsubs_;

@@ -96,6 +96,12 @@ constexpr uint32_t kDescMerge = 1u << 31;
 
 constexpr uint32_t kMaxShards = 16;  // sharded index: shards a batch's exchange can join
 
+// One imported cross-shard list: per-topic offsets (.g) into its entries.
+struct XSrc {
+  const struct TopicOff* xoff;
+  const XEnt* xent;
+};
+
 // Span-format records (include/mqmatch.h mq_span / mq_patch / mq_topic_spans).
 struct SpanRec {  // one gathered particle: subs[sub_off, + n_sub), shr[shr_off, + n_shr)
   uint32_t sub_off, n_sub, shr_off, n_shr;
@@ -131,10 +137,10 @@ struct EmitArgs {
   unsigned long long* pcount;     //   reserves in region t % kPatchRegions with atomicAdd on
   uint64_t rcap;                  //   pcount[region] (may exceed rcap: the host grows the pool)
   unsigned long long* work;       // MQ_PROF_WORK: per region kWork counters (null: off)
-  // sharded index: the other shards' exported cross-shard nodes of every topic (k_xlist)
+  // sharded index: the other shards' exported cross-shard nodes of every topic (k_xlist), a
+  // device table (a kernel-argument array indexed at run time would go through scratch)
   uint32_t n_xf;
-  const TopicOff* xoff[kMaxShards - 1];  // per foreign shard: per-topic offsets (.g) into
-  const XEnt* xent[kMaxShards - 1];      //   its entries
+  const struct XSrc* xsrc;
 };
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile

@@ -638,7 +638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t w_ent = 0, w_rec = 0, w_link = 0;  // this lane's work (MQ_PROF_WORK)
 
   // reserve n patch slots for this topic in its region (wave-uniform)
-  auto reserve = [&](uint64_t n) {
+  auto reserve = [&](uint64_t n) __attribute__((always_inline)) {
     const uint32_t region = t & (kPatchRegions - 1);
     unsigned long long b = 0;
     if (lane == 0 && n) b = atomicAdd(a.pcount + region, (unsigned long long)n);
@@ -647,7 +647,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     pbase = (uint64_t)region * a.rcap + b;
   };
   // one patch per lane that wants one, compacted by ballot (wave-uniform)
-  auto emit_patch = [&](bool want, uint32_t row, uint32_t meta) {
+  auto emit_patch = [&](bool want, uint32_t row, uint32_t meta) __attribute__((always_inline)) {
     const uint64_t m = __ballot(want);
     if (want && pfit) a.patches[pbase + n_patch + prefix_before(m)] = PatchRec{row, meta};
     n_patch += (uint32_t)__popcll(m);
@@ -695,12 +695,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // n_map.. (their partner links name them kForeign | fid; their rank keys order them)
     uint32_t n_ent = n_map;
     for (uint32_t f = 0; XS && f < a.n_xf; f++) {
-      const uint64_t x0 = a.xoff[f][t].g, x1 = a.xoff[f][t + 1].g;
+      const XSrc src = a.xsrc[f];
+      const uint64_t x0 = src.xoff[t].g, x1 = src.xoff[t + 1].g;
       for (uint64_t k0 = x0; k0 < x1; k0 += 64) {
         const uint64_t k = k0 + lane;
         const uint32_t x = n_ent + (uint32_t)(k - x0);
         if (k < x1 && x < kEnt && n_map <= kPairMax) {
-          const XEnt e = a.xent[f][k];
+          const XEnt e = src.xent[k];
           const uint32_t key = kForeign | e.fid;
           uint32_t sl = hash32(key) & (kMapSlots - 1);
           while (atomicCAS(&map_key[wv][sl], kNone, key) != kNone) sl = (sl + 1) & (kMapSlots - 1);
@@ -715,44 +716,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     wave_sync_lds();
     const bool slow = n_map > kPairMax || n_ent > kEnt;  // beyond the map: linear lookups
     // Is node h (or kForeign | fid) gathered for this topic? Its DFS position: rank key, then
-    // gather index (kNone for another shard's node).
-    auto gathered = [&](uint32_t h, uint64_t* rk, uint32_t* gi) -> bool {
+    // gather index (kNone for another shard's node); found = false otherwise.
+    struct Pos {
+      uint64_t rk;
+      uint32_t gi;
+      bool found;
+    };
+    auto gathered = [&](uint32_t h) __attribute__((always_inline)) -> Pos {
       if (!slow) {
         uint32_t sl = hash32(h) & (kMapSlots - 1);
         for (;;) {
           const uint32_t k = map_key[wv][sl];
           if (k == h) {
             const uint32_t y = map_val[wv][sl];
-            *rk = XS ? mg_rank[wv][y] : 0ull;
-            *gi = mg_gi[wv][y];
-            return true;
+            return Pos{XS ? mg_rank[wv][y] : 0ull, mg_gi[wv][y], true};
           }
-          if (k == kNone) return false;
+          if (k == kNone) return Pos{0, kNone, false};
           sl = (sl + 1) & (kMapSlots - 1);
         }
       }
       if (XS && (h & kForeign)) {
-        for (uint32_t f = 0; f < a.n_xf; f++)
-          for (uint64_t k = a.xoff[f][t].g; k < a.xoff[f][t + 1].g; k++)
-            if ((kForeign | a.xent[f][k].fid) == h) {
-              *rk = a.xent[f][k].rank;
-              *gi = kNone;
-              return true;
-            }
-        return false;
+        for (uint32_t f = 0; f < a.n_xf; f++) {
+          const XSrc src = a.xsrc[f];
+          for (uint64_t k = src.xoff[t].g; k < src.xoff[t + 1].g; k++)
+            if ((kForeign | src.xent[k].fid) == h) return Pos{src.xent[k].rank, kNone, true};
+        }
+        return Pos{0, kNone, false};
       }
       for (uint32_t i = 0; i < n_g; i++) {
         const GDesc d = gd[i];
-        if ((d.word & kGatherNode) == h && (d.word & kGatherSubs)) {
-          *rk = rank_of(d);
-          *gi = i;
-          return true;
-        }
+        if ((d.word & kGatherNode) == h && (d.word & kGatherSubs)) return Pos{rank_of(d), i, true};
       }
-      return false;
+      return Pos{0, kNone, false};
     };
     // does the gathered node at (rh, gh) come before the record's own (rg, gg) in DFS order?
-    auto before = [&](uint64_t rh, uint32_t gh, uint64_t rg, uint32_t gg) -> bool {
+    auto before = [&](uint64_t rh, uint32_t gh, uint64_t rg, uint32_t gg) __attribute__((always_inline)) -> bool {
       if (!XS) return gh < gg;
       if (rh != rg) return rh < rg;
       if (gh != kNone) return gh < gg;  // both on this shard: gather order is DFS order
@@ -771,7 +769,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // mw: the record's meta | kSlotIdentPos when its identifier is > 0 (PairSlot.meta); (rg, gi):
     // its gather's rank key and gather index.
     auto resolve = [&](bool active, uint32_t mw, uint32_t row, uint64_t rg, uint32_t gi, uint32_t via,
-                       uint32_t mp_off, uint32_t mp_cnt) {
+                       uint32_t mp_off, uint32_t mp_cnt) __attribute__((always_inline)) {
       bool counted = false, nonbase = false, want = false;
       uint32_t pmeta = 0;
       if (active) {
@@ -790,12 +788,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (uint32_t u = 0; u < kPartBatch; u++) {
             if (!base || pb[u].node == kNone) continue;
-            uint64_t rh;
-            uint32_t gh;
-            if (!gathered(pb[u].node, &rh, &gh)) continue;
+            const Pos ph = gathered(pb[u].node);
+            if (!ph.found) continue;
             if (!bound) first = pb[u].node;
             bound = true;
-            if (before(rh, gh, rg, gi)) {
+            if (before(ph.rk, ph.gi, rg, gi)) {
               base = false;
               continue;
             }
@@ -826,7 +823,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // whose client also subscribes at h. Hit lists are staged in LDS and their concatenation
       // is resolved 64 records per wave-instruction.
       uint32_t n_hit = 0, tot = 0;
-      auto flush_hits = [&]() {
+      auto flush_hits = [&]() __attribute__((always_inline)) {
         if (lane == 0) h_pre[wv][n_hit] = tot;
         wave_sync_lds();
         for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
@@ -853,7 +850,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // counting = false: stage and resolve (flush) as the lists come.
       uint64_t tot_all = 0;
       bool staged_all = true;
-      auto pairs = [&](bool counting) {
+      auto pairs = [&](bool counting) __attribute__((always_inline)) {
         const uint32_t np = n_map * n_ent;  // (g: a merge gather here, h: any entry)
         for (uint32_t p0 = 0; p0 < np; p0 += 64) {
           const uint32_t p = p0 + lane;
@@ -1061,7 +1058,8 @@ void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_bloc
   const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
   const dim3 g(blocks), b(256);
   if (spans && a.ix.xinfo) {  // sharded index
-    hipLaunchKernelGGL((k_merge<true, true, 1>), g, b, 0, s, a);
+    if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, true, 1>), g, b, 0, s, a);
   } else if (spans) {
     if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8>), g, b, 0, s, a);
     else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6>), g, b, 0, s, a);

@@ -114,6 +114,7 @@ struct NodeLists {
 constexpr uint32_t kRetainPath = 1u;  // particle.retainPath != "" (topics.go:755)
 constexpr uint32_t kRetainLive = 2u;  // Retained map holds the path (Q12 decouples the two)
 constexpr uint32_t kChildSys = 4u;    // key == "$SYS" under the root (topics.go:549)
+constexpr uint32_t kRetainFlag = 8u;  // host only: the live packet's FixedHeader.Retain
 struct NodeMsg {
   uint32_t child_off, child_cnt;  // children slab (ChildRec) for '+'/'#' enumeration
   uint32_t flags;                 // kRetainPath | kRetainLive | kChildSys
