@@ -180,13 +180,10 @@ int mq_subscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs,
                       const int32_t* identifiers, uint64_t n, uint8_t* out_new) {
   if (n && (!bytes || !offs || !client_ids || !filter_ids || !qos || !flags || !identifiers))
     return fail(MQ_EINVAL, "null column");
+  for (uint64_t i = 0; i < n; i++)
+    if (qos[i] > 2) return fail(MQ_EINVAL, "qos > 2");
   return guarded(idx, [&] {
-    for (uint64_t i = 0; i < n; i++) {
-      if (qos[i] > 2) return fail(MQ_EINVAL, "qos > 2");
-      int r = idx->ix->subscribe(std::string_view((const char*)bytes + offs[i], offs[i + 1] - offs[i]),
-                                 client_ids[i], filter_ids[i], qos[i], flags[i], identifiers[i]);
-      if (out_new) out_new[i] = (uint8_t)r;
-    }
+    idx->ix->subscribe_bulk(bytes, offs, client_ids, filter_ids, qos, flags, identifiers, n, out_new);
     return 0;
   }, true);
 }
@@ -195,9 +192,7 @@ int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, co
                    uint64_t n) {
   if (n && (!bytes || !offs || !handles)) return fail(MQ_EINVAL, "null column");
   return guarded(idx, [&] {
-    for (uint64_t i = 0; i < n; i++)
-      idx->ix->retain_message(std::string_view((const char*)bytes + offs[i], offs[i + 1] - offs[i]),
-                              handles[i], 1, true);
+    idx->ix->retain_bulk(bytes, offs, handles, n);
     return 0;
   }, true);
 }

@@ -60,6 +60,26 @@ void HashU64::put(uint64_t k, uint32_t v) {
   }
 }
 
+void HashU64::build_parallel(const uint64_t* keys, const uint32_t* vals, size_t n, unsigned threads) {
+  rehash(std::max<size_t>(n * 2 + 16, 16));
+  const size_t m = keys_.size() - 1;
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t j = b; j < e; j++) {
+      size_t i = slot(keys[j]);
+      for (;;) {
+        uint64_t expect = kEmpty;
+        if (__atomic_compare_exchange_n(&keys_[i], &expect, keys[j], false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+          vals_[i] = vals[j];
+          break;
+        }
+        i = (i + 1) & m;
+      }
+    }
+  });
+  n_ = n;
+  tombs_ = 0;
+}
+
 bool HashU64::erase(uint64_t k) {
   size_t m = keys_.size() - 1, i = slot(k);
   for (;;) {
@@ -122,7 +142,7 @@ void Index::path_of(std::string_view filter, int d, std::vector<std::string_view
     out.push_back(segs.back());
 }
 
-static std::string_view segment_at(std::string_view filter, int d) {  // isolateParticle value
+std::string_view segment_at(std::string_view filter, int d) {  // isolateParticle value
   size_t s = 0;
   for (int i = 0;; i++) {
     size_t e = filter.find('/', s);
@@ -268,9 +288,11 @@ uint32_t Index::find_child(uint32_t parent, const SegKey& k, std::string_view se
   }
 }
 
-void Index::edge_rehash(size_t cap) {
-  std::vector<EdgeSlot> old;
+void Index::edge_rehash(size_t cap, unsigned threads) {
+  std::vector<EdgeSlot> old, fresh;
+  reserve_resident(fresh, cap, threads);
   old.swap(edges.h);
+  edges.h.swap(fresh);
   edges.h.assign(cap, EdgeSlot{0, 0, kEdgeEmpty, kNone, 0, 0});
   edges.epoch++;
   edges.all_dirty = true;
@@ -912,7 +934,7 @@ void Index::foreign_unsubscribe(uint32_t client, uint32_t fid) {
 // (topics.go:406-411): its owner hashes the group and the particle's path — "$share/g/a" and
 // "$SHARE/g/a" are one key, and so are "$share/g" and "$share/g/g" (Q13: a short filter's
 // particle is its last segment, isolateParticle beyond range). Others hash the filter.
-static std::string shard_key(std::string_view filter, bool share) {
+std::string shard_key(std::string_view filter, bool share) {
   if (!share) return std::string(filter);
   std::string k(segment_at(filter, 1));
   k.push_back('\0');
@@ -1193,4 +1215,9 @@ int Index::retained_delete(std::string_view topic) {
   return 1;
 }
 
+}  // namespace mq
+
+namespace mq {
+// used by the bulk build (index_bulk.cpp)
+template void Index::list_push<ShrRec, ShrRec>(SlabPool<ShrRec>&, uint32_t&, uint32_t&, uint32_t&, const ShrRec&);
 }  // namespace mq

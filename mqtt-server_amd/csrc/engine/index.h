@@ -8,8 +8,12 @@
 // rather than rebuilt.
 #pragma once
 
+#include <sys/mman.h>
+
+#include <algorithm>
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <string_view>
 #include <unordered_map>
 #include <vector>
@@ -17,6 +21,28 @@
 #include "layout.h"
 
 namespace mq {
+
+// Grows v's capacity to at least n elements and makes the unused capacity resident — huge
+// pages where the kernel allows them, faulted in by `threads` threads — so that a bulk build's
+// first touch of a multi-GB array is not one thread's page-fault storm. Contents are unchanged.
+template <class T>
+void reserve_resident(std::vector<T>& v, size_t n, unsigned threads) {
+  if (n > v.capacity()) v.reserve(n);
+  constexpr uintptr_t kPage = 4096;
+  const uintptr_t b = ((uintptr_t)(v.data() + v.size()) + kPage - 1) & ~(kPage - 1);
+  const uintptr_t e = (uintptr_t)(v.data() + v.capacity()) & ~(kPage - 1);
+  if (e <= b || e - b < (64u << 20)) return;  // small: the ordinary faults are cheap
+  madvise((void*)b, e - b, MADV_HUGEPAGE);
+  constexpr uintptr_t kHuge = 2u << 20;
+  const unsigned t = std::max(1u, std::min<unsigned>(threads, (unsigned)((e - b) / (32u << 20))));
+  const uintptr_t per = ((e - b) / t + kHuge - 1) & ~(kHuge - 1);
+  std::vector<std::thread> th;
+  for (unsigned k = 0; k < t; k++) {
+    const uintptr_t lo = b + k * per, hi = std::min(e, lo + per);
+    if (lo < hi) th.emplace_back([lo, hi] { madvise((void*)lo, hi - lo, MADV_POPULATE_WRITE); });  // best effort
+  }
+  for (auto& x : th) x.join();
+}
 
 // A host vector mirrored into device memory; tracks which pages changed since the last sync.
 template <class T>
@@ -45,6 +71,13 @@ struct Mirror {
   T& at_w(size_t i) {  // write access
     mark(i);
     return h[i];
+  }
+  void reserve_resident(size_t n, unsigned threads) {  // capacity for n, resident (bulk builds)
+    if (n > h.capacity()) {
+      epoch++;
+      all_dirty = true;
+    }
+    mq::reserve_resident(h, n, threads);
   }
   void grow_to(size_t n, const T& fill) {
     if (n <= h.size()) return;
@@ -92,12 +125,31 @@ struct SlabPool {
   }
 };
 
+// Runs f(begin, end) over [0, n) split into contiguous pieces on up to `threads` threads.
+template <class F>
+void parallel_for(size_t n, unsigned threads, F&& f) {
+  threads = std::max(1u, std::min<unsigned>(threads, (unsigned)((n + 4095) / 4096)));
+  if (threads <= 1) {
+    if (n) f((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (n + threads - 1) / threads;
+  for (unsigned t = 0; t < threads; t++) {
+    const size_t b = std::min(n, t * per), e = std::min(n, b + per);
+    if (b < e) th.emplace_back([&f, b, e] { f(b, e); });
+  }
+  for (auto& x : th) x.join();
+}
+
 // Open-addressing u64 -> u32 map (linear probing), used for (node, client) positions.
 class HashU64 {
  public:
   explicit HashU64(size_t cap = 1024) { rehash(cap); }
   bool get(uint64_t k, uint32_t* v) const;
   void put(uint64_t k, uint32_t v);
+  // Replace the contents with n distinct keys (bulk build; threads insert with CAS).
+  void build_parallel(const uint64_t* keys, const uint32_t* vals, size_t n, unsigned threads);
   bool erase(uint64_t k);
   size_t size() const { return n_; }
   void reserve(size_t n) {
@@ -181,6 +233,14 @@ class Index {
   int inline_unsubscribe(std::string_view filter, int32_t ident);
   int64_t retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
                          bool retain);
+  // Restore path (server.go:1624-1640 loadSubscriptions, 1688-1692 loadRetained): the same as
+  // calling subscribe / retain_message per entry, in order. On an empty index the image is
+  // built directly in parallel passes (index_bulk.cpp); otherwise entry by entry.
+  void subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uint32_t* client_ids,
+                      const uint32_t* filter_ids, const uint8_t* qos, const uint8_t* flags,
+                      const int32_t* idents, uint64_t n, uint8_t* out_new);
+  void retain_bulk(const uint8_t* bytes, const uint64_t* offs, const uint64_t* handles, uint64_t n);
+  bool empty_image() const;
   int retained_delete(std::string_view topic);
   uint64_t retained_len() const { return n_retained_; }
 
@@ -238,7 +298,7 @@ class Index {
   void add_below_live(uint32_t n, int delta);
   void edge_insert(uint32_t parent, const SegKey& k, uint32_t child);
   void edge_erase(uint32_t parent, const SegKey& k, uint32_t child);
-  void edge_rehash(size_t cap);
+  void edge_rehash(size_t cap, unsigned threads = 1);
   uint32_t intern_str(std::string_view s);
 
   // subscription list primitives (positions are absolute pool indices)
@@ -250,6 +310,10 @@ class Index {
   bool compatible_foreign(uint32_t a, const ForeignSub& f) const;
   static bool compatible_strs(const uint32_t* pa, int la, const uint32_t* pb, int lb);
   void path_strs(uint32_t n, uint32_t* out, int* len) const;
+  // bulk build helpers (index_bulk.cpp)
+  struct BulkItem;
+  void bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsigned threads);
+  void bulk_children(uint32_t first_new, unsigned threads);
   // sharded: a non-shared subscription owned by another shard (Subscribe / Unsubscribe)
   int foreign_subscribe(std::string_view filter, uint32_t client, uint32_t fid, uint32_t meta);
   void foreign_unsubscribe(uint32_t client, uint32_t fid);
@@ -324,5 +388,9 @@ class Index {
 
 // strings.EqualFold(s, "$SHARE") under Go's Unicode simple folding (Q9: U+017F ~ 's').
 bool is_share_prefix(std::string_view s);
+// isolateParticle(filter, d)'s value (topics.go:679-698)
+std::string_view segment_at(std::string_view filter, int d);
+// the key a sharded index owns a subscription by (index.cpp)
+std::string shard_key(std::string_view filter, bool share);
 
 }  // namespace mq
