@@ -39,6 +39,23 @@ def log(msg):
     print(f"[bench_messages {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def handle_digests(base, count, hs):
+    """Per-filter digest of the sorted handles, as the oracle's messages_digest_batch computes
+    it (fold of the count, then of each handle in ascending order), vectorised over filters."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from digest import fold, SEED
+    n = len(count)
+    m = int(count.max()) if n else 0
+    mat = np.zeros((n, max(m, 1)), np.uint64)
+    for i in range(n):
+        mat[i, :count[i]] = np.sort(hs[int(base[i]):int(base[i]) + int(count[i])])
+    d = fold(np.full(n, SEED, np.uint64), count.astype(np.uint64))
+    for k in range(m):
+        live = count > k
+        d = np.where(live, fold(d, mat[:, k]), d)
+    return d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--retained", type=int, default=10_000_000)
@@ -48,6 +65,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--walk", action="store_true",
+                    help="Messages by the particle walk (MQ_OPT_MSG_IMAGE 0) instead of the level-order image")
     args = ap.parse_args()
     heartbeat()
     import torch
@@ -62,6 +81,8 @@ def main():
     log(f"generated {len(ro) - 1} retained topics, {n} filters in {time.time() - t0:.1f}s")
     t0 = time.time()
     eng = E.Engine(device=0)
+    if args.walk:
+        eng.set_option(E.OPT_MSG_IMAGE, 0)
     eng.retain_bulk(rb, ro, hd)
     log(f"engine index built in {time.time() - t0:.1f}s: {eng.stats()}")
     stream = torch.cuda.current_stream()
@@ -73,10 +94,11 @@ def main():
     def step():
         return eng.messages_device(d_fb.data_ptr(), d_fo.data_ptr(), n, stream.cuda_stream)
 
+    eng.profile(True)  # the first step builds the level-order image: timed apart
     for _ in range(args.warmup):
         r = step()
     torch.cuda.synchronize()
-    eng.profile(True)
+    build = eng.profile_read().get("msg_image")
     eng.profile_reset()
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -95,6 +117,8 @@ def main():
                                f"{n} wildcard filters per step", "retained": len(ro) - 1, "filters": n},
         "handles_per_step": handles, "handles_per_filter": handles / max(1, n),
         "kernels_ms_per_step": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
+        "path": "particle walk (k_msg)" if args.walk else "level-order image (k_msgq + k_msg_copy)",
+        "image_build_ms": build[1] if build else None,
     }
     cpu = None
     if not args.no_cpu:
@@ -105,7 +129,8 @@ def main():
         ns = min(n, 4096)
         dg, cnt, tot = orc.messages_digest_batch(fb, fo[:ns + 1], nthreads=16)
         base, count, hs = eng.messages_batch(fb, fo[:ns + 1])
-        out["parity_sample"] = {"filters": ns, "counts_equal": bool((count == cnt).all())}
+        out["parity_sample"] = {"filters": ns, "counts_equal": bool((count == cnt).all()),
+                                "digests_equal": bool((handle_digests(base, count, hs) == dg).all())}
         per = {k: v / ns for k, v in tot.items()}
         b = 8 * per["L"] + 4 + 16 * per["P"] + 16 * per["O"]
         out["alg_bytes_per_filter"] = {"B": b, **per, "sample_filters": ns}

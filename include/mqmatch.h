@@ -406,6 +406,8 @@ int mq_index_check(mq_index* idx);
 #define MQ_OPT_SERIAL 5          /* 1: no side-stream overlap (isolated kernel timings) */
 #define MQ_OPT_PATCH_CAP 6       /* span format: initial patch pool capacity (patches) */
 #define MQ_OPT_MERGE_WAVES 7     /* k_merge waves per SIMD the registers are budgeted for (1, 6, 8) */
+#define MQ_OPT_MSG_IMAGE 8       /* Messages: 1 (default) runs over the level-order retained image;
+                                    0 walks the particles (the path the Q6 state always takes) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. enable: 0 off,

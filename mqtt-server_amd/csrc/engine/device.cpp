@@ -213,6 +213,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_SERIAL: serial_ = v != 0; return true;
     case MQ_OPT_PATCH_CAP: patch_cap_init_ = std::max<uint64_t>(v, 64); return true;
     case MQ_OPT_MERGE_WAVES: merge_wpe_opt_ = (uint32_t)v; return true;
+    case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     default: return false;
   }
 }
@@ -225,7 +226,8 @@ Device::~Device() {
   for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
                     &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &acl_buf_, &sp_res_,
                     &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_, &sp_compact_, &sp_roff_,
-                    &sp_work_, &x_off_, &x_ents_, &x_cnt_, &x_src_})
+                    &sp_work_, &x_off_, &x_ents_, &x_cnt_, &x_src_, &img_node_, &img_pos_, &img_cl_,
+                    &img_lp_, &img_h_, &img_cnt_, &img_coff_, &img_bsum_, &img_bpre_, &msg_pieces_})
     b->release();
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
@@ -1081,24 +1083,120 @@ void Device::acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
 }
 
-void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
-                      hipStream_t s, HostMsg* host, mq_msg_result* out) {
-  hip_check(hipSetDevice(dev_), "hipSetDevice");
-  sync(ix, s);
-  *out = mq_msg_result{};
-  if (host) *host = HostMsg{};
-  if (!err_.p) {
-    err_.ensure(2 * sizeof(uint32_t));
-    hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
+// The level-order retained image (kernels.h MsgImg): level by level from the root, a count pass
+// (image children per parent), a scan (their positions), a fill pass; then the live handles are
+// packed in image order. Rebuilt when the retained state changed since the last build.
+void Device::ensure_img(const Index& ix, const DevIndex& di, hipStream_t s) {
+  if (img_version_ == ix.retained_version()) return;
+  const uint32_t slots = std::max<uint32_t>(ix.node_slots(), 1);
+  img_node_.ensure((size_t)slots * sizeof(uint32_t));
+  img_cl_.ensure((size_t)slots * sizeof(uint2));
+  img_lp_.ensure(((size_t)slots + 1) * sizeof(uint32_t));
+  img_pos_.ensure((size_t)slots * sizeof(uint32_t));
+  img_cnt_.ensure(((size_t)slots + 1) * sizeof(uint32_t));
+  img_coff_.ensure(((size_t)slots + 1) * sizeof(uint32_t));
+  const size_t nb = ((size_t)slots + kScanBlock) / kScanBlock + 1;
+  img_bsum_.ensure(nb * sizeof(uint32_t));
+  img_bpre_.ensure(nb * sizeof(uint32_t));
+  prof.begin(s);
+  hip_check(hipMemsetAsync(img_pos_.p, 0xFF, (size_t)slots * sizeof(uint32_t), s), "hipMemsetAsync(img pos)");
+  launch_img_root(img_node_.as<uint32_t>(), img_pos_.as<uint32_t>(), img_lp_.as<uint32_t>(), s);
+  ImgLevelArgs a;
+  a.node = img_node_.as<uint32_t>();
+  a.pos = img_pos_.as<uint32_t>();
+  a.cl = img_cl_.as<uint2>();
+  a.live = img_lp_.as<uint32_t>();  // live flags, scanned in place into lp below
+  a.cnt = img_cnt_.as<uint32_t>();
+  a.coff = img_coff_.as<uint32_t>();
+  uint32_t lo = 0, n = 1, levels = 0;
+  while (n) {
+    a.lo = lo;
+    a.n = n;
+    a.next = lo + n;
+    launch_img_level(false, di, a, s);
+    launch_scan32(a.cnt, n, img_bsum_.as<uint32_t>(), img_bpre_.as<uint32_t>(), img_coff_.as<uint32_t>(), s);
+    uint32_t next_n = 0;
+    hip_check(hipMemcpyAsync(&next_n, img_coff_.as<uint32_t>() + n, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+              "D2H image level");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if ((uint64_t)a.next + next_n > slots) throw HipError{hipErrorUnknown, "messages image beyond the node count"};
+    launch_img_level(true, di, a, s);
+    hip_check(hipGetLastError(), "k_img_level");
+    lo += n;
+    n = next_n;
+    levels++;
+  }
+  launch_scan32(img_lp_.as<uint32_t>(), lo, img_bsum_.as<uint32_t>(), img_bpre_.as<uint32_t>(),
+                img_lp_.as<uint32_t>(), s);
+  uint32_t live = 0;
+  hip_check(hipMemcpyAsync(&live, img_lp_.as<uint32_t>() + lo, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+            "D2H image live");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  img_h_.ensure(std::max<size_t>(live, 1) * sizeof(uint64_t));
+  launch_img_compact(di, img_node_.as<uint32_t>(), img_lp_.as<uint32_t>(), lo, img_h_.as<uint64_t>(), s);
+  hip_check(hipGetLastError(), "k_img_compact");
+  prof.end("msg_image", s);
+  img_n_ = lo;
+  img_n_pos_ = slots;
+  img_levels_ = levels;
+  img_live_ = live;
+  img_version_ = ix.retained_version();
+}
+
+MsgImg Device::msg_img() const {
+  MsgImg m;
+  m.node = img_node_.as<uint32_t>();
+  m.pos = img_pos_.as<uint32_t>();
+  m.cl = img_cl_.as<uint2>();
+  m.lp = img_lp_.as<uint32_t>();
+  m.h = img_h_.as<uint64_t>();
+  m.n = img_n_;
+  m.n_pos = img_n_pos_;
+  return m;
+}
+
+// k_msgq count pass, scan, fill pass, k_msg_copy. Returns false (nothing written) when a filter's
+// fan-out nesting exceeded kMsgStack: the batch then takes the particle walk.
+bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
+                          hipStream_t s, TopicOff* tot) {
+  const MsgImg img = msg_img();
+  const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+  prof.begin(s);
+  launch_msgq(false, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, nullptr,
+              s);
+  prof.end("msgq_count", s);
+  hip_check(hipGetLastError(), "k_msgq<count>");
+  launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
+  hip_check(hipGetLastError(), "k_scan");
+  uint32_t e = 0;
+  hip_check(hipMemcpyAsync(tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H total");
+  hip_check(hipMemcpyAsync(&e, err_.p, sizeof(e), hipMemcpyDeviceToHost, s), "D2H err");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (e == kErrMsgNest) {
+    hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
+    return false;
   }
   check_err(s);
-  if (n == 0) return;
-  const DevIndex di = dev_index(ix);
+  msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
+  msg_base_.ensure((size_t)n * sizeof(uint64_t));
+  msg_count_.ensure((size_t)n * sizeof(uint32_t));
+  msg_pieces_.ensure(std::max<uint64_t>(tot->g, 1) * sizeof(MsgPiece));
+  prof.begin(s);
+  launch_msgq(true, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
+              msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
+              msg_count_.as<uint32_t>(), s);
+  prof.end("msgq_fill", s);
+  hip_check(hipGetLastError(), "k_msgq<fill>");
+  prof.begin(s);
+  launch_msg_copy(msg_pieces_.as<MsgPiece>(), tot->g, img.h, msg_handles_.as<uint64_t>(), s);
+  prof.end("msg_copy", s);
+  hip_check(hipGetLastError(), "k_msg_copy");
+  return true;
+}
+
+void Device::messages_walk(Index& ix, const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
+                           hipStream_t s, TopicOff* tot) {
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
-  counts_.ensure((size_t)n * sizeof(TopicCount));
-  offs_.ensure((size_t)(n + 1) * sizeof(TopicOff));
-  bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
-  bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
   // k_msg register budget: on a large retained index the walk waits on HBM far more often, and
   // 6 waves per SIMD (with spills) beat 4 (10M retained: 54.8 -> 50.2 ms per 100k filters); on
   // a small, cache-resident one the spills cost more (1M: 8.7 vs 9.2 ms). MQ_MSG_WPE overrides.
@@ -1119,11 +1217,10 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   hip_check(hipGetLastError(), "k_msg<count>");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
   hip_check(hipGetLastError(), "k_scan");
-  TopicOff tot;
-  hip_check(hipMemcpyAsync(&tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H total");
+  hip_check(hipMemcpyAsync(tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H total");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   check_err(s);
-  msg_handles_.ensure(std::max<uint64_t>(tot.rows, 1) * sizeof(uint64_t));
+  msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
   msg_base_.ensure((size_t)n * sizeof(uint64_t));
   msg_count_.ensure((size_t)n * sizeof(uint32_t));
   if (cap) {
@@ -1138,6 +1235,35 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
              msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), spec, cap, msg_wpe, s);
   prof.end("msg_fill", s);
   hip_check(hipGetLastError(), "k_msg<fill>");
+}
+
+void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
+                      hipStream_t s, HostMsg* host, mq_msg_result* out) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  sync(ix, s);
+  *out = mq_msg_result{};
+  if (host) *host = HostMsg{};
+  if (!err_.p) {
+    err_.ensure(2 * sizeof(uint32_t));
+    hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
+  }
+  check_err(s);
+  if (n == 0) return;
+  const DevIndex di = dev_index(ix);
+  const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+  counts_.ensure((size_t)n * sizeof(TopicCount));
+  offs_.ensure((size_t)(n + 1) * sizeof(TopicOff));
+  bsum_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+  bpre_.ensure((size_t)(nb + 1) * sizeof(TopicOff));
+  TopicOff tot{0, 0, 0, 0, 0};
+  // The image path needs Retained.Get("") only on particles with a retain path; with the Q6
+  // entry live, a literal level can emit on any particle, which the particle walk covers.
+  bool done = false;
+  if (msg_img_on_ && !ix.empty_topic_live && ix.retained_len() != 0) {
+    ensure_img(ix, di, s);
+    done = messages_img(di, d_fb, d_fo, n, s, &tot);
+  }
+  if (!done) messages_walk(ix, di, d_fb, d_fo, n, s, &tot);
   out->n_filters = n;
   out->base = msg_base_.as<uint64_t>();
   out->count = msg_count_.as<uint32_t>();

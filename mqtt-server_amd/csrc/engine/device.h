@@ -186,6 +186,15 @@ class Device {
   // walk (count) + scan of n topics; returns the batch totals (synchronises s)
   TopicOff walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                      const uint32_t** gathers, uint32_t* gstride);
+  // Messages: the level-order retained image (rebuilt when ix.retained_version() moved) and the
+  // two query paths — run arithmetic over the image (k_msgq) and the particle walk (k_msg:
+  // the Q6 state, nesting beyond kMsgStack, MQ_OPT_MSG_IMAGE = 0)
+  void ensure_img(const Index& ix, const DevIndex& di, hipStream_t s);
+  MsgImg msg_img() const;
+  bool messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
+                    TopicOff* tot);
+  void messages_walk(Index& ix, const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
+                     hipStream_t s, TopicOff* tot);
 
   int dev_;
   uint64_t synced_version_ = ~0ull;
@@ -251,6 +260,12 @@ class Device {
   } sb_;
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
   uint64_t patch_cap_init_ = 1ull << 24;
+  DevBuf img_node_, img_pos_, img_cl_, img_lp_, img_h_, img_cnt_, img_coff_, img_bsum_, img_bpre_;
+  DevBuf msg_pieces_;               // k_msgq copy pieces of a batch
+  uint64_t img_version_ = ~0ull;    // ix.retained_version() the image was built at
+  uint32_t img_n_ = 0, img_n_pos_ = 0, img_levels_ = 0;
+  uint64_t img_live_ = 0;
+  bool msg_img_on_ = true;          // MQ_OPT_MSG_IMAGE
   DevBuf msg_spec_;              // speculative-count scratch: spec_cap handles per filter
   uint64_t msg_spec_bytes_ = 0;  // its budget (MQ_MSG_SPEC_MB)
   uint32_t msg_wpe_opt_ = 0;     // k_msg variant (MQ_OPT_MSG_WAVES; 0: by index size)

@@ -1159,6 +1159,7 @@ int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
 int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
                               bool retain) {
   version_++;
+  retained_version_++;
   if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;  // retained: by topic
   const uint32_t n = set(topic, 0);
   const bool path = !topic.empty();  // retainPath = pk.TopicName; "" means no path
@@ -1199,6 +1200,7 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
 // Retained.Delete (server.go:1726): the map entry only; the particle keeps retainPath (Q12).
 int Index::retained_delete(std::string_view topic) {
   version_++;
+  retained_version_++;
   if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;
   if (topic.empty()) {
     if (!empty_topic_live) return 0;

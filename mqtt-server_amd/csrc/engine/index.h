@@ -274,6 +274,10 @@ class Index {
   uint64_t n_subs_merge() const { return n_merge_; }
   uint32_t max_depth() const { return max_depth_; }
   uint64_t version() const { return version_; }
+  // bumped by every change of the retained state (live set or handles): the device's Messages
+  // image is rebuilt when it moved
+  uint64_t retained_version() const { return retained_version_; }
+  uint32_t node_slots() const { return (uint32_t)nh_.size(); }  // node ids are below this
   // Rebuild the device partner links of nodes whose may-merge slots, partner lists or
   // partners' positions changed since the last call (the Device calls this before uploading).
   // O(partner links of those nodes).
@@ -347,6 +351,7 @@ class Index {
   uint64_t n_live_nodes_ = 0, n_edges_ = 0, n_tombs_ = 0, n_merge_ = 0;
   uint32_t max_depth_ = 0;
   uint64_t version_ = 0;
+  uint64_t retained_version_ = 0;
 
   StrTable strs_;
   std::unordered_map<std::string, uint32_t> long_segs_;  // long segment -> SegInfo index

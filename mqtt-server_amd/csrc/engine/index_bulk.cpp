@@ -650,6 +650,7 @@ void Index::retain_bulk(const uint8_t* bytes, const uint64_t* offs, const uint64
     return;
   }
   version_++;
+  retained_version_++;
   const unsigned threads = build_threads();
   std::vector<uint8_t> mine(n, 1);
   std::vector<BulkItem> items;

@@ -225,4 +225,58 @@ void launch_patch_compact(const PatchRec* pool, uint64_t rcap, const unsigned lo
 void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
                       uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
 
+// ---------------------------------------------------------------------------------------------
+// Messages over the level-order retained image. The image holds the particles
+// with a live retained message at or below them, level by level, each particle's image children
+// consecutive and in its parent's order (the root's "$SYS" child last), so that
+//   - the image children of a consecutive run [a, b) of one level are the consecutive run
+//     [cl[a].x, cl[b - 1].y) of the next level;
+//   - the live handles of a run are the consecutive run [lp[a], lp[b]) of h.
+// A '+' level of a filter maps a run to a run, a final '+' or '#' emits whole runs of h; only a
+// literal level below a wildcard fans out into lookups.
+struct MsgImg {
+  const uint32_t* node;  // image position -> particle
+  const uint32_t* pos;   // particle -> image position (valid iff node[pos[p]] == p; n_pos entries)
+  const uint2* cl;       // image position -> [x, y) image positions of its image children
+  const uint32_t* lp;    // image position -> live particles before it in the image (n + 1)
+  const uint64_t* h;     // live handles in image order
+  uint32_t n, n_pos;
+};
+// A run of h copied to the output: out[dst + k] = h[h0 + k], k < len.
+struct MsgPiece {
+  uint32_t h0, len;
+  uint64_t dst;
+};
+constexpr uint32_t kMsgPiece = 4096;    // handles per copy piece (a wavefront's work item)
+constexpr uint32_t kMsgDirect = 8;      // runs this short are copied by the walk itself
+constexpr uint32_t kMsgStack = 16;      // nested fan-outs a lane can hold (deeper: kErrMsgNest)
+constexpr uint32_t kErrMsgNest = 16u;   // k_msgq: fan-out nesting beyond kMsgStack (walk k_msg)
+
+// u32 exclusive scan: out[i] = in[0] + ... + in[i - 1], out[n] = total (out may be in).
+// bsum / bpre: ceil(n / kScanBlock) + 1 entries each.
+void launch_scan32(const uint32_t* in, uint64_t n, uint32_t* bsum, uint32_t* bpre, uint32_t* out,
+                   hipStream_t s);
+// Image build, one level: the image children of the level's positions [lo, lo + n).
+// fill = false: cnt[p] = their number; fill = true (coff = scan of cnt): written from `next` on.
+struct ImgLevelArgs {
+  uint32_t* node;
+  uint32_t* pos;
+  uint2* cl;
+  uint32_t* live;  // per image position: 1 if the particle's retained message is live
+  uint32_t* cnt;
+  const uint32_t* coff;
+  uint32_t lo, n, next;
+};
+void launch_img_root(uint32_t* node, uint32_t* pos, uint32_t* live, hipStream_t s);
+void launch_img_level(bool fill, const DevIndex& ix, const ImgLevelArgs& a, hipStream_t s);
+// h[lp[q]] = handle of node[q] for the live positions (lp: the scan of live)
+void launch_img_compact(const DevIndex& ix, const uint32_t* node, const uint32_t* lp, uint32_t n,
+                        uint64_t* h, hipStream_t s);
+// Messages count (fill = false: TopicCount.gathers = pieces, .rows = handles) or fill pass
+// (pieces at off[t].g, short runs copied directly, base / count written).
+void launch_msgq(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                 const MsgImg& img, TopicCount* cnt, const TopicOff* off, MsgPiece* pieces,
+                 uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
+void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s);
+
 }  // namespace mq

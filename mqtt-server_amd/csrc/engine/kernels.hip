@@ -1652,4 +1652,405 @@ void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, co
                      base, count);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Messages over the level-order retained image (kernels.h MsgImg): the reverse
+// retained scan (topics.go:530-579) as run arithmetic. A '+' or '#' level with more segments
+// after it takes every image child of the run (its particles' children that have live retained
+// state at or below them: the others add nothing), a final '+' emits the children's live
+// handles, a final '#' every level below (isolateParticle repeats the last segment past the end,
+// topics.go:679-698), the root's "$SYS" child excluded at level 0 (topics.go:549, Q4). A literal
+// level looks the segment up under each particle of the run (topics.go:568-576); under a run of
+// more than one particle this is the only fan-out: the wave's lanes take the run's particles,
+// and a lane keeps deeper fan-outs on a small frame stack.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t block_scan_incl32(uint32_t v, uint32_t* wt /*4*/) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t tot;
+  const uint32_t ex = wave_excl_scan(v, lane, &tot);
+  if (lane == 0) wt[wv] = tot;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t w = 0; w < wv; w++) add += wt[w];
+  __syncthreads();
+  return ex + v + add;
+}
+
+__global__ __launch_bounds__(256) void k_scan32_reduce(const uint32_t* __restrict__ in, uint64_t n,
+                                                       uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t wt[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++)
+    if (base + k < n) v += in[base + k];
+  v = block_scan_incl32(v, wt);
+  if (threadIdx.x == 255) bsum[blockIdx.x] = v;
+}
+
+// Single workgroup: exclusive scan of the block sums; bpre[nb] = total.
+__global__ __launch_bounds__(256) void k_scan32_blocks(const uint32_t* __restrict__ bsum, uint32_t nb,
+                                                       uint32_t* __restrict__ bpre) {
+  __shared__ uint32_t wt[4];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t v = b < nb ? bsum[b] : 0u;
+    const uint32_t incl = block_scan_incl32(v, wt);
+    if (b < nb) bpre[b] = carry + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 255) carry += incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bpre[nb] = carry;
+}
+
+// in and out may alias: every thread reads its four elements before any is written
+__global__ __launch_bounds__(256) void k_scan32_apply(const uint32_t* in, uint64_t n,
+                                                      const uint32_t* __restrict__ bpre, uint32_t* out) {
+  __shared__ uint32_t wt[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  uint32_t c[4], v = 0;
+  for (int k = 0; k < 4; k++) {
+    c[k] = base + k < n ? in[base + k] : 0u;
+    v += c[k];
+  }
+  const uint32_t incl = block_scan_incl32(v, wt);
+  uint32_t ex = bpre[blockIdx.x] + incl - v;
+  for (int k = 0; k < 4; k++) {
+    if (base + k < n) out[base + k] = ex;
+    ex += c[k];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = bpre[gridDim.x];
+}
+
+void launch_scan32(const uint32_t* in, uint64_t n, uint32_t* bsum, uint32_t* bpre, uint32_t* out,
+                   hipStream_t s) {
+  if (n == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(uint32_t), s);  // errors surface at the caller's next check
+    return;
+  }
+  const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+  hipLaunchKernelGGL(k_scan32_reduce, dim3(nb), dim3(256), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(k_scan32_blocks, dim3(1), dim3(256), 0, s, bsum, nb, bpre);
+  hipLaunchKernelGGL(k_scan32_apply, dim3(nb), dim3(256), 0, s, in, n, bpre, out);
+}
+
+__global__ void k_img_root(uint32_t* node, uint32_t* pos, uint32_t* live) {
+  if (threadIdx.x == 0) {
+    node[0] = kRoot;
+    pos[kRoot] = 0;
+    live[0] = 0;  // the root has no retain path ("" is kept apart, Q6)
+  }
+}
+
+// Wavefront per parent of the level: its children slab (ChildRec) in slab order; a child is in
+// the image when its own retained message is live or one below it is (NodeMsg.below_live).
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_img_level(DevIndex ix, ImgLevelArgs a) {
+  const uint32_t lane = threadIdx.x & 63, wv = wave_id();
+  const uint32_t p = blockIdx.x * 4 + wv;
+  if (p >= a.n) return;  // wave-uniform
+  const uint32_t v = a.node[a.lo + p];
+  const NodeMsg m = ix.msg[v];
+  const bool root = v == kRoot;
+  const uint32_t base = FILL ? a.next + a.coff[p] : 0u;
+  uint32_t run = 0;
+  uint32_t sys_node = kNone, sys_live = 0;  // the root's "$SYS" child goes last
+  if (m.below_live != 0) {
+    for (uint32_t k0 = 0; k0 < m.child_cnt; k0 += 64) {  // wave-uniform
+      const uint32_t k = k0 + lane;
+      bool incl = false, live = false, sys = false;
+      uint32_t c = kNone;
+      if (k < m.child_cnt) {
+        const ChildRec r = ix.children[m.child_off + k];
+        c = r.node;
+        live = (r.flags & kRetainPath) && (r.flags & kRetainLive);
+        incl = live || ix.msg[c].below_live != 0;
+        sys = root && (r.flags & kChildSys);
+      }
+      const uint64_t bm = __ballot(incl && !sys);
+      if (FILL && incl && !sys) {
+        const uint32_t q = base + run + prefix_before(bm);
+        a.node[q] = c;
+        a.pos[c] = q;
+        a.live[q] = live ? 1u : 0u;
+      }
+      if (incl && sys) {
+        sys_node = c;
+        sys_live = live ? 1u : 0u;
+      }
+      run += (uint32_t)__popcll(bm);
+    }
+  }
+  const bool has_sys = __ballot(sys_node != kNone) != 0;
+  if (FILL && sys_node != kNone) {
+    const uint32_t q = base + run;
+    a.node[q] = sys_node;
+    a.pos[sys_node] = q;
+    a.live[q] = sys_live;
+  }
+  const uint32_t total = run + (has_sys ? 1u : 0u);
+  if (lane == 0) {
+    if (FILL) a.cl[a.lo + p] = make_uint2(base, base + total);
+    else a.cnt[p] = total;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_img_compact(DevIndex ix, const uint32_t* __restrict__ node,
+                                                     const uint32_t* __restrict__ lp, uint32_t n,
+                                                     uint64_t* __restrict__ h) {
+  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t l = lp[q];
+  if (lp[q + 1] != l) h[l] = ix.msg[node[q]].handle;
+}
+
+void launch_img_root(uint32_t* node, uint32_t* pos, uint32_t* live, hipStream_t s) {
+  hipLaunchKernelGGL(k_img_root, dim3(1), dim3(64), 0, s, node, pos, live);
+}
+
+void launch_img_level(bool fill, const DevIndex& ix, const ImgLevelArgs& a, hipStream_t s) {
+  if (!a.n) return;
+  const dim3 g((a.n + 3) / 4), b(256);
+  if (fill) hipLaunchKernelGGL(k_img_level<true>, g, b, 0, s, ix, a);
+  else hipLaunchKernelGGL(k_img_level<false>, g, b, 0, s, ix, a);
+}
+
+void launch_img_compact(const DevIndex& ix, const uint32_t* node, const uint32_t* lp, uint32_t n,
+                        uint64_t* h, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_img_compact, dim3((n + 255) / 256), dim3(256), 0, s, ix, node, lp, n, h);
+}
+
+// Image position of particle c, or kNone (not in the image: no live retained at or below it).
+__device__ __forceinline__ uint32_t img_pos(const MsgImg& img, uint32_t c) {
+  if (c >= img.n_pos) return kNone;  // kNone included
+  const uint32_t q = img.pos[c];
+  return (q < img.n && img.node[q] == c) ? q : kNone;
+}
+
+struct MsgFrame {  // a fan-out in progress: particles [cur, end) still to take segment s
+  uint32_t cur, end, s;
+};
+
+// FILL=false: counts the filter's handles and copy pieces; FILL=true: writes short runs and
+// piece records at the offsets of the count pass's scan. Wavefront per filter.
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, const uint64_t* __restrict__ fo,
+                                              uint32_t n, DevIndex ix, MsgImg img,
+                                              TopicCount* __restrict__ cnt, const TopicOff* __restrict__ off,
+                                              MsgPiece* __restrict__ pieces, uint64_t* __restrict__ handles,
+                                              uint64_t* __restrict__ base_out, uint32_t* __restrict__ count_out) {
+  __shared__ uint32_t hcur[4], pcur[4];  // FILL: next handle / piece of the wave's filter
+  const uint32_t lane = threadIdx.x & 63, wv = wave_id();
+  const uint32_t t = blockIdx.x * 4 + wv;
+  if (t >= n) return;  // wave-uniform
+  const uint64_t b0 = fo[t], b1 = fo[t + 1];
+  const uint64_t obase = FILL ? off[t].rows : 0, pbase = FILL ? off[t].g : 0;
+  if (FILL) {
+    if (lane == 0) hcur[wv] = pcur[wv] = 0;
+    wave_sync_lds();
+  }
+  uint32_t nh = 0, np = 0;  // count pass: this lane's handles and pieces
+  auto emit = [&](uint32_t h0, uint32_t len) __attribute__((always_inline)) {
+    if (len == 0) return;
+    const uint32_t npc = len > kMsgDirect ? (len + kMsgPiece - 1) / kMsgPiece : 0u;
+    if (!FILL) {
+      nh += len;
+      np += npc;
+      return;
+    }
+    const uint32_t dst = atomicAdd(&hcur[wv], len);
+    if (!npc) {
+      for (uint32_t k = 0; k < len; k++) handles[obase + dst + k] = img.h[h0 + k];
+      return;
+    }
+    const uint32_t slot = atomicAdd(&pcur[wv], npc);
+    for (uint32_t i = 0; i < npc; i++)
+      pieces[pbase + slot + i] = MsgPiece{h0 + i * kMsgPiece, (uint32_t)min(kMsgPiece, len - i * kMsgPiece),
+                                          obase + dst + (uint64_t)i * kMsgPiece};
+  };
+  // image children of the run [a, b) (a < b); at level 0 without "$SYS" (topics.go:549)
+  auto desc = [&](uint32_t a, uint32_t b, uint32_t& x, uint32_t& y) __attribute__((always_inline)) {
+    x = img.cl[a].x;
+    y = img.cl[b - 1].y;
+    if (a == 0 && y > x && (ix.msg[img.node[y - 1]].flags & kChildSys)) y--;
+  };
+  // a final '+' (one level) or '#' (every level below) over the children run [x, y)
+  auto emit_final = [&](bool hash, uint32_t x, uint32_t y) __attribute__((always_inline)) {
+    for (uint32_t guard = 0; x < y && guard < 4096; guard++) {
+      emit(img.lp[x], img.lp[y] - img.lp[x]);
+      if (!hash) break;
+      const uint32_t nx = img.cl[x].x, ny = img.cl[y - 1].y;
+      x = nx;
+      y = ny;
+    }
+  };
+  if (b1 > b0 && ix.retained_len != 0) {  // topics.go:535
+    ByteReader R(fb);
+    bool w = false;
+    for (uint64_t i = b0 + lane; i < b1; i += 64) {
+      const uint32_t ch = fb[i];
+      w |= (ch == '+') | (ch == '#');
+    }
+    if (!__any(w)) {  // Retained.Get(filter) (topics.go:539-544)
+      uint32_t node = kRoot;
+      SegKey key;
+      uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
+      for (;;) {
+        node = lookup(ix, node, key, fb + s, (uint32_t)(e - s));
+        if (node == kNone || e >= b1) break;
+        s = e + 1;
+        e = scan_segment(R, s, b1, &key);
+      }
+      if (lane == 0 && node != kNone && (ix.msg[node].flags & kRetainLive)) {
+        const uint32_t q = img_pos(img, node);
+        if (q != kNone) emit(img.lp[q], 1u);
+      }
+    } else {
+      // wave-uniform: the run [a, b) that segment s applies to, until a literal meets a longer run
+      uint32_t a = 0, b = 1;
+      uint64_t s = b0;
+      bool fan = false;
+      for (uint32_t guard = 0; guard < 4096; guard++) {
+        const uint64_t e = find_slash(R, s, b1);
+        const bool last = e >= b1;
+        const uint32_t len = (uint32_t)(e - s);
+        const uint32_t c0 = len == 1 ? R.at(s) : 0u;
+        if (c0 == '+' || c0 == '#') {  // topics.go:547-565
+          uint32_t x, y;
+          desc(a, b, x, y);
+          if (last) {
+            if (lane == 0) emit_final(c0 == '#', x, y);
+            break;
+          }
+          a = x;
+          b = y;
+          s = e + 1;
+          if (a >= b) break;
+          continue;
+        }
+        if (b - a > 1) {
+          fan = true;
+          break;
+        }
+        SegKey key = key_of(R, s, e);
+        const uint32_t qc = img_pos(img, lookup(ix, img.node[a], key, fb + s, len));
+        if (qc == kNone) break;
+        if (last) {
+          if (lane == 0) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+          break;
+        }
+        a = qc;
+        b = qc + 1;
+        s = e + 1;
+      }
+      if (fan) {  // lanes take the run's particles; each walks the rest of the filter alone
+        MsgFrame st[kMsgStack];
+        for (uint32_t u = a + lane; u < b; u += 64) {
+          uint32_t sp = 0, ua = u, ub = u + 1;
+          uint64_t us = s;
+          for (uint64_t guard = 0;; guard++) {
+            if (guard > kWalkGuard) {
+              atomicOr(ix.err, kErrWalkGuard);
+              break;
+            }
+            bool pop = false;
+            const uint64_t e = find_slash(R, us, b1);
+            const bool last = e >= b1;
+            const uint32_t len = (uint32_t)(e - us);
+            const uint32_t c0 = len == 1 ? R.at(us) : 0u;
+            if (c0 == '+' || c0 == '#') {
+              uint32_t x, y;
+              desc(ua, ub, x, y);
+              if (last) {
+                emit_final(c0 == '#', x, y);
+                pop = true;
+              } else {
+                ua = x;
+                ub = y;
+                us = e + 1;
+                pop = ua >= ub;
+              }
+            } else if (ub - ua > 1) {  // a literal under a run: one particle now, the rest later
+              if (sp == kMsgStack) {
+                atomicOr(ix.err, kErrMsgNest);
+                break;
+              }
+              st[sp++] = MsgFrame{ua + 1, ub, (uint32_t)(us - b0)};
+              ub = ua + 1;
+            } else {
+              SegKey key = key_of(R, us, e);
+              const uint32_t qc = img_pos(img, lookup(ix, img.node[ua], key, fb + us, len));
+              if (qc == kNone) {
+                pop = true;
+              } else if (last) {
+                emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+                pop = true;
+              } else {
+                ua = qc;
+                ub = qc + 1;
+                us = e + 1;
+              }
+            }
+            if (pop) {
+              if (sp == 0) break;
+              MsgFrame& f = st[sp - 1];
+              ua = f.cur;
+              ub = ua + 1;
+              us = b0 + f.s;
+              if (++f.cur >= f.end) sp--;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (!FILL) {
+    nh = wave_sum(nh);
+    np = wave_sum(np);
+    if (lane == 0) cnt[t] = TopicCount{np, nh, 0, 0, 0};
+  } else if (lane == 0) {
+    base_out[t] = obase;
+    count_out[t] = cnt[t].rows;
+  }
+}
+
+void launch_msgq(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                 const MsgImg& img, TopicCount* cnt, const TopicOff* off, MsgPiece* pieces,
+                 uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s) {
+  if (!n) return;
+  const dim3 g((n + 3) / 4), b(256);
+  if (fill)
+    hipLaunchKernelGGL(k_msgq<true>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count);
+  else
+    hipLaunchKernelGGL(k_msgq<false>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count);
+}
+
+// Wavefront per piece: four 64-handle loads in flight per lane, then the stores.
+__global__ __launch_bounds__(256) void k_msg_copy(const MsgPiece* __restrict__ pieces, uint64_t n,
+                                                  const uint64_t* __restrict__ h, uint64_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t i = (uint64_t)blockIdx.x * 4 + wave_id();
+  if (i >= n) return;
+  const MsgPiece p = pieces[i];
+  const uint64_t* src = h + p.h0;
+  uint64_t* dst = out + p.dst;
+  uint32_t k = lane;
+  for (; k + 192 < p.len; k += 256) {
+    const uint64_t v0 = src[k], v1 = src[k + 64], v2 = src[k + 128], v3 = src[k + 192];
+    __builtin_nontemporal_store(v0, dst + k);
+    __builtin_nontemporal_store(v1, dst + k + 64);
+    __builtin_nontemporal_store(v2, dst + k + 128);
+    __builtin_nontemporal_store(v3, dst + k + 192);
+  }
+  for (; k < p.len; k += 64) __builtin_nontemporal_store(src[k], dst + k);
+}
+
+void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, pieces, n, h, out);
+}
+
 }  // namespace mq

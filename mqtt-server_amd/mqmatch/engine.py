@@ -76,6 +76,7 @@ PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 # mq_set_option (include/mqmatch.h MQ_OPT_*)
 OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP, OPT_MERGE_WAVES = \
     1, 2, 3, 4, 5, 6, 7
+OPT_MSG_IMAGE = 8
 
 
 class MsgResult(C.Structure):

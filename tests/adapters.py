@@ -73,10 +73,12 @@ def canonical(subs):
 class EngineAdapter:
     name = "engine"
 
-    def __init__(self, fmt="spans"):
+    def __init__(self, fmt="spans", msg_image=True):
         from mqmatch import engine as E
         self.E = E
         self.x = E.TopicsIndex(0, fmt=fmt)
+        if not msg_image:  # Messages by the particle walk instead of the level-order image
+            self.x.engine.set_option(E.OPT_MSG_IMAGE, 0)
         self._h = 0
 
     def subscribe(self, client, filter, qos=0, identifier=0, no_local=False, rap=False, rh=0):

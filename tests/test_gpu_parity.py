@@ -403,20 +403,27 @@ def test_spans_result_pins_host_image(gpu_available):
 MSEGS = ["a", "b", "c", "", "$SYS", "$share", "g", "x", "averyveryverylongsegment", "ü", "$x"]
 
 
+@pytest.mark.parametrize("image", [True, False])
+@pytest.mark.parametrize("q6", [False, True])
 @pytest.mark.parametrize("seed", range(6))
-def test_messages_random_parity(seed, gpu_available):
+def test_messages_random_parity(seed, q6, image, gpu_available):
     """Messages (topics.go:525-579) on random retained sets, including Q4 ($SYS at level 0
-    only), Q5 (x/# excludes x), Q6 (particles without a retain path), Q12 (expired entries)."""
+    only), Q5 (x/# excludes x), Q6 (particles without a retain path; q6: a retained entry on
+    topic "" is live, which the level-order image path hands to the particle walk), Q12 (expired
+    entries). image: the level-order image (default) or the particle walk (MQ_OPT_MSG_IMAGE)."""
     r = random.Random(2000 + seed)
     topics = ["/".join(r.choice(MSEGS) for _ in range(r.randint(1, 5))) for _ in range(300)]
-    e, o = EngineAdapter(), OracleAdapter()
+    topics = [t for t in topics if t != ""] + ([""] if q6 else [])
+    e, o = EngineAdapter(msg_image=image), OracleAdapter()
     for i, t in enumerate(topics):
-        pl = b"" if r.random() < 0.1 else b"p"
+        pl = b"" if (r.random() < 0.1 and t != "") else b"p"
         ret = r.random() < 0.9
         a, _ = e.retain_message(t, pl, ret, handle=i + 1)
         b, _ = o.retain_message(t, pl, ret, handle=i + 1)
         assert a == b, t
     for t in topics[::13]:  # expiry sweep deletes map entries only (Q12)
+        if t == "":
+            continue
         e.retained_delete(t)
         o.retained_delete(t)
     for f in ["a/b", "q", "x/y"]:  # subscription-only particles (no retain path)
@@ -425,7 +432,53 @@ def test_messages_random_parity(seed, gpu_available):
     filters = ["/".join(r.choice(MSEGS + ["+", "+", "#"]) for _ in range(r.randint(1, 5)))
                for _ in range(300)]
     filters += ["#", "+", "+/+", "$SYS/#", "$SYS/+", "a/#", "a/+/#", "", "a", "a/b", "#/a",
-                "+/#", "a/#/b"]
+                "+/#", "a/#/b", "+/+/+", "+/a/+", "+/+/#", "$SYS", "+/$SYS/#"]
+    got = e.messages_batch(filters)
+    for f, g in zip(filters, got):
+        assert g == o.messages(f), f
+
+
+@pytest.mark.parametrize("image", [True, False])
+def test_messages_after_retained_changes(image, gpu_available):
+    """Retained changes between Messages batches (new topics, payload-less deletes, expiry
+    sweeps, handle replacement): each batch sees the current state (the image is rebuilt)."""
+    r = random.Random(77)
+    e, o = EngineAdapter(msg_image=image), OracleAdapter()
+    segs = ["a", "b", "c", "d", "$SYS", "x"]
+    filters = ["#", "+", "+/+", "a/#", "+/b/#", "a/+", "+/+/+", "$SYS/#", "a/b", "+/c/+", "x/+/+/#"]
+    handle = 0
+    for round_ in range(8):
+        for _ in range(60):
+            t = "/".join(r.choice(segs) for _ in range(r.randint(1, 4)))
+            u = r.random()
+            handle += 1
+            if u < 0.7:
+                assert e.retain_message(t, b"p", True, handle=handle)[0] == \
+                    o.retain_message(t, b"p", True, handle=handle)[0]
+            elif u < 0.85:
+                assert e.retain_message(t, b"", True, handle=handle)[0] == \
+                    o.retain_message(t, b"", True, handle=handle)[0]
+            else:
+                e.retained_delete(t)
+                o.retained_delete(t)
+        got = e.messages_batch(filters)
+        for f, g in zip(filters, got):
+            assert g == o.messages(f), (round_, f)
+
+
+def test_messages_deep_fanout(gpu_available):
+    """A filter whose literal levels meet runs of two particles 18 times over nests fan-outs
+    beyond a lane's frame stack (kMsgStack): the batch takes the particle walk, exactly."""
+    e, o = EngineAdapter(), OracleAdapter()
+    depth = 18
+    h = 0
+    for i in range(1, depth + 1):
+        chain = "/".join(["p", "k"] * i)
+        for t in (chain, chain[:-1] + "q", chain[:-3] + "q"):  # siblings at '+' levels
+            h += 1
+            e.retain_message(t, b"p", True, handle=h)
+            o.retain_message(t, b"p", True, handle=h)
+    filters = ["/".join(["+", "k"] * depth), "/".join(["+", "k"] * 3), "+/k/+/k/#", "#"]
     got = e.messages_batch(filters)
     for f, g in zip(filters, got):
         assert g == o.messages(f), f
@@ -443,11 +496,12 @@ def test_messages_empty_topic_retained(gpu_available):
         assert e.messages(f) == o.messages(f), f
 
 
-@pytest.mark.parametrize("spec_mb", [None, 0, 3])
-def test_messages_workload_parity(spec_mb, gpu_available):
-    """Messages on a config-5-shaped workload. spec_mb: the speculative count's scratch budget
-    (default: one walk for most filters; "0": count and fill walks; "3": a few hundred slots per
-    filter, so that many filters overflow their scratch and are walked again)."""
+@pytest.mark.parametrize("image,spec_mb", [(True, None), (False, None), (False, 0), (False, 3)])
+def test_messages_workload_parity(image, spec_mb, gpu_available):
+    """Messages on a config-5-shaped workload, over the level-order image (default) and the
+    particle walk. spec_mb (walk): the speculative count's scratch budget (default: one walk for
+    most filters; "0": count and fill walks; "3": a few hundred slots per filter, so that many
+    filters overflow their scratch and are walked again)."""
     from mqmatch import workload as W
     from mqmatch import engine as E
     rb, ro, hd, rh = W.gen_retained(100000, n_sys=1000, seed=61)
@@ -455,6 +509,8 @@ def test_messages_workload_parity(spec_mb, gpu_available):
     eng, orc = E.Engine(), O.OracleIndex()
     if spec_mb is not None:
         eng.set_option(E.OPT_MSG_SPEC_MB, spec_mb)
+    if not image:
+        eng.set_option(E.OPT_MSG_IMAGE, 0)
     eng.retain_bulk(rb, ro, hd)
     orc.retain_bulk(rb, ro, hd)
     base, count, hs = eng.messages_batch(fb, fo)
