@@ -119,6 +119,16 @@ int mq_retain_message(mq_index* idx, const char* topic, uint32_t tlen, uint64_t 
  * the map entry only; the particle keeps its retain path (Q12). Returns 1 if it existed. */
 int mq_retained_delete(mq_index* idx, const char* topic, uint32_t tlen);
 
+/* TopicsIndex.Retained.Add(topic, pk) called outside RetainMessage (packets/packets.go:79-83; the
+ * Go shim's Retained wrapper forwards it): the map entry (re)appears. Wildcard scans reach an
+ * entry through a particle whose retain path is the topic (topics.go:555): such a particle's
+ * entry becomes live with `handle` (Q12 re-add), and the "" entry is Q6's. Returns 1 then, 0 when
+ * the topic has no particle with a retain path — only a literal filter's Retained.Get(filter)
+ * sees such an entry (topics.go:539-544), and the caller's packet map answers that. payload_len
+ * and retain: the packet's, for RetainMessage's -1 answer (topics.go:467). */
+int mq_retained_set(mq_index* idx, const char* topic, uint32_t tlen, uint64_t handle, uint32_t payload_len,
+                    uint8_t retain);
+
 /* TopicsIndex.Retained.Len() (server.go:980) */
 uint64_t mq_retained_len(const mq_index* idx);
 

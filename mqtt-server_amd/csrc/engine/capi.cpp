@@ -169,6 +169,14 @@ int mq_retained_delete(mq_index* idx, const char* topic, uint32_t tlen) {
   return guarded(idx, [&] { return idx->ix->retained_delete(std::string_view(topic, tlen)); }, true);
 }
 
+int mq_retained_set(mq_index* idx, const char* topic, uint32_t tlen, uint64_t handle, uint32_t payload_len,
+                    uint8_t retain) {
+  if (bad_str(topic, tlen)) return fail(MQ_EINVAL, "null topic");
+  return guarded(idx, [&] {
+    return idx->ix->retained_set(std::string_view(topic, tlen), handle, payload_len, retain != 0);
+  }, true);
+}
+
 uint64_t mq_retained_len(const mq_index* idx) {
   if (!idx) return 0;
   std::lock_guard<std::mutex> lk(idx->lk->mu);

@@ -80,8 +80,14 @@ void DevMirror<T>::release() {
   cap = 0;
 }
 
+void Stager::add(void* dst, const void* src, size_t n) {
+  for (size_t o = 0; o < n; o += kScatterRun)
+    runs.push_back(Run{(uint8_t*)dst + o, (const uint8_t*)src + o, std::min<size_t>(kScatterRun, n - o)});
+  bytes += n;
+}
+
 template <class T>
-void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded) {
+void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager& st) {
   const size_t n = m.size();
   bool full = m.all_dirty;
   if (!d || m.epoch != epoch || cap < n) {
@@ -91,23 +97,32 @@ void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded) {
     epoch = m.epoch;
     full = true;
   }
+  const size_t pp = Mirror<T>::per_page();
+  const size_t npages = (n + pp - 1) / pp;
+  if (!full) {  // mostly dirty: one plain copy
+    size_t dp = 0;
+    for (size_t w = 0; w < m.dirty.size(); w++) dp += (size_t)__builtin_popcountll(m.dirty[w]);
+    full = dp * 4 > npages * 3;
+  }
   if (full) {
     if (n) hip_check(hipMemcpyAsync(d, m.h.data(), n * sizeof(T), hipMemcpyHostToDevice, s), "H2D mirror");
     *uploaded += n * sizeof(T);
   } else {
-    const size_t pp = Mirror<T>::per_page();
-    const size_t npages = (n + pp - 1) / pp;
     size_t p = 0;
-    while (p < npages) {
-      if (!(p / 64 < m.dirty.size() && (m.dirty[p / 64] >> (p % 64)) & 1)) {
-        p++;
+    while (p < npages) {  // runs of consecutive dirty pages; clean words are skipped whole
+      const size_t w = p / 64;
+      if (w >= m.dirty.size()) break;
+      const uint64_t bits = m.dirty[w] >> (p % 64);
+      if (!bits) {
+        p = (w + 1) * 64;
         continue;
       }
-      size_t q = p;
+      p += (size_t)__builtin_ctzll(bits);
+      if (p >= npages) break;
+      size_t q = p + 1;
       while (q < npages && q / 64 < m.dirty.size() && ((m.dirty[q / 64] >> (q % 64)) & 1)) q++;
       const size_t a = p * pp, b = std::min(n, q * pp);
-      hip_check(hipMemcpyAsync(d + a, m.h.data() + a, (b - a) * sizeof(T), hipMemcpyHostToDevice, s),
-                "H2D dirty pages");
+      st.add(d + a, m.h.data() + a, (b - a) * sizeof(T));
       *uploaded += (b - a) * sizeof(T);
       p = q;
     }
@@ -227,8 +242,13 @@ Device::~Device() {
                     &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &acl_buf_, &sp_res_,
                     &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_, &sp_compact_, &sp_roff_,
                     &sp_work_, &x_off_, &x_ents_, &x_cnt_, &x_src_, &img_node_, &img_pos_, &img_cl_,
-                    &img_lp_, &img_h_, &img_cnt_, &img_coff_, &img_bsum_, &img_bpre_, &msg_pieces_})
+                    &img_lp_, &img_h_, &img_cnt_, &img_coff_, &img_bsum_, &img_bpre_, &msg_pieces_, &d_stage_})
     b->release();
+  if (stage_done_) {
+    (void)hipEventSynchronize(stage_done_);
+    (void)hipEventDestroy(stage_done_);
+  }
+  pinned_free(h_stage_, h_stage_bytes_);
   for (int k = 0; k < 2; k++) {
     for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
     if (copy_done_[k]) (void)hipEventDestroy(copy_done_[k]);
@@ -269,22 +289,51 @@ void Device::sync(Index& ix, hipStream_t s) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   if (ix.version() == synced_version_ && edges_.d) return;
   ix.flush_merge();
-  edges_.sync(ix.edges, s, &uploaded_);
-  walk_.sync(ix.walk, s, &uploaded_);
-  lists_.sync(ix.lists, s, &uploaded_);
-  msg_.sync(ix.msg, s, &uploaded_);
-  seginfo_.sync(ix.seginfo, s, &uploaded_);
-  segbytes_.sync(ix.segbytes, s, &uploaded_);
-  subs_.sync(ix.subs.m, s, &uploaded_);
-  mref_.sync(ix.mref, s, &uploaded_);
-  mpart_.sync(ix.mpart.m, s, &uploaded_);
-  npair_.sync(ix.npair, s, &uploaded_);
-  pent_.sync(ix.pent.m, s, &uploaded_);
-  plist_.sync(ix.plist.m, s, &uploaded_);
-  shr_.sync(ix.shr.m, s, &uploaded_);
-  inl_.sync(ix.inl.m, s, &uploaded_);
-  children_.sync(ix.children.m, s, &uploaded_);
-  if (ix.sharded()) xinfo_.sync(ix.xinfo, s, &uploaded_);
+  Stager& st = stager_;
+  st.runs.clear();
+  st.bytes = 0;
+  edges_.sync(ix.edges, s, &uploaded_, st);
+  walk_.sync(ix.walk, s, &uploaded_, st);
+  lists_.sync(ix.lists, s, &uploaded_, st);
+  msg_.sync(ix.msg, s, &uploaded_, st);
+  seginfo_.sync(ix.seginfo, s, &uploaded_, st);
+  segbytes_.sync(ix.segbytes, s, &uploaded_, st);
+  subs_.sync(ix.subs.m, s, &uploaded_, st);
+  mref_.sync(ix.mref, s, &uploaded_, st);
+  mpart_.sync(ix.mpart.m, s, &uploaded_, st);
+  npair_.sync(ix.npair, s, &uploaded_, st);
+  pent_.sync(ix.pent.m, s, &uploaded_, st);
+  plist_.sync(ix.plist.m, s, &uploaded_, st);
+  shr_.sync(ix.shr.m, s, &uploaded_, st);
+  inl_.sync(ix.inl.m, s, &uploaded_, st);
+  children_.sync(ix.children.m, s, &uploaded_, st);
+  if (ix.sharded()) xinfo_.sync(ix.xinfo, s, &uploaded_, st);
+  if (!st.runs.empty()) {  // one staging buffer: the run table, then each run's bytes
+    const size_t table = (st.runs.size() * sizeof(ScatterRun) + 15) & ~size_t(15);
+    const size_t need = table + st.bytes + 16 * st.runs.size();
+    if (stage_done_) hip_check(hipEventSynchronize(stage_done_), "hipEventSynchronize(stage)");
+    else hip_check(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming), "hipEventCreate");
+    if (h_stage_bytes_ < need) {
+      pinned_free(h_stage_, h_stage_bytes_);
+      h_stage_ = pinned_alloc(need);
+      h_stage_bytes_ = need;
+    }
+    d_stage_.ensure(need);
+    uint8_t* hs = static_cast<uint8_t*>(h_stage_);
+    ScatterRun* tab = reinterpret_cast<ScatterRun*>(hs);
+    size_t o = table;
+    for (size_t k = 0; k < st.runs.size(); k++) {
+      const Stager::Run& r = st.runs[k];
+      o += ((uintptr_t)r.dst - o) & 15;  // source and destination agree mod 16
+      memcpy(hs + o, r.src, r.bytes);
+      tab[k] = ScatterRun{(uint64_t)(uintptr_t)r.dst, o, r.bytes};
+      o += r.bytes;
+    }
+    hip_check(hipMemcpyAsync(d_stage_.p, hs, o, hipMemcpyHostToDevice, s), "H2D staging");
+    launch_scatter(d_stage_.as<ScatterRun>(), (uint32_t)st.runs.size(), d_stage_.as<uint8_t>(), s);
+    hip_check(hipGetLastError(), "k_scatter");
+    hip_check(hipEventRecord(stage_done_, s), "hipEventRecord(stage)");
+  }
   retained_len_ = ix.retained_len();
   empty_live_ = ix.empty_topic_live;
   empty_handle_ = ix.empty_topic_handle;

@@ -30,12 +30,25 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Dirty runs of the host mirrors collected by one Device::sync (host source, device target).
+struct Stager {
+  struct Run {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  std::vector<Run> runs;
+  size_t bytes = 0;
+  void add(void* dst, const void* src, size_t n);  // split into runs of <= kScatterRun
+};
+
 template <class T>
 struct DevMirror {
   T* d = nullptr;
   size_t cap = 0;
   uint64_t epoch = ~0ull;
-  void sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded);
+  // reallocated or mostly dirty: uploaded whole now; else its dirty pages go to `st`
+  void sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager& st);
   void release();
 };
 
@@ -242,6 +255,11 @@ class Device {
   void ensure_streams();
   void pinned(size_t bytes);
   DevBuf err_;
+  Stager stager_;
+  DevBuf d_stage_;                 // the staging buffer on the device
+  void* h_stage_ = nullptr;        // ... and its pinned host side
+  size_t h_stage_bytes_ = 0;
+  hipEvent_t stage_done_ = nullptr;  // the last scatter finished reading both
   hipStream_t side_ = nullptr;
   hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_;

@@ -1217,6 +1217,33 @@ int Index::retained_delete(std::string_view topic) {
   return 1;
 }
 
+// Retained.Add outside RetainMessage (mq_retained_set): the entry of a particle whose retain path
+// is the topic becomes live again (Q12 re-add); the "" entry is kept apart (Q6).
+int Index::retained_set(std::string_view topic, uint64_t handle, uint32_t payload_len, bool retain) {
+  version_++;
+  retained_version_++;
+  if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;
+  const bool flag = retain && payload_len > 0;  // what RetainMessage's -1 answer reads (topics.go:467)
+  if (topic.empty()) {
+    if (!empty_topic_live) n_retained_++;
+    empty_topic_live = true;
+    empty_topic_handle = handle;
+    empty_topic_retain = flag;
+    return 1;
+  }
+  const uint32_t n = seek(topic, 0);
+  if (n == kNone || !nh_[n].retain_path) return 0;
+  NodeMsg& M = msg.at_w(n);
+  if (!(M.flags & kRetainLive)) {
+    add_below_live(n, 1);
+    n_retained_++;
+  }
+  M.flags = (M.flags & (kChildSys | kRetainPath)) | kRetainLive | (flag ? kRetainFlag : 0u);
+  M.handle = handle;
+  child_rec_sync(n);
+  return 1;
+}
+
 }  // namespace mq
 
 namespace mq {

@@ -47,13 +47,20 @@ void reserve_resident(std::vector<T>& v, size_t n, unsigned threads) {
 // A host vector mirrored into device memory; tracks which pages changed since the last sync.
 template <class T>
 struct Mirror {
-  static constexpr size_t kPageBytes = 1u << 16;
+  // Dirty tracking granule: an update touches single records at random places, and each
+  // touched page is uploaded whole, so pages are small (<= 512 B, a power of two elements, so
+  // that page starts are 16-byte aligned); the device applies them by scatter (Device::sync).
+  static constexpr size_t kPageBytes = 512;
   std::vector<T> h;
   std::vector<uint64_t> dirty;  // bitmap of pages
   bool all_dirty = true;
   uint64_t epoch = 0;  // bumped when the host array is reallocated (device must realloc too)
 
-  static size_t per_page() { return kPageBytes / sizeof(T) ? kPageBytes / sizeof(T) : 1; }
+  static constexpr size_t per_page() {
+    size_t p = 1;
+    while (p * 2 * sizeof(T) <= kPageBytes) p *= 2;
+    return p;
+  }
   size_t size() const { return h.size(); }
   T& operator[](size_t i) { return h[i]; }
   const T& operator[](size_t i) const { return h[i]; }
@@ -242,6 +249,7 @@ class Index {
   void retain_bulk(const uint8_t* bytes, const uint64_t* offs, const uint64_t* handles, uint64_t n);
   bool empty_image() const;
   int retained_delete(std::string_view topic);
+  int retained_set(std::string_view topic, uint64_t handle, uint32_t payload_len, bool retain);
   uint64_t retained_len() const { return n_retained_; }
 
   // Device image (layout.h); the Device uploads dirty pages of these.

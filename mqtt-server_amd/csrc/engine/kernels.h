@@ -225,6 +225,16 @@ void launch_patch_compact(const PatchRec* pool, uint64_t rcap, const unsigned lo
 void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
                       uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
 
+// Incremental upload of the index image (Device::sync): dirty runs of the host mirrors, packed
+// into one staging buffer (one H2D), copied into place on the device.
+struct ScatterRun {
+  uint64_t dst;    // device address
+  uint64_t src;    // offset in the staging buffer (src % 16 == dst % 16)
+  uint64_t bytes;  // <= kScatterRun
+};
+constexpr uint64_t kScatterRun = 64 << 10;
+void launch_scatter(const ScatterRun* runs, uint32_t n, const uint8_t* stage, hipStream_t s);
+
 // ---------------------------------------------------------------------------------------------
 // Messages over the level-order retained image. The image holds the particles
 // with a live retained message at or below them, level by level, each particle's image children

@@ -1652,6 +1652,26 @@ void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, co
                      base, count);
 }
 
+// Workgroup per run: byte head up to 16-byte alignment (source and destination agree mod 16),
+// 16-byte body, byte tail.
+__global__ __launch_bounds__(256) void k_scatter(const ScatterRun* __restrict__ runs,
+                                                 const uint8_t* __restrict__ stage) {
+  const ScatterRun r = runs[blockIdx.x];
+  uint8_t* d = reinterpret_cast<uint8_t*>(r.dst);
+  const uint8_t* s = stage + r.src;
+  const uint64_t head = min(r.bytes, (uint64_t)((16 - (r.dst & 15)) & 15));
+  for (uint64_t i = threadIdx.x; i < head; i += 256) d[i] = s[i];
+  const uint64_t body = (r.bytes - head) >> 4;
+  const u32x4* s4 = reinterpret_cast<const u32x4*>(s + head);
+  u32x4* d4 = reinterpret_cast<u32x4*>(d + head);
+  for (uint64_t i = threadIdx.x; i < body; i += 256) d4[i] = s4[i];
+  for (uint64_t i = head + (body << 4) + threadIdx.x; i < r.bytes; i += 256) d[i] = s[i];
+}
+
+void launch_scatter(const ScatterRun* runs, uint32_t n, const uint8_t* stage, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_scatter, dim3(n), dim3(256), 0, s, runs, stage);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Messages over the level-order retained image (kernels.h MsgImg): the reverse
 // retained scan (topics.go:530-579) as run arithmetic. A '+' or '#' level with more segments

@@ -1,6 +1,7 @@
 // C++ host mirror of the Go TopicsIndex over the C-ABI (topics_index.h).
 #include "topics_index.h"
 
+#include <climits>
 #include <cstring>
 
 namespace mq {
@@ -10,6 +11,62 @@ static void check(int rc, const char* what) {
   if (rc < 0) throw EngineError(rc, std::string(what) + ": " + mq_last_error());
 }
 
+// An id no subscription uses: Unsubscribe for a client the index never saw still answers
+// whether the filter's particle exists (topics.go:434-437).
+static constexpr uint32_t kNoClient = UINT32_MAX;
+
+uint64_t Epochs::begin() {
+  std::lock_guard<std::mutex> lk(mu_);
+  active_.insert(++clock_);
+  return clock_;
+}
+
+void Epochs::end(uint64_t stamp) {
+  std::lock_guard<std::mutex> lk(mu_);
+  active_.erase(active_.find(stamp));
+}
+
+uint64_t Epochs::now() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return ++clock_;
+}
+
+uint64_t Epochs::oldest_active() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return active_.empty() ? UINT64_MAX : *active_.begin();
+}
+
+uint32_t IdTable::intern(const std::string& s) {
+  auto it = ids_.find(s);
+  if (it != ids_.end()) return it->second;
+  uint32_t id;
+  if (!free_.empty() && free_.front().second < ep_.oldest_active()) {
+    id = free_.front().first;
+    free_.pop_front();
+    strs_[id] = s;
+  } else {
+    id = (uint32_t)strs_.size();
+    if (id == kNoClient) throw EngineError(MQ_ENOMEM, "id space exhausted");
+    strs_.push_back(s);
+    refs_.push_back(0);
+  }
+  ids_.emplace(s, id);
+  return id;
+}
+
+bool IdTable::find(const std::string& s, uint32_t* id) const {
+  auto it = ids_.find(s);
+  if (it == ids_.end()) return false;
+  *id = it->second;
+  return true;
+}
+
+void IdTable::unref(uint32_t id, uint64_t now) {
+  if (--refs_[id] != 0) return;
+  ids_.erase(strs_[id]);
+  free_.emplace_back(id, now);  // strs_[id] stays readable for batches still in flight
+}
+
 TopicsIndex::TopicsIndex(int device, bool select_shared) {
   mq_config cfg{device, select_shared ? MQ_CFG_SELECT_SHARED : 0u, 0, 0, 0, 0};
   check(mq_index_create(&cfg, &idx_), "mq_index_create");
@@ -17,65 +74,139 @@ TopicsIndex::TopicsIndex(int device, bool select_shared) {
 
 TopicsIndex::~TopicsIndex() { mq_index_destroy(idx_); }
 
-uint32_t TopicsIndex::cid(const std::string& c) {
-  auto it = client_ids_.find(c);
-  if (it != client_ids_.end()) return it->second;
-  const uint32_t id = (uint32_t)clients_.size();
-  clients_.push_back(c);
-  client_ids_.emplace(c, id);
-  return id;
+static uint8_t sub_flags(const Subscription& sub) {
+  return (sub.NoLocal ? MQ_SUB_NOLOCAL : 0) | (sub.RetainAsPublished ? MQ_SUB_RAP : 0) |
+         (uint8_t)((sub.RetainHandling & 3) << MQ_SUB_RH_SHIFT);
 }
 
-uint32_t TopicsIndex::fid(const std::string& f) {
-  auto it = filter_ids_.find(f);
-  if (it != filter_ids_.end()) return it->second;
-  const uint32_t id = (uint32_t)filters_.size();
-  filters_.push_back(f);
-  filter_ids_.emplace(f, id);
-  return id;
-}
-
-bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) {
-  std::lock_guard<std::mutex> lk(mu_);
-  const uint32_t c = cid(client), f = fid(sub.Filter);
-  const uint8_t flags = (sub.NoLocal ? MQ_SUB_NOLOCAL : 0) | (sub.RetainAsPublished ? MQ_SUB_RAP : 0) |
-                        (uint8_t)((sub.RetainHandling & 3) << MQ_SUB_RH_SHIFT);
-  const int rc = mq_subscribe(idx_, sub.Filter.data(), (uint32_t)sub.Filter.size(), c, f, sub.Qos, flags,
-                              sub.Identifier);
-  check(rc, "mq_subscribe");
+void TopicsIndex::store(uint32_t c, uint32_t f, const Subscription& sub) {
   Subscription stored = sub;
   stored.HasIdentifiers = false;
   stored.Identifiers.clear();
-  stored_[{c, f}] = stored;
+  auto it = stored_.find({c, f});
+  if (it != stored_.end()) {
+    it->second = stored;
+    return;
+  }
+  stored_.emplace(std::make_pair(c, f), stored);
+  clients_.ref(c);
+  filters_.ref(f);
+}
+
+bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) {
+  std::lock_guard<std::mutex> up(upd_mu_);
+  uint32_t c, f;
+  {
+    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    c = clients_.intern(client);
+    f = filters_.intern(sub.Filter);
+  }
+  const int rc = mq_subscribe(idx_, sub.Filter.data(), (uint32_t)sub.Filter.size(), c, f, sub.Qos,
+                              sub_flags(sub), sub.Identifier);
+  check(rc, "mq_subscribe");
+  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  store(c, f, sub);
   return rc == 1;
 }
 
 bool TopicsIndex::Unsubscribe(const std::string& filter, const std::string& client) {
-  std::lock_guard<std::mutex> lk(mu_);
-  const int rc = mq_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), cid(client));
+  std::lock_guard<std::mutex> up(upd_mu_);
+  uint32_t c = kNoClient, f = 0;
+  bool known_f;
+  {
+    std::shared_lock<std::shared_mutex> lk(tables_mu_);
+    if (!clients_.find(client, &c)) c = kNoClient;  // looked up, never interned
+    known_f = filters_.find(filter, &f);
+  }
+  const int rc = mq_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), c);
   check(rc, "mq_unsubscribe");
+  if (c != kNoClient && known_f) {
+    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    auto it = stored_.find({c, f});
+    if (it != stored_.end()) {
+      stored_.erase(it);
+      const uint64_t now = epochs_.now();
+      clients_.unref(c, now);
+      filters_.unref(f, now);
+    }
+  }
   return rc == 1;
 }
 
 bool TopicsIndex::InlineSubscribe(const InlineSubscription& sub) {
-  std::lock_guard<std::mutex> lk(mu_);
-  const uint32_t f = fid(sub.Sub.Filter);
+  std::lock_guard<std::mutex> up(upd_mu_);
+  uint32_t f;
+  {
+    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    f = filters_.intern(sub.Sub.Filter);
+  }
   const int rc = mq_inline_subscribe(idx_, sub.Sub.Filter.data(), (uint32_t)sub.Sub.Filter.size(),
                                      sub.Sub.Identifier, f);
   check(rc, "mq_inline_subscribe");
-  inline_[{sub.Sub.Identifier, f}] = sub;
+  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  auto it = inline_.find({sub.Sub.Identifier, f});
+  if (it != inline_.end()) {
+    it->second = sub;
+  } else {
+    inline_.emplace(std::make_pair(sub.Sub.Identifier, f), sub);
+    filters_.ref(f);
+  }
   return rc == 1;
 }
 
 bool TopicsIndex::InlineUnsubscribe(int id, const std::string& filter) {
-  std::lock_guard<std::mutex> lk(mu_);
+  std::lock_guard<std::mutex> up(upd_mu_);
   const int rc = mq_inline_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), id);
   check(rc, "mq_inline_unsubscribe");
+  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  uint32_t f;
+  if (filters_.find(filter, &f)) {
+    auto it = inline_.find({id, f});
+    if (it != inline_.end()) {
+      inline_.erase(it);
+      filters_.unref(f, epochs_.now());
+    }
+  }
   return rc == 1;
+}
+
+std::vector<bool> TopicsIndex::LoadSubscriptions(const std::vector<std::pair<std::string, Subscription>>& subs) {
+  std::lock_guard<std::mutex> up(upd_mu_);
+  const size_t n = subs.size();
+  std::string bytes;
+  std::vector<uint64_t> offs(1, 0);
+  std::vector<uint32_t> cids(n), fids(n);
+  std::vector<uint8_t> qos(n), flags(n), out_new(std::max<size_t>(n, 1));
+  std::vector<int32_t> idents(n);
+  {
+    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    for (size_t i = 0; i < n; i++) {
+      const Subscription& s = subs[i].second;
+      cids[i] = clients_.intern(subs[i].first);
+      fids[i] = filters_.intern(s.Filter);
+      qos[i] = s.Qos;
+      flags[i] = sub_flags(s);
+      idents[i] = s.Identifier;
+      bytes += s.Filter;
+      offs.push_back(bytes.size());
+    }
+  }
+  bytes.resize(bytes.size() + 16, '\0');
+  check(mq_subscribe_bulk(idx_, (const uint8_t*)bytes.data(), offs.data(), cids.data(), fids.data(), qos.data(),
+                          flags.data(), idents.data(), n, out_new.data()),
+        "mq_subscribe_bulk");
+  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  std::vector<bool> out(n);
+  for (size_t i = 0; i < n; i++) {
+    store(cids[i], fids[i], subs[i].second);
+    out[i] = out_new[i] != 0;
+  }
+  return out;
 }
 
 int64_t TopicsIndex::RetainMessage(const std::string& topic, uint64_t handle, uint32_t payload_len,
                                    bool retain) {
+  std::lock_guard<std::mutex> up(upd_mu_);
   int64_t out = 0;
   check(mq_retain_message(idx_, topic.data(), (uint32_t)topic.size(), handle, payload_len,
                           retain ? 1 : 0, &out),
@@ -84,17 +215,34 @@ int64_t TopicsIndex::RetainMessage(const std::string& topic, uint64_t handle, ui
 }
 
 void TopicsIndex::RetainedDelete(const std::string& topic) {
+  std::lock_guard<std::mutex> up(upd_mu_);
   check(mq_retained_delete(idx_, topic.data(), (uint32_t)topic.size()), "mq_retained_delete");
+}
+
+void TopicsIndex::RetainedAdd(const std::string& topic, uint64_t handle, uint32_t payload_len, bool retain) {
+  std::lock_guard<std::mutex> up(upd_mu_);
+  check(mq_retained_set(idx_, topic.data(), (uint32_t)topic.size(), handle, payload_len, retain ? 1 : 0),
+        "mq_retained_set");
 }
 
 uint64_t TopicsIndex::RetainedLen() const { return mq_retained_len(idx_); }
 
+size_t TopicsIndex::live_clients() const {
+  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  return clients_.live();
+}
+
+size_t TopicsIndex::live_filters() const {
+  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  return filters_.live();
+}
+
 std::vector<uint64_t> TopicsIndex::Messages(const std::string& filter) {
   const uint64_t offs[2] = {0, filter.size()};
-  uint8_t pad[16] = {0};
-  const uint8_t* bytes = filter.empty() ? pad : (const uint8_t*)filter.data();
+  std::string bytes = filter;
+  bytes.resize(bytes.size() + 16, '\0');  // readable padding (include/mqmatch.h)
   mq_msg_result* r = nullptr;
-  check(mq_messages_batch(idx_, bytes, offs, 1, &r), "mq_messages_batch");
+  check(mq_messages_batch(idx_, (const uint8_t*)bytes.data(), offs, 1, &r), "mq_messages_batch");
   std::vector<uint64_t> hs(r->handles + r->base[0], r->handles + r->base[0] + r->count[0]);
   mq_result_free(r);
   return hs;
@@ -102,11 +250,18 @@ std::vector<uint64_t> TopicsIndex::Messages(const std::string& filter) {
 
 Subscribers TopicsIndex::Subscribers_(const std::string& topic) { return SubscribersBatch({topic})[0]; }
 
-// One mq_match_spans call for the batch; each topic's Subscribers is rebuilt straight from its
-// spans (the index's records, pinned by the result) with the topic's patches applied — no row
-// copies (include/mqmatch.h, span format).
+// One mq_match_spans call for the batch, with no host lock held; then each topic's Subscribers
+// is rebuilt straight from its spans (the index's records, pinned by the result) with the
+// topic's patches applied — no row copies (include/mqmatch.h, span format) — under a shared
+// lock of the host tables. The batch's epoch keeps every id its rows name from being reused
+// meanwhile; a subscription removed since the match (its stored entry gone) is rebuilt from the
+// row itself.
 std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::string>& topics) {
-  std::lock_guard<std::mutex> lk(mu_);
+  struct Guard {
+    Epochs& ep;
+    uint64_t stamp;
+    ~Guard() { ep.end(stamp); }
+  } guard{epochs_, epochs_.begin()};
   std::string bytes;
   std::vector<uint64_t> offs(1, 0);
   for (const std::string& t : topics) {
@@ -118,6 +273,18 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::st
   check(mq_match_spans(idx_, (const uint8_t*)bytes.data(), offs.data(), (uint32_t)topics.size(), &r),
         "mq_match_spans");
   std::vector<Subscribers> out(topics.size());
+  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  auto stored = [&](uint32_t c, uint32_t f, const mq_client_row* row) {
+    auto it = stored_.find({c, f});
+    if (it != stored_.end()) return it->second;
+    Subscription s;  // unsubscribed since the match
+    s.Filter = filters_.str(f);
+    if (row) {
+      s.Identifier = row->identifier;
+      s.Qos = row->meta & MQ_META_QOS_MASK;
+    }
+    return s;
+  };
   std::unordered_map<uint32_t, uint32_t> patched;  // topic row -> meta
   for (size_t t = 0; t < topics.size(); t++) {
     const mq_topic_spans& ts = r->topics[t];
@@ -134,32 +301,43 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::st
         if (pit != patched.end()) row.meta = pit->second;
         const uint32_t kind = row.meta & MQ_ROW_KIND_MASK;
         if (kind == 0) {  // client row: merged Subscription
-          Subscription sub = stored_.at({row.client_id, row.filter_id});
+          Subscription sub = stored(row.client_id, row.filter_id, &row);
           sub.Qos = row.meta & MQ_META_QOS_MASK;
           sub.NoLocal = (row.meta & MQ_META_NOLOCAL) != 0;
           sub.HasIdentifiers = true;
           sub.Identifiers = {{sub.Filter, sub.Identifier}};
-          s.Subscriptions[clients_[row.client_id]] = sub;
+          s.Subscriptions[clients_.str(row.client_id)] = sub;
         } else if (kind == MQ_ROW_IDENT) {  // further Identifiers entry
-          s.Subscriptions[clients_[row.client_id]].Identifiers[filters_[row.filter_id]] = row.identifier;
+          s.Subscriptions[clients_.str(row.client_id)].Identifiers[filters_.str(row.filter_id)] = row.identifier;
         }
       }
       if (!(r->flags & MQ_SPANS_PICKED))
         for (uint32_t i = 0; i < sp.n_shr; i++) {
           const mq_shared_row& row = r->shared_pool[sp.shr_off + i];
-          s.Shared[filters_[row.filter_id]][clients_[row.client_id]] = stored_.at({row.client_id, row.filter_id});
+          s.Shared[filters_.str(row.filter_id)][clients_.str(row.client_id)] =
+              stored(row.client_id, row.filter_id, nullptr);
         }
     }
     if (r->flags & MQ_SPANS_PICKED)
       for (uint32_t i = 0; i < ts.n_shared; i++) {
         const mq_shared_row& row = r->picked_rows[ts.picked_base + i];
-        s.Shared[filters_[row.filter_id]][clients_[row.client_id]] = stored_.at({row.client_id, row.filter_id});
+        s.Shared[filters_.str(row.filter_id)][clients_.str(row.client_id)] =
+            stored(row.client_id, row.filter_id, nullptr);
       }
     for (uint32_t i = 0; i < ts.n_inline; i++) {
       const mq_inline_row& row = r->inline_rows[ts.inline_base + i];
-      s.InlineSubscriptions[row.identifier] = inline_.at({row.identifier, row.filter_id});
+      auto it = inline_.find({row.identifier, row.filter_id});
+      if (it != inline_.end()) {
+        s.InlineSubscriptions[row.identifier] = it->second;
+      } else {  // unsubscribed since the match
+        InlineSubscription is;
+        is.Sub.Filter = filters_.str(row.filter_id);
+        is.Sub.Identifier = row.identifier;
+        s.InlineSubscriptions[row.identifier] = is;
+      }
     }
   }
+  lk.unlock();
   mq_result_free(r);
   return out;
 }

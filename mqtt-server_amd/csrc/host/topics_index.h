@@ -7,8 +7,11 @@
 #pragma once
 
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <mutex>
+#include <set>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -82,6 +85,40 @@ struct EngineError : std::runtime_error {
   EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+// Match batches in flight, for id recycling: a batch's rows may name any id that was in use when
+// it began, so an id released at time r is reused only once every batch begun before r ended.
+class Epochs {
+ public:
+  uint64_t begin();               // a batch starts; returns its stamp
+  void end(uint64_t stamp);       // ... and ends
+  uint64_t now();                 // a release time
+  uint64_t oldest_active() const; // UINT64_MAX when no batch is in flight
+ private:
+  mutable std::mutex mu_;
+  uint64_t clock_ = 0;
+  std::multiset<uint64_t> active_;
+};
+
+// Dense u32 ids of strings (client ids, filter strings), referenced by the stored subscriptions
+// that use them; an unreferenced id is released and later reused (Epochs). Not synchronised:
+// TopicsIndex guards it.
+class IdTable {
+ public:
+  explicit IdTable(const Epochs& ep) : ep_(ep) {}
+  uint32_t intern(const std::string& s);          // the id of s, created unreferenced if new
+  bool find(const std::string& s, uint32_t* id) const;
+  const std::string& str(uint32_t id) const { return strs_[id]; }
+  void ref(uint32_t id) { refs_[id]++; }
+  void unref(uint32_t id, uint64_t now);          // at zero: released at `now`
+  size_t live() const { return ids_.size(); }
+ private:
+  const Epochs& ep_;
+  std::unordered_map<std::string, uint32_t> ids_;
+  std::deque<std::string> strs_;
+  std::vector<uint32_t> refs_;
+  std::deque<std::pair<uint32_t, uint64_t>> free_;  // (id, release time), oldest first
+};
+
 class TopicsIndex {
  public:
   // NewTopicsIndex (topics.go:356). select_shared: SelectShared on the device
@@ -92,28 +129,38 @@ class TopicsIndex {
   TopicsIndex(const TopicsIndex&) = delete;
   TopicsIndex& operator=(const TopicsIndex&) = delete;
 
+  // Updates are serialised among themselves (the engine serialises them too); readers
+  // (Messages, SubscribersBatch) never wait for an update's engine call, nor updates for a
+  // reader's GPU round trip.
   bool Subscribe(const std::string& client, const Subscription& sub);   // topics.go:401
   bool Unsubscribe(const std::string& filter, const std::string& client);  // topics.go:423
   bool InlineSubscribe(const InlineSubscription& sub);                   // topics.go:368
   bool InlineUnsubscribe(int id, const std::string& filter);             // topics.go:382
+  // The restore path (server.go:1624-1640 loadSubscriptions): every (client, subscription) as
+  // Subscribe would take it, in order, through one mq_subscribe_bulk; returns Subscribe's answers.
+  std::vector<bool> LoadSubscriptions(const std::vector<std::pair<std::string, Subscription>>& subs);
   // RetainMessage (topics.go:453): returns 1 / 0 / -1; `handle` names the packet.
   int64_t RetainMessage(const std::string& topic, uint64_t handle, uint32_t payload_len,
                         bool retain);
-  void RetainedDelete(const std::string& topic);  // server.go:1726 (Q12)
+  void RetainedDelete(const std::string& topic);  // Retained.Delete (server.go:1726, Q12)
+  // Retained.Add outside RetainMessage (mq_retained_set)
+  void RetainedAdd(const std::string& topic, uint64_t handle, uint32_t payload_len, bool retain);
   uint64_t RetainedLen() const;
   std::vector<uint64_t> Messages(const std::string& filter);  // topics.go:525 (handles)
   Subscribers Subscribers_(const std::string& topic);          // topics.go:583
   std::vector<Subscribers> SubscribersBatch(const std::vector<std::string>& topics);
 
   mq_index* handle() { return idx_; }
+  size_t live_clients() const;  // interned client ids in use (churn accounting)
+  size_t live_filters() const;
 
  private:
-  uint32_t cid(const std::string& c);
-  uint32_t fid(const std::string& f);
+  void store(uint32_t c, uint32_t f, const Subscription& sub);  // tables_mu_ held
   mq_index* idx_ = nullptr;
-  mutable std::mutex mu_;  // the host tables; every public method is thread-safe
-  std::unordered_map<std::string, uint32_t> client_ids_, filter_ids_;
-  std::vector<std::string> clients_, filters_;
+  std::mutex upd_mu_;                    // serialises updates
+  mutable std::shared_mutex tables_mu_;  // the tables below: exclusive to change, shared to read
+  Epochs epochs_;
+  IdTable clients_{epochs_}, filters_{epochs_};
   std::map<std::pair<uint32_t, uint32_t>, Subscription> stored_;  // (client, filter)
   std::map<std::pair<int, uint32_t>, InlineSubscription> inline_;  // (id, filter)
 };

@@ -105,7 +105,7 @@ class KernelTime(C.Structure):
 EXPORTS = [
     "mq_index_create", "mq_index_destroy", "mq_last_error", "mq_abi_version", "mq_subscribe",
     "mq_unsubscribe", "mq_inline_subscribe", "mq_inline_unsubscribe", "mq_retain_message",
-    "mq_retained_delete", "mq_retained_len", "mq_subscribe_bulk", "mq_retain_bulk",
+    "mq_retained_delete", "mq_retained_set", "mq_retained_len", "mq_subscribe_bulk", "mq_retain_bulk",
     "mq_match_batch", "mq_match_device", "mq_match_chunks", "mq_messages_batch",
     "mq_messages_device", "mq_result_free", "mq_sync", "mq_index_stats", "mq_profile_enable",
     "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
@@ -148,6 +148,7 @@ def lib():
         "mq_retain_message": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint64, C.c_uint32,
                                         C.c_uint8, _i64p]),
         "mq_retained_delete": (C.c_int, [vp, C.c_char_p, C.c_uint32]),
+        "mq_retained_set": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint8]),
         "mq_retained_len": (C.c_uint64, [vp]),
         "mq_subscribe_bulk": (C.c_int, [vp, _u8p, _u64p, _u32p, _u32p, _u8p, _u8p, _i32p,
                                         C.c_uint64, _u8p]),
@@ -336,6 +337,12 @@ class Engine:
     def retained_delete(self, topic):
         tb = _b(topic)
         return _check(lib().mq_retained_delete(self.h, tb, len(tb)), "mq_retained_delete")
+
+    def retained_set(self, topic, handle, payload_len=1, retain=True):
+        """mq_retained_set: Retained.Add outside RetainMessage."""
+        tb = _b(topic)
+        return _check(lib().mq_retained_set(self.h, tb, len(tb), handle, payload_len, 1 if retain else 0),
+                      "mq_retained_set")
 
     def retained_len(self):
         return int(lib().mq_retained_len(self.h))

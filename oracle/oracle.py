@@ -43,6 +43,7 @@ def lib():
                                      C.c_uint8]
     L.orc_retain_message.restype = C.c_int64
     L.orc_retained_delete.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32]
+    L.orc_retained_add.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint8]
     L.orc_retained_len.argtypes = [C.c_void_p]
     L.orc_retained_len.restype = C.c_uint64
     L.orc_particle_count.argtypes = [C.c_void_p]
@@ -179,6 +180,10 @@ class OracleIndex:
     def retained_delete(self, topic):
         tb = _b(topic)
         lib().orc_retained_delete(self.h, tb, len(tb))
+
+    def retained_add(self, topic, handle, payload_len=1, retain=True):  # Retained.Add
+        tb = _b(topic)
+        lib().orc_retained_add(self.h, tb, len(tb), handle, payload_len, 1 if retain else 0)
 
     def retained_len(self):
         return int(lib().orc_retained_len(self.h))

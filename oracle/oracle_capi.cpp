@@ -169,6 +169,11 @@ void orc_retained_delete(void* hp, const char* topic, uint32_t tlen) {
   ((Handle*)hp)->idx.retained_delete(std::string(topic, tlen));
 }
 
+void orc_retained_add(void* hp, const char* topic, uint32_t tlen, uint64_t handle, uint32_t payload_len,
+                      uint8_t retain) {
+  ((Handle*)hp)->idx.retained_add(std::string(topic, tlen), RetainedPacket{handle, payload_len, retain != 0});
+}
+
 uint64_t orc_retained_len(void* hp) { return ((Handle*)hp)->idx.retained_len(); }
 uint64_t orc_particle_count(void* hp) { return ((Handle*)hp)->idx.particle_count(); }
 

@@ -126,6 +126,7 @@ class TopicsIndex {
   // packets.Packets as TopicsIndex.Retained (topics.go:351): server.go:1726 deletes entries
   // directly (Q12); Len is consulted by scanMessages (topics.go:535).
   void retained_delete(const std::string& topic) { retained_.erase(topic); }
+  void retained_add(const std::string& topic, const RetainedPacket& pk) { retained_[topic] = pk; }  // packets.go:79-83
   size_t retained_len() const { return retained_.size(); }
   bool retained_get(const std::string& topic, RetainedPacket* out) const;
 

@@ -11,6 +11,7 @@
 #include "publish_batcher.h"
 #include "topics_index.h"
 
+#include <atomic>
 #include <future>
 #include <random>
 #include <thread>
@@ -300,6 +301,101 @@ static void TestPublishBatcher() {
     }
 }
 
+// Client churn: ids of clients and filters with no subscription left are released
+// and reused; Unsubscribe of an unknown client interns nothing but still answers whether the
+// particle exists (topics.go:434-437).
+static void TestChurnRecyclesIds() {
+  TopicsIndex ix;
+  ix.Subscribe("keep", S("k/+"));
+  const size_t c0 = ix.live_clients(), f0 = ix.live_filters();
+  for (int round = 0; round < 50; round++) {
+    for (int i = 0; i < 20; i++) {
+      const std::string c = "cl" + std::to_string(round * 100 + i);
+      REQUIRE(ix.Subscribe(c, S("a/" + std::to_string(i % 5) + "/#", 1)));
+    }
+    REQUIRE(ix.Unsubscribe("a/0/#", "never-seen"));  // the particle exists: true
+    REQUIRE(!ix.Unsubscribe("zz/top", "never-seen"));          // no particle: false
+    for (int i = 0; i < 20; i++) {
+      const std::string c = "cl" + std::to_string(round * 100 + i);
+      REQUIRE(ix.Unsubscribe("a/" + std::to_string(i % 5) + "/#", c));
+    }
+  }
+  REQUIRE(ix.live_clients() == c0);
+  REQUIRE(ix.live_filters() == f0);
+  REQUIRE(ix.Subscribers_("k/x").Subscriptions.count("keep") == 1);
+  REQUIRE(ix.Subscribers_("a/1/x").Subscriptions.empty());
+}
+
+// Readers and updates at once: matches run while other threads subscribe, unsubscribe and
+// churn client ids; every result names only strings the index has held, and the final state
+// matches exactly.
+static void TestConcurrentReadersAndUpdates() {
+  TopicsIndex ix;
+  for (int i = 0; i < 200; i++) ix.Subscribe("base" + std::to_string(i % 40), S("s/" + std::to_string(i % 10) + "/+", 1));
+  std::atomic<bool> stop{false};
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int w = 0; w < 3; w++)
+    th.emplace_back([&, w] {
+      for (int k = 0; !stop; k++) {
+        auto res = ix.SubscribersBatch({"s/" + std::to_string(k % 10) + "/x", "t/" + std::to_string(k % 7)});
+        for (auto& kv : res[0].Subscriptions)
+          if (kv.first.rfind("base", 0) != 0 && kv.first.rfind("tmp", 0) != 0) bad++;
+        for (auto& kv : res[1].Subscriptions)
+          if (kv.first.rfind("tmp", 0) != 0) bad++;
+      }
+    });
+  for (int u = 0; u < 2; u++)
+    th.emplace_back([&, u] {
+      for (int i = 0; i < 400; i++) {
+        const std::string c = "tmp" + std::to_string(u) + "_" + std::to_string(i);
+        ix.Subscribe(c, S("t/" + std::to_string(i % 7)));
+        ix.Subscribe(c, S("s/" + std::to_string(i % 10) + "/+"));
+        ix.Unsubscribe("t/" + std::to_string(i % 7), c);
+        ix.Unsubscribe("s/" + std::to_string(i % 10) + "/+", c);
+      }
+    });
+  th[3].join();
+  th[4].join();
+  stop = true;
+  for (int w = 0; w < 3; w++) th[w].join();
+  REQUIRE(bad == 0);
+  for (int k = 0; k < 10; k++) REQUIRE(ix.Subscribers_("s/" + std::to_string(k) + "/x").Subscriptions.size() == 4);
+  REQUIRE(ix.Subscribers_("t/1").Subscriptions.empty());
+}
+
+// The restore path: LoadSubscriptions answers as Subscribe would, in order (duplicates: the
+// last entry wins), and the Go-shaped results carry the stored subscriptions.
+static void TestLoadSubscriptions() {
+  TopicsIndex a, b;
+  std::vector<std::pair<std::string, Subscription>> subs;
+  std::mt19937 r(3);
+  for (int i = 0; i < 6000; i++)
+    subs.emplace_back("c" + std::to_string(r() % 300),
+                      S((i % 9 == 0 ? "$share/g/" : "") + std::string("l/") + std::to_string(r() % 40) + (i % 3 ? "/+" : "/#"),
+                        (uint8_t)(r() % 3), (int)(r() % 5)));
+  const std::vector<bool> got = a.LoadSubscriptions(subs);
+  for (size_t i = 0; i < subs.size(); i++) REQUIRE(got[i] == b.Subscribe(subs[i].first, subs[i].second));
+  for (int k = 0; k < 40; k++) {
+    const std::string t = "l/" + std::to_string(k) + "/x";
+    REQUIRE(same(a.Subscribers_(t), b.Subscribers_(t)));
+  }
+}
+
+// Retained.Add outside RetainMessage after an expiry sweep (Q12 re-add): found again.
+static void TestRetainedAddAfterExpiry() {
+  TopicsIndex ix;
+  ix.RetainMessage("a/b", 7, 3, true);
+  ix.RetainMessage("a/c", 8, 3, true);
+  ix.RetainedDelete("a/b");
+  REQUIRE(ix.Messages("a/+") == std::vector<uint64_t>{8});
+  ix.RetainedAdd("a/b", 9, 3, true);
+  std::vector<uint64_t> m = ix.Messages("a/+");
+  std::sort(m.begin(), m.end());
+  REQUIRE((m == std::vector<uint64_t>{8, 9}));
+  REQUIRE(ix.RetainMessage("a/b", 10, 0, true) == -1);  // the re-added packet had Retain and a payload
+}
+
 int main() {
   try {
     TestSubscribe();
@@ -314,6 +410,10 @@ int main() {
     TestPublishToSubscribersIdentifiers();
     TestMergeSharedSelected();
     TestPublishBatcher();
+    TestChurnRecyclesIds();
+    TestConcurrentReadersAndUpdates();
+    TestLoadSubscriptions();
+    TestRetainedAddAfterExpiry();
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 2;

@@ -130,3 +130,37 @@ def test_bulk_images_match_identically(gpu_available):
     assert (na == nb).all()
     for i in range(len(na)):
         assert set(ha[ba[i]:ba[i] + na[i]].tolist()) == set(hb[bb[i]:bb[i] + nb[i]].tolist())
+
+
+@pytest.mark.gpu
+def test_churn_after_sync_matches_oracle(gpu_available):
+    """Incremental sync (Device::sync: dirty 512-byte pages of every mirror, packed into one
+    staging upload and scattered on the device): a bulk-built, synced index takes rounds of
+    Unsubscribe / Subscribe churn, and each round's matches equal the oracle's."""
+    import oracle as O
+    from digest import engine_digests
+    w = W.gen_subscriptions(200_000, 20_000)
+    e, o = E.Engine(), O.OracleIndex()
+    e.subscribe_bulk(w)
+    o.subscribe_bulk(w)
+    tb, to = W.gen_topics(w, 4096)
+    raw, offs = w["bytes"].tobytes(), w["offs"]
+    rng = np.random.default_rng(3)
+    nxt = int(w["client_ids"].max()) + 1
+    n = len(w["client_ids"])
+    for rnd in range(4):
+        dg, cnt = engine_digests(e.match_batch_spans(tb, to))
+        od, ocnt, _ = o.digest_batch(tb, to)
+        assert (dg == od).all() and (cnt == ocnt).all(), rnd
+        up0 = e.stats()["upload_bytes_total"]
+        for i in rng.choice(n, 500 * (rnd + 1), replace=False):
+            f = raw[int(offs[i]):int(offs[i + 1])].decode("utf-8", "surrogateescape")
+            c = int(w["client_ids"][i])
+            assert e.unsubscribe(f, c) == o.unsubscribe(f, "c%07d" % c)
+            q, fl, ident = int(w["qos"][i]), int(w["flags"][i]), int(w["idents"][i])
+            assert e.subscribe(f, nxt, int(w["filter_ids"][i]), q, fl, ident) == \
+                o.subscribe("c%07d" % nxt, f, q, ident, bool(fl & 1), bool(fl & 2), (fl >> 2) & 3,
+                            client_id=nxt, filter_id=int(w["filter_ids"][i]))
+            nxt += 1
+        e.sync()
+        assert e.stats()["upload_bytes_total"] - up0 < 64 * 1024 * 500 * (rnd + 1)  # pages, not arrays

@@ -466,6 +466,46 @@ def test_messages_after_retained_changes(image, gpu_available):
             assert g == o.messages(f), (round_, f)
 
 
+@pytest.mark.parametrize("image", [True, False])
+def test_retained_add_after_expiry(image, gpu_available):
+    """Retained.Add outside RetainMessage (the Go shim's Retained wrapper, mq_retained_set) on
+    topics whose particle keeps its retain path: an expired entry (Q12) re-added is found by
+    wildcard and literal filters again, and RetainMessage's -1 answer reads the re-added packet."""
+    from mqmatch import engine as E
+    r = random.Random(5)
+    e = E.Engine()
+    if not image:
+        e.set_option(E.OPT_MSG_IMAGE, 0)
+    o = O.OracleIndex()
+    segs = ["a", "b", "c", "$SYS"]
+    path = set()  # topics whose particle has a retain path
+    for step in range(600):
+        t = "/".join(r.choice(segs) for _ in range(r.randint(1, 3)))
+        u = r.random()
+        h = step + 1
+        if u < 0.5:
+            pl = 0 if r.random() < 0.2 else 3
+            ret = r.random() < 0.8
+            assert e.retain_message(t, h, pl, ret) == o.retain_message(t, h, pl, ret), step
+            (path.add if pl else path.discard)(t)
+        elif u < 0.75:
+            e.retained_delete(t)
+            o.retained_delete(t)
+        elif t in path:
+            pl, ret = r.choice([0, 4]), r.random() < 0.5
+            assert e.retained_set(t, h, pl, ret) == 1
+            o.retained_add(t, h, pl, ret)
+    assert e.retained_len() == o.retained_len()
+    filters = ["#", "+", "+/+", "a/#", "+/b", "a/+/+", "$SYS/#"] + sorted(path)
+    fb = "".join(filters).encode()
+    offs = np.cumsum([0] + [len(f.encode()) for f in filters]).astype(np.uint64)
+    bytes_ = np.frombuffer(fb + b"\0" * 16, np.uint8)
+    base, count, hs = e.messages_batch(bytes_, offs)
+    for i, f in enumerate(filters):
+        got = sorted(hs[int(base[i]):int(base[i]) + int(count[i])].tolist())
+        assert got == o.messages(f), f
+
+
 def test_messages_deep_fanout(gpu_available):
     """A filter whose literal levels meet runs of two particles 18 times over nests fan-outs
     beyond a lane's frame stack (kMsgStack): the batch takes the particle walk, exactly."""
