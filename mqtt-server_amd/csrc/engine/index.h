@@ -11,6 +11,9 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <new>
+#include <type_traits>
 #include <cstdint>
 #include <string>
 #include <thread>
@@ -42,6 +45,17 @@ void reserve_resident(std::vector<T>& v, size_t n, unsigned threads) {
     if (lo < hi) th.emplace_back([lo, hi] { madvise((void*)lo, hi - lo, MADV_POPULATE_WRITE); });  // best effort
   }
   for (auto& x : th) x.join();
+}
+
+// Grows v's capacity to at least n elements and advises huge pages for the unused part (no
+// touch): a bulk build that then fills it takes 2 MiB faults instead of 4 KiB ones.
+template <class T>
+void reserve_huge(std::vector<T>& v, size_t n) {
+  if (n > v.capacity()) v.reserve(n);
+  constexpr uintptr_t kHuge = 2u << 20;
+  const uintptr_t b = ((uintptr_t)(v.data() + v.size()) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t e = (uintptr_t)(v.data() + v.capacity()) & ~(kHuge - 1);
+  if (e > b) madvise((void*)b, e - b, MADV_HUGEPAGE);
 }
 
 // A host vector mirrored into device memory; tracks which pages changed since the last sync.
@@ -148,6 +162,55 @@ void parallel_for(size_t n, unsigned threads, F&& f) {
   }
   for (auto& x : th) x.join();
 }
+
+// Growable array of trivially copyable records (the host-only particle table): like a
+// std::vector, but a bulk build's growth is filled on many threads (resize) and its reservation
+// can be huge-page advised before the first touch (reserve_huge).
+template <class T>
+class PodVec {
+  static_assert(std::is_trivially_copyable<T>::value, "PodVec holds trivially copyable records");
+
+ public:
+  PodVec() = default;
+  ~PodVec() { std::free(p_); }
+  PodVec(const PodVec&) = delete;
+  PodVec& operator=(const PodVec&) = delete;
+  size_t size() const { return n_; }
+  size_t capacity() const { return cap_; }
+  T* data() { return p_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  void reserve(size_t n) {
+    if (n <= cap_) return;
+    T* q = static_cast<T*>(std::realloc(p_, n * sizeof(T)));
+    if (!q) throw std::bad_alloc();
+    p_ = q;
+    cap_ = n;
+  }
+  void reserve_huge(size_t n) {  // reserve, then advise huge pages for the untouched part
+    reserve(n);
+    constexpr uintptr_t kHuge = 2u << 20;
+    const uintptr_t b = ((uintptr_t)(p_ + n_) + kHuge - 1) & ~(kHuge - 1);
+    const uintptr_t e = (uintptr_t)(p_ + cap_) & ~(kHuge - 1);
+    if (e > b) madvise((void*)b, e - b, MADV_HUGEPAGE);
+  }
+  void push_back(const T& v) {
+    if (n_ == cap_) reserve(std::max<size_t>(16, cap_ * 2));
+    p_[n_++] = v;
+  }
+  void resize(size_t n, unsigned threads = 1) {  // new records are T{}
+    if (n > cap_) reserve(std::max(n, cap_ + cap_ / 2));
+    if (n > n_)
+      parallel_for(n - n_, threads, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) new (p_ + n_ + i) T{};
+      });
+    n_ = n;
+  }
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+};
 
 // Open-addressing u64 -> u32 map (linear probing), used for (node, client) positions.
 class HashU64 {
@@ -354,7 +417,7 @@ class Index {
   void merge_release(uint32_t n);
   uint32_t sub_count(uint32_t n) const { return lists[n].n_direct + lists[n].n_merge; }
 
-  std::vector<NodeHost> nh_;
+  PodVec<NodeHost> nh_;
   std::vector<uint32_t> free_nodes_;
   uint64_t n_live_nodes_ = 0, n_edges_ = 0, n_tombs_ = 0, n_merge_ = 0;
   uint32_t max_depth_ = 0;

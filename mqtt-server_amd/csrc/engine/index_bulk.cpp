@@ -24,32 +24,95 @@ unsigned build_threads() {
   return std::min(16u, hw);
 }
 
-// Sort v by `less` on up to `threads` threads: sorted runs, then pairwise merges.
-template <class T, class Less>
-void parallel_sort(std::vector<T>& v, unsigned threads, Less less) {
+constexpr uint32_t kParts = 64;  // hash partitions of a level's (parent, segment) keys
+
+// Sort v by `less` on `threads` threads: a stable partition into nb buckets by bucket(x) < nb
+// (which must not decrease along `less`), then every bucket sorted on its own.
+template <class T, class Bucket, class Less>
+void bucket_sort(std::vector<T>& v, unsigned threads, uint32_t nb, Bucket&& bucket, Less&& less) {
   const size_t n = v.size();
-  unsigned parts = 1;
-  while (parts < threads && n / (parts * 2) >= 65536) parts *= 2;
-  std::vector<size_t> cut(parts + 1);
-  for (unsigned p = 0; p <= parts; p++) cut[p] = n * p / parts;
-  parallel_for(parts, parts, [&](size_t b, size_t e) {
-    for (size_t p = b; p < e; p++) std::sort(v.begin() + cut[p], v.begin() + cut[p + 1], less);
-  });
-  std::vector<T> tmp(n);
-  for (unsigned w = 1; w < parts; w *= 2) {
-    const unsigned pairs = (parts + 2 * w - 1) / (2 * w);
-    parallel_for(pairs, pairs, [&](size_t b, size_t e) {
-      for (size_t q = b; q < e; q++) {
-        const size_t lo = cut[std::min<size_t>(q * 2 * w, parts)], mid = cut[std::min<size_t>(q * 2 * w + w, parts)],
-                     hi = cut[std::min<size_t>(q * 2 * w + 2 * w, parts)];
-        std::merge(v.begin() + lo, v.begin() + mid, v.begin() + mid, v.begin() + hi, tmp.begin() + lo, less);
-      }
-    });
-    v.swap(tmp);
+  if (n < 65536) {
+    std::sort(v.begin(), v.end(), less);
+    return;
   }
+  const unsigned chunks = std::max(1u, std::min<unsigned>(threads * 4, (unsigned)(n / 65536)));
+  std::vector<uint64_t> cnt((size_t)chunks * nb, 0), at((size_t)chunks * nb);
+  parallel_for(chunks, chunks, [&](size_t cb, size_t ce) {
+    for (size_t c = cb; c < ce; c++)
+      for (size_t i = n * c / chunks; i < n * (c + 1) / chunks; i++) cnt[c * nb + bucket(v[i])]++;
+  });
+  std::vector<uint64_t> off(nb + 1);
+  uint64_t run = 0;
+  for (uint32_t b = 0; b < nb; b++) {
+    off[b] = run;
+    for (unsigned c = 0; c < chunks; c++) {
+      at[(size_t)c * nb + b] = run;
+      run += cnt[(size_t)c * nb + b];
+    }
+  }
+  off[nb] = run;
+  std::vector<T> tmp(n);
+  parallel_for(chunks, chunks, [&](size_t cb, size_t ce) {
+    for (size_t c = cb; c < ce; c++)
+      for (size_t i = n * c / chunks; i < n * (c + 1) / chunks; i++) tmp[at[c * nb + bucket(v[i])]++] = v[i];
+  });
+  std::atomic<uint32_t> next{0};
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < threads; t++)
+    th.emplace_back([&] {
+      for (uint32_t b; (b = next.fetch_add(1)) < nb;) std::sort(tmp.begin() + off[b], tmp.begin() + off[b + 1], less);
+    });
+  for (auto& x : th) x.join();
+  v.swap(tmp);
 }
 
-constexpr uint32_t kParts = 64;  // hash partitions of a level's (parent, segment) keys
+// Buckets for keys below `limit`: a power-of-two count (about 64 per thread) and the shift that
+// maps a key to its bucket.
+inline uint32_t bucket_shift(uint64_t limit, unsigned threads, uint32_t* nb) {
+  uint32_t bits = 1;
+  while ((1ull << bits) < limit) bits++;
+  uint32_t want = 1;
+  while (want < threads * 64) want <<= 1;
+  uint32_t wb = 0;
+  while ((1u << wb) < want) wb++;
+  const uint32_t shift = bits > wb ? bits - wb : 0;
+  *nb = (uint32_t)(((limit - 1) >> shift) + 1);
+  return shift;
+}
+
+// Stable partition of 0..n-1 by part(i) < nparts on `threads` threads (count, prefix, scatter):
+// the members of part p are flat[offs[p] .. offs[p + 1]), in increasing order.
+template <class Part>
+void partition_ids(uint32_t n, uint32_t nparts, unsigned threads, Part&& part, std::vector<uint32_t>& flat,
+                   std::vector<uint64_t>& offs) {
+  const unsigned chunks = std::max(1u, std::min<unsigned>(threads * 4, (n + 65535) / 65536));
+  std::vector<uint8_t> pid(n);  // nparts <= 256
+  std::vector<uint64_t> cnt((size_t)chunks * nparts, 0);
+  parallel_for(chunks, chunks, [&](size_t cb, size_t ce) {
+    for (size_t c = cb; c < ce; c++)
+      for (uint64_t i = (uint64_t)n * c / chunks; i < (uint64_t)n * (c + 1) / chunks; i++) {
+        pid[i] = (uint8_t)part((uint32_t)i);
+        cnt[c * nparts + pid[i]]++;
+      }
+  });
+  offs.assign(nparts + 1, 0);
+  std::vector<uint64_t> at((size_t)chunks * nparts);
+  uint64_t run = 0;
+  for (uint32_t p = 0; p < nparts; p++) {
+    offs[p] = run;
+    for (unsigned c = 0; c < chunks; c++) {
+      at[(size_t)c * nparts + p] = run;
+      run += cnt[(size_t)c * nparts + p];
+    }
+  }
+  offs[nparts] = run;
+  flat.resize(n);
+  parallel_for(chunks, chunks, [&](size_t cb, size_t ce) {
+    for (size_t c = cb; c < ce; c++)
+      for (uint64_t i = (uint64_t)n * c / chunks; i < (uint64_t)n * (c + 1) / chunks; i++)
+        flat[at[c * nparts + pid[i]]++] = (uint32_t)i;
+  });
+}
 
 // f(p) for every partition p on up to `threads` threads, partitions handed out one at a time
 // (parallel_for's 4096-item grain would run 64 partitions on one thread).
@@ -103,10 +166,10 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
       }
       segs += c;
     });
-    nh_.reserve(nh_.size() + segs.load());  // an upper bound: not made resident
-    rep_off.reserve(segs.load());
-    rep_len.reserve(segs.load());
-    node_parent.reserve(segs.load());
+    nh_.reserve_huge(nh_.size() + segs.load());  // an upper bound: reserved, not touched
+    reserve_huge(rep_off, segs.load());
+    reserve_huge(rep_len, segs.load());
+    reserve_huge(node_parent, segs.load());
   }
   struct Slot {  // a partition's dedup table entry
     uint64_t k0, k1;
@@ -180,7 +243,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
     std::vector<uint32_t> base(kParts + 1, (uint32_t)nh_.size());
     for (uint32_t p = 0; p < kParts; p++) base[p + 1] = base[p] + uniq[p];
     const uint32_t n1 = base[kParts];
-    nh_.resize(n1);
+    nh_.resize(n1, threads);
     rep_off.resize(n1 - first_new);
     rep_len.resize(n1 - first_new);
     node_parent.resize(n1 - first_new);
@@ -244,53 +307,51 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
       uint64_t k0, k1;
       uint32_t str;
     };
-    std::vector<std::vector<uint32_t>> parts(kParts);  // inline keys by hash, long ones apart
-    std::vector<uint32_t> longs;
-    for (uint32_t k = 0; k < n_new; k++) {
+    // inline keys by hash into kParts partitions, long ones into partition kParts
+    std::vector<uint32_t> pk;
+    std::vector<uint64_t> po;
+    partition_ids(n_new, kParts + 1, threads, [&](uint32_t k) {
       const SegKey& sk = nh_[first_new + k].key;
-      if (seg_is_long(sk)) longs.push_back(k);
-      else parts[mix64(sk.k0 ^ (sk.k1 * 0x9e3779b97f4a7c15ull)) % kParts].push_back(k);
-    }
+      return seg_is_long(sk) ? kParts : (uint32_t)(mix64(sk.k0 ^ (sk.k1 * 0x9e3779b97f4a7c15ull)) % kParts);
+    }, pk, po);
     std::vector<std::vector<uint32_t>> firsts(kParts);  // per partition: keys seen first, to intern
     std::vector<std::vector<KS>> tabs(kParts);
+    auto slot = [&](const std::vector<KS>& t, const SegKey& sk) {
+      size_t i = mix64(sk.k0 + sk.k1) & (t.size() - 1);
+      while (t[i].str != kNone && !(t[i].k0 == sk.k0 && t[i].k1 == sk.k1)) i = (i + 1) & (t.size() - 1);
+      return i;
+    };
+    auto grow = [&](std::vector<KS>& t) {  // a level holds few distinct segments: tables start small
+      std::vector<KS> old(t.size() * 2, KS{0, 0, kNone});
+      old.swap(t);
+      for (const KS& e : old)
+        if (e.str != kNone) t[slot(t, SegKey{e.k0, e.k1})] = e;
+    };
+    auto seg_of = [&](uint32_t k) { return std::string_view((const char*)bytes + rep_off[k], rep_len[k]); };
     for_parts(threads, [&](uint32_t p) {
-      {
-        std::vector<KS>& t = tabs[p];
-        size_t cap = 16;
-        while (cap < 2 * parts[p].size()) cap <<= 1;
-        t.assign(cap, KS{0, 0, kNone});
-        for (uint32_t k : parts[p]) {
-          const SegKey& sk = nh_[first_new + k].key;
-          size_t i = mix64(sk.k0 + sk.k1) & (cap - 1);
-          while (t[i].str != kNone && !(t[i].k0 == sk.k0 && t[i].k1 == sk.k1)) i = (i + 1) & (cap - 1);
-          if (t[i].str == kNone) {  // first particle with this segment: look the string up
-            t[i] = KS{sk.k0, sk.k1, strs_.find(std::string_view((const char*)bytes + rep_off[k], rep_len[k]))};
-            if (t[i].str == kNone) {
-              t[i].str = kNone - 1;  // to intern below (serially)
-              firsts[p].push_back(k);
-            }
-          }
+      std::vector<KS>& t = tabs[p];
+      t.assign(1024, KS{0, 0, kNone});
+      size_t used = 0;
+      for (uint64_t q = po[p]; q < po[p + 1]; q++) {
+        const uint32_t k = pk[q];
+        const SegKey& sk = nh_[first_new + k].key;
+        if (t[slot(t, sk)].str != kNone) continue;
+        if (2 * ++used > t.size()) grow(t);
+        KS& e = t[slot(t, sk)];
+        e = KS{sk.k0, sk.k1, strs_.find(seg_of(k))};  // first particle with this segment
+        if (e.str == kNone) {
+          e.str = kNone - 1;  // to intern below (serially)
+          firsts[p].push_back(k);
         }
       }
     });
     for (uint32_t p = 0; p < kParts; p++)
-      for (uint32_t k : firsts[p]) {
-        const SegKey& sk = nh_[first_new + k].key;
-        std::vector<KS>& t = tabs[p];
-        size_t i = mix64(sk.k0 + sk.k1) & (t.size() - 1);
-        while (!(t[i].k0 == sk.k0 && t[i].k1 == sk.k1)) i = (i + 1) & (t.size() - 1);
-        t[i].str = intern_str(std::string_view((const char*)bytes + rep_off[k], rep_len[k]));
-      }
+      for (uint32_t k : firsts[p]) tabs[p][slot(tabs[p], nh_[first_new + k].key)].str = intern_str(seg_of(k));
     for_parts(threads, [&](uint32_t p) {
-        for (uint32_t k : parts[p]) {
-          const SegKey& sk = nh_[first_new + k].key;
-          const std::vector<KS>& t = tabs[p];
-          size_t i = mix64(sk.k0 + sk.k1) & (t.size() - 1);
-          while (!(t[i].k0 == sk.k0 && t[i].k1 == sk.k1)) i = (i + 1) & (t.size() - 1);
-          str[k] = t[i].str;
-        }
+      const std::vector<KS>& t = tabs[p];
+      for (uint64_t q = po[p]; q < po[p + 1]; q++) str[pk[q]] = t[slot(t, nh_[first_new + pk[q]].key)].str;
     });
-    for (uint32_t k : longs) str[k] = intern_str(std::string_view((const char*)bytes + rep_off[k], rep_len[k]));
+    for (uint64_t q = po[kParts]; q < po[kParts + 1]; q++) str[pk[q]] = intern_str(seg_of(pk[q]));
   }
   // Node records, level by level (a level's parents are complete), each level on all threads.
   for (auto& t : grow) t.join();
@@ -488,9 +549,13 @@ void Index::subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uin
   std::vector<Ent> ns;
   for (uint64_t i : loc)
     if (kind[i] == 0) ns.push_back(Ent{items[i].node, client_ids[i], i});
-  parallel_sort(ns, threads, [](const Ent& a, const Ent& b) {
-    return a.node != b.node ? a.node < b.node : (a.client != b.client ? a.client < b.client : a.i < b.i);
-  });
+  {
+    uint32_t nb;
+    const uint32_t sh = bucket_shift(nh_.size(), threads, &nb);
+    bucket_sort(ns, threads, nb, [sh](const Ent& e) { return e.node >> sh; }, [](const Ent& a, const Ent& b) {
+      return a.node != b.node ? a.node < b.node : (a.client != b.client ? a.client < b.client : a.i < b.i);
+    });
+  }
   std::vector<Ent> slots;  // one per (particle, client): the last entry
   slots.reserve(ns.size());
   for (size_t k = 0; k < ns.size(); k++) {
@@ -503,7 +568,13 @@ void Index::subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uin
   // 2. partners: per client, its particles pairwise (Index::compatible)
   std::vector<uint64_t> cn(slots.size());  // client << 32 | node
   for (size_t k = 0; k < slots.size(); k++) cn[k] = (uint64_t)slots[k].client << 32 | slots[k].node;
-  parallel_sort(cn, threads, std::less<uint64_t>());
+  {
+    uint64_t max_c = 0;
+    for (const Ent& e : slots) max_c = std::max<uint64_t>(max_c, e.client);
+    uint32_t nb;
+    const uint32_t sh = bucket_shift(max_c + 1, threads, &nb) + 32;
+    bucket_sort(cn, threads, nb, [sh](uint64_t x) { return (uint32_t)(x >> sh); }, std::less<uint64_t>());
+  }
   std::vector<size_t> cstart;  // client groups in cn
   for (size_t k = 0; k < cn.size(); k++)
     if (k == 0 || (cn[k] >> 32) != (cn[k - 1] >> 32)) cstart.push_back(k);
@@ -537,9 +608,14 @@ void Index::subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uin
   std::vector<std::pair<uint64_t, uint32_t>> links;
   for (auto& v : plinks) links.insert(links.end(), v.begin(), v.end());
   std::vector<std::vector<std::pair<uint64_t, uint32_t>>>().swap(plinks);
-  parallel_sort(links, threads, [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
-    return a.first != b.first ? a.first < b.first : a.second < b.second;
-  });
+  {
+    uint32_t nb;
+    const uint32_t sh = bucket_shift(nh_.size(), threads, &nb) + 32;
+    bucket_sort(links, threads, nb, [sh](const std::pair<uint64_t, uint32_t>& x) { return (uint32_t)(x.first >> sh); },
+                [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) {
+                  return a.first != b.first ? a.first < b.first : a.second < b.second;
+                });
+  }
   // 3. subscription slabs: per particle [direct slots][may-merge slots], slots in client order
   std::vector<uint8_t> is_merge(slots.size(), 0);
   {

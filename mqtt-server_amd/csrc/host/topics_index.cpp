@@ -248,6 +248,46 @@ std::vector<uint64_t> TopicsIndex::Messages(const std::string& filter) {
   return hs;
 }
 
+SpanBatch::~SpanBatch() {
+  mq_result_free(r_);
+  ix_.epochs().end(stamp_);
+}
+
+std::string TopicView::client(uint32_t id) const { return b_->index().ClientName(id); }
+std::string TopicView::filter(uint32_t id) const { return b_->index().FilterName(id); }
+
+std::string TopicsIndex::ClientName(uint32_t id) const {
+  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  return clients_.str(id);
+}
+
+std::string TopicsIndex::FilterName(uint32_t id) const {
+  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  return filters_.str(id);
+}
+
+std::vector<TopicView> TopicsIndex::SubscribersViews(const std::vector<std::string>& topics) {
+  const uint64_t stamp = epochs_.begin();
+  std::string bytes;
+  std::vector<uint64_t> offs(1, 0);
+  for (const std::string& t : topics) {
+    bytes += t;
+    offs.push_back(bytes.size());
+  }
+  bytes.resize(bytes.size() + 16, '\0');  // readable padding (include/mqmatch.h)
+  mq_span_result* r = nullptr;
+  const int rc = mq_match_spans(idx_, (const uint8_t*)bytes.data(), offs.data(), (uint32_t)topics.size(), &r);
+  if (rc < 0) {
+    epochs_.end(stamp);
+    check(rc, "mq_match_spans");
+  }
+  auto batch = std::make_shared<const SpanBatch>(*this, r, stamp);
+  std::vector<TopicView> out;
+  out.reserve(topics.size());
+  for (uint32_t t = 0; t < topics.size(); t++) out.emplace_back(batch, t);
+  return out;
+}
+
 Subscribers TopicsIndex::Subscribers_(const std::string& topic) { return SubscribersBatch({topic})[0]; }
 
 // One mq_match_spans call for the batch, with no host lock held; then each topic's Subscribers

@@ -6,8 +6,10 @@
 // engine error throws mq::host::EngineError.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <deque>
+#include <memory>
 #include <map>
 #include <mutex>
 #include <set>
@@ -119,6 +121,81 @@ class IdTable {
   std::deque<std::pair<uint32_t, uint64_t>> free_;  // (id, release time), oldest first
 };
 
+class TopicsIndex;
+
+// One mq_match_spans result shared by the views of its topics (freed with the last view). It
+// pins the index's host image: updates wait until it is freed (include/mqmatch.h), so views are
+// for the fan-out of a batch, not for keeping. Its epoch keeps the ids its rows name in use.
+class SpanBatch {
+ public:
+  SpanBatch(TopicsIndex& ix, mq_span_result* r, uint64_t stamp) : ix_(ix), r_(r), stamp_(stamp) {}
+  ~SpanBatch();
+  SpanBatch(const SpanBatch&) = delete;
+  SpanBatch& operator=(const SpanBatch&) = delete;
+  const mq_span_result& result() const { return *r_; }
+  TopicsIndex& index() const { return ix_; }
+ private:
+  TopicsIndex& ix_;
+  mq_span_result* r_;
+  uint64_t stamp_;
+};
+
+// Subscribers(topic) as a view over its batch's span result: the recipients the fan-out
+// (server.go:1008-1021) iterates, without building the Go-shaped maps.
+class TopicView {
+ public:
+  TopicView() = default;
+  TopicView(std::shared_ptr<const SpanBatch> b, uint32_t t) : b_(std::move(b)), t_(t) {}
+  const mq_topic_spans& spans() const { return b_->result().topics[t_]; }
+  uint32_t n_client() const { return spans().n_client; }
+  uint32_t n_shared() const { return spans().n_shared; }
+  uint32_t n_inline() const { return spans().n_inline; }
+  // f(const mq_client_row&) for every client row (the merged subscription: Qos / NoLocal in
+  // meta) and ident row (MQ_ROW_IDENT) in gather order, patches applied; dropped rows skipped
+  template <class F>
+  void for_each_row(F&& f) const {
+    const mq_span_result& r = b_->result();
+    const mq_topic_spans& ts = spans();
+    std::vector<mq_patch> p(r.patches + ts.patch_base, r.patches + ts.patch_base + ts.n_patches);
+    std::sort(p.begin(), p.end(), [](const mq_patch& a, const mq_patch& b) { return a.row < b.row; });
+    size_t pi = 0;
+    uint32_t row = 0;
+    for (uint32_t k = 0; k < ts.n_spans; k++) {
+      const mq_span& sp = r.spans[ts.span_base + k];
+      for (uint32_t i = 0; i < sp.n_sub; i++, row++) {
+        mq_client_row cr = r.sub_pool[sp.sub_off + i];
+        if (pi < p.size() && p[pi].row == row) cr.meta = p[pi++].meta;
+        if ((cr.meta & MQ_ROW_KIND_MASK) != MQ_ROW_DROP) f(cr);
+      }
+    }
+  }
+  // f(const mq_shared_row&) for every shared member (the picked ones with MQ_SPANS_PICKED)
+  template <class F>
+  void for_each_shared(F&& f) const {
+    const mq_span_result& r = b_->result();
+    const mq_topic_spans& ts = spans();
+    if (r.flags & MQ_SPANS_PICKED) {
+      for (uint32_t i = 0; i < ts.n_shared; i++) f(r.picked_rows[ts.picked_base + i]);
+      return;
+    }
+    for (uint32_t k = 0; k < ts.n_spans; k++) {
+      const mq_span& sp = r.spans[ts.span_base + k];
+      for (uint32_t i = 0; i < sp.n_shr; i++) f(r.shared_pool[sp.shr_off + i]);
+    }
+  }
+  template <class F>
+  void for_each_inline(F&& f) const {
+    const mq_span_result& r = b_->result();
+    const mq_topic_spans& ts = spans();
+    for (uint32_t i = 0; i < ts.n_inline; i++) f(r.inline_rows[ts.inline_base + i]);
+  }
+  std::string client(uint32_t id) const;  // the client ID string of a row's client_id
+  std::string filter(uint32_t id) const;
+ private:
+  std::shared_ptr<const SpanBatch> b_;
+  uint32_t t_ = 0;
+};
+
 class TopicsIndex {
  public:
   // NewTopicsIndex (topics.go:356). select_shared: SelectShared on the device
@@ -149,8 +226,13 @@ class TopicsIndex {
   std::vector<uint64_t> Messages(const std::string& filter);  // topics.go:525 (handles)
   Subscribers Subscribers_(const std::string& topic);          // topics.go:583
   std::vector<Subscribers> SubscribersBatch(const std::vector<std::string>& topics);
+  // The same batch as views (no maps): what a fan-out iterates
+  std::vector<TopicView> SubscribersViews(const std::vector<std::string>& topics);
+  std::string ClientName(uint32_t id) const;
+  std::string FilterName(uint32_t id) const;
 
   mq_index* handle() { return idx_; }
+  Epochs& epochs() { return epochs_; }
   size_t live_clients() const;  // interned client ids in use (churn accounting)
   size_t live_filters() const;
 

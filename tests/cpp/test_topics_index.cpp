@@ -3,6 +3,7 @@
 // of index.root.particles are restated through the public API. Run by
 // tests/test_gpu_parity.py::test_cpp_host_mirror (needs a GPU).
 #include <algorithm>
+#include <map>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -396,6 +397,38 @@ static void TestRetainedAddAfterExpiry() {
   REQUIRE(ix.RetainMessage("a/b", 10, 0, true) == -1);  // the re-added packet had Retain and a payload
 }
 
+// The view batcher: each future's TopicView names exactly the recipients of Subscribers(topic)
+// (client rows with their merged Qos, shared members, inline identifiers).
+static void TestPublishViewBatcher() {
+  TopicsIndex ix;
+  std::mt19937 r(11);
+  for (int i = 0; i < 300; i++) {
+    const std::string f = std::string(i % 7 == 0 ? "$share/g/" : "") + "v/" + std::to_string(r() % 20) + (i % 2 ? "/+" : "/#");
+    ix.Subscribe("c" + std::to_string(r() % 40), S(f, (uint8_t)(r() % 3), (int)(r() % 3)));
+  }
+  std::vector<std::future<mq::host::TopicView>> futs;
+  {
+    mq::host::PublishViewBatcher b(ix, 256, std::chrono::microseconds(1000));
+    for (int i = 0; i < 400; i++) futs.push_back(b.Submit("v/" + std::to_string(i % 20) + "/x"));
+    for (auto& f : futs) f.wait();
+  }
+  for (int i = 0; i < 400; i++) {
+    const mq::host::TopicView v = futs[i].get();
+    const mq::host::Subscribers want = ix.Subscribers_("v/" + std::to_string(i % 20) + "/x");
+    std::map<std::string, int> qos;
+    v.for_each_row([&](const mq_client_row& cr) {
+      if ((cr.meta & MQ_ROW_KIND_MASK) == 0) qos[v.client(cr.client_id)] = cr.meta & MQ_META_QOS_MASK;
+    });
+    REQUIRE(qos.size() == want.Subscriptions.size());
+    for (auto& kv : want.Subscriptions) REQUIRE(qos.count(kv.first) && qos[kv.first] == kv.second.Qos);
+    size_t shared = 0;
+    v.for_each_shared([&](const mq_shared_row&) { shared++; });
+    size_t want_shared = 0;
+    for (auto& g : want.Shared) want_shared += g.second.size();
+    REQUIRE(shared == want_shared);
+  }
+}
+
 int main() {
   try {
     TestSubscribe();
@@ -414,6 +447,7 @@ int main() {
     TestConcurrentReadersAndUpdates();
     TestLoadSubscriptions();
     TestRetainedAddAfterExpiry();
+    TestPublishViewBatcher();
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 2;
