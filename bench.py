@@ -1,18 +1,25 @@
 """Benchmark: matched publishes/sec of the MI355X TopicsIndex engine (BASELINE.json metric).
 
 A step is one pass of the hot path over one batch: Subscribers() for every topic of a
-1M-topic publish batch already resident in HBM — walk, scan, expand/merge/emit of every
-client, identifier, shared and inline row (mq_match_device). The index (10M subscriptions,
-config-2/3 mix) is built through the C-ABI bulk path and kept resident.
+1M-topic publish batch already resident in HBM. Default (--format spans, mq_match_spans_device):
+walk, scan, k_desc (one span per gathered particle list) and k_merge (every record whose row
+differs from the stored subscription resolved into a patch: Subscription.Merge across the
+client's matches, the '$' rule, inline last-write) — the complete Subscribers result of every
+topic, the gathered lists named rather than copied. --format rows materialises
+every row (mq_match_device_chunks, each chunk consumed by a device-side checksum). The index
+(10M subscriptions, config-2/3 mix) is built through the C-ABI bulk path.
 
 Multi-GPU (`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`): one process
 per GPU, the index replicated on every GPU and each rank matching its own 1M-topic batch —
 topics are independent units, so there is no data-path collective ("scaling": "weak"); only
 the timing barrier and a max-over-ranks all-reduce of the elapsed time use the process group.
+`--shard filter` runs the north-star sharded mode instead (subscriptions sharded by filter hash,
+every rank matching the full batch, cross-shard lists all-gathered over RCCL each step).
 
-Rank 0 prints one JSON line with the roofline of the dominant kernel (k_copy; HIP events on
-its launch stream) and the CPU baseline (the oracle restatement of the Go trie, all allotted
-host cores, on a bounded sample of the same batch).
+Rank 0 prints one JSON line with the roofline of the dominant kernel (spans: k_merge; rows:
+k_copy; HIP events on its launch stream; PMC traffic from profiles/pmc_traffic.json) and the CPU
+baseline (the fast CPU restatement of the Go trie on all allotted host cores, on a bounded
+sample of the same batch).
 """
 import argparse
 import json
@@ -96,7 +103,20 @@ def read_traffic(path, n_subs, write_bytes_per_launch):
         return None
 
 
-def spans_roofline(prof, work, steps, n):
+def read_spans_traffic(path, n_subs, n_topics):
+    """HBM bytes per k_merge<spans> launch (FETCH_SIZE x2 + WRITE_SIZE) from a committed rocprofv3
+    PMC summary of the same configuration (subscriptions and topics per launch), if present."""
+    try:
+        with open(path) as f:
+            e = json.load(f).get("spans", {}).get(str(n_subs))
+        if e is None or int(e["topics"]) != n_topics:
+            return None
+        return float(e["hbm_bytes_per_merge_launch"])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def spans_roofline(prof, work, steps, n, n_subs):
     """Roofline of the span format's dominant kernel, k_merge. Its algorithmic bytes per launch
      are what it must read and write for the launch's topics: 40 B of offsets and a
     64 B result record per topic, the 32 B GDesc of every gather, 16 B per pair-table entry
@@ -115,7 +135,8 @@ def spans_roofline(prof, work, steps, n):
                   + 8 * g("merge_links") + 8 * g("merge_patches"))
     launch_ms = ms / launches
     achieved = per_launch / (launch_ms * 1e-3) / 1e9
-    roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, launch_ms=launch_ms, bytes_per_launch=per_launch)
+    roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, launch_ms=launch_ms, bytes_per_launch=per_launch,
+                traffic=read_spans_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n))
     return roof
 
 
@@ -243,8 +264,8 @@ def run_sharded(args, mix, n_clients, rank, world, local, backend):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--subs", type=int, default=10_000_000)
     ap.add_argument("--clients", type=int, default=0, help="default: subs/10 (mqtt mix), subs (iot mix)")
     ap.add_argument("--mix", choices=["mqtt", "iot"], default="mqtt",
@@ -382,7 +403,7 @@ def main():
         torch.cuda.synchronize()
         work = eng.profile_read()
         eng.profile(False)
-        out["roofline"] = spans_roofline(prof, work, args.steps, n)
+        out["roofline"] = spans_roofline(prof, work, args.steps, n, args.subs)
         out["merge_work_per_topic"] = {k[6:]: work[k][0] / n for k in work if k.startswith("merge_") and k != "merge_topics"}
     else:
         out["roofline"] = rows_roofline(prof, args, elapsed, out)

@@ -418,6 +418,8 @@ int mq_index_check(mq_index* idx);
 #define MQ_OPT_MERGE_WAVES 7     /* k_merge waves per SIMD the registers are budgeted for (1, 6, 8) */
 #define MQ_OPT_MSG_IMAGE 8       /* Messages: 1 (default) runs over the level-order retained image;
                                     0 walks the particles (the path the Q6 state always takes) */
+#define MQ_OPT_WALK_WAVES 9       /* k_walk count pass waves per SIMD the registers are budgeted for (1, 8) */
+#define MQ_OPT_WALK_LISTS 10      /* span format: 1 makes the walk count the lists (as the row format) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. enable: 0 off,

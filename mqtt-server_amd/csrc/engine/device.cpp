@@ -228,6 +228,8 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_SERIAL: serial_ = v != 0; return true;
     case MQ_OPT_PATCH_CAP: patch_cap_init_ = std::max<uint64_t>(v, 64); return true;
     case MQ_OPT_MERGE_WAVES: merge_wpe_opt_ = (uint32_t)v; return true;
+    case MQ_OPT_WALK_WAVES: walk_wpe_ = (uint32_t)v; return true;
+    case MQ_OPT_WALK_LISTS: walk_lists_ = v != 0; return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     default: return false;
   }
@@ -509,7 +511,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     const Sub& q = sub[b];
     TopicOff* off_b = offs_.as<TopicOff>() + q.t0 + b;
     prof.begin(wstream_);
-    launch_walk(false, d_tb, d_to + q.t0, q.n, di, counts_.as<TopicCount>() + q.t0, nullptr,
+    launch_walk(false, true, walk_wpe_, d_tb, d_to + q.t0, q.n, di, counts_.as<TopicCount>() + q.t0, nullptr,
                 gslots_.as<uint32_t>() + (size_t)q.t0 * kGatherCap, ovf_.as<uint32_t>() + b, wstream_);
     prof.end("walk", wstream_);
     hip_check(hipGetLastError(), "k_walk<count>");
@@ -568,7 +570,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     if (h_ovf[sb]) {
       grow(gathers_, std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
       prof.begin(s);
-      launch_walk(true, d_tb, d_to + q.t0, q.n, di, nullptr, off_b, gathers_.as<uint32_t>(), nullptr, s);
+      launch_walk(true, true, walk_wpe_, d_tb, d_to + q.t0, q.n, di, nullptr, off_b, gathers_.as<uint32_t>(), nullptr, s);
       prof.end("walk_fill", s);
       hip_check(hipGetLastError(), "k_walk<fill>");
       gathers = gathers_.as<uint32_t>();
@@ -650,6 +652,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     da.tiles = tiles_[p].as<uint32_t>();
     da.spans = nullptr;
     da.inl_out = nullptr;
+    da.tc_out = nullptr;
     prof.begin(s);
     launch_desc(da, false, s);
     prof.end("desc", s);
@@ -773,7 +776,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
 }
 
 TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                           const uint32_t** gathers, uint32_t* gstride) {
+                           const uint32_t** gathers, uint32_t* gstride, bool lists) {
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
   grow(counts_, (size_t)n * sizeof(TopicCount));
   grow(offs_, (size_t)(n + 1) * sizeof(TopicOff));
@@ -786,7 +789,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   uint32_t* h_ovf = reinterpret_cast<uint32_t*>(h_tot + 1);
   hip_check(hipMemsetAsync(ovf_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
   prof.begin(s);
-  launch_walk(false, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(), ovf_.as<uint32_t>(), s);
+  launch_walk(false, lists, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(), ovf_.as<uint32_t>(), s);
   prof.end("walk", s);
   hip_check(hipGetLastError(), "k_walk<count>");
   prof.begin(s);
@@ -802,7 +805,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   if (*h_ovf) {  // a topic with more gathers than its count-pass slots: write all lists compactly
     grow(gathers_, std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
     prof.begin(s);
-    launch_walk(true, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), nullptr, s);
+    launch_walk(true, lists, walk_wpe_, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), nullptr, s);
     prof.end("walk_fill", s);
     hip_check(hipGetLastError(), "k_walk<fill>");
     *gathers = gathers_.as<uint32_t>();
@@ -848,8 +851,12 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
 
   const uint32_t* gathers = nullptr;
   uint32_t gstride = 0;
-  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride);
+  // The walk counts only gathers when nothing needs the lists' totals before k_desc: no inline
+  // rows to place and no device share pick (k_desc<true> then counts rows / shared / merge).
+  sb_.lists = walk_lists_ || select_shared_ || ix.inl.live != 0;
+  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists);
   sb_.tot = tot;
+  if (!sb_.lists) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
   grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
   grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
   grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
@@ -874,6 +881,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   da.tiles = nullptr;
   da.spans = sp_spans_.as<SpanRec>();
   da.inl_out = sp_inl_.as<InlRec>();
+  da.tc_out = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
   prof.begin(s);
   launch_desc(da, true, s);
   prof.end("desc", s);
@@ -952,6 +960,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.inl_rows = sp_inl_.as<InlRec>();
   a.sres = sp_res_.as<TopicSpansDev>();
   a.pcount = sp_pcount_.as<unsigned long long>();
+  a.tc = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
   a.work = nullptr;
   if (prof.work()) {
     grow(sp_work_, kPatchRegions * kWork * sizeof(unsigned long long));
@@ -962,10 +971,10 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
   uint32_t* h_err = reinterpret_cast<uint32_t*>(h_roff + kPatchRegions + 1);
   uint64_t n_patches = 0, max_region = 0;
-  // k_merge register budget: on a large index the merge waits on memory more often and 6 waves
-  // per SIMD beat the unconstrained 5 (10M subscriptions: 7.7 -> 5.7 ms per 1M topics); on a
-  // small one the spills cost more (1M: 1.8 vs 2.4 ms). MQ_OPT_MERGE_WAVES overrides.
-  const uint32_t merge_wpe = merge_wpe_opt_ ? merge_wpe_opt_ : (ix.subs.live >= kMergeWpeMinSubs ? kMergeWavesPerEU : 1u);
+  // k_merge register budget: the kernel waits on memory, and eight waves per SIMD (64 VGPRs, a
+  // few spills) beat six (80 VGPRs) at 1M and 10M subscriptions (4.37 -> 4.17 ms and 1.37 -> 1.27
+  // ms per 1M topics, profiles/r02/tune_walk_merge.jsonl). MQ_OPT_MERGE_WAVES overrides.
+  const uint32_t merge_wpe = merge_wpe_opt_ ? merge_wpe_opt_ : kMergeWavesPerEU;
   for (int attempt = 0;; attempt++) {
     a.patches = sp_patches_.as<PatchRec>();
     a.rcap = rcap_;

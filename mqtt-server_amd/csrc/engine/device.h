@@ -198,7 +198,7 @@ class Device {
   void check_err(hipStream_t s);
   // walk (count) + scan of n topics; returns the batch totals (synchronises s)
   TopicOff walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                     const uint32_t** gathers, uint32_t* gstride);
+                     const uint32_t** gathers, uint32_t* gstride, bool lists);
   // Messages: the level-order retained image (rebuilt when ix.retained_version() moved) and the
   // two query paths — run arithmetic over the image (k_msgq) and the particle walk (k_msg:
   // the Q6 state, nesting beyond kMsgStack, MQ_OPT_MSG_IMAGE = 0)
@@ -275,7 +275,9 @@ class Device {
     uint64_t version = 0;
     TopicOff tot{0, 0, 0, 0, 0};
     DevIndex di{};
+    bool lists = true;             // the walk counted the lists (else k_desc did, into sp_tc_)
   } sb_;
+  DevBuf sp_tc_;                     // per-topic counts from k_desc<true> (walk without lists)
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
   uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf img_node_, img_pos_, img_cl_, img_lp_, img_h_, img_cnt_, img_coff_, img_bsum_, img_bpre_;
@@ -288,6 +290,8 @@ class Device {
   uint64_t msg_spec_bytes_ = 0;  // its budget (MQ_MSG_SPEC_MB)
   uint32_t msg_wpe_opt_ = 0;     // k_msg variant (MQ_OPT_MSG_WAVES; 0: by index size)
   uint32_t merge_wpe_opt_ = 0;   // k_merge variant (MQ_OPT_MERGE_WAVES; 0: by index size)
+  uint32_t walk_wpe_ = 8;        // k_walk count pass register budget (MQ_OPT_WALK_WAVES)
+  bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
   uint32_t n_cus_ = 1;
   bool serial_ = false;       // MQ_OPT_SERIAL: k_merge on the launch stream (isolated kernel times)

@@ -246,7 +246,7 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   size_t cap = 1024;
   uint64_t want = expected_nodes ? expected_nodes : expected_subs * 3;
   while (cap < want * 2) cap <<= 1;
-  edges.h.assign(cap, EdgeSlot{0, 0, kEdgeEmpty, kNone, 0, 0});
+  edges.h.assign(cap, EdgeSlot{0, 0, kEdgeEmpty, kNone, kNone, kNone});
   edges.epoch++;
   if (want) {
     walk.h.reserve(want);
@@ -293,15 +293,32 @@ void Index::edge_rehash(size_t cap, unsigned threads) {
   reserve_resident(fresh, cap, threads);
   old.swap(edges.h);
   edges.h.swap(fresh);
-  edges.h.assign(cap, EdgeSlot{0, 0, kEdgeEmpty, kNone, 0, 0});
+  edges.h.assign(cap, EdgeSlot{0, 0, kEdgeEmpty, kNone, kNone, kNone});
   edges.epoch++;
   edges.all_dirty = true;
   n_edges_ = n_tombs_ = 0;
   for (const EdgeSlot& e : old)
-    if (e.parent != kEdgeEmpty && e.parent != kEdgeTomb) edge_insert(e.parent, SegKey{e.k0, e.k1}, e.child);
+    if (e.parent != kEdgeEmpty && e.parent != kEdgeTomb) edge_insert(e.parent, SegKey{e.k0, e.k1}, e.child, e.plus, e.hash);
 }
 
-void Index::edge_insert(uint32_t parent, const SegKey& k, uint32_t child) {
+void Index::edge_walk_sync(uint32_t n) {
+  if (n == kRoot) return;  // the walk reads the root's NodeWalk itself
+  const uint32_t p = walk.h[n].parent_flags & kParentMask;
+  const SegKey& k = nh_[n].key;
+  const uint64_t m = edges.size() - 1;
+  for (uint64_t i = edge_hash(p, k) & m;; i = (i + 1) & m) {
+    EdgeSlot& e = edges.h[i];
+    if (e.parent == kEdgeEmpty) throw std::logic_error("edge_walk_sync: particle without an edge");
+    if (e.parent == p && e.child == n) {
+      e.plus = walk.h[n].plus_child;
+      e.hash = walk.h[n].hash_child;
+      edges.mark(i);
+      return;
+    }
+  }
+}
+
+void Index::edge_insert(uint32_t parent, const SegKey& k, uint32_t child, uint32_t plus, uint32_t hash) {
   if ((n_edges_ + n_tombs_ + 1) * 2 > edges.size())
     edge_rehash(n_edges_ * 4 > edges.size() ? edges.size() * 2 : edges.size());
   const uint64_t m = edges.size() - 1;
@@ -310,7 +327,7 @@ void Index::edge_insert(uint32_t parent, const SegKey& k, uint32_t child) {
     EdgeSlot& e = edges.h[i];
     if (e.parent == kEdgeEmpty || e.parent == kEdgeTomb) {
       if (e.parent == kEdgeTomb) n_tombs_--;
-      e = EdgeSlot{k.k0, k.k1, parent, child, 0, 0};
+      e = EdgeSlot{k.k0, k.k1, parent, child, plus, hash};
       edges.mark(i);
       n_edges_++;
       return;
@@ -411,6 +428,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   edge_insert(parent, k, id);
   if (h.str == 0) walk.at_w(parent).plus_child = id;
   if (h.str == 1) walk.at_w(parent).hash_child = id;
+  if (h.str <= 1) edge_walk_sync(parent);
   NodeMsg& pm = msg.at_w(parent);
   h.child_pos = pm.child_cnt;
   msg.h[id].child_pos = pm.child_cnt;
@@ -444,6 +462,7 @@ void Index::remove_node(uint32_t n) {
   edge_erase(p, h.key, n);
   if (h.str == 0) walk.at_w(p).plus_child = kNone;
   if (h.str == 1) walk.at_w(p).hash_child = kNone;
+  if (h.str <= 1) edge_walk_sync(p);
   NodeMsg& pm = msg.at_w(p);
   const ChildRec last = children.m.h[pm.child_off + pm.child_cnt - 1];
   children.m.at_w(pm.child_off + h.child_pos) = last;
@@ -623,6 +642,15 @@ bool Index::check(std::string* why) {
     if (!nh_[n].live) continue;
     const NodeLists& L = lists.h[n];
     const std::string at = "node " + std::to_string(n);
+    if (n != kRoot) {  // the incoming edge carries the node's '+' / '#' children
+      const uint32_t par = walk.h[n].parent_flags & kParentMask;
+      const uint64_t m = edges.size() - 1;
+      uint64_t i = edge_hash(par, nh_[n].key) & m;
+      while (edges.h[i].parent != kEdgeEmpty && !(edges.h[i].parent == par && edges.h[i].child == n)) i = (i + 1) & m;
+      const EdgeSlot& e = edges.h[i];
+      if (e.parent != par) return bad(at + ": no incoming edge");
+      if (e.plus != walk.h[n].plus_child || e.hash != walk.h[n].hash_child) return bad(at + ": edge '+'/'#' copy stale");
+    }
     if ((uint64_t)L.sub_off + L.n_direct + L.n_merge > subs.m.size() || L.n_direct + L.n_merge > nh_[n].sub_cap)
       return bad(at + ": subscription list out of bounds");
     if ((uint64_t)L.shr_off + L.shr_cnt > shr.m.size() || (uint64_t)L.inl_off + L.inl_cnt > inl.m.size())

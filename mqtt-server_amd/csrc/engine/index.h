@@ -371,7 +371,9 @@ class Index {
   // Refresh n's entry in its parent's children slab from msg[n] (after any NodeMsg change).
   void child_rec_sync(uint32_t n);
   void add_below_live(uint32_t n, int delta);
-  void edge_insert(uint32_t parent, const SegKey& k, uint32_t child);
+  void edge_insert(uint32_t parent, const SegKey& k, uint32_t child, uint32_t plus = kNone, uint32_t hash = kNone);
+  // Copy n's '+' / '#' children (NodeWalk) into n's incoming edge slot (EdgeSlot.plus / hash).
+  void edge_walk_sync(uint32_t n);
   void edge_erase(uint32_t parent, const SegKey& k, uint32_t child);
   void edge_rehash(size_t cap, unsigned threads = 1);
   uint32_t intern_str(std::string_view s);

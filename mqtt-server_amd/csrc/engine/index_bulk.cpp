@@ -424,6 +424,8 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
           E[i].k0 = sk.k0;
           E[i].k1 = sk.k1;
           E[i].child = id;
+          E[i].plus = walk.h[id].plus_child;  // final: every level is built before the edges
+          E[i].hash = walk.h[id].hash_child;
           break;
         }
         i = (i + 1) & em;

@@ -29,8 +29,7 @@ constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (on
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
 constexpr uint32_t kWork = 4;
-constexpr uint32_t kMergeWavesPerEU = 6;  // k_merge register budget: 1 (none), 6 or 8 waves per SIMD
-constexpr uint64_t kMergeWpeMinSubs = 4000000;  // ... used from this many subscriptions on
+constexpr uint32_t kMergeWavesPerEU = 8;  // k_merge<spans> register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.
 struct DevIndex {
@@ -141,6 +140,9 @@ struct EmitArgs {
   // device table (a kernel-argument array indexed at run time would go through scratch)
   uint32_t n_xf;
   const struct XSrc* xsrc;
+  // span format, walk without lists: per-topic counts from k_desc (rows, shared, merge; no inline
+  // rows) in place of the offsets' differences
+  const TopicCount* tc;
 };
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile
@@ -165,6 +167,7 @@ struct DescArgs {
   // span format: one SpanRec per gather, inline rows copied to inl_out at off[t].inl
   SpanRec* spans;
   InlRec* inl_out;
+  TopicCount* tc_out;  // span format, walk without lists: per-topic rows / shared / merge counts
 };
 
 // Batched auth.MatchTopic (k_acl).
@@ -198,8 +201,13 @@ struct PickArgs {
 };
 void launch_pick(const PickArgs& a, hipStream_t s);  // a.sres != null: span format
 
-void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
-                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf, hipStream_t s);
+// lists = true: the count pass reads every gathered particle's lists and counts its rows, shared
+// and inline members (the row format, and span batches with inline subscriptions or a device
+// share pick); false: it counts gathers only and k_desc<true> counts the rest (DescArgs.tc_out).
+// wpe: the count pass's register budget (8: eight waves per SIMD, with spills; else unconstrained).
+void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
+                 const DevIndex& ix, TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf,
+                 hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);

@@ -31,26 +31,29 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Byte reader with a one-chunk register cache: one 16-byte load serves 16 sequential byte
 // reads. The topic buffer must be readable up to its next 16-byte boundary (include/mqmatch.h):
-// every chunk this reader loads holds at least one byte of the buffer.
-struct ByteReader {
+// every chunk this reader loads holds at least one byte of the buffer. P: the position type —
+// 32-bit positions (relative to a 16-byte-aligned base) save registers in the walk.
+template <class P = uint64_t>
+struct ByteReaderT {
   const uint8_t* base;
-  uint64_t ci;
+  P ci;
   u32x4 c;
-  __device__ __forceinline__ explicit ByteReader(const uint8_t* b) : base(b), ci(~0ull) {}
-  __device__ __forceinline__ u32x4 chunk(uint64_t k) {
+  __device__ __forceinline__ explicit ByteReaderT(const uint8_t* b) : base(b), ci((P)~(P)0) {}
+  __device__ __forceinline__ u32x4 chunk(P k) {
     if (k != ci) {
-      c = *reinterpret_cast<const u32x4*>(base + (k << 4));
+      c = *reinterpret_cast<const u32x4*>(base + ((uint64_t)k << 4));
       ci = k;
     }
     return c;
   }
-  __device__ __forceinline__ uint32_t at(uint64_t i) {
+  __device__ __forceinline__ uint32_t at(P i) {
     const u32x4 v = chunk(i >> 4);
     const uint32_t w = ((uint32_t)i >> 2) & 3;
     const uint32_t word = w == 0 ? v.x : (w == 1 ? v.y : (w == 2 ? v.z : v.w));
     return (word >> (((uint32_t)i & 3) * 8)) & 0xffu;
   }
 };
+using ByteReader = ByteReaderT<uint64_t>;
 
 // SWAR segment scanning: a 16-byte chunk is searched for '/' with exact per-byte zero tests, so
 // the walk does per-chunk rather than per-byte work; only segments longer than 15 bytes (hashed
@@ -65,12 +68,13 @@ __device__ __forceinline__ uint32_t slash_mask(const u32x4& c) {  // bit i: byte
 }
 
 // First '/' in [s, end), or end. Bytes past `end` belong to the next topic.
-__device__ __forceinline__ uint64_t find_slash(ByteReader& R, uint64_t s, uint64_t end) {
+template <class P>
+__device__ __forceinline__ P find_slash(ByteReaderT<P>& R, P s, P end) {
   if (s >= end) return end;
-  uint64_t k = s >> 4;
+  P k = s >> 4;
   uint32_t m = slash_mask(R.chunk(k)) & (0xFFFFu << (s & 15));
   for (;;) {
-    if (m) return min((k << 4) + (uint64_t)(__ffs(m) - 1), end);
+    if (m) return min((P)((k << 4) + (P)(__ffs(m) - 1)), end);
     k++;
     if ((k << 4) >= end) return end;
     m = slash_mask(R.chunk(k));
@@ -78,13 +82,14 @@ __device__ __forceinline__ uint64_t find_slash(ByteReader& R, uint64_t s, uint64
 }
 
 // Start of the segment that ends at e: one past the last '/' in [b0, e), or b0.
-__device__ __forceinline__ uint64_t seg_start_before(ByteReader& R, uint64_t b0, uint64_t e) {
+template <class P>
+__device__ __forceinline__ P seg_start_before(ByteReaderT<P>& R, P b0, P e) {
   if (e <= b0) return b0;
-  uint64_t k = (e - 1) >> 4;
+  P k = (e - 1) >> 4;
   const uint32_t top = (uint32_t)((e - 1) & 15);
   uint32_t m = slash_mask(R.chunk(k)) & (top == 15 ? 0xFFFFu : ((2u << top) - 1u));
   for (;;) {
-    if (m) return max((k << 4) + (uint64_t)(31 - __clz(m)) + 1, b0);
+    if (m) return max((P)((k << 4) + (P)(31 - __clz(m)) + 1), b0);
     if ((k << 4) <= b0) return b0;
     k--;
     m = slash_mask(R.chunk(k));
@@ -93,15 +98,16 @@ __device__ __forceinline__ uint64_t seg_start_before(ByteReader& R, uint64_t b0,
 
 // Key (layout.h) of the segment [s, e): inline segments (<= 15 bytes) are cut out of at most two
 // chunks with funnel shifts; longer ones take the byte-wise hash of SegKeyBuilder.
-__device__ __forceinline__ SegKey key_of(ByteReader& R, uint64_t s, uint64_t e) {
+template <class P>
+__device__ __forceinline__ SegKey key_of(ByteReaderT<P>& R, P s, P e) {
   const uint32_t len = (uint32_t)(e - s);
   if (len > kInlineSegMax) {
     SegKeyBuilder kb;
-    for (uint64_t i = s; i < e; i++) kb.push(R.at(i));
+    for (P i = s; i < e; i++) kb.push(R.at(i));
     return kb.finish();
   }
   if (len == 0) return SegKey{0, 0};
-  const uint64_t k = s >> 4;
+  const P k = s >> 4;
   const u32x4 c0 = R.chunk(k);
   const u32x4 c1 = ((e - 1) >> 4) != k ? R.chunk(k + 1) : u32x4{0u, 0u, 0u, 0u};
   const uint64_t q0 = c0.x | (uint64_t)c0.y << 32, q1 = c0.z | (uint64_t)c0.w << 32;
@@ -119,123 +125,182 @@ __device__ __forceinline__ SegKey key_of(ByteReader& R, uint64_t s, uint64_t e) 
 
 // Scan the segment that starts at s: returns the position of its terminating '/' (or end) and
 // its key (layout.h).
-__device__ __forceinline__ uint64_t scan_segment(ByteReader& R, uint64_t s, uint64_t end, SegKey* key) {
-  const uint64_t e = find_slash(R, s, end);
+template <class P>
+__device__ __forceinline__ P scan_segment(ByteReaderT<P>& R, P s, P end, SegKey* key) {
+  const P e = find_slash(R, s, end);
   *key = key_of(R, s, e);
   return e;
 }
 
-// particles.get(key) (topics.go:803-807) through the global edge table.
-__device__ __forceinline__ uint32_t lookup(const DevIndex& ix, uint32_t parent, const SegKey& k,
-                                          const uint8_t* seg, uint32_t len) {
+// particles.get(key) (topics.go:803-807) through the global edge table. The slot that names the
+// child also carries the child's '+' and '#' children (EdgeSlot.plus / hash).
+struct EdgeHit {
+  uint32_t child, plus, hash;
+};
+__device__ __forceinline__ EdgeHit lookup_edge(const DevIndex& ix, uint32_t parent, const SegKey& k,
+                                               const uint8_t* seg, uint32_t len) {
   uint64_t i = edge_hash(parent, k) & ix.edge_mask;
   for (uint64_t probes = 0; probes <= ix.edge_mask; probes++) {
     const EdgeSlot e = ix.edges[i];
-    if (e.parent == kEdgeEmpty) return kNone;
+    if (e.parent == kEdgeEmpty) break;
     if (e.parent == parent && e.k0 == k.k0 && e.k1 == k.k1) {
-      if (!seg_is_long(k)) return e.child;
+      if (!seg_is_long(k)) return EdgeHit{e.child, e.plus, e.hash};
       const SegInfo si = ix.seginfo[ix.walk[e.child].seg];
       bool eq = si.len == len;
       for (uint32_t j = 0; eq && j < len; j++) eq = ix.segbytes[si.off + j] == seg[j];
-      if (eq) return e.child;
+      if (eq) return EdgeHit{e.child, e.plus, e.hash};
     }
     i = (i + 1) & ix.edge_mask;
   }
-  return kNone;
+  return EdgeHit{kNone, kNone, kNone};
+}
+
+__device__ __forceinline__ uint32_t lookup(const DevIndex& ix, uint32_t parent, const SegKey& k,
+                                          const uint8_t* seg, uint32_t len) {
+  return lookup_edge(ix, parent, k, seg, len).child;
 }
 
 // ---------------------------------------------------------------------------------------------
 // k_walk: the match walk (thread per topic)
 // ---------------------------------------------------------------------------------------------
+// The reference's DFS (topics.go:603-625): at a particle, the literal child's subtree, then the
+// '+' child's, then the '#' child's gather. A particle found by an edge probe comes with its '+'
+// and '#' children (EdgeSlot.plus / hash), so going down costs one probe. Coming back up needs
+// only the parent's '+' / '#' children (its literal child is done): for the first kWalkPath
+// levels they wait in LDS (8 B per level and thread), deeper levels return through the parent
+// pointers of the NodeWalk records (the stackless form).
 // FILL=false: count pass; also writes the first kGatherCap gathers of each topic to its slot
 // of `gathers` (stride kGatherCap) and flags a topic with more. FILL=true: writes every gather
 // compactly at off[t].g (run only when some topic overflowed its slot).
-template <bool FILL>
-__global__ __launch_bounds__(256) void k_walk(const uint8_t* __restrict__ tb,
+// LISTS=true: the count pass reads each gathered particle's lists (rows, shared, inline and
+// may-merge counts); LISTS=false: gathers only (k_desc<true> reads the lists).
+constexpr uint32_t kWalkPath = 8;
+// WPE: minimum waves per SIMD asked of the register allocator (1: no constraint).
+template <bool FILL, bool LISTS, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walk(const uint8_t* __restrict__ tb,
                                               const uint64_t* __restrict__ to, uint32_t n,
                                               DevIndex ix, TopicCount* __restrict__ cnt,
                                               const TopicOff* __restrict__ off,
                                               uint32_t* __restrict__ gathers, uint32_t* __restrict__ ovf) {
+  __shared__ uint2 path[kWalkPath][256];  // level d: the '+' / '#' children of the particle at depth d
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  const uint64_t b0 = to[t], b1 = to[t + 1];
+  const uint64_t a0 = to[t], a1 = to[t + 1];
   uint32_t ng = 0, rows = 0, shared = 0, inl = 0, merge = 0;
   uint32_t* gout = FILL ? gathers + off[t].g : gathers + (uint64_t)t * kGatherCap;
 
-  if (b1 > b0) {  // Subscribers("") matches nothing (topics.go:598-600)
-    ByteReader R(tb);
+  if (a1 > a0) {  // Subscribers("") matches nothing (topics.go:598-600)
+    // positions relative to the 16-byte chunk that holds the topic's first byte (a topic is far
+    // shorter than 4 GB: MQTT caps it at 65,535 bytes)
+    const uint8_t* tbase = tb + (a0 & ~15ull);
+    const uint32_t b0 = (uint32_t)(a0 & 15), b1 = b0 + (uint32_t)(a1 - a0);
+    ByteReaderT<uint32_t> R(tbase);
     const bool dollar = R.at(b0) == '$';
-    // gather{Subscriptions,SharedSubscriptions,InlineSubscriptions} of one particle
-    auto gather = [&](uint32_t node, bool with_inline) {
-      const NodeLists L = ix.lists[node];
-      // [MQTT-4.7.1-1]: '$' topics skip subscriptions whose filter starts with '+'/'#' (Q3)
-      const bool subs_ok = !(dollar && (L.flags & kFlagSeg0Wild));
-      const uint32_t gw = node | (subs_ok ? kGatherSubs : 0u) | (with_inline ? kGatherInline : 0u);
-      if (FILL || ng < kGatherCap) gout[ng] = gw;
-      if (!FILL) {
-        if (subs_ok) {
-          rows += L.n_direct + L.n_merge;
-          merge += L.n_merge;
+    // gather{Subscriptions,SharedSubscriptions,InlineSubscriptions} of one particle; wild: the
+    // particle's path starts with a '+'/'#' segment (kFlagSeg0Wild)
+    auto gather = [&](uint32_t node, bool with_inline, bool wild) __attribute__((always_inline)) {
+      if (LISTS) {
+        const NodeLists L = ix.lists[node];
+        // [MQTT-4.7.1-1]: '$' topics skip subscriptions whose filter starts with '+'/'#' (Q3)
+        const bool subs_ok = !(dollar && (L.flags & kFlagSeg0Wild));
+        const uint32_t gw = node | (subs_ok ? kGatherSubs : 0u) | (with_inline ? kGatherInline : 0u);
+        if (FILL || ng < kGatherCap) gout[ng] = gw;
+        if (!FILL) {
+          if (subs_ok) {
+            rows += L.n_direct + L.n_merge;
+            merge += L.n_merge;
+          }
+          shared += L.shr_cnt;
+          if (with_inline) inl += L.inl_cnt;
         }
-        shared += L.shr_cnt;
-        if (with_inline) inl += L.inl_cnt;
+      } else {
+        const bool subs_ok = !(dollar && wild);
+        const uint32_t gw = node | (subs_ok ? kGatherSubs : 0u) | (with_inline ? kGatherInline : 0u);
+        if (FILL || ng < kGatherCap) gout[ng] = gw;
       }
       ng++;
     };
 
-    uint32_t node = kRoot;
+    uint2* my_path = &path[0][threadIdx.x];  // level d at my_path[d * 256]
+    uint32_t p_isplus = 0;                   // bit d: the particle at depth d + 1 is a '+' child
+    const NodeWalk rw = ix.walk[kRoot];
+    uint32_t node = kRoot, plus = rw.plus_child, hash = rw.hash_child, depth = 0;
+    bool wild0 = false;  // segment 0 of the path is '+'/'#'
     SegKey key;
-    uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
+    uint32_t s = b0, e = scan_segment(R, b0, b1, &key);
     int state = 0;  // 0: literal child next, 1: '+' child next, 2: '#' gather and return
-    for (uint64_t guard = 0;; guard++) {
+    // go down to child c (its '+' / '#' children known), to match the next segment
+    auto descend = [&](uint32_t c, uint32_t cp, uint32_t ch, bool isplus) __attribute__((always_inline)) {
+      if (depth < kWalkPath) my_path[depth * 256] = make_uint2(plus, hash);
+      if (depth < 32) p_isplus = isplus ? (p_isplus | (1u << depth)) : (p_isplus & ~(1u << depth));
+      depth++;
+      node = c;
+      plus = cp;
+      hash = ch;
+      s = e + 1;
+      e = scan_segment(R, s, b1, &key);
+      state = 0;
+    };
+    for (uint32_t guard = 0;; guard++) {
       if (guard > kWalkGuard) {  // never reached on a well-formed image; fail loudly, not hang
         atomicOr(ix.err, kErrWalkGuard);
         break;
       }
       const bool has_next = e < b1;
+      const bool at_root = depth == 0;
       if (state == 0) {
         state = 1;
         const uint32_t len = (uint32_t)(e - s);
+        const uint32_t c0 = len ? R.at(s) : 0u;  // an empty last segment may end the buffer
         // A literal "+" segment makes the reference visit the '+' child twice with identical
         // results (topics.go:603); the '+' branch below covers it.
-        if (!(len == 1 && R.at(s) == '+')) {
-          const uint32_t p = lookup(ix, node, key, tb + s, len);
-          if (p != kNone) {
+        if (!(len == 1 && c0 == '+')) {
+          const EdgeHit h = lookup_edge(ix, node, key, tbase + s, len);
+          if (h.child != kNone) {
+            const bool cw = at_root ? (c0 == '+' || c0 == '#') : wild0;
             if (has_next) {
-              node = p;
-              s = e + 1;
-              e = scan_segment(R, s, b1, &key);
-              state = 0;
+              if (at_root) wild0 = cw;
+              descend(h.child, h.plus, h.hash, false);
               continue;
             }
-            gather(p, true);
-            const uint32_t w = ix.walk[p].hash_child;  // filter/# matches filter (topics.go:612)
-            if (w != kNone) gather(w, false);          // inline: the particle's own again (Q2)
-          }
+            gather(h.child, true, cw);
+            if (h.hash != kNone) gather(h.hash, false, cw);  // filter/# matches filter (topics.go:612)
+          }                                                   // inline: the particle's own again (Q2)
         }
       }
       if (state == 1) {
         state = 2;
-        const uint32_t p = ix.walk[node].plus_child;
-        if (p != kNone) {
+        if (plus != kNone) {
           if (has_next) {
-            node = p;
-            s = e + 1;
-            e = scan_segment(R, s, b1, &key);
-            state = 0;
+            const NodeWalk pw = ix.walk[plus];
+            if (at_root) wild0 = true;
+            descend(plus, pw.plus_child, pw.hash_child, true);
             continue;
           }
-          gather(p, true);
+          gather(plus, true, at_root || wild0);
         }
       }
-      const NodeWalk nw = ix.walk[node];
-      if (nw.hash_child != kNone) gather(nw.hash_child, true);  // topics.go:621-625
-      if (node == kRoot) break;
-      // return to the parent: restore its segment window and continue after this branch
-      node = nw.parent_flags & kParentMask;
+      if (hash != kNone) gather(hash, true, at_root || wild0);  // topics.go:621-625
+      if (at_root) break;
+      // return to the parent: its '+' / '#' children, and continue after this branch
+      const bool was_plus = depth - 1 < 32 ? ((p_isplus >> (depth - 1)) & 1u) != 0
+                                           : (ix.walk[node].parent_flags & kFlagPlusKey) != 0;
+      state = was_plus ? 2 : 1;
+      depth--;
+      if (depth < kWalkPath) {
+        const uint2 ph = my_path[depth * 256];
+        plus = ph.x;
+        hash = ph.y;
+        // `node` is not needed above kWalkPath: the parent's literal child is done, and every
+        // return from here on reads the path
+      } else {
+        node = ix.walk[node].parent_flags & kParentMask;
+        const NodeWalk pw = ix.walk[node];
+        plus = pw.plus_child;
+        hash = pw.hash_child;
+      }
       e = s - 1;
       s = seg_start_before(R, b0, e);
-      state = (nw.parent_flags & kFlagPlusKey) ? 2 : 1;
     }
   }
   if (!FILL) {
@@ -421,9 +486,28 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
   uint32_t* tile_s = SPANS ? nullptr : tile_r + cp.n_tiles0;
   uint32_t* tile_i = SPANS ? nullptr : tile_s + cp.n_tiles1;
   const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
-  for (uint32_t i = 0; i < n_g; i++) {
-    const uint32_t gw = gw_src[i];
-    const NodeLists L = a.ix.lists[gw & kGatherNode];
+  uint32_t n_merge = 0;
+  // four gathers per round: their gather words, lists and pair-block headers are loaded together
+  // (one latency per round instead of per gather)
+  constexpr uint32_t U = 4;
+  for (uint32_t i0 = 0; i0 < n_g; i0 += U) {
+    uint32_t gwv[U];
+    NodeLists Lv[U];
+    NodePair Pv[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) gwv[u] = i0 + u < n_g ? gw_src[i0 + u] : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) Lv[u] = a.ix.lists[gwv[u] & kGatherNode];
+    if (SPANS) {
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) Pv[u] = a.ix.npair[gwv[u] & kGatherNode];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+    const uint32_t i = i0 + u;
+    if (i >= n_g) break;
+    const uint32_t gw = gwv[u];
+    const NodeLists& L = Lv[u];
     const uint32_t rn = (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
     const uint32_t in = (gw & kGatherInline) ? L.inl_cnt : 0u;
     const uint64_t g = o0.g + i;
@@ -440,7 +524,7 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
       d.i_pos = 0;
       d.i_src = 0;
       if (d.mdir & kDescMerge) {
-        const NodePair P = a.ix.npair[gw & kGatherNode];
+        const NodePair& P = Pv[u];
         d.s_pos = P.ent_off;
         d.s_src = P.ent_mask;
         if (a.ix.xinfo) {
@@ -452,6 +536,7 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     }
     a.desc[g] = d;
     if (SPANS) {
+      if (gw & kGatherSubs) n_merge += L.n_merge;
       a.spans[g] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
       for (uint32_t k = 0; k < in; k++) a.inl_out[ipos + k] = a.ix.inl[L.inl_off + k];
     } else {
@@ -463,7 +548,9 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     rpos += rn;
     spos += L.shr_cnt;
     ipos += in;
+    }
   }
+  if (SPANS && a.tc_out) a.tc_out[t] = TopicCount{n_g, rpos, spos - (uint32_t)o0.shr, 0u, n_merge};
 }
 
 // Stream S of one tile: rows [x0, x1) of the chunk's stream S (0: client rows, 1: shared rows,
@@ -626,9 +713,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (uint32_t t = a.t0 + blockIdx.x * 4 + wv; t < a.t1; t += gridDim.x * 4) {
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
-  const uint32_t cap = (uint32_t)(o1.rows - o0.rows);
   const uint64_t ib = o0.inl - a.base.inl;
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
+  // per-topic counts: the offsets' differences, or k_desc's counts (walk without lists)
+  TopicCount tcn{n_g, (uint32_t)(o1.rows - o0.rows), (uint32_t)(o1.shr - o0.shr), (uint32_t)(o1.inl - o0.inl),
+                 (uint32_t)(o1.merge - o0.merge)};
+  if (SPANS && a.tc) tcn = a.tc[t];
+  const uint32_t cap = tcn.rows;
   const GDesc* __restrict__ gd = a.desc + o0.g;
   SubRec* __restrict__ crow = a.rows;  // chunk-relative rows (GDesc positions), row format
   uint32_t n_nonbase = 0, n_ext = 0;
@@ -637,23 +728,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   bool pfit = true;      // the reservation fits the pool
   uint32_t w_ent = 0, w_rec = 0, w_link = 0;  // this lane's work (MQ_PROF_WORK)
 
-  // reserve n patch slots for this topic in its region (wave-uniform)
+  // reserve n patch slots for this topic in its region (wave-uniform). The atomic's answer is
+  // taken only when the first patch is written (settle): by then the pair-slot loads issued
+  // after it have returned, so the reservation costs no round trip of its own.
+  unsigned long long resv = 0;  // lane 0: the region's counter before this topic's reservation
+  uint64_t resv_n = 0;
+  bool resv_pending = false;
   auto reserve = [&](uint64_t n) __attribute__((always_inline)) {
-    const uint32_t region = t & (kPatchRegions - 1);
-    unsigned long long b = 0;
-    if (lane == 0 && n) b = atomicAdd(a.pcount + region, (unsigned long long)n);
-    b = __shfl((unsigned long long)b, 0, 64);
-    pfit = b + n <= a.rcap;
-    pbase = (uint64_t)region * a.rcap + b;
+    if (lane == 0 && n) resv = atomicAdd(a.pcount + (t & (kPatchRegions - 1)), (unsigned long long)n);
+    resv_n = n;
+    resv_pending = true;
+  };
+  auto settle = [&]() __attribute__((always_inline)) {
+    if (resv_pending) {
+      const unsigned long long b = __shfl(resv, 0, 64);
+      pfit = b + resv_n <= a.rcap;
+      pbase = (uint64_t)(t & (kPatchRegions - 1)) * a.rcap + b;
+      resv_pending = false;
+    }
   };
   // one patch per lane that wants one, compacted by ballot (wave-uniform)
   auto emit_patch = [&](bool want, uint32_t row, uint32_t meta) __attribute__((always_inline)) {
+    settle();
     const uint64_t m = __ballot(want);
     if (want && pfit) a.patches[pbase + n_patch + prefix_before(m)] = PatchRec{row, meta};
     n_patch += (uint32_t)__popcll(m);
   };
 
-  if (o1.merge > o0.merge) {  // the topic gathers may-merge records
+  if (tcn.merge) {  // the topic gathers may-merge records
     // Map every gathered node that holds may-merge records (and whose subscriptions are
     // gathered, Q3) to its gather index, and list them in gather order. Nodes are distinct
     // within a topic.
@@ -826,17 +928,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       auto flush_hits = [&]() __attribute__((always_inline)) {
         if (lane == 0) h_pre[wv][n_hit] = tot;
         wave_sync_lds();
-        for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
-          const uint32_t r = r0 + lane;
+        // record r of the staged lists: its list (binary search of the prefix) and its pair slot
+        auto locate = [&](uint32_t r, uint32_t& jj) __attribute__((always_inline)) -> PairSlot {
           const uint32_t rc = min(r, tot - 1);
           uint32_t lo = 0, hi = n_hit;  // h_pre[lo] <= rc < h_pre[hi] (lists are non-empty)
           while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (h_pre[wv][mid] <= rc) lo = mid; else hi = mid;
           }
-          const uint32_t jj = lo;
+          jj = lo;
+          return a.ix.plist[h_off[wv][lo] + (rc - h_pre[wv][lo])];
+        };
+        // software-pipelined by one round: the next 64 records' pair slots are loaded before
+        // this round's partner links, so each round waits on one load latency, not two
+        uint32_t jj_next = 0;
+        PairSlot e_next = locate(lane, jj_next);
+        for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
+          const uint32_t r = r0 + lane;
+          const uint32_t jj = jj_next;
+          const PairSlot e = e_next;
+          if (r0 + 64 < tot) e_next = locate(r0 + 64 + lane, jj_next);  // wave-uniform
           const uint32_t xa = h_ga[wv][jj];
-          const PairSlot e = a.ix.plist[h_off[wv][jj] + (rc - h_pre[wv][jj])];
           w_rec += r < tot;
           resolve(r < tot, e.meta, mg_row[wv][xa] + e.k, XS ? mg_rank[wv][xa] : 0ull, mg_gi[wv][xa], h_via[wv][jj],
                   e.mp_off, e.mp_cnt);
@@ -931,7 +1043,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
     } else {
       // Too many merge gathers for the pair analysis: resolve every may-merge record.
-      if (SPANS) reserve(o1.merge - o0.merge);
+      if (SPANS) reserve(tcn.merge);
       for (uint32_t i = 0; i < n_g; i++) {
         const GDesc d = gd[i];
         if (!(d.word & kGatherSubs)) continue;
@@ -949,7 +1061,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
   }
 
-  uint32_t n_inl = (uint32_t)(o1.inl - o0.inl);
+  uint32_t n_inl = tcn.inlines;
   if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675)
     InlRec* __restrict__ ir = a.inl_rows + ib;
     uint32_t kept = 0;
@@ -981,6 +1093,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
   }
 
+  if (SPANS) settle();
   if (lane == 0) {
     if (SPANS) {
       TopicSpansDev res;
@@ -994,7 +1107,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       res.n_rows = cap;
       res.n_client = cap - n_nonbase;
       res.n_ident = n_ext;
-      res.n_shared = (uint32_t)(o1.shr - o0.shr);
+      res.n_shared = tcn.shared;
       res.reserved = 0;
       a.sres[t] = res;
     } else {
@@ -1018,14 +1131,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 namespace mq {
 
-void launch_walk(bool fill, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
-                 TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf, hipStream_t s) {
+void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
+                 const DevIndex& ix, TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf,
+                 hipStream_t s) {
   if (!n) return;
   dim3 grid((n + 255) / 256);
-  if (fill)
-    hipLaunchKernelGGL(k_walk<true>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf);
-  else
-    hipLaunchKernelGGL(k_walk<false>, grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf);
+#define MQ_WALK(F, L, W) hipLaunchKernelGGL((k_walk<F, L, W>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf)
+  if (fill) {
+    if (lists) MQ_WALK(true, true, 1);
+    else MQ_WALK(true, false, 1);
+  } else if (wpe >= 8) {
+    if (lists) MQ_WALK(false, true, 8);
+    else MQ_WALK(false, false, 8);
+  } else {
+    if (lists) MQ_WALK(false, true, 1);
+    else MQ_WALK(false, false, 1);
+  }
+#undef MQ_WALK
 }
 
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,

@@ -77,11 +77,14 @@ MQ_HD uint64_t edge_hash(uint32_t parent, const SegKey& k) {
 constexpr uint32_t kEdgeEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kEdgeTomb = 0xFFFFFFFEu;
 
+// The slot also carries the child's own '+' and '#' children (a copy of its NodeWalk fields,
+// Index::edge_walk_sync), so the walk learns them with the probe that finds the child instead
+// of a dependent NodeWalk read.
 struct EdgeSlot {  // 32 B
   uint64_t k0, k1;
   uint32_t parent;  // kEdgeEmpty / kEdgeTomb for free slots
   uint32_t child;
-  uint32_t pad0, pad1;
+  uint32_t plus, hash;  // the child's plus_child / hash_child
 };
 
 // ---- nodes (particles, topics.go:748-757) -----------------------------------------------------

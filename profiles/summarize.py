@@ -16,8 +16,22 @@ import os
 import sys
 
 
+def kernel_stats_db(path):
+    """Kernel stats from a rocprofv3 SQLite database (the default output format of ROCm 7)."""
+    import sqlite3
+    c = sqlite3.connect(path)
+    out = []
+    for name, calls, total, avg, pct in c.execute(
+            "select name, total_calls, total_duration, average, percentage from top_kernels"):
+        out.append({"kernel": name.split("(")[0], "calls": int(calls), "avg_us": float(avg),
+                    "total_ms": float(total) / 1e3, "pct": float(pct)})
+    return out
+
+
 def kernel_stats(d):
     out = []
+    for path in glob.glob(os.path.join(d, "*.db")):
+        out.extend(kernel_stats_db(path))
     for path in glob.glob(os.path.join(d, "*kernel_stats.csv")):
         for r in csv.DictReader(open(path)):
             out.append({"kernel": r["Name"].split("(")[0], "calls": int(r["Calls"]),
