@@ -218,7 +218,9 @@ int mq_match_device(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t*
                     uint32_t n, void* hip_stream, mq_match_result* out);
 /* Device-resident results of every chunk: like mq_match_device, and for each output chunk, once
  * its kernels are queued, fn(user, chunk, first_topic, chunk_stream) is called on the calling
- * thread. `chunk` holds device pointers (row offsets relative to the chunk) of topics
+ * thread. The call returns once the batch (and the consumers' queued work) has completed, with
+ * the batch's guard flags checked: a tripped guard fails this call with MQ_EIO. (mq_match_device
+ * itself stays asynchronous: a guard tripped by its kernels fails the index's next call.) `chunk` holds device pointers (row offsets relative to the chunk) of topics
  * [first_topic, first_topic + chunk->n_topics); they stay valid for work the consumer enqueues
  * on `chunk_stream` before returning (e.g. a device-side fan-out or a D2H copy): the buffers are
  * reused only after that work. Replaces the reference's per-topic Subscribers() for GPU-side
@@ -418,8 +420,10 @@ int mq_index_check(mq_index* idx);
 #define MQ_OPT_MERGE_WAVES 7     /* k_merge waves per SIMD the registers are budgeted for (1, 6, 8) */
 #define MQ_OPT_MSG_IMAGE 8       /* Messages: 1 (default) runs over the level-order retained image;
                                     0 walks the particles (the path the Q6 state always takes) */
-#define MQ_OPT_WALK_WAVES 9       /* k_walk count pass waves per SIMD the registers are budgeted for (1, 8) */
+#define MQ_OPT_WALK_WAVES 9       /* k_walk count pass waves per SIMD the registers are budgeted for (1, 8;
+                                     16: the shared-load walk k_walku, span format without lists) */
 #define MQ_OPT_WALK_LISTS 10      /* span format: 1 makes the walk count the lists (as the row format) */
+#define MQ_OPT_FUSE_DESC 11       /* span format, index not sharded: 1 has k_merge do k_desc's work (slower; off) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. enable: 0 off,

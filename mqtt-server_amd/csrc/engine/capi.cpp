@@ -520,7 +520,7 @@ int mq_index_check(mq_index* idx) {
 }
 
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
-  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_WALK_LISTS) return fail(MQ_EINVAL, "unknown option");
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_FUSE_DESC) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
     idx->options.emplace_back(option, value);  // applied when the device is first touched
     if (idx->dev) idx->dev->set_option(option, value);

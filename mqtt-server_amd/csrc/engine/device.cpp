@@ -20,7 +20,9 @@ namespace {
 std::mutex g_pin_mu;
 std::multimap<size_t, void*> g_pin_free;  // capacity -> block
 size_t g_pin_pooled = 0;
-constexpr size_t kPinMin = 64 << 10, kPinPoolCap = 32ull << 30;
+// Pooled pinned blocks are kept up to 4 GiB per process (a broker holds this much page-locked
+// memory at most after large host-result batches); larger frees go back to the system.
+constexpr size_t kPinMin = 64 << 10, kPinPoolCap = 4ull << 30;
 size_t pin_cap(size_t bytes) {
   size_t c = kPinMin;
   while (c < bytes) c <<= 1;
@@ -230,6 +232,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_MERGE_WAVES: merge_wpe_opt_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_WAVES: walk_wpe_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_LISTS: walk_lists_ = v != 0; return true;
+    case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     default: return false;
   }
@@ -697,7 +700,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
       }
       prof.begin(ms);
-      launch_merge(a, false, merge_wpe_opt_ ? merge_wpe_opt_ : 1u, merge_blocks_, ms);
+      launch_merge(a, false, false, merge_wpe_opt_ ? merge_wpe_opt_ : 1u, merge_blocks_, ms);
       prof.end("merge", ms);
       hip_check(hipGetLastError(), "k_merge");
       const uint32_t nt = a.t1 - a.t0;
@@ -771,6 +774,11 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         r.inline_base += g.inl + lo.inl;
       }
     }
+    check_err(s);
+  } else if (fn) {
+    // chunk consumers already used the rows: the batch's guard flags are read before returning,
+    // so a tripped guard fails this call (MQ_EIO), not a later one
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     check_err(s);
   }
 }
@@ -856,7 +864,11 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   sb_.lists = walk_lists_ || select_shared_ || ix.inl.live != 0;
   const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists);
   sb_.tot = tot;
-  if (!sb_.lists) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
+  sb_.gathers = gathers;
+  sb_.gstride = gstride;
+  // An index that is not sharded has k_merge do k_desc's work (k_xlist reads GDesc records)
+  sb_.fused = !ix.sharded() && fuse_desc_;
+  if (!sb_.lists && !sb_.fused) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
   grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
   grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
   grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
@@ -881,11 +893,13 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   da.tiles = nullptr;
   da.spans = sp_spans_.as<SpanRec>();
   da.inl_out = sp_inl_.as<InlRec>();
-  da.tc_out = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
-  prof.begin(s);
-  launch_desc(da, true, s);
-  prof.end("desc", s);
-  hip_check(hipGetLastError(), "k_desc<spans>");
+  da.tc_out = sb_.lists || sb_.fused ? nullptr : sp_tc_.as<TopicCount>();
+  if (!sb_.fused) {
+    prof.begin(s);
+    launch_desc(da, true, s);
+    prof.end("desc", s);
+    hip_check(hipGetLastError(), "k_desc<spans>");
+  }
 
   if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
@@ -960,7 +974,10 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.inl_rows = sp_inl_.as<InlRec>();
   a.sres = sp_res_.as<TopicSpansDev>();
   a.pcount = sp_pcount_.as<unsigned long long>();
-  a.tc = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
+  a.tc = sb_.lists || sb_.fused ? nullptr : sp_tc_.as<TopicCount>();
+  a.gathers = sb_.gathers;
+  a.gather_stride = sb_.gstride;
+  a.spans = sp_spans_.as<SpanRec>();
   a.work = nullptr;
   if (prof.work()) {
     grow(sp_work_, kPatchRegions * kWork * sizeof(unsigned long long));
@@ -981,7 +998,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
     if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
     prof.begin(s);
-    launch_merge(a, true, merge_wpe, merge_blocks_, s);
+    launch_merge(a, true, sb_.fused, merge_wpe, merge_blocks_, s);
     prof.end("merge", s);
     hip_check(hipGetLastError(), "k_merge<spans>");
     hip_check(hipMemcpyAsync(h_pc, a.pcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),

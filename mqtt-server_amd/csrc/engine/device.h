@@ -276,6 +276,9 @@ class Device {
     TopicOff tot{0, 0, 0, 0, 0};
     DevIndex di{};
     bool lists = true;             // the walk counted the lists (else k_desc did, into sp_tc_)
+    bool fused = false;            // k_desc's work is done by k_merge (index not sharded)
+    const uint32_t* gathers = nullptr;
+    uint32_t gstride = 0;
   } sb_;
   DevBuf sp_tc_;                     // per-topic counts from k_desc<true> (walk without lists)
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
@@ -292,6 +295,7 @@ class Device {
   uint32_t merge_wpe_opt_ = 0;   // k_merge variant (MQ_OPT_MERGE_WAVES; 0: by index size)
   uint32_t walk_wpe_ = 8;        // k_walk count pass register budget (MQ_OPT_WALK_WAVES)
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
+  bool fuse_desc_ = false;       // span format: k_merge does k_desc's work (MQ_OPT_FUSE_DESC)
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
   uint32_t n_cus_ = 1;
   bool serial_ = false;       // MQ_OPT_SERIAL: k_merge on the launch stream (isolated kernel times)

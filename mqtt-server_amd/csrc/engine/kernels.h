@@ -143,6 +143,13 @@ struct EmitArgs {
   // span format, walk without lists: per-topic counts from k_desc (rows, shared, merge; no inline
   // rows) in place of the offsets' differences
   const TopicCount* tc;
+  // span format, k_desc fused into k_merge (index not sharded): each topic's gather words
+  // (stride gather_stride per topic, or compact at off[t].g when 0); k_merge writes the spans,
+  // copies the inline rows, and writes GDesc records only for a topic that needs them (beyond
+  // the pair analysis)
+  const uint32_t* gathers;
+  uint32_t gather_stride;
+  SpanRec* spans;
 };
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile
@@ -212,7 +219,8 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
-void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
+// desc: span format with k_desc fused in (a.gathers / a.spans; not for a sharded index)
+void launch_merge(const EmitArgs& a, bool spans, bool desc, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
 // first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
 // fill pass must still walk; the fill pass then walks only those.
