@@ -423,6 +423,8 @@ int mq_index_check(mq_index* idx);
 #define MQ_OPT_WALK_WAVES 9       /* k_walk count pass waves per SIMD the registers are budgeted for (1, 8;
                                      16: the shared-load walk k_walku, span format without lists) */
 #define MQ_OPT_WALK_LISTS 10      /* span format: 1 makes the walk count the lists (as the row format) */
+#define MQ_OPT_MERGE_DEDUP 12     /* span format: 1 finds topics with the same merge gathers (counter
+                                     "merge_sets" under MQ_PROF_TIMES) */
 #define MQ_OPT_FUSE_DESC 11       /* span format, index not sharded: 1 has k_merge do k_desc's work (slower; off) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 

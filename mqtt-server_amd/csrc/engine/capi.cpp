@@ -499,6 +499,7 @@ int mq_index_stats(const mq_index* cidx, mq_stats* out) {
     out->shared = x.shr.live;
     out->inlines = x.inl.live;
     out->retained = x.retained_len();
+    out->retained_live = x.msg.h[kRoot].below_live;  // live retained particles (every one is below the root)
     out->max_depth = x.max_depth();
     out->partners = x.parts.live;
     out->foreign = x.foreign_subs();
@@ -520,7 +521,7 @@ int mq_index_check(mq_index* idx) {
 }
 
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
-  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_FUSE_DESC) return fail(MQ_EINVAL, "unknown option");
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MERGE_DEDUP) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
     idx->options.emplace_back(option, value);  // applied when the device is first touched
     if (idx->dev) idx->dev->set_option(option, value);

@@ -233,6 +233,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_WALK_WAVES: walk_wpe_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_LISTS: walk_lists_ = v != 0; return true;
     case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
+    case MQ_OPT_MERGE_DEDUP: dedup_ = (uint32_t)v; return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     default: return false;
   }
@@ -894,11 +895,56 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   da.spans = sp_spans_.as<SpanRec>();
   da.inl_out = sp_inl_.as<InlRec>();
   da.tc_out = sb_.lists || sb_.fused ? nullptr : sp_tc_.as<TopicCount>();
+  da.msig = nullptr;
+  da.mcount = nullptr;
+  da.mlist = nullptr;
+  sb_.dedup = dedup_ != 0 && !ix.sharded() && !sb_.fused;
+  if (sb_.dedup) {
+    grow(dd_sig_, (size_t)n * sizeof(uint64_t));
+    grow(dd_cnt_, (size_t)n * sizeof(uint32_t));
+    grow(dd_list_, (size_t)n * kPairMax * sizeof(uint32_t));
+    da.msig = dd_sig_.as<uint64_t>();
+    da.mcount = dd_cnt_.as<uint32_t>();
+    da.mlist = dd_list_.as<uint32_t>();
+  }
   if (!sb_.fused) {
     prof.begin(s);
     launch_desc(da, true, s);
     prof.end("desc", s);
     hip_check(hipGetLastError(), "k_desc<spans>");
+  }
+  if (sb_.dedup) {  // merge-set dedup: each topic's representative (DedupArgs)
+    uint64_t slots = 1024;
+    while (slots < 2ull * n) slots <<= 1;
+    grow(dd_keys_, slots * sizeof(unsigned long long));
+    grow(dd_vals_, slots * sizeof(uint32_t));
+    grow(dd_slot_, (size_t)n * sizeof(uint32_t));
+    grow(dd_rep_, (size_t)n * sizeof(uint32_t));
+    if (!dd_nsets_.p) dd_nsets_.ensure(sizeof(unsigned long long));
+    hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
+    hip_check(hipMemsetAsync(dd_vals_.p, 0xFF, slots * sizeof(uint32_t), s), "memset");
+    hip_check(hipMemsetAsync(dd_nsets_.p, 0, sizeof(unsigned long long), s), "memset");
+    DedupArgs dd;
+    dd.n = n;
+    dd.msig = dd_sig_.as<uint64_t>();
+    dd.mcount = dd_cnt_.as<uint32_t>();
+    dd.mlist = dd_list_.as<uint32_t>();
+    dd.keys = dd_keys_.as<unsigned long long>();
+    dd.vals = dd_vals_.as<uint32_t>();
+    dd.table_mask = slots - 1;
+    dd.tslot = dd_slot_.as<uint32_t>();
+    dd.rep = dd_rep_.as<uint32_t>();
+    dd.n_sets = dd_nsets_.as<unsigned long long>();
+    prof.begin(s);
+    launch_dedup(dd, s);
+    prof.end("dedup", s);
+    hip_check(hipGetLastError(), "k_dedup");
+    if (prof.on()) {
+      unsigned long long ns = 0;
+      hip_check(hipMemcpyAsync(&ns, dd_nsets_.p, sizeof(ns), hipMemcpyDeviceToHost, s), "D2H");
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      prof.count("merge_sets", ns);
+    }
   }
 
   if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
@@ -979,10 +1025,15 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.gather_stride = sb_.gstride;
   a.spans = sp_spans_.as<SpanRec>();
   a.work = nullptr;
-  if (prof.work()) {
-    grow(sp_work_, kPatchRegions * kWork * sizeof(unsigned long long));
+  if (prof.work()) {  // [0]: the topics' pass, [1]: the merge sets' pass (dedup)
+    grow(sp_work_, 2 * kPatchRegions * kWork * sizeof(unsigned long long));
     a.work = sp_work_.as<unsigned long long>();
+    hip_check(hipMemsetAsync(a.work + kPatchRegions * kWork, 0, kPatchRegions * kWork * sizeof(unsigned long long), s),
+              "memset");
   }
+  a.rep = nullptr;
+  a.tslot = nullptr;
+  a.dd_phase = 0;
   pinned((2 * kPatchRegions + 1) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
   unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
@@ -992,6 +1043,44 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   // few spills) beat six (80 VGPRs) at 1M and 10M subscriptions (4.37 -> 4.17 ms and 1.37 -> 1.27
   // ms per 1M topics, profiles/r02/tune_walk_merge.jsonl). MQ_OPT_MERGE_WAVES overrides.
   const uint32_t merge_wpe = merge_wpe_opt_ ? merge_wpe_opt_ : kMergeWavesPerEU;
+  if (sb_.dedup) {  // phase 1: one resolution per merge set, into the set pool (regions as below)
+    grow(dd_sets_, (size_t)n * sizeof(SetInfo));
+    if (!dd_spcount_.p) dd_spcount_.ensure(kPatchRegions * sizeof(unsigned long long));
+    if (srcap_ * kPatchRegions < patch_cap_init_) {
+      srcap_ = std::max<uint64_t>((patch_cap_init_ + kPatchRegions - 1) / kPatchRegions, 16);
+      dd_spatches_.release();
+      dd_spatches_.ensure(srcap_ * kPatchRegions * sizeof(PatchRec));
+    }
+    a.rep = dd_rep_.as<uint32_t>();
+    a.tslot = dd_slot_.as<uint32_t>();
+    a.sets = dd_sets_.as<SetInfo>();
+    a.spcount = dd_spcount_.as<unsigned long long>();
+    a.dd_phase = 1;
+    unsigned long long* work0 = a.work;
+    if (a.work) a.work += kPatchRegions * kWork;
+    for (int attempt = 0;; attempt++) {
+      a.spatches = dd_spatches_.as<PatchRec>();
+      a.srcap = srcap_;
+      hip_check(hipMemsetAsync(a.spcount, 0, kPatchRegions * sizeof(unsigned long long), s), "memset");
+      if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
+      prof.begin(s);
+      launch_merge(a, true, false, merge_wpe, merge_blocks_, s);
+      prof.end("merge_sets", s);
+      hip_check(hipGetLastError(), "k_merge<spans> (sets)");
+      hip_check(hipMemcpyAsync(h_pc, a.spcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
+                "D2H");
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      uint64_t mr = 0;
+      for (uint32_t r = 0; r < kPatchRegions; r++) mr = std::max<uint64_t>(mr, h_pc[r]);
+      if (mr <= srcap_) break;
+      if (attempt) throw HipError{hipErrorUnknown, "k_merge<spans>: set patch reservations changed between runs"};
+      srcap_ = mr + mr / 4 + 64;
+      dd_spatches_.release();
+      dd_spatches_.ensure(srcap_ * kPatchRegions * sizeof(PatchRec));
+    }
+    a.work = work0;
+    a.dd_phase = 2;
+  }
   for (int attempt = 0;; attempt++) {
     a.patches = sp_patches_.as<PatchRec>();
     a.rcap = rcap_;
@@ -1047,11 +1136,11 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   out->n_inline_rows = tot.inl;
   out->n_picked_rows = select_shared_ ? tot.shr : 0;
   if (a.work) {  // MQ_PROF_WORK: k_merge's work, for its algorithmic bytes (bench.py)
-    std::vector<unsigned long long> w(kPatchRegions * kWork);
+    std::vector<unsigned long long> w(2 * kPatchRegions * kWork);
     hip_check(hipMemcpyAsync(w.data(), a.work, w.size() * sizeof(w[0]), hipMemcpyDeviceToHost, s), "D2H work");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     uint64_t sum[kWork] = {0, 0, 0, 0};
-    for (uint32_t r = 0; r < kPatchRegions; r++)
+    for (uint32_t r = 0; r < 2 * kPatchRegions; r++)
       for (uint32_t k = 0; k < kWork; k++) sum[k] += w[r * kWork + k];
     prof.count("merge_pair_entries", sum[0]);
     prof.count("merge_records", sum[1]);

@@ -277,6 +277,7 @@ class Device {
     DevIndex di{};
     bool lists = true;             // the walk counted the lists (else k_desc did, into sp_tc_)
     bool fused = false;            // k_desc's work is done by k_merge (index not sharded)
+    bool dedup = false;            // merge-set dedup ran (dd_rep_ holds the representatives)
     const uint32_t* gathers = nullptr;
     uint32_t gstride = 0;
   } sb_;
@@ -296,6 +297,10 @@ class Device {
   uint32_t walk_wpe_ = 8;        // k_walk count pass register budget (MQ_OPT_WALK_WAVES)
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
   bool fuse_desc_ = false;       // span format: k_merge does k_desc's work (MQ_OPT_FUSE_DESC)
+  uint32_t dedup_ = 0;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
+  DevBuf dd_sig_, dd_cnt_, dd_list_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_;
+  DevBuf dd_sets_, dd_spatches_, dd_spcount_;  // phase 1 of the dedup merge: SetInfo, set pool
+  uint64_t srcap_ = 0;                         // set patches per region of dd_spatches_
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
   uint32_t n_cus_ = 1;
   bool serial_ = false;       // MQ_OPT_SERIAL: k_merge on the launch stream (isolated kernel times)

@@ -706,6 +706,17 @@ bool Index::check(std::string* why) {
       }
     }
   }
+  for (uint32_t n = 0; n < nh_.size(); n++) {  // children slabs: each particle once, in its parent's
+    if (!nh_[n].live) continue;
+    const NodeMsg& M = msg.h[n];
+    if (M.child_cnt != nh_[n].n_children || M.child_cnt > nh_[n].child_cap ||
+        (uint64_t)M.child_off + nh_[n].child_cap > children.m.size())
+      return bad("node " + std::to_string(n) + ": children slab out of bounds");
+    if (n == kRoot) continue;
+    const NodeMsg& P = msg.h[M.parent];
+    if (M.child_pos >= P.child_cnt || children.m.h[P.child_off + M.child_pos].node != n)
+      return bad("node " + std::to_string(n) + ": not at its position in the parent's children slab");
+  }
   {  // below_live == live retained particles strictly below, recomputed bottom-up
     std::vector<uint32_t> below(nh_.size(), 0);
     for (uint32_t n = 0; n < nh_.size(); n++) {

@@ -150,6 +150,22 @@ struct EmitArgs {
   const uint32_t* gathers;
   uint32_t gather_stride;
   SpanRec* spans;
+  // span format, merge-set dedup (rep == null: off). dd_phase 1: each set representative resolves
+  // its merge gathers once into set-relative patches (row = x << kSetRowBits | k: k-th may-merge
+  // slot of its x-th merge gather) in the set pool, and its SetInfo; dd_phase 2: every deduped
+  // topic copies its representative's patches, translating x to its own rows.
+  const uint32_t* rep;
+  const uint32_t* tslot;
+  uint32_t dd_phase;
+  struct SetInfo* sets;
+  PatchRec* spatches;
+  unsigned long long* spcount;
+  uint64_t srcap;
+};
+constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
+struct SetInfo {  // 24 B, per representative topic
+  uint64_t base;   // its patches in the set pool
+  uint32_t n, nonbase, ext, fit;
 };
 
 // Output chunk of a batch as k_desc sees it: where its rows start and where its k_copy tile
@@ -175,7 +191,30 @@ struct DescArgs {
   SpanRec* spans;
   InlRec* inl_out;
   TopicCount* tc_out;  // span format, walk without lists: per-topic rows / shared / merge counts
+  // span format, merge-set dedup (null: off): per topic, the signature of its merge gathers'
+  // particles (in gather order), their number, and the list itself (stride kPairMax)
+  uint64_t* msig;
+  uint32_t* mcount;
+  uint32_t* mlist;
 };
+
+// Merge-set dedup (span format): topics whose merge gathers are the same particles resolve to
+// the same patches (up to row positions). k_dedup finds, per topic, the smallest topic id with
+// the same merge gathers (exact: the lists are compared) — rep[t] == t for a topic that resolves
+// itself. Table: 2^k slots of (u64 signature, u32 smallest topic); n_sets counts the reps.
+struct DedupArgs {
+  uint32_t n;
+  const uint64_t* msig;
+  const uint32_t* mcount;
+  const uint32_t* mlist;
+  unsigned long long* keys;  // table_mask + 1 signatures (0 = empty)
+  uint32_t* vals;            // table_mask + 1 smallest topic ids (kNone = empty)
+  uint64_t table_mask;
+  uint32_t* tslot;           // per topic: its table slot (kNone: not deduped)
+  uint32_t* rep;             // per topic: its representative
+  unsigned long long* n_sets;  // topics with merge gathers that are their own representative
+};
+void launch_dedup(const DedupArgs& a, hipStream_t s);
 
 // Batched auth.MatchTopic (k_acl).
 struct AclArgs {

@@ -671,6 +671,8 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
   uint32_t* tile_i = SPANS ? nullptr : tile_s + cp.n_tiles1;
   const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
   uint32_t n_merge = 0;
+  uint64_t msig = 0x6D657267652D7365ull;  // merge-set signature (a.msig)
+  uint32_t n_mg = 0;
   // four gathers per round: their gather words, lists and pair-block headers are loaded together
   // (one latency per round instead of per gather)
   constexpr uint32_t U = 4;
@@ -721,6 +723,12 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     a.desc[g] = d;
     if (SPANS) {
       if (gw & kGatherSubs) n_merge += L.n_merge;
+      if (a.msig && (d.mdir & kDescMerge)) {
+        msig = mix64(msig ^ (gw & kGatherNode)) + 0x9e3779b97f4a7c15ull;
+        if (n_mg < kPairMax) a.mlist[(uint64_t)t * kPairMax + n_mg] = gw & kGatherNode;
+        // set-relative rows hold 26 bits of slot: a larger merge gather keeps the topic apart
+        n_mg += L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1;
+      }
       a.spans[g] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
       for (uint32_t k = 0; k < in; k++) a.inl_out[ipos + k] = a.ix.inl[L.inl_off + k];
     } else {
@@ -735,6 +743,64 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     }
   }
   if (SPANS && a.tc_out) a.tc_out[t] = TopicCount{n_g, rpos, spos - (uint32_t)o0.shr, 0u, n_merge};
+  if (SPANS && a.msig) {
+    a.msig[t] = msig | 1ull;  // never 0 (the dedup table's empty key)
+    a.mcount[t] = n_mg;
+  }
+}
+
+// k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, and the
+// smallest topic id seen there. k_dedup_rep: the representative, verified list against list (a
+// signature collision leaves the topic its own representative).
+__global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.n) return;
+  const uint32_t c = a.mcount[t];
+  if (c == 0 || c > kPairMax) {
+    a.tslot[t] = kNone;
+    return;
+  }
+  const unsigned long long k = a.msig[t];
+  uint64_t i = mix64(k) & a.table_mask;
+  for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
+    const unsigned long long prev = atomicCAS(a.keys + i, 0ull, k);
+    if (prev == 0ull || prev == k) {
+      a.tslot[t] = (uint32_t)i;
+      atomicMin(a.vals + i, t);
+      return;
+    }
+    i = (i + 1) & a.table_mask;
+  }
+  a.tslot[t] = kNone;  // full table (sized 2x the topics: cannot happen)
+}
+
+__global__ __launch_bounds__(256) void k_dedup_rep(DedupArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.n) return;
+  const uint32_t sl = a.tslot[t];
+  uint32_t r = t;
+  if (sl != kNone) {
+    const uint32_t v = a.vals[sl];
+    if (v != t) {
+      const uint32_t c = a.mcount[t];
+      bool eq = a.mcount[v] == c;
+      const uint32_t* x = a.mlist + (uint64_t)t * kPairMax;
+      const uint32_t* y = a.mlist + (uint64_t)v * kPairMax;
+      for (uint32_t j = 0; eq && j < c; j++) eq = x[j] == y[j];
+      if (eq) r = v;
+    }
+  }
+  a.rep[t] = r;
+  const bool own = r == t && sl != kNone;
+  const uint64_t b = __ballot(own);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(a.n_sets, (unsigned long long)__popcll(b));
+}
+
+void launch_dedup(const DedupArgs& a, hipStream_t s) {
+  if (!a.n) return;
+  const dim3 g((a.n + 255) / 256), b(256);
+  hipLaunchKernelGGL(k_dedup_insert, g, b, 0, s, a);
+  hipLaunchKernelGGL(k_dedup_rep, g, b, 0, s, a);
 }
 
 // Stream S of one tile: rows [x0, x1) of the chunk's stream S (0: client rows, 1: shared rows,
@@ -909,6 +975,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (SPANS && a.tc) tcn = a.tc[t];
   const GDesc* __restrict__ gd = a.desc + o0.g;
   SubRec* __restrict__ crow = a.rows;  // chunk-relative rows (GDesc positions), row format
+  // merge-set dedup (wave-uniform): a representative resolves in phase 1, a deduped topic copies
+  // in phase 2, a topic that is not deduped resolves itself in phase 2
+  const uint32_t dslot = (SPANS && a.rep) ? a.tslot[t] : kNone;
+  const uint32_t drep = dslot != kNone ? a.rep[t] : t;
+  if (SPANS && a.rep && a.dd_phase == 1 && (dslot == kNone || drep != t)) continue;
+  const bool setrel = SPANS && a.rep && a.dd_phase == 1;
+  const bool dcopy = SPANS && a.rep && a.dd_phase == 2 && dslot != kNone;
+  PatchRec* __restrict__ ppool = setrel ? a.spatches : a.patches;
+  unsigned long long* __restrict__ pcnt = setrel ? a.spcount : a.pcount;
+  const uint64_t prcap = setrel ? a.srcap : a.rcap;
   uint32_t n_nonbase = 0, n_ext = 0;
   uint64_t pbase = 0;    // span format: the topic's patch range [pbase, pbase + reserved)
   uint32_t n_patch = 0;
@@ -922,15 +998,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint64_t resv_n = 0;
   bool resv_pending = false;
   auto reserve = [&](uint64_t n) __attribute__((always_inline)) {
-    if (lane == 0 && n) resv = atomicAdd(a.pcount + (t & (kPatchRegions - 1)), (unsigned long long)n);
+    if (lane == 0 && n) resv = atomicAdd(pcnt + (t & (kPatchRegions - 1)), (unsigned long long)n);
     resv_n = n;
     resv_pending = true;
   };
   auto settle = [&]() __attribute__((always_inline)) {
     if (resv_pending) {
       const unsigned long long b = __shfl(resv, 0, 64);
-      pfit = b + resv_n <= a.rcap;
-      pbase = (uint64_t)(t & (kPatchRegions - 1)) * a.rcap + b;
+      pfit = b + resv_n <= prcap;
+      pbase = (uint64_t)(t & (kPatchRegions - 1)) * prcap + b;
       resv_pending = false;
     }
   };
@@ -938,7 +1014,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   auto emit_patch = [&](bool want, uint32_t row, uint32_t meta) __attribute__((always_inline)) {
     settle();
     const uint64_t m = __ballot(want);
-    if (want && pfit) a.patches[pbase + n_patch + prefix_before(m)] = PatchRec{row, meta};
+    if (want && pfit) ppool[pbase + n_patch + prefix_before(m)] = PatchRec{row, meta};
     n_patch += (uint32_t)__popcll(m);
   };
 
@@ -1174,7 +1250,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       n_ext += __popcll(bx);
     };
 
-    if (!slow) {
+    if (dcopy) {
+      // the representative's resolution: its set-relative patches, rows translated through this
+      // topic's merge gathers (the same particles in the same order: k_dedup compared them)
+      const SetInfo si = a.sets[drep];
+      reserve(si.n);
+      for (uint32_t j0 = 0; j0 < si.n; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool want = j < si.n;
+        PatchRec pr{0, 0};
+        if (want) pr = a.spatches[si.base + j];
+        emit_patch(want, mg_row[wv][pr.row >> kSetRowBits] + (pr.row & ((1u << kSetRowBits) - 1)), pr.meta);
+      }
+      n_nonbase = si.nonbase;
+      n_ext = si.ext;
+    } else if (!slow) {
       // Pair analysis over ordered pairs (g, h) of merge gathers: g's pair block lists the slots
       // whose client also subscribes at h. Hit lists are staged in LDS and their concatenation
       // is resolved 64 records per wave-instruction.
@@ -1204,8 +1294,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           if (r0 + 64 < tot) e_next = locate(r0 + 64 + lane, jj_next);  // wave-uniform
           const uint32_t xa = h_ga[wv][jj];
           w_rec += r < tot;
-          resolve(r < tot, e.meta, mg_row[wv][xa] + e.k, XS ? mg_rank[wv][xa] : 0ull, mg_gi[wv][xa], h_via[wv][jj],
-                  e.mp_off, e.mp_cnt);
+          resolve(r < tot, e.meta, setrel ? (xa << kSetRowBits | e.k) : mg_row[wv][xa] + e.k,
+                  XS ? mg_rank[wv][xa] : 0ull, mg_gi[wv][xa], h_via[wv][jj], e.mp_off, e.mp_cnt);
         }
         n_hit = 0;
         tot = 0;
@@ -1315,6 +1405,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
   }
 
+  if (setrel) {  // phase 1: the set's resolution; the topic itself is finished in phase 2
+    settle();
+    if (lane == 0) a.sets[t] = SetInfo{pbase, n_patch, n_nonbase, n_ext, pfit ? 1u : 0u};
+    if (a.work) {  // MQ_PROF_WORK (the resolution work happens here, once per set)
+      const uint32_t e = wave_sum(w_ent), rr = wave_sum(w_rec), l = wave_sum(w_link);
+      unsigned long long* wc = a.work + (uint64_t)(t & (kPatchRegions - 1)) * kWork;
+      if (lane == 0 && (e | rr | l)) {
+        atomicAdd(wc + 0, (unsigned long long)e);
+        atomicAdd(wc + 1, (unsigned long long)rr);
+        atomicAdd(wc + 2, (unsigned long long)l);
+      }
+    }
+    continue;
+  }
   uint32_t n_inl = tcn.inlines;
   if (n_inl) {  // InlineSubscriptions[id] = last gathered (topics.go:673-675)
     InlRec* __restrict__ ir = a.inl_rows + ib;

@@ -77,7 +77,7 @@ PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP, OPT_MERGE_WAVES = \
     1, 2, 3, 4, 5, 6, 7
 OPT_MSG_IMAGE = 8
-OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_FUSE_DESC = 9, 10, 11
+OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_FUSE_DESC, OPT_MERGE_DEDUP = 9, 10, 11, 12
 
 
 class MsgResult(C.Structure):
@@ -297,6 +297,12 @@ class Engine:
         h = C.c_void_p()
         _check(L.mq_index_create(C.byref(cfg), C.byref(h)), "mq_index_create")
         self.h = h
+        # MQ_ENGINE_OPTIONS="opt=value,..." (MQ_OPT_* numbers): engine options for every index this
+        # process creates — how a test run exercises a non-default engine path
+        for kv in os.environ.get("MQ_ENGINE_OPTIONS", "").split(","):
+            if kv.strip():
+                k, v = kv.split("=")
+                self.set_option(int(k), int(v))
 
     def close(self):
         if self.h:
