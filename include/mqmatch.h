@@ -409,6 +409,9 @@ int mq_index_stats(const mq_index* idx, mq_stats* out);
    the partner's current slot). Returns 0, or MQ_EIO with the first violation in
    mq_last_error(). */
 int mq_index_check(mq_index* idx);
+/* Diagnostic, with device work: pushes pending updates, reads every device array back and
+   compares it with the host mirror. Returns 0, or MQ_EIO with the first difference. */
+int mq_device_check(mq_index* idx);
 
 /* Engine options (tuning; the defaults are the product). Returns 0 or MQ_EINVAL. */
 #define MQ_OPT_CHUNK_ROWS 1      /* row format: output rows per chunk (default 0xF0000000) */

@@ -520,6 +520,14 @@ int mq_index_check(mq_index* idx) {
   });
 }
 
+int mq_device_check(mq_index* idx) {
+  return guarded(idx, [&]() -> int {
+    const std::string why = idx->device().verify(*idx->ix);
+    if (!why.empty()) return fail(MQ_EIO, "device check: " + why);
+    return 0;
+  });
+}
+
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
   if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MERGE_DEDUP) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {

@@ -8,6 +8,8 @@
 #include <map>
 #include <mutex>
 #include <new>
+#include <string>
+#include <vector>
 
 namespace mq {
 
@@ -107,8 +109,14 @@ void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
     full = dp * 4 > npages * 3;
   }
   if (full) {
-    if (n) hip_check(hipMemcpyAsync(d, m.h.data(), n * sizeof(T), hipMemcpyHostToDevice, s), "H2D mirror");
-    *uploaded += n * sizeof(T);
+    // pieces of at most 1 GiB: one pageable H2D copy of a multi-GiB array (the 100M-retained
+    // image has 10 GB arrays) is not relied on
+    const size_t bytes = n * sizeof(T), piece = 1ull << 30;
+    for (size_t o = 0; o < bytes; o += piece)
+      hip_check(hipMemcpyAsync(reinterpret_cast<uint8_t*>(d) + o, reinterpret_cast<const uint8_t*>(m.h.data()) + o,
+                               std::min(piece, bytes - o), hipMemcpyHostToDevice, s),
+                "H2D mirror");
+    *uploaded += bytes;
   } else {
     size_t p = 0;
     while (p < npages) {  // runs of consecutive dirty pages; clean words are skipped whole
@@ -289,6 +297,51 @@ uint64_t Device::device_bytes() const {
   for (int k = 0; k < 2; k++)
     for (const DevBuf* x : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b += x->bytes;
   return b;
+}
+
+namespace {
+template <class T>
+std::string cmp_mirror(const DevMirror<T>& dm, const Mirror<T>& m, const char* name) {
+  const size_t bytes = m.size() * sizeof(T);
+  if (!bytes) return "";
+  if (!dm.d) return std::string(name) + ": not on the device";
+  std::vector<uint8_t> buf(std::min<size_t>(bytes, 256ull << 20));
+  const uint8_t* h = reinterpret_cast<const uint8_t*>(m.h.data());
+  for (size_t o = 0; o < bytes; o += buf.size()) {
+    const size_t k = std::min(buf.size(), bytes - o);
+    hip_check(hipMemcpy(buf.data(), reinterpret_cast<const uint8_t*>(dm.d) + o, k, hipMemcpyDeviceToHost), "D2H verify");
+    if (memcmp(buf.data(), h + o, k) != 0) {
+      size_t i = 0;
+      while (buf[i] == h[o + i]) i++;
+      return std::string(name) + ": device differs from the host mirror at byte " + std::to_string(o + i) + " of " +
+             std::to_string(bytes);
+    }
+  }
+  return "";
+}
+}  // namespace
+
+std::string Device::verify(Index& ix) {
+  sync(ix, nullptr);
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  std::string r;
+  if (r.empty()) r = cmp_mirror(edges_, ix.edges, "edges");
+  if (r.empty()) r = cmp_mirror(walk_, ix.walk, "walk");
+  if (r.empty()) r = cmp_mirror(lists_, ix.lists, "lists");
+  if (r.empty()) r = cmp_mirror(msg_, ix.msg, "msg");
+  if (r.empty()) r = cmp_mirror(seginfo_, ix.seginfo, "seginfo");
+  if (r.empty()) r = cmp_mirror(segbytes_, ix.segbytes, "segbytes");
+  if (r.empty()) r = cmp_mirror(subs_, ix.subs.m, "subs");
+  if (r.empty()) r = cmp_mirror(mref_, ix.mref, "mref");
+  if (r.empty()) r = cmp_mirror(mpart_, ix.mpart.m, "mpart");
+  if (r.empty()) r = cmp_mirror(npair_, ix.npair, "npair");
+  if (r.empty()) r = cmp_mirror(pent_, ix.pent.m, "pent");
+  if (r.empty()) r = cmp_mirror(plist_, ix.plist.m, "plist");
+  if (r.empty()) r = cmp_mirror(shr_, ix.shr.m, "shr");
+  if (r.empty()) r = cmp_mirror(inl_, ix.inl.m, "inl");
+  if (r.empty()) r = cmp_mirror(children_, ix.children.m, "children");
+  if (r.empty() && ix.sharded()) r = cmp_mirror(xinfo_, ix.xinfo, "xinfo");
+  return r;
 }
 
 void Device::sync(Index& ix, hipStream_t s) {
@@ -898,14 +951,17 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   da.msig = nullptr;
   da.mcount = nullptr;
   da.mlist = nullptr;
+  da.mrow = nullptr;
   sb_.dedup = dedup_ != 0 && !ix.sharded() && !sb_.fused;
   if (sb_.dedup) {
     grow(dd_sig_, (size_t)n * sizeof(uint64_t));
     grow(dd_cnt_, (size_t)n * sizeof(uint32_t));
     grow(dd_list_, (size_t)n * kPairMax * sizeof(uint32_t));
+    grow(dd_mrow_, (size_t)n * kPairMax * sizeof(uint32_t));
     da.msig = dd_sig_.as<uint64_t>();
     da.mcount = dd_cnt_.as<uint32_t>();
     da.mlist = dd_list_.as<uint32_t>();
+    da.mrow = dd_mrow_.as<uint32_t>();
   }
   if (!sb_.fused) {
     prof.begin(s);
@@ -922,7 +978,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     grow(dd_rep_, (size_t)n * sizeof(uint32_t));
     if (!dd_nsets_.p) dd_nsets_.ensure(sizeof(unsigned long long));
     hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
-    hip_check(hipMemsetAsync(dd_vals_.p, 0xFF, slots * sizeof(uint32_t), s), "memset");
+
     hip_check(hipMemsetAsync(dd_nsets_.p, 0, sizeof(unsigned long long), s), "memset");
     DedupArgs dd;
     dd.n = n;
@@ -1053,6 +1109,8 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
     a.rep = dd_rep_.as<uint32_t>();
     a.tslot = dd_slot_.as<uint32_t>();
+    a.mcount = dd_cnt_.as<uint32_t>();
+    a.mrow = dd_mrow_.as<uint32_t>();
     a.sets = dd_sets_.as<SetInfo>();
     a.spcount = dd_spcount_.as<unsigned long long>();
     a.dd_phase = 1;

@@ -152,6 +152,9 @@ class Device {
 
   // Upload dirty pages of the index image (incremental device-side update).
   void sync(Index& ix, hipStream_t s);
+  // Diagnostic: sync, then read every device array back and compare it with the host mirror;
+  // returns "" or the first difference.
+  std::string verify(Index& ix);
   // Match n topics resident on the device. Fills `out` with device pointers of the last chunk;
   // when `host` is set every chunk's rows are also copied into it (global offsets).
   // fn (optional): per-chunk consumer (mq_match_device_chunks), called before the chunk's
@@ -298,7 +301,7 @@ class Device {
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
   bool fuse_desc_ = false;       // span format: k_merge does k_desc's work (MQ_OPT_FUSE_DESC)
   uint32_t dedup_ = 0;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
-  DevBuf dd_sig_, dd_cnt_, dd_list_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_;
+  DevBuf dd_sig_, dd_cnt_, dd_list_, dd_mrow_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_;
   DevBuf dd_sets_, dd_spatches_, dd_spcount_;  // phase 1 of the dedup merge: SetInfo, set pool
   uint64_t srcap_ = 0;                         // set patches per region of dd_spatches_
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)

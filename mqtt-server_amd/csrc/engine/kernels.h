@@ -156,6 +156,8 @@ struct EmitArgs {
   // topic copies its representative's patches, translating x to its own rows.
   const uint32_t* rep;
   const uint32_t* tslot;
+  const uint32_t* mcount;  // merge gathers per topic, and their rows (k_desc, stride kPairMax)
+  const uint32_t* mrow;
   uint32_t dd_phase;
   struct SetInfo* sets;
   PatchRec* spatches;
@@ -196,19 +198,21 @@ struct DescArgs {
   uint64_t* msig;
   uint32_t* mcount;
   uint32_t* mlist;
+  uint32_t* mrow;  // the topic-relative row of each merge gather's first may-merge slot (stride kPairMax)
 };
 
 // Merge-set dedup (span format): topics whose merge gathers are the same particles resolve to
-// the same patches (up to row positions). k_dedup finds, per topic, the smallest topic id with
+// the same patches (up to row positions). k_dedup finds, per topic, a representative topic with
 // the same merge gathers (exact: the lists are compared) — rep[t] == t for a topic that resolves
-// itself. Table: 2^k slots of (u64 signature, u32 smallest topic); n_sets counts the reps.
+// itself. Table: 2^k slots of (u64 signature, u32 the topic that inserted it); n_sets counts the
+// representatives.
 struct DedupArgs {
   uint32_t n;
   const uint64_t* msig;
   const uint32_t* mcount;
   const uint32_t* mlist;
   unsigned long long* keys;  // table_mask + 1 signatures (0 = empty)
-  uint32_t* vals;            // table_mask + 1 smallest topic ids (kNone = empty)
+  uint32_t* vals;            // table_mask + 1 inserting topics (valid where keys != 0)
   uint64_t table_mask;
   uint32_t* tslot;           // per topic: its table slot (kNone: not deduped)
   uint32_t* rep;             // per topic: its representative

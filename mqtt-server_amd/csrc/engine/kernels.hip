@@ -725,7 +725,10 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
       if (gw & kGatherSubs) n_merge += L.n_merge;
       if (a.msig && (d.mdir & kDescMerge)) {
         msig = mix64(msig ^ (gw & kGatherNode)) + 0x9e3779b97f4a7c15ull;
-        if (n_mg < kPairMax) a.mlist[(uint64_t)t * kPairMax + n_mg] = gw & kGatherNode;
+        if (n_mg < kPairMax) {
+          a.mlist[(uint64_t)t * kPairMax + n_mg] = gw & kGatherNode;
+          a.mrow[(uint64_t)t * kPairMax + n_mg] = rpos + L.n_direct;
+        }
         // set-relative rows hold 26 bits of slot: a larger merge gather keeps the topic apart
         n_mg += L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1;
       }
@@ -749,8 +752,8 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
   }
 }
 
-// k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, and the
-// smallest topic id seen there. k_dedup_rep: the representative, verified list against list (a
+// k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, whose
+// value is the topic that inserted the signature. k_dedup_rep: the representative, verified list against list (a
 // signature collision leaves the topic its own representative).
 __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -763,10 +766,19 @@ __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
   const unsigned long long k = a.msig[t];
   uint64_t i = mix64(k) & a.table_mask;
   for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
-    const unsigned long long prev = atomicCAS(a.keys + i, 0ull, k);
-    if (prev == 0ull || prev == k) {
+    // most topics find their signature already in place: a plain load, no atomic on a hot slot;
+    // the topic whose CAS fills a slot is the representative of its signature
+    unsigned long long prev = __atomic_load_n(a.keys + i, __ATOMIC_RELAXED);
+    if (prev == 0ull) {
+      prev = atomicCAS(a.keys + i, 0ull, k);
+      if (prev == 0ull) {
+        a.vals[i] = t;
+        a.tslot[t] = (uint32_t)i;
+        return;
+      }
+    }
+    if (prev == k) {
       a.tslot[t] = (uint32_t)i;
-      atomicMin(a.vals + i, t);
       return;
     }
     i = (i + 1) & a.table_mask;
@@ -1079,7 +1091,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   const uint32_t cap = tcn.rows;
 
-  if (tcn.merge) {  // the topic gathers may-merge records
+  if (dcopy) {
+    // the representative's resolution: its set-relative patches, rows translated through this
+    // topic's merge gathers (the same particles in the same order: k_dedup compared them)
+    const SetInfo si = a.sets[drep];
+    const uint32_t mc = a.mcount[t];
+    const uint32_t my_row = lane < mc ? a.mrow[(uint64_t)t * kPairMax + lane] : 0u;
+    reserve(si.n);
+    for (uint32_t j0 = 0; j0 < si.n; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool want = j < si.n;
+      PatchRec pr{0, 0};
+      if (want) pr = a.spatches[si.base + j];
+      const uint32_t base_row = __shfl(my_row, (int)(pr.row >> kSetRowBits), 64);
+      emit_patch(want, base_row + (pr.row & ((1u << kSetRowBits) - 1)), pr.meta);
+    }
+    n_nonbase = si.nonbase;
+    n_ext = si.ext;
+  } else if (tcn.merge) {  // the topic gathers may-merge records
     // Map every gathered node that holds may-merge records (and whose subscriptions are
     // gathered, Q3) to its gather index, and list them in gather order. Nodes are distinct
     // within a topic.
@@ -1250,21 +1279,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       n_ext += __popcll(bx);
     };
 
-    if (dcopy) {
-      // the representative's resolution: its set-relative patches, rows translated through this
-      // topic's merge gathers (the same particles in the same order: k_dedup compared them)
-      const SetInfo si = a.sets[drep];
-      reserve(si.n);
-      for (uint32_t j0 = 0; j0 < si.n; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        const bool want = j < si.n;
-        PatchRec pr{0, 0};
-        if (want) pr = a.spatches[si.base + j];
-        emit_patch(want, mg_row[wv][pr.row >> kSetRowBits] + (pr.row & ((1u << kSetRowBits) - 1)), pr.meta);
-      }
-      n_nonbase = si.nonbase;
-      n_ext = si.ext;
-    } else if (!slow) {
+    if (!slow) {
       // Pair analysis over ordered pairs (g, h) of merge gathers: g's pair block lists the slots
       // whose client also subscribes at h. Hit lists are staged in LDS and their concatenation
       // is resolved 64 records per wave-instruction.

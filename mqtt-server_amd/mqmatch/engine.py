@@ -112,7 +112,7 @@ EXPORTS = [
     "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
     "mq_acl_match_batch", "mq_select_shared_device", "mq_match_spans", "mq_match_spans_device",
     "mq_spans_expand", "mq_set_option", "mq_match_spans_begin", "mq_match_spans_end",
-    "mq_match_spans_end_host",
+    "mq_match_spans_end_host", "mq_device_check",
 ]
 
 CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
@@ -175,6 +175,7 @@ def lib():
         "mq_sync": (C.c_int, [vp, vp]),
         "mq_index_stats": (C.c_int, [vp, C.POINTER(Stats)]),
         "mq_index_check": (C.c_int, [vp]),
+        "mq_device_check": (C.c_int, [vp]),
         "mq_profile_enable": (C.c_int, [vp, C.c_int]),
         "mq_profile_read": (C.c_int, [vp, C.POINTER(KernelTime), C.c_uint32]),
         "mq_profile_reset": (C.c_int, [vp]),
@@ -370,6 +371,10 @@ class Engine:
 
     def sync(self, stream=None):
         _check(lib().mq_sync(self.h, stream), "mq_sync")
+
+    def device_check(self):
+        """mq_device_check: the device arrays equal the host mirror (diagnostic)."""
+        _check(lib().mq_device_check(self.h), "mq_device_check")
 
     def check(self):
         """mq_index_check: host-side invariants of the device-bound image (raises on violation)."""

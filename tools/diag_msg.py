@@ -22,6 +22,11 @@ print("built", round(time.time() - t, 1), e.stats(), flush=True)
 if "--check" in sys.argv:
     e.check()
     print("host check ok", round(time.time() - t, 1), flush=True)
+try:
+    e.device_check()
+    print("device check ok", round(time.time() - t, 1), flush=True)
+except Exception as ex:
+    print("device check FAILED:", ex, flush=True)
 for img in (1, 0):
     e.set_option(E.OPT_MSG_IMAGE, img)
     try:
