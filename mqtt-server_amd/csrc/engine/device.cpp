@@ -976,6 +976,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     grow(dd_vals_, slots * sizeof(uint32_t));
     grow(dd_slot_, (size_t)n * sizeof(uint32_t));
     grow(dd_rep_, (size_t)n * sizeof(uint32_t));
+    grow(dd_rlist_, (size_t)n * sizeof(uint32_t));
     if (!dd_nsets_.p) dd_nsets_.ensure(sizeof(unsigned long long));
     hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
 
@@ -991,6 +992,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     dd.tslot = dd_slot_.as<uint32_t>();
     dd.rep = dd_rep_.as<uint32_t>();
     dd.n_sets = dd_nsets_.as<unsigned long long>();
+    dd.rep_list = dd_rlist_.as<uint32_t>();
     prof.begin(s);
     launch_dedup(dd, s);
     prof.end("dedup", s);
@@ -1113,6 +1115,8 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     a.mrow = dd_mrow_.as<uint32_t>();
     a.sets = dd_sets_.as<SetInfo>();
     a.spcount = dd_spcount_.as<unsigned long long>();
+    a.rep_list = dd_rlist_.as<uint32_t>();
+    a.n_reps = dd_nsets_.as<unsigned long long>();
     a.dd_phase = 1;
     unsigned long long* work0 = a.work;
     if (a.work) a.work += kPatchRegions * kWork;
@@ -1336,6 +1340,7 @@ void Device::ensure_img(const Index& ix, const DevIndex& di, hipStream_t s) {
     a.n = n;
     a.next = lo + n;
     launch_img_level(false, di, a, s);
+    hip_check(hipGetLastError(), "k_img_level (count)");
     launch_scan32(a.cnt, n, img_bsum_.as<uint32_t>(), img_bpre_.as<uint32_t>(), img_coff_.as<uint32_t>(), s);
     uint32_t next_n = 0;
     hip_check(hipMemcpyAsync(&next_n, img_coff_.as<uint32_t>() + n, sizeof(uint32_t), hipMemcpyDeviceToHost, s),
@@ -1471,6 +1476,8 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   }
   check_err(s);
   if (n == 0) return;
+  // the Messages kernels launch a wavefront per filter (a grid is limited to 2^32 threads)
+  if (n > kMaxWaveBlocks * 4) throw HipError{hipErrorInvalidValue, "more than 2^24 filters in one Messages batch"};
   const DevIndex di = dev_index(ix);
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
   counts_.ensure((size_t)n * sizeof(TopicCount));

@@ -7,6 +7,8 @@
 
 namespace mq {
 
+constexpr uint32_t kMaxWaveBlocks = 1u << 22;  // grid cap of grid-stride wave-per-item kernels
+                                                //   (a grid is limited to 2^32 threads)
 constexpr uint32_t kScanBlock = 1024;  // topics per scan block (= chunk granule)
 constexpr uint32_t kGatherCap = 64;    // per-topic gather slots written by the count pass
 constexpr uint64_t kChunkRows = 0xF0000000ull;  // output rows per chunk (60 GiB of 16-B rows; u32 row indices)
@@ -163,6 +165,8 @@ struct EmitArgs {
   PatchRec* spatches;
   unsigned long long* spcount;
   uint64_t srcap;
+  const uint32_t* rep_list;            // dd_phase 1: the set representatives (k_dedup_rep)
+  const unsigned long long* n_reps;    //   and their number, in device memory
 };
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
 struct SetInfo {  // 24 B, per representative topic
@@ -217,6 +221,7 @@ struct DedupArgs {
   uint32_t* tslot;           // per topic: its table slot (kNone: not deduped)
   uint32_t* rep;             // per topic: its representative
   unsigned long long* n_sets;  // topics with merge gathers that are their own representative
+  uint32_t* rep_list;          // those topics (n_sets of them, in no particular order)
 };
 void launch_dedup(const DedupArgs& a, hipStream_t s);
 

@@ -756,40 +756,53 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
 // value is the topic that inserted the signature. k_dedup_rep: the representative, verified list against list (a
 // signature collision leaves the topic its own representative).
 __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.n) return;
-  const uint32_t c = a.mcount[t];
-  if (c == 0 || c > kPairMax) {
-    a.tslot[t] = kNone;
-    return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  const bool act = t < a.n;
+  const uint32_t c = act ? a.mcount[t] : 0u;
+  const bool ok = c != 0 && c <= kPairMax;
+  const unsigned long long k = ok ? a.msig[t] : 0ull;
+  // one table operation per distinct signature in the wavefront: a hot signature (the topics
+  // under the same busy particles) would otherwise have every topic's CAS on one slot at once
+  uint32_t leader = lane;
+  for (uint64_t rem = __ballot(ok); rem;) {  // wave-uniform: a leader per distinct signature
+    const uint32_t l = (uint32_t)__builtin_ctzll(rem);
+    const unsigned long long kl = __shfl(k, (int)l, 64);
+    const uint64_t same = __ballot(ok && k == kl) & rem;
+    if ((same >> lane) & 1) leader = l;
+    rem &= ~same;
   }
-  const unsigned long long k = a.msig[t];
-  uint64_t i = mix64(k) & a.table_mask;
-  for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
-    // most topics find their signature already in place: a plain load, no atomic on a hot slot;
-    // the topic whose CAS fills a slot is the representative of its signature
-    unsigned long long prev = __atomic_load_n(a.keys + i, __ATOMIC_RELAXED);
-    if (prev == 0ull) {
-      prev = atomicCAS(a.keys + i, 0ull, k);
+  uint32_t slot = kNone;
+  if (ok && leader == lane) {
+    uint64_t i = mix64(k) & a.table_mask;
+    for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
+      // most leaders find their signature already in place: a plain load, no atomic on a hot
+      // slot; the topic whose CAS fills a slot is the representative of its signature
+      unsigned long long prev = __atomic_load_n(a.keys + i, __ATOMIC_RELAXED);
       if (prev == 0ull) {
-        a.vals[i] = t;
-        a.tslot[t] = (uint32_t)i;
-        return;
+        prev = atomicCAS(a.keys + i, 0ull, k);
+        if (prev == 0ull) {
+          a.vals[i] = t;
+          slot = (uint32_t)i;
+          break;
+        }
       }
-    }
-    if (prev == k) {
-      a.tslot[t] = (uint32_t)i;
-      return;
-    }
-    i = (i + 1) & a.table_mask;
+      if (prev == k) {
+        slot = (uint32_t)i;
+        break;
+      }
+      i = (i + 1) & a.table_mask;
+    }  // slot stays kNone only for a full table (sized 2x the topics: cannot happen)
   }
-  a.tslot[t] = kNone;  // full table (sized 2x the topics: cannot happen)
+  slot = __shfl(slot, (int)leader, 64);
+  if (act) a.tslot[t] = ok ? slot : kNone;
 }
 
+// k_dedup_rep also lists the topics that resolve a merge set (rep_list, n_sets of them): the
+// merge's set pass walks that list instead of every topic.
 __global__ __launch_bounds__(256) void k_dedup_rep(DedupArgs a) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.n) return;
-  const uint32_t sl = a.tslot[t];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  const bool act = t < a.n;
+  const uint32_t sl = act ? a.tslot[t] : kNone;
   uint32_t r = t;
   if (sl != kNone) {
     const uint32_t v = a.vals[sl];
@@ -802,10 +815,13 @@ __global__ __launch_bounds__(256) void k_dedup_rep(DedupArgs a) {
       if (eq) r = v;
     }
   }
-  a.rep[t] = r;
+  if (act) a.rep[t] = r;
   const bool own = r == t && sl != kNone;
   const uint64_t b = __ballot(own);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(a.n_sets, (unsigned long long)__popcll(b));
+  unsigned long long base = 0;
+  if (lane == 0 && b) base = atomicAdd(a.n_sets, (unsigned long long)__popcll(b));
+  base = __shfl(base, 0, 64);
+  if (own) a.rep_list[base + prefix_before(b)] = t;
 }
 
 void launch_dedup(const DedupArgs& a, hipStream_t s) {
@@ -976,7 +992,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t wv = wave_id(), lane = threadIdx.x & 63;
   auto rank_of = [](const GDesc& d) { return gdesc_rank<XS>(d); };
   // persistent: a.merge grid's waves stride over the chunk's topics (wave-uniform loop)
-  for (uint32_t t = a.t0 + blockIdx.x * 4 + wv; t < a.t1; t += gridDim.x * 4) {
+  // (dedup's set pass: the waves stride over the list of set representatives instead)
+  const bool set_pass = SPANS && a.rep && a.dd_phase == 1;
+  const uint32_t i_end = set_pass ? (uint32_t)*a.n_reps : a.t1;
+  for (uint32_t i = a.t0 + blockIdx.x * 4 + wv; i < i_end; i += gridDim.x * 4) {
+  const uint32_t t = set_pass ? a.rep_list[i] : i;
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
   const uint64_t ib = o0.inl - a.base.inl;
@@ -2274,10 +2294,11 @@ __global__ void k_img_root(uint32_t* node, uint32_t* pos, uint32_t* live) {
 // Wavefront per parent of the level: its children slab (ChildRec) in slab order; a child is in
 // the image when its own retained message is live or one below it is (NodeMsg.below_live).
 template <bool FILL>
+// Grid-stride over the level's parents (a level of a 100M-topic index holds more parents than
+// one wavefront each can launch: a grid is limited to 2^32 threads).
 __global__ __launch_bounds__(256) void k_img_level(DevIndex ix, ImgLevelArgs a) {
   const uint32_t lane = threadIdx.x & 63, wv = wave_id();
-  const uint32_t p = blockIdx.x * 4 + wv;
-  if (p >= a.n) return;  // wave-uniform
+  for (uint32_t p = blockIdx.x * 4 + wv; p < a.n; p += gridDim.x * 4) {  // wave-uniform
   const uint32_t v = a.node[a.lo + p];
   const NodeMsg m = ix.msg[v];
   const bool root = v == kRoot;
@@ -2322,6 +2343,7 @@ __global__ __launch_bounds__(256) void k_img_level(DevIndex ix, ImgLevelArgs a) 
     if (FILL) a.cl[a.lo + p] = make_uint2(base, base + total);
     else a.cnt[p] = total;
   }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_img_compact(DevIndex ix, const uint32_t* __restrict__ node,
@@ -2339,7 +2361,7 @@ void launch_img_root(uint32_t* node, uint32_t* pos, uint32_t* live, hipStream_t 
 
 void launch_img_level(bool fill, const DevIndex& ix, const ImgLevelArgs& a, hipStream_t s) {
   if (!a.n) return;
-  const dim3 g((a.n + 3) / 4), b(256);
+  const dim3 g(std::min<uint32_t>((a.n + 3) / 4, kMaxWaveBlocks)), b(256);
   if (fill) hipLaunchKernelGGL(k_img_level<true>, g, b, 0, s, ix, a);
   else hipLaunchKernelGGL(k_img_level<false>, g, b, 0, s, ix, a);
 }
@@ -2559,8 +2581,7 @@ void launch_msgq(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, c
 __global__ __launch_bounds__(256) void k_msg_copy(const MsgPiece* __restrict__ pieces, uint64_t n,
                                                   const uint64_t* __restrict__ h, uint64_t* __restrict__ out) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t i = (uint64_t)blockIdx.x * 4 + wave_id();
-  if (i >= n) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + wave_id(); i < n; i += (uint64_t)gridDim.x * 4) {
   const MsgPiece p = pieces[i];
   const uint64_t* src = h + p.h0;
   uint64_t* dst = out + p.dst;
@@ -2573,11 +2594,12 @@ __global__ __launch_bounds__(256) void k_msg_copy(const MsgPiece* __restrict__ p
     __builtin_nontemporal_store(v3, dst + k + 192);
   }
   for (; k < p.len; k += 64) __builtin_nontemporal_store(src[k], dst + k);
+  }
 }
 
 void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, pieces, n, h, out);
+  hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)std::min<uint64_t>((n + 3) / 4, kMaxWaveBlocks)), dim3(256), 0, s, pieces, n, h, out);
 }
 
 }  // namespace mq

@@ -3,6 +3,7 @@
   python tools/diag_msg.py 100000000"""
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -13,6 +14,15 @@ from mqmatch import workload as W  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
 t = time.time()
+
+
+def _beat():  # a line every 30 s: long host phases are not a hung run
+    while True:
+        time.sleep(30)
+        print(f"... working ({time.time() - t:.0f}s)", flush=True)
+
+
+threading.Thread(target=_beat, daemon=True).start()
 rb, ro, hd, rh = W.gen_retained(n, n_sys=1000, seed=W.BASE_SEED + 3)
 fb, fo = W.gen_msg_filters(rh, 1000, seed=W.BASE_SEED + 4)
 print("generated", n, round(time.time() - t, 1), flush=True)
