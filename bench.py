@@ -104,39 +104,46 @@ def read_traffic(path, n_subs, write_bytes_per_launch):
 
 
 def read_spans_traffic(path, n_subs, n_topics):
-    """HBM bytes per k_merge<spans> launch (FETCH_SIZE x2 + WRITE_SIZE) from a committed rocprofv3
-    PMC summary of the same configuration (subscriptions and topics per launch), if present."""
+    """HBM bytes per step of the k_merge<spans> launches (FETCH_SIZE x2 + WRITE_SIZE, both passes
+    with merge-set dedup) from a committed rocprofv3 PMC summary of the same configuration
+    (subscriptions, topics per step, dedup), if present."""
     try:
         with open(path) as f:
-            e = json.load(f).get("spans", {}).get(str(n_subs))
+            e = json.load(f).get("spans_dedup", {}).get(str(n_subs))
         if e is None or int(e["topics"]) != n_topics:
             return None
-        return float(e["hbm_bytes_per_merge_launch"])
+        return float(e["hbm_bytes_per_step"])
     except (OSError, ValueError, KeyError, TypeError):
         return None
 
 
 def spans_roofline(prof, work, steps, n, n_subs):
-    """Roofline of the span format's dominant kernel, k_merge. Its algorithmic bytes per launch
-     are what it must read and write for the launch's topics: 40 B of offsets and a
+    """Roofline of the span format's merge stage, k_merge<spans>: with merge-set dedup (the
+    default) two launches per step — the set pass (one resolution per distinct merge set) and the
+    topic pass (the other topics, set references, result records). Its algorithmic bytes per step
+     are what it must read and write for the step's topics: 40 B of offsets and a
     64 B result record per topic, the 32 B GDesc of every gather, 16 B per pair-table entry
     probed, 16 B per pair slot resolved, 8 B per partner link, 8 B per patch — priced from the
-    work counters of an extra step (the same batch, so the same work) — over the launch's mean
+    work counters of an extra step (the same batch, so the same work) — over the two launches'
     time from HIP events in the timed region. Latency-bound (dependent probes of hash tables and
-    lists), so the HBM fraction is low by nature; the step's other kernels are walk and desc."""
+    lists), so the HBM fraction is low by nature; the step's other kernels are walk, desc, dedup."""
     launches, ms = prof.get("merge", (0, 0.0))
+    set_launches, set_ms = prof.get("merge_sets", (0, 0.0))
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-            "traffic": None, "kernel": "k_merge<spans>",
+            "traffic": None, "kernel": "k_merge<spans>" + (" (set pass + topic pass)" if set_launches else ""),
             "bytes": "offsets + result + GDesc + pair entries + pair slots + partner links + patches"}
     if not launches or ms <= 0:
         return roof
     g = lambda k: work.get(k, (0, 0.0))[0]
-    per_launch = (104 * n + 32 * g("gathers") + 16 * g("merge_pair_entries") + 16 * g("merge_records")
-                  + 8 * g("merge_links") + 8 * g("merge_patches"))
-    launch_ms = ms / launches
-    achieved = per_launch / (launch_ms * 1e-3) / 1e9
-    roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, launch_ms=launch_ms, bytes_per_launch=per_launch,
-                traffic=read_spans_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n))
+    per_step = (104 * n + 32 * g("gathers") + 16 * g("merge_pair_entries") + 16 * g("merge_records")
+                + 8 * g("merge_links") + 8 * g("merge_patches"))
+    step_ms = (ms + set_ms) / max(1, steps)
+    achieved = per_step / (step_ms * 1e-3) / 1e9
+    roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, ms_per_step=step_ms,
+                launches_per_step=(launches + set_launches) / max(1, steps),
+                launch_ms_avg=(ms + set_ms) / max(1, launches + set_launches), bytes_per_step=per_step,
+                traffic=read_spans_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n)
+                if set_launches else None)
     return roof
 
 
@@ -399,7 +406,7 @@ def main():
         # One extra, untimed step with k_merge's work counters (MQ_PROF_WORK costs atomics).
         eng.profile(True, work=True)
         eng.profile_reset()
-        step()
+        r_last = step()
         torch.cuda.synchronize()
         work = eng.profile_read()
         eng.profile(False)
@@ -447,9 +454,16 @@ def main():
         ns = min(m, 4096)
         dg_o, cnt_o, tot = orc.digest_batch(tb, to[:ns + 1], cores)
         if not args.select_shared:  # picked shared rows are checked by tests/test_gpu_select.py
-            res = eng.match_batch_spans(tb, to[:ns + 1]) if args.format == "spans" else eng.match_batch(tb, to[:ns + 1])
+            # span format: the first ns topics of the measured step's own device result (the whole
+            # batch's merge sets), expanded as a device consumer would
+            res = (E.expand_device_spans(r_last, n, ns) if args.format == "spans"
+                   else eng.match_batch(tb, to[:ns + 1]))
             dg_e, _ = engine_digests(res)
-            out["parity_sample"] = {"topics": ns, "format": args.format, "bit_exact": bool((dg_e == dg_o).all())}
+            out["parity_sample"] = {"topics": ns, "format": args.format, "bit_exact": bool((dg_e == dg_o).all()),
+                                    "checked": "device result of the timed batch" if args.format == "spans"
+                                               else "mq_match_batch"}
+            if args.format == "spans":
+                out["parity_sample"]["set_patch_topics"] = res["set_topics"]
         per_topic = {k: v / ns for k, v in tot.items()}
         b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"] + 16 * per_topic["S"] + 16 * per_topic["O"]
         out["alg_bytes_per_topic"] = {"B": b_topic, "L": per_topic["L"], "P": per_topic["P"],

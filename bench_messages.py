@@ -56,6 +56,27 @@ def handle_digests(base, count, hs):
     return d
 
 
+def oracle_side(rb, ro, hd, fb, fo, n, args):
+    """The oracle's part of the bench: sample digests and counters (SURVEY.md §8d B terms) and
+    the CPU baseline (the oracle's Messages on 16 host threads over a bounded sample)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    t0 = time.time()
+    orc = O.OracleIndex()
+    orc.retain_bulk(rb, ro, hd)
+    log(f"oracle index built in {time.time() - t0:.1f}s")
+    ns = min(n, 4096)
+    dg, cnt, tot = orc.messages_digest_batch(fb, fo[:ns + 1], nthreads=16)
+    cal = min(n, 2048)
+    secs, _ = orc.bench_messages(fb, fo[:cal + 1], 16)
+    m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
+    secs, _ = orc.bench_messages(fb, fo[:m + 1], 16)
+    cpu = {"value": m / secs, "unit": "filters/s", "cores": 16, "kind": "port",
+           "sample": f"first {m} filters, 16 threads, Messages() per filter (oracle/)"}
+    return {"sample_filters": ns, "digests": [format(int(x), "x") for x in dg], "counts": [int(x) for x in cnt],
+            "per_filter": {k: v / ns for k, v in tot.items()}, "cpu": cpu}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--retained", type=int, default=10_000_000)
@@ -67,18 +88,33 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--walk", action="store_true",
                     help="Messages by the particle walk (MQ_OPT_MSG_IMAGE 0) instead of the level-order image")
+    ap.add_argument("--oracle-only", metavar="OUT",
+                    help="CPU side only (no GPU): build the oracle, write its sample digests, counters and "
+                         "CPU baseline to OUT (JSON). At config 5's full size the oracle and the engine's "
+                         "host mirror do not fit one process's memory cap together")
+    ap.add_argument("--oracle-file", metavar="IN",
+                    help="GPU run: take the parity sample, counters and CPU baseline from a --oracle-only "
+                         "file of the same workload instead of building the oracle here")
     args = ap.parse_args()
     heartbeat()
-    import torch
-    from mqmatch import engine as E
     from mqmatch import workload as W
 
-    torch.cuda.set_device(0)
     t0 = time.time()
     rb, ro, hd, rh = W.gen_retained(args.retained, n_sys=args.sys, seed=W.BASE_SEED + 3)
     fb, fo = W.gen_msg_filters(rh, args.filters, seed=W.BASE_SEED + 4)
     n = len(fo) - 1
     log(f"generated {len(ro) - 1} retained topics, {n} filters in {time.time() - t0:.1f}s")
+    if args.oracle_only:
+        del rh
+        o = oracle_side(rb, ro, hd, fb, fo, n, args)
+        o.update(retained=len(ro) - 1, filters=n)
+        with open(args.oracle_only, "w") as f:
+            json.dump(o, f)
+        log(f"oracle side written to {args.oracle_only}")
+        return
+    import torch
+    from mqmatch import engine as E
+    torch.cuda.set_device(0)
     t0 = time.time()
     eng = E.Engine(device=0)
     if args.walk:
@@ -121,30 +157,32 @@ def main():
         "image_build_ms": build[1] if build else None,
     }
     cpu = None
-    if not args.no_cpu:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle as O
-        orc = O.OracleIndex()
-        orc.retain_bulk(rb, ro, hd)
-        ns = min(n, 4096)
-        dg, cnt, tot = orc.messages_digest_batch(fb, fo[:ns + 1], nthreads=16)
+    o = None
+    if args.oracle_file:
+        with open(args.oracle_file) as f:
+            o = json.load(f)
+        if o["retained"] != len(ro) - 1 or o["filters"] != n:
+            raise SystemExit(f"{args.oracle_file} is for another workload")
+        out["oracle_side"] = f"{args.oracle_file} (bench_messages.py --oracle-only, same seeds and sizes)"
+    elif not args.no_cpu:
+        o = oracle_side(rb, ro, hd, fb, fo, n, args)
+    if o is not None:
+        ns = o["sample_filters"]
+        dg = np.array([int(x, 16) for x in o["digests"]], np.uint64)
+        cnt = np.array(o["counts"], np.uint32)
         base, count, hs = eng.messages_batch(fb, fo[:ns + 1])
         out["parity_sample"] = {"filters": ns, "counts_equal": bool((count == cnt).all()),
                                 "digests_equal": bool((handle_digests(base, count, hs) == dg).all())}
-        per = {k: v / ns for k, v in tot.items()}
+        per = o["per_filter"]
         b = 8 * per["L"] + 4 + 16 * per["P"] + 16 * per["O"]
         out["alg_bytes_per_filter"] = {"B": b, **per, "sample_filters": ns}
-        kms = sum(v[1] for k, v in prof.items() if k.startswith("msg")) / args.steps
+        kms = sum(v[1] for k, v in prof.items() if k.startswith("msg") and k != "msg_image") / args.steps
         if kms > 0:
             ach = b * n / (kms * 1e-3) / 1e9
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "k_msg (count + fill)"}
-        cal = min(n, 2048)
-        secs, _ = orc.bench_messages(fb, fo[:cal + 1], 16)
-        m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
-        secs, _ = orc.bench_messages(fb, fo[:m + 1], 16)
-        cpu = {"value": m / secs, "unit": "filters/s", "cores": 16, "kind": "port",
-               "sample": f"first {m} filters, 16 threads, Messages() per filter (oracle/)"}
+                               "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                               "kernel": "k_msgq + k_msg_copy" if not args.walk else "k_msg (count + fill)"}
+        cpu = o["cpu"]
     out["cpu_baseline"] = cpu
     try:
         with open("/proc/self/status") as f:

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 5
+#define MQ_ABI_VERSION 6
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
@@ -241,7 +241,7 @@ uint32_t mq_match_chunks(const mq_index* idx);
 int mq_select_shared_device(mq_index* idx, const mq_match_result* chunk, void* hip_stream,
                             mq_shared_row* d_selected, uint32_t* d_n_selected);
 
-/* ---- span format: Subscribers without copying the gathered lists (ABI v5) ----
+/* ---- span format: Subscribers without copying the gathered lists (ABI v5; v6: set patches) ----
  *
  * The row format above copies every gathered subscription of every topic into output rows; at
  * 10M subscriptions a topic gathers ~15k of them (the root '#', '+/...', 'x/#' lists, the same
@@ -256,6 +256,13 @@ int mq_select_shared_device(mq_index* idx, const mq_match_result* chunk, void* h
  *     in no particular order;
  *   - the inline rows, last-write applied (as in the row format).
  * Expanding spans and applying patches gives exactly the row format's rows (mq_spans_expand).
+ * Device results (mq_match_spans_device) may share patches between topics: topics whose gathered
+ * particles with may-merge records are the same particles in the same order resolve to the same
+ * patches up to where those particles' records sit in each topic's rows, so the batch resolves
+ * each such merge set once. A topic with MQ_TOPIC_SET_PATCHES in its flags has its n_patches
+ * patches at set_patches[patch_base, + n_patches), each naming its row as (x << 26 | k): the
+ * k-th may-merge record of the topic's x-th particle with may-merge records, i.e. topic row
+ * merge_rows[topic * 64 + x] + k. Host results (mq_match_spans) always hold per-topic patches.
  * With MQ_CFG_SELECT_SHARED the picked shared members are materialised (picked_rows at
  * picked_base, n_shared of them) and flags has MQ_SPANS_PICKED. */
 typedef struct mq_span {
@@ -274,10 +281,13 @@ typedef struct mq_topic_spans {
   uint32_t n_rows;   /* gathered non-shared records (client + ident + dropped rows) */
   uint32_t n_client, n_ident;
   uint32_t n_shared; /* shared members (picked members with MQ_SPANS_PICKED) */
-  uint32_t reserved;
+  uint32_t flags;    /* MQ_TOPIC_SET_PATCHES (device results only) */
 } mq_topic_spans;
 
 #define MQ_SPANS_PICKED 1u
+#define MQ_TOPIC_SET_PATCHES 1u
+#define MQ_SET_ROW_BITS 26   /* set patch rows: x << MQ_SET_ROW_BITS | k */
+#define MQ_MERGE_ROWS_STRIDE 64
 
 typedef struct mq_span_result {
   uint32_t n_topics;
@@ -294,6 +304,11 @@ typedef struct mq_span_result {
                          (topic ranges lie in per-region parts of it, with unused gaps) */
   uint64_t n_inline_rows, n_picked_rows;
   uint64_t sub_pool_len, shared_pool_len;
+  /* device results: patches shared by topics with MQ_TOPIC_SET_PATCHES, and every topic's merge
+     rows (MQ_MERGE_ROWS_STRIDE per topic); null / 0 when no topic shares */
+  const mq_patch* set_patches;
+  const uint32_t* merge_rows;
+  uint64_t n_set_patches;
 } mq_span_result;
 
 /* Span-format Subscribers for a batch of host topics (as mq_match_batch). The result's arrays

@@ -11,6 +11,10 @@
 #include <string>
 #include <vector>
 
+static_assert(mq::kTopicSetPatches == MQ_TOPIC_SET_PATCHES && mq::kSetRowBits == MQ_SET_ROW_BITS &&
+                  mq::kPairMax == MQ_MERGE_ROWS_STRIDE,
+              "set patch layout (include/mqmatch.h)");
+
 namespace mq {
 
 void hip_check(hipError_t e, const char* where) {
@@ -280,6 +284,9 @@ Device::~Device() {
     tiles_[k].release();
   }
   plan_.release();
+  for (DevBuf* b : {&sp_tc_, &dd_sig_, &dd_cnt_, &dd_list_, &dd_mrow_, &dd_keys_, &dd_vals_, &dd_slot_, &dd_rep_,
+                    &dd_nsets_, &dd_rlist_, &dd_sets_, &dd_spatches_, &dd_spcount_, &msg_runs_, &msg_nruns_})
+    b->release();
   if (h_plan_) (void)hipHostFree(h_plan_);
   if (h_pin_) (void)hipHostFree(h_pin_);
 }
@@ -1126,7 +1133,8 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       hip_check(hipMemsetAsync(a.spcount, 0, kPatchRegions * sizeof(unsigned long long), s), "memset");
       if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
       prof.begin(s);
-      launch_merge(a, true, false, merge_wpe, merge_blocks_, s);
+      // persistent: the waves stride over the representative list (its length is on the device)
+      launch_merge(a, true, false, merge_wpe, merge_blocks_ ? merge_blocks_ : n_cus_ * 8, s);
       prof.end("merge_sets", s);
       hip_check(hipGetLastError(), "k_merge<spans> (sets)");
       hip_check(hipMemcpyAsync(h_pc, a.spcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
@@ -1142,6 +1150,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
     a.work = work0;
     a.dd_phase = 2;
+    a.set_ref = host ? 0u : 1u;  // host results get per-topic patches (copied in phase 2)
   }
   for (int attempt = 0;; attempt++) {
     a.patches = sp_patches_.as<PatchRec>();
@@ -1197,6 +1206,11 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   out->n_patches = rcap_ * kPatchRegions;  // the pool's extent: topic ranges sit in regions
   out->n_inline_rows = tot.inl;
   out->n_picked_rows = select_shared_ ? tot.shr : 0;
+  if (sb_.dedup && a.set_ref) {
+    out->set_patches = reinterpret_cast<const mq_patch*>(dd_spatches_.p);
+    out->merge_rows = dd_mrow_.as<uint32_t>();
+    out->n_set_patches = srcap_ * kPatchRegions;
+  }
   if (a.work) {  // MQ_PROF_WORK: k_merge's work, for its algorithmic bytes (bench.py)
     std::vector<unsigned long long> w(2 * kPatchRegions * kWork);
     hip_check(hipMemcpyAsync(w.data(), a.work, w.size() * sizeof(w[0]), hipMemcpyDeviceToHost, s), "D2H work");
@@ -1388,9 +1402,20 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
                           hipStream_t s, TopicOff* tot) {
   const MsgImg img = msg_img();
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+  // One walk per filter: the count pass records each filter's runs (up to run_cap of them, from
+  // the speculative-scratch budget) and the second pass places them; a filter with more runs
+  // walks again in the second pass. Without the budget: count walk, then fill walk.
+  const uint32_t run_cap = (uint32_t)std::min<uint64_t>(kMsgRunCap, msg_spec_bytes_ / ((uint64_t)n * sizeof(MsgRun)));
+  const bool runs = run_cap >= 8;
+  if (runs) {
+    msg_runs_.ensure((size_t)n * run_cap * sizeof(MsgRun));
+    msg_nruns_.ensure((size_t)n * sizeof(uint32_t));
+  }
+  MsgRun* d_runs = runs ? msg_runs_.as<MsgRun>() : nullptr;
+  uint32_t* d_nruns = runs ? msg_nruns_.as<uint32_t>() : nullptr;
   prof.begin(s);
-  launch_msgq(false, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, nullptr,
-              s);
+  launch_msgq(runs ? kMsgRuns : kMsgCount, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), nullptr, nullptr,
+              nullptr, nullptr, nullptr, d_runs, run_cap, d_nruns, s);
   prof.end("msgq_count", s);
   hip_check(hipGetLastError(), "k_msgq<count>");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
@@ -1409,9 +1434,9 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
   msg_count_.ensure((size_t)n * sizeof(uint32_t));
   msg_pieces_.ensure(std::max<uint64_t>(tot->g, 1) * sizeof(MsgPiece));
   prof.begin(s);
-  launch_msgq(true, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
+  launch_msgq(runs ? kMsgPlace : kMsgFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
               msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
-              msg_count_.as<uint32_t>(), s);
+              msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, s);
   prof.end("msgq_fill", s);
   hip_check(hipGetLastError(), "k_msgq<fill>");
   prof.begin(s);

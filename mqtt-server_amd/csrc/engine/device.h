@@ -289,6 +289,7 @@ class Device {
   uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf img_node_, img_pos_, img_cl_, img_lp_, img_h_, img_cnt_, img_coff_, img_bsum_, img_bpre_;
   DevBuf msg_pieces_;               // k_msgq copy pieces of a batch
+  DevBuf msg_runs_, msg_nruns_;     // k_msgq runs recorded by the count pass (kMsgRuns)
   uint64_t img_version_ = ~0ull;    // ix.retained_version() the image was built at
   uint32_t img_n_ = 0, img_n_pos_ = 0, img_levels_ = 0;
   uint64_t img_live_ = 0;
@@ -300,7 +301,7 @@ class Device {
   uint32_t walk_wpe_ = 8;        // k_walk count pass register budget (MQ_OPT_WALK_WAVES)
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
   bool fuse_desc_ = false;       // span format: k_merge does k_desc's work (MQ_OPT_FUSE_DESC)
-  uint32_t dedup_ = 0;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
+  uint32_t dedup_ = 1;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
   DevBuf dd_sig_, dd_cnt_, dd_list_, dd_mrow_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_, dd_rlist_;
   DevBuf dd_sets_, dd_spatches_, dd_spcount_;  // phase 1 of the dedup merge: SetInfo, set pool
   uint64_t srcap_ = 0;                         // set patches per region of dd_spatches_

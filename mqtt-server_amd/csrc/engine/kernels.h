@@ -113,7 +113,7 @@ struct PatchRec {  // topic-relative record row -> replacement meta (merge base 
 struct TopicSpansDev {  // == mq_topic_spans
   uint64_t span_base, patch_base, inline_base, picked_base;
   uint32_t n_spans, n_patches, n_inline, n_rows;
-  uint32_t n_client, n_ident, n_shared, reserved;
+  uint32_t n_client, n_ident, n_shared, flags;  // flags: MQ_TOPIC_SET_PATCHES
 };
 static_assert(sizeof(TopicSpansDev) == 64, "mq_topic_spans layout");
 
@@ -165,10 +165,14 @@ struct EmitArgs {
   PatchRec* spatches;
   unsigned long long* spcount;
   uint64_t srcap;
+  uint32_t set_ref;                    // dd_phase 2: a deduped topic references its set's patches
+                                       //   (device results) instead of copying them
   const uint32_t* rep_list;            // dd_phase 1: the set representatives (k_dedup_rep)
   const unsigned long long* n_reps;    //   and their number, in device memory
 };
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
+constexpr uint32_t kTopicSetPatches = 1;  // TopicSpansDev.flags: patches shared with a merge set
+                                          //   (MQ_TOPIC_SET_PATCHES)
 struct SetInfo {  // 24 B, per representative topic
   uint64_t base;   // its patches in the set pool
   uint32_t n, nonbase, ext, fit;
@@ -346,11 +350,23 @@ void launch_img_level(bool fill, const DevIndex& ix, const ImgLevelArgs& a, hipS
 // h[lp[q]] = handle of node[q] for the live positions (lp: the scan of live)
 void launch_img_compact(const DevIndex& ix, const uint32_t* node, const uint32_t* lp, uint32_t n,
                         uint64_t* h, hipStream_t s);
-// Messages count (fill = false: TopicCount.gathers = pieces, .rows = handles) or fill pass
-// (pieces at off[t].g, short runs copied directly, base / count written).
-void launch_msgq(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+// A filter's output run as its walk found it (k_msgq run mode): handles h[h0, + len) go to the
+// filter's output at dst; a long run's pieces start at the filter's piece slot pslot.
+struct MsgRun {
+  uint32_t h0, len, dst, pslot;
+};
+constexpr uint32_t kMsgRunCap = 64;  // runs recorded per filter (more: the filter is walked again)
+// Messages passes (k_msgq):
+//   kMsgCount  TopicCount.gathers = pieces, .rows = handles
+//   kMsgFill   pieces at off[t].g, short runs copied directly, base / count written
+//   kMsgRuns   as kMsgCount, and the filter's runs recorded (runs[t * run_cap ..], n_runs[t];
+//              kNone: more than run_cap runs)
+//   kMsgPlace  as kMsgFill, from the recorded runs without walking (a filter without them walks)
+enum MsgMode : int { kMsgCount = 0, kMsgFill = 1, kMsgRuns = 2, kMsgPlace = 3 };
+void launch_msgq(int mode, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                  const MsgImg& img, TopicCount* cnt, const TopicOff* off, MsgPiece* pieces,
-                 uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
+                 uint64_t* handles, uint64_t* base, uint32_t* count, MsgRun* runs, uint32_t run_cap,
+                 uint32_t* n_runs, hipStream_t s);
 void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s);
 
 }  // namespace mq

@@ -1111,7 +1111,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   const uint32_t cap = tcn.rows;
 
-  if (dcopy) {
+  uint32_t res_flags = 0;
+  if (dcopy && a.set_ref) {
+    // device result: the topic names its representative's set-relative patches (translated by the
+    // consumer through the topic's merge rows, MQ_TOPIC_SET_PATCHES)
+    const SetInfo si = a.sets[drep];
+    pbase = si.base;
+    n_patch = si.n;
+    n_nonbase = si.nonbase;
+    n_ext = si.ext;
+    res_flags = kTopicSetPatches;
+  } else if (dcopy) {
     // the representative's resolution: its set-relative patches, rows translated through this
     // topic's merge gathers (the same particles in the same order: k_dedup compared them)
     const SetInfo si = a.sets[drep];
@@ -1450,6 +1460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         atomicAdd(wc + 0, (unsigned long long)e);
         atomicAdd(wc + 1, (unsigned long long)rr);
         atomicAdd(wc + 2, (unsigned long long)l);
+        atomicAdd(wc + 3, (unsigned long long)n_patch);
       }
     }
     continue;
@@ -1501,7 +1512,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       res.n_client = cap - n_nonbase;
       res.n_ident = n_ext;
       res.n_shared = tcn.shared;
-      res.reserved = 0;
+      res.flags = res_flags;
       a.sres[t] = res;
     } else {
       mq_topic_result_dev res;
@@ -2383,22 +2394,53 @@ struct MsgFrame {  // a fan-out in progress: particles [cur, end) still to take 
   uint32_t cur, end, s;
 };
 
-// FILL=false: counts the filter's handles and copy pieces; FILL=true: writes short runs and
-// piece records at the offsets of the count pass's scan. Wavefront per filter.
-template <bool FILL>
+// Wavefront per filter. MODE (kernels.h MsgMode): kMsgCount counts the filter's handles and copy
+// pieces; kMsgFill writes short runs and piece records at the offsets of the count pass's scan;
+// kMsgRuns counts and records the runs (their output and piece offsets fixed by the same LDS
+// cursors the fill pass uses); kMsgPlace places recorded runs without walking again — the
+// filter's walk then runs once per batch instead of twice.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, const uint64_t* __restrict__ fo,
                                               uint32_t n, DevIndex ix, MsgImg img,
                                               TopicCount* __restrict__ cnt, const TopicOff* __restrict__ off,
                                               MsgPiece* __restrict__ pieces, uint64_t* __restrict__ handles,
-                                              uint64_t* __restrict__ base_out, uint32_t* __restrict__ count_out) {
-  __shared__ uint32_t hcur[4], pcur[4];  // FILL: next handle / piece of the wave's filter
+                                              uint64_t* __restrict__ base_out, uint32_t* __restrict__ count_out,
+                                              MsgRun* __restrict__ runs, uint32_t run_cap,
+                                              uint32_t* __restrict__ n_runs) {
+  constexpr bool FILL = MODE == kMsgFill || MODE == kMsgPlace;  // the walk writes output
+  constexpr bool RUNS = MODE == kMsgRuns;
+  __shared__ uint32_t hcur[4], pcur[4], rcur[4];  // next handle / piece / run of the wave's filter
   const uint32_t lane = threadIdx.x & 63, wv = wave_id();
   const uint32_t t = blockIdx.x * 4 + wv;
   if (t >= n) return;  // wave-uniform
   const uint64_t b0 = fo[t], b1 = fo[t + 1];
   const uint64_t obase = FILL ? off[t].rows : 0, pbase = FILL ? off[t].g : 0;
-  if (FILL) {
-    if (lane == 0) hcur[wv] = pcur[wv] = 0;
+  // one piece record per kMsgPiece handles of a long run
+  auto put_pieces = [&](uint32_t h0, uint32_t len, uint32_t dst, uint32_t slot) __attribute__((always_inline)) {
+    const uint32_t npc = (len + kMsgPiece - 1) / kMsgPiece;
+    for (uint32_t i = 0; i < npc; i++)
+      pieces[pbase + slot + i] = MsgPiece{h0 + i * kMsgPiece, (uint32_t)min(kMsgPiece, len - i * kMsgPiece),
+                                          obase + dst + (uint64_t)i * kMsgPiece};
+  };
+  if (MODE == kMsgPlace) {
+    const uint32_t nr = n_runs[t];
+    if (nr != kNone) {  // wave-uniform: the count pass recorded every run of this filter
+      const MsgRun* __restrict__ fr = runs + (uint64_t)t * run_cap;
+      for (uint32_t k = lane; k < nr; k += 64) {
+        const MsgRun r = fr[k];
+        if (r.len > kMsgDirect) put_pieces(r.h0, r.len, r.dst, r.pslot);
+        else
+          for (uint32_t j = 0; j < r.len; j++) handles[obase + r.dst + j] = img.h[r.h0 + j];
+      }
+      if (lane == 0) {
+        base_out[t] = obase;
+        count_out[t] = cnt[t].rows;
+      }
+      return;
+    }
+  }
+  if (FILL || RUNS) {
+    if (lane == 0) hcur[wv] = pcur[wv] = rcur[wv] = 0;
     wave_sync_lds();
   }
   uint32_t nh = 0, np = 0;  // count pass: this lane's handles and pieces
@@ -2408,17 +2450,20 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
     if (!FILL) {
       nh += len;
       np += npc;
-      return;
+      if (!RUNS) return;
     }
     const uint32_t dst = atomicAdd(&hcur[wv], len);
+    const uint32_t slot = npc ? atomicAdd(&pcur[wv], npc) : 0u;
+    if (RUNS) {
+      const uint32_t ri = atomicAdd(&rcur[wv], 1u);
+      if (ri < run_cap) runs[(uint64_t)t * run_cap + ri] = MsgRun{h0, len, dst, slot};
+      return;
+    }
     if (!npc) {
       for (uint32_t k = 0; k < len; k++) handles[obase + dst + k] = img.h[h0 + k];
       return;
     }
-    const uint32_t slot = atomicAdd(&pcur[wv], npc);
-    for (uint32_t i = 0; i < npc; i++)
-      pieces[pbase + slot + i] = MsgPiece{h0 + i * kMsgPiece, (uint32_t)min(kMsgPiece, len - i * kMsgPiece),
-                                          obase + dst + (uint64_t)i * kMsgPiece};
+    put_pieces(h0, len, dst, slot);
   };
   // image children of the run [a, b) (a < b); at level 0 without "$SYS" (topics.go:549)
   auto desc = [&](uint32_t a, uint32_t b, uint32_t& x, uint32_t& y) __attribute__((always_inline)) {
@@ -2559,22 +2604,32 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
   if (!FILL) {
     nh = wave_sum(nh);
     np = wave_sum(np);
-    if (lane == 0) cnt[t] = TopicCount{np, nh, 0, 0, 0};
+    if (RUNS) wave_sync_lds();  // every lane's run reservations are in rcur
+    if (lane == 0) {
+      cnt[t] = TopicCount{np, nh, 0, 0, 0};
+      if (RUNS) n_runs[t] = rcur[wv] <= run_cap ? rcur[wv] : kNone;
+    }
   } else if (lane == 0) {
     base_out[t] = obase;
     count_out[t] = cnt[t].rows;
   }
 }
 
-void launch_msgq(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+void launch_msgq(int mode, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                  const MsgImg& img, TopicCount* cnt, const TopicOff* off, MsgPiece* pieces,
-                 uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s) {
+                 uint64_t* handles, uint64_t* base, uint32_t* count, MsgRun* runs, uint32_t run_cap,
+                 uint32_t* n_runs, hipStream_t s) {
   if (!n) return;
   const dim3 g((n + 3) / 4), b(256);
-  if (fill)
-    hipLaunchKernelGGL(k_msgq<true>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count);
-  else
-    hipLaunchKernelGGL(k_msgq<false>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count);
+#define MQ_MSGQ(M) \
+  hipLaunchKernelGGL(k_msgq<M>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count, runs, run_cap, n_runs)
+  switch (mode) {
+    case kMsgCount: MQ_MSGQ(kMsgCount); break;
+    case kMsgFill: MQ_MSGQ(kMsgFill); break;
+    case kMsgRuns: MQ_MSGQ(kMsgRuns); break;
+    default: MQ_MSGQ(kMsgPlace); break;
+  }
+#undef MQ_MSGQ
 }
 
 // Wavefront per piece: four 64-handle loads in flight per lane, then the stores.

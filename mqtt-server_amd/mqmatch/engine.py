@@ -59,7 +59,7 @@ class TopicSpans(C.Structure):
     _fields_ = [("span_base", C.c_uint64), ("patch_base", C.c_uint64), ("inline_base", C.c_uint64),
                 ("picked_base", C.c_uint64), ("n_spans", C.c_uint32), ("n_patches", C.c_uint32),
                 ("n_inline", C.c_uint32), ("n_rows", C.c_uint32), ("n_client", C.c_uint32),
-                ("n_ident", C.c_uint32), ("n_shared", C.c_uint32), ("reserved", C.c_uint32)]
+                ("n_ident", C.c_uint32), ("n_shared", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class SpanResult(C.Structure):
@@ -67,7 +67,8 @@ class SpanResult(C.Structure):
                 ("patches", C.c_void_p), ("inline_rows", C.c_void_p), ("picked_rows", C.c_void_p),
                 ("sub_pool", C.c_void_p), ("shared_pool", C.c_void_p), ("n_spans", C.c_uint64),
                 ("n_patches", C.c_uint64), ("n_inline_rows", C.c_uint64), ("n_picked_rows", C.c_uint64),
-                ("sub_pool_len", C.c_uint64), ("shared_pool_len", C.c_uint64)]
+                ("sub_pool_len", C.c_uint64), ("shared_pool_len", C.c_uint64),
+                ("set_patches", C.c_void_p), ("merge_rows", C.c_void_p), ("n_set_patches", C.c_uint64)]
 
 
 SPANS_PICKED = 1  # MQ_SPANS_PICKED
@@ -617,7 +618,7 @@ class Engine:
 _TOPIC_SPANS_DT = np.dtype([("span_base", np.uint64), ("patch_base", np.uint64), ("inline_base", np.uint64),
                             ("picked_base", np.uint64), ("n_spans", np.uint32), ("n_patches", np.uint32),
                             ("n_inline", np.uint32), ("n_rows", np.uint32), ("n_client", np.uint32),
-                            ("n_ident", np.uint32), ("n_shared", np.uint32), ("reserved", np.uint32)])
+                            ("n_ident", np.uint32), ("n_shared", np.uint32), ("flags", np.uint32)])
 
 
 def _span_arrays(r, n):
@@ -659,6 +660,66 @@ def _expand_host_spans(rp, n):
         "sub_cap": t["n_rows"].copy(), "n_client": t["n_client"].copy(), "n_ident": t["n_ident"].copy(),
         "n_shared": t["n_shared"].copy(), "n_inline": t["n_inline"].copy(),
         "rows": rows[:int(nr.value)], "shared": shared[:int(ns.value)], "inline": a["inline"],
+        "n_patches": int(t["n_patches"].sum()), "n_spans": int(t["n_spans"].sum()),
+    }
+
+
+def _ranges(starts, counts):
+    """Concatenated index ranges [starts[i], starts[i] + counts[i])."""
+    counts = np.asarray(counts, np.int64)
+    total = int(counts.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    rep = np.repeat(np.asarray(starts, np.int64) - np.concatenate(([0], np.cumsum(counts)[:-1])), counts)
+    return rep + np.arange(total, dtype=np.int64)
+
+
+def expand_device_spans(r, n, count=None):
+    """Expand a DEVICE span result of n topics (mq_match_spans_device; r: SpanResult of device
+    pointers) into match_batch()'s dict on the host, for its first `count` topics (default all):
+    every topic's spans' records with its patches applied — per-topic patches, or set-shared ones
+    (MQ_TOPIC_SET_PATCHES) translated through the topic's merge rows. What a device consumer of
+    the format does; used by the tests and bench.py's parity sample."""
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    hip.hipDeviceSynchronize.argtypes = []
+    assert hip.hipDeviceSynchronize() == 0
+
+    def d2h(ptr, count, dtype, width=1):
+        out = np.zeros((count, width), dtype) if width > 1 else np.zeros(count, dtype)
+        if count and ptr:
+            assert hip.hipMemcpy(out.ctypes.data, ptr, out.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+        return out
+    count = n if count is None else min(count, n)
+    t = d2h(r.topics, 64 * count, np.uint8).view(_TOPIC_SPANS_DT)
+    n = count
+    n_sp = int(t["span_base"][-1]) + int(t["n_spans"][-1]) if n else 0  # spans are in topic order
+    spans = d2h(r.spans, n_sp, np.uint32, 4)
+    pool = d2h(r.sub_pool, int(r.sub_pool_len), np.uint32, 4)
+    spool = d2h(r.shared_pool, int(r.shared_pool_len), np.uint32, 2)
+    patches = d2h(r.patches, int(r.n_patches), np.uint32, 2)
+    sets = d2h(r.set_patches, int(r.n_set_patches), np.uint32, 2)
+    mrows = d2h(r.merge_rows, 64 * n if r.merge_rows else 0, np.uint32)
+    inl = d2h(r.inline_rows, int(r.n_inline_rows), np.uint32, 2)
+    excl = lambda c: np.concatenate(([0], np.cumsum(c)[:-1])).astype(np.uint64) if len(c) else np.zeros(0, np.uint64)
+    rows = pool[_ranges(spans[:, 0], spans[:, 1])].copy() if len(spans) else np.zeros((0, 4), np.uint32)
+    shared = spool[_ranges(spans[:, 2], spans[:, 3])] if len(spans) else np.zeros((0, 2), np.uint32)
+    sub_base = excl(t["n_rows"].astype(np.uint64))
+    setf = (t["flags"] & 1) != 0
+    for own in (True, False):
+        sel = ~setf if own else setf
+        tid = np.repeat(np.arange(n)[sel], t["n_patches"][sel].astype(np.int64))
+        src = patches if own else sets
+        pr = src[_ranges(t["patch_base"][sel], t["n_patches"][sel])]
+        row = pr[:, 0].astype(np.int64)
+        if not own:
+            row = mrows[tid * 64 + (row >> 26)].astype(np.int64) + (row & ((1 << 26) - 1))
+        rows[sub_base[tid].astype(np.int64) + row, 3] = pr[:, 1]
+    return {
+        "sub_base": sub_base, "shared_base": excl(t["n_shared"].astype(np.uint64)),
+        "inline_base": t["inline_base"].copy(), "sub_cap": t["n_rows"].copy(), "n_client": t["n_client"].copy(),
+        "n_ident": t["n_ident"].copy(), "n_shared": t["n_shared"].copy(), "n_inline": t["n_inline"].copy(),
+        "rows": rows, "shared": shared, "inline": inl, "set_topics": int(setf.sum()),
         "n_patches": int(t["n_patches"].sum()), "n_spans": int(t["n_spans"].sum()),
     }
 

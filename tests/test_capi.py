@@ -27,7 +27,7 @@ def test_library_exports_all_symbols():
     L = E.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.mq_abi_version() == 5
+    assert L.mq_abi_version() == 6
 
 
 def test_errors_are_reported():

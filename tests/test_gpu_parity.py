@@ -377,6 +377,31 @@ def test_spans_device_matches_host(gpu_available):
     assert r.n_spans == len(host["spans"]) and r.n_patches >= int(host["topics"]["n_patches"].sum())
 
 
+@pytest.mark.parametrize("dedup", [1, 0])
+def test_spans_device_digest_parity(dedup, gpu_available):
+    """mq_match_spans_device expanded as a device consumer would (spans, then per-topic patches or
+    set-shared patches through the topic's merge rows, inline rows): per-topic digests equal the
+    oracle's. With merge-set dedup (the default) topics share their merge set's patches
+    (MQ_TOPIC_SET_PATCHES); without it every topic holds its own."""
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(60000, 3000, seed=63)
+    eng.set_option(E.OPT_MERGE_DEDUP, dedup)
+    tb, to = W.gen_topics(w, 6000, seed=64)
+    n = len(to) - 1
+    d_tb = torch.from_numpy(tb).cuda()
+    d_to = torch.from_numpy(to.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
+    res = E.expand_device_spans(r, n)
+    assert (res["set_topics"] > 0) == bool(dedup)
+    dg, cnt = engine_digests(res)
+    od, ocnt, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+    bad = np.nonzero(dg != od)[0]
+    assert len(bad) == 0, f"{len(bad)} of {n} topics differ (first {bad[:5]})"
+
+
 def test_spans_result_pins_host_image(gpu_available):
     """A host span result pins the pools it points into: an update from another thread waits
     until the result is freed."""

@@ -1,0 +1,20 @@
+# Parity file (single-walk Messages, set patches), then rocprofv3 kernel trace + PMC passes
+# (FETCH_SIZE, WRITE_SIZE: separate runs) of the default 10M span step, then Messages at 10M.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+D=$R/gpurun_out/${1:-r2c_pmc}
+mkdir -p $D
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > $D/parity.log 2>&1 || { echo "parity rc=$?"; tail -30 $D/parity.log; exit 1; }
+tail -2 $D/parity.log
+cd /tmp && export TMPDIR=/tmp
+ARGS="--steps 3 --warmup 1 --no-cpu"
+KR="k_walk|k_merge|k_desc|k_scan|k_dedup"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 $R/bench.py $ARGS > $D/trace.json 2> $D/trace.err || { echo "trace rc=$?"; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" --output-format csv -d $D/fetch -o run -- python3 $R/bench.py $ARGS > $D/fetch.json 2> $D/fetch.err || { echo "fetch rc=$?"; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" --output-format csv -d $D/write -o run -- python3 $R/bench.py $ARGS > $D/write.json 2> $D/write.err || { echo "write rc=$?"; exit 1; }
+cd $R
+python profiles/summarize.py $D/trace > $D/kernel_stats.json
+python profiles/summarize.py $D/fetch $D/write --pmc > $D/pmc.json
+head -c 1500 $D/kernel_stats.json; grep -B2 -A4 hbm_bytes $D/pmc.json | head -60
+timeout -k 10 500 python -u bench_messages.py --retained 10000000 > $D/msg_10m.json 2> $D/msg_10m.err || { echo "msg rc=$?"; tail -5 $D/msg_10m.err; exit 1; }
+cut -c1-1800 $D/msg_10m.json
