@@ -117,6 +117,41 @@ def read_spans_traffic(path, n_subs, n_topics):
         return None
 
 
+def read_walk_traffic(path, n_subs, n_topics):
+    """HBM bytes per k_walk launch (FETCH_SIZE x2 + WRITE_SIZE) from a committed rocprofv3 PMC
+    summary of the same configuration, if present."""
+    try:
+        with open(path) as f:
+            e = json.load(f).get("walk", {}).get(str(n_subs))
+        if e is None or int(e["topics"]) != n_topics:
+            return None
+        return float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step):
+    """Roofline of k_walk (the match walk, thread per topic). Its algorithmic bytes per topic are
+    SURVEY.md §8(d)'s walk terms, 8·L + 4 + 16·P (L levels, P child lookups of the reference's
+    DFS, counted exactly by the oracle on a sample of the batch), plus the 4-byte gather word it
+    writes per gathered particle; over its mean launch time from HIP events in the timed region.
+    Dependent probes of a 2 GB edge table: bound by random-access latency and request rate, far
+    below streaming bandwidth."""
+    launches, ms = prof.get("walk", (0, 0.0))
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+            "traffic": None, "kernel": "k_walk (count pass, gathers only)",
+            "bytes": "8 B per level + 4 B offset + 16 B per child lookup (SURVEY 8d: 8L + 4 + 16P) + 4 B per gather word"}
+    if not launches or ms <= 0 or per_topic is None:
+        return roof
+    b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"]
+    per_launch = b_topic * n + 4 * gathers_per_step
+    launch_ms = ms / launches
+    achieved = per_launch / (launch_ms * 1e-3) / 1e9
+    roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, launch_ms=launch_ms, bytes_per_launch=per_launch,
+                traffic=read_walk_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n))
+    return roof
+
+
 def spans_roofline(prof, work, steps, n, n_subs):
     """Roofline of the span format's merge stage, k_merge<spans>: with merge-set dedup (the
     default) two launches per step — the set pass (one resolution per distinct merge set) and the
@@ -468,6 +503,18 @@ def main():
         b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"] + 16 * per_topic["S"] + 16 * per_topic["O"]
         out["alg_bytes_per_topic"] = {"B": b_topic, "L": per_topic["L"], "P": per_topic["P"],
                                       "S": per_topic["S"], "O": per_topic["O"], "sample_topics": ns}
+        if args.format == "spans":
+            # `roofline` names the step's dominant kernel: the walk or the merge stage, whichever
+            # takes longer per step; the other is reported beside it
+            wr = walk_roofline(prof, args.steps, n, args.subs, per_topic,
+                               out["counters_per_step"].get("gathers", 0))
+            mr = out["roofline"]
+            walk_ms = wr.get("launch_ms") or 0.0
+            merge_ms = mr.get("ms_per_step") or 0.0
+            if walk_ms > merge_ms and wr["achieved"] is not None:
+                out["roofline"], out["roofline_merge"] = wr, mr
+            else:
+                out["roofline_walk"] = wr
         # End-to-end through the host-buffer boundary on a bounded sample (H2D of the topics, the
         # kernels, D2H of the results into host memory), reported beside `value`, never as it
         # (DESIGN.md §5). Span format: mq_match_spans, and separately with every row expanded

@@ -285,7 +285,8 @@ Device::~Device() {
   }
   plan_.release();
   for (DevBuf* b : {&sp_tc_, &dd_sig_, &dd_cnt_, &dd_list_, &dd_mrow_, &dd_keys_, &dd_vals_, &dd_slot_, &dd_rep_,
-                    &dd_nsets_, &dd_rlist_, &dd_sets_, &dd_spatches_, &dd_spcount_, &msg_runs_, &msg_nruns_})
+                    &dd_nsets_, &dd_rlist_, &dd_sets_, &dd_spatches_, &dd_spcount_, &dd_wlist_, &dd_nwave_, &msg_runs_,
+                    &msg_nruns_})
     b->release();
   if (h_plan_) (void)hipHostFree(h_plan_);
   if (h_pin_) (void)hipHostFree(h_pin_);
@@ -1008,7 +1009,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
       unsigned long long ns = 0;
       hip_check(hipMemcpyAsync(&ns, dd_nsets_.p, sizeof(ns), hipMemcpyDeviceToHost, s), "D2H");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-      prof.count("merge_sets", ns);
+      prof.count("dedup_sets", ns);
     }
   }
 
@@ -1151,6 +1152,27 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     a.work = work0;
     a.dd_phase = 2;
     a.set_ref = host ? 0u : 1u;  // host results get per-topic patches (copied in phase 2)
+    if (a.set_ref) {  // results that need no wavefront: k_finish, thread per topic
+      grow(dd_wlist_, (size_t)n * sizeof(uint32_t));
+      if (!dd_nwave_.p) dd_nwave_.ensure(sizeof(unsigned long long));
+      hip_check(hipMemsetAsync(dd_nwave_.p, 0, sizeof(unsigned long long), s), "memset");
+      FinishArgs fa;
+      fa.n = n;
+      fa.off = a.off;
+      fa.tc = a.tc;
+      fa.tslot = a.tslot;
+      fa.rep = a.rep;
+      fa.sets = a.sets;
+      fa.sres = a.sres;
+      fa.wave_list = dd_wlist_.as<uint32_t>();
+      fa.n_wave = dd_nwave_.as<unsigned long long>();
+      prof.begin(s);
+      launch_finish(fa, s);
+      prof.end("finish", s);
+      hip_check(hipGetLastError(), "k_finish");
+      a.wave_list = fa.wave_list;
+      a.n_wave = fa.n_wave;
+    }
   }
   for (int attempt = 0;; attempt++) {
     a.patches = sp_patches_.as<PatchRec>();
@@ -1158,7 +1180,8 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
     if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
     prof.begin(s);
-    launch_merge(a, true, sb_.fused, merge_wpe, merge_blocks_, s);
+    // after k_finish the waves stride over its list (its length is on the device)
+    launch_merge(a, true, sb_.fused, merge_wpe, a.wave_list && !merge_blocks_ ? n_cus_ * 8 : merge_blocks_, s);
     prof.end("merge", s);
     hip_check(hipGetLastError(), "k_merge<spans>");
     hip_check(hipMemcpyAsync(h_pc, a.pcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),

@@ -169,6 +169,8 @@ struct EmitArgs {
                                        //   (device results) instead of copying them
   const uint32_t* rep_list;            // dd_phase 1: the set representatives (k_dedup_rep)
   const unsigned long long* n_reps;    //   and their number, in device memory
+  const uint32_t* wave_list;           // dd_phase 2 after k_finish: the topics that still need a
+  const unsigned long long* n_wave;    //   wavefront (k_finish wrote the others' results)
 };
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
 constexpr uint32_t kTopicSetPatches = 1;  // TopicSpansDev.flags: patches shared with a merge set
@@ -273,6 +275,23 @@ void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
 // desc: span format with k_desc fused in (a.gathers / a.spans; not for a sharded index)
 void launch_merge(const EmitArgs& a, bool spans, bool desc, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
+
+// k_finish (span format, merge-set dedup, device results): thread per topic, after the set pass.
+// A topic whose result needs no wavefront — no inline rows, and no may-merge records or a merge
+// set (it references the set's patches) — gets its result record here; the others are listed
+// for k_merge's topic pass.
+struct FinishArgs {
+  uint32_t n;
+  const TopicOff* off;
+  const TopicCount* tc;  // per-topic counts (k_desc), or null: the offsets' differences
+  const uint32_t* tslot;
+  const uint32_t* rep;
+  const SetInfo* sets;
+  TopicSpansDev* sres;
+  uint32_t* wave_list;
+  unsigned long long* n_wave;
+};
+void launch_finish(const FinishArgs& a, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
 // first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
 // fill pass must still walk; the fill pass then walks only those.
@@ -355,7 +374,7 @@ void launch_img_compact(const DevIndex& ix, const uint32_t* node, const uint32_t
 struct MsgRun {
   uint32_t h0, len, dst, pslot;
 };
-constexpr uint32_t kMsgRunCap = 64;  // runs recorded per filter (more: the filter is walked again)
+constexpr uint32_t kMsgRunCap = 256;  // runs recorded per filter (more: the filter is walked again)
 // Messages passes (k_msgq):
 //   kMsgCount  TopicCount.gathers = pieces, .rows = handles
 //   kMsgFill   pieces at off[t].g, short runs copied directly, base / count written

@@ -809,9 +809,14 @@ __global__ __launch_bounds__(256) void k_dedup_rep(DedupArgs a) {
     if (v != t) {
       const uint32_t c = a.mcount[t];
       bool eq = a.mcount[v] == c;
-      const uint32_t* x = a.mlist + (uint64_t)t * kPairMax;
-      const uint32_t* y = a.mlist + (uint64_t)v * kPairMax;
-      for (uint32_t j = 0; eq && j < c; j++) eq = x[j] == y[j];
+      // the lists, four nodes per load (rows of kPairMax u32 are 16-byte aligned; entries past c
+      // are not compared)
+      const uint4* x = reinterpret_cast<const uint4*>(a.mlist + (uint64_t)t * kPairMax);
+      const uint4* y = reinterpret_cast<const uint4*>(a.mlist + (uint64_t)v * kPairMax);
+      for (uint32_t j = 0; eq && j < c; j += 4) {
+        const uint4 p = x[j >> 2], q = y[j >> 2];
+        eq = p.x == q.x && (j + 1 >= c || p.y == q.y) && (j + 2 >= c || p.z == q.z) && (j + 3 >= c || p.w == q.w);
+      }
       if (eq) r = v;
     }
   }
@@ -822,6 +827,55 @@ __global__ __launch_bounds__(256) void k_dedup_rep(DedupArgs a) {
   if (lane == 0 && b) base = atomicAdd(a.n_sets, (unsigned long long)__popcll(b));
   base = __shfl(base, 0, 64);
   if (own) a.rep_list[base + prefix_before(b)] = t;
+}
+
+__global__ __launch_bounds__(256) void k_finish(FinishArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  bool wave = false;
+  if (t < a.n) {
+    const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+    const TopicCount c = a.tc ? a.tc[t]
+                              : TopicCount{(uint32_t)(o1.g - o0.g), (uint32_t)(o1.rows - o0.rows),
+                                           (uint32_t)(o1.shr - o0.shr), (uint32_t)(o1.inl - o0.inl),
+                                           (uint32_t)(o1.merge - o0.merge)};
+    const uint32_t sl = a.tslot[t];
+    const bool set = sl != kNone;
+    wave = c.inlines != 0 || (c.merge != 0 && !set);
+    if (!wave) {
+      TopicSpansDev res;
+      res.span_base = o0.g;
+      res.patch_base = 0;
+      res.inline_base = o0.inl;
+      res.picked_base = o0.shr;
+      res.n_spans = (uint32_t)(o1.g - o0.g);
+      res.n_patches = 0;
+      res.n_inline = 0;
+      res.n_rows = c.rows;
+      res.n_client = c.rows;
+      res.n_ident = 0;
+      res.n_shared = c.shared;
+      res.flags = 0;
+      if (set) {  // the representative's resolution (k_merge's set pass), by reference
+        const SetInfo si = a.sets[a.rep[t]];
+        res.patch_base = si.base;
+        res.n_patches = si.n;
+        res.n_client = c.rows - si.nonbase;
+        res.n_ident = si.ext;
+        res.flags = kTopicSetPatches;
+      }
+      a.sres[t] = res;
+    }
+  }
+  const uint64_t b = __ballot(wave);
+  unsigned long long base = 0;
+  if (lane == 0 && b) base = atomicAdd(a.n_wave, (unsigned long long)__popcll(b));
+  base = __shfl(base, 0, 64);
+  if (wave) a.wave_list[base + prefix_before(b)] = t;
+}
+
+void launch_finish(const FinishArgs& a, hipStream_t s) {
+  if (!a.n) return;
+  hipLaunchKernelGGL(k_finish, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 
 void launch_dedup(const DedupArgs& a, hipStream_t s) {
@@ -992,11 +1046,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t wv = wave_id(), lane = threadIdx.x & 63;
   auto rank_of = [](const GDesc& d) { return gdesc_rank<XS>(d); };
   // persistent: a.merge grid's waves stride over the chunk's topics (wave-uniform loop)
-  // (dedup's set pass: the waves stride over the list of set representatives instead)
-  const bool set_pass = SPANS && a.rep && a.dd_phase == 1;
-  const uint32_t i_end = set_pass ? (uint32_t)*a.n_reps : a.t1;
+  // (dedup's set pass: the waves stride over the list of set representatives instead; its topic
+  // pass after k_finish: over the topics k_finish left)
+  const uint32_t* __restrict__ tlist = !(SPANS && a.rep) ? nullptr
+                                     : a.dd_phase == 1 ? a.rep_list : a.wave_list;
+  const uint32_t i_end = tlist ? (uint32_t)*(a.dd_phase == 1 ? a.n_reps : a.n_wave) : a.t1;
   for (uint32_t i = a.t0 + blockIdx.x * 4 + wv; i < i_end; i += gridDim.x * 4) {
-  const uint32_t t = set_pass ? a.rep_list[i] : i;
+  const uint32_t t = tlist ? tlist[i] : i;
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
   const uint64_t ib = o0.inl - a.base.inl;
