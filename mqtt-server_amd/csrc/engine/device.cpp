@@ -285,7 +285,7 @@ Device::~Device() {
   }
   plan_.release();
   for (DevBuf* b : {&sp_tc_, &dd_sig_, &dd_cnt_, &dd_list_, &dd_mrow_, &dd_keys_, &dd_vals_, &dd_slot_, &dd_rep_,
-                    &dd_nsets_, &dd_rlist_, &dd_sets_, &dd_spatches_, &dd_spcount_, &dd_wlist_, &dd_nwave_, &msg_runs_,
+                    &dd_nsets_, &dd_rlist_, &dd_sets_, &dd_spatches_, &dd_spcount_, &dd_wlist_, &dd_nwave_, &dd_mpair_, &msg_runs_,
                     &msg_nruns_})
     b->release();
   if (h_plan_) (void)hipHostFree(h_plan_);
@@ -960,12 +960,15 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   da.mcount = nullptr;
   da.mlist = nullptr;
   da.mrow = nullptr;
+  da.mpair = nullptr;
   sb_.dedup = dedup_ != 0 && !ix.sharded() && !sb_.fused;
   if (sb_.dedup) {
     grow(dd_sig_, (size_t)n * sizeof(uint64_t));
     grow(dd_cnt_, (size_t)n * sizeof(uint32_t));
     grow(dd_list_, (size_t)n * kPairMax * sizeof(uint32_t));
     grow(dd_mrow_, (size_t)n * kPairMax * sizeof(uint32_t));
+    grow(dd_mpair_, (size_t)n * kPairMax * sizeof(uint2));
+    da.mpair = dd_mpair_.as<uint2>();
     da.msig = dd_sig_.as<uint64_t>();
     da.mcount = dd_cnt_.as<uint32_t>();
     da.mlist = dd_list_.as<uint32_t>();
@@ -1121,6 +1124,8 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     a.tslot = dd_slot_.as<uint32_t>();
     a.mcount = dd_cnt_.as<uint32_t>();
     a.mrow = dd_mrow_.as<uint32_t>();
+    a.mlist = dd_list_.as<uint32_t>();
+    a.mpair = dd_mpair_.as<uint2>();
     a.sets = dd_sets_.as<SetInfo>();
     a.spcount = dd_spcount_.as<unsigned long long>();
     a.rep_list = dd_rlist_.as<uint32_t>();

@@ -305,6 +305,7 @@ class Device {
   DevBuf dd_sig_, dd_cnt_, dd_list_, dd_mrow_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_, dd_rlist_;
   DevBuf dd_sets_, dd_spatches_, dd_spcount_;  // phase 1 of the dedup merge: SetInfo, set pool
   DevBuf dd_wlist_, dd_nwave_;                 // k_finish: topics left for k_merge's topic pass
+  DevBuf dd_mpair_;                            // k_desc: merge gathers' pair-block headers
   uint64_t srcap_ = 0;                         // set patches per region of dd_spatches_
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
   uint32_t n_cus_ = 1;

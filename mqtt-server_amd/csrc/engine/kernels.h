@@ -160,6 +160,8 @@ struct EmitArgs {
   const uint32_t* tslot;
   const uint32_t* mcount;  // merge gathers per topic, and their rows (k_desc, stride kPairMax)
   const uint32_t* mrow;
+  const uint32_t* mlist;   // dedup: their particles and pair-block headers (k_desc, stride kPairMax):
+  const uint2* mpair;      //   the map is built from these (topics with <= kPairMax merge gathers)
   uint32_t dd_phase;
   struct SetInfo* sets;
   PatchRec* spatches;
@@ -209,6 +211,9 @@ struct DescArgs {
   uint32_t* mcount;
   uint32_t* mlist;
   uint32_t* mrow;  // the topic-relative row of each merge gather's first may-merge slot (stride kPairMax)
+  uint2* mpair;    // its pair-block header (NodePair ent_off, ent_mask; stride kPairMax). With these
+                   // lists k_merge maps a topic's merge gathers without GDesc records, which are
+                   // then written only for a topic with more than kPairMax merge gathers
 };
 
 // Merge-set dedup (span format): topics whose merge gathers are the same particles resolve to

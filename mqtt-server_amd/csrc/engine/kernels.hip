@@ -720,7 +720,7 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
         }
       }
     }
-    a.desc[g] = d;
+    if (!SPANS || !a.msig) a.desc[g] = d;  // dedup lists: GDesc only for a wide topic (below)
     if (SPANS) {
       if (gw & kGatherSubs) n_merge += L.n_merge;
       if (a.msig && (d.mdir & kDescMerge)) {
@@ -728,6 +728,7 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
         if (n_mg < kPairMax) {
           a.mlist[(uint64_t)t * kPairMax + n_mg] = gw & kGatherNode;
           a.mrow[(uint64_t)t * kPairMax + n_mg] = rpos + L.n_direct;
+          a.mpair[(uint64_t)t * kPairMax + n_mg] = make_uint2(d.s_pos, d.s_src);
         }
         // set-relative rows hold 26 bits of slot: a larger merge gather keeps the topic apart
         n_mg += L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1;
@@ -749,6 +750,19 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
   if (SPANS && a.msig) {
     a.msig[t] = msig | 1ull;  // never 0 (the dedup table's empty key)
     a.mcount[t] = n_mg;
+    if (n_mg > kPairMax) {  // k_merge maps this topic from its GDesc records: write them (rare)
+      uint32_t rp = 0, sp = (uint32_t)o0.shr;
+      for (uint32_t i = 0; i < n_g; i++) {
+        const uint32_t gw = gw_src[i];
+        const NodeLists L = a.ix.lists[gw & kGatherNode];
+        const bool mg = (gw & kGatherSubs) && L.n_merge;
+        const NodePair P = mg ? a.ix.npair[gw & kGatherNode] : NodePair{0, kNone, 0, 0};
+        a.desc[o0.g + i] = GDesc{rp, L.sub_off, mg ? P.ent_off : sp, mg ? P.ent_mask : L.shr_off, 0u, 0u, gw,
+                                 L.n_direct | (mg ? kDescMerge : 0u)};
+        rp += (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
+        sp += L.shr_cnt;
+      }
+    }
   }
 }
 
@@ -1198,7 +1212,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // Map every gathered node that holds may-merge records (and whose subscriptions are
     // gathered, Q3) to its gather index, and list them in gather order. Nodes are distinct
     // within a topic.
-    if (!DESC) {
+    // merge-set dedup's lists (k_desc): the topic's merge gathers directly, x standing for the
+    // gather index (the same order); a topic with more than kPairMax of them has GDesc records
+    const uint32_t lc = (SPANS && !XS && !DESC && a.mlist) ? a.mcount[t] : kNone;
+    if (lc <= kPairMax) {
+      for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
+      wave_sync_lds();
+      if (lane < lc) {
+        const uint64_t k = (uint64_t)t * kPairMax + lane;
+        const uint32_t node = a.mlist[k];
+        const uint2 P = a.mpair[k];
+        uint32_t sl = hash32(node) & (kMapSlots - 1);
+        while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
+        map_val[wv][sl] = lane;
+        mg_node[wv][lane] = node;
+        mg_gi[wv][lane] = lane;
+        mg_row[wv][lane] = a.mrow[k];
+        mg_eoff[wv][lane] = P.x;
+        mg_emask[wv][lane] = P.y;
+      }
+      n_map = lc;
+    } else if (!DESC) {
     for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
     wave_sync_lds();
     for (uint32_t i0 = 0; i0 < n_g; i0 += 64) {
