@@ -813,8 +813,10 @@ __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
 
 // k_dedup_rep also lists the topics that resolve a merge set (rep_list, n_sets of them): the
 // merge's set pass walks that list instead of every topic.
-__global__ __launch_bounds__(256) void k_dedup_rep(DedupArgs a) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+__global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
+  __shared__ uint32_t wcnt[16];
+  __shared__ unsigned long long bbase;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63, wv = wave_id();
   const bool act = t < a.n;
   const uint32_t sl = act ? a.tslot[t] : kNone;
   uint32_t r = t;
@@ -837,10 +839,21 @@ __global__ __launch_bounds__(256) void k_dedup_rep(DedupArgs a) {
   if (act) a.rep[t] = r;
   const bool own = r == t && sl != kNone;
   const uint64_t b = __ballot(own);
-  unsigned long long base = 0;
-  if (lane == 0 && b) base = atomicAdd(a.n_sets, (unsigned long long)__popcll(b));
-  base = __shfl(base, 0, 64);
-  if (own) a.rep_list[base + prefix_before(b)] = t;
+  // one atomic per workgroup on the list's counter (one per wavefront serialised ~16k atomics on
+  // one address per 1M topics)
+  if (lane == 0) wcnt[wv] = (uint32_t)__popcll(b);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; w++) {
+      const uint32_t c = wcnt[w];
+      wcnt[w] = tot;
+      tot += c;
+    }
+    bbase = tot ? atomicAdd(a.n_sets, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  if (own) a.rep_list[bbase + wcnt[wv] + prefix_before(b)] = t;
 }
 
 __global__ __launch_bounds__(256) void k_finish(FinishArgs a) {
@@ -896,7 +909,7 @@ void launch_dedup(const DedupArgs& a, hipStream_t s) {
   if (!a.n) return;
   const dim3 g((a.n + 255) / 256), b(256);
   hipLaunchKernelGGL(k_dedup_insert, g, b, 0, s, a);
-  hipLaunchKernelGGL(k_dedup_rep, g, b, 0, s, a);
+  hipLaunchKernelGGL(k_dedup_rep, dim3((a.n + 1023) / 1024), dim3(1024), 0, s, a);
 }
 
 // Stream S of one tile: rows [x0, x1) of the chunk's stream S (0: client rows, 1: shared rows,
