@@ -178,10 +178,21 @@ def main():
         out["alg_bytes_per_filter"] = {"B": b, **per, "sample_filters": ns}
         kms = sum(v[1] for k, v in prof.items() if k.startswith("msg") and k != "msg_image") / args.steps
         if kms > 0:
-            ach = b * n / (kms * 1e-3) / 1e9
+            # The image path's own algorithmic bytes: the filter's bytes and offset, and every
+            # emitted handle read once from the image and written once to the output. SURVEY
+            # §8d's B also prices the reference walk's child enumerations (16·P), which the image
+            # path does not perform: that rate is reported beside it (it can exceed HBM peak).
+            handles_per_filter = r.n_handles / max(1, n)
+            b_img = 8 * per["L"] + 4 + 16 * handles_per_filter
+            ach = b_img * n / (kms * 1e-3) / 1e9
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                               "kernel": "k_msgq + k_msg_copy" if not args.walk else "k_msg (count + fill)"}
+                               "kernel": "k_msgq (count, place) + k_msg_copy" if not args.walk else "k_msg (count + fill)",
+                               "bytes": "8 B per level + 4 B offset per filter, 16 B per emitted handle (read + write)",
+                               "bytes_per_step": b_img * n, "ms_per_step": kms}
+            out["survey_B_rate"] = {"GBps": b * n / (kms * 1e-3) / 1e9,
+                                    "note": "SURVEY 8d B (incl. 16 B per child enumeration of the reference walk) "
+                                            "per step time: the reference's work rate, not HBM traffic"}
         cpu = o["cpu"]
     out["cpu_baseline"] = cpu
     try:
