@@ -1148,7 +1148,9 @@ __device__ __forceinline__ uint64_t gdesc_rank(const GDesc& d) {
 // gathers — the spans (coalesced stores), the per-topic counts, the inline rows and the map of
 // merge gathers come from one round of loads (gather word, then lists and pair header
 // together); GDesc records are written only for a topic that takes the slow paths.
-template <bool SPANS, bool XS, int WPE, bool DESC>
+// SET (span format, merge-set dedup): the set pass (a.dd_phase 1), compiled apart so that the
+// topic pass's copy, inline and result code does not weigh on its register allocation.
+template <bool SPANS, bool XS, int WPE, bool DESC, bool SET = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
   __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records (or
@@ -1170,8 +1172,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // (dedup's set pass: the waves stride over the list of set representatives instead; its topic
   // pass after k_finish: over the topics k_finish left)
   const uint32_t* __restrict__ tlist = !(SPANS && a.rep) ? nullptr
-                                     : a.dd_phase == 1 ? a.rep_list : a.wave_list;
-  const uint32_t i_end = tlist ? (uint32_t)*(a.dd_phase == 1 ? a.n_reps : a.n_wave) : a.t1;
+                                     : SET ? a.rep_list : a.wave_list;
+  const uint32_t i_end = tlist ? (uint32_t)*(SET ? a.n_reps : a.n_wave) : a.t1;
   for (uint32_t i = a.t0 + blockIdx.x * 4 + wv; i < i_end; i += gridDim.x * 4) {
   const uint32_t t = tlist ? tlist[i] : i;
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
@@ -1188,9 +1190,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // in phase 2, a topic that is not deduped resolves itself in phase 2
   const uint32_t dslot = (SPANS && a.rep) ? a.tslot[t] : kNone;
   const uint32_t drep = dslot != kNone ? a.rep[t] : t;
-  if (SPANS && a.rep && a.dd_phase == 1 && (dslot == kNone || drep != t)) continue;
-  const bool setrel = SPANS && a.rep && a.dd_phase == 1;
-  const bool dcopy = SPANS && a.rep && a.dd_phase == 2 && dslot != kNone;
+  if (SET && (dslot == kNone || drep != t)) continue;
+  const bool setrel = SET;
+  const bool dcopy = !SET && SPANS && a.rep && dslot != kNone;
   PatchRec* __restrict__ ppool = setrel ? a.spatches : a.patches;
   unsigned long long* __restrict__ pcnt = setrel ? a.spcount : a.pcount;
   const uint64_t prcap = setrel ? a.srcap : a.rcap;
@@ -1797,6 +1799,10 @@ void launch_merge(const EmitArgs& a, bool spans, bool desc, uint32_t wpe, uint32
     if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, true>), g, b, 0, s, a);
     else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_merge<true, false, 1, true>), g, b, 0, s, a);
+  } else if (spans && a.rep && a.dd_phase == 1) {  // merge-set dedup: the set pass
+    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, false, true>), g, b, 0, s, a);
+    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, false, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, false, 1, false, true>), g, b, 0, s, a);
   } else if (spans) {
     if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, false>), g, b, 0, s, a);
     else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, false>), g, b, 0, s, a);
