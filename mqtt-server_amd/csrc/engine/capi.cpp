@@ -8,6 +8,7 @@
 #include <mutex>
 #include <cstring>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -529,8 +530,13 @@ int mq_device_check(mq_index* idx) {
 }
 
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
-  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MERGE_DEDUP) return fail(MQ_EINVAL, "unknown option");
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_EDGE_LOAD) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
+    if (option == MQ_OPT_EDGE_LOAD) {  // the host image's option
+      if (value != 2 && value != 4 && value != 8) throw std::invalid_argument("MQ_OPT_EDGE_LOAD: 2, 4 or 8");
+      idx->ix->set_edge_load((uint32_t)value);
+      return 0;
+    }
     idx->options.emplace_back(option, value);  // applied when the device is first touched
     if (idx->dev) idx->dev->set_option(option, value);
     return 0;

@@ -319,8 +319,12 @@ void Index::edge_walk_sync(uint32_t n) {
 }
 
 void Index::edge_insert(uint32_t parent, const SegKey& k, uint32_t child, uint32_t plus, uint32_t hash) {
-  if ((n_edges_ + n_tombs_ + 1) * 2 > edges.size())
-    edge_rehash(n_edges_ * 4 > edges.size() ? edges.size() * 2 : edges.size());
+  if ((n_edges_ + n_tombs_ + 1) * edge_load_at(edges.size()) > edges.size()) {
+    size_t cap = edges.size();
+    if ((n_edges_ + 1) * 2 * edge_load_at(cap) > cap) cap <<= 1;  // double unless mostly tombstones
+    while ((n_edges_ + 1) * edge_load_at(cap) > cap) cap <<= 1;   // (the bound was lowered)
+    edge_rehash(cap);
+  }
   const uint64_t m = edges.size() - 1;
   uint64_t i = edge_hash(parent, k) & m;
   for (;;) {

@@ -78,7 +78,7 @@ PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP, OPT_MERGE_WAVES = \
     1, 2, 3, 4, 5, 6, 7
 OPT_MSG_IMAGE = 8
-OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_FUSE_DESC, OPT_MERGE_DEDUP = 9, 10, 11, 12
+OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_FUSE_DESC, OPT_MERGE_DEDUP, OPT_EDGE_LOAD = 9, 10, 11, 12, 13
 
 
 class MsgResult(C.Structure):
