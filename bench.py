@@ -117,13 +117,21 @@ def read_spans_traffic(path, n_subs, n_topics):
         return None
 
 
+def engine_option(opt, default):
+    """An engine option as MQ_ENGINE_OPTIONS sets it for this process (mqmatch/engine.py)."""
+    for kv in os.environ.get("MQ_ENGINE_OPTIONS", "").split(","):
+        if kv.strip() and int(kv.split("=")[0]) == opt:
+            return int(kv.split("=")[1])
+    return default
+
+
 def read_walk_traffic(path, n_subs, n_topics):
     """HBM bytes per k_walk launch (FETCH_SIZE x2 + WRITE_SIZE) from a committed rocprofv3 PMC
-    summary of the same configuration, if present."""
+    summary of the same configuration (subscriptions, topics, edge-table load), if present."""
     try:
         with open(path) as f:
             e = json.load(f).get("walk", {}).get(str(n_subs))
-        if e is None or int(e["topics"]) != n_topics:
+        if e is None or int(e["topics"]) != n_topics or int(e.get("edge_load", 2)) != engine_option(13, 4):
             return None
         return float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError, TypeError):
