@@ -246,6 +246,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_WALK_LISTS: walk_lists_ = v != 0; return true;
     case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
     case MQ_OPT_MERGE_DEDUP: dedup_ = (uint32_t)v; return true;
+    case MQ_OPT_SET_GRID: set_grid_ = (uint32_t)v; return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     default: return false;
   }
@@ -1008,11 +1009,13 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     launch_dedup(dd, s);
     prof.end("dedup", s);
     hip_check(hipGetLastError(), "k_dedup");
-    if (prof.on()) {
+    sb_.n_sets = 0;
+    if (prof.on() || set_grid_) {
       unsigned long long ns = 0;
       hip_check(hipMemcpyAsync(&ns, dd_nsets_.p, sizeof(ns), hipMemcpyDeviceToHost, s), "D2H");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-      prof.count("dedup_sets", ns);
+      if (prof.on()) prof.count("dedup_sets", ns);
+      sb_.n_sets = ns;
     }
   }
 
@@ -1140,7 +1143,11 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
       prof.begin(s);
       // persistent: the waves stride over the representative list (its length is on the device)
-      launch_merge(a, true, false, merge_wpe, merge_blocks_ ? merge_blocks_ : n_cus_ * 8, s);
+      // MQ_OPT_SET_GRID 1: a wavefront per set (the dispatcher balances heavy sets); else
+      // persistent waves striding over the list
+      const uint32_t set_blocks = set_grid_ ? std::max<uint32_t>(1, (uint32_t)((sb_.n_sets + 3) / 4))
+                                            : (merge_blocks_ ? merge_blocks_ : n_cus_ * 8);
+      launch_merge(a, true, false, merge_wpe, set_blocks, s);
       prof.end("merge_sets", s);
       hip_check(hipGetLastError(), "k_merge<spans> (sets)");
       hip_check(hipMemcpyAsync(h_pc, a.spcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),

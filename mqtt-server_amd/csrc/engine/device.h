@@ -281,6 +281,7 @@ class Device {
     bool lists = true;             // the walk counted the lists (else k_desc did, into sp_tc_)
     bool fused = false;            // k_desc's work is done by k_merge (index not sharded)
     bool dedup = false;            // merge-set dedup ran (dd_rep_ holds the representatives)
+    uint64_t n_sets = 0;           // their number, when read back (profiling, MQ_OPT_SET_GRID)
     const uint32_t* gathers = nullptr;
     uint32_t gstride = 0;
   } sb_;
@@ -302,6 +303,7 @@ class Device {
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
   bool fuse_desc_ = false;       // span format: k_merge does k_desc's work (MQ_OPT_FUSE_DESC)
   uint32_t dedup_ = 1;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
+  uint32_t set_grid_ = 1;        // MQ_OPT_SET_GRID (10M: set pass 1.18 -> 1.05 ms against persistent waves)
   DevBuf dd_sig_, dd_cnt_, dd_list_, dd_mrow_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_, dd_rlist_;
   DevBuf dd_sets_, dd_spatches_, dd_spcount_;  // phase 1 of the dedup merge: SetInfo, set pool
   DevBuf dd_wlist_, dd_nwave_;                 // k_finish: topics left for k_merge's topic pass
