@@ -444,8 +444,8 @@ int mq_device_check(mq_index* idx);
 #define MQ_OPT_MERGE_DEDUP 12     /* span format: 1 finds topics with the same merge gathers (counter
                                      "merge_sets" under MQ_PROF_TIMES) */
 #define MQ_OPT_FUSE_DESC 11       /* span format, index not sharded: 1 has k_merge do k_desc's work (slower; off) */
-#define MQ_OPT_SET_GRID 14        /* merge-set dedup: 1 (default): a wavefront per set; 0: persistent set pass
-                                     (the host reads the set count) */
+#define MQ_OPT_SET_GRID 14        /* merge-set dedup: 1 (default): a wavefront per set (the host reads the set
+                                     count); 0: persistent waves striding the set list */
 #define MQ_OPT_EDGE_LOAD 13       /* edge table: at most 1/v of its slots used (2, 4 = default, 8: sparser means
                                      shorter probe chains for the walk, more memory; a table of 2^30 slots or
                                      more keeps 1/2); applies from the next growth */

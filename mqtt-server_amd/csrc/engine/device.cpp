@@ -989,10 +989,10 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     grow(dd_slot_, (size_t)n * sizeof(uint32_t));
     grow(dd_rep_, (size_t)n * sizeof(uint32_t));
     grow(dd_rlist_, (size_t)n * sizeof(uint32_t));
-    if (!dd_nsets_.p) dd_nsets_.ensure(sizeof(unsigned long long));
+    if (!dd_nsets_.p) dd_nsets_.ensure(2 * sizeof(unsigned long long));
     hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
 
-    hip_check(hipMemsetAsync(dd_nsets_.p, 0, sizeof(unsigned long long), s), "memset");
+    hip_check(hipMemsetAsync(dd_nsets_.p, 0, 2 * sizeof(unsigned long long), s), "memset");
     DedupArgs dd;
     dd.n = n;
     dd.msig = dd_sig_.as<uint64_t>();
@@ -1004,6 +1004,8 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     dd.tslot = dd_slot_.as<uint32_t>();
     dd.rep = dd_rep_.as<uint32_t>();
     dd.n_sets = dd_nsets_.as<unsigned long long>();
+    dd.tc = sp_tc_.as<TopicCount>();
+    dd.heavy = kSetHeavy;
     dd.rep_list = dd_rlist_.as<uint32_t>();
     prof.begin(s);
     launch_dedup(dd, s);
@@ -1011,9 +1013,10 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     hip_check(hipGetLastError(), "k_dedup");
     sb_.n_sets = 0;
     if (prof.on() || set_grid_) {
-      unsigned long long ns = 0;
-      hip_check(hipMemcpyAsync(&ns, dd_nsets_.p, sizeof(ns), hipMemcpyDeviceToHost, s), "D2H");
+      unsigned long long two[2] = {0, 0};
+      hip_check(hipMemcpyAsync(two, dd_nsets_.p, sizeof(two), hipMemcpyDeviceToHost, s), "D2H");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      const unsigned long long ns = two[0] + two[1];
       if (prof.on()) prof.count("dedup_sets", ns);
       sb_.n_sets = ns;
     }

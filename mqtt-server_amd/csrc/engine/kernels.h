@@ -169,11 +169,12 @@ struct EmitArgs {
   uint64_t srcap;
   uint32_t set_ref;                    // dd_phase 2: a deduped topic references its set's patches
                                        //   (device results) instead of copying them
-  const uint32_t* rep_list;            // dd_phase 1: the set representatives (k_dedup_rep)
-  const unsigned long long* n_reps;    //   and their number, in device memory
+  const uint32_t* rep_list;            // dd_phase 1: the set representatives (k_dedup_rep,
+  const unsigned long long* n_reps;    //   DedupArgs layout) and their two counts, in device memory
   const uint32_t* wave_list;           // dd_phase 2 after k_finish: the topics that still need a
   const unsigned long long* n_wave;    //   wavefront (k_finish wrote the others' results)
 };
+constexpr uint32_t kSetHeavy = 1024;  // a merge set with this many may-merge records goes first
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
 constexpr uint32_t kTopicSetPatches = 1;  // TopicSpansDev.flags: patches shared with a merge set
                                           //   (MQ_TOPIC_SET_PATCHES)
@@ -231,8 +232,11 @@ struct DedupArgs {
   uint64_t table_mask;
   uint32_t* tslot;           // per topic: its table slot (kNone: not deduped)
   uint32_t* rep;             // per topic: its representative
-  unsigned long long* n_sets;  // topics with merge gathers that are their own representative
-  uint32_t* rep_list;          // those topics (n_sets of them, in no particular order)
+  unsigned long long* n_sets;  // [2]: representatives listed from the front (heavy) and the back
+  uint32_t* rep_list;          // those topics: heavy sets at [0, n_sets[0]), the others at
+                               //   [n - n_sets[1], n) (heavy first: the set pass's tail is short)
+  const TopicCount* tc;        // per-topic counts (k_desc): a set is heavy with >= heavy records
+  uint32_t heavy;
 };
 void launch_dedup(const DedupArgs& a, hipStream_t s);
 

@@ -908,8 +908,8 @@ __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
 // k_dedup_rep also lists the topics that resolve a merge set (rep_list, n_sets of them): the
 // merge's set pass walks that list instead of every topic.
 __global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
-  __shared__ uint32_t wcnt[16];
-  __shared__ unsigned long long bbase;
+  __shared__ uint32_t wcnt[2][16];
+  __shared__ unsigned long long bbase[2];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63, wv = wave_id();
   const bool act = t < a.n;
   const uint32_t sl = act ? a.tslot[t] : kNone;
@@ -932,22 +932,28 @@ __global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
   }
   if (act) a.rep[t] = r;
   const bool own = r == t && sl != kNone;
-  const uint64_t b = __ballot(own);
-  // one atomic per workgroup on the list's counter (one per wavefront serialised ~16k atomics on
-  // one address per 1M topics)
-  if (lane == 0) wcnt[wv] = (uint32_t)__popcll(b);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (uint32_t w = 0; w < blockDim.x / 64; w++) {
-      const uint32_t c = wcnt[w];
-      wcnt[w] = tot;
-      tot += c;
-    }
-    bbase = tot ? atomicAdd(a.n_sets, (unsigned long long)tot) : 0ull;
+  const bool heavy = own && a.tc[t].merge >= a.heavy;
+  const uint64_t bh = __ballot(heavy), bl = __ballot(own && !heavy);
+  // one atomic per workgroup and list end on the counters (one per wavefront serialised ~16k
+  // atomics on one address per 1M topics)
+  if (lane == 0) {
+    wcnt[0][wv] = (uint32_t)__popcll(bh);
+    wcnt[1][wv] = (uint32_t)__popcll(bl);
   }
   __syncthreads();
-  if (own) a.rep_list[bbase + wcnt[wv] + prefix_before(b)] = t;
+  if (threadIdx.x < 2) {
+    const uint32_t e = threadIdx.x;
+    uint32_t tot = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; w++) {
+      const uint32_t c = wcnt[e][w];
+      wcnt[e][w] = tot;
+      tot += c;
+    }
+    bbase[e] = tot ? atomicAdd(a.n_sets + e, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  if (heavy) a.rep_list[bbase[0] + wcnt[0][wv] + prefix_before(bh)] = t;
+  else if (own) a.rep_list[a.n - 1 - (bbase[1] + wcnt[1][wv] + prefix_before(bl))] = t;
 }
 
 __global__ __launch_bounds__(256) void k_finish(FinishArgs a) {
@@ -1173,9 +1179,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // pass after k_finish: over the topics k_finish left)
   const uint32_t* __restrict__ tlist = !(SPANS && a.rep) ? nullptr
                                      : SET ? a.rep_list : a.wave_list;
-  const uint32_t i_end = tlist ? (uint32_t)*(SET ? a.n_reps : a.n_wave) : a.t1;
+  const uint32_t n_front = SET && tlist ? (uint32_t)a.n_reps[0] : 0u;  // heavy sets, then the back
+  const uint32_t i_end = tlist ? (SET ? n_front + (uint32_t)a.n_reps[1] : (uint32_t)*a.n_wave) : a.t1;
   for (uint32_t i = a.t0 + blockIdx.x * 4 + wv; i < i_end; i += gridDim.x * 4) {
-  const uint32_t t = tlist ? tlist[i] : i;
+  const uint32_t t = !tlist ? i : (SET && i >= n_front) ? tlist[a.t1 - 1 - (i - n_front)] : tlist[i];
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint64_t rb = o0.rows - a.base.rows;
   const uint64_t ib = o0.inl - a.base.inl;
