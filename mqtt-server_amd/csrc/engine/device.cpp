@@ -1004,7 +1004,8 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     dd.tslot = dd_slot_.as<uint32_t>();
     dd.rep = dd_rep_.as<uint32_t>();
     dd.n_sets = dd_nsets_.as<unsigned long long>();
-    dd.tc = sp_tc_.as<TopicCount>();
+    dd.tc = da.tc_out;
+    dd.off = offs_.as<TopicOff>();
     dd.heavy = kSetHeavy;
     dd.rep_list = dd_rlist_.as<uint32_t>();
     prof.begin(s);

@@ -235,7 +235,8 @@ struct DedupArgs {
   unsigned long long* n_sets;  // [2]: representatives listed from the front (heavy) and the back
   uint32_t* rep_list;          // those topics: heavy sets at [0, n_sets[0]), the others at
                                //   [n - n_sets[1], n) (heavy first: the set pass's tail is short)
-  const TopicCount* tc;        // per-topic counts (k_desc): a set is heavy with >= heavy records
+  const TopicCount* tc;        // per-topic counts (k_desc; null: the offsets' differences): a set
+  const struct TopicOff* off;  //   is heavy with >= heavy may-merge records
   uint32_t heavy;
 };
 void launch_dedup(const DedupArgs& a, hipStream_t s);

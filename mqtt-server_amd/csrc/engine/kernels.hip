@@ -932,7 +932,7 @@ __global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
   }
   if (act) a.rep[t] = r;
   const bool own = r == t && sl != kNone;
-  const bool heavy = own && a.tc[t].merge >= a.heavy;
+  const bool heavy = own && (a.tc ? a.tc[t].merge : (uint32_t)(a.off[t + 1].merge - a.off[t].merge)) >= a.heavy;
   const uint64_t bh = __ballot(heavy), bl = __ballot(own && !heavy);
   // one atomic per workgroup and list end on the counters (one per wavefront serialised ~16k
   // atomics on one address per 1M topics)
