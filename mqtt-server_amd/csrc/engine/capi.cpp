@@ -84,10 +84,10 @@ int fail(int code, const std::string& msg) {
 
 // Runs f under the handle's lock; an update (writes the host image) first waits for the host
 // span results that pin it to be freed.
-// pins: the call creates a host span result. Writers are preferred, boundedly: while an update
-// waits for the views to drain, a call that would pin the image again waits for it (up to 2 ms,
-// since the calling thread may itself hold a result) — otherwise readers that keep overlapping
-// would starve the update forever.
+// pins: the call creates a host span result. Writers are preferred: while an update waits for
+// the views to drain, a call that would pin the image again waits until the update has run —
+// otherwise readers whose results keep overlapping starve the update forever. The wait is
+// bounded (100 ms) in case the calling thread itself holds a result the update waits for.
 template <class F>
 int guarded(mq_index* idx, F&& f, bool update = false, bool pins = false) {
   if (!idx) return fail(MQ_EINVAL, "null index");
@@ -99,7 +99,7 @@ int guarded(mq_index* idx, F&& f, bool update = false, bool pins = false) {
       L.cv.wait(lk, [&] { return L.views == 0; });
       L.writers--;
     } else if (pins && L.writers) {
-      L.cv.wait_for(lk, std::chrono::milliseconds(2), [&] { return L.writers == 0; });
+      L.cv.wait_for(lk, std::chrono::milliseconds(100), [&] { return L.writers == 0; });
     }
     const int rc = f();
     if (update) {

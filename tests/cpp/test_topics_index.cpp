@@ -429,25 +429,33 @@ static void TestPublishViewBatcher() {
   }
 }
 
+// progress on stderr: a test that does not return is named by the last line
+#define RUN(f)                             \
+  do {                                     \
+    std::fprintf(stderr, "%s\n", #f);      \
+    std::fflush(stderr);                   \
+    f();                                   \
+  } while (0)
+
 int main() {
   try {
-    TestSubscribe();
-    TestUnsubscribe();
-    TestRetainMessage();
-    TestScanSubscribers();
-    TestScanSubscribersShared();
-    TestScanSubscribersSharedSelected();
-    TestSubscribersFind();
-    TestMessagesPattern();
-    TestInline();
-    TestPublishToSubscribersIdentifiers();
-    TestMergeSharedSelected();
-    TestPublishBatcher();
-    TestChurnRecyclesIds();
-    TestConcurrentReadersAndUpdates();
-    TestLoadSubscriptions();
-    TestRetainedAddAfterExpiry();
-    TestPublishViewBatcher();
+    RUN(TestSubscribe);
+    RUN(TestUnsubscribe);
+    RUN(TestRetainMessage);
+    RUN(TestScanSubscribers);
+    RUN(TestScanSubscribersShared);
+    RUN(TestScanSubscribersSharedSelected);
+    RUN(TestSubscribersFind);
+    RUN(TestMessagesPattern);
+    RUN(TestInline);
+    RUN(TestPublishToSubscribersIdentifiers);
+    RUN(TestMergeSharedSelected);
+    RUN(TestPublishBatcher);
+    RUN(TestChurnRecyclesIds);
+    RUN(TestConcurrentReadersAndUpdates);
+    RUN(TestLoadSubscriptions);
+    RUN(TestRetainedAddAfterExpiry);
+    RUN(TestPublishViewBatcher);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 2;
