@@ -3,7 +3,6 @@
 // and HIP failures into negative errno codes with a thread-local message.
 #include <hip/hip_runtime.h>
 
-#include <chrono>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -28,7 +27,6 @@ struct IndexLock {
   std::mutex mu;
   std::condition_variable cv;
   uint64_t views = 0;
-  uint32_t writers = 0;  // updates waiting for the views to be freed
 };
 
 struct mq_index {
@@ -84,29 +82,14 @@ int fail(int code, const std::string& msg) {
 
 // Runs f under the handle's lock; an update (writes the host image) first waits for the host
 // span results that pin it to be freed.
-// pins: the call creates a host span result. Writers are preferred: while an update waits for
-// the views to drain, a call that would pin the image again waits until the update has run —
-// otherwise readers whose results keep overlapping starve the update forever. The wait is
-// bounded (100 ms) in case the calling thread itself holds a result the update waits for.
 template <class F>
-int guarded(mq_index* idx, F&& f, bool update = false, bool pins = false) {
+int guarded(mq_index* idx, F&& f, bool update = false) {
   if (!idx) return fail(MQ_EINVAL, "null index");
   try {
     IndexLock& L = *idx->lk;
     std::unique_lock<std::mutex> lk(L.mu);
-    if (update) {
-      L.writers++;
-      L.cv.wait(lk, [&] { return L.views == 0; });
-      L.writers--;
-    } else if (pins && L.writers) {
-      L.cv.wait_for(lk, std::chrono::milliseconds(100), [&] { return L.writers == 0; });
-    }
-    const int rc = f();
-    if (update) {
-      lk.unlock();
-      L.cv.notify_all();  // readers waiting for this update
-    }
-    return rc;
+    if (update) L.cv.wait(lk, [&] { return L.views == 0; });
+    return f();
   } catch (const HipError& e) {
     return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
   } catch (const std::bad_alloc&) {
@@ -290,7 +273,7 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
     mq_span_result dev_out;
     d.match_spans(*idx->ix, dtb, dto, n, nullptr, &h->data, &dev_out);
     return publish_host_spans(idx, std::move(h), dev_out, out);
-  }, false, true);
+  });
 }
 
 int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, mq_span_result** out) {
@@ -300,7 +283,7 @@ int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_f
     mq_span_result dev_out;
     idx->device().spans_end(*idx->ix, foreign, n_foreign, nullptr, &h->data, &dev_out);
     return publish_host_spans(idx, std::move(h), dev_out, out);
-  }, false, true);
+  });
 }
 
 int mq_match_spans_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
