@@ -314,8 +314,10 @@ typedef struct mq_span_result {
 /* Span-format Subscribers for a batch of host topics (as mq_match_batch). The result's arrays
  * are host copies; its pools point at the index's host image, which the result pins: updates
  * issued while it is held wait until mq_result_free (as the reference's writers wait for the
- * per-node read locks a gather holds, topics.go:270-277), so free it before updating from the
- * same thread. */
+ * per-node read locks a gather holds, topics.go:270-277). Writers are preferred, as with Go's
+ * sync.RWMutex: while an update waits, new mq_match_spans calls wait for it, so overlapping
+ * readers cannot starve updates. Free a result before updating or calling mq_match_spans again
+ * from the same thread (a second read while an update waits would wait for itself). */
 int mq_match_spans(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets, uint32_t n,
                    mq_span_result** out);
 /* Device-resident span format (inputs in HBM, enqueued on hip_stream, as mq_match_device). All
@@ -449,6 +451,8 @@ int mq_device_check(mq_index* idx);
 #define MQ_OPT_EDGE_LOAD 13       /* edge table: at most 1/v of its slots used (2, 4 = default, 8: sparser means
                                      shorter probe chains for the walk, more memory; a table of 2^30 slots or
                                      more keeps 1/2); applies from the next growth */
+#define MQ_OPT_WALK_GROUP 15       /* the match walk: 16 (default), 8 or 4 lanes per topic (level-synchronous
+                                     frontier walk); 0: thread per topic (stackless DFS) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. enable: 0 off,

@@ -20,13 +20,24 @@
 
 using namespace mq;
 
-// The handle's lock. `views` counts host span results that pin the host image (their pools
-// point into it); updates wait until they are freed. Results hold a reference, so freeing one
-// after mq_index_destroy is safe.
+// The handle's lock, a writer-preferring read/write protocol in the manner of Go's
+// sync.RWMutex (the reference's root lock, topics.go:402): `mu` serialises the handle's work
+// (updates, and the GPU round trip of a match); `views` counts host span results alive, which
+// pin the host image (their pools point into it) until mq_result_free. An update announces
+// itself (`writers`), takes `mu`, and waits for the views to drain; a call that would take a new
+// view first waits while any update is announced, with no time bound, so a steady stream of
+// overlapping readers cannot starve updates. `views` / `writers` live under their own mutex
+// `vmu`, which is never held across GPU work, so freeing a result never waits for a match in
+// flight. As with a Go RWMutex read lock, a thread must free its span results before it takes a
+// new one or updates the index (a reader that holds a view and asks for another while an update
+// waits would wait for itself). Results hold a reference, so freeing one after
+// mq_index_destroy is safe.
 struct IndexLock {
   std::mutex mu;
-  std::condition_variable cv;
+  std::mutex vmu;
+  std::condition_variable vcv;
   uint64_t views = 0;
+  uint64_t writers = 0;
 };
 
 struct mq_index {
@@ -80,15 +91,43 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
-// Runs f under the handle's lock; an update (writes the host image) first waits for the host
-// span results that pin it to be freed.
+// What a guarded call does to the host image (IndexLock).
+enum class Access { kRead, kUpdate, kPin };
+
+// Runs f under the handle's lock. kUpdate (writes the host image): announce, take the lock, wait
+// for the host span results that pin the image to be freed. kPin (publishes a host span result):
+// wait until no update is announced, then take the lock.
 template <class F>
-int guarded(mq_index* idx, F&& f, bool update = false) {
+int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
   if (!idx) return fail(MQ_EINVAL, "null index");
+  IndexLock& L = *idx->lk;
+  struct Writer {  // the announcement, withdrawn however the call ends
+    IndexLock* L = nullptr;
+    ~Writer() {
+      if (!L) return;
+      {
+        std::lock_guard<std::mutex> g(L->vmu);
+        L->writers--;
+      }
+      L->vcv.notify_all();
+    }
+  } writer;
   try {
-    IndexLock& L = *idx->lk;
+    if (access == Access::kUpdate) {
+      {
+        std::lock_guard<std::mutex> g(L.vmu);
+        L.writers++;
+      }
+      writer.L = &L;
+    } else if (access == Access::kPin) {
+      std::unique_lock<std::mutex> g(L.vmu);
+      L.vcv.wait(g, [&] { return L.writers == 0; });
+    }
     std::unique_lock<std::mutex> lk(L.mu);
-    if (update) L.cv.wait(lk, [&] { return L.views == 0; });
+    if (access == Access::kUpdate) {
+      std::unique_lock<std::mutex> g(L.vmu);
+      L.vcv.wait(g, [&] { return L.views == 0; });
+    }
     return f();
   } catch (const HipError& e) {
     return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
@@ -134,12 +173,12 @@ int mq_subscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t clie
   if (qos > 2) return fail(MQ_EINVAL, "qos > 2");
   return guarded(idx, [&] {
     return idx->ix->subscribe(std::string_view(filter, flen), client_id, filter_id, qos, flags, identifier);
-  }, true);
+  }, Access::kUpdate);
 }
 
 int mq_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t client_id) {
   if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
-  return guarded(idx, [&] { return idx->ix->unsubscribe(std::string_view(filter, flen), client_id); }, true);
+  return guarded(idx, [&] { return idx->ix->unsubscribe(std::string_view(filter, flen), client_id); }, Access::kUpdate);
 }
 
 int mq_inline_subscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier,
@@ -147,12 +186,12 @@ int mq_inline_subscribe(mq_index* idx, const char* filter, uint32_t flen, int32_
   if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
   return guarded(idx, [&] {
     return idx->ix->inline_subscribe(std::string_view(filter, flen), identifier, filter_id);
-  }, true);
+  }, Access::kUpdate);
 }
 
 int mq_inline_unsubscribe(mq_index* idx, const char* filter, uint32_t flen, int32_t identifier) {
   if (bad_str(filter, flen)) return fail(MQ_EINVAL, "null filter");
-  return guarded(idx, [&] { return idx->ix->inline_unsubscribe(std::string_view(filter, flen), identifier); }, true);
+  return guarded(idx, [&] { return idx->ix->inline_unsubscribe(std::string_view(filter, flen), identifier); }, Access::kUpdate);
 }
 
 int mq_retain_message(mq_index* idx, const char* topic, uint32_t tlen, uint64_t handle,
@@ -162,12 +201,12 @@ int mq_retain_message(mq_index* idx, const char* topic, uint32_t tlen, uint64_t 
     int64_t r = idx->ix->retain_message(std::string_view(topic, tlen), handle, payload_len, retain != 0);
     if (out) *out = r;
     return 0;
-  }, true);
+  }, Access::kUpdate);
 }
 
 int mq_retained_delete(mq_index* idx, const char* topic, uint32_t tlen) {
   if (bad_str(topic, tlen)) return fail(MQ_EINVAL, "null topic");
-  return guarded(idx, [&] { return idx->ix->retained_delete(std::string_view(topic, tlen)); }, true);
+  return guarded(idx, [&] { return idx->ix->retained_delete(std::string_view(topic, tlen)); }, Access::kUpdate);
 }
 
 int mq_retained_set(mq_index* idx, const char* topic, uint32_t tlen, uint64_t handle, uint32_t payload_len,
@@ -175,7 +214,7 @@ int mq_retained_set(mq_index* idx, const char* topic, uint32_t tlen, uint64_t ha
   if (bad_str(topic, tlen)) return fail(MQ_EINVAL, "null topic");
   return guarded(idx, [&] {
     return idx->ix->retained_set(std::string_view(topic, tlen), handle, payload_len, retain != 0);
-  }, true);
+  }, Access::kUpdate);
 }
 
 uint64_t mq_retained_len(const mq_index* idx) {
@@ -194,7 +233,7 @@ int mq_subscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs,
   return guarded(idx, [&] {
     idx->ix->subscribe_bulk(bytes, offs, client_ids, filter_ids, qos, flags, identifiers, n, out_new);
     return 0;
-  }, true);
+  }, Access::kUpdate);
 }
 
 int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint64_t* handles,
@@ -203,7 +242,7 @@ int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, co
   return guarded(idx, [&] {
     idx->ix->retain_bulk(bytes, offs, handles, n);
     return 0;
-  }, true);
+  }, Access::kUpdate);
 }
 
 int mq_match_batch(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_match_result** out) {
@@ -253,7 +292,10 @@ int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_sp
   r.sub_pool_len = idx->ix->subs.m.size();
   r.shared_pool_len = idx->ix->shr.m.size();
   h->lk = idx->lk;
-  idx->lk->views++;  // the pools stay put until mq_result_free
+  {
+    std::lock_guard<std::mutex> g(idx->lk->vmu);
+    idx->lk->views++;  // the pools stay put until mq_result_free
+  }
   *out = &h->pub;
   std::lock_guard<std::mutex> lk(g_res_mu);
   g_results[&h->pub] = 4;
@@ -273,7 +315,7 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
     mq_span_result dev_out;
     d.match_spans(*idx->ix, dtb, dto, n, nullptr, &h->data, &dev_out);
     return publish_host_spans(idx, std::move(h), dev_out, out);
-  });
+  }, Access::kPin);
 }
 
 int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, mq_span_result** out) {
@@ -283,7 +325,7 @@ int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_f
     mq_span_result dev_out;
     idx->device().spans_end(*idx->ix, foreign, n_foreign, nullptr, &h->data, &dev_out);
     return publish_host_spans(idx, std::move(h), dev_out, out);
-  });
+  }, Access::kPin);
 }
 
 int mq_match_spans_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
@@ -472,10 +514,10 @@ void mq_result_free(void* r) {
     std::shared_ptr<IndexLock> lk = h->lk;
     delete h;
     {
-      std::lock_guard<std::mutex> g(lk->mu);
+      std::lock_guard<std::mutex> g(lk->vmu);
       lk->views--;
     }
-    lk->cv.notify_all();
+    lk->vcv.notify_all();
   }
 }
 
@@ -530,7 +572,7 @@ int mq_device_check(mq_index* idx) {
 }
 
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
-  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_SET_GRID) return fail(MQ_EINVAL, "unknown option");
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_WALK_GROUP) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
     if (option == MQ_OPT_EDGE_LOAD) {  // the host image's option
       if (value != 2 && value != 4 && value != 8) throw std::invalid_argument("MQ_OPT_EDGE_LOAD: 2, 4 or 8");

@@ -247,6 +247,10 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
     case MQ_OPT_MERGE_DEDUP: dedup_ = (uint32_t)v; return true;
     case MQ_OPT_SET_GRID: set_grid_ = (uint32_t)v; return true;
+    case MQ_OPT_WALK_GROUP:
+      if (v != 0 && v != 4 && v != 8 && v != 16) return false;
+      walk_group_ = (uint32_t)v;
+      return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     default: return false;
   }
@@ -855,12 +859,23 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   grow(bpre_, (size_t)(nb + 1) * sizeof(TopicOff));
   grow(gslots_, (size_t)n * kGatherCap * sizeof(uint32_t));
   grow(ovf_, sizeof(uint32_t));
-  pinned(sizeof(TopicOff) + sizeof(uint32_t));
+  pinned(sizeof(TopicOff) + 2 * sizeof(uint32_t));
   TopicOff* h_tot = static_cast<TopicOff*>(h_pin_);
   uint32_t* h_ovf = reinterpret_cast<uint32_t*>(h_tot + 1);
   hip_check(hipMemsetAsync(ovf_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
+  const bool front = walk_group_ != 0;
+  if (front) {
+    grow(fb_list_, (size_t)n * sizeof(uint32_t));
+    grow(fb_cnt_, sizeof(uint32_t));
+    hip_check(hipMemsetAsync(fb_cnt_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(fb)");
+  }
   prof.begin(s);
-  launch_walk(false, lists, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(), ovf_.as<uint32_t>(), s);
+  if (front)
+    launch_walk_front(walk_group_, lists, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(),
+                      ovf_.as<uint32_t>(), fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, s);
+  else
+    launch_walk(false, lists, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(),
+                ovf_.as<uint32_t>(), s);
   prof.end("walk", s);
   hip_check(hipGetLastError(), "k_walk<count>");
   prof.begin(s);
@@ -869,8 +884,11 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   hip_check(hipGetLastError(), "k_scan");
   hip_check(hipMemcpyAsync(h_tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H totals");
   hip_check(hipMemcpyAsync(h_ovf, ovf_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H overflow");
+  if (front && prof.on())
+    hip_check(hipMemcpyAsync(h_ovf + 1, fb_cnt_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H fallback");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   const TopicOff tot = *h_tot;
+  if (front && prof.on()) prof.count("walk_fallback", h_ovf[1]);
   *gathers = gslots_.as<uint32_t>();
   *gstride = kGatherCap;
   if (*h_ovf) {  // a topic with more gathers than its count-pass slots: write all lists compactly
@@ -962,7 +980,10 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   da.mlist = nullptr;
   da.mrow = nullptr;
   da.mpair = nullptr;
-  sb_.dedup = dedup_ != 0 && !ix.sharded() && !sb_.fused;
+  da.mrank = nullptr;
+  // merge-set dedup (on a sharded index too: a set is then also the other shards' entries,
+  // which spans_end knows after the exchange)
+  sb_.dedup = dedup_ != 0 && !sb_.fused;
   if (sb_.dedup) {
     grow(dd_sig_, (size_t)n * sizeof(uint64_t));
     grow(dd_cnt_, (size_t)n * sizeof(uint32_t));
@@ -974,61 +995,24 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     da.mcount = dd_cnt_.as<uint32_t>();
     da.mlist = dd_list_.as<uint32_t>();
     da.mrow = dd_mrow_.as<uint32_t>();
+    if (ix.sharded()) {
+      grow(dd_mrank_, (size_t)n * kPairMax * sizeof(uint64_t));
+      da.mrank = dd_mrank_.as<uint64_t>();
+    }
   }
+  sb_.tc = da.tc_out;
   if (!sb_.fused) {
     prof.begin(s);
     launch_desc(da, true, s);
     prof.end("desc", s);
     hip_check(hipGetLastError(), "k_desc<spans>");
   }
-  if (sb_.dedup) {  // merge-set dedup: each topic's representative (DedupArgs)
-    uint64_t slots = 1024;
-    while (slots < 2ull * n) slots <<= 1;
-    grow(dd_keys_, slots * sizeof(unsigned long long));
-    grow(dd_vals_, slots * sizeof(uint32_t));
-    grow(dd_slot_, (size_t)n * sizeof(uint32_t));
-    grow(dd_rep_, (size_t)n * sizeof(uint32_t));
-    grow(dd_rlist_, (size_t)n * sizeof(uint32_t));
-    if (!dd_nsets_.p) dd_nsets_.ensure(2 * sizeof(unsigned long long));
-    hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
-
-    hip_check(hipMemsetAsync(dd_nsets_.p, 0, 2 * sizeof(unsigned long long), s), "memset");
-    DedupArgs dd;
-    dd.n = n;
-    dd.msig = dd_sig_.as<uint64_t>();
-    dd.mcount = dd_cnt_.as<uint32_t>();
-    dd.mlist = dd_list_.as<uint32_t>();
-    dd.keys = dd_keys_.as<unsigned long long>();
-    dd.vals = dd_vals_.as<uint32_t>();
-    dd.table_mask = slots - 1;
-    dd.tslot = dd_slot_.as<uint32_t>();
-    dd.rep = dd_rep_.as<uint32_t>();
-    dd.n_sets = dd_nsets_.as<unsigned long long>();
-    dd.tc = da.tc_out;
-    dd.off = offs_.as<TopicOff>();
-    dd.heavy = kSetHeavy;
-    dd.rep_list = dd_rlist_.as<uint32_t>();
-    prof.begin(s);
-    launch_dedup(dd, s);
-    prof.end("dedup", s);
-    hip_check(hipGetLastError(), "k_dedup");
-    sb_.n_sets = 0;
-    if (prof.on() || set_grid_) {
-      unsigned long long two[2] = {0, 0};
-      hip_check(hipMemcpyAsync(two, dd_nsets_.p, sizeof(two), hipMemcpyDeviceToHost, s), "D2H");
-      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-      const unsigned long long ns = two[0] + two[1];
-      if (prof.on()) prof.count("dedup_sets", ns);
-      sb_.n_sets = ns;
-    }
-  }
-
   if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
     grow(x_cnt_, (size_t)n * sizeof(uint32_t));
     prof.begin(s);
-    launch_xlist(true, di, n, offs_.as<TopicOff>(), desc_[0].as<GDesc>(), counts_.as<TopicCount>(), nullptr, nullptr,
+    launch_xlist(true, di, n, offs_.as<TopicOff>(), gathers, gstride, counts_.as<TopicCount>(), nullptr, nullptr,
                  nullptr, s);
     launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
     TopicOff* h_tot = static_cast<TopicOff*>(h_pin_);
@@ -1036,7 +1020,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     const uint64_t n_ents = h_tot->g;
     grow(x_ents_, std::max<uint64_t>(n_ents, 1) * sizeof(XEnt));
-    launch_xlist(false, di, n, offs_.as<TopicOff>(), desc_[0].as<GDesc>(), nullptr, x_off_.as<TopicOff>(),
+    launch_xlist(false, di, n, offs_.as<TopicOff>(), gathers, gstride, nullptr, x_off_.as<TopicOff>(),
                  x_ents_.as<XEnt>(), x_cnt_.as<uint32_t>(), s);
     prof.end("xlist", s);
     hip_check(hipGetLastError(), "k_xlist");
@@ -1087,6 +1071,72 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");  // h_src is on the stack
     a.xsrc = x_src_.as<XSrc>();
   }
+  if (sb_.dedup) {  // merge-set dedup: each topic's representative (DedupArgs)
+    uint64_t slots = 1024;
+    while (slots < 2ull * n) slots <<= 1;
+    grow(dd_keys_, slots * sizeof(unsigned long long));
+    grow(dd_vals_, slots * sizeof(uint32_t));
+    grow(dd_slot_, (size_t)n * sizeof(uint32_t));
+    grow(dd_rep_, (size_t)n * sizeof(uint32_t));
+    grow(dd_rlist_, (size_t)n * sizeof(uint32_t));
+    if (!dd_nsets_.p) dd_nsets_.ensure(2 * sizeof(unsigned long long));
+    hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
+
+    hip_check(hipMemsetAsync(dd_nsets_.p, 0, 2 * sizeof(unsigned long long), s), "memset");
+    DedupArgs dd;
+    dd.n = n;
+    dd.msig = dd_sig_.as<uint64_t>();
+    dd.mcount = dd_cnt_.as<uint32_t>();
+    dd.mlist = dd_list_.as<uint32_t>();
+    dd.keys = dd_keys_.as<unsigned long long>();
+    dd.vals = dd_vals_.as<uint32_t>();
+    dd.table_mask = slots - 1;
+    dd.tslot = dd_slot_.as<uint32_t>();
+    dd.rep = dd_rep_.as<uint32_t>();
+    dd.n_sets = dd_nsets_.as<unsigned long long>();
+    dd.tc = sb_.tc;
+    dd.off = offs_.as<TopicOff>();
+    dd.heavy = kSetHeavy;
+    dd.rep_list = dd_rlist_.as<uint32_t>();
+    dd.fcount = nullptr;
+    dd.n_xf = nf;
+    dd.xsrc = a.xsrc;
+    if (nf) {  // the other shards' entries join each topic's signature
+      grow(dd_fcnt_, (size_t)n * sizeof(uint32_t));
+      XSigArgs xa;
+      xa.ix = di;
+      xa.n = n;
+      xa.n_xf = nf;
+      xa.xsrc = a.xsrc;
+      xa.msig = dd_sig_.as<uint64_t>();
+      xa.mcount = dd_cnt_.as<uint32_t>();
+      xa.fcount = dd_fcnt_.as<uint32_t>();
+      xa.off = offs_.as<TopicOff>();
+      xa.gathers = sb_.gathers;
+      xa.gather_stride = sb_.gstride;
+      xa.desc = desc_[0].as<GDesc>();
+      prof.begin(s);
+      launch_xsig(xa, s);
+      prof.end("xsig", s);
+      hip_check(hipGetLastError(), "k_xsig");
+      dd.fcount = xa.fcount;
+    }
+    prof.begin(s);
+    launch_dedup(dd, s);
+    prof.end("dedup", s);
+    hip_check(hipGetLastError(), "k_dedup");
+    sb_.n_sets = 0;
+    if (prof.on() || set_grid_) {
+      unsigned long long two[2] = {0, 0};
+      hip_check(hipMemcpyAsync(two, dd_nsets_.p, sizeof(two), hipMemcpyDeviceToHost, s), "D2H");
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      const unsigned long long ns = two[0] + two[1];
+      if (prof.on()) prof.count("dedup_sets", ns);
+      sb_.n_sets = ns;
+    }
+  }
+
+
   a.ix = di;
   a.t0 = 0;
   a.t1 = n;
@@ -1110,6 +1160,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.rep = nullptr;
   a.tslot = nullptr;
   a.dd_phase = 0;
+  a.mrank = ix.sharded() && sb_.dedup ? dd_mrank_.as<uint64_t>() : nullptr;
   pinned((2 * kPatchRegions + 1) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
   unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]

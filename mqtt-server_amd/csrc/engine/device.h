@@ -251,6 +251,7 @@ class Device {
   void* h_pin_ = nullptr;  // pinned: block offsets + overflow flags of every sub-batch
   size_t h_pin_bytes_ = 0;
   DevBuf ovf_;             // per sub-batch gather-slot overflow flags
+  DevBuf fb_list_, fb_cnt_;  // frontier walk: topics it handed to k_walk, and their number
   hipStream_t wstream_ = nullptr;  // walk + scan of the sub-batches
   hipEvent_t ev_in_ = nullptr, sb_done_[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> ev_scan_;
@@ -284,6 +285,7 @@ class Device {
     uint64_t n_sets = 0;           // their number, when read back (profiling, MQ_OPT_SET_GRID)
     const uint32_t* gathers = nullptr;
     uint32_t gstride = 0;
+    TopicCount* tc = nullptr;      // k_desc's per-topic counts (walk without lists), or null
   } sb_;
   DevBuf sp_tc_;                     // per-topic counts from k_desc<true> (walk without lists)
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
@@ -301,6 +303,7 @@ class Device {
   uint32_t merge_wpe_opt_ = 0;   // k_merge variant (MQ_OPT_MERGE_WAVES; 0: by index size)
   uint32_t walk_wpe_ = 8;        // k_walk count pass register budget (MQ_OPT_WALK_WAVES)
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
+  uint32_t walk_group_ = 16;     // frontier walk lanes per topic (MQ_OPT_WALK_GROUP; 0: k_walk)
   bool fuse_desc_ = false;       // span format: k_merge does k_desc's work (MQ_OPT_FUSE_DESC)
   uint32_t dedup_ = 1;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
   uint32_t set_grid_ = 1;        // MQ_OPT_SET_GRID (10M: set pass 1.18 -> 1.05 ms against persistent waves)
@@ -308,6 +311,8 @@ class Device {
   DevBuf dd_sets_, dd_spatches_, dd_spcount_;  // phase 1 of the dedup merge: SetInfo, set pool
   DevBuf dd_wlist_, dd_nwave_;                 // k_finish: topics left for k_merge's topic pass
   DevBuf dd_mpair_;                            // k_desc: merge gathers' pair-block headers
+  DevBuf dd_mrank_;                            // ... and rank keys (sharded index)
+  DevBuf dd_fcnt_;                             // k_xsig: cross-shard entries per topic
   uint64_t srcap_ = 0;                         // set patches per region of dd_spatches_
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
   uint32_t n_cus_ = 1;

@@ -340,21 +340,31 @@ void Index::edge_insert(uint32_t parent, const SegKey& k, uint32_t child, uint32
   }
 }
 
+// Backward-shift deletion: the slots after the erased one that probed past it move back, so the
+// table never holds tombstones — churn (unsubscribe + subscribe) does not lengthen the walk's
+// probe chains (a tombstone is probed like a full slot) nor force a whole-table rehash and upload.
 void Index::edge_erase(uint32_t parent, const SegKey& k, uint32_t child) {
   const uint64_t m = edges.size() - 1;
   uint64_t i = edge_hash(parent, k) & m;
   for (;;) {
-    EdgeSlot& e = edges.h[i];
+    const EdgeSlot& e = edges.h[i];
     if (e.parent == kEdgeEmpty) return;
-    if (e.parent == parent && e.child == child) {
-      e.parent = kEdgeTomb;
-      edges.mark(i);
-      n_edges_--;
-      n_tombs_++;
-      return;
-    }
+    if (e.parent == parent && e.child == child) break;
     i = (i + 1) & m;
   }
+  n_edges_--;
+  for (uint64_t j = (i + 1) & m;; j = (j + 1) & m) {
+    const EdgeSlot& e = edges.h[j];
+    if (e.parent == kEdgeEmpty) break;
+    if (e.parent == kEdgeTomb) continue;  // (none are made; one would stay, occupied)
+    const uint64_t h = edge_hash(e.parent, SegKey{e.k0, e.k1}) & m;
+    // the entry at j may move to the hole at i iff its home is not cyclically in (i, j]
+    const bool stays = i <= j ? (h > i && h <= j) : (h > i || h <= j);
+    if (stays) continue;
+    edges.at_w(i) = e;
+    i = j;
+  }
+  edges.at_w(i).parent = kEdgeEmpty;
 }
 
 // ---- nodes ---------------------------------------------------------------------------------------

@@ -173,6 +173,7 @@ struct EmitArgs {
   const unsigned long long* n_reps;    //   DedupArgs layout) and their two counts, in device memory
   const uint32_t* wave_list;           // dd_phase 2 after k_finish: the topics that still need a
   const unsigned long long* n_wave;    //   wavefront (k_finish wrote the others' results)
+  const uint64_t* mrank;               // sharded index: the merge gathers' rank keys (DescArgs)
 };
 constexpr uint32_t kSetHeavy = 1024;  // a merge set with this many may-merge records goes first
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
@@ -215,6 +216,7 @@ struct DescArgs {
   uint2* mpair;    // its pair-block header (NodePair ent_off, ent_mask; stride kPairMax). With these
                    // lists k_merge maps a topic's merge gathers without GDesc records, which are
                    // then written only for a topic with more than kPairMax merge gathers
+  uint64_t* mrank; // sharded index: each merge gather's DFS rank key (XInfo.rank; stride kPairMax)
 };
 
 // Merge-set dedup (span format): topics whose merge gathers are the same particles resolve to
@@ -238,8 +240,33 @@ struct DedupArgs {
   const TopicCount* tc;        // per-topic counts (k_desc; null: the offsets' differences): a set
   const struct TopicOff* off;  //   is heavy with >= heavy may-merge records
   uint32_t heavy;
+  // sharded index (null / 0 otherwise): a merge set is also the same cross-shard entries of the
+  // other shards (compared list by list); fcount[t]: their number (a topic whose local merge
+  // gathers and foreign entries exceed k_merge's map is not deduped)
+  const uint32_t* fcount;
+  uint32_t n_xf;
+  const struct XSrc* xsrc;
 };
 void launch_dedup(const DedupArgs& a, hipStream_t s);
+
+// Sharded index, after the exchange (k_xsig): per topic, fold the imported cross-shard entries
+// into the merge-set signature (msig) and count them (fcount); a topic whose map would overflow
+// (local merge gathers + foreign entries >= kMapSlots) gets the GDesc records of k_merge's slow
+// path (with rank keys), which k_desc_g16 wrote only for topics with > kPairMax merge gathers.
+struct XSigArgs {
+  DevIndex ix;
+  uint32_t n;
+  uint32_t n_xf;
+  const struct XSrc* xsrc;
+  uint64_t* msig;
+  const uint32_t* mcount;
+  uint32_t* fcount;
+  const struct TopicOff* off;
+  const uint32_t* gathers;
+  uint32_t gather_stride;
+  struct GDesc* desc;
+};
+void launch_xsig(const XSigArgs& a, hipStream_t s);
 
 // Batched auth.MatchTopic (k_acl).
 struct AclArgs {
@@ -279,6 +306,12 @@ void launch_pick(const PickArgs& a, hipStream_t s);  // a.sres != null: span for
 void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
                  const DevIndex& ix, TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf,
                  hipStream_t s);
+// The frontier walk (k_walkf, `group` lanes per topic: 4, 8 or 16), count pass: the same counts
+// and gather slots as launch_walk(false, ...). Topics it cannot hold are listed in fb_list
+// (*fb_count, zeroed by the caller) and walked by k_walk in fb_blocks persistent workgroups.
+void launch_walk_front(uint32_t group, bool lists, const uint8_t* tb, const uint64_t* to, uint32_t n,
+                       const DevIndex& ix, TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list,
+                       uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
@@ -311,8 +344,9 @@ void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, co
 // Sharded index: the topics' gathered cross-shard nodes (kFlagXNode, subscriptions gathered).
 // count = true: TopicCount.gathers = their number per topic; else written as XEnt at
 // off[t].g with their number in counts[t] (the exported list, mq_xlist).
-void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const GDesc* desc,
-                  TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts, hipStream_t s);
+void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const uint32_t* gathers,
+                  uint32_t gather_stride, TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts,
+                  hipStream_t s);
 // TopicCount.gathers = counts[t] (an imported list's counts, for launch_scan)
 void launch_counts(const uint32_t* counts, uint32_t n, TopicCount* cnt, hipStream_t s);
 // Pack the used prefix of every patch region (pcount[r] patches of region r) into `out` at

@@ -132,6 +132,49 @@ __device__ __forceinline__ P scan_segment(ByteReaderT<P>& R, P s, P end, SegKey*
   return e;
 }
 
+// wavefront helpers
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t prefix_before(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+// Exclusive wave-wide prefix sum (64 lanes); *total receives the sum.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t* total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Index of the calling wavefront in its workgroup, as a wave-uniform (scalar) value: the
+// compiler cannot prove threadIdx.x >> 6 uniform, and per-wave work indexed by it would
+// otherwise run as vector code under exec masks.
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // particles.get(key) (topics.go:803-807) through the global edge table. The slot that names the
 // child also carries the child's '+' and '#' children (EdgeSlot.plus / hash).
 struct EdgeHit {
@@ -176,15 +219,11 @@ __device__ __forceinline__ uint32_t lookup(const DevIndex& ix, uint32_t parent, 
 // may-merge counts); LISTS=false: gathers only (k_desc<true> reads the lists).
 constexpr uint32_t kWalkPath = 8;
 // WPE: minimum waves per SIMD asked of the register allocator (1: no constraint).
-template <bool FILL, bool LISTS, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walk(const uint8_t* __restrict__ tb,
-                                              const uint64_t* __restrict__ to, uint32_t n,
-                                              DevIndex ix, TopicCount* __restrict__ cnt,
-                                              const TopicOff* __restrict__ off,
-                                              uint32_t* __restrict__ gathers, uint32_t* __restrict__ ovf) {
-  __shared__ uint2 path[kWalkPath][256];  // level d: the '+' / '#' children of the particle at depth d
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+template <bool FILL, bool LISTS>
+__device__ __forceinline__ void walk_topic(uint32_t t, const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
+                                           const DevIndex& ix, TopicCount* __restrict__ cnt,
+                                           const TopicOff* __restrict__ off, uint32_t* __restrict__ gathers,
+                                           uint32_t* __restrict__ ovf, uint2 (*path)[256]) {
   const uint64_t a0 = to[t], a1 = to[t + 1];
   uint32_t ng = 0, rows = 0, shared = 0, inl = 0, merge = 0;
   uint32_t* gout = FILL ? gathers + off[t].g : gathers + (uint64_t)t * kGatherCap;
@@ -312,6 +351,237 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     c.merge = merge;
     cnt[t] = c;
     if (ng > kGatherCap) atomicOr(ovf, 1u);
+  }
+}
+
+// list == null: thread per topic t < n. Else the topics list[0, *n_list), grid-stride (the
+// frontier walk's fallback: its length is known on the device only).
+template <bool FILL, bool LISTS, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walk(const uint8_t* __restrict__ tb,
+                                              const uint64_t* __restrict__ to, uint32_t n,
+                                              DevIndex ix, TopicCount* __restrict__ cnt,
+                                              const TopicOff* __restrict__ off,
+                                              uint32_t* __restrict__ gathers, uint32_t* __restrict__ ovf,
+                                              const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list) {
+  __shared__ uint2 path[kWalkPath][256];  // level d: the '+' / '#' children of the particle at depth d
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!list) {
+    if (i0 < n) walk_topic<FILL, LISTS>(i0, tb, to, ix, cnt, off, gathers, ovf, path);
+    return;
+  }
+  const uint32_t nl = *n_list;
+  for (uint32_t i = i0; i < nl; i += gridDim.x * blockDim.x) walk_topic<FILL, LISTS>(list[i], tb, to, ix, cnt, off, gathers, ovf, path);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_walkf: the match walk as a level-synchronous frontier expansion (the north-star design):
+// G lanes per topic (64 / G topics per wavefront). The group tokenises its topic together —
+// lane j takes 16-byte chunks j, j + G, ... (coalesced), finds the '/' bytes with SWAR masks
+// and places them with a group prefix sum — then walks it level by level. The frontier (the
+// particles that match the topic's first d segments, each with its '+' / '#' children and its
+// path code) is held one particle per lane; at level d every lane probes its particle's literal
+// child and reads its '+' child's walk record at once, so a topic costs about two dependent
+// round trips per level instead of one per probe of the reference's recursion, and the
+// wavefront's loads are issued together. Gathers are staged in LDS with their DFS rank — the
+// path code of SURVEY.md App. A.3, two bits per level (literal 1, '+' 2, '#' 3), zero padded,
+// so that comparing ranks is comparing positions in scanSubscribers' order (topics.go:603-625):
+// the literal subtree, then the '+' subtree, then the '#' gather; at the final level the
+// particle before its '#' child (topics.go:612). The group then sorts them by rank (each lane
+// counts the smaller ranks) and writes them in the reference's order, exactly what k_walk
+// writes. A topic the frontier cannot hold — more than kFrontLevels levels (the rank's 32 bits),
+// more than G particles at one level, more than kGatherCap gathers — goes to `fb_list` and is
+// walked by k_walk (thread per topic, stackless DFS) right after.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kFrontLevels = 15;  // levels a topic may have: its deepest gather rank needs 2 bits more
+
+// Inclusive prefix sum over the G lanes of a group (G a power of two <= 64; sub = lane % G).
+template <uint32_t G>
+__device__ __forceinline__ uint32_t grp_incl(uint32_t v, uint32_t sub) {
+#pragma unroll
+  for (uint32_t d = 1; d < G; d <<= 1) {
+    const uint32_t y = __shfl_up(v, d, G);
+    if (sub >= d) v += y;
+  }
+  return v;
+}
+template <uint32_t G>
+__device__ __forceinline__ uint32_t grp_sum(uint32_t v) {
+#pragma unroll
+  for (uint32_t d = 1; d < G; d <<= 1) v += __shfl_xor(v, d, G);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+  return v;
+}
+
+struct FrontEnt {  // one frontier particle: its '+' / '#' children and its path code
+  uint32_t node, plus, hash, code;
+};
+
+template <uint32_t G, bool LISTS>
+__global__ __launch_bounds__(256) void k_walkf(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
+                                               uint32_t n, DevIndex ix, TopicCount* __restrict__ cnt,
+                                               uint32_t* __restrict__ gathers, uint32_t* __restrict__ fb_list,
+                                               uint32_t* __restrict__ fb_count) {
+  constexpr uint32_t kTopics = 256 / G;  // topics per workgroup
+  __shared__ uint32_t sl[kTopics][kFrontLevels];      // '/' positions (relative to the topic's chunk base)
+  __shared__ uint2 gat[kTopics][kGatherCap];          // staged gathers: (word, rank)
+  __shared__ FrontEnt xf[kTopics][G];                 // next level's frontier, compacted
+  const uint32_t q = threadIdx.x / G, sub = threadIdx.x % G;
+  const uint32_t t = blockIdx.x * kTopics + q;
+  const bool live = t < n;
+  uint64_t a0 = 0, a1 = 0;
+  if (live) {
+    a0 = to[t];
+    a1 = to[t + 1];
+  }
+  const uint8_t* tbase = tb + (a0 & ~15ull);
+  const uint32_t b0 = (uint32_t)(a0 & 15), b1 = b0 + (uint32_t)(a1 - a0);
+  ByteReaderT<uint32_t> R(tbase);
+  // --- tokenise: the group's lanes over the topic's chunks -------------------------------------
+  const uint32_t nch = a1 > a0 ? (b1 + 15) >> 4 : 0u;
+  uint32_t nsl = 0;  // '/' found so far (group-uniform)
+  const uint32_t rounds = wave_max((nch + G - 1) / G);
+  for (uint32_t r = 0; r < rounds; r++) {
+    const uint32_t k = r * G + sub;
+    uint32_t m = 0;
+    if (k < nch) {
+      m = slash_mask(*reinterpret_cast<const u32x4*>(tbase + ((uint64_t)k << 4)));
+      if (k == 0) m &= 0xFFFFu << b0;
+      if (k == nch - 1 && (b1 & 15)) m &= (1u << (b1 & 15)) - 1u;
+    }
+    const uint32_t c = __popc(m);
+    const uint32_t inc = grp_incl<G>(c, sub);
+    uint32_t idx = nsl + inc - c;
+    for (; m; m &= m - 1, idx++)
+      if (idx < kFrontLevels) sl[q][idx] = (k << 4) + (uint32_t)(__ffs(m) - 1);
+    nsl += __shfl(inc, G - 1, G);
+  }
+  const uint32_t L = nch ? nsl + 1 : 0u;  // levels (0: the empty topic, which matches nothing)
+  bool fb = live && L > kFrontLevels;
+  wave_sync_lds();
+  const bool dollar = L && R.at(b0) == '$';
+  bool lit0wild = false;  // segment 0 starts with '+' / '#' (a literal child there is 'wild', Q3)
+  if (L) {
+    const uint32_t e0 = L > 1 ? sl[q][0] : b1;
+    if (e0 > b0) {
+      const uint32_t c0 = R.at(b0);
+      lit0wild = c0 == '+' || c0 == '#';
+    }
+  }
+  // --- the frontier, level by level ------------------------------------------------------------
+  FrontEnt fe{kNone, kNone, kNone, 0u};
+  if (sub == 0) {
+    const NodeWalk rw = ix.walk[kRoot];
+    fe = FrontEnt{kRoot, rw.plus_child, rw.hash_child, 0u};
+  }
+  uint32_t F = 1, ng = 0;  // frontier size, gathers staged (group-uniform)
+  const uint32_t levels = wave_max(live && !fb ? L : 0u);
+  for (uint32_t d = 0; d < levels; d++) {
+    const bool act = live && !fb && d < L && F != 0;
+    const bool mine = act && sub < F;
+    const bool has_next = d + 1 < L;
+    const uint32_t s = d ? sl[q][d - 1] + 1 : b0, e = has_next ? sl[q][d] : b1;
+    const uint32_t sh = 30 - 2 * d;  // level d's two bits of the rank
+    SegKey key{0, 0};
+    uint32_t len = 0, c0 = 0;
+    if (act) {
+      len = e - s;
+      c0 = len ? R.at(s) : 0u;
+      key = key_of(R, s, e);
+    }
+    NodeWalk pw{kNone, kNone, 0, 0};
+    if (mine && has_next && fe.plus != kNone) pw = ix.walk[fe.plus];
+    EdgeHit h{kNone, kNone, kNone};
+    // a literal "+" segment: the reference visits the '+' child twice alike (topics.go:603)
+    if (mine && !(len == 1 && c0 == '+')) h = lookup_edge(ix, fe.node, key, tbase + s, len);
+    // this lane's gathers (at most four): the particle's '#' child (topics.go:621); at the last
+    // level the literal child, its '#' child (filter/# matches filter, topics.go:612; inline: the
+    // particle's own again, Q2) and the '+' child
+    const bool gH = mine && fe.hash != kNone;
+    const bool gL = mine && !has_next && h.child != kNone;
+    const bool gC = gL && h.hash != kNone;
+    const bool gP = mine && !has_next && fe.plus != kNone;
+    const uint32_t gc = (uint32_t)gH + (uint32_t)gL + (uint32_t)gC + (uint32_t)gP;
+    const uint32_t gi = grp_incl<G>(gc, sub);
+    const uint32_t gtot = __shfl(gi, G - 1, G);
+    if (act && ng + gtot > kGatherCap) fb = true;
+    if (act && !fb) {
+      uint32_t p = ng + gi - gc;
+      if (gH) gat[q][p++] = make_uint2(fe.hash | kGatherInline, fe.code | 3u << sh);
+      if (gL) gat[q][p++] = make_uint2(h.child | kGatherInline, fe.code | 1u << sh);
+      if (gC) gat[q][p++] = make_uint2(h.hash, fe.code | 1u << sh | 3u << (sh - 2));
+      if (gP) gat[q][p++] = make_uint2(fe.plus | kGatherInline, fe.code | 2u << sh);
+    }
+    ng += gtot;
+    // next level's frontier: the literal and '+' children, compacted over the group
+    const bool fL = mine && has_next && h.child != kNone;
+    const bool fP = mine && has_next && fe.plus != kNone;
+    const uint32_t fc = (uint32_t)fL + (uint32_t)fP;
+    const uint32_t fi = grp_incl<G>(fc, sub);
+    const uint32_t ftot = __shfl(fi, G - 1, G);
+    if (act && has_next && ftot > G) fb = true;
+    if (act && !fb && has_next) {
+      uint32_t p = fi - fc;
+      if (fL) xf[q][p++] = FrontEnt{h.child, h.plus, h.hash, fe.code | 1u << sh};
+      if (fP) xf[q][p] = FrontEnt{fe.plus, pw.plus_child, pw.hash_child, fe.code | 2u << sh};
+    }
+    wave_sync_lds();
+    if (act) {
+      F = has_next ? ftot : 0u;
+      if (!fb && sub < F) fe = xf[q][sub];
+    }
+    wave_sync_lds();  // the frontier is read before the next level overwrites it
+  }
+  if (!live) return;
+  if (fb) {
+    if (sub == 0) fb_list[atomicAdd(fb_count, 1u)] = t;
+    return;
+  }
+  // --- the gathers in the reference's order ------------------------------------------------------
+  wave_sync_lds();
+  uint32_t rows = 0, shared = 0, inl = 0, merge = 0;
+  uint32_t* gout = gathers + (uint64_t)t * kGatherCap;
+  for (uint32_t i = sub; i < ng; i += G) {
+    const uint2 gi = gat[q][i];
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < ng; j++) pos += gat[q][j].y < gi.y ? 1u : 0u;
+    const uint32_t node = gi.x & kGatherNode;
+    uint32_t gw = gi.x;
+    if (LISTS) {
+      const NodeLists Ls = ix.lists[node];
+      // [MQTT-4.7.1-1]: '$' topics skip subscriptions whose filter starts with '+'/'#' (Q3)
+      const bool subs_ok = !(dollar && (Ls.flags & kFlagSeg0Wild));
+      if (subs_ok) {
+        gw |= kGatherSubs;
+        rows += Ls.n_direct + Ls.n_merge;
+        merge += Ls.n_merge;
+      }
+      shared += Ls.shr_cnt;
+      if (gi.x & kGatherInline) inl += Ls.inl_cnt;
+    } else {
+      const uint32_t k0 = gi.y >> 30;  // how the path starts: literal 1, '+' 2, '#' 3
+      const bool wild = k0 >= 2 || (k0 == 1 && lit0wild);
+      if (!(dollar && wild)) gw |= kGatherSubs;
+    }
+    gout[pos] = gw;
+  }
+  if (LISTS) {
+    rows = grp_sum<G>(rows);
+    shared = grp_sum<G>(shared);
+    inl = grp_sum<G>(inl);
+    merge = grp_sum<G>(merge);
+  }
+  if (sub == 0) {
+    TopicCount c;
+    c.gathers = ng;
+    c.rows = rows;
+    c.shared = shared;
+    c.inlines = inl;
+    c.merge = merge;
+    cnt[t] = c;
   }
 }
 
@@ -609,48 +879,6 @@ __global__ __launch_bounds__(256) void k_scan_apply(const TopicCount* __restrict
 //            packets/packets.go:254-274), applies the inline last-write rule (topics.go:668-676)
 //            and writes the topic's result record.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t hash32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-__device__ __forceinline__ uint32_t prefix_before(uint64_t mask) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-}
-
-// Exclusive wave-wide prefix sum (64 lanes); *total receives the sum.
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t* total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
-  *total = __shfl(x, 63, 64);
-  return x - v;
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
-
-// Index of the calling wavefront in its workgroup, as a wave-uniform (scalar) value: the
-// compiler cannot prove threadIdx.x >> 6 uniform, and per-wave work indexed by it would
-// otherwise run as vector code under exec masks.
-__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
-
-__device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // SPANS=false (row format): positions are relative to the topic's output chunk and the k_copy
 // tiles starting in each gather are marked. SPANS=true: positions are topic-relative (k_merge
 // patches name a topic's rows), every gather also becomes a SpanRec at its gather index, and
@@ -776,6 +1004,25 @@ __device__ __forceinline__ uint32_t g16_incl(uint32_t v, uint32_t sub) {
   return v;
 }
 
+// The GDesc records of one topic's gathers for k_merge's slow paths (a topic beyond the map):
+// rows topic-relative, a merge gather's pair-block header in s_pos / s_src and, on a sharded
+// index, its rank key in i_pos (low) / i_src (high).
+__device__ __forceinline__ void write_gdesc(const DevIndex& ix, const uint32_t* gw_src, uint32_t n_g, uint32_t sp,
+                                            GDesc* out) {
+  uint32_t rp = 0;
+  for (uint32_t i = 0; i < n_g; i++) {
+    const uint32_t gw = gw_src[i];
+    const NodeLists L = ix.lists[gw & kGatherNode];
+    const bool mg = (gw & kGatherSubs) && L.n_merge;
+    const NodePair P = mg ? ix.npair[gw & kGatherNode] : NodePair{0, kNone, 0, 0};
+    const uint64_t rk = mg && ix.xinfo ? ix.xinfo[gw & kGatherNode].rank : 0ull;
+    out[i] = GDesc{rp, L.sub_off, mg ? P.ent_off : sp, mg ? P.ent_mask : L.shr_off, (uint32_t)rk, (uint32_t)(rk >> 32),
+                   gw, L.n_direct | (mg ? kDescMerge : 0u)};
+    rp += (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
+    sp += L.shr_cnt;
+  }
+}
+
 // k_desc for the span format with merge-set dedup lists (the default): 16 lanes per topic, four
 // topics per wavefront, the lanes over the topic's gathers. A topic's gather words, spans and
 // merge lists are contiguous, so its loads and stores coalesce; a thread per topic stores to 64
@@ -828,6 +1075,7 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
         a.mlist[q] = gw & kGatherNode;
         a.mrow[q] = rp + L.n_direct;
         a.mpair[q] = make_uint2(P.ent_off, P.ent_mask);
+        if (a.mrank) a.mrank[q] = a.ix.xinfo[gw & kGatherNode].rank;
       }
     }
     if (subs) n_merge += L.n_merge;
@@ -845,19 +1093,8 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
   if (a.tc_out) a.tc_out[t] = TopicCount{n_g, rpos, spos, 0u, n_merge};
   a.msig[t] = mix64(sig + n_mg) | 1ull;  // never 0 (the dedup table's empty key)
   a.mcount[t] = n_mg;
-  if (n_mg > kPairMax) {  // k_merge maps this topic from its GDesc records: write them (rare)
-    uint32_t rp = 0, sp = (uint32_t)o0.shr;
-    for (uint32_t i = 0; i < n_g; i++) {
-      const uint32_t gw = gw_src[i];
-      const NodeLists L = a.ix.lists[gw & kGatherNode];
-      const bool mg = (gw & kGatherSubs) && L.n_merge;
-      const NodePair P = mg ? a.ix.npair[gw & kGatherNode] : NodePair{0, kNone, 0, 0};
-      a.desc[o0.g + i] = GDesc{rp, L.sub_off, mg ? P.ent_off : sp, mg ? P.ent_mask : L.shr_off, 0u, 0u, gw,
-                               L.n_direct | (mg ? kDescMerge : 0u)};
-      rp += (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
-      sp += L.shr_cnt;
-    }
-  }
+  // k_merge maps this topic from its GDesc records: write them (rare)
+  if (n_mg > kPairMax) write_gdesc(a.ix, gw_src, n_g, (uint32_t)o0.shr, a.desc + o0.g);
 }
 
 // k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, whose
@@ -867,7 +1104,8 @@ __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
   const bool act = t < a.n;
   const uint32_t c = act ? a.mcount[t] : 0u;
-  const bool ok = c != 0 && c <= kPairMax;
+  // (sharded: the merge gathers and the other shards' entries must fit k_merge's map)
+  const bool ok = c != 0 && c <= kPairMax && (!a.fcount || c + a.fcount[t] < kMapSlots);
   const unsigned long long k = ok ? a.msig[t] : 0ull;
   // one table operation per distinct signature in the wavefront: a hot signature (the topics
   // under the same busy particles) would otherwise have every topic's CAS on one slot at once
@@ -926,6 +1164,16 @@ __global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
       for (uint32_t j = 0; eq && j < c; j += 4) {
         const uint4 p = x[j >> 2], q = y[j >> 2];
         eq = p.x == q.x && (j + 1 >= c || p.y == q.y) && (j + 2 >= c || p.z == q.z) && (j + 3 >= c || p.w == q.w);
+      }
+      // sharded: the same cross-shard entries of every other shard, in the same order
+      for (uint32_t f = 0; eq && f < a.n_xf; f++) {
+        const XSrc src = a.xsrc[f];
+        const uint64_t t0 = src.xoff[t].g, t1 = src.xoff[t + 1].g, v0 = src.xoff[v].g;
+        eq = src.xoff[v + 1].g - v0 == t1 - t0;
+        for (uint64_t k = 0; eq && k < t1 - t0; k++) {
+          const XEnt p = src.xent[t0 + k], q = src.xent[v0 + k];
+          eq = p.fid == q.fid && p.rank == q.rank;
+        }
       }
       if (eq) r = v;
     }
@@ -998,6 +1246,36 @@ __global__ __launch_bounds__(256) void k_finish(FinishArgs a) {
   if (lane == 0 && b) base = atomicAdd(a.n_wave, (unsigned long long)__popcll(b));
   base = __shfl(base, 0, 64);
   if (wave) a.wave_list[base + prefix_before(b)] = t;
+}
+
+__global__ __launch_bounds__(256) void k_xsig(XSigArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.n) return;
+  uint64_t sig = 0;
+  uint32_t fc = 0;
+  for (uint32_t f = 0; f < a.n_xf; f++) {
+    const XSrc src = a.xsrc[f];
+    const uint64_t x0 = src.xoff[t].g, x1 = src.xoff[t + 1].g;
+    for (uint64_t k = x0; k < x1; k++) {
+      const XEnt e = src.xent[k];
+      sig = mix64(sig ^ ((uint64_t)f << 56 | (uint64_t)fc << 32 | e.fid)) + e.rank;
+      fc++;
+    }
+  }
+  a.fcount[t] = fc;
+  const uint32_t mc = a.mcount[t];
+  if (!fc || !mc) return;
+  a.msig[t] = mix64(a.msig[t] ^ sig) | 1ull;
+  if (mc <= kPairMax && mc + fc >= kMapSlots) {  // k_merge's slow path reads GDesc records
+    const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+    const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
+    write_gdesc(a.ix, gw_src, (uint32_t)(o1.g - o0.g), (uint32_t)o0.shr, a.desc + o0.g);
+  }
+}
+
+void launch_xsig(const XSigArgs& a, hipStream_t s) {
+  if (!a.n) return;
+  hipLaunchKernelGGL(k_xsig, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 
 void launch_finish(const FinishArgs& a, hipStream_t s) {
@@ -1330,7 +1608,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // within a topic.
     // merge-set dedup's lists (k_desc): the topic's merge gathers directly, x standing for the
     // gather index (the same order); a topic with more than kPairMax of them has GDesc records
-    const uint32_t lc = (SPANS && !XS && !DESC && a.mlist) ? a.mcount[t] : kNone;
+    const uint32_t lc = (SPANS && !DESC && a.mlist) ? a.mcount[t] : kNone;
     if (lc <= kPairMax) {
       for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
       wave_sync_lds();
@@ -1343,6 +1621,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         map_val[wv][sl] = lane;
         mg_node[wv][lane] = node;
         mg_gi[wv][lane] = lane;
+        if (XS) mg_rank[wv][lane] = a.mrank[k];
         mg_row[wv][lane] = a.mrow[k];
         mg_eoff[wv][lane] = P.x;
         mg_emask[wv][lane] = P.y;
@@ -1406,7 +1685,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       n_ent += (uint32_t)(x1 - x0);
     }
     wave_sync_lds();
-    const bool slow = n_map > kPairMax || n_ent > kEnt;  // beyond the map: linear lookups
+    // beyond the map: linear lookups (the map's hash table keeps a free slot: kMapSlots - 1
+    // entries at most, so a lookup of a node that is not there ends)
+    const bool slow = n_map > kPairMax || n_ent > (XS ? kEnt - 1 : kEnt);
     if (DESC && slow) {  // the slow paths read the topic's GDesc records
       desc_pass(false, true);
       __threadfence_block();
@@ -1754,7 +2035,8 @@ void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const u
     else hipLaunchKernelGGL((k_walku<false, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf);
     return;
   }
-#define MQ_WALK(F, L, W) hipLaunchKernelGGL((k_walk<F, L, W>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf)
+#define MQ_WALK(F, L, W) \
+  hipLaunchKernelGGL((k_walk<F, L, W>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf, nullptr, nullptr)
   if (fill) {
     if (lists) MQ_WALK(true, true, 1);
     else MQ_WALK(true, false, 1);
@@ -1766,6 +2048,33 @@ void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const u
     else MQ_WALK(false, false, 1);
   }
 #undef MQ_WALK
+}
+
+void launch_walk_front(uint32_t group, bool lists, const uint8_t* tb, const uint64_t* to, uint32_t n,
+                       const DevIndex& ix, TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list,
+                       uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s) {
+  if (!n) return;
+  const dim3 grid((n + 256 / group - 1) / (256 / group));
+#define MQ_WALKF(G, L) hipLaunchKernelGGL((k_walkf<G, L>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
+  if (group == 8) {
+    if (lists) MQ_WALKF(8, true);
+    else MQ_WALKF(8, false);
+  } else if (group == 16) {
+    if (lists) MQ_WALKF(16, true);
+    else MQ_WALKF(16, false);
+  } else {
+    if (lists) MQ_WALKF(4, true);
+    else MQ_WALKF(4, false);
+  }
+#undef MQ_WALKF
+  // the topics the frontier could not hold: thread per topic, grid-stride over the list
+  const dim3 fgrid(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, fb_blocks)));
+  if (lists)
+    hipLaunchKernelGGL((k_walk<false, true, 1>), fgrid, dim3(256), 0, s, tb, to, n, ix, cnt, nullptr, gathers, ovf,
+                       fb_list, fb_count);
+  else
+    hipLaunchKernelGGL((k_walk<false, false, 1>), fgrid, dim3(256), 0, s, tb, to, n, ix, cnt, nullptr, gathers, ovf,
+                       fb_list, fb_count);
 }
 
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
@@ -1799,7 +2108,10 @@ void launch_merge(const EmitArgs& a, bool spans, bool desc, uint32_t wpe, uint32
   if (!waves) return;
   const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
   const dim3 g(blocks), b(256);
-  if (spans && a.ix.xinfo) {  // sharded index
+  if (spans && a.ix.xinfo && a.rep && a.dd_phase == 1) {  // sharded index, merge-set dedup: the set pass
+    if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6, false, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, true, 1, false, true>), g, b, 0, s, a);
+  } else if (spans && a.ix.xinfo) {  // sharded index
     if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6, false>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_merge<true, true, 1, false>), g, b, 0, s, a);
   } else if (spans && desc) {
@@ -2289,16 +2601,17 @@ void launch_pick(const PickArgs& a, hipStream_t s) {
 // Sharded index: each topic's gathered cross-shard nodes (the exported list).
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_xlist(DevIndex ix, uint32_t n, const TopicOff* __restrict__ off,
-                                               const GDesc* __restrict__ desc, TopicCount* __restrict__ cnt,
-                                               const TopicOff* __restrict__ xoff, XEnt* __restrict__ ents,
-                                               uint32_t* __restrict__ counts) {
+                                               const uint32_t* __restrict__ gathers, uint32_t gather_stride,
+                                               TopicCount* __restrict__ cnt, const TopicOff* __restrict__ xoff,
+                                               XEnt* __restrict__ ents, uint32_t* __restrict__ counts) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  const uint64_t g0 = off[t].g, g1 = off[t + 1].g;
+  const uint32_t n_g = (uint32_t)(off[t + 1].g - off[t].g);
+  const uint32_t* gw_src = gather_stride ? gathers + (uint64_t)t * gather_stride : gathers + off[t].g;
   uint32_t k = 0;
   XEnt* out = COUNT ? nullptr : ents + xoff[t].g;
-  for (uint64_t g = g0; g < g1; g++) {
-    const uint32_t gw = desc[g].word;
+  for (uint32_t g = 0; g < n_g; g++) {
+    const uint32_t gw = gw_src[g];
     if (!(gw & kGatherSubs)) continue;
     const uint32_t node = gw & kGatherNode;
     if (!(ix.lists[node].flags & kFlagXNode)) continue;
@@ -2312,13 +2625,16 @@ __global__ __launch_bounds__(256) void k_xlist(DevIndex ix, uint32_t n, const To
   else counts[t] = k;
 }
 
-void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const GDesc* desc,
-                  TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts, hipStream_t s) {
+void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const uint32_t* gathers,
+                  uint32_t gather_stride, TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts,
+                  hipStream_t s) {
   if (!n) return;
   if (count)
-    hipLaunchKernelGGL(k_xlist<true>, dim3((n + 255) / 256), dim3(256), 0, s, ix, n, off, desc, cnt, xoff, ents, counts);
+    hipLaunchKernelGGL(k_xlist<true>, dim3((n + 255) / 256), dim3(256), 0, s, ix, n, off, gathers, gather_stride, cnt,
+                       xoff, ents, counts);
   else
-    hipLaunchKernelGGL(k_xlist<false>, dim3((n + 255) / 256), dim3(256), 0, s, ix, n, off, desc, cnt, xoff, ents, counts);
+    hipLaunchKernelGGL(k_xlist<false>, dim3((n + 255) / 256), dim3(256), 0, s, ix, n, off, gathers, gather_stride, cnt,
+                       xoff, ents, counts);
 }
 
 __global__ __launch_bounds__(256) void k_counts(const uint32_t* __restrict__ counts, uint32_t n,

@@ -67,6 +67,26 @@ void IdTable::unref(uint32_t id, uint64_t now) {
   free_.emplace_back(id, now);  // strs_[id] stays readable for batches still in flight
 }
 
+void IdTable::tidy(uint32_t id, uint64_t now) {
+  if (refs_[id] != 0) return;
+  auto it = ids_.find(strs_[id]);
+  if (it == ids_.end() || it->second != id) return;  // already released
+  ids_.erase(it);
+  free_.emplace_back(id, now);
+}
+
+void TopicsIndex::fail_tidy(int rc, const char* what, const uint32_t* clients, size_t nc, const uint32_t* filters,
+                            size_t nf) {
+  {
+    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    const uint64_t now = epochs_.now();
+    for (size_t i = 0; i < nc; i++) clients_.tidy(clients[i], now);
+    for (size_t i = 0; i < nf; i++) filters_.tidy(filters[i], now);
+  }
+  check(rc, what);
+  throw EngineError(rc, what);  // rc < 0 here: check threw
+}
+
 TopicsIndex::TopicsIndex(int device, bool select_shared) {
   mq_config cfg{device, select_shared ? MQ_CFG_SELECT_SHARED : 0u, 0, 0, 0, 0};
   check(mq_index_create(&cfg, &idx_), "mq_index_create");
@@ -103,7 +123,7 @@ bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) 
   }
   const int rc = mq_subscribe(idx_, sub.Filter.data(), (uint32_t)sub.Filter.size(), c, f, sub.Qos,
                               sub_flags(sub), sub.Identifier);
-  check(rc, "mq_subscribe");
+  if (rc < 0) fail_tidy(rc, "mq_subscribe", &c, 1, &f, 1);
   std::unique_lock<std::shared_mutex> lk(tables_mu_);
   store(c, f, sub);
   return rc == 1;
@@ -142,7 +162,7 @@ bool TopicsIndex::InlineSubscribe(const InlineSubscription& sub) {
   }
   const int rc = mq_inline_subscribe(idx_, sub.Sub.Filter.data(), (uint32_t)sub.Sub.Filter.size(),
                                      sub.Sub.Identifier, f);
-  check(rc, "mq_inline_subscribe");
+  if (rc < 0) fail_tidy(rc, "mq_inline_subscribe", nullptr, 0, &f, 1);
   std::unique_lock<std::shared_mutex> lk(tables_mu_);
   auto it = inline_.find({sub.Sub.Identifier, f});
   if (it != inline_.end()) {
@@ -192,9 +212,9 @@ std::vector<bool> TopicsIndex::LoadSubscriptions(const std::vector<std::pair<std
     }
   }
   bytes.resize(bytes.size() + 16, '\0');
-  check(mq_subscribe_bulk(idx_, (const uint8_t*)bytes.data(), offs.data(), cids.data(), fids.data(), qos.data(),
-                          flags.data(), idents.data(), n, out_new.data()),
-        "mq_subscribe_bulk");
+  const int rc = mq_subscribe_bulk(idx_, (const uint8_t*)bytes.data(), offs.data(), cids.data(), fids.data(),
+                                   qos.data(), flags.data(), idents.data(), n, out_new.data());
+  if (rc < 0) fail_tidy(rc, "mq_subscribe_bulk", cids.data(), n, fids.data(), n);
   std::unique_lock<std::shared_mutex> lk(tables_mu_);
   std::vector<bool> out(n);
   for (size_t i = 0; i < n; i++) {
@@ -281,7 +301,16 @@ std::vector<TopicView> TopicsIndex::SubscribersViews(const std::vector<std::stri
     epochs_.end(stamp);
     check(rc, "mq_match_spans");
   }
-  auto batch = std::make_shared<const SpanBatch>(*this, r, stamp);
+  // the result (and its pin of the host image) is owned from here on, whatever throws
+  std::unique_ptr<mq_span_result, void (*)(void*)> own(r, mq_result_free);
+  std::shared_ptr<const SpanBatch> batch;
+  try {
+    batch = std::make_shared<const SpanBatch>(*this, r, stamp);
+  } catch (...) {
+    epochs_.end(stamp);
+    throw;
+  }
+  own.release();  // the batch frees it
   std::vector<TopicView> out;
   out.reserve(topics.size());
   for (uint32_t t = 0; t < topics.size(); t++) out.emplace_back(batch, t);
@@ -312,6 +341,9 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::st
   mq_span_result* r = nullptr;
   check(mq_match_spans(idx_, (const uint8_t*)bytes.data(), offs.data(), (uint32_t)topics.size(), &r),
         "mq_match_spans");
+  // freed however this ends (an exception while building the maps must not leak the pin, or
+  // every later update would wait for it); declared before the table lock, so released after it
+  std::unique_ptr<mq_span_result, void (*)(void*)> own(r, mq_result_free);
   std::vector<Subscribers> out(topics.size());
   std::shared_lock<std::shared_mutex> lk(tables_mu_);
   auto stored = [&](uint32_t c, uint32_t f, const mq_client_row* row) {
@@ -377,8 +409,6 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::st
       }
     }
   }
-  lk.unlock();
-  mq_result_free(r);
   return out;
 }
 

@@ -112,6 +112,8 @@ class IdTable {
   const std::string& str(uint32_t id) const { return strs_[id]; }
   void ref(uint32_t id) { refs_[id]++; }
   void unref(uint32_t id, uint64_t now);          // at zero: released at `now`
+  // an id interned for a call that then failed: released at `now` unless something references it
+  void tidy(uint32_t id, uint64_t now);
   size_t live() const { return ids_.size(); }
  private:
   const Epochs& ep_;
@@ -238,6 +240,9 @@ class TopicsIndex {
 
  private:
   void store(uint32_t c, uint32_t f, const Subscription& sub);  // tables_mu_ held
+  // an engine call that interned ids failed: release the ones nothing references, then throw
+  [[noreturn]] void fail_tidy(int rc, const char* what, const uint32_t* clients, size_t nc, const uint32_t* filters,
+                              size_t nf);
   mq_index* idx_ = nullptr;
   std::mutex upd_mu_;                    // serialises updates
   mutable std::shared_mutex tables_mu_;  // the tables below: exclusive to change, shared to read

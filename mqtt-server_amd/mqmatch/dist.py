@@ -104,40 +104,66 @@ def _device_view(ptr, nbytes):
     return torch.as_tensor(_Buf(), device="cuda")
 
 
+def exchange_exact(counts, ents):
+    """The exchange of exchange_xlists on tensors of the process group's device: every rank's
+    per-topic counts (int32, n each: all-gathered) and its entry bytes (uint8, 16 B per entry,
+    any size: sent to every other rank with grouped point-to-point ops of exactly that size).
+    Returns (all counts [world * n], {rank: its entry bytes} of the other ranks, entries per rank,
+    the send buffer — keep it alive until the receivers are done)."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    on = counts.device
+    ne = torch.tensor([ents.numel() // 16], dtype=torch.int64, device=on)
+    ne_all = torch.empty(world, dtype=torch.int64, device=on)
+    dist.all_gather_into_tensor(ne_all, ne)
+    c_all = torch.empty(world * counts.numel(), dtype=torch.int32, device=on)
+    dist.all_gather_into_tensor(c_all, counts)
+    ne_host = ne_all.cpu().tolist()  # the receive sizes
+    recv = {r: torch.empty(16 * ne_host[r], dtype=torch.uint8, device=on) for r in range(world) if r != rank}
+    ops = []
+    for r in range(world):
+        if r == rank:
+            continue
+        if ne_host[rank]:
+            ops.append(dist.P2POp(dist.isend, ents, r))
+        if ne_host[r]:
+            ops.append(dist.P2POp(dist.irecv, recv[r], r))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return c_all, recv, ne_host, ents
+
+
 def exchange_xlists(x, backend):
-    """All-gather every rank's exported list (mq_xlist from Engine.match_spans_begin): returns
-    the other ranks' lists as XList structs over device tensors, and the tensors (keep them
-    alive until mq_match_spans_end). nccl: two all-gathers of device buffers (counts, entries
-    padded to the largest rank's) plus one of the entry counts; gloo: the same through host
-    memory."""
+    """Exchange every rank's exported list (mq_xlist from Engine.match_spans_begin): returns the
+    other ranks' lists as XList structs over device tensors, and the tensors (keep them alive
+    until mq_match_spans_end). Counts first, then exact sizes: one all-gather of the per-topic
+    counts (n x 4 B per rank) and of the entry totals, then the entries themselves moved with
+    grouped point-to-point sends and receives of exactly each rank's size (batch_isend_irecv:
+    ncclSend / ncclRecv in one group over xGMI, SURVEY.md §5 — RCCL has no all-gather-v, and
+    padding every rank to the largest one moved the largest rank's volume from every rank).
+    gloo: the same through host memory."""
     import torch
     import torch.distributed as dist
     from .engine import XList
     world, rank = dist.get_world_size(), dist.get_rank()
     n = int(x.n_topics)
     dev = torch.device("cuda", torch.cuda.current_device())
+    on = dev if backend == "nccl" else torch.device("cpu")
     counts = _device_view(x.counts, 4 * n).view(torch.int32) if n else torch.zeros(0, dtype=torch.int32, device=dev)
     ents = _device_view(x.ents, 16 * int(x.n_ents)) if x.n_ents else torch.zeros(0, dtype=torch.uint8, device=dev)
-    on = dev if backend == "nccl" else torch.device("cpu")
-    ne = torch.tensor([int(x.n_ents)], dtype=torch.int64, device=on)
-    ne_all = torch.empty(world, dtype=torch.int64, device=on)
-    dist.all_gather_into_tensor(ne_all, ne)
-    ne_host = ne_all.cpu().tolist()
-    maxe = max(1, max(ne_host))
-    c_all = torch.empty(world * n, dtype=torch.int32, device=on)
-    dist.all_gather_into_tensor(c_all, counts.to(on))
-    pad = torch.zeros(16 * maxe, dtype=torch.uint8, device=on)
-    pad[:ents.numel()] = ents.to(on)
-    e_all = torch.empty(world * 16 * maxe, dtype=torch.uint8, device=on)
-    dist.all_gather_into_tensor(e_all, pad)
+    c_all, recv, ne_host, mine = exchange_exact(counts.to(on), ents.to(on))
     if on.type != "cuda":
-        c_all, e_all = c_all.to(dev), e_all.to(dev)
+        c_all = c_all.to(dev)
+        recv = {r: t.to(dev) for r, t in recv.items()}
     out = []
     for r in range(world):
         if r == rank:
             continue
-        out.append(XList(n, r, c_all[r * n:].data_ptr() if n else None, e_all[r * 16 * maxe:].data_ptr(), ne_host[r]))
-    return out, (c_all, e_all)
+        out.append(XList(n, r, c_all[r * n:].data_ptr() if n else None,
+                         recv[r].data_ptr() if ne_host[r] else None, ne_host[r]))
+    return out, (c_all, recv, mine)
 
 
 def finalize(backend):

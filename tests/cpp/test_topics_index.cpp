@@ -13,6 +13,7 @@
 #include "topics_index.h"
 
 #include <atomic>
+#include <chrono>
 #include <future>
 #include <random>
 #include <thread>
@@ -329,12 +330,36 @@ static void TestChurnRecyclesIds() {
 
 // Readers and updates at once: matches run while other threads subscribe, unsubscribe and
 // churn client ids; every result names only strings the index has held, and the final state
-// matches exactly.
+// matches exactly. Liveness: three readers match back to back (their span results overlap all
+// the time), yet every update must finish within kUpdateDeadline (the handle lock prefers a
+// waiting update over new readers, as Go's RWMutex does); a watchdog prints every thread's
+// progress and fails the run if the test has not finished after kWatchdog.
 static void TestConcurrentReadersAndUpdates() {
+  using clk = std::chrono::steady_clock;
+  constexpr auto kUpdateDeadline = std::chrono::seconds(5);
+  constexpr auto kWatchdog = std::chrono::seconds(20);
   TopicsIndex ix;
   for (int i = 0; i < 200; i++) ix.Subscribe("base" + std::to_string(i % 40), S("s/" + std::to_string(i % 10) + "/+", 1));
-  std::atomic<bool> stop{false};
-  std::atomic<int> bad{0};
+  std::atomic<bool> stop{false}, done{false};
+  std::atomic<int> bad{0}, late{0};
+  std::atomic<long> progress[5];
+  std::atomic<long> worst_us{0};
+  for (auto& p : progress) p = 0;
+  std::thread watchdog([&] {
+    const auto t0 = clk::now();
+    while (!done) {
+      if (clk::now() - t0 > kWatchdog) {
+        std::fprintf(stderr, "TestConcurrentReadersAndUpdates: stalled after %lld s; progress: readers %ld %ld %ld, "
+                             "updaters %ld %ld of 400\n",
+                     (long long)std::chrono::duration_cast<std::chrono::seconds>(kWatchdog).count(),
+                     progress[0].load(), progress[1].load(), progress[2].load(), progress[3].load(),
+                     progress[4].load());
+        std::fflush(stderr);
+        std::_Exit(3);
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+  });
   std::vector<std::thread> th;
   for (int w = 0; w < 3; w++)
     th.emplace_back([&, w] {
@@ -344,22 +369,38 @@ static void TestConcurrentReadersAndUpdates() {
           if (kv.first.rfind("base", 0) != 0 && kv.first.rfind("tmp", 0) != 0) bad++;
         for (auto& kv : res[1].Subscriptions)
           if (kv.first.rfind("tmp", 0) != 0) bad++;
+        progress[w]++;
       }
     });
   for (int u = 0; u < 2; u++)
     th.emplace_back([&, u] {
+      auto timed = [&](auto&& f) {
+        const auto t0 = clk::now();
+        f();
+        const auto dt = clk::now() - t0;
+        const long us = (long)std::chrono::duration_cast<std::chrono::microseconds>(dt).count();
+        for (long w = worst_us.load(); us > w && !worst_us.compare_exchange_weak(w, us);) {
+        }
+        if (dt > kUpdateDeadline) late++;
+      };
       for (int i = 0; i < 400; i++) {
         const std::string c = "tmp" + std::to_string(u) + "_" + std::to_string(i);
-        ix.Subscribe(c, S("t/" + std::to_string(i % 7)));
-        ix.Subscribe(c, S("s/" + std::to_string(i % 10) + "/+"));
-        ix.Unsubscribe("t/" + std::to_string(i % 7), c);
-        ix.Unsubscribe("s/" + std::to_string(i % 10) + "/+", c);
+        timed([&] { ix.Subscribe(c, S("t/" + std::to_string(i % 7))); });
+        timed([&] { ix.Subscribe(c, S("s/" + std::to_string(i % 10) + "/+")); });
+        timed([&] { ix.Unsubscribe("t/" + std::to_string(i % 7), c); });
+        timed([&] { ix.Unsubscribe("s/" + std::to_string(i % 10) + "/+", c); });
+        progress[3 + u]++;
       }
     });
   th[3].join();
   th[4].join();
   stop = true;
   for (int w = 0; w < 3; w++) th[w].join();
+  done = true;
+  watchdog.join();
+  std::fprintf(stderr, "  readers matched %ld batches during 3200 updates; slowest update %.1f ms\n",
+               progress[0].load() + progress[1].load() + progress[2].load(), worst_us.load() / 1000.0);
+  REQUIRE(late == 0);
   REQUIRE(bad == 0);
   for (int k = 0; k < 10; k++) REQUIRE(ix.Subscribers_("s/" + std::to_string(k) + "/x").Subscriptions.size() == 4);
   REQUIRE(ix.Subscribers_("t/1").Subscriptions.empty());

@@ -69,3 +69,51 @@ def test_two_rank_gloo_partition():
         tb, to = W.gen_topics(w, 300, seed=D.topic_seed(r))
         ref.append(orc.digest_batch(tb, to, nthreads=1)[0])
     assert got == np.concatenate(ref).tolist()
+
+
+def _xworker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "mqtt-server_amd"))
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MQ_DIST_BACKEND="gloo")
+    import torch
+    from mqmatch import dist as D
+    backend = D.init(rank)
+    n = 7
+    # rank r exports r * 5 entries (rank 0 none): uneven sizes, one rank empty
+    counts = torch.tensor([(rank * 5 * (t + 1)) // 28 - (rank * 5 * t) // 28 for t in range(n)], dtype=torch.int32)
+    ents = torch.arange(16 * rank * 5, dtype=torch.int64).to(torch.uint8) + rank
+    c_all, recv, ne, _ = D.exchange_exact(counts, ents)
+    D.barrier(backend)
+    out.put((rank, c_all.tolist(), {r: t.tolist() for r, t in recv.items()}, ne))
+    D.finalize(backend)
+
+
+def test_exact_size_exchange_three_ranks():
+    """dist.exchange_exact (the sharded mode's cross-shard list exchange): counts all-gathered,
+    entries moved with grouped point-to-point ops of exactly each rank's size (uneven, one rank
+    exporting nothing)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xworker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, c_all, recv, ne = q.get(timeout=240)
+        res[rank] = (c_all, recv, ne)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 7
+    want_counts = []
+    for r in range(world):
+        want_counts += [(r * 5 * (t + 1)) // 28 - (r * 5 * t) // 28 for t in range(n)]
+    for rank, (c_all, recv, ne) in res.items():
+        assert ne == [0, 5, 10]
+        assert c_all == want_counts
+        assert sorted(recv) == [r for r in range(world) if r != rank]
+        for r, got in recv.items():
+            assert got == [(i + r) % 256 for i in range(16 * r * 5)]

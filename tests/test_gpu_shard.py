@@ -16,8 +16,12 @@ from digest import engine_digest_parts, fold_parts
 pytestmark = pytest.mark.gpu
 
 
-def _sharded_digests(shards, tb, to):
+def _sharded_digests(shards, tb, to, device=False):
+    """device=False: host results (mq_match_spans_end_host, per-topic patches); True: device
+    results (mq_match_spans_end, merge sets' patches referenced and translated as a device
+    consumer would)."""
     import torch
+    from mqmatch import engine as E
     n = len(to) - 1
     d_tb = torch.from_numpy(tb).cuda()
     d_to = torch.from_numpy(to.view(np.int64)).cuda()
@@ -25,7 +29,11 @@ def _sharded_digests(shards, tb, to):
     counts = np.zeros((n, 4), np.int64)
     sums = np.zeros((n, 4), np.uint64)
     for k, e in enumerate(shards):
-        res = e.match_spans_end_expanded([x for j, x in enumerate(xs) if j != k], n)
+        foreign = [x for j, x in enumerate(xs) if j != k]
+        if device:
+            res = E.expand_device_spans(e.match_spans_end(foreign), n)
+        else:
+            res = e.match_spans_end_expanded(foreign, n)
         c, s = engine_digest_parts(res)
         counts += c
         with np.errstate(over="ignore"):
@@ -48,13 +56,13 @@ def _build(n_shards, w, extra):
     return shards, orc
 
 
-@pytest.mark.parametrize("n_shards", [2, 3])
-def test_sharded_workload_parity(n_shards, gpu_available):
+@pytest.mark.parametrize("n_shards,device", [(2, False), (3, False), (3, True)])
+def test_sharded_workload_parity(n_shards, device, gpu_available):
     from mqmatch import workload as W
     w = W.gen_subscriptions(120000, 6000, seed=81)
     shards, orc = _build(n_shards, w, [])
     tb, to = W.gen_topics(w, 6000, seed=82)
-    dg, cnt, n_ents = _sharded_digests(shards, tb, to)
+    dg, cnt, n_ents = _sharded_digests(shards, tb, to, device=device)
     od, ocnt, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
     assert (cnt == ocnt).all()
     bad = np.nonzero(dg != od)[0]
@@ -64,7 +72,27 @@ def test_sharded_workload_parity(n_shards, gpu_available):
         e.check()
 
 
-def test_sharded_many_merging_clients(gpu_available):
+@pytest.mark.parametrize("device", [False, True])
+def test_config3_eight_shards(device, gpu_available):
+    """Config 3 in its stated form on one GPU: the config-3 mix at 1M
+    subscriptions sharded by filter hash over 8 shard handles, every shard matching the full
+    4096-topic batch, the exported cross-shard lists exchanged, merge-set dedup on every shard
+    (sets keyed by the local merge gathers and the other shards' entries). The shards' disjoint
+    results add up to the oracle's digests, bit for bit, with host and device results."""
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(1_000_000, 100_000, seed=W.BASE_SEED)
+    shards, orc = _build(8, w, [])
+    tb, to = W.gen_topics(w, 4096, seed=W.BASE_SEED)
+    dg, cnt, n_ents = _sharded_digests(shards, tb, to, device=device)
+    od, ocnt, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+    assert (cnt == ocnt).all()
+    bad = np.nonzero(dg != od)[0]
+    assert len(bad) == 0, f"{len(bad)} topics differ, first {bad[:5]}"
+    assert n_ents > 0 and cnt[:, 1].sum() > 0
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_sharded_many_merging_clients(device, gpu_available):
     """Clients whose co-matching filters are spread over the shards: bases, max Qos, OR'd NoLocal
     and identifier rows decided across shards (the rank keys order them)."""
     from mqmatch import engine as E
@@ -83,7 +111,7 @@ def test_sharded_many_merging_clients(gpu_available):
             o.subscribe(f"c{c}", f, q, ident, nl, client_id=c, filter_id=fid[f])
     topics = ["a/b/c/d", "a/b/c", "a/x/c/d", "$SYS/b/c/d", "a/b/c/d/e", "q", "a", "x/b/c/d"]
     tb, to = E.pack_strings(topics)
-    dg, cnt, _ = _sharded_digests(shards, tb, to)
+    dg, cnt, _ = _sharded_digests(shards, tb, to, device=device)
     od, ocnt, _ = o.digest_batch(tb, to, nthreads=4)
     assert (cnt == ocnt).all() and (dg == od).all()
 

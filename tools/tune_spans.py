@@ -54,7 +54,8 @@ def main():
             prof = eng.profile_read()
             eng.profile(False)
             print(json.dumps({"config": c, "rep": rep, "subs": args.subs, "ms_per_step": ms,
-                              "kernels_ms": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0}}),
+                              "kernels_ms": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
+                              "counters": {k: v[0] / args.steps for k, v in prof.items() if v[1] == 0}}),
                   flush=True)
 
 
