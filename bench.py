@@ -64,14 +64,19 @@ def _device_view(ptr, nbytes):
     return torch.as_tensor(_Buf(), device="cuda")
 
 
+def affinity_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def host_cores():
     """Host threads for the CPU baseline: every core this process may use (the GOMAXPROCS
-    analogue), capped by OMP_NUM_THREADS where the machine sets a per-job share (the GPU box
-    allots 16 host threads per GPU and sets it to 16)."""
-    try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:
-        n = os.cpu_count() or 1
+    analogue), capped by OMP_NUM_THREADS where the machine sets this job's share of a shared
+    host (the GPU box shows all of its CPUs to every job but allots 16 per GPU, sets
+    OMP_NUM_THREADS=16 and asks that worker pools stay within it)."""
+    n = affinity_cpus()
     cap = os.environ.get("OMP_NUM_THREADS", "")
     if cap.isdigit() and int(cap) > 0:
         n = min(n, int(cap))
@@ -131,7 +136,8 @@ def read_walk_traffic(path, n_subs, n_topics):
     try:
         with open(path) as f:
             e = json.load(f).get("walk", {}).get(str(n_subs))
-        if e is None or int(e["topics"]) != n_topics or int(e.get("edge_load", 2)) != engine_option(13, 4):
+        if (e is None or int(e["topics"]) != n_topics or int(e.get("edge_load", 2)) != engine_option(13, 4)
+                or int(e.get("walk_group", 0)) != engine_option(15, 16)):
             return None
         return float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError, TypeError):
@@ -147,7 +153,7 @@ def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step):
     below streaming bandwidth."""
     launches, ms = prof.get("walk", (0, 0.0))
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-            "traffic": None, "kernel": "k_walk (count pass, gathers only)",
+            "traffic": None, "kernel": "k_walkf (frontier walk, 16 lanes per topic, count pass)",
             "bytes": "8 B per level + 4 B offset + 16 B per child lookup (SURVEY 8d: 8L + 4 + 16P) + 4 B per gather word"}
     if not launches or ms <= 0 or per_topic is None:
         return roof
@@ -478,8 +484,14 @@ def main():
         secs, _ = fast.bench_subscribers(tb, to[:cal + 1], cores)
         m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
         secs, _ = fast.bench_subscribers(tb, to[:m + 1], cores)
+        # one thread on a short sample: the per-core rate (the restatement scales with threads: a
+        # shared frozen index, no locks), for reading the baseline against a whole host
+        m1 = int(min(n, max(64, (m / max(cores, 1)) * min(3.0, args.cpu_seconds / 5) / max(args.cpu_seconds, 1e-6))))
+        secs1, _ = fast.bench_subscribers(tb, to[:m1 + 1], 1)
         cpu = {"value": m / secs, "unit": "publishes/s", "cores": cores, "kind": "port",
-               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": affinity_cpus(),
+               "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+               "single_thread": {"value": m1 / secs1, "sample_topics": m1},
                "sample": f"first {m} topics of the rank-0 batch on the same {args.subs}-subscription index, "
                          f"{cores} threads (std::thread, shared frozen index), Subscribers() per topic: the "
                          f"fast CPU restatement of the Go particle trie (oracle/topics_fast.cpp: interned "

@@ -430,29 +430,15 @@ int mq_index_check(mq_index* idx);
    compares it with the host mirror. Returns 0, or MQ_EIO with the first difference. */
 int mq_device_check(mq_index* idx);
 
-/* Engine options (tuning; the defaults are the product). Returns 0 or MQ_EINVAL. */
-#define MQ_OPT_CHUNK_ROWS 1      /* row format: output rows per chunk (default 0xF0000000) */
-#define MQ_OPT_SUBBATCH_TOPICS 2 /* row format: topics per pipelined sub-batch */
-#define MQ_OPT_MSG_SPEC_MB 3     /* Messages: speculative-count scratch budget (MiB; 0: two walks) */
-#define MQ_OPT_MSG_WAVES 4       /* Messages: k_msg waves per SIMD (1, 6, 8; 0: by index size) */
-#define MQ_OPT_SERIAL 5          /* 1: no side-stream overlap (isolated kernel timings) */
-#define MQ_OPT_PATCH_CAP 6       /* span format: initial patch pool capacity (patches) */
-#define MQ_OPT_MERGE_WAVES 7     /* k_merge waves per SIMD the registers are budgeted for (1, 6, 8) */
-#define MQ_OPT_MSG_IMAGE 8       /* Messages: 1 (default) runs over the level-order retained image;
-                                    0 walks the particles (the path the Q6 state always takes) */
-#define MQ_OPT_WALK_WAVES 9       /* k_walk count pass waves per SIMD the registers are budgeted for (1, 8;
-                                     16: the shared-load walk k_walku, span format without lists) */
-#define MQ_OPT_WALK_LISTS 10      /* span format: 1 makes the walk count the lists (as the row format) */
-#define MQ_OPT_MERGE_DEDUP 12     /* span format: 1 finds topics with the same merge gathers (counter
-                                     "merge_sets" under MQ_PROF_TIMES) */
-#define MQ_OPT_FUSE_DESC 11       /* span format, index not sharded: 1 has k_merge do k_desc's work (slower; off) */
-#define MQ_OPT_SET_GRID 14        /* merge-set dedup: 1 (default): a wavefront per set (the host reads the set
-                                     count); 0: persistent waves striding the set list */
+/* Engine options. The defaults are the product; these three trade memory for speed or size a
+ * pool up front. Returns 0, or MQ_EINVAL for an unknown option or value. The measurement and
+ * tuning knobs the benchmarks use (kernel variants, register budgets, synchronisation modes) are
+ * in mqmatch_dev.h: development options, not part of the ABI's contract. */
+#define MQ_OPT_CHUNK_ROWS 1       /* row format: output rows per chunk (default 0xF0000000) */
+#define MQ_OPT_PATCH_CAP 6        /* span format: initial patch pool capacity (patches) */
 #define MQ_OPT_EDGE_LOAD 13       /* edge table: at most 1/v of its slots used (2, 4 = default, 8: sparser means
                                      shorter probe chains for the walk, more memory; a table of 2^30 slots or
                                      more keeps 1/2); applies from the next growth */
-#define MQ_OPT_WALK_GROUP 15       /* the match walk: 16 (default), 8 or 4 lanes per topic (level-synchronous
-                                     frontier walk); 0: thread per topic (stackless DFS) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. enable: 0 off,

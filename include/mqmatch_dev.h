@@ -1,0 +1,30 @@
+/*
+ * mqmatch_dev.h — development and measurement options of the engine (mq_set_option, declared in
+ * mqmatch.h). They select kernel variants and synchronisation modes for A/B measurements and
+ * tuning sweeps (tools/tune_spans.py, tools/gpu/); the defaults are the product configuration
+ * and a broker never sets them. No functions are declared here.
+ */
+#ifndef MQMATCH_DEV_H
+#define MQMATCH_DEV_H
+
+#define MQ_OPT_SUBBATCH_TOPICS 2  /* row format: topics per pipelined sub-batch */
+#define MQ_OPT_MSG_SPEC_MB 3      /* Messages: speculative-count scratch budget (MiB; 0: two walks) */
+#define MQ_OPT_MSG_WAVES 4        /* Messages: k_msg waves per SIMD (1, 6, 8; 0: by index size) */
+#define MQ_OPT_SERIAL 5           /* 1: no side-stream overlap (isolated kernel timings) */
+#define MQ_OPT_MERGE_WAVES 7      /* k_merge waves per SIMD the registers are budgeted for (1, 6, 8) */
+#define MQ_OPT_MSG_IMAGE 8        /* Messages: 1 (default) runs over the level-order retained image;
+                                     0 walks the particles (the path the Q6 state always takes) */
+#define MQ_OPT_WALK_WAVES 9       /* thread-per-topic k_walk: waves per SIMD the registers are budgeted for (1, 8) */
+#define MQ_OPT_WALK_LISTS 10      /* span format: 1 makes the walk count the lists (as the row format) */
+#define MQ_OPT_MERGE_DEDUP 12     /* span format: 1 (default) resolves topics with the same merge gathers once
+                                     (merge sets); 0: every topic resolves itself (a cross-check) */
+#define MQ_OPT_SET_GRID 14        /* merge-set dedup: 1 (default): a wavefront per set; 0: persistent waves
+                                     striding the set list */
+#define MQ_OPT_WALK_GROUP 15      /* the match walk: 16 (default), 8 or 4 lanes per topic (level-synchronous
+                                     frontier walk, k_walkf); 0: thread per topic (stackless DFS, k_walk) */
+#define MQ_OPT_ONE_SYNC 16        /* span format, device results: 1 (default) runs a batch with one host
+                                     synchronisation, at its end (buffers sized by earlier batches; a batch
+                                     they cannot hold runs again, sized by the host); 0: the host reads the
+                                     walk's totals and the patch counts between kernels */
+
+#endif

@@ -1,5 +1,6 @@
 // Device side of the engine (device.h): HBM mirror + batch pipeline.
 #include "device.h"
+#include "mqmatch_dev.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -107,11 +108,7 @@ void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
   }
   const size_t pp = Mirror<T>::per_page();
   const size_t npages = (n + pp - 1) / pp;
-  if (!full) {  // mostly dirty: one plain copy
-    size_t dp = 0;
-    for (size_t w = 0; w < m.dirty.size(); w++) dp += (size_t)__builtin_popcountll(m.dirty[w]);
-    full = dp * 4 > npages * 3;
-  }
+  if (!full) full = m.dirty_pages * 4 > npages * 3;  // mostly dirty: one plain copy
   if (full) {
     // pieces of at most 1 GiB: one pageable H2D copy of a multi-GiB array (the 100M-retained
     // image has 10 GB arrays) is not relied on
@@ -122,24 +119,35 @@ void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
                 "H2D mirror");
     *uploaded += bytes;
   } else {
-    size_t p = 0;
-    while (p < npages) {  // runs of consecutive dirty pages; clean words are skipped whole
-      const size_t w = p / 64;
-      if (w >= m.dirty.size()) break;
-      const uint64_t bits = m.dirty[w] >> (p % 64);
-      if (!bits) {
-        p = (w + 1) * 64;
-        continue;
+    // runs of consecutive dirty pages, from the listed bitmap words in address order
+    std::sort(m.dirty_words.begin(), m.dirty_words.end());
+    size_t ra = 0, rb = 0;  // the open run: pages [ra, rb)
+    auto flush = [&] {
+      const size_t a = ra * pp, b = std::min(n, rb * pp);
+      if (a < b) {
+        st.add(d + a, m.h.data() + a, (b - a) * sizeof(T));
+        *uploaded += (b - a) * sizeof(T);
       }
-      p += (size_t)__builtin_ctzll(bits);
-      if (p >= npages) break;
-      size_t q = p + 1;
-      while (q < npages && q / 64 < m.dirty.size() && ((m.dirty[q / 64] >> (q % 64)) & 1)) q++;
-      const size_t a = p * pp, b = std::min(n, q * pp);
-      st.add(d + a, m.h.data() + a, (b - a) * sizeof(T));
-      *uploaded += (b - a) * sizeof(T);
-      p = q;
+      ra = rb = 0;
+    };
+    for (uint32_t w : m.dirty_words) {
+      uint64_t bits = m.dirty[w];
+      while (bits) {
+        const uint32_t lo = (uint32_t)__builtin_ctzll(bits);
+        const uint64_t x = bits >> lo;
+        const uint32_t len = ~x ? (uint32_t)__builtin_ctzll(~x) : 64u - lo;
+        const size_t pa = (size_t)w * 64 + lo, pb = pa + len;
+        if (rb != 0 && pa == rb) {
+          rb = pb;
+        } else {
+          flush();
+          ra = pa;
+          rb = pb;
+        }
+        bits = lo + len >= 64 ? 0ull : bits & ~(((1ull << len) - 1) << lo);
+      }
     }
+    flush();
   }
   m.clear_dirty();
 }
@@ -244,9 +252,9 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_MERGE_WAVES: merge_wpe_opt_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_WAVES: walk_wpe_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_LISTS: walk_lists_ = v != 0; return true;
-    case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
     case MQ_OPT_MERGE_DEDUP: dedup_ = (uint32_t)v; return true;
     case MQ_OPT_SET_GRID: set_grid_ = (uint32_t)v; return true;
+    case MQ_OPT_ONE_SYNC: one_sync_ = v != 0; return true;
     case MQ_OPT_WALK_GROUP:
       if (v != 0 && v != 4 && v != 8 && v != 16) return false;
       walk_group_ = (uint32_t)v;
@@ -711,6 +719,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
 
     // every topic's gathers become GDesc records and k_copy tile starts, in one launch
     DescArgs da;
+    memset(&da, 0, sizeof(da));
     da.ix = di;
     da.n = q.n;
     da.gather_stride = gstride;
@@ -723,6 +732,9 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     da.spans = nullptr;
     da.inl_out = nullptr;
     da.tc_out = nullptr;
+    da.msig = nullptr;
+    da.mrank = nullptr;
+    da.unsafe = nullptr;
     prof.begin(s);
     launch_desc(da, false, s);
     prof.end("desc", s);
@@ -737,6 +749,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       const TopicOff& lo = hb[c.b0];
       const TopicOff& hi = hb[c.b1];
       EmitArgs a;
+      memset(&a, 0, sizeof(a));  // (every field the row format does not use: null / zero)
       a.ix = di;
       a.t0 = c.b0 * kScanBlock;
       a.t1 = std::min<uint64_t>(q.n, (uint64_t)c.b1 * kScanBlock);
@@ -767,7 +780,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
       }
       prof.begin(ms);
-      launch_merge(a, false, false, merge_wpe_opt_ ? merge_wpe_opt_ : 1u, merge_blocks_, ms);
+      launch_merge(a, false, merge_wpe_opt_ ? merge_wpe_opt_ : 1u, merge_blocks_, ms);
       prof.end("merge", ms);
       hip_check(hipGetLastError(), "k_merge");
       const uint32_t nt = a.t1 - a.t0;
@@ -851,7 +864,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
 }
 
 TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                           const uint32_t** gathers, uint32_t* gstride, bool lists) {
+                           const uint32_t** gathers, uint32_t* gstride, bool lists, bool one_sync) {
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
   grow(counts_, (size_t)n * sizeof(TopicCount));
   grow(offs_, (size_t)(n + 1) * sizeof(TopicOff));
@@ -872,16 +885,26 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   prof.begin(s);
   if (front)
     launch_walk_front(walk_group_, lists, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(),
-                      ovf_.as<uint32_t>(), fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, s);
+                      ovf_.as<uint32_t>(), fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, s, one_sync);
   else
     launch_walk(false, lists, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(),
-                ovf_.as<uint32_t>(), s);
+                ovf_.as<uint32_t>(), s, one_sync);
   prof.end("walk", s);
   hip_check(hipGetLastError(), "k_walk<count>");
   prof.begin(s);
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
   prof.end("scan", s);
   hip_check(hipGetLastError(), "k_scan");
+  if (one_sync) {  // read at the batch's end; the gather slots are the gather lists
+    hip_check(hipMemcpyAsync(&h_fast_->tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s),
+              "D2H totals");
+    hip_check(hipMemcpyAsync(&h_fast_->ovf, ovf_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H overflow");
+    if (front) hip_check(hipMemcpyAsync(&h_fast_->fallback, fb_cnt_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+    *gathers = gslots_.as<uint32_t>();
+    *gstride = kGatherCap;
+    prof.count("topics", n);
+    return TopicOff{0, 0, 0, 0, 0};
+  }
   hip_check(hipMemcpyAsync(h_tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H totals");
   hip_check(hipMemcpyAsync(h_ovf, ovf_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H overflow");
   if (front && prof.on())
@@ -913,12 +936,15 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
 void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                          HostSpans* host, mq_span_result* out) {
   mq_xlist x;
-  spans_begin(ix, d_tb, d_to, n, s, &x);
+  spans_begin(ix, d_tb, d_to, n, s, &x, one_sync_ && !host);
+  if (spans_end(ix, nullptr, 0, s, host, out)) return;
+  // the one-sync run's buffers did not hold the batch: again, sized by the host
+  spans_begin(ix, d_tb, d_to, n, s, &x, false);
   spans_end(ix, nullptr, 0, s, host, out);
 }
 
 void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                         mq_xlist* x) {
+                         mq_xlist* x, bool one_sync) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   sync(ix, s);
   memset(x, 0, sizeof(*x));
@@ -929,7 +955,20 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     err_.ensure(2 * sizeof(uint32_t));
     hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
   }
-  check_err(s);  // faults flagged by an earlier row-format batch
+  // The walk counts only gathers when nothing needs the lists' totals before k_desc: no inline
+  // rows to place and no device share pick (k_desc<true> then counts rows / shared / merge).
+  const bool lists = walk_lists_ || select_shared_ || ix.inl.live != 0;
+  // One host synchronisation for the whole batch (at its end): device results of an index that is
+  // not sharded, without inline rows or a device share pick (whose buffers the walk's totals size)
+  one_sync = one_sync && !ix.sharded() && !lists && dedup_ != 0 && set_grid_;
+  if (one_sync) {
+    if (!h_fast_) h_fast_ = static_cast<FastBack*>(pinned_alloc(sizeof(FastBack)));
+    if (!unsafe_.p) unsafe_.ensure(sizeof(uint32_t));
+    memset(h_fast_, 0, sizeof(FastBack));
+    hip_check(hipMemsetAsync(unsafe_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(unsafe)");
+  } else {
+    check_err(s);  // faults flagged by an earlier row-format batch (one-sync batches read it at their end)
+  }
   const DevIndex di = dev_index(ix);
   sb_.pending = true;
   sb_.n = n;
@@ -940,18 +979,17 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
 
   const uint32_t* gathers = nullptr;
   uint32_t gstride = 0;
-  // The walk counts only gathers when nothing needs the lists' totals before k_desc: no inline
-  // rows to place and no device share pick (k_desc<true> then counts rows / shared / merge).
-  sb_.lists = walk_lists_ || select_shared_ || ix.inl.live != 0;
-  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists);
+  sb_.lists = lists;
+  sb_.one_sync = one_sync;
+  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, one_sync);
   sb_.tot = tot;
   sb_.gathers = gathers;
   sb_.gstride = gstride;
-  // An index that is not sharded has k_merge do k_desc's work (k_xlist reads GDesc records)
-  sb_.fused = !ix.sharded() && fuse_desc_;
-  if (!sb_.lists && !sb_.fused) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
-  grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
-  grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
+  if (!sb_.lists) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
+  if (!one_sync) {  // (one-sync: the buffers as earlier batches left them; the kernels check)
+    grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
+    grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
+  }
   grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
   grow(sp_res_, (size_t)n * sizeof(TopicSpansDev));
   if (select_shared_) grow(sp_picked_, std::max<uint64_t>(tot.shr, 1) * sizeof(ShrRec));
@@ -963,6 +1001,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   }
 
   DescArgs da;
+  memset(&da, 0, sizeof(da));
   da.ix = di;
   da.n = n;
   da.gather_stride = gstride;
@@ -974,16 +1013,19 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   da.tiles = nullptr;
   da.spans = sp_spans_.as<SpanRec>();
   da.inl_out = sp_inl_.as<InlRec>();
-  da.tc_out = sb_.lists || sb_.fused ? nullptr : sp_tc_.as<TopicCount>();
+  da.tc_out = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
   da.msig = nullptr;
   da.mcount = nullptr;
   da.mlist = nullptr;
   da.mrow = nullptr;
   da.mpair = nullptr;
   da.mrank = nullptr;
+  da.spans_cap = sp_spans_.bytes / sizeof(SpanRec);
+  da.desc_cap = desc_[0].bytes / sizeof(GDesc);
+  da.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
   // merge-set dedup (on a sharded index too: a set is then also the other shards' entries,
   // which spans_end knows after the exchange)
-  sb_.dedup = dedup_ != 0 && !sb_.fused;
+  sb_.dedup = dedup_ != 0;
   if (sb_.dedup) {
     grow(dd_sig_, (size_t)n * sizeof(uint64_t));
     grow(dd_cnt_, (size_t)n * sizeof(uint32_t));
@@ -1001,12 +1043,10 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     }
   }
   sb_.tc = da.tc_out;
-  if (!sb_.fused) {
-    prof.begin(s);
-    launch_desc(da, true, s);
-    prof.end("desc", s);
-    hip_check(hipGetLastError(), "k_desc<spans>");
-  }
+  prof.begin(s);
+  launch_desc(da, true, s);
+  prof.end("desc", s);
+  hip_check(hipGetLastError(), "k_desc<spans>");
   if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
@@ -1032,7 +1072,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   }
 }
 
-void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host,
+bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host,
                        mq_span_result* out) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   memset(out, 0, sizeof(*out));
@@ -1042,7 +1082,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   if (ix.version() != sb_.version) throw HipError{hipErrorInvalidValue, "index updated between spans_begin and spans_end"};
   const DevIndex di = sb_.di;
   const uint32_t n = sb_.n;
-  const TopicOff tot = sb_.tot;
+  TopicOff tot = sb_.tot;
   out->sub_pool = reinterpret_cast<const mq_client_row*>(di.subs);
   out->shared_pool = reinterpret_cast<const mq_shared_row*>(di.shr);
   out->sub_pool_len = ix.subs.m.size();
@@ -1050,7 +1090,8 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   out->flags = select_shared_ ? MQ_SPANS_PICKED : 0u;
   if (nf > kMaxShards - 1) throw HipError{hipErrorInvalidValue, "more foreign lists than kMaxShards - 1"};
   if (nf && !ix.sharded()) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
-  if (n == 0) return;
+  if (n == 0) return true;
+  const bool one_sync = sb_.one_sync;
 
   EmitArgs a;
   memset(&a, 0, sizeof(a));
@@ -1084,6 +1125,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
 
     hip_check(hipMemsetAsync(dd_nsets_.p, 0, 2 * sizeof(unsigned long long), s), "memset");
     DedupArgs dd;
+    memset(&dd, 0, sizeof(dd));
     dd.n = n;
     dd.msig = dd_sig_.as<uint64_t>();
     dd.mcount = dd_cnt_.as<uint32_t>();
@@ -1126,7 +1168,11 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.end("dedup", s);
     hip_check(hipGetLastError(), "k_dedup");
     sb_.n_sets = 0;
-    if (prof.on() || set_grid_) {
+    if (one_sync) {  // the set count is read at the batch's end; the set pass strides over it
+      hip_check(hipMemcpyAsync(h_fast_->n_sets, dd_nsets_.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
+                "D2H");
+      sb_.n_sets = last_sets_ + last_sets_ / 8 + 256;  // the grid: the last batch's count, with room
+    } else if (prof.on() || set_grid_) {
       unsigned long long two[2] = {0, 0};
       hip_check(hipMemcpyAsync(two, dd_nsets_.p, sizeof(two), hipMemcpyDeviceToHost, s), "D2H");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -1146,10 +1192,7 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.inl_rows = sp_inl_.as<InlRec>();
   a.sres = sp_res_.as<TopicSpansDev>();
   a.pcount = sp_pcount_.as<unsigned long long>();
-  a.tc = sb_.lists || sb_.fused ? nullptr : sp_tc_.as<TopicCount>();
-  a.gathers = sb_.gathers;
-  a.gather_stride = sb_.gstride;
-  a.spans = sp_spans_.as<SpanRec>();
+  a.tc = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
   a.work = nullptr;
   if (prof.work()) {  // [0]: the topics' pass, [1]: the merge sets' pass (dedup)
     grow(sp_work_, 2 * kPatchRegions * kWork * sizeof(unsigned long long));
@@ -1161,6 +1204,8 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.tslot = nullptr;
   a.dd_phase = 0;
   a.mrank = ix.sharded() && sb_.dedup ? dd_mrank_.as<uint64_t>() : nullptr;
+  a.desc_cap = desc_[0].bytes / sizeof(GDesc);
+  a.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
   pinned((2 * kPatchRegions + 1) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
   unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
@@ -1202,9 +1247,10 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       // persistent waves striding over the list
       const uint32_t set_blocks = set_grid_ ? std::max<uint32_t>(1, (uint32_t)((sb_.n_sets + 3) / 4))
                                             : (merge_blocks_ ? merge_blocks_ : n_cus_ * 8);
-      launch_merge(a, true, false, merge_wpe, set_blocks, s);
+      launch_merge(a, true, merge_wpe, set_blocks, s);
       prof.end("merge_sets", s);
       hip_check(hipGetLastError(), "k_merge<spans> (sets)");
+      if (one_sync) break;  // a reservation past its region sets *unsafe (read at the end)
       hip_check(hipMemcpyAsync(h_pc, a.spcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
                 "D2H");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -1248,9 +1294,10 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
     prof.begin(s);
     // after k_finish the waves stride over its list (its length is on the device)
-    launch_merge(a, true, sb_.fused, merge_wpe, a.wave_list && !merge_blocks_ ? n_cus_ * 8 : merge_blocks_, s);
+    launch_merge(a, true, merge_wpe, a.wave_list && !merge_blocks_ ? n_cus_ * 8 : merge_blocks_, s);
     prof.end("merge", s);
     hip_check(hipGetLastError(), "k_merge<spans>");
+    if (one_sync) break;  // as the set pass
     hip_check(hipMemcpyAsync(h_pc, a.pcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
               "D2H pcount");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -1283,6 +1330,24 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     launch_pick(pa, s);
     prof.end("pick", s);
     hip_check(hipGetLastError(), "k_pick<spans>");
+  }
+  if (one_sync) {  // the batch's one synchronisation: totals, overflow, unsafe bits, errors
+    hip_check(hipMemcpyAsync(&h_fast_->unsafe, unsafe_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+    hip_check(hipMemcpyAsync(&h_fast_->err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (h_fast_->err) check_err(s);  // throws with the tripped guard's name
+    if (h_fast_->ovf || h_fast_->unsafe) {
+      prof.count("one_sync_retries", 1);
+      return false;
+    }
+    tot = h_fast_->tot;
+    sb_.tot = tot;
+    last_sets_ = h_fast_->n_sets[0] + h_fast_->n_sets[1];
+    if (prof.on()) {
+      prof.count("gathers", tot.g);
+      prof.count("dedup_sets", last_sets_);
+      if (walk_group_) prof.count("walk_fallback", h_fast_->fallback);
+    }
   }
   prof.count("patch_slots", n_patches);  // reserved; the written ones: merge_patches (MQ_PROF_WORK)
   prof.count("spans", tot.g);
@@ -1339,12 +1404,14 @@ void Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       hip_check(hipMemcpyAsync(host->picked.data(), sp_picked_.p, out->n_picked_rows * sizeof(ShrRec),
                                hipMemcpyDeviceToHost, s), "D2H");
   }
+  if (one_sync) return true;  // (checked above)
   hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   if (*h_err) check_err(s);  // throws with the tripped guard's name
   if (host)
     for (TopicSpansDev& t : host->topics)
       if (t.n_patches) t.patch_base = h_roff[t.patch_base / rcap_] + t.patch_base % rcap_;
+  return true;
 }
 
 void Device::acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb, const uint64_t* to,

@@ -169,8 +169,12 @@ class Device {
   // The same in two phases, for a sharded index: begin walks the batch and
   // exports the topics' gathered cross-shard nodes (device pointers in *x, valid until end);
   // the caller exchanges the lists between the shards; end merges with the other shards' lists.
-  void spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x);
-  void spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out);
+  // one_sync (match_spans only): the batch may run with one host synchronisation (at its end),
+  // its buffers sized by earlier batches; spans_end then returns false when they did not hold it
+  // and the caller runs the batch again without one_sync (host-sized buffers).
+  void spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x,
+                   bool one_sync = false);
+  bool spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
                 HostMsg* host, mq_msg_result* out);
@@ -200,8 +204,10 @@ class Device {
   DevIndex dev_index(const Index& ix) const;
   void check_err(hipStream_t s);
   // walk (count) + scan of n topics; returns the batch totals (synchronises s)
+  // (one_sync: the totals are not read back - the returned TopicOff is zero - and every topic's
+  // gather count is clamped to its slot; the totals are read at the batch's end)
   TopicOff walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                     const uint32_t** gathers, uint32_t* gstride, bool lists);
+                     const uint32_t** gathers, uint32_t* gstride, bool lists, bool one_sync = false);
   // Messages: the level-order retained image (rebuilt when ix.retained_version() moved) and the
   // two query paths — run arithmetic over the image (k_msgq) and the particle walk (k_msg:
   // the Q6 state, nesting beyond kMsgStack, MQ_OPT_MSG_IMAGE = 0)
@@ -280,13 +286,24 @@ class Device {
     TopicOff tot{0, 0, 0, 0, 0};
     DevIndex di{};
     bool lists = true;             // the walk counted the lists (else k_desc did, into sp_tc_)
-    bool fused = false;            // k_desc's work is done by k_merge (index not sharded)
     bool dedup = false;            // merge-set dedup ran (dd_rep_ holds the representatives)
     uint64_t n_sets = 0;           // their number, when read back (profiling, MQ_OPT_SET_GRID)
     const uint32_t* gathers = nullptr;
     uint32_t gstride = 0;
     TopicCount* tc = nullptr;      // k_desc's per-topic counts (walk without lists), or null
+    bool one_sync = false;         // one host synchronisation (spans_begin)
   } sb_;
+  // one-sync batches: values read back at the batch's end (pinned): the walk's totals, its
+  // overflow and fallback counts, the *unsafe bits, the error word and the merge-set counts
+  struct FastBack {
+    TopicOff tot;
+    uint32_t ovf, fallback, unsafe, err;
+    unsigned long long n_sets[2];
+  };
+  FastBack* h_fast_ = nullptr;
+  DevBuf unsafe_;
+  bool one_sync_ = true;      // MQ_OPT_ONE_SYNC
+  uint64_t last_sets_ = 0;    // merge sets of the last batch: the grid of the next set pass
   DevBuf sp_tc_;                     // per-topic counts from k_desc<true> (walk without lists)
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)
   uint64_t patch_cap_init_ = 1ull << 24;
@@ -304,7 +321,6 @@ class Device {
   uint32_t walk_wpe_ = 8;        // k_walk count pass register budget (MQ_OPT_WALK_WAVES)
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
   uint32_t walk_group_ = 16;     // frontier walk lanes per topic (MQ_OPT_WALK_GROUP; 0: k_walk)
-  bool fuse_desc_ = false;       // span format: k_merge does k_desc's work (MQ_OPT_FUSE_DESC)
   uint32_t dedup_ = 1;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
   uint32_t set_grid_ = 1;        // MQ_OPT_SET_GRID (10M: set pass 1.18 -> 1.05 ms against persistent waves)
   DevBuf dd_sig_, dd_cnt_, dd_list_, dd_mrow_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_, dd_rlist_;

@@ -62,11 +62,15 @@ void reserve_huge(std::vector<T>& v, size_t n) {
 template <class T>
 struct Mirror {
   // Dirty tracking granule: an update touches single records at random places, and each
-  // touched page is uploaded whole, so pages are small (<= 512 B, a power of two elements, so
-  // that page starts are 16-byte aligned); the device applies them by scatter (Device::sync).
-  static constexpr size_t kPageBytes = 512;
+  // touched page is uploaded whole, so pages are small (64 B: a power of two elements, at least
+  // one; page starts are 16-byte aligned); the device applies them by scatter (Device::sync). The
+  // bitmap's non-zero words are also listed, so a sync visits only those (a 10M-subscription
+  // edge table has a million bitmap words).
+  static constexpr size_t kPageBytes = 64;
   std::vector<T> h;
-  std::vector<uint64_t> dirty;  // bitmap of pages
+  std::vector<uint64_t> dirty;        // bitmap of pages
+  std::vector<uint32_t> dirty_words;  // its non-zero words, in marking order
+  size_t dirty_pages = 0;
   bool all_dirty = true;
   uint64_t epoch = 0;  // bumped when the host array is reallocated (device must realloc too)
 
@@ -78,16 +82,20 @@ struct Mirror {
   size_t size() const { return h.size(); }
   T& operator[](size_t i) { return h[i]; }
   const T& operator[](size_t i) const { return h[i]; }
-  void mark(size_t i) {
-    size_t p = i / per_page();
-    if (p / 64 >= dirty.size()) dirty.resize(p / 64 + 1, 0);
-    dirty[p / 64] |= 1ull << (p % 64);
+  void mark_page(size_t p) {
+    const size_t w = p / 64;
+    if (w >= dirty.size()) dirty.resize(std::max(w + 1, dirty.size() + dirty.size() / 2), 0);
+    const uint64_t bit = 1ull << (p % 64);
+    if (dirty[w] & bit) return;
+    if (!dirty[w]) dirty_words.push_back((uint32_t)w);
+    dirty[w] |= bit;
+    dirty_pages++;
   }
+  void mark(size_t i) { mark_page(i / per_page()); }
   void mark_range(size_t i, size_t n) {
     if (!n) return;
-    size_t p0 = i / per_page(), p1 = (i + n - 1) / per_page();
-    if (p1 / 64 >= dirty.size()) dirty.resize(p1 / 64 + 1, 0);
-    for (size_t p = p0; p <= p1; p++) dirty[p / 64] |= 1ull << (p % 64);
+    const size_t p0 = i / per_page(), p1 = (i + n - 1) / per_page();
+    for (size_t p = p0; p <= p1; p++) mark_page(p);
   }
   T& at_w(size_t i) {  // write access
     mark(i);
@@ -109,11 +117,13 @@ struct Mirror {
       all_dirty = true;
     }
     h.resize(n, fill);
-    mark_range(old, n - old);
+    if (!all_dirty) mark_range(old, n - old);  // (a whole upload is coming anyway)
   }
   void clear_dirty() {
     all_dirty = false;
-    dirty.assign(dirty.size(), 0);
+    for (uint32_t w : dirty_words) dirty[w] = 0;
+    dirty_words.clear();
+    dirty_pages = 0;
   }
 };
 

@@ -63,6 +63,10 @@ constexpr uint32_t kErrWalkGuard = 1u;
 constexpr uint32_t kErrTableFull = 2u;
 constexpr uint32_t kErrPickGuard = 4u;  // k_pick: hash partitions exhausted
 constexpr uint32_t kErrDeepRank = 8u;   // sharded merge: two ranks tie beyond the rank key's 32 levels
+// one-sync batches (*unsafe bits): the batch must run again with host-sized buffers
+constexpr uint32_t kUnsafeSpans = 1u;    // spans / GDesc records past their buffers
+constexpr uint32_t kUnsafeDesc = 2u;     // k_merge: a slow-path topic without GDesc records
+constexpr uint32_t kUnsafePatches = 4u;  // k_merge: a patch reservation past its region
 constexpr uint64_t kWalkGuard = 1ull << 26;
 
 // Exclusive offsets of a topic's outputs (scan of TopicCount).
@@ -145,13 +149,6 @@ struct EmitArgs {
   // span format, walk without lists: per-topic counts from k_desc (rows, shared, merge; no inline
   // rows) in place of the offsets' differences
   const TopicCount* tc;
-  // span format, k_desc fused into k_merge (index not sharded): each topic's gather words
-  // (stride gather_stride per topic, or compact at off[t].g when 0); k_merge writes the spans,
-  // copies the inline rows, and writes GDesc records only for a topic that needs them (beyond
-  // the pair analysis)
-  const uint32_t* gathers;
-  uint32_t gather_stride;
-  SpanRec* spans;
   // span format, merge-set dedup (rep == null: off). dd_phase 1: each set representative resolves
   // its merge gathers once into set-relative patches (row = x << kSetRowBits | k: k-th may-merge
   // slot of its x-th merge gather) in the set pool, and its SetInfo; dd_phase 2: every deduped
@@ -174,6 +171,10 @@ struct EmitArgs {
   const uint32_t* wave_list;           // dd_phase 2 after k_finish: the topics that still need a
   const unsigned long long* n_wave;    //   wavefront (k_finish wrote the others' results)
   const uint64_t* mrank;               // sharded index: the merge gathers' rank keys (DescArgs)
+  // one-sync batches: GDesc capacity (records); a topic whose slow path would read past it, or
+  // whose patch reservation does not fit its region, sets *unsafe (bit 2 / bit 4) instead
+  uint64_t desc_cap;
+  uint32_t* unsafe;
 };
 constexpr uint32_t kSetHeavy = 1024;  // a merge set with this many may-merge records goes first
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
@@ -217,6 +218,11 @@ struct DescArgs {
                    // lists k_merge maps a topic's merge gathers without GDesc records, which are
                    // then written only for a topic with more than kPairMax merge gathers
   uint64_t* mrank; // sharded index: each merge gather's DFS rank key (XInfo.rank; stride kPairMax)
+  // one-sync batches (Device, MQ_OPT_ONE_SYNC): the capacities of spans / desc in records; a topic
+  // that would write past them writes nothing and sets bit 1 of *unsafe (the batch is run again
+  // with host-sized buffers). unsafe == null: sized by the host (no checks).
+  uint64_t spans_cap, desc_cap;
+  uint32_t* unsafe;
 };
 
 // Merge-set dedup (span format): topics whose merge gathers are the same particles resolve to
@@ -303,21 +309,22 @@ void launch_pick(const PickArgs& a, hipStream_t s);  // a.sres != null: span for
 // and inline members (the row format, and span batches with inline subscriptions or a device
 // share pick); false: it counts gathers only and k_desc<true> counts the rest (DescArgs.tc_out).
 // wpe: the count pass's register budget (8: eight waves per SIMD, with spills; else unconstrained).
+// clamp (count pass): a topic's gather count is stored as at most kGatherCap (its slot), so the
+// batch's offsets stay within n * kGatherCap; the overflow flag still says that one had more.
 void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
                  const DevIndex& ix, TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf,
-                 hipStream_t s);
+                 hipStream_t s, bool clamp = false);
 // The frontier walk (k_walkf, `group` lanes per topic: 4, 8 or 16), count pass: the same counts
 // and gather slots as launch_walk(false, ...). Topics it cannot hold are listed in fb_list
 // (*fb_count, zeroed by the caller) and walked by k_walk in fb_blocks persistent workgroups.
 void launch_walk_front(uint32_t group, bool lists, const uint8_t* tb, const uint64_t* to, uint32_t n,
                        const DevIndex& ix, TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list,
-                       uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s);
+                       uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s, bool clamp = false);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
-// desc: span format with k_desc fused in (a.gathers / a.spans; not for a sharded index)
-void launch_merge(const EmitArgs& a, bool spans, bool desc, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
+void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
 
 // k_finish (span format, merge-set dedup, device results): thread per topic, after the set pass.
 // A topic whose result needs no wavefront — no inline rows, and no may-merge records or a merge

@@ -223,7 +223,7 @@ template <bool FILL, bool LISTS>
 __device__ __forceinline__ void walk_topic(uint32_t t, const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
                                            const DevIndex& ix, TopicCount* __restrict__ cnt,
                                            const TopicOff* __restrict__ off, uint32_t* __restrict__ gathers,
-                                           uint32_t* __restrict__ ovf, uint2 (*path)[256]) {
+                                           uint32_t* __restrict__ ovf, uint2 (*path)[256], bool clamp) {
   const uint64_t a0 = to[t], a1 = to[t + 1];
   uint32_t ng = 0, rows = 0, shared = 0, inl = 0, merge = 0;
   uint32_t* gout = FILL ? gathers + off[t].g : gathers + (uint64_t)t * kGatherCap;
@@ -344,7 +344,7 @@ __device__ __forceinline__ void walk_topic(uint32_t t, const uint8_t* __restrict
   }
   if (!FILL) {
     TopicCount c;
-    c.gathers = ng;
+    c.gathers = clamp ? min(ng, kGatherCap) : ng;
     c.rows = rows;
     c.shared = shared;
     c.inlines = inl;
@@ -362,15 +362,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                               DevIndex ix, TopicCount* __restrict__ cnt,
                                               const TopicOff* __restrict__ off,
                                               uint32_t* __restrict__ gathers, uint32_t* __restrict__ ovf,
-                                              const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list) {
+                                              const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
+                                              bool clamp) {
   __shared__ uint2 path[kWalkPath][256];  // level d: the '+' / '#' children of the particle at depth d
   const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (!list) {
-    if (i0 < n) walk_topic<FILL, LISTS>(i0, tb, to, ix, cnt, off, gathers, ovf, path);
+    if (i0 < n) walk_topic<FILL, LISTS>(i0, tb, to, ix, cnt, off, gathers, ovf, path, clamp);
     return;
   }
   const uint32_t nl = *n_list;
-  for (uint32_t i = i0; i < nl; i += gridDim.x * blockDim.x) walk_topic<FILL, LISTS>(list[i], tb, to, ix, cnt, off, gathers, ovf, path);
+  for (uint32_t i = i0; i < nl; i += gridDim.x * blockDim.x)
+    walk_topic<FILL, LISTS>(list[i], tb, to, ix, cnt, off, gathers, ovf, path, clamp);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -582,190 +584,6 @@ __global__ __launch_bounds__(256) void k_walkf(const uint8_t* __restrict__ tb, c
     c.inlines = inl;
     c.merge = merge;
     cnt[t] = c;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_walku: the same walk (gathers only, the span format without inline subscriptions or a device
-// share pick) restructured so the lanes of a wavefront share their loads. A thread per topic
-// runs a state machine whose transitions need no global load except three: an edge-table slot
-// (literal child lookup), a NodeWalk record (going down into a '+' child) and topic bytes. Each
-// round, every lane advances through load-free transitions (gathers, returns, scanning its next
-// segment) until it needs a slot or a record; then the whole wavefront issues that round's loads
-// together — one edge slot or record per lane, one round trip — and consumes them. k_walk's
-// per-lane DFS diverges so much that its lanes' loads are issued one lane at a time (r02 SQ
-// counters: 1,469 load instructions per wavefront for 23 per topic); here a wavefront issues
-// about as many load rounds as its longest topic needs.
-// Returns need no backward scan: the LDS path holds each ancestor's '+' / '#' children and the
-// start of its segment (topics up to 65,535 bytes; longer ones scan back).
-// ---------------------------------------------------------------------------------------------
-template <bool FILL, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walku(const uint8_t* __restrict__ tb,
-                                               const uint64_t* __restrict__ to, uint32_t n,
-                                               DevIndex ix, TopicCount* __restrict__ cnt,
-                                               const TopicOff* __restrict__ off,
-                                               uint32_t* __restrict__ gathers, uint32_t* __restrict__ ovf) {
-  __shared__ uint2 path[kWalkPath][256];       // depth d: the '+' / '#' children of the ancestor at d
-  __shared__ uint16_t path_s[kWalkPath][256];  //          and the start of its segment
-  enum : uint32_t { kLit = 0, kPlus = 1, kHash = 2, kDone = 3 };   // next transition
-  enum : uint32_t { kLdNone = 0, kLdEdge = 1, kLdWalk = 2 };       // load the lane waits for
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = t < n;
-  uint64_t a0 = 0, a1 = 0;
-  if (live) {
-    a0 = to[t];
-    a1 = to[t + 1];
-  }
-  uint32_t ng = 0;
-  uint32_t* gout = FILL ? gathers + (live ? off[t].g : 0) : gathers + (uint64_t)t * kGatherCap;
-  const uint8_t* tbase = tb + (a0 & ~15ull);
-  const uint32_t b0 = (uint32_t)(a0 & 15), b1 = b0 + (uint32_t)(a1 - a0);
-  const bool short_topic = b1 < 65536u;
-  ByteReaderT<uint32_t> R(tbase);
-  // Subscribers("") matches nothing (topics.go:598-600)
-  uint32_t st = (live && a1 > a0) ? kLit : kDone, ld = kLdNone;
-  const bool dollar = st != kDone && R.at(b0) == '$';
-  uint2* my_path = &path[0][threadIdx.x];
-  uint16_t* my_s = &path_s[0][threadIdx.x];
-  uint32_t p_isplus = 0;  // bit d: the particle at depth d + 1 is a '+' child
-  uint32_t node = kRoot, plus = kNone, hash = kNone, depth = 0;
-  if (st != kDone) {
-    const NodeWalk rw = ix.walk[kRoot];
-    plus = rw.plus_child;
-    hash = rw.hash_child;
-  }
-  bool wild0 = false;  // segment 0 of the path is '+'/'#'
-  SegKey key{0, 0};
-  uint32_t s = b0, e = b0;
-  if (st != kDone) e = scan_segment(R, b0, b1, &key);
-  uint32_t pi = 0, probes = 0;  // kLdEdge: slot index, probes so far; kLdWalk: pi = the record
-
-  auto gather = [&](uint32_t g, bool with_inline, bool wild) __attribute__((always_inline)) {
-    const bool subs_ok = !(dollar && wild);  // [MQTT-4.7.1-1], Q3
-    const uint32_t gw = g | (subs_ok ? kGatherSubs : 0u) | (with_inline ? kGatherInline : 0u);
-    if (FILL || ng < kGatherCap) gout[ng] = gw;
-    ng++;
-  };
-  auto descend = [&](uint32_t c, uint32_t cp, uint32_t ch, bool isplus) __attribute__((always_inline)) {
-    if (depth < kWalkPath) {
-      my_path[depth * 256] = make_uint2(plus, hash);
-      my_s[depth * 256] = (uint16_t)s;
-    }
-    if (depth < 32) p_isplus = isplus ? (p_isplus | (1u << depth)) : (p_isplus & ~(1u << depth));
-    depth++;
-    node = c;
-    plus = cp;
-    hash = ch;
-    s = e + 1;
-    e = scan_segment(R, s, b1, &key);
-    st = kLit;
-  };
-
-  for (uint32_t round = 0;; round++) {
-    // load-free transitions until the lane needs a load (or is done)
-    for (uint32_t g = 0; ld == kLdNone && st != kDone; g++) {
-      if (g + round > kWalkGuard) {  // never reached on a well-formed image; fail loudly, not hang
-        atomicOr(ix.err, kErrWalkGuard);
-        st = kDone;
-        break;
-      }
-      const bool has_next = e < b1;
-      const bool at_root = depth == 0;
-      if (st == kLit) {
-        const uint32_t len = e - s;
-        const uint32_t c0 = len ? R.at(s) : 0u;  // an empty last segment may end the buffer
-        // a literal "+" segment: the reference visits the '+' child twice with identical
-        // results (topics.go:603); the '+' transition covers it
-        if (len == 1 && c0 == '+') {
-          st = kPlus;
-        } else {
-          pi = (uint32_t)(edge_hash(node, key) & ix.edge_mask);
-          probes = 0;
-          ld = kLdEdge;
-        }
-      } else if (st == kPlus) {
-        st = kHash;
-        if (plus != kNone) {
-          if (has_next) {
-            pi = plus;
-            ld = kLdWalk;
-          } else {
-            gather(plus, true, at_root || wild0);
-          }
-        }
-      } else {  // kHash: gather the '#' child, then return to the parent
-        if (hash != kNone) gather(hash, true, at_root || wild0);  // topics.go:621-625
-        if (at_root) {
-          st = kDone;
-        } else {
-          const bool was_plus = depth - 1 < 32 ? ((p_isplus >> (depth - 1)) & 1u) != 0
-                                               : (ix.walk[node].parent_flags & kFlagPlusKey) != 0;
-          st = was_plus ? kHash : kPlus;
-          depth--;
-          e = s - 1;
-          if (depth < kWalkPath) {
-            const uint2 ph = my_path[depth * 256];
-            plus = ph.x;
-            hash = ph.y;
-            s = short_topic ? (uint32_t)my_s[depth * 256] : seg_start_before(R, b0, e);
-          } else {  // deeper than the path: the parent pointers (`node` is exact down here)
-            node = ix.walk[node].parent_flags & kParentMask;
-            const NodeWalk pw = ix.walk[node];
-            plus = pw.plus_child;
-            hash = pw.hash_child;
-            s = seg_start_before(R, b0, e);
-          }
-        }
-      }
-    }
-    if (!__any(ld != kLdNone)) break;  // every lane is done
-    // one round trip for the wavefront: each waiting lane's slot or record
-    EdgeSlot es{0, 0, kEdgeEmpty, kNone, kNone, kNone};
-    NodeWalk nw{kNone, kNone, 0, kNone};
-    if (ld == kLdEdge) es = ix.edges[pi];
-    if (ld == kLdWalk) nw = ix.walk[pi];
-    if (ld == kLdWalk) {
-      ld = kLdNone;
-      if (depth == 0) wild0 = true;
-      descend(pi, nw.plus_child, nw.hash_child, true);
-    } else if (ld == kLdEdge) {
-      bool found = false, miss = es.parent == kEdgeEmpty;
-      if (!miss && es.parent == node && es.k0 == key.k0 && es.k1 == key.k1) {
-        found = true;
-        if (seg_is_long(key)) {  // verify the bytes of a hashed key (rare)
-          const uint32_t len = e - s;
-          const SegInfo si = ix.seginfo[ix.walk[es.child].seg];
-          found = si.len == len;
-          for (uint32_t j = 0; found && j < len; j++) found = ix.segbytes[si.off + j] == R.at(s + j);
-        }
-      }
-      if (found || miss) {
-        ld = kLdNone;
-        st = kPlus;
-        if (found) {
-          const bool at_root = depth == 0;
-          const uint32_t c0 = e > s ? R.at(s) : 0u;
-          const bool cw = at_root ? (c0 == '+' || c0 == '#') : wild0;
-          if (e < b1) {
-            if (at_root) wild0 = cw;
-            descend(es.child, es.plus, es.hash, false);
-          } else {
-            gather(es.child, true, cw);
-            if (es.hash != kNone) gather(es.hash, false, cw);  // filter/# matches filter (topics.go:612)
-          }                                                   // inline: the particle's own again (Q2)
-        }
-      } else {
-        pi = (uint32_t)((pi + 1) & ix.edge_mask);
-        if (++probes > ix.edge_mask) {  // a full table without the key: cannot happen at load <= 1/2
-          ld = kLdNone;
-          st = kPlus;
-        }
-      }
-    }
-  }
-  if (!FILL && live) {
-    cnt[t] = TopicCount{ng, 0u, 0u, 0u, 0u};
-    if (ng > kGatherCap) atomicOr(ovf, 1u);
   }
 }
 
@@ -1040,6 +858,9 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
   }
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
   const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
+  // one-sync batch: spans past the buffer are not written (the batch runs again, host-sized)
+  const bool fits = !a.unsafe || o1.g <= a.spans_cap;
+  if (live && !fits && sub == 0) atomicOr(a.unsafe, kUnsafeSpans);
   uint32_t m = n_g;  // the wavefront's longest topic bounds its (wave-uniform) rounds
   m = max(m, (uint32_t)__shfl_xor(m, 16, 64));
   m = max(m, (uint32_t)__shfl_xor(m, 32, 64));
@@ -1066,7 +887,7 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
     const uint32_t sh_i = g16_incl(act ? L.shr_cnt : 0u, sub);
     const uint32_t rp = rpos + rn_i - rn, x = n_mg + inc_i - inc;
     const uint64_t ip = ipos + (in_i - in);
-    if (act) a.spans[o0.g + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
+    if (act && fits) a.spans[o0.g + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
     for (uint32_t k = 0; k < in; k++) a.inl_out[ip + k] = a.ix.inl[L.inl_off + k];
     if (ismg) {
       sig += mix64(((uint64_t)x << 32 | (gw & kGatherNode)) + 0x9e3779b97f4a7c15ull);
@@ -1094,7 +915,10 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
   a.msig[t] = mix64(sig + n_mg) | 1ull;  // never 0 (the dedup table's empty key)
   a.mcount[t] = n_mg;
   // k_merge maps this topic from its GDesc records: write them (rare)
-  if (n_mg > kPairMax) write_gdesc(a.ix, gw_src, n_g, (uint32_t)o0.shr, a.desc + o0.g);
+  if (n_mg > kPairMax) {
+    if (!a.unsafe || o1.g <= a.desc_cap) write_gdesc(a.ix, gw_src, n_g, (uint32_t)o0.shr, a.desc + o0.g);
+    else atomicOr(a.unsafe, kUnsafeSpans);
+  }
 }
 
 // k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, whose
@@ -1428,13 +1252,9 @@ __device__ __forceinline__ uint64_t gdesc_rank(const GDesc& d) {
 // latency-bound, so occupancy can pay for a few spills). MQ_OPT_MERGE_WAVES picks the variant.
 // XS (span format of a sharded index): the other shards' exported nodes join the topic's map
 // and DFS order compares rank keys first (SPANS must be true).
-// DESC (span format, index not sharded): k_desc's work is done here, lanes over the topic's
-// gathers — the spans (coalesced stores), the per-topic counts, the inline rows and the map of
-// merge gathers come from one round of loads (gather word, then lists and pair header
-// together); GDesc records are written only for a topic that takes the slow paths.
 // SET (span format, merge-set dedup): the set pass (a.dd_phase 1), compiled apart so that the
 // topic pass's copy, inline and result code does not weigh on its register allocation.
-template <bool SPANS, bool XS, int WPE, bool DESC, bool SET = false>
+template <bool SPANS, bool XS, int WPE, bool SET = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
   __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records (or
@@ -1502,6 +1322,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (resv_pending) {
       const unsigned long long b = __shfl(resv, 0, 64);
       pfit = b + resv_n <= prcap;
+      if (!pfit && a.unsafe && lane == 0) atomicOr(a.unsafe, kUnsafePatches);
       pbase = (uint64_t)(t & (kPatchRegions - 1)) * prcap + b;
       resv_pending = false;
     }
@@ -1515,64 +1336,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   };
 
   uint32_t n_map = 0;
-  // DESC: lanes over the gathers. build: write spans, copy inline rows, count, fill the map;
-  // store: write the GDesc records the slow paths read.
-  auto desc_pass = [&](bool build, bool store) __attribute__((always_inline)) {
-    const uint32_t* __restrict__ gsrc = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
-    uint32_t cr = 0, cs = 0, ci = 0, cm = 0;
-    if (build) n_map = 0;
-    for (uint32_t i0 = 0; i0 < n_g; i0 += 64) {  // wave-uniform
-      const uint32_t i = i0 + lane;
-      uint32_t gw = 0;
-      NodeLists L{0, 0, 0, 0, 0, 0, 0, 0};
-      NodePair P{0, kNone, 0, 0};
-      if (i < n_g) {
-        gw = gsrc[i];
-        L = a.ix.lists[gw & kGatherNode];
-        P = a.ix.npair[gw & kGatherNode];
-      }
-      const bool subs = i < n_g && (gw & kGatherSubs);
-      const uint32_t rn = subs ? L.n_direct + L.n_merge : 0u;
-      const uint32_t in = (i < n_g && (gw & kGatherInline)) ? L.inl_cnt : 0u;
-      uint32_t tr, ts, ti;
-      const uint32_t rp = cr + wave_excl_scan(rn, lane, &tr);
-      ts = wave_sum(L.shr_cnt);
-      const uint32_t ip = ci + wave_excl_scan(in, lane, &ti);
-      const bool ins = subs && L.n_merge != 0;
-      if (build) {
-        if (i < n_g) a.spans[o0.g + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
-        for (uint32_t k = 0; k < in; k++) a.inl_rows[ib + ip + k] = a.ix.inl[L.inl_off + k];
-        const uint64_t bi = __ballot(ins);
-        const uint32_t x = n_map + prefix_before(bi);
-        if (ins && x < kPairMax) {
-          const uint32_t node = gw & kGatherNode;
-          uint32_t sl = hash32(node) & (kMapSlots - 1);
-          while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
-          map_val[wv][sl] = x;
-          mg_node[wv][x] = node;
-          mg_gi[wv][x] = i;
-          mg_row[wv][x] = rp + L.n_direct;
-          mg_eoff[wv][x] = P.ent_off;
-          mg_emask[wv][x] = P.ent_mask;
-        }
-        n_map += __popcll(bi);
-        cm += wave_sum(ins ? L.n_merge : 0u);
-      }
-      if (store && i < n_g)
-        a.desc[o0.g + i] = GDesc{rp, L.sub_off, P.ent_off, P.ent_mask, 0u, 0u, gw, L.n_direct | (ins ? kDescMerge : 0u)};
-      cr += tr;
-      cs += ts;
-      ci += ti;
-    }
-    if (build) tcn = TopicCount{n_g, cr, cs, ci, cm};
-  };
-  if (DESC) {
-    for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
-    wave_sync_lds();
-    desc_pass(true, false);
-    if (tcn.inlines) __threadfence_block();  // the inline rows copied above are read back below
-    wave_sync_lds();
-  }
   const uint32_t cap = tcn.rows;
 
   uint32_t res_flags = 0;
@@ -1608,7 +1371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // within a topic.
     // merge-set dedup's lists (k_desc): the topic's merge gathers directly, x standing for the
     // gather index (the same order); a topic with more than kPairMax of them has GDesc records
-    const uint32_t lc = (SPANS && !DESC && a.mlist) ? a.mcount[t] : kNone;
+    const uint32_t lc = (SPANS && a.mlist) ? a.mcount[t] : kNone;
     if (lc <= kPairMax) {
       for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
       wave_sync_lds();
@@ -1627,7 +1390,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         mg_emask[wv][lane] = P.y;
       }
       n_map = lc;
-    } else if (!DESC) {
+    } else {
+    if (a.unsafe && o1.g > a.desc_cap) {  // one-sync batch: no GDesc records to read
+      if (lane == 0) atomicOr(a.unsafe, kUnsafeDesc);
+      continue;
+    }
     for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
     wave_sync_lds();
     for (uint32_t i0 = 0; i0 < n_g; i0 += 64) {
@@ -1661,7 +1428,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       n_map += __popcll(bi);
     }
-    }  // !DESC
+    }
     // sharded index: the other shards' gathered cross-shard nodes join the map as entries
     // n_map.. (their partner links name them kForeign | fid; their rank keys order them)
     uint32_t n_ent = n_map;
@@ -1688,10 +1455,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // beyond the map: linear lookups (the map's hash table keeps a free slot: kMapSlots - 1
     // entries at most, so a lookup of a node that is not there ends)
     const bool slow = n_map > kPairMax || n_ent > (XS ? kEnt - 1 : kEnt);
-    if (DESC && slow) {  // the slow paths read the topic's GDesc records
-      desc_pass(false, true);
-      __threadfence_block();
-      wave_sync_lds();
+    if (slow && a.unsafe && o1.g > a.desc_cap) {  // one-sync batch: no GDesc records to read
+      if (lane == 0) atomicOr(a.unsafe, kUnsafeDesc);
+      continue;
     }
     // Is node h (or kForeign | fid) gathered for this topic? Its DFS position: rank key, then
     // gather index (kNone for another shard's node); found = false otherwise.
@@ -2024,19 +1790,11 @@ namespace mq {
 
 void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
                  const DevIndex& ix, TopicCount* cnt, const TopicOff* off, uint32_t* gathers, uint32_t* ovf,
-                 hipStream_t s) {
+                 hipStream_t s, bool clamp) {
   if (!n) return;
   dim3 grid((n + 255) / 256);
-  // wpe 16 (MQ_OPT_WALK_WAVES): the shared-load walk k_walku (slot indices are 32-bit). Measured
-  // slower than k_walk at 10M subscriptions (2.73 vs 1.89 ms per 1M topics), kept
-  // for the comparison.
-  if (!lists && wpe == 16 && ix.edge_mask <= 0xFFFFFFFFull) {
-    if (fill) hipLaunchKernelGGL((k_walku<true, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf);
-    else hipLaunchKernelGGL((k_walku<false, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf);
-    return;
-  }
 #define MQ_WALK(F, L, W) \
-  hipLaunchKernelGGL((k_walk<F, L, W>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf, nullptr, nullptr)
+  hipLaunchKernelGGL((k_walk<F, L, W>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, off, gathers, ovf, nullptr, nullptr, clamp)
   if (fill) {
     if (lists) MQ_WALK(true, true, 1);
     else MQ_WALK(true, false, 1);
@@ -2052,7 +1810,7 @@ void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const u
 
 void launch_walk_front(uint32_t group, bool lists, const uint8_t* tb, const uint64_t* to, uint32_t n,
                        const DevIndex& ix, TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list,
-                       uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s) {
+                       uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s, bool clamp) {
   if (!n) return;
   const dim3 grid((n + 256 / group - 1) / (256 / group));
 #define MQ_WALKF(G, L) hipLaunchKernelGGL((k_walkf<G, L>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
@@ -2071,10 +1829,10 @@ void launch_walk_front(uint32_t group, bool lists, const uint8_t* tb, const uint
   const dim3 fgrid(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, fb_blocks)));
   if (lists)
     hipLaunchKernelGGL((k_walk<false, true, 1>), fgrid, dim3(256), 0, s, tb, to, n, ix, cnt, nullptr, gathers, ovf,
-                       fb_list, fb_count);
+                       fb_list, fb_count, clamp);
   else
     hipLaunchKernelGGL((k_walk<false, false, 1>), fgrid, dim3(256), 0, s, tb, to, n, ix, cnt, nullptr, gathers, ovf,
-                       fb_list, fb_count);
+                       fb_list, fb_count, clamp);
 }
 
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
@@ -2103,33 +1861,29 @@ void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s) {
   hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, a);
 }
 
-void launch_merge(const EmitArgs& a, bool spans, bool desc, uint32_t wpe, uint32_t max_blocks, hipStream_t s) {
+void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_blocks, hipStream_t s) {
   const uint32_t waves = a.t1 - a.t0;
   if (!waves) return;
   const uint32_t blocks = max_blocks ? std::min((waves + 3) / 4, max_blocks) : (waves + 3) / 4;
   const dim3 g(blocks), b(256);
   if (spans && a.ix.xinfo && a.rep && a.dd_phase == 1) {  // sharded index, merge-set dedup: the set pass
-    if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6, false, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_merge<true, true, 1, false, true>), g, b, 0, s, a);
+    if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, true, 1, true>), g, b, 0, s, a);
   } else if (spans && a.ix.xinfo) {  // sharded index
-    if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6, false>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_merge<true, true, 1, false>), g, b, 0, s, a);
-  } else if (spans && desc) {
+    if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, true, 1>), g, b, 0, s, a);
+  } else if (spans && a.rep && a.dd_phase == 1) {  // merge-set dedup: the set pass
     if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, true>), g, b, 0, s, a);
     else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_merge<true, false, 1, true>), g, b, 0, s, a);
-  } else if (spans && a.rep && a.dd_phase == 1) {  // merge-set dedup: the set pass
-    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, false, true>), g, b, 0, s, a);
-    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, false, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_merge<true, false, 1, false, true>), g, b, 0, s, a);
   } else if (spans) {
-    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, false>), g, b, 0, s, a);
-    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, false>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_merge<true, false, 1, false>), g, b, 0, s, a);
+    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8>), g, b, 0, s, a);
+    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, false, 1>), g, b, 0, s, a);
   } else {
-    if (wpe >= 8) hipLaunchKernelGGL((k_merge<false, false, 8, false>), g, b, 0, s, a);
-    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<false, false, 6, false>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_merge<false, false, 1, false>), g, b, 0, s, a);
+    if (wpe >= 8) hipLaunchKernelGGL((k_merge<false, false, 8>), g, b, 0, s, a);
+    else if (wpe >= 6) hipLaunchKernelGGL((k_merge<false, false, 6>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<false, false, 1>), g, b, 0, s, a);
   }
 }
 

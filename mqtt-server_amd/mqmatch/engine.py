@@ -74,11 +74,11 @@ class SpanResult(C.Structure):
 SPANS_PICKED = 1  # MQ_SPANS_PICKED
 PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 
-# mq_set_option (include/mqmatch.h MQ_OPT_*)
-OPT_CHUNK_ROWS, OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_PATCH_CAP, OPT_MERGE_WAVES = \
-    1, 2, 3, 4, 5, 6, 7
-OPT_MSG_IMAGE = 8
-OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_FUSE_DESC, OPT_MERGE_DEDUP, OPT_EDGE_LOAD = 9, 10, 11, 12, 13
+# mq_set_option: product options (include/mqmatch.h) and development ones (include/mqmatch_dev.h)
+OPT_CHUNK_ROWS, OPT_PATCH_CAP, OPT_EDGE_LOAD = 1, 6, 13
+OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_MERGE_WAVES = 2, 3, 4, 5, 7
+OPT_MSG_IMAGE, OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_MERGE_DEDUP = 8, 9, 10, 12
+OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC = 14, 15, 16
 
 
 class MsgResult(C.Structure):
@@ -607,8 +607,8 @@ class Engine:
         _check(lib().mq_profile_enable(self.h, mode), "mq_profile_enable")
 
     def profile_read(self):
-        arr = (KernelTime * 32)()
-        n = _check(lib().mq_profile_read(self.h, arr, 32), "mq_profile_read")
+        arr = (KernelTime * 64)()
+        n = _check(lib().mq_profile_read(self.h, arr, 64), "mq_profile_read")
         return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms)) for i in range(n)}
 
     def profile_reset(self):

@@ -402,6 +402,37 @@ def test_spans_device_digest_parity(dedup, gpu_available):
     assert len(bad) == 0, f"{len(bad)} of {n} topics differ (first {bad[:5]})"
 
 
+def test_one_sync_batches_grow_and_repeat(gpu_available):
+    """One-sync batches (MQ_OPT_ONE_SYNC, the default for device results): buffers sized by
+    earlier batches. A fresh index, a small batch, then a batch several times larger (its spans
+    and patches do not fit what the small one left: it runs again, sized by the host), then the
+    large batch again (fits: one synchronisation) and the small one: every result equals the
+    oracle's, and the profile counts exactly the runs that had to repeat."""
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(60000, 3000, seed=71)
+    eng.profile(True)
+    batches = [W.gen_topics(w, k, seed=72 + i) for i, k in enumerate((300, 6000))]
+    retried = []
+    for tb, to in (batches[0], batches[1], batches[1], batches[0]):
+        n = len(to) - 1
+        d_tb = torch.from_numpy(tb).cuda()
+        d_to = torch.from_numpy(to.view(np.int64)).cuda()
+        torch.cuda.synchronize()
+        eng.profile_reset()
+        r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
+        prof = eng.profile_read()
+        # a topic with more gathers than its slot (walk_fill in the host-sized run) always repeats
+        retried.append((prof.get("one_sync_retries", (0, 0.0))[0], "walk_fill" in prof))
+        dg, _ = engine_digests(E.expand_device_spans(r, n))
+        od, _, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+        assert (dg == od).all()
+    # the first batch (nothing sized yet) and the first large one repeat; the others only for a
+    # slot overflow
+    assert [x[0] for x in retried] == [1, 1, int(retried[2][1]), int(retried[3][1])], retried
+
+
 def test_spans_result_pins_host_image(gpu_available):
     """A host span result pins the pools it points into: an update from another thread waits
     until the result is freed."""

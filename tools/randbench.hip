@@ -53,18 +53,38 @@ __global__ __launch_bounds__(256) void k_probe(const Rec* __restrict__ t, uint64
   out[i] = acc;
 }
 
+// Coalesced streaming read of the whole table, 16 B per lane (the access width the guide's FETCH_SIZE
+// correction is stated for): a known byte count to calibrate the counters against.
+__global__ __launch_bounds__(256) void k_stream(const uint4* __restrict__ t, uint64_t n16, uint64_t* __restrict__ out) {
+  uint64_t acc = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 v = t[i];
+    acc += v.x ^ v.w;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 int main() {
   const uint64_t slots = 1ull << 27;  // 134M x 32 B = 4.3 GB
   const uint32_t topics = 1u << 20, k = 20;
   Rec* t;
   uint64_t* out;
   CK(hipMalloc(&t, slots * sizeof(Rec)));
-  CK(hipMalloc(&out, topics * sizeof(uint64_t)));
+  CK(hipMalloc(&out, (topics > 65536 * 256 ? topics : 65536 * 256) * sizeof(uint64_t)));
   hipLaunchKernelGGL(k_fill, dim3(65536), dim3(256), 0, 0, t, slots);
   CK(hipDeviceSynchronize());
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; rep++) {  // known bytes: slots x 32 B read, coalesced
+    CK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL(k_stream, dim3(65536), dim3(256), 0, 0, reinterpret_cast<const uint4*>(t), slots * 2, out);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    printf("stream read of %.2f GB, 16 B per lane: %.3f ms  %.0f GB/s\n", slots * 32 / 1e9, ms, slots * 32 / ms / 1e6);
+  }
   for (int dep = 1; dep >= 0; dep--) {
     for (int rep = 0; rep < 4; rep++) {
       CK(hipEventRecord(a, 0));
