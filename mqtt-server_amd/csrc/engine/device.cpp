@@ -884,7 +884,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   }
   prof.begin(s);
   if (front)
-    launch_walk_front(walk_group_, lists, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(),
+    launch_walk_front(walk_group_, lists, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(),
                       ovf_.as<uint32_t>(), fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, s, one_sync);
   else
     launch_walk(false, lists, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), nullptr, gslots_.as<uint32_t>(),

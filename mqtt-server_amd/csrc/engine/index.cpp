@@ -216,14 +216,15 @@ void Index::set_shard(uint32_t shard, uint32_t n_shards) {
 }
 
 // rank key of node n from its parent's (layout.h XInfo)
-void Index::set_rank(uint32_t n, uint32_t parent, std::string_view seg) {
+void Index::set_rank(uint32_t n, uint32_t parent, std::string_view seg, bool mark) {
   const XInfo& P = xinfo.h[parent];
   XInfo x{kNone, P.deep, P.rank};
   const uint32_t d = nh_[n].depth;  // 1-based
   const uint64_t code = seg == "+" ? 2 : (seg == "#" ? 3 : 1);
   if (d <= 32) x.rank |= code << (64 - 2 * d);
   else x.deep = 1;
-  xinfo.at_w(n) = x;
+  if (mark) xinfo.at_w(n) = x;
+  else xinfo.h[n] = x;
 }
 
 // Qos | NoLocal of partner `p` (a node of this shard, or kForeign | fid) of `client`'s slot

@@ -82,7 +82,8 @@ struct Mirror {
   size_t size() const { return h.size(); }
   T& operator[](size_t i) { return h[i]; }
   const T& operator[](size_t i) const { return h[i]; }
-  void mark_page(size_t p) {
+  void mark_page(size_t p) {  // (not thread-safe: parallel bulk builds write h directly, all_dirty)
+    if (all_dirty) return;     // the whole array is uploaded anyway
     const size_t w = p / 64;
     if (w >= dirty.size()) dirty.resize(std::max(w + 1, dirty.size() + dirty.size() / 2), 0);
     const uint64_t bit = 1ull << (p % 64);
@@ -412,7 +413,8 @@ class Index {
   void touch_partner(uint32_t p) {
     if (!(p & kForeign)) merge_dirty(p);
   }
-  void set_rank(uint32_t n, uint32_t parent, std::string_view seg);
+  // (mark = false: a parallel bulk build, which marks the whole array dirty itself)
+  void set_rank(uint32_t n, uint32_t parent, std::string_view seg, bool mark = true);
   void move_slot(uint32_t n, uint32_t from, uint32_t to);
   void part_set(uint32_t pos, const std::vector<uint32_t>& nodes);
   void part_add(uint32_t pos, uint32_t node);

@@ -400,7 +400,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
         if (h.str == 0) walk.h[parent].plus_child = id;  // a parent has one "+" and one "#" child
         if (h.str == 1) walk.h[parent].hash_child = id;
         __atomic_fetch_add(&nh_[parent].n_children, 1u, __ATOMIC_RELAXED);
-        if (sharded()) set_rank(id, parent, seg);
+        if (sharded()) set_rank(id, parent, seg, false);
       }
       uint32_t cur = __atomic_load_n(&max_depth_, __ATOMIC_RELAXED);
       while (depth_max > cur && !__atomic_compare_exchange_n(&max_depth_, &cur, depth_max, true, __ATOMIC_RELAXED,

@@ -317,7 +317,7 @@ void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const u
 // The frontier walk (k_walkf, `group` lanes per topic: 4, 8 or 16), count pass: the same counts
 // and gather slots as launch_walk(false, ...). Topics it cannot hold are listed in fb_list
 // (*fb_count, zeroed by the caller) and walked by k_walk in fb_blocks persistent workgroups.
-void launch_walk_front(uint32_t group, bool lists, const uint8_t* tb, const uint64_t* to, uint32_t n,
+void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
                        const DevIndex& ix, TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list,
                        uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s, bool clamp = false);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,

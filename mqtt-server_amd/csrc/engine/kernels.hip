@@ -422,13 +422,17 @@ struct FrontEnt {  // one frontier particle: its '+' / '#' children and its path
   uint32_t node, plus, hash, code;
 };
 
-template <uint32_t G, bool LISTS>
-__global__ __launch_bounds__(256) void k_walkf(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
+// WPE: waves per SIMD asked of the register allocator (8: a few SGPRs spill to VGPR lanes; 1:
+// no constraint, 7 waves).
+template <uint32_t G, bool LISTS, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walkf(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
                                                uint32_t n, DevIndex ix, TopicCount* __restrict__ cnt,
                                                uint32_t* __restrict__ gathers, uint32_t* __restrict__ fb_list,
                                                uint32_t* __restrict__ fb_count) {
   constexpr uint32_t kTopics = 256 / G;  // topics per workgroup
   __shared__ uint32_t sl[kTopics][kFrontLevels];      // '/' positions (relative to the topic's chunk base)
+  __shared__ uint4 skey[kTopics][kFrontLevels];       // each level's segment key (SegKey)
+  __shared__ uint2 sseg[kTopics][kFrontLevels];       // ... its start, and length | "+" segment << 31
   __shared__ uint2 gat[kTopics][kGatherCap];          // staged gathers: (word, rank)
   __shared__ FrontEnt xf[kTopics][G];                 // next level's frontier, compacted
   const uint32_t q = threadIdx.x / G, sub = threadIdx.x % G;
@@ -464,6 +468,16 @@ __global__ __launch_bounds__(256) void k_walkf(const uint8_t* __restrict__ tb, c
   const uint32_t L = nch ? nsl + 1 : 0u;  // levels (0: the empty topic, which matches nothing)
   bool fb = live && L > kFrontLevels;
   wave_sync_lds();
+  // every level's key, lanes over the levels: the walk below then reads them from LDS instead of
+  // loading topic bytes on each level's critical path
+  if (live && !fb)
+    for (uint32_t d = sub; d < L; d += G) {
+      const uint32_t s = d ? sl[q][d - 1] + 1 : b0, e = d + 1 < L ? sl[q][d] : b1;
+      const SegKey k = key_of(R, s, e);
+      const bool plusseg = e - s == 1 && R.at(s) == '+';
+      skey[q][d] = make_uint4((uint32_t)k.k0, (uint32_t)(k.k0 >> 32), (uint32_t)k.k1, (uint32_t)(k.k1 >> 32));
+      sseg[q][d] = make_uint2(s, (e - s) | (plusseg ? 0x80000000u : 0u));
+    }
   const bool dollar = L && R.at(b0) == '$';
   bool lit0wild = false;  // segment 0 starts with '+' / '#' (a literal child there is 'wild', Q3)
   if (L) {
@@ -473,6 +487,7 @@ __global__ __launch_bounds__(256) void k_walkf(const uint8_t* __restrict__ tb, c
       lit0wild = c0 == '+' || c0 == '#';
     }
   }
+  wave_sync_lds();
   // --- the frontier, level by level ------------------------------------------------------------
   FrontEnt fe{kNone, kNone, kNone, 0u};
   if (sub == 0) {
@@ -485,20 +500,23 @@ __global__ __launch_bounds__(256) void k_walkf(const uint8_t* __restrict__ tb, c
     const bool act = live && !fb && d < L && F != 0;
     const bool mine = act && sub < F;
     const bool has_next = d + 1 < L;
-    const uint32_t s = d ? sl[q][d - 1] + 1 : b0, e = has_next ? sl[q][d] : b1;
     const uint32_t sh = 30 - 2 * d;  // level d's two bits of the rank
     SegKey key{0, 0};
-    uint32_t len = 0, c0 = 0;
+    uint32_t s = 0, len = 0;
+    bool plusseg = false;
     if (act) {
-      len = e - s;
-      c0 = len ? R.at(s) : 0u;
-      key = key_of(R, s, e);
+      const uint4 kk = skey[q][d];
+      const uint2 sg = sseg[q][d];
+      key = SegKey{kk.x | (uint64_t)kk.y << 32, kk.z | (uint64_t)kk.w << 32};
+      s = sg.x;
+      len = sg.y & 0x7FFFFFFFu;
+      plusseg = (sg.y >> 31) != 0;
     }
     NodeWalk pw{kNone, kNone, 0, 0};
     if (mine && has_next && fe.plus != kNone) pw = ix.walk[fe.plus];
     EdgeHit h{kNone, kNone, kNone};
     // a literal "+" segment: the reference visits the '+' child twice alike (topics.go:603)
-    if (mine && !(len == 1 && c0 == '+')) h = lookup_edge(ix, fe.node, key, tbase + s, len);
+    if (mine && !plusseg) h = lookup_edge(ix, fe.node, key, tbase + s, len);
     // this lane's gathers (at most four): the particle's '#' child (topics.go:621); at the last
     // level the literal child, its '#' child (filter/# matches filter, topics.go:612; inline: the
     // particle's own again, Q2) and the '+' child
@@ -1808,12 +1826,16 @@ void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const u
 #undef MQ_WALK
 }
 
-void launch_walk_front(uint32_t group, bool lists, const uint8_t* tb, const uint64_t* to, uint32_t n,
+void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
                        const DevIndex& ix, TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list,
                        uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s, bool clamp) {
   if (!n) return;
   const dim3 grid((n + 256 / group - 1) / (256 / group));
-#define MQ_WALKF(G, L) hipLaunchKernelGGL((k_walkf<G, L>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
+#define MQ_WALKF(G, L)                                                                                              \
+  if (wpe >= 8)                                                                                                  \
+    hipLaunchKernelGGL((k_walkf<G, L, 8>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count); \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_walkf<G, L, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
   if (group == 8) {
     if (lists) MQ_WALKF(8, true);
     else MQ_WALKF(8, false);

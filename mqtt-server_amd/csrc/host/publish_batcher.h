@@ -1,23 +1,33 @@
 // The batching stage of the publish pipeline (north star): publishToSubscribers
 // (/root/reference/server.go:984-1021) asks Topics.Subscribers(pk.TopicName) once per publish,
 // from many connection goroutines at once. Here those calls are accumulated and matched as one
-// GPU batch: producers Submit() a topic and wait on the future; a dispatcher thread seals a
-// batch when it holds max_batch topics or its oldest topic has waited max_delay, matches it and
-// fulfils the futures in submission order. The results are exactly those of Subscribers(topic)
-// on the index state the batch was matched against (readers take no root lock in the reference
-// either, topics.go:583, Q11); SelectShared / MergeSharedSelected and the fan-out stay with the
-// caller, as in the reference.
-//   PublishBatcher      futures of Subscribers (the Go-shaped maps, TopicsIndex::SubscribersBatch)
-//   PublishViewBatcher  futures of TopicView (the recipients as a view over the batch's span
+// GPU batch: producers Submit() a topic and get() its ticket; a dispatcher thread seals a batch
+// and matches it with one engine call. The results are exactly those of Subscribers(topic) on
+// the index state the batch was matched against (readers take no root lock in the reference
+// either, topics.go:583, Q11); the OnSelectSubscribers hook, SelectShared / MergeSharedSelected
+// and the fan-out stay with the caller, as in the reference (hooks.go:360-367).
+//
+// Submission is sharded: a producer appends to one of kShards queues (picked per thread), each
+// with its own lock, so thousands of submitters do not serialise on one mutex; a ticket names
+// its queue's segment of the batch (one shared, reference-counted record per queue and batch,
+// not one promise per topic), and a batch is completed by one notification per segment.
+//
+// Sealing policy: the dispatcher takes everything queued when the previous batch is done — so
+// under load a batch holds what arrived while the last one was matched — and, when fewer than
+// min_fill topics are queued, waits up to max_delay for more. max_batch bounds a batch.
+//   PublishBatcher      tickets of Subscribers (the Go-shaped maps, TopicsIndex::SubscribersBatch)
+//   PublishViewBatcher  tickets of TopicView (the recipients as a view over the batch's span
 //                       result, TopicsIndex::SubscribersViews: no maps are built)
 #pragma once
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <exception>
 #include <functional>
-#include <future>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -31,6 +41,22 @@ namespace host {
 
 template <class R>
 class BasicBatcher {
+  // One queue's part of one batch: its topics are the batch's [base, base + n).
+  struct Segment {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    std::shared_ptr<const std::vector<R>> results;  // the batch's results (null: it failed)
+    std::exception_ptr err;
+    uint32_t base = 0;
+  };
+  struct alignas(64) Shard {
+    std::mutex mu;
+    std::vector<std::string> topics;
+    std::shared_ptr<Segment> seg;  // the segment the queued topics belong to
+  };
+  static constexpr uint32_t kShards = 16;
+
  public:
   struct Stats {
     uint64_t batches = 0;     // match calls
@@ -39,9 +65,36 @@ class BasicBatcher {
   };
   using MatchFn = std::function<std::vector<R>(const std::vector<std::string>&)>;
 
-  BasicBatcher(MatchFn match, size_t max_batch, std::chrono::microseconds max_delay)
+  // A submitted topic: get() waits for its batch and returns its result (throws EngineError if
+  // the batch's match failed). Valid until destroyed; copies share the result.
+  class Ticket {
+   public:
+    Ticket() = default;
+    const R& get() const {
+      wait();
+      if (seg_->err) std::rethrow_exception(seg_->err);
+      return (*seg_->results)[seg_->base + idx_];
+    }
+    void wait() const {
+      std::unique_lock<std::mutex> lk(seg_->mu);
+      seg_->cv.wait(lk, [&] { return seg_->done; });
+    }
+    bool ready() const {
+      std::lock_guard<std::mutex> lk(seg_->mu);
+      return seg_->done;
+    }
+    bool valid() const { return seg_ != nullptr; }
+
+   private:
+    friend class BasicBatcher;
+    Ticket(std::shared_ptr<Segment> s, uint32_t i) : seg_(std::move(s)), idx_(i) {}
+    std::shared_ptr<Segment> seg_;
+    uint32_t idx_ = 0;
+  };
+
+  BasicBatcher(MatchFn match, size_t max_batch, std::chrono::microseconds max_delay, size_t min_fill = 1024)
       : match_(std::move(match)), max_batch_(max_batch ? max_batch : 1), max_delay_(max_delay),
-        th_([this] { run(); }) {}
+        min_fill_(std::min(min_fill, max_batch_)), th_([this] { run(); }) {}
   ~BasicBatcher() {  // matches what is still queued, then stops the dispatcher
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -53,23 +106,27 @@ class BasicBatcher {
   BasicBatcher(const BasicBatcher&) = delete;
   BasicBatcher& operator=(const BasicBatcher&) = delete;
 
-  // Thread-safe. The future throws EngineError if the batch's match failed.
-  std::future<R> Submit(std::string topic) {
-    std::promise<R> p;
-    std::future<R> f = p.get_future();
-    bool wake = false;
+  // Thread-safe.
+  Ticket Submit(std::string topic) {
+    static std::atomic<uint32_t> next_shard{0};
+    thread_local const uint32_t my = next_shard.fetch_add(1, std::memory_order_relaxed);
+    Shard& sh = shards_[my % kShards];
+    Ticket t;
+    uint64_t q;
     {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (topics_.empty()) {
-        oldest_ = std::chrono::steady_clock::now();
-        wake = true;  // starts the delay timer
-      }
-      topics_.push_back(std::move(topic));
-      waiters_.push_back(std::move(p));
-      wake |= topics_.size() >= max_batch_;
+      std::lock_guard<std::mutex> lk(sh.mu);
+      if (!sh.seg) sh.seg = std::make_shared<Segment>();
+      t = Ticket(sh.seg, (uint32_t)sh.topics.size());
+      sh.topics.push_back(std::move(topic));
+      // counted under the queue's lock: the dispatcher subtracts only topics it took, so the
+      // count never runs below what is queued
+      q = queued_.fetch_add(1, std::memory_order_acq_rel) + 1;
     }
-    if (wake) cv_.notify_one();
-    return f;
+    if (q == 1 || q == min_fill_ || q == max_batch_) {  // the dispatcher may be waiting for this
+      std::lock_guard<std::mutex> lk(mu_);
+      cv_.notify_one();
+    }
+    return t;
   }
   Stats stats() const {
     std::lock_guard<std::mutex> lk(mu_);
@@ -78,46 +135,70 @@ class BasicBatcher {
 
  private:
   void run() {
+    std::vector<std::string> topics;
+    std::vector<std::pair<std::shared_ptr<Segment>, uint32_t>> segs;  // (segment, its topics)
     for (;;) {
-      std::vector<std::string> topics;
-      std::vector<std::promise<R>> waiters;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        for (;;) {
-          if (!topics_.empty() &&
-              (stop_ || topics_.size() >= max_batch_ || std::chrono::steady_clock::now() - oldest_ >= max_delay_))
-            break;
-          if (stop_) return;  // nothing queued
-          if (topics_.empty()) cv_.wait(lk);
-          else cv_.wait_until(lk, oldest_ + max_delay_);
+        cv_.wait(lk, [&] { return stop_ || queued_.load(std::memory_order_acquire) != 0; });
+        if (stop_ && queued_.load() == 0) return;
+        // a small batch waits up to max_delay for more (the clock starts at its first topic)
+        if (!stop_ && queued_.load() < min_fill_) {
+          const auto until = std::chrono::steady_clock::now() + max_delay_;
+          cv_.wait_until(lk, until, [&] { return stop_ || queued_.load() >= min_fill_; });
         }
-        const size_t n = std::min(topics_.size(), max_batch_);
-        topics.assign(std::make_move_iterator(topics_.begin()), std::make_move_iterator(topics_.begin() + n));
-        waiters.assign(std::make_move_iterator(waiters_.begin()), std::make_move_iterator(waiters_.begin() + n));
-        topics_.erase(topics_.begin(), topics_.begin() + n);
-        waiters_.erase(waiters_.begin(), waiters_.begin() + n);
-        if (!topics_.empty()) oldest_ = std::chrono::steady_clock::now();
-        st_.batches++;
-        st_.topics += n;
-        if (n > st_.largest) st_.largest = n;
       }
+      // seal: every queue's topics, in queue order (at most max_batch; a queue that would
+      // overflow the batch keeps its topics and its segment for the next one)
+      topics.clear();
+      segs.clear();
+      for (uint32_t s = 0; s < kShards; s++) {
+        Shard& sh = shards_[(s + rr_) % kShards];
+        std::lock_guard<std::mutex> lk(sh.mu);
+        if (sh.topics.empty()) continue;
+        if (!topics.empty() && topics.size() + sh.topics.size() > max_batch_) continue;
+        const uint32_t base = (uint32_t)topics.size();
+        for (std::string& t : sh.topics) topics.push_back(std::move(t));
+        segs.emplace_back(std::move(sh.seg), base);
+        sh.topics.clear();
+        sh.seg.reset();
+      }
+      rr_++;  // the next batch starts at another queue (none waits behind the others for ever)
+      if (topics.empty()) continue;
+      queued_.fetch_sub(topics.size(), std::memory_order_acq_rel);
+      std::shared_ptr<const std::vector<R>> res;
+      std::exception_ptr err;
       try {
-        std::vector<R> res = match_(topics);
-        for (size_t i = 0; i < waiters.size(); i++) waiters[i].set_value(std::move(res[i]));
+        res = std::make_shared<const std::vector<R>>(match_(topics));
       } catch (...) {
-        for (auto& w : waiters) w.set_exception(std::current_exception());
+        err = std::current_exception();
       }
+      for (auto& sg : segs) {
+        {
+          std::lock_guard<std::mutex> lk(sg.first->mu);
+          sg.first->results = res;
+          sg.first->err = err;
+          sg.first->base = sg.second;
+          sg.first->done = true;
+        }
+        sg.first->cv.notify_all();
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      st_.batches++;
+      st_.topics += topics.size();
+      st_.largest = std::max<uint64_t>(st_.largest, topics.size());
     }
   }
 
   MatchFn match_;
   const size_t max_batch_;
   const std::chrono::microseconds max_delay_;
+  const size_t min_fill_;
+  Shard shards_[kShards];
+  std::atomic<uint64_t> queued_{0};
+  uint32_t rr_ = 0;
   mutable std::mutex mu_;
   std::condition_variable cv_;
-  std::vector<std::string> topics_;
-  std::vector<std::promise<R>> waiters_;
-  std::chrono::steady_clock::time_point oldest_;
   bool stop_ = false;
   Stats st_;
   std::thread th_;
@@ -125,18 +206,20 @@ class BasicBatcher {
 
 class PublishBatcher : public BasicBatcher<Subscribers> {
  public:
-  explicit PublishBatcher(TopicsIndex& ix, size_t max_batch = 65536,
-                          std::chrono::microseconds max_delay = std::chrono::microseconds(200))
+  explicit PublishBatcher(TopicsIndex& ix, size_t max_batch = 16384,
+                          std::chrono::microseconds max_delay = std::chrono::microseconds(200),
+                          size_t min_fill = 1024)
       : BasicBatcher([&ix](const std::vector<std::string>& t) { return ix.SubscribersBatch(t); }, max_batch,
-                     max_delay) {}
+                     max_delay, min_fill) {}
 };
 
 class PublishViewBatcher : public BasicBatcher<TopicView> {
  public:
-  explicit PublishViewBatcher(TopicsIndex& ix, size_t max_batch = 65536,
-                              std::chrono::microseconds max_delay = std::chrono::microseconds(200))
+  explicit PublishViewBatcher(TopicsIndex& ix, size_t max_batch = 16384,
+                              std::chrono::microseconds max_delay = std::chrono::microseconds(200),
+                              size_t min_fill = 1024)
       : BasicBatcher([&ix](const std::vector<std::string>& t) { return ix.SubscribersViews(t); }, max_batch,
-                     max_delay) {}
+                     max_delay, min_fill) {}
 };
 
 }  // namespace host

@@ -27,6 +27,7 @@ import (
 	"math"
 	"strings"
 	"sync"
+	"time"
 	"unsafe"
 
 	"github.com/xyzj/mqtt-server/packets"
@@ -195,6 +196,9 @@ type TopicsIndex struct {
 	upd      sync.Mutex
 	tables   sync.RWMutex
 	ep       *epochs
+	// the batching stage Subscribers goes through (started on first use)
+	batcherOnce sync.Once
+	batcher     *MatchBatcher
 	clients  *idTable
 	filters  *idTable
 	topics   *idTable // retained topic names: handle = topic id, referenced while in Retained
@@ -438,9 +442,129 @@ func (x *TopicsIndex) Messages(filter string) []packets.Packet {
 	return pks
 }
 
-// Subscribers (topics.go:583-590): a batch of one.
+// Subscribers (topics.go:583-590). publishToSubscribers calls it once per publish from every
+// connection goroutine (server.go:1000); the call goes through the index's batching stage, which
+// matches the topics of many goroutines with one engine call (MatchBatcher below), so server.go
+// keeps calling Subscribers unchanged.
 func (x *TopicsIndex) Subscribers(topic string) *Subscribers {
-	return x.SubscribersBatch([]string{topic})[0]
+	x.batcherOnce.Do(func() { x.batcher = NewMatchBatcher(x, DefaultMaxBatch, DefaultMinFill, DefaultMaxDelay) })
+	return x.batcher.Subscribers(topic)
+}
+
+// The batching stage's defaults (SURVEY.md §8f.1; DESIGN.md §7 has the measured batch latency).
+const (
+	DefaultMaxBatch = 16384                  // topics per engine call at most
+	DefaultMinFill  = 1024                   // a batch with fewer topics waits for more ...
+	DefaultMaxDelay = 200 * time.Microsecond // ... up to this long
+)
+
+// MatchBatcher is the batching stage of the publish pipeline (SURVEY.md §8f.1): connection
+// goroutines hand their topic to one loop goroutine per index and wait for their result; the loop
+// takes every request queued when the previous batch is done — under load, what arrived while it
+// was matched — waits up to maxDelay for more when it holds fewer than minFill, and matches the
+// batch with one SubscribersBatch call (one cgo call). Each caller gets exactly Subscribers(topic)
+// on the index state the batch ran against (readers take no root lock in the reference either,
+// topics.go:583, Q11), so the OnSelectSubscribers hook (hooks.go:360-367), SelectShared /
+// MergeSharedSelected and the fan-out after it (server.go:1001-1021) are unchanged.
+type MatchBatcher struct {
+	x        *TopicsIndex
+	in       chan matchReq
+	maxBatch int
+	minFill  int
+	maxDelay time.Duration
+	done     chan struct{}
+}
+
+type matchReq struct {
+	topic string
+	reply chan *Subscribers
+}
+
+var replyChans = sync.Pool{New: func() any { return make(chan *Subscribers, 1) }}
+
+// NewMatchBatcher starts a batching stage over x.
+func NewMatchBatcher(x *TopicsIndex, maxBatch, minFill int, maxDelay time.Duration) *MatchBatcher {
+	if maxBatch <= 0 {
+		maxBatch = DefaultMaxBatch
+	}
+	if minFill <= 0 || minFill > maxBatch {
+		minFill = maxBatch
+	}
+	b := &MatchBatcher{x: x, in: make(chan matchReq, 4*maxBatch), maxBatch: maxBatch, minFill: minFill,
+		maxDelay: maxDelay, done: make(chan struct{})}
+	go b.loop()
+	return b
+}
+
+// Subscribers enqueues topic and waits for the batch it joins.
+func (b *MatchBatcher) Subscribers(topic string) *Subscribers {
+	r := replyChans.Get().(chan *Subscribers)
+	b.in <- matchReq{topic, r}
+	s := <-r
+	replyChans.Put(r)
+	return s
+}
+
+// Close matches what is queued and stops the loop; no Subscribers call may follow.
+func (b *MatchBatcher) Close() {
+	close(b.in)
+	<-b.done
+}
+
+func (b *MatchBatcher) loop() {
+	defer close(b.done)
+	batch := make([]matchReq, 0, b.maxBatch)
+	topics := make([]string, 0, b.maxBatch)
+	timer := time.NewTimer(time.Hour)
+	timer.Stop()
+	for {
+		r, ok := <-b.in
+		if !ok {
+			return
+		}
+		batch = append(batch[:0], r)
+		open := true
+	drain: // everything queued now, without waiting
+		for len(batch) < b.maxBatch {
+			select {
+			case r, ok := <-b.in:
+				if !ok {
+					open = false
+					break drain
+				}
+				batch = append(batch, r)
+			default:
+				break drain
+			}
+		}
+		if open && len(batch) < b.minFill && b.maxDelay > 0 { // a small batch waits a little for more
+			timer.Reset(b.maxDelay)
+		wait:
+			for len(batch) < b.maxBatch {
+				select {
+				case r, ok := <-b.in:
+					if !ok {
+						break wait
+					}
+					batch = append(batch, r)
+					if len(batch) >= b.minFill {
+						break wait
+					}
+				case <-timer.C:
+					break wait
+				}
+			}
+			timer.Stop()
+		}
+		topics = topics[:0]
+		for _, r := range batch {
+			topics = append(topics, r.topic)
+		}
+		for i, s := range b.x.SubscribersBatch(topics) {
+			batch[i].reply <- s
+		}
+		clear(batch) // drop the references to the replies
+	}
 }
 
 // SubscribersBatch matches many topics in one engine call (span format: the index's own

@@ -279,7 +279,7 @@ static void TestPublishBatcher() {
     for (int k = 0; k < n; k++) t += (k ? "/" : "") + std::string(segs[r() % 4]);
     topics.push_back(t);
   }
-  std::vector<std::vector<std::future<mq::host::Subscribers>>> futs(8);
+  std::vector<std::vector<mq::host::PublishBatcher::Ticket>> futs(8);
   {
     mq::host::PublishBatcher b(ix, 4096, std::chrono::microseconds(2000));
     std::vector<std::thread> th;
@@ -447,14 +447,14 @@ static void TestPublishViewBatcher() {
     const std::string f = std::string(i % 7 == 0 ? "$share/g/" : "") + "v/" + std::to_string(r() % 20) + (i % 2 ? "/+" : "/#");
     ix.Subscribe("c" + std::to_string(r() % 40), S(f, (uint8_t)(r() % 3), (int)(r() % 3)));
   }
-  std::vector<std::future<mq::host::TopicView>> futs;
+  std::vector<mq::host::PublishViewBatcher::Ticket> futs;
   {
     mq::host::PublishViewBatcher b(ix, 256, std::chrono::microseconds(1000));
     for (int i = 0; i < 400; i++) futs.push_back(b.Submit("v/" + std::to_string(i % 20) + "/x"));
     for (auto& f : futs) f.wait();
   }
   for (int i = 0; i < 400; i++) {
-    const mq::host::TopicView v = futs[i].get();
+    const mq::host::TopicView& v = futs[i].get();
     const mq::host::Subscribers want = ix.Subscribers_("v/" + std::to_string(i % 20) + "/x");
     std::map<std::string, int> qos;
     v.for_each_row([&](const mq_client_row& cr) {
@@ -468,6 +468,189 @@ static void TestPublishViewBatcher() {
     for (auto& g : want.Shared) want_shared += g.second.size();
     REQUIRE(shared == want_shared);
   }
+}
+
+// The batching stage under many submitters, checked against the ORACLE (the CPU restatement of
+// the Go TopicsIndex, oracle/liboracle.so, test infrastructure): 32 threads keep 64 topics each
+// in flight through PublishBatcher; a sample of the tickets is compared with the oracle's
+// Subscribers(topic), as canonical JSON (sorted keys: Go map order is irrelevant).
+extern "C" {
+void* orc_new();
+void orc_free(void*);
+int orc_subscribe(void* h, const char* client, uint32_t clen, const char* filter, uint32_t flen, uint32_t client_id,
+                  uint32_t filter_id, uint8_t qos, uint8_t flags, int64_t identifier);
+int orc_inline_subscribe(void* h, const char* filter, uint32_t flen, int64_t id, uint32_t filter_id);
+uint64_t orc_subscribers_json(void* h, const char* topic, uint32_t tlen, char* buf, uint64_t cap);
+}
+
+static std::string jesc(const std::string& s) {
+  std::string o;
+  for (unsigned char ch : s) {
+    if (ch == '"' || ch == '\\') {
+      o += '\\';
+      o += (char)ch;
+    } else if (ch < 0x20) {
+      char b[8];
+      std::snprintf(b, sizeof b, "\\u%04x", ch);
+      o += b;
+    } else {
+      o += (char)ch;
+    }
+  }
+  return o;
+}
+
+static void sub_json(std::string& o, const Subscription& s, bool with_idents) {
+  char b[160];
+  o += "{\"filter\":\"" + jesc(s.Filter) + "\"";
+  std::snprintf(b, sizeof b, ",\"identifier\":%lld,\"qos\":%u,\"no_local\":%s,\"rap\":%s,\"rh\":%u",
+                (long long)s.Identifier, s.Qos, s.NoLocal ? "true" : "false", s.RetainAsPublished ? "true" : "false",
+                s.RetainHandling);
+  o += b;
+  if (with_idents) {
+    o += ",\"identifiers\":";
+    if (!s.HasIdentifiers) {
+      o += "null";
+    } else {
+      o += "{";
+      bool first = true;
+      for (auto& kv : s.Identifiers) {
+        if (!first) o += ",";
+        first = false;
+        o += "\"" + jesc(kv.first) + "\":" + std::to_string(kv.second);
+      }
+      o += "}";
+    }
+  }
+  o += "}";
+}
+
+static std::string subscribers_json(const mq::host::Subscribers& s) {
+  std::string o = "{\"subscriptions\":{";
+  bool first = true;
+  for (auto& kv : s.Subscriptions) {
+    if (!first) o += ",";
+    first = false;
+    o += "\"" + jesc(kv.first) + "\":";
+    sub_json(o, kv.second, true);
+  }
+  o += "},\"shared\":{";
+  first = true;
+  for (auto& g : s.Shared) {
+    if (!first) o += ",";
+    first = false;
+    o += "\"" + jesc(g.first) + "\":{";
+    bool f2 = true;
+    for (auto& kv : g.second) {
+      if (!f2) o += ",";
+      f2 = false;
+      o += "\"" + jesc(kv.first) + "\":";
+      sub_json(o, kv.second, true);
+    }
+    o += "}";
+  }
+  o += "},\"inline\":{";
+  first = true;
+  for (auto& kv : s.InlineSubscriptions) {
+    if (!first) o += ",";
+    first = false;
+    o += "\"" + std::to_string(kv.first) + "\":";
+    sub_json(o, kv.second.Sub, false);
+  }
+  o += "}}";
+  return o;
+}
+
+static std::string oracle_json(void* orc, const std::string& t) {
+  std::string buf(orc_subscribers_json(orc, t.data(), (uint32_t)t.size(), nullptr, 0), '\0');
+  orc_subscribers_json(orc, t.data(), (uint32_t)t.size(), &buf[0], buf.size());
+  return buf;
+}
+
+static void TestBatcherManySubmittersVsOracle() {
+  TopicsIndex ix;
+  void* orc = orc_new();
+  std::mt19937 r(23);
+  const char* segs[] = {"a", "b", "c", "d", "e", "+", "#"};
+  std::map<std::string, uint32_t> fids, cids;
+  for (int i = 0; i < 6000; i++) {
+    std::string f;
+    const int n = 1 + (int)(r() % 5);
+    for (int k = 0; k < n; k++) f += (k ? "/" : "") + std::string(segs[r() % (k + 1 == n ? 7 : 6)]);
+    if (i % 9 == 0) f = std::string(i % 2 ? "$share" : "$SHARE") + "/g" + std::to_string(i % 4) + "/" + f;
+    const std::string c = "c" + std::to_string(r() % 400);
+    Subscription s = S(f, (uint8_t)(r() % 3), (int)(r() % 5), r() % 11 == 0);
+    s.RetainAsPublished = r() % 2;
+    s.RetainHandling = (uint8_t)(r() % 3);
+    ix.Subscribe(c, s);
+    const uint32_t fid = fids.emplace(f, (uint32_t)fids.size()).first->second;
+    const uint32_t cid = cids.emplace(c, (uint32_t)cids.size()).first->second;
+    orc_subscribe(orc, c.data(), (uint32_t)c.size(), f.data(), (uint32_t)f.size(), cid, fid, s.Qos,
+                  (uint8_t)((s.NoLocal ? 1 : 0) | (s.RetainAsPublished ? 2 : 0) | (s.RetainHandling << 2)),
+                  s.Identifier);
+  }
+  for (int id = 1; id <= 3; id++) {  // inline subscriptions (last write wins, Q8)
+    InlineSubscription in;
+    in.Sub.Filter = id == 1 ? "a/#" : id == 2 ? "+/b" : "a/b";
+    in.Sub.Identifier = id;
+    ix.InlineSubscribe(in);
+    const uint32_t fid = fids.emplace(in.Sub.Filter, (uint32_t)fids.size()).first->second;
+    orc_inline_subscribe(orc, in.Sub.Filter.data(), (uint32_t)in.Sub.Filter.size(), id, fid);
+  }
+  std::vector<std::string> topics;
+  for (int i = 0; i < 512; i++) {
+    std::string t = i % 53 == 0 ? "$SYS" : std::string(segs[r() % 5]);
+    const int n = (int)(r() % 5);
+    for (int k = 0; k < n; k++) t += "/" + std::string(segs[r() % 5]);
+    topics.push_back(t);
+  }
+  constexpr int kThreads = 32, kPer = 600, kWindow = 64;
+  std::atomic<int> bad{0}, checked{0};
+  mq::host::PublishBatcher::Stats st;
+  {
+    mq::host::PublishBatcher b(ix, 4096, std::chrono::microseconds(500), 512);
+    std::vector<std::thread> th;
+    std::mutex omu;  // the oracle is not thread-safe
+    for (int w = 0; w < kThreads; w++)
+      th.emplace_back([&, w] {
+        std::vector<std::pair<int, mq::host::PublishBatcher::Ticket>> q;
+        size_t head = 0;
+        for (int i = 0; i < kPer || head < q.size();) {
+          while (i < kPer && (int)(q.size() - head) < kWindow) {
+            const int k = (w * 131 + i * 7) % (int)topics.size();
+            q.emplace_back(k, b.Submit(topics[k]));
+            i++;
+          }
+          const auto& [k, tk] = q[head];
+          const mq::host::Subscribers& got = tk.get();
+          if (head % 5 == 0) {
+            const std::string mine = subscribers_json(got);
+            std::string want;
+            {
+              std::lock_guard<std::mutex> lk(omu);
+              want = oracle_json(orc, topics[k]);
+            }
+            if (mine != want) {
+              if (bad++ < 3) std::fprintf(stderr, "batcher vs oracle, topic %s:\n  got  %s\n  want %s\n",
+                                          topics[k].c_str(), mine.c_str(), want.c_str());
+            }
+            checked++;
+          }
+          q[head].second = mq::host::PublishBatcher::Ticket();
+          head++;
+        }
+      });
+    for (auto& t : th) t.join();
+    st = b.stats();
+  }
+  std::printf("batcher, %d submitters: %llu topics in %llu batches (largest %llu); %d checked against the oracle\n",
+              kThreads, (unsigned long long)st.topics, (unsigned long long)st.batches,
+              (unsigned long long)st.largest, checked.load());
+  REQUIRE(bad == 0);
+  REQUIRE(checked > 1000);
+  REQUIRE(st.topics == (uint64_t)kThreads * kPer);
+  REQUIRE(st.largest > 64);  // submitters' topics were matched together
+  orc_free(orc);
 }
 
 // progress on stderr: a test that does not return is named by the last line
@@ -497,6 +680,7 @@ int main() {
     RUN(TestLoadSubscriptions);
     RUN(TestRetainedAddAfterExpiry);
     RUN(TestPublishViewBatcher);
+    RUN(TestBatcherManySubmittersVsOracle);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());
     return 2;

@@ -21,7 +21,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _replicated_worker(rank, world, port, out):
+def _guarded(fn, rank, world, port, out):
+    """A worker that fails reports its traceback through the queue (the test fails at once
+    instead of waiting for a result that never comes)."""
+    try:
+        fn(rank, world, port, out)
+    except BaseException:
+        import traceback
+        out.put(("error", rank, traceback.format_exc()))
+        raise
+
+
+def _get(q, timeout=150):
+    got = q.get(timeout=timeout)
+    if isinstance(got, tuple) and got and got[0] == "error":
+        raise AssertionError(f"rank {got[1]} failed:\n{got[2]}")
+    return got
+
+
+def _replicated_worker_body(rank, world, port, out):
     import sys
     sys.path.insert(0, os.path.join(REPO, "mqtt-server_amd"))
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -44,6 +62,10 @@ def _replicated_worker(rank, world, port, out):
     D.finalize(backend)
 
 
+def _replicated_worker(rank, world, port, out):
+    _guarded(_replicated_worker_body, rank, world, port, out)
+
+
 def test_two_rank_engine_replicated(gpu_available):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -51,7 +73,7 @@ def test_two_rank_engine_replicated(gpu_available):
     procs = [ctx.Process(target=_replicated_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    got = _get(q)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -70,7 +92,7 @@ def test_two_rank_engine_replicated(gpu_available):
     assert got == np.concatenate(ref).tolist()
 
 
-def _sharded_worker(rank, world, port, out):
+def _sharded_worker_body(rank, world, port, out):
     import sys
     sys.path.insert(0, os.path.join(REPO, "mqtt-server_amd"))
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -100,6 +122,10 @@ def _sharded_worker(rank, world, port, out):
     D.finalize(backend)
 
 
+def _sharded_worker(rank, world, port, out):
+    _guarded(_sharded_worker_body, rank, world, port, out)
+
+
 def test_two_rank_engine_sharded(gpu_available):
     """The sharded mode across processes: each rank holds one shard, matches the full batch and
     exchanges its cross-shard list through the process group (gloo here; RCCL under the bench)."""
@@ -109,7 +135,7 @@ def test_two_rank_engine_sharded(gpu_available):
     procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    parts = q.get(timeout=240)
+    parts = _get(q)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -2,16 +2,18 @@
 // 10M, config-3 mix, restored through TopicsIndex::LoadSubscriptions), for batch sizes 1, 64,
 // 1k, 16k and 64k:
 //   match   one mq_match_spans call (host span result) per batch: call latency p50 / p99
-//   batcher PublishViewBatcher(max_batch = B): a producer keeps 2B topics in flight; latency of
-//           each Submit until its future is ready (p50 / p99), throughput, and the recipients
-//           per topic of the views the producer read (one in 64: the broker's fan-out reads
-//           them on its connection goroutines, not on one thread)
+//   batcher PublishViewBatcher(max_batch = B >= 1024): 64 submitter threads (connection
+//           goroutines) keep 2B topics in flight together; latency of each Submit until its
+//           ticket is ready (p50 / p99), throughput, batches formed, and the recipients per
+//           topic of the views read (one in 64: the fan-out reads them on the connection
+//           goroutines, not on the submitting thread)
 // Prints one JSON object per line. Built by mqtt-server_amd/Makefile (build/latency).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <atomic>
 #include <future>
 #include <string>
 #include <thread>
@@ -118,47 +120,61 @@ int main(int argc, char** argv) {
                 B, calls, p50, p99, calls * B / mt, (double)rows / (calls * B));
     std::fflush(stdout);
 
-    // batcher: 2B topics in flight
-    std::vector<double> wl;
-    uint64_t recipients = 0, sampled = 0;
+    // batcher: kSubmitters threads (connection goroutines) keep 2B topics in flight together
+    if (B < 1024) continue;  // (the stage is measured at the batch sizes a broker would run)
+    constexpr int kSubmitters = 64;
+    const size_t window = std::max<size_t>(1, 2 * B / kSubmitters);
+    std::vector<std::vector<double>> wl(kSubmitters);
+    std::vector<uint64_t> recipients(kSubmitters, 0), sampled(kSubmitters, 0), done(kSubmitters, 0);
     {
-      mq::host::PublishViewBatcher pb(ix, B, std::chrono::microseconds(200));
-      std::deque<std::pair<Clock::time_point, std::future<mq::host::TopicView>>> q;
+      mq::host::PublishViewBatcher pb(ix, B, std::chrono::microseconds(200), std::min<size_t>(B, 1024));
       const auto b0 = Clock::now();
-      size_t submitted = 0, done = 0;
-      while (std::chrono::duration<double>(Clock::now() - b0).count() < secs || done < 20 * B) {
-        while (q.size() < 2 * B) {
-          q.emplace_back(Clock::now(), pb.Submit(topics[at]));
-          at = (at + 1) % topics.size();
-          submitted++;
-        }
-        auto& f = q.front();
-        f.second.wait();
-        wl.push_back(std::chrono::duration<double, std::micro>(Clock::now() - f.first).count());
-        const mq::host::TopicView v = f.second.get();
-        // the fan-out reads every view on the broker's connection goroutines; here one view in
-        // 64 is read (on this, the submitting thread) so the stage, not one reader, is measured
-        if (done % 64 == 0) {
-          v.for_each_row([&](const mq_client_row&) { recipients++; });
-          sampled++;
-        }
-        q.pop_front();
-        done++;
-        if (done >= 4000000) break;
-      }
-      while (!q.empty()) {
-        q.front().second.wait();
-        q.pop_front();
-      }
+      std::atomic<bool> stop{false};
+      std::vector<std::thread> th;
+      for (int w = 0; w < kSubmitters; w++)
+        th.emplace_back([&, w] {
+          std::deque<std::pair<Clock::time_point, mq::host::PublishViewBatcher::Ticket>> q;
+          size_t at_w = (size_t)w * 9973;
+          for (;;) {
+            while (!stop && q.size() < window) {
+              q.emplace_back(Clock::now(), pb.Submit(topics[at_w % topics.size()]));
+              at_w += 7;
+            }
+            if (q.empty()) break;
+            auto& f = q.front();
+            const mq::host::TopicView& v = f.second.get();
+            wl[w].push_back(std::chrono::duration<double, std::micro>(Clock::now() - f.first).count());
+            // the fan-out reads every view on the broker's connection goroutines; one in 64 is
+            // read here, so that the stage, not the readers, is measured
+            if (done[w] % 64 == 0) {
+              v.for_each_row([&](const mq_client_row&) { recipients[w]++; });
+              sampled[w]++;
+            }
+            q.pop_front();
+            done[w]++;
+          }
+        });
+      std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+      stop = true;
+      for (auto& t : th) t.join();
       const double bt = std::chrono::duration<double>(Clock::now() - b0).count();
       const auto st = pb.stats();
-      const double w50 = pct(wl, 0.50), w99 = pct(wl, 0.99);
-      std::printf("{\"path\": \"PublishViewBatcher\", \"batch\": %zu, \"topics\": %zu, \"p50_us\": %.1f, "
-                  "\"p99_us\": %.1f, \"topics_per_s\": %.0f, \"mean_batch\": %.1f, \"recipients_per_topic\": %.1f}\n",
-                  B, done, w50, w99, done / bt, (double)st.topics / std::max<uint64_t>(st.batches, 1),
-                  (double)recipients / std::max<uint64_t>(sampled, 1));
+      std::vector<double> all;
+      uint64_t n_done = 0, n_rec = 0, n_smp = 0;
+      for (int w = 0; w < kSubmitters; w++) {
+        all.insert(all.end(), wl[w].begin(), wl[w].end());
+        n_done += done[w];
+        n_rec += recipients[w];
+        n_smp += sampled[w];
+      }
+      const double w50 = pct(all, 0.50), w99 = pct(all, 0.99);
+      std::printf("{\"path\": \"PublishViewBatcher\", \"max_batch\": %zu, \"submitters\": %d, \"in_flight\": %zu, "
+                  "\"topics\": %llu, \"p50_us\": %.1f, \"p99_us\": %.1f, \"topics_per_s\": %.0f, \"mean_batch\": %.1f, "
+                  "\"largest_batch\": %llu, \"recipients_per_topic\": %.1f}\n",
+                  B, kSubmitters, window * kSubmitters, (unsigned long long)n_done, w50, w99, n_done / bt,
+                  (double)st.topics / std::max<uint64_t>(st.batches, 1), (unsigned long long)st.largest,
+                  (double)n_rec / std::max<uint64_t>(n_smp, 1));
       std::fflush(stdout);
-      (void)submitted;
     }
   }
   return 0;
