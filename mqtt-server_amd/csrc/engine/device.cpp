@@ -1171,7 +1171,9 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (one_sync) {  // the set count is read at the batch's end; the set pass strides over it
       hip_check(hipMemcpyAsync(h_fast_->n_sets, dd_nsets_.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
                 "D2H");
-      sb_.n_sets = last_sets_ + last_sets_ / 8 + 256;  // the grid: the last batch's count, with room
+      // the grid: the last batch's count with room (the set pass strides over the true count);
+      // with none yet, as many waves as topics (an unused one exits at once)
+      sb_.n_sets = last_sets_ ? last_sets_ + last_sets_ / 8 + 256 : n;
     } else if (prof.on() || set_grid_) {
       unsigned long long two[2] = {0, 0};
       hip_check(hipMemcpyAsync(two, dd_nsets_.p, sizeof(two), hipMemcpyDeviceToHost, s), "D2H");
@@ -1179,6 +1181,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       const unsigned long long ns = two[0] + two[1];
       if (prof.on()) prof.count("dedup_sets", ns);
       sb_.n_sets = ns;
+      last_sets_ = ns;
     }
   }
 

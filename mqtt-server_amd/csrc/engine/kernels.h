@@ -26,7 +26,7 @@ constexpr uint32_t kMergeBlocksPerCU = 0;  // persistent k_merge beside it (side
 constexpr uint32_t kMapSlots = 128;    // per-wave LDS map (gathered merge node -> gather index)
 constexpr uint32_t kPairMax = 64;     // merge gathers covered by the pair analysis
 constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
-constexpr uint32_t kPartBatch = 8;     // partner links loaded together per record
+constexpr uint32_t kPartBatch = 4;     // partner links loaded together per record
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
@@ -398,6 +398,7 @@ struct MsgPiece {
 constexpr uint32_t kMsgPiece = 4096;    // handles per copy piece (a wavefront's work item)
 constexpr uint32_t kMsgDirect = 8;      // runs this short are copied by the walk itself
 constexpr uint32_t kMsgStack = 16;      // nested fan-outs a lane can hold (deeper: kErrMsgNest)
+constexpr uint32_t kMsgFront = 256;     // k_msgq fan-out frontier: runs per level a wavefront holds in LDS
 constexpr uint32_t kErrMsgNest = 16u;   // k_msgq: fan-out nesting beyond kMsgStack (walk k_msg)
 
 // u32 exclusive scan: out[i] = in[0] + ... + in[i - 1], out[n] = total (out may be in).

@@ -1836,15 +1836,20 @@ void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* 
     hipLaunchKernelGGL((k_walkf<G, L, 8>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count); \
   else                                                                                                           \
     hipLaunchKernelGGL((k_walkf<G, L, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
-  if (group == 8) {
-    if (lists) MQ_WALKF(8, true);
-    else MQ_WALKF(8, false);
-  } else if (group == 16) {
+  if (group == 16) {
     if (lists) MQ_WALKF(16, true);
     else MQ_WALKF(16, false);
-  } else {
-    if (lists) MQ_WALKF(4, true);
-    else MQ_WALKF(4, false);
+  } else {  // (narrower groups: more topics per workgroup, so LDS bounds them below 8 waves)
+#define MQ_WALKF1(G, L) \
+  hipLaunchKernelGGL((k_walkf<G, L, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
+    if (group == 8) {
+      if (lists) MQ_WALKF1(8, true);
+      else MQ_WALKF1(8, false);
+    } else {
+      if (lists) MQ_WALKF1(4, true);
+      else MQ_WALKF1(4, false);
+    }
+#undef MQ_WALKF1
   }
 #undef MQ_WALKF
   // the topics the frontier could not hold: thread per topic, grid-stride over the list
@@ -2714,6 +2719,8 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
   constexpr bool FILL = MODE == kMsgFill || MODE == kMsgPlace;  // the walk writes output
   constexpr bool RUNS = MODE == kMsgRuns;
   __shared__ uint32_t hcur[4], pcur[4], rcur[4];  // next handle / piece / run of the wave's filter
+  __shared__ uint2 mfront[4][2][kMsgFront];       // fan-out frontier: runs of one level (two buffers)
+  __shared__ uint32_t mpre[4][kMsgFront + 1];      // ... particles before each run
   const uint32_t lane = threadIdx.x & 63, wv = wave_id();
   const uint32_t t = blockIdx.x * 4 + wv;
   if (t >= n) return;  // wave-uniform
@@ -2844,63 +2851,157 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         b = qc + 1;
         s = e + 1;
       }
-      if (fan) {  // lanes take the run's particles; each walks the rest of the filter alone
-        MsgFrame st[kMsgStack];
-        for (uint32_t u = a + lane; u < b; u += 64) {
-          uint32_t sp = 0, ua = u, ub = u + 1;
-          uint64_t us = s;
-          for (uint64_t guard = 0;; guard++) {
-            if (guard > kWalkGuard) {
-              atomicOr(ix.err, kErrWalkGuard);
-              break;
-            }
-            bool pop = false;
-            const uint64_t e = find_slash(R, us, b1);
-            const bool last = e >= b1;
-            const uint32_t len = (uint32_t)(e - us);
-            const uint32_t c0 = len == 1 ? R.at(us) : 0u;
-            if (c0 == '+' || c0 == '#') {
-              uint32_t x, y;
-              desc(ua, ub, x, y);
-              if (last) {
-                emit_final(c0 == '#', x, y);
-                pop = true;
-              } else {
-                ua = x;
-                ub = y;
-                us = e + 1;
-                pop = ua >= ub;
-              }
-            } else if (ub - ua > 1) {  // a literal under a run: one particle now, the rest later
-              if (sp == kMsgStack) {
-                atomicOr(ix.err, kErrMsgNest);
+      if (fan) {
+        // A literal segment under a run of several particles. Level-synchronous fan-out: the
+        // frontier is a list of runs [x, y) of one level, in LDS; every lane takes particles of
+        // the same level, so a literal level's lookups are issued together with one key for the
+        // wave, a '+' maps each run to its children's run, and a final '+' / '#' emits each run.
+        // A frontier that outgrows its LDS falls back, run by run, to the per-lane walk
+        // (dfs_run: lanes take a run's particles, each walks the rest of the filter alone with
+        // deeper fan-outs on a frame stack).
+        auto dfs_run = [&](uint32_t ra, uint32_t rb, uint64_t rs) __attribute__((always_inline)) {
+          MsgFrame st[kMsgStack];
+          for (uint32_t u = ra + lane; u < rb; u += 64) {
+            uint32_t sp = 0, ua = u, ub = u + 1;
+            uint64_t us = rs;
+            for (uint64_t guard = 0;; guard++) {
+              if (guard > kWalkGuard) {
+                atomicOr(ix.err, kErrWalkGuard);
                 break;
               }
-              st[sp++] = MsgFrame{ua + 1, ub, (uint32_t)(us - b0)};
-              ub = ua + 1;
-            } else {
-              SegKey key = key_of(R, us, e);
-              const uint32_t qc = img_pos(img, lookup(ix, img.node[ua], key, fb + us, len));
-              if (qc == kNone) {
-                pop = true;
-              } else if (last) {
-                emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
-                pop = true;
+              bool pop = false;
+              const uint64_t e = find_slash(R, us, b1);
+              const bool last = e >= b1;
+              const uint32_t len = (uint32_t)(e - us);
+              const uint32_t c0 = len == 1 ? R.at(us) : 0u;
+              if (c0 == '+' || c0 == '#') {
+                uint32_t x, y;
+                desc(ua, ub, x, y);
+                if (last) {
+                  emit_final(c0 == '#', x, y);
+                  pop = true;
+                } else {
+                  ua = x;
+                  ub = y;
+                  us = e + 1;
+                  pop = ua >= ub;
+                }
+              } else if (ub - ua > 1) {  // a literal under a run: one particle now, the rest later
+                if (sp == kMsgStack) {
+                  atomicOr(ix.err, kErrMsgNest);
+                  break;
+                }
+                st[sp++] = MsgFrame{ua + 1, ub, (uint32_t)(us - b0)};
+                ub = ua + 1;
               } else {
-                ua = qc;
-                ub = qc + 1;
-                us = e + 1;
+                SegKey key = key_of(R, us, e);
+                const uint32_t qc = img_pos(img, lookup(ix, img.node[ua], key, fb + us, len));
+                if (qc == kNone) {
+                  pop = true;
+                } else if (last) {
+                  emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+                  pop = true;
+                } else {
+                  ua = qc;
+                  ub = qc + 1;
+                  us = e + 1;
+                }
+              }
+              if (pop) {
+                if (sp == 0) break;
+                MsgFrame& f = st[sp - 1];
+                ua = f.cur;
+                ub = ua + 1;
+                us = b0 + f.s;
+                if (++f.cur >= f.end) sp--;
               }
             }
-            if (pop) {
-              if (sp == 0) break;
-              MsgFrame& f = st[sp - 1];
-              ua = f.cur;
-              ub = ua + 1;
-              us = b0 + f.s;
-              if (++f.cur >= f.end) sp--;
+          }
+        };
+        uint2* cur = mfront[wv][0];
+        uint2* nxt = mfront[wv][1];
+        uint32_t nr = 1;
+        if (lane == 0) cur[0] = make_uint2(a, b);
+        wave_sync_lds();
+        uint64_t ls = s;  // the segment the frontier's runs take next
+        for (uint32_t guard = 0; guard < 4096; guard++) {
+          const uint64_t e = find_slash(R, ls, b1);
+          const bool last = e >= b1;
+          const uint32_t len = (uint32_t)(e - ls);
+          const uint32_t c0 = len == 1 ? R.at(ls) : 0u;
+          uint32_t nn = 0;  // the next frontier's runs (wave-uniform)
+          if (c0 == '+' || c0 == '#') {
+            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+              const uint32_t r = r0 + lane;
+              uint32_t x = 0, y = 0;
+              if (r < nr) {
+                const uint2 ru = cur[r];
+                desc(ru.x, ru.y, x, y);
+              }
+              if (last) {
+                if (r < nr) emit_final(c0 == '#', x, y);
+                continue;
+              }
+              const bool keep = r < nr && x < y;
+              const uint64_t bk = __ballot(keep);
+              const uint32_t at = nn + prefix_before(bk);
+              if (keep && at < kMsgFront) nxt[at] = make_uint2(x, y);
+              nn += (uint32_t)__popcll(bk);
+            }
+          } else {
+            // literal: every particle of every run looks the segment up; particle p of the
+            // frontier is found through the runs' prefix sums
+            const SegKey key = key_of(R, ls, e);
+            uint32_t tot = 0;
+            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+              const uint32_t r = r0 + lane;
+              const uint32_t v = r < nr ? cur[r].y - cur[r].x : 0u;
+              uint32_t ct;
+              const uint32_t ex = wave_excl_scan(v, lane, &ct);
+              if (r < nr) mpre[wv][r] = tot + ex;
+              tot += ct;
+            }
+            if (lane == 0) mpre[wv][nr] = tot;
+            wave_sync_lds();
+            for (uint32_t p0 = 0; p0 < tot; p0 += 64) {
+              const uint32_t p = p0 + lane;
+              uint32_t qc = kNone;
+              if (p < tot) {
+                uint32_t lo = 0, hi = nr;  // mpre[lo] <= p < mpre[hi]
+                while (hi - lo > 1) {
+                  const uint32_t mid = (lo + hi) >> 1;
+                  if (mpre[wv][mid] <= p) lo = mid;
+                  else hi = mid;
+                }
+                const uint32_t u = cur[lo].x + (p - mpre[wv][lo]);
+                qc = img_pos(img, lookup(ix, img.node[u], key, fb + ls, len));
+              }
+              if (last) {
+                if (qc != kNone) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+                continue;
+              }
+              const bool keep = qc != kNone;
+              const uint64_t bk = __ballot(keep);
+              const uint32_t at = nn + prefix_before(bk);
+              if (keep && at < kMsgFront) nxt[at] = make_uint2(qc, qc + 1);
+              nn += (uint32_t)__popcll(bk);
             }
           }
+          if (last) break;
+          if (nn > kMsgFront) {  // too wide for LDS: the per-lane walk from this level
+            for (uint32_t r = 0; r < nr; r++) {
+              const uint2 ru = cur[r];
+              dfs_run(ru.x, ru.y, ls);
+            }
+            break;
+          }
+          wave_sync_lds();  // the next frontier is complete; the current one is free
+          uint2* tmp = cur;
+          cur = nxt;
+          nxt = tmp;
+          nr = nn;
+          ls = e + 1;
+          if (nr == 0) break;
         }
       }
     }

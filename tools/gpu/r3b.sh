@@ -6,6 +6,9 @@ R=$GRAFT_REPO_ROOT
 D=$R/gpurun_out/${1:-r3b}
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp
+cd $R && timeout -k 10 300 python -u tools/tune_spans.py --subs 10000000 --reps 2 --configs "9=8;9=1" > $D/tune_walk_wpe.jsonl 2> $D/tune_walk_wpe.err || { echo "tune rc=$?"; tail -5 $D/tune_walk_wpe.err; exit 1; }
+cut -c1-300 $D/tune_walk_wpe.jsonl
+cd /tmp
 timeout -k 10 120 $R/tools/randbench > $D/randbench.txt 2>&1 || { echo "randbench rc=$?"; exit 1; }
 cat $D/randbench.txt
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/rb_fetch -o run -- $R/tools/randbench > /dev/null 2>$D/rb_fetch.err || { echo "rb fetch rc=$?"; exit 1; }
