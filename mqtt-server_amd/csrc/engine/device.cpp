@@ -1197,8 +1197,14 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.pcount = sp_pcount_.as<unsigned long long>();
   a.tc = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
   a.work = nullptr;
+  a.set_rec = nullptr;
   if (prof.work()) {  // [0]: the topics' pass, [1]: the merge sets' pass (dedup)
     grow(sp_work_, 2 * kPatchRegions * kWork * sizeof(unsigned long long));
+    if (sb_.dedup) {
+      grow(set_rec_, (size_t)n * sizeof(uint32_t));
+      hip_check(hipMemsetAsync(set_rec_.p, 0, (size_t)n * sizeof(uint32_t), s), "memset");
+      a.set_rec = set_rec_.as<uint32_t>();
+    }
     a.work = sp_work_.as<unsigned long long>();
     hip_check(hipMemsetAsync(a.work + kPatchRegions * kWork, 0, kPatchRegions * kWork * sizeof(unsigned long long), s),
               "memset");
@@ -1264,6 +1270,20 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       srcap_ = mr + mr / 4 + 64;
       dd_spatches_.release();
       dd_spatches_.ensure(srcap_ * kPatchRegions * sizeof(PatchRec));
+    }
+    if (a.set_rec) {  // MQ_PROF_WORK: how the resolution work spreads over the sets
+      std::vector<uint32_t> rec(n);
+      hip_check(hipMemcpyAsync(rec.data(), a.set_rec, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      std::sort(rec.begin(), rec.end(), std::greater<uint32_t>());
+      uint64_t tot = 0, top = 0, sets = 0;
+      for (uint32_t r : rec) tot += r, sets += r != 0;
+      for (uint64_t i = 0; i < sets / 100; i++) top += rec[i];
+      prof.count("set_records_max", rec.empty() ? 0 : rec[0]);
+      prof.count("set_records_top1pct", top);
+      prof.count("set_records_total", tot);
+      prof.count("sets_over_4096_records", (uint64_t)std::count_if(rec.begin(), rec.end(), [](uint32_t r) { return r > 4096; }));
+      a.set_rec = nullptr;
     }
     a.work = work0;
     a.dd_phase = 2;

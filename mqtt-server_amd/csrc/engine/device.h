@@ -329,6 +329,7 @@ class Device {
   DevBuf dd_mpair_;                            // k_desc: merge gathers' pair-block headers
   DevBuf dd_mrank_;                            // ... and rank keys (sharded index)
   DevBuf dd_fcnt_;                             // k_xsig: cross-shard entries per topic
+  DevBuf set_rec_;                             // MQ_PROF_WORK: records resolved per merge set
   uint64_t srcap_ = 0;                         // set patches per region of dd_spatches_
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)
   uint32_t n_cus_ = 1;

@@ -538,16 +538,15 @@ void Index::trim(uint32_t n) {  // topics.go:516-522
 
 // ---- subscription lists ----------------------------------------------------------------------------
 // A slot is the SubRec plus its partner list; they always move together, and the
-// (node, client) -> slot map follows. A move changes the positions the device partner links
-// name: those of this node's slots and those held by the slot's partners.
+// (node, client) -> slot map follows. A move changes this node's device merge records (its
+// partner links sit at slot positions, its pair lists name slots); the partners' records name
+// this node and the subscription's Qos / NoLocal, not its position, so they stay as they are.
 void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
   const SubRec r = subs.m.h[from];
   subs.m.at_w(to) = r;
   subp_[to] = subp_[from];
   sub_pos_.put((uint64_t)n << 32 | r.client, to);
   merge_dirty(n);
-  const PartList& p = subp_[to];
-  for (uint32_t i = 0; i < p.cnt; i++) touch_partner(parts.m.h[p.off + i]);
 }
 
 void Index::merge_release(uint32_t n) {
@@ -823,7 +822,6 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
   subs.m.at_w(other) = a;
   subp_[other] = ap;
   sub_pos_.put((uint64_t)n << 32 | a.client, other);
-  for (uint32_t i = 0; i < ap.cnt; i++) touch_partner(parts.m.h[ap.off + i]);
 }
 
 void Index::part_set(uint32_t pos, const std::vector<uint32_t>& nodes) {
@@ -1057,10 +1055,13 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
                  ((uint32_t)((flags >> 2) & 3) << kMetaRhShift)};
   uint32_t pos;
   if (sub_pos_.get((uint64_t)n << 32 | client, &pos)) {
+    const SubRec old = subs.m.h[pos];
     subs.m.at_w(pos) = rec;
-    const PartList& p = subp_[pos];  // the partners' links carry this subscription's meta,
-    for (uint32_t i = 0; i < p.cnt; i++) touch_partner(parts.m.h[p.off + i]);
-    if (sub_is_merge(n, pos)) merge_dirty(n);  // and n's pair slots copy it
+    const PartList& p = subp_[pos];  // the partners' links carry this subscription's Qos / NoLocal,
+    if ((old.meta ^ rec.meta) & (kMetaQos | kMetaNoLocal))
+      for (uint32_t i = 0; i < p.cnt; i++) touch_partner(parts.m.h[p.off + i]);
+    // and n's pair slots copy its meta and whether its identifier is > 0
+    if (sub_is_merge(n, pos) && (old.meta != rec.meta || (old.ident > 0) != (rec.ident > 0))) merge_dirty(n);
     return 0;
   }
   // Partners: the client's other subscriptions that could match the same topic (the merge

@@ -142,6 +142,7 @@ struct EmitArgs {
   unsigned long long* pcount;     //   reserves in region t % kPatchRegions with atomicAdd on
   uint64_t rcap;                  //   pcount[region] (may exceed rcap: the host grows the pool)
   unsigned long long* work;       // MQ_PROF_WORK: per region kWork counters (null: off)
+  uint32_t* set_rec;              // MQ_PROF_WORK, set pass: records each representative resolved
   // sharded index: the other shards' exported cross-shard nodes of every topic (k_xlist), a
   // device table (a kernel-argument array indexed at run time would go through scratch)
   uint32_t n_xf;

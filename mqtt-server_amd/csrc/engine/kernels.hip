@@ -1726,6 +1726,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (lane == 0) a.sets[t] = SetInfo{pbase, n_patch, n_nonbase, n_ext, pfit ? 1u : 0u};
     if (a.work) {  // MQ_PROF_WORK (the resolution work happens here, once per set)
       const uint32_t e = wave_sum(w_ent), rr = wave_sum(w_rec), l = wave_sum(w_link);
+      if (a.set_rec && lane == 0) a.set_rec[t] = rr;
       unsigned long long* wc = a.work + (uint64_t)(t & (kPatchRegions - 1)) * kWork;
       if (lane == 0 && (e | rr | l)) {
         atomicAdd(wc + 0, (unsigned long long)e);

@@ -5,8 +5,9 @@ per-kernel tables kept under profiles/.
   python profiles/summarize.py gpurun_out/pmc1 gpurun_out/pmc2 --pmc
 
 HBM bytes follow MI355X_MICROARCH.md's HBM/rocprofv3 section: FETCH_SIZE and WRITE_SIZE are
-in KiB, come from separate passes, and FETCH_SIZE reads half the bytes of a wide coalesced
-stream on gfx950, so it is reported both raw and x2 ("corrected") next to WRITE_SIZE.
+in KiB, come from separate passes. FETCH_SIZE tallies 64 B per L2-to-fabric read request: a wide
+coalesced stream issues 128 B requests (x2, "corrected"), random sub-line loads 64 B ones (x1,
+"random"; calibrated with tools/randbench on the GPU, profiles/r03/walk_frontier/rb_pmc.json).
 """
 import collections
 import csv
@@ -59,8 +60,11 @@ def pmc(dirs):
             nf, nw = len(calls[(k, "FETCH_SIZE")]), len(calls[(k, "WRITE_SIZE")])
             fetch = v["FETCH_SIZE"] * 1024 / max(1, nf)
             write = v["WRITE_SIZE"] * 1024 / max(1, nw)
+            # FETCH_SIZE = 64 B per read request: x2 for 128 B streaming requests, x1 for the 64 B
+            # requests of random sub-line loads (calibrated with tools/randbench, pmc_traffic.json)
             e["hbm_bytes_per_dispatch"] = {"fetch_raw": fetch, "fetch_corrected_x2": 2 * fetch,
-                                           "write": write, "total_corrected": 2 * fetch + write}
+                                           "write": write, "total_corrected": 2 * fetch + write,
+                                           "total_random_x1": fetch + write}
         out[k] = e
     return out
 
