@@ -260,9 +260,10 @@ int mq_select_shared_device(mq_index* idx, const mq_match_result* chunk, void* h
  * particles with may-merge records are the same particles in the same order resolve to the same
  * patches up to where those particles' records sit in each topic's rows, so the batch resolves
  * each such merge set once. A topic with MQ_TOPIC_SET_PATCHES in its flags has its n_patches
- * patches at set_patches[patch_base, + n_patches), each naming its row as (x << 26 | k): the
- * k-th may-merge record of the topic's x-th particle with may-merge records, i.e. topic row
- * merge_rows[topic * 64 + x] + k. Host results (mq_match_spans) always hold per-topic patches.
+ * patches at set_patches[patch_base, + n_patches), each naming its row as (x << 26 | k): record
+ * k of the span of the topic's x-th particle with may-merge records, i.e. topic row
+ * merge_rows[topic * 64 + x] + k (merge_rows: the row of that span's first record). Host results
+ * (mq_match_spans) always hold per-topic patches.
  * With MQ_CFG_SELECT_SHARED the picked shared members are materialised (picked_rows at
  * picked_base, n_shared of them) and flags has MQ_SPANS_PICKED. */
 typedef struct mq_span {

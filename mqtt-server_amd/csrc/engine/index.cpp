@@ -541,22 +541,39 @@ void Index::trim(uint32_t n) {  // topics.go:516-522
 // (node, client) -> slot map follows. A move changes this node's device merge records (its
 // partner links sit at slot positions, its pair lists name slots); the partners' records name
 // this node and the subscription's Qos / NoLocal, not its position, so they stay as they are.
-void Index::move_slot(uint32_t n, uint32_t from, uint32_t to) {
+void Index::move_slot(uint32_t n, uint32_t from, uint32_t to, bool mark) {
   const SubRec r = subs.m.h[from];
   subs.m.at_w(to) = r;
   subp_[to] = subp_[from];
   sub_pos_.put((uint64_t)n << 32 | r.client, to);
-  merge_dirty(n);
+  if (mark) {
+    merge_dirty_slot(n, from);
+    merge_dirty_slot(n, to);
+  }
 }
 
 void Index::merge_release(uint32_t n) {
   NodeHost& h = nh_[n];
+  const NodePair& P = npair.h[n];
+  auto it = minc_.find(n);
+  if (it != minc_.end()) {  // slabs the in-place updates allocated outside the base slabs
+    for (const MergeInc::Slot& sl : it->second.slot)
+      if (sl.mp_cap && !(sl.mp_cap & kPairBase)) {
+        mpart.release(sl.mp_off, sl.mp_cap);
+        mpart.live -= sl.mp_cap;
+      }
+    if (P.ent_mask != kNone)
+      for (uint32_t i = 0; i <= P.ent_mask; i++) {
+        const PairEnt& e = pent.m.h[P.ent_off + i];
+        if (e.h != kNone && !(e.cap & kPairBase)) plist.release(e.off, e.cap);
+      }
+    minc_.erase(it);
+  }
   if (h.mpart_cap) {
     mpart.release(h.mpart_off, h.mpart_cap);
     mpart.live -= h.mpart_cap;
   }
   h.mpart_off = h.mpart_cap = 0;
-  const NodePair& P = npair.h[n];
   if (P.ent_mask != kNone) {
     pent.live -= P.n_lists;
     uint32_t links = 0;
@@ -564,7 +581,7 @@ void Index::merge_release(uint32_t n) {
       if (pent.m.h[P.ent_off + i].h != kNone) links += pent.m.h[P.ent_off + i].cnt;
     plist.live -= links;
     pent.release(P.ent_off, h.pent_cap);
-    plist.release(P.list_off, h.plist_cap);
+    if (h.plist_cap) plist.release(P.list_off, h.plist_cap);
   }
   h.pent_cap = h.plist_cap = 0;
   if (P.ent_mask != kNone || P.n_lists) npair.at_w(n) = NodePair{0, kNone, 0, 0};
@@ -574,76 +591,277 @@ void Index::flush_merge() {
   if (mref.size() < subs.m.size()) mref.grow_to(subs.m.size(), MergeRef{0, 0});
   for (uint32_t n : merge_dirty_) {
     merge_dirty_flag_[n] = 0;
+    auto it = minc_.find(n);
+    // in place while the base slabs' unused records stay below the ones in use
+    if (it != minc_.end() && nh_[n].live && it->second.garbage <= 2 * it->second.links + 4096) {
+      merge_patch(n, it->second);
+      continue;
+    }
     merge_release(n);
-    if (!nh_[n].live) continue;
-    const NodeLists& L = lists.h[n];
-    uint32_t links = 0, xs = 0;
-    for (uint32_t k = 0; k < L.n_merge; k++) {
-      const PartList& p = subp_[L.sub_off + L.n_direct + k];
-      links += p.cnt;
-      bool x = false;
-      for (uint32_t i = 0; i < p.cnt && !x; i++) x = (parts.m.h[p.off + i] & kForeign) != 0;
-      xs += x;
-    }
-    if ((xs != 0) != ((L.flags & kFlagXNode) != 0)) {
-      NodeLists& W = lists.at_w(n);
-      W.flags = xs ? (W.flags | kFlagXNode) : (W.flags & ~kFlagXNode);
-    }
-    nh_[n].x_slots = xs;
-    if (!links) continue;
-    uint32_t cap = 1;
-    while (cap < links) cap <<= 1;
-    const uint32_t off = mpart.alloc(cap);
-    uint32_t at = off;
-    for (uint32_t k = 0; k < L.n_merge; k++) {
-      const uint32_t pos = L.sub_off + L.n_direct + k;
-      const PartList& p = subp_[pos];
-      const uint32_t client = subs.m.h[pos].client;
-      mref.at_w(pos) = MergeRef{at, p.cnt};
-      for (uint32_t i = 0; i < p.cnt; i++) {
-        const uint32_t m = parts.m.h[p.off + i];
-        mpart.m.at_w(at++) = MergePart{m, partner_meta(m, client)};
-      }
-    }
-    nh_[n].mpart_off = off;
-    nh_[n].mpart_cap = cap;
-    mpart.live += cap;
-
-    // pair block: partner node h -> g's slots k whose client also subscribes at h
-    thread_local std::vector<std::pair<uint32_t, uint32_t>> hk;
-    hk.clear();
-    for (uint32_t k = 0; k < L.n_merge; k++) {
-      const PartList& p = subp_[L.sub_off + L.n_direct + k];
-      for (uint32_t i = 0; i < p.cnt; i++) hk.emplace_back(parts.m.h[p.off + i], k);
-    }
-    std::sort(hk.begin(), hk.end());
-    uint32_t lists_n = 0;
-    for (size_t i = 0; i < hk.size(); i++) lists_n += i == 0 || hk[i].first != hk[i - 1].first;
-    uint32_t ecap = 2, lcap = 1;
-    while (ecap < 4 * lists_n) ecap <<= 1;  // load <= 1/4: k_merge probes four slots per load round
-    while (lcap < hk.size()) lcap <<= 1;
-    const uint32_t eo = pent.alloc(ecap), lo = plist.alloc(lcap), mask = ecap - 1;
-    for (uint32_t i = 0; i < ecap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
-    for (size_t i = 0; i < hk.size(); i++) {
-      const MergeRef r = mref.h[L.sub_off + L.n_direct + hk[i].second];
-      const SubRec& rec = subs.m.h[L.sub_off + L.n_direct + hk[i].second];
-      plist.m.at_w(lo + i) = PairSlot{hk[i].second, r.off, r.cnt, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u)};
-    }
-    for (size_t b = 0; b < hk.size();) {
-      size_t e = b + 1;
-      while (e < hk.size() && hk[e].first == hk[b].first) e++;
-      uint32_t sl = pair_hash(hk[b].first) & mask;
-      while (pent.m.h[eo + sl].h != kNone) sl = (sl + 1) & mask;
-      pent.m.at_w(eo + sl) = PairEnt{hk[b].first, lo + (uint32_t)b, (uint32_t)(e - b), 0};
-      b = e;
-    }
-    pent.live += lists_n;
-    plist.live += hk.size();
-    npair.at_w(n) = NodePair{eo, mask, lo, lists_n};
-    nh_[n].pent_cap = ecap;
-    nh_[n].plist_cap = lcap;
+    if (nh_[n].live) merge_rebuild(n);
   }
   merge_dirty_.clear();
+}
+
+// The node's merge records from scratch: every may-merge slot's partner links (one base slab),
+// and the pair block — a hash table of partner nodes, each with the list of slots whose client
+// also subscribes there (one base slab of lists). A node with kIncLinks links or more is then
+// updated in place (merge_patch).
+void Index::merge_rebuild(uint32_t n) {
+  const NodeLists& L = lists.h[n];
+  uint32_t links = 0, xs = 0;
+  for (uint32_t k = 0; k < L.n_merge; k++) {
+    const PartList& p = subp_[L.sub_off + L.n_direct + k];
+    links += p.cnt;
+    bool x = false;
+    for (uint32_t i = 0; i < p.cnt && !x; i++) x = (parts.m.h[p.off + i] & kForeign) != 0;
+    xs += x;
+  }
+  if ((xs != 0) != ((L.flags & kFlagXNode) != 0)) {
+    NodeLists& W = lists.at_w(n);
+    W.flags = xs ? (W.flags | kFlagXNode) : (W.flags & ~kFlagXNode);
+  }
+  nh_[n].x_slots = xs;
+  if (!links) return;
+  uint32_t cap = 1;
+  while (cap < links) cap <<= 1;
+  const uint32_t off = mpart.alloc(cap);
+  uint32_t at = off;
+  for (uint32_t k = 0; k < L.n_merge; k++) {
+    const uint32_t pos = L.sub_off + L.n_direct + k;
+    const PartList& p = subp_[pos];
+    const uint32_t client = subs.m.h[pos].client;
+    mref.at_w(pos) = MergeRef{at, p.cnt};
+    for (uint32_t i = 0; i < p.cnt; i++) {
+      const uint32_t m = parts.m.h[p.off + i];
+      mpart.m.at_w(at++) = MergePart{m, partner_meta(m, client)};
+    }
+  }
+  nh_[n].mpart_off = off;
+  nh_[n].mpart_cap = cap;
+  mpart.live += cap;
+
+  // pair block: partner node h -> g's slots (their places k in g's list) whose client also
+  // subscribes at h
+  thread_local std::vector<std::pair<uint32_t, uint32_t>> hk;
+  hk.clear();
+  for (uint32_t k = L.n_direct; k < L.n_direct + L.n_merge; k++) {
+    const PartList& p = subp_[L.sub_off + k];
+    for (uint32_t i = 0; i < p.cnt; i++) hk.emplace_back(parts.m.h[p.off + i], k);
+  }
+  std::sort(hk.begin(), hk.end());
+  uint32_t lists_n = 0;
+  for (size_t i = 0; i < hk.size(); i++) lists_n += i == 0 || hk[i].first != hk[i - 1].first;
+  uint32_t ecap = 2, lcap = 1;
+  while (ecap < 4 * lists_n) ecap <<= 1;  // load <= 1/4: k_merge probes four slots per load round
+  while (lcap < hk.size()) lcap <<= 1;
+  const uint32_t eo = pent.alloc(ecap), lo = plist.alloc(lcap), mask = ecap - 1;
+  for (uint32_t i = 0; i < ecap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
+  for (size_t i = 0; i < hk.size(); i++) {
+    const uint32_t pos = L.sub_off + hk[i].second;
+    const MergeRef r = mref.h[pos];
+    const SubRec& rec = subs.m.h[pos];
+    plist.m.at_w(lo + i) = PairSlot{hk[i].second, r.off, r.cnt, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u)};
+  }
+  const bool inc = links >= kIncLinks;
+  MergeInc* I = nullptr;
+  if (inc) {
+    I = &minc_[n];
+    I->slot.assign(L.n_direct + L.n_merge, MergeInc::Slot{});
+    for (uint32_t k = L.n_direct; k < L.n_direct + L.n_merge; k++) {
+      const MergeRef r = mref.h[L.sub_off + k];
+      I->slot[k] = MergeInc::Slot{r.off, r.cnt, r.cnt | kPairBase};
+    }
+    I->where.reserve(hk.size());
+    I->links = links;
+  }
+  for (size_t b = 0; b < hk.size();) {
+    size_t e = b + 1;
+    while (e < hk.size() && hk[e].first == hk[b].first) e++;
+    uint32_t sl = pair_hash(hk[b].first) & mask;
+    while (pent.m.h[eo + sl].h != kNone) sl = (sl + 1) & mask;
+    const uint32_t cnt = (uint32_t)(e - b);
+    pent.m.at_w(eo + sl) = PairEnt{hk[b].first, lo + (uint32_t)b, cnt, cnt | kPairBase};
+    if (inc)
+      for (size_t i = b; i < e; i++) I->where.put((uint64_t)hk[i].first << 32 | hk[i].second, (uint32_t)(i - b));
+    b = e;
+  }
+  pent.live += lists_n;
+  plist.live += hk.size();
+  npair.at_w(n) = NodePair{eo, mask, lo, lists_n};
+  nh_[n].pent_cap = ecap;
+  nh_[n].plist_cap = lcap;
+}
+
+// In place: every changed slot (by its place k) comes off the pair lists of its old partners
+// and its old links are dropped; then every slot that is a may-merge slot now gets new links
+// and goes onto the lists of its partners. A list or links slab that outgrows its room moves
+// to a slab of its own; emptied lists leave the table (backward shift).
+void Index::merge_patch(uint32_t n, MergeInc& I) {
+  std::sort(I.dirty.begin(), I.dirty.end());
+  I.dirty.erase(std::unique(I.dirty.begin(), I.dirty.end()), I.dirty.end());
+  int32_t xs = 0;
+  for (uint32_t k : I.dirty) {
+    if (k >= I.slot.size() || !I.slot[k].mp_cnt) continue;
+    const MergeInc::Slot S = I.slot[k];
+    bool x = false;
+    for (uint32_t e = 0; e < S.mp_cnt; e++) {
+      const uint32_t h = mpart.m.h[S.mp_off + e].node;
+      x |= (h & kForeign) != 0;
+      pair_remove(n, I, h, k);
+    }
+    xs -= x;
+    if (S.mp_cap & kPairBase) {
+      I.garbage += S.mp_cnt;
+    } else {
+      mpart.release(S.mp_off, S.mp_cap);
+      mpart.live -= S.mp_cap;
+    }
+    I.links -= S.mp_cnt;
+    I.slot[k] = MergeInc::Slot{};
+  }
+  const NodeLists& L = lists.h[n];
+  for (uint32_t k : I.dirty) {
+    if (k < L.n_direct || k >= L.n_direct + L.n_merge) continue;
+    const uint32_t pos = L.sub_off + k;
+    const PartList p = subp_[pos];
+    if (!p.cnt) continue;
+    uint32_t cap = 1;
+    while (cap < p.cnt) cap <<= 1;
+    const uint32_t off = mpart.alloc(cap);
+    mpart.live += cap;
+    const SubRec rec = subs.m.h[pos];
+    bool x = false;
+    for (uint32_t i = 0; i < p.cnt; i++) {
+      const uint32_t m = parts.m.h[p.off + i];
+      mpart.m.at_w(off + i) = MergePart{m, partner_meta(m, rec.client)};
+      x |= (m & kForeign) != 0;
+    }
+    xs += x;
+    mref.at_w(pos) = MergeRef{off, p.cnt};
+    if (k >= I.slot.size()) I.slot.resize(k + 1);
+    I.slot[k] = MergeInc::Slot{off, p.cnt, cap};
+    I.links += p.cnt;
+    const PairSlot ps{k, off, p.cnt, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u)};
+    for (uint32_t i = 0; i < p.cnt; i++) pair_add(n, I, parts.m.h[p.off + i], ps);
+  }
+  I.dirty.clear();
+  if (xs) {
+    nh_[n].x_slots = (uint32_t)((int32_t)nh_[n].x_slots + xs);
+    const bool want = nh_[n].x_slots != 0;
+    if (want != ((L.flags & kFlagXNode) != 0)) {
+      NodeLists& W = lists.at_w(n);
+      W.flags = want ? (W.flags | kFlagXNode) : (W.flags & ~kFlagXNode);
+    }
+  }
+}
+
+uint32_t Index::pair_find(const NodePair& P, uint32_t h) const {
+  if (P.ent_mask == kNone) return kNone;
+  uint32_t sl = pair_hash(h) & P.ent_mask;
+  for (uint32_t i = 0; i <= P.ent_mask; i++, sl = (sl + 1) & P.ent_mask) {
+    const PairEnt& e = pent.m.h[P.ent_off + sl];
+    if (e.h == h) return P.ent_off + sl;
+    if (e.h == kNone) return kNone;
+  }
+  return kNone;
+}
+
+void Index::pair_rehash(uint32_t n, uint32_t ecap) {
+  NodePair P = npair.h[n];
+  const uint32_t eo = pent.alloc(ecap), mask = ecap - 1;
+  for (uint32_t i = 0; i < ecap; i++) pent.m.at_w(eo + i) = PairEnt{kNone, 0, 0, 0};
+  if (P.ent_mask != kNone) {
+    for (uint32_t i = 0; i <= P.ent_mask; i++) {
+      const PairEnt e = pent.m.h[P.ent_off + i];
+      if (e.h == kNone) continue;
+      uint32_t sl = pair_hash(e.h) & mask;
+      while (pent.m.h[eo + sl].h != kNone) sl = (sl + 1) & mask;
+      pent.m.at_w(eo + sl) = e;
+    }
+    pent.release(P.ent_off, nh_[n].pent_cap);
+  }
+  nh_[n].pent_cap = ecap;
+  P.ent_off = eo;
+  P.ent_mask = mask;
+  npair.at_w(n) = P;
+}
+
+void Index::pair_add(uint32_t n, MergeInc& I, uint32_t h, const PairSlot& ps) {
+  NodePair P = npair.h[n];
+  uint32_t ei = pair_find(P, h);
+  if (ei == kNone) {  // a new partner node: a list of its own in the table (load <= 1/4)
+    if (P.ent_mask == kNone || (P.n_lists + 1) * 4 > P.ent_mask + 1) {
+      pair_rehash(n, P.ent_mask == kNone ? 4u : 2 * (P.ent_mask + 1));
+      P = npair.h[n];
+    }
+    uint32_t sl = pair_hash(h) & P.ent_mask;
+    while (pent.m.h[P.ent_off + sl].h != kNone) sl = (sl + 1) & P.ent_mask;
+    ei = P.ent_off + sl;
+    pent.m.at_w(ei) = PairEnt{h, plist.alloc(1), 0, 1};
+    P.n_lists++;
+    npair.at_w(n) = P;
+    pent.live++;
+  }
+  PairEnt e = pent.m.h[ei];
+  const uint32_t cap = e.cap & ~kPairBase;
+  if (e.cnt == cap) {  // full: the list moves to a slab twice as large
+    uint32_t nc = 1;
+    while (nc < e.cnt + 1) nc <<= 1;
+    if (nc < 2 * cap && !(e.cap & kPairBase)) nc = 2 * cap;
+    const uint32_t no = plist.alloc(nc);
+    for (uint32_t i = 0; i < e.cnt; i++) plist.m.at_w(no + i) = plist.m.h[e.off + i];
+    if (e.cap & kPairBase) I.garbage += cap;
+    else plist.release(e.off, cap);
+    e.off = no;
+    e.cap = nc;
+  }
+  plist.m.at_w(e.off + e.cnt) = ps;
+  I.where.put((uint64_t)h << 32 | ps.k, e.cnt);
+  e.cnt++;
+  plist.live++;
+  pent.m.at_w(ei) = e;
+}
+
+void Index::pair_remove(uint32_t n, MergeInc& I, uint32_t h, uint32_t k) {
+  NodePair P = npair.h[n];
+  const uint32_t ei = pair_find(P, h);
+  const uint64_t key = (uint64_t)h << 32 | k;
+  uint32_t idx = kNone;
+  if (ei == kNone || !I.where.get(key, &idx)) throw std::logic_error("flush_merge: pair-list entry missing");
+  PairEnt e = pent.m.h[ei];
+  const uint32_t last = e.cnt - 1;
+  if (idx != last) {
+    const PairSlot mv = plist.m.h[e.off + last];
+    plist.m.at_w(e.off + idx) = mv;
+    I.where.put((uint64_t)h << 32 | mv.k, idx);
+  }
+  I.where.erase(key);
+  e.cnt--;
+  plist.live--;
+  if (e.cnt) {
+    pent.m.at_w(ei) = e;
+    return;
+  }
+  // the list is empty: its slab goes, and its entry leaves the table by backward shift (the
+  // kernels' probes stop at an empty entry)
+  if (e.cap & kPairBase) I.garbage += e.cap & ~kPairBase;
+  else plist.release(e.off, e.cap);
+  const uint32_t m = P.ent_mask;
+  uint32_t i = ei - P.ent_off;
+  for (uint32_t j = (i + 1) & m;; j = (j + 1) & m) {
+    const PairEnt f = pent.m.h[P.ent_off + j];
+    if (f.h == kNone) break;
+    const uint32_t home = pair_hash(f.h) & m;
+    const bool stays = i <= j ? (home > i && home <= j) : (home > i || home <= j);
+    if (stays) continue;
+    pent.m.at_w(P.ent_off + i) = f;
+    i = j;
+  }
+  pent.m.at_w(P.ent_off + i) = PairEnt{kNone, 0, 0, 0};
+  P.n_lists--;
+  npair.at_w(n) = P;
+  pent.live--;
 }
 
 bool Index::check(std::string* why) {
@@ -714,10 +932,25 @@ bool Index::check(std::string* why) {
         const uint32_t want_meta = rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u);
         for (uint32_t i = 0; i < pe.cnt && !listed; i++) {
           const PairSlot& ps = plist.m.h[pe.off + i];
-          listed = ps.k == k - L.n_direct && ps.mp_off == r.off && ps.mp_cnt == r.cnt && ps.meta == want_meta;
+          listed = ps.k == k && ps.mp_off == r.off && ps.mp_cnt == r.cnt && ps.meta == want_meta;
         }
         if (!listed) return bad(at + ": pair list misses a slot");
       }
+    }
+    // and the pair block lists nothing else: one entry per partner link, n_lists lists
+    const NodePair& P = npair.h[n];
+    if (P.ent_mask != kNone) {
+      uint64_t want = 0, have = 0;
+      uint32_t nl = 0;
+      for (uint32_t k = L.n_direct; k < L.n_direct + L.n_merge; k++) want += mref.h[L.sub_off + k].cnt;
+      for (uint32_t i = 0; i <= P.ent_mask; i++) {
+        const PairEnt& e = pent.m.h[P.ent_off + i];
+        if (e.h == kNone) continue;
+        if (!e.cnt || e.cnt > (e.cap & ~kPairBase)) return bad(at + ": pair list count out of bounds");
+        have += e.cnt;
+        nl++;
+      }
+      if (have != want || nl != P.n_lists) return bad(at + ": pair block holds stale entries");
     }
   }
   for (uint32_t n = 0; n < nh_.size(); n++) {  // children slabs: each particle once, in its parent's
@@ -755,7 +988,11 @@ void Index::sub_ensure(uint32_t n, uint32_t need) {
   NodeLists& L = lists.at_w(n);
   uint32_t no = subs.alloc(nc), cnt = L.n_direct + L.n_merge;
   subp_.resize(subs.m.size(), PartList{0, 0, 0});
-  for (uint32_t i = 0; i < cnt; i++) move_slot(n, L.sub_off + i, no + i);
+  for (uint32_t i = 0; i < cnt; i++) move_slot(n, L.sub_off + i, no + i, false);
+  if (L.n_merge) {  // the merge refs follow their slots (pair slots name places, not positions)
+    if (mref.size() < subs.m.size()) mref.grow_to(subs.m.size(), MergeRef{0, 0});
+    for (uint32_t i = L.n_direct; i < cnt; i++) mref.at_w(no + i) = mref.h[L.sub_off + i];
+  }
   subs.release(L.sub_off, cap);
   L.sub_off = no;
   nh_[n].sub_cap = nc;
@@ -769,7 +1006,7 @@ uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
     pos = base + L.n_direct + L.n_merge;
     L.n_merge++;
     n_merge_++;
-    merge_dirty(n);
+    merge_dirty_slot(n, pos);
   } else {
     pos = base + L.n_direct;
     if (L.n_merge) move_slot(n, pos, base + L.n_direct + L.n_merge);
@@ -792,10 +1029,11 @@ void Index::sub_remove(uint32_t n, uint32_t pos) {
     L.n_direct--;
   } else {
     uint32_t last = base + L.n_direct + L.n_merge - 1;
+    merge_dirty_slot(n, pos);
+    merge_dirty_slot(n, last);
     if (pos != last) move_slot(n, last, pos);
     L.n_merge--;
     n_merge_--;
-    merge_dirty(n);
   }
   subs.live--;
 }
@@ -818,7 +1056,8 @@ void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
     L.n_merge--;
     n_merge_--;
   }
-  merge_dirty(n);
+  merge_dirty_slot(n, pos);
+  merge_dirty_slot(n, other);
   subs.m.at_w(other) = a;
   subp_[other] = ap;
   sub_pos_.put((uint64_t)n << 32 | a.client, other);
@@ -916,7 +1155,7 @@ int Index::foreign_subscribe(std::string_view filter, uint32_t client, uint32_t 
   auto cn = client_nodes_.find(client);
   if (fsub_pos_.get(key, &i)) {  // re-Subscribe: the partners' links carry its meta
     if (fsubs_[i].meta != meta && cn != client_nodes_.end())
-      for (uint32_t m : cn->second) merge_dirty(m);
+      for (uint32_t m : cn->second) touch_partner(m, client);
     fsubs_[i].meta = meta;
     return 0;
   }
@@ -944,7 +1183,7 @@ int Index::foreign_subscribe(std::string_view filter, uint32_t client, uint32_t 
         sub_pos_.get((uint64_t)m << 32 | client, &mp);
       }
       part_add(mp, kForeign | fid);
-      merge_dirty(m);
+      merge_dirty_slot(m, mp);
     }
   return 0;
 }
@@ -962,11 +1201,11 @@ void Index::foreign_unsubscribe(uint32_t client, uint32_t fid) {
       bool linked = false;
       for (uint32_t k = 0; k < p.cnt && !linked; k++) linked = parts.m.h[p.off + k] == (kForeign | fid);
       if (!linked) continue;
+      merge_dirty_slot(m, mp);
       if (part_remove(mp, kForeign | fid) == 0) {
         part_release(mp);
         sub_set_merge(m, mp, false);
       }
-      merge_dirty(m);
     }
   fsub_pos_.erase(key);
   auto cf = client_foreign_.find(client);
@@ -1059,9 +1298,9 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
     subs.m.at_w(pos) = rec;
     const PartList& p = subp_[pos];  // the partners' links carry this subscription's Qos / NoLocal,
     if ((old.meta ^ rec.meta) & (kMetaQos | kMetaNoLocal))
-      for (uint32_t i = 0; i < p.cnt; i++) touch_partner(parts.m.h[p.off + i]);
+      for (uint32_t i = 0; i < p.cnt; i++) touch_partner(parts.m.h[p.off + i], client);
     // and n's pair slots copy its meta and whether its identifier is > 0
-    if (sub_is_merge(n, pos) && (old.meta != rec.meta || (old.ident > 0) != (rec.ident > 0))) merge_dirty(n);
+    if (sub_is_merge(n, pos) && (old.meta != rec.meta || (old.ident > 0) != (rec.ident > 0))) merge_dirty_slot(n, pos);
     return 0;
   }
   // Partners: the client's other subscriptions that could match the same topic (the merge
@@ -1091,7 +1330,7 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
       sub_pos_.get((uint64_t)m << 32 | client, &mp);
     }
     part_add(mp, n);
-    merge_dirty(m);
+    merge_dirty_slot(m, mp);
   }
   mine.push_back(n);
   return 1;
@@ -1146,11 +1385,11 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
         if (m & kForeign) continue;  // another shard's subscription: no link back on this shard
         uint32_t mp;
         if (!sub_pos_.get((uint64_t)m << 32 | client, &mp)) continue;
+        merge_dirty_slot(m, mp);
         if (part_remove(mp, n) == 0) {
           part_release(mp);
           sub_set_merge(m, mp, false);
         }
-        merge_dirty(m);
       }
     }
   }

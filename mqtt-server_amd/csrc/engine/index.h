@@ -410,12 +410,15 @@ class Index {
   int foreign_subscribe(std::string_view filter, uint32_t client, uint32_t fid, uint32_t meta);
   void foreign_unsubscribe(uint32_t client, uint32_t fid);
   uint32_t partner_meta(uint32_t partner, uint32_t client) const;  // Qos | NoLocal of a partner
-  void touch_partner(uint32_t p) {
-    if (!(p & kForeign)) merge_dirty(p);
+  // client's slot at partner node p carries a changed Qos / NoLocal in its partner links
+  void touch_partner(uint32_t p, uint32_t client) {
+    uint32_t pos;
+    if (!(p & kForeign) && sub_pos_.get((uint64_t)p << 32 | client, &pos)) merge_dirty_slot(p, pos);
   }
   // (mark = false: a parallel bulk build, which marks the whole array dirty itself)
   void set_rank(uint32_t n, uint32_t parent, std::string_view seg, bool mark = true);
-  void move_slot(uint32_t n, uint32_t from, uint32_t to);
+  // (mark = false: the whole list moves to a new slab; no slot changes its place k)
+  void move_slot(uint32_t n, uint32_t from, uint32_t to, bool mark = true);
   void part_set(uint32_t pos, const std::vector<uint32_t>& nodes);
   void part_add(uint32_t pos, uint32_t node);
   uint32_t part_remove(uint32_t pos, uint32_t node);
@@ -432,7 +435,34 @@ class Index {
       merge_dirty_.push_back(n);
     }
   }
+  // the slot at pool position pos of n changed (its record, partners or place): n's merge records
+  // are stale; a node updated incrementally also notes the slot's place
+  void merge_dirty_slot(uint32_t n, uint32_t pos) {
+    merge_dirty(n);
+    auto it = minc_.find(n);
+    if (it != minc_.end()) it->second.dirty.push_back(pos - lists.h[n].sub_off);
+  }
   void merge_release(uint32_t n);
+  // Merge records of a node with many partner links, updated in place (flush_merge): the
+  // changed slots are taken off the pair lists and put back, instead of rebuilding the node's
+  // links and pair block (a hot node's block is megabytes). Host only.
+  struct MergeInc {
+    struct Slot {
+      uint32_t mp_off = 0, mp_cnt = 0, mp_cap = 0;  // its MergePart records; mp_cap | kPairBase: in the base slab
+    };
+    std::vector<Slot> slot;       // by place k in the node's subscription list
+    std::vector<uint32_t> dirty;  // places changed since the last flush
+    HashU64 where{64};            // (h << 32 | k) -> index of slot k on the list of partner node h
+    uint64_t links = 0;           // MergePart records in use (= pair-list entries)
+    uint64_t garbage = 0;         // records of the base slabs no longer in use
+  };
+  static constexpr uint64_t kIncLinks = 256;  // nodes with this many partner links update in place
+  void merge_rebuild(uint32_t n);
+  void merge_patch(uint32_t n, MergeInc& I);
+  uint32_t pair_find(const NodePair& P, uint32_t h) const;  // pent index of partner h, or kNone
+  void pair_add(uint32_t n, MergeInc& I, uint32_t h, const PairSlot& ps);
+  void pair_remove(uint32_t n, MergeInc& I, uint32_t h, uint32_t k);
+  void pair_rehash(uint32_t n, uint32_t ecap);
   uint32_t sub_count(uint32_t n) const { return lists[n].n_direct + lists[n].n_merge; }
 
   PodVec<NodeHost> nh_;
@@ -468,6 +498,7 @@ class Index {
   std::vector<PartList> subp_;       // each slot's partner slab
   std::vector<uint32_t> merge_dirty_;  // nodes whose device partner links are stale
   std::vector<uint8_t> merge_dirty_flag_;
+  std::unordered_map<uint32_t, MergeInc> minc_;  // nodes whose merge records update in place
   std::unordered_map<uint32_t, std::vector<uint32_t>> client_nodes_;  // non-shared subs
   uint64_t n_retained_ = 0;  // live Retained entries (topic "" included)
   // sharding

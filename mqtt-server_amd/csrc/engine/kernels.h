@@ -151,12 +151,12 @@ struct EmitArgs {
   // rows) in place of the offsets' differences
   const TopicCount* tc;
   // span format, merge-set dedup (rep == null: off). dd_phase 1: each set representative resolves
-  // its merge gathers once into set-relative patches (row = x << kSetRowBits | k: k-th may-merge
-  // slot of its x-th merge gather) in the set pool, and its SetInfo; dd_phase 2: every deduped
+  // its merge gathers once into set-relative patches (row = x << kSetRowBits | k: record k of
+  // its x-th merge gather's list) in the set pool, and its SetInfo; dd_phase 2: every deduped
   // topic copies its representative's patches, translating x to its own rows.
   const uint32_t* rep;
   const uint32_t* tslot;
-  const uint32_t* mcount;  // merge gathers per topic, and their rows (k_desc, stride kPairMax)
+  const uint32_t* mcount;  // merge gathers per topic, and the rows of their lists (k_desc, stride kPairMax)
   const uint32_t* mrow;
   const uint32_t* mlist;   // dedup: their particles and pair-block headers (k_desc, stride kPairMax):
   const uint2* mpair;      //   the map is built from these (topics with <= kPairMax merge gathers)

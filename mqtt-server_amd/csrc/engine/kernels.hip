@@ -791,11 +791,11 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
         msig = mix64(msig ^ (gw & kGatherNode)) + 0x9e3779b97f4a7c15ull;
         if (n_mg < kPairMax) {
           a.mlist[(uint64_t)t * kPairMax + n_mg] = gw & kGatherNode;
-          a.mrow[(uint64_t)t * kPairMax + n_mg] = rpos + L.n_direct;
+          a.mrow[(uint64_t)t * kPairMax + n_mg] = rpos;
           a.mpair[(uint64_t)t * kPairMax + n_mg] = make_uint2(d.s_pos, d.s_src);
         }
         // set-relative rows hold 26 bits of slot: a larger merge gather keeps the topic apart
-        n_mg += L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1;
+        n_mg += L.n_direct + L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1;
       }
       a.spans[g] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
       for (uint32_t k = 0; k < in; k++) a.inl_out[ipos + k] = a.ix.inl[L.inl_off + k];
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
     const uint32_t in = (act && (gw & kGatherInline)) ? L.inl_cnt : 0u;
     const bool ismg = subs && L.n_merge != 0;
     // set-relative rows hold 26 bits of slot: a larger merge gather keeps the topic apart
-    const uint32_t inc = ismg ? (L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1) : 0u;
+    const uint32_t inc = ismg ? (L.n_direct + L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1) : 0u;
     const uint32_t rn_i = g16_incl(rn, sub), in_i = g16_incl(in, sub), inc_i = g16_incl(inc, sub);
     const uint32_t sh_i = g16_incl(act ? L.shr_cnt : 0u, sub);
     const uint32_t rp = rpos + rn_i - rn, x = n_mg + inc_i - inc;
@@ -912,7 +912,7 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
       if (x < kPairMax) {
         const uint64_t q = (uint64_t)t * kPairMax + x;
         a.mlist[q] = gw & kGatherNode;
-        a.mrow[q] = rp + L.n_direct;
+        a.mrow[q] = rp;
         a.mpair[q] = make_uint2(P.ent_off, P.ent_mask);
         if (a.mrank) a.mrank[q] = a.ix.xinfo[gw & kGatherNode].rank;
       }
@@ -1281,7 +1281,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ uint32_t mg_node[4][kEnt];        // entries: the topic's merge gathers in gather
   __shared__ uint32_t mg_gi[4][kEnt];          //   order (node, gather index), then (XS) the
   __shared__ uint64_t mg_rank[4][XS ? kEnt : 1];  // other shards' (kForeign | fid, kNone, rank)
-  __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first may-merge slot,
+  __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first record (pair slots name
+                                               //   a record by its place k in the particle's list),
   __shared__ uint32_t mg_eoff[4][kPairMax];    //   its pair-block hash table (NodePair)
   __shared__ uint32_t mg_emask[4][kPairMax];
   __shared__ uint32_t h_ga[4][kHitMax];        // staged hit lists: merge gather of g,
@@ -1424,8 +1425,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const GDesc d = gd[i];
         node = d.word & kGatherNode;
         ins = (d.mdir & kDescMerge) != 0;
-        const uint32_t nd = d.mdir & ~kDescMerge;
-        mrow = d.r_pos + nd;
+        mrow = d.r_pos;  // (pair slots name records by their place in the particle's list)
         if (ins) {
           if (SPANS) P = NodePair{d.s_pos, d.s_src, 0, 0};  // folded in by k_desc<true>
           else P = a.ix.npair[node];

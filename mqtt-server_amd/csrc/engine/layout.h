@@ -188,8 +188,9 @@ struct MergePart {  // 8 B
 };
 // Pair blocks find a topic's merging records without touching the others. For a node g, the
 // block maps each partner node h (a node holding a partner of one of g's may-merge
-// subscriptions) to the list of g's may-merge slots, relative k in [0, n_merge), whose client
-// also subscribes at h. A topic probes (g, h) only for pairs of nodes it gathers; the slots on
+// subscriptions) to the list of g's may-merge slots whose client also subscribes at h, each
+// named by its place k in g's subscription list (position sub_off + k: a slot keeps its k when
+// the list's slab moves or a direct subscription is added, so updates patch single entries). A topic probes (g, h) only for pairs of nodes it gathers; the slots on
 // the hit lists are exactly the records whose client has another match for the topic. Every
 // other record is its client's only match and stays a plain client row.
 struct NodePair {   // per node (16 B)
@@ -202,10 +203,12 @@ struct PairEnt {  // 16 B
   uint32_t h;     // partner node; kNone = empty
   uint32_t off;   // absolute offset of the list in the pair-list pool
   uint32_t cnt;   // slots on the list
-  uint32_t pad;
+  uint32_t cap;   // host bookkeeping: the list's capacity | kPairBase (inside the node's base
+                  // slab of lists, not released by itself); the kernels do not read it
 };
+constexpr uint32_t kPairBase = 0x80000000u;
 struct PairSlot {  // 16 B: one slot on a pair list, with its partner links
-  uint32_t k;       // may-merge slot of g, relative to g's may-merge slots
+  uint32_t k;       // the slot's place in g's subscription list (its row: the list's first + k)
   uint32_t mp_off;  // its MergePart records
   uint32_t mp_cnt;
   uint32_t meta;    // the slot's SubRec meta | kSlotIdentPos (its identifier is > 0): resolving

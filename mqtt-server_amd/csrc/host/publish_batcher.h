@@ -62,6 +62,8 @@ class BasicBatcher {
     uint64_t batches = 0;     // match calls
     uint64_t topics = 0;      // topics matched
     uint64_t largest = 0;     // largest batch
+    // the dispatcher's time (ns): waiting for topics, sealing, in the match call, completing
+    uint64_t wait_ns = 0, seal_ns = 0, match_ns = 0, complete_ns = 0;
   };
   using MatchFn = std::function<std::vector<R>(const std::vector<std::string>&)>;
 
@@ -137,7 +139,12 @@ class BasicBatcher {
   void run() {
     std::vector<std::string> topics;
     std::vector<std::pair<std::shared_ptr<Segment>, uint32_t>> segs;  // (segment, its topics)
+    using Clock = std::chrono::steady_clock;
+    auto ns = [](Clock::time_point a, Clock::time_point b) {
+      return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+    };
     for (;;) {
+      const auto c0 = Clock::now();
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || queued_.load(std::memory_order_acquire) != 0; });
@@ -148,6 +155,7 @@ class BasicBatcher {
           cv_.wait_until(lk, until, [&] { return stop_ || queued_.load() >= min_fill_; });
         }
       }
+      const auto c1 = Clock::now();
       // seal: every queue's topics, in queue order (at most max_batch; a queue that would
       // overflow the batch keeps its topics and its segment for the next one)
       topics.clear();
@@ -168,11 +176,13 @@ class BasicBatcher {
       queued_.fetch_sub(topics.size(), std::memory_order_acq_rel);
       std::shared_ptr<const std::vector<R>> res;
       std::exception_ptr err;
+      const auto c2 = Clock::now();
       try {
         res = std::make_shared<const std::vector<R>>(match_(topics));
       } catch (...) {
         err = std::current_exception();
       }
+      const auto c3 = Clock::now();
       for (auto& sg : segs) {
         {
           std::lock_guard<std::mutex> lk(sg.first->mu);
@@ -183,10 +193,15 @@ class BasicBatcher {
         }
         sg.first->cv.notify_all();
       }
+      const auto c4 = Clock::now();
       std::lock_guard<std::mutex> lk(mu_);
       st_.batches++;
       st_.topics += topics.size();
       st_.largest = std::max<uint64_t>(st_.largest, topics.size());
+      st_.wait_ns += ns(c0, c1);
+      st_.seal_ns += ns(c1, c2);
+      st_.match_ns += ns(c2, c3);
+      st_.complete_ns += ns(c3, c4);
     }
   }
 

@@ -188,3 +188,40 @@ def test_edge_load_option():
     s = sparse.stats()
     assert s["edges"] * 4 <= s["edge_capacity"]
     sparse.check()
+
+
+@pytest.mark.parametrize("n_shards", [1, 2])
+def test_merge_records_update_in_place(n_shards):
+    """Nodes with at least Index::kIncLinks (256) partner links update their merge records in
+    place (flush_merge -> merge_patch): the changed slots come off the pair lists and go back
+    on. Hot nodes here: '#', 'a/+', 'a/b' and 'a/#' shared by 400 clients. Every round mixes new
+    and dropped partners, Qos / NoLocal / identifier changes (the partners' links and the pair
+    slots copy them), direct subscriptions coming and going (merge slots move within the list)
+    and lists outgrowing their slabs; after each, mq_index_check holds — every link and pair
+    entry current and nothing stale left on a list — on every shard."""
+    r = random.Random(40 + n_shards)
+    filters = ["#", "a/+", "a/b", "a/#", "x/y", "x/+", "q/r/s", "+/b"]
+    engs = [E.Engine(shard=k, n_shards=n_shards) for k in range(n_shards)]
+    state = {}
+    for c in range(400):
+        for f in r.sample(filters, 3):
+            state[(c, f)] = True
+            for e in engs:
+                e.subscribe(f, c, filters.index(f), r.randint(0, 2), 0, 0)
+    for e in engs:
+        e.check()
+    for rnd in range(6):
+        for _ in range(800):
+            c, f = r.randrange(460), r.choice(filters)
+            if r.random() < 0.4 and (c, f) in state:
+                del state[(c, f)]
+                for e in engs:
+                    e.unsubscribe(f, c)
+            else:
+                state[(c, f)] = True
+                q, fl, ident = r.randint(0, 2), r.choice([0, 1]), r.choice([0, 0, 5])
+                for e in engs:
+                    e.subscribe(f, c, filters.index(f), q, fl, ident)
+        for e in engs:
+            e.check()
+    assert sum(e.stats()["subs_merge"] for e in engs) > 500

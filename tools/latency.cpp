@@ -46,6 +46,7 @@ static double pct(std::vector<double>& v, double p) {
 int main(int argc, char** argv) {
   const uint64_t n_subs = argc > 1 ? strtoull(argv[1], nullptr, 10) : 10000000ull;
   const double secs = argc > 2 ? atof(argv[2]) : 3.0;
+  const int kSubmitters = argc > 3 ? atoi(argv[3]) : 64;  // connection goroutines
   const uint64_t seed = 0x6D716D61;
   void* g = mqgen_subs(n_subs, (uint32_t)std::max<uint64_t>(1, n_subs / 10), seed, 0);
   const uint64_t n = mqgen_subs_n(g);
@@ -122,7 +123,6 @@ int main(int argc, char** argv) {
 
     // batcher: kSubmitters threads (connection goroutines) keep 2B topics in flight together
     if (B < 1024) continue;  // (the stage is measured at the batch sizes a broker would run)
-    constexpr int kSubmitters = 64;
     const size_t window = std::max<size_t>(1, 2 * B / kSubmitters);
     std::vector<std::vector<double>> wl(kSubmitters);
     std::vector<uint64_t> recipients(kSubmitters, 0), sampled(kSubmitters, 0), done(kSubmitters, 0);
@@ -170,10 +170,13 @@ int main(int argc, char** argv) {
       const double w50 = pct(all, 0.50), w99 = pct(all, 0.99);
       std::printf("{\"path\": \"PublishViewBatcher\", \"max_batch\": %zu, \"submitters\": %d, \"in_flight\": %zu, "
                   "\"topics\": %llu, \"p50_us\": %.1f, \"p99_us\": %.1f, \"topics_per_s\": %.0f, \"mean_batch\": %.1f, "
-                  "\"largest_batch\": %llu, \"recipients_per_topic\": %.1f}\n",
+                  "\"largest_batch\": %llu, \"recipients_per_topic\": %.1f, \"dispatcher_ms_per_batch\": "
+                  "{\"wait\": %.3f, \"seal\": %.3f, \"match\": %.3f, \"complete\": %.3f}}\n",
                   B, kSubmitters, window * kSubmitters, (unsigned long long)n_done, w50, w99, n_done / bt,
                   (double)st.topics / std::max<uint64_t>(st.batches, 1), (unsigned long long)st.largest,
-                  (double)n_rec / std::max<uint64_t>(n_smp, 1));
+                  (double)n_rec / std::max<uint64_t>(n_smp, 1), st.wait_ns / 1e6 / std::max<uint64_t>(st.batches, 1),
+                  st.seal_ns / 1e6 / std::max<uint64_t>(st.batches, 1), st.match_ns / 1e6 / std::max<uint64_t>(st.batches, 1),
+                  st.complete_ns / 1e6 / std::max<uint64_t>(st.batches, 1));
       std::fflush(stdout);
     }
   }
