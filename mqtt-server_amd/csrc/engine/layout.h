@@ -71,7 +71,7 @@ MQ_HD uint64_t edge_hash(uint32_t parent, const SegKey& k) {
 }
 
 // ---- trie edges -----------------------------------------------------------------------------
-// Global open-addressing table (linear probing, load <= 1/2): (parent node, segment key) ->
+// Global open-addressing table (linear probing, load <= 1/4 by default, MQ_OPT_EDGE_LOAD): (parent node, segment key) ->
 // child node. Every child is here, '+' and '#' children included, so a literal topic
 // segment "+"/"#" walks exactly like the reference's particles.get(key) (topics.go:604).
 constexpr uint32_t kEdgeEmpty = 0xFFFFFFFFu;
