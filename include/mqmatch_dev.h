@@ -26,5 +26,10 @@
                                      synchronisation, at its end (buffers sized by earlier batches; a batch
                                      they cannot hold runs again, sized by the host); 0: the host reads the
                                      walk's totals and the patch counts between kernels */
+#define MQ_OPT_SET_EXP 18         /* attribution experiments on the merge set pass (results WRONG; timing only):
+                                     bit 0 no partner links, bit 1 links loaded but not looked up, bit 2 no
+                                     patch stores, bit 3 no binary search for a record's hit list */
+#define MQ_OPT_FUSE_DESC 17       /* one-sync span batches: 1 (default) runs k_desc in the frontier walk's
+                                     epilogue (spans and merge lists at t * 64, no scan); 0: walk, scan, k_desc */
 
 #endif

@@ -255,6 +255,8 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_MERGE_DEDUP: dedup_ = (uint32_t)v; return true;
     case MQ_OPT_SET_GRID: set_grid_ = (uint32_t)v; return true;
     case MQ_OPT_ONE_SYNC: one_sync_ = v != 0; return true;
+    case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
+    case MQ_OPT_SET_EXP: set_exp_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_GROUP:
       if (v != 0 && v != 4 && v != 8 && v != 16) return false;
       walk_group_ = (uint32_t)v;
@@ -864,7 +866,8 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
 }
 
 TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                           const uint32_t** gathers, uint32_t* gstride, bool lists, bool one_sync) {
+                           const uint32_t** gathers, uint32_t* gstride, bool lists, bool one_sync,
+                           const DescArgs* fused) {
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
   grow(counts_, (size_t)n * sizeof(TopicCount));
   grow(offs_, (size_t)(n + 1) * sizeof(TopicOff));
@@ -883,6 +886,18 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
     hip_check(hipMemsetAsync(fb_cnt_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(fb)");
   }
   prof.begin(s);
+  if (fused) {  // one-sync batch, k_desc in the walk's epilogue: no scan (the dedup totals the gathers)
+    launch_walk_desc(walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(), ovf_.as<uint32_t>(),
+                     fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, *fused, s);
+    prof.end("walk", s);
+    hip_check(hipGetLastError(), "k_walkf<desc>");
+    hip_check(hipMemcpyAsync(&h_fast_->ovf, ovf_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H overflow");
+    hip_check(hipMemcpyAsync(&h_fast_->fallback, fb_cnt_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+    *gathers = gslots_.as<uint32_t>();
+    *gstride = kGatherCap;
+    prof.count("topics", n);
+    return TopicOff{0, 0, 0, 0, 0};
+  }
   if (front)
     launch_walk_front(walk_group_, lists, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(),
                       ovf_.as<uint32_t>(), fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, s, one_sync);
@@ -981,11 +996,61 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   uint32_t gstride = 0;
   sb_.lists = lists;
   sb_.one_sync = one_sync;
-  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, one_sync);
+  // k_desc in the frontier walk's epilogue (one-sync batches): spans and GDesc records at
+  // t * kGatherCap, so nothing waits for a scan of the gather counts
+  const bool fused = one_sync && fuse_desc_ && walk_group_ == 16;
+  sb_.fused = fused;
+  if (!sb_.lists) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
+  if (fused) {
+    grow(desc_[0], (size_t)n * kGatherCap * sizeof(GDesc));
+    grow(sp_spans_, (size_t)n * kGatherCap * sizeof(SpanRec));
+  }
+  sb_.dedup = dedup_ != 0;
+  if (sb_.dedup) {
+    grow(dd_sig_, (size_t)n * sizeof(uint64_t));
+    grow(dd_cnt_, (size_t)n * sizeof(uint32_t));
+    grow(dd_list_, (size_t)n * kPairMax * sizeof(uint32_t));
+    grow(dd_mrow_, (size_t)n * kPairMax * sizeof(uint32_t));
+    grow(dd_mpair_, (size_t)n * kPairMax * sizeof(uint2));
+    if (ix.sharded()) grow(dd_mrank_, (size_t)n * kPairMax * sizeof(uint64_t));
+  }
+  // k_desc's arguments (the buffers are (re)sized below unless the batch is one-sync)
+  auto desc_args = [&]() {
+    DescArgs da;
+    memset(&da, 0, sizeof(da));
+    da.ix = di;
+    da.n = n;
+    da.gather_stride = gstride;
+    da.off = offs_.as<TopicOff>();
+    da.gathers = gathers;
+    da.desc = desc_[0].as<GDesc>();
+    da.spans = sp_spans_.as<SpanRec>();
+    da.inl_out = sp_inl_.as<InlRec>();
+    da.tc_out = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
+    if (sb_.dedup) {  // merge-set dedup (on a sharded index too: a set is then also the other
+                      // shards' entries, which spans_end knows after the exchange)
+      da.mpair = dd_mpair_.as<uint2>();
+      da.msig = dd_sig_.as<uint64_t>();
+      da.mcount = dd_cnt_.as<uint32_t>();
+      da.mlist = dd_list_.as<uint32_t>();
+      da.mrow = dd_mrow_.as<uint32_t>();
+      if (ix.sharded()) da.mrank = dd_mrank_.as<uint64_t>();
+    }
+    da.spans_cap = sp_spans_.bytes / sizeof(SpanRec);
+    da.desc_cap = desc_[0].bytes / sizeof(GDesc);
+    da.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
+    da.g_stride = fused ? kGatherCap : 0u;
+    return da;
+  };
+  DescArgs fda;
+  if (fused) {
+    grow(sp_inl_, sizeof(InlRec));
+    fda = desc_args();
+  }
+  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, one_sync, fused ? &fda : nullptr);
   sb_.tot = tot;
   sb_.gathers = gathers;
   sb_.gstride = gstride;
-  if (!sb_.lists) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
   if (!one_sync) {  // (one-sync: the buffers as earlier batches left them; the kernels check)
     grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
     grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
@@ -999,54 +1064,14 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     sp_patches_.release();
     sp_patches_.ensure(rcap_ * kPatchRegions * sizeof(PatchRec));
   }
-
-  DescArgs da;
-  memset(&da, 0, sizeof(da));
-  da.ix = di;
-  da.n = n;
-  da.gather_stride = gstride;
-  da.off = offs_.as<TopicOff>();
-  da.gathers = gathers;
-  da.chunk_of_block = nullptr;
-  da.plan = nullptr;
-  da.desc = desc_[0].as<GDesc>();
-  da.tiles = nullptr;
-  da.spans = sp_spans_.as<SpanRec>();
-  da.inl_out = sp_inl_.as<InlRec>();
-  da.tc_out = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
-  da.msig = nullptr;
-  da.mcount = nullptr;
-  da.mlist = nullptr;
-  da.mrow = nullptr;
-  da.mpair = nullptr;
-  da.mrank = nullptr;
-  da.spans_cap = sp_spans_.bytes / sizeof(SpanRec);
-  da.desc_cap = desc_[0].bytes / sizeof(GDesc);
-  da.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
-  // merge-set dedup (on a sharded index too: a set is then also the other shards' entries,
-  // which spans_end knows after the exchange)
-  sb_.dedup = dedup_ != 0;
-  if (sb_.dedup) {
-    grow(dd_sig_, (size_t)n * sizeof(uint64_t));
-    grow(dd_cnt_, (size_t)n * sizeof(uint32_t));
-    grow(dd_list_, (size_t)n * kPairMax * sizeof(uint32_t));
-    grow(dd_mrow_, (size_t)n * kPairMax * sizeof(uint32_t));
-    grow(dd_mpair_, (size_t)n * kPairMax * sizeof(uint2));
-    da.mpair = dd_mpair_.as<uint2>();
-    da.msig = dd_sig_.as<uint64_t>();
-    da.mcount = dd_cnt_.as<uint32_t>();
-    da.mlist = dd_list_.as<uint32_t>();
-    da.mrow = dd_mrow_.as<uint32_t>();
-    if (ix.sharded()) {
-      grow(dd_mrank_, (size_t)n * kPairMax * sizeof(uint64_t));
-      da.mrank = dd_mrank_.as<uint64_t>();
-    }
-  }
+  const DescArgs da = fused ? fda : desc_args();
   sb_.tc = da.tc_out;
-  prof.begin(s);
-  launch_desc(da, true, s);
-  prof.end("desc", s);
-  hip_check(hipGetLastError(), "k_desc<spans>");
+  if (!fused) {
+    prof.begin(s);
+    launch_desc(da, true, s);
+    prof.end("desc", s);
+    hip_check(hipGetLastError(), "k_desc<spans>");
+  }
   if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
@@ -1120,10 +1145,10 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     grow(dd_slot_, (size_t)n * sizeof(uint32_t));
     grow(dd_rep_, (size_t)n * sizeof(uint32_t));
     grow(dd_rlist_, (size_t)n * sizeof(uint32_t));
-    if (!dd_nsets_.p) dd_nsets_.ensure(2 * sizeof(unsigned long long));
+    if (!dd_nsets_.p) dd_nsets_.ensure(3 * sizeof(unsigned long long));
     hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
 
-    hip_check(hipMemsetAsync(dd_nsets_.p, 0, 2 * sizeof(unsigned long long), s), "memset");
+    hip_check(hipMemsetAsync(dd_nsets_.p, 0, 3 * sizeof(unsigned long long), s), "memset");
     DedupArgs dd;
     memset(&dd, 0, sizeof(dd));
     dd.n = n;
@@ -1169,7 +1194,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipGetLastError(), "k_dedup");
     sb_.n_sets = 0;
     if (one_sync) {  // the set count is read at the batch's end; the set pass strides over it
-      hip_check(hipMemcpyAsync(h_fast_->n_sets, dd_nsets_.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
+      hip_check(hipMemcpyAsync(h_fast_->n_sets, dd_nsets_.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
                 "D2H");
       // the grid: the last batch's count with room (the set pass strides over the true count);
       // with none yet, as many waves as topics (an unused one exits at once)
@@ -1215,6 +1240,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.mrank = ix.sharded() && sb_.dedup ? dd_mrank_.as<uint64_t>() : nullptr;
   a.desc_cap = desc_[0].bytes / sizeof(GDesc);
   a.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
+  a.g_stride = sb_.fused ? kGatherCap : 0u;
+  a.exp = set_exp_;
   pinned((2 * kPatchRegions + 1) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
   unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
@@ -1302,6 +1329,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       fa.sres = a.sres;
       fa.wave_list = dd_wlist_.as<uint32_t>();
       fa.n_wave = dd_nwave_.as<unsigned long long>();
+      fa.g_stride = a.g_stride;
       prof.begin(s);
       launch_finish(fa, s);
       prof.end("finish", s);
@@ -1364,6 +1392,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       return false;
     }
     tot = h_fast_->tot;
+    if (sb_.fused) tot.g = h_fast_->n_sets[2];  // (no scan: k_dedup_rep totals the gathers)
     sb_.tot = tot;
     last_sets_ = h_fast_->n_sets[0] + h_fast_->n_sets[1];
     if (prof.on()) {
@@ -1380,7 +1409,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   out->patches = reinterpret_cast<const mq_patch*>(sp_patches_.p);
   out->inline_rows = reinterpret_cast<const mq_inline_row*>(sp_inl_.p);
   out->picked_rows = select_shared_ ? reinterpret_cast<const mq_shared_row*>(sp_picked_.p) : nullptr;
-  out->n_spans = tot.g;
+  out->n_spans = sb_.fused ? (uint64_t)n * kGatherCap : tot.g;  // (the stride layout's extent)
   out->n_patches = rcap_ * kPatchRegions;  // the pool's extent: topic ranges sit in regions
   out->n_inline_rows = tot.inl;
   out->n_picked_rows = select_shared_ ? tot.shr : 0;
@@ -1393,13 +1422,17 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     std::vector<unsigned long long> w(2 * kPatchRegions * kWork);
     hip_check(hipMemcpyAsync(w.data(), a.work, w.size() * sizeof(w[0]), hipMemcpyDeviceToHost, s), "D2H work");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-    uint64_t sum[kWork] = {0, 0, 0, 0};
+    uint64_t sum[kWork] = {};
     for (uint32_t r = 0; r < 2 * kPatchRegions; r++)
       for (uint32_t k = 0; k < kWork; k++) sum[k] += w[r * kWork + k];
     prof.count("merge_pair_entries", sum[0]);
     prof.count("merge_records", sum[1]);
     prof.count("merge_links", sum[2]);
     prof.count("merge_patches", sum[3]);
+    prof.count("set_cycles_map", sum[4]);
+    prof.count("set_cycles_pairs", sum[5]);
+    prof.count("set_cycles_resolve", sum[6]);
+    prof.count("set_cycles_total", sum[7]);
     prof.count("merge_topics", n);
   }
   if (host) {

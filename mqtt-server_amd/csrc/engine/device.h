@@ -207,7 +207,8 @@ class Device {
   // (one_sync: the totals are not read back - the returned TopicOff is zero - and every topic's
   // gather count is clamped to its slot; the totals are read at the batch's end)
   TopicOff walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                     const uint32_t** gathers, uint32_t* gstride, bool lists, bool one_sync = false);
+                     const uint32_t** gathers, uint32_t* gstride, bool lists, bool one_sync = false,
+                     const DescArgs* fused = nullptr);
   // Messages: the level-order retained image (rebuilt when ix.retained_version() moved) and the
   // two query paths — run arithmetic over the image (k_msgq) and the particle walk (k_msg:
   // the Q6 state, nesting beyond kMsgStack, MQ_OPT_MSG_IMAGE = 0)
@@ -292,17 +293,20 @@ class Device {
     uint32_t gstride = 0;
     TopicCount* tc = nullptr;      // k_desc's per-topic counts (walk without lists), or null
     bool one_sync = false;         // one host synchronisation (spans_begin)
+    bool fused = false;            // k_desc ran in the walk's epilogue: spans at t * kGatherCap
   } sb_;
   // one-sync batches: values read back at the batch's end (pinned): the walk's totals, its
   // overflow and fallback counts, the *unsafe bits, the error word and the merge-set counts
   struct FastBack {
     TopicOff tot;
     uint32_t ovf, fallback, unsafe, err;
-    unsigned long long n_sets[2];
+    unsigned long long n_sets[3];  // merge sets (heavy, light), the batch's gathers (walk-fused desc)
   };
   FastBack* h_fast_ = nullptr;
   DevBuf unsafe_;
   bool one_sync_ = true;      // MQ_OPT_ONE_SYNC
+  bool fuse_desc_ = true;     // MQ_OPT_FUSE_DESC
+  uint32_t set_exp_ = 0;      // MQ_OPT_SET_EXP (timing experiments only)
   uint64_t last_sets_ = 0;    // merge sets of the last batch: the grid of the next set pass
   DevBuf sp_tc_;                     // per-topic counts from k_desc<true> (walk without lists)
   uint64_t rcap_ = 0;                // patches per region of sp_patches_ (kPatchRegions regions)

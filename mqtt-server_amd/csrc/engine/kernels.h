@@ -30,7 +30,7 @@ constexpr uint32_t kPartBatch = 4;     // partner links loaded together per reco
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
-constexpr uint32_t kWork = 4;
+constexpr uint32_t kWork = 8;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set)
 constexpr uint32_t kMergeWavesPerEU = 8;  // k_merge<spans> register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.
@@ -176,6 +176,8 @@ struct EmitArgs {
   // whose patch reservation does not fit its region, sets *unsafe (bit 2 / bit 4) instead
   uint64_t desc_cap;
   uint32_t* unsafe;
+  uint32_t g_stride;  // != 0: topic t's gathers at [t * g_stride, + tc[t].gathers) (DescArgs.g_stride)
+  uint32_t exp;       // MQ_OPT_SET_EXP bits (set pass attribution; 0 in the product)
 };
 constexpr uint32_t kSetHeavy = 1024;  // a merge set with this many may-merge records goes first
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
@@ -224,6 +226,14 @@ struct DescArgs {
   // with host-sized buffers). unsafe == null: sized by the host (no checks).
   uint64_t spans_cap, desc_cap;
   uint32_t* unsafe;
+  // g_stride != 0 (the walk-fused desc of one-sync batches): topic t's spans and GDesc records sit
+  // at [t * g_stride, + its gathers) instead of at off[t].g (no scan: off is unused), and
+  // tc_out[t].gathers is its number of gathers. list != null: only the topics list[0, *n_list)
+  // (the frontier walk's fallback topics), grid-stride.
+  uint32_t g_stride;
+  const uint32_t* list;
+  const uint32_t* n_list;
+  const TopicCount* g_count;  // list mode: the listed topics' gathers (their walk's counts)
 };
 
 // Merge-set dedup (span format): topics whose merge gathers are the same particles resolve to
@@ -241,7 +251,8 @@ struct DedupArgs {
   uint64_t table_mask;
   uint32_t* tslot;           // per topic: its table slot (kNone: not deduped)
   uint32_t* rep;             // per topic: its representative
-  unsigned long long* n_sets;  // [2]: representatives listed from the front (heavy) and the back
+  unsigned long long* n_sets;  // [2]: representatives listed from the front (heavy) and the back;
+                               //   [2]: the batch's gathers (sum of tc[t].gathers; tc != null)
   uint32_t* rep_list;          // those topics: heavy sets at [0, n_sets[0]), the others at
                                //   [n - n_sets[1], n) (heavy first: the set pass's tail is short)
   const TopicCount* tc;        // per-topic counts (k_desc; null: the offsets' differences): a set
@@ -321,6 +332,13 @@ void launch_walk(bool fill, bool lists, uint32_t wpe, const uint8_t* tb, const u
 void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n,
                        const DevIndex& ix, TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list,
                        uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s, bool clamp = false);
+// The frontier walk with k_desc fused into its epilogue (span format, dedup lists, no inline rows
+// or share pick, one-sync batches): each topic's gathers go straight from LDS to its spans and
+// merge lists at t * kGatherCap (da.g_stride); the fallback topics' k_walk and k_desc_g16 (list
+// mode) follow. No scan: da.tc_out holds the per-topic counts.
+void launch_walk_desc(uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
+                      TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list, uint32_t* fb_count,
+                      uint32_t fb_blocks, const DescArgs& da, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
@@ -341,6 +359,7 @@ struct FinishArgs {
   TopicSpansDev* sres;
   uint32_t* wave_list;
   unsigned long long* n_wave;
+  uint32_t g_stride;  // != 0: topic t's spans at t * g_stride (DescArgs.g_stride)
 };
 void launch_finish(const FinishArgs& a, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's

@@ -20,6 +20,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace mq {
 
@@ -424,11 +425,19 @@ struct FrontEnt {  // one frontier particle: its '+' / '#' children and its path
 
 // WPE: waves per SIMD asked of the register allocator (8: a few SGPRs spill to VGPR lanes; 1:
 // no constraint, 7 waves).
-template <uint32_t G, bool LISTS, int WPE>
+template <class GW>
+__device__ __forceinline__ void desc_g16(const DescArgs& a, uint32_t t, uint32_t n_g, uint64_t g0, uint64_t ipos,
+                                         uint32_t shr0, uint32_t sub, GW gw_at);
+
+// DESC (G = 16, LISTS = false): k_desc fused into the epilogue — the gathers, placed in the
+// reference's order in LDS, go straight to the topic's spans and merge lists (desc_g16 with the
+// stride layout, da.g_stride); neither the gather slots nor the counts are written.
+template <uint32_t G, bool LISTS, int WPE, bool DESC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walkf(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
                                                uint32_t n, DevIndex ix, TopicCount* __restrict__ cnt,
                                                uint32_t* __restrict__ gathers, uint32_t* __restrict__ fb_list,
-                                               uint32_t* __restrict__ fb_count) {
+                                               uint32_t* __restrict__ fb_count, DescArgs da) {
+  static_assert(!DESC || (G == 16 && !LISTS), "the fused desc runs on 16-lane groups of a gathers-only walk");
   constexpr uint32_t kTopics = 256 / G;  // topics per workgroup
   __shared__ uint32_t sl[kTopics][kFrontLevels];      // '/' positions (relative to the topic's chunk base)
   __shared__ uint4 skey[kTopics][kFrontLevels];       // each level's segment key (SegKey)
@@ -562,6 +571,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   // --- the gathers in the reference's order ------------------------------------------------------
   wave_sync_lds();
+  if (DESC) {
+    // each gather's place (the smaller ranks), then the words in place in LDS, then k_desc's work
+    uint32_t pw[kGatherCap / G], ww[kGatherCap / G];
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherCap / G; k++) {
+      const uint32_t i = sub + k * G;
+      pw[k] = kNone;
+      if (i < ng) {
+        const uint2 gi = gat[q][i];
+        uint32_t pos = 0;
+        for (uint32_t j = 0; j < ng; j++) pos += gat[q][j].y < gi.y ? 1u : 0u;
+        const uint32_t k0 = gi.y >> 30;  // how the path starts: literal 1, '+' 2, '#' 3
+        const bool wild = k0 >= 2 || (k0 == 1 && lit0wild);
+        pw[k] = pos;
+        ww[k] = gi.x | (!(dollar && wild) ? kGatherSubs : 0u);
+      }
+    }
+    wave_sync_lds();
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherCap / G; k++)
+      if (pw[k] != kNone) gat[q][pw[k]].x = ww[k];
+    wave_sync_lds();
+    desc_g16(da, t, ng, (uint64_t)t * da.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gat[q][i].x; });
+    return;
+  }
   uint32_t rows = 0, shared = 0, inl = 0, merge = 0;
   uint32_t* gout = gathers + (uint64_t)t * kGatherCap;
   for (uint32_t i = sub; i < ng; i += G) {
@@ -865,33 +899,25 @@ __device__ __forceinline__ void write_gdesc(const DevIndex& ix, const uint32_t* 
 // scattered places per instruction (1.18 GB written per 1M topics at 10M subscriptions for
 // 0.3 GB of records). Same outputs as k_desc<true> with dedup lists; the merge-set signature is
 // position-keyed (a sum over the merge gathers of a hash of (particle, merge index)).
-__global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
-  const uint32_t lane = threadIdx.x & 63, sub = lane & 15;
-  const uint32_t t = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-  const bool live = t < a.n;
-  TopicOff o0{0, 0, 0, 0, 0}, o1{0, 0, 0, 0, 0};
-  if (live) {
-    o0 = a.off[t];
-    o1 = a.off[t + 1];
-  }
-  const uint32_t n_g = (uint32_t)(o1.g - o0.g);
-  const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
+// desc_g16: one topic on its 16-lane group (sub = lane & 15; group-uniform control flow): n_g
+// gathers, gw_at(i) the word of gather i, spans / GDesc at g0, inline rows copied to ipos, shared
+// rows counted from shr0 (GDesc records only). Also run by the walk-fused k_walkf<..., DESC>.
+template <class GW>
+__device__ __forceinline__ void desc_g16(const DescArgs& a, uint32_t t, uint32_t n_g, uint64_t g0, uint64_t ipos,
+                                         uint32_t shr0, uint32_t sub, GW gw_at) {
   // one-sync batch: spans past the buffer are not written (the batch runs again, host-sized)
-  const bool fits = !a.unsafe || o1.g <= a.spans_cap;
-  if (live && !fits && sub == 0) atomicOr(a.unsafe, kUnsafeSpans);
-  uint32_t m = n_g;  // the wavefront's longest topic bounds its (wave-uniform) rounds
-  m = max(m, (uint32_t)__shfl_xor(m, 16, 64));
-  m = max(m, (uint32_t)__shfl_xor(m, 32, 64));
+  const bool fits = !a.unsafe || g0 + n_g <= a.spans_cap;
+  if (!fits && sub == 0) atomicOr(a.unsafe, kUnsafeSpans);
   uint32_t rpos = 0, spos = 0, n_mg = 0, n_merge = 0;
-  uint64_t ipos = o0.inl, sig = 0;
-  for (uint32_t r0 = 0; r0 < m; r0 += 16) {
+  uint64_t sig = 0;
+  for (uint32_t r0 = 0; r0 < n_g; r0 += 16) {
     const uint32_t i = r0 + sub;
     const bool act = i < n_g;
     uint32_t gw = 0;
     NodeLists L{0, 0, 0, 0, 0, 0, 0, 0};
     NodePair P{0, kNone, 0, 0};
     if (act) {
-      gw = gw_src[i];
+      gw = gw_at(i);
       L = a.ix.lists[gw & kGatherNode];
       P = a.ix.npair[gw & kGatherNode];
     }
@@ -905,7 +931,7 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
     const uint32_t sh_i = g16_incl(act ? L.shr_cnt : 0u, sub);
     const uint32_t rp = rpos + rn_i - rn, x = n_mg + inc_i - inc;
     const uint64_t ip = ipos + (in_i - in);
-    if (act && fits) a.spans[o0.g + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
+    if (act && fits) a.spans[g0 + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
     for (uint32_t k = 0; k < in; k++) a.inl_out[ip + k] = a.ix.inl[L.inl_off + k];
     if (ismg) {
       sig += mix64(((uint64_t)x << 32 | (gw & kGatherNode)) + 0x9e3779b97f4a7c15ull);
@@ -928,15 +954,52 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
     sig += __shfl_xor(sig, d, 16);
     n_merge += __shfl_xor(n_merge, d, 16);
   }
-  if (!live || sub != 0) return;
+  if (sub != 0) return;
   if (a.tc_out) a.tc_out[t] = TopicCount{n_g, rpos, spos, 0u, n_merge};
   a.msig[t] = mix64(sig + n_mg) | 1ull;  // never 0 (the dedup table's empty key)
   a.mcount[t] = n_mg;
-  // k_merge maps this topic from its GDesc records: write them (rare)
+  // k_merge maps this topic from its GDesc records: write them (rare; gather words re-read)
   if (n_mg > kPairMax) {
-    if (!a.unsafe || o1.g <= a.desc_cap) write_gdesc(a.ix, gw_src, n_g, (uint32_t)o0.shr, a.desc + o0.g);
-    else atomicOr(a.unsafe, kUnsafeSpans);
+    if (!a.unsafe || g0 + n_g <= a.desc_cap) {
+      uint32_t rp = 0, sp = shr0;
+      for (uint32_t i = 0; i < n_g; i++) {
+        const uint32_t gw = gw_at(i);
+        const NodeLists L = a.ix.lists[gw & kGatherNode];
+        const bool mg = (gw & kGatherSubs) && L.n_merge;
+        const NodePair P = mg ? a.ix.npair[gw & kGatherNode] : NodePair{0, kNone, 0, 0};
+        const uint64_t rk = mg && a.ix.xinfo ? a.ix.xinfo[gw & kGatherNode].rank : 0ull;
+        a.desc[g0 + i] = GDesc{rp, L.sub_off, mg ? P.ent_off : sp, mg ? P.ent_mask : L.shr_off, (uint32_t)rk,
+                               (uint32_t)(rk >> 32), gw, L.n_direct | (mg ? kDescMerge : 0u)};
+        rp += (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
+        sp += L.shr_cnt;
+      }
+    } else {
+      atomicOr(a.unsafe, kUnsafeSpans);
+    }
   }
+}
+
+// list == null: topic t = (global thread) / 16 < n, at off[t] (or at t * g_stride). Else the
+// topics list[0, *n_list), group-strided (stride layout; their gathers counted in g_count).
+__global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
+  const uint32_t sub = threadIdx.x & 15;
+  const uint32_t gid = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  if (a.list) {
+    const uint32_t nl = *a.n_list;
+    for (uint32_t i = gid; i < nl; i += (gridDim.x * blockDim.x) >> 4) {
+      const uint32_t t = a.list[i];
+      const uint32_t n_g = min(a.g_count[t].gathers, kGatherCap);
+      const uint32_t* gw_src = a.gathers + (uint64_t)t * a.gather_stride;
+      desc_g16(a, t, n_g, (uint64_t)t * a.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gw_src[i]; });
+    }
+    return;
+  }
+  const uint32_t t = gid;
+  if (t >= a.n) return;  // (group-uniform)
+  const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+  const uint32_t n_g = (uint32_t)(o1.g - o0.g);
+  const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
+  desc_g16(a, t, n_g, o0.g, o0.inl, (uint32_t)o0.shr, sub, [&](uint32_t i) { return gw_src[i]; });
 }
 
 // k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, whose
@@ -988,7 +1051,7 @@ __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
 // k_dedup_rep also lists the topics that resolve a merge set (rep_list, n_sets of them): the
 // merge's set pass walks that list instead of every topic.
 __global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
-  __shared__ uint32_t wcnt[2][16];
+  __shared__ uint32_t wcnt[3][16];
   __shared__ unsigned long long bbase[2];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63, wv = wave_id();
   const bool act = t < a.n;
@@ -1023,14 +1086,22 @@ __global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
   if (act) a.rep[t] = r;
   const bool own = r == t && sl != kNone;
   const bool heavy = own && (a.tc ? a.tc[t].merge : (uint32_t)(a.off[t + 1].merge - a.off[t].merge)) >= a.heavy;
+  // the batch's gathers (the walk-fused desc has no scan to total them)
+  const uint32_t gsum = a.tc ? wave_sum(act ? a.tc[t].gathers : 0u) : 0u;
   const uint64_t bh = __ballot(heavy), bl = __ballot(own && !heavy);
   // one atomic per workgroup and list end on the counters (one per wavefront serialised ~16k
   // atomics on one address per 1M topics)
   if (lane == 0) {
     wcnt[0][wv] = (uint32_t)__popcll(bh);
     wcnt[1][wv] = (uint32_t)__popcll(bl);
+    wcnt[2][wv] = gsum;
   }
   __syncthreads();
+  if (a.tc && threadIdx.x == 64) {
+    unsigned long long g = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; w++) g += wcnt[2][w];
+    if (g) atomicAdd(a.n_sets + 2, g);
+  }
   if (threadIdx.x < 2) {
     const uint32_t e = threadIdx.x;
     uint32_t tot = 0;
@@ -1050,7 +1121,15 @@ __global__ __launch_bounds__(256) void k_finish(FinishArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
   bool wave = false;
   if (t < a.n) {
-    const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+    TopicOff o0, o1;
+    if (a.g_stride) {  // the stride layout of the walk-fused desc (a.tc holds the counts)
+      o0 = TopicOff{(uint64_t)t * a.g_stride, 0, 0, 0, 0};
+      o1 = o0;
+      o1.g += a.tc[t].gathers;
+    } else {
+      o0 = a.off[t];
+      o1 = a.off[t + 1];
+    }
     const TopicCount c = a.tc ? a.tc[t]
                               : TopicCount{(uint32_t)(o1.g - o0.g), (uint32_t)(o1.rows - o0.rows),
                                            (uint32_t)(o1.shr - o0.shr), (uint32_t)(o1.inl - o0.inl),
@@ -1300,7 +1379,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t i_end = tlist ? (SET ? n_front + (uint32_t)a.n_reps[1] : (uint32_t)*a.n_wave) : a.t1;
   for (uint32_t i = a.t0 + blockIdx.x * 4 + wv; i < i_end; i += gridDim.x * 4) {
   const uint32_t t = !tlist ? i : (SET && i >= n_front) ? tlist[a.t1 - 1 - (i - n_front)] : tlist[i];
-  const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+  TopicOff o0, o1;
+  if (SPANS && a.g_stride) {  // the stride layout of the walk-fused desc: no offsets
+    o0 = TopicOff{(uint64_t)t * a.g_stride, 0, 0, 0, 0};
+    o1 = o0;
+    o1.g += a.tc[t].gathers;
+  } else {
+    o0 = a.off[t];
+    o1 = a.off[t + 1];
+  }
   const uint64_t rb = o0.rows - a.base.rows;
   const uint64_t ib = o0.inl - a.base.inl;
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
@@ -1316,6 +1403,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t drep = dslot != kNone ? a.rep[t] : t;
   if (SET && (dslot == kNone || drep != t)) continue;
   const bool setrel = SET;
+  // MQ_PROF_WORK: the set pass's phases in shader clocks (map, pair analysis, resolution)
+  const bool stamp = SET && a.work != nullptr;
+  uint64_t c_start = stamp ? clock64() : 0ull, c_map = c_start, c_pairs = c_start;
   const bool dcopy = !SET && SPANS && a.rep && dslot != kNone;
   PatchRec* __restrict__ ppool = setrel ? a.spatches : a.patches;
   unsigned long long* __restrict__ pcnt = setrel ? a.spcount : a.pcount;
@@ -1470,6 +1560,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       n_ent += (uint32_t)(x1 - x0);
     }
     wave_sync_lds();
+    if (stamp) c_map = clock64();
     // beyond the map: linear lookups (the map's hash table keeps a free slot: kMapSlots - 1
     // entries at most, so a lookup of a node that is not there ends)
     const bool slow = n_map > kPairMax || n_ent > (XS ? kEnt - 1 : kEnt);
@@ -1540,6 +1631,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         bool bound = false, base = true;
         uint32_t first = kNone;
         uint32_t q = rmeta & kMetaQos, nl = rmeta & kMetaNoLocal;
+        if (SET && (a.exp & 1u)) mp_cnt = 0;
         // partner links in batches of kPartBatch independent loads (one latency per batch)
         for (uint32_t e0 = 0; e0 < mp_cnt && base; e0 += kPartBatch) {
           MergePart pb[kPartBatch];
@@ -1550,6 +1642,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
           for (uint32_t u = 0; u < kPartBatch; u++) {
             if (!base || pb[u].node == kNone) continue;
+            if (SET && (a.exp & 2u)) {
+              q = max(q, pb[u].meta & kMetaQos);
+              continue;
+            }
             const Pos ph = gathered(pb[u].node);
             if (!ph.found) continue;
             if (!bound) first = pb[u].node;
@@ -1573,12 +1669,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
         }
       }
-      if (SPANS) emit_patch(want, row, pmeta);
+      if (SPANS) emit_patch(want && !(SET && (a.exp & 4u)), row, pmeta);
       const uint64_t bn = __ballot(counted && nonbase);
       const uint64_t bx = __ballot(counted && nonbase && (pmeta & kRowIdent));
       n_nonbase += __popcll(bn);
       n_ext += __popcll(bx);
     };
+
 
     if (!slow) {
       // Pair analysis over ordered pairs (g, h) of merge gathers: g's pair block lists the slots
@@ -1592,6 +1689,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         auto locate = [&](uint32_t r, uint32_t& jj) __attribute__((always_inline)) -> PairSlot {
           const uint32_t rc = min(r, tot - 1);
           uint32_t lo = 0, hi = n_hit;  // h_pre[lo] <= rc < h_pre[hi] (lists are non-empty)
+          if (SET && (a.exp & 8u)) {  // (a list's first slot: in bounds, not the record's)
+            jj = rc % n_hit;
+            return a.ix.plist[h_off[wv][jj]];
+          }
           while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (h_pre[wv][mid] <= rc) lo = mid; else hi = mid;
@@ -1687,6 +1788,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       };
       if (SPANS) {
         pairs(true);
+        if (stamp) c_pairs = clock64();
         reserve(tot_all);
         if (staged_all) {
           if (n_hit) flush_hits();
@@ -1733,6 +1835,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         atomicAdd(wc + 1, (unsigned long long)rr);
         atomicAdd(wc + 2, (unsigned long long)l);
         atomicAdd(wc + 3, (unsigned long long)n_patch);
+      }
+      const uint64_t c_end = clock64();
+      if (lane == 0 && c_pairs != c_start) {  // (the map / pair-analysis path)
+        atomicAdd(wc + 4, (unsigned long long)(c_map - c_start));
+        atomicAdd(wc + 5, (unsigned long long)(c_pairs - c_map));
+        atomicAdd(wc + 6, (unsigned long long)(c_end - c_pairs));
+        atomicAdd(wc + 7, (unsigned long long)(c_end - c_start));
       }
     }
     continue;
@@ -1832,17 +1941,19 @@ void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* 
                        uint32_t* fb_count, uint32_t fb_blocks, hipStream_t s, bool clamp) {
   if (!n) return;
   const dim3 grid((n + 256 / group - 1) / (256 / group));
+  DescArgs nd;
+  std::memset(&nd, 0, sizeof(nd));
 #define MQ_WALKF(G, L)                                                                                              \
   if (wpe >= 8)                                                                                                  \
-    hipLaunchKernelGGL((k_walkf<G, L, 8>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count); \
+    hipLaunchKernelGGL((k_walkf<G, L, 8>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count, nd); \
   else                                                                                                           \
-    hipLaunchKernelGGL((k_walkf<G, L, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
+    hipLaunchKernelGGL((k_walkf<G, L, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count, nd)
   if (group == 16) {
     if (lists) MQ_WALKF(16, true);
     else MQ_WALKF(16, false);
   } else {  // (narrower groups: more topics per workgroup, so LDS bounds them below 8 waves)
 #define MQ_WALKF1(G, L) \
-  hipLaunchKernelGGL((k_walkf<G, L, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count)
+  hipLaunchKernelGGL((k_walkf<G, L, 1>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list, fb_count, nd)
     if (group == 8) {
       if (lists) MQ_WALKF1(8, true);
       else MQ_WALKF1(8, false);
@@ -1861,6 +1972,30 @@ void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* 
   else
     hipLaunchKernelGGL((k_walk<false, false, 1>), fgrid, dim3(256), 0, s, tb, to, n, ix, cnt, nullptr, gathers, ovf,
                        fb_list, fb_count, clamp);
+}
+
+void launch_walk_desc(uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
+                      TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list, uint32_t* fb_count,
+                      uint32_t fb_blocks, const DescArgs& da, hipStream_t s) {
+  if (!n) return;
+  const dim3 grid((n + 15) / 16);
+  if (wpe >= 8)
+    hipLaunchKernelGGL((k_walkf<16, false, 8, true>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list,
+                       fb_count, da);
+  else
+    hipLaunchKernelGGL((k_walkf<16, false, 1, true>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list,
+                       fb_count, da);
+  // the topics the frontier could not hold: k_walk's gather slots (clamped counts), then k_desc
+  const dim3 fgrid(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, fb_blocks)));
+  hipLaunchKernelGGL((k_walk<false, false, 1>), fgrid, dim3(256), 0, s, tb, to, n, ix, cnt, nullptr, gathers, ovf,
+                     fb_list, fb_count, true);
+  DescArgs fa = da;
+  fa.list = fb_list;
+  fa.n_list = fb_count;
+  fa.g_count = cnt;
+  fa.gathers = gathers;
+  fa.gather_stride = kGatherCap;
+  hipLaunchKernelGGL(k_desc_g16, fgrid, dim3(256), 0, s, fa);
 }
 
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,

@@ -5,8 +5,8 @@
 namespace mq {
 namespace host {
 
-template class BasicBatcher<Subscribers>;
-template class BasicBatcher<TopicView>;
+template class BasicBatcher<MapsPolicy>;
+template class BasicBatcher<ViewsPolicy>;
 
 }  // namespace host
 }  // namespace mq

@@ -30,6 +30,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -39,23 +40,30 @@
 namespace mq {
 namespace host {
 
-template <class R>
+// Policy: Batch — one match call's result; Item — what a ticket's get() gives;
+// item(batch, i) — topic i's Item; match(index, packed topics) — the engine call.
+template <class Policy>
 class BasicBatcher {
+  using Batch = typename Policy::Batch;
+  using Item = typename Policy::Item;
   // One queue's part of one batch: its topics are the batch's [base, base + n).
   struct Segment {
     std::mutex mu;
     std::condition_variable cv;
     bool done = false;
-    std::shared_ptr<const std::vector<R>> results;  // the batch's results (null: it failed)
+    std::shared_ptr<const Batch> results;  // the batch's results (null: it failed)
     std::exception_ptr err;
     uint32_t base = 0;
+    std::chrono::steady_clock::time_point done_at;  // when the batch completed
   };
+  // A submission queue: its topics packed as they come (bytes + offsets: sealing swaps the
+  // buffers out, it does not move strings one by one).
   struct alignas(64) Shard {
     std::mutex mu;
-    std::vector<std::string> topics;
+    PackedTopics q;
     std::shared_ptr<Segment> seg;  // the segment the queued topics belong to
   };
-  static constexpr uint32_t kShards = 16;
+  static constexpr uint32_t kShards = 64;  // (as many as typical submitters: each thread its own lock)
 
  public:
   struct Stats {
@@ -65,17 +73,17 @@ class BasicBatcher {
     // the dispatcher's time (ns): waiting for topics, sealing, in the match call, completing
     uint64_t wait_ns = 0, seal_ns = 0, match_ns = 0, complete_ns = 0;
   };
-  using MatchFn = std::function<std::vector<R>(const std::vector<std::string>&)>;
+  using MatchFn = std::function<std::shared_ptr<const Batch>(const PackedTopics&)>;
 
   // A submitted topic: get() waits for its batch and returns its result (throws EngineError if
   // the batch's match failed). Valid until destroyed; copies share the result.
   class Ticket {
    public:
     Ticket() = default;
-    const R& get() const {
+    Item get() const {
       wait();
       if (seg_->err) std::rethrow_exception(seg_->err);
-      return (*seg_->results)[seg_->base + idx_];
+      return Policy::item(seg_->results, seg_->base + idx_);
     }
     void wait() const {
       std::unique_lock<std::mutex> lk(seg_->mu);
@@ -86,6 +94,11 @@ class BasicBatcher {
       return seg_->done;
     }
     bool valid() const { return seg_ != nullptr; }
+    // when the ticket's batch completed (valid once ready()): for latency measurements
+    std::chrono::steady_clock::time_point done_at() const {
+      std::lock_guard<std::mutex> lk(seg_->mu);
+      return seg_->done_at;
+    }
 
    private:
     friend class BasicBatcher;
@@ -109,7 +122,7 @@ class BasicBatcher {
   BasicBatcher& operator=(const BasicBatcher&) = delete;
 
   // Thread-safe.
-  Ticket Submit(std::string topic) {
+  Ticket Submit(std::string_view topic) {
     static std::atomic<uint32_t> next_shard{0};
     thread_local const uint32_t my = next_shard.fetch_add(1, std::memory_order_relaxed);
     Shard& sh = shards_[my % kShards];
@@ -118,8 +131,8 @@ class BasicBatcher {
     {
       std::lock_guard<std::mutex> lk(sh.mu);
       if (!sh.seg) sh.seg = std::make_shared<Segment>();
-      t = Ticket(sh.seg, (uint32_t)sh.topics.size());
-      sh.topics.push_back(std::move(topic));
+      t = Ticket(sh.seg, sh.q.size());
+      sh.q.add(topic);
       // counted under the queue's lock: the dispatcher subtracts only topics it took, so the
       // count never runs below what is queued
       q = queued_.fetch_add(1, std::memory_order_acq_rel) + 1;
@@ -137,8 +150,10 @@ class BasicBatcher {
 
  private:
   void run() {
-    std::vector<std::string> topics;
-    std::vector<std::pair<std::shared_ptr<Segment>, uint32_t>> segs;  // (segment, its topics)
+    PackedTopics batch;
+    PackedTopics spare[kShards];  // emptied buffers, swapped into the queues at the next seal
+    std::vector<std::pair<std::shared_ptr<Segment>, uint32_t>> segs;  // (segment, its first topic)
+    std::vector<uint32_t> taken;                                       // queues sealed into the batch
     using Clock = std::chrono::steady_clock;
     auto ns = [](Clock::time_point a, Clock::time_point b) {
       return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
@@ -157,28 +172,43 @@ class BasicBatcher {
       }
       const auto c1 = Clock::now();
       // seal: every queue's topics, in queue order (at most max_batch; a queue that would
-      // overflow the batch keeps its topics and its segment for the next one)
-      topics.clear();
+      // overflow the batch keeps its topics and its segment for the next one). Under a queue's
+      // lock only its buffers are swapped for empty ones; the packing happens after.
       segs.clear();
-      for (uint32_t s = 0; s < kShards; s++) {
-        Shard& sh = shards_[(s + rr_) % kShards];
+      taken.clear();
+      uint64_t n = 0;
+      for (uint32_t k = 0; k < kShards; k++) {
+        const uint32_t s = (k + rr_) % kShards;
+        Shard& sh = shards_[s];
         std::lock_guard<std::mutex> lk(sh.mu);
-        if (sh.topics.empty()) continue;
-        if (!topics.empty() && topics.size() + sh.topics.size() > max_batch_) continue;
-        const uint32_t base = (uint32_t)topics.size();
-        for (std::string& t : sh.topics) topics.push_back(std::move(t));
-        segs.emplace_back(std::move(sh.seg), base);
-        sh.topics.clear();
-        sh.seg.reset();
+        if (sh.q.empty()) continue;
+        if (n && n + sh.q.size() > max_batch_) continue;
+        segs.emplace_back(std::move(sh.seg), (uint32_t)n);
+        n += sh.q.size();
+        std::swap(sh.q, spare[s]);
+        taken.push_back(s);
       }
       rr_++;  // the next batch starts at another queue (none waits behind the others for ever)
-      if (topics.empty()) continue;
-      queued_.fetch_sub(topics.size(), std::memory_order_acq_rel);
-      std::shared_ptr<const std::vector<R>> res;
+      if (!n) continue;
+      queued_.fetch_sub(n, std::memory_order_acq_rel);
+      batch.clear();
+      size_t nb = 0;
+      for (uint32_t s : taken) nb += spare[s].bytes.size();
+      batch.bytes.reserve(nb + 16);
+      batch.offs.reserve(n + 1);
+      for (uint32_t s : taken) {
+        PackedTopics& q = spare[s];
+        const uint64_t b0 = batch.bytes.size();
+        batch.bytes.append(q.bytes);
+        for (uint32_t i = 1; i < q.offs.size(); i++) batch.offs.push_back(b0 + q.offs[i]);
+        q.clear();
+      }
+      batch.finish();
+      std::shared_ptr<const Batch> res;
       std::exception_ptr err;
       const auto c2 = Clock::now();
       try {
-        res = std::make_shared<const std::vector<R>>(match_(topics));
+        res = match_(batch);
       } catch (...) {
         err = std::current_exception();
       }
@@ -186,6 +216,7 @@ class BasicBatcher {
       for (auto& sg : segs) {
         {
           std::lock_guard<std::mutex> lk(sg.first->mu);
+          sg.first->done_at = c3;
           sg.first->results = res;
           sg.first->err = err;
           sg.first->base = sg.second;
@@ -193,11 +224,13 @@ class BasicBatcher {
         }
         sg.first->cv.notify_all();
       }
+      segs.clear();  // (the last ticket of a segment frees it, and with it the batch)
+      res.reset();
       const auto c4 = Clock::now();
       std::lock_guard<std::mutex> lk(mu_);
       st_.batches++;
-      st_.topics += topics.size();
-      st_.largest = std::max<uint64_t>(st_.largest, topics.size());
+      st_.topics += n;
+      st_.largest = std::max<uint64_t>(st_.largest, n);
       st_.wait_ns += ns(c0, c1);
       st_.seal_ns += ns(c1, c2);
       st_.match_ns += ns(c2, c3);
@@ -219,22 +252,39 @@ class BasicBatcher {
   std::thread th_;
 };
 
-class PublishBatcher : public BasicBatcher<Subscribers> {
+// Tickets of Subscribers (the Go-shaped maps, TopicsIndex::SubscribersBatch)
+struct MapsPolicy {
+  using Batch = std::vector<Subscribers>;
+  using Item = const Subscribers&;
+  static Item item(const std::shared_ptr<const Batch>& b, uint32_t i) { return (*b)[i]; }
+};
+// Tickets of TopicView: each view is made by the thread that takes it (one reference count per
+// get()), so the dispatcher does no per-topic work after the match
+struct ViewsPolicy {
+  using Batch = SpanBatch;
+  using Item = TopicView;
+  static Item item(const std::shared_ptr<const Batch>& b, uint32_t i) { return TopicView(b, i); }
+};
+
+class PublishBatcher : public BasicBatcher<MapsPolicy> {
  public:
   explicit PublishBatcher(TopicsIndex& ix, size_t max_batch = 16384,
                           std::chrono::microseconds max_delay = std::chrono::microseconds(200),
                           size_t min_fill = 1024)
-      : BasicBatcher([&ix](const std::vector<std::string>& t) { return ix.SubscribersBatch(t); }, max_batch,
-                     max_delay, min_fill) {}
+      : BasicBatcher(
+            [&ix](const PackedTopics& t) {
+              return std::make_shared<const std::vector<Subscribers>>(ix.SubscribersBatch(t));
+            },
+            max_batch, max_delay, min_fill) {}
 };
 
-class PublishViewBatcher : public BasicBatcher<TopicView> {
+class PublishViewBatcher : public BasicBatcher<ViewsPolicy> {
  public:
   explicit PublishViewBatcher(TopicsIndex& ix, size_t max_batch = 16384,
                               std::chrono::microseconds max_delay = std::chrono::microseconds(200),
                               size_t min_fill = 1024)
-      : BasicBatcher([&ix](const std::vector<std::string>& t) { return ix.SubscribersViews(t); }, max_batch,
-                     max_delay, min_fill) {}
+      : BasicBatcher([&ix](const PackedTopics& t) { return ix.SubscribersSpans(t); }, max_batch, max_delay,
+                     min_fill) {}
 };
 
 }  // namespace host

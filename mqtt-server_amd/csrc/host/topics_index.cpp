@@ -286,17 +286,21 @@ std::string TopicsIndex::FilterName(uint32_t id) const {
   return filters_.str(id);
 }
 
-std::vector<TopicView> TopicsIndex::SubscribersViews(const std::vector<std::string>& topics) {
+static PackedTopics pack(const std::vector<std::string>& topics) {
+  PackedTopics p;
+  size_t nb = 0;
+  for (const std::string& t : topics) nb += t.size();
+  p.bytes.reserve(nb + 16);
+  p.offs.reserve(topics.size() + 1);
+  for (const std::string& t : topics) p.add(t);
+  p.finish();
+  return p;
+}
+
+std::shared_ptr<const SpanBatch> TopicsIndex::SubscribersSpans(const PackedTopics& topics) {
   const uint64_t stamp = epochs_.begin();
-  std::string bytes;
-  std::vector<uint64_t> offs(1, 0);
-  for (const std::string& t : topics) {
-    bytes += t;
-    offs.push_back(bytes.size());
-  }
-  bytes.resize(bytes.size() + 16, '\0');  // readable padding (include/mqmatch.h)
   mq_span_result* r = nullptr;
-  const int rc = mq_match_spans(idx_, (const uint8_t*)bytes.data(), offs.data(), (uint32_t)topics.size(), &r);
+  const int rc = mq_match_spans(idx_, (const uint8_t*)topics.bytes.data(), topics.offs.data(), topics.size(), &r);
   if (rc < 0) {
     epochs_.end(stamp);
     check(rc, "mq_match_spans");
@@ -311,13 +315,18 @@ std::vector<TopicView> TopicsIndex::SubscribersViews(const std::vector<std::stri
     throw;
   }
   own.release();  // the batch frees it
+  return batch;
+}
+
+std::vector<TopicView> TopicsIndex::SubscribersViews(const std::vector<std::string>& topics) {
+  std::shared_ptr<const SpanBatch> batch = SubscribersSpans(pack(topics));
   std::vector<TopicView> out;
   out.reserve(topics.size());
   for (uint32_t t = 0; t < topics.size(); t++) out.emplace_back(batch, t);
   return out;
 }
 
-Subscribers TopicsIndex::Subscribers_(const std::string& topic) { return SubscribersBatch({topic})[0]; }
+Subscribers TopicsIndex::Subscribers_(const std::string& topic) { return SubscribersBatch(std::vector<std::string>{topic})[0]; }
 
 // One mq_match_spans call for the batch, with no host lock held; then each topic's Subscribers
 // is rebuilt straight from its spans (the index's records, pinned by the result) with the
@@ -326,20 +335,17 @@ Subscribers TopicsIndex::Subscribers_(const std::string& topic) { return Subscri
 // meanwhile; a subscription removed since the match (its stored entry gone) is rebuilt from the
 // row itself.
 std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::string>& topics) {
+  return SubscribersBatch(pack(topics));
+}
+
+std::vector<Subscribers> TopicsIndex::SubscribersBatch(const PackedTopics& topics) {
   struct Guard {
     Epochs& ep;
     uint64_t stamp;
     ~Guard() { ep.end(stamp); }
   } guard{epochs_, epochs_.begin()};
-  std::string bytes;
-  std::vector<uint64_t> offs(1, 0);
-  for (const std::string& t : topics) {
-    bytes += t;
-    offs.push_back(bytes.size());
-  }
-  bytes.resize(bytes.size() + 16, '\0');  // readable padding (include/mqmatch.h)
   mq_span_result* r = nullptr;
-  check(mq_match_spans(idx_, (const uint8_t*)bytes.data(), offs.data(), (uint32_t)topics.size(), &r),
+  check(mq_match_spans(idx_, (const uint8_t*)topics.bytes.data(), topics.offs.data(), topics.size(), &r),
         "mq_match_spans");
   // freed however this ends (an exception while building the maps must not leak the pin, or
   // every later update would wait for it); declared before the table lock, so released after it
@@ -358,7 +364,7 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const std::vector<std::st
     return s;
   };
   std::unordered_map<uint32_t, uint32_t> patched;  // topic row -> meta
-  for (size_t t = 0; t < topics.size(); t++) {
+  for (size_t t = 0; t < out.size(); t++) {
     const mq_topic_spans& ts = r->topics[t];
     Subscribers& s = out[t];
     patched.clear();

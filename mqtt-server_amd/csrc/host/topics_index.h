@@ -16,6 +16,7 @@
 #include <shared_mutex>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -125,6 +126,25 @@ class IdTable {
 
 class TopicsIndex;
 
+// A batch of topics packed as the engine takes them (include/mqmatch.h): the topics' bytes back
+// to back, offsets[n + 1]; finish() adds the 16 readable padding bytes the engine's reader needs.
+struct PackedTopics {
+  std::string bytes;
+  std::vector<uint64_t> offs = std::vector<uint64_t>(1, 0);
+  uint32_t size() const { return (uint32_t)(offs.size() - 1); }
+  bool empty() const { return offs.size() == 1; }
+  void add(std::string_view t) {
+    bytes.append(t.data(), t.size());
+    offs.push_back(bytes.size());
+  }
+  void clear() {  // (keeps the capacity)
+    bytes.clear();
+    offs.resize(1);
+  }
+  void finish() { bytes.resize(offs.back() + 16, '\0'); }
+  std::string_view at(uint32_t i) const { return std::string_view(bytes).substr(offs[i], offs[i + 1] - offs[i]); }
+};
+
 // One mq_match_spans result shared by the views of its topics (freed with the last view). It
 // pins the index's host image: updates wait until it is freed (include/mqmatch.h), so views are
 // for the fan-out of a batch, not for keeping. Its epoch keeps the ids its rows name in use.
@@ -228,8 +248,12 @@ class TopicsIndex {
   std::vector<uint64_t> Messages(const std::string& filter);  // topics.go:525 (handles)
   Subscribers Subscribers_(const std::string& topic);          // topics.go:583
   std::vector<Subscribers> SubscribersBatch(const std::vector<std::string>& topics);
+  std::vector<Subscribers> SubscribersBatch(const PackedTopics& topics);  // topics.finish()ed
   // The same batch as views (no maps): what a fan-out iterates
   std::vector<TopicView> SubscribersViews(const std::vector<std::string>& topics);
+  // ... as the batch itself: TopicView(batch, t) is topic t's view (the batching stage makes the
+  // views on the threads that take them, not on its dispatcher)
+  std::shared_ptr<const SpanBatch> SubscribersSpans(const PackedTopics& topics);  // topics.finish()ed
   std::string ClientName(uint32_t id) const;
   std::string FilterName(uint32_t id) const;
 

@@ -78,7 +78,7 @@ PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 OPT_CHUNK_ROWS, OPT_PATCH_CAP, OPT_EDGE_LOAD = 1, 6, 13
 OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_MERGE_WAVES = 2, 3, 4, 5, 7
 OPT_MSG_IMAGE, OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_MERGE_DEDUP = 8, 9, 10, 12
-OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC = 14, 15, 16
+OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC, OPT_FUSE_DESC, OPT_SET_EXP = 14, 15, 16, 17, 18
 
 
 class MsgResult(C.Structure):
@@ -693,8 +693,11 @@ def expand_device_spans(r, n, count=None):
     count = n if count is None else min(count, n)
     t = d2h(r.topics, 64 * count, np.uint8).view(_TOPIC_SPANS_DT)
     n = count
-    n_sp = int(t["span_base"][-1]) + int(t["n_spans"][-1]) if n else 0  # spans are in topic order
-    spans = d2h(r.spans, n_sp, np.uint32, 4)
+    # a topic's spans are contiguous at span_base (topics in order; one-sync batches place topic t's
+    # at t * 64, the walk-fused desc's stride layout)
+    sb, ns = t["span_base"].astype(np.int64), t["n_spans"].astype(np.int64)
+    n_sp = int((sb + ns).max()) if n else 0
+    spans = d2h(r.spans, n_sp, np.uint32, 4)[_ranges(sb, ns)]
     pool = d2h(r.sub_pool, int(r.sub_pool_len), np.uint32, 4)
     spool = d2h(r.shared_pool, int(r.shared_pool_len), np.uint32, 2)
     patches = d2h(r.patches, int(r.n_patches), np.uint32, 2)

@@ -364,7 +364,7 @@ static void TestConcurrentReadersAndUpdates() {
   for (int w = 0; w < 3; w++)
     th.emplace_back([&, w] {
       for (int k = 0; !stop; k++) {
-        auto res = ix.SubscribersBatch({"s/" + std::to_string(k % 10) + "/x", "t/" + std::to_string(k % 7)});
+        auto res = ix.SubscribersBatch(std::vector<std::string>{"s/" + std::to_string(k % 10) + "/x", "t/" + std::to_string(k % 7)});
         for (auto& kv : res[0].Subscriptions)
           if (kv.first.rfind("base", 0) != 0 && kv.first.rfind("tmp", 0) != 0) bad++;
         for (auto& kv : res[1].Subscriptions)

@@ -372,22 +372,32 @@ def test_spans_device_matches_host(gpu_available):
     hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
     assert hip.hipMemcpy(top.data_ptr(), r.topics, n * 64, 3) == 0
     got = top.cpu().numpy().view(E._TOPIC_SPANS_DT)
-    for k in ("span_base", "n_spans", "n_rows", "n_client", "n_ident", "n_shared", "n_inline", "n_patches"):
+    for k in ("n_spans", "n_rows", "n_client", "n_ident", "n_shared", "n_inline", "n_patches"):
         assert (got[k] == host["topics"][k]).all(), k
-    assert r.n_spans == len(host["spans"]) and r.n_patches >= int(host["topics"]["n_patches"].sum())
+    # the same spans per topic (a one-sync device batch places topic t's at t * 64: the walk-fused
+    # desc's stride layout; host results are packed)
+    sb, ns = got["span_base"].astype(np.int64), got["n_spans"].astype(np.int64)
+    ext = int((sb + ns).max())
+    assert r.n_spans >= ext and r.n_patches >= int(host["topics"]["n_patches"].sum())
+    dsp = torch.empty(ext * 4, dtype=torch.int32, device="cuda")
+    assert hip.hipMemcpy(dsp.data_ptr(), r.spans, ext * 16, 3) == 0
+    dsp = dsp.cpu().numpy().view(np.uint32).reshape(-1, 4)
+    assert (dsp[E._ranges(sb, ns)] == host["spans"]).all()
 
 
-@pytest.mark.parametrize("dedup", [1, 0])
-def test_spans_device_digest_parity(dedup, gpu_available):
+@pytest.mark.parametrize("dedup,fuse", [(1, 1), (1, 0), (0, 1)])
+def test_spans_device_digest_parity(dedup, fuse, gpu_available):
     """mq_match_spans_device expanded as a device consumer would (spans, then per-topic patches or
     set-shared patches through the topic's merge rows, inline rows): per-topic digests equal the
     oracle's. With merge-set dedup (the default) topics share their merge set's patches
-    (MQ_TOPIC_SET_PATCHES); without it every topic holds its own."""
+    (MQ_TOPIC_SET_PATCHES); without it every topic holds its own. fuse: k_desc in the walk's
+    epilogue (the stride layout of one-sync batches, MQ_OPT_FUSE_DESC) or walk, scan, k_desc."""
     import torch
     from mqmatch import engine as E
     from mqmatch import workload as W
     w, eng, orc = _workload_pair(60000, 3000, seed=63)
     eng.set_option(E.OPT_MERGE_DEDUP, dedup)
+    eng.set_option(E.OPT_FUSE_DESC, fuse)
     tb, to = W.gen_topics(w, 6000, seed=64)
     n = len(to) - 1
     d_tb = torch.from_numpy(tb).cuda()
@@ -402,16 +412,20 @@ def test_spans_device_digest_parity(dedup, gpu_available):
     assert len(bad) == 0, f"{len(bad)} of {n} topics differ (first {bad[:5]})"
 
 
-def test_one_sync_batches_grow_and_repeat(gpu_available):
+@pytest.mark.parametrize("fuse", [0, 1])
+def test_one_sync_batches_grow_and_repeat(fuse, gpu_available):
     """One-sync batches (MQ_OPT_ONE_SYNC, the default for device results): buffers sized by
     earlier batches. A fresh index, a small batch, then a batch several times larger (its spans
     and patches do not fit what the small one left: it runs again, sized by the host), then the
     large batch again (fits: one synchronisation) and the small one: every result equals the
-    oracle's, and the profile counts exactly the runs that had to repeat."""
+    oracle's, and the profile counts exactly the runs that had to repeat. With k_desc fused into
+    the walk (MQ_OPT_FUSE_DESC, the default) the spans' stride layout is sized by the batch
+    itself, so only a gather-slot overflow repeats a run."""
     import torch
     from mqmatch import engine as E
     from mqmatch import workload as W
     w, eng, orc = _workload_pair(60000, 3000, seed=71)
+    eng.set_option(E.OPT_FUSE_DESC, fuse)
     eng.profile(True)
     batches = [W.gen_topics(w, k, seed=72 + i) for i, k in enumerate((300, 6000))]
     retried = []
@@ -428,9 +442,10 @@ def test_one_sync_batches_grow_and_repeat(gpu_available):
         dg, _ = engine_digests(E.expand_device_spans(r, n))
         od, _, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
         assert (dg == od).all()
-    # the first batch (nothing sized yet) and the first large one repeat; the others only for a
-    # slot overflow
-    assert [x[0] for x in retried] == [1, 1, int(retried[2][1]), int(retried[3][1])], retried
+    # unfused: the first batch (nothing sized yet) and the first large one repeat; the others
+    # only for a slot overflow
+    first = (1, 1) if not fuse else (int(retried[0][1]), int(retried[1][1]))
+    assert [x[0] for x in retried] == [*first, int(retried[2][1]), int(retried[3][1])], retried
 
 
 def test_spans_result_pins_host_image(gpu_available):

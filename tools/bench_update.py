@@ -104,6 +104,23 @@ def main():
     call_ns = (time.perf_counter() - t) / 100_000 * 1e9
     churn = []
     next_client = int(w["client_ids"].max()) + 1
+    step = None
+    if torch.cuda.is_available():
+        # one span-format match step of a fixed batch, clean and after each churn round (the
+        # image is updated in place: probe chains, pair lists and slabs must not degrade)
+        tb_, to_ = W.gen_topics(w, a.topics)
+        d_b = torch.from_numpy(tb_).cuda()
+        d_o = torch.from_numpy(to_.view(np.int64)).cuda()
+
+        def step(reps=5):
+            e.match_spans_device(d_b.data_ptr(), d_o.data_ptr(), len(to_) - 1)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(reps):
+                e.match_spans_device(d_b.data_ptr(), d_o.data_ptr(), len(to_) - 1)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t) / reps * 1e3
+        out["match_clean_ms_per_step"] = step()
     for k in (int(x) for x in a.churn.split(",") if x):
         k = min(k, n // 2)
         idx = rng.choice(n, k, replace=False)
@@ -129,22 +146,13 @@ def main():
         churn.append({"ops": k, "unsubscribed": int(removed),
                       "unsubscribe_per_s": k / tu, "unsubscribe_per_s_less_call": k / max(1e-9, tu - k * call_ns * 1e-9),
                       "subscribe_per_s": k / ts, "sync_ms": ms, "sync_bytes": nb,
-                      "sync_bytes_per_op": None if nb is None else nb / (2 * k)})
+                      "sync_bytes_per_op": None if nb is None else nb / (2 * k),
+                      "match_ms_per_step": step() if step else None})
     out["churn"] = churn
     out["ctypes_call_ns"] = call_ns
     e.check()
-    if torch.cuda.is_available():
-        # the image still matches: one span-format step
-        tb_, to_ = W.gen_topics(w, a.topics)
-        d_b = torch.from_numpy(tb_).cuda()
-        d_o = torch.from_numpy(to_.view(np.int64)).cuda()
-        e.match_spans_device(d_b.data_ptr(), d_o.data_ptr(), len(to_) - 1)
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        for _ in range(5):
-            e.match_spans_device(d_b.data_ptr(), d_o.data_ptr(), len(to_) - 1)
-        torch.cuda.synchronize()
-        out["match_after_churn_ms_per_step"] = (time.perf_counter() - t) / 5 * 1e3
+    if step:
+        out["match_after_churn_ms_per_step"] = churn[-1]["match_ms_per_step"] if churn else step()
     e.close()
     del w
 

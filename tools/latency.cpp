@@ -7,6 +7,10 @@
 //           ticket is ready (p50 / p99), throughput, batches formed, and the recipients per
 //           topic of the views read (one in 64: the fan-out reads them on the connection
 //           goroutines, not on the submitting thread)
+//   open    PublishViewBatcher(max_batch = 16k) under an open-loop offered load (publishes
+//           arriving at a fixed rate, as at a broker, whatever the stage's latency): 64 submitters
+//           each submit on their share of the schedule; latency from each Submit until its batch
+//           completed (p50 / p99), achieved rate, batches formed
 // Prints one JSON object per line. Built by mqtt-server_amd/Makefile (build/latency).
 #include <algorithm>
 #include <chrono>
@@ -87,6 +91,70 @@ int main(int argc, char** argv) {
   mqgen_batch_free(tb);
   mqgen_subs_free(g);
   (void)ix.Subscribers_(topics[0]);  // first sync
+
+  // open loop: offered rates (topics/s) at max_batch 16k
+  auto open_loop = [&](double rate, size_t B) {
+    mq::host::PublishViewBatcher pb(ix, B, std::chrono::microseconds(200), std::min<size_t>(B, 1024));
+    using Ticket = mq::host::PublishViewBatcher::Ticket;
+    std::vector<std::vector<double>> wl(kSubmitters);
+    std::vector<uint64_t> done(kSubmitters, 0);
+    std::atomic<bool> stop{false};
+    const auto b0 = Clock::now() + std::chrono::milliseconds(5);
+    const double period = kSubmitters / rate;  // seconds between one submitter's topics
+    std::vector<std::thread> th;
+    for (int w = 0; w < kSubmitters; w++)
+      th.emplace_back([&, w] {
+        std::deque<std::pair<Clock::time_point, Ticket>> q;
+        size_t at_w = (size_t)w * 9973;
+        uint64_t k = 0;
+        auto harvest = [&](bool all) {
+          while (!q.empty() && (all || q.front().second.ready())) {
+            q.front().second.wait();
+            wl[w].push_back(std::chrono::duration<double, std::micro>(q.front().second.done_at() - q.front().first).count());
+            q.pop_front();
+            done[w]++;
+          }
+        };
+        while (!stop) {
+          const auto now = Clock::now();
+          // every topic due by now (the schedule, not this thread's wake-ups, sets the load)
+          while (!stop) {
+            const auto due = b0 + std::chrono::duration_cast<Clock::duration>(
+                                      std::chrono::duration<double>((k + (double)w / kSubmitters) * period));
+            if (due > now) break;
+            q.emplace_back(Clock::now(), pb.Submit(topics[at_w % topics.size()]));
+            at_w += 7;
+            k++;
+          }
+          harvest(false);
+          std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        harvest(true);
+      });
+    std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+    stop = true;
+    for (auto& t : th) t.join();
+    const double bt = std::chrono::duration<double>(Clock::now() - b0).count();
+    const auto st = pb.stats();
+    std::vector<double> all;
+    uint64_t n_done = 0;
+    for (int w = 0; w < kSubmitters; w++) {
+      all.insert(all.end(), wl[w].begin(), wl[w].end());
+      n_done += done[w];
+    }
+    const double w50 = pct(all, 0.50), w99 = pct(all, 0.99);
+    std::printf("{\"path\": \"PublishViewBatcher open loop\", \"offered_per_s\": %.0f, \"max_batch\": %zu, "
+                "\"submitters\": %d, \"topics\": %llu, \"topics_per_s\": %.0f, \"p50_us\": %.1f, \"p99_us\": %.1f, "
+                "\"mean_batch\": %.1f, \"largest_batch\": %llu, \"dispatcher_ms_per_batch\": {\"wait\": %.3f, "
+                "\"seal\": %.3f, \"match\": %.3f, \"complete\": %.3f}}\n",
+                rate, B, kSubmitters, (unsigned long long)n_done, n_done / bt, w50, w99,
+                (double)st.topics / std::max<uint64_t>(st.batches, 1), (unsigned long long)st.largest,
+                st.wait_ns / 1e6 / std::max<uint64_t>(st.batches, 1), st.seal_ns / 1e6 / std::max<uint64_t>(st.batches, 1),
+                st.match_ns / 1e6 / std::max<uint64_t>(st.batches, 1),
+                st.complete_ns / 1e6 / std::max<uint64_t>(st.batches, 1));
+    std::fflush(stdout);
+  };
+  for (const double rate : {1e6, 2e6, 5e6, 10e6}) open_loop(rate, 16384);
 
   for (const size_t B : {(size_t)1, (size_t)64, (size_t)1024, (size_t)16384, (size_t)65536}) {
     // match: one call per batch
