@@ -137,7 +137,8 @@ def read_walk_traffic(path, n_subs, n_topics):
         with open(path) as f:
             e = json.load(f).get("walk", {}).get(str(n_subs))
         if (e is None or int(e["topics"]) != n_topics or int(e.get("edge_load", 2)) != engine_option(13, 4)
-                or int(e.get("walk_group", 0)) != engine_option(15, 16)):
+                or int(e.get("walk_group", 0)) != engine_option(15, 16)
+                or int(e.get("fused_desc", 0)) != engine_option(17, 1)):
             return None
         return float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError, TypeError):
@@ -145,20 +146,29 @@ def read_walk_traffic(path, n_subs, n_topics):
 
 
 def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step):
-    """Roofline of k_walk (the match walk, thread per topic). Its algorithmic bytes per topic are
-    SURVEY.md §8(d)'s walk terms, 8·L + 4 + 16·P (L levels, P child lookups of the reference's
-    DFS, counted exactly by the oracle on a sample of the batch), plus the 4-byte gather word it
-    writes per gathered particle; over its mean launch time from HIP events in the timed region.
-    Dependent probes of a 2 GB edge table: bound by random-access latency and request rate, far
+    """Roofline of the match walk, k_walkf (16 lanes per topic), with k_desc fused into its
+    epilogue (the default for device results, MQ_OPT_FUSE_DESC). Its algorithmic bytes per topic
+    are SURVEY.md §8(d)'s walk terms, 8·L + 4 + 16·P (L levels, P child lookups of the
+    reference's DFS, counted exactly by the oracle on a sample of the batch), plus the desc's:
+    per gathered particle its 32 B list record and 16 B pair-block header read and its 16 B span
+    written, per topic 32 B of counts and signature (the merge lists' 16 B per merge gather are not
+    counted: an understatement). Unfused (MQ_OPT_FUSE_DESC 0): the walk terms plus the 4 B gather
+    word per gathered particle. Over its mean launch time from HIP events in the timed region.
+    Dependent probes of a 4 GB edge table: bound by random-access latency and request rate, far
     below streaming bandwidth."""
     launches, ms = prof.get("walk", (0, 0.0))
+    fused = engine_option(17, 1) != 0 and "desc" not in prof
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-            "traffic": None, "kernel": "k_walkf (frontier walk, 16 lanes per topic, count pass)",
-            "bytes": "8 B per level + 4 B offset + 16 B per child lookup (SURVEY 8d: 8L + 4 + 16P) + 4 B per gather word"}
+            "traffic": None,
+            "kernel": "k_walkf (frontier walk, 16 lanes per topic) + k_desc fused" if fused
+                      else "k_walkf (frontier walk, 16 lanes per topic, count pass)",
+            "bytes": ("8 B per level + 4 B offset + 16 B per child lookup (SURVEY 8d: 8L + 4 + 16P) + 64 B per "
+                      "gathered particle (list record, pair header, span) + 32 B per topic") if fused else
+                     "8 B per level + 4 B offset + 16 B per child lookup (SURVEY 8d: 8L + 4 + 16P) + 4 B per gather word"}
     if not launches or ms <= 0 or per_topic is None:
         return roof
     b_topic = 8 * per_topic["L"] + 4 + 16 * per_topic["P"]
-    per_launch = b_topic * n + 4 * gathers_per_step
+    per_launch = (b_topic + 32) * n + 64 * gathers_per_step if fused else b_topic * n + 4 * gathers_per_step
     launch_ms = ms / launches
     achieved = per_launch / (launch_ms * 1e-3) / 1e9
     traffic = read_walk_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n)
@@ -555,10 +565,16 @@ def main():
             t0 = time.perf_counter()
             _, nrows = eng.match_spans_host(tb, to[:ne + 1], expand=True)
             dtx = time.perf_counter() - t0
+            th = host_cores()
+            t0 = time.perf_counter()
+            _, nrows_n = eng.match_spans_host(tb, to[:ne + 1], expand=True, threads=th, block=256)
+            dtn = time.perf_counter() - t0
             out["end_to_end"] = {"value": ne / dt, "unit": "publishes/s", "sample_topics": ne,
-                                 "result_bytes": nbytes, "GBps_to_host": nbytes / dt / 1e9,
+                                 "result_bytes": nbytes, "bytes_per_topic": nbytes / ne, "GBps_to_host": nbytes / dt / 1e9,
                                  "expanded": {"value": ne / dtx, "rows": nrows, "host_threads": 1,
-                                              "rows_GBps": 16 * nrows / dtx / 1e9}}
+                                              "rows_GBps": 16 * nrows / dtx / 1e9},
+                                 "expanded_threads": {"value": ne / dtn, "rows": nrows_n, "host_threads": th,
+                                                      "rows_GBps": 16 * nrows_n / dtn / 1e9}}
         else:
             ne = min(n, 20000)
             eng.match_batch_rows(tb, to[:ne + 1])

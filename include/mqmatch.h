@@ -324,7 +324,10 @@ int mq_match_spans(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* of
 /* Device-resident span format (inputs in HBM, enqueued on hip_stream, as mq_match_device). All
  * pointers in *out are DEVICE pointers owned by the index, valid until its next update or match
  * call. The whole batch is one result (no chunks); the call returns after the batch's kernels
- * have completed, with their guard flags checked (MQ_EIO when one tripped). */
+ * have completed, with their guard flags checked (MQ_EIO when one tripped). A topic's spans are
+ * spans[span_base, + n_spans): topics' ranges may have gaps between them (a batch run with one
+ * host synchronisation places topic t's at t * 64), and n_spans of the result is the array's
+ * extent. */
 int mq_match_spans_device(mq_index* idx, const uint8_t* d_topic_bytes, const uint64_t* d_offsets,
                           uint32_t n, void* hip_stream, mq_span_result* out);
 /* Materialise the rows of topics [first, first + count) of a HOST span result (mq_match_spans):

@@ -29,6 +29,9 @@
 #define MQ_OPT_SET_EXP 18         /* attribution experiments on the merge set pass (results WRONG; timing only):
                                      bit 0 no partner links, bit 1 links loaded but not looked up, bit 2 no
                                      patch stores, bit 3 no binary search for a record's hit list */
+#define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than
+                                     kMsgExportMin particles to work items any wavefront takes; > 1: that
+                                     threshold; 0: the filter's wavefront walks it alone */
 #define MQ_OPT_FUSE_DESC 17       /* one-sync span batches: 1 (default) runs k_desc in the frontier walk's
                                      epilogue (spans and merge lists at t * 64, no scan); 0: walk, scan, k_desc */
 

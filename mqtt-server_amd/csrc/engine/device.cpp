@@ -257,6 +257,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_ONE_SYNC: one_sync_ = v != 0; return true;
     case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
     case MQ_OPT_SET_EXP: set_exp_ = (uint32_t)v; return true;
+    case MQ_OPT_MSG_EXPORT: msg_export_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_GROUP:
       if (v != 0 && v != 4 && v != 8 && v != 16) return false;
       walk_group_ = (uint32_t)v;
@@ -878,21 +879,19 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   pinned(sizeof(TopicOff) + 2 * sizeof(uint32_t));
   TopicOff* h_tot = static_cast<TopicOff*>(h_pin_);
   uint32_t* h_ovf = reinterpret_cast<uint32_t*>(h_tot + 1);
-  hip_check(hipMemsetAsync(ovf_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
+  if (!one_sync) hip_check(hipMemsetAsync(ovf_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(ovf)");
   const bool front = walk_group_ != 0;
   if (front) {
     grow(fb_list_, (size_t)n * sizeof(uint32_t));
     grow(fb_cnt_, sizeof(uint32_t));
-    hip_check(hipMemsetAsync(fb_cnt_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(fb)");
-  }
+    if (!one_sync) hip_check(hipMemsetAsync(fb_cnt_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(fb)");
+  }  // (one-sync batches: zeroed by spans_begin's k_reset)
   prof.begin(s);
   if (fused) {  // one-sync batch, k_desc in the walk's epilogue: no scan (the dedup totals the gathers)
     launch_walk_desc(walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(), ovf_.as<uint32_t>(),
                      fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, *fused, s);
     prof.end("walk", s);
     hip_check(hipGetLastError(), "k_walkf<desc>");
-    hip_check(hipMemcpyAsync(&h_fast_->ovf, ovf_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H overflow");
-    hip_check(hipMemcpyAsync(&h_fast_->fallback, fb_cnt_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
     *gathers = gslots_.as<uint32_t>();
     *gstride = kGatherCap;
     prof.count("topics", n);
@@ -910,11 +909,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
   prof.end("scan", s);
   hip_check(hipGetLastError(), "k_scan");
-  if (one_sync) {  // read at the batch's end; the gather slots are the gather lists
-    hip_check(hipMemcpyAsync(&h_fast_->tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s),
-              "D2H totals");
-    hip_check(hipMemcpyAsync(&h_fast_->ovf, ovf_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H overflow");
-    if (front) hip_check(hipMemcpyAsync(&h_fast_->fallback, fb_cnt_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+  if (one_sync) {  // read at the batch's end (k_readback); the gather slots are the gather lists
     *gathers = gslots_.as<uint32_t>();
     *gstride = kGatherCap;
     prof.count("topics", n);
@@ -977,10 +972,38 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   // not sharded, without inline rows or a device share pick (whose buffers the walk's totals size)
   one_sync = one_sync && !ix.sharded() && !lists && dedup_ != 0 && set_grid_;
   if (one_sync) {
-    if (!h_fast_) h_fast_ = static_cast<FastBack*>(pinned_alloc(sizeof(FastBack)));
+    if (!h_fast_) {
+      h_fast_ = static_cast<FastBack*>(pinned_alloc(sizeof(FastBack)));
+      void* dp = nullptr;
+      hip_check(hipHostGetDevicePointer(&dp, h_fast_, 0), "hipHostGetDevicePointer");
+      d_fast_ = static_cast<FastBack*>(dp);
+    }
     if (!unsafe_.p) unsafe_.ensure(sizeof(uint32_t));
     memset(h_fast_, 0, sizeof(FastBack));
-    hip_check(hipMemsetAsync(unsafe_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(unsafe)");
+    // every counter of the batch, zeroed by one launch (k_reset): sized here, before the walk
+    grow(counts_, (size_t)n * sizeof(TopicCount));
+    grow(ovf_, sizeof(uint32_t));
+    grow(fb_cnt_, sizeof(uint32_t));
+    uint64_t slots = 1024;
+    while (slots < 2ull * n) slots <<= 1;
+    grow(dd_keys_, slots * sizeof(unsigned long long));
+    if (!dd_nsets_.p) dd_nsets_.ensure(3 * sizeof(unsigned long long));
+    if (!dd_spcount_.p) dd_spcount_.ensure(kPatchRegions * sizeof(unsigned long long));
+    if (!sp_pcount_.p) sp_pcount_.ensure(kPatchRegions * sizeof(unsigned long long));
+    if (!dd_nwave_.p) dd_nwave_.ensure(sizeof(unsigned long long));
+    ResetArgs ra;
+    memset(&ra, 0, sizeof(ra));
+    void* ps[] = {unsafe_.p, ovf_.p, fb_cnt_.p, dd_nsets_.p, dd_spcount_.p, sp_pcount_.p, dd_nwave_.p};
+    const uint32_t bs[] = {4, 4, 4, 3 * 8, kPatchRegions * 8, kPatchRegions * 8, 8};
+    ra.n = 7;
+    for (uint32_t k = 0; k < ra.n; k++) {
+      ra.p[k] = ps[k];
+      ra.bytes[k] = bs[k];
+    }
+    ra.big = dd_keys_.as<unsigned long long>();
+    ra.big_words = slots;
+    launch_reset(ra, s);
+    hip_check(hipGetLastError(), "k_reset");
   } else {
     check_err(s);  // faults flagged by an earlier row-format batch (one-sync batches read it at their end)
   }
@@ -1146,9 +1169,10 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     grow(dd_rep_, (size_t)n * sizeof(uint32_t));
     grow(dd_rlist_, (size_t)n * sizeof(uint32_t));
     if (!dd_nsets_.p) dd_nsets_.ensure(3 * sizeof(unsigned long long));
-    hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
-
-    hip_check(hipMemsetAsync(dd_nsets_.p, 0, 3 * sizeof(unsigned long long), s), "memset");
+    if (!one_sync) {  // (one-sync batches: zeroed by spans_begin's k_reset)
+      hip_check(hipMemsetAsync(dd_keys_.p, 0, slots * sizeof(unsigned long long), s), "memset");
+      hip_check(hipMemsetAsync(dd_nsets_.p, 0, 3 * sizeof(unsigned long long), s), "memset");
+    }
     DedupArgs dd;
     memset(&dd, 0, sizeof(dd));
     dd.n = n;
@@ -1194,8 +1218,6 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipGetLastError(), "k_dedup");
     sb_.n_sets = 0;
     if (one_sync) {  // the set count is read at the batch's end; the set pass strides over it
-      hip_check(hipMemcpyAsync(h_fast_->n_sets, dd_nsets_.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
-                "D2H");
       // the grid: the last batch's count with room (the set pass strides over the true count);
       // with none yet, as many waves as topics (an unused one exits at once)
       sb_.n_sets = last_sets_ ? last_sets_ + last_sets_ / 8 + 256 : n;
@@ -1275,7 +1297,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     for (int attempt = 0;; attempt++) {
       a.spatches = dd_spatches_.as<PatchRec>();
       a.srcap = srcap_;
-      hip_check(hipMemsetAsync(a.spcount, 0, kPatchRegions * sizeof(unsigned long long), s), "memset");
+      if (!one_sync) hip_check(hipMemsetAsync(a.spcount, 0, kPatchRegions * sizeof(unsigned long long), s), "memset");
       if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
       prof.begin(s);
       // persistent: the waves stride over the representative list (its length is on the device)
@@ -1318,7 +1340,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (a.set_ref) {  // results that need no wavefront: k_finish, thread per topic
       grow(dd_wlist_, (size_t)n * sizeof(uint32_t));
       if (!dd_nwave_.p) dd_nwave_.ensure(sizeof(unsigned long long));
-      hip_check(hipMemsetAsync(dd_nwave_.p, 0, sizeof(unsigned long long), s), "memset");
+      if (!one_sync) hip_check(hipMemsetAsync(dd_nwave_.p, 0, sizeof(unsigned long long), s), "memset");
       FinishArgs fa;
       fa.n = n;
       fa.off = a.off;
@@ -1341,7 +1363,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   for (int attempt = 0;; attempt++) {
     a.patches = sp_patches_.as<PatchRec>();
     a.rcap = rcap_;
-    hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
+    if (!one_sync)
+      hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
     if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
     prof.begin(s);
     // after k_finish the waves stride over its list (its length is on the device)
@@ -1383,8 +1406,16 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipGetLastError(), "k_pick<spans>");
   }
   if (one_sync) {  // the batch's one synchronisation: totals, overflow, unsafe bits, errors
-    hip_check(hipMemcpyAsync(&h_fast_->unsafe, unsafe_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
-    hip_check(hipMemcpyAsync(&h_fast_->err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
+    ReadbackArgs rb;
+    rb.tot = sb_.fused ? nullptr : bpre_.as<TopicOff>() + (n + kScanBlock - 1) / kScanBlock;
+    rb.ovf = ovf_.as<uint32_t>();
+    rb.fallback = walk_group_ ? fb_cnt_.as<uint32_t>() : nullptr;
+    rb.unsafe = unsafe_.as<uint32_t>();
+    rb.err = err_.as<uint32_t>();
+    rb.n_sets = sb_.dedup ? dd_nsets_.as<unsigned long long>() : nullptr;
+    rb.out = d_fast_;
+    launch_readback(rb, s);
+    hip_check(hipGetLastError(), "k_readback");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     if (h_fast_->err) check_err(s);  // throws with the tripped guard's name
     if (h_fast_->ovf || h_fast_->unsafe) {
@@ -1606,6 +1637,8 @@ MsgImg Device::msg_img() const {
   m.h = img_h_.as<uint64_t>();
   m.n = img_n_;
   m.n_pos = img_n_pos_;
+  m.cyc = nullptr;
+  m.work = nullptr;
   return m;
 }
 
@@ -1613,8 +1646,14 @@ MsgImg Device::msg_img() const {
 // fan-out nesting exceeded kMsgStack: the batch then takes the particle walk.
 bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
                           hipStream_t s, TopicOff* tot) {
-  const MsgImg img = msg_img();
+  MsgImg img = msg_img();
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+  if (prof.work()) {  // MQ_PROF_WORK: per-filter clocks and fan-out work of the count pass
+    grow(msg_cyc_, (size_t)n * sizeof(uint32_t) + 4 * sizeof(unsigned long long));
+    img.work = reinterpret_cast<unsigned long long*>(msg_cyc_.p);
+    img.cyc = reinterpret_cast<uint32_t*>(img.work + 4);
+    hip_check(hipMemsetAsync(msg_cyc_.p, 0, (size_t)n * sizeof(uint32_t) + 4 * sizeof(unsigned long long), s), "memset");
+  }
   // One walk per filter: the count pass records each filter's runs (up to run_cap of them, from
   // the speculative-scratch budget) and the second pass places them; a filter with more runs
   // walks again in the second pass. Without the budget: count walk, then fill walk.
@@ -1626,10 +1665,33 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
   }
   MsgRun* d_runs = runs ? msg_runs_.as<MsgRun>() : nullptr;
   uint32_t* d_nruns = runs ? msg_nruns_.as<uint32_t>() : nullptr;
+  // wide filters: the count pass exports a fan-out of more than kMsgExportMin particles as work
+  // items that every wavefront of the grid can take (recorded-runs passes only)
+  MsgWide wide;
+  memset(&wide, 0, sizeof(wide));
+  const bool exp = runs && msg_export_ != 0;
+  if (exp) {
+    msg_wq_.ensure(kMsgWorkCap * sizeof(MsgWork) + sizeof(uint32_t));
+    wide.items = msg_wq_.as<MsgWork>();
+    wide.n_items = reinterpret_cast<uint32_t*>(wide.items + kMsgWorkCap);
+    wide.cap = kMsgWorkCap;
+    wide.min_tot = msg_export_ > 1 ? msg_export_ : kMsgExportMin;
+    msg_wscratch_.ensure((size_t)n_cus_ * 8 * 4 * kMsgWideRuns * sizeof(MsgRun));
+    wide.scratch = msg_wscratch_.as<MsgRun>();
+    wide.per_wave = kMsgWideRuns;
+    hip_check(hipMemsetAsync(wide.n_items, 0, sizeof(uint32_t), s), "hipMemsetAsync(n_items)");
+  }
+  const uint32_t wide_blocks = n_cus_ * 8;
   prof.begin(s);
   launch_msgq(runs ? kMsgRuns : kMsgCount, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), nullptr, nullptr,
-              nullptr, nullptr, nullptr, d_runs, run_cap, d_nruns, s);
+              nullptr, nullptr, nullptr, d_runs, run_cap, d_nruns, wide, wide_blocks, s);
   prof.end("msgq_count", s);
+  if (exp) {  // the exported items' counts
+    prof.begin(s);
+    launch_msgq(kMsgWideCount, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr,
+                nullptr, d_runs, run_cap, d_nruns, wide, wide_blocks, s);
+    prof.end("msgq_wide_count", s);
+  }
   hip_check(hipGetLastError(), "k_msgq<count>");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
   hip_check(hipGetLastError(), "k_scan");
@@ -1642,6 +1704,26 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
     return false;
   }
   check_err(s);
+  if (img.work) {  // the count pass's cost over the filters: total, max, heaviest 1 % and 0.1 %
+    std::vector<uint32_t> c(n);
+    unsigned long long w[4];
+    hip_check(hipMemcpy(w, img.work, sizeof(w), hipMemcpyDeviceToHost), "D2H");
+    hip_check(hipMemcpy(c.data(), img.cyc, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost), "D2H");
+    std::sort(c.begin(), c.end(), std::greater<uint32_t>());
+    uint64_t tot_c = 0, top1 = 0, top01 = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      tot_c += c[i];
+      if (i < n / 100) top1 += c[i];
+      if (i < n / 1000) top01 += c[i];
+    }
+    prof.count("msg_cyc16_total", tot_c);
+    prof.count("msg_cyc16_max", n ? c[0] : 0);
+    prof.count("msg_cyc16_top1pct", top1);
+    prof.count("msg_cyc16_top01pct", top01);
+    prof.count("msg_fanout_lookups", w[0]);
+    prof.count("msg_lane_walk_filters", w[1]);
+    prof.count("msg_lane_walk_particles", w[2]);
+  }
   msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
   msg_base_.ensure((size_t)n * sizeof(uint64_t));
   msg_count_.ensure((size_t)n * sizeof(uint32_t));
@@ -1649,8 +1731,15 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
   prof.begin(s);
   launch_msgq(runs ? kMsgPlace : kMsgFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
               msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
-              msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, s);
+              msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
   prof.end("msgq_fill", s);
+  if (exp) {
+    prof.begin(s);
+    launch_msgq(kMsgWideFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
+                msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
+                msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
+    prof.end("msgq_wide_fill", s);
+  }
   hip_check(hipGetLastError(), "k_msgq<fill>");
   prof.begin(s);
   launch_msg_copy(msg_pieces_.as<MsgPiece>(), tot->g, img.h, msg_handles_.as<uint64_t>(), s);

@@ -297,12 +297,9 @@ class Device {
   } sb_;
   // one-sync batches: values read back at the batch's end (pinned): the walk's totals, its
   // overflow and fallback counts, the *unsafe bits, the error word and the merge-set counts
-  struct FastBack {
-    TopicOff tot;
-    uint32_t ovf, fallback, unsafe, err;
-    unsigned long long n_sets[3];  // merge sets (heavy, light), the batch's gathers (walk-fused desc)
-  };
+  using FastBack = FastBackRec;     // (kernels.h: k_readback writes it)
   FastBack* h_fast_ = nullptr;
+  FastBack* d_fast_ = nullptr;      // its device view
   DevBuf unsafe_;
   bool one_sync_ = true;      // MQ_OPT_ONE_SYNC
   bool fuse_desc_ = true;     // MQ_OPT_FUSE_DESC
@@ -333,6 +330,10 @@ class Device {
   DevBuf dd_mpair_;                            // k_desc: merge gathers' pair-block headers
   DevBuf dd_mrank_;                            // ... and rank keys (sharded index)
   DevBuf dd_fcnt_;                             // k_xsig: cross-shard entries per topic
+  DevBuf msg_wq_;                              // Messages: exported work items of wide filters (+ count)
+  DevBuf msg_wscratch_;                        // ... the runs their count recorded (per wavefront)
+  uint32_t msg_export_ = 1;                    // MQ_OPT_MSG_EXPORT (0 off, 1 kMsgExportMin, else the threshold)
+  DevBuf msg_cyc_;                             // MQ_PROF_WORK: Messages count-pass clocks per filter
   DevBuf set_rec_;                             // MQ_PROF_WORK: records resolved per merge set
   uint64_t srcap_ = 0;                         // set patches per region of dd_spatches_
   uint32_t copy_blocks_ = 0, merge_blocks_ = 0;  // persistent k_copy / k_merge grids (workgroups)

@@ -409,6 +409,11 @@ struct MsgImg {
   const uint32_t* lp;    // image position -> live particles before it in the image (n + 1)
   const uint64_t* h;     // live handles in image order
   uint32_t n, n_pos;
+  // MQ_PROF_WORK (null: off): the count pass's clocks per filter (shader clocks >> 4, saturated)
+  // and work counters: [0] fan-out lookups (particles probed level by level), [1] filters whose
+  // frontier outgrew LDS (per-lane walk), [2] particles those walked per lane
+  uint32_t* cyc;
+  unsigned long long* work;
 };
 // A run of h copied to the output: out[dst + k] = h[h0 + k], k < len.
 struct MsgPiece {
@@ -453,11 +458,63 @@ constexpr uint32_t kMsgRunCap = 256;  // runs recorded per filter (more: the fil
 //   kMsgRuns   as kMsgCount, and the filter's runs recorded (runs[t * run_cap ..], n_runs[t];
 //              kNone: more than run_cap runs)
 //   kMsgPlace  as kMsgFill, from the recorded runs without walking (a filter without them walks)
-enum MsgMode : int { kMsgCount = 0, kMsgFill = 1, kMsgRuns = 2, kMsgPlace = 3 };
+//   kMsgWideCount / kMsgWideFill  the work items a kMsgRuns pass exported (MsgWide): a wavefront
+//              per item walks its particles lane by lane; the count records the item's runs (in
+//              its wavefront's scratch) and adds its handles and pieces to its filter's counts (one
+//              atomic each on cnt[t], after the count pass), which gives where they start; the fill
+//              places the recorded runs from there (an item whose runs did not fit walks again)
+enum MsgMode : int { kMsgCount = 0, kMsgFill = 1, kMsgRuns = 2, kMsgPlace = 3, kMsgWideCount = 4, kMsgWideFill = 5 };
+// Wide filters (a literal segment under a fan-out of more than min_tot particles): the count
+// pass (kMsgRuns) exports the fan-out's runs as work items of at most kMsgChunk particles and
+// stops walking the filter (cnt[t].shared = 1 marks it; a kMsgFill walk of the filter stops at the
+// same place), so one heavy filter spreads over the grid instead of holding one wavefront while
+// the rest of the batch has long finished (10M retained: the heaviest filter took 1.8 ms of a
+// 3.2 ms count pass).
+struct MsgWork {  // filter t: particles [x, y) of a fan-out, to take the filter from byte s on
+  uint32_t t, x, y, s;
+  // the count's answers: where the item's handles and pieces start in its filter's output, and its
+  // runs recorded in the scratch (run_off, n_runs; kNone: they did not fit, the fill walks again)
+  uint32_t dst, pslot, run_off, n_runs;
+};
+struct MsgWide {
+  MsgWork* items;
+  uint32_t cap, min_tot;  // min_tot 0: no export
+  uint32_t* n_items;      // items reserved (a reservation past cap fails: that filter walks alone)
+  MsgRun* scratch;        // the counting wavefronts' recorded runs: wavefront w's at [w * per_wave, ...)
+  uint32_t per_wave;
+};
+constexpr uint32_t kMsgChunk = 256;       // particles per exported work item
+constexpr uint32_t kMsgWorkCap = 1u << 20;  // work items per batch (32 MB)
+constexpr uint32_t kMsgWideRuns = 4096;     // recorded runs per wide-count wavefront (64 KB each)
+constexpr uint32_t kMsgExportMin = 512;   // export a literal level under a fan-out of more particles (10M: 2048 -> 512, 2.75 -> 2.50 ms)
 void launch_msgq(int mode, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                  const MsgImg& img, TopicCount* cnt, const TopicOff* off, MsgPiece* pieces,
                  uint64_t* handles, uint64_t* base, uint32_t* count, MsgRun* runs, uint32_t run_cap,
-                 uint32_t* n_runs, hipStream_t s);
+                 uint32_t* n_runs, const MsgWide& w, uint32_t wide_blocks, hipStream_t s);
+// One-sync span batches: every counter the batch's kernels accumulate into is zeroed by one
+// launch at its start (small arrays by block 0, `big` grid-stride), and what the host reads at its
+// end is gathered by one thread into the pinned FastBack record (no fill or copy commands on the
+// stream: each cost a few microseconds of its own).
+struct ResetArgs {
+  void* p[8];
+  uint32_t bytes[8];  // multiples of 4
+  uint32_t n;
+  unsigned long long* big;
+  uint64_t big_words;
+};
+void launch_reset(const ResetArgs& a, hipStream_t s);
+struct FastBackRec {  // == Device::FastBack
+  TopicOff tot;
+  uint32_t ovf, fallback, unsafe, err;
+  unsigned long long n_sets[3];
+};
+struct ReadbackArgs {
+  const TopicOff* tot;  // null: not read (the walk-fused desc has no scan)
+  const uint32_t *ovf, *fallback, *unsafe, *err;
+  const unsigned long long* n_sets;  // null: not read
+  FastBackRec* out;                  // device view of the pinned record
+};
+void launch_readback(const ReadbackArgs& a, hipStream_t s);
 void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s);
 
 }  // namespace mq

@@ -2851,17 +2851,24 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
                                               MsgPiece* __restrict__ pieces, uint64_t* __restrict__ handles,
                                               uint64_t* __restrict__ base_out, uint32_t* __restrict__ count_out,
                                               MsgRun* __restrict__ runs, uint32_t run_cap,
-                                              uint32_t* __restrict__ n_runs) {
-  constexpr bool FILL = MODE == kMsgFill || MODE == kMsgPlace;  // the walk writes output
+                                              uint32_t* __restrict__ n_runs, MsgWide w) {
+  constexpr bool WIDE = MODE == kMsgWideCount || MODE == kMsgWideFill;  // exported work items
+  constexpr bool FILL = MODE == kMsgFill || MODE == kMsgPlace || MODE == kMsgWideFill;  // the walk writes output
   constexpr bool RUNS = MODE == kMsgRuns;
   __shared__ uint32_t hcur[4], pcur[4], rcur[4];  // next handle / piece / run of the wave's filter
   __shared__ uint2 mfront[4][2][kMsgFront];       // fan-out frontier: runs of one level (two buffers)
   __shared__ uint32_t mpre[4][kMsgFront + 1];      // ... particles before each run
   const uint32_t lane = threadIdx.x & 63, wv = wave_id();
-  const uint32_t t = blockIdx.x * 4 + wv;
-  if (t >= n) return;  // wave-uniform
-  const uint64_t b0 = fo[t], b1 = fo[t + 1];
-  const uint64_t obase = FILL ? off[t].rows : 0, pbase = FILL ? off[t].g : 0;
+  uint32_t t = blockIdx.x * 4 + wv;  // (a work item's filter in the wide modes)
+  if (!WIDE && t >= n) return;  // wave-uniform
+  const uint64_t c_start = (!FILL && !WIDE && img.cyc) ? clock64() : 0ull;
+  uint64_t b0 = 0, b1 = 0, obase = 0, pbase = 0;
+  if (!WIDE) {
+    b0 = fo[t];
+    b1 = fo[t + 1];
+    obase = FILL ? off[t].rows : 0;
+    pbase = FILL ? off[t].g : 0;
+  }
   // one piece record per kMsgPiece handles of a long run
   auto put_pieces = [&](uint32_t h0, uint32_t len, uint32_t dst, uint32_t slot) __attribute__((always_inline)) {
     const uint32_t npc = (len + kMsgPiece - 1) / kMsgPiece;
@@ -2886,7 +2893,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       return;
     }
   }
-  if (FILL || RUNS) {
+  if (FILL || RUNS || WIDE) {
     if (lane == 0) hcur[wv] = pcur[wv] = rcur[wv] = 0;
     wave_sync_lds();
   }
@@ -2897,13 +2904,18 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
     if (!FILL) {
       nh += len;
       np += npc;
-      if (!RUNS) return;
+      if (!RUNS && MODE != kMsgWideCount) return;
     }
     const uint32_t dst = atomicAdd(&hcur[wv], len);
     const uint32_t slot = npc ? atomicAdd(&pcur[wv], npc) : 0u;
     if (RUNS) {
       const uint32_t ri = atomicAdd(&rcur[wv], 1u);
       if (ri < run_cap) runs[(uint64_t)t * run_cap + ri] = MsgRun{h0, len, dst, slot};
+      return;
+    }
+    if (MODE == kMsgWideCount) {  // into the wavefront's scratch (its cursor runs across items)
+      const uint32_t ri = atomicAdd(&rcur[wv], 1u);
+      if (ri < w.per_wave) w.scratch[(uint64_t)(blockIdx.x * 4 + wv) * w.per_wave + ri] = MsgRun{h0, len, dst, slot};
       return;
     }
     if (!npc) {
@@ -2928,14 +2940,120 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       y = ny;
     }
   };
+  ByteReader R(fb);
+  auto dfs_run = [&](uint32_t ra, uint32_t rb, uint64_t rs) __attribute__((always_inline)) {
+    MsgFrame st[kMsgStack];
+    for (uint32_t u = ra + lane; u < rb; u += 64) {
+      uint32_t sp = 0, ua = u, ub = u + 1;
+      uint64_t us = rs;
+      for (uint64_t guard = 0;; guard++) {
+        if (guard > kWalkGuard) {
+          atomicOr(ix.err, kErrWalkGuard);
+          break;
+        }
+        bool pop = false;
+        const uint64_t e = find_slash(R, us, b1);
+        const bool last = e >= b1;
+        const uint32_t len = (uint32_t)(e - us);
+        const uint32_t c0 = len == 1 ? R.at(us) : 0u;
+        if (c0 == '+' || c0 == '#') {
+          uint32_t x, y;
+          desc(ua, ub, x, y);
+          if (last) {
+            emit_final(c0 == '#', x, y);
+            pop = true;
+          } else {
+            ua = x;
+            ub = y;
+            us = e + 1;
+            pop = ua >= ub;
+          }
+        } else if (ub - ua > 1) {  // a literal under a run: one particle now, the rest later
+          if (sp == kMsgStack) {
+            atomicOr(ix.err, kErrMsgNest);
+            break;
+          }
+          st[sp++] = MsgFrame{ua + 1, ub, (uint32_t)(us - b0)};
+          ub = ua + 1;
+        } else {
+          SegKey key = key_of(R, us, e);
+          const uint32_t qc = img_pos(img, lookup(ix, img.node[ua], key, fb + us, len));
+          if (qc == kNone) {
+            pop = true;
+          } else if (last) {
+            emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+            pop = true;
+          } else {
+            ua = qc;
+            ub = qc + 1;
+            us = e + 1;
+          }
+        }
+        if (pop) {
+          if (sp == 0) break;
+          MsgFrame& f = st[sp - 1];
+          ua = f.cur;
+          ub = ua + 1;
+          us = b0 + f.s;
+          if (++f.cur >= f.end) sp--;
+        }
+      }
+    }
+  };
+  if (WIDE) {  // wavefront per exported item: its particles, lane by lane (dfs_run)
+    const uint32_t ni = min(*w.n_items, w.cap);
+    const uint32_t wbase = (blockIdx.x * 4 + wv) * w.per_wave;  // (wide count: this wavefront's scratch)
+    for (uint32_t i = blockIdx.x * 4 + wv; i < ni; i += gridDim.x * 4) {
+      const MsgWork it = w.items[i];
+      t = it.t;
+      b0 = fo[t];
+      b1 = fo[t + 1];
+      if (FILL && it.n_runs != kNone) {  // the count's runs, placed after the filter's own part
+        obase = off[t].rows + it.dst;
+        pbase = off[t].g + it.pslot;
+        for (uint32_t k = lane; k < it.n_runs; k += 64) {
+          const MsgRun r = w.scratch[(uint64_t)it.run_off + k];
+          if (r.len > kMsgDirect) put_pieces(r.h0, r.len, r.dst, r.pslot);
+          else
+            for (uint32_t j = 0; j < r.len; j++) handles[obase + r.dst + j] = img.h[r.h0 + j];
+        }
+        continue;
+      }
+      uint32_t r0 = 0;
+      if (lane == 0) {
+        if (FILL) {
+          hcur[wv] = it.dst;
+          pcur[wv] = it.pslot;
+        } else {
+          hcur[wv] = pcur[wv] = 0;
+          r0 = rcur[wv];
+        }
+      }
+      if (FILL) {
+        obase = off[t].rows;
+        pbase = off[t].g;
+      }
+      wave_sync_lds();
+      dfs_run(it.x, it.y, b0 + it.s);
+      wave_sync_lds();
+      if (!FILL && lane == 0) {  // the item's place in its filter's output: after the count pass's own part
+        const uint32_t r1 = rcur[wv];
+        w.items[i].dst = atomicAdd(&cnt[t].rows, hcur[wv]);
+        w.items[i].pslot = atomicAdd(&cnt[t].gathers, pcur[wv]);
+        w.items[i].run_off = wbase + r0;
+        w.items[i].n_runs = r1 <= w.per_wave ? r1 - r0 : kNone;
+      }
+    }
+    return;
+  }
+  bool exported = false;  // the count pass handed the filter's fan-out to work items (MsgWide)
   if (b1 > b0 && ix.retained_len != 0) {  // topics.go:535
-    ByteReader R(fb);
-    bool w = false;
+    bool wild = false;
     for (uint64_t i = b0 + lane; i < b1; i += 64) {
       const uint32_t ch = fb[i];
-      w |= (ch == '+') | (ch == '#');
+      wild |= (ch == '+') | (ch == '#');
     }
-    if (!__any(w)) {  // Retained.Get(filter) (topics.go:539-544)
+    if (!__any(wild)) {  // Retained.Get(filter) (topics.go:539-544)
       uint32_t node = kRoot;
       SegKey key;
       uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
@@ -2995,65 +3113,6 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         // A frontier that outgrows its LDS falls back, run by run, to the per-lane walk
         // (dfs_run: lanes take a run's particles, each walks the rest of the filter alone with
         // deeper fan-outs on a frame stack).
-        auto dfs_run = [&](uint32_t ra, uint32_t rb, uint64_t rs) __attribute__((always_inline)) {
-          MsgFrame st[kMsgStack];
-          for (uint32_t u = ra + lane; u < rb; u += 64) {
-            uint32_t sp = 0, ua = u, ub = u + 1;
-            uint64_t us = rs;
-            for (uint64_t guard = 0;; guard++) {
-              if (guard > kWalkGuard) {
-                atomicOr(ix.err, kErrWalkGuard);
-                break;
-              }
-              bool pop = false;
-              const uint64_t e = find_slash(R, us, b1);
-              const bool last = e >= b1;
-              const uint32_t len = (uint32_t)(e - us);
-              const uint32_t c0 = len == 1 ? R.at(us) : 0u;
-              if (c0 == '+' || c0 == '#') {
-                uint32_t x, y;
-                desc(ua, ub, x, y);
-                if (last) {
-                  emit_final(c0 == '#', x, y);
-                  pop = true;
-                } else {
-                  ua = x;
-                  ub = y;
-                  us = e + 1;
-                  pop = ua >= ub;
-                }
-              } else if (ub - ua > 1) {  // a literal under a run: one particle now, the rest later
-                if (sp == kMsgStack) {
-                  atomicOr(ix.err, kErrMsgNest);
-                  break;
-                }
-                st[sp++] = MsgFrame{ua + 1, ub, (uint32_t)(us - b0)};
-                ub = ua + 1;
-              } else {
-                SegKey key = key_of(R, us, e);
-                const uint32_t qc = img_pos(img, lookup(ix, img.node[ua], key, fb + us, len));
-                if (qc == kNone) {
-                  pop = true;
-                } else if (last) {
-                  emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
-                  pop = true;
-                } else {
-                  ua = qc;
-                  ub = qc + 1;
-                  us = e + 1;
-                }
-              }
-              if (pop) {
-                if (sp == 0) break;
-                MsgFrame& f = st[sp - 1];
-                ua = f.cur;
-                ub = ua + 1;
-                us = b0 + f.s;
-                if (++f.cur >= f.end) sp--;
-              }
-            }
-          }
-        };
         uint2* cur = mfront[wv][0];
         uint2* nxt = mfront[wv][1];
         uint32_t nr = 1;
@@ -3098,7 +3157,43 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
               tot += ct;
             }
             if (lane == 0) mpre[wv][nr] = tot;
+            if (!FILL && img.work && lane == 0) atomicAdd(img.work + 0, (unsigned long long)tot);
             wave_sync_lds();
+            if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && tot > w.min_tot) {
+              if (FILL) {  // the count pass exported from here: its items write the rest
+                if (cnt[t].shared) break;
+              } else {
+                // the runs as items of at most kMsgChunk particles (one reservation for all)
+                uint32_t nit = 0;
+                for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+                  const uint32_t r = r0 + lane;
+                  const uint32_t c = r < nr ? (cur[r].y - cur[r].x + kMsgChunk - 1) / kMsgChunk : 0u;
+                  nit += wave_sum(c);
+                }
+                uint32_t ib = 0;
+                if (lane == 0) ib = atomicAdd(w.n_items, nit);
+                ib = __shfl(ib, 0, 64);
+                if (ib + nit <= w.cap) {
+                  for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+                    const uint32_t r = r0 + lane;
+                    uint32_t x = 0, y = 0;
+                    if (r < nr) {
+                      x = cur[r].x;
+                      y = cur[r].y;
+                    }
+                    const uint32_t c = (y - x + kMsgChunk - 1) / kMsgChunk;
+                    uint32_t ct;
+                    const uint32_t ex = wave_excl_scan(c, lane, &ct);
+                    for (uint32_t k = 0; k < c; k++)
+                      w.items[ib + ex + k] = MsgWork{t, x + k * kMsgChunk, min(y, x + (k + 1) * kMsgChunk),
+                                                     (uint32_t)(ls - b0), 0u, 0u, 0u, kNone};
+                    ib += ct;
+                  }
+                  exported = true;
+                  break;
+                }  // (the queue is full: this filter walks alone, as a fill walk will)
+              }
+            }
             for (uint32_t p0 = 0; p0 < tot; p0 += 64) {
               const uint32_t p = p0 + lane;
               uint32_t qc = kNone;
@@ -3125,6 +3220,12 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
           }
           if (last) break;
           if (nn > kMsgFront) {  // too wide for LDS: the per-lane walk from this level
+            if (!FILL && img.work && lane == 0) {
+              uint32_t np = 0;
+              for (uint32_t r = 0; r < nr; r++) np += cur[r].y - cur[r].x;
+              atomicAdd(img.work + 1, 1ull);
+              atomicAdd(img.work + 2, (unsigned long long)np);
+            }
             for (uint32_t r = 0; r < nr; r++) {
               const uint2 ru = cur[r];
               dfs_run(ru.x, ru.y, ls);
@@ -3147,8 +3248,9 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
     np = wave_sum(np);
     if (RUNS) wave_sync_lds();  // every lane's run reservations are in rcur
     if (lane == 0) {
-      cnt[t] = TopicCount{np, nh, 0, 0, 0};
+      cnt[t] = TopicCount{np, nh, exported ? 1u : 0u, 0, 0};
       if (RUNS) n_runs[t] = rcur[wv] <= run_cap ? rcur[wv] : kNone;
+      if (img.cyc) img.cyc[t] = (uint32_t)min((clock64() - c_start) >> 4, 0xFFFFFFFFull);
     }
   } else if (lane == 0) {
     base_out[t] = obase;
@@ -3159,18 +3261,54 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
 void launch_msgq(int mode, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
                  const MsgImg& img, TopicCount* cnt, const TopicOff* off, MsgPiece* pieces,
                  uint64_t* handles, uint64_t* base, uint32_t* count, MsgRun* runs, uint32_t run_cap,
-                 uint32_t* n_runs, hipStream_t s) {
+                 uint32_t* n_runs, const MsgWide& w, uint32_t wide_blocks, hipStream_t s) {
   if (!n) return;
-  const dim3 g((n + 3) / 4), b(256);
+  // the wide modes: persistent wavefronts over the items (their number is on the device)
+  const dim3 g(mode == kMsgWideCount || mode == kMsgWideFill ? std::max(1u, wide_blocks) : (n + 3) / 4), b(256);
 #define MQ_MSGQ(M) \
-  hipLaunchKernelGGL(k_msgq<M>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count, runs, run_cap, n_runs)
+  hipLaunchKernelGGL(k_msgq<M>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count, runs, run_cap, \
+                     n_runs, w)
   switch (mode) {
     case kMsgCount: MQ_MSGQ(kMsgCount); break;
     case kMsgFill: MQ_MSGQ(kMsgFill); break;
     case kMsgRuns: MQ_MSGQ(kMsgRuns); break;
+    case kMsgWideCount: MQ_MSGQ(kMsgWideCount); break;
+    case kMsgWideFill: MQ_MSGQ(kMsgWideFill); break;
     default: MQ_MSGQ(kMsgPlace); break;
   }
 #undef MQ_MSGQ
+}
+
+__global__ __launch_bounds__(256) void k_reset(ResetArgs a) {
+  if (blockIdx.x == 0)
+    for (uint32_t k = 0; k < a.n; k++) {
+      uint32_t* p = static_cast<uint32_t*>(a.p[k]);
+      for (uint32_t i = threadIdx.x; i < a.bytes[k] / 4; i += blockDim.x) p[i] = 0u;
+    }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.big_words; i += (uint64_t)gridDim.x * blockDim.x)
+    a.big[i] = 0ull;
+}
+
+void launch_reset(const ResetArgs& a, hipStream_t s) {
+  const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>(1, (a.big_words + 255) / 256), 2048);
+  hipLaunchKernelGGL(k_reset, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+}
+
+__global__ void k_readback(ReadbackArgs a) {
+  if (threadIdx.x != 0) return;
+  FastBackRec r;
+  r.tot = a.tot ? *a.tot : TopicOff{0, 0, 0, 0, 0};
+  r.ovf = *a.ovf;
+  r.fallback = a.fallback ? *a.fallback : 0u;
+  r.unsafe = *a.unsafe;
+  r.err = *a.err;
+  for (int k = 0; k < 3; k++) r.n_sets[k] = a.n_sets ? a.n_sets[k] : 0ull;
+  *a.out = r;
+  __threadfence_system();
+}
+
+void launch_readback(const ReadbackArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, a);
 }
 
 // Wavefront per piece: four 64-handle loads in flight per lane, then the stores.

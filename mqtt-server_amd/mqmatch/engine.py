@@ -78,7 +78,7 @@ PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 OPT_CHUNK_ROWS, OPT_PATCH_CAP, OPT_EDGE_LOAD = 1, 6, 13
 OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_MERGE_WAVES = 2, 3, 4, 5, 7
 OPT_MSG_IMAGE, OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_MERGE_DEDUP = 8, 9, 10, 12
-OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC, OPT_FUSE_DESC, OPT_SET_EXP = 14, 15, 16, 17, 18
+OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC, OPT_FUSE_DESC, OPT_SET_EXP, OPT_MSG_EXPORT = 14, 15, 16, 17, 18, 19
 
 
 class MsgResult(C.Structure):
@@ -416,11 +416,13 @@ class Engine:
         _check(lib().mq_match_spans_end_host(self.h, arr, len(foreign), C.byref(rp)), "mq_match_spans_end_host")
         return _expand_host_spans(rp, n)
 
-    def match_spans_host(self, bytes_, offs, expand=False, block=1024):
+    def match_spans_host(self, bytes_, offs, expand=False, block=1024, threads=1):
         """mq_match_spans with its results left in the library's host buffers (the end-to-end
         path: H2D topics, kernels, D2H of the span-format arrays). expand=True also materialises
-        every topic's rows with mq_spans_expand, `block` topics per call into one reused buffer
-        (what a consumer that wants rows pays). Returns (result bytes, rows expanded)."""
+        every topic's rows with mq_spans_expand, `block` topics per call into a reused buffer per
+        thread, on `threads` host threads (mq_spans_expand is thread-safe for disjoint outputs;
+        ctypes releases the GIL during the call) — what a consumer that wants rows pays. Returns
+        (result bytes, rows expanded)."""
         n = len(offs) - 1
         rp = C.POINTER(SpanResult)()
         _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
@@ -436,13 +438,25 @@ class Engine:
                 starts = list(range(0, n, block))
                 cap_r = max(int(max(csum[min(b + block, n)] - csum[b] for b in starts)), 1)
                 cap_s = max(int(max(ssum[min(b + block, n)] - ssum[b] for b in starts)), 1)
-                rows = np.empty((cap_r, 4), np.uint32)
-                shared = np.empty((cap_s, 2), np.uint32)
-                nr, ns = C.c_uint64(), C.c_uint64()
-                for b in starts:
-                    _check(lib().mq_spans_expand(rp, b, min(block, n - b), rows.ctypes.data, cap_r, shared.ctypes.data,
-                                                 cap_s, C.byref(nr), C.byref(ns)), "mq_spans_expand")
-                    done += int(nr.value)
+                threads = max(1, min(int(threads), len(starts)))
+
+                def work(k):
+                    rows = np.empty((cap_r, 4), np.uint32)
+                    shared = np.empty((cap_s, 2), np.uint32)
+                    nr, ns = C.c_uint64(), C.c_uint64()
+                    got = 0
+                    for b in starts[k::threads]:
+                        _check(lib().mq_spans_expand(rp, b, min(block, n - b), rows.ctypes.data, cap_r,
+                                                     shared.ctypes.data, cap_s, C.byref(nr), C.byref(ns)),
+                               "mq_spans_expand")
+                        got += int(nr.value)
+                    return got
+                if threads == 1:
+                    done = work(0)
+                else:
+                    from concurrent.futures import ThreadPoolExecutor
+                    with ThreadPoolExecutor(threads) as pool:
+                        done = sum(pool.map(work, range(threads)))
         finally:
             lib().mq_result_free(rp)
         return int(nbytes), done

@@ -595,6 +595,36 @@ def test_messages_deep_fanout(gpu_available):
         assert g == o.messages(f), f
 
 
+@pytest.mark.parametrize("export", [1, 0])
+def test_messages_wide_fanout_export(export, gpu_available):
+    """Filters whose literal segment meets a fan-out of thousands of particles (w/+/c/...: 6,000
+    children of w): the count pass hands those particles to work items every wavefront takes
+    (MQ_OPT_MSG_EXPORT, kMsgExportMin) and their outputs land after the filter's own part. Mixed
+    with small filters in one batch; equal to the oracle with and without the export."""
+    from mqmatch import engine as E
+    e, o = EngineAdapter(), OracleAdapter()
+    e.x.engine.set_option(E.OPT_MSG_EXPORT, export)
+    h = 0
+    topics = []
+    for i in range(6000):
+        topics.append(f"w/{i}/c/{i % 3}")
+        if i % 5 == 0:
+            topics.append(f"w/{i}/d")
+        if i % 7 == 0:
+            topics.append(f"w/{i}/c/{i % 3}/e")
+        if i % 2 == 0:
+            topics.append(f"v/{i}/c/x")
+    for t in topics + ["w/c", "q/r", "$SYS/w/1"]:
+        h += 1
+        assert e.retain_message(t, b"p", True, handle=h) == o.retain_message(t, b"p", True, handle=h)
+    filters = ["w/+/c/+", "w/+/c/#", "w/+/d", "w/+/c/1", "+/+/c/+", "+/+/c/x", "w/+/c/+/e", "+/+/c/#",
+               "v/+/c/+", "w/#", "q/+", "#", "w/1/c/1", "+/17/c/+"]
+    filters = filters * 40  # many wide filters at once: items from several filters interleave
+    got = e.messages_batch(filters)
+    for f, g in zip(filters, got):
+        assert g == o.messages(f), f
+
+
 def test_messages_empty_topic_retained(gpu_available):
     """Q6: a retained packet on topic "" is returned for literal-final particles without a
     retain path (topics.go:573)."""

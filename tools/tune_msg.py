@@ -1,6 +1,7 @@
 """Development helper: build one retained index, then time Messages batches under several
-MQ_MSG_WPE / MQ_MSG_SPEC_MB settings (read by the engine per batch), interleaved to expose
-run-to-run noise. python tools/tune_msg.py --retained 10000000 --configs "1;6;8" """
+engine option settings (`opt=value` pairs, ','-separated; configs ';'-separated), interleaved to
+expose run-to-run noise; --work adds one step with the count pass's per-filter clocks and fan-out
+counters (MQ_PROF_WORK). python tools/tune_msg.py --retained 10000000 --configs "3=64;3=0" --work"""
 import argparse
 import json
 import os
@@ -19,7 +20,8 @@ def main():
     ap.add_argument("--filters", type=int, default=100_000)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--repeat", type=int, default=2)
-    ap.add_argument("--configs", default="1;6;8", help="MQ_MSG_WPE values, ';'-separated")
+    ap.add_argument("--configs", default="3=64", help="option=value pairs (',') per config (';')")
+    ap.add_argument("--work", action="store_true")
     args = ap.parse_args()
     import torch
     from mqmatch import engine as E
@@ -35,16 +37,33 @@ def main():
     res = {}
     for rep in range(args.repeat):
         for c in args.configs.split(";"):
-            os.environ["MQ_MSG_WPE"] = c.strip()
+            for kv in c.split(","):
+                if kv.strip():
+                    k, v = kv.split("=")
+                    eng.set_option(int(k), int(v))
             eng.messages_device(d_fb.data_ptr(), d_fo.data_ptr(), n, s.cuda_stream)
             torch.cuda.synchronize()
+            eng.profile(True)
+            eng.profile_reset()
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 eng.messages_device(d_fb.data_ptr(), d_fo.data_ptr(), n, s.cuda_stream)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3 / args.steps
+            prof = eng.profile_read()
+            eng.profile(False)
             res.setdefault(c.strip(), []).append(ms)
-            print(json.dumps({"MQ_MSG_WPE": c.strip(), "rep": rep, "ms_per_step": ms}), flush=True)
+            out = {"config": c.strip(), "rep": rep, "ms_per_step": ms,
+                   "kernels_ms": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0}}
+            if args.work and rep == 0:
+                eng.profile(True, work=True)
+                eng.profile_reset()
+                eng.messages_device(d_fb.data_ptr(), d_fo.data_ptr(), n, s.cuda_stream)
+                torch.cuda.synchronize()
+                w = eng.profile_read()
+                eng.profile(False)
+                out["work"] = {k: v[0] for k, v in w.items() if v[1] == 0}
+            print(json.dumps(out), flush=True)
     print(json.dumps({k: min(v) for k, v in res.items()}), flush=True)
 
 
