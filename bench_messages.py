@@ -39,6 +39,20 @@ def log(msg):
     print(f"[bench_messages {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def read_msg_traffic(n_retained, n_filters):
+    """HBM bytes per Messages step (k_msgq passes + k_msg_copy: FETCH_SIZE x1 for the walks' random
+    loads, x2 for k_msg_copy's streams, + WRITE_SIZE) from a committed rocprofv3 PMC summary of the
+    same configuration (retained topics, filters per step, export threshold), if present."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
+            e = json.load(f).get("messages", {}).get(str(n_retained))
+        if e is None or int(e["filters"]) != n_filters or int(e.get("export", 1)) != 1:
+            return None
+        return float(e["hbm_bytes_per_step"])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
 def handle_digests(base, count, hs):
     """Per-filter digest of the sorted handles, as the oracle's messages_digest_batch computes
     it (fold of the count, then of each handle in ascending order), vectorised over filters."""
@@ -185,11 +199,16 @@ def main():
             handles_per_filter = r.n_handles / max(1, n)
             b_img = 8 * per["L"] + 4 + 16 * handles_per_filter
             ach = b_img * n / (kms * 1e-3) / 1e9
+            traffic = read_msg_traffic(len(ro) - 1, n) if not args.walk else None
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                               "kernel": "k_msgq (count, place) + k_msg_copy" if not args.walk else "k_msg (count + fill)",
+                               "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                               "kernel": ("k_msgq (count, wide count, place, wide place) + k_msg_copy" if not args.walk
+                                          else "k_msg (count + fill)"),
                                "bytes": "8 B per level + 4 B offset per filter, 16 B per emitted handle (read + write)",
                                "bytes_per_step": b_img * n, "ms_per_step": kms}
+            if traffic:  # the measured HBM bytes (calibrated PMC, profiles/pmc_traffic.json) over the same time
+                out["roofline"]["hbm_traffic_GBps"] = traffic / (kms * 1e-3) / 1e9
+                out["roofline"]["hbm_traffic_frac"] = out["roofline"]["hbm_traffic_GBps"] / HBM_PEAK_GBS
             out["survey_B_rate"] = {"GBps": b * n / (kms * 1e-3) / 1e9,
                                     "note": "SURVEY 8d B (incl. 16 B per child enumeration of the reference walk) "
                                             "per step time: the reference's work rate, not HBM traffic"}

@@ -888,7 +888,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   }  // (one-sync batches: zeroed by spans_begin's k_reset)
   prof.begin(s);
   if (fused) {  // one-sync batch, k_desc in the walk's epilogue: no scan (the dedup totals the gathers)
-    launch_walk_desc(walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(), ovf_.as<uint32_t>(),
+    launch_walk_desc(walk_group_, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(), ovf_.as<uint32_t>(),
                      fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, *fused, s);
     prof.end("walk", s);
     hip_check(hipGetLastError(), "k_walkf<desc>");
@@ -1021,7 +1021,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   sb_.one_sync = one_sync;
   // k_desc in the frontier walk's epilogue (one-sync batches): spans and GDesc records at
   // t * kGatherCap, so nothing waits for a scan of the gather counts
-  const bool fused = one_sync && fuse_desc_ && walk_group_ == 16;
+  const bool fused = one_sync && fuse_desc_ && (walk_group_ == 16 || walk_group_ == 8);
   sb_.fused = fused;
   if (!sb_.lists) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
   if (fused) {

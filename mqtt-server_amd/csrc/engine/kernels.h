@@ -336,7 +336,7 @@ void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* 
 // or share pick, one-sync batches): each topic's gathers go straight from LDS to its spans and
 // merge lists at t * kGatherCap (da.g_stride); the fallback topics' k_walk and k_desc_g16 (list
 // mode) follow. No scan: da.tc_out holds the per-topic counts.
-void launch_walk_desc(uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
+void launch_walk_desc(uint32_t group, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
                       TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list, uint32_t* fb_count,
                       uint32_t fb_blocks, const DescArgs& da, hipStream_t s);
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,

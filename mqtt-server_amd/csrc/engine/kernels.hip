@@ -425,8 +425,8 @@ struct FrontEnt {  // one frontier particle: its '+' / '#' children and its path
 
 // WPE: waves per SIMD asked of the register allocator (8: a few SGPRs spill to VGPR lanes; 1:
 // no constraint, 7 waves).
-template <class GW>
-__device__ __forceinline__ void desc_g16(const DescArgs& a, uint32_t t, uint32_t n_g, uint64_t g0, uint64_t ipos,
+template <uint32_t G, class GW>
+__device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t n_g, uint64_t g0, uint64_t ipos,
                                          uint32_t shr0, uint32_t sub, GW gw_at);
 
 // DESC (G = 16, LISTS = false): k_desc fused into the epilogue — the gathers, placed in the
@@ -437,12 +437,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                                uint32_t n, DevIndex ix, TopicCount* __restrict__ cnt,
                                                uint32_t* __restrict__ gathers, uint32_t* __restrict__ fb_list,
                                                uint32_t* __restrict__ fb_count, DescArgs da) {
-  static_assert(!DESC || (G == 16 && !LISTS), "the fused desc runs on 16-lane groups of a gathers-only walk");
+  static_assert(!DESC || ((G == 16 || G == 8) && !LISTS), "the fused desc runs on 8- or 16-lane groups of a gathers-only walk");
   constexpr uint32_t kTopics = 256 / G;  // topics per workgroup
-  __shared__ uint32_t sl[kTopics][kFrontLevels];      // '/' positions (relative to the topic's chunk base)
-  __shared__ uint4 skey[kTopics][kFrontLevels];       // each level's segment key (SegKey)
-  __shared__ uint2 sseg[kTopics][kFrontLevels];       // ... its start, and length | "+" segment << 31
-  __shared__ uint2 gat[kTopics][kGatherCap];          // staged gathers: (word, rank)
+  // levels and gathers a group holds: 8-lane groups keep 32 topics per workgroup within 20 KB of
+  // LDS (8 workgroups per CU: twice the topics in flight of 16-lane groups); a topic beyond them
+  // is walked by k_walk
+  constexpr uint32_t kLv = G >= 16 ? kFrontLevels : 10u;
+  constexpr uint32_t kStage = G >= 16 ? kGatherCap : 24u;
+  __shared__ uint32_t sl[kTopics][kLv];      // '/' positions (relative to the topic's chunk base)
+  __shared__ uint4 skey[kTopics][kLv];       // each level's segment key (SegKey)
+  __shared__ uint2 sseg[kTopics][kLv];       // ... its start, and length | "+" segment << 31
+  __shared__ uint2 gat[kTopics][kStage];     // staged gathers: (word, rank)
   __shared__ FrontEnt xf[kTopics][G];                 // next level's frontier, compacted
   const uint32_t q = threadIdx.x / G, sub = threadIdx.x % G;
   const uint32_t t = blockIdx.x * kTopics + q;
@@ -471,11 +476,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t inc = grp_incl<G>(c, sub);
     uint32_t idx = nsl + inc - c;
     for (; m; m &= m - 1, idx++)
-      if (idx < kFrontLevels) sl[q][idx] = (k << 4) + (uint32_t)(__ffs(m) - 1);
+      if (idx < kLv) sl[q][idx] = (k << 4) + (uint32_t)(__ffs(m) - 1);
     nsl += __shfl(inc, G - 1, G);
   }
   const uint32_t L = nch ? nsl + 1 : 0u;  // levels (0: the empty topic, which matches nothing)
-  bool fb = live && L > kFrontLevels;
+  bool fb = live && L > kLv;
   wave_sync_lds();
   // every level's key, lanes over the levels: the walk below then reads them from LDS instead of
   // loading topic bytes on each level's critical path
@@ -536,7 +541,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const uint32_t gc = (uint32_t)gH + (uint32_t)gL + (uint32_t)gC + (uint32_t)gP;
     const uint32_t gi = grp_incl<G>(gc, sub);
     const uint32_t gtot = __shfl(gi, G - 1, G);
-    if (act && ng + gtot > kGatherCap) fb = true;
+    if (act && ng + gtot > kStage) fb = true;
     if (act && !fb) {
       uint32_t p = ng + gi - gc;
       if (gH) gat[q][p++] = make_uint2(fe.hash | kGatherInline, fe.code | 3u << sh);
@@ -573,9 +578,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   wave_sync_lds();
   if (DESC) {
     // each gather's place (the smaller ranks), then the words in place in LDS, then k_desc's work
-    uint32_t pw[kGatherCap / G], ww[kGatherCap / G];
+    constexpr uint32_t kPer = (kStage + G - 1) / G;  // gathers per lane
+    uint32_t pw[kPer], ww[kPer];
 #pragma unroll
-    for (uint32_t k = 0; k < kGatherCap / G; k++) {
+    for (uint32_t k = 0; k < kPer; k++) {
       const uint32_t i = sub + k * G;
       pw[k] = kNone;
       if (i < ng) {
@@ -590,10 +596,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
     wave_sync_lds();
 #pragma unroll
-    for (uint32_t k = 0; k < kGatherCap / G; k++)
+    for (uint32_t k = 0; k < kPer; k++)
       if (pw[k] != kNone) gat[q][pw[k]].x = ww[k];
     wave_sync_lds();
-    desc_g16(da, t, ng, (uint64_t)t * da.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gat[q][i].x; });
+    desc_grp<G>(da, t, ng, (uint64_t)t * da.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gat[q][i].x; });
     return;
   }
   uint32_t rows = 0, shared = 0, inl = 0, merge = 0;
@@ -902,15 +908,15 @@ __device__ __forceinline__ void write_gdesc(const DevIndex& ix, const uint32_t* 
 // desc_g16: one topic on its 16-lane group (sub = lane & 15; group-uniform control flow): n_g
 // gathers, gw_at(i) the word of gather i, spans / GDesc at g0, inline rows copied to ipos, shared
 // rows counted from shr0 (GDesc records only). Also run by the walk-fused k_walkf<..., DESC>.
-template <class GW>
-__device__ __forceinline__ void desc_g16(const DescArgs& a, uint32_t t, uint32_t n_g, uint64_t g0, uint64_t ipos,
+template <uint32_t G, class GW>
+__device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t n_g, uint64_t g0, uint64_t ipos,
                                          uint32_t shr0, uint32_t sub, GW gw_at) {
   // one-sync batch: spans past the buffer are not written (the batch runs again, host-sized)
   const bool fits = !a.unsafe || g0 + n_g <= a.spans_cap;
   if (!fits && sub == 0) atomicOr(a.unsafe, kUnsafeSpans);
   uint32_t rpos = 0, spos = 0, n_mg = 0, n_merge = 0;
   uint64_t sig = 0;
-  for (uint32_t r0 = 0; r0 < n_g; r0 += 16) {
+  for (uint32_t r0 = 0; r0 < n_g; r0 += G) {
     const uint32_t i = r0 + sub;
     const bool act = i < n_g;
     uint32_t gw = 0;
@@ -927,8 +933,8 @@ __device__ __forceinline__ void desc_g16(const DescArgs& a, uint32_t t, uint32_t
     const bool ismg = subs && L.n_merge != 0;
     // set-relative rows hold 26 bits of slot: a larger merge gather keeps the topic apart
     const uint32_t inc = ismg ? (L.n_direct + L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1) : 0u;
-    const uint32_t rn_i = g16_incl(rn, sub), in_i = g16_incl(in, sub), inc_i = g16_incl(inc, sub);
-    const uint32_t sh_i = g16_incl(act ? L.shr_cnt : 0u, sub);
+    const uint32_t rn_i = grp_incl<G>(rn, sub), in_i = grp_incl<G>(in, sub), inc_i = grp_incl<G>(inc, sub);
+    const uint32_t sh_i = grp_incl<G>(act ? L.shr_cnt : 0u, sub);
     const uint32_t rp = rpos + rn_i - rn, x = n_mg + inc_i - inc;
     const uint64_t ip = ipos + (in_i - in);
     if (act && fits) a.spans[g0 + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
@@ -944,15 +950,15 @@ __device__ __forceinline__ void desc_g16(const DescArgs& a, uint32_t t, uint32_t
       }
     }
     if (subs) n_merge += L.n_merge;
-    rpos += __shfl(rn_i, 15, 16);
-    spos += __shfl(sh_i, 15, 16);
-    ipos += __shfl(in_i, 15, 16);
-    n_mg += __shfl(inc_i, 15, 16);
+    rpos += __shfl(rn_i, G - 1, G);
+    spos += __shfl(sh_i, G - 1, G);
+    ipos += __shfl(in_i, G - 1, G);
+    n_mg += __shfl(inc_i, G - 1, G);
   }
 #pragma unroll
-  for (uint32_t d = 1; d < 16; d <<= 1) {
-    sig += __shfl_xor(sig, d, 16);
-    n_merge += __shfl_xor(n_merge, d, 16);
+  for (uint32_t d = 1; d < G; d <<= 1) {
+    sig += __shfl_xor(sig, d, G);
+    n_merge += __shfl_xor(n_merge, d, G);
   }
   if (sub != 0) return;
   if (a.tc_out) a.tc_out[t] = TopicCount{n_g, rpos, spos, 0u, n_merge};
@@ -990,7 +996,7 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
       const uint32_t t = a.list[i];
       const uint32_t n_g = min(a.g_count[t].gathers, kGatherCap);
       const uint32_t* gw_src = a.gathers + (uint64_t)t * a.gather_stride;
-      desc_g16(a, t, n_g, (uint64_t)t * a.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gw_src[i]; });
+      desc_grp<16>(a, t, n_g, (uint64_t)t * a.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gw_src[i]; });
     }
     return;
   }
@@ -999,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
   const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
   const uint32_t n_g = (uint32_t)(o1.g - o0.g);
   const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
-  desc_g16(a, t, n_g, o0.g, o0.inl, (uint32_t)o0.shr, sub, [&](uint32_t i) { return gw_src[i]; });
+  desc_grp<16>(a, t, n_g, o0.g, o0.inl, (uint32_t)o0.shr, sub, [&](uint32_t i) { return gw_src[i]; });
 }
 
 // k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, whose
@@ -1974,17 +1980,19 @@ void launch_walk_front(uint32_t group, bool lists, uint32_t wpe, const uint8_t* 
                        fb_list, fb_count, clamp);
 }
 
-void launch_walk_desc(uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
+void launch_walk_desc(uint32_t group, uint32_t wpe, const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix,
                       TopicCount* cnt, uint32_t* gathers, uint32_t* ovf, uint32_t* fb_list, uint32_t* fb_count,
                       uint32_t fb_blocks, const DescArgs& da, hipStream_t s) {
   if (!n) return;
-  const dim3 grid((n + 15) / 16);
-  if (wpe >= 8)
-    hipLaunchKernelGGL((k_walkf<16, false, 8, true>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list,
-                       fb_count, da);
+  if (group == 8)
+    hipLaunchKernelGGL((k_walkf<8, false, 8, true>), dim3((n + 31) / 32), dim3(256), 0, s, tb, to, n, ix, cnt, gathers,
+                       fb_list, fb_count, da);
+  else if (wpe >= 8)
+    hipLaunchKernelGGL((k_walkf<16, false, 8, true>), dim3((n + 15) / 16), dim3(256), 0, s, tb, to, n, ix, cnt, gathers,
+                       fb_list, fb_count, da);
   else
-    hipLaunchKernelGGL((k_walkf<16, false, 1, true>), grid, dim3(256), 0, s, tb, to, n, ix, cnt, gathers, fb_list,
-                       fb_count, da);
+    hipLaunchKernelGGL((k_walkf<16, false, 1, true>), dim3((n + 15) / 16), dim3(256), 0, s, tb, to, n, ix, cnt, gathers,
+                       fb_list, fb_count, da);
   // the topics the frontier could not hold: k_walk's gather slots (clamped counts), then k_desc
   const dim3 fgrid(std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, fb_blocks)));
   hipLaunchKernelGGL((k_walk<false, false, 1>), fgrid, dim3(256), 0, s, tb, to, n, ix, cnt, nullptr, gathers, ovf,

@@ -1,0 +1,22 @@
+# Round 3 final evidence (headline): standalone C++ mirror test, the whole GPU suite, the default
+# bench line, a kernel trace and PMC passes (FETCH_SIZE, WRITE_SIZE: separate runs) of the 10M step.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+D=$R/gpurun_out/${1:-r3u}
+mkdir -p $D
+timeout -k 5 150 ./mqtt-server_amd/build/test_topics_index > $D/cpp.log 2>&1 || { echo "cpp rc=$?"; tail -20 $D/cpp.log; exit 1; }
+tail -2 $D/cpp.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > $D/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -60 $D/pytest_gpu.log; exit 1; }
+tail -2 $D/pytest_gpu.log
+timeout -k 10 400 python -u bench.py > $D/bench_default.json 2> $D/bench_default.err || { echo "bench rc=$?"; tail -5 $D/bench_default.err; exit 1; }
+cut -c1-300 $D/bench_default.json
+cd /tmp && export TMPDIR=/tmp
+ARGS="--steps 3 --warmup 1 --no-cpu"
+KR="k_walk|k_merge|k_desc|k_dedup|k_finish|k_reset|k_readback"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 $R/bench.py $ARGS > $D/trace.json 2> $D/trace.err || { echo "trace rc=$?"; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" --output-format csv -d $D/fetch -o run -- python3 $R/bench.py $ARGS > $D/fetch.json 2> $D/fetch.err || { echo "fetch rc=$?"; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" --output-format csv -d $D/write -o run -- python3 $R/bench.py $ARGS > $D/write.json 2> $D/write.err || { echo "write rc=$?"; exit 1; }
+cd $R
+python profiles/summarize.py $D/trace > $D/kernel_stats.json
+python profiles/summarize.py $D/fetch $D/write --pmc > $D/pmc.json
+head -c 1500 $D/kernel_stats.json
