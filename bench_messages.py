@@ -81,12 +81,25 @@ def oracle_side(rb, ro, hd, fb, fo, n, args):
     log(f"oracle index built in {time.time() - t0:.1f}s")
     ns = min(n, 4096)
     dg, cnt, tot = orc.messages_digest_batch(fb, fo[:ns + 1], nthreads=16)
+    # the baseline: the fast restatement (oracle/topics_fast.h FastMsgIndex: flat nodes, handles
+    # looked up at build time, segments split once; digest-equal to the oracle), 16 threads; the
+    # literal restatement beside it
+    t0 = time.time()
+    fast = orc.fast_messages()
+    log(f"fast CPU restatement built in {time.time() - t0:.1f}s")
     cal = min(n, 2048)
-    secs, _ = orc.bench_messages(fb, fo[:cal + 1], 16)
+    secs, _ = fast.bench_messages(fb, fo[:cal + 1], 16)
     m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
-    secs, _ = orc.bench_messages(fb, fo[:m + 1], 16)
+    secs, _ = fast.bench_messages(fb, fo[:m + 1], 16)
     cpu = {"value": m / secs, "unit": "filters/s", "cores": 16, "kind": "port",
-           "sample": f"first {m} filters, 16 threads, Messages() per filter (oracle/)"}
+           "sample": f"first {m} filters, 16 threads, Messages() per filter: the fast CPU restatement of the Go "
+                     f"trie's scanMessages (oracle/topics_fast.cpp FastMsgIndex; digest-equal to the oracle)"}
+    del fast
+    lcal = min(n, 2048)
+    lsecs, _ = orc.bench_messages(fb, fo[:lcal + 1], 16)
+    lm = int(min(n, max(lcal, lcal * min(5.0, args.cpu_seconds / 2) / max(lsecs, 1e-6))))
+    lsecs, _ = orc.bench_messages(fb, fo[:lm + 1], 16)
+    cpu["literal"] = {"value": lm / lsecs, "sample": f"first {lm} filters, 16 threads, oracle/topics_oracle.cpp"}
     return {"sample_filters": ns, "digests": [format(int(x), "x") for x in dg], "counts": [int(x) for x in cnt],
             "per_filter": {k: v / ns for k, v in tot.items()}, "cpu": cpu}
 

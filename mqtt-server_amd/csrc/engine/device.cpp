@@ -987,6 +987,8 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     uint64_t slots = 1024;
     while (slots < 2ull * n) slots <<= 1;
     grow(dd_keys_, slots * sizeof(unsigned long long));
+    grow(dd_vals_, slots * sizeof(uint32_t));
+    grow(dd_slot_, (size_t)n * sizeof(uint32_t));
     if (!dd_nsets_.p) dd_nsets_.ensure(3 * sizeof(unsigned long long));
     if (!dd_spcount_.p) dd_spcount_.ensure(kPatchRegions * sizeof(unsigned long long));
     if (!sp_pcount_.p) sp_pcount_.ensure(kPatchRegions * sizeof(unsigned long long));
@@ -1069,6 +1071,13 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   if (fused) {
     grow(sp_inl_, sizeof(InlRec));
     fda = desc_args();
+    // k_dedup_insert folded into the walk's epilogue (the table was zeroed by k_reset)
+    fda.dd_keys = dd_keys_.as<unsigned long long>();
+    fda.dd_vals = dd_vals_.as<uint32_t>();
+    uint64_t slots = 1024;  // (as zeroed by k_reset above)
+    while (slots < 2ull * n) slots <<= 1;
+    fda.dd_mask = slots - 1;
+    fda.dd_tslot = dd_slot_.as<uint32_t>();
   }
   const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, one_sync, fused ? &fda : nullptr);
   sb_.tot = tot;
@@ -1213,7 +1222,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       dd.fcount = xa.fcount;
     }
     prof.begin(s);
-    launch_dedup(dd, s);
+    launch_dedup(dd, s, !sb_.fused);
     prof.end("dedup", s);
     hip_check(hipGetLastError(), "k_dedup");
     sb_.n_sets = 0;

@@ -234,6 +234,12 @@ struct DescArgs {
   const uint32_t* list;
   const uint32_t* n_list;
   const TopicCount* g_count;  // list mode: the listed topics' gathers (their walk's counts)
+  // k_dedup_insert folded in (dd_keys != null; DedupArgs' table): each topic with 1..kPairMax
+  // merge gathers inserts its signature and gets its slot (dd_tslot; kNone: not deduped)
+  unsigned long long* dd_keys;
+  uint32_t* dd_vals;
+  uint64_t dd_mask;
+  uint32_t* dd_tslot;
 };
 
 // Merge-set dedup (span format): topics whose merge gathers are the same particles resolve to
@@ -265,7 +271,8 @@ struct DedupArgs {
   uint32_t n_xf;
   const struct XSrc* xsrc;
 };
-void launch_dedup(const DedupArgs& a, hipStream_t s);
+// insert = false: the signatures were inserted by the walk-fused desc (DescArgs.dd_keys)
+void launch_dedup(const DedupArgs& a, hipStream_t s, bool insert = true);
 
 // Sharded index, after the exchange (k_xsig): per topic, fold the imported cross-shard entries
 // into the merge-set signature (msig) and count them (fcount); a topic whose map would overflow

@@ -908,6 +908,9 @@ __device__ __forceinline__ void write_gdesc(const DevIndex& ix, const uint32_t* 
 // desc_g16: one topic on its 16-lane group (sub = lane & 15; group-uniform control flow): n_g
 // gathers, gw_at(i) the word of gather i, spans / GDesc at g0, inline rows copied to ipos, shared
 // rows counted from shr0 (GDesc records only). Also run by the walk-fused k_walkf<..., DESC>.
+__device__ __forceinline__ uint32_t dedup_insert(unsigned long long* keys, uint32_t* vals, uint64_t mask, uint32_t t,
+                                                bool ok, unsigned long long k);
+
 template <uint32_t G, class GW>
 __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t n_g, uint64_t g0, uint64_t ipos,
                                          uint32_t shr0, uint32_t sub, GW gw_at) {
@@ -960,9 +963,15 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
     sig += __shfl_xor(sig, d, G);
     n_merge += __shfl_xor(n_merge, d, G);
   }
+  const unsigned long long msig = mix64(sig + n_mg) | 1ull;  // never 0 (the dedup table's empty key)
+  if (a.dd_keys) {  // k_dedup_insert's work, one lane per topic
+    const uint32_t slot = dedup_insert(a.dd_keys, a.dd_vals, a.dd_mask, t, sub == 0 && n_mg != 0 && n_mg <= kPairMax,
+                                       msig);
+    if (sub == 0) a.dd_tslot[t] = slot;
+  }
   if (sub != 0) return;
   if (a.tc_out) a.tc_out[t] = TopicCount{n_g, rpos, spos, 0u, n_merge};
-  a.msig[t] = mix64(sig + n_mg) | 1ull;  // never 0 (the dedup table's empty key)
+  a.msig[t] = msig;
   a.mcount[t] = n_mg;
   // k_merge maps this topic from its GDesc records: write them (rare; gather words re-read)
   if (n_mg > kPairMax) {
@@ -1011,17 +1020,16 @@ __global__ __launch_bounds__(256) void k_desc_g16(DescArgs a) {
 // k_dedup_insert: thread per topic with 1..kPairMax merge gathers; its signature's slot, whose
 // value is the topic that inserted the signature. k_dedup_rep: the representative, verified list against list (a
 // signature collision leaves the topic its own representative).
-__global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
-  const bool act = t < a.n;
-  const uint32_t c = act ? a.mcount[t] : 0u;
-  // (sharded: the merge gathers and the other shards' entries must fit k_merge's map)
-  const bool ok = c != 0 && c <= kPairMax && (!a.fcount || c + a.fcount[t] < kMapSlots);
-  const unsigned long long k = ok ? a.msig[t] : 0ull;
-  // one table operation per distinct signature in the wavefront: a hot signature (the topics
-  // under the same busy particles) would otherwise have every topic's CAS on one slot at once
+// The insert of topic t's signature k (ok: it is deduped) into the table; called by every active
+// lane of the wavefront (the lanes with ok == false take part in the leader choice). One table
+// operation per distinct signature in the wavefront: a hot signature (the topics under the same
+// busy particles) would otherwise have every topic's CAS on one slot at once. Returns the slot
+// (kNone when !ok).
+__device__ __forceinline__ uint32_t dedup_insert(unsigned long long* keys, uint32_t* vals, uint64_t mask, uint32_t t,
+                                                bool ok, unsigned long long k) {
+  const uint32_t lane = threadIdx.x & 63;
   uint32_t leader = lane;
-  for (uint64_t rem = __ballot(ok); rem;) {  // wave-uniform: a leader per distinct signature
+  for (uint64_t rem = __ballot(ok); rem;) {  // uniform over the active lanes: a leader per signature
     const uint32_t l = (uint32_t)__builtin_ctzll(rem);
     const unsigned long long kl = __shfl(k, (int)l, 64);
     const uint64_t same = __ballot(ok && k == kl) & rem;
@@ -1030,15 +1038,15 @@ __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
   }
   uint32_t slot = kNone;
   if (ok && leader == lane) {
-    uint64_t i = mix64(k) & a.table_mask;
-    for (uint64_t probes = 0; probes <= a.table_mask; probes++) {
+    uint64_t i = mix64(k) & mask;
+    for (uint64_t probes = 0; probes <= mask; probes++) {
       // most leaders find their signature already in place: a plain load, no atomic on a hot
       // slot; the topic whose CAS fills a slot is the representative of its signature
-      unsigned long long prev = __atomic_load_n(a.keys + i, __ATOMIC_RELAXED);
+      unsigned long long prev = __atomic_load_n(keys + i, __ATOMIC_RELAXED);
       if (prev == 0ull) {
-        prev = atomicCAS(a.keys + i, 0ull, k);
+        prev = atomicCAS(keys + i, 0ull, k);
         if (prev == 0ull) {
-          a.vals[i] = t;
+          vals[i] = t;
           slot = (uint32_t)i;
           break;
         }
@@ -1047,11 +1055,22 @@ __global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
         slot = (uint32_t)i;
         break;
       }
-      i = (i + 1) & a.table_mask;
+      i = (i + 1) & mask;
     }  // slot stays kNone only for a full table (sized 2x the topics: cannot happen)
   }
   slot = __shfl(slot, (int)leader, 64);
-  if (act) a.tslot[t] = ok ? slot : kNone;
+  return ok ? slot : kNone;
+}
+
+__global__ __launch_bounds__(256) void k_dedup_insert(DedupArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = t < a.n;
+  const uint32_t c = act ? a.mcount[t] : 0u;
+  // (sharded: the merge gathers and the other shards' entries must fit k_merge's map)
+  const bool ok = c != 0 && c <= kPairMax && (!a.fcount || c + a.fcount[t] < kMapSlots);
+  const unsigned long long k = ok ? a.msig[t] : 0ull;
+  const uint32_t slot = dedup_insert(a.keys, a.vals, a.table_mask, t, ok, k);
+  if (act) a.tslot[t] = slot;
 }
 
 // k_dedup_rep also lists the topics that resolve a merge set (rep_list, n_sets of them): the
@@ -1210,10 +1229,10 @@ void launch_finish(const FinishArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_finish, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 
-void launch_dedup(const DedupArgs& a, hipStream_t s) {
+void launch_dedup(const DedupArgs& a, hipStream_t s, bool insert) {
   if (!a.n) return;
   const dim3 g((a.n + 255) / 256), b(256);
-  hipLaunchKernelGGL(k_dedup_insert, g, b, 0, s, a);
+  if (insert) hipLaunchKernelGGL(k_dedup_insert, g, b, 0, s, a);
   hipLaunchKernelGGL(k_dedup_rep, dim3((a.n + 1023) / 1024), dim3(1024), 0, s, a);
 }
 

@@ -77,6 +77,12 @@ def lib():
     L.orc_fast_digest_batch.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint32, _u64p, _u32p]
     L.orc_fast_bench.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint32, _u64p]
     L.orc_fast_bench.restype = C.c_double
+    L.orc_fast_msg_build.argtypes = [C.c_void_p]
+    L.orc_fast_msg_build.restype = C.c_void_p
+    L.orc_fast_msg_free.argtypes = [C.c_void_p]
+    L.orc_fast_msg_digest_batch.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint32, _u64p, _u32p]
+    L.orc_fast_msg_bench.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint32, _u64p]
+    L.orc_fast_msg_bench.restype = C.c_double
     L.orc_root_children.argtypes = [C.c_void_p]
     L.orc_root_children.restype = C.c_uint64
     _LIB = L
@@ -265,6 +271,10 @@ class OracleIndex:
         """FastIndex snapshot of this index (topics_fast.h): the CPU baseline's restatement."""
         return FastIndex(self)
 
+    def fast_messages(self):
+        """FastMsgIndex snapshot of this index (topics_fast.h): bench_messages.py's CPU baseline."""
+        return FastMsgIndex(self)
+
     def bench_messages(self, bytes_, offs, nthreads):
         n = len(offs) - 1
         sink = C.c_uint64()
@@ -304,4 +314,38 @@ class FastIndex:
         n = len(offs) - 1
         sink = C.c_uint64()
         secs = lib().orc_fast_bench(self.h, _ptr(bytes_, _u8p), _ptr(offs, _u64p), n, nthreads, C.byref(sink))
+        return float(secs), int(sink.value)
+
+
+class FastMsgIndex:
+    """The fast CPU restatement of Messages (oracle/topics_fast.h) over a frozen OracleIndex:
+    bench_messages.py's cpu_baseline; digest-checked against the oracle in tests/test_oracle_kat.py."""
+
+    def __init__(self, orc):
+        self.orc = orc  # (it reads the oracle's retained map for filters without wildcards)
+        self.h = lib().orc_fast_msg_build(orc.h)
+
+    def close(self):
+        if self.h:
+            lib().orc_fast_msg_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def digest_batch(self, bytes_, offs, nthreads=8):
+        n = len(offs) - 1
+        dig = np.zeros(n, np.uint64)
+        cnt = np.zeros(n, np.uint32)
+        lib().orc_fast_msg_digest_batch(self.h, _ptr(bytes_, _u8p), _ptr(offs, _u64p), n, nthreads,
+                                        _ptr(dig, _u64p), _ptr(cnt, _u32p))
+        return dig, cnt
+
+    def bench_messages(self, bytes_, offs, nthreads):
+        n = len(offs) - 1
+        sink = C.c_uint64()
+        secs = lib().orc_fast_msg_bench(self.h, _ptr(bytes_, _u8p), _ptr(offs, _u64p), n, nthreads, C.byref(sink))
         return float(secs), int(sink.value)

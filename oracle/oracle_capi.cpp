@@ -367,6 +367,55 @@ double orc_bench_messages(void* hp, const uint8_t* bytes, const uint64_t* offs, 
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// ---- the fast Messages restatement (topics_fast.h): bench_messages.py's cpu_baseline ----
+void* orc_fast_msg_build(void* hp) { return fast_msg_build(((Handle*)hp)->idx); }
+void orc_fast_msg_free(void* fp) { fast_msg_free((FastMsgIndex*)fp); }
+
+int orc_fast_msg_digest_batch(void* fp, const uint8_t* bytes, const uint64_t* offs, uint64_t n, uint32_t nthreads,
+                              uint64_t* digests, uint32_t* counts) {
+  const FastMsgIndex& f = *(FastMsgIndex*)fp;
+  if (nthreads == 0) nthreads = 1;
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nthreads; t++) {
+    th.emplace_back([&, t] {
+      std::vector<uint64_t> hs;
+      for (uint64_t i = t; i < n; i += nthreads) {
+        fast_messages(f, (const char*)bytes + offs[i], (uint32_t)(offs[i + 1] - offs[i]), hs);
+        std::sort(hs.begin(), hs.end());
+        uint64_t d = 0x6d716d61ull;
+        d = fold(d, hs.size());
+        for (uint64_t x : hs) d = fold(d, x);
+        digests[i] = d;
+        if (counts) counts[i] = (uint32_t)hs.size();
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  return 0;
+}
+
+double orc_fast_msg_bench(void* fp, const uint8_t* bytes, const uint64_t* offs, uint64_t n, uint32_t nthreads,
+                          uint64_t* sink) {
+  const FastMsgIndex& f = *(FastMsgIndex*)fp;
+  if (nthreads == 0) nthreads = 1;
+  std::atomic<uint64_t> acc{0};
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nthreads; t++) {
+    th.emplace_back([&, t] {
+      std::vector<uint64_t> hs;
+      uint64_t local = 0;
+      for (uint64_t i = t; i < n; i += nthreads)
+        local += fast_messages(f, (const char*)bytes + offs[i], (uint32_t)(offs[i + 1] - offs[i]), hs);
+      acc += local;
+    });
+  }
+  for (auto& x : th) x.join();
+  auto t1 = std::chrono::steady_clock::now();
+  if (sink) *sink = acc.load();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
 // ---- the fast CPU restatement (topics_fast.h): bench.py's cpu_baseline, checked against the
 // oracle's digests in the tests ----
 void* orc_fast_build(void* hp) {

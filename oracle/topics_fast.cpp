@@ -250,4 +250,101 @@ uint64_t fast_subscribers(const FastIndex& f, FastScratch& s, const char* topic,
   return s.res.size() + s.shared.size() + n_inl;
 }
 
+// ---- Messages ----
+
+namespace {
+struct FMNode {
+  std::unordered_map<std::string, uint32_t> kids;  // particles, keyed by segment
+  std::vector<uint32_t> list;                      // the same children, for '+' / '#' (getAll)
+  int64_t h = -1;          // Retained.Get(retain_path) at build time (-1: none)
+  bool path = false;       // retain_path != "" (the enumerations' check, topics.go:558)
+  bool sys = false;        // key == "$SYS" (skipped at level 0, topics.go:549)
+};
+}  // namespace
+
+struct FastMsgIndex {
+  const TopicsIndex* idx = nullptr;  // Retained.Get(filter) of a filter without wildcards
+  std::vector<FMNode> nodes;
+  bool empty = true;                 // Retained.Len() == 0
+};
+
+FastMsgIndex* fast_msg_build(const TopicsIndex& idx) {
+  FastMsgIndex* f = new FastMsgIndex();
+  f->idx = &idx;
+  f->empty = idx.retained_len() == 0;
+  std::vector<std::pair<const Particle*, uint32_t>> stack{{idx.root(), 0u}};
+  f->nodes.emplace_back();
+  while (!stack.empty()) {
+    const Particle* p = stack.back().first;
+    const uint32_t id = stack.back().second;
+    stack.pop_back();
+    RetainedPacket pk;
+    if (idx.retained_get(p->retain_path, &pk)) f->nodes[id].h = (int64_t)pk.handle;
+    f->nodes[id].path = !p->retain_path.empty();
+    f->nodes[id].sys = p->key == "$SYS";
+    for (auto& kv : p->particles) {
+      const uint32_t c = (uint32_t)f->nodes.size();
+      f->nodes.emplace_back();
+      f->nodes[id].kids.emplace(kv.first, c);
+      f->nodes[id].list.push_back(c);
+      stack.emplace_back(kv.second.get(), c);
+    }
+  }
+  return f;
+}
+
+void fast_msg_free(FastMsgIndex* f) { delete f; }
+
+namespace {
+// scanMessages (topics.go:546-578) over pre-split segments
+void scan_msg(const FastMsgIndex& f, const std::vector<std::string_view>& segs, std::string& key, uint32_t d,
+              uint32_t node, std::vector<uint64_t>& out) {
+  // isolateParticle past the last segment gives the last one again ('#' recurses below itself)
+  const std::string_view seg = segs[std::min<size_t>(d, segs.size() - 1)];
+  const bool has_next = d + 1 < segs.size();
+  const FMNode& n = f.nodes[node];
+  if (seg == "+" || seg == "#") {
+    for (uint32_t c : n.list) {
+      const FMNode& a = f.nodes[c];
+      if (d == 0 && a.sys) continue;
+      if (!has_next && a.path && a.h >= 0) out.push_back((uint64_t)a.h);
+      if (has_next || seg == "#") scan_msg(f, segs, key, d + 1, c, out);
+    }
+    return;
+  }
+  key.assign(seg.data(), seg.size());
+  auto it = n.kids.find(key);
+  if (it == n.kids.end()) return;
+  if (has_next) {
+    scan_msg(f, segs, key, d + 1, it->second, out);
+    return;
+  }
+  const FMNode& p = f.nodes[it->second];
+  if (p.h >= 0) out.push_back((uint64_t)p.h);  // Q6: no emptiness check
+}
+}  // namespace
+
+uint64_t fast_messages(const FastMsgIndex& f, const char* filter, uint32_t len, std::vector<uint64_t>& out) {
+  out.clear();
+  if (!len || f.empty) return 0;  // topics.go:535
+  bool wild = false;
+  for (uint32_t i = 0; i < len && !wild; i++) wild = filter[i] == '+' || filter[i] == '#';
+  if (!wild) {  // Retained.Get(filter) (topics.go:539-544)
+    RetainedPacket pk;
+    if (f.idx->retained_get(std::string(filter, len), &pk)) out.push_back(pk.handle);
+    return out.size();
+  }
+  thread_local std::vector<std::string_view> segs;
+  thread_local std::string key;
+  segs.clear();
+  uint32_t b = 0;
+  for (uint32_t i = 0; i <= len; i++)
+    if (i == len || filter[i] == '/') {
+      segs.emplace_back(filter + b, i - b);
+      b = i + 1;
+    }
+  scan_msg(f, segs, key, 0, 0, out);
+  return out.size();
+}
+
 }  // namespace oracle

@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "topics_oracle.h"
 
@@ -39,5 +40,16 @@ void fast_scratch_free(FastScratch* s);
 // and the four row counts.
 uint64_t fast_subscribers(const FastIndex& f, FastScratch& s, const char* topic, uint32_t len,
                           uint64_t* digest, uint64_t counts[4]);
+
+// Messages (topics.go:525-579), restated for speed the same way (bench_messages.py's
+// cpu_baseline): the particle tree snapshotted into flat nodes (children maps keyed by segment
+// plus a child list for the '+' / '#' enumerations), each node's retained handle looked up once
+// at build time (the Retained map lookup scanMessages does per emitted particle), the filter
+// split into segments once. Digest-checked against the oracle in tests/test_oracle_kat.py.
+struct FastMsgIndex;
+FastMsgIndex* fast_msg_build(const TopicsIndex& idx);
+void fast_msg_free(FastMsgIndex* f);
+// Messages(filter): the handles, appended to `out` (cleared first); returns their number.
+uint64_t fast_messages(const FastMsgIndex& f, const char* filter, uint32_t len, std::vector<uint64_t>& out);
 
 }  // namespace oracle

@@ -151,3 +151,35 @@ def test_fast_baseline_matches_oracle():
     assert (fcnt == ocnt).all()
     assert (fd == od).all(), np.nonzero(fd != od)[0][:5]
     assert ocnt[:, 0].sum() > len(topics) and ocnt[:, 3].sum() > 0
+
+
+def test_fast_messages_baseline_matches_oracle():
+    """The Messages CPU baseline's fast restatement (oracle/topics_fast.h, FastMsgIndex) gives the
+    oracle's digests: a config-5-shaped workload plus the Q4 ($SYS at level 0), Q5 (x/# excludes x)
+    and Q6 (a retained "" entry, particles without a retain path) corners."""
+    import random
+    import numpy as np
+    from mqmatch import workload as W
+    rb, ro, hd, rh = W.gen_retained(20000, n_sys=200, seed=94)
+    fb, fo = W.gen_msg_filters(rh, 2000, seed=95)
+    orc = O.OracleIndex()
+    orc.retain_bulk(rb, ro, hd)
+    r = random.Random(96)
+    h = 10 ** 9
+    for t in ["", "q/r", "q/r/s", "$SYS/x/y", "a/$SYS"]:
+        h += 1
+        orc.retain_message(t, h, 1, True)
+    for f in ["q/z", "zz/top"]:  # subscription-only particles (no retain path)
+        orc.subscribe("c1", f)
+    extra = ["#", "+", "+/+", "$SYS/#", "+/$SYS/#", "q/#", "q/+", "q/r", "q/z", "zz/+", "+/z", "", "q/+/#",
+             "/".join(r.choice(["+", "#", "q", "r"]) for _ in range(3))]
+    filters = W.strings(fb, fo) + extra
+    raw = [f.encode("utf-8", "surrogateescape") for f in filters]
+    offs = np.zeros(len(raw) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in raw])
+    b = np.frombuffer(b"".join(raw) + b"\0" * 16, np.uint8).copy()
+    od, ocnt, _ = orc.messages_digest_batch(b, offs, nthreads=4)
+    fd, fcnt = orc.fast_messages().digest_batch(b, offs, nthreads=4)
+    assert (fcnt == ocnt).all(), np.nonzero(fcnt != ocnt)[0][:5]
+    assert (fd == od).all(), np.nonzero(fd != od)[0][:5]
+    assert ocnt.sum() > len(filters)
