@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 6
+#define MQ_ABI_VERSION 7
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
@@ -263,7 +263,9 @@ int mq_select_shared_device(mq_index* idx, const mq_match_result* chunk, void* h
  * patches at set_patches[patch_base, + n_patches), each naming its row as (x << 26 | k): record
  * k of the span of the topic's x-th particle with may-merge records, i.e. topic row
  * merge_rows[topic * 64 + x] + k (merge_rows: the row of that span's first record). Host results
- * (mq_match_spans) always hold per-topic patches.
+ * (mq_match_spans, ABI v7) share them the same way, packed: the set patches in set_patches and
+ * each such topic's merge rows at merge_rows[merge_row_base[topic]] (one per may-merge particle);
+ * mq_topic_patch() below resolves either layout.
  * With MQ_CFG_SELECT_SHARED the picked shared members are materialised (picked_rows at
  * picked_base, n_shared of them) and flags has MQ_SPANS_PICKED. */
 typedef struct mq_span {
@@ -305,12 +307,30 @@ typedef struct mq_span_result {
                          (topic ranges lie in per-region parts of it, with unused gaps) */
   uint64_t n_inline_rows, n_picked_rows;
   uint64_t sub_pool_len, shared_pool_len;
-  /* device results: patches shared by topics with MQ_TOPIC_SET_PATCHES, and every topic's merge
-     rows (MQ_MERGE_ROWS_STRIDE per topic); null / 0 when no topic shares */
+  /* patches shared by topics with MQ_TOPIC_SET_PATCHES and the topics' merge rows; null / 0 when
+     no topic shares. Device results: MQ_MERGE_ROWS_STRIDE merge rows per topic at topic * 64,
+     merge_row_base null, set_patches the pool's extent (per-region parts with gaps). Host results
+     (v7): set_patches packed, merge rows packed at merge_row_base[topic] (n_topics entries; 0 for
+     a topic without MQ_TOPIC_SET_PATCHES) */
   const mq_patch* set_patches;
   const uint32_t* merge_rows;
   uint64_t n_set_patches;
+  const uint32_t* merge_row_base;
+  uint64_t n_merge_rows;
 } mq_span_result;
+
+/* Patch k (< n_patches) of topic t of a span result whose arrays the caller can read (a host
+ * result, or a device result copied to the host): the topic's own patch, or its set patch with
+ * the row translated through the topic's merge rows. */
+static inline mq_patch mq_topic_patch(const mq_span_result* r, uint32_t t, uint32_t k) {
+  const mq_topic_spans* ts = &r->topics[t];
+  if (!(ts->flags & MQ_TOPIC_SET_PATCHES)) return r->patches[ts->patch_base + k];
+  mq_patch p = r->set_patches[ts->patch_base + k];
+  const uint32_t* mr = r->merge_rows + (r->merge_row_base ? (uint64_t)r->merge_row_base[t]
+                                                           : (uint64_t)t * MQ_MERGE_ROWS_STRIDE);
+  p.row = mr[p.row >> MQ_SET_ROW_BITS] + (p.row & ((1u << MQ_SET_ROW_BITS) - 1u));
+  return p;
+}
 
 /* Span-format Subscribers for a batch of host topics (as mq_match_batch). The result's arrays
  * are host copies; its pools point at the index's host image, which the result pins: updates

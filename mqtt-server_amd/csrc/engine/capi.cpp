@@ -288,6 +288,12 @@ int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_sp
   r.inline_rows = reinterpret_cast<const mq_inline_row*>(h->data.inl.data());
   r.picked_rows = reinterpret_cast<const mq_shared_row*>(h->data.picked.data());
   r.n_patches = h->data.patches.size();  // packed (the device pool has per-region gaps)
+  const bool sets = !h->data.merge_base.empty();  // (topics with MQ_TOPIC_SET_PATCHES, ABI v7)
+  r.set_patches = sets ? reinterpret_cast<const mq_patch*>(h->data.set_patches.data()) : nullptr;
+  r.n_set_patches = sets ? h->data.set_patches.size() : 0;
+  r.merge_rows = sets ? h->data.merge_rows.data() : nullptr;
+  r.n_merge_rows = sets ? h->data.merge_rows.size() : 0;
+  r.merge_row_base = sets ? h->data.merge_base.data() : nullptr;
   r.sub_pool = reinterpret_cast<const mq_client_row*>(idx->ix->subs.m.h.data());
   r.shared_pool = reinterpret_cast<const mq_shared_row*>(idx->ix->shr.m.h.data());
   r.sub_pool_len = idx->ix->subs.m.size();
@@ -382,8 +388,15 @@ int mq_spans_expand(const mq_span_result* r, uint32_t first, uint32_t count, mq_
       }
     }
     if (w != ts.n_rows) return fail(MQ_EIO, "spans disagree with n_rows");
+    const bool set = (ts.flags & MQ_TOPIC_SET_PATCHES) != 0;
+    if (ts.n_patches && (set ? ts.patch_base + ts.n_patches > r->n_set_patches || !r->merge_row_base
+                             : ts.patch_base + ts.n_patches > r->n_patches))
+      return fail(MQ_EIO, "patch range out of bounds");
     for (uint32_t k = 0; k < ts.n_patches; k++) {
-      const mq_patch& p = r->patches[ts.patch_base + k];
+      if (set && (uint64_t)r->merge_row_base[t] + (r->set_patches[ts.patch_base + k].row >> MQ_SET_ROW_BITS) >=
+                     r->n_merge_rows)
+        return fail(MQ_EIO, "merge row out of bounds");
+      const mq_patch p = mq_topic_patch(r, t, k);
       if (p.row >= ts.n_rows) return fail(MQ_EIO, "patch row out of range");
       out[p.row].meta = p.meta;
     }

@@ -213,6 +213,8 @@ int Profiler::read(mq_kernel_time* out, uint32_t cap) {
   uint32_t n = 0;
   for (auto& t : totals_) {
     if (n >= cap) break;
+    // A name the record cannot hold whole would reach the caller under another key.
+    if (t.name.size() >= sizeof(out[n].name)) throw std::runtime_error("profile name too long: " + t.name);
     memset(&out[n], 0, sizeof(out[n]));
     strncpy(out[n].name, t.name.c_str(), sizeof(out[n].name) - 1);
     out[n].launches = t.launches;
@@ -261,6 +263,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_WALK_GROUP:
       if (v != 0 && v != 4 && v != 8 && v != 16) return false;
       walk_group_ = (uint32_t)v;
+      walk_auto_ = false;  // (a fixed choice: no trials)
       return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     default: return false;
@@ -971,6 +974,29 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   // One host synchronisation for the whole batch (at its end): device results of an index that is
   // not sharded, without inline rows or a device share pick (whose buffers the walk's totals size)
   one_sync = one_sync && !ix.sharded() && !lists && dedup_ != 0 && set_grid_;
+  sb_.trial = -1;
+  if (one_sync && walk_auto_ && n >= kWalkTrialMin) {
+    // Which walk suits this index (§4): the frontier walk with the fused desc, or the walk
+    // thread per topic + scan + desc. The first batches of each index size try both (one batch
+    // each, timed on the device); later batches take the faster per topic. A wildcard-heavy index
+    // (config 3) favours the frontier (its DFS diverges), an exact-match one (config 4, 50M IoT
+    // filters) the thread per topic (64 topics per wavefront in flight).
+    const uint64_t nodes = ix.n_nodes();
+    if (nodes > 2 * walk_trial_nodes_ || 2 * nodes < walk_trial_nodes_) {  // a new size: try again
+      walk_trial_nodes_ = nodes;
+      walk_trial_ns_[0] = walk_trial_ns_[1] = 0.0;
+    }
+    const int k = walk_trial_ns_[0] == 0.0 ? 0 : walk_trial_ns_[1] == 0.0 ? 1 : -1;
+    if (k >= 0) {
+      sb_.trial = k;
+      if (!walk_ev_[0]) {
+        hip_check(hipEventCreate(&walk_ev_[0]), "hipEventCreate");
+        hip_check(hipEventCreate(&walk_ev_[1]), "hipEventCreate");
+      }
+      hip_check(hipEventRecord(walk_ev_[0], s), "hipEventRecord");
+    }
+    walk_group_ = (k == 1 || (k < 0 && walk_trial_ns_[1] < walk_trial_ns_[0])) ? 0u : 16u;
+  }
   if (one_sync) {
     if (!h_fast_) {
       h_fast_ = static_cast<FastBack*>(pinned_alloc(sizeof(FastBack)));
@@ -1273,10 +1299,13 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
   a.g_stride = sb_.fused ? kGatherCap : 0u;
   a.exp = set_exp_;
-  pinned((2 * kPatchRegions + 1) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
+  pinned((3 * kPatchRegions + 3) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
   unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
-  uint32_t* h_err = reinterpret_cast<uint32_t*>(h_roff + kPatchRegions + 1);
+  uint32_t* h_err = reinterpret_cast<uint32_t*>(h_roff + kPatchRegions + 1);  // [2]
+  uint64_t* h_sroff = reinterpret_cast<uint64_t*>(h_err + 2);                 // [kPatchRegions + 1]
+  unsigned long long* h_mrtot = reinterpret_cast<unsigned long long*>(h_sroff + kPatchRegions + 1);  // [1]
+  if (host && one_sync) throw HipError{hipErrorInvalidValue, "host span results take the synchronised path"};
   uint64_t n_patches = 0, max_region = 0;
   // k_merge register budget: the kernel waits on memory, and eight waves per SIMD (64 VGPRs, a
   // few spills) beat six (80 VGPRs) at 1M and 10M subscriptions (4.37 -> 4.17 ms and 1.37 -> 1.27
@@ -1323,7 +1352,11 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
       uint64_t mr = 0;
       for (uint32_t r = 0; r < kPatchRegions; r++) mr = std::max<uint64_t>(mr, h_pc[r]);
-      if (mr <= srcap_) break;
+      if (mr <= srcap_) {  // the set regions' parts, for packing a host result's set patches
+        h_sroff[0] = 0;
+        for (uint32_t r = 0; r < kPatchRegions; r++) h_sroff[r + 1] = h_sroff[r] + h_pc[r];
+        break;
+      }
       if (attempt) throw HipError{hipErrorUnknown, "k_merge<spans>: set patch reservations changed between runs"};
       srcap_ = mr + mr / 4 + 64;
       dd_spatches_.release();
@@ -1345,8 +1378,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
     a.work = work0;
     a.dd_phase = 2;
-    a.set_ref = host ? 0u : 1u;  // host results get per-topic patches (copied in phase 2)
-    if (a.set_ref) {  // results that need no wavefront: k_finish, thread per topic
+    a.set_ref = 1u;  // a deduped topic references its set's patches (host results too: ABI v7)
+    {  // results that need no wavefront: k_finish, thread per topic
       grow(dd_wlist_, (size_t)n * sizeof(uint32_t));
       if (!dd_nwave_.p) dd_nwave_.ensure(sizeof(unsigned long long));
       if (!one_sync) hip_check(hipMemsetAsync(dd_nwave_.p, 0, sizeof(unsigned long long), s), "memset");
@@ -1367,6 +1400,17 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       hip_check(hipGetLastError(), "k_finish");
       a.wave_list = fa.wave_list;
       a.n_wave = fa.n_wave;
+    }
+    if (host) {  // the merge rows of the topics with a set, packed (their total read with pcount)
+      if ((uint64_t)n * kPairMax > UINT32_MAX) throw HipError{hipErrorInvalidValue, "host span batch too large"};
+      grow(mr_base_, (size_t)n * sizeof(uint32_t));
+      grow(mr_rows_, (size_t)n * kPairMax * sizeof(uint32_t));
+      if (!mr_total_.p) mr_total_.ensure(sizeof(unsigned long long));
+      hip_check(hipMemsetAsync(mr_total_.p, 0, sizeof(unsigned long long), s), "memset");
+      launch_mrow_pack(n, a.tslot, a.mcount, a.mrow, mr_base_.as<uint32_t>(), mr_rows_.as<uint32_t>(),
+                       mr_total_.as<unsigned long long>(), s);
+      hip_check(hipGetLastError(), "k_mrow_pack");
+      hip_check(hipMemcpyAsync(h_mrtot, mr_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
     }
   }
   for (int attempt = 0;; attempt++) {
@@ -1425,7 +1469,15 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     rb.out = d_fast_;
     launch_readback(rb, s);
     hip_check(hipGetLastError(), "k_readback");
+    if (sb_.trial >= 0) hip_check(hipEventRecord(walk_ev_[1], s), "hipEventRecord");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (sb_.trial >= 0 && !h_fast_->err && !h_fast_->ovf && !h_fast_->unsafe) {  // a walk trial: its time per topic
+      float ms = 0.f;
+      hip_check(hipEventElapsedTime(&ms, walk_ev_[0], walk_ev_[1]), "hipEventElapsedTime");
+      walk_trial_ns_[sb_.trial] = std::max(1e-3, 1e6 * (double)ms / n);
+      prof.count(sb_.trial ? "trial_thread_ps_per_topic" : "trial_frontier_ps_per_topic",
+                 std::max<uint64_t>(1, (uint64_t)(1e3 * walk_trial_ns_[sb_.trial])));
+    }
     if (h_fast_->err) check_err(s);  // throws with the tripped guard's name
     if (h_fast_->ovf || h_fast_->unsafe) {
       prof.count("one_sync_retries", 1);
@@ -1457,6 +1509,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     out->set_patches = reinterpret_cast<const mq_patch*>(dd_spatches_.p);
     out->merge_rows = dd_mrow_.as<uint32_t>();
     out->n_set_patches = srcap_ * kPatchRegions;
+    out->n_merge_rows = (uint64_t)n * kPairMax;  // (MQ_MERGE_ROWS_STRIDE per topic)
   }
   if (a.work) {  // MQ_PROF_WORK: k_merge's work, for its algorithmic bytes (bench.py)
     std::vector<unsigned long long> w(2 * kPatchRegions * kWork);
@@ -1499,14 +1552,43 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (out->n_picked_rows)
       hip_check(hipMemcpyAsync(host->picked.data(), sp_picked_.p, out->n_picked_rows * sizeof(ShrRec),
                                hipMemcpyDeviceToHost, s), "D2H");
+    if (sb_.dedup) {  // the set patches (their regions' parts, packed) and the packed merge rows
+      const uint64_t n_set = h_sroff[kPatchRegions];
+      host->set_patches.resize(n_set);
+      host->merge_rows.resize(*h_mrtot);
+      host->merge_base.resize(n);
+      if (n_set) {
+        grow(sp_scompact_, n_set * sizeof(PatchRec));
+        grow(sp_sroff_, kPatchRegions * sizeof(uint64_t));
+        hip_check(hipMemcpyAsync(sp_sroff_.p, h_sroff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s),
+                  "H2D");
+        launch_patch_compact(dd_spatches_.as<PatchRec>(), srcap_, a.spcount, sp_sroff_.as<uint64_t>(),
+                             sp_scompact_.as<PatchRec>(), s);
+        hip_check(hipGetLastError(), "k_patch_compact (sets)");
+        hip_check(hipMemcpyAsync(host->set_patches.data(), sp_scompact_.p, n_set * sizeof(PatchRec),
+                                 hipMemcpyDeviceToHost, s), "D2H");
+      }
+      if (*h_mrtot)
+        hip_check(hipMemcpyAsync(host->merge_rows.data(), mr_rows_.p, *h_mrtot * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, s), "D2H");
+      hip_check(hipMemcpyAsync(host->merge_base.data(), mr_base_.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
+                "D2H");
+    }
   }
   if (one_sync) return true;  // (checked above)
   hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   if (*h_err) check_err(s);  // throws with the tripped guard's name
-  if (host)
-    for (TopicSpansDev& t : host->topics)
-      if (t.n_patches) t.patch_base = h_roff[t.patch_base / rcap_] + t.patch_base % rcap_;
+  if (host) {  // patch bases into the packed arrays
+    for (TopicSpansDev& t : host->topics) {
+      if (!t.n_patches)
+        t.patch_base = 0;
+      else if (t.flags & kTopicSetPatches)
+        t.patch_base = h_sroff[t.patch_base / srcap_] + t.patch_base % srcap_;
+      else
+        t.patch_base = h_roff[t.patch_base / rcap_] + t.patch_base % rcap_;
+    }
+  }
   return true;
 }
 

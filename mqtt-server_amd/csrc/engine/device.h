@@ -101,6 +101,9 @@ struct HostSpans {
   PinnedVec<PatchRec> patches;
   PinnedVec<InlRec> inl;
   PinnedVec<ShrRec> picked;
+  PinnedVec<PatchRec> set_patches;  // merge-set patches, packed (set_patches of the result)
+  PinnedVec<uint32_t> merge_rows;   // merge rows of the topics that reference a set, packed
+  PinnedVec<uint32_t> merge_base;   //   and where each topic's start
 };
 
 // Host-side destination of a batch's results (mq_match_batch).
@@ -277,6 +280,8 @@ class Device {
   // span format outputs
   DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;
   DevBuf sp_compact_, sp_roff_;      // host results: the patch regions packed
+  DevBuf sp_scompact_, sp_sroff_;    //   the set patch regions packed
+  DevBuf mr_base_, mr_rows_, mr_total_;  // and the merge rows of the topics with a set
   DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
   // sharded: the exported list (offsets, entries, counts) and the imported lists' offsets
   DevBuf x_off_, x_ents_, x_cnt_, x_src_, x_foff_[kMaxShards - 1];
@@ -294,6 +299,7 @@ class Device {
     TopicCount* tc = nullptr;      // k_desc's per-topic counts (walk without lists), or null
     bool one_sync = false;         // one host synchronisation (spans_begin)
     bool fused = false;            // k_desc ran in the walk's epilogue: spans at t * kGatherCap
+    int trial = -1;                // a timed walk trial: 0 frontier, 1 thread per topic
   } sb_;
   // one-sync batches: values read back at the batch's end (pinned): the walk's totals, its
   // overflow and fallback counts, the *unsafe bits, the error word and the merge-set counts
@@ -322,6 +328,12 @@ class Device {
   uint32_t walk_wpe_ = 8;        // k_walk count pass register budget (MQ_OPT_WALK_WAVES)
   bool walk_lists_ = false;      // span format: the walk counts the lists (MQ_OPT_WALK_LISTS)
   uint32_t walk_group_ = 16;     // frontier walk lanes per topic (MQ_OPT_WALK_GROUP; 0: k_walk)
+  // one-sync batches choose the walk by trial (spans_begin) unless MQ_OPT_WALK_GROUP fixed it
+  bool walk_auto_ = true;
+  static constexpr uint32_t kWalkTrialMin = 65536;  // batches this large are timed for the trial
+  uint64_t walk_trial_nodes_ = 0;                    // the index size the trials ran at
+  double walk_trial_ns_[2] = {0.0, 0.0};             // batch time per topic: frontier, thread per topic
+  hipEvent_t walk_ev_[2] = {nullptr, nullptr};
   uint32_t dedup_ = 1;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
   uint32_t set_grid_ = 1;        // MQ_OPT_SET_GRID (10M: set pass 1.18 -> 1.05 ms against persistent waves)
   DevBuf dd_sig_, dd_cnt_, dd_list_, dd_mrow_, dd_keys_, dd_vals_, dd_slot_, dd_rep_, dd_nsets_, dd_rlist_;

@@ -369,6 +369,10 @@ struct FinishArgs {
   uint32_t g_stride;  // != 0: topic t's spans at t * g_stride (DescArgs.g_stride)
 };
 void launch_finish(const FinishArgs& a, hipStream_t s);
+// Host span results: pack the merge rows of the topics with a merge set (tslot != kNone),
+// mcount[t] of them from mrow[t * kPairMax]; base[t] their start, *total (zeroed) the count.
+void launch_mrow_pack(uint32_t n, const uint32_t* tslot, const uint32_t* mcount, const uint32_t* mrow,
+                      uint32_t* base, uint32_t* rows, unsigned long long* total, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
 // first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
 // fill pass must still walk; the fill pass then walks only those.

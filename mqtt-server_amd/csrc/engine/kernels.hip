@@ -1194,6 +1194,30 @@ __global__ __launch_bounds__(256) void k_finish(FinishArgs a) {
   if (wave) a.wave_list[base + prefix_before(b)] = t;
 }
 
+// Host span results (mq_match_spans): the merge rows of every topic that references its set's
+// patches, packed (topics in any order; one atomic per wavefront). base[t]: where topic t's
+// start (0 for a topic without a set); *total: the packed count.
+__global__ __launch_bounds__(256) void k_mrow_pack(uint32_t n, const uint32_t* __restrict__ tslot,
+                                                   const uint32_t* __restrict__ mcount,
+                                                   const uint32_t* __restrict__ mrow, uint32_t* __restrict__ base,
+                                                   uint32_t* __restrict__ rows, unsigned long long* total) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  const uint32_t c = t < n && tslot[t] != kNone ? mcount[t] : 0u;
+  uint32_t sum;
+  const uint32_t pre = wave_excl_scan(c, lane, &sum);
+  unsigned long long b = 0;
+  if (lane == 0 && sum) b = atomicAdd(total, (unsigned long long)sum);
+  b = __shfl(b, 0, 64) + pre;
+  if (t < n) base[t] = c ? (uint32_t)b : 0u;
+  for (uint32_t x = 0; x < c; x++) rows[b + x] = mrow[(uint64_t)t * kPairMax + x];
+}
+
+void launch_mrow_pack(uint32_t n, const uint32_t* tslot, const uint32_t* mcount, const uint32_t* mrow,
+                      uint32_t* base, uint32_t* rows, unsigned long long* total, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_mrow_pack, dim3((n + 255) / 256), dim3(256), 0, s, n, tslot, mcount, mrow, base, rows, total);
+}
+
 __global__ __launch_bounds__(256) void k_xsig(XSigArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= a.n) return;
@@ -1654,11 +1678,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint32_t rmeta = mw & ~kSlotIdentPos;
         const bool idpos = (mw & kSlotIdentPos) != 0;
         bool bound = false, base = true;
+        // (span format) a visit through a partner that is not the record's first gathered one
+        // counts and emits nothing: it stops at that first one (the row format rewrites the row on
+        // every visit, so it reads every link)
+        bool other = false;
         uint32_t first = kNone;
         uint32_t q = rmeta & kMetaQos, nl = rmeta & kMetaNoLocal;
         if (SET && (a.exp & 1u)) mp_cnt = 0;
         // partner links in batches of kPartBatch independent loads (one latency per batch)
-        for (uint32_t e0 = 0; e0 < mp_cnt && base; e0 += kPartBatch) {
+        for (uint32_t e0 = 0; e0 < mp_cnt && base && !other; e0 += kPartBatch) {
           MergePart pb[kPartBatch];
 #pragma unroll
           for (uint32_t u = 0; u < kPartBatch; u++)
@@ -1666,14 +1694,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           w_link += min(kPartBatch, mp_cnt - e0);
 #pragma unroll
           for (uint32_t u = 0; u < kPartBatch; u++) {
-            if (!base || pb[u].node == kNone) continue;
+            if (!base || other || pb[u].node == kNone) continue;
             if (SET && (a.exp & 2u)) {
               q = max(q, pb[u].meta & kMetaQos);
               continue;
             }
             const Pos ph = gathered(pb[u].node);
             if (!ph.found) continue;
-            if (!bound) first = pb[u].node;
+            if (!bound) {
+              first = pb[u].node;
+              other = SPANS && via != kNone && first != via && !(SET && (a.exp & 16u));
+            }
             bound = true;
             if (before(ph.rk, ph.gi, rg, gi)) {
               base = false;

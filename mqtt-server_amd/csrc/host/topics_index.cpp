@@ -368,7 +368,10 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const PackedTopics& topic
     const mq_topic_spans& ts = r->topics[t];
     Subscribers& s = out[t];
     patched.clear();
-    for (uint32_t k = 0; k < ts.n_patches; k++) patched[r->patches[ts.patch_base + k].row] = r->patches[ts.patch_base + k].meta;
+    for (uint32_t k = 0; k < ts.n_patches; k++) {  // own or merge-set patches (mq_topic_patch)
+      const mq_patch p = mq_topic_patch(r, (uint32_t)t, k);
+      patched[p.row] = p.meta;
+    }
     // records in gather order: a client's client row precedes its ident rows
     uint32_t rowi = 0;
     for (uint32_t k = 0; k < ts.n_spans; k++) {

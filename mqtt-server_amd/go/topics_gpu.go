@@ -568,7 +568,7 @@ func (b *MatchBatcher) loop() {
 }
 
 // SubscribersBatch matches many topics in one engine call (span format: the index's own
-// records plus per-topic patches, include/mqmatch.h); the batching stage in
+// records plus patches, per topic or shared by a merge set, include/mqmatch.h); the batching stage in
 // publishToSubscribers (server.go:984-1021) feeds it. A subscription removed between the match
 // and the rebuild below is rebuilt from its record.
 func (x *TopicsIndex) SubscribersBatch(topics []string) []*Subscribers {
@@ -582,6 +582,15 @@ func (x *TopicsIndex) SubscribersBatch(topics []string) []*Subscribers {
 	ts := unsafe.Slice(r.topics, int(r.n_topics))
 	spans := unsafe.Slice(r.spans, int(r.n_spans))
 	patches := unsafe.Slice(r.patches, int(r.n_patches))
+	// merge-set patches (MQ_TOPIC_SET_PATCHES): row x<<MQ_SET_ROW_BITS|k is record k of the
+	// topic's x-th may-merge particle, whose first row is merge_rows[merge_row_base[topic]+x]
+	setPatches := unsafe.Slice(r.set_patches, int(r.n_set_patches))
+	mergeRows := unsafe.Slice(r.merge_rows, int(r.n_merge_rows))
+	var mergeBase []C.uint32_t
+	if r.merge_row_base != nil {
+		mergeBase = unsafe.Slice(r.merge_row_base, int(r.n_topics))
+	}
+	const rowBits = uint32(C.MQ_SET_ROW_BITS)
 	inl := unsafe.Slice(r.inline_rows, int(r.n_inline_rows))
 	picked := unsafe.Slice(r.picked_rows, int(r.n_picked_rows))
 	subPool := unsafe.Slice(r.sub_pool, int(r.sub_pool_len))
@@ -607,8 +616,16 @@ func (x *TopicsIndex) SubscribersBatch(topics []string) []*Subscribers {
 			InlineSubscriptions: map[int]InlineSubscription{},
 		}
 		clear(patched)
-		for _, pt := range patches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
-			patched[uint32(pt.row)] = uint32(pt.meta)
+		if t.flags&C.MQ_TOPIC_SET_PATCHES != 0 {
+			mr := mergeRows[mergeBase[i]:]
+			for _, pt := range setPatches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
+				row := uint32(pt.row)
+				patched[uint32(mr[row>>rowBits])+row&(1<<rowBits-1)] = uint32(pt.meta)
+			}
+		} else {
+			for _, pt := range patches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
+				patched[uint32(pt.row)] = uint32(pt.meta)
+			}
 		}
 		addShared := func(sr C.mq_shared_row) {
 			f, c := x.filters.strs[sr.filter_id], x.clients.strs[sr.client_id]

@@ -68,7 +68,8 @@ class SpanResult(C.Structure):
                 ("sub_pool", C.c_void_p), ("shared_pool", C.c_void_p), ("n_spans", C.c_uint64),
                 ("n_patches", C.c_uint64), ("n_inline_rows", C.c_uint64), ("n_picked_rows", C.c_uint64),
                 ("sub_pool_len", C.c_uint64), ("shared_pool_len", C.c_uint64),
-                ("set_patches", C.c_void_p), ("merge_rows", C.c_void_p), ("n_set_patches", C.c_uint64)]
+                ("set_patches", C.c_void_p), ("merge_rows", C.c_void_p), ("n_set_patches", C.c_uint64),
+                ("merge_row_base", C.c_void_p), ("n_merge_rows", C.c_uint64)]
 
 
 SPANS_PICKED = 1  # MQ_SPANS_PICKED
@@ -392,7 +393,8 @@ class Engine:
 
     def match_spans(self, bytes_, offs):
         """mq_match_spans -> dict of numpy copies of the span-format result (topics as a
-        structured array, spans [n,4], patches [n,2], inline rows, picked rows, flags)."""
+        structured array, spans [n,4], patches [n,2], inline rows, picked rows, flags, and the
+        merge-set patches with the packed merge rows; host_topic_patches() resolves both kinds)."""
         n = len(offs) - 1
         rp = C.POINTER(SpanResult)()
         _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
@@ -428,7 +430,8 @@ class Engine:
         _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
         try:
             r = rp.contents
-            nbytes = 64 * n + 16 * r.n_spans + 8 * r.n_patches + 8 * r.n_inline_rows + 8 * r.n_picked_rows
+            nbytes = (64 * n + 16 * r.n_spans + 8 * r.n_patches + 8 * r.n_inline_rows + 8 * r.n_picked_rows
+                      + 8 * r.n_set_patches + 4 * r.n_merge_rows + (4 * n if r.merge_row_base else 0))
             done = 0
             if expand and n:
                 buf = (C.c_char * (n * 64)).from_address(r.topics)
@@ -651,7 +654,32 @@ def _span_arrays(r, n):
         "inline": arr(r.inline_rows, int(r.n_inline_rows), np.uint32, 2),
         "picked": arr(r.picked_rows, int(r.n_picked_rows), np.uint32, 2),
         "flags": int(r.flags),
+        "set_patches": arr(r.set_patches, int(r.n_set_patches), np.uint32, 2),
+        "merge_rows": arr(r.merge_rows, int(r.n_merge_rows), np.uint32),
+        "merge_base": arr(r.merge_row_base, n if r.merge_row_base else 0, np.uint32),
     }
+
+
+def host_topic_patches(a):
+    """Every patch of a match_spans() dict as (topic, topic row, meta) arrays: the topics' own
+    patches and, for MQ_TOPIC_SET_PATCHES topics, their merge set's patches with rows translated
+    through the topic's packed merge rows (include/mqmatch.h mq_topic_patch)."""
+    t = a["topics"]
+    n = len(t)
+    setf = (t["flags"] & 1) != 0
+    tids, rows, metas = [], [], []
+    for own in (True, False):
+        sel = ~setf if own else setf
+        tid = np.repeat(np.arange(n)[sel], t["n_patches"][sel].astype(np.int64))
+        pr = (a["patches"] if own else a["set_patches"])[_ranges(t["patch_base"][sel], t["n_patches"][sel])]
+        row = pr[:, 0].astype(np.int64)
+        if not own and len(row):
+            row = a["merge_rows"][a["merge_base"][tid].astype(np.int64) + (row >> 26)].astype(np.int64) \
+                + (row & ((1 << 26) - 1))
+        tids.append(tid)
+        rows.append(row)
+        metas.append(pr[:, 1])
+    return np.concatenate(tids), np.concatenate(rows), np.concatenate(metas)
 
 
 def _expand_host_spans(rp, n):

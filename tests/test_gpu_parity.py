@@ -335,21 +335,27 @@ def test_spans_patch_pool_growth(gpu_available):
 def test_spans_format_shape(gpu_available):
     """The span format itself: spans in gather order cover exactly n_rows records, patch rows are
     in range and unique per topic, and a topic without co-matching records has no patches."""
+    from mqmatch import engine as E
     from mqmatch import workload as W
     w, eng, orc = _workload_pair(40000, 4000, seed=49)
     tb, to = W.gen_topics(w, 3000, seed=50)
     a = eng.match_spans(tb, to)
-    t, spans, patches = a["topics"], a["spans"], a["patches"]
+    t, spans = a["topics"], a["spans"]
+    tid, prow, pmeta = E.host_topic_patches(a)
+    assert len(tid) == int(t["n_patches"].sum())
     for i in range(len(t)):
         sp = spans[int(t["span_base"][i]):int(t["span_base"][i]) + int(t["n_spans"][i])]
         assert int(sp[:, 1].sum()) == int(t["n_rows"][i])
         assert int(sp[:, 3].sum()) == int(t["n_shared"][i])
-        pr = patches[int(t["patch_base"][i]):int(t["patch_base"][i]) + int(t["n_patches"][i]), 0]
+        pr, pm = prow[tid == i], pmeta[tid == i]
         assert len(set(pr.tolist())) == len(pr) and (pr < max(1, int(t["n_rows"][i]))).all()
         if int(t["n_client"][i]) == int(t["n_rows"][i]):
-            assert all((patches[int(t["patch_base"][i]) + k, 1] & 0xC0000000) == 0 for k in range(len(pr)))
+            assert ((pm & 0xC0000000) == 0).all()
+    # host results share merge-set patches as device results do (ABI v7)
+    assert ((t["flags"] & 1) != 0).any() and len(a["merge_base"]) == len(t)
     rows_bytes = 16 * int(t["n_rows"].sum())
-    span_bytes = 64 * len(t) + 16 * len(spans) + 8 * len(patches)
+    span_bytes = (64 * len(t) + 16 * len(spans) + 8 * len(a["patches"]) + 8 * len(a["set_patches"])
+                  + 4 * len(a["merge_rows"]) + 4 * len(a["merge_base"]))
     assert span_bytes * 4 < rows_bytes  # the point of the format
 
 
@@ -378,15 +384,17 @@ def test_spans_device_matches_host(gpu_available):
     # desc's stride layout; host results are packed)
     sb, ns = got["span_base"].astype(np.int64), got["n_spans"].astype(np.int64)
     ext = int((sb + ns).max())
-    assert r.n_spans >= ext and r.n_patches >= int(host["topics"]["n_patches"].sum())
+    own = (host["topics"]["flags"] & 1) == 0
+    assert (got["flags"] == host["topics"]["flags"]).all()
+    assert r.n_spans >= ext and r.n_patches >= int(host["topics"]["n_patches"][own].sum())
     dsp = torch.empty(ext * 4, dtype=torch.int32, device="cuda")
     assert hip.hipMemcpy(dsp.data_ptr(), r.spans, ext * 16, 3) == 0
     dsp = dsp.cpu().numpy().view(np.uint32).reshape(-1, 4)
     assert (dsp[E._ranges(sb, ns)] == host["spans"]).all()
 
 
-@pytest.mark.parametrize("dedup,fuse", [(1, 1), (1, 0), (0, 1)])
-def test_spans_device_digest_parity(dedup, fuse, gpu_available):
+@pytest.mark.parametrize("dedup,fuse,group", [(1, 1, 16), (1, 0, 16), (0, 1, 16), (1, 1, 0)])
+def test_spans_device_digest_parity(dedup, fuse, group, gpu_available):
     """mq_match_spans_device expanded as a device consumer would (spans, then per-topic patches or
     set-shared patches through the topic's merge rows, inline rows): per-topic digests equal the
     oracle's. With merge-set dedup (the default) topics share their merge set's patches
@@ -398,6 +406,7 @@ def test_spans_device_digest_parity(dedup, fuse, gpu_available):
     w, eng, orc = _workload_pair(60000, 3000, seed=63)
     eng.set_option(E.OPT_MERGE_DEDUP, dedup)
     eng.set_option(E.OPT_FUSE_DESC, fuse)
+    eng.set_option(E.OPT_WALK_GROUP, group)  # 0: the walk thread per topic (+ scan + k_desc)
     tb, to = W.gen_topics(w, 6000, seed=64)
     n = len(to) - 1
     d_tb = torch.from_numpy(tb).cuda()
@@ -410,6 +419,29 @@ def test_spans_device_digest_parity(dedup, fuse, gpu_available):
     od, ocnt, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
     bad = np.nonzero(dg != od)[0]
     assert len(bad) == 0, f"{len(bad)} of {n} topics differ (first {bad[:5]})"
+
+
+def test_walk_trials_choose_and_stay_exact(gpu_available):
+    """Device batches of 64k+ topics time both walks on their first batches (the frontier walk with
+    the fused desc, the walk thread per topic with scan + desc) and keep the faster: every batch,
+    trial or not, equals the oracle, and both trials ran."""
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(20000, 2000, seed=81)
+    tb, to = W.gen_topics(w, 70000, seed=82)
+    n = len(to) - 1
+    d_tb = torch.from_numpy(tb).cuda()
+    d_to = torch.from_numpy(to.view(np.int64)).cuda()
+    od, _, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+    eng.profile(True)
+    for _ in range(4):
+        torch.cuda.synchronize()
+        r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
+        dg, _ = engine_digests(E.expand_device_spans(r, n))
+        assert (dg == od).all()
+    prof = eng.profile_read()
+    assert "trial_frontier_ps_per_topic" in prof and "trial_thread_ps_per_topic" in prof, sorted(prof)
 
 
 @pytest.mark.parametrize("fuse", [0, 1])

@@ -43,8 +43,11 @@ def test_headline_10m_subscriptions(gpu_available):
     t = a["topics"]
     assert (t["n_client"] <= t["n_rows"]).all() and (t["n_ident"] <= t["n_rows"] - t["n_client"]).all()
     # patch ranges are reserved per topic before resolving (hit-list records); the written part
-    # of each range is n_patches
-    assert int(t["n_spans"].sum()) == len(a["spans"]) and int(t["n_patches"].sum()) <= len(a["patches"])
+    # of each range is n_patches; topics of a merge set name its patches (packed, ABI v7)
+    setf = (t["flags"] & 1) != 0
+    assert int(t["n_spans"].sum()) == len(a["spans"]) and int(t["n_patches"][~setf].sum()) <= len(a["patches"])
+    tid, prow, _ = E.host_topic_patches(a)
+    assert len(tid) == int(t["n_patches"].sum()) and (prow < t["n_rows"][tid]).all()
     sb, ns = t["span_base"].astype(np.int64), t["n_spans"].astype(np.int64)
     cs = np.concatenate(([0], np.cumsum(a["spans"][:, 1].astype(np.int64))))
     assert (cs[sb + ns] - cs[sb] == t["n_rows"]).all()  # spans cover exactly the gathered records
