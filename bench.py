@@ -184,23 +184,26 @@ def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step):
 def spans_roofline(prof, work, steps, n, n_subs):
     """Roofline of the span format's merge stage, k_merge<spans>: with merge-set dedup (the
     default) two launches per step — the set pass (one resolution per distinct merge set) and the
-    topic pass (the other topics, set references, result records). Its algorithmic bytes per step
-     are what it must read and write for the step's topics: 40 B of offsets and a
-    64 B result record per topic, the 32 B GDesc of every gather, 16 B per pair-table entry
-    probed, 16 B per pair slot resolved, 8 B per partner link, 8 B per patch — priced from the
-    work counters of an extra step (the same batch, so the same work) — over the two launches'
-    time from HIP events in the timed region. Latency-bound (dependent probes of hash tables and
+    topic pass (the topics k_finish left: inline rows, or beyond the dedup). Its algorithmic bytes
+    per step are what the two launches read and write for the topics they resolve
+    (k_finish, a separate kernel, writes every other topic's record): 64 B per topic resolved
+    (its counts and set slot read, its result record or SetInfo written), its map's sources (16 B
+    per merge gather from the dedup lists, or the 32 B GDesc of every gather), 16 B per
+    pair-table entry probed, 16 B per pair slot resolved, 8 B per partner link, 8 B per patch —
+    priced from the work counters of an extra step (the same batch, so the same work) — over the
+    two launches' time from HIP events in the timed region. Latency-bound (dependent probes of hash tables and
     lists), so the HBM fraction is low by nature; the step's other kernels are walk, desc, dedup."""
     launches, ms = prof.get("merge", (0, 0.0))
     set_launches, set_ms = prof.get("merge_sets", (0, 0.0))
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
             "traffic": None, "kernel": "k_merge<spans>" + (" (set pass + topic pass)" if set_launches else ""),
-            "bytes": "offsets + result + GDesc + pair entries + pair slots + partner links + patches"}
+            "bytes": "per topic resolved: counts + result/SetInfo + map sources; pair entries + pair slots + "
+                     "partner links + patches"}
     if not launches or ms <= 0:
         return roof
     g = lambda k: work.get(k, (0, 0.0))[0]
-    per_step = (104 * n + 32 * g("gathers") + 16 * g("merge_pair_entries") + 16 * g("merge_records")
-                + 8 * g("merge_links") + 8 * g("merge_patches"))
+    per_step = (64 * g("merge_topics_resolved") + g("merge_map_bytes") + 16 * g("merge_pair_entries")
+                + 16 * g("merge_records") + 8 * g("merge_links") + 8 * g("merge_patches"))
     step_ms = (ms + set_ms) / max(1, steps)
     achieved = per_step / (step_ms * 1e-3) / 1e9
     traffic = read_spans_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n) if set_launches else None
@@ -478,7 +481,8 @@ def main():
         work = eng.profile_read()
         eng.profile(False)
         out["roofline"] = spans_roofline(prof, work, args.steps, n, args.subs)
-        out["merge_work_per_topic"] = {k[6:]: work[k][0] / n for k in work if k.startswith("merge_") and k != "merge_topics"}
+        out["merge_work_per_topic"] = {k[6:]: work[k][0] / n for k in work
+                                       if k.startswith("merge_") and k not in ("merge_topics", "merge_sets")}
     else:
         out["roofline"] = rows_roofline(prof, args, elapsed, out)
     cpu = None
@@ -565,6 +569,7 @@ def main():
             t0 = time.perf_counter()
             nbytes, _ = eng.match_spans_host(tb, to)
             dt = time.perf_counter() - t0
+            parts = dict(eng.last_host_bytes)
             ne_h = n
             ne = min(n, 200000)
             t0 = time.perf_counter()
@@ -576,6 +581,7 @@ def main():
             dtn = time.perf_counter() - t0
             out["end_to_end"] = {"value": ne_h / dt, "unit": "publishes/s", "sample_topics": ne_h,
                                  "result_bytes": nbytes, "bytes_per_topic": nbytes / ne_h, "GBps_to_host": nbytes / dt / 1e9,
+                                 "bytes_per_topic_by_array": {k: v / ne_h for k, v in parts.items()},
                                  "expanded": {"value": ne / dtx, "rows": nrows, "host_threads": 1, "sample_topics": ne,
                                               "rows_GBps": 16 * nrows / dtx / 1e9},
                                  "expanded_threads": {"value": ne / dtn, "rows": nrows_n, "host_threads": th, "sample_topics": ne,

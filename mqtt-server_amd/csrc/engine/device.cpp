@@ -1526,6 +1526,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.count("set_cycles_pairs", sum[5]);
     prof.count("set_cycles_resolve", sum[6]);
     prof.count("set_cycles_total", sum[7]);
+    prof.count("merge_topics_resolved", sum[8]);
+    prof.count("merge_map_bytes", sum[9]);
     prof.count("merge_topics", n);
   }
   if (host) {

@@ -30,7 +30,8 @@ constexpr uint32_t kPartBatch = 4;     // partner links loaded together per reco
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
-constexpr uint32_t kWork = 8;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set)
+constexpr uint32_t kWork = 10;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
+                                // [8] topics the kernel resolved, [9] bytes of their maps' sources read
 constexpr uint32_t kMergeWavesPerEU = 8;  // k_merge<spans> register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.

@@ -1464,6 +1464,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t n_patch = 0;
   bool pfit = true;      // the reservation fits the pool
   uint32_t w_ent = 0, w_rec = 0, w_link = 0;  // this lane's work (MQ_PROF_WORK)
+  uint32_t w_map = 0;  // bytes of the map's sources read (merge lists or GDesc records; wave-uniform)
 
   // reserve n patch slots for this topic in its region (wave-uniform). The atomic's answer is
   // taken only when the first patch is written (settle): by then the pair-slot loads issued
@@ -1548,6 +1549,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         mg_emask[wv][lane] = P.y;
       }
       n_map = lc;
+      w_map = (XS ? 24u : 16u) * lc;
     } else {
     if (a.unsafe && o1.g > a.desc_cap) {  // one-sync batch: no GDesc records to read
       if (lane == 0) atomicOr(a.unsafe, kUnsafeDesc);
@@ -1555,6 +1557,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
     for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
     wave_sync_lds();
+    w_map = (uint32_t)sizeof(GDesc) * n_g;
     for (uint32_t i0 = 0; i0 < n_g; i0 += 64) {
       const uint32_t i = i0 + lane;
       bool ins = false;
@@ -1757,7 +1760,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           return a.ix.plist[h_off[wv][lo] + (rc - h_pre[wv][lo])];
         };
         // software-pipelined by one round: the next 64 records' pair slots are loaded before
-        // this round's partner links, so each round waits on one load latency, not two
+        // this round's partner links, so each round waits on one load latency, not two (two
+        // rounds, with the next round's first links in flight too, spilled registers and was
+        // slower: 1.15 -> 1.36 ms at 8 waves per SIMD, 1.24 ms at 6; profiles/r03/s2_hostsets/)
         uint32_t jj_next = 0;
         PairSlot e_next = locate(lane, jj_next);
         for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
@@ -1892,6 +1897,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         atomicAdd(wc + 2, (unsigned long long)l);
         atomicAdd(wc + 3, (unsigned long long)n_patch);
       }
+      if (lane == 0) {
+        atomicAdd(wc + 8, 1ull);
+        if (w_map) atomicAdd(wc + 9, (unsigned long long)w_map);
+      }
       const uint64_t c_end = clock64();
       if (lane == 0 && c_pairs != c_start) {  // (the map / pair-analysis path)
         atomicAdd(wc + 4, (unsigned long long)(c_map - c_start));
@@ -1931,6 +1940,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       atomicAdd(wc + 1, (unsigned long long)rr);
       atomicAdd(wc + 2, (unsigned long long)l);
       atomicAdd(wc + 3, (unsigned long long)n_patch);
+    }
+    if (lane == 0) {
+      atomicAdd(wc + 8, 1ull);
+      if (w_map) atomicAdd(wc + 9, (unsigned long long)w_map);
     }
   }
 

@@ -178,7 +178,8 @@ class TopicView {
   void for_each_row(F&& f) const {
     const mq_span_result& r = b_->result();
     const mq_topic_spans& ts = spans();
-    std::vector<mq_patch> p(r.patches + ts.patch_base, r.patches + ts.patch_base + ts.n_patches);
+    std::vector<mq_patch> p(ts.n_patches);  // own or merge-set patches (mq_topic_patch)
+    for (uint32_t k = 0; k < ts.n_patches; k++) p[k] = mq_topic_patch(&r, t_, k);
     std::sort(p.begin(), p.end(), [](const mq_patch& a, const mq_patch& b) { return a.row < b.row; });
     size_t pi = 0;
     uint32_t row = 0;

@@ -430,8 +430,12 @@ class Engine:
         _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
         try:
             r = rp.contents
-            nbytes = (64 * n + 16 * r.n_spans + 8 * r.n_patches + 8 * r.n_inline_rows + 8 * r.n_picked_rows
-                      + 8 * r.n_set_patches + 4 * r.n_merge_rows + (4 * n if r.merge_row_base else 0))
+            parts = {"topics": 64 * n, "spans": 16 * r.n_spans, "patches": 8 * r.n_patches,
+                     "inline_rows": 8 * r.n_inline_rows, "picked_rows": 8 * r.n_picked_rows,
+                     "set_patches": 8 * r.n_set_patches, "merge_rows": 4 * r.n_merge_rows,
+                     "merge_row_base": 4 * n if r.merge_row_base else 0}
+            self.last_host_bytes = parts  # the result's bytes per array (bench.py's end_to_end)
+            nbytes = sum(parts.values())
             done = 0
             if expand and n:
                 buf = (C.c_char * (n * 64)).from_address(r.topics)

@@ -393,6 +393,32 @@ def test_spans_device_matches_host(gpu_available):
     assert (dsp[E._ranges(sb, ns)] == host["spans"]).all()
 
 
+@pytest.mark.parametrize("exp,waves", [(16, 8), (0, 6)])
+def test_set_pass_variants_exact(exp, waves, gpu_available):
+    """The merge set pass's exact variants: MQ_OPT_SET_EXP bit 4 (a visit through a partner other
+    than the record's first reads all its links), and 6 waves per SIMD (MQ_OPT_MERGE_WAVES):
+    per-topic digests of device results equal the oracle's."""
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(60000, 3000, seed=65)
+    eng.set_option(E.OPT_SET_EXP, exp)
+    eng.set_option(E.OPT_MERGE_WAVES, waves)
+    tb, to = W.gen_topics(w, 6000, seed=66)
+    n = len(to) - 1
+    d_tb = torch.from_numpy(tb).cuda()
+    d_to = torch.from_numpy(to.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    od, _, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+    for _ in range(2):  # (the second batch: one synchronisation, sized by the first)
+        r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
+        res = E.expand_device_spans(r, n)
+        assert res["set_topics"] > 0
+        dg, _ = engine_digests(res)
+        bad = np.nonzero(dg != od)[0]
+        assert len(bad) == 0, f"{len(bad)} of {n} topics differ (first {bad[:5]})"
+
+
 @pytest.mark.parametrize("dedup,fuse,group", [(1, 1, 16), (1, 0, 16), (0, 1, 16), (1, 1, 0)])
 def test_spans_device_digest_parity(dedup, fuse, group, gpu_available):
     """mq_match_spans_device expanded as a device consumer would (spans, then per-topic patches or

@@ -1,7 +1,7 @@
 # Round 3 (session 2): host span results with merge-set patches (ABI v7). Standalone C++ mirror
 # test (SubscribersBatch reads host results), smoke, the whole GPU suite, the default bench line
 # (its end_to_end leg: spans through host memory on the whole batch), then the set pass's early
-# stop A/B (MQ_OPT_SET_EXP bit 4 turns it off) on the same box.
+# stop A/B (MQ_OPT_SET_EXP bit 4 turns it off) and the link prefetch (bit 5) on the same box.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 D=$R/gpurun_out/${1:-r3za}
@@ -14,5 +14,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout
 tail -3 $D/pytest_gpu.log
 timeout -k 10 400 python -u bench.py > $D/bench_default.json 2> $D/bench_default.err || { echo "bench rc=$?"; tail -5 $D/bench_default.err; exit 1; }
 cut -c1-600 $D/bench_default.json
-timeout -k 10 400 python -u tools/tune_spans.py --subs 10000000 --configs "18=0;18=16" --reps 3 > $D/early_stop_ab.jsonl 2> $D/early_stop_ab.err || { echo "ab rc=$?"; tail -5 $D/early_stop_ab.err; exit 1; }
+timeout -k 10 400 python -u tools/tune_spans.py --subs 10000000 --configs "18=0,7=8;18=16,7=8;18=32,7=8;18=32,7=6" --reps 3 > $D/early_stop_ab.jsonl 2> $D/early_stop_ab.err || { echo "ab rc=$?"; tail -5 $D/early_stop_ab.err; exit 1; }
 cut -c1-300 $D/early_stop_ab.jsonl
