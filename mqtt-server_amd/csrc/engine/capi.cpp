@@ -318,9 +318,10 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
     std::unique_ptr<SpanHolder> h(new SpanHolder());
     const uint8_t* dtb = nullptr;
     const uint64_t* dto = nullptr;
-    if (n) d.stage_inputs(tb, to, n, nullptr, &dtb, &dto);
+    hipStream_t hs = d.host_stream();
+    if (n) d.stage_inputs(tb, to, n, hs, &dtb, &dto);
     mq_span_result dev_out;
-    d.match_spans(*idx->ix, dtb, dto, n, nullptr, &h->data, &dev_out);
+    d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out);
     return publish_host_spans(idx, std::move(h), dev_out, out);
   }, Access::kPin);
 }

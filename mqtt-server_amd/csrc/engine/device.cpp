@@ -292,7 +292,9 @@ Device::~Device() {
     if (merge_done_[k]) (void)hipEventDestroy(merge_done_[k]);
   }
   if (side_done_) (void)hipEventDestroy(side_done_);
+  if (spans_ev_) (void)hipEventDestroy(spans_ev_);
   if (side_) (void)hipStreamDestroy(side_);
+  if (hstream_) (void)hipStreamDestroy(hstream_);
   if (wstream_) (void)hipStreamDestroy(wstream_);
   if (ev_in_) (void)hipEventDestroy(ev_in_);
   for (hipEvent_t e : ev_scan_) (void)hipEventDestroy(e);
@@ -506,9 +508,19 @@ static void grow(DevBuf& b, size_t bytes) {
   b.ensure(bytes);
 }
 
+hipStream_t Device::host_stream() {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  if (!hstream_) hip_check(hipStreamCreateWithFlags(&hstream_, hipStreamNonBlocking), "hipStreamCreate");
+  return hstream_;
+}
+
 void Device::ensure_streams() {
   if (side_) return;
-  hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate");
+  // the side stream at the greatest priority: a hardware queue of its own, so its copies run
+  // beside the other streams' kernels instead of in turn with them on a shared queue
+  int least = 0, greatest = 0;
+  hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+  hip_check(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, greatest), "hipStreamCreate");
   hip_check(hipStreamCreateWithFlags(&wstream_, hipStreamNonBlocking), "hipStreamCreate");
   for (int k = 0; k < 2; k++) {
     hip_check(hipEventCreateWithFlags(&copy_done_[k], hipEventDisableTiming), "hipEventCreate");
@@ -516,6 +528,7 @@ void Device::ensure_streams() {
     hip_check(hipEventCreateWithFlags(&sb_done_[k], hipEventDisableTiming), "hipEventCreate");
   }
   hip_check(hipEventCreateWithFlags(&side_done_, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&spans_ev_, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
 }
 
@@ -1175,6 +1188,26 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   if (nf && !ix.sharded()) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
   if (n == 0) return true;
   const bool one_sync = sb_.one_sync;
+  // host results: the spans are final once k_desc has run (spans_begin), so their copy to the
+  // host runs on the side stream under the dedup and merge kernels (joined before the end)
+  const bool early_spans = host && !one_sync && tot.g;
+  struct SideJoin {  // however this call ends, the copy into *host is done before *host can go
+    hipStream_t st;
+    bool on;
+    ~SideJoin() {
+      if (on) (void)hipStreamSynchronize(st);
+    }
+  } side_join{side_, false};
+  if (early_spans) {
+    ensure_streams();
+    host->spans.resize(tot.g);
+    hip_check(hipEventRecord(spans_ev_, s), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(side_, spans_ev_, 0), "hipStreamWaitEvent");
+    hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, side_),
+              "D2H spans");
+    hip_check(hipEventRecord(side_done_, side_), "hipEventRecord");
+    side_join = SideJoin{side_, true};
+  }
 
   EmitArgs a;
   memset(&a, 0, sizeof(a));
@@ -1299,12 +1332,12 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
   a.g_stride = sb_.fused ? kGatherCap : 0u;
   a.exp = set_exp_;
-  pinned((3 * kPatchRegions + 3) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
+  pinned((2 * kPatchRegions + 3) * sizeof(unsigned long long) + 2 * sizeof(uint32_t));
   unsigned long long* h_pc = static_cast<unsigned long long*>(h_pin_);        // [kPatchRegions]
   uint64_t* h_roff = reinterpret_cast<uint64_t*>(h_pc + kPatchRegions);       // [kPatchRegions + 1]
   uint32_t* h_err = reinterpret_cast<uint32_t*>(h_roff + kPatchRegions + 1);  // [2]
-  uint64_t* h_sroff = reinterpret_cast<uint64_t*>(h_err + 2);                 // [kPatchRegions + 1]
-  unsigned long long* h_mrtot = reinterpret_cast<unsigned long long*>(h_sroff + kPatchRegions + 1);  // [1]
+  unsigned long long* h_mrtot = reinterpret_cast<unsigned long long*>(h_err + 2);  // [1]
+  unsigned long long* h_stot = h_mrtot + 1;                                         // [1]
   if (host && one_sync) throw HipError{hipErrorInvalidValue, "host span results take the synchronised path"};
   uint64_t n_patches = 0, max_region = 0;
   // k_merge register budget: the kernel waits on memory, and eight waves per SIMD (64 VGPRs, a
@@ -1352,11 +1385,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
       uint64_t mr = 0;
       for (uint32_t r = 0; r < kPatchRegions; r++) mr = std::max<uint64_t>(mr, h_pc[r]);
-      if (mr <= srcap_) {  // the set regions' parts, for packing a host result's set patches
-        h_sroff[0] = 0;
-        for (uint32_t r = 0; r < kPatchRegions; r++) h_sroff[r + 1] = h_sroff[r] + h_pc[r];
-        break;
-      }
+      if (mr <= srcap_) break;
       if (attempt) throw HipError{hipErrorUnknown, "k_merge<spans>: set patch reservations changed between runs"};
       srcap_ = mr + mr / 4 + 64;
       dd_spatches_.release();
@@ -1400,6 +1429,16 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       hip_check(hipGetLastError(), "k_finish");
       a.wave_list = fa.wave_list;
       a.n_wave = fa.n_wave;
+    }
+    if (host) {  // the sets' written patches, packed (their total read with pcount)
+      grow(set_nbase_, (size_t)n * sizeof(uint64_t));
+      grow(sp_scompact_, srcap_ * kPatchRegions * sizeof(PatchRec));  // (at most every reservation)
+      if (!set_total_.p) set_total_.ensure(sizeof(unsigned long long));
+      hip_check(hipMemsetAsync(set_total_.p, 0, sizeof(unsigned long long), s), "memset");
+      launch_set_pack(n, a.tslot, a.rep, a.sets, dd_spatches_.as<PatchRec>(), set_nbase_.as<uint64_t>(),
+                      sp_scompact_.as<PatchRec>(), set_total_.as<unsigned long long>(), s);
+      hip_check(hipGetLastError(), "k_set_pack");
+      hip_check(hipMemcpyAsync(h_stot, set_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
     }
     if (host) {  // the merge rows of the topics with a set, packed (their total read with pcount)
       if ((uint64_t)n * kPairMax > UINT32_MAX) throw HipError{hipErrorInvalidValue, "host span batch too large"};
@@ -1531,14 +1570,15 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.count("merge_topics", n);
   }
   if (host) {
+    if (sb_.dedup) {  // the set topics' patch_base into the packed set patches
+      launch_set_rebase(n, a.rep, set_nbase_.as<uint64_t>(), a.sres, s);
+      hip_check(hipGetLastError(), "k_set_rebase");
+    }
     host->topics.resize(n);
-    host->spans.resize(tot.g);
     host->patches.resize(n_patches);
     host->inl.resize(tot.inl);
     host->picked.resize(out->n_picked_rows);
     hip_check(hipMemcpyAsync(host->topics.data(), a.sres, n * sizeof(TopicSpansDev), hipMemcpyDeviceToHost, s), "D2H");
-    if (tot.g)
-      hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, s), "D2H");
     if (n_patches) {  // the regions' used parts, packed; patch_base is remapped below
       grow(sp_compact_, n_patches * sizeof(PatchRec));
       grow(sp_roff_, kPatchRegions * sizeof(uint64_t));
@@ -1554,22 +1594,14 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (out->n_picked_rows)
       hip_check(hipMemcpyAsync(host->picked.data(), sp_picked_.p, out->n_picked_rows * sizeof(ShrRec),
                                hipMemcpyDeviceToHost, s), "D2H");
-    if (sb_.dedup) {  // the set patches (their regions' parts, packed) and the packed merge rows
-      const uint64_t n_set = h_sroff[kPatchRegions];
+    if (sb_.dedup) {  // the sets' written patches and the merge rows (packed by k_set_pack, k_mrow_pack)
+      const uint64_t n_set = *h_stot;
       host->set_patches.resize(n_set);
       host->merge_rows.resize(*h_mrtot);
       host->merge_base.resize(n);
-      if (n_set) {
-        grow(sp_scompact_, n_set * sizeof(PatchRec));
-        grow(sp_sroff_, kPatchRegions * sizeof(uint64_t));
-        hip_check(hipMemcpyAsync(sp_sroff_.p, h_sroff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s),
-                  "H2D");
-        launch_patch_compact(dd_spatches_.as<PatchRec>(), srcap_, a.spcount, sp_sroff_.as<uint64_t>(),
-                             sp_scompact_.as<PatchRec>(), s);
-        hip_check(hipGetLastError(), "k_patch_compact (sets)");
+      if (n_set)
         hip_check(hipMemcpyAsync(host->set_patches.data(), sp_scompact_.p, n_set * sizeof(PatchRec),
                                  hipMemcpyDeviceToHost, s), "D2H");
-      }
       if (*h_mrtot)
         hip_check(hipMemcpyAsync(host->merge_rows.data(), mr_rows_.p, *h_mrtot * sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, s), "D2H");
@@ -1578,6 +1610,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
   }
   if (one_sync) return true;  // (checked above)
+  if (early_spans) hip_check(hipStreamWaitEvent(s, side_done_, 0), "hipStreamWaitEvent");
   hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   if (*h_err) check_err(s);  // throws with the tripped guard's name
@@ -1585,9 +1618,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     for (TopicSpansDev& t : host->topics) {
       if (!t.n_patches)
         t.patch_base = 0;
-      else if (t.flags & kTopicSetPatches)
-        t.patch_base = h_sroff[t.patch_base / srcap_] + t.patch_base % srcap_;
-      else
+      else if (!(t.flags & kTopicSetPatches))  // (set topics: k_set_rebase)
         t.patch_base = h_roff[t.patch_base / rcap_] + t.patch_base % rcap_;
     }
   }

@@ -152,6 +152,9 @@ class Device {
   explicit Device(int dev);
   ~Device();
   int device() const { return dev_; }
+  // The stream of host-buffer calls (mq_match_spans): non-blocking, so waiting on it does not wait
+  // for the side stream's copies (a host result's spans go to the host under the merge kernels).
+  hipStream_t host_stream();
 
   // Upload dirty pages of the index image (incremental device-side update).
   void sync(Index& ix, hipStream_t s);
@@ -275,12 +278,14 @@ class Device {
   size_t h_stage_bytes_ = 0;
   hipEvent_t stage_done_ = nullptr;  // the last scatter finished reading both
   hipStream_t side_ = nullptr;
+  hipStream_t hstream_ = nullptr;  // host_stream()
   hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
+  hipEvent_t spans_ev_ = nullptr;  // host span results: k_desc done (the spans' early copy waits on it)
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_;
   // span format outputs
   DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;
   DevBuf sp_compact_, sp_roff_;      // host results: the patch regions packed
-  DevBuf sp_scompact_, sp_sroff_;    //   the set patch regions packed
+  DevBuf sp_scompact_, set_nbase_, set_total_;  //   the sets' written patches packed
   DevBuf mr_base_, mr_rows_, mr_total_;  // and the merge rows of the topics with a set
   DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
   // sharded: the exported list (offsets, entries, counts) and the imported lists' offsets

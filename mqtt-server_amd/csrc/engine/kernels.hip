@@ -1196,12 +1196,13 @@ __global__ __launch_bounds__(256) void k_finish(FinishArgs a) {
 
 // Host span results (mq_match_spans): the merge rows of every topic that references its set's
 // patches, packed (topics in any order; one atomic per wavefront). base[t]: where topic t's
-// start (0 for a topic without a set); *total: the packed count.
+// start (0 for a topic without a set); *total: the packed count. The wavefront copies its
+// topics' rows one topic at a time, a lane per row (coalesced).
 __global__ __launch_bounds__(256) void k_mrow_pack(uint32_t n, const uint32_t* __restrict__ tslot,
                                                    const uint32_t* __restrict__ mcount,
                                                    const uint32_t* __restrict__ mrow, uint32_t* __restrict__ base,
                                                    uint32_t* __restrict__ rows, unsigned long long* total) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63, t0 = t - lane;
   const uint32_t c = t < n && tslot[t] != kNone ? mcount[t] : 0u;
   uint32_t sum;
   const uint32_t pre = wave_excl_scan(c, lane, &sum);
@@ -1209,13 +1210,63 @@ __global__ __launch_bounds__(256) void k_mrow_pack(uint32_t n, const uint32_t* _
   if (lane == 0 && sum) b = atomicAdd(total, (unsigned long long)sum);
   b = __shfl(b, 0, 64) + pre;
   if (t < n) base[t] = c ? (uint32_t)b : 0u;
-  for (uint32_t x = 0; x < c; x++) rows[b + x] = mrow[(uint64_t)t * kPairMax + x];
+  for (uint64_t m = __ballot(c != 0); m; m &= m - 1) {
+    const int j = __builtin_ctzll(m);
+    const uint32_t cj = __shfl(c, j, 64);
+    const unsigned long long bj = __shfl(b, j, 64);
+    if (lane < cj) rows[bj + lane] = mrow[(uint64_t)(t0 + j) * kPairMax + lane];
+  }
+}
+
+// Host span results: the written patches of every merge set packed (the set pool holds each
+// set's reservation, of which SetInfo.n are written); nbase[rep]: where the set's start.
+// One atomic per wavefront; the wavefront copies its sets one at a time (coalesced).
+__global__ __launch_bounds__(256) void k_set_pack(uint32_t n, const uint32_t* __restrict__ tslot,
+                                                  const uint32_t* __restrict__ rep, const SetInfo* __restrict__ sets,
+                                                  const PatchRec* __restrict__ pool, uint64_t* __restrict__ nbase,
+                                                  PatchRec* __restrict__ out, unsigned long long* total) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  const bool own = t < n && tslot[t] != kNone && rep[t] == t;  // a set's representative
+  SetInfo si{0, 0, 0, 0, 0};
+  if (own) si = sets[t];
+  const uint32_t c = own ? si.n : 0u;
+  uint32_t sum;
+  const uint32_t pre = wave_excl_scan(c, lane, &sum);
+  unsigned long long b = 0;
+  if (lane == 0 && sum) b = atomicAdd(total, (unsigned long long)sum);
+  b = __shfl(b, 0, 64) + pre;
+  if (own) nbase[t] = b;
+  for (uint64_t m = __ballot(c != 0); m; m &= m - 1) {
+    const int j = __builtin_ctzll(m);
+    const uint32_t cj = __shfl(c, j, 64);
+    const unsigned long long bj = __shfl(b, j, 64), sj = __shfl((unsigned long long)si.base, j, 64);
+    for (uint32_t k = lane; k < cj; k += 64) out[bj + k] = pool[sj + k];
+  }
+}
+
+// Host span results: a topic that references its set's patches names them in the packed array.
+__global__ __launch_bounds__(256) void k_set_rebase(uint32_t n, const uint32_t* __restrict__ rep,
+                                                    const uint64_t* __restrict__ nbase, TopicSpansDev* sres) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  if (sres[t].flags & kTopicSetPatches) sres[t].patch_base = nbase[rep[t]];
 }
 
 void launch_mrow_pack(uint32_t n, const uint32_t* tslot, const uint32_t* mcount, const uint32_t* mrow,
                       uint32_t* base, uint32_t* rows, unsigned long long* total, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_mrow_pack, dim3((n + 255) / 256), dim3(256), 0, s, n, tslot, mcount, mrow, base, rows, total);
+}
+
+void launch_set_pack(uint32_t n, const uint32_t* tslot, const uint32_t* rep, const SetInfo* sets,
+                     const PatchRec* pool, uint64_t* nbase, PatchRec* out, unsigned long long* total, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_set_pack, dim3((n + 255) / 256), dim3(256), 0, s, n, tslot, rep, sets, pool, nbase, out, total);
+}
+
+void launch_set_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, TopicSpansDev* sres, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_set_rebase, dim3((n + 255) / 256), dim3(256), 0, s, n, rep, nbase, sres);
 }
 
 __global__ __launch_bounds__(256) void k_xsig(XSigArgs a) {
