@@ -29,7 +29,8 @@
 #define MQ_OPT_SET_EXP 18         /* attribution experiments on the merge set pass (results WRONG; timing only):
                                      bit 0 no partner links, bit 1 links loaded but not looked up, bit 2 no
                                      patch stores, bit 3 no binary search for a record's hit list; bit 4 (results
-                                     exact) no early stop of a visit through a partner other than the record's first */
+                                     exact) no early stop of a visit through a partner other than the record's first; bits 5 / 6 (exact)
+                                     partner links loaded 1 / 4 per batch instead of 2 */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than
                                      kMsgExportMin particles to work items any wavefront takes; > 1: that
                                      threshold; 0: the filter's wavefront walks it alone */

@@ -1203,8 +1203,13 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     host->spans.resize(tot.g);
     hip_check(hipEventRecord(spans_ev_, s), "hipEventRecord");
     hip_check(hipStreamWaitEvent(side_, spans_ev_, 0), "hipStreamWaitEvent");
-    hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, side_),
-              "D2H spans");
+    // (a kernel writing the mapped pinned buffer: a D2H copy call held the host thread until it
+    // was done, so the merge kernels waited for it — profiles/r03/s2_e2e/)
+    void* dst = nullptr;
+    hip_check(hipHostGetDevicePointer(&dst, host->spans.data(), 0), "hipHostGetDevicePointer");
+    static_assert(sizeof(SpanRec) == 16, "k_host_copy moves 16-byte words");
+    launch_host_copy(sp_spans_.p, dst, tot.g, std::max<uint32_t>(1, n_cus_ / 2), side_);
+    hip_check(hipGetLastError(), "k_host_copy");
     hip_check(hipEventRecord(side_done_, side_), "hipEventRecord");
     side_join = SideJoin{side_, true};
   }

@@ -1264,6 +1264,20 @@ void launch_set_pack(uint32_t n, const uint32_t* tslot, const uint32_t* rep, con
   hipLaunchKernelGGL(k_set_pack, dim3((n + 255) / 256), dim3(256), 0, s, n, tslot, rep, sets, pool, nbase, out, total);
 }
 
+// Host span results: 16-byte words copied by the GPU into mapped pinned host memory (the
+// stores cross PCIe), so the copy is a kernel on the side stream's queue beside the merge kernels.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_host_copy(const u32x4* __restrict__ src, u32x4* dst, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(src[i], dst + i);
+}
+
+void launch_host_copy(const void* src, void* dst_mapped, uint64_t words16, uint32_t blocks, hipStream_t s) {
+  if (!words16) return;
+  hipLaunchKernelGGL(k_host_copy, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
+                     static_cast<u32x4*>(dst_mapped), words16);
+}
+
 void launch_set_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, TopicSpansDev* sres, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_set_rebase, dim3((n + 255) / 256), dim3(256), 0, s, n, rep, nbase, sres);
@@ -1451,7 +1465,7 @@ __device__ __forceinline__ uint64_t gdesc_rank(const GDesc& d) {
 // and DFS order compares rank keys first (SPANS must be true).
 // SET (span format, merge-set dedup): the set pass (a.dd_phase 1), compiled apart so that the
 // topic pass's copy, inline and result code does not weigh on its register allocation.
-template <bool SPANS, bool XS, int WPE, bool SET = false>
+template <bool SPANS, bool XS, int WPE, bool SET = false, uint32_t PB = kPartBatch>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
   __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records (or
@@ -1739,15 +1753,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         uint32_t first = kNone;
         uint32_t q = rmeta & kMetaQos, nl = rmeta & kMetaNoLocal;
         if (SET && (a.exp & 1u)) mp_cnt = 0;
-        // partner links in batches of kPartBatch independent loads (one latency per batch)
-        for (uint32_t e0 = 0; e0 < mp_cnt && base && !other; e0 += kPartBatch) {
-          MergePart pb[kPartBatch];
+        // partner links in batches of PB independent loads (one latency per batch)
+        for (uint32_t e0 = 0; e0 < mp_cnt && base && !other; e0 += PB) {
+          MergePart pb[PB];
 #pragma unroll
-          for (uint32_t u = 0; u < kPartBatch; u++)
+          for (uint32_t u = 0; u < PB; u++)
             pb[u] = e0 + u < mp_cnt ? a.ix.mpart[mp_off + e0 + u] : MergePart{kNone, 0};
-          w_link += min(kPartBatch, mp_cnt - e0);
+          w_link += min(PB, mp_cnt - e0);
 #pragma unroll
-          for (uint32_t u = 0; u < kPartBatch; u++) {
+          for (uint32_t u = 0; u < PB; u++) {
             if (!base || other || pb[u].node == kNone) continue;
             if (SET && (a.exp & 2u)) {
               q = max(q, pb[u].meta & kMetaQos);
@@ -2158,7 +2172,10 @@ void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_bloc
     if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_merge<true, true, 1>), g, b, 0, s, a);
   } else if (spans && a.rep && a.dd_phase == 1) {  // merge-set dedup: the set pass
-    if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, true>), g, b, 0, s, a);
+    // (MQ_OPT_SET_EXP bits 5 / 6: partner links 1 / 4 per batch instead of kPartBatch)
+    if (wpe >= 8 && (a.exp & 32u)) hipLaunchKernelGGL((k_merge<true, false, 8, true, 1>), g, b, 0, s, a);
+    else if (wpe >= 8 && (a.exp & 64u)) hipLaunchKernelGGL((k_merge<true, false, 8, true, 4>), g, b, 0, s, a);
+    else if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, true>), g, b, 0, s, a);
     else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_merge<true, false, 1, true>), g, b, 0, s, a);
   } else if (spans) {
