@@ -292,7 +292,6 @@ Device::~Device() {
     if (merge_done_[k]) (void)hipEventDestroy(merge_done_[k]);
   }
   if (side_done_) (void)hipEventDestroy(side_done_);
-  if (spans_ev_) (void)hipEventDestroy(spans_ev_);
   if (side_) (void)hipStreamDestroy(side_);
   if (hstream_) (void)hipStreamDestroy(hstream_);
   if (wstream_) (void)hipStreamDestroy(wstream_);
@@ -516,11 +515,7 @@ hipStream_t Device::host_stream() {
 
 void Device::ensure_streams() {
   if (side_) return;
-  // the side stream at the greatest priority: a hardware queue of its own, so its copies run
-  // beside the other streams' kernels instead of in turn with them on a shared queue
-  int least = 0, greatest = 0;
-  hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-  hip_check(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, greatest), "hipStreamCreate");
+  hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate");
   hip_check(hipStreamCreateWithFlags(&wstream_, hipStreamNonBlocking), "hipStreamCreate");
   for (int k = 0; k < 2; k++) {
     hip_check(hipEventCreateWithFlags(&copy_done_[k], hipEventDisableTiming), "hipEventCreate");
@@ -528,7 +523,6 @@ void Device::ensure_streams() {
     hip_check(hipEventCreateWithFlags(&sb_done_[k], hipEventDisableTiming), "hipEventCreate");
   }
   hip_check(hipEventCreateWithFlags(&side_done_, hipEventDisableTiming), "hipEventCreate");
-  hip_check(hipEventCreateWithFlags(&spans_ev_, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming), "hipEventCreate");
 }
 
@@ -1188,31 +1182,6 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   if (nf && !ix.sharded()) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
   if (n == 0) return true;
   const bool one_sync = sb_.one_sync;
-  // host results: the spans are final once k_desc has run (spans_begin), so their copy to the
-  // host runs on the side stream under the dedup and merge kernels (joined before the end)
-  const bool early_spans = host && !one_sync && tot.g;
-  struct SideJoin {  // however this call ends, the copy into *host is done before *host can go
-    hipStream_t st;
-    bool on;
-    ~SideJoin() {
-      if (on) (void)hipStreamSynchronize(st);
-    }
-  } side_join{side_, false};
-  if (early_spans) {
-    ensure_streams();
-    host->spans.resize(tot.g);
-    hip_check(hipEventRecord(spans_ev_, s), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(side_, spans_ev_, 0), "hipStreamWaitEvent");
-    // (a kernel writing the mapped pinned buffer: a D2H copy call held the host thread until it
-    // was done, so the merge kernels waited for it — profiles/r03/s2_e2e/)
-    void* dst = nullptr;
-    hip_check(hipHostGetDevicePointer(&dst, host->spans.data(), 0), "hipHostGetDevicePointer");
-    static_assert(sizeof(SpanRec) == 16, "k_host_copy moves 16-byte words");
-    launch_host_copy(sp_spans_.p, dst, tot.g, std::max<uint32_t>(1, n_cus_ / 2), side_);
-    hip_check(hipGetLastError(), "k_host_copy");
-    hip_check(hipEventRecord(side_done_, side_), "hipEventRecord");
-    side_join = SideJoin{side_, true};
-  }
 
   EmitArgs a;
   memset(&a, 0, sizeof(a));
@@ -1580,10 +1549,15 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       hip_check(hipGetLastError(), "k_set_rebase");
     }
     host->topics.resize(n);
+    host->spans.resize(tot.g);
     host->patches.resize(n_patches);
     host->inl.resize(tot.inl);
     host->picked.resize(out->n_picked_rows);
     hip_check(hipMemcpyAsync(host->topics.data(), a.sres, n * sizeof(TopicSpansDev), hipMemcpyDeviceToHost, s), "D2H");
+    // (copied here with the rest: on a side stream under the merge kernels, by a copy or by a
+    // kernel storing to mapped memory, the two streams ran in turn — profiles/r03/s2_e2e/)
+    if (tot.g)
+      hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, s), "D2H");
     if (n_patches) {  // the regions' used parts, packed; patch_base is remapped below
       grow(sp_compact_, n_patches * sizeof(PatchRec));
       grow(sp_roff_, kPatchRegions * sizeof(uint64_t));
@@ -1615,7 +1589,6 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
   }
   if (one_sync) return true;  // (checked above)
-  if (early_spans) hip_check(hipStreamWaitEvent(s, side_done_, 0), "hipStreamWaitEvent");
   hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   if (*h_err) check_err(s);  // throws with the tripped guard's name

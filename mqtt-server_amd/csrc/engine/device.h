@@ -152,8 +152,7 @@ class Device {
   explicit Device(int dev);
   ~Device();
   int device() const { return dev_; }
-  // The stream of host-buffer calls (mq_match_spans): non-blocking, so waiting on it does not wait
-  // for the side stream's copies (a host result's spans go to the host under the merge kernels).
+  // The stream of host-buffer calls (mq_match_spans): its own, non-blocking.
   hipStream_t host_stream();
 
   // Upload dirty pages of the index image (incremental device-side update).
@@ -280,7 +279,6 @@ class Device {
   hipStream_t side_ = nullptr;
   hipStream_t hstream_ = nullptr;  // host_stream()
   hipEvent_t copy_done_[2] = {nullptr, nullptr}, merge_done_[2] = {nullptr, nullptr}, side_done_ = nullptr;
-  hipEvent_t spans_ev_ = nullptr;  // host span results: k_desc done (the spans' early copy waits on it)
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_;
   // span format outputs
   DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;

@@ -379,8 +379,6 @@ void launch_mrow_pack(uint32_t n, const uint32_t* tslot, const uint32_t* mcount,
 void launch_set_pack(uint32_t n, const uint32_t* tslot, const uint32_t* rep, const SetInfo* sets,
                      const PatchRec* pool, uint64_t* nbase, PatchRec* out, unsigned long long* total, hipStream_t s);
 void launch_set_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, TopicSpansDev* sres, hipStream_t s);
-// words16 16-byte words from device memory into mapped pinned host memory (a device pointer of it)
-void launch_host_copy(const void* src, void* dst_mapped, uint64_t words16, uint32_t blocks, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
 // first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
 // fill pass must still walk; the fill pass then walks only those.

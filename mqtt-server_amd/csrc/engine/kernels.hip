@@ -1264,20 +1264,6 @@ void launch_set_pack(uint32_t n, const uint32_t* tslot, const uint32_t* rep, con
   hipLaunchKernelGGL(k_set_pack, dim3((n + 255) / 256), dim3(256), 0, s, n, tslot, rep, sets, pool, nbase, out, total);
 }
 
-// Host span results: 16-byte words copied by the GPU into mapped pinned host memory (the
-// stores cross PCIe), so the copy is a kernel on the side stream's queue beside the merge kernels.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void k_host_copy(const u32x4* __restrict__ src, u32x4* dst, uint64_t n) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    __builtin_nontemporal_store(src[i], dst + i);
-}
-
-void launch_host_copy(const void* src, void* dst_mapped, uint64_t words16, uint32_t blocks, hipStream_t s) {
-  if (!words16) return;
-  hipLaunchKernelGGL(k_host_copy, dim3(blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
-                     static_cast<u32x4*>(dst_mapped), words16);
-}
-
 void launch_set_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, TopicSpansDev* sres, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_set_rebase, dim3((n + 255) / 256), dim3(256), 0, s, n, rep, nbase, sres);

@@ -1,0 +1,30 @@
+# Round 3 (session 2) final evidence on the committed tree: smoke, the C++ mirror, the GPU suite,
+# the default bench line, its
+# kernel trace (rocprofv3 --kernel-trace --stats), the PMC traffic of the step's kernels (FETCH_SIZE
+# and WRITE_SIZE in passes of their own), config 4 (50M IoT) and the 8-shard simulation at 10M.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+D=$R/gpurun_out/${1:-r3zf}
+mkdir -p $D
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $D/smoke.log; exit 1; }
+cat $D/smoke.log
+timeout -k 5 150 ./mqtt-server_amd/build/test_topics_index > $D/cpp.log 2>&1 || { echo "cpp rc=$?"; tail -20 $D/cpp.log; exit 1; }
+tail -1 $D/cpp.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > $D/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -60 $D/pytest_gpu.log; exit 1; }
+tail -1 $D/pytest_gpu.log
+timeout -k 10 400 python -u bench.py > $D/bench_default.json 2> $D/bench_default.err || { echo "bench rc=$?"; tail -5 $D/bench_default.err; exit 1; }
+cut -c1-300 $D/bench_default.json
+cd /tmp && export TMPDIR=/tmp
+ARGS="--steps 3 --warmup 1 --no-cpu"
+KR="k_walk|k_merge|k_desc|k_dedup|k_finish|k_reset|k_readback"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 $R/bench.py $ARGS > $D/trace.json 2> $D/trace.err || { echo "trace rc=$?"; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" --output-format csv -d $D/fetch -o run -- python3 $R/bench.py $ARGS > $D/fetch.json 2> $D/fetch.err || { echo "fetch rc=$?"; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" --output-format csv -d $D/write -o run -- python3 $R/bench.py $ARGS > $D/write.json 2> $D/write.err || { echo "write rc=$?"; exit 1; }
+cd $R
+python profiles/summarize.py $D/trace > $D/kernel_stats.json
+python profiles/summarize.py $D/fetch $D/write --pmc > $D/pmc.json
+head -c 1500 $D/kernel_stats.json
+timeout -k 10 400 python -u bench.py --mix iot --subs 50000000 --no-cpu > $D/bench_iot_50m.json 2> $D/bench_iot_50m.err || { echo "iot rc=$?"; tail -5 $D/bench_iot_50m.err; exit 1; }
+cut -c1-300 $D/bench_iot_50m.json
+timeout -k 10 420 python -u bench.py --sim-shards 8 --steps 5 --warmup 2 --no-cpu > $D/bench_sim8_10m.json 2> $D/bench_sim8_10m.err || { echo "sim8 rc=$?"; tail -5 $D/bench_sim8_10m.err; exit 1; }
+cut -c1-300 $D/bench_sim8_10m.json
