@@ -1544,10 +1544,18 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.count("merge_topics", n);
   }
   if (host) {
-    if (sb_.dedup) {  // the set topics' patch_base into the packed set patches
-      launch_set_rebase(n, a.rep, set_nbase_.as<uint64_t>(), a.sres, s);
-      hip_check(hipGetLastError(), "k_set_rebase");
+    grow(sp_roff_, (kPatchRegions + 1) * sizeof(uint64_t));
+    if (n_patches) {  // the regions' used parts, packed
+      grow(sp_compact_, n_patches * sizeof(PatchRec));
+      hip_check(hipMemcpyAsync(sp_roff_.p, h_roff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D");
+      launch_patch_compact(sp_patches_.as<PatchRec>(), rcap_, a.pcount, sp_roff_.as<uint64_t>(),
+                           sp_compact_.as<PatchRec>(), s);
+      hip_check(hipGetLastError(), "k_patch_compact");
     }
+    // every topic's patch_base into the packed arrays (its own patches' or its set's)
+    launch_host_rebase(n, sb_.dedup ? a.rep : nullptr, sb_.dedup ? set_nbase_.as<uint64_t>() : nullptr,
+                       n_patches ? sp_roff_.as<uint64_t>() : nullptr, rcap_, a.sres, s);
+    hip_check(hipGetLastError(), "k_host_rebase");
     host->topics.resize(n);
     host->spans.resize(tot.g);
     host->patches.resize(n_patches);
@@ -1558,16 +1566,9 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     // kernel storing to mapped memory, the two streams ran in turn — profiles/r03/s2_e2e/)
     if (tot.g)
       hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, s), "D2H");
-    if (n_patches) {  // the regions' used parts, packed; patch_base is remapped below
-      grow(sp_compact_, n_patches * sizeof(PatchRec));
-      grow(sp_roff_, kPatchRegions * sizeof(uint64_t));
-      hip_check(hipMemcpyAsync(sp_roff_.p, h_roff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D");
-      launch_patch_compact(sp_patches_.as<PatchRec>(), rcap_, a.pcount, sp_roff_.as<uint64_t>(),
-                           sp_compact_.as<PatchRec>(), s);
-      hip_check(hipGetLastError(), "k_patch_compact");
+    if (n_patches)
       hip_check(hipMemcpyAsync(host->patches.data(), sp_compact_.p, n_patches * sizeof(PatchRec),
                                hipMemcpyDeviceToHost, s), "D2H");
-    }
     if (tot.inl)
       hip_check(hipMemcpyAsync(host->inl.data(), sp_inl_.p, tot.inl * sizeof(InlRec), hipMemcpyDeviceToHost, s), "D2H");
     if (out->n_picked_rows)
@@ -1592,14 +1593,6 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
   hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
   if (*h_err) check_err(s);  // throws with the tripped guard's name
-  if (host) {  // patch bases into the packed arrays
-    for (TopicSpansDev& t : host->topics) {
-      if (!t.n_patches)
-        t.patch_base = 0;
-      else if (!(t.flags & kTopicSetPatches))  // (set topics: k_set_rebase)
-        t.patch_base = h_roff[t.patch_base / rcap_] + t.patch_base % rcap_;
-    }
-  }
   return true;
 }
 

@@ -374,11 +374,12 @@ void launch_finish(const FinishArgs& a, hipStream_t s);
 // mcount[t] of them from mrow[t * kPairMax]; base[t] their start, *total (zeroed) the count.
 void launch_mrow_pack(uint32_t n, const uint32_t* tslot, const uint32_t* mcount, const uint32_t* mrow,
                       uint32_t* base, uint32_t* rows, unsigned long long* total, hipStream_t s);
-// Host span results: the sets' written patches packed (nbase[rep], *total zeroed), and the set
-// topics' patch_base pointed at them.
+// Host span results: the sets' written patches packed (nbase[rep], *total zeroed), and every
+// topic's patch_base pointed into the packed arrays (its set's, or its own via the regions' roff).
 void launch_set_pack(uint32_t n, const uint32_t* tslot, const uint32_t* rep, const SetInfo* sets,
                      const PatchRec* pool, uint64_t* nbase, PatchRec* out, unsigned long long* total, hipStream_t s);
-void launch_set_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, TopicSpansDev* sres, hipStream_t s);
+void launch_host_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, const uint64_t* roff, uint64_t rcap,
+                        TopicSpansDev* sres, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
 // first spec_cap handles to spec[t * spec_cap ...] and flags (TopicCount.gathers) the filters the
 // fill pass must still walk; the fill pass then walks only those.

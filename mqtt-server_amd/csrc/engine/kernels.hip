@@ -1244,12 +1244,20 @@ __global__ __launch_bounds__(256) void k_set_pack(uint32_t n, const uint32_t* __
   }
 }
 
-// Host span results: a topic that references its set's patches names them in the packed array.
-__global__ __launch_bounds__(256) void k_set_rebase(uint32_t n, const uint32_t* __restrict__ rep,
-                                                    const uint64_t* __restrict__ nbase, TopicSpansDev* sres) {
+// Host span results: every topic's patch_base into the packed arrays — its set's patches
+// (nbase of its representative) or its own (the regions' packed offsets roff), 0 without patches.
+__global__ __launch_bounds__(256) void k_host_rebase(uint32_t n, const uint32_t* __restrict__ rep,
+                                                     const uint64_t* __restrict__ nbase,
+                                                     const uint64_t* __restrict__ roff, uint64_t rcap,
+                                                     TopicSpansDev* sres) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
-  if (sres[t].flags & kTopicSetPatches) sres[t].patch_base = nbase[rep[t]];
+  const uint32_t np = sres[t].n_patches, fl = sres[t].flags;
+  const uint64_t pb = sres[t].patch_base;
+  uint64_t b = 0;
+  if (np && (fl & kTopicSetPatches)) b = nbase[rep[t]];
+  else if (np) b = roff[pb / rcap] + pb % rcap;
+  sres[t].patch_base = b;
 }
 
 void launch_mrow_pack(uint32_t n, const uint32_t* tslot, const uint32_t* mcount, const uint32_t* mrow,
@@ -1264,9 +1272,10 @@ void launch_set_pack(uint32_t n, const uint32_t* tslot, const uint32_t* rep, con
   hipLaunchKernelGGL(k_set_pack, dim3((n + 255) / 256), dim3(256), 0, s, n, tslot, rep, sets, pool, nbase, out, total);
 }
 
-void launch_set_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, TopicSpansDev* sres, hipStream_t s) {
+void launch_host_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, const uint64_t* roff, uint64_t rcap,
+                        TopicSpansDev* sres, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_set_rebase, dim3((n + 255) / 256), dim3(256), 0, s, n, rep, nbase, sres);
+  hipLaunchKernelGGL(k_host_rebase, dim3((n + 255) / 256), dim3(256), 0, s, n, rep, nbase, roff, rcap, sres);
 }
 
 __global__ __launch_bounds__(256) void k_xsig(XSigArgs a) {

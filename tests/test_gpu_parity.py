@@ -359,6 +359,27 @@ def test_spans_format_shape(gpu_available):
     assert span_bytes * 4 < rows_bytes  # the point of the format
 
 
+@pytest.mark.parametrize("dedup", [0, 1])
+def test_host_spans_own_and_set_patches(dedup, gpu_available):
+    """Host span results (mq_match_spans) with merge-set dedup (topics name their set's packed
+    patches through their packed merge rows) and without (every topic's own packed patches):
+    expanded rows equal the oracle's, and the patch arrays are what the mode says."""
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(40000, 3000, seed=71)
+    eng.set_option(E.OPT_MERGE_DEDUP, dedup)
+    tb, to = W.gen_topics(w, 4000, seed=72)
+    _digest_parity(eng, orc, tb, to, fmts=("spans",))
+    a = eng.match_spans(tb, to)
+    setf = (a["topics"]["flags"] & 1) != 0
+    if dedup:
+        assert setf.any() and len(a["set_patches"]) > 0 and len(a["merge_base"]) == len(setf)
+    else:
+        assert not setf.any() and len(a["set_patches"]) == 0 and len(a["patches"]) > 0
+    tid, prow, _ = E.host_topic_patches(a)
+    assert len(tid) == int(a["topics"]["n_patches"].sum()) and (prow < a["topics"]["n_rows"][tid]).all()
+
+
 def test_spans_device_matches_host(gpu_available):
     """mq_match_spans_device on torch buffers: the same per-topic records as mq_match_spans."""
     import ctypes as C
