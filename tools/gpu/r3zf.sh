@@ -1,7 +1,7 @@
 # Round 3 (session 2) final evidence on the committed tree: smoke, the C++ mirror, the GPU suite,
-# the default bench line, its
+# the end-to-end probe, the default bench line, its
 # kernel trace (rocprofv3 --kernel-trace --stats), the PMC traffic of the step's kernels (FETCH_SIZE
-# and WRITE_SIZE in passes of their own), config 4 (50M IoT) and the 8-shard simulation at 10M.
+# and WRITE_SIZE in passes of their own) and config 4 (50M IoT).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 D=$R/gpurun_out/${1:-r3zf}
@@ -12,6 +12,8 @@ timeout -k 5 150 ./mqtt-server_amd/build/test_topics_index > $D/cpp.log 2>&1 || 
 tail -1 $D/cpp.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread > $D/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -60 $D/pytest_gpu.log; exit 1; }
 tail -1 $D/pytest_gpu.log
+timeout -k 10 300 python -u tools/e2e_probe.py > $D/e2e_probe.jsonl 2> $D/e2e_probe.err || { echo "probe rc=$?"; tail -5 $D/e2e_probe.err; exit 1; }
+cut -c1-200 $D/e2e_probe.jsonl
 timeout -k 10 400 python -u bench.py > $D/bench_default.json 2> $D/bench_default.err || { echo "bench rc=$?"; tail -5 $D/bench_default.err; exit 1; }
 cut -c1-300 $D/bench_default.json
 cd /tmp && export TMPDIR=/tmp
@@ -26,5 +28,3 @@ python profiles/summarize.py $D/fetch $D/write --pmc > $D/pmc.json
 head -c 1500 $D/kernel_stats.json
 timeout -k 10 400 python -u bench.py --mix iot --subs 50000000 --no-cpu > $D/bench_iot_50m.json 2> $D/bench_iot_50m.err || { echo "iot rc=$?"; tail -5 $D/bench_iot_50m.err; exit 1; }
 cut -c1-300 $D/bench_iot_50m.json
-timeout -k 10 420 python -u bench.py --sim-shards 8 --steps 5 --warmup 2 --no-cpu > $D/bench_sim8_10m.json 2> $D/bench_sim8_10m.err || { echo "sim8 rc=$?"; tail -5 $D/bench_sim8_10m.err; exit 1; }
-cut -c1-300 $D/bench_sim8_10m.json
