@@ -11,7 +11,7 @@
 #define MQ_OPT_MSG_SPEC_MB 3      /* Messages: speculative-count scratch budget (MiB; 0: two walks) */
 #define MQ_OPT_MSG_WAVES 4        /* Messages: k_msg waves per SIMD (1, 6, 8; 0: by index size) */
 #define MQ_OPT_SERIAL 5           /* 1: no side-stream overlap (isolated kernel timings) */
-#define MQ_OPT_MERGE_WAVES 7      /* k_merge waves per SIMD the registers are budgeted for (1, 6, 8) */
+#define MQ_OPT_MERGE_WAVES 7      /* k_merge waves per SIMD the registers are budgeted for (1, 6, 7: set pass only, 8) */
 #define MQ_OPT_MSG_IMAGE 8        /* Messages: 1 (default) runs over the level-order retained image;
                                      0 walks the particles (the path the Q6 state always takes) */
 #define MQ_OPT_WALK_WAVES 9       /* thread-per-topic k_walk: waves per SIMD the registers are budgeted for (1, 8) */
@@ -30,7 +30,7 @@
                                      bit 0 no partner links, bit 1 links loaded but not looked up, bit 2 no
                                      patch stores, bit 3 no binary search for a record's hit list; bit 4 (results
                                      exact) no early stop of a visit through a partner other than the record's first; bits 5 / 6 (exact)
-                                     partner links loaded 1 / 4 per batch instead of 2 */
+                                     partner links loaded 3 / 4 per batch instead of 2 */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than
                                      kMsgExportMin particles to work items any wavefront takes; > 1: that
                                      threshold; 0: the filter's wavefront walks it alone */

@@ -2167,10 +2167,11 @@ void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_bloc
     if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, true, 6>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_merge<true, true, 1>), g, b, 0, s, a);
   } else if (spans && a.rep && a.dd_phase == 1) {  // merge-set dedup: the set pass
-    // (MQ_OPT_SET_EXP bits 5 / 6: partner links 1 / 4 per batch instead of kPartBatch)
-    if (wpe >= 8 && (a.exp & 32u)) hipLaunchKernelGGL((k_merge<true, false, 8, true, 1>), g, b, 0, s, a);
+    // (MQ_OPT_SET_EXP bits 5 / 6: partner links 3 / 4 per batch instead of kPartBatch)
+    if (wpe >= 8 && (a.exp & 32u)) hipLaunchKernelGGL((k_merge<true, false, 8, true, 3>), g, b, 0, s, a);
     else if (wpe >= 8 && (a.exp & 64u)) hipLaunchKernelGGL((k_merge<true, false, 8, true, 4>), g, b, 0, s, a);
     else if (wpe >= 8) hipLaunchKernelGGL((k_merge<true, false, 8, true>), g, b, 0, s, a);
+    else if (wpe == 7) hipLaunchKernelGGL((k_merge<true, false, 7, true>), g, b, 0, s, a);
     else if (wpe >= 6) hipLaunchKernelGGL((k_merge<true, false, 6, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((k_merge<true, false, 1, true>), g, b, 0, s, a);
   } else if (spans) {

@@ -226,3 +226,17 @@ def test_merge_records_update_in_place(n_shards):
         for e in engs:
             e.check()
     assert sum(e.stats()["subs_merge"] for e in engs) > 500
+
+
+def test_header_compiles_as_c(tmp_path):
+    """include/mqmatch.h (with its inline mq_topic_patch) is plain C99: what cgo compiles."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    src = tmp_path / "h.c"
+    src.write_text('#include "mqmatch.h"\nint main(void) { return (int)MQ_ABI_VERSION - 7; }\n')
+    r = subprocess.run([cc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-fsyntax-only",
+                        "-I", os.path.join(REPO, "include"), str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -414,11 +414,11 @@ def test_spans_device_matches_host(gpu_available):
     assert (dsp[E._ranges(sb, ns)] == host["spans"]).all()
 
 
-@pytest.mark.parametrize("exp,waves", [(16, 8), (32, 8), (64, 8), (0, 6)])  # bits 5 / 6: 1 / 4 links
+@pytest.mark.parametrize("exp,waves", [(16, 8), (32, 8), (64, 8), (0, 7), (0, 6)])  # bits 5 / 6: 3 / 4 links
 def test_set_pass_variants_exact(exp, waves, gpu_available):
     """The merge set pass's exact variants: MQ_OPT_SET_EXP bit 4 (a visit through a partner other
-    than the record's first reads all its links), bits 5 / 6 (1 / 4 partner links per batch), and
-    6 waves per SIMD (MQ_OPT_MERGE_WAVES): per-topic digests of device results equal the oracle's."""
+    than the record's first reads all its links), bits 5 / 6 (3 / 4 partner links per batch), and
+    7 or 6 waves per SIMD (MQ_OPT_MERGE_WAVES): per-topic digests of device results equal the oracle's."""
     import torch
     from mqmatch import engine as E
     from mqmatch import workload as W
