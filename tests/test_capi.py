@@ -240,3 +240,22 @@ def test_header_compiles_as_c(tmp_path):
     r = subprocess.run([cc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-fsyntax-only",
                         "-I", os.path.join(REPO, "include"), str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_host_topic_patches_resolves_own_and_set_patches():
+    """host_topic_patches (the Python form of mq_topic_patch) on a hand-built host result: a topic
+    with its own patches, and two topics of one merge set whose set patches (x << 26 | k) land on
+    their own rows through their packed merge rows."""
+    import numpy as np
+    dt = E._TOPIC_SPANS_DT
+    t = np.zeros(3, dt)
+    t["n_rows"] = [10, 20, 30]
+    t["patch_base"], t["n_patches"], t["flags"] = [0, 0, 0], [2, 2, 2], [0, 1, 1]
+    a = {"topics": t,
+         "patches": np.array([[3, 7], [5, 9]], np.uint32),
+         "set_patches": np.array([[0 << 26 | 1, 11], [1 << 26 | 2, 12]], np.uint32),
+         "merge_rows": np.array([4, 8, 0, 0, 20, 25], np.uint32),   # topic 1: rows 4, 8; topic 2: 20, 25
+         "merge_base": np.array([0, 0, 4], np.uint32)}
+    tid, row, meta = E.host_topic_patches(a)
+    got = sorted(zip(tid.tolist(), row.tolist(), meta.tolist()))
+    assert got == [(0, 3, 7), (0, 5, 9), (1, 5, 11), (1, 10, 12), (2, 21, 11), (2, 27, 12)]
