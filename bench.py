@@ -338,6 +338,101 @@ def run_sharded(args, mix, n_clients, rank, world, local, backend):
     D.finalize(backend)
 
 
+class OracleSide:
+    """The CPU side of the bench line — the oracle's parity-sample digests and L / P / S / O
+    counters, and the CPU baselines — in a child process (`bench.py --oracle-side`) started
+    before this process touches the GPU. It regenerates the same workload from the same seeds,
+    builds the oracle while the engine is built and timed here, and times the CPU baselines only
+    when told to (finish()), so that they do not share the host with this process's work. At
+    config 4's 50M subscriptions the oracle and the engine's host mirror live in two processes."""
+
+    def __init__(self, args):
+        import subprocess
+        import tempfile
+        self.path = os.path.join(tempfile.gettempdir(), f"mq_oracle_side_{os.getpid()}.json")
+        cmd = [sys.executable, "-u", os.path.abspath(__file__), "--oracle-side", self.path,
+               "--subs", str(args.subs), "--clients", str(args.clients), "--mix", args.mix,
+               "--topics", str(args.topics), "--cpu-seconds", str(args.cpu_seconds),
+               "--parity-topics", str(args.parity_topics)]
+        self.p = subprocess.Popen(cmd, stdin=subprocess.PIPE)
+
+    def finish(self, timeout=1800):
+        self.p.stdin.write(b"go\n")
+        self.p.stdin.flush()
+        self.p.stdin.close()
+        rc = self.p.wait(timeout=timeout)
+        if rc != 0:
+            raise SystemExit(f"bench.py --oracle-side failed (rc {rc})")
+        with open(self.path) as f:
+            o = json.load(f)
+        os.unlink(self.path)
+        return o
+
+
+def oracle_side_main(args):
+    """Child process of OracleSide: no torch, no GPU."""
+    from mqmatch import dist as D
+    from mqmatch import workload as W
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    mix = W.MIX_IOT if args.mix == "iot" else W.MIX_MQTT
+    n_clients = args.clients or (args.subs if args.mix == "iot" else max(1, args.subs // 10))
+    t0 = time.time()
+    w = W.gen_subscriptions(args.subs, n_clients, seed=W.BASE_SEED, mix=mix)
+    tb, to = W.gen_topics(w, args.topics, seed=D.topic_seed(0), mix=mix)
+    n = len(to) - 1
+    log(f"oracle side: workload generated in {time.time()-t0:.1f}s")
+    t0 = time.time()
+    orc = O.OracleIndex()
+    orc.subscribe_bulk(w)
+    del w
+    log(f"oracle side: oracle index built in {time.time()-t0:.1f}s")
+    cores = host_cores()
+    # oracle counters (SURVEY.md §8d: B = 8L + 4 + 16P + 16S + 16O per topic) + parity digests
+    ns = min(n, args.parity_topics)
+    t0 = time.time()
+    dg_o, cnt_o, tot = orc.digest_batch(tb, to[:ns + 1], cores)
+    log(f"oracle side: {ns} sample digests in {time.time()-t0:.1f}s; waiting for the GPU side")
+    if sys.stdin.readline().strip() != "go":  # the GPU side is done: the host is this process's
+        log("oracle side: the GPU side went away; exiting")
+        return
+    # The baseline is the fast restatement (oracle/topics_fast.h: the Go trie's algorithm with
+    # client ids interned at build time and flat per-thread result tables; digest-equal to the
+    # oracle): calibrate, then time a sample of about --cpu-seconds of CPU work.
+    t0 = time.time()
+    fast = orc.fast()
+    log(f"oracle side: fast CPU restatement built in {time.time()-t0:.1f}s")
+    cal = min(n, 256 * cores)
+    secs, _ = fast.bench_subscribers(tb, to[:cal + 1], cores)
+    m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
+    secs, _ = fast.bench_subscribers(tb, to[:m + 1], cores)
+    # one thread on a short sample: the per-core rate (the restatement scales with threads: a
+    # shared frozen index, no locks), for reading the baseline against a whole host
+    m1 = int(min(n, max(64, (m / max(cores, 1)) * min(3.0, args.cpu_seconds / 5) / max(args.cpu_seconds, 1e-6))))
+    secs1, _ = fast.bench_subscribers(tb, to[:m1 + 1], 1)
+    cpu = {"value": m / secs, "unit": "publishes/s", "cores": cores, "kind": "port",
+           "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": affinity_cpus(),
+           "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+           "single_thread": {"value": m1 / secs1, "sample_topics": m1},
+           "sample": f"first {m} topics of the rank-0 batch on the same {args.subs}-subscription index, "
+                     f"{cores} threads (std::thread, shared frozen index), Subscribers() per topic: the "
+                     f"fast CPU restatement of the Go particle trie (oracle/topics_fast.cpp: interned "
+                     f"client ids, flat per-thread result tables; digest-equal to the oracle)"}
+    del fast
+    # the literal restatement (per-call ordered result maps, as the oracle checks with)
+    lit_cal = min(n, 16 * cores)
+    lsecs, _ = orc.bench_subscribers(tb, to[:lit_cal + 1], cores)
+    lm = int(min(n, max(lit_cal, lit_cal * min(5.0, args.cpu_seconds / 3) / max(lsecs, 1e-6))))
+    lsecs, _ = orc.bench_subscribers(tb, to[:lm + 1], cores)
+    lit = {"value": lm / lsecs, "unit": "publishes/s", "cores": cores,
+           "sample": f"first {lm} topics; oracle/topics_oracle.cpp (ordered std::map results, string keys, "
+                     f"map copy per gather)"}
+    with open(args.oracle_side, "w") as f:
+        json.dump({"sample_topics": ns, "digests": [format(int(x), "x") for x in dg_o],
+                   "counts": cnt_o.astype(np.int64).tolist(), "totals": tot, "cpu": cpu, "cpu_literal": lit}, f)
+    log("oracle side: done")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -363,8 +458,19 @@ def main():
                     help="spans: mq_match_spans_device (gathered lists named, merges patched); rows: "
                          "mq_match_device_chunks with every row materialised and each chunk consumed "
                          "by a device-side checksum")
+    ap.add_argument("--parity-topics", type=int, default=0,
+                    help="topics of the timed batch checked against the oracle (default: 4096; iot mix 20000)")
+    ap.add_argument("--oracle-side", metavar="OUT", help=argparse.SUPPRESS)  # OracleSide's child process
     args = ap.parse_args()
+    if not args.parity_topics:
+        args.parity_topics = 20000 if args.mix == "iot" else 4096
     heartbeat()
+    if args.oracle_side:
+        return oracle_side_main(args)
+    rank, world, _ = (int(os.environ.get(k, d)) for k, d in (("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")))
+    oside = None
+    if not args.no_cpu and world == 1 and args.shard == "none" and args.sim_shards <= 1:
+        oside = OracleSide(args)  # before any GPU call: the child forks no GPU state
 
     import torch
     from mqmatch import dist as D
@@ -486,59 +592,29 @@ def main():
     else:
         out["roofline"] = rows_roofline(prof, args, elapsed, out)
     cpu = None
-    if not args.no_cpu and world == 1:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
+    if oside is not None:
+        # the oracle side (a child process started before any GPU call): its parity-sample
+        # digests and L / P / S / O counters are ready or nearly; the CPU baseline is timed now,
+        # with this process idle
+        o = oside.finish()
+        cpu = o["cpu"]
+        out["cpu_baseline_literal"] = o["cpu_literal"]
+        ns = o["sample_topics"]
+        dg_o = np.array([int(x, 16) for x in o["digests"]], np.uint64)
+        tot = o["totals"]
         sys.path.insert(0, os.path.join(REPO, "tests"))
-        import oracle as O
         from digest import engine_digests
-        t0 = time.time()
-        orc = O.OracleIndex()
-        orc.subscribe_bulk(w)
-        log(f"oracle index built in {time.time()-t0:.1f}s")
-        cores = host_cores()
-        # The baseline is the fast restatement (oracle/topics_fast.h: the Go trie's algorithm with
-        # client ids interned at build time and flat per-thread result tables; digest-equal to the
-        # oracle): calibrate, then time a sample of about --cpu-seconds of CPU work.
-        t0 = time.time()
-        fast = orc.fast()
-        log(f"fast CPU restatement built in {time.time()-t0:.1f}s")
-        cal = min(n, 256 * cores)
-        secs, _ = fast.bench_subscribers(tb, to[:cal + 1], cores)
-        m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
-        secs, _ = fast.bench_subscribers(tb, to[:m + 1], cores)
-        # one thread on a short sample: the per-core rate (the restatement scales with threads: a
-        # shared frozen index, no locks), for reading the baseline against a whole host
-        m1 = int(min(n, max(64, (m / max(cores, 1)) * min(3.0, args.cpu_seconds / 5) / max(args.cpu_seconds, 1e-6))))
-        secs1, _ = fast.bench_subscribers(tb, to[:m1 + 1], 1)
-        cpu = {"value": m / secs, "unit": "publishes/s", "cores": cores, "kind": "port",
-               "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "affinity_cpus": affinity_cpus(),
-               "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-               "single_thread": {"value": m1 / secs1, "sample_topics": m1},
-               "sample": f"first {m} topics of the rank-0 batch on the same {args.subs}-subscription index, "
-                         f"{cores} threads (std::thread, shared frozen index), Subscribers() per topic: the "
-                         f"fast CPU restatement of the Go particle trie (oracle/topics_fast.cpp: interned "
-                         f"client ids, flat per-thread result tables; digest-equal to the oracle)"}
-        # the literal restatement (per-call ordered result maps, as the oracle checks with)
-        lit_cal = min(n, 16 * cores)
-        lsecs, _ = orc.bench_subscribers(tb, to[:lit_cal + 1], cores)
-        lm = int(min(n, max(lit_cal, lit_cal * min(5.0, args.cpu_seconds / 3) / max(lsecs, 1e-6))))
-        lsecs, _ = orc.bench_subscribers(tb, to[:lm + 1], cores)
-        out["cpu_baseline_literal"] = {"value": lm / lsecs, "unit": "publishes/s", "cores": cores,
-                                       "sample": f"first {lm} topics; oracle/topics_oracle.cpp (ordered "
-                                                 f"std::map results, string keys, map copy per gather)"}
-        del fast
-        # oracle counters (B = 8L + 4 + 16P + 16S + 16O per topic) + parity on a sample
-        ns = min(m, 4096)
-        dg_o, cnt_o, tot = orc.digest_batch(tb, to[:ns + 1], cores)
         if not args.select_shared:  # picked shared rows are checked by tests/test_gpu_select.py
             # span format: the first ns topics of the measured step's own device result (the whole
             # batch's merge sets), expanded as a device consumer would
             res = (E.expand_device_spans(r_last, n, ns) if args.format == "spans"
                    else eng.match_batch(tb, to[:ns + 1]))
-            dg_e, _ = engine_digests(res)
+            dg_e, cnt_e = engine_digests(res)
             out["parity_sample"] = {"topics": ns, "format": args.format, "bit_exact": bool((dg_e == dg_o).all()),
+                                    "counts_equal": bool((cnt_e.astype(np.int64) == np.array(o["counts"], np.int64)).all()),
                                     "checked": "device result of the timed batch" if args.format == "spans"
-                                               else "mq_match_batch"}
+                                               else "mq_match_batch",
+                                    "oracle": "oracle/topics_oracle.cpp in a child process (bench.py --oracle-side)"}
             if args.format == "spans":
                 out["parity_sample"]["set_patch_topics"] = res["set_topics"]
         per_topic = {k: v / ns for k, v in tot.items()}

@@ -270,26 +270,19 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
   }
 }
 
+// Device buffers and mirrors release themselves (DevBuf / DevMirror destructors, run after this
+// body with the device still selected); streams, events and pinned host blocks are freed here.
 Device::~Device() {
   (void)hipSetDevice(dev_);
-  edges_.release(); walk_.release(); lists_.release(); msg_.release(); seginfo_.release();
-  segbytes_.release(); subs_.release(); shr_.release(); inl_.release(); children_.release();
-  mref_.release(); mpart_.release(); npair_.release(); pent_.release(); plist_.release(); xinfo_.release();
-  for (DevBuf* b : {&in_bytes_, &in_offs_, &counts_, &offs_, &bsum_, &bpre_, &gathers_, &err_, &ovf_,
-                    &msg_handles_, &msg_base_, &msg_count_, &msg_spec_, &gslots_, &acl_buf_, &sp_res_,
-                    &sp_spans_, &sp_inl_, &sp_picked_, &sp_patches_, &sp_pcount_, &sp_compact_, &sp_roff_,
-                    &sp_work_, &x_off_, &x_ents_, &x_cnt_, &x_src_, &img_node_, &img_pos_, &img_cl_,
-                    &img_lp_, &img_h_, &img_cnt_, &img_coff_, &img_bsum_, &img_bpre_, &msg_pieces_, &d_stage_})
-    b->release();
-  if (stage_done_) {
-    (void)hipEventSynchronize(stage_done_);
-    (void)hipEventDestroy(stage_done_);
-  }
+  (void)hipDeviceSynchronize();  // no kernel of this index still reads a buffer freed below
+  if (stage_done_) (void)hipEventDestroy(stage_done_);
   pinned_free(h_stage_, h_stage_bytes_);
+  if (h_fast_) pinned_free(h_fast_, sizeof(FastBack));
   for (int k = 0; k < 2; k++) {
-    for (DevBuf* b : {&rows_[k], &shr_rows_[k], &inl_rows_[k], &res_[k], &sel_rows_[k]}) b->release();
     if (copy_done_[k]) (void)hipEventDestroy(copy_done_[k]);
     if (merge_done_[k]) (void)hipEventDestroy(merge_done_[k]);
+    if (sb_done_[k]) (void)hipEventDestroy(sb_done_[k]);
+    if (walk_ev_[k]) (void)hipEventDestroy(walk_ev_[k]);
   }
   if (side_done_) (void)hipEventDestroy(side_done_);
   if (side_) (void)hipStreamDestroy(side_);
@@ -297,17 +290,6 @@ Device::~Device() {
   if (wstream_) (void)hipStreamDestroy(wstream_);
   if (ev_in_) (void)hipEventDestroy(ev_in_);
   for (hipEvent_t e : ev_scan_) (void)hipEventDestroy(e);
-  for (DevBuf& b : x_foff_) b.release();
-  for (int k = 0; k < 2; k++) {
-    if (sb_done_[k]) (void)hipEventDestroy(sb_done_[k]);
-    desc_[k].release();
-    tiles_[k].release();
-  }
-  plan_.release();
-  for (DevBuf* b : {&sp_tc_, &dd_sig_, &dd_cnt_, &dd_list_, &dd_mrow_, &dd_keys_, &dd_vals_, &dd_slot_, &dd_rep_,
-                    &dd_nsets_, &dd_rlist_, &dd_sets_, &dd_spatches_, &dd_spcount_, &dd_wlist_, &dd_nwave_, &dd_mpair_, &msg_runs_,
-                    &msg_nruns_})
-    b->release();
   if (h_plan_) (void)hipHostFree(h_plan_);
   if (h_pin_) (void)hipHostFree(h_pin_);
 }

@@ -21,9 +21,15 @@ struct HipError {
 };
 void hip_check(hipError_t e, const char* where);
 
+// Device allocation owned by its holder: released by the destructor (a buffer added to Device
+// cannot leak on mq_index_destroy), never copied.
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   void ensure(size_t b);
   void release();
   template <class T>
@@ -47,6 +53,10 @@ struct DevMirror {
   T* d = nullptr;
   size_t cap = 0;
   uint64_t epoch = ~0ull;
+  DevMirror() = default;
+  DevMirror(const DevMirror&) = delete;
+  DevMirror& operator=(const DevMirror&) = delete;
+  ~DevMirror() { release(); }
   // reallocated or mostly dirty: uploaded whole now; else its dirty pages go to `st`
   void sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager& st);
   void release();
@@ -116,6 +126,17 @@ struct HostMatch {
 
 class Profiler {
  public:
+  Profiler() = default;
+  Profiler(const Profiler&) = delete;
+  Profiler& operator=(const Profiler&) = delete;
+  ~Profiler() {
+    for (auto& p : pending_) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    for (hipEvent_t e : free_) (void)hipEventDestroy(e);
+    if (cur_) (void)hipEventDestroy(cur_);
+  }
   void enable(bool on, bool work = false) {
     on_ = on;
     work_ = on && work;

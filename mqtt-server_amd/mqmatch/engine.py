@@ -773,6 +773,20 @@ def expand_device_spans(r, n, count=None):
     }
 
 
+def device_messages(r, n):
+    """Copy a DEVICE Messages result of n filters (mq_messages_device; r: MsgResult of device
+    pointers) to the host: (base u64[n], count u32[n], handles u64[n_handles])."""
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipDeviceSynchronize() == 0
+    base, count = np.zeros(n, np.uint64), np.zeros(n, np.uint32)
+    hs = np.zeros(int(r.n_handles), np.uint64)
+    for a, p in ((base, r.base), (count, r.count), (hs, r.handles)):
+        if a.nbytes and p:
+            assert hip.hipMemcpy(a.ctypes.data, p, a.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+    return base, count, hs
+
+
 ROW_IDENT = 0x40000000  # MQ_ROW_IDENT (include/mqmatch.h)
 ROW_DROP = 0x80000000   # MQ_ROW_DROP
 ROW_KIND_MASK = 0xC0000000

@@ -85,6 +85,7 @@ def lib():
     L.orc_fast_msg_bench.restype = C.c_double
     L.orc_root_children.argtypes = [C.c_void_p]
     L.orc_root_children.restype = C.c_uint64
+    L.orc_handle_digests.argtypes = [_u64p, _u32p, _u64p, C.c_uint64, C.c_uint32, _u64p]
     _LIB = L
     return L
 
@@ -128,6 +129,19 @@ def is_shared_filter(f):
 def equal_fold(s, t):
     sb, tb = _b(s), _b(t)
     return bool(lib().orc_equal_fold_ascii(sb, len(sb), tb, len(tb)))
+
+
+def handle_digests(base, count, handles, nthreads=8):
+    """Per-filter digests of an engine Messages result (handles[base[i], + count[i]) in any
+    order), computed as messages_digest_batch computes the oracle's."""
+    n = len(count)
+    base = np.ascontiguousarray(base, np.uint64)
+    count = np.ascontiguousarray(count, np.uint32)
+    handles = np.ascontiguousarray(handles, np.uint64)
+    dig = np.zeros(n, np.uint64)
+    lib().orc_handle_digests(_ptr(base, _u64p), _ptr(count, _u32p), _ptr(handles, _u64p), n, nthreads,
+                             _ptr(dig, _u64p))
+    return dig
 
 
 class OracleIndex:

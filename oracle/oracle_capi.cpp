@@ -319,6 +319,30 @@ int orc_messages_digest_batch(void* hp, const uint8_t* bytes, const uint64_t* of
   return 0;
 }
 
+// The same per-filter digest of an engine's Messages result (filter i's handles at
+// handles[base[i], + count[i]), any order): the checker's side of a comparison with the digests
+// above, for results too large to digest in numpy.
+int orc_handle_digests(const uint64_t* base, const uint32_t* count, const uint64_t* handles, uint64_t n,
+                       uint32_t nthreads, uint64_t* digests) {
+  if (nthreads == 0) nthreads = 1;
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nthreads; t++) {
+    th.emplace_back([&, t] {
+      std::vector<uint64_t> hs;
+      for (uint64_t i = t; i < n; i += nthreads) {
+        hs.assign(handles + base[i], handles + base[i] + count[i]);
+        std::sort(hs.begin(), hs.end());
+        uint64_t d = 0x6d716d61ull;
+        d = fold(d, hs.size());
+        for (uint64_t x : hs) d = fold(d, x);
+        digests[i] = d;
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  return 0;
+}
+
 // CPU baseline: `nthreads` std::threads each call Subscribers(topic) on the
 // frozen shared index, as Go connection goroutines do (topics.go:583 takes no writer lock).
 // Returns wall seconds; *sink receives a value derived from every result.
