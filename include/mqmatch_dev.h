@@ -26,7 +26,8 @@
                                      synchronisation, at its end (buffers sized by earlier batches; a batch
                                      they cannot hold runs again, sized by the host); 0: the host reads the
                                      walk's totals and the patch counts between kernels */
-#define MQ_OPT_SET_EXP 18         /* attribution experiments on the merge set pass (results WRONG; timing only):
+#define MQ_OPT_SET_EXP 18         /* attribution experiments on the merge set pass (bits 0-3: results WRONG,
+                                     timing only; accepted only by a library built with MQ_DEV_BUILD):
                                      bit 0 no partner links, bit 1 links loaded but not looked up, bit 2 no
                                      patch stores, bit 3 no binary search for a record's hit list; bit 4 (results
                                      exact) no early stop of a visit through a partner other than the record's first; bits 5 / 6 (exact)

@@ -258,7 +258,12 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_SET_GRID: set_grid_ = (uint32_t)v; return true;
     case MQ_OPT_ONE_SYNC: one_sync_ = v != 0; return true;
     case MQ_OPT_FUSE_DESC: fuse_desc_ = v != 0; return true;
-    case MQ_OPT_SET_EXP: set_exp_ = (uint32_t)v; return true;
+    case MQ_OPT_SET_EXP:
+#ifndef MQ_DEV_BUILD
+      if (v & 0xFu) return false;  // (bits 0-3 make results wrong: development builds only)
+#endif
+      set_exp_ = (uint32_t)v;
+      return true;
     case MQ_OPT_MSG_EXPORT: msg_export_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_GROUP:
       if (v != 0 && v != 4 && v != 8 && v != 16) return false;

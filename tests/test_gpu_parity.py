@@ -468,6 +468,51 @@ def test_spans_device_digest_parity(dedup, fuse, group, gpu_available):
     assert len(bad) == 0, f"{len(bad)} of {n} topics differ (first {bad[:5]})"
 
 
+@pytest.mark.parametrize("group", [16, 0])
+def test_walk_same_segment_many_parents(group, gpu_available):
+    """Thousands of particles share the segment "a" under other parents, so probe runs hold
+    slots of the topic's own segment under foreign parents before (or instead of) the topic's
+    edge; long (hashed) segments and a '+' level are mixed in, and the edge table runs at load
+    1/2 for longer probe runs. Both walks (the frontier walk, the walk thread per topic)."""
+    from mqmatch import engine as E
+    e, o = EngineAdapter(), OracleAdapter()
+    e.x.engine.set_option(E.OPT_EDGE_LOAD, 2)
+    e.x.engine.set_option(E.OPT_WALK_GROUP, group)
+    long = "s" * 40
+    subs = []
+    for i in range(3000):
+        subs += [(f"c{i % 97}", f"p{i}/a"), (f"d{i % 89}", f"p{i}/a/a/#")]
+        if i % 3 == 0:
+            subs.append((f"e{i % 13}", f"p{i}/+/a/{long}"))
+        if i % 5 == 0:
+            subs.append((f"f{i % 7}", "+/a/a/a"))
+    for c, f in subs:
+        assert e.subscribe(c, f, identifier=len(f) % 3) == o.subscribe(c, f, identifier=len(f) % 3)
+    topics = ([f"p{i}/a" for i in range(0, 3000, 7)] + [f"q{i}/a" for i in range(300)] +
+              [f"p{i}/a/a/a" for i in range(0, 3000, 11)] + [f"p{i}/x/a/{long}" for i in range(0, 3000, 9)] +
+              [f"p{i}/+/a/{long}" for i in range(0, 300, 9)] + [f"p{i}/a/a/a/a/a" for i in range(0, 3000, 13)])
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
+
+
+def test_walk_nested_plus_paths(gpu_available):
+    """Every literal/'+' path of depth 5 and 6 subscribed (and their '#' parents), so a topic's
+    frontier is as wide as it gets at each level (beyond the frontier's 16 particles the topic
+    goes to the walk thread per topic)."""
+    import itertools
+    e, o = EngineAdapter(), OracleAdapter()
+    for depth in (5, 6):
+        for k, bits in enumerate(itertools.product((0, 1), repeat=depth)):
+            f = "/".join(f"a{i}" if b == 0 else "+" for i, b in enumerate(bits))
+            assert e.subscribe(f"c{k % 50}", f, identifier=k % 4) == o.subscribe(f"c{k % 50}", f, identifier=k % 4)
+            if k % 3 == 0:
+                f2 = "/".join(f"a{i}" if b == 0 else "+" for i, b in enumerate(bits[:-1])) + "/#"
+                assert e.subscribe(f"h{k % 7}", f2) == o.subscribe(f"h{k % 7}", f2)
+    topics = ["/".join(f"a{i}" for i in range(d)) for d in range(1, 8)] + ["a0/x/a2/a3/x", "x/x/x/x/x/x"]
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
+
+
 def test_walk_trials_choose_and_stay_exact(gpu_available):
     """Device batches of 64k+ topics time both walks on their first batches (the frontier walk with
     the fused desc, the walk thread per topic with scan + desc) and keep the faster: every batch,
