@@ -301,7 +301,7 @@ Device::~Device() {
 
 uint64_t Device::device_bytes() const {
   uint64_t b = edges_.cap * sizeof(EdgeSlot) + walk_.cap * sizeof(NodeWalk) +
-               lists_.cap * sizeof(NodeLists) + msg_.cap * sizeof(NodeMsg) +
+               lists_.cap * sizeof(NodeLists) + inls_.cap * sizeof(NodeInl) + msg_.cap * sizeof(NodeMsg) +
                seginfo_.cap * sizeof(SegInfo) + segbytes_.cap + subs_.cap * sizeof(SubRec) +
                shr_.cap * sizeof(ShrRec) + inl_.cap * sizeof(InlRec) + children_.cap * sizeof(ChildRec) +
                mref_.cap * sizeof(MergeRef) + mpart_.cap * sizeof(MergePart) +
@@ -343,6 +343,7 @@ std::string Device::verify(Index& ix) {
   if (r.empty()) r = cmp_mirror(edges_, ix.edges, "edges");
   if (r.empty()) r = cmp_mirror(walk_, ix.walk, "walk");
   if (r.empty()) r = cmp_mirror(lists_, ix.lists, "lists");
+  if (r.empty()) r = cmp_mirror(inls_, ix.inls, "inls");
   if (r.empty()) r = cmp_mirror(msg_, ix.msg, "msg");
   if (r.empty()) r = cmp_mirror(seginfo_, ix.seginfo, "seginfo");
   if (r.empty()) r = cmp_mirror(segbytes_, ix.segbytes, "segbytes");
@@ -369,6 +370,7 @@ void Device::sync(Index& ix, hipStream_t s) {
   edges_.sync(ix.edges, s, &uploaded_, st);
   walk_.sync(ix.walk, s, &uploaded_, st);
   lists_.sync(ix.lists, s, &uploaded_, st);
+  inls_.sync(ix.inls, s, &uploaded_, st);
   msg_.sync(ix.msg, s, &uploaded_, st);
   seginfo_.sync(ix.seginfo, s, &uploaded_, st);
   segbytes_.sync(ix.segbytes, s, &uploaded_, st);
@@ -421,6 +423,7 @@ DevIndex Device::dev_index(const Index& ix) const {
   d.edge_mask = ix.edge_mask();
   d.walk = walk_.d;
   d.lists = lists_.d;
+  d.inls = inls_.d;
   d.msg = msg_.d;
   d.seginfo = seginfo_.d;
   d.segbytes = segbytes_.d;
@@ -1924,6 +1927,7 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
 template struct DevMirror<EdgeSlot>;
 template struct DevMirror<NodeWalk>;
 template struct DevMirror<NodeLists>;
+template struct DevMirror<NodeInl>;
 template struct DevMirror<NodeMsg>;
 template struct DevMirror<SegInfo>;
 template struct DevMirror<uint8_t>;

@@ -255,6 +255,7 @@ class Device {
   DevMirror<EdgeSlot> edges_;
   DevMirror<NodeWalk> walk_;
   DevMirror<NodeLists> lists_;
+  DevMirror<NodeInl> inls_;
   DevMirror<NodeMsg> msg_;
   DevMirror<SegInfo> seginfo_;
   DevMirror<uint8_t> segbytes_;

@@ -261,7 +261,8 @@ Index::Index(uint64_t expected_subs, uint64_t expected_nodes) {
   nh_.push_back(NodeHost{});
   nh_[0].live = true;
   walk.grow_to(1, NodeWalk{kNone, kNone, kParentMask, kNone});
-  lists.grow_to(1, NodeLists{});
+  lists.grow_to(1, kEmptyLists);
+  inls.grow_to(1, NodeInl{0, 0});
   msg.grow_to(1, NodeMsg{});
   seginfo.grow_to(1, SegInfo{0, 0});
   segbytes.grow_to(1, 0);
@@ -393,7 +394,8 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
     id = (uint32_t)nh_.size();
     nh_.push_back(NodeHost{});
     walk.grow_to(id + 1, NodeWalk{kNone, kNone, 0, kNone});
-    lists.grow_to(id + 1, NodeLists{});
+    lists.grow_to(id + 1, kEmptyLists);
+    inls.grow_to(id + 1, NodeInl{0, 0});
     msg.grow_to(id + 1, NodeMsg{});
     npair.grow_to(id + 1, NodePair{0, kNone, 0, 0});
   }
@@ -428,7 +430,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
     }
   }
   walk.at_w(id) = NodeWalk{kNone, kNone, parent | flags, segref};
-  NodeLists L{};
+  NodeLists L = kEmptyLists;
   L.flags = flags & kFlagSeg0Wild;
   lists.at_w(id) = L;
   NodeMsg M{};
@@ -490,11 +492,12 @@ void Index::remove_node(uint32_t n) {
   // release the node's (empty) slabs
   subs.release(lists.h[n].sub_off, h.sub_cap);
   shr.release(lists.h[n].shr_off, h.shr_cap);
-  inl.release(lists.h[n].inl_off, h.inl_cap);
+  inl.release(inls.h[n].off, h.inl_cap);
   children.release(msg.h[n].child_off, h.child_cap);
   merge_release(n);
   walk.at_w(n) = NodeWalk{kNone, kNone, 0, kNone};
-  lists.at_w(n) = NodeLists{};
+  lists.at_w(n) = kEmptyLists;
+  if (inls.h[n].cnt || inls.h[n].off) inls.at_w(n) = NodeInl{0, 0};
   msg.at_w(n) = NodeMsg{};
   if (sharded()) xinfo.at_w(n) = XInfo{kNone, 0, 0};
   h = NodeHost{};
@@ -529,7 +532,7 @@ uint32_t Index::seek(std::string_view filter, int d) const {  // topics.go:499-5
 
 void Index::trim(uint32_t n) {  // topics.go:516-522
   while (n != kRoot && !nh_[n].retain_path && nh_[n].n_children == 0 && sub_count(n) == 0 &&
-         lists.h[n].shr_cnt == 0 && lists.h[n].inl_cnt == 0) {
+         lists.h[n].shr_cnt == 0 && inls.h[n].cnt == 0) {
     uint32_t p = walk.h[n].parent_flags & kParentMask;
     remove_node(n);
     n = p;
@@ -584,7 +587,7 @@ void Index::merge_release(uint32_t n) {
     if (h.plist_cap) plist.release(P.list_off, h.plist_cap);
   }
   h.pent_cap = h.plist_cap = 0;
-  if (P.ent_mask != kNone || P.n_lists) npair.at_w(n) = NodePair{0, kNone, 0, 0};
+  if (P.ent_mask != kNone || P.n_lists) set_pair_header(n, NodePair{0, kNone, 0, 0});
 }
 
 void Index::flush_merge() {
@@ -688,7 +691,7 @@ void Index::merge_rebuild(uint32_t n) {
   }
   pent.live += lists_n;
   plist.live += hk.size();
-  npair.at_w(n) = NodePair{eo, mask, lo, lists_n};
+  set_pair_header(n, NodePair{eo, mask, lo, lists_n});
   nh_[n].pent_cap = ecap;
   nh_[n].plist_cap = lcap;
 }
@@ -784,7 +787,7 @@ void Index::pair_rehash(uint32_t n, uint32_t ecap) {
   nh_[n].pent_cap = ecap;
   P.ent_off = eo;
   P.ent_mask = mask;
-  npair.at_w(n) = P;
+  set_pair_header(n, P);
 }
 
 void Index::pair_add(uint32_t n, MergeInc& I, uint32_t h, const PairSlot& ps) {
@@ -800,7 +803,7 @@ void Index::pair_add(uint32_t n, MergeInc& I, uint32_t h, const PairSlot& ps) {
     ei = P.ent_off + sl;
     pent.m.at_w(ei) = PairEnt{h, plist.alloc(1), 0, 1};
     P.n_lists++;
-    npair.at_w(n) = P;
+    set_pair_header(n, P);
     pent.live++;
   }
   PairEnt e = pent.m.h[ei];
@@ -860,7 +863,7 @@ void Index::pair_remove(uint32_t n, MergeInc& I, uint32_t h, uint32_t k) {
   }
   pent.m.at_w(P.ent_off + i) = PairEnt{kNone, 0, 0, 0};
   P.n_lists--;
-  npair.at_w(n) = P;
+  set_pair_header(n, P);
   pent.live--;
 }
 
@@ -885,7 +888,9 @@ bool Index::check(std::string* why) {
     }
     if ((uint64_t)L.sub_off + L.n_direct + L.n_merge > subs.m.size() || L.n_direct + L.n_merge > nh_[n].sub_cap)
       return bad(at + ": subscription list out of bounds");
-    if ((uint64_t)L.shr_off + L.shr_cnt > shr.m.size() || (uint64_t)L.inl_off + L.inl_cnt > inl.m.size())
+    if ((uint64_t)L.shr_off + L.shr_cnt > shr.m.size() || (uint64_t)inls.h[n].off + inls.h[n].cnt > inl.m.size() ||
+        ((L.flags & kFlagInline) != 0) != (inls.h[n].cnt != 0) || L.ent_off != npair.h[n].ent_off ||
+        L.ent_mask != npair.h[n].ent_mask)
       return bad(at + ": shared/inline list out of bounds");
     for (uint32_t k = 0; k < L.n_direct + L.n_merge; k++) {
       const uint32_t pos = L.sub_off + k;
@@ -1413,13 +1418,14 @@ int Index::inline_subscribe(std::string_view filter, int32_t ident, uint32_t fil
     inl.m.at_w(pos) = rec;
     return 0;
   }
-  NodeLists& L = lists.at_w(n);
-  uint32_t old_off = L.inl_off, cnt = L.inl_cnt;
-  list_push(inl, L.inl_off, L.inl_cnt, nh_[n].inl_cap, rec);
-  if (L.inl_off != old_off)
+  NodeInl& I = inls.at_w(n);
+  uint32_t old_off = I.off, cnt = I.cnt;
+  list_push(inl, I.off, I.cnt, nh_[n].inl_cap, rec);
+  if (I.off != old_off)
     for (uint32_t i = 0; i < cnt; i++)
-      inl_pos_.put((uint64_t)n << 32 | (uint32_t)inl.m.h[L.inl_off + i].ident, L.inl_off + i);
-  inl_pos_.put(key, L.inl_off + cnt);
+      inl_pos_.put((uint64_t)n << 32 | (uint32_t)inl.m.h[I.off + i].ident, I.off + i);
+  inl_pos_.put(key, I.off + cnt);
+  if (!(lists.h[n].flags & kFlagInline)) lists.at_w(n).flags |= kFlagInline;
   return 1;
 }
 
@@ -1432,17 +1438,18 @@ int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
   uint64_t key = (uint64_t)n << 32 | (uint32_t)ident;
   uint32_t pos;
   if (inl_pos_.get(key, &pos)) {
-    NodeLists& L = lists.at_w(n);
-    uint32_t last = L.inl_off + L.inl_cnt - 1;
+    NodeInl& I = inls.at_w(n);
+    uint32_t last = I.off + I.cnt - 1;
     inl_pos_.erase(key);
     if (pos != last) {
       inl.m.at_w(pos) = inl.m.h[last];
       inl_pos_.put((uint64_t)n << 32 | (uint32_t)inl.m.h[pos].ident, pos);
     }
-    L.inl_cnt--;
+    I.cnt--;
     inl.live--;
+    if (!I.cnt) lists.at_w(n).flags &= ~kFlagInline;
   }
-  if (lists.h[n].inl_cnt == 0) trim(n);
+  if (inls.h[n].cnt == 0) trim(n);
   return 1;
 }
 

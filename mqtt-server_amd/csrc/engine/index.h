@@ -330,6 +330,7 @@ class Index {
   Mirror<EdgeSlot> edges;
   Mirror<NodeWalk> walk;
   Mirror<NodeLists> lists;
+  Mirror<NodeInl> inls;       // per node: its inline subscriptions (NodeLists kFlagInline)
   Mirror<NodeMsg> msg;
   Mirror<SegInfo> seginfo;
   Mirror<uint8_t> segbytes;
@@ -443,6 +444,15 @@ class Index {
     if (it != minc_.end()) it->second.dirty.push_back(pos - lists.h[n].sub_off);
   }
   void merge_release(uint32_t n);
+  // npair[n] = P, and the copy of its header in lists[n] (the walk's epilogue reads that one)
+  void set_pair_header(uint32_t n, const NodePair& P) {
+    npair.at_w(n) = P;
+    if (lists.h[n].ent_off != P.ent_off || lists.h[n].ent_mask != P.ent_mask) {
+      NodeLists& L = lists.at_w(n);
+      L.ent_off = P.ent_off;
+      L.ent_mask = P.ent_mask;
+    }
+  }
   // Merge records of a node with many partner links, updated in place (flush_merge): the
   // changed slots are taken off the pair lists and put back, instead of rebuilding the node's
   // links and pair block (a hot node's block is megabytes). Host only.

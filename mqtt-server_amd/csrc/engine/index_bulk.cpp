@@ -283,7 +283,8 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
   });
   grow.emplace_back([&] {
     lists.reserve_resident(n_end, threads);
-    lists.grow_to(n_end, NodeLists{});
+    lists.grow_to(n_end, kEmptyLists);
+    inls.grow_to(n_end, NodeInl{0, 0});
   });
   grow.emplace_back([&] {
     msg.reserve_resident(n_end, threads);
@@ -390,7 +391,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
           flags |= walk.h[parent].parent_flags & kFlagSeg0Wild;
         }
         walk.h[id] = NodeWalk{kNone, kNone, parent | flags, segref[k]};
-        NodeLists L{};
+        NodeLists L = kEmptyLists;
         L.flags = flags & kFlagSeg0Wild;
         lists.h[id] = L;
         NodeMsg M{};
@@ -434,7 +435,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
   });
   n_edges_ += n_new;
   edges.all_dirty = true;
-  walk.all_dirty = lists.all_dirty = msg.all_dirty = npair.all_dirty = true;
+  walk.all_dirty = lists.all_dirty = inls.all_dirty = msg.all_dirty = npair.all_dirty = true;
   if (sharded()) xinfo.all_dirty = true;
   bulk_children(first_new, threads);
 }

@@ -40,6 +40,7 @@ struct DevIndex {
   uint64_t edge_mask;
   const NodeWalk* walk;
   const NodeLists* lists;
+  const NodeInl* inls;  // per node: its inline subscriptions (read under NodeLists kFlagInline)
   const NodeMsg* msg;
   const SegInfo* seginfo;
   const uint8_t* segbytes;

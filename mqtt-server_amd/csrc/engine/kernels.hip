@@ -251,7 +251,7 @@ __device__ __forceinline__ void walk_topic(uint32_t t, const uint8_t* __restrict
             merge += L.n_merge;
           }
           shared += L.shr_cnt;
-          if (with_inline) inl += L.inl_cnt;
+          if (with_inline && (L.flags & kFlagInline)) inl += ix.inls[node].cnt;
         }
       } else {
         const bool subs_ok = !(dollar && wild);
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         merge += Ls.n_merge;
       }
       shared += Ls.shr_cnt;
-      if (gi.x & kGatherInline) inl += Ls.inl_cnt;
+      if ((gi.x & kGatherInline) && (Ls.flags & kFlagInline)) inl += ix.inls[node].cnt;
     } else {
       const uint32_t k0 = gi.y >> 30;  // how the path starts: literal 1, '+' 2, '#' 3
       const bool wild = k0 >= 2 || (k0 == 1 && lit0wild);
@@ -783,15 +783,10 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
   for (uint32_t i0 = 0; i0 < n_g; i0 += U) {
     uint32_t gwv[U];
     NodeLists Lv[U];
-    NodePair Pv[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) gwv[u] = i0 + u < n_g ? gw_src[i0 + u] : 0u;
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) Lv[u] = a.ix.lists[gwv[u] & kGatherNode];
-    if (SPANS) {
-#pragma unroll
-      for (uint32_t u = 0; u < U; u++) Pv[u] = a.ix.npair[gwv[u] & kGatherNode];
-    }
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
     const uint32_t i = i0 + u;
@@ -799,7 +794,8 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     const uint32_t gw = gwv[u];
     const NodeLists& L = Lv[u];
     const uint32_t rn = (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
-    const uint32_t in = (gw & kGatherInline) ? L.inl_cnt : 0u;
+    const NodeInl I = ((gw & kGatherInline) && (L.flags & kFlagInline)) ? a.ix.inls[gw & kGatherNode] : NodeInl{0, 0};
+    const uint32_t in = I.cnt;
     const uint64_t g = o0.g + i;
     GDesc d;
     d.r_pos = rpos;
@@ -807,16 +803,15 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
     d.s_pos = spos;
     d.s_src = L.shr_off;
     d.i_pos = (uint32_t)ipos;
-    d.i_src = L.inl_off;
+    d.i_src = I.off;
     d.word = gw;
     d.mdir = L.n_direct | ((gw & kGatherSubs) && L.n_merge ? kDescMerge : 0u);
     if (SPANS) {  // k_merge reads the pair block's header (and the rank key) from here
       d.i_pos = 0;
       d.i_src = 0;
       if (d.mdir & kDescMerge) {
-        const NodePair& P = Pv[u];
-        d.s_pos = P.ent_off;
-        d.s_src = P.ent_mask;
+        d.s_pos = L.ent_off;
+        d.s_src = L.ent_mask;
         if (a.ix.xinfo) {
           const uint64_t rk = a.ix.xinfo[gw & kGatherNode].rank;
           d.i_pos = (uint32_t)rk;
@@ -838,7 +833,7 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
         n_mg += L.n_direct + L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1;
       }
       a.spans[g] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
-      for (uint32_t k = 0; k < in; k++) a.inl_out[ipos + k] = a.ix.inl[L.inl_off + k];
+      for (uint32_t k = 0; k < in; k++) a.inl_out[ipos + k] = a.ix.inl[I.off + k];
     } else {
       // the k_copy tiles whose first row falls inside this gather start their cursor here
       for (uint32_t k = (rpos + kCopyTile - 1) / kCopyTile; k * kCopyTile < rpos + rn; k++) tile_r[k] = (uint32_t)g;
@@ -860,8 +855,7 @@ __global__ __launch_bounds__(256) void k_desc(DescArgs a) {
         const uint32_t gw = gw_src[i];
         const NodeLists L = a.ix.lists[gw & kGatherNode];
         const bool mg = (gw & kGatherSubs) && L.n_merge;
-        const NodePair P = mg ? a.ix.npair[gw & kGatherNode] : NodePair{0, kNone, 0, 0};
-        a.desc[o0.g + i] = GDesc{rp, L.sub_off, mg ? P.ent_off : sp, mg ? P.ent_mask : L.shr_off, 0u, 0u, gw,
+        a.desc[o0.g + i] = GDesc{rp, L.sub_off, mg ? L.ent_off : sp, mg ? L.ent_mask : L.shr_off, 0u, 0u, gw,
                                  L.n_direct | (mg ? kDescMerge : 0u)};
         rp += (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
         sp += L.shr_cnt;
@@ -890,9 +884,8 @@ __device__ __forceinline__ void write_gdesc(const DevIndex& ix, const uint32_t* 
     const uint32_t gw = gw_src[i];
     const NodeLists L = ix.lists[gw & kGatherNode];
     const bool mg = (gw & kGatherSubs) && L.n_merge;
-    const NodePair P = mg ? ix.npair[gw & kGatherNode] : NodePair{0, kNone, 0, 0};
     const uint64_t rk = mg && ix.xinfo ? ix.xinfo[gw & kGatherNode].rank : 0ull;
-    out[i] = GDesc{rp, L.sub_off, mg ? P.ent_off : sp, mg ? P.ent_mask : L.shr_off, (uint32_t)rk, (uint32_t)(rk >> 32),
+    out[i] = GDesc{rp, L.sub_off, mg ? L.ent_off : sp, mg ? L.ent_mask : L.shr_off, (uint32_t)rk, (uint32_t)(rk >> 32),
                    gw, L.n_direct | (mg ? kDescMerge : 0u)};
     rp += (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
     sp += L.shr_cnt;
@@ -923,16 +916,16 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
     const uint32_t i = r0 + sub;
     const bool act = i < n_g;
     uint32_t gw = 0;
-    NodeLists L{0, 0, 0, 0, 0, 0, 0, 0};
-    NodePair P{0, kNone, 0, 0};
-    if (act) {
+    NodeLists L = kEmptyLists;
+    if (act) {  // one record per gathered particle: its lists and its pair-block header
       gw = gw_at(i);
       L = a.ix.lists[gw & kGatherNode];
-      P = a.ix.npair[gw & kGatherNode];
     }
     const bool subs = act && (gw & kGatherSubs);
     const uint32_t rn = subs ? L.n_direct + L.n_merge : 0u;
-    const uint32_t in = (act && (gw & kGatherInline)) ? L.inl_cnt : 0u;
+    const NodeInl I = (act && (gw & kGatherInline) && (L.flags & kFlagInline)) ? a.ix.inls[gw & kGatherNode]
+                                                                                 : NodeInl{0, 0};
+    const uint32_t in = I.cnt;
     const bool ismg = subs && L.n_merge != 0;
     // set-relative rows hold 26 bits of slot: a larger merge gather keeps the topic apart
     const uint32_t inc = ismg ? (L.n_direct + L.n_merge < (1u << kSetRowBits) ? 1u : kPairMax + 1) : 0u;
@@ -941,14 +934,14 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
     const uint32_t rp = rpos + rn_i - rn, x = n_mg + inc_i - inc;
     const uint64_t ip = ipos + (in_i - in);
     if (act && fits) a.spans[g0 + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
-    for (uint32_t k = 0; k < in; k++) a.inl_out[ip + k] = a.ix.inl[L.inl_off + k];
+    for (uint32_t k = 0; k < in; k++) a.inl_out[ip + k] = a.ix.inl[I.off + k];
     if (ismg) {
       sig += mix64(((uint64_t)x << 32 | (gw & kGatherNode)) + 0x9e3779b97f4a7c15ull);
       if (x < kPairMax) {
         const uint64_t q = (uint64_t)t * kPairMax + x;
         a.mlist[q] = gw & kGatherNode;
         a.mrow[q] = rp;
-        a.mpair[q] = make_uint2(P.ent_off, P.ent_mask);
+        a.mpair[q] = make_uint2(L.ent_off, L.ent_mask);
         if (a.mrank) a.mrank[q] = a.ix.xinfo[gw & kGatherNode].rank;
       }
     }
@@ -981,9 +974,8 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
         const uint32_t gw = gw_at(i);
         const NodeLists L = a.ix.lists[gw & kGatherNode];
         const bool mg = (gw & kGatherSubs) && L.n_merge;
-        const NodePair P = mg ? a.ix.npair[gw & kGatherNode] : NodePair{0, kNone, 0, 0};
         const uint64_t rk = mg && a.ix.xinfo ? a.ix.xinfo[gw & kGatherNode].rank : 0ull;
-        a.desc[g0 + i] = GDesc{rp, L.sub_off, mg ? P.ent_off : sp, mg ? P.ent_mask : L.shr_off, (uint32_t)rk,
+        a.desc[g0 + i] = GDesc{rp, L.sub_off, mg ? L.ent_off : sp, mg ? L.ent_mask : L.shr_off, (uint32_t)rk,
                                (uint32_t)(rk >> 32), gw, L.n_direct | (mg ? kDescMerge : 0u)};
         rp += (gw & kGatherSubs) ? L.n_direct + L.n_merge : 0u;
         sp += L.shr_cnt;

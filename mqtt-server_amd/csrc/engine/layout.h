@@ -106,11 +106,19 @@ struct NodeWalk {
 // [sub_off, sub_off + n_direct) can never merge with another subscription of the same client
 // for any topic; [sub_off + n_direct, + n_merge) may (the client has another filter that can
 // co-match), and go through the per-topic merge table.
+// The record also carries the node's pair-block header (NodePair.ent_off / ent_mask, kept equal by
+// Index::set_pair_header), so the walk's epilogue reads one record per gathered particle instead
+// of two. Inline subscriptions (rare) have their own array, NodeInl, read only under kFlagInline.
 struct NodeLists {
   uint32_t sub_off, n_direct, n_merge;
   uint32_t shr_off, shr_cnt;
-  uint32_t inl_off, inl_cnt;
-  uint32_t flags;  // kFlagSeg0Wild
+  uint32_t ent_off, ent_mask;  // pair block: PairEnt hash table (kNone mask: no may-merge slots)
+  uint32_t flags;              // kFlagSeg0Wild | kFlagXNode | kFlagInline
+};
+constexpr NodeLists kEmptyLists{0, 0, 0, 0, 0, 0, 0xFFFFFFFFu, 0};
+constexpr uint32_t kFlagInline = 1u << 27;  // NodeLists.flags: the node holds inline subscriptions
+struct NodeInl {  // a node's inline subscriptions: inl[off, off + cnt)
+  uint32_t off, cnt;
 };
 
 // Retained-message state and children of a node, for Messages (32 B).
