@@ -21,24 +21,20 @@
 
 using namespace mq;
 
-// The handle's lock, a writer-preferring read/write protocol in the manner of Go's
-// sync.RWMutex (the reference's root lock, topics.go:402): `mu` serialises the handle's work
-// (updates, and the GPU round trip of a match); `views` counts host span results alive, which
-// pin the host image (their pools point into it) until mq_result_free. An update announces
-// itself (`writers`), takes `mu`, and waits for the views to drain; a call that would take a new
-// view first waits while any update is announced, with no time bound, so a steady stream of
-// overlapping readers cannot starve updates. `views` / `writers` live under their own mutex
-// `vmu`, which is never held across GPU work, so freeing a result never waits for a match in
-// flight. As with a Go RWMutex read lock, a thread must free its span results before it takes a
-// new one or updates the index (a reader that holds a view and asks for another while an update
-// waits would wait for itself). Results hold a reference, so freeing one after
+// The handle's lock (the reference's root lock, topics.go:402): `mu` serialises the handle's work
+// (updates, and the GPU round trip of a match). Host span results point into the host image's
+// subscription pools until mq_result_free; `views` records them by generation, and the index
+// copies a slab before it changes one that a live result may see and keeps what it frees until
+// no live result can see it (Index::begin_op), so an update never waits for results. The one
+// exception is a bulk subscribe (mq_subscribe_bulk), which rewrites the pools in place: it
+// announces itself (`views.drains`), takes `mu` and waits for the live results to be freed; a
+// call that would publish a new result first waits while a bulk update is announced (so readers
+// cannot starve it). `views` has its own mutex, never held across GPU work, so freeing a result
+// never waits for a match in flight. Results hold a reference, so freeing one after
 // mq_index_destroy is safe.
 struct IndexLock {
   std::mutex mu;
-  std::mutex vmu;
-  std::condition_variable vcv;
-  uint64_t views = 0;
-  uint64_t writers = 0;
+  ViewTracker views;
 };
 
 struct mq_index {
@@ -72,7 +68,8 @@ struct MatchHolder {
 struct SpanHolder {
   mq_span_result pub;
   HostSpans data;
-  std::shared_ptr<IndexLock> lk;  // the pinned index's lock (views)
+  std::shared_ptr<IndexLock> lk;  // the index's lock (views)
+  uint64_t gen = 0;                // this result's generation (ViewTracker)
 };
 struct MsgHolder {
   mq_msg_result pub;
@@ -93,41 +90,56 @@ int fail(int code, const std::string& msg) {
 }
 
 // What a guarded call does to the host image (IndexLock).
-enum class Access { kRead, kUpdate, kPin };
+// kUpdate: copy-on-write against the live results, never waits for them; kDrain: rewrites the pools
+// in place, waits for the live results to be freed; kPin: publishes a host span result.
+enum class Access { kRead, kUpdate, kDrain, kPin };
 
-// Runs f under the handle's lock. kUpdate (writes the host image): announce, take the lock, wait
-// for the host span results that pin the image to be freed. kPin (publishes a host span result):
-// wait until no update is announced, then take the lock.
+// Runs f under the handle's lock (IndexLock).
 template <class F>
 int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
   if (!idx) return fail(MQ_EINVAL, "null index");
   IndexLock& L = *idx->lk;
-  struct Writer {  // the announcement, withdrawn however the call ends
-    IndexLock* L = nullptr;
-    ~Writer() {
-      if (!L) return;
+  ViewTracker& V = L.views;
+  struct Drain {  // the announcement, withdrawn however the call ends
+    ViewTracker* V = nullptr;
+    ~Drain() {
+      if (!V) return;
       {
-        std::lock_guard<std::mutex> g(L->vmu);
-        L->writers--;
+        std::lock_guard<std::mutex> g(V->mu);
+        V->drains--;
       }
-      L->vcv.notify_all();
+      V->cv.notify_all();
     }
-  } writer;
+  } drain;
   try {
-    if (access == Access::kUpdate) {
+    if (access == Access::kDrain) {
       {
-        std::lock_guard<std::mutex> g(L.vmu);
-        L.writers++;
+        std::lock_guard<std::mutex> g(V.mu);
+        V.drains++;
       }
-      writer.L = &L;
+      drain.V = &V;
     } else if (access == Access::kPin) {
-      std::unique_lock<std::mutex> g(L.vmu);
-      L.vcv.wait(g, [&] { return L.writers == 0; });
+      std::unique_lock<std::mutex> g(V.mu);
+      V.cv.wait(g, [&] { return V.drains == 0; });
     }
-    std::unique_lock<std::mutex> lk(L.mu);
-    if (access == Access::kUpdate) {
-      std::unique_lock<std::mutex> g(L.vmu);
-      L.vcv.wait(g, [&] { return L.views == 0; });
+    std::unique_lock<std::mutex> lk(L.mu, std::defer_lock);
+    if (access == Access::kDrain) {  // wait for the live results without holding `mu`
+      for (;;) {
+        {
+          std::unique_lock<std::mutex> g(V.mu);
+          V.cv.wait(g, [&] { return V.live.empty(); });
+        }
+        lk.lock();
+        bool empty;
+        {
+          std::lock_guard<std::mutex> g(V.mu);
+          empty = V.live.empty();
+        }
+        if (empty) break;  // (a match that was already past the announcement published one)
+        lk.unlock();
+      }
+    } else {
+      lk.lock();
     }
     return f();
   } catch (const HipError& e) {
@@ -158,6 +170,7 @@ int mq_index_create(const mq_config* cfg, mq_index** out) {
       return fail(MQ_EINVAL, "bad shard_index / shard_count");
     }
     idx->ix.reset(new Index(idx->cfg.expected_subs, idx->cfg.expected_nodes));
+    idx->ix->set_views(&idx->lk->views);
     if (idx->cfg.shard_count > 1) idx->ix->set_shard(idx->cfg.shard_index, idx->cfg.shard_count);
     *out = idx;
     return 0;
@@ -234,7 +247,7 @@ int mq_subscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs,
   return guarded(idx, [&] {
     idx->ix->subscribe_bulk(bytes, offs, client_ids, filter_ids, qos, flags, identifiers, n, out_new);
     return 0;
-  }, Access::kUpdate);
+  }, Access::kDrain);
 }
 
 int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint64_t* handles,
@@ -277,7 +290,7 @@ int mq_match_batch(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
 
 namespace {
 // A host span result: the device arrays copied into h->data, the pools pointing at the host
-// image, which the result pins (views) until mq_result_free. Under the handle lock.
+// image (copy-on-write keeps what the result sees until mq_result_free). Under the handle lock.
 int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_span_result& dev_out,
                        mq_span_result** out) {
   mq_span_result& r = h->pub;
@@ -299,10 +312,7 @@ int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_sp
   r.sub_pool_len = idx->ix->subs.m.size();
   r.shared_pool_len = idx->ix->shr.m.size();
   h->lk = idx->lk;
-  {
-    std::lock_guard<std::mutex> g(idx->lk->vmu);
-    idx->lk->views++;  // the pools stay put until mq_result_free
-  }
+  h->gen = idx->lk->views.publish();
   *out = &h->pub;
   std::lock_guard<std::mutex> lk(g_res_mu);
   g_results[&h->pub] = 4;
@@ -527,12 +537,9 @@ void mq_result_free(void* r) {
   if (kind == 4) {
     SpanHolder* h = reinterpret_cast<SpanHolder*>(r);
     std::shared_ptr<IndexLock> lk = h->lk;
+    const uint64_t gen = h->gen;
     delete h;
-    {
-      std::lock_guard<std::mutex> g(lk->vmu);
-      lk->views--;
-    }
-    lk->vcv.notify_all();
+    lk->views.release(gen);
   }
 }
 

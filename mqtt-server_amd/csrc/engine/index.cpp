@@ -372,11 +372,14 @@ void Index::edge_erase(uint32_t parent, const SegKey& k, uint32_t child) {
 // ---- nodes ---------------------------------------------------------------------------------------
 template <class T, class Rec>
 void Index::list_push(SlabPool<T>& pool, uint32_t& off, uint32_t& cnt, uint32_t& cap, const Rec& r) {
+  constexpr bool kShared = std::is_same<T, ShrRec>::value;  // (live host results point into shr)
   if (cnt + 1 > cap) {
     uint32_t nc = cap ? cap * 2 : 1;
+    if constexpr (kShared) guard_growth(pool.m, pool.m.size() + nc, retired_shr_);
     uint32_t no = pool.alloc(nc);
     for (uint32_t i = 0; i < cnt; i++) pool.m.at_w(no + i) = pool.m.h[off + i];
-    pool.release(off, cap);
+    if constexpr (kShared) retire(1, off, cap);
+    else pool.release(off, cap);
     off = no;
     cap = nc;
   }
@@ -490,8 +493,8 @@ void Index::remove_node(uint32_t n) {
   child_rec_sync(p);
   nh_[p].n_children--;
   // release the node's (empty) slabs
-  subs.release(lists.h[n].sub_off, h.sub_cap);
-  shr.release(lists.h[n].shr_off, h.shr_cap);
+  retire(0, lists.h[n].sub_off, h.sub_cap);
+  retire(1, lists.h[n].shr_off, h.shr_cap);
   inl.release(inls.h[n].off, h.inl_cap);
   children.release(msg.h[n].child_off, h.child_cap);
   merge_release(n);
@@ -985,11 +988,93 @@ bool Index::check(std::string* why) {
   return true;
 }
 
+// ---- copy-on-write against live host results (ViewTracker) ------------------------------------
+void Index::begin_op() {
+  if (!views_) return;
+  uint64_t min_live = 0;
+  {
+    std::lock_guard<std::mutex> g(views_->mu);
+    op_gen_ = views_->gen;
+    op_max_ = views_->live.empty() ? 0 : *views_->live.rbegin();
+    min_live = views_->live.empty() ? 0 : *views_->live.begin();
+  }
+  // what was retired at generation `tag` is seen only by live results of that generation or older
+  // (the tags grow along the queues)
+  auto unseen = [&](uint64_t tag) { return min_live == 0 || min_live > tag; };
+  while (!retired_.empty() && unseen(retired_.front().tag)) {
+    const Retired r = retired_.front();
+    retired_.pop_front();
+    if (r.pool == 0) subs.release(r.off, r.cap);
+    else shr.release(r.off, r.cap);
+  }
+  while (!retired_subs_.empty() && unseen(retired_subs_.front().first)) retired_subs_.pop_front();
+  while (!retired_shr_.empty() && unseen(retired_shr_.front().first)) retired_shr_.pop_front();
+}
+
+uint32_t Index::fresh_gen() {
+  if (op_gen_ + 1 - gen_base_ >= 0xFFFFFFF0ull) {  // the 32-bit generations run out: every slab is old
+    for (size_t n = 0; n < nh_.size(); n++) nh_[n].sub_gen = nh_[n].shr_gen = 0;
+    gen_base_ = op_gen_;
+  }
+  return (uint32_t)(op_gen_ + 1 - gen_base_);  // seen by results published from now on
+}
+
+void Index::retire(int pool, uint32_t off, uint32_t cap) {
+  if (!cap) return;
+  if (!op_max_) {  // no live result
+    if (pool == 0) subs.release(off, cap);
+    else shr.release(off, cap);
+    return;
+  }
+  retired_.push_back(Retired{op_gen_, pool, off, cap});
+}
+
+template <class T>
+void Index::guard_growth(Mirror<T>& m, size_t need, std::deque<std::pair<uint64_t, std::vector<T>>>& keep) {
+  if (!op_max_ || need <= m.h.capacity()) return;
+  // a live result points into this buffer: the pool moves to a new one, the old one stays for it
+  std::vector<T> fresh;
+  fresh.reserve(std::max(need, 2 * m.h.capacity()));
+  fresh.assign(m.h.begin(), m.h.end());
+  keep.emplace_back(op_gen_, std::move(m.h));
+  m.h = std::move(fresh);
+  m.epoch++;
+  m.all_dirty = true;
+}
+
+void Index::sub_cow(uint32_t n) {
+  if (nh_[n].sub_cap && seen(nh_[n].sub_gen)) sub_move(n, nh_[n].sub_cap);
+}
+
+void Index::shr_cow(uint32_t n) {
+  const uint32_t cap = nh_[n].shr_cap;
+  if (!cap || !seen(nh_[n].shr_gen)) return;
+  guard_growth(shr.m, shr.m.size() + cap, retired_shr_);
+  NodeLists& L = lists.at_w(n);
+  const uint32_t no = shr.alloc(cap), old = L.shr_off;
+  if (shr_group_.size() < shr.m.size()) shr_group_.resize(shr.m.size());
+  for (uint32_t i = 0; i < L.shr_cnt; i++) {
+    shr.m.at_w(no + i) = shr.m.h[old + i];
+    shr_group_[no + i] = shr_group_[old + i];
+    shr_pos_[ShrKey{n, shr_group_[no + i], shr.m.h[no + i].client}] = no + i;
+  }
+  retire(1, old, cap);
+  L.shr_off = no;
+  nh_[n].shr_gen = fresh_gen();
+}
+
 void Index::sub_ensure(uint32_t n, uint32_t need) {
   uint32_t cap = nh_[n].sub_cap;
   if (need <= cap) return;
   uint32_t nc = cap ? cap : 1;
   while (nc < need) nc *= 2;
+  sub_move(n, nc);
+}
+
+// n's subscription list to a new slab of nc records (the slots keep their places k)
+void Index::sub_move(uint32_t n, uint32_t nc) {
+  const uint32_t cap = nh_[n].sub_cap;
+  guard_growth(subs.m, subs.m.size() + nc, retired_subs_);
   NodeLists& L = lists.at_w(n);
   uint32_t no = subs.alloc(nc), cnt = L.n_direct + L.n_merge;
   subp_.resize(subs.m.size(), PartList{0, 0, 0});
@@ -998,13 +1083,21 @@ void Index::sub_ensure(uint32_t n, uint32_t need) {
     if (mref.size() < subs.m.size()) mref.grow_to(subs.m.size(), MergeRef{0, 0});
     for (uint32_t i = L.n_direct; i < cnt; i++) mref.at_w(no + i) = mref.h[L.sub_off + i];
   }
-  subs.release(L.sub_off, cap);
+  retire(0, L.sub_off, cap);
   L.sub_off = no;
   nh_[n].sub_cap = nc;
+  nh_[n].sub_gen = fresh_gen();
+}
+
+uint32_t Index::cow_pos(uint32_t n, uint32_t pos) {
+  const uint32_t k = pos - lists.h[n].sub_off;
+  sub_cow(n);
+  return lists.h[n].sub_off + k;
 }
 
 uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
   sub_ensure(n, sub_count(n) + 1);
+  if (!merge && lists.h[n].n_merge) sub_cow(n);  // (the first may-merge slot moves behind the others)
   NodeLists& L = lists.at_w(n);
   uint32_t base = L.sub_off, pos;
   if (merge) {
@@ -1025,6 +1118,7 @@ uint32_t Index::sub_add(uint32_t n, const SubRec& r, bool merge) {
 }
 
 void Index::sub_remove(uint32_t n, uint32_t pos) {
+  pos = cow_pos(n, pos);
   NodeLists& L = lists.at_w(n);
   uint32_t base = L.sub_off;
   if (pos < base + L.n_direct) {
@@ -1044,10 +1138,10 @@ void Index::sub_remove(uint32_t n, uint32_t pos) {
 }
 
 void Index::sub_set_merge(uint32_t n, uint32_t pos, bool merge) {
+  if (merge == (pos >= lists.h[n].sub_off + lists.h[n].n_direct)) return;
+  pos = cow_pos(n, pos);
   NodeLists& L = lists.at_w(n);
   uint32_t base = L.sub_off;
-  bool is_merge = pos >= base + L.n_direct;
-  if (merge == is_merge) return;
   uint32_t other = merge ? base + L.n_direct - 1 : base + L.n_direct;
   const SubRec a = subs.m.h[pos];
   const PartList ap = subp_[pos];
@@ -1255,6 +1349,7 @@ std::string shard_key(std::string_view filter, bool share) {
 int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_id, uint8_t qos,
                      uint8_t flags, int32_t ident) {
   version_++;
+  begin_op();
   const bool share = is_share_prefix(segment_at(filter, 0));
   if (sharded() && shard_hash(shard_key(filter, share)) % n_shards_ != shard_) {
     if (share) return 0;  // the owner answers
@@ -1275,7 +1370,8 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
     auto it = shr_pos_.find(key);
     ShrRec rec{filter_id, client};
     if (it != shr_pos_.end()) {
-      shr.m.at_w(it->second) = rec;
+      shr_cow(n);
+      shr.m.at_w(shr_pos_[key]) = rec;
       return 0;
     }
     NodeLists& L = lists.at_w(n);
@@ -1288,6 +1384,7 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
         shr_group_[L.shr_off + i] = g;
         shr_pos_[ShrKey{n, g, shr.m.h[L.shr_off + i].client}] = L.shr_off + i;
       }
+      nh_[n].shr_gen = fresh_gen();
     }
     shr_pos_[key] = L.shr_off + cnt;
     shr_group_[L.shr_off + cnt] = gid;
@@ -1299,6 +1396,7 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
                  ((uint32_t)((flags >> 2) & 3) << kMetaRhShift)};
   uint32_t pos;
   if (sub_pos_.get((uint64_t)n << 32 | client, &pos)) {
+    pos = cow_pos(n, pos);
     const SubRec old = subs.m.h[pos];
     subs.m.at_w(pos) = rec;
     const PartList& p = subp_[pos];  // the partners' links carry this subscription's Qos / NoLocal,
@@ -1344,6 +1442,7 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
 // topics.go:423-448
 int Index::unsubscribe(std::string_view filter, uint32_t client) {
   version_++;
+  begin_op();
   bool share = is_share_prefix(segment_at(filter, 0));
   if (sharded() && shard_hash(shard_key(filter, share)) % n_shards_ != shard_) {
     if (!share) {  // the owner drops the subscription; here it stops being a foreign partner
@@ -1359,6 +1458,8 @@ int Index::unsubscribe(std::string_view filter, uint32_t client) {
     if (git != group_ids_.end()) {
       auto it = shr_pos_.find(ShrKey{n, git->second, client});
       if (it != shr_pos_.end()) {
+        shr_cow(n);
+        it = shr_pos_.find(ShrKey{n, git->second, client});
         NodeLists& L = lists.at_w(n);
         uint32_t pos = it->second, last = L.shr_off + L.shr_cnt - 1;
         shr_pos_.erase(it);
@@ -1409,6 +1510,7 @@ static std::string_view inline_key(const int32_t& ident) {
 
 int Index::inline_subscribe(std::string_view filter, int32_t ident, uint32_t filter_id) {
   version_++;
+  begin_op();
   if (sharded() && shard_hash(inline_key(ident)) % n_shards_ != shard_) return 0;  // by identifier
   uint32_t n = set(filter, 0);
   uint64_t key = (uint64_t)n << 32 | (uint32_t)ident;
@@ -1432,6 +1534,7 @@ int Index::inline_subscribe(std::string_view filter, int32_t ident, uint32_t fil
 // topics.go:382-397
 int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
   version_++;
+  begin_op();
   uint32_t n = seek(filter, 0);
   if (n == kNone) return 0;
   if (sharded() && shard_hash(inline_key(ident)) % n_shards_ != shard_) return 1;  // exists here
@@ -1460,6 +1563,7 @@ int Index::inline_unsubscribe(std::string_view filter, int32_t ident) {
 int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t payload_len,
                               bool retain) {
   version_++;
+  begin_op();
   retained_version_++;
   if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;  // retained: by topic
   const uint32_t n = set(topic, 0);
@@ -1501,6 +1605,7 @@ int64_t Index::retain_message(std::string_view topic, uint64_t handle, uint32_t 
 // Retained.Delete (server.go:1726): the map entry only; the particle keeps retainPath (Q12).
 int Index::retained_delete(std::string_view topic) {
   version_++;
+  begin_op();
   retained_version_++;
   if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;
   if (topic.empty()) {
@@ -1522,6 +1627,7 @@ int Index::retained_delete(std::string_view topic) {
 // is the topic becomes live again (Q12 re-add); the "" entry is kept apart (Q6).
 int Index::retained_set(std::string_view topic, uint64_t handle, uint32_t payload_len, bool retain) {
   version_++;
+  begin_op();
   retained_version_++;
   if (sharded() && shard_hash(topic) % n_shards_ != shard_) return 0;
   const bool flag = retain && payload_len > 0;  // what RetainMessage's -1 answer reads (topics.go:467)

@@ -12,7 +12,11 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <new>
+#include <set>
 #include <type_traits>
 #include <cstdint>
 #include <string>
@@ -267,6 +271,31 @@ class StrTable {
   std::vector<uint32_t> slots_;
 };
 
+// Host span results alive (mq_match_spans results point into the subscription pools; capi.cpp).
+// Each gets a generation when published; the index copies a slab before it changes one that a live
+// result may see, and keeps released slabs and outgrown pool buffers until no live result can see
+// them (Index::begin_op) — so updates never wait for results (the reference's writers never wait
+// for a reader's maps either, topics.go:270-277, 401-419). Owned by the handle's lock record, so a
+// result freed after the index is destroyed still finds it.
+struct ViewTracker {
+  std::mutex mu;
+  std::multiset<uint64_t> live;  // generations of the live results
+  uint64_t gen = 0;              // generations handed out
+  uint64_t publish() {
+    std::lock_guard<std::mutex> g(mu);
+    live.insert(++gen);
+    return gen;
+  }
+  std::condition_variable cv;  // a bulk update waits on it for the live results to drain
+  uint64_t drains = 0;          // bulk updates announced (a new result waits for them)
+  void release(uint64_t v) {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = live.find(v);
+    if (it != live.end()) live.erase(it);
+    cv.notify_all();
+  }
+};
+
 struct NodeHost {
   SegKey key{0, 0};
   uint32_t str = 0;        // interned segment string id (0 = "+", 1 = "#")
@@ -277,6 +306,8 @@ struct NodeHost {
   uint32_t mpart_off = 0, mpart_cap = 0;  // the node's slab of device partner links
   uint32_t pent_cap = 0, plist_cap = 0;    // its pair block slabs
   uint32_t x_slots = 0;                    // sharded: may-merge slots with a foreign partner
+  uint32_t sub_gen = 0, shr_gen = 0;       // when its subs / shared slab was filled (Index::fresh_gen;
+                                           //   0: before the generation base)
   uint16_t depth = 0;
   bool live = false;
   bool retain_path = false;
@@ -301,6 +332,9 @@ class Index {
   // is the owner's (Subscribe, InlineSubscribe, RetainMessage: others return 0) or the OR over
   // shards (Unsubscribe / InlineUnsubscribe: particle exists, Q10). Call before any update.
   void set_shard(uint32_t shard, uint32_t n_shards);
+  // The live host results (ViewTracker): set by the C-ABI when the index is created.
+  void set_views(ViewTracker* v) { views_ = v; }
+  uint64_t retired_slabs() const { return retired_.size(); }
   uint32_t shard() const { return shard_; }
   uint32_t n_shards() const { return n_shards_; }
   bool sharded() const { return n_shards_ > 1; }
@@ -427,6 +461,17 @@ class Index {
 
   template <class T, class Rec>
   void list_push(SlabPool<T>& pool, uint32_t& off, uint32_t& cnt, uint32_t& cap, const Rec& r);
+  // copy-on-write against live host results (ViewTracker)
+  void begin_op();  // an update starts: snapshot the live results; free what none of them can see
+  bool seen(uint32_t g) const { return op_max_ && (g == 0 || op_max_ >= gen_base_ + g); }
+  uint32_t fresh_gen();  // the generation of a slab filled now
+  void retire(int pool, uint32_t off, uint32_t cap);  // pool 0 subs, 1 shr: free now or once unseen
+  void sub_cow(uint32_t n);  // n's subs slab moves to a copy if a live result may see it
+  void sub_move(uint32_t n, uint32_t nc);
+  uint32_t cow_pos(uint32_t n, uint32_t pos);  // sub_cow, then pos's place in the (new) slab
+  void shr_cow(uint32_t n);
+  template <class T>
+  void guard_growth(Mirror<T>& m, size_t need, std::deque<std::pair<uint64_t, std::vector<T>>>& keep);
 
   bool sub_is_merge(uint32_t n, uint32_t pos) const { return pos >= lists.h[n].sub_off + lists.h[n].n_direct; }
   void merge_dirty(uint32_t n) {
@@ -475,6 +520,17 @@ class Index {
   void pair_rehash(uint32_t n, uint32_t ecap);
   uint32_t sub_count(uint32_t n) const { return lists[n].n_direct + lists[n].n_merge; }
 
+  ViewTracker* views_ = nullptr;
+  uint64_t op_gen_ = 0, op_max_ = 0;  // this update's snapshot: generations handed out, newest live (0: none)
+  uint64_t gen_base_ = 0;             // NodeHost gens count from here
+  struct Retired {
+    uint64_t tag;  // freed once no live result is this old
+    int pool;
+    uint32_t off, cap;
+  };
+  std::deque<Retired> retired_;
+  std::deque<std::pair<uint64_t, std::vector<SubRec>>> retired_subs_;  // outgrown pool buffers
+  std::deque<std::pair<uint64_t, std::vector<ShrRec>>> retired_shr_;
   PodVec<NodeHost> nh_;
   std::vector<uint32_t> free_nodes_;
   uint64_t n_live_nodes_ = 0, n_edges_ = 0, n_tombs_ = 0, n_merge_ = 0;

@@ -508,6 +508,7 @@ void Index::subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uin
     return;
   }
   version_++;
+  begin_op();  // (no live result: mq_subscribe_bulk drains them)
   const unsigned threads = build_threads();
   // 0. classify: this shard's non-shared / shared entries and their paths (Index::set(f, 0) /
   // set(f, 2), isolateParticle semantics for short shared filters, Q13); the rest is foreign

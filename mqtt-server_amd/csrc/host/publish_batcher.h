@@ -14,7 +14,14 @@
 //
 // Sealing policy: the dispatcher takes everything queued when the previous batch is done — so
 // under load a batch holds what arrived while the last one was matched — and, when fewer than
-// min_fill topics are queued, waits up to max_delay for more. max_batch bounds a batch.
+// min_fill topics are queued and the previous batch held more than one (there is concurrent
+// load), waits up to max_delay for more; a lone topic on an idle stage is matched at once.
+// max_batch bounds a batch.
+//
+// Errors: a match call that throws is tried once more (a transient failure costs one retry, not
+// the batch); if that throws too, every ticket of the batch rethrows it from get() — the callers
+// of that one batch see the error, the stage goes on with the next batch (the Go shim's batcher
+// answers them with empty results instead, go/topics_gpu.go).
 //   PublishBatcher      tickets of Subscribers (the Go-shaped maps, TopicsIndex::SubscribersBatch)
 //   PublishViewBatcher  tickets of TopicView (the recipients as a view over the batch's span
 //                       result, TopicsIndex::SubscribersViews: no maps are built)
@@ -68,6 +75,8 @@ class BasicBatcher {
  public:
   struct Stats {
     uint64_t batches = 0;     // match calls
+    uint64_t retried = 0;     // batches whose first match call failed
+    uint64_t failed = 0;      // batches whose retry failed too (their tickets throw)
     uint64_t topics = 0;      // topics matched
     uint64_t largest = 0;     // largest batch
     // the dispatcher's time (ns): waiting for topics, sealing, in the match call, completing
@@ -165,7 +174,7 @@ class BasicBatcher {
         cv_.wait(lk, [&] { return stop_ || queued_.load(std::memory_order_acquire) != 0; });
         if (stop_ && queued_.load() == 0) return;
         // a small batch waits up to max_delay for more (the clock starts at its first topic)
-        if (!stop_ && queued_.load() < min_fill_) {
+        if (!stop_ && last_n_ > 1 && queued_.load() < min_fill_) {
           const auto until = std::chrono::steady_clock::now() + max_delay_;
           cv_.wait_until(lk, until, [&] { return stop_ || queued_.load() >= min_fill_; });
         }
@@ -207,11 +216,17 @@ class BasicBatcher {
       std::shared_ptr<const Batch> res;
       std::exception_ptr err;
       const auto c2 = Clock::now();
-      try {
-        res = match_(batch);
-      } catch (...) {
-        err = std::current_exception();
+      bool retried = false;
+      for (int attempt = 0; attempt < 2 && !res; attempt++) {
+        try {
+          err = nullptr;
+          res = match_(batch);
+        } catch (...) {
+          err = std::current_exception();
+          retried = attempt == 0;
+        }
       }
+      last_n_ = n;
       const auto c3 = Clock::now();
       for (auto& sg : segs) {
         {
@@ -229,6 +244,8 @@ class BasicBatcher {
       const auto c4 = Clock::now();
       std::lock_guard<std::mutex> lk(mu_);
       st_.batches++;
+      st_.retried += retried;
+      st_.failed += err != nullptr;
       st_.topics += n;
       st_.largest = std::max<uint64_t>(st_.largest, n);
       st_.wait_ns += ns(c0, c1);
@@ -245,6 +262,7 @@ class BasicBatcher {
   Shard shards_[kShards];
   std::atomic<uint64_t> queued_{0};
   uint32_t rr_ = 0;
+  uint64_t last_n_ = 0;  // the previous batch's topics (dispatcher thread)
   mutable std::mutex mu_;
   std::condition_variable cv_;
   bool stop_ = false;

@@ -24,9 +24,11 @@ import "C"
 
 import (
 	"fmt"
+	"log/slog"
 	"math"
 	"strings"
 	"sync"
+	"sync/atomic"
 	"time"
 	"unsafe"
 
@@ -161,7 +163,8 @@ type RetainedPackets struct {
 	x *TopicsIndex
 }
 
-// Add (packets/packets.go:79-83).
+// Add (packets/packets.go:79-83). An engine error is logged and the store left as it was, so the
+// store and the engine stay in step.
 func (r *RetainedPackets) Add(id string, val packets.Packet) {
 	x := r.x
 	x.upd.Lock()
@@ -170,8 +173,11 @@ func (r *RetainedPackets) Add(id string, val packets.Packet) {
 	h := x.topics.intern(id)
 	x.tables.Unlock()
 	p, n := cstr(id)
-	must(C.mq_retained_set(x.h, p, n, C.uint64_t(h), C.uint32_t(len(val.Payload)), boolU8(val.FixedHeader.Retain)),
-		"mq_retained_set")
+	if _, err := check(C.mq_retained_set(x.h, p, n, C.uint64_t(h), C.uint32_t(len(val.Payload)),
+		boolU8(val.FixedHeader.Retain)), "mq_retained_set"); err != nil {
+		x.tidyTopic(id)
+		return
+	}
 	x.mapAdd(id, h, val)
 }
 
@@ -181,32 +187,44 @@ func (r *RetainedPackets) Delete(id string) {
 	x.upd.Lock()
 	defer x.upd.Unlock()
 	p, n := cstr(id)
-	must(C.mq_retained_delete(x.h, p, n), "mq_retained_delete")
+	if _, err := check(C.mq_retained_delete(x.h, p, n), "mq_retained_delete"); err != nil {
+		return
+	}
 	x.mapDelete(id)
 }
 
 // TopicsIndex is the engine-backed index; same exported surface as topics.go:350-353.
 //
 // Locking: updates are serialised by upd (the engine serialises them as well); readers
-// (Subscribers, Messages) never take it, so a GPU round trip never waits for an update's lock
-// nor an update for a match. tables guards the id tables and the stored subscriptions.
+// (Subscribers, Messages) never take it, and the engine's updates never wait for a reader's
+// result (it copies what a live result may see, capi.cpp IndexLock), so a GPU round trip never
+// waits for an update's lock nor an update for a reader. tables guards the id tables and the
+// stored subscriptions.
+//
+// Errors: the reference's index cannot fail; the engine can (a lost device, MQ_EIO from a kernel
+// guard). An update that fails is logged and answers false (nothing changed); a match batch that
+// fails is tried once more, then logged, and its callers get empty results — one publish is lost,
+// the broker stays up (server.go:984-1021 delivers to no one for an empty Subscribers).
 type TopicsIndex struct {
 	Retained *RetainedPackets
 	h        *C.mq_index
 	upd      sync.Mutex
 	tables   sync.RWMutex
 	ep       *epochs
-	// the batching stage Subscribers goes through (started on first use)
+	// the batching stages Subscribers and Messages go through (started on first use)
 	batcherOnce sync.Once
 	batcher     *MatchBatcher
-	clients  *idTable
-	filters  *idTable
-	topics   *idTable // retained topic names: handle = topic id, referenced while in Retained
-	stored   map[subKey]packets.Subscription
-	inlineBy map[subKey]InlineSubscription // (identifier, filter)
+	msgOnce     sync.Once
+	msgBatcher  *MessagesBatcher
+	clients     *idTable
+	filters     *idTable
+	topics      *idTable // retained topic names: handle = topic id, referenced while in Retained
+	stored      map[subKey]packets.Subscription
+	inlineBy    map[subKey]InlineSubscription // (identifier, filter)
 }
 
-// NewTopicsIndex (topics.go:356-364).
+// NewTopicsIndex (topics.go:356-364). A broker that cannot open its engine cannot start, so this
+// one failure panics, at start-up.
 func NewTopicsIndex() *TopicsIndex {
 	var h *C.mq_index
 	cfg := C.mq_config{device: 0}
@@ -234,11 +252,24 @@ func cstr(s string) (*C.char, C.uint32_t) {
 	return (*C.char)(unsafe.Pointer(unsafe.StringData(s))), C.uint32_t(len(s))
 }
 
-func must(rc C.int, what string) C.int {
-	if rc < 0 {
-		panic(fmt.Sprintf("%s: %d %s", what, rc, C.GoString(C.mq_last_error())))
+// EngineError is a failed engine call: the C-ABI's code (MQ_E*) and message.
+type EngineError struct {
+	Call string
+	Code int
+	Msg  string
+}
+
+func (e *EngineError) Error() string { return fmt.Sprintf("mqmatch: %s: %d %s", e.Call, e.Code, e.Msg) }
+
+// check turns a C-ABI return code into an error, logged where it happens (the engine's message
+// is per thread: read it now).
+func check(rc C.int, what string) (C.int, error) {
+	if rc >= 0 {
+		return rc, nil
 	}
-	return rc
+	err := &EngineError{Call: what, Code: int(rc), Msg: C.GoString(C.mq_last_error())}
+	slog.Error("mqmatch engine call failed", "call", what, "code", int(rc), "err", err.Msg)
+	return rc, err
 }
 
 func boolU8(b bool) C.uint8_t {
@@ -264,16 +295,22 @@ func (x *TopicsIndex) Subscribe(client string, sub packets.Subscription) bool {
 	}
 	flags |= C.uint8_t(sub.RetainHandling&3) << C.MQ_SUB_RH_SHIFT
 	p, n := cstr(sub.Filter)
-	rc := must(C.mq_subscribe(x.h, p, n, C.uint32_t(cid), C.uint32_t(fid), C.uint8_t(sub.Qos), flags,
+	rc, err := check(C.mq_subscribe(x.h, p, n, C.uint32_t(cid), C.uint32_t(fid), C.uint8_t(sub.Qos), flags,
 		C.int32_t(sub.Identifier)), "mq_subscribe")
 	x.tables.Lock()
+	defer x.tables.Unlock()
 	k := subKey{cid, fid}
+	if err != nil { // the interned ids go back if nothing references them
+		now := x.ep.now()
+		x.clients.tidy(cid, now)
+		x.filters.tidy(fid, now)
+		return false
+	}
 	if _, ok := x.stored[k]; !ok {
 		x.clients.ref(cid)
 		x.filters.ref(fid)
 	}
 	x.stored[k] = sub
-	x.tables.Unlock()
 	return rc == 1
 }
 
@@ -290,7 +327,10 @@ func (x *TopicsIndex) Unsubscribe(filter, client string) bool {
 		c = cid
 	}
 	p, n := cstr(filter)
-	rc := must(C.mq_unsubscribe(x.h, p, n, C.uint32_t(c)), "mq_unsubscribe")
+	rc, err := check(C.mq_unsubscribe(x.h, p, n, C.uint32_t(c)), "mq_unsubscribe")
+	if err != nil {
+		return false
+	}
 	if okc && okf {
 		x.tables.Lock()
 		k := subKey{cid, fid}
@@ -313,14 +353,18 @@ func (x *TopicsIndex) InlineSubscribe(sub InlineSubscription) bool {
 	fid := x.filters.intern(sub.Filter)
 	x.tables.Unlock()
 	p, n := cstr(sub.Filter)
-	rc := must(C.mq_inline_subscribe(x.h, p, n, C.int32_t(sub.Identifier), C.uint32_t(fid)), "mq_inline_subscribe")
+	rc, err := check(C.mq_inline_subscribe(x.h, p, n, C.int32_t(sub.Identifier), C.uint32_t(fid)), "mq_inline_subscribe")
 	x.tables.Lock()
+	defer x.tables.Unlock()
+	if err != nil {
+		x.filters.tidy(fid, x.ep.now())
+		return false
+	}
 	k := subKey{uint32(sub.Identifier), fid}
 	if _, ok := x.inlineBy[k]; !ok {
 		x.filters.ref(fid)
 	}
 	x.inlineBy[k] = sub
-	x.tables.Unlock()
 	return rc == 1
 }
 
@@ -329,7 +373,10 @@ func (x *TopicsIndex) InlineUnsubscribe(id int, filter string) bool {
 	x.upd.Lock()
 	defer x.upd.Unlock()
 	p, n := cstr(filter)
-	rc := must(C.mq_inline_unsubscribe(x.h, p, n, C.int32_t(id)), "mq_inline_unsubscribe")
+	rc, err := check(C.mq_inline_unsubscribe(x.h, p, n, C.int32_t(id)), "mq_inline_unsubscribe")
+	if err != nil {
+		return false
+	}
 	x.tables.Lock()
 	if fid, ok := x.filters.find(filter); ok {
 		k := subKey{uint32(id), fid}
@@ -366,9 +413,18 @@ func (x *TopicsIndex) mapDelete(topic string) {
 	x.tables.Unlock()
 }
 
+// tidyTopic releases a topic id interned for an update that failed (upd held).
+func (x *TopicsIndex) tidyTopic(topic string) {
+	x.tables.Lock()
+	if h, ok := x.topics.find(topic); ok {
+		x.topics.tidy(h, x.ep.now())
+	}
+	x.tables.Unlock()
+}
+
 // RetainMessage (topics.go:453-476). The Go packets map stays the store of packets and answers
 // the -1 case from the replaced packet as the reference does; the engine keeps the retain paths
-// and liveness.
+// and liveness. A failed engine call changes nothing and answers 0.
 func (x *TopicsIndex) RetainMessage(pk packets.Packet) int64 {
 	x.upd.Lock()
 	defer x.upd.Unlock()
@@ -377,8 +433,11 @@ func (x *TopicsIndex) RetainMessage(pk packets.Packet) int64 {
 	x.tables.Unlock()
 	p, n := cstr(pk.TopicName)
 	var out C.int64_t
-	must(C.mq_retain_message(x.h, p, n, C.uint64_t(h), C.uint32_t(len(pk.Payload)),
-		boolU8(pk.FixedHeader.Retain), &out), "mq_retain_message")
+	if _, err := check(C.mq_retain_message(x.h, p, n, C.uint64_t(h), C.uint32_t(len(pk.Payload)),
+		boolU8(pk.FixedHeader.Retain), &out), "mq_retain_message"); err != nil {
+		x.tidyTopic(pk.TopicName)
+		return 0
+	}
 	if len(pk.Payload) > 0 {
 		x.mapAdd(pk.TopicName, h, pk)
 		return 1
@@ -409,114 +468,202 @@ func pack(items []string) ([]byte, []uint64) {
 }
 
 // Messages (topics.go:525-579). A filter without wildcards is the packet store's own lookup,
-// as in the reference (topics.go:539-544); the others run on the engine.
+// as in the reference (topics.go:539-544); the others go through the index's Messages batching
+// stage: publishRetainedToClient calls Messages once per filter of every SUBSCRIBE, from every
+// connection goroutine (server.go:1115-1133), so the wildcard filters of many goroutines share
+// one engine call. An engine failure answers no retained messages (logged).
 func (x *TopicsIndex) Messages(filter string) []packets.Packet {
-	pks := []packets.Packet{}
 	if len(filter) == 0 || x.Retained.Len() == 0 {
-		return pks
+		return []packets.Packet{}
 	}
 	if !strings.ContainsRune(filter, '#') && !strings.ContainsRune(filter, '+') {
+		pks := []packets.Packet{}
 		if pk, ok := x.Retained.Get(filter); ok {
 			pks = append(pks, pk)
 		}
 		return pks
 	}
-	stamp := x.ep.begin()
-	defer x.ep.end(stamp)
-	buf, offs := pack([]string{filter})
-	var r *C.mq_msg_result
-	must(C.mq_messages_batch(x.h, (*C.uint8_t)(&buf[0]), (*C.uint64_t)(&offs[0]), 1, &r), "mq_messages_batch")
-	hs := unsafe.Slice((*uint64)(unsafe.Pointer(r.handles)), int(r.n_handles))
-	topics := make([]string, len(hs))
-	x.tables.RLock()
-	for i, h := range hs {
-		topics[i] = x.topics.strs[h]
+	x.msgOnce.Do(func() { x.msgBatcher = NewMessagesBatcher(x, DefaultMaxBatch, DefaultMinFill, DefaultMaxDelay) })
+	return x.msgBatcher.get(filter)
+}
+
+// MessagesBatch answers Messages for many filters with one engine call.
+func (x *TopicsIndex) MessagesBatch(filters []string) ([][]packets.Packet, error) {
+	v, err := x.matchMessages(filters)
+	if err != nil {
+		return nil, err
 	}
-	x.tables.RUnlock()
-	C.mq_result_free(unsafe.Pointer(r))
+	v.refs.Store(1)
+	out := make([][]packets.Packet, len(filters))
+	for i := range filters {
+		out[i] = v.get(i)
+	}
+	v.release()
+	return out, nil
+}
+
+// msgView is one mq_messages_batch result, shared by the callers whose filters it matched.
+type msgView struct {
+	x      *TopicsIndex
+	r      *C.mq_msg_result
+	stamp  uint64
+	refs   atomic.Int32
+	base   []C.uint64_t
+	count  []C.uint32_t
+	handle []uint64
+}
+
+func (x *TopicsIndex) matchMessages(filters []string) (*msgView, error) {
+	stamp := x.ep.begin()
+	buf, offs := pack(filters)
+	var r *C.mq_msg_result
+	if _, err := check(C.mq_messages_batch(x.h, (*C.uint8_t)(&buf[0]), (*C.uint64_t)(&offs[0]), C.uint32_t(len(filters)), &r),
+		"mq_messages_batch"); err != nil {
+		x.ep.end(stamp)
+		return nil, err
+	}
+	v := &msgView{x: x, r: r, stamp: stamp}
+	v.base = unsafe.Slice(r.base, int(r.n_filters))
+	v.count = unsafe.Slice(r.count, int(r.n_filters))
+	v.handle = unsafe.Slice((*uint64)(unsafe.Pointer(r.handles)), int(r.n_handles))
+	return v, nil
+}
+
+// get resolves filter i's handles to packets, on the caller's goroutine.
+func (v *msgView) get(i int) []packets.Packet {
+	hs := v.handle[v.base[i] : v.base[i]+C.uint64_t(v.count[i])]
+	topics := make([]string, len(hs))
+	v.x.tables.RLock()
+	for k, h := range hs {
+		topics[k] = v.x.topics.strs[h]
+	}
+	v.x.tables.RUnlock()
+	pks := []packets.Packet{}
 	for _, t := range topics {
-		if pk, ok := x.Retained.Get(t); ok {
+		if pk, ok := v.x.Retained.Get(t); ok {
 			pks = append(pks, pk)
 		}
 	}
 	return pks
 }
 
+func (v *msgView) release() {
+	if v.refs.Add(-1) == 0 {
+		C.mq_result_free(unsafe.Pointer(v.r))
+		v.x.ep.end(v.stamp)
+	}
+}
+
 // Subscribers (topics.go:583-590). publishToSubscribers calls it once per publish from every
 // connection goroutine (server.go:1000); the call goes through the index's batching stage, which
 // matches the topics of many goroutines with one engine call (MatchBatcher below), so server.go
-// keeps calling Subscribers unchanged.
+// keeps calling Subscribers unchanged. The maps are built here, on the caller's goroutine, from the
+// batch's shared span result, as the reference builds them on every connection goroutine.
 func (x *TopicsIndex) Subscribers(topic string) *Subscribers {
 	x.batcherOnce.Do(func() { x.batcher = NewMatchBatcher(x, DefaultMaxBatch, DefaultMinFill, DefaultMaxDelay) })
-	return x.batcher.Subscribers(topic)
+	return x.batcher.get(topic)
 }
 
-// The batching stage's defaults (SURVEY.md §8f.1; DESIGN.md §7 has the measured batch latency).
+func emptySubscribers() *Subscribers {
+	return &Subscribers{
+		Shared:              map[string]map[string]packets.Subscription{},
+		SharedSelected:      map[string]packets.Subscription{},
+		Subscriptions:       map[string]packets.Subscription{},
+		InlineSubscriptions: map[int]InlineSubscription{},
+	}
+}
+
+// The batching stages' defaults (SURVEY.md §8f.1; DESIGN.md §7 has the measured batch latency).
 const (
-	DefaultMaxBatch = 16384                  // topics per engine call at most
-	DefaultMinFill  = 1024                   // a batch with fewer topics waits for more ...
+	DefaultMaxBatch = 16384                  // items per engine call at most
+	DefaultMinFill  = 1024                   // under load, a batch with fewer items waits for more ...
 	DefaultMaxDelay = 200 * time.Microsecond // ... up to this long
 )
 
-// MatchBatcher is the batching stage of the publish pipeline (SURVEY.md §8f.1): connection
-// goroutines hand their topic to one loop goroutine per index and wait for their result; the loop
-// takes every request queued when the previous batch is done — under load, what arrived while it
-// was matched — waits up to maxDelay for more when it holds fewer than minFill, and matches the
-// batch with one SubscribersBatch call (one cgo call). Each caller gets exactly Subscribers(topic)
-// on the index state the batch ran against (readers take no root lock in the reference either,
-// topics.go:583, Q11), so the OnSelectSubscribers hook (hooks.go:360-367), SelectShared /
-// MergeSharedSelected and the fan-out after it (server.go:1001-1021) are unchanged.
-type MatchBatcher struct {
-	x        *TopicsIndex
-	in       chan matchReq
+// batchView is one engine call's result, shared by the callers whose items it matched: each
+// caller builds its own answer from it (get, on the caller's goroutine), then releases it; the
+// last release frees the engine's result.
+type batchView[T any] interface {
+	get(i int) T
+	release()
+	setRefs(n int) // the number of releases to come (set before any caller gets the view)
+}
+
+type batchReq[T any] struct {
+	item  string
+	reply chan batchReply[T]
+}
+
+type batchReply[T any] struct {
+	view batchView[T]
+	i    int
+	err  error
+}
+
+// batcher is a batching stage (SURVEY.md §8f.1): caller goroutines hand their item to one loop
+// goroutine per stage and wait for their reply; the loop takes every request queued when the
+// previous batch is done — under load, what arrived while it was matched — and matches the batch
+// with one engine call (run). When the previous batch held more than one request (there is
+// concurrent load), a batch with fewer than minFill items first waits up to maxDelay for more; a
+// lone request on an idle stage is matched at once. A failed engine call is tried once more; if
+// that fails too, every caller of the batch gets the empty answer (the error is logged by check).
+type batcher[T any] struct {
+	run      func(items []string) (batchView[T], error)
+	empty    func() T
+	in       chan batchReq[T]
 	maxBatch int
 	minFill  int
 	maxDelay time.Duration
 	done     chan struct{}
+	replies  sync.Pool
+	failed   atomic.Uint64 // batches whose callers got the empty answer
 }
 
-type matchReq struct {
-	topic string
-	reply chan *Subscribers
-}
-
-var replyChans = sync.Pool{New: func() any { return make(chan *Subscribers, 1) }}
-
-// NewMatchBatcher starts a batching stage over x.
-func NewMatchBatcher(x *TopicsIndex, maxBatch, minFill int, maxDelay time.Duration) *MatchBatcher {
+func newBatcher[T any](run func([]string) (batchView[T], error), empty func() T, maxBatch, minFill int,
+	maxDelay time.Duration) *batcher[T] {
 	if maxBatch <= 0 {
 		maxBatch = DefaultMaxBatch
 	}
 	if minFill <= 0 || minFill > maxBatch {
 		minFill = maxBatch
 	}
-	b := &MatchBatcher{x: x, in: make(chan matchReq, 4*maxBatch), maxBatch: maxBatch, minFill: minFill,
-		maxDelay: maxDelay, done: make(chan struct{})}
+	b := &batcher[T]{run: run, empty: empty, in: make(chan batchReq[T], 4*maxBatch), maxBatch: maxBatch,
+		minFill: minFill, maxDelay: maxDelay, done: make(chan struct{})}
+	b.replies.New = func() any { return make(chan batchReply[T], 1) }
 	go b.loop()
 	return b
 }
 
-// Subscribers enqueues topic and waits for the batch it joins.
-func (b *MatchBatcher) Subscribers(topic string) *Subscribers {
-	r := replyChans.Get().(chan *Subscribers)
-	b.in <- matchReq{topic, r}
-	s := <-r
-	replyChans.Put(r)
-	return s
+// get enqueues item, waits for the batch it joins and builds its answer.
+func (b *batcher[T]) get(item string) T {
+	r := b.replies.Get().(chan batchReply[T])
+	b.in <- batchReq[T]{item, r}
+	rep := <-r
+	b.replies.Put(r)
+	if rep.err != nil {
+		return b.empty()
+	}
+	v := rep.view.get(rep.i)
+	rep.view.release()
+	return v
 }
 
-// Close matches what is queued and stops the loop; no Subscribers call may follow.
-func (b *MatchBatcher) Close() {
+// Failed counts the batches whose callers got the empty answer.
+func (b *batcher[T]) Failed() uint64 { return b.failed.Load() }
+
+// Close matches what is queued and stops the loop; no get may follow.
+func (b *batcher[T]) Close() {
 	close(b.in)
 	<-b.done
 }
 
-func (b *MatchBatcher) loop() {
+func (b *batcher[T]) loop() {
 	defer close(b.done)
-	batch := make([]matchReq, 0, b.maxBatch)
-	topics := make([]string, 0, b.maxBatch)
+	batch := make([]batchReq[T], 0, b.maxBatch)
+	items := make([]string, 0, b.maxBatch)
 	timer := time.NewTimer(time.Hour)
 	timer.Stop()
+	last := 0 // the previous batch's size
 	for {
 		r, ok := <-b.in
 		if !ok {
@@ -537,7 +684,7 @@ func (b *MatchBatcher) loop() {
 				break drain
 			}
 		}
-		if open && len(batch) < b.minFill && b.maxDelay > 0 { // a small batch waits a little for more
+		if open && last > 1 && len(batch) < b.minFill && b.maxDelay > 0 { // under load: wait a little for more
 			timer.Reset(b.maxDelay)
 		wait:
 			for len(batch) < b.maxBatch {
@@ -556,47 +703,156 @@ func (b *MatchBatcher) loop() {
 			}
 			timer.Stop()
 		}
-		topics = topics[:0]
+		last = len(batch)
+		items = items[:0]
 		for _, r := range batch {
-			topics = append(topics, r.topic)
+			items = append(items, r.item)
 		}
-		for i, s := range b.x.SubscribersBatch(topics) {
-			batch[i].reply <- s
+		v, err := b.call(items)
+		if err != nil {
+			v, err = b.call(items) // once more: a transient failure costs one retry, not the batch
+		}
+		if err != nil {
+			b.failed.Add(1)
+			for _, r := range batch {
+				r.reply <- batchReply[T]{err: err}
+			}
+		} else {
+			for i, r := range batch {
+				r.reply <- batchReply[T]{view: v, i: i}
+			}
 		}
 		clear(batch) // drop the references to the replies
 	}
 }
 
-// SubscribersBatch matches many topics in one engine call (span format: the index's own
-// records plus patches, per topic or shared by a merge set, include/mqmatch.h); the batching stage in
-// publishToSubscribers (server.go:984-1021) feeds it. A subscription removed between the match
-// and the rebuild below is rebuilt from its record.
-func (x *TopicsIndex) SubscribersBatch(topics []string) []*Subscribers {
+// call runs the engine call with the view's reference count set before any caller can release
+// it; a panic in it (a bug, not an engine error) becomes this batch's error.
+func (b *batcher[T]) call(items []string) (v batchView[T], err error) {
+	defer func() {
+		if p := recover(); p != nil {
+			v, err = nil, fmt.Errorf("mqmatch: batch of %d: %v", len(items), p)
+			slog.Error("mqmatch batch panicked", "items", len(items), "panic", p)
+		}
+	}()
+	v, err = b.run(items)
+	if err == nil {
+		v.setRefs(len(items))
+	}
+	return v, err
+}
+
+// MatchBatcher is the Subscribers stage; MessagesBatcher the Messages stage.
+type (
+	MatchBatcher    = batcher[*Subscribers]
+	MessagesBatcher = batcher[[]packets.Packet]
+)
+
+// NewMatchBatcher starts a Subscribers batching stage over x.
+func NewMatchBatcher(x *TopicsIndex, maxBatch, minFill int, maxDelay time.Duration) *MatchBatcher {
+	run := func(items []string) (batchView[*Subscribers], error) {
+		v, err := x.matchSpans(items)
+		if err != nil {
+			return nil, err
+		}
+		return v, nil
+	}
+	return newBatcher[*Subscribers](run, emptySubscribers, maxBatch, minFill, maxDelay)
+}
+
+// NewMessagesBatcher starts a Messages batching stage over x (wildcard filters only).
+func NewMessagesBatcher(x *TopicsIndex, maxBatch, minFill int, maxDelay time.Duration) *MessagesBatcher {
+	run := func(items []string) (batchView[[]packets.Packet], error) {
+		v, err := x.matchMessages(items)
+		if err != nil {
+			return nil, err
+		}
+		return v, nil
+	}
+	return newBatcher[[]packets.Packet](run, func() []packets.Packet { return []packets.Packet{} }, maxBatch, minFill,
+		maxDelay)
+}
+
+func (v *msgView) setRefs(n int)  { v.refs.Store(int32(n)) }
+func (v *spanView) setRefs(n int) { v.refs.Store(int32(n)) }
+
+// spanView is one mq_match_spans result (span format: the index's own records plus patches, per
+// topic or shared by a merge set, include/mqmatch.h), shared by the callers whose topics it
+// matched. The host records it points into stay as they were at the match until it is freed
+// (the engine copies what it changes), and the ids it names stay reserved until then (epochs);
+// a subscription removed between the match and a caller's get is rebuilt from its record.
+type spanView struct {
+	x          *TopicsIndex
+	r          *C.mq_span_result
+	stamp      uint64
+	refs       atomic.Int32
+	ts         []C.mq_topic_spans
+	spans      []C.mq_span
+	patches    []C.mq_patch
+	setPatches []C.mq_patch
+	mergeRows  []C.uint32_t
+	mergeBase  []C.uint32_t
+	inl        []C.mq_inline_row
+	picked     []C.mq_shared_row
+	subPool    []C.mq_client_row
+	shrPool    []C.mq_shared_row
+	pickedOnly bool
+}
+
+func (x *TopicsIndex) matchSpans(topics []string) (*spanView, error) {
 	stamp := x.ep.begin()
-	defer x.ep.end(stamp)
 	buf, offs := pack(topics)
 	var r *C.mq_span_result
-	must(C.mq_match_spans(x.h, (*C.uint8_t)(&buf[0]), (*C.uint64_t)(&offs[0]), C.uint32_t(len(topics)), &r),
-		"mq_match_spans")
-	defer C.mq_result_free(unsafe.Pointer(r)) // after the tables' read lock below is released
-	ts := unsafe.Slice(r.topics, int(r.n_topics))
-	spans := unsafe.Slice(r.spans, int(r.n_spans))
-	patches := unsafe.Slice(r.patches, int(r.n_patches))
+	if _, err := check(C.mq_match_spans(x.h, (*C.uint8_t)(&buf[0]), (*C.uint64_t)(&offs[0]), C.uint32_t(len(topics)), &r),
+		"mq_match_spans"); err != nil {
+		x.ep.end(stamp)
+		return nil, err
+	}
+	v := &spanView{x: x, r: r, stamp: stamp}
+	v.ts = unsafe.Slice(r.topics, int(r.n_topics))
+	v.spans = unsafe.Slice(r.spans, int(r.n_spans))
+	v.patches = unsafe.Slice(r.patches, int(r.n_patches))
 	// merge-set patches (MQ_TOPIC_SET_PATCHES): row x<<MQ_SET_ROW_BITS|k is record k of the
 	// topic's x-th may-merge particle, whose first row is merge_rows[merge_row_base[topic]+x]
-	setPatches := unsafe.Slice(r.set_patches, int(r.n_set_patches))
-	mergeRows := unsafe.Slice(r.merge_rows, int(r.n_merge_rows))
-	var mergeBase []C.uint32_t
+	v.setPatches = unsafe.Slice(r.set_patches, int(r.n_set_patches))
+	v.mergeRows = unsafe.Slice(r.merge_rows, int(r.n_merge_rows))
 	if r.merge_row_base != nil {
-		mergeBase = unsafe.Slice(r.merge_row_base, int(r.n_topics))
+		v.mergeBase = unsafe.Slice(r.merge_row_base, int(r.n_topics))
 	}
-	const rowBits = uint32(C.MQ_SET_ROW_BITS)
-	inl := unsafe.Slice(r.inline_rows, int(r.n_inline_rows))
-	picked := unsafe.Slice(r.picked_rows, int(r.n_picked_rows))
-	subPool := unsafe.Slice(r.sub_pool, int(r.sub_pool_len))
-	shrPool := unsafe.Slice(r.shared_pool, int(r.shared_pool_len))
-	pickedOnly := r.flags&C.MQ_SPANS_PICKED != 0
+	v.inl = unsafe.Slice(r.inline_rows, int(r.n_inline_rows))
+	v.picked = unsafe.Slice(r.picked_rows, int(r.n_picked_rows))
+	v.subPool = unsafe.Slice(r.sub_pool, int(r.sub_pool_len))
+	v.shrPool = unsafe.Slice(r.shared_pool, int(r.shared_pool_len))
+	v.pickedOnly = r.flags&C.MQ_SPANS_PICKED != 0
+	return v, nil
+}
 
+func (v *spanView) release() {
+	if v.refs.Add(-1) == 0 {
+		C.mq_result_free(unsafe.Pointer(v.r))
+		v.x.ep.end(v.stamp)
+	}
+}
+
+// SubscribersBatch matches many topics in one engine call and builds their Subscribers here.
+func (x *TopicsIndex) SubscribersBatch(topics []string) ([]*Subscribers, error) {
+	v, err := x.matchSpans(topics)
+	if err != nil {
+		return nil, err
+	}
+	v.refs.Store(1)
+	out := make([]*Subscribers, len(topics))
+	for i := range topics {
+		out[i] = v.get(i)
+	}
+	v.release()
+	return out, nil
+}
+
+// get builds topic i's Subscribers (topics.go:583-590, Subscription.Merge packets.go:254-274 as
+// the engine resolved it), on the caller's goroutine.
+func (v *spanView) get(i int) *Subscribers {
+	x := v.x
 	x.tables.RLock()
 	defer x.tables.RUnlock()
 	stored := func(c, f uint32, ident int32, meta uint32) packets.Subscription {
@@ -605,76 +861,70 @@ func (x *TopicsIndex) SubscribersBatch(topics []string) []*Subscribers {
 		}
 		return packets.Subscription{Filter: x.filters.strs[f], Identifier: int(ident), Qos: byte(meta & C.MQ_META_QOS_MASK)}
 	}
-	out := make([]*Subscribers, len(topics))
-	patched := map[uint32]uint32{} // topic row -> meta
-	for i := range topics {
-		t := ts[i]
-		s := &Subscribers{
-			Shared:              map[string]map[string]packets.Subscription{},
-			SharedSelected:      map[string]packets.Subscription{},
-			Subscriptions:       map[string]packets.Subscription{},
-			InlineSubscriptions: map[int]InlineSubscription{},
+	const rowBits = uint32(C.MQ_SET_ROW_BITS)
+	t := v.ts[i]
+	s := emptySubscribers()
+	var patched map[uint32]uint32 // topic row -> meta
+	if t.n_patches > 0 {
+		patched = make(map[uint32]uint32, int(t.n_patches))
+	}
+	if t.flags&C.MQ_TOPIC_SET_PATCHES != 0 {
+		mr := v.mergeRows[v.mergeBase[i]:]
+		for _, pt := range v.setPatches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
+			row := uint32(pt.row)
+			patched[uint32(mr[row>>rowBits])+row&(1<<rowBits-1)] = uint32(pt.meta)
 		}
-		clear(patched)
-		if t.flags&C.MQ_TOPIC_SET_PATCHES != 0 {
-			mr := mergeRows[mergeBase[i]:]
-			for _, pt := range setPatches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
-				row := uint32(pt.row)
-				patched[uint32(mr[row>>rowBits])+row&(1<<rowBits-1)] = uint32(pt.meta)
-			}
-		} else {
-			for _, pt := range patches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
-				patched[uint32(pt.row)] = uint32(pt.meta)
-			}
+	} else {
+		for _, pt := range v.patches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
+			patched[uint32(pt.row)] = uint32(pt.meta)
 		}
-		addShared := func(sr C.mq_shared_row) {
-			f, c := x.filters.strs[sr.filter_id], x.clients.strs[sr.client_id]
-			if _, ok := s.Shared[f]; !ok {
-				s.Shared[f] = map[string]packets.Subscription{}
-			}
-			s.Shared[f][c] = stored(uint32(sr.client_id), uint32(sr.filter_id), 0, 0)
+	}
+	addShared := func(sr C.mq_shared_row) {
+		f, c := x.filters.strs[sr.filter_id], x.clients.strs[sr.client_id]
+		if _, ok := s.Shared[f]; !ok {
+			s.Shared[f] = map[string]packets.Subscription{}
 		}
-		// records in gather order: a client's client row precedes its ident rows
-		row := uint32(0)
-		for _, sp := range spans[t.span_base : t.span_base+C.uint64_t(t.n_spans)] {
-			for _, cr := range subPool[sp.sub_off : sp.sub_off+sp.n_sub] {
-				meta := uint32(cr.meta)
-				if m, ok := patched[row]; ok {
-					meta = m
-				}
-				row++
-				switch meta & C.MQ_ROW_KIND_MASK {
-				case 0: // client row: the merged Subscription
-					base := stored(uint32(cr.client_id), uint32(cr.filter_id), int32(cr.identifier), meta)
-					base.Qos = byte(meta & C.MQ_META_QOS_MASK)
-					base.NoLocal = meta&C.MQ_META_NOLOCAL != 0
-					base.Identifiers = map[string]int{base.Filter: base.Identifier}
-					s.Subscriptions[x.clients.strs[cr.client_id]] = base
-				case C.MQ_ROW_IDENT: // a further Identifiers entry of that client
-					sub := s.Subscriptions[x.clients.strs[cr.client_id]]
-					sub.Identifiers[x.filters.strs[cr.filter_id]] = int(cr.identifier)
-				}
+		s.Shared[f][c] = stored(uint32(sr.client_id), uint32(sr.filter_id), 0, 0)
+	}
+	// records in gather order: a client's client row precedes its ident rows
+	row := uint32(0)
+	for _, sp := range v.spans[t.span_base : t.span_base+C.uint64_t(t.n_spans)] {
+		for _, cr := range v.subPool[sp.sub_off : sp.sub_off+sp.n_sub] {
+			meta := uint32(cr.meta)
+			if m, ok := patched[row]; ok {
+				meta = m
 			}
-			if !pickedOnly {
-				for _, sr := range shrPool[sp.shr_off : sp.shr_off+sp.n_shr] {
-					addShared(sr)
-				}
+			row++
+			switch meta & C.MQ_ROW_KIND_MASK {
+			case 0: // client row: the merged Subscription
+				base := stored(uint32(cr.client_id), uint32(cr.filter_id), int32(cr.identifier), meta)
+				base.Qos = byte(meta & C.MQ_META_QOS_MASK)
+				base.NoLocal = meta&C.MQ_META_NOLOCAL != 0
+				base.Identifiers = map[string]int{base.Filter: base.Identifier}
+				s.Subscriptions[x.clients.strs[cr.client_id]] = base
+			case C.MQ_ROW_IDENT: // a further Identifiers entry of that client
+				sub := s.Subscriptions[x.clients.strs[cr.client_id]]
+				sub.Identifiers[x.filters.strs[cr.filter_id]] = int(cr.identifier)
 			}
 		}
-		if pickedOnly {
-			for _, sr := range picked[t.picked_base : t.picked_base+C.uint64_t(t.n_shared)] {
+		if !v.pickedOnly {
+			for _, sr := range v.shrPool[sp.shr_off : sp.shr_off+sp.n_shr] {
 				addShared(sr)
 			}
 		}
-		for _, lr := range inl[t.inline_base : t.inline_base+C.uint64_t(t.n_inline)] {
-			in, ok := x.inlineBy[subKey{uint32(lr.identifier), uint32(lr.filter_id)}]
-			if !ok { // unsubscribed since the match
-				in = InlineSubscription{Subscription: packets.Subscription{Filter: x.filters.strs[lr.filter_id],
-					Identifier: int(lr.identifier)}}
-			}
-			s.InlineSubscriptions[int(lr.identifier)] = in
-		}
-		out[i] = s
 	}
-	return out
+	if v.pickedOnly {
+		for _, sr := range v.picked[t.picked_base : t.picked_base+C.uint64_t(t.n_shared)] {
+			addShared(sr)
+		}
+	}
+	for _, lr := range v.inl[t.inline_base : t.inline_base+C.uint64_t(t.n_inline)] {
+		in, ok := x.inlineBy[subKey{uint32(lr.identifier), uint32(lr.filter_id)}]
+		if !ok { // unsubscribed since the match
+			in = InlineSubscription{Subscription: packets.Subscription{Filter: x.filters.strs[lr.filter_id],
+				Identifier: int(lr.identifier)}}
+		}
+		s.InlineSubscriptions[int(lr.identifier)] = in
+	}
+	return s
 }

@@ -331,15 +331,17 @@ static void TestChurnRecyclesIds() {
 // Readers and updates at once: matches run while other threads subscribe, unsubscribe and
 // churn client ids; every result names only strings the index has held, and the final state
 // matches exactly. Liveness: three readers match back to back (their span results overlap all
-// the time), yet every update must finish within kUpdateDeadline (the handle lock prefers a
-// waiting update over new readers, as Go's RWMutex does); a watchdog prints every thread's
-// progress and fails the run if the test has not finished after kWatchdog.
+// the time), yet every update must finish within kUpdateDeadline: updates copy what a live result
+// may see instead of waiting for it (capi.cpp IndexLock), so an update waits at most for the one
+// match whose GPU round trip holds the handle lock. A watchdog prints every thread's progress and
+// fails the run if the test has not finished after kWatchdog.
 static void TestConcurrentReadersAndUpdates() {
   using clk = std::chrono::steady_clock;
-  constexpr auto kUpdateDeadline = std::chrono::seconds(5);
+  constexpr auto kUpdateDeadline = std::chrono::milliseconds(10);
   constexpr auto kWatchdog = std::chrono::seconds(20);
   TopicsIndex ix;
   for (int i = 0; i < 200; i++) ix.Subscribe("base" + std::to_string(i % 40), S("s/" + std::to_string(i % 10) + "/+", 1));
+  ix.SubscribersBatch(std::vector<std::string>{"s/0/x", "t/0"});  // (device set-up outside the timing)
   std::atomic<bool> stop{false}, done{false};
   std::atomic<int> bad{0}, late{0};
   std::atomic<long> progress[5];
@@ -468,6 +470,80 @@ static void TestPublishViewBatcher() {
     for (auto& g : want.Shared) want_shared += g.second.size();
     REQUIRE(shared == want_shared);
   }
+}
+
+// A view held across updates and later batches: a consumer keeps batch N's TopicView while
+// another thread subscribes and a later batch is matched; the update does not wait for the view
+// (capi.cpp IndexLock: the index copies what a live result may see), the held view still names
+// exactly the recipients it was matched with, and the later batch sees the new subscription.
+static void TestViewHeldAcrossUpdates() {
+  using clk = std::chrono::steady_clock;
+  TopicsIndex ix;
+  for (int i = 0; i < 64; i++) ix.Subscribe("h" + std::to_string(i), S(i % 2 ? "w/+" : "w/x", 1));
+  auto recipients = [](const mq::host::TopicView& v) {
+    std::map<std::string, int> q;
+    v.for_each_row([&](const mq_client_row& cr) {
+      if ((cr.meta & MQ_ROW_KIND_MASK) == 0) q[v.client(cr.client_id)] = cr.meta & MQ_META_QOS_MASK;
+    });
+    return q;
+  };
+  mq::host::PublishViewBatcher b(ix, 256, std::chrono::microseconds(200));
+  const mq::host::TopicView held = b.Submit("w/x").get();
+  const auto before = recipients(held);
+  REQUIRE(before.size() == 64);
+  std::atomic<long> worst_us{0};
+  std::thread upd([&] {
+    for (int i = 0; i < 200; i++) {
+      const auto t0 = clk::now();
+      ix.Subscribe("n" + std::to_string(i), S("w/x", 2));
+      if (i % 3 == 0) ix.Unsubscribe(i % 2 ? "w/+" : "w/x", "h" + std::to_string(i % 64));
+      const long us = (long)std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - t0).count();
+      if (us > worst_us) worst_us = us;
+    }
+  });
+  upd.join();
+  const mq::host::TopicView later = b.Submit("w/x").get();  // batch N+1, while `held` lives
+  REQUIRE(recipients(held) == before);
+  const auto after = recipients(later);
+  REQUIRE(after.count("n199") && after.at("n199") == 2);
+  REQUIRE(after.size() == ix.Subscribers_("w/x").Subscriptions.size());
+  std::fprintf(stderr, "  200 updates while a view was held: slowest %.2f ms\n", worst_us.load() / 1000.0);
+  REQUIRE(worst_us.load() < 10000);
+}
+
+// The batching stage's failure path: a match call that fails (an injected MQ_EIO, as a kernel
+// guard would raise) is retried once; when the retry fails as well, that batch's tickets throw
+// the EngineError and the stage goes on with the next batch.
+static void TestBatcherEngineError() {
+  TopicsIndex ix;
+  for (int i = 0; i < 20; i++) ix.Subscribe("e" + std::to_string(i), S("e/+", 1));
+  std::atomic<int> fail_next{0};
+  mq::host::BasicBatcher<mq::host::ViewsPolicy> b(
+      [&](const mq::host::PackedTopics& t) {
+        if (fail_next > 0) {
+          fail_next--;
+          throw mq::host::EngineError(MQ_EIO, "injected MQ_EIO");
+        }
+        return ix.SubscribersSpans(t);
+      },
+      64, std::chrono::microseconds(100));
+  fail_next = 1;  // the first call fails, its retry succeeds
+  size_t n = 0;
+  b.Submit("e/a").get().for_each_row([&](const mq_client_row&) { n++; });
+  REQUIRE(n == 20);
+  fail_next = 2;  // both fail: the ticket throws
+  bool threw = false;
+  try {
+    b.Submit("e/b").get();
+  } catch (const mq::host::EngineError& e) {
+    threw = e.code == MQ_EIO;
+  }
+  REQUIRE(threw);
+  n = 0;  // the next batch is matched as usual
+  b.Submit("e/c").get().for_each_row([&](const mq_client_row&) { n++; });
+  REQUIRE(n == 20);
+  const auto st = b.stats();
+  REQUIRE(st.retried == 2 && st.failed == 1 && st.batches == 3);
 }
 
 // The batching stage under many submitters, checked against the ORACLE (the CPU restatement of
@@ -680,6 +756,8 @@ int main() {
     RUN(TestLoadSubscriptions);
     RUN(TestRetainedAddAfterExpiry);
     RUN(TestPublishViewBatcher);
+    RUN(TestViewHeldAcrossUpdates);
+    RUN(TestBatcherEngineError);
     RUN(TestBatcherManySubmittersVsOracle);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());

@@ -572,27 +572,73 @@ def test_one_sync_batches_grow_and_repeat(fuse, gpu_available):
     assert [x[0] for x in retried] == [*first, int(retried[2][1]), int(retried[3][1])], retried
 
 
-def test_spans_result_pins_host_image(gpu_available):
-    """A host span result pins the pools it points into: an update from another thread waits
-    until the result is freed."""
+def test_spans_result_survives_updates(gpu_available):
+    """A host span result points into the host image's subscription pools until it is freed;
+    updates do not wait for it (capi.cpp IndexLock): the index copies a slab before it changes one
+    a live result may see and keeps freed slabs and outgrown pool buffers until no live result
+    can see them. While results are held, the same thread and another one overwrite, remove,
+    flip may-merge slots, add shared members and grow both pools past their capacity; each held
+    result still expands to exactly what it matched, and the image stays consistent."""
     import ctypes as C
     import threading
-    import time
     from mqmatch import engine as E
     eng = E.Engine()
     for c in range(50):
         eng.subscribe("a/+", c, 0, 1, 0, 0)
-    tb, to = E.pack_strings(["a/b"])
-    rp = C.POINTER(E.SpanResult)()
-    assert E.lib().mq_match_spans(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), 1, C.byref(rp)) == 0
+        eng.subscribe("a/b", 200 + c, 1, 0, 0, 0)
+    for c in range(12):
+        eng.subscribe("$share/g/a/+", 400 + c, 2, 0, 0, 0)
+    tb, to = E.pack_strings(["a/b", "a/c", "x"])
+
+    def held():
+        rp = C.POINTER(E.SpanResult)()
+        assert E.lib().mq_match_spans(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), 3, C.byref(rp)) == 0
+        return rp
+
+    def same(a, b):
+        for k in ("rows", "shared", "sub_cap", "n_client", "n_shared"):
+            assert np.array_equal(a[k], b[k]), k
+
+    want0 = eng.match_batch_spans(tb, to)
+    r0 = held()
+    # in place: overwrite (qos), remove from the middle, flip slots to may-merge and back
+    for c in range(0, 50, 3):
+        assert eng.subscribe("a/+", c, 0, 2, 0, 0) == 0
+    for c in range(1, 50, 4):
+        assert eng.unsubscribe("a/+", c) == 1
+    for c in range(0, 50, 5):
+        eng.subscribe("a/#", c, 3, 0, 0, 0)
+    for c in range(0, 50, 10):
+        eng.unsubscribe("a/#", c)
+    for c in range(0, 12, 2):
+        eng.subscribe("$share/g/a/+", 400 + c, 7, 0, 0, 0)
+    eng.unsubscribe("$share/g/a/+", 401)
+    want1 = eng.match_batch_spans(tb, to)
+    r1 = held()
+    # from another thread, while r0 and r1 are held: grow both pools past their capacity
     done = []
-    th = threading.Thread(target=lambda: done.append(eng.subscribe("a/b", 999, 1, 0, 0, 0)))
+
+    def grow():
+        for c in range(3000):
+            eng.subscribe("a/+", 1000 + c, 0, 0, 0, 0)
+            eng.subscribe("$share/h/a/b", 5000 + c, 8, 0, 0, 0)
+            eng.subscribe("f/%d" % c, c, 9, 0, 0, 0)
+        done.append(1)
+    th = threading.Thread(target=grow)
     th.start()
-    time.sleep(0.5)
-    assert not done  # waiting for the view
-    E.lib().mq_result_free(rp)
-    th.join(timeout=30)
-    assert done == [1]
+    th.join(timeout=120)
+    assert done == [1]  # did not wait for the held results
+    eng.check()
+    same(E._expand_host_spans(r0, 3), want0)  # (frees r0)
+    same(E._expand_host_spans(r1, 3), want1)
+    for c in range(3000):  # the slabs kept for r0 / r1 go back to the pools
+        eng.unsubscribe("f/%d" % c, c)
+    eng.check()
+    got = eng.match_batch_spans(tb, to)
+    plus = set(range(50)) - set(range(1, 50, 4)) | set(range(1000, 4000))
+    clients = plus | set(range(200, 250)) | set(range(5, 50, 10))  # a/+, a/b, a/#
+    assert int(got["n_client"][0]) == len(clients)
+    assert int(got["n_shared"][0]) == (12 - 1) + 3000  # members of $share/g/a/+ and $share/h/a/b
 
 
 MSEGS = ["a", "b", "c", "", "$SYS", "$share", "g", "x", "averyveryverylongsegment", "ü", "$x"]
