@@ -649,6 +649,15 @@ def main():
                 calls.append(time.perf_counter() - t0)
             dt = sorted(calls)[1]
             parts = dict(eng.last_host_bytes)
+            # pipelined: consecutive batches, each result's copy beside the next batch's kernels
+            # (mq_match_spans_submit / _wait); the median of three runs of 4 batches after one untimed
+            eng.match_spans_pipelined(tb, to, 2)
+            pcalls = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                pbytes = eng.match_spans_pipelined(tb, to, 4)
+                pcalls.append(time.perf_counter() - t0)
+            pdt = sorted(pcalls)[1]
             ne_h = n
             ne = min(n, 200000)
             t0 = time.perf_counter()
@@ -660,6 +669,10 @@ def main():
             dtn = time.perf_counter() - t0
             out["end_to_end"] = {"value": ne_h / dt, "unit": "publishes/s", "sample_topics": ne_h,
                                  "calls_ms": [round(1e3 * c, 3) for c in calls],
+                                 "pipelined": {"value": 4 * ne_h / pdt, "unit": "publishes/s", "batches": 4,
+                                               "topics_per_batch": ne_h, "runs_ms": [round(1e3 * c, 3) for c in pcalls],
+                                               "bytes_per_topic": pbytes / ne_h,
+                                               "GBps_to_host": 4 * pbytes / pdt / 1e9},
                                  "result_bytes": nbytes, "bytes_per_topic": nbytes / ne_h, "GBps_to_host": nbytes / dt / 1e9,
                                  "bytes_per_topic_by_array": {k: v / ne_h for k, v in parts.items()},
                                  "expanded": {"value": ne / dtx, "rows": nrows, "host_threads": 1, "sample_topics": ne,

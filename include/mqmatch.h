@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 7
+#define MQ_ABI_VERSION 8
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
@@ -288,9 +288,18 @@ typedef struct mq_topic_spans {
 } mq_topic_spans;
 
 #define MQ_SPANS_PICKED 1u
+#define MQ_SPANS_PATCH_CODES 2u /* host results (ABI v8): patches / set_patches hold 4-byte codes */
 #define MQ_TOPIC_SET_PATCHES 1u
 #define MQ_SET_ROW_BITS 26   /* set patch rows: x << MQ_SET_ROW_BITS | k */
 #define MQ_MERGE_ROWS_STRIDE 64
+/* Patch codes (host results with MQ_SPANS_PATCH_CODES; the arrays are then uint32_t): code =
+ * row << 3 | op. op 1..6: the merge base of its client, Qos (op - 1) % 3, NoLocal (op - 1) / 3;
+ * op 7: a later match of the client (MQ_ROW_IDENT when the record's identifier is > 0, else
+ * MQ_ROW_DROP). The record's other meta bits are unchanged, so the code and the pool record give
+ * the row's meta (mq_patch_apply). A set patch code's row is x << MQ_CODE_SET_ROW_BITS | k. Host
+ * results use codes when every subscription list has fewer than 2^23 records. */
+#define MQ_CODE_SET_ROW_BITS 23
+#define MQ_PATCH_OP 0x20000000u /* mq_topic_patch's meta of a code: MQ_PATCH_OP | op */
 
 typedef struct mq_span_result {
   uint32_t n_topics;
@@ -321,26 +330,57 @@ typedef struct mq_span_result {
 
 /* Patch k (< n_patches) of topic t of a span result whose arrays the caller can read (a host
  * result, or a device result copied to the host): the topic's own patch, or its set patch with
- * the row translated through the topic's merge rows. */
+ * the row translated through the topic's merge rows. Its meta is the row's new meta, or, for a
+ * patch code, MQ_PATCH_OP | op: mq_patch_apply gives the row's meta in either case. */
 static inline mq_patch mq_topic_patch(const mq_span_result* r, uint32_t t, uint32_t k) {
   const mq_topic_spans* ts = &r->topics[t];
-  if (!(ts->flags & MQ_TOPIC_SET_PATCHES)) return r->patches[ts->patch_base + k];
-  mq_patch p = r->set_patches[ts->patch_base + k];
+  const int set = (ts->flags & MQ_TOPIC_SET_PATCHES) != 0;
+  uint32_t xbits = MQ_SET_ROW_BITS;
+  mq_patch p;
+  if (r->flags & MQ_SPANS_PATCH_CODES) {
+    const uint32_t* codes = (const uint32_t*)(set ? (const void*)r->set_patches : (const void*)r->patches);
+    const uint32_t c = codes[ts->patch_base + k];
+    p.row = c >> 3;
+    p.meta = MQ_PATCH_OP | (c & 7u);
+    xbits = MQ_CODE_SET_ROW_BITS;
+  } else {
+    p = set ? r->set_patches[ts->patch_base + k] : r->patches[ts->patch_base + k];
+  }
+  if (!set) return p;
   const uint32_t* mr = r->merge_rows + (r->merge_row_base ? (uint64_t)r->merge_row_base[t]
                                                            : (uint64_t)t * MQ_MERGE_ROWS_STRIDE);
-  p.row = mr[p.row >> MQ_SET_ROW_BITS] + (p.row & ((1u << MQ_SET_ROW_BITS) - 1u));
+  p.row = mr[p.row >> xbits] + (p.row & ((1u << xbits) - 1u));
   return p;
 }
 
+/* The meta of a patched row: a patch's meta (mq_topic_patch) applied to the pool record's. */
+static inline uint32_t mq_patch_apply(uint32_t patch_meta, uint32_t meta, int32_t identifier) {
+  if (!(patch_meta & MQ_PATCH_OP)) return patch_meta;
+  const uint32_t op = patch_meta & 7u;
+  if (op == 7u) return meta | (identifier > 0 ? MQ_ROW_IDENT : MQ_ROW_DROP);
+  return (meta & ~(MQ_META_QOS_MASK | MQ_META_NOLOCAL)) | ((op - 1u) % 3u) | ((op - 1u) / 3u ? MQ_META_NOLOCAL : 0u);
+}
+
 /* Span-format Subscribers for a batch of host topics (as mq_match_batch). The result's arrays
- * are host copies; its pools point at the index's host image, which the result pins: updates
- * issued while it is held wait until mq_result_free (as the reference's writers wait for the
- * per-node read locks a gather holds, topics.go:270-277). Writers are preferred, as with Go's
- * sync.RWMutex: while an update waits, new mq_match_spans calls wait for it, so overlapping
- * readers cannot starve updates. Free a result before updating or calling mq_match_spans again
- * from the same thread (a second read while an update waits would wait for itself). */
+ * are host copies; its pools point at the index's host image, and what they show a result stays
+ * as it was at the match until mq_result_free: an update never waits for a result — the index
+ * copies a subscription slab before it changes one a live result may see, and keeps what it
+ * frees until no live result can see it (the reference's writers never wait for a reader's maps
+ * either, topics.go:270-277, 401-419). Updates are preferred, as with Go's sync.RWMutex: while an
+ * update waits (for the match in flight), new matches wait for it, so readers matching back to
+ * back cannot starve updates. Only mq_subscribe_bulk waits for the live results to be freed. */
 int mq_match_spans(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets, uint32_t n,
                    mq_span_result** out);
+/* The same, pipelined (ABI v8): mq_match_spans_submit runs the batch's kernels and returns with
+ * the copy of its result into host memory still running on a copy stream, beside the next
+ * submitted batch's kernels; mq_match_spans_wait waits for that copy and returns the result
+ * (exactly mq_match_spans's), freeing the ticket. Every ticket must be waited for; results are
+ * freed with mq_result_free. Batches k and k + 1 overlap: for consecutive batches the host-result
+ * rate is bound by the larger of the kernels and the copies, not their sum. */
+typedef struct mq_spans_ticket mq_spans_ticket;
+int mq_match_spans_submit(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets, uint32_t n,
+                          mq_spans_ticket** out);
+int mq_match_spans_wait(mq_spans_ticket* ticket, mq_span_result** out);
 /* Device-resident span format (inputs in HBM, enqueued on hip_stream, as mq_match_device). All
  * pointers in *out are DEVICE pointers owned by the index, valid until its next update or match
  * call. The whole batch is one result (no chunks); the call returns after the batch's kernels
@@ -390,8 +430,7 @@ int mq_match_spans_begin(mq_index* idx, const uint8_t* d_topic_bytes, const uint
  * this index's device; 0 for an index that is not sharded): results as mq_match_spans_device. */
 int mq_match_spans_end(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, void* hip_stream,
                        mq_span_result* out);
-/* The same with the results copied to host memory (as mq_match_spans: the result pins the
- * host image until mq_result_free). */
+/* The same with the results copied to host memory (as mq_match_spans). */
 int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, mq_span_result** out);
 
 /* ---- batched reverse retained scan: TopicsIndex.Messages (topics.go:525-579) ---- */

@@ -31,7 +31,12 @@
                                      bit 0 no partner links, bit 1 links loaded but not looked up, bit 2 no
                                      patch stores, bit 3 no binary search for a record's hit list; bit 4 (results
                                      exact) no early stop of a visit through a partner other than the record's first; bits 5 / 6 (exact)
-                                     partner links loaded 3 / 4 per batch instead of 2 */
+                                     partner links loaded 3 / 4 per batch instead of 2 (bits 4-6 act on the
+                                     link path: with bit 7); bit 7 (exact) records resolved through their
+                                     partner links instead of the fold; bit 8 (exact) fold chunks of 16
+                                     visits */
+#define MQ_OPT_PATCH_CODES 20     /* host span results: 1 (default) 4-byte patch codes when the index allows them
+                                     (MQ_SPANS_PATCH_CODES); 0: 8-byte mq_patch records */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than
                                      kMsgExportMin particles to work items any wavefront takes; > 1: that
                                      threshold; 0: the filter's wavefront walks it alone */

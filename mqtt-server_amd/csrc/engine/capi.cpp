@@ -22,16 +22,19 @@
 using namespace mq;
 
 // The handle's lock (the reference's root lock, topics.go:402): `mu` serialises the handle's work
-// (updates, and the GPU round trip of a match). Host span results point into the host image's
-// subscription pools until mq_result_free; `views` records them by generation, and the index
-// copies a slab before it changes one that a live result may see and keeps what it frees until
-// no live result can see it (Index::begin_op), so an update never waits for results. The one
-// exception is a bulk subscribe (mq_subscribe_bulk), which rewrites the pools in place: it
-// announces itself (`views.drains`), takes `mu` and waits for the live results to be freed; a
-// call that would publish a new result first waits while a bulk update is announced (so readers
-// cannot starve it). `views` has its own mutex, never held across GPU work, so freeing a result
-// never waits for a match in flight. Results hold a reference, so freeing one after
-// mq_index_destroy is safe.
+// (updates, and the GPU round trip of a match). It prefers updates, as Go's sync.RWMutex prefers
+// writers: an update announces itself (`views.writers`) before it takes `mu`, and a call that is
+// not an update waits while one is announced, so readers matching back to back cannot starve
+// updates. Host span results point into the host image's subscription pools until
+// mq_result_free; `views` records them by generation, and the index copies a slab before it
+// changes one that a live result may see and keeps what it frees until no live result can see it
+// (Index::begin_op), so an update never waits for results — only for the match in flight, if any.
+// The one exception is a bulk subscribe (mq_subscribe_bulk), which rewrites the pools in place:
+// it also announces itself as a drain (`views.drains`) and waits, without holding `mu`, for the
+// live results to be freed; a call that would publish a new result waits while a drain is
+// announced. `views` has its own mutex, never held across GPU work, so freeing a result never
+// waits for a match in flight. Results hold a reference, so freeing one after mq_index_destroy is
+// safe.
 struct IndexLock {
   std::mutex mu;
   ViewTracker views;
@@ -100,27 +103,31 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
   if (!idx) return fail(MQ_EINVAL, "null index");
   IndexLock& L = *idx->lk;
   ViewTracker& V = L.views;
-  struct Drain {  // the announcement, withdrawn however the call ends
+  struct Announce {  // an update's announcement, withdrawn however the call ends
     ViewTracker* V = nullptr;
-    ~Drain() {
+    bool drain = false;
+    ~Announce() {
       if (!V) return;
       {
         std::lock_guard<std::mutex> g(V->mu);
-        V->drains--;
+        V->writers--;
+        if (drain) V->drains--;
       }
       V->cv.notify_all();
     }
-  } drain;
+  } ann;
   try {
-    if (access == Access::kDrain) {
+    if (access == Access::kUpdate || access == Access::kDrain) {
       {
         std::lock_guard<std::mutex> g(V.mu);
-        V.drains++;
+        V.writers++;
+        if (access == Access::kDrain) V.drains++;
       }
-      drain.V = &V;
-    } else if (access == Access::kPin) {
+      ann.V = &V;
+      ann.drain = access == Access::kDrain;
+    } else {
       std::unique_lock<std::mutex> g(V.mu);
-      V.cv.wait(g, [&] { return V.drains == 0; });
+      V.cv.wait(g, [&] { return V.writers == 0; });
     }
     std::unique_lock<std::mutex> lk(L.mu, std::defer_lock);
     if (access == Access::kDrain) {  // wait for the live results without holding `mu`
@@ -300,10 +307,20 @@ int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_sp
   r.patches = reinterpret_cast<const mq_patch*>(h->data.patches.data());
   r.inline_rows = reinterpret_cast<const mq_inline_row*>(h->data.inl.data());
   r.picked_rows = reinterpret_cast<const mq_shared_row*>(h->data.picked.data());
-  r.n_patches = h->data.patches.size();  // packed (the device pool has per-region gaps)
+  const bool codes = h->data.codes;  // 4-byte patch codes (MQ_SPANS_PATCH_CODES)
+  if (codes) {
+    r.flags |= MQ_SPANS_PATCH_CODES;
+    r.patches = reinterpret_cast<const mq_patch*>(h->data.patch_codes.data());
+  }
+  r.n_patches = codes ? h->data.patch_codes.size() : h->data.patches.size();  // packed (the device pool has gaps)
+  r.n_spans = h->data.spans.size();      // packed (a one-sync device batch leaves them at t * 64)
+  r.n_inline_rows = h->data.inl.size();
+  r.n_picked_rows = h->data.picked.size();
   const bool sets = !h->data.merge_base.empty();  // (topics with MQ_TOPIC_SET_PATCHES, ABI v7)
-  r.set_patches = sets ? reinterpret_cast<const mq_patch*>(h->data.set_patches.data()) : nullptr;
-  r.n_set_patches = sets ? h->data.set_patches.size() : 0;
+  r.set_patches = !sets ? nullptr
+                  : codes ? reinterpret_cast<const mq_patch*>(h->data.set_codes.data())
+                          : reinterpret_cast<const mq_patch*>(h->data.set_patches.data());
+  r.n_set_patches = !sets ? 0 : codes ? h->data.set_codes.size() : h->data.set_patches.size();
   r.merge_rows = sets ? h->data.merge_rows.data() : nullptr;
   r.n_merge_rows = sets ? h->data.merge_rows.size() : 0;
   r.merge_row_base = sets ? h->data.merge_base.data() : nullptr;
@@ -334,6 +351,56 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
     d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out);
     return publish_host_spans(idx, std::move(h), dev_out, out);
   }, Access::kPin);
+}
+
+// A submitted batch: its result, published (its arrays being filled by the copy stream), and the
+// event recorded when the copy is done.
+struct mq_spans_ticket {
+  mq_span_result* res = nullptr;
+  hipEvent_t ready = nullptr;
+};
+
+int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_spans_ticket** out) {
+  if (!out || (n && (!to || (!tb && to[n] != 0)))) return fail(MQ_EINVAL, "null argument");
+  *out = nullptr;
+  return guarded(idx, [&] {
+    Device& d = idx->device();
+    std::unique_ptr<mq_spans_ticket> tk(new mq_spans_ticket());
+    hip_check(hipEventCreateWithFlags(&tk->ready, hipEventDisableTiming), "hipEventCreate");
+    struct EvGuard {  // the event goes if the submit fails
+      mq_spans_ticket* t;
+      ~EvGuard() {
+        if (t && t->ready) (void)hipEventDestroy(t->ready);
+      }
+    } eg{tk.get()};
+    std::unique_ptr<SpanHolder> h(new SpanHolder());
+    const uint8_t* dtb = nullptr;
+    const uint64_t* dto = nullptr;
+    hipStream_t hs = d.host_stream();
+    if (n) d.stage_inputs(tb, to, n, hs, &dtb, &dto);
+    mq_span_result dev_out;
+    d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out, tk->ready);
+    const int rc = publish_host_spans(idx, std::move(h), dev_out, &tk->res);
+    if (rc) return rc;
+    eg.t = nullptr;
+    *out = tk.release();
+    return 0;
+  }, Access::kPin);
+}
+
+int mq_match_spans_wait(mq_spans_ticket* t, mq_span_result** out) {
+  if (!t || !out) return fail(MQ_EINVAL, "null argument");
+  *out = nullptr;
+  const hipError_t e = hipEventSynchronize(t->ready);
+  (void)hipEventDestroy(t->ready);
+  mq_span_result* r = t->res;
+  delete t;
+  if (e != hipSuccess) {
+    mq_result_free(r);
+    return fail(MQ_EIO, std::string("hipEventSynchronize: ") + hipGetErrorString(e));
+  }
+  *out = r;
+  return 0;
 }
 
 int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, mq_span_result** out) {
@@ -403,13 +470,16 @@ int mq_spans_expand(const mq_span_result* r, uint32_t first, uint32_t count, mq_
     if (ts.n_patches && (set ? ts.patch_base + ts.n_patches > r->n_set_patches || !r->merge_row_base
                              : ts.patch_base + ts.n_patches > r->n_patches))
       return fail(MQ_EIO, "patch range out of bounds");
+    const bool codes = (r->flags & MQ_SPANS_PATCH_CODES) != 0;
     for (uint32_t k = 0; k < ts.n_patches; k++) {
-      if (set && (uint64_t)r->merge_row_base[t] + (r->set_patches[ts.patch_base + k].row >> MQ_SET_ROW_BITS) >=
-                     r->n_merge_rows)
-        return fail(MQ_EIO, "merge row out of bounds");
+      const uint32_t x = !set ? 0u
+                         : codes ? (reinterpret_cast<const uint32_t*>(r->set_patches)[ts.patch_base + k] >> 3) >>
+                                       MQ_CODE_SET_ROW_BITS
+                                 : r->set_patches[ts.patch_base + k].row >> MQ_SET_ROW_BITS;
+      if (set && (uint64_t)r->merge_row_base[t] + x >= r->n_merge_rows) return fail(MQ_EIO, "merge row out of bounds");
       const mq_patch p = mq_topic_patch(r, t, k);
       if (p.row >= ts.n_rows) return fail(MQ_EIO, "patch row out of range");
-      out[p.row].meta = p.meta;
+      out[p.row].meta = mq_patch_apply(p.meta, out[p.row].meta, out[p.row].identifier);
     }
     if (picked && ts.n_shared) {
       memcpy(shared + ns, r->picked_rows + ts.picked_base, (size_t)ts.n_shared * sizeof(mq_shared_row));
@@ -594,7 +664,7 @@ int mq_device_check(mq_index* idx) {
 }
 
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
-  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MSG_EXPORT || option == 11) return fail(MQ_EINVAL, "unknown option");
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_PATCH_CODES || option == 11) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
     if (option == MQ_OPT_EDGE_LOAD) {  // the host image's option
       if (value != 2 && value != 4 && value != 8) throw std::invalid_argument("MQ_OPT_EDGE_LOAD: 2, 4 or 8");

@@ -3,6 +3,7 @@
 #include "mqmatch_dev.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -266,11 +267,12 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
       return true;
     case MQ_OPT_MSG_EXPORT: msg_export_ = (uint32_t)v; return true;
     case MQ_OPT_WALK_GROUP:
-      if (v != 0 && v != 4 && v != 8 && v != 16) return false;
+      if (v != 0 && v != 16 && !(kDevBuild && (v == 4 || v == 8))) return false;  // (8 / 4: DEV=1 builds)
       walk_group_ = (uint32_t)v;
       walk_auto_ = false;  // (a fixed choice: no trials)
       return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
+    case MQ_OPT_PATCH_CODES: patch_codes_ = v != 0; return true;
     default: return false;
   }
 }
@@ -290,6 +292,11 @@ Device::~Device() {
     if (walk_ev_[k]) (void)hipEventDestroy(walk_ev_[k]);
   }
   if (side_done_) (void)hipEventDestroy(side_done_);
+  for (HostStage& h : hst_) {
+    if (h.packed) (void)hipEventDestroy(h.packed);
+    if (h.copied) (void)hipEventDestroy(h.copied);
+  }
+  if (hcopy_) (void)hipStreamDestroy(hcopy_);
   if (side_) (void)hipStreamDestroy(side_);
   if (hstream_) (void)hipStreamDestroy(hstream_);
   if (wstream_) (void)hipStreamDestroy(wstream_);
@@ -501,6 +508,15 @@ hipStream_t Device::host_stream() {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   if (!hstream_) hip_check(hipStreamCreateWithFlags(&hstream_, hipStreamNonBlocking), "hipStreamCreate");
   return hstream_;
+}
+
+void Device::ensure_hcopy() {
+  if (hcopy_) return;
+  hip_check(hipStreamCreateWithFlags(&hcopy_, hipStreamNonBlocking), "hipStreamCreate");
+  for (HostStage& h : hst_) {
+    hip_check(hipEventCreateWithFlags(&h.packed, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&h.copied, hipEventDisableTiming), "hipEventCreate");
+  }
 }
 
 void Device::ensure_streams() {
@@ -944,13 +960,13 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
 // patch pool grows when a batch reserves more than it holds (the batch's k_merge then runs
 // again); the call ends with the stream synchronised and the guard flags checked.
 void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                         HostSpans* host, mq_span_result* out) {
+                         HostSpans* host, mq_span_result* out, hipEvent_t ready) {
   mq_xlist x;
-  spans_begin(ix, d_tb, d_to, n, s, &x, one_sync_ && !host);
-  if (spans_end(ix, nullptr, 0, s, host, out)) return;
+  spans_begin(ix, d_tb, d_to, n, s, &x, one_sync_);
+  if (spans_end(ix, nullptr, 0, s, host, out, ready)) return;
   // the one-sync run's buffers did not hold the batch: again, sized by the host
   spans_begin(ix, d_tb, d_to, n, s, &x, false);
-  spans_end(ix, nullptr, 0, s, host, out);
+  spans_end(ix, nullptr, 0, s, host, out, ready);
 }
 
 void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
@@ -978,9 +994,14 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     // each, timed on the device); later batches take the faster per topic. A wildcard-heavy index
     // (config 3) favours the frontier (its DFS diverges), an exact-match one (config 4, 50M IoT
     // filters) the thread per topic (64 topics per wavefront in flight).
+    // a new size, or a new wildcard mix (the share of '+' / '#' particles moved by more than a
+    // quarter of itself and by more than 0.02 of all particles): try again
     const uint64_t nodes = ix.n_nodes();
-    if (nodes > 2 * walk_trial_nodes_ || 2 * nodes < walk_trial_nodes_) {  // a new size: try again
+    const double wild = nodes ? (double)ix.n_wild_nodes() / (double)nodes : 0.0;
+    const double dw = std::fabs(wild - walk_trial_wild_);
+    if (nodes > 2 * walk_trial_nodes_ || 2 * nodes < walk_trial_nodes_ || (dw > 0.02 && dw > 0.25 * walk_trial_wild_)) {
       walk_trial_nodes_ = nodes;
+      walk_trial_wild_ = wild;
       walk_trial_ns_[0] = walk_trial_ns_[1] = 0.0;
     }
     const int k = walk_trial_ns_[0] == 0.0 ? 0 : walk_trial_ns_[1] == 0.0 ? 1 : -1;
@@ -1153,7 +1174,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
 }
 
 bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host,
-                       mq_span_result* out) {
+                       mq_span_result* out, hipEvent_t ready) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   memset(out, 0, sizeof(*out));
   if (host) *host = HostSpans{};
@@ -1170,8 +1191,23 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   out->flags = select_shared_ ? MQ_SPANS_PICKED : 0u;
   if (nf > kMaxShards - 1) throw HipError{hipErrorInvalidValue, "more foreign lists than kMaxShards - 1"};
   if (nf && !ix.sharded()) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
-  if (n == 0) return true;
+  if (n == 0) {
+    if (ready) hip_check(hipEventRecord(ready, s), "hipEventRecord");
+    return true;
+  }
   const bool one_sync = sb_.one_sync;
+  // host results: this batch's stage, free once the copy of its last batch is done; 4-byte patch
+  // codes while every subscription list is shorter than 2^23 (set rows) and the rows of a topic
+  // fit 29 bits (MQ_SPANS_PATCH_CODES)
+  HostStage* hs = nullptr;
+  const bool codes = host && patch_codes_ && ix.max_sub_cap() <= (1u << kCodeSetRowBits) &&
+                     ix.subs.m.size() < (1ull << 29);
+  if (host) {
+    host->codes = codes;
+    ensure_hcopy();
+    hs = &hst_[hpar_];
+    if (hs->used) hip_check(hipStreamWaitEvent(s, hs->copied, 0), "hipStreamWaitEvent");
+  }
 
   EmitArgs a;
   memset(&a, 0, sizeof(a));
@@ -1272,7 +1308,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.base = TopicOff{0, 0, 0, 0, 0};
   a.desc = desc_[0].as<GDesc>();
   a.inl_rows = sp_inl_.as<InlRec>();
-  a.sres = sp_res_.as<TopicSpansDev>();
+  if (hs) grow(hs->topics, (size_t)n * sizeof(TopicSpansDev));
+  a.sres = hs ? hs->topics.as<TopicSpansDev>() : sp_res_.as<TopicSpansDev>();
   a.pcount = sp_pcount_.as<unsigned long long>();
   a.tc = sb_.lists ? nullptr : sp_tc_.as<TopicCount>();
   a.work = nullptr;
@@ -1302,7 +1339,6 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   uint32_t* h_err = reinterpret_cast<uint32_t*>(h_roff + kPatchRegions + 1);  // [2]
   unsigned long long* h_mrtot = reinterpret_cast<unsigned long long*>(h_err + 2);  // [1]
   unsigned long long* h_stot = h_mrtot + 1;                                         // [1]
-  if (host && one_sync) throw HipError{hipErrorInvalidValue, "host span results take the synchronised path"};
   uint64_t n_patches = 0, max_region = 0;
   // k_merge register budget: the kernel waits on memory, and eight waves per SIMD (64 VGPRs, a
   // few spills) beat six (80 VGPRs) at 1M and 10M subscriptions (4.37 -> 4.17 ms and 1.37 -> 1.27
@@ -1396,21 +1432,22 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
     if (host) {  // the sets' written patches, packed (their total read with pcount)
       grow(set_nbase_, (size_t)n * sizeof(uint64_t));
-      grow(sp_scompact_, srcap_ * kPatchRegions * sizeof(PatchRec));  // (at most every reservation)
+      grow(hs->set_patches, srcap_ * kPatchRegions * sizeof(PatchRec));  // (at most every reservation)
       if (!set_total_.p) set_total_.ensure(sizeof(unsigned long long));
       hip_check(hipMemsetAsync(set_total_.p, 0, sizeof(unsigned long long), s), "memset");
       launch_set_pack(n, a.tslot, a.rep, a.sets, dd_spatches_.as<PatchRec>(), set_nbase_.as<uint64_t>(),
-                      sp_scompact_.as<PatchRec>(), set_total_.as<unsigned long long>(), s);
+                      hs->set_patches.as<PatchRec>(), codes ? hs->set_patches.as<uint32_t>() : nullptr,
+                      set_total_.as<unsigned long long>(), s);
       hip_check(hipGetLastError(), "k_set_pack");
       hip_check(hipMemcpyAsync(h_stot, set_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
     }
     if (host) {  // the merge rows of the topics with a set, packed (their total read with pcount)
       if ((uint64_t)n * kPairMax > UINT32_MAX) throw HipError{hipErrorInvalidValue, "host span batch too large"};
-      grow(mr_base_, (size_t)n * sizeof(uint32_t));
-      grow(mr_rows_, (size_t)n * kPairMax * sizeof(uint32_t));
+      grow(hs->merge_base, (size_t)n * sizeof(uint32_t));
+      grow(hs->merge_rows, (size_t)n * kPairMax * sizeof(uint32_t));
       if (!mr_total_.p) mr_total_.ensure(sizeof(unsigned long long));
       hip_check(hipMemsetAsync(mr_total_.p, 0, sizeof(unsigned long long), s), "memset");
-      launch_mrow_pack(n, a.tslot, a.mcount, a.mrow, mr_base_.as<uint32_t>(), mr_rows_.as<uint32_t>(),
+      launch_mrow_pack(n, a.tslot, a.mcount, a.mrow, hs->merge_base.as<uint32_t>(), hs->merge_rows.as<uint32_t>(),
                        mr_total_.as<unsigned long long>(), s);
       hip_check(hipGetLastError(), "k_mrow_pack");
       hip_check(hipMemcpyAsync(h_mrtot, mr_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
@@ -1472,6 +1509,9 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     rb.out = d_fast_;
     launch_readback(rb, s);
     hip_check(hipGetLastError(), "k_readback");
+    if (host)  // the topic pass's patch counts per region (the host packs them below)
+      hip_check(hipMemcpyAsync(h_pc, a.pcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
+                "D2H pcount");
     if (sb_.trial >= 0) hip_check(hipEventRecord(walk_ev_[1], s), "hipEventRecord");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     if (sb_.trial >= 0 && !h_fast_->err && !h_fast_->ovf && !h_fast_->unsafe) {  // a walk trial: its time per topic
@@ -1488,6 +1528,14 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
     tot = h_fast_->tot;
     if (sb_.fused) tot.g = h_fast_->n_sets[2];  // (no scan: k_dedup_rep totals the gathers)
+    if (host) {
+      n_patches = 0;
+      for (uint32_t r = 0; r < kPatchRegions; r++) {
+        h_roff[r] = n_patches;
+        n_patches += h_pc[r];
+      }
+      h_roff[kPatchRegions] = n_patches;
+    }
     sb_.tot = tot;
     last_sets_ = h_fast_->n_sets[0] + h_fast_->n_sets[1];
     if (prof.on()) {
@@ -1533,51 +1581,69 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.count("merge_map_bytes", sum[9]);
     prof.count("merge_topics", n);
   }
-  if (host) {
+  if (host) {  // pack the result into the stage, then copy it on the copy stream
     grow(sp_roff_, (kPatchRegions + 1) * sizeof(uint64_t));
     if (n_patches) {  // the regions' used parts, packed
-      grow(sp_compact_, n_patches * sizeof(PatchRec));
+      grow(hs->patches, n_patches * sizeof(PatchRec));
       hip_check(hipMemcpyAsync(sp_roff_.p, h_roff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D");
       launch_patch_compact(sp_patches_.as<PatchRec>(), rcap_, a.pcount, sp_roff_.as<uint64_t>(),
-                           sp_compact_.as<PatchRec>(), s);
+                           hs->patches.as<PatchRec>(), codes ? hs->patches.as<uint32_t>() : nullptr, s);
       hip_check(hipGetLastError(), "k_patch_compact");
     }
     // every topic's patch_base into the packed arrays (its own patches' or its set's)
     launch_host_rebase(n, sb_.dedup ? a.rep : nullptr, sb_.dedup ? set_nbase_.as<uint64_t>() : nullptr,
                        n_patches ? sp_roff_.as<uint64_t>() : nullptr, rcap_, a.sres, s);
     hip_check(hipGetLastError(), "k_host_rebase");
+    // the spans packed (one-sync batches leave them at t * 64), span_base into the packed array
+    grow(hs->spans, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
+    if (!hs->span_total.p) hs->span_total.ensure(sizeof(unsigned long long));
+    hip_check(hipMemsetAsync(hs->span_total.p, 0, sizeof(unsigned long long), s), "memset");
+    launch_span_pack(n, a.sres, sp_spans_.as<SpanRec>(), hs->spans.as<SpanRec>(),
+                     hs->span_total.as<unsigned long long>(), s);
+    hip_check(hipGetLastError(), "k_span_pack");
+    if (tot.inl) {
+      grow(hs->inl, tot.inl * sizeof(InlRec));
+      hip_check(hipMemcpyAsync(hs->inl.p, sp_inl_.p, tot.inl * sizeof(InlRec), hipMemcpyDeviceToDevice, s), "D2D");
+    }
+    if (out->n_picked_rows) {
+      grow(hs->picked, out->n_picked_rows * sizeof(ShrRec));
+      hip_check(hipMemcpyAsync(hs->picked.p, sp_picked_.p, out->n_picked_rows * sizeof(ShrRec),
+                               hipMemcpyDeviceToDevice, s), "D2D");
+    }
+    hip_check(hipEventRecord(hs->packed, s), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(hcopy_, hs->packed, 0), "hipStreamWaitEvent");
+    const uint64_t n_set = sb_.dedup ? *h_stot : 0, n_mrows = sb_.dedup ? *h_mrtot : 0;
+    const size_t pw = codes ? sizeof(uint32_t) : sizeof(PatchRec);  // bytes per patch
     host->topics.resize(n);
     host->spans.resize(tot.g);
-    host->patches.resize(n_patches);
+    if (codes) host->patch_codes.resize(n_patches);
+    else host->patches.resize(n_patches);
     host->inl.resize(tot.inl);
     host->picked.resize(out->n_picked_rows);
-    hip_check(hipMemcpyAsync(host->topics.data(), a.sres, n * sizeof(TopicSpansDev), hipMemcpyDeviceToHost, s), "D2H");
-    // (copied here with the rest: on a side stream under the merge kernels, by a copy or by a
-    // kernel storing to mapped memory, the two streams ran in turn — profiles/r03/s2_e2e/)
-    if (tot.g)
-      hip_check(hipMemcpyAsync(host->spans.data(), sp_spans_.p, tot.g * sizeof(SpanRec), hipMemcpyDeviceToHost, s), "D2H");
-    if (n_patches)
-      hip_check(hipMemcpyAsync(host->patches.data(), sp_compact_.p, n_patches * sizeof(PatchRec),
-                               hipMemcpyDeviceToHost, s), "D2H");
-    if (tot.inl)
-      hip_check(hipMemcpyAsync(host->inl.data(), sp_inl_.p, tot.inl * sizeof(InlRec), hipMemcpyDeviceToHost, s), "D2H");
-    if (out->n_picked_rows)
-      hip_check(hipMemcpyAsync(host->picked.data(), sp_picked_.p, out->n_picked_rows * sizeof(ShrRec),
-                               hipMemcpyDeviceToHost, s), "D2H");
+    auto d2h = [&](void* dst, const DevBuf& src, size_t bytes) {
+      if (bytes) hip_check(hipMemcpyAsync(dst, src.p, bytes, hipMemcpyDeviceToHost, hcopy_), "D2H");
+    };
+    d2h(host->topics.data(), hs->topics, n * sizeof(TopicSpansDev));
+    d2h(host->spans.data(), hs->spans, tot.g * sizeof(SpanRec));
+    d2h(codes ? (void*)host->patch_codes.data() : (void*)host->patches.data(), hs->patches, n_patches * pw);
+    d2h(host->inl.data(), hs->inl, tot.inl * sizeof(InlRec));
+    d2h(host->picked.data(), hs->picked, out->n_picked_rows * sizeof(ShrRec));
     if (sb_.dedup) {  // the sets' written patches and the merge rows (packed by k_set_pack, k_mrow_pack)
-      const uint64_t n_set = *h_stot;
-      host->set_patches.resize(n_set);
-      host->merge_rows.resize(*h_mrtot);
+      if (codes) host->set_codes.resize(n_set);
+      else host->set_patches.resize(n_set);
+      host->merge_rows.resize(n_mrows);
       host->merge_base.resize(n);
-      if (n_set)
-        hip_check(hipMemcpyAsync(host->set_patches.data(), sp_scompact_.p, n_set * sizeof(PatchRec),
-                                 hipMemcpyDeviceToHost, s), "D2H");
-      if (*h_mrtot)
-        hip_check(hipMemcpyAsync(host->merge_rows.data(), mr_rows_.p, *h_mrtot * sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost, s), "D2H");
-      hip_check(hipMemcpyAsync(host->merge_base.data(), mr_base_.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s),
-                "D2H");
+      d2h(codes ? (void*)host->set_codes.data() : (void*)host->set_patches.data(), hs->set_patches, n_set * pw);
+      d2h(host->merge_rows.data(), hs->merge_rows, n_mrows * sizeof(uint32_t));
+      d2h(host->merge_base.data(), hs->merge_base, n * sizeof(uint32_t));
     }
+    hip_check(hipEventRecord(hs->copied, hcopy_), "hipEventRecord");
+    hs->used = true;
+    hpar_ ^= 1u;
+    if (ready) hip_check(hipEventRecord(ready, hcopy_), "hipEventRecord");
+    else hip_check(hipStreamSynchronize(hcopy_), "hipStreamSynchronize(copy)");
+  } else if (ready) {
+    hip_check(hipEventRecord(ready, s), "hipEventRecord");
   }
   if (one_sync) return true;  // (checked above)
   hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");

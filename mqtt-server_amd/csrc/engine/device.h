@@ -114,6 +114,8 @@ struct HostSpans {
   PinnedVec<PatchRec> set_patches;  // merge-set patches, packed (set_patches of the result)
   PinnedVec<uint32_t> merge_rows;   // merge rows of the topics that reference a set, packed
   PinnedVec<uint32_t> merge_base;   //   and where each topic's start
+  bool codes = false;               // patches / set patches as 4-byte codes (MQ_SPANS_PATCH_CODES):
+  PinnedVec<uint32_t> patch_codes, set_codes;  //   then these instead of patches / set_patches
 };
 
 // Host-side destination of a batch's results (mq_match_batch).
@@ -190,8 +192,11 @@ class Device {
   // Span format (mq_match_spans*): spans + patches + inline rows of n topics on the device; the
   // call returns after the kernels completed and their guard flags were checked. `host`: also
   // copies every array into it (out's pointers then still name the device arrays).
+  // ready (host results): the copy into `host` runs on the copy stream beside whatever the
+  // device does next (the next batch's kernels), and `ready` is recorded when it is done; without
+  // it the call returns after the copy.
   void match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                   HostSpans* host, mq_span_result* out);
+                   HostSpans* host, mq_span_result* out, hipEvent_t ready = nullptr);
   // The same in two phases, for a sharded index: begin walks the batch and
   // exports the topics' gathered cross-shard nodes (device pointers in *x, valid until end);
   // the caller exchanges the lists between the shards; end merges with the other shards' lists.
@@ -200,7 +205,8 @@ class Device {
   // and the caller runs the batch again without one_sync (host-sized buffers).
   void spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x,
                    bool one_sync = false);
-  bool spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out);
+  bool spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out,
+                 hipEvent_t ready = nullptr);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
                 HostMsg* host, mq_msg_result* out);
@@ -304,9 +310,20 @@ class Device {
   DevBuf msg_handles_, msg_base_, msg_count_, gslots_;
   // span format outputs
   DevBuf sp_res_, sp_spans_, sp_inl_, sp_picked_, sp_patches_, sp_pcount_;
-  DevBuf sp_compact_, sp_roff_;      // host results: the patch regions packed
-  DevBuf sp_scompact_, set_nbase_, set_total_;  //   the sets' written patches packed
-  DevBuf mr_base_, mr_rows_, mr_total_;  // and the merge rows of the topics with a set
+  DevBuf sp_roff_, set_nbase_, set_total_, mr_total_;  // host results: packing offsets and totals
+  // Host results, double-buffered: a batch's arrays are packed into a stage that the copy stream
+  // then reads, while the next batch's kernels fill the other stage (copied: the copy that last
+  // read it; the next use of the stage waits for it on the device).
+  struct HostStage {
+    DevBuf topics, spans, patches, set_patches, merge_rows, merge_base, inl, picked, span_total;
+    hipEvent_t packed = nullptr, copied = nullptr;
+    bool used = false;
+  };
+  HostStage hst_[2];
+  uint32_t hpar_ = 0;              // the stage of the next host batch
+  bool patch_codes_ = true;        // MQ_OPT_PATCH_CODES
+  hipStream_t hcopy_ = nullptr;    // the copy stream of host results
+  void ensure_hcopy();
   DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
   // sharded: the exported list (offsets, entries, counts) and the imported lists' offsets
   DevBuf x_off_, x_ents_, x_cnt_, x_src_, x_foff_[kMaxShards - 1];
@@ -357,6 +374,7 @@ class Device {
   bool walk_auto_ = true;
   static constexpr uint32_t kWalkTrialMin = 65536;  // batches this large are timed for the trial
   uint64_t walk_trial_nodes_ = 0;                    // the index size the trials ran at
+  double walk_trial_wild_ = 0.0;                     //   and its share of '+' / '#' particles
   double walk_trial_ns_[2] = {0.0, 0.0};             // batch time per topic: frontier, thread per topic
   hipEvent_t walk_ev_[2] = {nullptr, nullptr};
   uint32_t dedup_ = 1;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)

@@ -457,6 +457,7 @@ uint32_t Index::new_node(uint32_t parent, std::string_view seg, const SegKey& k)
   child_rec_sync(parent);  // the parent's slab may have moved
   nh_[parent].n_children++;
   n_live_nodes_++;
+  n_wild_nodes_ += h.str <= 1;
   return id;
 }
 
@@ -503,6 +504,7 @@ void Index::remove_node(uint32_t n) {
   if (inls.h[n].cnt || inls.h[n].off) inls.at_w(n) = NodeInl{0, 0};
   msg.at_w(n) = NodeMsg{};
   if (sharded()) xinfo.at_w(n) = XInfo{kNone, 0, 0};
+  n_wild_nodes_ -= h.str <= 1;
   h = NodeHost{};
   free_nodes_.push_back(n);
   n_live_nodes_--;
@@ -667,7 +669,9 @@ void Index::merge_rebuild(uint32_t n) {
     const uint32_t pos = L.sub_off + hk[i].second;
     const MergeRef r = mref.h[pos];
     const SubRec& rec = subs.m.h[pos];
-    plist.m.at_w(lo + i) = PairSlot{hk[i].second, r.off, r.cnt, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u)};
+    plist.m.at_w(lo + i) = PairSlot{hk[i].second, r.off, r.cnt,
+                                    rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u) |
+                                        slot_partner_bits(partner_meta(hk[i].first, rec.client))};
   }
   const bool inc = links >= kIncLinks;
   MergeInc* I = nullptr;
@@ -748,8 +752,9 @@ void Index::merge_patch(uint32_t n, MergeInc& I) {
     if (k >= I.slot.size()) I.slot.resize(k + 1);
     I.slot[k] = MergeInc::Slot{off, p.cnt, cap};
     I.links += p.cnt;
-    const PairSlot ps{k, off, p.cnt, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u)};
-    for (uint32_t i = 0; i < p.cnt; i++) pair_add(n, I, parts.m.h[p.off + i], ps);
+    const uint32_t own = rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u);
+    for (uint32_t i = 0; i < p.cnt; i++)
+      pair_add(n, I, parts.m.h[p.off + i], PairSlot{k, off, p.cnt, own | slot_partner_bits(mpart.m.h[off + i].meta)});
   }
   I.dirty.clear();
   if (xs) {
@@ -876,6 +881,9 @@ bool Index::check(std::string* why) {
     *why = m;
     return false;
   };
+  uint64_t wild = 0;
+  for (uint32_t n = 0; n < nh_.size(); n++) wild += nh_[n].live && n != kRoot && nh_[n].str <= 1;
+  if (wild != n_wild_nodes_) return bad("wildcard particle count stale");
   for (uint32_t n = 0; n < nh_.size(); n++) {
     if (!nh_[n].live) continue;
     const NodeLists& L = lists.h[n];
@@ -937,7 +945,7 @@ bool Index::check(std::string* why) {
         if (pe.h != mp.node) return bad(at + ": pair block misses a partner node");
         bool listed = false;
         const SubRec& rec = subs.m.h[pos];
-        const uint32_t want_meta = rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u);
+        const uint32_t want_meta = rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u) | slot_partner_bits(mp.meta);
         for (uint32_t i = 0; i < pe.cnt && !listed; i++) {
           const PairSlot& ps = plist.m.h[pe.off + i];
           listed = ps.k == k && ps.mp_off == r.off && ps.mp_cnt == r.cnt && ps.meta == want_meta;
@@ -1086,6 +1094,7 @@ void Index::sub_move(uint32_t n, uint32_t nc) {
   retire(0, L.sub_off, cap);
   L.sub_off = no;
   nh_[n].sub_cap = nc;
+  max_sub_cap_ = std::max(max_sub_cap_, nc);
   nh_[n].sub_gen = fresh_gen();
 }
 

@@ -288,6 +288,7 @@ struct ViewTracker {
   }
   std::condition_variable cv;  // a bulk update waits on it for the live results to drain
   uint64_t drains = 0;          // bulk updates announced (a new result waits for them)
+  uint64_t writers = 0;         // updates announced (a new match waits for them: capi.cpp)
   void release(uint64_t v) {
     std::lock_guard<std::mutex> g(mu);
     auto it = live.find(v);
@@ -387,6 +388,8 @@ class Index {
 
   uint64_t edge_mask() const { return edges.size() - 1; }
   uint64_t n_nodes() const { return n_live_nodes_; }
+  uint64_t n_wild_nodes() const { return n_wild_nodes_; }  // '+' / '#' particles
+  uint32_t max_sub_cap() const { return max_sub_cap_; }     // the largest subscription slab ever
   uint64_t n_edges() const { return n_edges_; }
   // edge table: at most 1/load of its slots used (MQ_OPT_EDGE_LOAD); from the next growth. A
   // table of 2^30 slots or more keeps load <= 1/2 (32 GB of slots at 2^30).
@@ -534,6 +537,8 @@ class Index {
   PodVec<NodeHost> nh_;
   std::vector<uint32_t> free_nodes_;
   uint64_t n_live_nodes_ = 0, n_edges_ = 0, n_tombs_ = 0, n_merge_ = 0;
+  uint64_t n_wild_nodes_ = 0;
+  uint32_t max_sub_cap_ = 0;
   uint32_t edge_load_ = 4;  // sparser than 1/2: shorter probe chains for k_walk (10M: 1.90 -> 1.64 ms)
   uint32_t max_depth_ = 0;
   uint64_t version_ = 0;

@@ -374,6 +374,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
   for (uint32_t hi : level_end) {
     parallel_for(hi - lo, threads, [&](size_t b, size_t e) {
       uint32_t depth_max = 0;
+      uint64_t wild = 0;
       for (size_t q = b; q < e; q++) {
         const uint32_t id = lo + (uint32_t)q, k = id - first_new, parent = node_parent[k];
         NodeHost& h = nh_[id];
@@ -382,6 +383,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
         h.depth = (uint16_t)(nh_[parent].depth + 1);
         h.seg0 = parent == kRoot ? h.str : nh_[parent].seg0;
         h.live = true;
+        wild += h.str <= 1;
         depth_max = std::max<uint32_t>(depth_max, h.depth);
         uint32_t flags = 0;
         if (h.str == 0) flags |= kFlagPlusKey;
@@ -403,6 +405,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
         __atomic_fetch_add(&nh_[parent].n_children, 1u, __ATOMIC_RELAXED);
         if (sharded()) set_rank(id, parent, seg, false);
       }
+      __atomic_fetch_add(&n_wild_nodes_, wild, __ATOMIC_RELAXED);
       uint32_t cur = __atomic_load_n(&max_depth_, __ATOMIC_RELAXED);
       while (depth_max > cur && !__atomic_compare_exchange_n(&max_depth_, &cur, depth_max, true, __ATOMIC_RELAXED,
                                                              __ATOMIC_RELAXED)) {
@@ -640,6 +643,7 @@ void Index::subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uin
     NodeLists& L = lists.h[node];
     L.sub_off = subs.alloc(c);
     nh_[node].sub_cap = c;
+    max_sub_cap_ = std::max(max_sub_cap_, c);
     uint32_t nd = 0;
     for (size_t k = b; k < e; k++) nd += !is_merge[k];
     L.n_direct = nd;

@@ -27,6 +27,19 @@ constexpr uint32_t kMapSlots = 128;    // per-wave LDS map (gathered merge node 
 constexpr uint32_t kPairMax = 64;     // merge gathers covered by the pair analysis
 constexpr uint32_t kHitMax = 128;      // hit lists staged per k_merge wave
 constexpr uint32_t kPartBatch = 2;     // partner links loaded together per record
+#ifdef MQ_DEV_BUILD
+constexpr bool kDevBuild = true;       // make DEV=1: measurement variants and attribution bits
+#else
+constexpr bool kDevBuild = false;
+#endif
+// the set pass's fold (k_merge): per-wave LDS hash table of records (in the node map's place:
+// kMapSlots keys and values), at most kFoldCap visits per chunk; a record's value: its meta
+// (kSlotOwnMask bits) | what its visits found
+constexpr uint32_t kFoldSlots = kMapSlots;
+constexpr uint32_t kFoldCap = kFoldSlots * 3 / 4;
+constexpr uint32_t kFoldNonBase = 1u << 13;  // a visit's partner comes before the record
+constexpr uint32_t kFoldNoLocal = 1u << 14;  // a partner has NoLocal
+constexpr uint32_t kFoldQos0 = 1u << 15;     // bit 15 + q: a partner has Qos q
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
@@ -183,6 +196,7 @@ struct EmitArgs {
 };
 constexpr uint32_t kSetHeavy = 1024;  // a merge set with this many may-merge records goes first
 constexpr uint32_t kSetRowBits = 26;  // set-relative patch rows: 6 bits of merge gather, 26 of slot
+constexpr uint32_t kCodeSetRowBits = 23;  // == MQ_CODE_SET_ROW_BITS (host patch codes)
 constexpr uint32_t kTopicSetPatches = 1;  // TopicSpansDev.flags: patches shared with a merge set
                                           //   (MQ_TOPIC_SET_PATCHES)
 struct SetInfo {  // 24 B, per representative topic
@@ -373,12 +387,16 @@ struct FinishArgs {
 void launch_finish(const FinishArgs& a, hipStream_t s);
 // Host span results: pack the merge rows of the topics with a merge set (tslot != kNone),
 // mcount[t] of them from mrow[t * kPairMax]; base[t] their start, *total (zeroed) the count.
+void launch_span_pack(uint32_t n, TopicSpansDev* sres, const SpanRec* src, SpanRec* dst, unsigned long long* total,
+                      hipStream_t s);
 void launch_mrow_pack(uint32_t n, const uint32_t* tslot, const uint32_t* mcount, const uint32_t* mrow,
                       uint32_t* base, uint32_t* rows, unsigned long long* total, hipStream_t s);
-// Host span results: the sets' written patches packed (nbase[rep], *total zeroed), and every
-// topic's patch_base pointed into the packed arrays (its set's, or its own via the regions' roff).
+// Host span results: the sets' written patches packed (nbase[rep], *total zeroed) as PatchRecs
+// (out) or patch codes (codes != null: MQ_SPANS_PATCH_CODES), and every topic's patch_base
+// pointed into the packed arrays (its set's, or its own via the regions' roff).
 void launch_set_pack(uint32_t n, const uint32_t* tslot, const uint32_t* rep, const SetInfo* sets,
-                     const PatchRec* pool, uint64_t* nbase, PatchRec* out, unsigned long long* total, hipStream_t s);
+                     const PatchRec* pool, uint64_t* nbase, PatchRec* out, uint32_t* codes, unsigned long long* total,
+                     hipStream_t s);
 void launch_host_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, const uint64_t* roff, uint64_t rcap,
                         TopicSpansDev* sres, hipStream_t s);
 // k_msg count (fill = false) or fill pass. spec != null: the count pass also writes each filter's
@@ -396,9 +414,9 @@ void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* of
 // TopicCount.gathers = counts[t] (an imported list's counts, for launch_scan)
 void launch_counts(const uint32_t* counts, uint32_t n, TopicCount* cnt, hipStream_t s);
 // Pack the used prefix of every patch region (pcount[r] patches of region r) into `out` at
-// roff[r] (span format, host results).
+// roff[r] (span format, host results), or as patch codes into `codes` when it is not null.
 void launch_patch_compact(const PatchRec* pool, uint64_t rcap, const unsigned long long* pcount,
-                          const uint64_t* roff, PatchRec* out, hipStream_t s);
+                          const uint64_t* roff, PatchRec* out, uint32_t* codes, hipStream_t s);
 void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
                       uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s);
 

@@ -220,9 +220,17 @@ struct PairSlot {  // 16 B: one slot on a pair list, with its partner links
   uint32_t mp_off;  // its MergePart records
   uint32_t mp_cnt;
   uint32_t meta;    // the slot's SubRec meta | kSlotIdentPos (its identifier is > 0): resolving
-                    // the slot needs no load of the record itself
+                    // the slot needs no load of the record itself; | the partner's bits (below)
 };
 constexpr uint32_t kSlotIdentPos = 0x1000u;  // the reserved meta bit (include/mqmatch.h)
+// PairSlot.meta also carries the partner's Qos | NoLocal (MergePart.meta of the partner node h the
+// list is for) at bits 16-18: meta | identpos | (qos | (nolocal ? 4 : 0)) << kSlotPartShift
+constexpr uint32_t kSlotPartShift = 16;
+constexpr uint32_t kSlotMetaMask = 0x0FFFu;  // the SubRec meta bits of PairSlot.meta
+constexpr uint32_t kSlotOwnMask = 0x1FFFu;   //   and kSlotIdentPos
+MQ_HD uint32_t slot_partner_bits(uint32_t partner_meta) {  // MergePart.meta -> PairSlot.meta bits
+  return ((partner_meta & 3u) | ((partner_meta & 0x100u) ? 4u : 0u)) << kSlotPartShift;
+}
 
 MQ_HD uint32_t pair_hash(uint32_t x) {
   x ^= x >> 16;

@@ -1,0 +1,962 @@
+// gfx950 Messages: the particle walk k_msg, the level-order retained image and k_msgq (DESIGN.md
+// §4.8).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "kern_common.h"
+
+namespace mq {
+
+// ---------------------------------------------------------------------------------------------
+// k_msg: Messages(filter), the reverse retained scan (topics.go:525-579). One wavefront per
+// filter. The literal prefix of the filter is walked first (all lanes alike) down to its first
+// '+'/'#' level, whose children are the units of parallel work: lane k takes child k of that
+// enumeration frame (and k + 64, ...), applies the frame's per-child rule (Q4 $SYS skip at level
+// 0, emit at the last level, descend otherwise) and walks the child's subtree depth-first
+// without a stack — a frame is (node, level d); a '+'/'#' level enumerates the node's children
+// slab (ChildRec: each child's retained state and own slab, read sequentially; childless
+// children are never entered) and, after returning from child c, resumes at c's slab position
+// + 1 (NodeMsg.child_pos, NodeMsg.parent);
+// levels past the last segment repeat it (isolateParticle, topics.go:679-698), which is how a
+// trailing '#' covers the subtree. A lane stops when it returns to the enumeration frame.
+// FILL=false counts the packets per filter; FILL=true walks again and appends them at the
+// filter's offset through a per-wave LDS cursor (Messages' order is Go map order, i.e. none).
+// ---------------------------------------------------------------------------------------------
+// WPE: minimum waves per SIMD asked of the register allocator (1 = no constraint). The walk
+// needs ~127 VGPRs (4 waves per SIMD); fewer registers with some spills buy occupancy for
+// this latency-bound kernel (MQ_MSG_WPE picks the variant).
+template <bool FILL, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_msg(const uint8_t* __restrict__ fb,
+                                             const uint64_t* __restrict__ fo, uint32_t n,
+                                             DevIndex ix, TopicCount* __restrict__ cnt,
+                                             const TopicOff* __restrict__ off,
+                                             uint64_t* __restrict__ handles,
+                                             uint64_t* __restrict__ base_out,
+                                             uint32_t* __restrict__ count_out,
+                                             uint64_t* __restrict__ spec, uint32_t spec_cap) {
+  __shared__ uint32_t cursor[4];  // FILL / speculative count: next free slot of the filter
+  const uint32_t lane = threadIdx.x & 63, wv = wave_id();
+  const uint32_t t = blockIdx.x * 4 + wv;
+  if (t >= n) return;  // wave-uniform
+  // FILL after a speculative count: only the filters k_msg_place could not place are walked
+  if (FILL && spec && cnt[t].gathers == 0) return;
+  const uint64_t b0 = fo[t], b1 = fo[t + 1];
+  uint32_t total = 0;  // packets of this filter (wave-uniform)
+  uint64_t* out = FILL ? handles + off[t].rows : nullptr;
+  // speculative count: the handles also go to the filter's scratch slots (first spec_cap)
+  uint64_t* sp = (!FILL && spec) ? spec + (uint64_t)t * spec_cap : nullptr;
+  bool partial = false;  // a count shortcut (below_live) left the scratch incomplete
+  // len(filter) == 0 || Retained.Len() == 0 (topics.go:535)
+  if (b1 > b0 && ix.retained_len != 0) {
+    ByteReader R(fb);
+    bool w = false;
+    for (uint64_t i = b0 + lane; i < b1; i += 64) {
+      const uint32_t ch = fb[i];
+      w |= (ch == '+') | (ch == '#');
+    }
+    const bool wild = __any(w);
+    // the literal prefix, down to the first '+'/'#' level (all lanes alike)
+    uint32_t node = kRoot, d = 0;
+    SegKey key;
+    uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
+    bool frame = false;  // an enumeration frame was reached at (node, d)
+    if (!wild) {
+      // no wildcard: Retained.Get(filter) (topics.go:539-544)
+      for (;;) {
+        node = lookup(ix, node, key, fb + s, (uint32_t)(e - s));
+        if (node == kNone || e >= b1) break;
+        s = e + 1;
+        e = scan_segment(R, s, b1, &key);
+      }
+      if (node != kNone && (ix.msg[node].flags & kRetainLive)) {
+        if (FILL && lane == 0) out[0] = ix.msg[node].handle;
+        if (sp && lane == 0 && spec_cap) sp[0] = ix.msg[node].handle;
+        total = 1;
+      }
+    } else {
+      for (;;) {
+        const uint32_t len = (uint32_t)(e - s);
+        const uint32_t c0 = len == 1 ? R.at(s) : 0;
+        if (c0 == '+' || c0 == '#') {
+          frame = true;
+          break;
+        }
+        const uint32_t p = lookup(ix, node, key, fb + s, len);  // literal level (topics.go:568-576)
+        if (p == kNone) break;
+        if (e < b1) {
+          node = p;
+          d++;
+          s = e + 1;
+          e = scan_segment(R, s, b1, &key);
+          continue;
+        }
+        const NodeMsg m = ix.msg[p];
+        uint64_t h = 0;
+        bool hit = false;
+        if (m.flags & kRetainPath) {
+          hit = (m.flags & kRetainLive) != 0;
+          h = m.handle;
+        } else if (ix.empty_topic_live) {
+          hit = true;
+          h = ix.empty_topic_handle;  // Retained.Get("") on a particle without a path (Q6)
+        }
+        if (hit) {
+          if (FILL && lane == 0) out[0] = h;
+          if (sp && lane == 0 && spec_cap) sp[0] = h;
+          total = 1;
+        }
+        break;
+      }
+    }
+    if (frame) {  // topics.go:547-565 at (node, d), segment [s, e)
+      const uint32_t fd = d;
+      const uint64_t fs = s, fe = e;
+      const SegKey fkey = key;
+      const bool has_next = fe < b1;
+      const bool hash = R.at(fs) == '#';
+      const NodeMsg nm = ix.msg[node];
+      // packets under child k of the frame (its own and its subtree's), counted or appended
+      auto child = [&](uint32_t k) -> uint32_t {
+        uint32_t c = 0;
+        auto emit = [&](uint64_t h) {
+          if (FILL) {
+            out[atomicAdd(&cursor[wv], 1u)] = h;
+          } else if (sp) {
+            const uint32_t q = atomicAdd(&cursor[wv], 1u);
+            if (q < spec_cap) sp[q] = h;
+          }
+          c++;
+        };
+        const ChildRec r0 = ix.children[nm.child_off + k];
+        if (fd == 0 && (r0.flags & kChildSys)) return 0u;  // only the exact $SYS particle, level 0 (Q4)
+        if (!has_next && (r0.flags & kRetainPath) && (r0.flags & kRetainLive)) emit(r0.handle);
+        // a childless particle has nothing below it for any further level: not entered
+        if (!(has_next || hash) || r0.child_cnt == 0) return c;
+        // count pass, '#' frame: every live retained topic below the child, from its aggregate
+        if (!FILL && hash) {
+          partial = true;
+          return c + ix.msg[r0.node].below_live;
+        }
+        uint32_t node = r0.node, d = fd + 1, wd = fd;  // wd: level of the segment in the window
+        uint32_t coff = r0.child_off, ccnt = r0.child_cnt;  // node's children slab
+        uint64_t s = fs, e = fe;
+        SegKey key = fkey;
+        if (e < b1) {
+          s = e + 1;
+          e = scan_segment(R, s, b1, &key);
+          wd++;
+        }
+        uint32_t cursor = 0;
+        bool resume = false;  // re-entering an enumeration frame after a child returned
+        for (uint64_t guard = 0;; guard++) {
+          if (guard > kWalkGuard * 64) {
+            atomicOr(ix.err, kErrWalkGuard);
+            break;
+          }
+          const bool has_nx = (wd == d) && (e < b1);
+          const uint32_t len = (uint32_t)(e - s);
+          const uint32_t c0 = len == 1 ? R.at(s) : 0;
+          const bool plus = c0 == '+';
+          const bool hsh = c0 == '#';
+          bool descended = false;
+          if (!FILL && hsh) {  // count pass: the subtree's live retained topics (below_live)
+            c += ix.msg[node].below_live;
+            partial = true;
+          } else if (plus || hsh) {  // topics.go:547-565: the slab copy holds what each child needs
+            if (!resume) cursor = 0;
+            while (cursor < ccnt) {
+              const ChildRec cr = ix.children[coff + cursor];
+              cursor++;
+              if (!has_nx && (cr.flags & kRetainPath) && (cr.flags & kRetainLive)) emit(cr.handle);
+              if ((has_nx || hsh) && cr.child_cnt != 0) {
+                node = cr.node;
+                coff = cr.child_off;
+                ccnt = cr.child_cnt;
+                d++;
+                if (e < b1) {
+                  s = e + 1;
+                  e = scan_segment(R, s, b1, &key);
+                  wd++;
+                }
+                descended = true;
+                break;
+              }
+            }
+          } else if (!resume) {  // literal level (topics.go:568-576)
+            const uint32_t p = lookup(ix, node, key, fb + s, len);
+            if (p != kNone) {
+              const NodeMsg m = ix.msg[p];
+              if (has_nx) {
+                if (m.child_cnt != 0) {
+                  node = p;
+                  coff = m.child_off;
+                  ccnt = m.child_cnt;
+                  d++;
+                  s = e + 1;
+                  e = scan_segment(R, s, b1, &key);
+                  wd++;
+                  descended = true;
+                }
+              } else if (m.flags & kRetainPath) {
+                if (m.flags & kRetainLive) emit(m.handle);
+              } else if (ix.empty_topic_live) {
+                emit(ix.empty_topic_handle);  // Q6
+              }
+            }
+          }
+          if (descended) {
+            resume = false;
+            continue;
+          }
+          // frame finished: return to the parent frame; the child of the wave's enumeration
+          // frame is done when we would return into it
+          if (d == fd + 1) break;
+          const NodeMsg cm = ix.msg[node];
+          node = cm.parent;
+          const NodeMsg pm = ix.msg[node];
+          coff = pm.child_off;
+          ccnt = pm.child_cnt;
+          if (wd == d) {
+            e = s - 1;
+            s = seg_start_before(R, b0, e);
+            wd--;
+          }
+          d--;
+          cursor = cm.child_pos + 1;
+          resume = true;
+        }
+        return c;
+      };
+      if ((FILL || sp) && lane == 0) cursor[wv] = total;
+      wave_sync_lds();
+      if (!FILL && hash && fd > 0) {
+        // count pass, '#' below level 0 (no $SYS exclusion): the frame's aggregate
+        total += nm.below_live;
+        partial = true;
+      } else
+      for (uint32_t k0 = 0; k0 < nm.child_cnt; k0 += 64) {  // wave-uniform
+        const uint32_t k = k0 + lane;
+        total += wave_sum(k < nm.child_cnt ? child(k) : 0u);
+      }
+    }
+  }
+  const bool walk_again = __any(partial) || total > spec_cap;  // for the FILL pass
+  if (lane == 0) {
+    if (!FILL) {
+      cnt[t] = TopicCount{(sp && !walk_again) ? 0u : 1u, total, 0, 0, 0};
+    } else {
+      base_out[t] = off[t].rows;
+      count_out[t] = total;
+    }
+  }
+}
+
+template <int WPE>
+static void launch_msg_wpe(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                           TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
+                           uint32_t* count, uint64_t* spec, uint32_t spec_cap, hipStream_t s) {
+  dim3 grid((n + 3) / 4);  // one wavefront per filter
+  if (fill)
+    hipLaunchKernelGGL((k_msg<true, WPE>), grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base, count,
+                       spec, spec_cap);
+  else
+    hipLaunchKernelGGL((k_msg<false, WPE>), grid, dim3(256), 0, s, fb, fo, n, ix, cnt, off, handles, base,
+                       count, spec, spec_cap);
+}
+
+void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                TopicCount* cnt, const TopicOff* off, uint64_t* handles, uint64_t* base,
+                uint32_t* count, uint64_t* spec, uint32_t spec_cap, uint32_t wpe, hipStream_t s) {
+  if (!n) return;
+  if (wpe >= 8)
+    launch_msg_wpe<8>(fill, fb, fo, n, ix, cnt, off, handles, base, count, spec, spec_cap, s);
+  else if (wpe >= 6)
+    launch_msg_wpe<6>(fill, fb, fo, n, ix, cnt, off, handles, base, count, spec, spec_cap, s);
+  else
+    launch_msg_wpe<1>(fill, fb, fo, n, ix, cnt, off, handles, base, count, spec, spec_cap, s);
+}
+
+// k_msg_place: after a speculative count, every filter whose handles all sit in its scratch
+// slots is moved to its output range (one wavefront per filter, coalesced 8-byte rows); the
+// others (more than spec_cap handles, or counted through a below_live shortcut) are left to
+// k_msg<true>, which walks only them.
+__global__ __launch_bounds__(256) void k_msg_place(uint32_t n, const TopicCount* __restrict__ cnt,
+                                                   const TopicOff* __restrict__ off,
+                                                   const uint64_t* __restrict__ spec, uint32_t spec_cap,
+                                                   uint64_t* __restrict__ handles,
+                                                   uint64_t* __restrict__ base_out,
+                                                   uint32_t* __restrict__ count_out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * 4 + wave_id();
+  if (t >= n) return;
+  const TopicCount c = cnt[t];
+  if (c.gathers != 0) return;  // walked again by the FILL pass
+  const uint64_t o = off[t].rows;
+  const uint64_t* src = spec + (uint64_t)t * spec_cap;
+  for (uint32_t i = lane; i < c.rows; i += 64) handles[o + i] = src[i];
+  if (lane == 0) {
+    base_out[t] = o;
+    count_out[t] = c.rows;
+  }
+}
+
+void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, const uint64_t* spec,
+                      uint32_t spec_cap, uint64_t* handles, uint64_t* base, uint32_t* count, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_msg_place, dim3((n + 3) / 4), dim3(256), 0, s, n, cnt, off, spec, spec_cap, handles,
+                     base, count);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Messages over the level-order retained image (kernels.h MsgImg): the reverse
+// retained scan (topics.go:530-579) as run arithmetic. A '+' or '#' level with more segments
+// after it takes every image child of the run (its particles' children that have live retained
+// state at or below them: the others add nothing), a final '+' emits the children's live
+// handles, a final '#' every level below (isolateParticle repeats the last segment past the end,
+// topics.go:679-698), the root's "$SYS" child excluded at level 0 (topics.go:549, Q4). A literal
+// level looks the segment up under each particle of the run (topics.go:568-576); under a run of
+// more than one particle this is the only fan-out: the wave's lanes take the run's particles,
+// and a lane keeps deeper fan-outs on a small frame stack.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t block_scan_incl32(uint32_t v, uint32_t* wt /*4*/) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t tot;
+  const uint32_t ex = wave_excl_scan(v, lane, &tot);
+  if (lane == 0) wt[wv] = tot;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t w = 0; w < wv; w++) add += wt[w];
+  __syncthreads();
+  return ex + v + add;
+}
+
+__global__ __launch_bounds__(256) void k_scan32_reduce(const uint32_t* __restrict__ in, uint64_t n,
+                                                       uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t wt[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++)
+    if (base + k < n) v += in[base + k];
+  v = block_scan_incl32(v, wt);
+  if (threadIdx.x == 255) bsum[blockIdx.x] = v;
+}
+
+// Single workgroup: exclusive scan of the block sums; bpre[nb] = total.
+__global__ __launch_bounds__(256) void k_scan32_blocks(const uint32_t* __restrict__ bsum, uint32_t nb,
+                                                       uint32_t* __restrict__ bpre) {
+  __shared__ uint32_t wt[4];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t v = b < nb ? bsum[b] : 0u;
+    const uint32_t incl = block_scan_incl32(v, wt);
+    if (b < nb) bpre[b] = carry + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 255) carry += incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bpre[nb] = carry;
+}
+
+// in and out may alias: every thread reads its four elements before any is written
+__global__ __launch_bounds__(256) void k_scan32_apply(const uint32_t* in, uint64_t n,
+                                                      const uint32_t* __restrict__ bpre, uint32_t* out) {
+  __shared__ uint32_t wt[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  uint32_t c[4], v = 0;
+  for (int k = 0; k < 4; k++) {
+    c[k] = base + k < n ? in[base + k] : 0u;
+    v += c[k];
+  }
+  const uint32_t incl = block_scan_incl32(v, wt);
+  uint32_t ex = bpre[blockIdx.x] + incl - v;
+  for (int k = 0; k < 4; k++) {
+    if (base + k < n) out[base + k] = ex;
+    ex += c[k];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = bpre[gridDim.x];
+}
+
+void launch_scan32(const uint32_t* in, uint64_t n, uint32_t* bsum, uint32_t* bpre, uint32_t* out,
+                   hipStream_t s) {
+  if (n == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(uint32_t), s);  // errors surface at the caller's next check
+    return;
+  }
+  const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+  hipLaunchKernelGGL(k_scan32_reduce, dim3(nb), dim3(256), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(k_scan32_blocks, dim3(1), dim3(256), 0, s, bsum, nb, bpre);
+  hipLaunchKernelGGL(k_scan32_apply, dim3(nb), dim3(256), 0, s, in, n, bpre, out);
+}
+
+__global__ void k_img_root(uint32_t* node, uint32_t* pos, uint32_t* live) {
+  if (threadIdx.x == 0) {
+    node[0] = kRoot;
+    pos[kRoot] = 0;
+    live[0] = 0;  // the root has no retain path ("" is kept apart, Q6)
+  }
+}
+
+// Wavefront per parent of the level: its children slab (ChildRec) in slab order; a child is in
+// the image when its own retained message is live or one below it is (NodeMsg.below_live).
+template <bool FILL>
+// Grid-stride over the level's parents (a level of a 100M-topic index holds more parents than
+// one wavefront each can launch: a grid is limited to 2^32 threads).
+__global__ __launch_bounds__(256) void k_img_level(DevIndex ix, ImgLevelArgs a) {
+  const uint32_t lane = threadIdx.x & 63, wv = wave_id();
+  for (uint32_t p = blockIdx.x * 4 + wv; p < a.n; p += gridDim.x * 4) {  // wave-uniform
+  const uint32_t v = a.node[a.lo + p];
+  const NodeMsg m = ix.msg[v];
+  const bool root = v == kRoot;
+  const uint32_t base = FILL ? a.next + a.coff[p] : 0u;
+  uint32_t run = 0;
+  uint32_t sys_node = kNone, sys_live = 0;  // the root's "$SYS" child goes last
+  if (m.below_live != 0) {
+    for (uint32_t k0 = 0; k0 < m.child_cnt; k0 += 64) {  // wave-uniform
+      const uint32_t k = k0 + lane;
+      bool incl = false, live = false, sys = false;
+      uint32_t c = kNone;
+      if (k < m.child_cnt) {
+        const ChildRec r = ix.children[m.child_off + k];
+        c = r.node;
+        live = (r.flags & kRetainPath) && (r.flags & kRetainLive);
+        incl = live || ix.msg[c].below_live != 0;
+        sys = root && (r.flags & kChildSys);
+      }
+      const uint64_t bm = __ballot(incl && !sys);
+      if (FILL && incl && !sys) {
+        const uint32_t q = base + run + prefix_before(bm);
+        a.node[q] = c;
+        a.pos[c] = q;
+        a.live[q] = live ? 1u : 0u;
+      }
+      if (incl && sys) {
+        sys_node = c;
+        sys_live = live ? 1u : 0u;
+      }
+      run += (uint32_t)__popcll(bm);
+    }
+  }
+  const bool has_sys = __ballot(sys_node != kNone) != 0;
+  if (FILL && sys_node != kNone) {
+    const uint32_t q = base + run;
+    a.node[q] = sys_node;
+    a.pos[sys_node] = q;
+    a.live[q] = sys_live;
+  }
+  const uint32_t total = run + (has_sys ? 1u : 0u);
+  if (lane == 0) {
+    if (FILL) a.cl[a.lo + p] = make_uint2(base, base + total);
+    else a.cnt[p] = total;
+  }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_img_compact(DevIndex ix, const uint32_t* __restrict__ node,
+                                                     const uint32_t* __restrict__ lp, uint32_t n,
+                                                     uint64_t* __restrict__ h) {
+  const uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t l = lp[q];
+  if (lp[q + 1] != l) h[l] = ix.msg[node[q]].handle;
+}
+
+void launch_img_root(uint32_t* node, uint32_t* pos, uint32_t* live, hipStream_t s) {
+  hipLaunchKernelGGL(k_img_root, dim3(1), dim3(64), 0, s, node, pos, live);
+}
+
+void launch_img_level(bool fill, const DevIndex& ix, const ImgLevelArgs& a, hipStream_t s) {
+  if (!a.n) return;
+  const dim3 g(std::min<uint32_t>((a.n + 3) / 4, kMaxWaveBlocks)), b(256);
+  if (fill) hipLaunchKernelGGL(k_img_level<true>, g, b, 0, s, ix, a);
+  else hipLaunchKernelGGL(k_img_level<false>, g, b, 0, s, ix, a);
+}
+
+void launch_img_compact(const DevIndex& ix, const uint32_t* node, const uint32_t* lp, uint32_t n,
+                        uint64_t* h, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_img_compact, dim3((n + 255) / 256), dim3(256), 0, s, ix, node, lp, n, h);
+}
+
+// Image position of particle c, or kNone (not in the image: no live retained at or below it).
+__device__ __forceinline__ uint32_t img_pos(const MsgImg& img, uint32_t c) {
+  if (c >= img.n_pos) return kNone;  // kNone included
+  const uint32_t q = img.pos[c];
+  return (q < img.n && img.node[q] == c) ? q : kNone;
+}
+
+struct MsgFrame {  // a fan-out in progress: particles [cur, end) still to take segment s
+  uint32_t cur, end, s;
+};
+
+// Wavefront per filter. MODE (kernels.h MsgMode): kMsgCount counts the filter's handles and copy
+// pieces; kMsgFill writes short runs and piece records at the offsets of the count pass's scan;
+// kMsgRuns counts and records the runs (their output and piece offsets fixed by the same LDS
+// cursors the fill pass uses); kMsgPlace places recorded runs without walking again — the
+// filter's walk then runs once per batch instead of twice.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, const uint64_t* __restrict__ fo,
+                                              uint32_t n, DevIndex ix, MsgImg img,
+                                              TopicCount* __restrict__ cnt, const TopicOff* __restrict__ off,
+                                              MsgPiece* __restrict__ pieces, uint64_t* __restrict__ handles,
+                                              uint64_t* __restrict__ base_out, uint32_t* __restrict__ count_out,
+                                              MsgRun* __restrict__ runs, uint32_t run_cap,
+                                              uint32_t* __restrict__ n_runs, MsgWide w) {
+  constexpr bool WIDE = MODE == kMsgWideCount || MODE == kMsgWideFill;  // exported work items
+  constexpr bool FILL = MODE == kMsgFill || MODE == kMsgPlace || MODE == kMsgWideFill;  // the walk writes output
+  constexpr bool RUNS = MODE == kMsgRuns;
+  __shared__ uint32_t hcur[4], pcur[4], rcur[4];  // next handle / piece / run of the wave's filter
+  __shared__ uint2 mfront[4][2][kMsgFront];       // fan-out frontier: runs of one level (two buffers)
+  __shared__ uint32_t mpre[4][kMsgFront + 1];      // ... particles before each run
+  const uint32_t lane = threadIdx.x & 63, wv = wave_id();
+  uint32_t t = blockIdx.x * 4 + wv;  // (a work item's filter in the wide modes)
+  if (!WIDE && t >= n) return;  // wave-uniform
+  const uint64_t c_start = (!FILL && !WIDE && img.cyc) ? clock64() : 0ull;
+  uint64_t b0 = 0, b1 = 0, obase = 0, pbase = 0;
+  if (!WIDE) {
+    b0 = fo[t];
+    b1 = fo[t + 1];
+    obase = FILL ? off[t].rows : 0;
+    pbase = FILL ? off[t].g : 0;
+  }
+  // one piece record per kMsgPiece handles of a long run
+  auto put_pieces = [&](uint32_t h0, uint32_t len, uint32_t dst, uint32_t slot) __attribute__((always_inline)) {
+    const uint32_t npc = (len + kMsgPiece - 1) / kMsgPiece;
+    for (uint32_t i = 0; i < npc; i++)
+      pieces[pbase + slot + i] = MsgPiece{h0 + i * kMsgPiece, (uint32_t)min(kMsgPiece, len - i * kMsgPiece),
+                                          obase + dst + (uint64_t)i * kMsgPiece};
+  };
+  if (MODE == kMsgPlace) {
+    const uint32_t nr = n_runs[t];
+    if (nr != kNone) {  // wave-uniform: the count pass recorded every run of this filter
+      const MsgRun* __restrict__ fr = runs + (uint64_t)t * run_cap;
+      for (uint32_t k = lane; k < nr; k += 64) {
+        const MsgRun r = fr[k];
+        if (r.len > kMsgDirect) put_pieces(r.h0, r.len, r.dst, r.pslot);
+        else
+          for (uint32_t j = 0; j < r.len; j++) handles[obase + r.dst + j] = img.h[r.h0 + j];
+      }
+      if (lane == 0) {
+        base_out[t] = obase;
+        count_out[t] = cnt[t].rows;
+      }
+      return;
+    }
+  }
+  if (FILL || RUNS || WIDE) {
+    if (lane == 0) hcur[wv] = pcur[wv] = rcur[wv] = 0;
+    wave_sync_lds();
+  }
+  uint32_t nh = 0, np = 0;  // count pass: this lane's handles and pieces
+  auto emit = [&](uint32_t h0, uint32_t len) __attribute__((always_inline)) {
+    if (len == 0) return;
+    const uint32_t npc = len > kMsgDirect ? (len + kMsgPiece - 1) / kMsgPiece : 0u;
+    if (!FILL) {
+      nh += len;
+      np += npc;
+      if (!RUNS && MODE != kMsgWideCount) return;
+    }
+    const uint32_t dst = atomicAdd(&hcur[wv], len);
+    const uint32_t slot = npc ? atomicAdd(&pcur[wv], npc) : 0u;
+    if (RUNS) {
+      const uint32_t ri = atomicAdd(&rcur[wv], 1u);
+      if (ri < run_cap) runs[(uint64_t)t * run_cap + ri] = MsgRun{h0, len, dst, slot};
+      return;
+    }
+    if (MODE == kMsgWideCount) {  // into the wavefront's scratch (its cursor runs across items)
+      const uint32_t ri = atomicAdd(&rcur[wv], 1u);
+      if (ri < w.per_wave) w.scratch[(uint64_t)(blockIdx.x * 4 + wv) * w.per_wave + ri] = MsgRun{h0, len, dst, slot};
+      return;
+    }
+    if (!npc) {
+      for (uint32_t k = 0; k < len; k++) handles[obase + dst + k] = img.h[h0 + k];
+      return;
+    }
+    put_pieces(h0, len, dst, slot);
+  };
+  // image children of the run [a, b) (a < b); at level 0 without "$SYS" (topics.go:549)
+  auto desc = [&](uint32_t a, uint32_t b, uint32_t& x, uint32_t& y) __attribute__((always_inline)) {
+    x = img.cl[a].x;
+    y = img.cl[b - 1].y;
+    if (a == 0 && y > x && (ix.msg[img.node[y - 1]].flags & kChildSys)) y--;
+  };
+  // a final '+' (one level) or '#' (every level below) over the children run [x, y)
+  auto emit_final = [&](bool hash, uint32_t x, uint32_t y) __attribute__((always_inline)) {
+    for (uint32_t guard = 0; x < y && guard < 4096; guard++) {
+      emit(img.lp[x], img.lp[y] - img.lp[x]);
+      if (!hash) break;
+      const uint32_t nx = img.cl[x].x, ny = img.cl[y - 1].y;
+      x = nx;
+      y = ny;
+    }
+  };
+  ByteReader R(fb);
+  auto dfs_run = [&](uint32_t ra, uint32_t rb, uint64_t rs) __attribute__((always_inline)) {
+    MsgFrame st[kMsgStack];
+    for (uint32_t u = ra + lane; u < rb; u += 64) {
+      uint32_t sp = 0, ua = u, ub = u + 1;
+      uint64_t us = rs;
+      for (uint64_t guard = 0;; guard++) {
+        if (guard > kWalkGuard) {
+          atomicOr(ix.err, kErrWalkGuard);
+          break;
+        }
+        bool pop = false;
+        const uint64_t e = find_slash(R, us, b1);
+        const bool last = e >= b1;
+        const uint32_t len = (uint32_t)(e - us);
+        const uint32_t c0 = len == 1 ? R.at(us) : 0u;
+        if (c0 == '+' || c0 == '#') {
+          uint32_t x, y;
+          desc(ua, ub, x, y);
+          if (last) {
+            emit_final(c0 == '#', x, y);
+            pop = true;
+          } else {
+            ua = x;
+            ub = y;
+            us = e + 1;
+            pop = ua >= ub;
+          }
+        } else if (ub - ua > 1) {  // a literal under a run: one particle now, the rest later
+          if (sp == kMsgStack) {
+            atomicOr(ix.err, kErrMsgNest);
+            break;
+          }
+          st[sp++] = MsgFrame{ua + 1, ub, (uint32_t)(us - b0)};
+          ub = ua + 1;
+        } else {
+          SegKey key = key_of(R, us, e);
+          const uint32_t qc = img_pos(img, lookup(ix, img.node[ua], key, fb + us, len));
+          if (qc == kNone) {
+            pop = true;
+          } else if (last) {
+            emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+            pop = true;
+          } else {
+            ua = qc;
+            ub = qc + 1;
+            us = e + 1;
+          }
+        }
+        if (pop) {
+          if (sp == 0) break;
+          MsgFrame& f = st[sp - 1];
+          ua = f.cur;
+          ub = ua + 1;
+          us = b0 + f.s;
+          if (++f.cur >= f.end) sp--;
+        }
+      }
+    }
+  };
+  if (WIDE) {  // wavefront per exported item: its particles, lane by lane (dfs_run)
+    const uint32_t ni = min(*w.n_items, w.cap);
+    const uint32_t wbase = (blockIdx.x * 4 + wv) * w.per_wave;  // (wide count: this wavefront's scratch)
+    for (uint32_t i = blockIdx.x * 4 + wv; i < ni; i += gridDim.x * 4) {
+      const MsgWork it = w.items[i];
+      t = it.t;
+      b0 = fo[t];
+      b1 = fo[t + 1];
+      if (FILL && it.n_runs != kNone) {  // the count's runs, placed after the filter's own part
+        obase = off[t].rows + it.dst;
+        pbase = off[t].g + it.pslot;
+        for (uint32_t k = lane; k < it.n_runs; k += 64) {
+          const MsgRun r = w.scratch[(uint64_t)it.run_off + k];
+          if (r.len > kMsgDirect) put_pieces(r.h0, r.len, r.dst, r.pslot);
+          else
+            for (uint32_t j = 0; j < r.len; j++) handles[obase + r.dst + j] = img.h[r.h0 + j];
+        }
+        continue;
+      }
+      uint32_t r0 = 0;
+      if (lane == 0) {
+        if (FILL) {
+          hcur[wv] = it.dst;
+          pcur[wv] = it.pslot;
+        } else {
+          hcur[wv] = pcur[wv] = 0;
+          r0 = rcur[wv];
+        }
+      }
+      if (FILL) {
+        obase = off[t].rows;
+        pbase = off[t].g;
+      }
+      wave_sync_lds();
+      dfs_run(it.x, it.y, b0 + it.s);
+      wave_sync_lds();
+      if (!FILL && lane == 0) {  // the item's place in its filter's output: after the count pass's own part
+        const uint32_t r1 = rcur[wv];
+        w.items[i].dst = atomicAdd(&cnt[t].rows, hcur[wv]);
+        w.items[i].pslot = atomicAdd(&cnt[t].gathers, pcur[wv]);
+        w.items[i].run_off = wbase + r0;
+        w.items[i].n_runs = r1 <= w.per_wave ? r1 - r0 : kNone;
+      }
+    }
+    return;
+  }
+  bool exported = false;  // the count pass handed the filter's fan-out to work items (MsgWide)
+  if (b1 > b0 && ix.retained_len != 0) {  // topics.go:535
+    bool wild = false;
+    for (uint64_t i = b0 + lane; i < b1; i += 64) {
+      const uint32_t ch = fb[i];
+      wild |= (ch == '+') | (ch == '#');
+    }
+    if (!__any(wild)) {  // Retained.Get(filter) (topics.go:539-544)
+      uint32_t node = kRoot;
+      SegKey key;
+      uint64_t s = b0, e = scan_segment(R, b0, b1, &key);
+      for (;;) {
+        node = lookup(ix, node, key, fb + s, (uint32_t)(e - s));
+        if (node == kNone || e >= b1) break;
+        s = e + 1;
+        e = scan_segment(R, s, b1, &key);
+      }
+      if (lane == 0 && node != kNone && (ix.msg[node].flags & kRetainLive)) {
+        const uint32_t q = img_pos(img, node);
+        if (q != kNone) emit(img.lp[q], 1u);
+      }
+    } else {
+      // wave-uniform: the run [a, b) that segment s applies to, until a literal meets a longer run
+      uint32_t a = 0, b = 1;
+      uint64_t s = b0;
+      bool fan = false;
+      for (uint32_t guard = 0; guard < 4096; guard++) {
+        const uint64_t e = find_slash(R, s, b1);
+        const bool last = e >= b1;
+        const uint32_t len = (uint32_t)(e - s);
+        const uint32_t c0 = len == 1 ? R.at(s) : 0u;
+        if (c0 == '+' || c0 == '#') {  // topics.go:547-565
+          uint32_t x, y;
+          desc(a, b, x, y);
+          if (last) {
+            if (lane == 0) emit_final(c0 == '#', x, y);
+            break;
+          }
+          a = x;
+          b = y;
+          s = e + 1;
+          if (a >= b) break;
+          continue;
+        }
+        if (b - a > 1) {
+          fan = true;
+          break;
+        }
+        SegKey key = key_of(R, s, e);
+        const uint32_t qc = img_pos(img, lookup(ix, img.node[a], key, fb + s, len));
+        if (qc == kNone) break;
+        if (last) {
+          if (lane == 0) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+          break;
+        }
+        a = qc;
+        b = qc + 1;
+        s = e + 1;
+      }
+      if (fan) {
+        // A literal segment under a run of several particles. Level-synchronous fan-out: the
+        // frontier is a list of runs [x, y) of one level, in LDS; every lane takes particles of
+        // the same level, so a literal level's lookups are issued together with one key for the
+        // wave, a '+' maps each run to its children's run, and a final '+' / '#' emits each run.
+        // A frontier that outgrows its LDS falls back, run by run, to the per-lane walk
+        // (dfs_run: lanes take a run's particles, each walks the rest of the filter alone with
+        // deeper fan-outs on a frame stack).
+        uint2* cur = mfront[wv][0];
+        uint2* nxt = mfront[wv][1];
+        uint32_t nr = 1;
+        if (lane == 0) cur[0] = make_uint2(a, b);
+        wave_sync_lds();
+        uint64_t ls = s;  // the segment the frontier's runs take next
+        for (uint32_t guard = 0; guard < 4096; guard++) {
+          const uint64_t e = find_slash(R, ls, b1);
+          const bool last = e >= b1;
+          const uint32_t len = (uint32_t)(e - ls);
+          const uint32_t c0 = len == 1 ? R.at(ls) : 0u;
+          uint32_t nn = 0;  // the next frontier's runs (wave-uniform)
+          if (c0 == '+' || c0 == '#') {
+            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+              const uint32_t r = r0 + lane;
+              uint32_t x = 0, y = 0;
+              if (r < nr) {
+                const uint2 ru = cur[r];
+                desc(ru.x, ru.y, x, y);
+              }
+              if (last) {
+                if (r < nr) emit_final(c0 == '#', x, y);
+                continue;
+              }
+              const bool keep = r < nr && x < y;
+              const uint64_t bk = __ballot(keep);
+              const uint32_t at = nn + prefix_before(bk);
+              if (keep && at < kMsgFront) nxt[at] = make_uint2(x, y);
+              nn += (uint32_t)__popcll(bk);
+            }
+          } else {
+            // literal: every particle of every run looks the segment up; particle p of the
+            // frontier is found through the runs' prefix sums
+            const SegKey key = key_of(R, ls, e);
+            uint32_t tot = 0;
+            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+              const uint32_t r = r0 + lane;
+              const uint32_t v = r < nr ? cur[r].y - cur[r].x : 0u;
+              uint32_t ct;
+              const uint32_t ex = wave_excl_scan(v, lane, &ct);
+              if (r < nr) mpre[wv][r] = tot + ex;
+              tot += ct;
+            }
+            if (lane == 0) mpre[wv][nr] = tot;
+            if (!FILL && img.work && lane == 0) atomicAdd(img.work + 0, (unsigned long long)tot);
+            wave_sync_lds();
+            if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && tot > w.min_tot) {
+              if (FILL) {  // the count pass exported from here: its items write the rest
+                if (cnt[t].shared) break;
+              } else {
+                // the runs as items of at most kMsgChunk particles (one reservation for all)
+                uint32_t nit = 0;
+                for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+                  const uint32_t r = r0 + lane;
+                  const uint32_t c = r < nr ? (cur[r].y - cur[r].x + kMsgChunk - 1) / kMsgChunk : 0u;
+                  nit += wave_sum(c);
+                }
+                uint32_t ib = 0;
+                if (lane == 0) ib = atomicAdd(w.n_items, nit);
+                ib = __shfl(ib, 0, 64);
+                if (ib + nit <= w.cap) {
+                  for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+                    const uint32_t r = r0 + lane;
+                    uint32_t x = 0, y = 0;
+                    if (r < nr) {
+                      x = cur[r].x;
+                      y = cur[r].y;
+                    }
+                    const uint32_t c = (y - x + kMsgChunk - 1) / kMsgChunk;
+                    uint32_t ct;
+                    const uint32_t ex = wave_excl_scan(c, lane, &ct);
+                    for (uint32_t k = 0; k < c; k++)
+                      w.items[ib + ex + k] = MsgWork{t, x + k * kMsgChunk, min(y, x + (k + 1) * kMsgChunk),
+                                                     (uint32_t)(ls - b0), 0u, 0u, 0u, kNone};
+                    ib += ct;
+                  }
+                  exported = true;
+                  break;
+                }  // (the queue is full: this filter walks alone, as a fill walk will)
+              }
+            }
+            for (uint32_t p0 = 0; p0 < tot; p0 += 64) {
+              const uint32_t p = p0 + lane;
+              uint32_t qc = kNone;
+              if (p < tot) {
+                uint32_t lo = 0, hi = nr;  // mpre[lo] <= p < mpre[hi]
+                while (hi - lo > 1) {
+                  const uint32_t mid = (lo + hi) >> 1;
+                  if (mpre[wv][mid] <= p) lo = mid;
+                  else hi = mid;
+                }
+                const uint32_t u = cur[lo].x + (p - mpre[wv][lo]);
+                qc = img_pos(img, lookup(ix, img.node[u], key, fb + ls, len));
+              }
+              if (last) {
+                if (qc != kNone) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+                continue;
+              }
+              const bool keep = qc != kNone;
+              const uint64_t bk = __ballot(keep);
+              const uint32_t at = nn + prefix_before(bk);
+              if (keep && at < kMsgFront) nxt[at] = make_uint2(qc, qc + 1);
+              nn += (uint32_t)__popcll(bk);
+            }
+          }
+          if (last) break;
+          if (nn > kMsgFront) {  // too wide for LDS: the per-lane walk from this level
+            if (!FILL && img.work && lane == 0) {
+              uint32_t np = 0;
+              for (uint32_t r = 0; r < nr; r++) np += cur[r].y - cur[r].x;
+              atomicAdd(img.work + 1, 1ull);
+              atomicAdd(img.work + 2, (unsigned long long)np);
+            }
+            for (uint32_t r = 0; r < nr; r++) {
+              const uint2 ru = cur[r];
+              dfs_run(ru.x, ru.y, ls);
+            }
+            break;
+          }
+          wave_sync_lds();  // the next frontier is complete; the current one is free
+          uint2* tmp = cur;
+          cur = nxt;
+          nxt = tmp;
+          nr = nn;
+          ls = e + 1;
+          if (nr == 0) break;
+        }
+      }
+    }
+  }
+  if (!FILL) {
+    nh = wave_sum(nh);
+    np = wave_sum(np);
+    if (RUNS) wave_sync_lds();  // every lane's run reservations are in rcur
+    if (lane == 0) {
+      cnt[t] = TopicCount{np, nh, exported ? 1u : 0u, 0, 0};
+      if (RUNS) n_runs[t] = rcur[wv] <= run_cap ? rcur[wv] : kNone;
+      if (img.cyc) img.cyc[t] = (uint32_t)min((clock64() - c_start) >> 4, 0xFFFFFFFFull);
+    }
+  } else if (lane == 0) {
+    base_out[t] = obase;
+    count_out[t] = cnt[t].rows;
+  }
+}
+
+void launch_msgq(int mode, const uint8_t* fb, const uint64_t* fo, uint32_t n, const DevIndex& ix,
+                 const MsgImg& img, TopicCount* cnt, const TopicOff* off, MsgPiece* pieces,
+                 uint64_t* handles, uint64_t* base, uint32_t* count, MsgRun* runs, uint32_t run_cap,
+                 uint32_t* n_runs, const MsgWide& w, uint32_t wide_blocks, hipStream_t s) {
+  if (!n) return;
+  // the wide modes: persistent wavefronts over the items (their number is on the device)
+  const dim3 g(mode == kMsgWideCount || mode == kMsgWideFill ? std::max(1u, wide_blocks) : (n + 3) / 4), b(256);
+#define MQ_MSGQ(M) \
+  hipLaunchKernelGGL(k_msgq<M>, g, b, 0, s, fb, fo, n, ix, img, cnt, off, pieces, handles, base, count, runs, run_cap, \
+                     n_runs, w)
+  switch (mode) {
+    case kMsgCount: MQ_MSGQ(kMsgCount); break;
+    case kMsgFill: MQ_MSGQ(kMsgFill); break;
+    case kMsgRuns: MQ_MSGQ(kMsgRuns); break;
+    case kMsgWideCount: MQ_MSGQ(kMsgWideCount); break;
+    case kMsgWideFill: MQ_MSGQ(kMsgWideFill); break;
+    default: MQ_MSGQ(kMsgPlace); break;
+  }
+#undef MQ_MSGQ
+}
+
+// Wavefront per piece: four 64-handle loads in flight per lane, then the stores.
+__global__ __launch_bounds__(256) void k_msg_copy(const MsgPiece* __restrict__ pieces, uint64_t n,
+                                                  const uint64_t* __restrict__ h, uint64_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + wave_id(); i < n; i += (uint64_t)gridDim.x * 4) {
+  const MsgPiece p = pieces[i];
+  const uint64_t* src = h + p.h0;
+  uint64_t* dst = out + p.dst;
+  uint32_t k = lane;
+  for (; k + 192 < p.len; k += 256) {
+    const uint64_t v0 = src[k], v1 = src[k + 64], v2 = src[k + 128], v3 = src[k + 192];
+    __builtin_nontemporal_store(v0, dst + k);
+    __builtin_nontemporal_store(v1, dst + k + 64);
+    __builtin_nontemporal_store(v2, dst + k + 128);
+    __builtin_nontemporal_store(v3, dst + k + 192);
+  }
+  for (; k < p.len; k += 64) __builtin_nontemporal_store(src[k], dst + k);
+  }
+}
+
+void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)std::min<uint64_t>((n + 3) / 4, kMaxWaveBlocks)), dim3(256), 0, s, pieces, n, h, out);
+}
+
+
+}  // namespace mq

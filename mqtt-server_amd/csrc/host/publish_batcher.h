@@ -223,7 +223,7 @@ class BasicBatcher {
           res = match_(batch);
         } catch (...) {
           err = std::current_exception();
-          retried = attempt == 0;
+          if (attempt == 0) retried = true;
         }
       }
       last_n_ = n;

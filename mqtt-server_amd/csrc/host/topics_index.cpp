@@ -78,7 +78,7 @@ void IdTable::tidy(uint32_t id, uint64_t now) {
 void TopicsIndex::fail_tidy(int rc, const char* what, const uint32_t* clients, size_t nc, const uint32_t* filters,
                             size_t nf) {
   {
-    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
     const uint64_t now = epochs_.now();
     for (size_t i = 0; i < nc; i++) clients_.tidy(clients[i], now);
     for (size_t i = 0; i < nf; i++) filters_.tidy(filters[i], now);
@@ -117,14 +117,14 @@ bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) 
   std::lock_guard<std::mutex> up(upd_mu_);
   uint32_t c, f;
   {
-    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
     c = clients_.intern(client);
     f = filters_.intern(sub.Filter);
   }
   const int rc = mq_subscribe(idx_, sub.Filter.data(), (uint32_t)sub.Filter.size(), c, f, sub.Qos,
                               sub_flags(sub), sub.Identifier);
   if (rc < 0) fail_tidy(rc, "mq_subscribe", &c, 1, &f, 1);
-  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
   store(c, f, sub);
   return rc == 1;
 }
@@ -134,14 +134,14 @@ bool TopicsIndex::Unsubscribe(const std::string& filter, const std::string& clie
   uint32_t c = kNoClient, f = 0;
   bool known_f;
   {
-    std::shared_lock<std::shared_mutex> lk(tables_mu_);
+    std::shared_lock<WriterPreferringMutex> lk(tables_mu_);
     if (!clients_.find(client, &c)) c = kNoClient;  // looked up, never interned
     known_f = filters_.find(filter, &f);
   }
   const int rc = mq_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), c);
   check(rc, "mq_unsubscribe");
   if (c != kNoClient && known_f) {
-    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
     auto it = stored_.find({c, f});
     if (it != stored_.end()) {
       stored_.erase(it);
@@ -157,13 +157,13 @@ bool TopicsIndex::InlineSubscribe(const InlineSubscription& sub) {
   std::lock_guard<std::mutex> up(upd_mu_);
   uint32_t f;
   {
-    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
     f = filters_.intern(sub.Sub.Filter);
   }
   const int rc = mq_inline_subscribe(idx_, sub.Sub.Filter.data(), (uint32_t)sub.Sub.Filter.size(),
                                      sub.Sub.Identifier, f);
   if (rc < 0) fail_tidy(rc, "mq_inline_subscribe", nullptr, 0, &f, 1);
-  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
   auto it = inline_.find({sub.Sub.Identifier, f});
   if (it != inline_.end()) {
     it->second = sub;
@@ -178,7 +178,7 @@ bool TopicsIndex::InlineUnsubscribe(int id, const std::string& filter) {
   std::lock_guard<std::mutex> up(upd_mu_);
   const int rc = mq_inline_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), id);
   check(rc, "mq_inline_unsubscribe");
-  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
   uint32_t f;
   if (filters_.find(filter, &f)) {
     auto it = inline_.find({id, f});
@@ -199,7 +199,7 @@ std::vector<bool> TopicsIndex::LoadSubscriptions(const std::vector<std::pair<std
   std::vector<uint8_t> qos(n), flags(n), out_new(std::max<size_t>(n, 1));
   std::vector<int32_t> idents(n);
   {
-    std::unique_lock<std::shared_mutex> lk(tables_mu_);
+    std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
     for (size_t i = 0; i < n; i++) {
       const Subscription& s = subs[i].second;
       cids[i] = clients_.intern(subs[i].first);
@@ -215,7 +215,7 @@ std::vector<bool> TopicsIndex::LoadSubscriptions(const std::vector<std::pair<std
   const int rc = mq_subscribe_bulk(idx_, (const uint8_t*)bytes.data(), offs.data(), cids.data(), fids.data(),
                                    qos.data(), flags.data(), idents.data(), n, out_new.data());
   if (rc < 0) fail_tidy(rc, "mq_subscribe_bulk", cids.data(), n, fids.data(), n);
-  std::unique_lock<std::shared_mutex> lk(tables_mu_);
+  std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
   std::vector<bool> out(n);
   for (size_t i = 0; i < n; i++) {
     store(cids[i], fids[i], subs[i].second);
@@ -248,12 +248,12 @@ void TopicsIndex::RetainedAdd(const std::string& topic, uint64_t handle, uint32_
 uint64_t TopicsIndex::RetainedLen() const { return mq_retained_len(idx_); }
 
 size_t TopicsIndex::live_clients() const {
-  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  std::shared_lock<WriterPreferringMutex> lk(tables_mu_);
   return clients_.live();
 }
 
 size_t TopicsIndex::live_filters() const {
-  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  std::shared_lock<WriterPreferringMutex> lk(tables_mu_);
   return filters_.live();
 }
 
@@ -277,12 +277,12 @@ std::string TopicView::client(uint32_t id) const { return b_->index().ClientName
 std::string TopicView::filter(uint32_t id) const { return b_->index().FilterName(id); }
 
 std::string TopicsIndex::ClientName(uint32_t id) const {
-  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  std::shared_lock<WriterPreferringMutex> lk(tables_mu_);
   return clients_.str(id);
 }
 
 std::string TopicsIndex::FilterName(uint32_t id) const {
-  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  std::shared_lock<WriterPreferringMutex> lk(tables_mu_);
   return filters_.str(id);
 }
 
@@ -351,7 +351,7 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const PackedTopics& topic
   // every later update would wait for it); declared before the table lock, so released after it
   std::unique_ptr<mq_span_result, void (*)(void*)> own(r, mq_result_free);
   std::vector<Subscribers> out(topics.size());
-  std::shared_lock<std::shared_mutex> lk(tables_mu_);
+  std::shared_lock<WriterPreferringMutex> lk(tables_mu_);
   auto stored = [&](uint32_t c, uint32_t f, const mq_client_row* row) {
     auto it = stored_.find({c, f});
     if (it != stored_.end()) return it->second;
@@ -379,7 +379,7 @@ std::vector<Subscribers> TopicsIndex::SubscribersBatch(const PackedTopics& topic
       for (uint32_t i = 0; i < sp.n_sub; i++, rowi++) {
         mq_client_row row = r->sub_pool[sp.sub_off + i];
         auto pit = patched.find(rowi);
-        if (pit != patched.end()) row.meta = pit->second;
+        if (pit != patched.end()) row.meta = mq_patch_apply(pit->second, row.meta, row.identifier);
         const uint32_t kind = row.meta & MQ_ROW_KIND_MASK;
         if (kind == 0) {  // client row: merged Subscription
           Subscription sub = stored(row.client_id, row.filter_id, &row);

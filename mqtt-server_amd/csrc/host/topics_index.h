@@ -7,6 +7,7 @@
 #pragma once
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <deque>
 #include <memory>
@@ -102,6 +103,47 @@ class Epochs {
   std::multiset<uint64_t> active_;
 };
 
+// A shared mutex that prefers writers, as Go's sync.RWMutex does (the reference's tables sit
+// behind one, topics.go:402): once a writer waits, new readers wait for it, so readers that hold
+// the lock back to back (the batchers' map building) cannot starve an update. (glibc's
+// std::shared_mutex prefers readers.) Usable with std::unique_lock / std::shared_lock.
+class WriterPreferringMutex {
+ public:
+  void lock() {
+    std::unique_lock<std::mutex> g(mu_);
+    waiting_++;
+    cv_.wait(g, [&] { return !writer_ && readers_ == 0; });
+    waiting_--;
+    writer_ = true;
+  }
+  void unlock() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      writer_ = false;
+    }
+    cv_.notify_all();
+  }
+  void lock_shared() {
+    std::unique_lock<std::mutex> g(mu_);
+    cv_.wait(g, [&] { return !writer_ && waiting_ == 0; });
+    readers_++;
+  }
+  void unlock_shared() {
+    bool last;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      last = --readers_ == 0;
+    }
+    if (last) cv_.notify_all();
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  uint32_t readers_ = 0, waiting_ = 0;
+  bool writer_ = false;
+};
+
 // Dense u32 ids of strings (client ids, filter strings), referenced by the stored subscriptions
 // that use them; an unreferenced id is released and later reused (Epochs). Not synchronised:
 // TopicsIndex guards it.
@@ -187,7 +229,7 @@ class TopicView {
       const mq_span& sp = r.spans[ts.span_base + k];
       for (uint32_t i = 0; i < sp.n_sub; i++, row++) {
         mq_client_row cr = r.sub_pool[sp.sub_off + i];
-        if (pi < p.size() && p[pi].row == row) cr.meta = p[pi++].meta;
+        if (pi < p.size() && p[pi].row == row) cr.meta = mq_patch_apply(p[pi++].meta, cr.meta, cr.identifier);
         if ((cr.meta & MQ_ROW_KIND_MASK) != MQ_ROW_DROP) f(cr);
       }
     }
@@ -270,7 +312,7 @@ class TopicsIndex {
                               size_t nf);
   mq_index* idx_ = nullptr;
   std::mutex upd_mu_;                    // serialises updates
-  mutable std::shared_mutex tables_mu_;  // the tables below: exclusive to change, shared to read
+  mutable WriterPreferringMutex tables_mu_;  // the tables below: exclusive to change, shared to read
   Epochs epochs_;
   IdTable clients_{epochs_}, filters_{epochs_};
   std::map<std::pair<uint32_t, uint32_t>, Subscription> stored_;  // (client, filter)

@@ -797,6 +797,9 @@ type spanView struct {
 	subPool    []C.mq_client_row
 	shrPool    []C.mq_shared_row
 	pickedOnly bool
+	codes      bool     // 4-byte patch codes (MQ_SPANS_PATCH_CODES): patchCodes / setCodes instead
+	patchCodes []uint32 // of patches / setPatches
+	setCodes   []uint32
 }
 
 func (x *TopicsIndex) matchSpans(topics []string) (*spanView, error) {
@@ -811,10 +814,17 @@ func (x *TopicsIndex) matchSpans(topics []string) (*spanView, error) {
 	v := &spanView{x: x, r: r, stamp: stamp}
 	v.ts = unsafe.Slice(r.topics, int(r.n_topics))
 	v.spans = unsafe.Slice(r.spans, int(r.n_spans))
-	v.patches = unsafe.Slice(r.patches, int(r.n_patches))
-	// merge-set patches (MQ_TOPIC_SET_PATCHES): row x<<MQ_SET_ROW_BITS|k is record k of the
-	// topic's x-th may-merge particle, whose first row is merge_rows[merge_row_base[topic]+x]
-	v.setPatches = unsafe.Slice(r.set_patches, int(r.n_set_patches))
+	v.codes = r.flags&C.MQ_SPANS_PATCH_CODES != 0
+	// merge-set patches (MQ_TOPIC_SET_PATCHES): row x<<MQ_SET_ROW_BITS|k (codes:
+	// x<<MQ_CODE_SET_ROW_BITS|k) is record k of the topic's x-th may-merge particle, whose first
+	// row is merge_rows[merge_row_base[topic]+x]
+	if v.codes {
+		v.patchCodes = unsafe.Slice((*uint32)(unsafe.Pointer(r.patches)), int(r.n_patches))
+		v.setCodes = unsafe.Slice((*uint32)(unsafe.Pointer(r.set_patches)), int(r.n_set_patches))
+	} else {
+		v.patches = unsafe.Slice(r.patches, int(r.n_patches))
+		v.setPatches = unsafe.Slice(r.set_patches, int(r.n_set_patches))
+	}
 	v.mergeRows = unsafe.Slice(r.merge_rows, int(r.n_merge_rows))
 	if r.merge_row_base != nil {
 		v.mergeBase = unsafe.Slice(r.merge_row_base, int(r.n_topics))
@@ -825,6 +835,29 @@ func (x *TopicsIndex) matchSpans(topics []string) (*spanView, error) {
 	v.shrPool = unsafe.Slice(r.shared_pool, int(r.shared_pool_len))
 	v.pickedOnly = r.flags&C.MQ_SPANS_PICKED != 0
 	return v, nil
+}
+
+// patchOp marks a patch code's op in the patched map (MQ_PATCH_OP); patchApply is mq_patch_apply:
+// op 1..6 the merge base with Qos (op-1)%3 and NoLocal (op-1)/3, op 7 a later match.
+const patchOp = uint32(C.MQ_PATCH_OP)
+
+func patchApply(p, meta uint32, ident int32) uint32 {
+	if p&patchOp == 0 {
+		return p
+	}
+	op := p & 7
+	if op == 7 {
+		if ident > 0 {
+			return meta | C.MQ_ROW_IDENT
+		}
+		return meta | C.MQ_ROW_DROP
+	}
+	meta &^= C.MQ_META_QOS_MASK | C.MQ_META_NOLOCAL
+	meta |= (op - 1) % 3
+	if (op-1)/3 != 0 {
+		meta |= C.MQ_META_NOLOCAL
+	}
+	return meta
 }
 
 func (v *spanView) release() {
@@ -861,21 +894,39 @@ func (v *spanView) get(i int) *Subscribers {
 		}
 		return packets.Subscription{Filter: x.filters.strs[f], Identifier: int(ident), Qos: byte(meta & C.MQ_META_QOS_MASK)}
 	}
-	const rowBits = uint32(C.MQ_SET_ROW_BITS)
 	t := v.ts[i]
 	s := emptySubscribers()
-	var patched map[uint32]uint32 // topic row -> meta
+	var patched map[uint32]uint32 // topic row -> meta, or patchOp | op (a patch code)
 	if t.n_patches > 0 {
 		patched = make(map[uint32]uint32, int(t.n_patches))
 	}
-	if t.flags&C.MQ_TOPIC_SET_PATCHES != 0 {
-		mr := v.mergeRows[v.mergeBase[i]:]
-		for _, pt := range v.setPatches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
-			row := uint32(pt.row)
-			patched[uint32(mr[row>>rowBits])+row&(1<<rowBits-1)] = uint32(pt.meta)
+	lo, hi := t.patch_base, t.patch_base+C.uint64_t(t.n_patches)
+	set := t.flags&C.MQ_TOPIC_SET_PATCHES != 0
+	var mr []C.uint32_t
+	if set {
+		mr = v.mergeRows[v.mergeBase[i]:]
+	}
+	topicRow := func(row, bits uint32) uint32 { // a set patch's row, through the topic's merge rows
+		if !set {
+			return row
 		}
-	} else {
-		for _, pt := range v.patches[t.patch_base : t.patch_base+C.uint64_t(t.n_patches)] {
+		return uint32(mr[row>>bits]) + row&(1<<bits-1)
+	}
+	switch {
+	case v.codes && set:
+		for _, c := range v.setCodes[lo:hi] {
+			patched[topicRow(c>>3, C.MQ_CODE_SET_ROW_BITS)] = patchOp | c&7
+		}
+	case v.codes:
+		for _, c := range v.patchCodes[lo:hi] {
+			patched[c>>3] = patchOp | c&7
+		}
+	case set:
+		for _, pt := range v.setPatches[lo:hi] {
+			patched[topicRow(uint32(pt.row), C.MQ_SET_ROW_BITS)] = uint32(pt.meta)
+		}
+	default:
+		for _, pt := range v.patches[lo:hi] {
 			patched[uint32(pt.row)] = uint32(pt.meta)
 		}
 	}
@@ -892,7 +943,7 @@ func (v *spanView) get(i int) *Subscribers {
 		for _, cr := range v.subPool[sp.sub_off : sp.sub_off+sp.n_sub] {
 			meta := uint32(cr.meta)
 			if m, ok := patched[row]; ok {
-				meta = m
+				meta = patchApply(m, meta, int32(cr.identifier))
 			}
 			row++
 			switch meta & C.MQ_ROW_KIND_MASK {

@@ -80,6 +80,7 @@ OPT_CHUNK_ROWS, OPT_PATCH_CAP, OPT_EDGE_LOAD = 1, 6, 13
 OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_MERGE_WAVES = 2, 3, 4, 5, 7
 OPT_MSG_IMAGE, OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_MERGE_DEDUP = 8, 9, 10, 12
 OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC, OPT_FUSE_DESC, OPT_SET_EXP, OPT_MSG_EXPORT = 14, 15, 16, 17, 18, 19
+OPT_PATCH_CODES = 20
 
 
 class MsgResult(C.Structure):
@@ -114,10 +115,12 @@ EXPORTS = [
     "mq_profile_read", "mq_profile_reset", "mq_index_check", "mq_match_device_chunks",
     "mq_acl_match_batch", "mq_select_shared_device", "mq_match_spans", "mq_match_spans_device",
     "mq_spans_expand", "mq_set_option", "mq_match_spans_begin", "mq_match_spans_end",
-    "mq_match_spans_end_host", "mq_device_check",
+    "mq_match_spans_end_host", "mq_device_check", "mq_match_spans_submit", "mq_match_spans_wait",
 ]
 
 CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
+SPANS_PATCH_CODES = 2  # MQ_SPANS_PATCH_CODES
+PATCH_OP = 0x20000000  # MQ_PATCH_OP
 
 CHUNK_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(MatchResult), C.c_uint32, C.c_void_p)
 
@@ -160,6 +163,8 @@ def lib():
         "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
         "mq_match_spans": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(SpanResult))]),
         "mq_match_spans_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(SpanResult)]),
+        "mq_match_spans_submit": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(vp)]),
+        "mq_match_spans_wait": (C.c_int, [vp, C.POINTER(C.POINTER(SpanResult))]),
         "mq_spans_expand": (C.c_int, [C.POINTER(SpanResult), C.c_uint32, C.c_uint32, vp, C.c_uint64, vp,
                                       C.c_uint64, _u64p, _u64p]),
         "mq_set_option": (C.c_int, [vp, C.c_uint32, C.c_uint64]),
@@ -418,6 +423,34 @@ class Engine:
         _check(lib().mq_match_spans_end_host(self.h, arr, len(foreign), C.byref(rp)), "mq_match_spans_end_host")
         return _expand_host_spans(rp, n)
 
+    def match_spans_pipelined(self, bytes_, offs, batches):
+        """`batches` consecutive mq_match_spans_submit calls of the same host topics, each waited
+        for (mq_match_spans_wait) after the next one is submitted, so that a batch's copy into host
+        memory runs beside the next batch's kernels; every result is freed. Returns the results'
+        bytes (each batch's are the same)."""
+        n = len(offs) - 1
+        pending, nbytes = [], 0
+
+        def finish(t):
+            nonlocal nbytes
+            rp = C.POINTER(SpanResult)()
+            _check(lib().mq_match_spans_wait(t, C.byref(rp)), "mq_match_spans_wait")
+            r = rp.contents
+            pw = 4 if r.flags & SPANS_PATCH_CODES else 8
+            nbytes = (64 * n + 16 * r.n_spans + pw * r.n_patches + 8 * r.n_inline_rows + 8 * r.n_picked_rows +
+                      pw * r.n_set_patches + 4 * r.n_merge_rows + (4 * n if r.merge_row_base else 0))
+            lib().mq_result_free(rp)
+        for _ in range(batches):
+            t = C.c_void_p()
+            _check(lib().mq_match_spans_submit(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(t)),
+                   "mq_match_spans_submit")
+            pending.append(t)
+            if len(pending) == 2:
+                finish(pending.pop(0))
+        while pending:
+            finish(pending.pop(0))
+        return int(nbytes)
+
     def match_spans_host(self, bytes_, offs, expand=False, block=1024, threads=1):
         """mq_match_spans with its results left in the library's host buffers (the end-to-end
         path: H2D topics, kernels, D2H of the span-format arrays). expand=True also materialises
@@ -430,9 +463,10 @@ class Engine:
         _check(lib().mq_match_spans(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)), "mq_match_spans")
         try:
             r = rp.contents
-            parts = {"topics": 64 * n, "spans": 16 * r.n_spans, "patches": 8 * r.n_patches,
+            pw = 4 if r.flags & SPANS_PATCH_CODES else 8  # (4-byte patch codes)
+            parts = {"topics": 64 * n, "spans": 16 * r.n_spans, "patches": pw * r.n_patches,
                      "inline_rows": 8 * r.n_inline_rows, "picked_rows": 8 * r.n_picked_rows,
-                     "set_patches": 8 * r.n_set_patches, "merge_rows": 4 * r.n_merge_rows,
+                     "set_patches": pw * r.n_set_patches, "merge_rows": 4 * r.n_merge_rows,
                      "merge_row_base": 4 * n if r.merge_row_base else 0}
             self.last_host_bytes = parts  # the result's bytes per array (bench.py's end_to_end)
             nbytes = sum(parts.values())
@@ -651,14 +685,26 @@ def _span_arrays(r, n):
         nbytes = count * np.dtype(dtype).itemsize * (width or 1)
         buf = (C.c_char * nbytes).from_address(ptr)
         return np.frombuffer(buf, dtype).reshape(shape).copy()
+    codes = (int(r.flags) & SPANS_PATCH_CODES) != 0
+
+    def patches(ptr, count, set_rows):
+        if not codes:
+            return arr(ptr, count, np.uint32, 2)
+        # 4-byte patch codes (row << 3 | op): as (row, MQ_PATCH_OP | op), set rows as x << 26 | k
+        c = arr(ptr, count, np.uint32)
+        row = c >> 3
+        if set_rows:
+            row = ((row >> 23) << 26) | (row & ((1 << 23) - 1))
+        return np.stack([row, PATCH_OP | (c & 7)], axis=1).astype(np.uint32) if count else np.zeros((0, 2), np.uint32)
     return {
         "topics": arr(r.topics, n, _TOPIC_SPANS_DT),
         "spans": arr(r.spans, int(r.n_spans), np.uint32, 4),
-        "patches": arr(r.patches, int(r.n_patches), np.uint32, 2),
+        "patches": patches(r.patches, int(r.n_patches), False),
         "inline": arr(r.inline_rows, int(r.n_inline_rows), np.uint32, 2),
         "picked": arr(r.picked_rows, int(r.n_picked_rows), np.uint32, 2),
         "flags": int(r.flags),
-        "set_patches": arr(r.set_patches, int(r.n_set_patches), np.uint32, 2),
+        "patch_codes": codes,
+        "set_patches": patches(r.set_patches, int(r.n_set_patches), True),
         "merge_rows": arr(r.merge_rows, int(r.n_merge_rows), np.uint32),
         "merge_base": arr(r.merge_row_base, n if r.merge_row_base else 0, np.uint32),
     }

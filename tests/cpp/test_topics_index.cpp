@@ -13,6 +13,7 @@
 #include "topics_index.h"
 
 #include <atomic>
+#include <mutex>
 #include <chrono>
 #include <future>
 #include <random>
@@ -346,6 +347,9 @@ static void TestConcurrentReadersAndUpdates() {
   std::atomic<int> bad{0}, late{0};
   std::atomic<long> progress[5];
   std::atomic<long> worst_us{0};
+  std::mutex slow_mu;
+  std::vector<std::pair<long, long>> slow;  // (us, ms since the start) of updates over 2 ms
+  const auto t_start = clk::now();
   for (auto& p : progress) p = 0;
   std::thread watchdog([&] {
     const auto t0 = clk::now();
@@ -383,6 +387,10 @@ static void TestConcurrentReadersAndUpdates() {
         const long us = (long)std::chrono::duration_cast<std::chrono::microseconds>(dt).count();
         for (long w = worst_us.load(); us > w && !worst_us.compare_exchange_weak(w, us);) {
         }
+        if (us > 2000) {
+          std::lock_guard<std::mutex> g(slow_mu);
+          slow.emplace_back(us, (long)std::chrono::duration_cast<std::chrono::milliseconds>(t0 - t_start).count());
+        }
         if (dt > kUpdateDeadline) late++;
       };
       for (int i = 0; i < 400; i++) {
@@ -402,6 +410,10 @@ static void TestConcurrentReadersAndUpdates() {
   watchdog.join();
   std::fprintf(stderr, "  readers matched %ld batches during 3200 updates; slowest update %.1f ms\n",
                progress[0].load() + progress[1].load() + progress[2].load(), worst_us.load() / 1000.0);
+  std::sort(slow.begin(), slow.end(), std::greater<std::pair<long, long>>());
+  std::fprintf(stderr, "  updates over 2 ms: %zu;", slow.size());
+  for (size_t i = 0; i < slow.size() && i < 8; i++) std::fprintf(stderr, " %.1f ms at +%ld ms;", slow[i].first / 1e3, slow[i].second);
+  std::fprintf(stderr, "\n");
   REQUIRE(late == 0);
   REQUIRE(bad == 0);
   for (int k = 0; k < 10; k++) REQUIRE(ix.Subscribers_("s/" + std::to_string(k) + "/x").Subscriptions.size() == 4);
@@ -542,7 +554,11 @@ static void TestBatcherEngineError() {
   n = 0;  // the next batch is matched as usual
   b.Submit("e/c").get().for_each_row([&](const mq_client_row&) { n++; });
   REQUIRE(n == 20);
-  const auto st = b.stats();
+  auto st = b.stats();  // (a batch's stats are recorded just after its tickets complete)
+  for (int i = 0; i < 1000 && st.batches < 3; i++) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    st = b.stats();
+  }
   REQUIRE(st.retried == 2 && st.failed == 1 && st.batches == 3);
 }
 

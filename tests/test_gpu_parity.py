@@ -359,18 +359,21 @@ def test_spans_format_shape(gpu_available):
     assert span_bytes * 4 < rows_bytes  # the point of the format
 
 
-@pytest.mark.parametrize("dedup", [0, 1])
-def test_host_spans_own_and_set_patches(dedup, gpu_available):
+@pytest.mark.parametrize("dedup,codes", [(0, 1), (1, 1), (0, 0), (1, 0)])
+def test_host_spans_own_and_set_patches(dedup, codes, gpu_available):
     """Host span results (mq_match_spans) with merge-set dedup (topics name their set's packed
-    patches through their packed merge rows) and without (every topic's own packed patches):
-    expanded rows equal the oracle's, and the patch arrays are what the mode says."""
+    patches through their packed merge rows) and without (every topic's own packed patches), with
+    4-byte patch codes (MQ_SPANS_PATCH_CODES, the default) and 8-byte patches: expanded rows equal
+    the oracle's, and the patch arrays are what the mode says."""
     from mqmatch import engine as E
     from mqmatch import workload as W
     w, eng, orc = _workload_pair(40000, 3000, seed=71)
     eng.set_option(E.OPT_MERGE_DEDUP, dedup)
+    eng.set_option(E.OPT_PATCH_CODES, codes)
     tb, to = W.gen_topics(w, 4000, seed=72)
     _digest_parity(eng, orc, tb, to, fmts=("spans",))
     a = eng.match_spans(tb, to)
+    assert a["patch_codes"] == bool(codes)
     setf = (a["topics"]["flags"] & 1) != 0
     if dedup:
         assert setf.any() and len(a["set_patches"]) > 0 and len(a["merge_base"]) == len(setf)
@@ -378,6 +381,57 @@ def test_host_spans_own_and_set_patches(dedup, gpu_available):
         assert not setf.any() and len(a["set_patches"]) == 0 and len(a["patches"]) > 0
     tid, prow, _ = E.host_topic_patches(a)
     assert len(tid) == int(a["topics"]["n_patches"].sum()) and (prow < a["topics"]["n_rows"][tid]).all()
+
+
+def test_spans_pipelined_batches(gpu_available):
+    """Pipelined host results (mq_match_spans_submit / _wait, ABI v8): consecutive batches of
+    different sizes (an empty one, small ones, one several times larger than the others, so its
+    buffers are outgrown and it runs again), each waited for after the next is submitted — so a
+    batch's copy into host memory runs while the next batch's kernels write the other stage —
+    expand to the oracle's digests; an update between submits shows in the later batches only."""
+    import ctypes as C
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(40000, 3000, seed=73)
+    sizes = [3000, 0, 500, 12000, 3000, 1]
+    batches = [W.gen_topics(w, k, seed=74 + i) if k else (np.zeros(16, np.uint8), np.zeros(1, np.uint64))
+               for i, k in enumerate(sizes)]
+    want = [orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0] for tb, to in batches]
+
+    def submit(tb, to):
+        t = C.c_void_p()
+        assert E.lib().mq_match_spans_submit(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), len(to) - 1,
+                                             C.byref(t)) == 0
+        return t
+
+    def wait(t, n):
+        rp = C.POINTER(E.SpanResult)()
+        assert E.lib().mq_match_spans_wait(t, C.byref(rp)) == 0
+        return E._expand_host_spans(rp, n)
+
+    for rnd in range(2):  # (the second round: every stage and buffer sized already)
+        pend = []
+        for i, (tb, to) in enumerate(batches):
+            pend.append((i, submit(tb, to)))
+            if len(pend) == 2:
+                j, t = pend.pop(0)
+                dg, _ = engine_digests(wait(t, len(batches[j][1]) - 1))
+                assert (dg == want[j]).all(), (rnd, j)
+        for j, t in pend:
+            dg, _ = engine_digests(wait(t, len(batches[j][1]) - 1))
+            assert (dg == want[j]).all(), (rnd, j)
+    # an update between two submits: the first result is the index before it, the second after
+    tb, to = W.gen_topics(w, 2000, seed=90)
+    t0 = submit(tb, to)
+    before = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0]
+    # (a plain update: mq_subscribe_bulk would wait for t0's result to be freed)
+    assert eng.subscribe("#", 999999, 777, 2, 0, 0) == int(orc.subscribe("c999999", "#", qos=2, client_id=999999,
+                                                                          filter_id=777))
+    after = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0]
+    t1 = submit(tb, to)
+    assert (engine_digests(wait(t0, 2000))[0] == before).all()
+    assert (engine_digests(wait(t1, 2000))[0] == after).all()
+    assert not (before == after).all()
 
 
 def test_spans_device_matches_host(gpu_available):
@@ -414,11 +468,15 @@ def test_spans_device_matches_host(gpu_available):
     assert (dsp[E._ranges(sb, ns)] == host["spans"]).all()
 
 
-@pytest.mark.parametrize("exp,waves", [(16, 8), (32, 8), (64, 8), (0, 7), (0, 6)])  # bits 5 / 6: 3 / 4 links
+@pytest.mark.parametrize("exp,waves", [(0, 8), (16 | 128, 8), (32 | 128, 8), (64 | 128, 8), (0, 7), (0, 6),
+                                       (128, 8), (256, 8)])
 def test_set_pass_variants_exact(exp, waves, gpu_available):
-    """The merge set pass's exact variants: MQ_OPT_SET_EXP bit 4 (a visit through a partner other
-    than the record's first reads all its links), bits 5 / 6 (3 / 4 partner links per batch), and
-    7 or 6 waves per SIMD (MQ_OPT_MERGE_WAVES): per-topic digests of device results equal the oracle's."""
+    """The merge set pass's exact variants: the fold (default: records folded over their visits, no
+    partner links), bit 7 (records resolved through their partner links), with bit 4 (a visit
+    through a partner other than the record's first reads all its links) or bits 5 / 6 (3 / 4
+    partner links per batch); bit 8 (fold chunks of 16 visits: many chunks per set, and merge
+    gathers beyond a chunk resolved through the links); 7 or 6 waves per SIMD
+    (MQ_OPT_MERGE_WAVES): per-topic digests of device results equal the oracle's."""
     import torch
     from mqmatch import engine as E
     from mqmatch import workload as W
@@ -533,6 +591,46 @@ def test_walk_trials_choose_and_stay_exact(gpu_available):
         dg, _ = engine_digests(E.expand_device_spans(r, n))
         assert (dg == od).all()
     prof = eng.profile_read()
+    assert "trial_frontier_ps_per_topic" in prof and "trial_thread_ps_per_topic" in prof, sorted(prof)
+
+
+def test_walk_trials_rearm_on_wildcard_mix(gpu_available):
+    """The walk trials run again when the index's wildcard mix moves without its size doubling:
+    an exact-match (IoT) index runs its trials, then wildcard-heavy subscriptions join (the share
+    of '+' / '#' particles rises well past a quarter of itself), and the next batches time both
+    walks again; every batch equals the oracle."""
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(30000, 30000, seed=91, mix=W.MIX_IOT)
+    eng, orc = E.Engine(), O.OracleIndex()
+    assert (eng.subscribe_bulk(w) == orc.subscribe_bulk(w)).all()
+    w2 = W.gen_subscriptions(6000, 600, seed=92)  # (the mqtt mix: wildcard-heavy)
+
+    def batches(wt, seed, k):
+        tb, to = W.gen_topics(wt, 70000, seed=seed)
+        n = len(to) - 1
+        d_tb = torch.from_numpy(tb).cuda()
+        d_to = torch.from_numpy(to.view(np.int64)).cuda()
+        od, _, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+        eng.profile(True)
+        eng.profile_reset()
+        for _ in range(k):
+            torch.cuda.synchronize()
+            r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
+            dg, _ = engine_digests(E.expand_device_spans(r, n))
+            assert (dg == od).all()
+        return eng.profile_read()
+
+    prof = batches(w, 93, 3)
+    assert "trial_frontier_ps_per_topic" in prof and "trial_thread_ps_per_topic" in prof, sorted(prof)
+    prof = batches(w, 94, 2)
+    assert "trial_frontier_ps_per_topic" not in prof  # same index: the choice stays
+    nodes0 = eng.stats().get("nodes")
+    assert (eng.subscribe_bulk(w2) == orc.subscribe_bulk(w2)).all()
+    nodes1 = eng.stats().get("nodes")
+    assert nodes0 is None or nodes1 < 2 * nodes0  # (not a new size: a new mix)
+    prof = batches(w2, 95, 3)
     assert "trial_frontier_ps_per_topic" in prof and "trial_thread_ps_per_topic" in prof, sorted(prof)
 
 
