@@ -139,6 +139,11 @@ int mq_subscribe_bulk(mq_index* idx, const uint8_t* filter_bytes, const uint64_t
                       const uint8_t* flags, const int32_t* identifiers, uint64_t n,
                       uint8_t* out_new);
 
+/* Columnar Unsubscribe (topics.go:423-448) of n (filter, client) pairs, in order, under one
+ * lock: out_existed[i] (nullable) = what mq_unsubscribe would return for pair i. */
+int mq_unsubscribe_bulk(mq_index* idx, const uint8_t* filter_bytes, const uint64_t* offsets,
+                        const uint32_t* client_ids, uint64_t n, uint8_t* out_existed);
+
 /* Columnar bulk RetainMessage with payload (server.go:1688-1692). */
 int mq_retain_bulk(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets,
                    const uint64_t* handles, uint64_t n);

@@ -257,6 +257,19 @@ int mq_subscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs,
   }, Access::kDrain);
 }
 
+int mq_unsubscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint32_t* client_ids,
+                        uint64_t n, uint8_t* out_existed) {
+  if (n && (!bytes || !offs || !client_ids)) return fail(MQ_EINVAL, "null column");
+  return guarded(idx, [&] {
+    for (uint64_t i = 0; i < n; i++) {
+      const int r = idx->ix->unsubscribe(std::string_view((const char*)bytes + offs[i], offs[i + 1] - offs[i]),
+                                         client_ids[i]);
+      if (out_existed) out_existed[i] = (uint8_t)r;
+    }
+    return 0;
+  }, Access::kUpdate);
+}
+
 int mq_retain_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint64_t* handles,
                    uint64_t n) {
   if (n && (!bytes || !offs || !handles)) return fail(MQ_EINVAL, "null column");

@@ -654,7 +654,146 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       }
     }
   };
-  if (WIDE) {  // wavefront per exported item: its particles, lane by lane (dfs_run)
+  // A literal segment under a run of several particles: the level-synchronous fan-out from the run
+  // [fa, fbnd) at segment fs. The frontier is a list of runs [x, y) of one level, in LDS; every lane
+  // takes particles of the same level, so a literal level's lookups are issued together with one
+  // key for the wave, a '+' maps each run to its children's run, and a final '+' / '#' emits each
+  // run. A frontier that outgrows its LDS falls back, run by run, to the per-lane walk (dfs_run:
+  // lanes take a run's particles, each walks the rest of the filter alone with deeper fan-outs on
+  // a frame stack). The filter's own count pass may export the fan-out to work items (MsgWide)
+  // instead; an item runs the same fan-out from its run (the wide modes).
+  bool exported = false;  // the count pass handed the filter's fan-out to work items (MsgWide)
+  auto fan_out = [&](uint32_t fa, uint32_t fbnd, uint64_t fs) __attribute__((always_inline)) {
+    uint2* cur = mfront[wv][0];
+    uint2* nxt = mfront[wv][1];
+    uint32_t nr = 1;
+    wave_sync_lds();  // (the frontier's LDS is free)
+    if (lane == 0) cur[0] = make_uint2(fa, fbnd);
+    wave_sync_lds();
+    uint64_t ls = fs;  // the segment the frontier's runs take next
+    for (uint32_t guard = 0; guard < 4096; guard++) {
+      const uint64_t e = find_slash(R, ls, b1);
+      const bool last = e >= b1;
+      const uint32_t len = (uint32_t)(e - ls);
+      const uint32_t c0 = len == 1 ? R.at(ls) : 0u;
+      uint32_t nn = 0;  // the next frontier's runs (wave-uniform)
+      if (c0 == '+' || c0 == '#') {
+        for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+          const uint32_t r = r0 + lane;
+          uint32_t x = 0, y = 0;
+          if (r < nr) {
+            const uint2 ru = cur[r];
+            desc(ru.x, ru.y, x, y);
+          }
+          if (last) {
+            if (r < nr) emit_final(c0 == '#', x, y);
+            continue;
+          }
+          const bool keep = r < nr && x < y;
+          const uint64_t bk = __ballot(keep);
+          const uint32_t at = nn + prefix_before(bk);
+          if (keep && at < kMsgFront) nxt[at] = make_uint2(x, y);
+          nn += (uint32_t)__popcll(bk);
+        }
+      } else {
+        // literal: every particle of every run looks the segment up; particle p of the
+        // frontier is found through the runs' prefix sums
+        const SegKey key = key_of(R, ls, e);
+        uint32_t tot = 0;
+        for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+          const uint32_t r = r0 + lane;
+          const uint32_t v = r < nr ? cur[r].y - cur[r].x : 0u;
+          uint32_t ct;
+          const uint32_t ex = wave_excl_scan(v, lane, &ct);
+          if (r < nr) mpre[wv][r] = tot + ex;
+          tot += ct;
+        }
+        if (lane == 0) mpre[wv][nr] = tot;
+        if (!FILL && img.work && lane == 0) atomicAdd(img.work + 0, (unsigned long long)tot);
+        wave_sync_lds();
+        if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && tot > w.min_tot) {
+          if (FILL) {  // the count pass exported from here: its items write the rest
+            if (cnt[t].shared) break;
+          } else {
+            // the runs as items of at most kMsgChunk particles (one reservation for all)
+            uint32_t nit = 0;
+            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+              const uint32_t r = r0 + lane;
+              const uint32_t c = r < nr ? (cur[r].y - cur[r].x + kMsgChunk - 1) / kMsgChunk : 0u;
+              nit += wave_sum(c);
+            }
+            uint32_t ib = 0;
+            if (lane == 0) ib = atomicAdd(w.n_items, nit);
+            ib = __shfl(ib, 0, 64);
+            if (ib + nit <= w.cap) {
+              for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
+                const uint32_t r = r0 + lane;
+                uint32_t x = 0, y = 0;
+                if (r < nr) {
+                  x = cur[r].x;
+                  y = cur[r].y;
+                }
+                const uint32_t c = (y - x + kMsgChunk - 1) / kMsgChunk;
+                uint32_t ct;
+                const uint32_t ex = wave_excl_scan(c, lane, &ct);
+                for (uint32_t k = 0; k < c; k++)
+                  w.items[ib + ex + k] = MsgWork{t, x + k * kMsgChunk, (uint32_t)min((uint32_t)y, (uint32_t)(x + (k + 1) * kMsgChunk)),
+                                                 (uint32_t)(ls - b0), 0u, 0u, 0u, kNone};
+                ib += ct;
+              }
+              exported = true;
+              break;
+            }  // (the queue is full: this filter walks alone, as a fill walk will)
+          }
+        }
+        for (uint32_t p0 = 0; p0 < tot; p0 += 64) {
+          const uint32_t p = p0 + lane;
+          uint32_t qc = kNone;
+          if (p < tot) {
+            uint32_t lo = 0, hi = nr;  // mpre[lo] <= p < mpre[hi]
+            while (hi - lo > 1) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (mpre[wv][mid] <= p) lo = mid;
+              else hi = mid;
+            }
+            const uint32_t u = cur[lo].x + (p - mpre[wv][lo]);
+            qc = img_pos(img, lookup(ix, img.node[u], key, fb + ls, len));
+          }
+          if (last) {
+            if (qc != kNone) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
+            continue;
+          }
+          const bool keep = qc != kNone;
+          const uint64_t bk = __ballot(keep);
+          const uint32_t at = nn + prefix_before(bk);
+          if (keep && at < kMsgFront) nxt[at] = make_uint2(qc, qc + 1);
+          nn += (uint32_t)__popcll(bk);
+        }
+      }
+      if (last) break;
+      if (nn > kMsgFront) {  // too wide for LDS: the per-lane walk from this level
+        if (!FILL && img.work && lane == 0) {
+          uint32_t np = 0;
+          for (uint32_t r = 0; r < nr; r++) np += cur[r].y - cur[r].x;
+          atomicAdd(img.work + 1, 1ull);
+          atomicAdd(img.work + 2, (unsigned long long)np);
+        }
+        for (uint32_t r = 0; r < nr; r++) {
+          const uint2 ru = cur[r];
+          dfs_run(ru.x, ru.y, ls);
+        }
+        break;
+      }
+      wave_sync_lds();  // the next frontier is complete; the current one is free
+      uint2* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+      nr = nn;
+      ls = e + 1;
+      if (nr == 0) break;
+    }
+  };
+  if (WIDE) {  // wavefront per exported item: its run, level-synchronous (fan_out)
     const uint32_t ni = min(*w.n_items, w.cap);
     const uint32_t wbase = (blockIdx.x * 4 + wv) * w.per_wave;  // (wide count: this wavefront's scratch)
     for (uint32_t i = blockIdx.x * 4 + wv; i < ni; i += gridDim.x * 4) {
@@ -688,7 +827,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         pbase = off[t].g;
       }
       wave_sync_lds();
-      dfs_run(it.x, it.y, b0 + it.s);
+      fan_out(it.x, it.y, b0 + it.s);
       wave_sync_lds();
       if (!FILL && lane == 0) {  // the item's place in its filter's output: after the count pass's own part
         const uint32_t r1 = rcur[wv];
@@ -700,7 +839,6 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
     }
     return;
   }
-  bool exported = false;  // the count pass handed the filter's fan-out to work items (MsgWide)
   if (b1 > b0 && ix.retained_len != 0) {  // topics.go:535
     bool wild = false;
     for (uint64_t i = b0 + lane; i < b1; i += 64) {
@@ -759,142 +897,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         b = qc + 1;
         s = e + 1;
       }
-      if (fan) {
-        // A literal segment under a run of several particles. Level-synchronous fan-out: the
-        // frontier is a list of runs [x, y) of one level, in LDS; every lane takes particles of
-        // the same level, so a literal level's lookups are issued together with one key for the
-        // wave, a '+' maps each run to its children's run, and a final '+' / '#' emits each run.
-        // A frontier that outgrows its LDS falls back, run by run, to the per-lane walk
-        // (dfs_run: lanes take a run's particles, each walks the rest of the filter alone with
-        // deeper fan-outs on a frame stack).
-        uint2* cur = mfront[wv][0];
-        uint2* nxt = mfront[wv][1];
-        uint32_t nr = 1;
-        if (lane == 0) cur[0] = make_uint2(a, b);
-        wave_sync_lds();
-        uint64_t ls = s;  // the segment the frontier's runs take next
-        for (uint32_t guard = 0; guard < 4096; guard++) {
-          const uint64_t e = find_slash(R, ls, b1);
-          const bool last = e >= b1;
-          const uint32_t len = (uint32_t)(e - ls);
-          const uint32_t c0 = len == 1 ? R.at(ls) : 0u;
-          uint32_t nn = 0;  // the next frontier's runs (wave-uniform)
-          if (c0 == '+' || c0 == '#') {
-            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-              const uint32_t r = r0 + lane;
-              uint32_t x = 0, y = 0;
-              if (r < nr) {
-                const uint2 ru = cur[r];
-                desc(ru.x, ru.y, x, y);
-              }
-              if (last) {
-                if (r < nr) emit_final(c0 == '#', x, y);
-                continue;
-              }
-              const bool keep = r < nr && x < y;
-              const uint64_t bk = __ballot(keep);
-              const uint32_t at = nn + prefix_before(bk);
-              if (keep && at < kMsgFront) nxt[at] = make_uint2(x, y);
-              nn += (uint32_t)__popcll(bk);
-            }
-          } else {
-            // literal: every particle of every run looks the segment up; particle p of the
-            // frontier is found through the runs' prefix sums
-            const SegKey key = key_of(R, ls, e);
-            uint32_t tot = 0;
-            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-              const uint32_t r = r0 + lane;
-              const uint32_t v = r < nr ? cur[r].y - cur[r].x : 0u;
-              uint32_t ct;
-              const uint32_t ex = wave_excl_scan(v, lane, &ct);
-              if (r < nr) mpre[wv][r] = tot + ex;
-              tot += ct;
-            }
-            if (lane == 0) mpre[wv][nr] = tot;
-            if (!FILL && img.work && lane == 0) atomicAdd(img.work + 0, (unsigned long long)tot);
-            wave_sync_lds();
-            if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && tot > w.min_tot) {
-              if (FILL) {  // the count pass exported from here: its items write the rest
-                if (cnt[t].shared) break;
-              } else {
-                // the runs as items of at most kMsgChunk particles (one reservation for all)
-                uint32_t nit = 0;
-                for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-                  const uint32_t r = r0 + lane;
-                  const uint32_t c = r < nr ? (cur[r].y - cur[r].x + kMsgChunk - 1) / kMsgChunk : 0u;
-                  nit += wave_sum(c);
-                }
-                uint32_t ib = 0;
-                if (lane == 0) ib = atomicAdd(w.n_items, nit);
-                ib = __shfl(ib, 0, 64);
-                if (ib + nit <= w.cap) {
-                  for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-                    const uint32_t r = r0 + lane;
-                    uint32_t x = 0, y = 0;
-                    if (r < nr) {
-                      x = cur[r].x;
-                      y = cur[r].y;
-                    }
-                    const uint32_t c = (y - x + kMsgChunk - 1) / kMsgChunk;
-                    uint32_t ct;
-                    const uint32_t ex = wave_excl_scan(c, lane, &ct);
-                    for (uint32_t k = 0; k < c; k++)
-                      w.items[ib + ex + k] = MsgWork{t, x + k * kMsgChunk, min(y, x + (k + 1) * kMsgChunk),
-                                                     (uint32_t)(ls - b0), 0u, 0u, 0u, kNone};
-                    ib += ct;
-                  }
-                  exported = true;
-                  break;
-                }  // (the queue is full: this filter walks alone, as a fill walk will)
-              }
-            }
-            for (uint32_t p0 = 0; p0 < tot; p0 += 64) {
-              const uint32_t p = p0 + lane;
-              uint32_t qc = kNone;
-              if (p < tot) {
-                uint32_t lo = 0, hi = nr;  // mpre[lo] <= p < mpre[hi]
-                while (hi - lo > 1) {
-                  const uint32_t mid = (lo + hi) >> 1;
-                  if (mpre[wv][mid] <= p) lo = mid;
-                  else hi = mid;
-                }
-                const uint32_t u = cur[lo].x + (p - mpre[wv][lo]);
-                qc = img_pos(img, lookup(ix, img.node[u], key, fb + ls, len));
-              }
-              if (last) {
-                if (qc != kNone) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
-                continue;
-              }
-              const bool keep = qc != kNone;
-              const uint64_t bk = __ballot(keep);
-              const uint32_t at = nn + prefix_before(bk);
-              if (keep && at < kMsgFront) nxt[at] = make_uint2(qc, qc + 1);
-              nn += (uint32_t)__popcll(bk);
-            }
-          }
-          if (last) break;
-          if (nn > kMsgFront) {  // too wide for LDS: the per-lane walk from this level
-            if (!FILL && img.work && lane == 0) {
-              uint32_t np = 0;
-              for (uint32_t r = 0; r < nr; r++) np += cur[r].y - cur[r].x;
-              atomicAdd(img.work + 1, 1ull);
-              atomicAdd(img.work + 2, (unsigned long long)np);
-            }
-            for (uint32_t r = 0; r < nr; r++) {
-              const uint2 ru = cur[r];
-              dfs_run(ru.x, ru.y, ls);
-            }
-            break;
-          }
-          wave_sync_lds();  // the next frontier is complete; the current one is free
-          uint2* tmp = cur;
-          cur = nxt;
-          nxt = tmp;
-          nr = nn;
-          ls = e + 1;
-          if (nr == 0) break;
-        }
-      }
+      if (fan) fan_out(a, b, s);
     }
   }
   if (!FILL) {

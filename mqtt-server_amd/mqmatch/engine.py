@@ -116,6 +116,7 @@ EXPORTS = [
     "mq_acl_match_batch", "mq_select_shared_device", "mq_match_spans", "mq_match_spans_device",
     "mq_spans_expand", "mq_set_option", "mq_match_spans_begin", "mq_match_spans_end",
     "mq_match_spans_end_host", "mq_device_check", "mq_match_spans_submit", "mq_match_spans_wait",
+    "mq_unsubscribe_bulk",
 ]
 
 CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
@@ -159,6 +160,7 @@ def lib():
         "mq_subscribe_bulk": (C.c_int, [vp, _u8p, _u64p, _u32p, _u32p, _u8p, _u8p, _i32p,
                                         C.c_uint64, _u8p]),
         "mq_retain_bulk": (C.c_int, [vp, _u8p, _u64p, _u64p, C.c_uint64]),
+        "mq_unsubscribe_bulk": (C.c_int, [vp, _u8p, _u64p, _u32p, C.c_uint64, _u8p]),
         "mq_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MatchResult))]),
         "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
         "mq_match_spans": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(SpanResult))]),
@@ -370,6 +372,14 @@ class Engine:
                                        _p(w["qos"], _u8p), _p(w["flags"], _u8p),
                                        _p(w["idents"], _i32p), n, _p(out, _u8p)),
                "mq_subscribe_bulk")
+        return out[:n]
+
+    def unsubscribe_bulk(self, bytes_, offs, client_ids):
+        """mq_unsubscribe_bulk: per pair, whether the filter's particle existed (as unsubscribe)."""
+        n = len(offs) - 1
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(lib().mq_unsubscribe_bulk(self.h, _p(bytes_, _u8p), _p(offs, _u64p), _p(client_ids, _u32p), n,
+                                         _p(out, _u8p)), "mq_unsubscribe_bulk")
         return out[:n]
 
     def retain_bulk(self, bytes_, offs, handles):

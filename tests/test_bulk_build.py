@@ -85,6 +85,27 @@ def test_bulk_image_takes_updates():
     b.check()
 
 
+def test_bulk_unsubscribe_equals_per_entry():
+    """mq_unsubscribe_bulk answers exactly as mq_unsubscribe, in order (repeats, unknown clients,
+    filters never subscribed), and leaves the same image."""
+    ents = _entries(21, 6000)
+    w = _pack(ents)
+    (a, _), (b, _) = _pair(w)
+    r = random.Random(22)
+    pairs = [(f, c) for f, c, _, _, _ in r.sample(ents, 2500)] + [("no/such/filter", 1), (ents[3][0], 999)]
+    pairs += pairs[:100]  # (already removed: false, the particle may be gone)
+    bs = [f.encode() for f, _ in pairs]
+    offs = np.zeros(len(bs) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in bs])
+    got = a.unsubscribe_bulk(np.frombuffer(b"".join(bs), np.uint8).copy(), offs,
+                             np.array([c for _, c in pairs], np.uint32))
+    want = [b.unsubscribe(f, c) for f, c in pairs]
+    assert got.tolist() == want
+    assert a.stats() == b.stats()
+    a.check()
+    b.check()
+
+
 def _retained(seed, n):
     r = random.Random(seed)
     ts = ["/".join(r.choice(["a", "b", "c", "", "x", "$SYS", "dev"]) for _ in range(r.randint(1, 6)))

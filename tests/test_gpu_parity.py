@@ -424,9 +424,13 @@ def test_spans_pipelined_batches(gpu_available):
     tb, to = W.gen_topics(w, 2000, seed=90)
     t0 = submit(tb, to)
     before = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0]
-    # (a plain update: mq_subscribe_bulk would wait for t0's result to be freed)
-    assert eng.subscribe("#", 999999, 777, 2, 0, 0) == int(orc.subscribe("c999999", "#", qos=2, client_id=999999,
-                                                                          filter_id=777))
+    # (a plain update: mq_subscribe_bulk would wait for t0's result to be freed). A new client on
+    # the root '#' list every topic gathers (its filter id is the workload's id of "#": ids name
+    # filter strings)
+    offs = w["offs"].astype(np.int64)
+    fid = next(int(w["filter_ids"][i]) for i in range(len(offs) - 1) if bytes(w["bytes"][offs[i]:offs[i + 1]]) == b"#")
+    assert eng.subscribe("#", 999999, fid, 2, 0, 0) == int(orc.subscribe("c999999", "#", qos=2, client_id=999999,
+                                                                          filter_id=fid))
     after = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0]
     t1 = submit(tb, to)
     assert (engine_digests(wait(t0, 2000))[0] == before).all()
@@ -465,7 +469,9 @@ def test_spans_device_matches_host(gpu_available):
     dsp = torch.empty(ext * 4, dtype=torch.int32, device="cuda")
     assert hip.hipMemcpy(dsp.data_ptr(), r.spans, ext * 16, 3) == 0
     dsp = dsp.cpu().numpy().view(np.uint32).reshape(-1, 4)
-    assert (dsp[E._ranges(sb, ns)] == host["spans"]).all()
+    ht = host["topics"]  # (host spans are packed, each topic's run at its span_base, in no set order)
+    hsp = host["spans"][E._ranges(ht["span_base"].astype(np.int64), ht["n_spans"].astype(np.int64))]
+    assert (dsp[E._ranges(sb, ns)] == hsp).all()
 
 
 @pytest.mark.parametrize("exp,waves", [(0, 8), (16 | 128, 8), (32 | 128, 8), (64 | 128, 8), (0, 7), (0, 6),

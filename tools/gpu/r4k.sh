@@ -6,7 +6,7 @@ D=$R/gpurun_out/${1:-r4k}
 mkdir -p $D
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $D/smoke.log; exit 1; }
 tail -1 $D/smoke.log
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shard.py -x -q --timeout 170 --timeout-method thread -k "pipelined or host or trials or set_pass or digest_parity or many_merging or partner_map or long_lists or random_small or incremental or shard or survives or spans" > $D/pytest.log 2>&1 || { echo "pytest rc=$?"; tail -40 $D/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shard.py -x -q --timeout 170 --timeout-method thread -k "messages or pipelined or host or trials or set_pass or digest_parity or many_merging or partner_map or long_lists or random_small or incremental or shard or survives or spans" > $D/pytest.log 2>&1 || { echo "pytest rc=$?"; tail -40 $D/pytest.log; exit 1; }
 tail -2 $D/pytest.log
 timeout -k 10 300 ./mqtt-server_amd/build/test_topics_index > $D/cpp.log 2>&1 || { echo "cpp rc=$?"; grep -E "slowest|over 2 ms|REQUIRE|failed" $D/cpp.log; exit 1; }
 grep -E "slowest|over 2 ms|passed|FAIL" $D/cpp.log
@@ -20,3 +20,8 @@ print('$v', round(d['value']/1e6,1), 'M/s', round(d['ms_per_step'],3), 'ms', {k:
 "
   if [ $v = fold ]; then unset MQ_ENGINE_OPTIONS; break_links=0; fi
 done
+timeout -k 10 400 python -u bench_messages.py --retained 10000000 > $D/msg_10m.json 2> $D/msg_10m.err || { echo "msg rc=$?"; tail -5 $D/msg_10m.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('$D/msg_10m.json'))
+print('msg10m', round(d['value']/1e6,1), 'M filters/s', round(d['ms_per_step'],3), 'ms', {k: round(v,3) for k,v in d['kernels_ms_per_step'].items()}, d.get('parity_sample'))
+"
