@@ -38,6 +38,7 @@ using namespace mq;
 struct IndexLock {
   std::mutex mu;
   ViewTracker views;
+  Device* dev = nullptr;  // the index's device, while it lives (pipelined results flush through it)
 };
 
 struct mq_index {
@@ -52,6 +53,7 @@ struct mq_index {
   Device& device() {
     if (!dev) {
       dev.reset(new Device(cfg.device));
+      lk->dev = dev.get();
       dev->prof.enable(profile != 0, (profile & MQ_PROF_WORK) != 0);
       dev->set_select_shared((cfg.flags & MQ_CFG_SELECT_SHARED) != 0);
       for (auto& o : options) dev->set_option(o.first, o.second);
@@ -186,7 +188,14 @@ int mq_index_create(const mq_config* cfg, mq_index** out) {
   }
 }
 
-void mq_index_destroy(mq_index* idx) { delete idx; }
+void mq_index_destroy(mq_index* idx) {
+  if (!idx) return;
+  {
+    std::lock_guard<std::mutex> g(idx->lk->mu);
+    idx->lk->dev = nullptr;  // (tickets still held flush through it no more; ~Device issues their copies)
+  }
+  delete idx;
+}
 
 int mq_subscribe(mq_index* idx, const char* filter, uint32_t flen, uint32_t client_id,
                  uint32_t filter_id, uint8_t qos, uint8_t flags, int32_t identifier) {
@@ -371,6 +380,7 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
 struct mq_spans_ticket {
   mq_span_result* res = nullptr;
   hipEvent_t ready = nullptr;
+  std::shared_ptr<IndexLock> lk;  // the index's lock (its device issues the pending copy)
 };
 
 int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_spans_ticket** out) {
@@ -390,9 +400,11 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
     const uint8_t* dtb = nullptr;
     const uint64_t* dto = nullptr;
     hipStream_t hs = d.host_stream();
-    if (n) d.stage_inputs(tb, to, n, hs, &dtb, &dto);
+    if (n) d.stage_inputs(tb, to, n, hs, &dtb, &dto);  // (ahead of the last batch's copy: below)
+    d.flush_host_copy();
     mq_span_result dev_out;
     d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out, tk->ready);
+    tk->lk = idx->lk;
     const int rc = publish_host_spans(idx, std::move(h), dev_out, &tk->res);
     if (rc) return rc;
     eg.t = nullptr;
@@ -404,6 +416,17 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
 int mq_match_spans_wait(mq_spans_ticket* t, mq_span_result** out) {
   if (!t || !out) return fail(MQ_EINVAL, "null argument");
   *out = nullptr;
+  if (t->lk) {  // the copy may still be pending (queued behind a next batch's upload)
+    std::lock_guard<std::mutex> g(t->lk->mu);
+    try {
+      if (t->lk->dev) t->lk->dev->flush_host_copy();
+    } catch (const HipError& he) {
+      (void)hipEventDestroy(t->ready);
+      mq_result_free(t->res);
+      delete t;
+      return fail(MQ_EIO, he.where);
+    }
+  }
   const hipError_t e = hipEventSynchronize(t->ready);
   (void)hipEventDestroy(t->ready);
   mq_span_result* r = t->res;

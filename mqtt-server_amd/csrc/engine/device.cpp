@@ -281,6 +281,10 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
 // body with the device still selected); streams, events and pinned host blocks are freed here.
 Device::~Device() {
   (void)hipSetDevice(dev_);
+  try {
+    flush_host_copy();  // a pipelined result still waiting for its copy gets it
+  } catch (...) {
+  }
   (void)hipDeviceSynchronize();  // no kernel of this index still reads a buffer freed below
   if (stage_done_) (void)hipEventDestroy(stage_done_);
   pinned_free(h_stage_, h_stage_bytes_);
@@ -508,6 +512,36 @@ hipStream_t Device::host_stream() {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   if (!hstream_) hip_check(hipStreamCreateWithFlags(&hstream_, hipStreamNonBlocking), "hipStreamCreate");
   return hstream_;
+}
+
+void Device::issue_host_copy(const PendingCopy& c) {
+  HostStage* hs = c.hs;
+  HostSpans* host = c.host;
+  hip_check(hipStreamWaitEvent(hcopy_, hs->packed, 0), "hipStreamWaitEvent");
+  const size_t pw = c.codes ? sizeof(uint32_t) : sizeof(PatchRec);  // bytes per patch
+  auto d2h = [&](void* dst, const DevBuf& src, size_t bytes) {
+    if (bytes) hip_check(hipMemcpyAsync(dst, src.p, bytes, hipMemcpyDeviceToHost, hcopy_), "D2H");
+  };
+  d2h(host->topics.data(), hs->topics, (size_t)c.n * sizeof(TopicSpansDev));
+  d2h(host->spans.data(), hs->spans, c.spans * sizeof(SpanRec));
+  d2h(c.codes ? (void*)host->patch_codes.data() : (void*)host->patches.data(), hs->patches, c.patches * pw);
+  d2h(host->inl.data(), hs->inl, c.inl * sizeof(InlRec));
+  d2h(host->picked.data(), hs->picked, c.picked * sizeof(ShrRec));
+  if (c.dedup) {  // the sets' written patches and the merge rows (packed by k_set_pack, k_mrow_pack)
+    d2h(c.codes ? (void*)host->set_codes.data() : (void*)host->set_patches.data(), hs->set_patches, c.set * pw);
+    d2h(host->merge_rows.data(), hs->merge_rows, c.mrows * sizeof(uint32_t));
+    d2h(host->merge_base.data(), hs->merge_base, (size_t)c.n * sizeof(uint32_t));
+  }
+  hip_check(hipEventRecord(hs->copied, hcopy_), "hipEventRecord");
+  if (c.ready) hip_check(hipEventRecord(c.ready, hcopy_), "hipEventRecord");
+}
+
+void Device::flush_host_copy() {
+  if (!pc_.on) return;
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  const PendingCopy c = pc_;
+  pc_.on = false;
+  issue_host_copy(c);
 }
 
 void Device::ensure_hcopy() {
@@ -972,6 +1006,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
 void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                          mq_xlist* x, bool one_sync) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
+  flush_host_copy();  // (a pipelined batch's copy: before this batch reuses any stage)
   sync(ix, s);
   memset(x, 0, sizeof(*x));
   x->n_topics = n;
@@ -1611,37 +1646,41 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
                                hipMemcpyDeviceToDevice, s), "D2D");
     }
     hip_check(hipEventRecord(hs->packed, s), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(hcopy_, hs->packed, 0), "hipStreamWaitEvent");
-    const uint64_t n_set = sb_.dedup ? *h_stot : 0, n_mrows = sb_.dedup ? *h_mrtot : 0;
-    const size_t pw = codes ? sizeof(uint32_t) : sizeof(PatchRec);  // bytes per patch
+    PendingCopy c;
+    c.on = true;
+    c.hs = hs;
+    c.host = host;
+    c.n = n;
+    c.spans = tot.g;
+    c.patches = n_patches;
+    c.inl = tot.inl;
+    c.picked = out->n_picked_rows;
+    c.dedup = sb_.dedup;
+    c.codes = codes;
+    c.set = sb_.dedup ? *h_stot : 0;
+    c.mrows = sb_.dedup ? *h_mrtot : 0;
+    c.ready = ready;
+    // the result's host arrays exist now (the caller publishes them); the copy fills them
     host->topics.resize(n);
-    host->spans.resize(tot.g);
-    if (codes) host->patch_codes.resize(n_patches);
-    else host->patches.resize(n_patches);
-    host->inl.resize(tot.inl);
-    host->picked.resize(out->n_picked_rows);
-    auto d2h = [&](void* dst, const DevBuf& src, size_t bytes) {
-      if (bytes) hip_check(hipMemcpyAsync(dst, src.p, bytes, hipMemcpyDeviceToHost, hcopy_), "D2H");
-    };
-    d2h(host->topics.data(), hs->topics, n * sizeof(TopicSpansDev));
-    d2h(host->spans.data(), hs->spans, tot.g * sizeof(SpanRec));
-    d2h(codes ? (void*)host->patch_codes.data() : (void*)host->patches.data(), hs->patches, n_patches * pw);
-    d2h(host->inl.data(), hs->inl, tot.inl * sizeof(InlRec));
-    d2h(host->picked.data(), hs->picked, out->n_picked_rows * sizeof(ShrRec));
-    if (sb_.dedup) {  // the sets' written patches and the merge rows (packed by k_set_pack, k_mrow_pack)
-      if (codes) host->set_codes.resize(n_set);
-      else host->set_patches.resize(n_set);
-      host->merge_rows.resize(n_mrows);
+    host->spans.resize(c.spans);
+    if (codes) host->patch_codes.resize(c.patches);
+    else host->patches.resize(c.patches);
+    host->inl.resize(c.inl);
+    host->picked.resize(c.picked);
+    if (c.dedup) {
+      if (codes) host->set_codes.resize(c.set);
+      else host->set_patches.resize(c.set);
+      host->merge_rows.resize(c.mrows);
       host->merge_base.resize(n);
-      d2h(codes ? (void*)host->set_codes.data() : (void*)host->set_patches.data(), hs->set_patches, n_set * pw);
-      d2h(host->merge_rows.data(), hs->merge_rows, n_mrows * sizeof(uint32_t));
-      d2h(host->merge_base.data(), hs->merge_base, n * sizeof(uint32_t));
     }
-    hip_check(hipEventRecord(hs->copied, hcopy_), "hipEventRecord");
     hs->used = true;
     hpar_ ^= 1u;
-    if (ready) hip_check(hipEventRecord(ready, hcopy_), "hipEventRecord");
-    else hip_check(hipStreamSynchronize(hcopy_), "hipStreamSynchronize(copy)");
+    if (ready) {
+      pc_ = c;  // pipelined: issued behind the next batch's upload (flush_host_copy)
+    } else {
+      issue_host_copy(c);
+      hip_check(hipStreamSynchronize(hcopy_), "hipStreamSynchronize(copy)");
+    }
   } else if (ready) {
     hip_check(hipEventRecord(ready, s), "hipEventRecord");
   }

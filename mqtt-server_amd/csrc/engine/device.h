@@ -197,6 +197,10 @@ class Device {
   // it the call returns after the copy.
   void match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                    HostSpans* host, mq_span_result* out, hipEvent_t ready = nullptr);
+  // Issue the pipelined host batch's copy that is still pending (match_spans with `ready` defers
+  // it until the next batch's inputs are staged, or its result is waited for). Under the handle
+  // lock.
+  void flush_host_copy();
   // The same in two phases, for a sharded index: begin walks the batch and
   // exports the topics' gathered cross-shard nodes (device pointers in *x, valid until end);
   // the caller exchanges the lists between the shards; end merges with the other shards' lists.
@@ -321,6 +325,19 @@ class Device {
   };
   HostStage hst_[2];
   uint32_t hpar_ = 0;              // the stage of the next host batch
+  // A pipelined host batch's copy, not yet issued (flush_host_copy): it is queued behind the next
+  // batch's input upload, so that upload does not wait for the copy on the DMA engine.
+  struct PendingCopy {
+    bool on = false;
+    HostStage* hs = nullptr;
+    HostSpans* host = nullptr;
+    uint32_t n = 0;
+    uint64_t spans = 0, patches = 0, inl = 0, picked = 0, set = 0, mrows = 0;
+    bool dedup = false, codes = false;
+    hipEvent_t ready = nullptr;
+  };
+  PendingCopy pc_;
+  void issue_host_copy(const PendingCopy& c);
   bool patch_codes_ = true;        // MQ_OPT_PATCH_CODES
   hipStream_t hcopy_ = nullptr;    // the copy stream of host results
   void ensure_hcopy();
