@@ -1,6 +1,8 @@
 // C++ host mirror of the Go TopicsIndex over the C-ABI (topics_index.h).
 #include "topics_index.h"
 
+#include <chrono>
+
 #include <climits>
 #include <cstring>
 
@@ -113,18 +115,35 @@ void TopicsIndex::store(uint32_t c, uint32_t f, const Subscription& sub) {
   filters_.ref(f);
 }
 
+namespace {
+using WClock = std::chrono::steady_clock;
+void note_max(std::atomic<uint64_t>& m, WClock::time_point a, WClock::time_point b) {
+  const uint64_t us = (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+  for (uint64_t v = m.load(); us > v && !m.compare_exchange_weak(v, us);) {
+  }
+}
+}  // namespace
+
 bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) {
+  const auto t0 = WClock::now();
   std::lock_guard<std::mutex> up(upd_mu_);
+  const auto t1 = WClock::now();
+  note_max(waits_.upd, t0, t1);
   uint32_t c, f;
   {
     std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
+    note_max(waits_.tables, t1, WClock::now());
     c = clients_.intern(client);
     f = filters_.intern(sub.Filter);
   }
+  const auto t2 = WClock::now();
   const int rc = mq_subscribe(idx_, sub.Filter.data(), (uint32_t)sub.Filter.size(), c, f, sub.Qos,
                               sub_flags(sub), sub.Identifier);
+  const auto t3 = WClock::now();
+  note_max(waits_.engine, t2, t3);
   if (rc < 0) fail_tidy(rc, "mq_subscribe", &c, 1, &f, 1);
   std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
+  note_max(waits_.tables, t3, WClock::now());
   store(c, f, sub);
   return rc == 1;
 }

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -301,6 +302,12 @@ class TopicsIndex {
   std::string FilterName(uint32_t id) const;
 
   mq_index* handle() { return idx_; }
+  // The longest wait of Subscribe / Unsubscribe so far in each phase (µs): for the update lock,
+  // for the tables' lock, in the engine call (diagnostics of update latency under read load).
+  struct UpdateWaits {
+    std::atomic<uint64_t> upd{0}, tables{0}, engine{0};
+  };
+  const UpdateWaits& update_waits() const { return waits_; }
   Epochs& epochs() { return epochs_; }
   size_t live_clients() const;  // interned client ids in use (churn accounting)
   size_t live_filters() const;
@@ -311,6 +318,7 @@ class TopicsIndex {
   [[noreturn]] void fail_tidy(int rc, const char* what, const uint32_t* clients, size_t nc, const uint32_t* filters,
                               size_t nf);
   mq_index* idx_ = nullptr;
+  UpdateWaits waits_;
   std::mutex upd_mu_;                    // serialises updates
   mutable WriterPreferringMutex tables_mu_;  // the tables below: exclusive to change, shared to read
   Epochs epochs_;
