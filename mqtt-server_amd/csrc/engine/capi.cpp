@@ -18,6 +18,7 @@
 #include "index.h"
 #include "mqmatch.h"
 #include "mqmatch_dev.h"
+#include "fifo_mutex.h"
 
 using namespace mq;
 
@@ -36,7 +37,7 @@ using namespace mq;
 // waits for a match in flight. Results hold a reference, so freeing one after mq_index_destroy is
 // safe.
 struct IndexLock {
-  std::mutex mu;
+  FifoMutex mu;  // (in arrival order: fifo_mutex.h)
   ViewTracker views;
   Device* dev = nullptr;  // the index's device, while it lives (pipelined results flush through it)
 };
@@ -131,7 +132,7 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
       std::unique_lock<std::mutex> g(V.mu);
       V.cv.wait(g, [&] { return V.writers == 0; });
     }
-    std::unique_lock<std::mutex> lk(L.mu, std::defer_lock);
+    std::unique_lock<FifoMutex> lk(L.mu, std::defer_lock);
     if (access == Access::kDrain) {  // wait for the live results without holding `mu`
       for (;;) {
         {
@@ -191,7 +192,7 @@ int mq_index_create(const mq_config* cfg, mq_index** out) {
 void mq_index_destroy(mq_index* idx) {
   if (!idx) return;
   {
-    std::lock_guard<std::mutex> g(idx->lk->mu);
+    std::lock_guard<FifoMutex> g(idx->lk->mu);
     idx->lk->dev = nullptr;  // (tickets still held flush through it no more; ~Device issues their copies)
   }
   delete idx;
@@ -249,7 +250,7 @@ int mq_retained_set(mq_index* idx, const char* topic, uint32_t tlen, uint64_t ha
 
 uint64_t mq_retained_len(const mq_index* idx) {
   if (!idx) return 0;
-  std::lock_guard<std::mutex> lk(idx->lk->mu);
+  std::lock_guard<FifoMutex> lk(idx->lk->mu);
   return idx->ix->retained_len();
 }
 
@@ -417,7 +418,7 @@ int mq_match_spans_wait(mq_spans_ticket* t, mq_span_result** out) {
   if (!t || !out) return fail(MQ_EINVAL, "null argument");
   *out = nullptr;
   if (t->lk) {  // the copy may still be pending (queued behind a next batch's upload)
-    std::lock_guard<std::mutex> g(t->lk->mu);
+    std::lock_guard<FifoMutex> g(t->lk->mu);
     try {
       if (t->lk->dev) t->lk->dev->flush_host_copy();
     } catch (const HipError& he) {

@@ -31,6 +31,12 @@ size_t g_pin_pooled = 0;
 // Pooled pinned blocks are kept up to 4 GiB per process (a broker holds this much page-locked
 // memory at most after large host-result batches); larger frees go back to the system.
 constexpr size_t kPinMin = 64 << 10, kPinPoolCap = 4ull << 30;
+// Small blocks (a result's arrays for a few topics) are carved from 8 MiB slabs and always
+// pooled: a host result holds up to eight of them, and page-locking each one on its own costs
+// about half a millisecond, which readers meeting for the first time would pay inside a match.
+constexpr size_t kPinSlab = 8 << 20, kPinSmall = 256 << 10;
+uint8_t* g_slab = nullptr;
+size_t g_slab_left = 0;
 size_t pin_cap(size_t bytes) {
   size_t c = kPinMin;
   while (c < bytes) c <<= 1;
@@ -46,7 +52,19 @@ void* pinned_alloc(size_t bytes) {
     if (it != g_pin_free.end()) {
       void* p = it->second;
       g_pin_free.erase(it);
-      g_pin_pooled -= cap;
+      if (cap > kPinSmall) g_pin_pooled -= cap;
+      return p;
+    }
+    if (cap <= kPinSmall) {
+      if (g_slab_left < cap) {
+        void* sp = nullptr;
+        if (hipHostMalloc(&sp, kPinSlab, hipHostMallocDefault) != hipSuccess || !sp) throw std::bad_alloc();
+        g_slab = static_cast<uint8_t*>(sp);  // (the rest of the old slab is left unused)
+        g_slab_left = kPinSlab;
+      }
+      void* p = g_slab;
+      g_slab += cap;
+      g_slab_left -= cap;
       return p;
     }
   }
@@ -60,6 +78,10 @@ void pinned_free(void* p, size_t bytes) {
   const size_t cap = pin_cap(bytes);
   {
     std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (cap <= kPinSmall) {  // a slab's block: back to the pool, always
+      g_pin_free.emplace(cap, p);
+      return;
+    }
     if (g_pin_pooled + cap <= kPinPoolCap) {
       g_pin_free.emplace(cap, p);
       g_pin_pooled += cap;
@@ -288,7 +310,7 @@ Device::~Device() {
   (void)hipDeviceSynchronize();  // no kernel of this index still reads a buffer freed below
   if (stage_done_) (void)hipEventDestroy(stage_done_);
   pinned_free(h_stage_, h_stage_bytes_);
-  if (h_fast_) pinned_free(h_fast_, sizeof(FastBack));
+  if (h_fast_) (void)hipHostFree(h_fast_);
   for (int k = 0; k < 2; k++) {
     if (copy_done_[k]) (void)hipEventDestroy(copy_done_[k]);
     if (merge_done_[k]) (void)hipEventDestroy(merge_done_[k]);
@@ -1052,7 +1074,9 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   }
   if (one_sync) {
     if (!h_fast_) {
-      h_fast_ = static_cast<FastBack*>(pinned_alloc(sizeof(FastBack)));
+      void* hp = nullptr;  // (its own allocation, not a slab block: the device reads it by address)
+      hip_check(hipHostMalloc(&hp, sizeof(FastBack), hipHostMallocDefault), "hipHostMalloc");
+      h_fast_ = static_cast<FastBack*>(hp);
       void* dp = nullptr;
       hip_check(hipHostGetDevicePointer(&dp, h_fast_, 0), "hipHostGetDevicePointer");
       d_fast_ = static_cast<FastBack*>(dp);

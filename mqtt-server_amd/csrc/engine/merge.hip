@@ -189,7 +189,9 @@ __global__ __launch_bounds__(256) void k_set_pack(uint32_t n, const uint32_t* __
   const bool own = t < n && tslot[t] != kNone && rep[t] == t;  // a set's representative
   SetInfo si{0, 0, 0, 0, 0};
   if (own) si = sets[t];
-  const uint32_t c = own ? si.n : 0u;
+  // a set whose reservation did not fit its region (a one-sync batch that runs again) has no
+  // patches in the pool: nothing to copy (its count would run past the pool and the stage)
+  const uint32_t c = own && si.fit ? si.n : 0u;
   uint32_t sum;
   const uint32_t pre = wave_excl_scan(c, lane, &sum);
   unsigned long long b = 0;

@@ -122,13 +122,29 @@ void note_max(std::atomic<uint64_t>& m, WClock::time_point a, WClock::time_point
   for (uint64_t v = m.load(); us > v && !m.compare_exchange_weak(v, us);) {
   }
 }
+// the update lock, with its wait and hold times noted (UpdateWaits)
+struct UpdLock {
+  FifoMutex& mu;
+  std::atomic<uint64_t>& held;
+  WClock::time_point t;
+  UpdLock(FifoMutex& m, std::atomic<uint64_t>& wait_max, std::atomic<uint64_t>& held_max) : mu(m), held(held_max) {
+    const auto t0 = WClock::now();
+    mu.lock();
+    t = WClock::now();
+    note_max(wait_max, t0, t);
+  }
+  ~UpdLock() {
+    note_max(held, t, WClock::now());
+    mu.unlock();
+  }
+};
 }  // namespace
 
+#define MQ_UPDATE_LOCK UpdLock up(upd_mu_, waits_.upd, waits_.held)
+
 bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) {
-  const auto t0 = WClock::now();
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   const auto t1 = WClock::now();
-  note_max(waits_.upd, t0, t1);
   uint32_t c, f;
   {
     std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
@@ -149,18 +165,24 @@ bool TopicsIndex::Subscribe(const std::string& client, const Subscription& sub) 
 }
 
 bool TopicsIndex::Unsubscribe(const std::string& filter, const std::string& client) {
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   uint32_t c = kNoClient, f = 0;
   bool known_f;
+  const auto t1 = WClock::now();
   {
     std::shared_lock<WriterPreferringMutex> lk(tables_mu_);
+    note_max(waits_.tables, t1, WClock::now());
     if (!clients_.find(client, &c)) c = kNoClient;  // looked up, never interned
     known_f = filters_.find(filter, &f);
   }
+  const auto t2 = WClock::now();
   const int rc = mq_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), c);
+  const auto t3 = WClock::now();
+  note_max(waits_.engine, t2, t3);
   check(rc, "mq_unsubscribe");
   if (c != kNoClient && known_f) {
     std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
+    note_max(waits_.tables, t3, WClock::now());
     auto it = stored_.find({c, f});
     if (it != stored_.end()) {
       stored_.erase(it);
@@ -173,7 +195,7 @@ bool TopicsIndex::Unsubscribe(const std::string& filter, const std::string& clie
 }
 
 bool TopicsIndex::InlineSubscribe(const InlineSubscription& sub) {
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   uint32_t f;
   {
     std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
@@ -194,7 +216,7 @@ bool TopicsIndex::InlineSubscribe(const InlineSubscription& sub) {
 }
 
 bool TopicsIndex::InlineUnsubscribe(int id, const std::string& filter) {
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   const int rc = mq_inline_unsubscribe(idx_, filter.data(), (uint32_t)filter.size(), id);
   check(rc, "mq_inline_unsubscribe");
   std::unique_lock<WriterPreferringMutex> lk(tables_mu_);
@@ -210,7 +232,7 @@ bool TopicsIndex::InlineUnsubscribe(int id, const std::string& filter) {
 }
 
 std::vector<bool> TopicsIndex::LoadSubscriptions(const std::vector<std::pair<std::string, Subscription>>& subs) {
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   const size_t n = subs.size();
   std::string bytes;
   std::vector<uint64_t> offs(1, 0);
@@ -245,7 +267,7 @@ std::vector<bool> TopicsIndex::LoadSubscriptions(const std::vector<std::pair<std
 
 int64_t TopicsIndex::RetainMessage(const std::string& topic, uint64_t handle, uint32_t payload_len,
                                    bool retain) {
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   int64_t out = 0;
   check(mq_retain_message(idx_, topic.data(), (uint32_t)topic.size(), handle, payload_len,
                           retain ? 1 : 0, &out),
@@ -254,12 +276,12 @@ int64_t TopicsIndex::RetainMessage(const std::string& topic, uint64_t handle, ui
 }
 
 void TopicsIndex::RetainedDelete(const std::string& topic) {
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   check(mq_retained_delete(idx_, topic.data(), (uint32_t)topic.size()), "mq_retained_delete");
 }
 
 void TopicsIndex::RetainedAdd(const std::string& topic, uint64_t handle, uint32_t payload_len, bool retain) {
-  std::lock_guard<std::mutex> up(upd_mu_);
+  MQ_UPDATE_LOCK;
   check(mq_retained_set(idx_, topic.data(), (uint32_t)topic.size(), handle, payload_len, retain ? 1 : 0),
         "mq_retained_set");
 }

@@ -22,6 +22,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "fifo_mutex.h"
 #include "mqmatch.h"
 
 namespace mq {
@@ -306,6 +307,7 @@ class TopicsIndex {
   // for the tables' lock, in the engine call (diagnostics of update latency under read load).
   struct UpdateWaits {
     std::atomic<uint64_t> upd{0}, tables{0}, engine{0};
+    std::atomic<uint64_t> held{0};  // the longest time one update held the update lock
   };
   const UpdateWaits& update_waits() const { return waits_; }
   Epochs& epochs() { return epochs_; }
@@ -319,7 +321,7 @@ class TopicsIndex {
                               size_t nf);
   mq_index* idx_ = nullptr;
   UpdateWaits waits_;
-  std::mutex upd_mu_;                    // serialises updates
+  FifoMutex upd_mu_;                     // serialises updates, in arrival order
   mutable WriterPreferringMutex tables_mu_;  // the tables below: exclusive to change, shared to read
   Epochs epochs_;
   IdTable clients_{epochs_}, filters_{epochs_};

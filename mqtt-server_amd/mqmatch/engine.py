@@ -9,6 +9,7 @@ calls raise.
 """
 import ctypes as C
 import os
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -433,11 +434,12 @@ class Engine:
         _check(lib().mq_match_spans_end_host(self.h, arr, len(foreign), C.byref(rp)), "mq_match_spans_end_host")
         return _expand_host_spans(rp, n)
 
-    def match_spans_pipelined(self, bytes_, offs, batches):
+    def match_spans_pipelined(self, bytes_, offs, batches, log=None):
         """`batches` consecutive mq_match_spans_submit calls of the same host topics, each waited
         for (mq_match_spans_wait) after the next one is submitted, so that a batch's copy into host
         memory runs beside the next batch's kernels; every result is freed. Returns the results'
-        bytes (each batch's are the same)."""
+        bytes (each batch's are the same). `log` (a list): each batch's (submit ms, ms waiting for
+        the batch before it) is appended."""
         n = len(offs) - 1
         pending, nbytes = [], 0
 
@@ -452,11 +454,15 @@ class Engine:
             lib().mq_result_free(rp)
         for _ in range(batches):
             t = C.c_void_p()
+            t0 = time.perf_counter()
             _check(lib().mq_match_spans_submit(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(t)),
                    "mq_match_spans_submit")
+            t1 = time.perf_counter()
             pending.append(t)
             if len(pending) == 2:
                 finish(pending.pop(0))
+            if log is not None:
+                log.append((round(1e3 * (t1 - t0), 3), round(1e3 * (time.perf_counter() - t1), 3)))
         while pending:
             finish(pending.pop(0))
         return int(nbytes)

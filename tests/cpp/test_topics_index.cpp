@@ -435,9 +435,9 @@ static void TestConcurrentReadersAndUpdates() {
                progress[0].load() + progress[1].load() + progress[2].load(), worst_us.load() / 1000.0);
   std::sort(slow.begin(), slow.end(), std::greater<std::pair<long, long>>());
   std::fprintf(stderr, "  engine-handle updates (no mirror): slowest %.1f ms\n", raw_worst_us.load() / 1000.0);
-  std::fprintf(stderr, "  Subscribe's longest waits: update lock %.1f ms, tables %.1f ms, engine call %.1f ms\n",
-               ix.update_waits().upd.load() / 1e3, ix.update_waits().tables.load() / 1e3,
-               ix.update_waits().engine.load() / 1e3);
+  std::fprintf(stderr, "  updates' longest waits: update lock %.1f ms (longest hold %.1f ms), tables %.1f ms, engine call %.1f ms\n",
+               ix.update_waits().upd.load() / 1e3, ix.update_waits().held.load() / 1e3,
+               ix.update_waits().tables.load() / 1e3, ix.update_waits().engine.load() / 1e3);
   std::fprintf(stderr, "  updates over 2 ms: %zu;", slow.size());
   for (size_t i = 0; i < slow.size() && i < 8; i++) std::fprintf(stderr, " %.1f ms at +%ld ms;", slow[i].first / 1e3, slow[i].second);
   std::fprintf(stderr, "\n");

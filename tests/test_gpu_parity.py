@@ -332,6 +332,30 @@ def test_spans_patch_pool_growth(gpu_available):
     _digest_parity(eng, orc, tb, to, fmts=("spans",))  # the grown pool is kept
 
 
+@pytest.mark.parametrize("codes", [1, 0])
+def test_host_spans_first_batch_outgrows_pools(codes, gpu_available):
+    """The first batch of a fresh index, host results, with patch pools far too small (64 slots):
+    its one-sync run overflows both pools, so the packing kernels that run before the batch's
+    readback must copy nothing from a set whose reservation did not fit (a regression: k_set_pack
+    copied such sets' counts past the pool and the stage). Pipelined submit first, then a plain
+    host match; both equal the oracle."""
+    import ctypes as C
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(200000, 20000, seed=83)
+    eng.set_option(E.OPT_PATCH_CAP, 64)
+    eng.set_option(E.OPT_PATCH_CODES, codes)
+    tb, to = W.gen_topics(w, 30000, seed=84)
+    n = len(to) - 1
+    want = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0]
+    t = C.c_void_p()
+    E._check(E.lib().mq_match_spans_submit(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), n, C.byref(t)), "submit")
+    rp = C.POINTER(E.SpanResult)()
+    E._check(E.lib().mq_match_spans_wait(t, C.byref(rp)), "wait")
+    assert (engine_digests(E._expand_host_spans(rp, n))[0] == want).all()
+    _digest_parity(eng, orc, tb, to, fmts=("spans",))
+
+
 def test_spans_format_shape(gpu_available):
     """The span format itself: spans in gather order cover exactly n_rows records, patch rows are
     in range and unique per topic, and a topic without co-matching records has no patches."""

@@ -32,13 +32,13 @@ if pinned:
 
 def submit():
     t = C.c_void_p()
-    assert E.lib().mq_match_spans_submit(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), n, C.byref(t)) == 0
+    E._check(E.lib().mq_match_spans_submit(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), n, C.byref(t)), "submit")
     return t
 
 
 def wait(t):
     rp = C.POINTER(E.SpanResult)()
-    assert E.lib().mq_match_spans_wait(t, C.byref(rp)) == 0
+    E._check(E.lib().mq_match_spans_wait(t, C.byref(rp)), "wait")
     E.lib().mq_result_free(rp)
 
 
