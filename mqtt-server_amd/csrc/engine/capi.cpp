@@ -18,6 +18,9 @@
 #include "index.h"
 #include "mqmatch.h"
 #include "mqmatch_dev.h"
+#include <cstdlib>
+#include <cstdio>
+#include <chrono>
 #include "fifo_mutex.h"
 
 using namespace mq;
@@ -401,12 +404,23 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
     const uint8_t* dtb = nullptr;
     const uint64_t* dto = nullptr;
     hipStream_t hs = d.host_stream();
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     if (n) d.stage_inputs(tb, to, n, hs, &dtb, &dto);  // (ahead of the last batch's copy: below)
+    const auto t1 = clk::now();
     d.flush_host_copy();
+    const auto t2 = clk::now();
     mq_span_result dev_out;
     d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out, tk->ready);
+    const auto t3 = clk::now();
     tk->lk = idx->lk;
     const int rc = publish_host_spans(idx, std::move(h), dev_out, &tk->res);
+    static const bool trace = std::getenv("MQ_TRACE_SUBMIT") != nullptr;
+    if (trace) {
+      auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      std::fprintf(stderr, "mq_match_spans_submit: upload %.3f flush %.3f match %.3f (runs %d, sync wait %.3f) publish %.3f ms\n",
+                   ms(t0, t1), ms(t1, t2), ms(t2, t3), d.trace_runs, d.trace_sync_ms, ms(t3, clk::now()));
+    }
     if (rc) return rc;
     eg.t = nullptr;
     *out = tk.release();

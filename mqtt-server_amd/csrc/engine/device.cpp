@@ -3,6 +3,7 @@
 #include "mqmatch_dev.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -532,7 +533,14 @@ static void grow(DevBuf& b, size_t bytes) {
 
 hipStream_t Device::host_stream() {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
-  if (!hstream_) hip_check(hipStreamCreateWithFlags(&hstream_, hipStreamNonBlocking), "hipStreamCreate");
+  if (!hstream_) {
+    // the copy stream right after it: streams share the device's few hardware queues (4 by
+    // default), and a copy stream on the host stream's queue would run each batch's result copy
+    // in line with the next batch's kernels (measured: a pipelined submit waited for the previous
+    // batch's whole copy when bench.py's other streams had been created between the two)
+    hip_check(hipStreamCreateWithFlags(&hstream_, hipStreamNonBlocking), "hipStreamCreate");
+    ensure_hcopy();
+  }
   return hstream_;
 }
 
@@ -568,7 +576,11 @@ void Device::flush_host_copy() {
 
 void Device::ensure_hcopy() {
   if (hcopy_) return;
-  hip_check(hipStreamCreateWithFlags(&hcopy_, hipStreamNonBlocking), "hipStreamCreate");
+  // the copy stream at the high priority: the runtime keeps separate hardware queues per priority,
+  // so no kernel stream of this process (ours, or a framework's) shares the copies' queue
+  int least = 0, greatest = 0;
+  hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+  hip_check(hipStreamCreateWithPriority(&hcopy_, hipStreamNonBlocking, greatest), "hipStreamCreate");
   for (HostStage& h : hst_) {
     hip_check(hipEventCreateWithFlags(&h.packed, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventCreateWithFlags(&h.copied, hipEventDisableTiming), "hipEventCreate");
@@ -1018,8 +1030,10 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
 void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                          HostSpans* host, mq_span_result* out, hipEvent_t ready) {
   mq_xlist x;
+  trace_runs = 1;
   spans_begin(ix, d_tb, d_to, n, s, &x, one_sync_);
   if (spans_end(ix, nullptr, 0, s, host, out, ready)) return;
+  trace_runs = 2;
   // the one-sync run's buffers did not hold the batch: again, sized by the host
   spans_begin(ix, d_tb, d_to, n, s, &x, false);
   spans_end(ix, nullptr, 0, s, host, out, ready);
@@ -1264,6 +1278,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   if (host) {
     host->codes = codes;
     ensure_hcopy();
+    grow(sp_roff_, (kPatchRegions + 1) * sizeof(uint64_t));  // (written by k_readback in one-sync batches)
     hs = &hst_[hpar_];
     if (hs->used) hip_check(hipStreamWaitEvent(s, hs->copied, 0), "hipStreamWaitEvent");
   }
@@ -1498,7 +1513,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
                       hs->set_patches.as<PatchRec>(), codes ? hs->set_patches.as<uint32_t>() : nullptr,
                       set_total_.as<unsigned long long>(), s);
       hip_check(hipGetLastError(), "k_set_pack");
-      hip_check(hipMemcpyAsync(h_stot, set_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
+      if (!one_sync)  // (one-sync: k_readback reads it)
+        hip_check(hipMemcpyAsync(h_stot, set_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
     }
     if (host) {  // the merge rows of the topics with a set, packed (their total read with pcount)
       if ((uint64_t)n * kPairMax > UINT32_MAX) throw HipError{hipErrorInvalidValue, "host span batch too large"};
@@ -1509,7 +1525,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       launch_mrow_pack(n, a.tslot, a.mcount, a.mrow, hs->merge_base.as<uint32_t>(), hs->merge_rows.as<uint32_t>(),
                        mr_total_.as<unsigned long long>(), s);
       hip_check(hipGetLastError(), "k_mrow_pack");
-      hip_check(hipMemcpyAsync(h_mrtot, mr_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
+      if (!one_sync)
+        hip_check(hipMemcpyAsync(h_mrtot, mr_total_.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s), "D2H");
     }
   }
   for (int attempt = 0;; attempt++) {
@@ -1565,14 +1582,19 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     rb.unsafe = unsafe_.as<uint32_t>();
     rb.err = err_.as<uint32_t>();
     rb.n_sets = sb_.dedup ? dd_nsets_.as<unsigned long long>() : nullptr;
+    // host results: the topic pass's region offsets (on the device, for the packing below) and
+    // the totals, with the rest
+    rb.pcount = host ? a.pcount : nullptr;
+    rb.roff = host ? sp_roff_.as<uint64_t>() : nullptr;
+    rb.set_total = host && sb_.dedup ? set_total_.as<unsigned long long>() : nullptr;
+    rb.mrow_total = host && sb_.dedup ? mr_total_.as<unsigned long long>() : nullptr;
     rb.out = d_fast_;
     launch_readback(rb, s);
     hip_check(hipGetLastError(), "k_readback");
-    if (host)  // the topic pass's patch counts per region (the host packs them below)
-      hip_check(hipMemcpyAsync(h_pc, a.pcount, kPatchRegions * sizeof(unsigned long long), hipMemcpyDeviceToHost, s),
-                "D2H pcount");
     if (sb_.trial >= 0) hip_check(hipEventRecord(walk_ev_[1], s), "hipEventRecord");
+    const auto ts0 = std::chrono::steady_clock::now();
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    trace_sync_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     if (sb_.trial >= 0 && !h_fast_->err && !h_fast_->ovf && !h_fast_->unsafe) {  // a walk trial: its time per topic
       float ms = 0.f;
       hip_check(hipEventElapsedTime(&ms, walk_ev_[0], walk_ev_[1]), "hipEventElapsedTime");
@@ -1587,14 +1609,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
     tot = h_fast_->tot;
     if (sb_.fused) tot.g = h_fast_->n_sets[2];  // (no scan: k_dedup_rep totals the gathers)
-    if (host) {
-      n_patches = 0;
-      for (uint32_t r = 0; r < kPatchRegions; r++) {
-        h_roff[r] = n_patches;
-        n_patches += h_pc[r];
-      }
-      h_roff[kPatchRegions] = n_patches;
-    }
+    if (host) n_patches = h_fast_->n_patches;  // (the region offsets: sp_roff_, k_readback)
     sb_.tot = tot;
     last_sets_ = h_fast_->n_sets[0] + h_fast_->n_sets[1];
     if (prof.on()) {
@@ -1641,10 +1656,10 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.count("merge_topics", n);
   }
   if (host) {  // pack the result into the stage, then copy it on the copy stream
-    grow(sp_roff_, (kPatchRegions + 1) * sizeof(uint64_t));
     if (n_patches) {  // the regions' used parts, packed
       grow(hs->patches, n_patches * sizeof(PatchRec));
-      hip_check(hipMemcpyAsync(sp_roff_.p, h_roff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D");
+      if (!one_sync)  // (one-sync: k_readback wrote them)
+        hip_check(hipMemcpyAsync(sp_roff_.p, h_roff, kPatchRegions * sizeof(uint64_t), hipMemcpyHostToDevice, s), "H2D");
       launch_patch_compact(sp_patches_.as<PatchRec>(), rcap_, a.pcount, sp_roff_.as<uint64_t>(),
                            hs->patches.as<PatchRec>(), codes ? hs->patches.as<uint32_t>() : nullptr, s);
       hip_check(hipGetLastError(), "k_patch_compact");
@@ -1681,8 +1696,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     c.picked = out->n_picked_rows;
     c.dedup = sb_.dedup;
     c.codes = codes;
-    c.set = sb_.dedup ? *h_stot : 0;
-    c.mrows = sb_.dedup ? *h_mrtot : 0;
+    c.set = !sb_.dedup ? 0 : one_sync ? h_fast_->set_total : *h_stot;
+    c.mrows = !sb_.dedup ? 0 : one_sync ? h_fast_->mrow_total : *h_mrtot;
     c.ready = ready;
     // the result's host arrays exist now (the caller publishes them); the copy fills them
     host->topics.resize(n);

@@ -367,6 +367,10 @@ class Device {
   FastBack* d_fast_ = nullptr;      // its device view
   DevBuf unsafe_;
   bool one_sync_ = true;      // MQ_OPT_ONE_SYNC
+ public:
+  double trace_sync_ms = 0.0;  // (MQ_TRACE_SUBMIT) the last one-sync batch's wait at its synchronisation
+  int trace_runs = 0;          //   and how many runs the last match took
+ private:
   bool fuse_desc_ = true;     // MQ_OPT_FUSE_DESC
   uint32_t set_exp_ = 0;      // MQ_OPT_SET_EXP (timing experiments only)
   uint64_t last_sets_ = 0;    // merge sets of the last batch: the grid of the next set pass

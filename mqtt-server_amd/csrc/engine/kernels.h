@@ -544,11 +544,21 @@ struct FastBackRec {  // == Device::FastBack
   TopicOff tot;
   uint32_t ovf, fallback, unsafe, err;
   unsigned long long n_sets[3];
+  // host results: the topic pass's patches (all regions), the packed set patches and merge rows
+  unsigned long long n_patches, set_total, mrow_total;
 };
+// k_readback: every count the host reads at a one-sync batch's end, written by a kernel straight
+// into pinned host memory — no small device-to-host copies, which would queue on the DMA engine
+// behind the previous pipelined batch's result copy and hold this batch's synchronisation.
 struct ReadbackArgs {
   const TopicOff* tot;  // null: not read (the walk-fused desc has no scan)
   const uint32_t *ovf, *fallback, *unsafe, *err;
   const unsigned long long* n_sets;  // null: not read
+  // host results (null: not read): the topic pass's per-region patch counts, whose exclusive
+  // prefix (kPatchRegions + 1 entries) goes to roff in device memory; the packed totals
+  const unsigned long long* pcount;
+  uint64_t* roff;
+  const unsigned long long *set_total, *mrow_total;
   FastBackRec* out;                  // device view of the pinned record
 };
 void launch_readback(const ReadbackArgs& a, hipStream_t s);

@@ -315,7 +315,32 @@ void launch_reset(const ResetArgs& a, hipStream_t s) {
 }
 
 __global__ void k_readback(ReadbackArgs a) {
-  if (threadIdx.x != 0) return;
+  const uint32_t lane = threadIdx.x;  // one wavefront
+  unsigned long long np = 0;
+  if (a.pcount) {  // the regions' exclusive prefix, kPatchRegions / 64 regions per lane
+    constexpr uint32_t kPer = kPatchRegions / 64;
+    unsigned long long c[kPer], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      c[k] = a.pcount[lane * kPer + k];
+      sum += c[k];
+    }
+    unsigned long long x = sum;  // inclusive scan of the lanes' sums
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    unsigned long long off = x - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; k++) {
+      a.roff[lane * kPer + k] = off;
+      off += c[k];
+    }
+    np = __shfl(x, 63, 64);
+    if (lane == 63) a.roff[kPatchRegions] = np;
+  }
+  if (lane != 0) return;
   FastBackRec r;
   r.tot = a.tot ? *a.tot : TopicOff{0, 0, 0, 0, 0};
   r.ovf = *a.ovf;
@@ -323,6 +348,9 @@ __global__ void k_readback(ReadbackArgs a) {
   r.unsafe = *a.unsafe;
   r.err = *a.err;
   for (int k = 0; k < 3; k++) r.n_sets[k] = a.n_sets ? a.n_sets[k] : 0ull;
+  r.n_patches = np;
+  r.set_total = a.set_total ? *a.set_total : 0ull;
+  r.mrow_total = a.mrow_total ? *a.mrow_total : 0ull;
   *a.out = r;
   __threadfence_system();
 }

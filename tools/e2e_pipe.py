@@ -15,8 +15,11 @@ from mqmatch import engine as E  # noqa: E402
 from mqmatch import workload as W  # noqa: E402
 
 subs = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+if "--torch" in sys.argv:  # as bench.py: torch's HIP runtime up first, a tensor on the device
+    import torch
+    _keep = torch.zeros(1 << 20, device="cuda")
 w = W.gen_subscriptions(subs, subs // 10)
-eng = E.Engine()
+eng = E.Engine(expected_subs=subs if "--expected" in sys.argv else 0)
 eng.subscribe_bulk(w)
 tb, to = W.gen_topics(w, 1_000_000)
 n = len(to) - 1
@@ -44,6 +47,9 @@ def wait(t):
 
 for _ in range(2):
     wait(submit())
+if "--seq-first" in sys.argv:  # as bench.py: plain host-result calls before the pipelined ones
+    for _ in range(4):
+        eng.match_spans_host(tb, to)
 log = []
 t0 = time.perf_counter()
 pend = []
@@ -58,7 +64,7 @@ for k in range(6):
 while pend:
     wait(pend.pop(0))
 dt = time.perf_counter() - t0
-print(json.dumps({"pinned": pinned, "batches": 6, "ms_per_batch": 1e3 * dt / 6, "publishes_per_s": 6 * n / dt,
+print(json.dumps({"argv": sys.argv[1:], "pinned": pinned, "batches": 6, "ms_per_batch": 1e3 * dt / 6, "publishes_per_s": 6 * n / dt,
                   "steps": log}))
 t = time.perf_counter()
 for _ in range(3):
