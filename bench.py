@@ -210,6 +210,11 @@ def spans_roofline(prof, work, steps, n, n_subs):
     step_ms = (ms + set_ms) / max(1, steps)
     achieved = per_step / (step_ms * 1e-3) / 1e9
     traffic = read_spans_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n) if set_launches else None
+    # the work counters themselves, and the set pass's phase clocks (shader clocks summed over its
+    # wavefronts: map, pair analysis, resolution of the records, whole set)
+    roof["work"] = {k: g(k) for k in ("merge_pair_entries", "merge_records", "merge_links", "merge_patches",
+                                      "merge_topics_resolved", "set_cycles_map", "set_cycles_pairs",
+                                      "set_cycles_resolve", "set_cycles_total")}
     roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, ms_per_step=step_ms,
                 launches_per_step=(launches + set_launches) / max(1, steps),
                 launch_ms_avg=(ms + set_ms) / max(1, launches + set_launches), bytes_per_step=per_step,

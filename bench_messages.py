@@ -115,6 +115,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--walk", action="store_true",
                     help="Messages by the particle walk (MQ_OPT_MSG_IMAGE 0) instead of the level-order image")
+    ap.add_argument("--no-img-edges", action="store_true",
+                    help="literal lookups through the index's edge table instead of the image's (MQ_OPT_MSG_EDGES 0)")
     ap.add_argument("--oracle-only", metavar="OUT",
                     help="CPU side only (no GPU): build the oracle, write its sample digests, counters and "
                          "CPU baseline to OUT (JSON). At config 5's full size the oracle and the engine's "
@@ -146,6 +148,8 @@ def main():
     eng = E.Engine(device=0)
     if args.walk:
         eng.set_option(E.OPT_MSG_IMAGE, 0)
+    if args.no_img_edges:
+        eng.set_option(E.OPT_MSG_EDGES, 0)
     eng.retain_bulk(rb, ro, hd)
     log(f"engine index built in {time.time() - t0:.1f}s: {eng.stats()}")
     stream = torch.cuda.current_stream()
@@ -180,7 +184,9 @@ def main():
                                f"{n} wildcard filters per step", "retained": len(ro) - 1, "filters": n},
         "handles_per_step": handles, "handles_per_filter": handles / max(1, n),
         "kernels_ms_per_step": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
-        "path": "particle walk (k_msg)" if args.walk else "level-order image (k_msgq + k_msg_copy)",
+        "path": "particle walk (k_msg)" if args.walk else ("level-order image (k_msgq + k_msg_copy), literal lookups "
+                                                          + ("through the index's edge table" if args.no_img_edges
+                                                             else "in the image's edge table")),
         "image_build_ms": build[1] if build else None,
     }
     cpu = None

@@ -40,6 +40,9 @@
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than
                                      kMsgExportMin particles to work items any wavefront takes; > 1: that
                                      threshold; 0: the filter's wavefront walks it alone */
+#define MQ_OPT_MSG_EDGES 21       /* Messages: 1 (default) looks a literal segment up in the retained image's own
+                                     edge table (parent image position, segment) -> child image position, one
+                                     probe; 0: the index's edge table, then the particle's image position */
 #define MQ_OPT_FUSE_DESC 17       /* one-sync span batches: 1 (default) runs k_desc in the frontier walk's
                                      epilogue (spans and merge lists at t * 64, no scan); 0: walk, scan, k_desc */
 

@@ -715,7 +715,7 @@ int mq_device_check(mq_index* idx) {
 }
 
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
-  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_PATCH_CODES || option == 11) return fail(MQ_EINVAL, "unknown option");
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MSG_EDGES || option == 11) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
     if (option == MQ_OPT_EDGE_LOAD) {  // the host image's option
       if (value != 2 && value != 4 && value != 8) throw std::invalid_argument("MQ_OPT_EDGE_LOAD: 2, 4 or 8");

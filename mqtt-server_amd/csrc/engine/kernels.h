@@ -439,12 +439,23 @@ void launch_scatter(const ScatterRun* runs, uint32_t n, const uint8_t* stage, hi
 //   - the live handles of a run are the consecutive run [lp[a], lp[b]) of h.
 // A '+' level of a filter maps a run to a run, a final '+' or '#' emits whole runs of h; only a
 // literal level below a wildcard fans out into lookups.
+// The retained image's own edge table: (parent image position, segment key) -> child image
+// position, for the image's particles only (a child with no live retained message at or below it
+// has no entry). A literal lookup in the Messages walk is then one probe, where the index's edge
+// table needs the probe, then the particle's image position and its check (two more random loads).
+struct ImgEdge {  // 32 B, two per 64 B line; parent kImgEdgeEmpty: free
+  uint32_t parent, child;
+  uint64_t k0, k1, pad;
+};
+constexpr uint32_t kImgEdgeEmpty = 0xFFFFFFFFu;
 struct MsgImg {
   const uint32_t* node;  // image position -> particle
   const uint32_t* pos;   // particle -> image position (valid iff node[pos[p]] == p; n_pos entries)
   const uint2* cl;       // image position -> [x, y) image positions of its image children
   const uint32_t* lp;    // image position -> live particles before it in the image (n + 1)
   const uint64_t* h;     // live handles in image order
+  const ImgEdge* edges;  // the image's edge table (null: look up through the index's, MQ_OPT_MSG_EDGES 0)
+  uint64_t edge_mask;
   uint32_t n, n_pos;
   // MQ_PROF_WORK (null: off): the count pass's clocks per filter (shader clocks >> 4, saturated)
   // and work counters: [0] fan-out lookups (particles probed level by level), [1] filters whose
@@ -478,6 +489,10 @@ struct ImgLevelArgs {
   const uint32_t* coff;
   uint32_t lo, n, next;
 };
+// the image's edge table (ImgEdge, mask + 1 slots, all free) from the index's edges between image
+// particles (node / pos: the image, n positions, n_pos particle slots)
+void launch_img_edges(const DevIndex& ix, const uint32_t* node, const uint32_t* pos, uint32_t n, uint32_t n_pos,
+                      ImgEdge* edges, uint64_t mask, hipStream_t s);
 void launch_img_root(uint32_t* node, uint32_t* pos, uint32_t* live, hipStream_t s);
 void launch_img_level(bool fill, const DevIndex& ix, const ImgLevelArgs& a, hipStream_t s);
 // h[lp[q]] = handle of node[q] for the live positions (lp: the scan of live)

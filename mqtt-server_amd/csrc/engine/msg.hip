@@ -465,6 +465,52 @@ __global__ __launch_bounds__(256) void k_img_compact(DevIndex ix, const uint32_t
   if (lp[q + 1] != l) h[l] = ix.msg[node[q]].handle;
 }
 
+// Thread per slot of the index's edge table (a grid-stride loop): an edge whose parent and child
+// are both in the image becomes the image's edge (parent's image position, the same key) -> the
+// child's image position. Every image particle but the root has exactly one such edge (short
+// segments live only in the edge slots: NodeWalk.seg names long ones). A parent's children have
+// distinct keys, so a slot is claimed once (CAS on the position pair); the keys follow the claim
+// (no reader runs until the kernel ends).
+__global__ __launch_bounds__(256) void k_img_edges(DevIndex ix, const uint32_t* __restrict__ node,
+                                                   const uint32_t* __restrict__ pos, uint32_t n, uint32_t n_pos,
+                                                   ImgEdge* __restrict__ edges, uint64_t mask) {
+  auto in_img = [&](uint32_t c) __attribute__((always_inline)) -> uint32_t {
+    if (c >= n_pos) return kNone;
+    const uint32_t q = pos[c];
+    return (q < n && node[q] == c) ? q : kNone;
+  };
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i <= ix.edge_mask; i += (uint64_t)gridDim.x * 256) {
+    const EdgeSlot e = ix.edges[i];
+    if (e.parent >= kEdgeTomb) continue;  // a free slot
+    const uint32_t qc = in_img(e.child);
+    if (qc == kNone) continue;
+    const uint32_t qp = in_img(e.parent);
+    if (qp == kNone) continue;  // (not reached: an image particle's parent is in the image)
+    const SegKey k{e.k0, e.k1};
+    const unsigned long long want = (unsigned long long)qp | ((unsigned long long)qc << 32);
+    uint64_t j = edge_hash(qp, k) & mask;
+    bool put = false;
+    for (uint64_t probes = 0; probes <= mask && !put; probes++) {
+      unsigned long long* w = reinterpret_cast<unsigned long long*>(&edges[j]);
+      if (atomicCAS(w, ~0ull, want) == ~0ull) {
+        edges[j].k0 = k.k0;
+        edges[j].k1 = k.k1;
+        put = true;
+      }
+      j = (j + 1) & mask;
+    }
+    if (!put) atomicOr(ix.err, kErrWalkGuard);  // (the table holds twice the particles: not reached)
+  }
+}
+
+void launch_img_edges(const DevIndex& ix, const uint32_t* node, const uint32_t* pos, uint32_t n, uint32_t n_pos,
+                      ImgEdge* edges, uint64_t mask, hipStream_t s) {
+  if (n <= 1) return;
+  const uint64_t slots = ix.edge_mask + 1;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_img_edges, dim3(g), dim3(256), 0, s, ix, node, pos, n, n_pos, edges, mask);
+}
+
 void launch_img_root(uint32_t* node, uint32_t* pos, uint32_t* live, hipStream_t s) {
   hipLaunchKernelGGL(k_img_root, dim3(1), dim3(64), 0, s, node, pos, live);
 }
@@ -487,6 +533,28 @@ __device__ __forceinline__ uint32_t img_pos(const MsgImg& img, uint32_t c) {
   if (c >= img.n_pos) return kNone;  // kNone included
   const uint32_t q = img.pos[c];
   return (q < img.n && img.node[q] == c) ? q : kNone;
+}
+
+// The image child of image particle u for segment (key, seg, len), or kNone: one probe of the
+// image's edge table (a long segment's bytes compared as the index's lookup does), or — without
+// the table — the index's edge table, then the child's image position.
+__device__ __forceinline__ uint32_t img_child(const MsgImg& img, const DevIndex& ix, uint32_t u, const SegKey& k,
+                                              const uint8_t* seg, uint32_t len) {
+  if (!img.edges) return img_pos(img, lookup(ix, img.node[u], k, seg, len));
+  uint64_t i = edge_hash(u, k) & img.edge_mask;
+  for (uint64_t probes = 0; probes <= img.edge_mask; probes++) {
+    const ImgEdge e = img.edges[i];
+    if (e.parent == kImgEdgeEmpty) break;
+    if (e.parent == u && e.k0 == k.k0 && e.k1 == k.k1) {
+      if (!seg_is_long(k)) return e.child;
+      const SegInfo si = ix.seginfo[ix.walk[img.node[e.child]].seg];
+      bool eq = si.len == len;
+      for (uint32_t j = 0; eq && j < len; j++) eq = ix.segbytes[si.off + j] == seg[j];
+      if (eq) return e.child;
+    }
+    i = (i + 1) & img.edge_mask;
+  }
+  return kNone;
 }
 
 struct MsgFrame {  // a fan-out in progress: particles [cur, end) still to take segment s
@@ -631,7 +699,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
           ub = ua + 1;
         } else {
           SegKey key = key_of(R, us, e);
-          const uint32_t qc = img_pos(img, lookup(ix, img.node[ua], key, fb + us, len));
+          const uint32_t qc = img_child(img, ix, ua, key, fb + us, len);
           if (qc == kNone) {
             pop = true;
           } else if (last) {
@@ -757,7 +825,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
               else hi = mid;
             }
             const uint32_t u = cur[lo].x + (p - mpre[wv][lo]);
-            qc = img_pos(img, lookup(ix, img.node[u], key, fb + ls, len));
+            qc = img_child(img, ix, u, key, fb + ls, len);
           }
           if (last) {
             if (qc != kNone) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);
@@ -796,6 +864,9 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
   if (WIDE) {  // wavefront per exported item: its run, level-synchronous (fan_out)
     const uint32_t ni = min(*w.n_items, w.cap);
     const uint32_t wbase = (blockIdx.x * 4 + wv) * w.per_wave;  // (wide count: this wavefront's scratch)
+    // (a fixed stride over the items: taking them from one shared counter was slower — 8,192
+    // wavefronts contending on one atomic, and the wavefronts that took many overflowed their run
+    // scratch, so the fill walked those items again: 1.83 -> 3.48 ms at 10M retained)
     for (uint32_t i = blockIdx.x * 4 + wv; i < ni; i += gridDim.x * 4) {
       const MsgWork it = w.items[i];
       t = it.t;
@@ -887,7 +958,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
           break;
         }
         SegKey key = key_of(R, s, e);
-        const uint32_t qc = img_pos(img, lookup(ix, img.node[a], key, fb + s, len));
+        const uint32_t qc = img_child(img, ix, a, key, fb + s, len);
         if (qc == kNone) break;
         if (last) {
           if (lane == 0) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);

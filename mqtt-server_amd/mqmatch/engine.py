@@ -82,6 +82,7 @@ OPT_SUBBATCH_TOPICS, OPT_MSG_SPEC_MB, OPT_MSG_WAVES, OPT_SERIAL, OPT_MERGE_WAVES
 OPT_MSG_IMAGE, OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_MERGE_DEDUP = 8, 9, 10, 12
 OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC, OPT_FUSE_DESC, OPT_SET_EXP, OPT_MSG_EXPORT = 14, 15, 16, 17, 18, 19
 OPT_PATCH_CODES = 20
+OPT_MSG_EDGES = 21
 
 
 class MsgResult(C.Structure):

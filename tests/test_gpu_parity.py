@@ -893,15 +893,18 @@ def test_messages_deep_fanout(gpu_available):
         assert g == o.messages(f), f
 
 
-@pytest.mark.parametrize("export", [1, 0])
-def test_messages_wide_fanout_export(export, gpu_available):
+@pytest.mark.parametrize("export,edges", [(1, 1), (0, 1), (1, 0)])
+def test_messages_wide_fanout_export(export, edges, gpu_available):
     """Filters whose literal segment meets a fan-out of thousands of particles (w/+/c/...: 6,000
     children of w): the count pass hands those particles to work items every wavefront takes
     (MQ_OPT_MSG_EXPORT, kMsgExportMin) and their outputs land after the filter's own part. Mixed
-    with small filters in one batch; equal to the oracle with and without the export."""
+    with small filters in one batch; equal to the oracle with and without the export, and with
+    the literal lookups through the image's edge table (MQ_OPT_MSG_EDGES, the default) or the
+    index's."""
     from mqmatch import engine as E
     e, o = EngineAdapter(), OracleAdapter()
     e.x.engine.set_option(E.OPT_MSG_EXPORT, export)
+    e.x.engine.set_option(E.OPT_MSG_EDGES, edges)
     h = 0
     topics = []
     for i in range(6000):
@@ -935,8 +938,9 @@ def test_messages_empty_topic_retained(gpu_available):
         assert e.messages(f) == o.messages(f), f
 
 
-@pytest.mark.parametrize("image,spec_mb", [(True, None), (False, None), (False, 0), (False, 3)])
-def test_messages_workload_parity(image, spec_mb, gpu_available):
+@pytest.mark.parametrize("image,spec_mb,edges", [(True, None, 1), (True, None, 0), (False, None, 1), (False, 0, 1),
+                                                 (False, 3, 1)])
+def test_messages_workload_parity(image, spec_mb, edges, gpu_available):
     """Messages on a config-5-shaped workload, over the level-order image (default) and the
     particle walk. spec_mb (walk): the speculative count's scratch budget (default: one walk for
     most filters; "0": count and fill walks; "3": a few hundred slots per filter, so that many
@@ -950,6 +954,7 @@ def test_messages_workload_parity(image, spec_mb, gpu_available):
         eng.set_option(E.OPT_MSG_SPEC_MB, spec_mb)
     if not image:
         eng.set_option(E.OPT_MSG_IMAGE, 0)
+    eng.set_option(E.OPT_MSG_EDGES, edges)  # (the image's edge table or the index's, image path)
     eng.retain_bulk(rb, ro, hd)
     orc.retain_bulk(rb, ro, hd)
     base, count, hs = eng.messages_batch(fb, fo)
