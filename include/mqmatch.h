@@ -504,7 +504,7 @@ int mq_device_check(mq_index* idx);
  * in mqmatch_dev.h: development options, not part of the ABI's contract. */
 #define MQ_OPT_CHUNK_ROWS 1       /* row format: output rows per chunk (default 0xF0000000) */
 #define MQ_OPT_PATCH_CAP 6        /* span format: initial patch pool capacity (patches) */
-#define MQ_OPT_EDGE_LOAD 13       /* edge table: at most 1/v of its slots used (2, 4, 8 = default: sparser means
+#define MQ_OPT_EDGE_LOAD 13       /* edge table: at most 1/v of its slots used (2, 4, 8, 16 = default: sparser means
                                      shorter probe chains for the walk, more memory; a table of 2^30 slots or
                                      more keeps 1/2); applies from the next growth */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);

@@ -718,7 +718,7 @@ int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
   if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MSG_EDGES || option == 11) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
     if (option == MQ_OPT_EDGE_LOAD) {  // the host image's option
-      if (value != 2 && value != 4 && value != 8) throw std::invalid_argument("MQ_OPT_EDGE_LOAD: 2, 4 or 8");
+      if (value != 2 && value != 4 && value != 8 && value != 16) throw std::invalid_argument("MQ_OPT_EDGE_LOAD: 2, 4, 8 or 16");
       idx->ix->set_edge_load((uint32_t)value);
       return 0;
     }

@@ -540,8 +540,9 @@ class Index {
   uint64_t n_wild_nodes_ = 0;
   uint32_t max_sub_cap_ = 0;
   // sparser than 1/2: shorter probe chains (r02 k_walk at 10M: 1/2 1.90 ms, 1/4 1.64 ms; round 4,
-  // the frontier walk with the fused desc: 1/4 1.204 ms, 1/8 1.079 ms, profiles/r04/y/)
-  uint32_t edge_load_ = 8;
+  // the frontier walk with the fused desc: 1/4 1.204 ms, 1/8 1.079 ms, 1/16 1.027 ms — 17 GB of
+  // HBM at 10M subscriptions, profiles/r04/y/, r04/yb/)
+  uint32_t edge_load_ = 16;
   uint32_t max_depth_ = 0;
   uint64_t version_ = 0;
   uint64_t retained_version_ = 0;

@@ -295,7 +295,7 @@ void Index::bulk_trie(std::vector<BulkItem>& items, const uint8_t* bytes, unsign
     npair.grow_to(n_end, NodePair{0, kNone, 0, 0});
     if (sharded()) xinfo.grow_to(n_end, XInfo{kNone, 0, 0});
   });
-  grow.emplace_back([&] {  // sized for every particle at load <= 1/edge_load_ (default 1/8; 2^30+ slots keep 1/2)
+  grow.emplace_back([&] {  // sized for every particle at load <= 1/edge_load_ (default 1/16; 2^30+ slots keep 1/2)
     size_t cap = 1024;
     while (cap < edge_load_at(cap) * ((size_t)n_edges_ + n_new + 1)) cap <<= 1;
     if (cap > edges.size()) edge_rehash(cap, threads);

@@ -171,7 +171,7 @@ def test_options_without_device():
 
 
 def test_edge_load_option():
-    """MQ_OPT_EDGE_LOAD 8 (the default) keeps the edge table at most an eighth full, 2 at most half;
+    """MQ_OPT_EDGE_LOAD 16 (the default) keeps the edge table at most a sixteenth full, 2 at most half;
     other values are rejected; answers are unchanged."""
     from mqmatch import workload as W
     w = W.gen_subscriptions(20000, 2000, seed=71)
@@ -181,13 +181,13 @@ def test_edge_load_option():
         sparse.set_option(E.OPT_EDGE_LOAD, 3)
     assert (sparse.subscribe_bulk(w) == dense.subscribe_bulk(w)).all()
     s, d = sparse.stats(), dense.stats()
-    assert s["edges"] == d["edges"] and s["edges"] * 8 <= s["edge_capacity"]
+    assert s["edges"] == d["edges"] and s["edges"] * 16 <= s["edge_capacity"]
     assert s["edge_capacity"] > d["edge_capacity"]
     sparse.check()
     for c in range(300):  # per-entry growth keeps the bound
         assert sparse.subscribe(f"x/{c}/y/{c % 7}", c, 0, 1, 0, 0) == dense.subscribe(f"x/{c}/y/{c % 7}", c, 0, 1, 0, 0)
     s = sparse.stats()
-    assert s["edges"] * 8 <= s["edge_capacity"]
+    assert s["edges"] * 16 <= s["edge_capacity"]
     sparse.check()
 
 
