@@ -1886,6 +1886,7 @@ MsgImg Device::msg_img() const {
   m.h = img_h_.as<uint64_t>();
   m.edges = img_edge_mask_ ? img_edges_.as<ImgEdge>() : nullptr;
   m.edge_mask = img_edge_mask_;
+  m.gate = nullptr;
   m.n = img_n_;
   m.n_pos = img_n_pos_;
   m.cyc = nullptr;
@@ -1946,6 +1947,65 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
   hip_check(hipGetLastError(), "k_msgq<count>");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
   hip_check(hipGetLastError(), "k_scan");
+  // the fill and copy passes, given the output buffers as they are; true when they held the batch
+  auto fill_copy = [&](const uint32_t* gate, const uint64_t* n_pieces) {
+    img.gate = gate;
+    prof.begin(s);
+    launch_msgq(runs ? kMsgPlace : kMsgFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
+                msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
+                msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
+    prof.end("msgq_fill", s);
+    if (exp) {
+      prof.begin(s);
+      launch_msgq(kMsgWideFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
+                  msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
+                  msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
+      prof.end("msgq_wide_fill", s);
+    }
+    hip_check(hipGetLastError(), "k_msgq<fill>");
+    prof.begin(s);
+    if (n_pieces)
+      launch_msg_copy_dev(msg_pieces_.as<MsgPiece>(), n_pieces, msg_pieces_.bytes / sizeof(MsgPiece), img.h,
+                          msg_handles_.as<uint64_t>(), s);
+    else
+      launch_msg_copy(msg_pieces_.as<MsgPiece>(), tot->g, img.h, msg_handles_.as<uint64_t>(), s);
+    prof.end("msg_copy", s);
+    hip_check(hipGetLastError(), "k_msg_copy");
+  };
+  if (!img.work) {
+    // One host synchronisation per batch: the fill and copy passes run on the output buffers as
+    // earlier batches left them, behind a gate (k_msg_gate: the totals fit); the totals, the error
+    // word and the gate are read once at the end, and a batch that did not fit fills again into
+    // buffers sized by the host (the counts stand). Errors flagged earlier surface here too.
+    msg_base_.ensure((size_t)n * sizeof(uint64_t));
+    msg_count_.ensure((size_t)n * sizeof(uint32_t));
+    if (!msg_handles_.p) msg_handles_.ensure(sizeof(uint64_t));
+    if (!msg_pieces_.p) msg_pieces_.ensure(sizeof(MsgPiece));
+    if (!msg_gate_.p) msg_gate_.ensure(2 * sizeof(uint64_t));
+    uint32_t* gate = msg_gate_.as<uint32_t>();
+    uint64_t* n_pieces = msg_gate_.as<uint64_t>() + 1;
+    launch_msg_gate(bpre_.as<TopicOff>() + nb, msg_handles_.bytes / sizeof(uint64_t), msg_pieces_.bytes / sizeof(MsgPiece),
+                    gate, n_pieces, s);
+    hip_check(hipGetLastError(), "k_msg_gate");
+    fill_copy(gate, n_pieces);
+    uint32_t e = 0, g = 0;
+    hip_check(hipMemcpyAsync(tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H total");
+    hip_check(hipMemcpyAsync(&e, err_.p, sizeof(e), hipMemcpyDeviceToHost, s), "D2H err");
+    hip_check(hipMemcpyAsync(&g, gate, sizeof(g), hipMemcpyDeviceToHost, s), "D2H gate");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (e == kErrMsgNest) {  // (the fill wrote within its buffers; the particle walk redoes the batch)
+      hip_check(hipMemsetAsync(err_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(err)");
+      return false;
+    }
+    if (e) check_err(s);  // throws with the tripped guard's name
+    if (!g) {
+      prof.count("msg_one_sync_retries", 1);
+      msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
+      msg_pieces_.ensure(std::max<uint64_t>(tot->g, 1) * sizeof(MsgPiece));
+      fill_copy(nullptr, nullptr);
+    }
+    return true;
+  }
   uint32_t e = 0;
   hip_check(hipMemcpyAsync(tot, bpre_.as<TopicOff>() + nb, sizeof(TopicOff), hipMemcpyDeviceToHost, s), "D2H total");
   hip_check(hipMemcpyAsync(&e, err_.p, sizeof(e), hipMemcpyDeviceToHost, s), "D2H err");
@@ -1979,23 +2039,7 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
   msg_base_.ensure((size_t)n * sizeof(uint64_t));
   msg_count_.ensure((size_t)n * sizeof(uint32_t));
   msg_pieces_.ensure(std::max<uint64_t>(tot->g, 1) * sizeof(MsgPiece));
-  prof.begin(s);
-  launch_msgq(runs ? kMsgPlace : kMsgFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
-              msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
-              msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
-  prof.end("msgq_fill", s);
-  if (exp) {
-    prof.begin(s);
-    launch_msgq(kMsgWideFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
-                msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
-                msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
-    prof.end("msgq_wide_fill", s);
-  }
-  hip_check(hipGetLastError(), "k_msgq<fill>");
-  prof.begin(s);
-  launch_msg_copy(msg_pieces_.as<MsgPiece>(), tot->g, img.h, msg_handles_.as<uint64_t>(), s);
-  prof.end("msg_copy", s);
-  hip_check(hipGetLastError(), "k_msg_copy");
+  fill_copy(nullptr, nullptr);
   return true;
 }
 
@@ -2052,7 +2096,9 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
     err_.ensure(2 * sizeof(uint32_t));
     hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
   }
-  check_err(s);
+  // (one-sync image batches read the error word at their end instead, messages_img)
+  const bool img_path = msg_img_on_ && !ix.empty_topic_live && ix.retained_len() != 0;
+  if (!img_path || prof.work()) check_err(s);
   if (n == 0) return;
   // the Messages kernels launch a wavefront per filter (a grid is limited to 2^32 threads)
   if (n > kMaxWaveBlocks * 4) throw HipError{hipErrorInvalidValue, "more than 2^24 filters in one Messages batch"};
@@ -2066,7 +2112,7 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   // The image path needs Retained.Get("") only on particles with a retain path; with the Q6
   // entry live, a literal level can emit on any particle, which the particle walk covers.
   bool done = false;
-  if (msg_img_on_ && !ix.empty_topic_live && ix.retained_len() != 0) {
+  if (img_path) {
     ensure_img(ix, di, s);
     done = messages_img(di, d_fb, d_fo, n, s, &tot);
   }

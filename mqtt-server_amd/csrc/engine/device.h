@@ -379,6 +379,7 @@ class Device {
   uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf img_node_, img_pos_, img_cl_, img_lp_, img_h_, img_cnt_, img_coff_, img_bsum_, img_bpre_;
   DevBuf img_edges_;                  // the image's edge table (MsgImg.edges)
+  DevBuf msg_gate_;                   // one-sync Messages batches: the gate and the piece count (k_msg_gate)
   uint64_t img_edge_mask_ = 0;
   bool msg_edges_on_ = true;          // MQ_OPT_MSG_EDGES
   DevBuf msg_pieces_;               // k_msgq copy pieces of a batch

@@ -456,6 +456,7 @@ struct MsgImg {
   const uint64_t* h;     // live handles in image order
   const ImgEdge* edges;  // the image's edge table (null: look up through the index's, MQ_OPT_MSG_EDGES 0)
   uint64_t edge_mask;
+  const uint32_t* gate;  // the fill passes run only while *gate != 0 (one-sync batches; null: always)
   uint32_t n, n_pos;
   // MQ_PROF_WORK (null: off): the count pass's clocks per filter (shader clocks >> 4, saturated)
   // and work counters: [0] fan-out lookups (particles probed level by level), [1] filters whose
@@ -578,5 +579,13 @@ struct ReadbackArgs {
 };
 void launch_readback(const ReadbackArgs& a, hipStream_t s);
 void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s);
+// One-sync Messages batches: the output buffers are sized by earlier batches. k_msg_gate compares
+// the batch's totals (the scan's last entry, on the device) with their capacities and opens the
+// fill passes (gate[0] = 1) and the copy (*n_pieces = the piece count) only if they fit; the copy
+// then runs a grid for up to cap_g pieces and reads its count from the device.
+void launch_msg_gate(const TopicOff* tot, uint64_t cap_rows, uint64_t cap_g, uint32_t* gate, uint64_t* n_pieces,
+                     hipStream_t s);
+void launch_msg_copy_dev(const MsgPiece* pieces, const uint64_t* n_pieces, uint64_t cap_g, const uint64_t* h,
+                         uint64_t* out, hipStream_t s);
 
 }  // namespace mq

@@ -577,6 +577,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
   constexpr bool WIDE = MODE == kMsgWideCount || MODE == kMsgWideFill;  // exported work items
   constexpr bool FILL = MODE == kMsgFill || MODE == kMsgPlace || MODE == kMsgWideFill;  // the walk writes output
   constexpr bool RUNS = MODE == kMsgRuns;
+  if (FILL && img.gate && *img.gate == 0u) return;  // (block-uniform: the batch's outputs do not fit)
   __shared__ uint32_t hcur[4], pcur[4], rcur[4];  // next handle / piece / run of the wave's filter
   __shared__ uint2 mfront[4][2][kMsgFront];       // fan-out frontier: runs of one level (two buffers)
   __shared__ uint32_t mpre[4][kMsgFront + 1];      // ... particles before each run
@@ -1009,8 +1010,10 @@ void launch_msgq(int mode, const uint8_t* fb, const uint64_t* fo, uint32_t n, co
 
 // Wavefront per piece: four 64-handle loads in flight per lane, then the stores.
 __global__ __launch_bounds__(256) void k_msg_copy(const MsgPiece* __restrict__ pieces, uint64_t n,
-                                                  const uint64_t* __restrict__ h, uint64_t* __restrict__ out) {
+                                                  const uint64_t* __restrict__ h, uint64_t* __restrict__ out,
+                                                  const uint64_t* __restrict__ n_dev) {
   const uint32_t lane = threadIdx.x & 63;
+  if (n_dev) n = *n_dev;  // (one-sync batches: the count on the device, 0 when the gate is shut)
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + wave_id(); i < n; i += (uint64_t)gridDim.x * 4) {
   const MsgPiece p = pieces[i];
   const uint64_t* src = h + p.h0;
@@ -1029,7 +1032,28 @@ __global__ __launch_bounds__(256) void k_msg_copy(const MsgPiece* __restrict__ p
 
 void launch_msg_copy(const MsgPiece* pieces, uint64_t n, const uint64_t* h, uint64_t* out, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)std::min<uint64_t>((n + 3) / 4, kMaxWaveBlocks)), dim3(256), 0, s, pieces, n, h, out);
+  hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)std::min<uint64_t>((n + 3) / 4, kMaxWaveBlocks)), dim3(256), 0, s, pieces, n, h, out,
+                     (const uint64_t*)nullptr);
+}
+
+void launch_msg_copy_dev(const MsgPiece* pieces, const uint64_t* n_pieces, uint64_t cap_g, const uint64_t* h,
+                         uint64_t* out, hipStream_t s) {
+  if (!cap_g) return;
+  hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)std::min<uint64_t>((cap_g + 3) / 4, kMaxWaveBlocks)), dim3(256), 0, s,
+                     pieces, cap_g, h, out, n_pieces);
+}
+
+__global__ void k_msg_gate(const TopicOff* tot, uint64_t cap_rows, uint64_t cap_g, uint32_t* gate, uint64_t* n_pieces) {
+  if (threadIdx.x != 0) return;
+  const TopicOff t = *tot;
+  const bool ok = t.rows <= cap_rows && t.g <= cap_g;
+  gate[0] = ok ? 1u : 0u;
+  *n_pieces = ok ? t.g : 0ull;
+}
+
+void launch_msg_gate(const TopicOff* tot, uint64_t cap_rows, uint64_t cap_g, uint32_t* gate, uint64_t* n_pieces,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_msg_gate, dim3(1), dim3(64), 0, s, tot, cap_rows, cap_g, gate, n_pieces);
 }
 
 
