@@ -218,7 +218,7 @@ def main():
             handles_per_filter = r.n_handles / max(1, n)
             b_img = 8 * per["L"] + 4 + 16 * handles_per_filter
             ach = b_img * n / (kms * 1e-3) / 1e9
-            traffic = read_msg_traffic(len(ro) - 1, n) if not args.walk else None
+            traffic = read_msg_traffic(args.retained, n) if not args.walk else None  # (keyed by --retained)
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                                "kernel": ("k_msgq (count, wide count, place, wide place) + k_msg_copy" if not args.walk
