@@ -35,9 +35,9 @@ sys.path.insert(0, os.path.join(REPO, "mqtt-server_amd"))
 METRIC = "matched publishes/sec (whole node) at 10M subs; HBM GB/s fraction of peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
-
-
 PIPE_BATCHES = 8  # batches per timed run of the pipelined end-to-end leg
+WALK_TRIAL_MIN = 65536  # device.h kWalkTrialMin: batches this large run the engine's walk trials
+WALK_TRIAL_BATCHES = 6  # device.h kWalkTrialSeq: untimed F, T, then timed T, F, F, T
 
 def heartbeat(period=30.0):
     """Log a line every `period` s from a daemon thread, so that long host phases (generating or
@@ -133,22 +133,23 @@ def engine_option(opt, default):
     return default
 
 
-def read_walk_traffic(path, n_subs, n_topics):
-    """HBM bytes per k_walk launch (FETCH_SIZE x2 + WRITE_SIZE) from a committed rocprofv3 PMC
-    summary of the same configuration (subscriptions, topics, edge-table load), if present."""
+def read_walk_traffic(path, n_subs, n_topics, edge_load, walk_group, fused):
+    """HBM bytes per walk launch (FETCH_SIZE x1 + WRITE_SIZE) from a committed rocprofv3 PMC
+    summary of the configuration that ran (subscriptions, topics, the index's edge-table load as
+    mq_index_stats reports it, the walk the engine's trials chose, the fused desc), if present."""
     try:
         with open(path) as f:
             e = json.load(f).get("walk", {}).get(str(n_subs))
-        if (e is None or int(e["topics"]) != n_topics or int(e.get("edge_load", 2)) != engine_option(13, 4)
-                or int(e.get("walk_group", 0)) != engine_option(15, 16)
-                or int(e.get("fused_desc", 0)) != engine_option(17, 1)):
+        if (e is None or int(e["topics"]) != n_topics or int(e.get("edge_load", 2)) != int(edge_load)
+                or int(e.get("walk_group", 0)) != int(walk_group)
+                or int(e.get("fused_desc", 0)) != int(fused)):
             return None
         return float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError, TypeError):
         return None
 
 
-def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step):
+def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step, edge_load=16, walk_group=16):
     """Roofline of the match walk, k_walkf (16 lanes per topic), with k_desc fused into its
     epilogue (the default for device results, MQ_OPT_FUSE_DESC). Its algorithmic bytes per topic
     are SURVEY.md §8(d)'s walk terms, 8·L + 4 + 16·P (L levels, P child lookups of the
@@ -175,7 +176,10 @@ def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step):
     per_launch = (b_topic + 32) * n + 64 * gathers_per_step if fused else b_topic * n + 4 * gathers_per_step
     launch_ms = ms / launches
     achieved = per_launch / (launch_ms * 1e-3) / 1e9
-    traffic = read_walk_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n)
+    traffic = read_walk_traffic(os.path.join(REPO, "profiles", "pmc_traffic.json"), n_subs, n, edge_load,
+                                walk_group, 1 if fused else 0)
+    roof["traffic_key"] = {"subs": n_subs, "topics": n, "edge_load": edge_load, "walk_group": walk_group,
+                           "fused_desc": 1 if fused else 0}
     roof.update(achieved=achieved, frac=achieved / HBM_PEAK_GBS, launch_ms=launch_ms, bytes_per_launch=per_launch,
                 traffic=traffic)
     if traffic:  # the measured HBM bytes (calibrated PMC) over the same launch time
@@ -534,6 +538,24 @@ def main():
             consumed.clear()
             eng.match_device_chunks(d_tb.data_ptr(), d_to.data_ptr(), n, stream.cuda_stream, consume)
 
+    # The engine's walk trials (device.cpp: one untimed batch per walk, then two timed batches
+    # per walk in ABBA order; the faster is kept for this index) run before the warm-up steps, so
+    # that no trial batch falls in the timed region whatever --warmup is
+    eng.profile(True)
+    eng.profile_reset()
+    calibration = 0
+    if args.format == "spans" and n >= WALK_TRIAL_MIN:
+        for _ in range(WALK_TRIAL_BATCHES):
+            step()
+            calibration += 1
+    torch.cuda.synchronize()
+    trial_prof = eng.profile_read()
+    eng.profile(False)
+    walk_trials = {k: v[0] for k, v in trial_prof.items() if k.startswith("trial_")}
+    for k in ("trial_frontier_ps_per_topic", "trial_thread_ps_per_topic"):
+        if k in walk_trials:  # (two timed batches each: the mean)
+            walk_trials[k] = walk_trials[k] / max(1, walk_trials.get(k.replace("ps_per_topic", "batches"), 1))
+    walk_group = engine_option(15, 0 if "trial_chose_thread" in walk_trials else 16)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -584,6 +606,8 @@ def main():
         "kernels_ms_per_step": {k: v[1] / max(1, args.steps) for k, v in prof.items() if v[1] > 0},
         "counters_per_step": {k: v[0] / max(1, args.steps) for k, v in prof.items() if v[1] == 0},
         "chunks_per_step": chunks,
+        "walk_trials": {"calibration_batches": calibration, "chosen_walk_group": walk_group, **walk_trials},
+        "edge_load": int(eng.stats()["edge_load"]),
     }
 
     if args.format == "spans":
@@ -633,7 +657,7 @@ def main():
             # `roofline` names the step's dominant kernel: the walk or the merge stage, whichever
             # takes longer per step; the other is reported beside it
             wr = walk_roofline(prof, args.steps, n, args.subs, per_topic,
-                               out["counters_per_step"].get("gathers", 0))
+                               out["counters_per_step"].get("gathers", 0), out["edge_load"], walk_group)
             mr = out["roofline"]
             walk_ms = wr.get("launch_ms") or 0.0
             merge_ms = mr.get("ms_per_step") or 0.0
@@ -704,7 +728,8 @@ def main():
     elif args.format == "spans":
         # without the oracle's L / P counters (--no-cpu, multi-rank) the walk's bytes are not
         # known; the walk is still named when it is the longer kernel (achieved: null)
-        wr = walk_roofline(prof, args.steps, n, args.subs, None, out["counters_per_step"].get("gathers", 0))
+        wr = walk_roofline(prof, args.steps, n, args.subs, None, out["counters_per_step"].get("gathers", 0),
+                           out["edge_load"], walk_group)
         walk_ms = prof.get("walk", (0, 0.0))[1] / max(1, args.steps)
         if walk_ms > (out["roofline"].get("ms_per_step") or 0.0):
             wr["launch_ms"] = walk_ms

@@ -70,9 +70,11 @@ def handle_digests(base, count, hs):
     return d
 
 
-def oracle_side(rb, ro, hd, fb, fo, n, args):
+def oracle_side(rb, ro, hd, fb, fo, n, args, early=None):
     """The oracle's part of the bench: sample digests and counters (SURVEY.md §8d B terms) and
-    the CPU baseline (the oracle's Messages on 16 host threads over a bounded sample)."""
+    the CPU baseline (the oracle's Messages on 16 host threads over a bounded sample). early(o):
+    called with the parity part as soon as it exists (--oracle-only writes it before the CPU
+    baselines are timed)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     t0 = time.time()
@@ -87,21 +89,72 @@ def oracle_side(rb, ro, hd, fb, fo, n, args):
     t0 = time.time()
     fast = orc.fast_messages()
     log(f"fast CPU restatement built in {time.time() - t0:.1f}s")
+    # every filter of the batch through the fast restatement, pinned to the oracle on the sample
+    t0 = time.time()
+    fdg, fcnt = fast.digest_batch(fb, fo, nthreads=16)
+    pinned = bool((fdg[:ns] == dg).all() and (fcnt[:ns] == cnt).all())
+    log(f"fast restatement digests of all {n} filters in {time.time() - t0:.1f}s; equal to the oracle's "
+        f"on the {ns}-filter sample: {pinned}")
+    if not pinned:
+        raise SystemExit("the fast restatement differs from the oracle on the sample")
+    o = {"sample_filters": ns, "digests": [format(int(x), "x") for x in dg], "counts": [int(x) for x in cnt],
+         "all_digests": [format(int(x), "x") for x in fdg], "all_counts": [int(x) for x in fcnt],
+         "all_note": "fast restatement (oracle/topics_fast.cpp), equal to the oracle on the sample",
+         "per_filter": {k: v / ns for k, v in tot.items()}, "cpu": None}
+    if early:
+        early(o)
     cal = min(n, 2048)
     secs, _ = fast.bench_messages(fb, fo[:cal + 1], 16)
     m = int(min(n, max(cal, cal * args.cpu_seconds / max(secs, 1e-6))))
+    log(f"CPU baseline: calibration {cal} filters in {secs:.2f}s; timing {m} filters")
     secs, _ = fast.bench_messages(fb, fo[:m + 1], 16)
+    log(f"CPU baseline: {m} filters in {secs:.2f}s")
     cpu = {"value": m / secs, "unit": "filters/s", "cores": 16, "kind": "port",
            "sample": f"first {m} filters, 16 threads, Messages() per filter: the fast CPU restatement of the Go "
                      f"trie's scanMessages (oracle/topics_fast.cpp FastMsgIndex; digest-equal to the oracle)"}
+    fast.close()
     del fast
-    lcal = min(n, 2048)
-    lsecs, _ = orc.bench_messages(fb, fo[:lcal + 1], 16)
-    lm = int(min(n, max(lcal, lcal * min(5.0, args.cpu_seconds / 2) / max(lsecs, 1e-6))))
-    lsecs, _ = orc.bench_messages(fb, fo[:lm + 1], 16)
-    cpu["literal"] = {"value": lm / lsecs, "sample": f"first {lm} filters, 16 threads, oracle/topics_oracle.cpp"}
-    return {"sample_filters": ns, "digests": [format(int(x), "x") for x in dg], "counts": [int(x) for x in cnt],
-            "per_filter": {k: v / ns for k, v in tot.items()}, "cpu": cpu}
+    if len(ro) - 1 < 50_000_000:  # (the literal restatement beside it; at config 5's full size it is
+        lcal = min(n, 512)        #  ~600 filters/s and holds ~120 GB: not timed)
+        lsecs, _ = orc.bench_messages(fb, fo[:lcal + 1], 16)
+        lm = int(min(n, max(lcal, lcal * min(5.0, args.cpu_seconds / 2) / max(lsecs, 1e-6))))
+        lsecs, _ = orc.bench_messages(fb, fo[:lm + 1], 16)
+        cpu["literal"] = {"value": lm / lsecs, "sample": f"first {lm} filters, 16 threads, oracle/topics_oracle.cpp"}
+        log(f"literal CPU baseline: {lm} filters in {lsecs:.2f}s")
+    o["cpu"] = cpu
+    return o
+
+
+def full_parity(eng, fb, fo, o, max_handles=150_000_000):
+    """Every filter of the batch: the engine's Messages (mq_messages_batch, host results, in chunks
+    of at most ~max_handles handles) digested per filter as the oracle digests its own
+    (oracle/oracle_capi.cpp orc_handle_digests, the checker), against the --oracle-only side's
+    fast-restatement digests of all filters."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    n = len(fo) - 1
+    want = np.array([int(x, 16) for x in o["all_digests"]], np.uint64)
+    wcnt = np.array(o["all_counts"], np.uint64)
+    # chunk boundaries from the expected counts, so that no chunk's host result outgrows memory
+    bounds, acc, a = [], 0, 0
+    for i in range(n):
+        acc += int(wcnt[i])
+        if acc >= max_handles or i - a >= 16383:
+            bounds.append((a, i + 1))
+            a, acc = i + 1, 0
+    if a < n:
+        bounds.append((a, n))
+    bad_d = bad_c = 0
+    for a, b in bounds:
+        sub_o = (fo[a:b + 1] - fo[a]).astype(np.uint64)
+        sub_b = np.ascontiguousarray(fb[int(fo[a]):int(fo[b])])
+        base, count, hs = eng.messages_batch(sub_b, sub_o)
+        bad_c += int((count.astype(np.uint64) != wcnt[a:b]).sum())
+        bad_d += int((O.handle_digests(base, count, hs, nthreads=16) != want[a:b]).sum())
+        del base, count, hs
+    return {"filters": n, "chunks": len(bounds), "counts_differ": bad_c, "digests_differ": bad_d,
+            "digests_equal": bad_c == 0 and bad_d == 0,
+            "against": o.get("all_note", "fast restatement")}
 
 
 def main():
@@ -126,6 +179,8 @@ def main():
                          "file of the same workload instead of building the oracle here")
     args = ap.parse_args()
     heartbeat()
+    import faulthandler  # (every thread's stack every 2 minutes: a stall names itself)
+    faulthandler.dump_traceback_later(120, repeat=True, file=sys.stderr)
     from mqmatch import workload as W
 
     t0 = time.time()
@@ -135,11 +190,14 @@ def main():
     log(f"generated {len(ro) - 1} retained topics, {n} filters in {time.time() - t0:.1f}s")
     if args.oracle_only:
         del rh
-        o = oracle_side(rb, ro, hd, fb, fo, n, args)
-        o.update(retained=len(ro) - 1, filters=n)
-        with open(args.oracle_only, "w") as f:
-            json.dump(o, f)
-        log(f"oracle side written to {args.oracle_only}")
+
+        def write(o):
+            o = dict(o, retained=len(ro) - 1, filters=n)
+            with open(args.oracle_only + ".tmp", "w") as f:
+                json.dump(o, f)
+            os.replace(args.oracle_only + ".tmp", args.oracle_only)
+            log(f"oracle side written to {args.oracle_only} (cpu baseline: {'yes' if o['cpu'] else 'not yet'})")
+        write(oracle_side(rb, ro, hd, fb, fo, n, args, early=write))
         return
     import torch
     from mqmatch import engine as E
@@ -206,6 +264,11 @@ def main():
         base, count, hs = eng.messages_batch(fb, fo[:ns + 1])
         out["parity_sample"] = {"filters": ns, "counts_equal": bool((count == cnt).all()),
                                 "digests_equal": bool((handle_digests(base, count, hs) == dg).all())}
+        del base, count, hs
+        if "all_digests" in o:
+            t0 = time.time()
+            out["parity_all"] = full_parity(eng, fb, fo, o)
+            log(f"parity over all {n} filters in {time.time() - t0:.1f}s: {out['parity_all']}")
         per = o["per_filter"]
         b = 8 * per["L"] + 4 + 16 * per["P"] + 16 * per["O"]
         out["alg_bytes_per_filter"] = {"B": b, **per, "sample_filters": ns}

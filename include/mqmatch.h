@@ -133,7 +133,9 @@ int mq_retained_set(mq_index* idx, const char* topic, uint32_t tlen, uint64_t ha
 uint64_t mq_retained_len(const mq_index* idx);
 
 /* Columnar bulk Subscribe for the restore path (server.go:1624-1640): n filters as
- * concatenated bytes + n+1 u64 offsets. out_new (nullable) receives Subscribe's results. */
+ * concatenated bytes + n+1 u64 offsets. out_new (nullable) receives Subscribe's results. An empty
+ * index with no live host result is built in parallel; otherwise the entries are applied one by
+ * one, as mq_subscribe would (never waiting for a live result). */
 int mq_subscribe_bulk(mq_index* idx, const uint8_t* filter_bytes, const uint64_t* offsets,
                       const uint32_t* client_ids, const uint32_t* filter_ids, const uint8_t* qos,
                       const uint8_t* flags, const int32_t* identifiers, uint64_t n,
@@ -373,7 +375,9 @@ static inline uint32_t mq_patch_apply(uint32_t patch_meta, uint32_t meta, int32_
  * frees until no live result can see it (the reference's writers never wait for a reader's maps
  * either, topics.go:270-277, 401-419). Updates are preferred, as with Go's sync.RWMutex: while an
  * update waits (for the match in flight), new matches wait for it, so readers matching back to
- * back cannot starve updates. Only mq_subscribe_bulk waits for the live results to be freed. */
+ * back cannot starve updates. mq_subscribe_bulk does not wait for results either: while one is
+ * live it takes the per-entry path (copy-on-write), so a pipelined caller holding a ticket or a
+ * result may overlap a restore. */
 int mq_match_spans(mq_index* idx, const uint8_t* topic_bytes, const uint64_t* offsets, uint32_t n,
                    mq_span_result** out);
 /* The same, pipelined (ABI v8): mq_match_spans_submit runs the batch's kernels and returns with
@@ -485,7 +489,10 @@ typedef struct mq_stats {
   uint64_t device_bytes, upload_bytes_total, syncs;
   uint64_t partners; /* partner links between may-merge subscriptions */
   uint64_t foreign;  /* sharded: other shards' subscriptions recorded as merge partners */
-  uint32_t max_depth, reserved;
+  uint32_t max_depth;
+  uint32_t edge_load; /* the edge table's load bound at its current size: at most 1/edge_load of
+                         its slots used (MQ_OPT_EDGE_LOAD, 2 from 2^30 slots on or beyond the
+                         index's HBM budget for it) */
 } mq_stats;
 int mq_index_stats(const mq_index* idx, mq_stats* out);
 
@@ -506,7 +513,11 @@ int mq_device_check(mq_index* idx);
 #define MQ_OPT_PATCH_CAP 6        /* span format: initial patch pool capacity (patches) */
 #define MQ_OPT_EDGE_LOAD 13       /* edge table: at most 1/v of its slots used (2, 4, 8, 16 = default: sparser means
                                      shorter probe chains for the walk, more memory; a table of 2^30 slots or
-                                     more keeps 1/2); applies from the next growth */
+                                     more keeps 1/2); applies from the next growth. Memory: 32 B per slot in
+                                     HBM and again in the host mirror — 10M config-3 subscriptions (32.6M
+                                     particles) take 537M slots, 17 GB, at 1/16 (4.3 GB at 1/4). A table that
+                                     would outgrow an eighth of the device's memory (mq_index_create reads
+                                     it) at 1/8 or 1/16 is kept at 1/4 instead (mq_stats.edge_load) */
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
 
 /* Kernel timing by HIP events recorded on the launch stream around each kernel. enable: 0 off,

@@ -34,7 +34,8 @@
                                      partner links loaded 3 / 4 per batch instead of 2 (bits 4-6 act on the
                                      link path: with bit 7); bit 7 (exact) records resolved through their
                                      partner links instead of the fold; bit 8 (exact) fold chunks of 16
-                                     visits */
+                                     visits; bit 9 (exact) merge gathers too big for the hash fold resolved through
+                                     their partner links instead of the record-indexed bit fold (round 5) */
 #define MQ_OPT_PATCH_CODES 20     /* host span results: 1 (default) 4-byte patch codes when the index allows them
                                      (MQ_SPANS_PATCH_CODES); 0: 8-byte mq_patch records */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than
@@ -43,6 +44,12 @@
 #define MQ_OPT_MSG_EDGES 21       /* Messages: 1 (default) looks a literal segment up in the retained image's own
                                      edge table (parent image position, segment) -> child image position, one
                                      probe; 0: the index's edge table, then the particle's image position */
+#define MQ_OPT_MSG_EDGE_BUDGET 22  /* Messages: the image edge table's budget in MiB at 1/16 load (default 8192;
+                                     4x that at 1/8, else 1/4): a small budget forces the sparser tables'
+                                     fallbacks at a small index (their parity test) */
+#define MQ_OPT_FAIL_NEXT 23       /* test hook: the next v span batches fail as if a kernel guard had tripped
+                                     (MQ_EIO), to exercise the callers' error paths */
+#define MQ_OPT_MAX 23             /* the highest option number mq_set_option admits */
 #define MQ_OPT_FUSE_DESC 17       /* one-sync span batches: 1 (default) runs k_desc in the frontier walk's
                                      epilogue (spans and merge lists at t * 64, no scan); 0: walk, scan, k_desc */
 

@@ -3,6 +3,7 @@
 // and HIP failures into negative errno codes with a thread-local message.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -99,9 +100,9 @@ int fail(int code, const std::string& msg) {
 }
 
 // What a guarded call does to the host image (IndexLock).
-// kUpdate: copy-on-write against the live results, never waits for them; kDrain: rewrites the pools
-// in place, waits for the live results to be freed; kPin: publishes a host span result.
-enum class Access { kRead, kUpdate, kDrain, kPin };
+// kUpdate: copy-on-write against the live results, never waits for them (a bulk subscribe too: it
+// takes the per-entry path while a result is live); kPin: publishes a host span result.
+enum class Access { kRead, kUpdate, kPin };
 
 // Runs f under the handle's lock (IndexLock).
 template <class F>
@@ -111,49 +112,27 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
   ViewTracker& V = L.views;
   struct Announce {  // an update's announcement, withdrawn however the call ends
     ViewTracker* V = nullptr;
-    bool drain = false;
     ~Announce() {
       if (!V) return;
       {
         std::lock_guard<std::mutex> g(V->mu);
         V->writers--;
-        if (drain) V->drains--;
       }
       V->cv.notify_all();
     }
   } ann;
   try {
-    if (access == Access::kUpdate || access == Access::kDrain) {
+    if (access == Access::kUpdate) {
       {
         std::lock_guard<std::mutex> g(V.mu);
         V.writers++;
-        if (access == Access::kDrain) V.drains++;
       }
       ann.V = &V;
-      ann.drain = access == Access::kDrain;
     } else {
       std::unique_lock<std::mutex> g(V.mu);
       V.cv.wait(g, [&] { return V.writers == 0; });
     }
-    std::unique_lock<FifoMutex> lk(L.mu, std::defer_lock);
-    if (access == Access::kDrain) {  // wait for the live results without holding `mu`
-      for (;;) {
-        {
-          std::unique_lock<std::mutex> g(V.mu);
-          V.cv.wait(g, [&] { return V.live.empty(); });
-        }
-        lk.lock();
-        bool empty;
-        {
-          std::lock_guard<std::mutex> g(V.mu);
-          empty = V.live.empty();
-        }
-        if (empty) break;  // (a match that was already past the announcement published one)
-        lk.unlock();
-      }
-    } else {
-      lk.lock();
-    }
+    std::lock_guard<FifoMutex> lk(L.mu);
     return f();
   } catch (const HipError& e) {
     return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
@@ -184,6 +163,18 @@ int mq_index_create(const mq_config* cfg, mq_index** out) {
     }
     idx->ix.reset(new Index(idx->cfg.expected_subs, idx->cfg.expected_nodes));
     idx->ix->set_views(&idx->lk->views);
+    {  // the edge table's HBM budget at its sparse loads: an eighth of the device's memory
+      int nd = 0;
+      size_t freeb = 0, total = 0;
+      if (hipGetDeviceCount(&nd) == hipSuccess && idx->cfg.device >= 0 && idx->cfg.device < nd) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (hipSetDevice(idx->cfg.device) == hipSuccess && hipMemGetInfo(&freeb, &total) == hipSuccess)
+          idx->ix->set_edge_budget(total / 8);
+        (void)hipSetDevice(cur);
+      }
+      (void)hipGetLastError();
+    }
     if (idx->cfg.shard_count > 1) idx->ix->set_shard(idx->cfg.shard_index, idx->cfg.shard_count);
     *out = idx;
     return 0;
@@ -267,7 +258,7 @@ int mq_subscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs,
   return guarded(idx, [&] {
     idx->ix->subscribe_bulk(bytes, offs, client_ids, filter_ids, qos, flags, identifiers, n, out_new);
     return 0;
-  }, Access::kDrain);
+  }, Access::kUpdate);
 }
 
 int mq_unsubscribe_bulk(mq_index* idx, const uint8_t* bytes, const uint64_t* offs, const uint32_t* client_ids,
@@ -385,6 +376,7 @@ struct mq_spans_ticket {
   mq_span_result* res = nullptr;
   hipEvent_t ready = nullptr;
   std::shared_ptr<IndexLock> lk;  // the index's lock (its device issues the pending copy)
+  std::atomic<bool> issued{false};  // the copy was queued (a dropped copy leaves it false)
 };
 
 int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_spans_ticket** out) {
@@ -411,7 +403,14 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
     d.flush_host_copy();
     const auto t2 = clk::now();
     mq_span_result dev_out;
-    d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out, tk->ready);
+    struct Disarm {  // a result that is not published takes its armed copy with it
+      Device* d;
+      const std::atomic<bool>* f;
+      ~Disarm() {
+        if (d) d->drop_pending_copy(f);
+      }
+    } da{&d, &tk->issued};
+    d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out, tk->ready, &tk->issued);
     const auto t3 = clk::now();
     tk->lk = idx->lk;
     const int rc = publish_host_spans(idx, std::move(h), dev_out, &tk->res);
@@ -422,6 +421,7 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
                    ms(t0, t1), ms(t1, t2), ms(t2, t3), d.trace_runs, d.trace_sync_ms, ms(t3, clk::now()));
     }
     if (rc) return rc;
+    da.d = nullptr;
     eg.t = nullptr;
     *out = tk.release();
     return 0;
@@ -441,6 +441,12 @@ int mq_match_spans_wait(mq_spans_ticket* t, mq_span_result** out) {
       delete t;
       return fail(MQ_EIO, he.where);
     }
+  }
+  if (!t->issued.load()) {  // its copy was dropped: a later submit's flush of it failed
+    (void)hipEventDestroy(t->ready);
+    mq_result_free(t->res);
+    delete t;
+    return fail(MQ_EIO, "the result's copy into host memory was never issued (an earlier flush failed)");
   }
   const hipError_t e = hipEventSynchronize(t->ready);
   (void)hipEventDestroy(t->ready);
@@ -687,6 +693,7 @@ int mq_index_stats(const mq_index* cidx, mq_stats* out) {
     out->retained = x.retained_len();
     out->retained_live = x.msg.h[kRoot].below_live;  // live retained particles (every one is below the root)
     out->max_depth = x.max_depth();
+    out->edge_load = x.edge_load_at(x.edges.size());
     out->partners = x.parts.live;
     out->foreign = x.foreign_subs();
     if (idx->dev) {
@@ -715,7 +722,7 @@ int mq_device_check(mq_index* idx) {
 }
 
 int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
-  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MSG_EDGES || option == 11) return fail(MQ_EINVAL, "unknown option");
+  if (option < MQ_OPT_CHUNK_ROWS || option > MQ_OPT_MAX || option == 11) return fail(MQ_EINVAL, "unknown option");
   return guarded(idx, [&] {
     if (option == MQ_OPT_EDGE_LOAD) {  // the host image's option
       if (value != 2 && value != 4 && value != 8 && value != 16) throw std::invalid_argument("MQ_OPT_EDGE_LOAD: 2, 4, 8 or 16");

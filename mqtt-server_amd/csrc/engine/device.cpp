@@ -300,6 +300,11 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
       msg_edges_on_ = v != 0;
       img_version_ = ~0ull;  // (the image is rebuilt, with or without its table)
       return true;
+    case MQ_OPT_MSG_EDGE_BUDGET:
+      msg_edge_budget_ = v ? (v << 20) : (8ull << 30);
+      img_version_ = ~0ull;
+      return true;
+    case MQ_OPT_FAIL_NEXT: fail_next_ = (uint32_t)v; return true;
     default: return false;
   }
 }
@@ -568,6 +573,7 @@ void Device::issue_host_copy(const PendingCopy& c) {
   }
   hip_check(hipEventRecord(hs->copied, hcopy_), "hipEventRecord");
   if (c.ready) hip_check(hipEventRecord(c.ready, hcopy_), "hipEventRecord");
+  if (c.issued) c.issued->store(true);
 }
 
 void Device::flush_host_copy() {
@@ -1032,15 +1038,15 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
 // patch pool grows when a batch reserves more than it holds (the batch's k_merge then runs
 // again); the call ends with the stream synchronised and the guard flags checked.
 void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                         HostSpans* host, mq_span_result* out, hipEvent_t ready) {
+                         HostSpans* host, mq_span_result* out, hipEvent_t ready, std::atomic<bool>* issued) {
   mq_xlist x;
   trace_runs = 1;
   spans_begin(ix, d_tb, d_to, n, s, &x, one_sync_);
-  if (spans_end(ix, nullptr, 0, s, host, out, ready)) return;
+  if (spans_end(ix, nullptr, 0, s, host, out, ready, issued)) return;
   trace_runs = 2;
   // the one-sync run's buffers did not hold the batch: again, sized by the host
   spans_begin(ix, d_tb, d_to, n, s, &x, false);
-  spans_end(ix, nullptr, 0, s, host, out, ready);
+  spans_end(ix, nullptr, 0, s, host, out, ready, issued);
 }
 
 void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
@@ -1078,8 +1084,9 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
       walk_trial_nodes_ = nodes;
       walk_trial_wild_ = wild;
       walk_trial_ns_[0] = walk_trial_ns_[1] = 0.0;
+      walk_trial_step_ = 0;
     }
-    const int k = walk_trial_ns_[0] == 0.0 ? 0 : walk_trial_ns_[1] == 0.0 ? 1 : -1;
+    const int k = walk_trial_step_ < 6 ? (int)kWalkTrialSeq[walk_trial_step_] : -1;
     if (k >= 0) {
       sb_.trial = k;
       if (!walk_ev_[0]) {
@@ -1201,6 +1208,10 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     fda.dd_tslot = dd_slot_.as<uint32_t>();
   }
   const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, one_sync, fused ? &fda : nullptr);
+  if (fail_next_) {  // MQ_OPT_FAIL_NEXT: as if a kernel guard had tripped in this batch
+    fail_next_--;
+    hip_check(hipMemsetD32Async((hipDeviceptr_t)err_.p, (int)kErrWalkGuard, 1, s), "hipMemsetD32Async(err)");
+  }
   sb_.tot = tot;
   sb_.gathers = gathers;
   sb_.gstride = gstride;
@@ -1251,7 +1262,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
 }
 
 bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host,
-                       mq_span_result* out, hipEvent_t ready) {
+                       mq_span_result* out, hipEvent_t ready, std::atomic<bool>* issued) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   memset(out, 0, sizeof(*out));
   if (host) *host = HostSpans{};
@@ -1270,6 +1281,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   if (nf && !ix.sharded()) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
   if (n == 0) {
     if (ready) hip_check(hipEventRecord(ready, s), "hipEventRecord");
+    if (issued) issued->store(true);
     return true;
   }
   const bool one_sync = sb_.one_sync;
@@ -1600,11 +1612,17 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     trace_sync_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     if (sb_.trial >= 0 && !h_fast_->err && !h_fast_->ovf && !h_fast_->unsafe) {  // a walk trial: its time per topic
-      float ms = 0.f;
-      hip_check(hipEventElapsedTime(&ms, walk_ev_[0], walk_ev_[1]), "hipEventElapsedTime");
-      walk_trial_ns_[sb_.trial] = std::max(1e-3, 1e6 * (double)ms / n);
-      prof.count(sb_.trial ? "trial_thread_ps_per_topic" : "trial_frontier_ps_per_topic",
-                 std::max<uint64_t>(1, (uint64_t)(1e3 * walk_trial_ns_[sb_.trial])));
+      if (walk_trial_step_ >= kWalkTrialWarm) {
+        float ms = 0.f;
+        hip_check(hipEventElapsedTime(&ms, walk_ev_[0], walk_ev_[1]), "hipEventElapsedTime");
+        const double ns = std::max(1e-3, 1e6 * (double)ms / n);
+        walk_trial_ns_[sb_.trial] += ns;
+        prof.count(sb_.trial ? "trial_thread_ps_per_topic" : "trial_frontier_ps_per_topic",
+                   std::max<uint64_t>(1, (uint64_t)(1e3 * ns)));
+        prof.count(sb_.trial ? "trial_thread_batches" : "trial_frontier_batches", 1);
+      }
+      walk_trial_step_++;
+      if (walk_trial_step_ == 6) prof.count(walk_trial_ns_[1] < walk_trial_ns_[0] ? "trial_chose_thread" : "trial_chose_frontier", 1);
     }
     if (h_fast_->err) check_err(s);  // throws with the tripped guard's name
     if (h_fast_->ovf || h_fast_->unsafe) {
@@ -1657,8 +1675,17 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.count("set_cycles_total", sum[7]);
     prof.count("merge_topics_resolved", sum[8]);
     prof.count("merge_map_bytes", sum[9]);
+    prof.count("merge_fold_visits", sum[10]);
+    prof.count("merge_big_visits", sum[11]);
+    prof.count("merge_big_gathers", sum[12]);
+    prof.count("merge_big_nmerge", sum[13]);
+    prof.count("merge_fold_nmerge", sum[14]);
+    prof.count("merge_fold_chunks", sum[15]);
     prof.count("merge_topics", n);
   }
+  // A pipelined copy is armed (pc_) only when the batch has passed its error check: a batch that
+  // throws frees the host arrays the copy would fill.
+  PendingCopy arm;
   if (host) {  // pack the result into the stage, then copy it on the copy stream
     if (n_patches) {  // the regions' used parts, packed
       grow(hs->patches, n_patches * sizeof(PatchRec));
@@ -1703,6 +1730,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     c.set = !sb_.dedup ? 0 : one_sync ? h_fast_->set_total : *h_stot;
     c.mrows = !sb_.dedup ? 0 : one_sync ? h_fast_->mrow_total : *h_mrtot;
     c.ready = ready;
+    c.issued = issued;
     // the result's host arrays exist now (the caller publishes them); the copy fills them
     host->topics.resize(n);
     host->spans.resize(c.spans);
@@ -1719,18 +1747,21 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hs->used = true;
     hpar_ ^= 1u;
     if (ready) {
-      pc_ = c;  // pipelined: issued behind the next batch's upload (flush_host_copy)
+      arm = c;  // pipelined: issued behind the next batch's upload (flush_host_copy)
     } else {
       issue_host_copy(c);
       hip_check(hipStreamSynchronize(hcopy_), "hipStreamSynchronize(copy)");
     }
   } else if (ready) {
     hip_check(hipEventRecord(ready, s), "hipEventRecord");
+    if (issued) issued->store(true);
   }
-  if (one_sync) return true;  // (checked above)
-  hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
-  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
-  if (*h_err) check_err(s);  // throws with the tripped guard's name
+  if (!one_sync) {  // (one-sync: checked above)
+    hip_check(hipMemcpyAsync(h_err, err_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H err");
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (*h_err) check_err(s);  // throws with the tripped guard's name
+  }
+  if (arm.on) pc_ = arm;
   return true;
 }
 
@@ -1858,11 +1889,14 @@ void Device::ensure_img(const Index& ix, const DevIndex& di, hipStream_t s) {
     // the image's edge table, sparse: most lookups miss (a literal under a wide run), and a miss
     // ends at the first free slot. At most a sixteenth full while that stays within 8 GiB, an
     // eighth within 32 GiB, else a quarter (10M retained: 1/8 -> 53.4M filters/s, 1/2 -> 37.9M)
+    // (MQ_OPT_MSG_EDGE_BUDGET lowers the 8 GiB budget, and the 32 GiB one with it: the tier test)
     uint64_t slots2 = 1024;
     while (slots2 < 16ull * lo) slots2 <<= 1;
     while (slots2 > 4ull * lo && slots2 > 1024 &&
-           slots2 * sizeof(ImgEdge) > (slots2 >= 16ull * lo ? (8ull << 30) : (32ull << 30)))
+           slots2 * sizeof(ImgEdge) > (slots2 >= 16ull * lo ? msg_edge_budget_ : 4 * msg_edge_budget_))
       slots2 >>= 1;
+    prof.count("msg_edge_slots", slots2);
+    prof.count("msg_edge_particles", lo);
     img_edges_.ensure(slots2 * sizeof(ImgEdge));
     hip_check(hipMemsetAsync(img_edges_.p, 0xFF, slots2 * sizeof(ImgEdge), s), "hipMemsetAsync(image edges)");
     launch_img_edges(di, img_node_.as<uint32_t>(), img_pos_.as<uint32_t>(), lo, slots, img_edges_.as<ImgEdge>(), slots2 - 1, s);

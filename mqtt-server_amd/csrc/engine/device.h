@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <new>
 #include <string>
 #include <utility>
@@ -194,13 +196,20 @@ class Device {
   // copies every array into it (out's pointers then still name the device arrays).
   // ready (host results): the copy into `host` runs on the copy stream beside whatever the
   // device does next (the next batch's kernels), and `ready` is recorded when it is done; without
-  // it the call returns after the copy.
+  // it the call returns after the copy. `issued` (with ready) is set when the deferred copy is queued:
+  // a copy that was dropped (its flush failed) leaves it false, and the waiter reports MQ_EIO.
   void match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                   HostSpans* host, mq_span_result* out, hipEvent_t ready = nullptr);
+                   HostSpans* host, mq_span_result* out, hipEvent_t ready = nullptr,
+                   std::atomic<bool>* issued = nullptr);
   // Issue the pipelined host batch's copy that is still pending (match_spans with `ready` defers
   // it until the next batch's inputs are staged, or its result is waited for). Under the handle
   // lock.
   void flush_host_copy();
+  // Forget the pending copy armed with this flag (its result was never published: the host arrays
+  // it would fill are gone).
+  void drop_pending_copy(const std::atomic<bool>* issued) {
+    if (pc_.on && pc_.issued == issued) pc_.on = false;
+  }
   // The same in two phases, for a sharded index: begin walks the batch and
   // exports the topics' gathered cross-shard nodes (device pointers in *x, valid until end);
   // the caller exchanges the lists between the shards; end merges with the other shards' lists.
@@ -210,7 +219,7 @@ class Device {
   void spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x,
                    bool one_sync = false);
   bool spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out,
-                 hipEvent_t ready = nullptr);
+                 hipEvent_t ready = nullptr, std::atomic<bool>* issued = nullptr);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
                 HostMsg* host, mq_msg_result* out);
@@ -335,6 +344,7 @@ class Device {
     uint64_t spans = 0, patches = 0, inl = 0, picked = 0, set = 0, mrows = 0;
     bool dedup = false, codes = false;
     hipEvent_t ready = nullptr;
+    std::atomic<bool>* issued = nullptr;  // the ticket's flag: set once the copy is queued
   };
   PendingCopy pc_;
   void issue_host_copy(const PendingCopy& c);
@@ -372,6 +382,8 @@ class Device {
   int trace_runs = 0;          //   and how many runs the last match took
  private:
   bool fuse_desc_ = true;     // MQ_OPT_FUSE_DESC
+  uint64_t msg_edge_budget_ = 8ull << 30;  // MQ_OPT_MSG_EDGE_BUDGET: the image edge table's 1/16 budget
+  uint32_t fail_next_ = 0;    // MQ_OPT_FAIL_NEXT: span batches still to fail as if a guard tripped
   uint32_t set_exp_ = 0;      // MQ_OPT_SET_EXP (timing experiments only)
   uint64_t last_sets_ = 0;    // merge sets of the last batch: the grid of the next set pass
   DevBuf sp_tc_;                     // per-topic counts from k_desc<true> (walk without lists)
@@ -400,7 +412,13 @@ class Device {
   static constexpr uint32_t kWalkTrialMin = 65536;  // batches this large are timed for the trial
   uint64_t walk_trial_nodes_ = 0;                    // the index size the trials ran at
   double walk_trial_wild_ = 0.0;                     //   and its share of '+' / '#' particles
-  double walk_trial_ns_[2] = {0.0, 0.0};             // batch time per topic: frontier, thread per topic
+  // The trial schedule (walk per trial batch: 0 frontier, 1 thread per topic): one untimed batch of
+  // each walk (caches, first-touch allocations), then two timed batches of each in ABBA order; the
+  // faster mean per topic is kept. walk_trial_step_ counts the completed trial batches.
+  static constexpr uint32_t kWalkTrialSeq[6] = {0, 1, 1, 0, 0, 1};
+  static constexpr uint32_t kWalkTrialWarm = 2;
+  uint32_t walk_trial_step_ = 0;
+  double walk_trial_ns_[2] = {0.0, 0.0};             // timed batch time per topic, summed: frontier, thread
   hipEvent_t walk_ev_[2] = {nullptr, nullptr};
   uint32_t dedup_ = 1;           // span format: merge-set dedup (MQ_OPT_MERGE_DEDUP)
   uint32_t set_grid_ = 1;        // MQ_OPT_SET_GRID (10M: set pass 1.18 -> 1.05 ms against persistent waves)

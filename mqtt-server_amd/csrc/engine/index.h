@@ -286,8 +286,7 @@ struct ViewTracker {
     live.insert(++gen);
     return gen;
   }
-  std::condition_variable cv;  // a bulk update waits on it for the live results to drain
-  uint64_t drains = 0;          // bulk updates announced (a new result waits for them)
+  std::condition_variable cv;  // new matches wait on it while updates are announced
   uint64_t writers = 0;         // updates announced (a new match waits for them: capi.cpp)
   void release(uint64_t v) {
     std::lock_guard<std::mutex> g(mu);
@@ -335,6 +334,11 @@ class Index {
   void set_shard(uint32_t shard, uint32_t n_shards);
   // The live host results (ViewTracker): set by the C-ABI when the index is created.
   void set_views(ViewTracker* v) { views_ = v; }
+  bool views_live() const {  // a host span result is live (it may read the pools)
+    if (!views_) return false;
+    std::lock_guard<std::mutex> g(views_->mu);
+    return !views_->live.empty();
+  }
   uint64_t retired_slabs() const { return retired_.size(); }
   uint32_t shard() const { return shard_; }
   uint32_t n_shards() const { return n_shards_; }
@@ -394,7 +398,15 @@ class Index {
   // edge table: at most 1/load of its slots used (MQ_OPT_EDGE_LOAD); from the next growth. A
   // table of 2^30 slots or more keeps load <= 1/2 (32 GB of slots at 2^30).
   void set_edge_load(uint32_t load) { edge_load_ = load; }
-  uint32_t edge_load_at(size_t cap) const { return cap >= (size_t(1) << 30) ? 2u : edge_load_; }
+  // HBM the edge table may take at a load sparser than 1/4 (0: no limit); mq_index_create sets it
+  // from the device's memory, so that several indexes on one GPU, or one far larger than config 3,
+  // fall back to 1/4 instead of running out
+  void set_edge_budget(uint64_t bytes) { edge_budget_ = bytes; }
+  uint32_t edge_load_at(size_t cap) const {  // (non-increasing in cap: the growth loops converge)
+    if (cap >= (size_t(1) << 30)) return 2u;
+    if (edge_budget_ && edge_load_ > 4 && cap * sizeof(EdgeSlot) > edge_budget_) return 4u;
+    return edge_load_;
+  }
   uint64_t n_subs_merge() const { return n_merge_; }
   uint32_t max_depth() const { return max_depth_; }
   uint64_t version() const { return version_; }
@@ -543,6 +555,7 @@ class Index {
   // the frontier walk with the fused desc: 1/4 1.204 ms, 1/8 1.079 ms, 1/16 1.027 ms — 17 GB of
   // HBM at 10M subscriptions, profiles/r04/y/, r04/yb/)
   uint32_t edge_load_ = 16;
+  uint64_t edge_budget_ = 0;
   uint32_t max_depth_ = 0;
   uint64_t version_ = 0;
   uint64_t retained_version_ = 0;

@@ -506,12 +506,15 @@ void Index::subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uin
                             filter_ids[i], qos[i], flags[i], idents[i]);
     if (out_new) out_new[i] = (uint8_t)r;
   };
-  if (!empty_image() || n < 4096) {  // the per-entry path
+  // The per-entry path (copy-on-write against live results, as every update) unless the image is
+  // empty and no result is live: the parallel build below lays the pools out afresh, over slabs
+  // that a result from before the image emptied might still read.
+  if (!empty_image() || n < 4096 || views_live()) {
     for (uint64_t i = 0; i < n; i++) one(i);
     return;
   }
   version_++;
-  begin_op();  // (no live result: mq_subscribe_bulk drains them)
+  begin_op();
   const unsigned threads = build_threads();
   // 0. classify: this shard's non-shared / shared entries and their paths (Index::set(f, 0) /
   // set(f, 2), isolateParticle semantics for short shared filters, Q13); the rest is foreign

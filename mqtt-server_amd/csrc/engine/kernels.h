@@ -40,11 +40,18 @@ constexpr uint32_t kFoldCap = kFoldSlots * 3 / 4;
 constexpr uint32_t kFoldNonBase = 1u << 13;  // a visit's partner comes before the record
 constexpr uint32_t kFoldNoLocal = 1u << 14;  // a partner has NoLocal
 constexpr uint32_t kFoldQos0 = 1u << 15;     // bit 15 + q: a partner has Qos q
+// The set pass's fold of a merge gather too big for the hash fold (merge.hip fold_big): 4 bits per
+// record of g's may-merge slots, kBitRecs records per pass (256 words: the map's LDS)
+constexpr uint32_t kBitRecs = 2 * kMapSlots * 8;
+constexpr uint32_t kBitNonBase = 1u, kBitNoLocal = 2u, kBitQos1 = 4u, kBitQos2 = 8u;
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
-constexpr uint32_t kWork = 10;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
-                                // [8] topics the kernel resolved, [9] bytes of their maps' sources read
+constexpr uint32_t kWork = 16;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
+                                // [8] topics the kernel resolved, [9] bytes of their maps' sources read;
+                                // set pass fold: [10] visits folded, [11] visits of merge gathers too big
+                                // to fold, [12] those gathers, [13] their may-merge records (n_merge),
+                                // [14] records of the folded chunks' gathers, [15] folded chunks
 constexpr uint32_t kMergeWavesPerEU = 8;  // k_merge<spans> register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.

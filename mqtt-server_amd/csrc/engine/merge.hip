@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   auto rank_of = [](const GDesc& d) { return gdesc_rank<XS>(d); };
   // MQ_OPT_SET_EXP: the exact variants (bit 7: partner links instead of the fold, bit 8: small fold
   // chunks) in every build; the attribution bits 0-4 in development builds only
-  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (128u | 256u));
+  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (128u | 256u | 512u));
   // persistent: a.merge grid's waves stride over the chunk's topics (wave-uniform loop)
   // (dedup's set pass: the waves stride over the list of set representatives instead; its topic
   // pass after k_finish: over the topics k_finish left)
@@ -908,6 +908,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         wave_sync_lds();  // (before the table is cleared again)
       };
+      // A merge gather whose lists hold more visits than the hash fold's chunk (the hot lists: root
+      // '#', '+/...', 'x/#'): the same fold, over a table indexed by the record's place in g's list
+      // instead of a hash — 4 bits per record (kBitNonBase: a visit's partner comes before g;
+      // kBitNoLocal; kBitQos1 / 2: a partner's Qos), kBitRecs records per pass, in the map's LDS —
+      // so it holds any number of visits. A list of more records takes several passes over the
+      // visits, each folding the records of its range. The emission reads each flagged record's own
+      // meta and identifier from the pool (the table has no room for them). No partner links.
+      auto fold_big = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
+        uint32_t* __restrict__ tbl_lo = map_key[wv];  // words [0, 128)
+        uint32_t* __restrict__ tbl_hi = map_val[wv];  // words [128, 256)
+        map_ok = false;
+        const uint32_t xa = h_ga[wv][j0];
+        const NodeLists L = a.ix.lists[mg_node[wv][xa]];
+        const uint32_t v0 = h_pre[wv][j0], v1 = h_pre[wv][j1];
+        const uint64_t rg = XS ? mg_rank[wv][xa] : 0ull;
+        const uint32_t gg = mg_gi[wv][xa];
+        for (uint32_t c0 = 0; c0 < L.n_merge; c0 += kBitRecs) {  // wave-uniform
+          for (uint32_t q = lane; q < kBitRecs / 8; q += 64) {
+            if (q < 128) tbl_lo[q] = 0u;
+            else tbl_hi[q - 128] = 0u;
+          }
+          uint32_t jj_next = j0;
+          PairSlot e_next = locate(v0 + lane, j0, j1, jj_next);
+          wave_sync_lds();
+          for (uint32_t r0 = v0; r0 < v1; r0 += 64) {
+            const uint32_t r = r0 + lane;
+            const uint32_t jj = jj_next;
+            const PairSlot e = e_next;
+            if (r0 + 64 < v1) e_next = locate(r0 + 64 + lane, j0, j1, jj_next);  // wave-uniform
+            const uint32_t idx = e.k - L.n_direct - c0;
+            if (r < v1 && idx < kBitRecs) {
+              const uint32_t hb = h_hb[wv][jj];
+              const bool earlier = before(XS ? mg_rank[wv][hb] : 0ull, mg_gi[wv][hb], rg, gg);
+              const uint32_t pm = e.meta >> kSlotPartShift;  // the partner's Qos | NoLocal << 2
+              const uint32_t bits = (earlier ? kBitNonBase : 0u) | ((pm & 4u) ? kBitNoLocal : 0u) |
+                                    ((pm & 3u) == 1u ? kBitQos1 : 0u) | ((pm & 3u) == 2u ? kBitQos2 : 0u);
+              if (bits) {
+                const uint32_t w = idx >> 3;
+                atomicOr(w < 128 ? &tbl_lo[w] : &tbl_hi[w - 128], bits << ((idx & 7u) * 4u));
+              }
+            }
+            w_rec += r < v1;
+          }
+          wave_sync_lds();
+          const uint32_t nrec = min(kBitRecs, L.n_merge - c0);
+          for (uint32_t w0 = 0; w0 < kBitRecs / 8 && w0 * 8 < nrec; w0 += 64) {  // wave-uniform
+            const uint32_t w = w0 + lane;
+            const uint32_t word = w < kBitRecs / 8 ? (w < 128 ? tbl_lo[w] : tbl_hi[w - 128]) : 0u;
+            // the flagged records' own meta and identifier, four loads in flight per lane
+#pragma unroll
+            for (uint32_t i0 = 0; i0 < 8; i0 += 4) {
+              uint2 mi[4];  // (ident, meta) of SubRec
+#pragma unroll
+              for (uint32_t u = 0; u < 4; u++) {
+                mi[u] = make_uint2(0u, 0u);
+                if ((word >> ((i0 + u) * 4u)) & 15u) {
+                  const uint32_t k = L.n_direct + c0 + w * 8 + i0 + u;
+                  mi[u] = *reinterpret_cast<const uint2*>(&a.ix.subs[L.sub_off + k].ident);
+                }
+              }
+#pragma unroll
+              for (uint32_t u = 0; u < 4; u++) {
+                const uint32_t nib = (word >> ((i0 + u) * 4u)) & 15u;
+                const uint32_t rmeta = mi[u].y & kSlotMetaMask;
+                const bool idpos = (int32_t)mi[u].x > 0;
+                const bool nonbase = (nib & kBitNonBase) != 0;
+                uint32_t pmeta;
+                if (nonbase) {
+                  pmeta = rmeta | (idpos ? kRowIdent : kRowDrop);
+                } else {
+                  const uint32_t qv = (nib & kBitQos2) ? 2u : (nib & kBitQos1) ? 1u : 0u;
+                  pmeta = (rmeta & ~(kMetaQos | kMetaNoLocal)) | max(rmeta & kMetaQos, qv) | (rmeta & kMetaNoLocal) |
+                          ((nib & kBitNoLocal) ? kMetaNoLocal : 0u);
+                }
+                const uint32_t k = L.n_direct + c0 + w * 8 + i0 + u;
+                emit_patch(nib != 0 && pmeta != rmeta && !(exp_bits & 4u), xa << kSetRowBits | k, pmeta);
+                n_nonbase += __popcll(__ballot(nonbase));
+                n_ext += __popcll(__ballot(nonbase && idpos));
+              }
+            }
+          }
+          wave_sync_lds();  // (before the table is cleared again)
+        }
+      };
       // the node -> entry map again (after a fold took its place), for the partner-link path
       auto map_rebuild = [&]() __attribute__((always_inline)) {
         for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
@@ -944,11 +1028,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             if (mf) best = c0 + 63 - (uint32_t)__builtin_clzll(mf);
           }
           if (best > j0) {
+            if (a.work && lane == 0) {  // MQ_PROF_WORK: the fold's shape
+              unsigned long long* wc = a.work + (uint64_t)(t & (kPatchRegions - 1)) * kWork;
+              atomicAdd(wc + 10, (unsigned long long)(h_pre[wv][best] - h_pre[wv][j0]));
+              uint64_t nm = 0;
+              for (uint32_t j = j0; j < best; j++)
+                if (j == j0 || h_ga[wv][j] != h_ga[wv][j - 1]) nm += a.ix.lists[mg_node[wv][h_ga[wv][j]]].n_merge;
+              atomicAdd(wc + 14, (unsigned long long)nm);
+              atomicAdd(wc + 15, 1ull);
+            }
             fold_lists(j0, best);
             j0 = best;
           } else {
-            if (!map_ok) map_rebuild();
-            resolve_lists(j0, next);
+            if (a.work && lane == 0) {
+              unsigned long long* wc = a.work + (uint64_t)(t & (kPatchRegions - 1)) * kWork;
+              atomicAdd(wc + 11, (unsigned long long)(h_pre[wv][next] - h_pre[wv][j0]));
+              atomicAdd(wc + 12, 1ull);
+              atomicAdd(wc + 13, (unsigned long long)a.ix.lists[mg_node[wv][h_ga[wv][j0]]].n_merge);
+            }
+            if (!(exp_bits & 512u)) {
+              fold_big(j0, next);
+            } else {  // (MQ_OPT_SET_EXP bit 9: through the partner links, as before round 5)
+              if (!map_ok) map_rebuild();
+              resolve_lists(j0, next);
+            }
             j0 = next;
           }
         }

@@ -288,20 +288,50 @@ void* mqgen_retained(uint64_t n, uint64_t n_sys, uint64_t seed, int mix) {
   Vocab voc(seed);
   Rng r(seed + 3);
   Batch* out = new Batch();
-  std::unordered_set<std::string> seen;
-  while (out->s.size() < n + n_sys) {
-    std::vector<std::string> seg;
+  const uint64_t want = n + n_sys;
+  out->s.bytes.reserve(want * 48);
+  out->s.offs.reserve(want + 1);
+  out->handles.reserve(want);
+  // Exact de-duplication (same topics, same order as a set of strings would give): an
+  // open-addressing table of (hash tag, topic index + 1) over the batch's own bytes, load <= 1/2.
+  uint64_t cap = 1024;
+  while (cap < 2 * want) cap <<= 1;
+  std::vector<uint64_t> table(cap, 0);
+  auto hash = [](const char* p, size_t len) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ len;
+    for (size_t i = 0; i < len; i++) h = (h ^ (uint8_t)p[i]) * 0x100000001B3ull;
+    return h ^ (h >> 29);
+  };
+  std::string t;
+  while (out->s.size() < want) {
+    t.clear();
+    auto add = [&](const std::string& s) {
+      if (!t.empty()) t += '/';
+      t += s;
+    };
     if (out->s.size() < n_sys) {
-      seg = {"$SYS", "broker", voc.draw(2, r), voc.draw(3, r)};
+      add("$SYS"); add("broker"); add(voc.draw(2, r)); add(voc.draw(3, r));
     } else if (mix == 1) {
-      seg = {"dev", "r" + std::to_string(r.below(64)), "s" + std::to_string(r.below(4096)),
-             "d" + std::to_string((uint32_t)r.next()), "telemetry"};
+      add("dev"); add("r" + std::to_string(r.below(64))); add("s" + std::to_string(r.below(4096)));
+      add("d" + std::to_string((uint32_t)r.next())); add("telemetry");
     } else {
       int k = 2 + (int)r.below(7);
-      for (int l = 0; l < k; l++) seg.push_back(voc.draw(l, r));
+      for (int l = 0; l < k; l++) add(voc.draw(l, r));
     }
-    std::string t = join(seg);
-    if (!seen.insert(t).second) continue;
+    const uint64_t h = hash(t.data(), t.size());
+    const uint64_t tag = h & 0xFFFFFFFF00000000ull;
+    bool dup = false;
+    uint64_t i = h & (cap - 1);
+    for (;; i = (i + 1) & (cap - 1)) {
+      const uint64_t e = table[i];
+      if (!e) break;
+      if ((e & 0xFFFFFFFF00000000ull) != tag) continue;
+      const uint64_t k = (e & 0xFFFFFFFFull) - 1;
+      const uint64_t o = out->s.offs[k], len = out->s.offs[k + 1] - o;
+      if (len == t.size() && !memcmp(out->s.bytes.data() + o, t.data(), len)) { dup = true; break; }
+    }
+    if (dup) continue;
+    table[i] = tag | (out->s.size() + 1);
     out->s.push(t);
     out->handles.push_back(out->s.size());
   }

@@ -74,6 +74,7 @@ class SpanResult(C.Structure):
 
 
 SPANS_PICKED = 1  # MQ_SPANS_PICKED
+MQ_EINVAL, MQ_ENOMEM, MQ_ENODEV, MQ_EIO = -22, -12, -19, -5  # include/mqmatch.h return codes
 PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
 
 # mq_set_option: product options (include/mqmatch.h) and development ones (include/mqmatch_dev.h)
@@ -83,6 +84,8 @@ OPT_MSG_IMAGE, OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_MERGE_DEDUP = 8, 9, 10, 12
 OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC, OPT_FUSE_DESC, OPT_SET_EXP, OPT_MSG_EXPORT = 14, 15, 16, 17, 18, 19
 OPT_PATCH_CODES = 20
 OPT_MSG_EDGES = 21
+OPT_MSG_EDGE_BUDGET, OPT_FAIL_NEXT = 22, 23
+OPT_MAX = 23  # (include/mqmatch_dev.h MQ_OPT_MAX)
 
 
 class MsgResult(C.Structure):
@@ -100,7 +103,7 @@ class Stats(C.Structure):
                                            "shared", "inlines", "retained", "retained_live",
                                            "device_bytes", "upload_bytes_total", "syncs", "partners",
                                            "foreign")] + \
-               [("max_depth", C.c_uint32), ("reserved", C.c_uint32)]
+               [("max_depth", C.c_uint32), ("edge_load", C.c_uint32)]
 
 
 class KernelTime(C.Structure):
@@ -402,7 +405,7 @@ class Engine:
     def stats(self):
         s = Stats()
         _check(lib().mq_index_stats(self.h, C.byref(s)), "mq_index_stats")
-        return {n: getattr(s, n) for n, _ in Stats._fields_ if n != "reserved"}
+        return {n: getattr(s, n) for n, _ in Stats._fields_}
 
     def set_option(self, option, value):
         """mq_set_option (MQ_OPT_*)."""

@@ -166,11 +166,11 @@ def test_options_without_device():
     eng = E.Engine()
     eng.set_option(E.OPT_CHUNK_ROWS, 1 << 20)
     eng.set_option(E.OPT_PATCH_CAP, 1024)
-    eng.set_option(E.OPT_MSG_EDGES, 0)  # (the newest option: the range check admits it)
+    eng.set_option(E.OPT_MAX, 0)  # (the newest option: the range check admits it)
     with pytest.raises(E.EngineError):
         eng.set_option(99, 1)
     with pytest.raises(E.EngineError):
-        eng.set_option(E.OPT_MSG_EDGES + 1, 1)
+        eng.set_option(E.OPT_MAX + 1, 1)
 
 
 def test_edge_load_option():

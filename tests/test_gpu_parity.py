@@ -448,7 +448,7 @@ def test_spans_pipelined_batches(gpu_available):
     tb, to = W.gen_topics(w, 2000, seed=90)
     t0 = submit(tb, to)
     before = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0]
-    # (a plain update: mq_subscribe_bulk would wait for t0's result to be freed). A new client on
+    # (a plain update; mq_subscribe_bulk behaves the same: test_bulk_subscribe_beside_pipelined). A new client on
     # the root '#' list every topic gathers (its filter id is the workload's id of "#": ids name
     # filter strings)
     offs = w["offs"].astype(np.int64)
@@ -460,6 +460,41 @@ def test_spans_pipelined_batches(gpu_available):
     assert (engine_digests(wait(t0, 2000))[0] == before).all()
     assert (engine_digests(wait(t1, 2000))[0] == after).all()
     assert not (before == after).all()
+
+
+def test_bulk_subscribe_beside_pipelined(gpu_available):
+    """A restore (mq_subscribe_bulk) while pipelined tickets are outstanding does not wait for them
+    (submit k+1 waited for the bulk update, which waited for ticket k's result — a
+    deadlock). Run on a worker thread with a deadline: an empty index with a live ticket takes the
+    per-entry path; the ticket shows the index before, the next submit the index after, both
+    equal to the oracle; the bulk results equal the oracle's."""
+    import threading
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(30000, 3000, seed=95)
+    eng, orc = E.Engine(device=0), O.OracleIndex()
+    tb, to = W.gen_topics(w, 2000, seed=96)
+    out = {}
+
+    def body():
+        rc, t0 = _submit(eng, tb, to)
+        assert rc == 0
+        out["bulk"] = eng.subscribe_bulk(w)  # (the ticket's result is live: per-entry, copy-on-write)
+        rc, t1 = _submit(eng, tb, to)
+        assert rc == 0
+        out["r0"] = _wait(t0, 2000)
+        out["r1"] = _wait(t1, 2000)
+
+    th = threading.Thread(target=body, daemon=True)
+    th.start()
+    th.join(timeout=90)
+    assert not th.is_alive(), "bulk subscribe beside an outstanding ticket did not finish"
+    empty = O.OracleIndex().digest_batch(tb, to, nthreads=4)[0]
+    assert (out["bulk"] == orc.subscribe_bulk(w)).all()
+    full = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0]
+    assert out["r0"][0] == 0 and (engine_digests(out["r0"][1])[0] == empty).all()
+    assert out["r1"][0] == 0 and (engine_digests(out["r1"][1])[0] == full).all()
+    eng.check()
 
 
 def test_spans_device_matches_host(gpu_available):
@@ -499,13 +534,14 @@ def test_spans_device_matches_host(gpu_available):
 
 
 @pytest.mark.parametrize("exp,waves", [(0, 8), (16 | 128, 8), (32 | 128, 8), (64 | 128, 8), (0, 7), (0, 6),
-                                       (128, 8), (256, 8)])
+                                       (128, 8), (256, 8), (512, 8), (256 | 512, 8)])
 def test_set_pass_variants_exact(exp, waves, gpu_available):
     """The merge set pass's exact variants: the fold (default: records folded over their visits, no
     partner links), bit 7 (records resolved through their partner links), with bit 4 (a visit
     through a partner other than the record's first reads all its links) or bits 5 / 6 (3 / 4
     partner links per batch); bit 8 (fold chunks of 16 visits: many chunks per set, and merge
-    gathers beyond a chunk resolved through the links); 7 or 6 waves per SIMD
+    gathers beyond a chunk take the record-indexed bit fold); bit 9 (merge gathers too big for the
+    hash fold resolved through their partner links, as before round 5); 7 or 6 waves per SIMD
     (MQ_OPT_MERGE_WAVES): per-topic digests of device results equal the oracle's."""
     import torch
     from mqmatch import engine as E
@@ -615,13 +651,15 @@ def test_walk_trials_choose_and_stay_exact(gpu_available):
     d_to = torch.from_numpy(to.view(np.int64)).cuda()
     od, _, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
     eng.profile(True)
-    for _ in range(4):
+    for _ in range(8):  # (6 trial batches: one untimed per walk, then two timed per walk, ABBA)
         torch.cuda.synchronize()
         r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
         dg, _ = engine_digests(E.expand_device_spans(r, n))
         assert (dg == od).all()
     prof = eng.profile_read()
     assert "trial_frontier_ps_per_topic" in prof and "trial_thread_ps_per_topic" in prof, sorted(prof)
+    assert prof["trial_frontier_batches"][0] == 2 and prof["trial_thread_batches"][0] == 2
+    assert ("trial_chose_thread" in prof) != ("trial_chose_frontier" in prof)
 
 
 def test_walk_trials_rearm_on_wildcard_mix(gpu_available):
@@ -652,15 +690,16 @@ def test_walk_trials_rearm_on_wildcard_mix(gpu_available):
             assert (dg == od).all()
         return eng.profile_read()
 
-    prof = batches(w, 93, 3)
+    prof = batches(w, 93, 6)
     assert "trial_frontier_ps_per_topic" in prof and "trial_thread_ps_per_topic" in prof, sorted(prof)
+    assert ("trial_chose_thread" in prof) != ("trial_chose_frontier" in prof)
     prof = batches(w, 94, 2)
     assert "trial_frontier_ps_per_topic" not in prof  # same index: the choice stays
     nodes0 = eng.stats().get("nodes")
     assert (eng.subscribe_bulk(w2) == orc.subscribe_bulk(w2)).all()
     nodes1 = eng.stats().get("nodes")
     assert nodes0 is None or nodes1 < 2 * nodes0  # (not a new size: a new mix)
-    prof = batches(w2, 95, 3)
+    prof = batches(w2, 95, 6)
     assert "trial_frontier_ps_per_topic" in prof and "trial_thread_ps_per_topic" in prof, sorted(prof)
 
 
@@ -969,6 +1008,96 @@ def test_messages_workload_parity(image, spec_mb, edges, gpu_available):
         assert d == od[i], i
 
 
+def test_messages_edge_table_tiers(gpu_available):
+    """The retained image's edge table at each of its size tiers (device.cpp build_image: at most
+    1/16 full within the budget, 1/8 within 4x the budget, else ~1/4 or denser). The product budget
+    (8 GiB) is only exceeded at config 5's full size, so MQ_OPT_MSG_EDGE_BUDGET lowers it here until
+    the table takes each sparser fallback; every tier's Messages equal the oracle's, and the table
+    shrinks from tier to tier (topics.go:530-579)."""
+    from mqmatch import workload as W
+    from mqmatch import engine as E
+    from digest import fold, SEED
+    rb, ro, hd, rh = W.gen_retained(200000, n_sys=1000, seed=65)
+    fb, fo = W.gen_msg_filters(rh, 6000, seed=66)
+    orc = O.OracleIndex()
+    orc.retain_bulk(rb, ro, hd)
+    od, ocnt, _ = orc.messages_digest_batch(fb, fo)
+
+    def run(budget_mb):
+        eng = E.Engine()
+        if budget_mb is not None:
+            eng.set_option(E.OPT_MSG_EDGE_BUDGET, budget_mb)
+        eng.retain_bulk(rb, ro, hd)
+        eng.profile(True)
+        base, count, hs = eng.messages_batch(fb, fo)
+        p = eng.profile_read()
+        assert (count == ocnt).all(), budget_mb
+        dg = O.handle_digests(base, count, hs)
+        assert (dg == od).all(), budget_mb
+        return p["msg_edge_slots"][0], p["msg_edge_particles"][0]
+
+    slots16, lo = run(None)
+    assert slots16 >= 16 * lo
+    full_mb = slots16 * 32 >> 20  # (32 B per slot)
+    slots8, _ = run(full_mb // 2)  # over the 1/16 budget, within 4x of it: the 1/8 tier
+    assert slots8 == slots16 // 2 and slots8 < 16 * lo
+    slots4, _ = run(max(1, full_mb // 16))  # over 4x the budget too: ~1/4
+    assert slots4 <= slots8 // 2 and slots4 >= 2 * lo
+    slots_min, _ = run(1)  # the densest table the loop allows (load < 1/2)
+    assert slots_min <= slots4 and slots_min > 2 * lo
+
+
+def _submit(eng, tb, to):
+    import ctypes as C
+    from mqmatch import engine as E
+    t = C.c_void_p()
+    rc = E.lib().mq_match_spans_submit(eng.h, E._p(tb, E._u8p), E._p(to, E._u64p), len(to) - 1, C.byref(t))
+    return rc, t
+
+
+def _wait(t, n):
+    import ctypes as C
+    from mqmatch import engine as E
+    rp = C.POINTER(E.SpanResult)()
+    rc = E.lib().mq_match_spans_wait(t, C.byref(rp))
+    return rc, (E._expand_host_spans(rp, n) if rc == 0 else None)
+
+
+@pytest.mark.parametrize("inline", [True, False])
+def test_pipelined_submit_fails_then_recovers(inline, gpu_available):
+    """A pipelined submit whose batch fails (MQ_OPT_FAIL_NEXT: as if a kernel guard tripped) returns
+    MQ_EIO and arms no copy into the freed result: the batch submitted before it still waits to its
+    exact result, and later submits and waits are exact. inline=True: an index with an inline
+    subscription (batches are not one-sync: the error is read at the batch's end, after its result
+    was packed); False: one-sync batches (a copy armed before the error check)."""
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w, eng, orc = _workload_pair(40000, 3000, seed=91)
+    if inline:
+        assert eng.inline_subscribe("#", 7, 1 << 30) == bool(orc.inline_subscribe("#", 7, filter_id=1 << 30))
+    batches = [W.gen_topics(w, 3000, seed=92 + i) for i in range(4)]
+    want = [orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0] for tb, to in batches]
+    rc, t0 = _submit(eng, *batches[0])
+    assert rc == 0
+    eng.set_option(E.OPT_FAIL_NEXT, 1)
+    rc, t1 = _submit(eng, *batches[1])
+    assert rc == E.MQ_EIO and not t1
+    rc, r0 = _wait(t0, 3000)  # (its copy was issued by the failed submit's flush)
+    assert rc == 0 and (engine_digests(r0)[0] == want[0]).all()
+    rc, t2 = _submit(eng, *batches[2])
+    assert rc == 0
+    rc, t3 = _submit(eng, *batches[3])
+    assert rc == 0
+    for t, k in ((t2, 2), (t3, 3)):
+        rc, r = _wait(t, 3000)
+        assert rc == 0 and (engine_digests(r)[0] == want[k]).all(), k
+    # a failure with no batch before it, then a plain host match
+    eng.set_option(E.OPT_FAIL_NEXT, 1)
+    rc, _ = _submit(eng, *batches[1])
+    assert rc == E.MQ_EIO
+    _digest_parity(eng, orc, *batches[1], fmts=("spans",))
+
+
 @pytest.mark.parametrize("fmt", FORMATS)
 def test_gather_slot_overflow(fmt, gpu_available):
     """A topic matching > 64 particles overflows its count-pass gather slots and takes the
@@ -1005,6 +1134,49 @@ def test_many_merging_clients(fmt, gpu_available):
     topics = ["o/p", "o/q", "o", "o/z", "o/p/x"]
     for t, g in zip(topics, e.subscribers_batch(topics)):
         assert g == o.subscribers(t), t
+
+
+@pytest.mark.parametrize("exp", [0, 512])
+def test_set_pass_big_gathers(exp, gpu_available):
+    """Merge gathers far beyond the set pass's hash fold: 5,000 clients on "o/#" (more may-merge
+    records than one pass of the bit fold holds, kBitRecs = 2048) with partners at "o/p", "o/+",
+    "+/p" and "o/p/#" (Qos 0-2, NoLocal, identifiers 0-4), next to clients with one filter; topics
+    that gather every subset of them. Device and host span results equal the oracle's (exp 512: the
+    partner-link path the bit fold replaced)."""
+    import random as R
+    import torch
+    from mqmatch import engine as E
+    rng = R.Random(97)
+    e, o = EngineAdapter("spans"), OracleAdapter()
+    e.x.engine.set_option(E.OPT_SET_EXP, exp)
+    for i in range(5000):
+        c = f"m{i}"
+        for f in ("o/#", "o/p", "o/+", "+/p", "o/p/#"):
+            if f != "o/#" and rng.random() < 0.35:
+                continue
+            q, ident, nl = rng.randrange(3), rng.randrange(5), rng.random() < 0.2
+            assert e.subscribe(c, f, qos=q, identifier=ident, no_local=nl) == o.subscribe(c, f, qos=q, identifier=ident,
+                                                                                        no_local=nl)
+    for i in range(500):
+        assert e.subscribe(f"s{i}", "o/#") == o.subscribe(f"s{i}", "o/#")
+    topics = ["o/p", "o/q", "o", "x/p", "o/p/x", "o/p/x/y"] * 20
+    for t, g in zip(topics, e.subscribers_batch(topics)):
+        assert g == o.subscribers(t), t
+    # device results of a batch large enough for the one-sync path (merge sets formed over it)
+    from mqmatch import workload as W
+    raw, offs = E.pack_strings(topics * 600)
+    n = len(offs) - 1
+    d_tb = torch.from_numpy(np.concatenate([raw, np.zeros(16, np.uint8)])).cuda()
+    d_to = torch.from_numpy(offs.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    # (digests name clients and filters by the adapter's ids: compare through the same adapter)
+    want = {t: canonical(o.subscribers(t)) for t in set(topics)}
+    r = e.x.engine.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
+    res = E.expand_device_spans(r, n)
+    got = e.x._rebuild(res, 0)  # (first topic through the mirror's rematerialisation)
+    assert canonical(got) == want[topics[0]]
+    for i in range(0, n, 997):
+        assert canonical(e.x._rebuild(res, i)) == want[(topics * 600)[i]], i
 
 
 @pytest.mark.parametrize("fmt", FORMATS)

@@ -63,7 +63,7 @@ def test_headline_10m_subscriptions(config3, gpu_available):
     d_tb = torch.from_numpy(tb).cuda()
     d_to = torch.from_numpy(to.view(np.int64)).cuda()
     torch.cuda.synchronize()
-    runs = [("trial 1", None), ("trial 2", None), ("chosen walk", None),
+    runs = [(f"trial {k + 1}", None) for k in range(6)] + [("chosen walk", None),
             ("frontier walk + fused desc", 16), ("walk thread per topic", 0)]
     for what, group in runs:
         if group is not None:
