@@ -544,12 +544,19 @@ def main():
     eng.profile(True)
     eng.profile_reset()
     calibration = 0
+    trial_prof = {}
     if args.format == "spans" and n >= WALK_TRIAL_MIN:
-        for _ in range(WALK_TRIAL_BATCHES):
+        for _ in range(2 * WALK_TRIAL_BATCHES):  # (a batch whose one-sync buffers overflowed repeats its trial)
             step()
             calibration += 1
+            torch.cuda.synchronize()
+            for k, v in eng.profile_read().items():
+                if k.startswith("trial_"):  # (summed over the batches: the profile is reset after each)
+                    trial_prof[k] = (trial_prof.get(k, (0, 0.0))[0] + v[0], 0.0)
+            if any(k.startswith("trial_chose_") for k in trial_prof):
+                break
+            eng.profile_reset()
     torch.cuda.synchronize()
-    trial_prof = eng.profile_read()
     eng.profile(False)
     walk_trials = {k: v[0] for k, v in trial_prof.items() if k.startswith("trial_")}
     for k in ("trial_frontier_ps_per_topic", "trial_thread_ps_per_topic"):

@@ -132,6 +132,11 @@ int mq_retained_set(mq_index* idx, const char* topic, uint32_t tlen, uint64_t ha
 /* TopicsIndex.Retained.Len() (server.go:980) */
 uint64_t mq_retained_len(const mq_index* idx);
 
+/* Set up the calling thread's HIP runtime state for the index's device (a thread's first HIP calls
+ * cost ~10 ms). Optional: every matching call does it before taking the index's lock; a caller
+ * may do it ahead on the threads that will match. */
+int mq_thread_warm(mq_index* idx);
+
 /* Columnar bulk Subscribe for the restore path (server.go:1624-1640): n filters as
  * concatenated bytes + n+1 u64 offsets. out_new (nullable) receives Subscribe's results. An empty
  * index with no live host result is built in parallel; otherwise the entries are applied one by

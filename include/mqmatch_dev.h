@@ -35,7 +35,10 @@
                                      link path: with bit 7); bit 7 (exact) records resolved through their
                                      partner links instead of the fold; bit 8 (exact) fold chunks of 16
                                      visits; bit 9 (exact) merge gathers too big for the hash fold resolved through
-                                     their partner links instead of the record-indexed bit fold (round 5) */
+                                     their partner links instead of the record-keyed fold (round 5); bits 10 / 11
+                                     (exact) that fold for merge gathers of up to two passes / any number of
+                                     passes over their visits (default: one pass, kBigFill visits); bit 13
+                                     (exact) k_merge's set pass instead of k_set (round 5) */
 #define MQ_OPT_PATCH_CODES 20     /* host span results: 1 (default) 4-byte patch codes when the index allows them
                                      (MQ_SPANS_PATCH_CODES); 0: 8-byte mq_patch records */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than

@@ -51,6 +51,7 @@ struct mq_index {
   mq_config cfg;
   std::unique_ptr<Index> ix;
   std::unique_ptr<Device> dev;
+  std::atomic<bool> dev_ready{false};  // dev exists (read without the lock: thread warm-up)
   int profile = 0;  // MQ_PROF_*
 
   std::vector<std::pair<uint32_t, uint64_t>> options;  // mq_set_option, in call order
@@ -62,6 +63,7 @@ struct mq_index {
       dev->prof.enable(profile != 0, (profile & MQ_PROF_WORK) != 0);
       dev->set_select_shared((cfg.flags & MQ_CFG_SELECT_SHARED) != 0);
       for (auto& o : options) dev->set_option(o.first, o.second);
+      dev_ready.store(true, std::memory_order_release);
     }
     return *dev;
   }
@@ -104,10 +106,31 @@ int fail(int code, const std::string& msg) {
 // takes the per-entry path while a result is live); kPin: publishes a host span result.
 enum class Access { kRead, kUpdate, kPin };
 
+// The calling thread's HIP runtime state for device dev, set up once per thread: a thread's first
+// HIP calls cost ~10 ms, which a match must not pay while it holds the handle
+// lock that updates wait for. (The Go batching stage also keeps its loop on one OS thread.)
+void thread_warm(int dev) {
+  static thread_local int warmed = -1;
+  if (warmed == dev) return;
+  if (hipSetDevice(dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+    (void)hipEventRecord(e, nullptr);
+    (void)hipEventSynchronize(e);
+    (void)hipEventDestroy(e);
+  }
+  (void)hipGetLastError();
+  warmed = dev;
+}
+
 // Runs f under the handle's lock (IndexLock).
 template <class F>
 int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
   if (!idx) return fail(MQ_EINVAL, "null index");
+  if (access != Access::kUpdate && idx->dev_ready.load(std::memory_order_acquire)) thread_warm(idx->cfg.device);
   IndexLock& L = *idx->lk;
   ViewTracker& V = L.views;
   struct Announce {  // an update's announcement, withdrawn however the call ends
@@ -150,6 +173,12 @@ bool bad_str(const void* p, uint32_t len) { return p == nullptr && len != 0; }
 extern "C" {
 
 uint32_t mq_abi_version(void) { return MQ_ABI_VERSION; }
+
+int mq_thread_warm(mq_index* idx) {
+  if (!idx) return fail(MQ_EINVAL, "null index");
+  thread_warm(idx->cfg.device);
+  return 0;
+}
 const char* mq_last_error(void) { return g_err.c_str(); }
 
 int mq_index_create(const mq_config* cfg, mq_index** out) {

@@ -1466,7 +1466,12 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       // persistent waves striding over the list
       const uint32_t set_blocks = set_grid_ ? std::max<uint32_t>(1, (uint32_t)((sb_.n_sets + 3) / 4))
                                             : (merge_blocks_ ? merge_blocks_ : n_cus_ * 8);
-      launch_merge(a, true, merge_wpe, set_blocks, s);
+      // k_set (sets.hip) unless the index is sharded (rank keys), a measurement variant of k_merge's
+      // set pass is asked for (MQ_OPT_SET_EXP bit 7, the attribution bits 0-4), or bit 13
+      if (!ix.sharded() && !(set_exp_ & (0x1Fu | 128u | 8192u)) && merge_wpe == kMergeWavesPerEU)
+        launch_set(a, set_blocks, s);
+      else
+        launch_merge(a, true, merge_wpe, set_blocks, s);
       prof.end("merge_sets", s);
       hip_check(hipGetLastError(), "k_merge<spans> (sets)");
       if (one_sync) break;  // a reservation past its region sets *unsafe (read at the end)
@@ -1681,6 +1686,11 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     prof.count("merge_big_nmerge", sum[13]);
     prof.count("merge_fold_nmerge", sum[14]);
     prof.count("merge_fold_chunks", sum[15]);
+    static const char* const kBig[4] = {"192", "384", "1024", "more"};
+    for (int b = 0; b < 4; b++) {
+      prof.count((std::string("merge_big_gathers_v") + kBig[b]).c_str(), sum[16 + b]);
+      prof.count((std::string("merge_big_visits_v") + kBig[b]).c_str(), sum[20 + b]);
+    }
     prof.count("merge_topics", n);
   }
   // A pipelined copy is armed (pc_) only when the batch has passed its error check: a batch that

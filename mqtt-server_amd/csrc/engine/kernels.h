@@ -40,18 +40,22 @@ constexpr uint32_t kFoldCap = kFoldSlots * 3 / 4;
 constexpr uint32_t kFoldNonBase = 1u << 13;  // a visit's partner comes before the record
 constexpr uint32_t kFoldNoLocal = 1u << 14;  // a partner has NoLocal
 constexpr uint32_t kFoldQos0 = 1u << 15;     // bit 15 + q: a partner has Qos q
-// The set pass's fold of a merge gather too big for the hash fold (merge.hip fold_big): 4 bits per
-// record of g's may-merge slots, kBitRecs records per pass (256 words: the map's LDS)
-constexpr uint32_t kBitRecs = 2 * kMapSlots * 8;
+// The set pass's fold of a merge gather too big for the hash fold (merge.hip fold_big): one word per
+// visited record, (k + 1) << 5 | kBit*, kBigSlots of them in the map's LDS (keys and values) and
+// the merge gathers' three kPairMax arrays, at most kBigFill visits per pass
+constexpr uint32_t kBigSlots = 2 * kMapSlots + 3 * kPairMax;
+constexpr uint32_t kBigFill = kBigSlots * 3 / 4;
 constexpr uint32_t kBitNonBase = 1u, kBitNoLocal = 2u, kBitQos1 = 4u, kBitQos2 = 8u;
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
-constexpr uint32_t kWork = 16;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
+constexpr uint32_t kWork = 24;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
                                 // [8] topics the kernel resolved, [9] bytes of their maps' sources read;
                                 // set pass fold: [10] visits folded, [11] visits of merge gathers too big
                                 // to fold, [12] those gathers, [13] their may-merge records (n_merge),
-                                // [14] records of the folded chunks' gathers, [15] folded chunks
+                                // [14] records of the folded chunks' gathers, [15] folded chunks;
+                                // [16..19] the big gathers by visits (<= 192, <= 384, <= 1024, more),
+                                // [20..23] their visits
 constexpr uint32_t kMergeWavesPerEU = 8;  // k_merge<spans> register budget: 1 (none), 6 or 8 waves per SIMD
 
 // Device pointers of the resident index image.
@@ -315,6 +319,9 @@ struct XSigArgs {
   struct GDesc* desc;
 };
 void launch_xsig(const XSigArgs& a, hipStream_t s);
+// The merge set pass of an index that is not sharded (sets.hip): k_merge<spans, SET>'s results with
+// only the set pass's code; a.rep_list / a.n_reps / a.sets / a.spatches as k_merge's dd_phase 1.
+void launch_set(const EmitArgs& a, uint32_t blocks, hipStream_t s);
 
 // Batched auth.MatchTopic (k_acl).
 struct AclArgs {

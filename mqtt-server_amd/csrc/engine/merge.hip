@@ -458,16 +458,20 @@ __device__ __forceinline__ uint64_t gdesc_rank(const GDesc& d) {
 template <bool SPANS, bool XS, int WPE, bool SET = false, uint32_t PB = kPartBatch>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
-  __shared__ uint32_t map_key[4][kMapSlots];   // gathered node with may-merge records (or
-                                               //   kForeign | fid: another shard's, XS)
-  __shared__ uint32_t map_val[4][kMapSlots];   // its entry below
+  // per-wave words, one contiguous block (the set pass's record-keyed fold spans the map and the
+  // merge gathers' three arrays): the map (gathered node with may-merge records, or kForeign | fid
+  // of another shard's, XS -> its entry below), then per merge gather the output row of its first
+  // record (pair slots name a record by its place k in the particle's list) and its pair-block hash
+  // table (NodePair)
+  __shared__ uint32_t wsm[4][2 * kMapSlots + 3 * kPairMax];
+  uint32_t* const map_key = wsm[wave_id()];
+  uint32_t* const map_val = map_key + kMapSlots;
+  uint32_t* const mg_row = map_key + 2 * kMapSlots;
+  uint32_t* const mg_eoff = mg_row + kPairMax;
+  uint32_t* const mg_emask = mg_eoff + kPairMax;
   __shared__ uint32_t mg_node[4][kEnt];        // entries: the topic's merge gathers in gather
   __shared__ uint32_t mg_gi[4][kEnt];          //   order (node, gather index), then (XS) the
   __shared__ uint64_t mg_rank[4][XS ? kEnt : 1];  // other shards' (kForeign | fid, kNone, rank)
-  __shared__ uint32_t mg_row[4][kPairMax];     //   output row of its first record (pair slots name
-                                               //   a record by its place k in the particle's list),
-  __shared__ uint32_t mg_eoff[4][kPairMax];    //   its pair-block hash table (NodePair)
-  __shared__ uint32_t mg_emask[4][kPairMax];
   __shared__ uint32_t h_ga[4][kHitMax];        // staged hit lists: merge gather of g,
   __shared__ uint32_t h_off[4][kHitMax];       //   pair-list offset,
   __shared__ uint32_t h_hb[4][kHitMax];        //   partner h's entry (mg_node[h_hb]: its node),
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   auto rank_of = [](const GDesc& d) { return gdesc_rank<XS>(d); };
   // MQ_OPT_SET_EXP: the exact variants (bit 7: partner links instead of the fold, bit 8: small fold
   // chunks) in every build; the attribution bits 0-4 in development builds only
-  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (128u | 256u | 512u));
+  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (128u | 256u | 512u | 1024u | 2048u));
   // persistent: a.merge grid's waves stride over the chunk's topics (wave-uniform loop)
   // (dedup's set pass: the waves stride over the list of set representatives instead; its topic
   // pass after k_finish: over the topics k_finish left)
@@ -590,21 +594,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // gather index (the same order); a topic with more than kPairMax of them has GDesc records
     const uint32_t lc = (SPANS && a.mlist) ? a.mcount[t] : kNone;
     if (lc <= kPairMax) {
-      for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
+      for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[q] = kNone;
       wave_sync_lds();
       if (lane < lc) {
         const uint64_t k = (uint64_t)t * kPairMax + lane;
         const uint32_t node = a.mlist[k];
         const uint2 P = a.mpair[k];
         uint32_t sl = hash32(node) & (kMapSlots - 1);
-        while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
-        map_val[wv][sl] = lane;
+        while (atomicCAS(&map_key[sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
+        map_val[sl] = lane;
         mg_node[wv][lane] = node;
         mg_gi[wv][lane] = lane;
         if (XS) mg_rank[wv][lane] = a.mrank[k];
-        mg_row[wv][lane] = a.mrow[k];
-        mg_eoff[wv][lane] = P.x;
-        mg_emask[wv][lane] = P.y;
+        mg_row[lane] = a.mrow[k];
+        mg_eoff[lane] = P.x;
+        mg_emask[lane] = P.y;
       }
       n_map = lc;
       w_map = (XS ? 24u : 16u) * lc;
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (lane == 0) atomicOr(a.unsafe, kUnsafeDesc);
       continue;
     }
-    for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
+    for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[q] = kNone;
     wave_sync_lds();
     w_map = (uint32_t)sizeof(GDesc) * n_g;
     for (uint32_t i0 = 0; i0 < n_g; i0 += 64) {
@@ -635,14 +639,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const uint32_t x = n_map + prefix_before(bi);
       if (ins && x < kPairMax) {
         uint32_t sl = hash32(node) & (kMapSlots - 1);
-        while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
-        map_val[wv][sl] = x;
+        while (atomicCAS(&map_key[sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
+        map_val[sl] = x;
         mg_node[wv][x] = node;
         mg_gi[wv][x] = i;
         if (XS) mg_rank[wv][x] = rank_of(gd[i]);
-        mg_row[wv][x] = mrow;
-        mg_eoff[wv][x] = P.ent_off;
-        mg_emask[wv][x] = P.ent_mask;
+        mg_row[x] = mrow;
+        mg_eoff[x] = P.ent_off;
+        mg_emask[x] = P.ent_mask;
       }
       n_map += __popcll(bi);
     }
@@ -660,8 +664,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const XEnt e = src.xent[k];
           const uint32_t key = kForeign | e.fid;
           uint32_t sl = hash32(key) & (kMapSlots - 1);
-          while (atomicCAS(&map_key[wv][sl], kNone, key) != kNone) sl = (sl + 1) & (kMapSlots - 1);
-          map_val[wv][sl] = x;
+          while (atomicCAS(&map_key[sl], kNone, key) != kNone) sl = (sl + 1) & (kMapSlots - 1);
+          map_val[sl] = x;
           mg_node[wv][x] = key;
           mg_gi[wv][x] = kNone;
           if (XS) mg_rank[wv][x] = e.rank;
@@ -689,9 +693,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (!slow) {
         uint32_t sl = hash32(h) & (kMapSlots - 1);
         for (;;) {
-          const uint32_t k = map_key[wv][sl];
+          const uint32_t k = map_key[sl];
           if (k == h) {
-            const uint32_t y = map_val[wv][sl];
+            const uint32_t y = map_val[sl];
             return Pos{XS ? mg_rank[wv][y] : 0ull, mg_gi[wv][y], true};
           }
           if (k == kNone) return Pos{0, kNone, false};
@@ -822,7 +826,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // latency, not two (two rounds, with the next round's first links in flight too, spilled
       // registers and was slower: 1.15 -> 1.36 ms at 8 waves per SIMD, 1.24 ms at 6;
       // profiles/r03/s2_hostsets/)
-      auto resolve_lists = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
+      // (pp, PP): only the records with hash32(k) % PP == pp (fold_big's partitions)
+      auto resolve_lists = [&](uint32_t j0, uint32_t j1, uint32_t pp = 0, uint32_t PP = 1) __attribute__((always_inline)) {
         const uint32_t v0 = h_pre[wv][j0], v1 = h_pre[wv][j1];
         uint32_t jj_next = j0;
         PairSlot e_next = locate(v0 + lane, j0, j1, jj_next);
@@ -833,7 +838,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           if (r0 + 64 < v1) e_next = locate(r0 + 64 + lane, j0, j1, jj_next);  // wave-uniform
           const uint32_t xa = h_ga[wv][jj];
           w_rec += r < v1;
-          resolve(r < v1, e.meta, setrel ? (xa << kSetRowBits | e.k) : mg_row[wv][xa] + e.k,
+          resolve(r < v1 && (PP == 1 || hash32(e.k) % PP == pp), e.meta, setrel ? (xa << kSetRowBits | e.k) : mg_row[xa] + e.k,
                   XS ? mg_rank[wv][xa] : 0ull, mg_gi[wv][xa], mg_node[wv][h_hb[wv][jj]], e.mp_off, e.mp_cnt);
         }
       };
@@ -853,8 +858,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // patch per record. Lists [j0, j1) hold whole merge gathers (a record's visits are all in
       // its g's lists) and at most kFoldCap visits.
       auto fold_lists = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
-        uint32_t* __restrict__ f_key = map_key[wv];  // (the table takes the map's place: the fold
-        uint32_t* __restrict__ f_val = map_val[wv];  //  does not look nodes up; map_rebuild restores it)
+        uint32_t* __restrict__ f_key = map_key;  // (the table takes the map's place: the fold
+        uint32_t* __restrict__ f_val = map_val;  //  does not look nodes up; map_rebuild restores it)
         const uint32_t v0 = h_pre[wv][j0], v1 = h_pre[wv][j1];
         for (uint32_t q = lane; q < kFoldSlots; q += 64) {
           f_key[q] = kNone;
@@ -876,15 +881,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             const bool earlier = before(XS ? mg_rank[wv][hb] : 0ull, mg_gi[wv][hb], XS ? mg_rank[wv][xa] : 0ull,
                                         mg_gi[wv][xa]);
             const uint32_t key = xa << kSetRowBits | e.k;
-            uint32_t sl = hash32(key) & (kFoldSlots - 1);
-            for (;;) {
-              const uint32_t prev = atomicCAS(&f_key[sl], kNone, key);
-              if (prev == kNone || prev == key) break;
-              sl = (sl + 1) & (kFoldSlots - 1);
+            if (!(exp_bits & 4096u)) {  // (MQ_OPT_SET_EXP bit 12, development builds: no table inserts)
+              uint32_t sl = hash32(key) & (kFoldSlots - 1);
+              for (;;) {
+                const uint32_t prev = atomicCAS(&f_key[sl], kNone, key);
+                if (prev == kNone || prev == key) break;
+                sl = (sl + 1) & (kFoldSlots - 1);
+              }
+              const uint32_t pm = e.meta >> kSlotPartShift;  // the partner's Qos | NoLocal << 2
+              atomicOr(&f_val[sl], (e.meta & kSlotOwnMask) | (earlier ? kFoldNonBase : 0u) |
+                                       ((pm & 4u) ? kFoldNoLocal : 0u) | (kFoldQos0 << (pm & 3u)));
             }
-            const uint32_t pm = e.meta >> kSlotPartShift;  // the partner's Qos | NoLocal << 2
-            atomicOr(&f_val[sl], (e.meta & kSlotOwnMask) | (earlier ? kFoldNonBase : 0u) |
-                                     ((pm & 4u) ? kFoldNoLocal : 0u) | (kFoldQos0 << (pm & 3u)));
           }
           w_rec += r < v1;
         }
@@ -908,102 +915,119 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         wave_sync_lds();  // (before the table is cleared again)
       };
+      // the node -> entry map again (after a fold took its place), for the partner-link path
+      auto map_rebuild = [&]() __attribute__((always_inline)) {
+        for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[q] = kNone;
+        wave_sync_lds();
+        for (uint32_t x = lane; x < n_ent; x += 64) {
+          const uint32_t node = mg_node[wv][x];
+          uint32_t sl = hash32(node) & (kMapSlots - 1);
+          while (atomicCAS(&map_key[sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
+          map_val[sl] = x;
+        }
+        wave_sync_lds();
+        map_ok = true;
+      };
       // A merge gather whose lists hold more visits than the hash fold's chunk (the hot lists: root
-      // '#', '+/...', 'x/#'): the same fold, over a table indexed by the record's place in g's list
-      // instead of a hash — 4 bits per record (kBitNonBase: a visit's partner comes before g;
-      // kBitNoLocal; kBitQos1 / 2: a partner's Qos), kBitRecs records per pass, in the map's LDS —
-      // so it holds any number of visits. A list of more records takes several passes over the
-      // visits, each folding the records of its range. The emission reads each flagged record's own
-      // meta and identifier from the pool (the table has no room for them). No partner links.
+      // '#', '+/...', 'x/#': ~10k may-merge records, ~200 of them visited per set): the same fold,
+      // keyed by the record's place k in g's list alone (one gather), so a table entry is one word
+      // — (k + 1) << 5 | kBit* — and kBigSlots of them fit in the map's LDS plus the merge gathers'
+      // pair-block and row arrays (free once the pair analysis is done: the set pass names rows
+      // set-relatively). The record's own meta and identifier are read from the pool at the
+      // emission (one load per folded record, a group of rounds in flight), not carried in the
+      // table. The caller folds a gather this way only while one pass holds its visits (more passes,
+      // over partitions hash(k) mod P, each re-read every visit and cost more than the partner
+      // links: profiles/r05/c/); a partition that still overflows the table resolves through the
+      // links. No partner links otherwise.
       auto fold_big = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
-        uint32_t* __restrict__ tbl_lo = map_key[wv];  // words [0, 128)
-        uint32_t* __restrict__ tbl_hi = map_val[wv];  // words [128, 256)
+        auto slot_ptr = [&](uint32_t q) __attribute__((always_inline)) -> uint32_t* { return map_key + q; };
         map_ok = false;
         const uint32_t xa = h_ga[wv][j0];
-        const NodeLists L = a.ix.lists[mg_node[wv][xa]];
+        const uint32_t sub_off = a.ix.lists[mg_node[wv][xa]].sub_off;
         const uint32_t v0 = h_pre[wv][j0], v1 = h_pre[wv][j1];
         const uint64_t rg = XS ? mg_rank[wv][xa] : 0ull;
         const uint32_t gg = mg_gi[wv][xa];
-        for (uint32_t c0 = 0; c0 < L.n_merge; c0 += kBitRecs) {  // wave-uniform
-          for (uint32_t q = lane; q < kBitRecs / 8; q += 64) {
-            if (q < 128) tbl_lo[q] = 0u;
-            else tbl_hi[q - 128] = 0u;
-          }
+        // the partitions: the records with hash(k) % PP == pp
+        const uint32_t PP = max(1u, (v1 - v0 + kBigFill - 1) / kBigFill);
+        for (uint32_t pp = 0; pp < PP; pp++) {  // wave-uniform
+          for (uint32_t q = lane; q < kBigSlots; q += 64) *slot_ptr(q) = 0u;
           uint32_t jj_next = j0;
           PairSlot e_next = locate(v0 + lane, j0, j1, jj_next);
           wave_sync_lds();
+          bool over = false;
           for (uint32_t r0 = v0; r0 < v1; r0 += 64) {
             const uint32_t r = r0 + lane;
             const uint32_t jj = jj_next;
             const PairSlot e = e_next;
             if (r0 + 64 < v1) e_next = locate(r0 + 64 + lane, j0, j1, jj_next);  // wave-uniform
-            const uint32_t idx = e.k - L.n_direct - c0;
-            if (r < v1 && idx < kBitRecs) {
+            const uint32_t hk = hash32(e.k);
+            if (r < v1 && hk % PP == pp) {
               const uint32_t hb = h_hb[wv][jj];
               const bool earlier = before(XS ? mg_rank[wv][hb] : 0ull, mg_gi[wv][hb], rg, gg);
               const uint32_t pm = e.meta >> kSlotPartShift;  // the partner's Qos | NoLocal << 2
               const uint32_t bits = (earlier ? kBitNonBase : 0u) | ((pm & 4u) ? kBitNoLocal : 0u) |
                                     ((pm & 3u) == 1u ? kBitQos1 : 0u) | ((pm & 3u) == 2u ? kBitQos2 : 0u);
-              if (bits) {
-                const uint32_t w = idx >> 3;
-                atomicOr(w < 128 ? &tbl_lo[w] : &tbl_hi[w - 128], bits << ((idx & 7u) * 4u));
+              const uint32_t key = (e.k + 1u) << 5;
+              uint32_t sl = (hk >> 8) % kBigSlots;
+              bool placed = (exp_bits & 4096u) != 0;  // (bit 12: no table inserts)
+              for (uint32_t probes = 0; !placed && probes < kBigSlots; probes++) {
+                const uint32_t prev = atomicCAS(slot_ptr(sl), 0u, key | bits);
+                if (prev == 0u) {
+                  placed = true;
+                  break;
+                }
+                if ((prev & ~31u) == key) {
+                  if (bits & ~prev) atomicOr(slot_ptr(sl), bits);
+                  placed = true;
+                  break;
+                }
+                sl = sl + 1 == kBigSlots ? 0u : sl + 1;
               }
+              over |= !placed;
             }
             w_rec += r < v1;
           }
           wave_sync_lds();
-          const uint32_t nrec = min(kBitRecs, L.n_merge - c0);
-          for (uint32_t w0 = 0; w0 < kBitRecs / 8 && w0 * 8 < nrec; w0 += 64) {  // wave-uniform
-            const uint32_t w = w0 + lane;
-            const uint32_t word = w < kBitRecs / 8 ? (w < 128 ? tbl_lo[w] : tbl_hi[w - 128]) : 0u;
-            // the flagged records' own meta and identifier, four loads in flight per lane
+          if (__ballot(over)) {  // (rare) this partition's records do not fit: through their links
+            map_rebuild();
+            resolve_lists(j0, j1, pp, PP);
+            map_ok = false;
+            continue;
+          }
+          // emission: every folded record, its own meta / identifier read from the pool (the
+          // table's rounds loaded together)
+          constexpr uint32_t kGroup = 4;
+          for (uint32_t u0 = 0; u0 < kBigSlots / 64; u0 += kGroup) {
+          uint32_t ent[kGroup];
+          uint2 mi[kGroup];
 #pragma unroll
-            for (uint32_t i0 = 0; i0 < 8; i0 += 4) {
-              uint2 mi[4];  // (ident, meta) of SubRec
+          for (uint32_t u = 0; u < kGroup; u++) {
+            ent[u] = (u0 + u) * 64 < kBigSlots ? *slot_ptr((u0 + u) * 64 + lane) : 0u;
+            mi[u] = make_uint2(0u, 0u);
+            if (ent[u]) mi[u] = *reinterpret_cast<const uint2*>(&a.ix.subs[sub_off + (ent[u] >> 5) - 1u].ident);
+          }
 #pragma unroll
-              for (uint32_t u = 0; u < 4; u++) {
-                mi[u] = make_uint2(0u, 0u);
-                if ((word >> ((i0 + u) * 4u)) & 15u) {
-                  const uint32_t k = L.n_direct + c0 + w * 8 + i0 + u;
-                  mi[u] = *reinterpret_cast<const uint2*>(&a.ix.subs[L.sub_off + k].ident);
-                }
-              }
-#pragma unroll
-              for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t nib = (word >> ((i0 + u) * 4u)) & 15u;
-                const uint32_t rmeta = mi[u].y & kSlotMetaMask;
-                const bool idpos = (int32_t)mi[u].x > 0;
-                const bool nonbase = (nib & kBitNonBase) != 0;
-                uint32_t pmeta;
-                if (nonbase) {
-                  pmeta = rmeta | (idpos ? kRowIdent : kRowDrop);
-                } else {
-                  const uint32_t qv = (nib & kBitQos2) ? 2u : (nib & kBitQos1) ? 1u : 0u;
-                  pmeta = (rmeta & ~(kMetaQos | kMetaNoLocal)) | max(rmeta & kMetaQos, qv) | (rmeta & kMetaNoLocal) |
-                          ((nib & kBitNoLocal) ? kMetaNoLocal : 0u);
-                }
-                const uint32_t k = L.n_direct + c0 + w * 8 + i0 + u;
-                emit_patch(nib != 0 && pmeta != rmeta && !(exp_bits & 4u), xa << kSetRowBits | k, pmeta);
-                n_nonbase += __popcll(__ballot(nonbase));
-                n_ext += __popcll(__ballot(nonbase && idpos));
-              }
+          for (uint32_t u = 0; u < kGroup; u++) {
+            const uint32_t nib = ent[u] & 31u;
+            const uint32_t k = (ent[u] >> 5) - 1u;
+            const uint32_t rmeta = mi[u].y & kSlotMetaMask;
+            const bool idpos = (int32_t)mi[u].x > 0;
+            const bool nonbase = ent[u] && (nib & kBitNonBase);
+            uint32_t pmeta;
+            if (nib & kBitNonBase) {
+              pmeta = rmeta | (idpos ? kRowIdent : kRowDrop);
+            } else {
+              const uint32_t qv = (nib & kBitQos2) ? 2u : (nib & kBitQos1) ? 1u : 0u;
+              pmeta = (rmeta & ~(kMetaQos | kMetaNoLocal)) | max(rmeta & kMetaQos, qv) | (rmeta & kMetaNoLocal) |
+                      ((nib & kBitNoLocal) ? kMetaNoLocal : 0u);
             }
+            emit_patch(ent[u] != 0u && pmeta != rmeta && !(exp_bits & 4u), xa << kSetRowBits | k, pmeta);
+            n_nonbase += __popcll(__ballot(nonbase));
+            n_ext += __popcll(__ballot(nonbase && idpos));
+          }
           }
           wave_sync_lds();  // (before the table is cleared again)
         }
-      };
-      // the node -> entry map again (after a fold took its place), for the partner-link path
-      auto map_rebuild = [&]() __attribute__((always_inline)) {
-        for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[wv][q] = kNone;
-        wave_sync_lds();
-        for (uint32_t x = lane; x < n_ent; x += 64) {
-          const uint32_t node = mg_node[wv][x];
-          uint32_t sl = hash32(node) & (kMapSlots - 1);
-          while (atomicCAS(&map_key[wv][sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
-          map_val[wv][sl] = x;
-        }
-        wave_sync_lds();
-        map_ok = true;
       };
       // the staged lists, folded in chunks of whole merge gathers; a merge gather whose lists
       // alone hold more than kFoldCap visits resolves through the partner links
@@ -1045,8 +1069,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
               atomicAdd(wc + 11, (unsigned long long)(h_pre[wv][next] - h_pre[wv][j0]));
               atomicAdd(wc + 12, 1ull);
               atomicAdd(wc + 13, (unsigned long long)a.ix.lists[mg_node[wv][h_ga[wv][j0]]].n_merge);
+              const uint32_t vb = h_pre[wv][next] - h_pre[wv][j0];
+              const uint32_t bk = vb <= 192 ? 0u : vb <= 384 ? 1u : vb <= 1024 ? 2u : 3u;
+              atomicAdd(wc + 16 + bk, 1ull);
+              atomicAdd(wc + 20 + bk, (unsigned long long)vb);
             }
-            if (!(exp_bits & 512u)) {
+            // the bit fold while its passes stay few (a pass re-reads the gather's visits: many passes
+            // cost more than the links); bits 10 / 11: up to two passes / any number (A/B)
+            const uint32_t vbig = h_pre[wv][next] - h_pre[wv][j0];
+            const uint32_t fold_max = (exp_bits & 2048u) ? ~0u : (exp_bits & 1024u) ? 2 * kBigFill : kBigFill;
+            if (!(exp_bits & 512u) && vbig <= fold_max) {
               fold_big(j0, next);
             } else {  // (MQ_OPT_SET_EXP bit 9: through the partner links, as before round 5)
               if (!map_ok) map_rebuild();
@@ -1074,7 +1106,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             ga = p / n_ent;
             hb = p - ga * n_ent;
             if (ga != hb) {
-              const uint32_t ent_mask = mg_emask[wv][ga], ent_off = mg_eoff[wv][ga];
+              const uint32_t ent_mask = mg_emask[ga], ent_off = mg_eoff[ga];
               if (ent_mask != kNone) {
                 hn = mg_node[wv][hb];
                 // linear probing, four slots per round: one load latency covers most probes

@@ -26,6 +26,7 @@ import (
 	"fmt"
 	"log/slog"
 	"math"
+	"runtime"
 	"strings"
 	"sync"
 	"sync/atomic"
@@ -658,6 +659,12 @@ func (b *batcher[T]) Close() {
 }
 
 func (b *batcher[T]) loop() {
+	// The loop stays on one OS thread: the HIP runtime sets up per-thread state on a thread's first
+	// call (~10 ms), and a goroutine that moved to a fresh thread would pay it again inside a match,
+	// under the index's lock (the engine also warms a new calling thread before taking the lock:
+	// mq_thread_warm, INTEGRATION.md §3).
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
 	defer close(b.done)
 	batch := make([]batchReq[T], 0, b.maxBatch)
 	items := make([]string, 0, b.maxBatch)

@@ -121,7 +121,7 @@ EXPORTS = [
     "mq_acl_match_batch", "mq_select_shared_device", "mq_match_spans", "mq_match_spans_device",
     "mq_spans_expand", "mq_set_option", "mq_match_spans_begin", "mq_match_spans_end",
     "mq_match_spans_end_host", "mq_device_check", "mq_match_spans_submit", "mq_match_spans_wait",
-    "mq_unsubscribe_bulk",
+    "mq_unsubscribe_bulk", "mq_thread_warm",
 ]
 
 CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
@@ -166,6 +166,7 @@ def lib():
                                         C.c_uint64, _u8p]),
         "mq_retain_bulk": (C.c_int, [vp, _u8p, _u64p, _u64p, C.c_uint64]),
         "mq_unsubscribe_bulk": (C.c_int, [vp, _u8p, _u64p, _u32p, C.c_uint64, _u8p]),
+        "mq_thread_warm": (C.c_int, [vp]),
         "mq_match_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MatchResult))]),
         "mq_match_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MatchResult)]),
         "mq_match_spans": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(SpanResult))]),

@@ -1073,8 +1073,10 @@ def test_pipelined_submit_fails_then_recovers(inline, gpu_available):
     from mqmatch import engine as E
     from mqmatch import workload as W
     w, eng, orc = _workload_pair(40000, 3000, seed=91)
-    if inline:
-        assert eng.inline_subscribe("#", 7, 1 << 30) == bool(orc.inline_subscribe("#", 7, filter_id=1 << 30))
+    if inline:  # (on "#", every topic gathers it; its filter id is the workload's: ids name filter strings)
+        offs = w["offs"].astype(np.int64)
+        fid = next(int(w["filter_ids"][i]) for i in range(len(offs) - 1) if bytes(w["bytes"][offs[i]:offs[i + 1]]) == b"#")
+        assert eng.inline_subscribe("#", 7, fid) == bool(orc.inline_subscribe("#", 7, filter_id=fid))
     batches = [W.gen_topics(w, 3000, seed=92 + i) for i in range(4)]
     want = [orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))[0] for tb, to in batches]
     rc, t0 = _submit(eng, *batches[0])
@@ -1170,7 +1172,7 @@ def test_set_pass_big_gathers(exp, gpu_available):
     d_to = torch.from_numpy(offs.view(np.int64)).cuda()
     torch.cuda.synchronize()
     # (digests name clients and filters by the adapter's ids: compare through the same adapter)
-    want = {t: canonical(o.subscribers(t)) for t in set(topics)}
+    want = {t: o.subscribers(t) for t in set(topics)}
     r = e.x.engine.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
     res = E.expand_device_spans(r, n)
     got = e.x._rebuild(res, 0)  # (first topic through the mirror's rematerialisation)
