@@ -314,7 +314,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const uint32_t xa = h_ga[j0];
       const uint32_t sub_off = ix.lists[mg_node[xa]].sub_off;
       const uint32_t v0 = h_pre[j0], v1 = h_pre[j1];
-      for (uint32_t q = lane; q < kBigSlots; q += 64) ws[q] = 0u;
+      // the table sized to the visits (at most 2/3 full: short probe runs, and a short emission scan)
+      const uint32_t ns = min(kBigSlots, ((v1 - v0) * 3 / 2 + 63) & ~63u);
+      for (uint32_t q = lane; q < ns; q += 64) ws[q] = 0u;
       uint32_t jj_next = j0;
       PairSlot e_next = locate(v0 + lane, j0, j1, jj_next);
       wave_sync_lds();
@@ -328,28 +330,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const uint32_t bits = (h_hb[jj] < xa ? kBitNonBase : 0u) | ((pm & 4u) ? kBitNoLocal : 0u) |
                                 ((pm & 3u) == 1u ? kBitQos1 : 0u) | ((pm & 3u) == 2u ? kBitQos2 : 0u);
           const uint32_t key = (e.k + 1u) << 5;
-          uint32_t sl = (hash32(e.k) >> 8) % kBigSlots;
-          for (;;) {  // (at most kBigFill keys in kBigSlots slots: a free slot is always found)
+          uint32_t sl = __umulhi(hash32(e.k), ns);
+          for (;;) {  // (at most kBigFill keys in ns >= 3/2 of them slots: a free slot is always found)
             const uint32_t prev = atomicCAS(&ws[sl], 0u, key | bits);
             if (prev == 0u) break;
             if ((prev & ~31u) == key) {
               if (bits & ~prev) atomicOr(&ws[sl], bits);
               break;
             }
-            sl = sl + 1 == kBigSlots ? 0u : sl + 1;
+            sl = sl + 1 == ns ? 0u : sl + 1;
           }
         }
         w_rec += r < v1;
       }
       wave_sync_lds();
       constexpr uint32_t kGroup = 4;
-      for (uint32_t u0 = 0; u0 < kBigSlots; u0 += kGroup * 64) {
+      for (uint32_t u0 = 0; u0 < ns; u0 += kGroup * 64) {
         uint32_t ent[kGroup];
         uint2 mi[kGroup];  // (identifier, meta) of the record
 #pragma unroll
         for (uint32_t u = 0; u < kGroup; u++) {
           const uint32_t q = u0 + u * 64 + lane;
-          ent[u] = q < kBigSlots ? ws[q] : 0u;
+          ent[u] = q < ns ? ws[q] : 0u;
           mi[u] = make_uint2(0u, 0u);
           if (ent[u]) mi[u] = *reinterpret_cast<const uint2*>(&ix.subs[sub_off + (ent[u] >> 5) - 1u].ident);
         }
