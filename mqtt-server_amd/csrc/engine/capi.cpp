@@ -512,7 +512,7 @@ int mq_match_spans_begin(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_t
                          mq_xlist* exported) {
   if (!exported || (n && !d_to)) return fail(MQ_EINVAL, "null argument");
   return guarded(idx, [&] {
-    idx->device().spans_begin(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, exported);
+    idx->device().spans_begin(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, exported, false, true);
     return 0;
   });
 }

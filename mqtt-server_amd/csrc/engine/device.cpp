@@ -305,6 +305,10 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
       img_version_ = ~0ull;
       return true;
     case MQ_OPT_FAIL_NEXT: fail_next_ = (uint32_t)v; return true;
+    case MQ_OPT_WALK_EXP:
+      if (!kDevBuild && v) return false;  // (development builds only)
+      walk_exp_ = (uint32_t)v;
+      return true;
     default: return false;
   }
 }
@@ -340,6 +344,7 @@ Device::~Device() {
   for (hipEvent_t e : ev_scan_) (void)hipEventDestroy(e);
   if (h_plan_) (void)hipHostFree(h_plan_);
   if (h_pin_) (void)hipHostFree(h_pin_);
+  if (h_xsrc_) (void)hipHostFree(h_xsrc_);
 }
 
 uint64_t Device::device_bytes() const {
@@ -1050,7 +1055,7 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
 }
 
 void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
-                         mq_xlist* x, bool one_sync) {
+                         mq_xlist* x, bool one_sync, bool shard_sync) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   flush_host_copy();  // (a pipelined batch's copy: before this batch reuses any stage)
   sync(ix, s);
@@ -1065,9 +1070,14 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   // The walk counts only gathers when nothing needs the lists' totals before k_desc: no inline
   // rows to place and no device share pick (k_desc<true> then counts rows / shared / merge).
   const bool lists = walk_lists_ || select_shared_ || ix.inl.live != 0;
+  // A sharded index's begin runs as a one-sync batch's does (k_reset, buffers as earlier batches
+  // left them, the export written by k_desc and packed by k_xpack) and synchronises once, at its
+  // end, for the export's size (the exchange needs it) and the guards; its spans_end is host-sized.
+  const bool xsync = shard_sync && one_sync_ && ix.sharded() && !lists && dedup_ != 0 && set_grid_;
   // One host synchronisation for the whole batch (at its end): device results of an index that is
   // not sharded, without inline rows or a device share pick (whose buffers the walk's totals size)
   one_sync = one_sync && !ix.sharded() && !lists && dedup_ != 0 && set_grid_;
+  const bool bsync = one_sync || xsync;  // the begin without host synchronisations
   sb_.trial = -1;
   if (one_sync && walk_auto_ && n >= kWalkTrialMin) {
     // Which walk suits this index (§4): the frontier walk with the fused desc, or the walk
@@ -1097,7 +1107,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     }
     walk_group_ = (k == 1 || (k < 0 && walk_trial_ns_[1] < walk_trial_ns_[0])) ? 0u : 16u;
   }
-  if (one_sync) {
+  if (bsync) {
     if (!h_fast_) {
       void* hp = nullptr;  // (its own allocation, not a slab block: the device reads it by address)
       hip_check(hipHostMalloc(&hp, sizeof(FastBack), hipHostMallocDefault), "hipHostMalloc");
@@ -1191,8 +1201,12 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     }
     da.spans_cap = sp_spans_.bytes / sizeof(SpanRec);
     da.desc_cap = desc_[0].bytes / sizeof(GDesc);
-    da.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
+    da.unsafe = bsync ? unsafe_.as<uint32_t>() : nullptr;
     da.g_stride = fused ? kGatherCap : 0u;
+    if (xsync) {
+      da.xents = x_stride_.as<XEnt>();
+      da.xcount = x_cnt_.as<uint32_t>();
+    }
     return da;
   };
   DescArgs fda;
@@ -1206,8 +1220,16 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     while (slots < 2ull * n) slots <<= 1;
     fda.dd_mask = slots - 1;
     fda.dd_tslot = dd_slot_.as<uint32_t>();
+    if (walk_exp_ & 1u) {  // MQ_OPT_WALK_EXP bit 0: the level-0 probes ahead of the walk
+      grow(root_hint_, (size_t)n * sizeof(uint4));
+      prof.begin(s);
+      launch_root_hint(d_tb, d_to, n, di, root_hint_.as<uint4>(), s);
+      prof.end("root_hint", s);
+      hip_check(hipGetLastError(), "k_root_hint");
+      fda.root_hint = root_hint_.as<uint4>();
+    }
   }
-  const TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, one_sync, fused ? &fda : nullptr);
+  TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, bsync, fused ? &fda : nullptr);
   if (fail_next_) {  // MQ_OPT_FAIL_NEXT: as if a kernel guard had tripped in this batch
     fail_next_--;
     hip_check(hipMemsetD32Async((hipDeviceptr_t)err_.p, (int)kErrWalkGuard, 1, s), "hipMemsetD32Async(err)");
@@ -1215,9 +1237,13 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   sb_.tot = tot;
   sb_.gathers = gathers;
   sb_.gstride = gstride;
-  if (!one_sync) {  // (one-sync: the buffers as earlier batches left them; the kernels check)
+  if (!bsync) {  // (one-sync: the buffers as earlier batches left them; the kernels check)
     grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
     grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
+  } else if (xsync) {  // (k_desc's export at the spans' positions: as many as the spans hold)
+    grow(sp_spans_, sizeof(SpanRec));
+    grow(x_stride_, sp_spans_.bytes / sizeof(SpanRec) * sizeof(XEnt));
+    grow(x_cnt_, (size_t)n * sizeof(uint32_t));
   }
   grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
   grow(sp_res_, (size_t)n * sizeof(TopicSpansDev));
@@ -1236,7 +1262,62 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     prof.end("desc", s);
     hip_check(hipGetLastError(), "k_desc<spans>");
   }
-  if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
+  if (xsync) {  // export: packed from k_desc's, then the begin's one synchronisation
+    const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+    grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
+    grow(xbsum_, (size_t)(nb + 1) * sizeof(TopicOff));
+    grow(xbpre_, (size_t)(nb + 1) * sizeof(TopicOff));
+    if (!x_tot_.p) x_tot_.ensure(3 * sizeof(unsigned long long));
+    grow(x_ents_, sizeof(XEnt));
+    auto pack = [&]() {
+      prof.begin(s);
+      launch_counts(x_cnt_.as<uint32_t>(), n, counts_.as<TopicCount>(), s);
+      launch_scan(counts_.as<TopicCount>(), n, xbsum_.as<TopicOff>(), xbpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
+      launch_xpack(n, offs_.as<TopicOff>(), x_cnt_.as<uint32_t>(), x_off_.as<TopicOff>(), xbpre_.as<TopicOff>() + nb,
+                   x_stride_.as<XEnt>(), x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt), unsafe_.as<uint32_t>(),
+                   x_tot_.as<unsigned long long>(), s);
+      prof.end("xpack", s);
+      hip_check(hipGetLastError(), "k_xpack");
+      ReadbackArgs rb;
+      memset(&rb, 0, sizeof(rb));
+      rb.tot = bpre_.as<TopicOff>() + nb;
+      rb.ovf = ovf_.as<uint32_t>();
+      rb.fallback = walk_group_ ? fb_cnt_.as<uint32_t>() : nullptr;
+      rb.unsafe = unsafe_.as<uint32_t>();
+      rb.err = err_.as<uint32_t>();
+      rb.n_sets = x_tot_.as<unsigned long long>();
+      rb.out = d_fast_;
+      launch_readback(rb, s);
+      hip_check(hipGetLastError(), "k_readback");
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    };
+    pack();
+    if (h_fast_->err) check_err(s);  // throws with the tripped guard's name
+    // (k_xsig writes GDesc records at the topics' gather offsets for k_merge's linear paths: the
+    // records must hold every gather)
+    if (h_fast_->ovf || (h_fast_->unsafe & (kUnsafeSpans | kUnsafeDesc)) ||
+        h_fast_->tot.g > desc_[0].bytes / sizeof(GDesc)) {
+      // the walk or k_desc outgrew what earlier batches left: the begin again, host-sized
+      prof.count("one_sync_retries", 1);
+      spans_begin(ix, d_tb, d_to, n, s, x, false, false);
+      return;
+    }
+    if (h_fast_->unsafe & kUnsafeXEnts) {  // only the packed export outgrew its buffer: pack again
+      x_ents_.release();
+      x_ents_.ensure(std::max<uint64_t>(h_fast_->n_sets[0] + h_fast_->n_sets[0] / 4 + 1024, 1) * sizeof(XEnt));
+      hip_check(hipMemsetAsync(unsafe_.p, 0, sizeof(uint32_t), s), "memset");
+      pack();
+      if (h_fast_->unsafe) throw HipError{hipErrorUnknown, "k_xpack: the export did not fit the grown buffer"};
+    }
+    sb_.tot = h_fast_->tot;
+    sb_.xsync = true;
+    if (walk_group_ && prof.on()) prof.count("walk_fallback", h_fast_->fallback);
+    x->counts = x_cnt_.as<uint32_t>();
+    x->ents = reinterpret_cast<const mq_xent*>(x_ents_.p);
+    x->n_ents = h_fast_->n_sets[0];
+    prof.count("xents", x->n_ents);
+    prof.count("topics", n);
+  } else if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
     grow(x_cnt_, (size_t)n * sizeof(uint32_t));
@@ -1284,7 +1365,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (issued) issued->store(true);
     return true;
   }
-  const bool one_sync = sb_.one_sync;
+  const bool one_sync = sb_.one_sync || sb_.xsync;
   // host results: this batch's stage, free once the copy of its last batch is done; 4-byte patch
   // codes while every subscription list is shorter than 2^23 (set rows) and the rows of a topic
   // fit 29 bits (MQ_SPANS_PATCH_CODES)
@@ -1302,7 +1383,13 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   EmitArgs a;
   memset(&a, 0, sizeof(a));
   a.n_xf = nf;
-  XSrc h_src[kMaxShards - 1];
+  if (nf && !h_xsrc_) {
+    void* hp = nullptr;
+    hip_check(hipHostMalloc(&hp, (kMaxShards - 1) * sizeof(XSrc), hipHostMallocDefault), "hipHostMalloc");
+    h_xsrc_ = static_cast<XSrc*>(hp);
+  }
+  XSrc* const h_src = h_xsrc_;  // (pinned: its copy runs in order with the batch; the previous batch
+                                //  synchronised before this one writes it again)
   for (uint32_t f = 0; f < nf; f++) {  // import: per-topic offsets of each foreign list
     if (xf[f].n_topics != n || (xf[f].n_ents && (!xf[f].counts || !xf[f].ents)))
       throw HipError{hipErrorInvalidValue, "foreign list does not match the batch"};
@@ -1315,7 +1402,6 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   if (nf) {
     grow(x_src_, sizeof(h_src));
     hip_check(hipMemcpyAsync(x_src_.p, h_src, nf * sizeof(XSrc), hipMemcpyHostToDevice, s), "H2D xsrc");
-    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");  // h_src is on the stack
     a.xsrc = x_src_.as<XSrc>();
   }
   if (sb_.dedup) {  // merge-set dedup: each topic's representative (DedupArgs)
@@ -1597,7 +1683,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   }
   if (one_sync) {  // the batch's one synchronisation: totals, overflow, unsafe bits, errors
     ReadbackArgs rb;
-    rb.tot = sb_.fused ? nullptr : bpre_.as<TopicOff>() + (n + kScanBlock - 1) / kScanBlock;
+    // (a sharded batch's totals were read by its begin: the imports' scans reused bpre_ since)
+    rb.tot = sb_.fused || sb_.xsync ? nullptr : bpre_.as<TopicOff>() + (n + kScanBlock - 1) / kScanBlock;
     rb.ovf = ovf_.as<uint32_t>();
     rb.fallback = walk_group_ ? fb_cnt_.as<uint32_t>() : nullptr;
     rb.unsafe = unsafe_.as<uint32_t>();
@@ -1632,9 +1719,14 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (h_fast_->err) check_err(s);  // throws with the tripped guard's name
     if (h_fast_->ovf || h_fast_->unsafe) {
       prof.count("one_sync_retries", 1);
+      if (sb_.xsync) {  // sharded: the begin's results and the imported lists stand; the end again,
+        sb_.pending = true;  // host-sized
+        sb_.xsync = false;
+        return spans_end(ix, xf, nf, s, host, out, ready, issued);
+      }
       return false;
     }
-    tot = h_fast_->tot;
+    tot = sb_.xsync ? sb_.tot : h_fast_->tot;
     if (sb_.fused) tot.g = h_fast_->n_sets[2];  // (no scan: k_dedup_rep totals the gathers)
     if (host) n_patches = h_fast_->n_patches;  // (the region offsets: sp_roff_, k_readback)
     sb_.tot = tot;

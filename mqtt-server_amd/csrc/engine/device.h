@@ -213,11 +213,13 @@ class Device {
   // The same in two phases, for a sharded index: begin walks the batch and
   // exports the topics' gathered cross-shard nodes (device pointers in *x, valid until end);
   // the caller exchanges the lists between the shards; end merges with the other shards' lists.
+  // shard_sync (mq_match_spans_begin): a sharded index's begin synchronises once, at its end
+  // (MQ_OPT_ONE_SYNC); its spans_end is host-sized either way.
   // one_sync (match_spans only): the batch may run with one host synchronisation (at its end),
   // its buffers sized by earlier batches; spans_end then returns false when they did not hold it
   // and the caller runs the batch again without one_sync (host-sized buffers).
   void spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x,
-                   bool one_sync = false);
+                   bool one_sync = false, bool shard_sync = false);
   bool spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out,
                  hipEvent_t ready = nullptr, std::atomic<bool>* issued = nullptr);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
@@ -354,6 +356,8 @@ class Device {
   DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
   // sharded: the exported list (offsets, entries, counts) and the imported lists' offsets
   DevBuf x_off_, x_ents_, x_cnt_, x_src_, x_foff_[kMaxShards - 1];
+  DevBuf x_stride_, xbsum_, xbpre_, x_tot_;  // sharded one-sync begins: k_desc's export, its scan, total
+  XSrc* h_xsrc_ = nullptr;                   // pinned: the imported lists' sources (no stack copy)
   struct SpanBatch {               // between spans_begin and spans_end
     bool pending = false;
     uint32_t n = 0;
@@ -367,6 +371,8 @@ class Device {
     uint32_t gstride = 0;
     TopicCount* tc = nullptr;      // k_desc's per-topic counts (walk without lists), or null
     bool one_sync = false;         // one host synchronisation (spans_begin)
+    bool xsync = false;            // a sharded index's one-sync begin: its end synchronises once too
+                                   //   (and runs again, host-sized, if a pool overflowed)
     bool fused = false;            // k_desc ran in the walk's epilogue: spans at t * kGatherCap
     int trial = -1;                // a timed walk trial: 0 frontier, 1 thread per topic
   } sb_;
@@ -384,6 +390,8 @@ class Device {
   bool fuse_desc_ = true;     // MQ_OPT_FUSE_DESC
   uint64_t msg_edge_budget_ = 8ull << 30;  // MQ_OPT_MSG_EDGE_BUDGET: the image edge table's 1/16 budget
   uint32_t fail_next_ = 0;    // MQ_OPT_FAIL_NEXT: span batches still to fail as if a guard tripped
+  uint32_t walk_exp_ = 0;     // MQ_OPT_WALK_EXP (development builds)
+  DevBuf root_hint_;
   uint32_t set_exp_ = 0;      // MQ_OPT_SET_EXP (timing experiments only)
   uint64_t last_sets_ = 0;    // merge sets of the last batch: the grid of the next set pass
   DevBuf sp_tc_;                     // per-topic counts from k_desc<true> (walk without lists)

@@ -304,7 +304,7 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
   // one-sync batch: spans past the buffer are not written (the batch runs again, host-sized)
   const bool fits = !a.unsafe || g0 + n_g <= a.spans_cap;
   if (!fits && sub == 0) atomicOr(a.unsafe, kUnsafeSpans);
-  uint32_t rpos = 0, spos = 0, n_mg = 0, n_merge = 0;
+  uint32_t rpos = 0, spos = 0, n_mg = 0, n_merge = 0, n_x = 0;
   uint64_t sig = 0;
   for (uint32_t r0 = 0; r0 < n_g; r0 += G) {
     const uint32_t i = r0 + sub;
@@ -340,6 +340,15 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
       }
     }
     if (subs) n_merge += L.n_merge;
+    if (a.xents) {  // sharded: the export (a gathered node whose subscriptions have a foreign partner)
+      const bool isx = subs && (L.flags & kFlagXNode);
+      const uint32_t xi = grp_incl<G>(isx ? 1u : 0u, sub);
+      if (isx && fits) {
+        const XInfo xn = a.ix.xinfo[gw & kGatherNode];
+        a.xents[g0 + n_x + xi - 1] = XEnt{xn.fid, xn.deep, xn.rank};
+      }
+      n_x += __shfl(xi, G - 1, G);
+    }
     rpos += __shfl(rn_i, G - 1, G);
     spos += __shfl(sh_i, G - 1, G);
     ipos += __shfl(in_i, G - 1, G);
@@ -357,6 +366,7 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
     if (sub == 0) a.dd_tslot[t] = slot;
   }
   if (sub != 0) return;
+  if (a.xcount) a.xcount[t] = n_x;
   if (a.tc_out) a.tc_out[t] = TopicCount{n_g, rpos, spos, 0u, n_merge};
   a.msig[t] = msig;
   a.mcount[t] = n_mg;

@@ -248,6 +248,14 @@ struct DescArgs {
                    // lists k_merge maps a topic's merge gathers without GDesc records, which are
                    // then written only for a topic with more than kPairMax merge gathers
   uint64_t* mrank; // sharded index: each merge gather's DFS rank key (XInfo.rank; stride kPairMax)
+  // sharded index, the export in k_desc (null: k_xlist exports): topic t's gathered cross-shard
+  // nodes (gathered subscriptions at a node with a foreign partner, kFlagXNode) at its spans' own
+  // positions (xents[g0, + xcount[t]): never more than its gathers), packed by k_xpack
+  XEnt* xents;
+  uint32_t* xcount;
+  // MQ_OPT_WALK_EXP bit 0 (development builds, an attribution of the walk's level-0 probes):
+  // topic t's root child (child, '+', '#') looked up before the walk by k_root_hint
+  const uint4* root_hint;
   // one-sync batches (Device, MQ_OPT_ONE_SYNC): the capacities of spans / desc in records; a topic
   // that would write past them writes nothing and sets bit 1 of *unsafe (the batch is run again
   // with host-sized buffers). unsafe == null: sized by the host (no checks).
@@ -379,6 +387,7 @@ void launch_walk_desc(uint32_t group, uint32_t wpe, const uint8_t* tb, const uin
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
+void launch_root_hint(const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix, uint4* out, hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
 void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
 
@@ -422,6 +431,13 @@ void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, co
 // Sharded index: the topics' gathered cross-shard nodes (kFlagXNode, subscriptions gathered).
 // count = true: TopicCount.gathers = their number per topic; else written as XEnt at
 // off[t].g with their number in counts[t] (the exported list, mq_xlist).
+// The export written by k_desc (DescArgs.xents), packed: k_counts + scan of xcount give xoff; each
+// topic's entries move from xents[off[t].g, ...) to ents[xoff[t].g, ...) unless the packed total
+// passes cap (then *unsafe |= kUnsafeXEnts, nothing is written); total[0] = the packed total.
+constexpr uint32_t kUnsafeXEnts = 16u;
+void launch_xpack(uint32_t n, const TopicOff* off, const uint32_t* xcount, const TopicOff* xoff, const TopicOff* xtot,
+                  const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total,
+                  hipStream_t s);
 void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const uint32_t* gathers,
                   uint32_t gather_stride, TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts,
                   hipStream_t s);

@@ -257,6 +257,31 @@ __global__ __launch_bounds__(256) void k_xlist(DevIndex ix, uint32_t n, const To
   else counts[t] = k;
 }
 
+__global__ __launch_bounds__(256) void k_xpack(uint32_t n, const TopicOff* __restrict__ off,
+                                               const uint32_t* __restrict__ xcount, const TopicOff* __restrict__ xoff,
+                                               const TopicOff* __restrict__ xtot, const XEnt* __restrict__ xents,
+                                               XEnt* __restrict__ ents, uint64_t cap, uint32_t* unsafe,
+                                               unsigned long long* total) {
+  const uint64_t all = xtot->g;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) {
+    total[0] = all;
+    if (all > cap) atomicOr(unsafe, kUnsafeXEnts);
+  }
+  if (t >= n || all > cap) return;
+  const uint32_t c = xcount[t];
+  const uint64_t src = off[t].g, dst = xoff[t].g;
+  for (uint32_t k = 0; k < c; k++) ents[dst + k] = xents[src + k];
+}
+
+void launch_xpack(uint32_t n, const TopicOff* off, const uint32_t* xcount, const TopicOff* xoff, const TopicOff* xtot,
+                  const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total,
+                  hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_xpack, dim3((n + 255) / 256), dim3(256), 0, s, n, off, xcount, xoff, xtot, xents, ents, cap,
+                     unsafe, total);
+}
+
 void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const uint32_t* gathers,
                   uint32_t gather_stride, TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts,
                   hipStream_t s) {

@@ -311,7 +311,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (mine && has_next && fe.plus != kNone) pw = ix.walk[fe.plus];
     EdgeHit h{kNone, kNone, kNone};
     // a literal "+" segment: the reference visits the '+' child twice alike (topics.go:603)
-    if (mine && !plusseg) h = lookup_edge(ix, fe.node, key, tbase + s, len);
+    if (mine && !plusseg) {
+      if (DESC && da.root_hint && d == 0) {  // (MQ_OPT_WALK_EXP bit 0: level 0 looked up before the walk)
+        const uint4 rh = da.root_hint[t];
+        h = EdgeHit{rh.x, rh.y, rh.z};
+      } else {
+        h = lookup_edge(ix, fe.node, key, tbase + s, len);
+      }
+    }
     // this lane's gathers (at most four): the particle's '#' child (topics.go:621); at the last
     // level the literal child, its '#' child (filter/# matches filter, topics.go:612; inline: the
     // particle's own again, Q2) and the '+' child
@@ -729,6 +736,32 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
   hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(256), 0, s, cnt, n, bsum);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(256), 0, s, bsum, nb, bpre);
   hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(256), 0, s, cnt, n, bpre, off);
+}
+
+// MQ_OPT_WALK_EXP bit 0 (development builds): each topic's level-0 probe (the root's literal
+// child of its first segment), thread per topic, ahead of the walk — the walk then reads it instead
+// of probing, so the two kernels' times attribute the level-0 probes (the north star's "hot trie
+// levels staged in LDS" would save at most that much)
+__global__ __launch_bounds__(256) void k_root_hint(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
+                                                   uint32_t n, DevIndex ix, uint4* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t a0 = to[t], a1 = to[t + 1];
+  const uint8_t* tbase = tb + (a0 & ~15ull);
+  const uint32_t b0 = (uint32_t)(a0 & 15), b1 = b0 + (uint32_t)(a1 - a0);
+  EdgeHit h{kNone, kNone, kNone};
+  if (a1 > a0) {
+    ByteReaderT<uint32_t> R(tbase);
+    const uint32_t e = find_slash(R, b0, b1);
+    const bool plusseg = e - b0 == 1 && R.at(b0) == '+';
+    if (!plusseg) h = lookup_edge(ix, kRoot, key_of(R, b0, e), tbase + b0, e - b0);
+  }
+  out[t] = make_uint4(h.child, h.plus, h.hash, 0u);
+}
+
+void launch_root_hint(const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix, uint4* out, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_root_hint, dim3((n + 255) / 256), dim3(256), 0, s, tb, to, n, ix, out);
 }
 
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s) {
