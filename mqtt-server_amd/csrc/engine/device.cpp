@@ -1161,12 +1161,18 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   sb_.one_sync = one_sync;
   // k_desc in the frontier walk's epilogue (one-sync batches): spans and GDesc records at
   // t * kGatherCap, so nothing waits for a scan of the gather counts
-  const bool fused = one_sync && fuse_desc_ && (walk_group_ == 16 || walk_group_ == 8);
+  const bool fused = bsync && fuse_desc_ && (walk_group_ == 16 || walk_group_ == 8);
   sb_.fused = fused;
+  sb_.walk_inserted = fused && !xsync;
   if (!sb_.lists) grow(sp_tc_, (size_t)n * sizeof(TopicCount));
   if (fused) {
     grow(desc_[0], (size_t)n * kGatherCap * sizeof(GDesc));
     grow(sp_spans_, (size_t)n * kGatherCap * sizeof(SpanRec));
+  }
+  if (xsync) {  // (k_desc's export at the spans' positions: as many as the spans hold)
+    if (!fused) grow(sp_spans_, sizeof(SpanRec));
+    grow(x_stride_, sp_spans_.bytes / sizeof(SpanRec) * sizeof(XEnt));
+    grow(x_cnt_, (size_t)n * sizeof(uint32_t));
   }
   sb_.dedup = dedup_ != 0;
   if (sb_.dedup) {
@@ -1206,15 +1212,18 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     if (xsync) {
       da.xents = x_stride_.as<XEnt>();
       da.xcount = x_cnt_.as<uint32_t>();
+      if (fused) da.gw_out = gslots_.as<uint32_t>();  // (walk_scan grew it; sized n * kGatherCap)
     }
     return da;
   };
   DescArgs fda;
   if (fused) {
     grow(sp_inl_, sizeof(InlRec));
+    grow(gslots_, (size_t)n * kGatherCap * sizeof(uint32_t));
     fda = desc_args();
-    // k_dedup_insert folded into the walk's epilogue (the table was zeroed by k_reset)
-    fda.dd_keys = dd_keys_.as<unsigned long long>();
+    // k_dedup_insert folded into the walk's epilogue (the table was zeroed by k_reset); not on a
+    // sharded index, whose signatures take the other shards' entries after the exchange (k_xsig)
+    fda.dd_keys = xsync ? nullptr : dd_keys_.as<unsigned long long>();
     fda.dd_vals = dd_vals_.as<uint32_t>();
     uint64_t slots = 1024;  // (as zeroed by k_reset above)
     while (slots < 2ull * n) slots <<= 1;
@@ -1240,10 +1249,6 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   if (!bsync) {  // (one-sync: the buffers as earlier batches left them; the kernels check)
     grow(desc_[0], std::max<uint64_t>(tot.g, 1) * sizeof(GDesc));
     grow(sp_spans_, std::max<uint64_t>(tot.g, 1) * sizeof(SpanRec));
-  } else if (xsync) {  // (k_desc's export at the spans' positions: as many as the spans hold)
-    grow(sp_spans_, sizeof(SpanRec));
-    grow(x_stride_, sp_spans_.bytes / sizeof(SpanRec) * sizeof(XEnt));
-    grow(x_cnt_, (size_t)n * sizeof(uint32_t));
   }
   grow(sp_inl_, std::max<uint64_t>(tot.inl, 1) * sizeof(InlRec));
   grow(sp_res_, (size_t)n * sizeof(TopicSpansDev));
@@ -1271,16 +1276,18 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     grow(x_ents_, sizeof(XEnt));
     auto pack = [&]() {
       prof.begin(s);
-      launch_counts(x_cnt_.as<uint32_t>(), n, counts_.as<TopicCount>(), s);
+      // (walk-fused: the scan also totals the batch's gathers, in .rows)
+      if (fused) launch_xcounts(x_cnt_.as<uint32_t>(), sp_tc_.as<TopicCount>(), n, counts_.as<TopicCount>(), s);
+      else launch_counts(x_cnt_.as<uint32_t>(), n, counts_.as<TopicCount>(), s);
       launch_scan(counts_.as<TopicCount>(), n, xbsum_.as<TopicOff>(), xbpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
-      launch_xpack(n, offs_.as<TopicOff>(), x_cnt_.as<uint32_t>(), x_off_.as<TopicOff>(), xbpre_.as<TopicOff>() + nb,
-                   x_stride_.as<XEnt>(), x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt), unsafe_.as<uint32_t>(),
-                   x_tot_.as<unsigned long long>(), s);
+      launch_xpack(n, offs_.as<TopicOff>(), fused ? kGatherCap : 0u, x_cnt_.as<uint32_t>(), x_off_.as<TopicOff>(),
+                   xbpre_.as<TopicOff>() + nb, x_stride_.as<XEnt>(), x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt),
+                   unsafe_.as<uint32_t>(), x_tot_.as<unsigned long long>(), s);
       prof.end("xpack", s);
       hip_check(hipGetLastError(), "k_xpack");
       ReadbackArgs rb;
       memset(&rb, 0, sizeof(rb));
-      rb.tot = bpre_.as<TopicOff>() + nb;
+      rb.tot = fused ? xbpre_.as<TopicOff>() + nb : bpre_.as<TopicOff>() + nb;
       rb.ovf = ovf_.as<uint32_t>();
       rb.fallback = walk_group_ ? fb_cnt_.as<uint32_t>() : nullptr;
       rb.unsafe = unsafe_.as<uint32_t>();
@@ -1295,8 +1302,9 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     if (h_fast_->err) check_err(s);  // throws with the tripped guard's name
     // (k_xsig writes GDesc records at the topics' gather offsets for k_merge's linear paths: the
     // records must hold every gather)
+    const uint64_t gathers_total = fused ? h_fast_->tot.rows : h_fast_->tot.g;
     if (h_fast_->ovf || (h_fast_->unsafe & (kUnsafeSpans | kUnsafeDesc)) ||
-        h_fast_->tot.g > desc_[0].bytes / sizeof(GDesc)) {
+        (!fused && gathers_total > desc_[0].bytes / sizeof(GDesc))) {
       // the walk or k_desc outgrew what earlier batches left: the begin again, host-sized
       prof.count("one_sync_retries", 1);
       spans_begin(ix, d_tb, d_to, n, s, x, false, false);
@@ -1309,7 +1317,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
       pack();
       if (h_fast_->unsafe) throw HipError{hipErrorUnknown, "k_xpack: the export did not fit the grown buffer"};
     }
-    sb_.tot = h_fast_->tot;
+    sb_.tot = fused ? TopicOff{gathers_total, 0, 0, 0, 0} : h_fast_->tot;
     sb_.xsync = true;
     if (walk_group_ && prof.on()) prof.count("walk_fallback", h_fast_->fallback);
     x->counts = x_cnt_.as<uint32_t>();
@@ -1449,6 +1457,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       xa.off = offs_.as<TopicOff>();
       xa.gathers = sb_.gathers;
       xa.gather_stride = sb_.gstride;
+      xa.g_stride = sb_.fused ? kGatherCap : 0u;
+      xa.tc = sb_.tc;
       xa.desc = desc_[0].as<GDesc>();
       prof.begin(s);
       launch_xsig(xa, s);
@@ -1457,7 +1467,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       dd.fcount = xa.fcount;
     }
     prof.begin(s);
-    launch_dedup(dd, s, !sb_.fused);
+    launch_dedup(dd, s, !sb_.walk_inserted);
     prof.end("dedup", s);
     hip_check(hipGetLastError(), "k_dedup");
     sb_.n_sets = 0;

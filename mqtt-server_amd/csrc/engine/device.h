@@ -374,6 +374,7 @@ class Device {
     bool xsync = false;            // a sharded index's one-sync begin: its end synchronises once too
                                    //   (and runs again, host-sized, if a pool overflowed)
     bool fused = false;            // k_desc ran in the walk's epilogue: spans at t * kGatherCap
+    bool walk_inserted = false;    //   and k_dedup_insert with it (not on a sharded index)
     int trial = -1;                // a timed walk trial: 0 frontier, 1 thread per topic
   } sb_;
   // one-sync batches: values read back at the batch's end (pinned): the walk's totals, its

@@ -328,6 +328,7 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
     const uint32_t rp = rpos + rn_i - rn, x = n_mg + inc_i - inc;
     const uint64_t ip = ipos + (in_i - in);
     if (act && fits) a.spans[g0 + i] = SpanRec{L.sub_off, rn, L.shr_off, L.shr_cnt};
+    if (act && fits && a.gw_out) a.gw_out[g0 + i] = gw;
     for (uint32_t k = 0; k < in; k++) a.inl_out[ip + k] = a.ix.inl[I.off + k];
     if (ismg) {
       sig += mix64(((uint64_t)x << 32 | (gw & kGatherNode)) + 0x9e3779b97f4a7c15ull);

@@ -253,6 +253,8 @@ struct DescArgs {
   // positions (xents[g0, + xcount[t]): never more than its gathers), packed by k_xpack
   XEnt* xents;
   uint32_t* xcount;
+  uint32_t* gw_out;  // sharded, walk-fused: every gather word at its span's position (k_xsig's GDesc
+                     //   records for k_merge's linear paths are made from them)
   // MQ_OPT_WALK_EXP bit 0 (development builds, an attribution of the walk's level-0 probes):
   // topic t's root child (child, '+', '#') looked up before the walk by k_root_hint
   const uint4* root_hint;
@@ -325,6 +327,8 @@ struct XSigArgs {
   const uint32_t* gathers;
   uint32_t gather_stride;
   struct GDesc* desc;
+  uint32_t g_stride;                // the walk-fused layout: topic t's gathers at t * g_stride, their
+  const struct TopicCount* tc;      //   number tc[t].gathers (off unused)
 };
 void launch_xsig(const XSigArgs& a, hipStream_t s);
 // The merge set pass of an index that is not sharded (sets.hip): k_merge<spans, SET>'s results with
@@ -435,9 +439,12 @@ void launch_msg(bool fill, const uint8_t* fb, const uint64_t* fo, uint32_t n, co
 // topic's entries move from xents[off[t].g, ...) to ents[xoff[t].g, ...) unless the packed total
 // passes cap (then *unsafe |= kUnsafeXEnts, nothing is written); total[0] = the packed total.
 constexpr uint32_t kUnsafeXEnts = 16u;
-void launch_xpack(uint32_t n, const TopicOff* off, const uint32_t* xcount, const TopicOff* xoff, const TopicOff* xtot,
-                  const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total,
-                  hipStream_t s);
+void launch_xpack(uint32_t n, const TopicOff* off, uint32_t g_stride, const uint32_t* xcount, const TopicOff* xoff,
+                  const TopicOff* xtot, const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe,
+                  unsigned long long* total, hipStream_t s);
+// cnt[t] = {xcount[t], tc[t].gathers, 0, 0, 0}: scanned, the export's offsets and (in .rows) the
+// batch's gathers (the walk-fused layout has no scan of its own)
+void launch_xcounts(const uint32_t* xcount, const TopicCount* tc, uint32_t n, TopicCount* cnt, hipStream_t s);
 void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const uint32_t* gathers,
                   uint32_t gather_stride, TopicCount* cnt, const TopicOff* xoff, XEnt* ents, uint32_t* counts,
                   hipStream_t s);

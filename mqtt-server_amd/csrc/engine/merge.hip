@@ -292,9 +292,14 @@ __global__ __launch_bounds__(256) void k_xsig(XSigArgs a) {
   if (!fc || !mc) return;
   a.msig[t] = mix64(a.msig[t] ^ sig) | 1ull;
   if (mc <= kPairMax && mc + fc >= kMapSlots) {  // k_merge's slow path reads GDesc records
-    const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
-    const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
-    write_gdesc(a.ix, gw_src, (uint32_t)(o1.g - o0.g), (uint32_t)o0.shr, a.desc + o0.g);
+    if (a.g_stride) {  // the walk-fused layout (the gather words at the spans' positions)
+      const uint64_t g0 = (uint64_t)t * a.g_stride;
+      write_gdesc(a.ix, a.gathers + g0, a.tc[t].gathers, 0u, a.desc + g0);
+    } else {
+      const TopicOff o0 = a.off[t], o1 = a.off[t + 1];
+      const uint32_t* gw_src = a.gather_stride ? a.gathers + (uint64_t)t * a.gather_stride : a.gathers + o0.g;
+      write_gdesc(a.ix, gw_src, (uint32_t)(o1.g - o0.g), (uint32_t)o0.shr, a.desc + o0.g);
+    }
   }
 }
 

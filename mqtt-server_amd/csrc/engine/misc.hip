@@ -257,7 +257,17 @@ __global__ __launch_bounds__(256) void k_xlist(DevIndex ix, uint32_t n, const To
   else counts[t] = k;
 }
 
-__global__ __launch_bounds__(256) void k_xpack(uint32_t n, const TopicOff* __restrict__ off,
+__global__ __launch_bounds__(256) void k_xcounts(const uint32_t* __restrict__ xcount, const TopicCount* __restrict__ tc,
+                                                 uint32_t n, TopicCount* __restrict__ cnt) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) cnt[t] = TopicCount{xcount[t], tc[t].gathers, 0, 0, 0};
+}
+
+void launch_xcounts(const uint32_t* xcount, const TopicCount* tc, uint32_t n, TopicCount* cnt, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_xcounts, dim3((n + 255) / 256), dim3(256), 0, s, xcount, tc, n, cnt);
+}
+
+__global__ __launch_bounds__(256) void k_xpack(uint32_t n, const TopicOff* __restrict__ off, uint32_t g_stride,
                                                const uint32_t* __restrict__ xcount, const TopicOff* __restrict__ xoff,
                                                const TopicOff* __restrict__ xtot, const XEnt* __restrict__ xents,
                                                XEnt* __restrict__ ents, uint64_t cap, uint32_t* unsafe,
@@ -270,16 +280,16 @@ __global__ __launch_bounds__(256) void k_xpack(uint32_t n, const TopicOff* __res
   }
   if (t >= n || all > cap) return;
   const uint32_t c = xcount[t];
-  const uint64_t src = off[t].g, dst = xoff[t].g;
+  const uint64_t src = g_stride ? (uint64_t)t * g_stride : off[t].g, dst = xoff[t].g;
   for (uint32_t k = 0; k < c; k++) ents[dst + k] = xents[src + k];
 }
 
-void launch_xpack(uint32_t n, const TopicOff* off, const uint32_t* xcount, const TopicOff* xoff, const TopicOff* xtot,
-                  const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total,
-                  hipStream_t s) {
+void launch_xpack(uint32_t n, const TopicOff* off, uint32_t g_stride, const uint32_t* xcount, const TopicOff* xoff,
+                  const TopicOff* xtot, const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe,
+                  unsigned long long* total, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_xpack, dim3((n + 255) / 256), dim3(256), 0, s, n, off, xcount, xoff, xtot, xents, ents, cap,
-                     unsafe, total);
+  hipLaunchKernelGGL(k_xpack, dim3((n + 255) / 256), dim3(256), 0, s, n, off, g_stride, xcount, xoff, xtot, xents, ents,
+                     cap, unsafe, total);
 }
 
 void launch_xlist(bool count, const DevIndex& ix, uint32_t n, const TopicOff* off, const uint32_t* gathers,

@@ -72,6 +72,33 @@ def test_sharded_workload_parity(n_shards, device, gpu_available):
         e.check()
 
 
+@pytest.mark.parametrize("one_sync,patch_cap", [(1, 0), (1, 64), (0, 0)])
+def test_sharded_begin_end_sync_modes(one_sync, patch_cap, gpu_available):
+    """The sharded step's synchronisation modes, three batches each (the first one-sync begin finds
+    no buffers from earlier batches and runs again host-sized; the later ones fit): the one-sync
+    begin (export from k_desc, packed by k_xpack; walk-fused) and end; with 64-slot patch pools
+    (the one-sync end overflows and runs again host-sized, the begin's results and the imported
+    lists kept); MQ_OPT_ONE_SYNC 0 (the classic begin, k_xlist). Device and host results equal the
+    oracle every batch."""
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    w = W.gen_subscriptions(150000, 8000, seed=85)
+    shards, orc = _build(4, w, [])
+    for e in shards:
+        e.set_option(E.OPT_ONE_SYNC, one_sync)
+        if patch_cap:
+            e.set_option(E.OPT_PATCH_CAP, patch_cap)
+    for b, k in enumerate((3000, 9000, 9000)):
+        tb, to = W.gen_topics(w, k, seed=86 + b)
+        od, ocnt, _ = orc.digest_batch(tb, to, nthreads=min(16, os.cpu_count() or 8))
+        for device in (True, False):
+            dg, cnt, n_ents = _sharded_digests(shards, tb, to, device=device)
+            assert (cnt == ocnt).all(), (b, device)
+            bad = np.nonzero(dg != od)[0]
+            assert len(bad) == 0, f"batch {b} device={device}: {len(bad)} topics differ, first {bad[:5]}"
+            assert n_ents > 0
+
+
 @pytest.mark.parametrize("device", [False, True])
 def test_config3_eight_shards(device, gpu_available):
     """Config 3 in its stated form on one GPU: the config-3 mix at 1M
