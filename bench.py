@@ -628,6 +628,10 @@ def main():
         out["roofline"] = spans_roofline(prof, work, args.steps, n, args.subs)
         out["merge_work_per_topic"] = {k[6:]: work[k][0] / n for k in work
                                        if k.startswith("merge_") and k not in ("merge_topics", "merge_sets")}
+        if "set_cycles_max" in work:  # the longest merge set's wave (shader clocks) and its records
+            out["set_longest"] = {"cycles": work["set_cycles_max"][0], "records": work["set_records_max_wave"][0],
+                                  "cycles_mean": work.get("set_cycles_total", (0, 0))[0]
+                                  / max(1, work.get("dedup_sets", (1, 0))[0])}
     else:
         out["roofline"] = rows_roofline(prof, args, elapsed, out)
     cpu = None

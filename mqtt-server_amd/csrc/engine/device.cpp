@@ -405,6 +405,8 @@ std::string Device::verify(Index& ix) {
   if (r.empty()) r = cmp_mirror(inl_, ix.inl.m, "inl");
   if (r.empty()) r = cmp_mirror(children_, ix.children.m, "children");
   if (r.empty() && ix.sharded()) r = cmp_mirror(xinfo_, ix.xinfo, "xinfo");
+  if (r.empty() && ix.deep.size()) r = cmp_mirror(deep_, ix.deep, "deep");
+  if (r.empty() && ix.deep_codes.size()) r = cmp_mirror(deep_codes_, ix.deep_codes, "deep_codes");
   return r;
 }
 
@@ -432,6 +434,10 @@ void Device::sync(Index& ix, hipStream_t s) {
   inl_.sync(ix.inl.m, s, &uploaded_, st);
   children_.sync(ix.children.m, s, &uploaded_, st);
   if (ix.sharded()) xinfo_.sync(ix.xinfo, s, &uploaded_, st);
+  if (ix.deep.size()) {
+    deep_.sync(ix.deep, s, &uploaded_, st);
+    deep_codes_.sync(ix.deep_codes, s, &uploaded_, st);
+  }
   if (!st.runs.empty()) {  // one staging buffer: the run table, then each run's bytes
     const size_t table = (st.runs.size() * sizeof(ScatterRun) + 15) & ~size_t(15);
     const size_t need = table + st.bytes + 16 * st.runs.size();
@@ -485,6 +491,9 @@ DevIndex Device::dev_index(const Index& ix) const {
   d.inl = inl_.d;
   d.children = children_.d;
   d.xinfo = ix.sharded() ? xinfo_.d : nullptr;
+  d.deep = ix.sharded() && ix.deep.size() ? deep_.d : nullptr;
+  d.deep_codes = d.deep ? deep_codes_.d : nullptr;
+  d.deep_mask = d.deep ? ix.deep.size() - 1 : 0;
   d.retained_len = retained_len_;
   d.empty_topic_handle = empty_handle_;
   d.empty_topic_live = empty_live_ ? 1u : 0u;
@@ -503,7 +512,7 @@ void Device::check_err(hipStream_t s) {
                                         ((e & kErrWalkGuard) ? "walk iteration bound " : "") +
                                         ((e & kErrTableFull) ? "merge table full " : "") +
                                         ((e & kErrPickGuard) ? "shared pick partitions " : "") +
-                                        ((e & kErrDeepRank) ? "cross-shard merge deeper than 32 levels" : "")};
+                                        ((e & kErrDeepRank) ? "cross-shard rank tie without a deep-path entry" : "")};
   }
 }
 
@@ -1771,7 +1780,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     uint64_t sum[kWork] = {};
     for (uint32_t r = 0; r < 2 * kPatchRegions; r++)
-      for (uint32_t k = 0; k < kWork; k++) sum[k] += w[r * kWork + k];
+      for (uint32_t k = 0; k < kWork; k++) sum[k] = k >= 24 ? std::max<uint64_t>(sum[k], w[r * kWork + k]) : sum[k] + w[r * kWork + k];
     prof.count("merge_pair_entries", sum[0]);
     prof.count("merge_records", sum[1]);
     prof.count("merge_links", sum[2]);
@@ -1793,6 +1802,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       prof.count((std::string("merge_big_gathers_v") + kBig[b]).c_str(), sum[16 + b]);
       prof.count((std::string("merge_big_visits_v") + kBig[b]).c_str(), sum[20 + b]);
     }
+    prof.count("set_cycles_max", sum[24]);
+    prof.count("set_records_max_wave", sum[25]);
     prof.count("merge_topics", n);
   }
   // A pipelined copy is armed (pc_) only when the batch has passed its error check: a batch that

@@ -290,6 +290,8 @@ class Device {
   DevMirror<InlRec> inl_;
   DevMirror<ChildRec> children_;
   DevMirror<XInfo> xinfo_;
+  DevMirror<DeepTail> deep_;
+  DevMirror<uint32_t> deep_codes_;
   DevBuf in_bytes_, in_offs_;
   DevBuf counts_, offs_, bsum_, bpre_, gathers_;
   // Output chunks alternate between two buffer sets so that k_merge of chunk i (side stream)

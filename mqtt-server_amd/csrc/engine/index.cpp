@@ -227,6 +227,56 @@ void Index::set_rank(uint32_t n, uint32_t parent, std::string_view seg, bool mar
   else xinfo.h[n] = x;
 }
 
+// The order of two deep paths whose rank keys tie (layout.h DeepTail): filter fid's codes for its
+// levels 33.., kept for the device's tie-break (merge.hip deep_before). Entries are overwritten
+// when a filter id is seen again (a filter id names one filter while it is subscribed).
+void Index::note_deep(uint32_t fid, const uint32_t* segs, uint32_t depth) {
+  if (depth <= 32 || fid == kNone) return;
+  const uint32_t n = (depth - 32 + 15) / 16;
+  thread_local std::vector<uint32_t> w;
+  w.assign(n, 0u);
+  for (uint32_t i = 32; i < depth; i++) {
+    const uint32_t code = segs[i] == 0 ? 2u : (segs[i] == 1 ? 3u : 1u);  // '+' 2, '#' 3, literal 1
+    const uint32_t j = i - 32;
+    w[j / 16] |= code << (30 - 2 * (j % 16));
+  }
+  auto find = [&](uint32_t f) -> size_t {
+    const size_t mask = deep.size() - 1;
+    size_t sl = mix64(f) & mask;
+    while (deep.h[sl].fid != kNone && deep.h[sl].fid != f) sl = (sl + 1) & mask;
+    return sl;
+  };
+  if (deep.size()) {
+    const DeepTail& e = deep.h[find(fid)];
+    if (e.fid == fid && e.n == n && std::equal(w.begin(), w.end(), deep_codes.h.begin() + e.off)) return;
+  }
+  if ((n_deep_ + 1) * 2 > deep.size()) {  // at most half full: rehash into twice the slots
+    std::vector<DeepTail> old;
+    old.swap(deep.h);
+    deep.h.assign(std::max<size_t>(64, old.size() * 2), DeepTail{kNone, 0, 0, 0});
+    deep.epoch++;
+    deep.all_dirty = true;
+    for (const DeepTail& e : old)
+      if (e.fid != kNone) deep.h[find(e.fid)] = e;
+  }
+  const size_t sl = find(fid);
+  if (deep.h[sl].fid == kNone) n_deep_++;
+  const uint32_t off = (uint32_t)deep_codes.size();
+  deep_codes.grow_to(off + n, 0u);
+  for (uint32_t k = 0; k < n; k++) deep_codes.at_w(off + k) = w[k];
+  deep.at_w(sl) = DeepTail{fid, off, n, 0};
+  version_++;
+}
+
+void Index::note_deep_node(uint32_t n, uint32_t fid) {
+  if (nh_[n].depth <= 32) return;
+  thread_local std::vector<uint32_t> pa;
+  pa.resize(nh_[n].depth);
+  int la;
+  path_strs(n, pa.data(), &la);
+  note_deep(fid, pa.data(), (uint32_t)la);
+}
+
 // Qos | NoLocal of partner `p` (a node of this shard, or kForeign | fid) of `client`'s slot
 uint32_t Index::partner_meta(uint32_t p, uint32_t client) const {
   uint32_t i = kNone;
@@ -1271,6 +1321,7 @@ int Index::foreign_subscribe(std::string_view filter, uint32_t client, uint32_t 
   path_of(filter, 0, path);
   ForeignSub f{client, fid, meta, (uint32_t)fpaths_.size(), (uint32_t)path.size()};
   for (std::string_view seg : path) fpaths_.push_back(intern_str(seg));
+  if (f.depth > 32) note_deep(fid, fpaths_.data() + f.path_off, f.depth);
   if (!fsub_free_.empty()) {
     i = fsub_free_.back();
     fsub_free_.pop_back();
@@ -1421,6 +1472,7 @@ int Index::subscribe(std::string_view filter, uint32_t client, uint32_t filter_i
   if (sharded() && xinfo.h[n].fid == kNone) {
     if (filter_id & kForeign) throw std::invalid_argument("sharded index: filter ids must be < 2^31");
     xinfo.at_w(n).fid = filter_id;
+    note_deep_node(n, filter_id);
   }
   std::vector<uint32_t>& mine = client_nodes_[client];
   thread_local std::vector<uint32_t> comp, all;

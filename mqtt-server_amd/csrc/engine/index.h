@@ -384,6 +384,8 @@ class Index {
   SlabPool<InlRec> inl;
   SlabPool<ChildRec> children;  // per node: its children (NodeMsg.child_off/child_cnt)
   Mirror<XInfo> xinfo;          // sharded only (empty otherwise): per node fid + rank key
+  Mirror<DeepTail> deep;        // sharded only: deep filters' codes beyond 32 levels, by fid
+  Mirror<uint32_t> deep_codes;  //   (layout.h DeepTail; empty while no filter is that deep)
   // Retained packet stored on topic "" (retainPath "" is "no path", Q6): literal-final
   // lookups of particles without a retain path read this entry (topics.go:573).
   bool empty_topic_live = false;
@@ -467,6 +469,10 @@ class Index {
   }
   // (mark = false: a parallel bulk build, which marks the whole array dirty itself)
   void set_rank(uint32_t n, uint32_t parent, std::string_view seg, bool mark = true);
+  // a deep filter's DeepTail from its segment string ids (path_strs / fpaths_: 0 '+', 1 '#')
+  void note_deep(uint32_t fid, const uint32_t* segs, uint32_t depth);
+  void note_deep_node(uint32_t n, uint32_t fid);
+  uint32_t n_deep_ = 0;
   // (mark = false: the whole list moves to a new slab; no slot changes its place k)
   void move_slot(uint32_t n, uint32_t from, uint32_t to, bool mark = true);
   void part_set(uint32_t pos, const std::vector<uint32_t>& nodes);

@@ -655,7 +655,10 @@ void Index::subscribe_bulk(const uint8_t* bytes, const uint64_t* offs, const uin
     for (size_t k = b; k < e; k++) pos[k] = L.sub_off + (is_merge[k] ? mi++ : di++);
     if (L.n_merge) merge_dirty(node);
     n_merge_ += L.n_merge;
-    if (sharded() && xinfo.h[node].fid == kNone) xinfo.h[node].fid = filter_ids[slots[b].i];
+    if (sharded() && xinfo.h[node].fid == kNone) {
+      xinfo.h[node].fid = filter_ids[slots[b].i];
+      note_deep_node(node, xinfo.h[node].fid);
+    }
     b = e;
   }
   subp_.resize(subs.m.size(), PartList{0, 0, 0});

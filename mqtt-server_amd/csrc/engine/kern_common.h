@@ -138,14 +138,22 @@ __device__ __forceinline__ uint32_t prefix_before(uint64_t mask) {
 }
 
 // Exclusive wave-wide prefix sum (64 lanes); *total receives the sum.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {  // lanes whose source is outside the row read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+// (DPP: rows' prefix sums by row_shr, then row 0's total into rows 1 and 3 by row_bcast:15 and
+// rows 0-1's into rows 2 and 3 by row_bcast:31; the total is lane 63's, read as a scalar)
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t* total) {
+  (void)lane;
   uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
-  *total = __shfl(x, 63, 64);
+  x += dpp<0x111>(x);
+  x += dpp<0x112>(x);
+  x += dpp<0x114>(x);
+  x += dpp<0x118>(x);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   return x - v;
 }
 
@@ -173,7 +181,7 @@ struct EdgeHit {
 };
 __device__ __forceinline__ EdgeHit lookup_edge(const DevIndex& ix, uint32_t parent, const SegKey& k,
                                                const uint8_t* seg, uint32_t len) {
-  uint64_t i = edge_hash(parent, k) & ix.edge_mask;
+  uint64_t i = edge_slot(parent, k, ix.edge_mask);
   for (uint64_t probes = 0; probes <= ix.edge_mask; probes++) {
     const EdgeSlot e = ix.edges[i];
     if (e.parent == kEdgeEmpty) break;
@@ -194,21 +202,70 @@ __device__ __forceinline__ uint32_t lookup(const DevIndex& ix, uint32_t parent, 
   return lookup_edge(ix, parent, k, seg, len).child;
 }
 
+// Group collectives. A 16-lane group is a DPP row (8 lanes: half a row), so its prefix sums and
+// sums are DPP moves folded into the adds — no LDS traffic, no lane-index arithmetic, no wait — and
+// the broadcast of its last lane one ds_swizzle; other widths go through ds_bpermute (__shfl).
+template <uint32_t G, int D = 1>
+__device__ __forceinline__ uint32_t grp_incl_dpp(uint32_t v, uint32_t sub) {
+  if constexpr (D >= (int)G) {
+    return v;
+  } else {
+    const uint32_t y = dpp<0x110 + D>(v);  // row_shr:D
+    if (G == 16 || sub >= (uint32_t)D) v += y;  // (8-lane groups: not across the group)
+    return grp_incl_dpp<G, 2 * D>(v, sub);
+  }
+}
 // Inclusive prefix sum over the G lanes of a group (G a power of two <= 64; sub = lane % G).
 template <uint32_t G>
 __device__ __forceinline__ uint32_t grp_incl(uint32_t v, uint32_t sub) {
+  if constexpr (G == 16 || G == 8) {
+    return grp_incl_dpp<G>(v, sub);
+  } else {
 #pragma unroll
-  for (uint32_t d = 1; d < G; d <<= 1) {
-    const uint32_t y = __shfl_up(v, d, G);
-    if (sub >= d) v += y;
+    for (uint32_t d = 1; d < G; d <<= 1) {
+      const uint32_t y = __shfl_up(v, d, G);
+      if (sub >= d) v += y;
+    }
+    return v;
   }
-  return v;
+}
+// lane G-1's value, to every lane of the group (ds_swizzle bit mode: lane (lane & and) | or)
+template <uint32_t G>
+__device__ __forceinline__ uint32_t grp_last(uint32_t v) {
+  if constexpr (G == 16 || G == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (32 - G) | (G - 1) << 5);
+  else return __shfl(v, G - 1, G);
 }
 template <uint32_t G>
 __device__ __forceinline__ uint32_t grp_sum(uint32_t v) {
+  if constexpr (G == 16 || G == 8) {
+    v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]: quad sums
+    v += dpp<0x141>(v);  // row_half_mirror: 8-lane sums
+    if (G == 16) v += dpp<0x140>(v);  // row_mirror
+    return v;
+  } else {
 #pragma unroll
-  for (uint32_t d = 1; d < G; d <<= 1) v += __shfl_xor(v, d, G);
-  return v;
+    for (uint32_t d = 1; d < G; d <<= 1) v += __shfl_xor(v, d, G);
+    return v;
+  }
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  return (uint64_t)dpp<CTRL>((uint32_t)v) | (uint64_t)dpp<CTRL>((uint32_t)(v >> 32)) << 32;
+}
+template <uint32_t G>
+__device__ __forceinline__ uint64_t grp_sum64(uint64_t v) {
+  if constexpr (G == 16 || G == 8) {
+    v += dpp64<0xB1>(v);
+    v += dpp64<0x4E>(v);
+    v += dpp64<0x141>(v);
+    if (G == 16) v += dpp64<0x140>(v);
+    return v;
+  } else {
+#pragma unroll
+    for (uint32_t d = 1; d < G; d <<= 1) v += __shfl_xor(v, d, G);
+    return v;
+  }
 }
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
@@ -259,14 +316,7 @@ __device__ TopicOff block_scan_incl(TopicOff v, TopicOff* wave_tot /*4*/) {
 
 
 // 16-lane inclusive scan (lanes of a 16-lane group of the wavefront; sub = lane & 15)
-__device__ __forceinline__ uint32_t g16_incl(uint32_t v, uint32_t sub) {
-#pragma unroll
-  for (uint32_t d = 1; d < 16; d <<= 1) {
-    const uint32_t y = __shfl_up(v, d, 16);
-    if (sub >= d) v += y;
-  }
-  return v;
-}
+__device__ __forceinline__ uint32_t g16_incl(uint32_t v, uint32_t sub) { return grp_incl<16>(v, sub); }
 
 // The GDesc records of one topic's gathers for k_merge's slow paths (a topic beyond the map):
 // rows topic-relative, a merge gather's pair-block header in s_pos / s_src and, on a sharded
@@ -348,18 +398,15 @@ __device__ __forceinline__ void desc_grp(const DescArgs& a, uint32_t t, uint32_t
         const XInfo xn = a.ix.xinfo[gw & kGatherNode];
         a.xents[g0 + n_x + xi - 1] = XEnt{xn.fid, xn.deep, xn.rank};
       }
-      n_x += __shfl(xi, G - 1, G);
+      n_x += grp_last<G>(xi);
     }
-    rpos += __shfl(rn_i, G - 1, G);
-    spos += __shfl(sh_i, G - 1, G);
-    ipos += __shfl(in_i, G - 1, G);
-    n_mg += __shfl(inc_i, G - 1, G);
+    rpos += grp_last<G>(rn_i);
+    spos += grp_last<G>(sh_i);
+    ipos += grp_last<G>(in_i);
+    n_mg += grp_last<G>(inc_i);
   }
-#pragma unroll
-  for (uint32_t d = 1; d < G; d <<= 1) {
-    sig += __shfl_xor(sig, d, G);
-    n_merge += __shfl_xor(n_merge, d, G);
-  }
+  sig = grp_sum64<G>(sig);
+  n_merge = grp_sum<G>(n_merge);
   const unsigned long long msig = mix64(sig + n_mg) | 1ull;  // never 0 (the dedup table's empty key)
   if (a.dd_keys) {  // k_dedup_insert's work, one lane per topic
     const uint32_t slot = dedup_insert(a.dd_keys, a.dd_vals, a.dd_mask, t, sub == 0 && n_mg != 0 && n_mg <= kPairMax,

@@ -49,7 +49,7 @@ constexpr uint32_t kBitNonBase = 1u, kBitNoLocal = 2u, kBitQos1 = 4u, kBitQos2 =
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
-constexpr uint32_t kWork = 24;  // [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
+constexpr uint32_t kWork = 26;  // [24], [25]: the longest set's cycles and records (max); [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
                                 // [8] topics the kernel resolved, [9] bytes of their maps' sources read;
                                 // set pass fold: [10] visits folded, [11] visits of merge gathers too big
                                 // to fold, [12] those gathers, [13] their may-merge records (n_merge),
@@ -78,6 +78,9 @@ struct DevIndex {
   const InlRec* inl;
   const ChildRec* children;
   const XInfo* xinfo;  // sharded index only (else null): per node filter id + rank key
+  const DeepTail* deep;       // sharded index with deep filters (else null): layout.h DeepTail
+  const uint32_t* deep_codes;
+  uint64_t deep_mask;         // the table's slots - 1
   uint64_t retained_len;
   uint64_t empty_topic_handle;
   uint32_t empty_topic_live;
@@ -88,7 +91,7 @@ struct DevIndex {
 constexpr uint32_t kErrWalkGuard = 1u;
 constexpr uint32_t kErrTableFull = 2u;
 constexpr uint32_t kErrPickGuard = 4u;  // k_pick: hash partitions exhausted
-constexpr uint32_t kErrDeepRank = 8u;   // sharded merge: two ranks tie beyond the rank key's 32 levels
+constexpr uint32_t kErrDeepRank = 8u;   // sharded merge: a rank tie no DeepTail entry orders (a missing entry)
 // one-sync batches (*unsafe bits): the batch must run again with host-sized buffers
 constexpr uint32_t kUnsafeSpans = 1u;    // spans / GDesc records past their buffers
 constexpr uint32_t kUnsafeDesc = 2u;     // k_merge: a slow-path topic without GDesc records

@@ -66,8 +66,31 @@ MQ_HD SegKey seg_key(const uint8_t* p, uint32_t len) {
 
 MQ_HD bool seg_is_long(const SegKey& k) { return (k.k1 & kLongMarker) == kLongMarker; }
 
+// The edge table's slot hash. 32-bit integer multiplies are quarter-rate on CDNA and the walk
+// hashes one key per frontier particle and level, so the key's four words are folded with rotates
+// and one multiply, then mixed by murmur3's 32-bit finalizer (three multiplies, against eleven
+// for a 64-bit mix of the same key). Tables of 2^32 slots or more take their high bits from a
+// second round (edge_hash); below that every probe uses edge_hash32 alone.
+MQ_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+MQ_HD uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+MQ_HD uint32_t edge_hash32(uint32_t parent, const SegKey& k) {
+  return fmix32((uint32_t)k.k0 ^ rotl32((uint32_t)(k.k0 >> 32), 11) ^ rotl32((uint32_t)k.k1, 21) ^
+                rotl32((uint32_t)(k.k1 >> 32), 5) ^ parent * 0x9e3779b1u);
+}
 MQ_HD uint64_t edge_hash(uint32_t parent, const SegKey& k) {
-  return mix64(k.k0 ^ (k.k1 * 0x9e3779b97f4a7c15ull) ^ ((uint64_t)parent * 0xd6e8feb86659fd93ull));
+  const uint32_t h = edge_hash32(parent, k);
+  return (uint64_t)fmix32(h ^ 0x5bd1e995u) << 32 | h;
+}
+// edge_hash(parent, k) & mask, the high half only for tables of 2^32 slots or more
+MQ_HD uint64_t edge_slot(uint32_t parent, const SegKey& k, uint64_t mask) {
+  return (mask >> 32) ? edge_hash(parent, k) & mask : (uint64_t)(edge_hash32(parent, k) & (uint32_t)mask);
 }
 
 // ---- trie edges -----------------------------------------------------------------------------
@@ -163,6 +186,18 @@ struct XEnt {  // 16 B
   uint32_t fid;
   uint32_t deep;
   uint64_t rank;
+};
+
+// The DFS order beyond the rank key's 32 levels (sharded index): a deep filter's codes for its
+// levels 33.. (kappa + 1 as in the rank key), 16 per word from the top, zero-padded, in
+// Index::deep_codes[off, off + n). Words compare as the rank keys do, so two deep paths that tie
+// in their keys are ordered by their first differing word (a proper prefix first). Entries sit
+// in an open-addressed table keyed by filter id (Index::deep; fid kNone: a free slot), holding
+// every deep filter the shard knows: its own nodes' and its foreign partners'.
+struct DeepTail {  // 16 B
+  uint32_t fid;
+  uint32_t off, n;
+  uint32_t pad;
 };
 
 struct SegInfo {  // long segment bytes in the segment pool

@@ -460,6 +460,36 @@ __device__ __forceinline__ uint64_t gdesc_rank(const GDesc& d) {
 // and DFS order compares rank keys first (SPANS must be true).
 // SET (span format, merge-set dedup): the set pass (a.dd_phase 1), compiled apart so that the
 // topic pass's copy, inline and result code does not weigh on its register allocation.
+// Sharded index: do filters fh and fg, whose rank keys tie, come in this DFS order? A tie means
+// that their first 32 levels agree: both are deeper (their DeepTail codes decide, compared as the
+// rank keys are, a proper prefix first), or one is exactly 32 levels deep — a proper prefix of
+// the other, so first. A tie no entry explains trips kErrDeepRank.
+__device__ __noinline__ bool deep_before(const DevIndex& ix, uint32_t fh, uint32_t fg) {
+  auto find = [&](uint32_t f) -> const DeepTail* {
+    if (!ix.deep) return nullptr;
+    uint64_t sl = mix64(f) & ix.deep_mask;
+    for (;;) {
+      const DeepTail* e = ix.deep + sl;
+      if (e->fid == f) return e;
+      if (e->fid == kNone) return nullptr;
+      sl = (sl + 1) & ix.deep_mask;
+    }
+  };
+  const DeepTail* h = find(fh);
+  const DeepTail* g = find(fg);
+  if (!h || !g) {
+    if (!h && !g) atomicOr(ix.err, kErrDeepRank);
+    return !h && g;
+  }
+  const uint32_t n = max(h->n, g->n);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t wh = i < h->n ? ix.deep_codes[h->off + i] : 0u;
+    const uint32_t wg = i < g->n ? ix.deep_codes[g->off + i] : 0u;
+    if (wh != wg) return wh < wg;
+  }
+  return false;  // one path (a filter lives on one shard): not reached
+}
+
 template <bool SPANS, bool XS, int WPE, bool SET = false, uint32_t PB = kPartBatch>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
@@ -722,12 +752,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       return Pos{0, kNone, false};
     };
     // does the gathered node at (rh, gh) come before the record's own (rg, gg) in DFS order?
-    auto before = [&](uint64_t rh, uint32_t gh, uint64_t rg, uint32_t gg) __attribute__((always_inline)) -> bool {
+    // hn / gn: the nodes (another shard's as kForeign | fid), read only on a tie
+    auto before = [&](uint64_t rh, uint32_t gh, uint64_t rg, uint32_t gg, auto&& hn, auto&& gn)
+        __attribute__((always_inline)) -> bool {
       if (!XS) return gh < gg;
       if (rh != rg) return rh < rg;
       if (gh != kNone) return gh < gg;  // both on this shard: gather order is DFS order
-      atomicOr(a.ix.err, kErrDeepRank);  // another shard's node tied beyond the key's 32 levels
-      return false;
+      // another shard's node tied with the record's beyond the key's 32 levels
+      const uint32_t h = hn(), g = gn();
+      return deep_before(a.ix, (h & kForeign) ? h & ~kForeign : a.ix.xinfo[h].fid,
+                         (g & kForeign) ? g & ~kForeign : a.ix.xinfo[g].fid);
     };
 
     // Resolve one record whose client may have other matches for this topic: its partners that
@@ -741,7 +775,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // mw: the record's meta | kSlotIdentPos when its identifier is > 0 (PairSlot.meta); (rg, gi):
     // its gather's rank key and gather index.
     auto resolve = [&](bool active, uint32_t mw, uint32_t row, uint64_t rg, uint32_t gi, uint32_t via,
-                       uint32_t mp_off, uint32_t mp_cnt) __attribute__((always_inline)) {
+                       uint32_t mp_off, uint32_t mp_cnt, auto&& gnode) __attribute__((always_inline)) {
       bool counted = false, nonbase = false, want = false;
       uint32_t pmeta = 0;
       if (active) {
@@ -776,7 +810,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
               other = SPANS && via != kNone && first != via && !(SET && (exp_bits & 16u));
             }
             bound = true;
-            if (before(ph.rk, ph.gi, rg, gi)) {
+            const uint32_t hnode = pb[u].node;
+            if (before(ph.rk, ph.gi, rg, gi, [&] { return hnode; }, gnode)) {
               base = false;
               continue;
             }
@@ -844,7 +879,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const uint32_t xa = h_ga[wv][jj];
           w_rec += r < v1;
           resolve(r < v1 && (PP == 1 || hash32(e.k) % PP == pp), e.meta, setrel ? (xa << kSetRowBits | e.k) : mg_row[xa] + e.k,
-                  XS ? mg_rank[wv][xa] : 0ull, mg_gi[wv][xa], mg_node[wv][h_hb[wv][jj]], e.mp_off, e.mp_cnt);
+                  XS ? mg_rank[wv][xa] : 0ull, mg_gi[wv][xa], mg_node[wv][h_hb[wv][jj]], e.mp_off, e.mp_cnt,
+                  [&] { return mg_node[wv][xa]; });
         }
       };
       auto flush_hits = [&]() __attribute__((always_inline)) {
@@ -884,7 +920,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           if (r < v1) {
             const uint32_t xa = h_ga[wv][jj], hb = h_hb[wv][jj];
             const bool earlier = before(XS ? mg_rank[wv][hb] : 0ull, mg_gi[wv][hb], XS ? mg_rank[wv][xa] : 0ull,
-                                        mg_gi[wv][xa]);
+                                        mg_gi[wv][xa], [&] { return mg_node[wv][hb]; }, [&] { return mg_node[wv][xa]; });
             const uint32_t key = xa << kSetRowBits | e.k;
             if (!(exp_bits & 4096u)) {  // (MQ_OPT_SET_EXP bit 12, development builds: no table inserts)
               uint32_t sl = hash32(key) & (kFoldSlots - 1);
@@ -968,7 +1004,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             const uint32_t hk = hash32(e.k);
             if (r < v1 && hk % PP == pp) {
               const uint32_t hb = h_hb[wv][jj];
-              const bool earlier = before(XS ? mg_rank[wv][hb] : 0ull, mg_gi[wv][hb], rg, gg);
+              const bool earlier = before(XS ? mg_rank[wv][hb] : 0ull, mg_gi[wv][hb], rg, gg,
+                                          [&] { return mg_node[wv][hb]; }, [&] { return mg_node[wv][xa]; });
               const uint32_t pm = e.meta >> kSlotPartShift;  // the partner's Qos | NoLocal << 2
               const uint32_t bits = (earlier ? kBitNonBase : 0u) | ((pm & 4u) ? kBitNoLocal : 0u) |
                                     ((pm & 3u) == 1u ? kBitQos1 : 0u) | ((pm & 3u) == 2u ? kBitQos2 : 0u);
@@ -1198,7 +1235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           const SubRec rec = a.ix.subs[pos];
           w_rec += act;
           resolve(act, rec.meta | (rec.ident > 0 ? kSlotIdentPos : 0u), d.r_pos + L.n_direct + c0 + lane, rank_of(d),
-                  i, kNone, mr.off, mr.cnt);
+                  i, kNone, mr.off, mr.cnt, [&] { return d.word & kGatherNode; });
         }
       }
     }

@@ -488,7 +488,7 @@ __global__ __launch_bounds__(256) void k_img_edges(DevIndex ix, const uint32_t* 
     if (qp == kNone) continue;  // (not reached: an image particle's parent is in the image)
     const SegKey k{e.k0, e.k1};
     const unsigned long long want = (unsigned long long)qp | ((unsigned long long)qc << 32);
-    uint64_t j = edge_hash(qp, k) & mask;
+    uint64_t j = edge_slot(qp, k, mask);
     bool put = false;
     for (uint64_t probes = 0; probes <= mask && !put; probes++) {
       unsigned long long* w = reinterpret_cast<unsigned long long*>(&edges[j]);
@@ -541,7 +541,7 @@ __device__ __forceinline__ uint32_t img_pos(const MsgImg& img, uint32_t c) {
 __device__ __forceinline__ uint32_t img_child(const MsgImg& img, const DevIndex& ix, uint32_t u, const SegKey& k,
                                               const uint8_t* seg, uint32_t len) {
   if (!img.edges) return img_pos(img, lookup(ix, img.node[u], k, seg, len));
-  uint64_t i = edge_hash(u, k) & img.edge_mask;
+  uint64_t i = edge_slot(u, k, img.edge_mask);
   for (uint64_t probes = 0; probes <= img.edge_mask; probes++) {
     const ImgEdge e = img.edges[i];
     if (e.parent == kImgEdgeEmpty) break;

@@ -454,6 +454,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         atomicAdd(wc + 5, (unsigned long long)(c_pairs - c_map));
         atomicAdd(wc + 6, (unsigned long long)(c_end - c_pairs));
         atomicAdd(wc + 7, (unsigned long long)(c_end - c_start));
+        atomicMax(wc + 24, (unsigned long long)(c_end - c_start));
+        atomicMax(wc + 25, (unsigned long long)rr);
       }
     }
   }

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t idx = nsl + inc - c;
     for (; m; m &= m - 1, idx++)
       if (idx < kLv) sl[q][idx] = (k << 4) + (uint32_t)(__ffs(m) - 1);
-    nsl += __shfl(inc, G - 1, G);
+    nsl += grp_last<G>(inc);
   }
   const uint32_t L = nch ? nsl + 1 : 0u;  // levels (0: the empty topic, which matches nothing)
   bool fb = live && L > kLv;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool gP = mine && !has_next && fe.plus != kNone;
     const uint32_t gc = (uint32_t)gH + (uint32_t)gL + (uint32_t)gC + (uint32_t)gP;
     const uint32_t gi = grp_incl<G>(gc, sub);
-    const uint32_t gtot = __shfl(gi, G - 1, G);
+    const uint32_t gtot = grp_last<G>(gi);
     if (act && ng + gtot > kStage) fb = true;
     if (act && !fb) {
       uint32_t p = ng + gi - gc;
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool fP = mine && has_next && fe.plus != kNone;
     const uint32_t fc = (uint32_t)fL + (uint32_t)fP;
     const uint32_t fi = grp_incl<G>(fc, sub);
-    const uint32_t ftot = __shfl(fi, G - 1, G);
+    const uint32_t ftot = grp_last<G>(fi);
     if (act && has_next && ftot > G) fb = true;
     if (act && !fb && has_next) {
       uint32_t p = fi - fc;

@@ -118,8 +118,19 @@ def exchange_exact(counts, ents):
     ne_all = torch.empty(world, dtype=torch.int64, device=on)
     dist.all_gather_into_tensor(ne_all, ne)
     c_all = torch.empty(world * counts.numel(), dtype=torch.int32, device=on)
-    dist.all_gather_into_tensor(c_all, counts)
-    ne_host = ne_all.cpu().tolist()  # the receive sizes
+    if on.type == "cuda":
+        # the receive sizes come back through pinned memory while the counts' all-gather runs
+        ne_pin = torch.empty(world, dtype=torch.int64, pin_memory=True)
+        ne_pin.copy_(ne_all, non_blocking=True)
+        sized = torch.cuda.Event()
+        sized.record()
+        counts_done = dist.all_gather_into_tensor(c_all, counts, async_op=True)
+        sized.synchronize()
+        ne_host = ne_pin.tolist()
+    else:
+        dist.all_gather_into_tensor(c_all, counts)
+        counts_done = None
+        ne_host = ne_all.tolist()
     recv = {r: torch.empty(16 * ne_host[r], dtype=torch.uint8, device=on) for r in range(world) if r != rank}
     ops = []
     for r in range(world):
@@ -132,6 +143,8 @@ def exchange_exact(counts, ents):
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    if counts_done is not None:
+        counts_done.wait()
     return c_all, recv, ne_host, ents
 
 

@@ -143,24 +143,39 @@ def test_sharded_many_merging_clients(device, gpu_available):
     assert (cnt == ocnt).all() and (dg == od).all()
 
 
-def test_sharded_deep_tie_fails_loudly(gpu_available):
-    """Two filters of one client, on different shards, agreeing in their first 32 levels' kinds
-    and both matching a topic: the rank keys tie, and the batch fails (MQ_EIO) instead of
-    guessing the order."""
+@pytest.mark.parametrize("device", [False, True])
+def test_sharded_deep_ties_match_oracle(device, gpu_available):
+    """Filters of one client on different shards agreeing in their first 32 levels' kinds (the
+    rank keys tie): the deep-path codes order them (layout.h DeepTail, merge.hip deep_before) —
+    deeper '+' / '#' / literal levels, a 32-level filter that is a proper prefix of a deeper one,
+    and paths beyond 48 levels (a second code word). The shards' results equal the oracle's."""
     from mqmatch import engine as E
-    shards = [E.Engine(shard=k, n_shards=2) for k in range(2)]
-    pre = "/".join(f"l{i}" for i in range(33))
-    cands = [pre + "/" + s for s in ("x", "+", "#")] + [pre + "/x/" + s for s in ("y", "+", "#")]
-    owner = {}
-    for f in cands:
-        for k, e in enumerate(shards):
-            if e.subscribe(f, 1, len(owner), 0, 0, 5) == 1:
-                owner[f] = k
-    assert len(set(owner.values())) == 2, owner
-    import torch
-    tb, to = E.pack_strings([pre + "/x/y"])
-    d_tb, d_to = torch.from_numpy(tb).cuda(), torch.from_numpy(to.view(np.int64)).cuda()
-    xs = [e.match_spans_begin(d_tb.data_ptr(), d_to.data_ptr(), 1) for e in shards]
-    with pytest.raises(E.EngineError):
-        for k, e in enumerate(shards):
-            e.match_spans_end_expanded([xs[1 - k]], 1)
+    n_shards = 3
+    shards = [E.Engine(shard=k, n_shards=n_shards) for k in range(n_shards)]
+    o = O.OracleIndex()
+    pre = "/".join(f"l{i}" for i in range(32))
+    pre52 = pre + "/" + "/".join(f"m{i}" for i in range(20))
+    fs = [pre, pre + "/#", pre + "/x", pre + "/+", pre + "/x/#", pre + "/x/y", pre + "/x/+", pre + "/+/y",
+          pre + "/+/#", pre + "/+/+", "/".join(["+"] * 32) + "/x/y", pre52, pre52 + "/#", pre52 + "/z",
+          pre52 + "/+", pre52 + "/z/#", pre + "/m0/#"]
+    owners = set()
+    r = random.Random(87)
+    for c in range(60):
+        for f in r.sample(fs, r.randint(2, 8)):
+            q, ident, nl = r.randint(0, 2), r.choice([0, 3, 9]), r.random() < 0.3
+            for k, e in enumerate(shards):
+                if e.subscribe(f, c, fs.index(f), q, 1 if nl else 0, ident) == 1:
+                    owners.add(k)
+            o.subscribe(f"c{c}", f, q, ident, nl, client_id=c, filter_id=fs.index(f))
+    assert len(owners) >= 2, owners
+    topics = [pre, pre + "/x", pre + "/x/y", pre + "/q/y", pre + "/x/q", pre52, pre52 + "/z", pre52 + "/z/w",
+              pre + "/m0", "/".join(f"l{i}" for i in range(31))]
+    tb, to = E.pack_strings(topics)
+    dg, cnt, n_ents = _sharded_digests(shards, tb, to, device=device)
+    od, ocnt, _ = o.digest_batch(tb, to, nthreads=4)
+    assert n_ents > 0
+    assert (cnt == ocnt).all()
+    bad = np.nonzero(dg != od)[0]
+    assert len(bad) == 0, f"topics {[topics[i] for i in bad]} differ"
+    for e in shards:
+        e.check()

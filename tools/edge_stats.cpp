@@ -2,6 +2,7 @@
 // root's and level 1's children take (the walk's level-0 / level-1 probes), for staging them in LDS.
 //   make -C mqtt-server_amd build/edge_stats && mqtt-server_amd/build/edge_stats 10000000
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -52,5 +53,21 @@ int main(int argc, char** argv) {
   printf("nodes %zu, edges %llu (table %zu slots, %.1f MB)\n", ix.walk.size(), (unsigned long long)total,
          ix.edges.size(), ix.edges.size() * sizeof(EdgeSlot) / 1e6);
   for (int d = 0; d < 8; d++) printf("  children of level-%d particles: %llu\n", d, (unsigned long long)per[d]);
+  // probe distances of the stored edges from their home slots (the walk's hit probes), and the
+  // run length from a key's home slot to the first empty slot (its miss probes)
+  const uint64_t mask = ix.edges.size() - 1;
+  uint64_t dsum = 0, dmax = 0, hist[5] = {0};
+  for (size_t i = 0; i < ix.edges.size(); i++) {
+    const EdgeSlot& e = ix.edges.h[i];
+    if (e.parent == kEdgeEmpty || e.parent == kEdgeTomb) continue;
+    const uint64_t d = (i - (edge_hash(e.parent, SegKey{e.k0, e.k1}) & mask)) & mask;
+    dsum += d;
+    dmax = std::max(dmax, d);
+    hist[std::min<uint64_t>(d, 4)]++;
+  }
+  printf("probe distance: mean %.4f, max %llu; 0: %llu, 1: %llu, 2: %llu, 3: %llu, 4+: %llu\n",
+         total ? (double)dsum / total : 0.0, (unsigned long long)dmax, (unsigned long long)hist[0],
+         (unsigned long long)hist[1], (unsigned long long)hist[2], (unsigned long long)hist[3],
+         (unsigned long long)hist[4]);
   return 0;
 }
