@@ -149,7 +149,7 @@ def read_walk_traffic(path, n_subs, n_topics, edge_load, walk_group, fused):
         return None
 
 
-def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step, edge_load=16, walk_group=16):
+def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step, edge_load=16, walk_group=16, no_desc=True):
     """Roofline of the match walk, k_walkf (16 lanes per topic), with k_desc fused into its
     epilogue (the default for device results, MQ_OPT_FUSE_DESC). Its algorithmic bytes per topic
     are SURVEY.md §8(d)'s walk terms, 8·L + 4 + 16·P (L levels, P child lookups of the
@@ -161,7 +161,7 @@ def walk_roofline(prof, steps, n, n_subs, per_topic, gathers_per_step, edge_load
     Dependent probes of a 4 GB edge table: bound by random-access latency and request rate, far
     below streaming bandwidth."""
     launches, ms = prof.get("walk", (0, 0.0))
-    fused = engine_option(17, 1) != 0 and "desc" not in prof
+    fused = engine_option(17, 1) != 0 and no_desc
     roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
             "traffic": None,
             "kernel": "k_walkf (frontier walk, 16 lanes per topic) + k_desc fused" if fused
@@ -566,7 +566,11 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    eng.profile(True)
+    # the timed steps carry HIP events around the walk's launches only (the roofline's kernel):
+    # with one host synchronisation per batch every event record is on the step's critical path
+    # (16 of them at 16k topics cost ~10 % of a step); the other kernels' times come from a
+    # separate profiled pass below
+    eng.profile(True, walk_only=args.format == "spans")
     eng.profile_reset()
     D.barrier(backend)
     torch.cuda.synchronize()
@@ -578,6 +582,16 @@ def main():
     elapsed = time.perf_counter() - t_start
     prof = eng.profile_read()
     eng.profile(False)
+    prof_all, kb = prof, args.steps
+    if args.format == "spans":  # every kernel's time: an untimed pass of the same batch
+        kb = min(args.steps, 20)
+        eng.profile(True)
+        eng.profile_reset()
+        for _ in range(kb):
+            step()
+        torch.cuda.synchronize()
+        prof_all = eng.profile_read()
+        eng.profile(False)
     elapsed = D.max_over_ranks(elapsed, backend)
     chunks = eng.match_chunks()
     log(f"timed {args.steps} steps in {elapsed:.3f}s; kernels {prof}; chunks/step {chunks}")
@@ -610,7 +624,9 @@ def main():
             "select_shared": bool(args.select_shared),
             "format": args.format,
         },
-        "kernels_ms_per_step": {k: v[1] / max(1, args.steps) for k, v in prof.items() if v[1] > 0},
+        "kernels_ms_per_step": {k: v[1] / max(1, kb) for k, v in prof_all.items() if v[1] > 0},
+        "kernels_pass": ("HIP events around every kernel in an untimed pass of %d steps; the timed steps time "
+                         "the walk only" % kb) if prof_all is not prof else "the timed steps",
         "counters_per_step": {k: v[0] / max(1, args.steps) for k, v in prof.items() if v[1] == 0},
         "chunks_per_step": chunks,
         "walk_trials": {"calibration_batches": calibration, "chosen_walk_group": walk_group, **walk_trials},
@@ -625,7 +641,7 @@ def main():
         torch.cuda.synchronize()
         work = eng.profile_read()
         eng.profile(False)
-        out["roofline"] = spans_roofline(prof, work, args.steps, n, args.subs)
+        out["roofline"] = spans_roofline(prof_all, work, kb, n, args.subs)
         out["merge_work_per_topic"] = {k[6:]: work[k][0] / n for k in work
                                        if k.startswith("merge_") and k not in ("merge_topics", "merge_sets")}
         if "set_cycles_max" in work:  # the longest merge set's wave (shader clocks) and its records
@@ -668,7 +684,8 @@ def main():
             # `roofline` names the step's dominant kernel: the walk or the merge stage, whichever
             # takes longer per step; the other is reported beside it
             wr = walk_roofline(prof, args.steps, n, args.subs, per_topic,
-                               out["counters_per_step"].get("gathers", 0), out["edge_load"], walk_group)
+                               out["counters_per_step"].get("gathers", 0), out["edge_load"], walk_group,
+                               "desc" not in prof_all)
             mr = out["roofline"]
             walk_ms = wr.get("launch_ms") or 0.0
             merge_ms = mr.get("ms_per_step") or 0.0
@@ -740,7 +757,7 @@ def main():
         # without the oracle's L / P counters (--no-cpu, multi-rank) the walk's bytes are not
         # known; the walk is still named when it is the longer kernel (achieved: null)
         wr = walk_roofline(prof, args.steps, n, args.subs, None, out["counters_per_step"].get("gathers", 0),
-                           out["edge_load"], walk_group)
+                           out["edge_load"], walk_group, "desc" not in prof_all)
         walk_ms = prof.get("walk", (0, 0.0))[1] / max(1, args.steps)
         if walk_ms > (out["roofline"].get("ms_per_step") or 0.0):
             wr["launch_ms"] = walk_ms

@@ -532,6 +532,7 @@ int mq_set_option(mq_index* idx, uint32_t option, uint64_t value);
  * atomics: enable them for a measurement pass, not in a timed one. */
 #define MQ_PROF_TIMES 1
 #define MQ_PROF_WORK 2
+#define MQ_PROF_WALK 4 /* times of the match walk's launches only (no events around the other kernels) */
 typedef struct mq_kernel_time {
   char name[32];
   uint64_t launches;

@@ -60,7 +60,7 @@ struct mq_index {
     if (!dev) {
       dev.reset(new Device(cfg.device));
       lk->dev = dev.get();
-      dev->prof.enable(profile != 0, (profile & MQ_PROF_WORK) != 0);
+      dev->prof.enable(profile != 0, (profile & MQ_PROF_WORK) != 0, (profile & MQ_PROF_WALK) != 0);
       dev->set_select_shared((cfg.flags & MQ_CFG_SELECT_SHARED) != 0);
       for (auto& o : options) dev->set_option(o.first, o.second);
       dev_ready.store(true, std::memory_order_release);
@@ -767,7 +767,7 @@ int mq_set_option(mq_index* idx, uint32_t option, uint64_t value) {
 int mq_profile_enable(mq_index* idx, int enable) {
   return guarded(idx, [&] {
     idx->profile = enable;
-    if (idx->dev) idx->dev->prof.enable(enable != 0, (enable & MQ_PROF_WORK) != 0);
+    if (idx->dev) idx->dev->prof.enable(enable != 0, (enable & MQ_PROF_WORK) != 0, (enable & MQ_PROF_WALK) != 0);
     return 0;
   });
 }

@@ -177,8 +177,12 @@ void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
 }
 
 // ---- profiler ----------------------------------------------------------------------------------
-void Profiler::begin(hipStream_t s) {
+void Profiler::begin(hipStream_t s, const char* name) {
   if (!on_) return;
+  if (walk_only_ && strcmp(name, "walk") != 0) {  // MQ_PROF_WALK: the walk's launches only
+    cur_ = nullptr;
+    return;
+  }
   if (free_.empty()) {
     hipEvent_t e;
     hip_check(hipEventCreate(&e), "hipEventCreate");
@@ -699,12 +703,12 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
   for (uint32_t b = 0; b < S; b++) {
     const Sub& q = sub[b];
     TopicOff* off_b = offs_.as<TopicOff>() + q.t0 + b;
-    prof.begin(wstream_);
+    prof.begin(wstream_, "walk");
     launch_walk(false, true, walk_wpe_, d_tb, d_to + q.t0, q.n, di, counts_.as<TopicCount>() + q.t0, nullptr,
                 gslots_.as<uint32_t>() + (size_t)q.t0 * kGatherCap, ovf_.as<uint32_t>() + b, wstream_);
     prof.end("walk", wstream_);
     hip_check(hipGetLastError(), "k_walk<count>");
-    prof.begin(wstream_);
+    prof.begin(wstream_, "scan");
     launch_scan(counts_.as<TopicCount>() + q.t0, q.n, bsum_.as<TopicOff>() + q.blk0 + b,
                 bpre_.as<TopicOff>() + q.blk0 + b, off_b, wstream_);
     prof.end("scan", wstream_);
@@ -758,7 +762,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     uint32_t gstride = kGatherCap;
     if (h_ovf[sb]) {
       grow(gathers_, std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
-      prof.begin(s);
+      prof.begin(s, "walk_fill");
       launch_walk(true, true, walk_wpe_, d_tb, d_to + q.t0, q.n, di, nullptr, off_b, gathers_.as<uint32_t>(), nullptr, s);
       prof.end("walk_fill", s);
       hip_check(hipGetLastError(), "k_walk<fill>");
@@ -846,7 +850,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
     da.msig = nullptr;
     da.mrank = nullptr;
     da.unsafe = nullptr;
-    prof.begin(s);
+    prof.begin(s, "desc");
     launch_desc(da, false, s);
     prof.end("desc", s);
     hip_check(hipGetLastError(), "k_desc");
@@ -882,7 +886,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
       a.rcap = 0;
       a.work = nullptr;
       if (ci >= 2) hip_check(hipStreamWaitEvent(s, merge_done_[b], 0), "hipStreamWaitEvent");
-      prof.begin(s);
+      prof.begin(s, "copy");
       launch_copy(a, copy_blocks_, s);
       prof.end("copy", s);
       hip_check(hipGetLastError(), "k_copy");
@@ -890,7 +894,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         hip_check(hipEventRecord(copy_done_[b], s), "hipEventRecord");
         hip_check(hipStreamWaitEvent(side_, copy_done_[b], 0), "hipStreamWaitEvent");
       }
-      prof.begin(ms);
+      prof.begin(ms, "merge");
       launch_merge(a, false, merge_wpe_opt_ ? merge_wpe_opt_ : 1u, merge_blocks_, ms);
       prof.end("merge", ms);
       hip_check(hipGetLastError(), "k_merge");
@@ -909,7 +913,7 @@ void Device::match(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_
         pa.n_out_stride = sizeof(mq_topic_result_dev) / sizeof(uint32_t);
         pa.n = nt;
         pa.err = err_.as<uint32_t>();
-        prof.begin(ms);
+        prof.begin(ms, "pick");
         launch_pick(pa, ms);
         prof.end("pick", ms);
         hip_check(hipGetLastError(), "k_pick");
@@ -994,7 +998,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
     grow(fb_cnt_, sizeof(uint32_t));
     if (!one_sync) hip_check(hipMemsetAsync(fb_cnt_.p, 0, sizeof(uint32_t), s), "hipMemsetAsync(fb)");
   }  // (one-sync batches: zeroed by spans_begin's k_reset)
-  prof.begin(s);
+  prof.begin(s, "walk");
   if (fused) {  // one-sync batch, k_desc in the walk's epilogue: no scan (the dedup totals the gathers)
     launch_walk_desc(walk_group_, walk_wpe_, d_tb, d_to, n, di, counts_.as<TopicCount>(), gslots_.as<uint32_t>(), ovf_.as<uint32_t>(),
                      fb_list_.as<uint32_t>(), fb_cnt_.as<uint32_t>(), n_cus_ * 2, *fused, s);
@@ -1013,7 +1017,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
                 ovf_.as<uint32_t>(), s, one_sync);
   prof.end("walk", s);
   hip_check(hipGetLastError(), "k_walk<count>");
-  prof.begin(s);
+  prof.begin(s, "scan");
   launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), offs_.as<TopicOff>(), s);
   prof.end("scan", s);
   hip_check(hipGetLastError(), "k_scan");
@@ -1034,7 +1038,7 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
   *gstride = kGatherCap;
   if (*h_ovf) {  // a topic with more gathers than its count-pass slots: write all lists compactly
     grow(gathers_, std::max<uint64_t>(tot.g, 1) * sizeof(uint32_t));
-    prof.begin(s);
+    prof.begin(s, "walk_fill");
     launch_walk(true, lists, walk_wpe_, d_tb, d_to, n, di, nullptr, offs_.as<TopicOff>(), gathers_.as<uint32_t>(), nullptr, s);
     prof.end("walk_fill", s);
     hip_check(hipGetLastError(), "k_walk<fill>");
@@ -1240,7 +1244,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     fda.dd_tslot = dd_slot_.as<uint32_t>();
     if (walk_exp_ & 1u) {  // MQ_OPT_WALK_EXP bit 0: the level-0 probes ahead of the walk
       grow(root_hint_, (size_t)n * sizeof(uint4));
-      prof.begin(s);
+      prof.begin(s, "root_hint");
       launch_root_hint(d_tb, d_to, n, di, root_hint_.as<uint4>(), s);
       prof.end("root_hint", s);
       hip_check(hipGetLastError(), "k_root_hint");
@@ -1271,7 +1275,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   const DescArgs da = fused ? fda : desc_args();
   sb_.tc = da.tc_out;
   if (!fused) {
-    prof.begin(s);
+    prof.begin(s, "desc");
     launch_desc(da, true, s);
     prof.end("desc", s);
     hip_check(hipGetLastError(), "k_desc<spans>");
@@ -1284,7 +1288,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     if (!x_tot_.p) x_tot_.ensure(3 * sizeof(unsigned long long));
     grow(x_ents_, sizeof(XEnt));
     auto pack = [&]() {
-      prof.begin(s);
+      prof.begin(s, "xpack");
       // (walk-fused: the scan also totals the batch's gathers, in .rows)
       if (fused) launch_xcounts(x_cnt_.as<uint32_t>(), sp_tc_.as<TopicCount>(), n, counts_.as<TopicCount>(), s);
       else launch_counts(x_cnt_.as<uint32_t>(), n, counts_.as<TopicCount>(), s);
@@ -1338,7 +1342,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
     grow(x_cnt_, (size_t)n * sizeof(uint32_t));
-    prof.begin(s);
+    prof.begin(s, "xlist");
     launch_xlist(true, di, n, offs_.as<TopicOff>(), gathers, gstride, counts_.as<TopicCount>(), nullptr, nullptr,
                  nullptr, s);
     launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
@@ -1469,13 +1473,13 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       xa.g_stride = sb_.fused ? kGatherCap : 0u;
       xa.tc = sb_.tc;
       xa.desc = desc_[0].as<GDesc>();
-      prof.begin(s);
+      prof.begin(s, "xsig");
       launch_xsig(xa, s);
       prof.end("xsig", s);
       hip_check(hipGetLastError(), "k_xsig");
       dd.fcount = xa.fcount;
     }
-    prof.begin(s);
+    prof.begin(s, "dedup");
     launch_dedup(dd, s, !sb_.walk_inserted);
     prof.end("dedup", s);
     hip_check(hipGetLastError(), "k_dedup");
@@ -1565,7 +1569,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       a.srcap = srcap_;
       if (!one_sync) hip_check(hipMemsetAsync(a.spcount, 0, kPatchRegions * sizeof(unsigned long long), s), "memset");
       if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
-      prof.begin(s);
+      prof.begin(s, "merge_sets");
       // persistent: the waves stride over the representative list (its length is on the device)
       // MQ_OPT_SET_GRID 1: a wavefront per set (the dispatcher balances heavy sets); else
       // persistent waves striding over the list
@@ -1623,7 +1627,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       fa.wave_list = dd_wlist_.as<uint32_t>();
       fa.n_wave = dd_nwave_.as<unsigned long long>();
       fa.g_stride = a.g_stride;
-      prof.begin(s);
+      prof.begin(s, "finish");
       launch_finish(fa, s);
       prof.end("finish", s);
       hip_check(hipGetLastError(), "k_finish");
@@ -1661,7 +1665,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     if (!one_sync)
       hip_check(hipMemsetAsync(a.pcount, 0, kPatchRegions * sizeof(unsigned long long), s), "hipMemsetAsync(pcount)");
     if (a.work) hip_check(hipMemsetAsync(a.work, 0, kPatchRegions * kWork * sizeof(unsigned long long), s), "memset");
-    prof.begin(s);
+    prof.begin(s, "merge");
     // after k_finish the waves stride over its list (its length is on the device)
     launch_merge(a, true, merge_wpe, a.wave_list && !merge_blocks_ ? n_cus_ * 8 : merge_blocks_, s);
     prof.end("merge", s);
@@ -1695,7 +1699,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     pa.n_out_stride = sizeof(TopicSpansDev) / sizeof(uint32_t);
     pa.n = n;
     pa.err = err_.as<uint32_t>();
-    prof.begin(s);
+    prof.begin(s, "pick");
     launch_pick(pa, s);
     prof.end("pick", s);
     hip_check(hipGetLastError(), "k_pick<spans>");
@@ -1944,7 +1948,7 @@ void Device::acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8
   a.matched = d + o_m;
   a.n_elems = reinterpret_cast<uint32_t*>(d + o_ne);
   a.elems = reinterpret_cast<uint32_t*>(d + o_el);
-  prof.begin(s);
+  prof.begin(s, "acl");
   launch_acl(a, s);
   prof.end("acl", s);
   hip_check(hipGetLastError(), "k_acl");
@@ -1969,7 +1973,7 @@ void Device::ensure_img(const Index& ix, const DevIndex& di, hipStream_t s) {
   const size_t nb = ((size_t)slots + kScanBlock) / kScanBlock + 1;
   img_bsum_.ensure(nb * sizeof(uint32_t));
   img_bpre_.ensure(nb * sizeof(uint32_t));
-  prof.begin(s);
+  prof.begin(s, "msg_image");
   hip_check(hipMemsetAsync(img_pos_.p, 0xFF, (size_t)slots * sizeof(uint32_t), s), "hipMemsetAsync(img pos)");
   launch_img_root(img_node_.as<uint32_t>(), img_pos_.as<uint32_t>(), img_lp_.as<uint32_t>(), s);
   ImgLevelArgs a;
@@ -2091,12 +2095,12 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
     hip_check(hipMemsetAsync(wide.n_items, 0, sizeof(uint32_t), s), "hipMemsetAsync(n_items)");
   }
   const uint32_t wide_blocks = n_cus_ * 8;
-  prof.begin(s);
+  prof.begin(s, "msgq_count");
   launch_msgq(runs ? kMsgRuns : kMsgCount, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), nullptr, nullptr,
               nullptr, nullptr, nullptr, d_runs, run_cap, d_nruns, wide, wide_blocks, s);
   prof.end("msgq_count", s);
   if (exp) {  // the exported items' counts
-    prof.begin(s);
+    prof.begin(s, "msgq_wide_count");
     launch_msgq(kMsgWideCount, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr,
                 nullptr, d_runs, run_cap, d_nruns, wide, wide_blocks, s);
     prof.end("msgq_wide_count", s);
@@ -2107,20 +2111,20 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
   // the fill and copy passes, given the output buffers as they are; true when they held the batch
   auto fill_copy = [&](const uint32_t* gate, const uint64_t* n_pieces) {
     img.gate = gate;
-    prof.begin(s);
+    prof.begin(s, "msgq_fill");
     launch_msgq(runs ? kMsgPlace : kMsgFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
                 msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
                 msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
     prof.end("msgq_fill", s);
     if (exp) {
-      prof.begin(s);
+      prof.begin(s, "msgq_wide_fill");
       launch_msgq(kMsgWideFill, d_fb, d_fo, n, di, img, counts_.as<TopicCount>(), offs_.as<TopicOff>(),
                   msg_pieces_.as<MsgPiece>(), msg_handles_.as<uint64_t>(), msg_base_.as<uint64_t>(),
                   msg_count_.as<uint32_t>(), d_runs, run_cap, d_nruns, wide, wide_blocks, s);
       prof.end("msgq_wide_fill", s);
     }
     hip_check(hipGetLastError(), "k_msgq<fill>");
-    prof.begin(s);
+    prof.begin(s, "msg_copy");
     if (n_pieces)
       launch_msg_copy_dev(msg_pieces_.as<MsgPiece>(), n_pieces, msg_pieces_.bytes / sizeof(MsgPiece), img.h,
                           msg_handles_.as<uint64_t>(), s);
@@ -2216,7 +2220,7 @@ void Device::messages_walk(Index& ix, const DevIndex& di, const uint8_t* d_fb, c
     msg_spec_.ensure((size_t)n * cap * sizeof(uint64_t));
     spec = msg_spec_.as<uint64_t>();
   }
-  prof.begin(s);
+  prof.begin(s, "msg_count");
   launch_msg(false, d_fb, d_fo, n, di, counts_.as<TopicCount>(), nullptr, nullptr, nullptr, nullptr, spec, cap,
              msg_wpe, s);
   prof.end("msg_count", s);
@@ -2230,13 +2234,13 @@ void Device::messages_walk(Index& ix, const DevIndex& di, const uint8_t* d_fb, c
   msg_base_.ensure((size_t)n * sizeof(uint64_t));
   msg_count_.ensure((size_t)n * sizeof(uint32_t));
   if (cap) {
-    prof.begin(s);
+    prof.begin(s, "msg_place");
     launch_msg_place(n, counts_.as<TopicCount>(), offs_.as<TopicOff>(), spec, cap, msg_handles_.as<uint64_t>(),
                      msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), s);
     prof.end("msg_place", s);
     hip_check(hipGetLastError(), "k_msg_place");
   }
-  prof.begin(s);
+  prof.begin(s, "msg_fill");
   launch_msg(true, d_fb, d_fo, n, di, counts_.as<TopicCount>(), offs_.as<TopicOff>(), msg_handles_.as<uint64_t>(),
              msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), spec, cap, msg_wpe, s);
   prof.end("msg_fill", s);

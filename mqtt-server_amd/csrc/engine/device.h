@@ -141,13 +141,14 @@ class Profiler {
     for (hipEvent_t e : free_) (void)hipEventDestroy(e);
     if (cur_) (void)hipEventDestroy(cur_);
   }
-  void enable(bool on, bool work = false) {
+  void enable(bool on, bool work = false, bool walk_only = false) {
     on_ = on;
     work_ = on && work;
+    walk_only_ = on && walk_only;
   }
   bool on() const { return on_; }
   bool work() const { return work_; }  // MQ_PROF_WORK: kernel work counters
-  void begin(hipStream_t s);
+  void begin(hipStream_t s, const char* name);  // (name: the launch's, as end() gives it)
   void end(const char* name, hipStream_t s);
   int read(mq_kernel_time* out, uint32_t cap);
   // Event counters reported next to the kernels (launches = count, total_ms = 0).
@@ -165,7 +166,7 @@ class Profiler {
     double ms = 0;
   };
   void drain();
-  bool on_ = false, work_ = false;
+  bool on_ = false, work_ = false, walk_only_ = false;
   hipEvent_t cur_ = nullptr;
   std::vector<Pending> pending_;
   std::vector<hipEvent_t> free_;

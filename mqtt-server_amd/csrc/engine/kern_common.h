@@ -183,7 +183,12 @@ __device__ __forceinline__ EdgeHit lookup_edge(const DevIndex& ix, uint32_t pare
                                                const uint8_t* seg, uint32_t len) {
   uint64_t i = edge_slot(parent, k, ix.edge_mask);
   for (uint64_t probes = 0; probes <= ix.edge_mask; probes++) {
-    const EdgeSlot e = ix.edges[i];
+    // both halves of the slot in one round trip: left to itself the compiler loads the key half
+    // only once the parent half has shown a full slot — a second, dependent load on every hit
+    const uint4* sp = reinterpret_cast<const uint4*>(ix.edges + i);
+    const uint4 q0 = sp[0], q1 = sp[1];
+    __asm__ volatile("" ::"v"(q0.x), "v"(q1.x));
+    const EdgeSlot e{q0.x | (uint64_t)q0.y << 32, q0.z | (uint64_t)q0.w << 32, q1.x, q1.y, q1.z, q1.w};
     if (e.parent == kEdgeEmpty) break;
     if (e.parent == parent && e.k0 == k.k0 && e.k1 == k.k1) {
       if (!seg_is_long(k)) return EdgeHit{e.child, e.plus, e.hash};

@@ -29,6 +29,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t off[kHitMax];       //   the list's offset in the pair-list pool,
     uint32_t hb[kHitMax];        //   h's merge gather,
     uint32_t pre[kHitMax + 1];   //   exclusive prefix of the lists' lengths (+ total)
+    uint8_t mark[64];            // locate_run: the list starts inside a window of 64 visits
   };
   __shared__ WaveLds lds[4];
   const uint32_t wv = wave_id(), lane = threadIdx.x & 63;
@@ -150,16 +151,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         tot += ct;
       }
     };
-    // visit r of the staged lists [j0, j1): its list jj (binary search of the prefix), its slot
-    auto locate = [&](uint32_t r, uint32_t j0, uint32_t j1, uint32_t& jj) __attribute__((always_inline)) -> PairSlot {
-      const uint32_t rc = min(r, h_pre[j1] - 1);
-      uint32_t lo = j0, hi = j1;  // h_pre[lo] <= rc < h_pre[hi] (lists are non-empty)
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (h_pre[mid] <= rc) lo = mid; else hi = mid;
-      }
-      jj = lo;
-      return ix.plist[h_off[lo] + (rc - h_pre[lo])];
+    // the visits [R, R + 64) of the staged lists [., j1), jb the list holding visit R, a lane
+    // each: lane l reads list jb + 1 + l's start, the starts inside the window are marked in LDS,
+    // and visit R + v's list is jb + the marks at or below v (lists are non-empty: one start per
+    // place) — locate's result for 64 consecutive visits in two dependent LDS round trips where
+    // the binary search takes log2(j1 - j0). jb_next: the list holding visit R + 64.
+    auto locate_run = [&](uint32_t R, uint32_t jb, uint32_t j1, uint32_t& jj, uint32_t& jb_next)
+        __attribute__((always_inline)) -> PairSlot {
+      const uint32_t jl = jb + 1 + lane;
+      const uint32_t pos = (jl < j1 ? h_pre[jl] : 0xFFFFFFFFu) - R;  // >= 1: list jb holds R
+      W.mark[lane] = 0;
+      if (pos < 64) W.mark[pos] = 1;
+      wave_sync_lds();
+      const uint64_t M = __ballot(W.mark[lane] != 0);
+      jb_next = jb + (uint32_t)__popcll(__ballot(pos <= 64));
+      jj = jb + (uint32_t)__popcll(M & (~0ull >> (63 - lane)));
+      const uint32_t rc = min(R + lane, h_pre[j1] - 1);
+      return ix.plist[h_off[jj] + (rc - h_pre[jj])];
     };
     // --- the partner-link path (a merge gather beyond the folds, or hit lists beyond the stage) --
     bool map_ok = false;
@@ -236,13 +244,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     auto resolve_lists = [&](uint32_t j0, uint32_t j1, uint32_t pp, uint32_t PP) __attribute__((always_inline)) {
       if (!map_ok) map_rebuild();
       const uint32_t v0 = h_pre[j0], v1 = h_pre[j1];
-      uint32_t jj_next = j0;
-      PairSlot e_next = locate(v0 + lane, j0, j1, jj_next);
+      uint32_t jj_next, jb = j0;
+      PairSlot e_next = locate_run(v0, jb, j1, jj_next, jb);
       for (uint32_t r0 = v0; r0 < v1; r0 += 64) {
         const uint32_t r = r0 + lane;
         const uint32_t jj = jj_next;
         const PairSlot e = e_next;
-        if (r0 + 64 < v1) e_next = locate(r0 + 64 + lane, j0, j1, jj_next);  // wave-uniform
+        if (r0 + 64 < v1) e_next = locate_run(r0 + 64, jb, j1, jj_next, jb);  // wave-uniform
         const uint32_t xa = h_ga[jj];
         w_rec += r < v1;
         resolve(r < v1 && (PP == 1 || hash32(e.k) % PP == pp), e.meta, xa << kSetRowBits | e.k, xa,
@@ -263,14 +271,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         f_val[q] = 0;
       }
       map_ok = false;
-      uint32_t jj_next = j0;
-      PairSlot e_next = locate(v0 + lane, j0, j1, jj_next);
+      uint32_t jj_next, jb = j0;
+      PairSlot e_next = locate_run(v0, jb, j1, jj_next, jb);
       wave_sync_lds();
       for (uint32_t r0 = v0; r0 < v1; r0 += 64) {
         const uint32_t r = r0 + lane;
         const uint32_t jj = jj_next;
         const PairSlot e = e_next;
-        if (r0 + 64 < v1) e_next = locate(r0 + 64 + lane, j0, j1, jj_next);  // wave-uniform
+        if (r0 + 64 < v1) e_next = locate_run(r0 + 64, jb, j1, jj_next, jb);  // wave-uniform
         if (r < v1) {
           const uint32_t xa = h_ga[jj], hb = h_hb[jj];
           const uint32_t key = xa << kSetRowBits | e.k;
@@ -317,14 +325,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       // the table sized to the visits (at most 2/3 full: short probe runs, and a short emission scan)
       const uint32_t ns = min(kBigSlots, ((v1 - v0) * 3 / 2 + 63) & ~63u);
       for (uint32_t q = lane; q < ns; q += 64) ws[q] = 0u;
-      uint32_t jj_next = j0;
-      PairSlot e_next = locate(v0 + lane, j0, j1, jj_next);
+      uint32_t jj_next, jb = j0;
+      PairSlot e_next = locate_run(v0, jb, j1, jj_next, jb);
       wave_sync_lds();
       for (uint32_t r0 = v0; r0 < v1; r0 += 64) {
         const uint32_t r = r0 + lane;
         const uint32_t jj = jj_next;
         const PairSlot e = e_next;
-        if (r0 + 64 < v1) e_next = locate(r0 + 64 + lane, j0, j1, jj_next);  // wave-uniform
+        if (r0 + 64 < v1) e_next = locate_run(r0 + 64, jb, j1, jj_next, jb);  // wave-uniform
         if (r < v1) {
           const uint32_t pm = e.meta >> kSlotPartShift;
           const uint32_t bits = (h_hb[jj] < xa ? kBitNonBase : 0u) | ((pm & 4u) ? kBitNoLocal : 0u) |

@@ -75,7 +75,7 @@ class SpanResult(C.Structure):
 
 SPANS_PICKED = 1  # MQ_SPANS_PICKED
 MQ_EINVAL, MQ_ENOMEM, MQ_ENODEV, MQ_EIO = -22, -12, -19, -5  # include/mqmatch.h return codes
-PROF_TIMES, PROF_WORK = 1, 2  # mq_profile_enable
+PROF_TIMES, PROF_WORK, PROF_WALK = 1, 2, 4  # mq_profile_enable
 
 # mq_set_option: product options (include/mqmatch.h) and development ones (include/mqmatch_dev.h)
 OPT_CHUNK_ROWS, OPT_PATCH_CAP, OPT_EDGE_LOAD = 1, 6, 13
@@ -677,9 +677,10 @@ class Engine:
             out.append((els, bool(matched[i])))
         return out
 
-    def profile(self, enable=True, work=False):
-        """mq_profile_enable: kernel times (HIP events); work=True adds k_merge's work counters."""
-        mode = (PROF_TIMES | (PROF_WORK if work else 0)) if enable else 0
+    def profile(self, enable=True, work=False, walk_only=False):
+        """mq_profile_enable: kernel times (HIP events); work=True adds k_merge's work counters;
+        walk_only=True times the walk's launches alone (no events between the other kernels)."""
+        mode = (PROF_TIMES | (PROF_WORK if work else 0) | (PROF_WALK if walk_only else 0)) if enable else 0
         _check(lib().mq_profile_enable(self.h, mode), "mq_profile_enable")
 
     def profile_read(self):
