@@ -646,6 +646,8 @@ def main():
                                        if k.startswith("merge_") and k not in ("merge_topics", "merge_sets")}
         if "set_cycles_max" in work:  # the longest merge set's wave (shader clocks) and its records
             out["set_longest"] = {"cycles": work["set_cycles_max"][0], "records": work["set_records_max_wave"][0],
+                                  **{k[4:]: work[k][0] for k in ("set_pairs_cycles_max", "set_resolve_cycles_max",
+                                                                 "set_gathers_max", "set_hit_lists_max") if k in work},
                                   "cycles_mean": work.get("set_cycles_total", (0, 0))[0]
                                   / max(1, work.get("dedup_sets", (1, 0))[0])}
     else:

@@ -1808,6 +1808,10 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
     }
     prof.count("set_cycles_max", sum[24]);
     prof.count("set_records_max_wave", sum[25]);
+    prof.count("set_pairs_cycles_max", sum[26]);
+    prof.count("set_resolve_cycles_max", sum[27]);
+    prof.count("set_gathers_max", sum[28]);
+    prof.count("set_hit_lists_max", sum[29]);
     prof.count("merge_topics", n);
   }
   // A pipelined copy is armed (pc_) only when the batch has passed its error check: a batch that

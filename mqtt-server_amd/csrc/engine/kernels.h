@@ -49,7 +49,8 @@ constexpr uint32_t kBitNonBase = 1u, kBitNoLocal = 2u, kBitQos1 = 4u, kBitQos2 =
 constexpr uint32_t kPatchRegions = 1024;  // span format: patch pool regions (one counter each)
 // k_merge work counters (MQ_PROF_WORK), kWork per region: pair-table entries loaded, records
 // resolved (pair slots read), partner links loaded, patches written
-constexpr uint32_t kWork = 26;  // [24], [25]: the longest set's cycles and records (max); [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
+constexpr uint32_t kWork = 30;  // [24] .. [29] (k_set, maxima over the sets): cycles, records, pair-analysis
+                                // cycles, resolution cycles, merge gathers, hit lists; [4..7]: set pass phase cycles (map, pair analysis, resolution, whole set);
                                 // [8] topics the kernel resolved, [9] bytes of their maps' sources read;
                                 // set pass fold: [10] visits folded, [11] visits of merge gathers too big
                                 // to fold, [12] those gathers, [13] their may-merge records (n_merge),

@@ -430,6 +430,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     };
     pairs(true, [] {});
     const uint64_t c_pairs = stamp ? clock64() : 0ull;
+    const uint32_t n_hit_max = staged_all ? n_hit : kHitMax + 1;
     if (lane == 0 && tot_all) resv = atomicAdd(a.spcount + (t & (kPatchRegions - 1)), (unsigned long long)tot_all);
     resv_n = tot_all;
     resv_pending = true;
@@ -464,6 +465,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         atomicAdd(wc + 7, (unsigned long long)(c_end - c_start));
         atomicMax(wc + 24, (unsigned long long)(c_end - c_start));
         atomicMax(wc + 25, (unsigned long long)rr);
+        atomicMax(wc + 26, (unsigned long long)(c_pairs - c_map));
+        atomicMax(wc + 27, (unsigned long long)(c_end - c_pairs));
+        atomicMax(wc + 28, (unsigned long long)lc);
+        atomicMax(wc + 29, (unsigned long long)n_hit_max);
       }
     }
   }
