@@ -447,6 +447,8 @@ void Device::sync(Index& ix, hipStream_t s) {
     const size_t need = table + st.bytes + 16 * st.runs.size();
     if (stage_done_) hip_check(hipEventSynchronize(stage_done_), "hipEventSynchronize(stage)");
     else hip_check(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming), "hipEventCreate");
+    // (the event is recorded only once a scatter has used it; before that, synchronising on it
+    // returns at once)
     if (h_stage_bytes_ < need) {
       pinned_free(h_stage_, h_stage_bytes_);
       h_stage_ = pinned_alloc(need);
@@ -467,6 +469,15 @@ void Device::sync(Index& ix, hipStream_t s) {
     launch_scatter(d_stage_.as<ScatterRun>(), (uint32_t)st.runs.size(), d_stage_.as<uint8_t>(), s);
     hip_check(hipGetLastError(), "k_scatter");
     hip_check(hipEventRecord(stage_done_, s), "hipEventRecord(stage)");
+  }
+  if (!h_stage_) {  // the first sync (a whole upload): the staging buffers for the updates' dirty
+    // pages, sized for ordinary update bursts, so that the first update after it does not
+    // page-lock host memory under the handle lock (a few ms)
+    constexpr size_t kStageInit = 4u << 20;
+    h_stage_ = pinned_alloc(kStageInit);
+    h_stage_bytes_ = kStageInit;
+    d_stage_.ensure(kStageInit);
+    if (!stage_done_) hip_check(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming), "hipEventCreate");
   }
   retained_len_ = ix.retained_len();
   empty_live_ = ix.empty_topic_live;

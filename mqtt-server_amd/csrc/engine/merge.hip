@@ -464,7 +464,7 @@ __device__ __forceinline__ uint64_t gdesc_rank(const GDesc& d) {
 // that their first 32 levels agree: both are deeper (their DeepTail codes decide, compared as the
 // rank keys are, a proper prefix first), or one is exactly 32 levels deep — a proper prefix of
 // the other, so first. A tie no entry explains trips kErrDeepRank.
-__device__ __noinline__ bool deep_before(const DevIndex& ix, uint32_t fh, uint32_t fg) {
+__device__ __forceinline__ bool deep_before(const DevIndex& ix, uint32_t fh, uint32_t fg) {
   auto find = [&](uint32_t f) -> const DeepTail* {
     if (!ix.deep) return nullptr;
     uint64_t sl = mix64(f) & ix.deep_mask;
@@ -490,8 +490,17 @@ __device__ __noinline__ bool deep_before(const DevIndex& ix, uint32_t fh, uint32
   return false;  // one path (a filter lives on one shard): not reached
 }
 
-template <bool SPANS, bool XS, int WPE, bool SET = false, uint32_t PB = kPartBatch>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs a) {
+// DEEP (a sharded index holding filters deeper than 32 levels, DevIndex.deep): rank-key ties are
+// ordered by deep_before; without DEEP no tie can occur (the keys hold every level), and the
+// tie-break's code and live values stay out of the kernel (the sharded set pass spills heavily
+// already: 0.44 -> 1.7 ms per shard with the tie-break compiled in, profiles/r05/shard2/)
+template <bool SPANS, bool XS, int WPE, bool SET = false, uint32_t PB = kPartBatch, bool DEEP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_merge(EmitArgs args) {
+  // the arguments, read from the kernarg segment where they are used (as in k_set: a by-value
+  // parameter is loaded whole at the entry and its pointers spill to vector lanes)
+  (void)args;
+  const EmitArgs& a = *(const EmitArgs*)(const __attribute__((address_space(4))) char*)
+                          __builtin_amdgcn_kernarg_segment_ptr();
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
   // per-wave words, one contiguous block (the set pass's record-keyed fold spans the map and the
   // merge gathers' three arrays): the map (gathered node with may-merge records, or kForeign | fid
@@ -759,9 +768,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (rh != rg) return rh < rg;
       if (gh != kNone) return gh < gg;  // both on this shard: gather order is DFS order
       // another shard's node tied with the record's beyond the key's 32 levels
-      const uint32_t h = hn(), g = gn();
-      return deep_before(a.ix, (h & kForeign) ? h & ~kForeign : a.ix.xinfo[h].fid,
-                         (g & kForeign) ? g & ~kForeign : a.ix.xinfo[g].fid);
+      if constexpr (DEEP) {
+        const uint32_t h = hn(), g = gn();
+        return deep_before(a.ix, (h & kForeign) ? h & ~kForeign : a.ix.xinfo[h].fid,
+                           (g & kForeign) ? g & ~kForeign : a.ix.xinfo[g].fid);
+      } else {
+        (void)hn;
+        (void)gn;
+        atomicOr(a.ix.err, kErrDeepRank);  // (no deep filters: not reached)
+        return false;
+      }
     };
 
     // Resolve one record whose client may have other matches for this topic: its partners that
@@ -1380,10 +1396,13 @@ void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_bloc
 #else
   (void)wpe;
 #endif
-  if (spans && a.ix.xinfo && a.rep && a.dd_phase == 1)  // sharded index, merge-set dedup: the set pass
-    hipLaunchKernelGGL((k_merge<true, true, 6, true>), g, b, 0, s, a);
-  else if (spans && a.ix.xinfo)  // sharded index
-    hipLaunchKernelGGL((k_merge<true, true, 6>), g, b, 0, s, a);
+  if (spans && a.ix.xinfo && a.rep && a.dd_phase == 1) {  // sharded index, merge-set dedup: the set pass
+    if (a.ix.deep) hipLaunchKernelGGL((k_merge<true, true, 6, true, kPartBatch, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, true, 6, true>), g, b, 0, s, a);
+  } else if (spans && a.ix.xinfo) {  // sharded index
+    if (a.ix.deep) hipLaunchKernelGGL((k_merge<true, true, 6, false, kPartBatch, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_merge<true, true, 6>), g, b, 0, s, a);
+  }
   else if (spans && a.rep && a.dd_phase == 1)  // merge-set dedup: the set pass
     hipLaunchKernelGGL((k_merge<true, false, 8, true>), g, b, 0, s, a);
   else if (spans)

@@ -213,12 +213,30 @@ struct FrontEnt {  // one frontier particle: its '+' / '#' children and its path
 // DESC (G = 16, LISTS = false): k_desc fused into the epilogue — the gathers, placed in the
 // reference's order in LDS, go straight to the topic's spans and merge lists (desc_g16 with the
 // stride layout, da.g_stride); neither the gather slots nor the counts are written.
+// k_walkf's parameters as they lie in the kernarg segment (natural alignment, in order)
+struct WalkfParams {
+  const uint8_t* tb;
+  const uint64_t* to;
+  uint32_t n;
+  DevIndex ix;
+  TopicCount* cnt;
+  uint32_t* gathers;
+  uint32_t* fb_list;
+  uint32_t* fb_count;
+  DescArgs da;
+};
+
 template <uint32_t G, bool LISTS, int WPE, bool DESC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walkf(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
                                                uint32_t n, DevIndex ix, TopicCount* __restrict__ cnt,
                                                uint32_t* __restrict__ gathers, uint32_t* __restrict__ fb_list,
                                                uint32_t* __restrict__ fb_count, DescArgs da) {
   static_assert(!DESC || ((G == 16 || G == 8) && !LISTS), "the fused desc runs on 8- or 16-lane groups of a gathers-only walk");
+  // the fused desc's arguments, read from the kernarg segment where the epilogue uses them: a
+  // by-value parameter is loaded at the kernel's entry and held across the walk (~60 scalar
+  // registers spilled to vector lanes, read back in the epilogue)
+  const DescArgs& dk = *(const DescArgs*)((const __attribute__((address_space(4))) char*)
+                                              __builtin_amdgcn_kernarg_segment_ptr() + offsetof(WalkfParams, da));
   constexpr uint32_t kTopics = 256 / G;  // topics per workgroup
   // levels and gathers a group holds: 8-lane groups keep 32 topics per workgroup within 20 KB of
   // LDS (8 workgroups per CU: twice the topics in flight of 16-lane groups); a topic beyond them
@@ -312,8 +330,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     EdgeHit h{kNone, kNone, kNone};
     // a literal "+" segment: the reference visits the '+' child twice alike (topics.go:603)
     if (mine && !plusseg) {
-      if (DESC && da.root_hint && d == 0) {  // (MQ_OPT_WALK_EXP bit 0: level 0 looked up before the walk)
-        const uint4 rh = da.root_hint[t];
+      if (DESC && kDevBuild && dk.root_hint && d == 0) {  // (MQ_OPT_WALK_EXP bit 0: level 0 looked up before the walk)
+        const uint4 rh = dk.root_hint[t];
         h = EdgeHit{rh.x, rh.y, rh.z};
       } else {
         h = lookup_edge(ix, fe.node, key, tbase + s, len);
@@ -327,8 +345,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool gC = gL && h.hash != kNone;
     const bool gP = mine && !has_next && fe.plus != kNone;
     const uint32_t gc = (uint32_t)gH + (uint32_t)gL + (uint32_t)gC + (uint32_t)gP;
-    const uint32_t gi = grp_incl<G>(gc, sub);
-    const uint32_t gtot = grp_last<G>(gi);
+    // next level's frontier: the literal and '+' children, compacted over the group
+    const bool fL = mine && has_next && h.child != kNone;
+    const bool fP = mine && has_next && fe.plus != kNone;
+    const uint32_t fc = (uint32_t)fL + (uint32_t)fP;
+    // one group scan for both counts (at most 4 and 2 a lane: 16 bits each)
+    const uint32_t gfi = grp_incl<G>(gc | fc << 16, sub);
+    const uint32_t gft = grp_last<G>(gfi);
+    const uint32_t gi = gfi & 0xFFFFu, gtot = gft & 0xFFFFu, fi = gfi >> 16, ftot = gft >> 16;
     if (act && ng + gtot > kStage) fb = true;
     if (act && !fb) {
       uint32_t p = ng + gi - gc;
@@ -338,12 +362,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (gP) gat[q][p++] = make_uint2(fe.plus | kGatherInline, fe.code | 2u << sh);
     }
     ng += gtot;
-    // next level's frontier: the literal and '+' children, compacted over the group
-    const bool fL = mine && has_next && h.child != kNone;
-    const bool fP = mine && has_next && fe.plus != kNone;
-    const uint32_t fc = (uint32_t)fL + (uint32_t)fP;
-    const uint32_t fi = grp_incl<G>(fc, sub);
-    const uint32_t ftot = grp_last<G>(fi);
     if (act && has_next && ftot > G) fb = true;
     if (act && !fb && has_next) {
       uint32_t p = fi - fc;
@@ -387,7 +405,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (uint32_t k = 0; k < kPer; k++)
       if (pw[k] != kNone) gat[q][pw[k]].x = ww[k];
     wave_sync_lds();
-    desc_grp<G>(da, t, ng, (uint64_t)t * da.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gat[q][i].x; });
+    desc_grp<G>(dk, t, ng, (uint64_t)t * dk.g_stride, 0ull, 0u, sub, [&](uint32_t i) { return gat[q][i].x; });
     return;
   }
   uint32_t rows = 0, shared = 0, inl = 0, merge = 0;
