@@ -163,6 +163,17 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+// A kernel parameter read from the kernarg segment where it is used. A by-value parameter (the
+// 200-byte DevIndex, an argument struct) is loaded whole at the kernel's entry and its pointers
+// held across the kernel, spilling scalar registers to vector lanes (v_readlane, a VALU
+// instruction, in the hot loops); read through this reference, each field is loaded (s_load)
+// where it is used. P: the kernel's parameters as a struct (same order: kernarg layout is the
+// struct's, natural alignment), OFF: offsetof(P, the parameter).
+template <class T>
+__device__ __forceinline__ const T& kernarg_at(size_t off) {
+  return *(const T*)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() + off);
+}
+
 // Index of the calling wavefront in its workgroup, as a wave-uniform (scalar) value: the
 // compiler cannot prove threadIdx.x >> 6 uniform, and per-wave work indexed by it would
 // otherwise run as vector code under exec masks.

@@ -499,8 +499,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // the arguments, read from the kernarg segment where they are used (as in k_set: a by-value
   // parameter is loaded whole at the entry and its pointers spill to vector lanes)
   (void)args;
-  const EmitArgs& a = *(const EmitArgs*)(const __attribute__((address_space(4))) char*)
-                          __builtin_amdgcn_kernarg_segment_ptr();
+  const EmitArgs& a = kernarg_at<EmitArgs>(0);
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // map entries
   // per-wave words, one contiguous block (the set pass's record-keyed fold spans the map and the
   // merge gathers' three arrays): the map (gathered node with may-merge records, or kForeign | fid

@@ -566,14 +566,39 @@ struct MsgFrame {  // a fan-out in progress: particles [cur, end) still to take 
 // kMsgRuns counts and records the runs (their output and piece offsets fixed by the same LDS
 // cursors the fill pass uses); kMsgPlace places recorded runs without walking again — the
 // filter's walk then runs once per batch instead of twice.
+// k_msgq's parameters as they lie in the kernarg segment
+struct MsgqParams {
+  const uint8_t* fb;
+  const uint64_t* fo;
+  uint32_t n;
+  DevIndex ix;
+  MsgImg img;
+  TopicCount* cnt;
+  const TopicOff* off;
+  MsgPiece* pieces;
+  uint64_t* handles;
+  uint64_t* base_out;
+  uint32_t* count_out;
+  MsgRun* runs;
+  uint32_t run_cap;
+  uint32_t* n_runs;
+  MsgWide w;
+};
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, const uint64_t* __restrict__ fo,
-                                              uint32_t n, DevIndex ix, MsgImg img,
+                                              uint32_t n, DevIndex ix_, MsgImg img_,
                                               TopicCount* __restrict__ cnt, const TopicOff* __restrict__ off,
                                               MsgPiece* __restrict__ pieces, uint64_t* __restrict__ handles,
                                               uint64_t* __restrict__ base_out, uint32_t* __restrict__ count_out,
                                               MsgRun* __restrict__ runs, uint32_t run_cap,
-                                              uint32_t* __restrict__ n_runs, MsgWide w) {
+                                              uint32_t* __restrict__ n_runs, MsgWide w_) {
+  (void)ix_;
+  (void)img_;
+  (void)w_;
+  const DevIndex& ix = kernarg_at<DevIndex>(offsetof(MsgqParams, ix));
+  const MsgImg& img = kernarg_at<MsgImg>(offsetof(MsgqParams, img));
+  const MsgWide& w = kernarg_at<MsgWide>(offsetof(MsgqParams, w));
   constexpr bool WIDE = MODE == kMsgWideCount || MODE == kMsgWideFill;  // exported work items
   constexpr bool FILL = MODE == kMsgFill || MODE == kMsgPlace || MODE == kMsgWideFill;  // the walk writes output
   constexpr bool RUNS = MODE == kMsgRuns;

@@ -21,8 +21,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // loaded whole at the kernel's entry, and its ~40 pointers and counts held across the kernel
   // spill to vector lanes (read back with v_readlane, a VALU instruction, in the hot loops)
   (void)args;
-  const EmitArgs& a = *(const EmitArgs*)(const __attribute__((address_space(4))) char*)
-                          __builtin_amdgcn_kernarg_segment_ptr();
+  const EmitArgs& a = kernarg_at<EmitArgs>(0);
   // per-wave LDS, one contiguous block: the node -> merge-gather map (links path only; the folds
   // use its words as their table, the record-keyed fold all kWsWords), then the merge gathers'
   // pair-block headers
@@ -50,18 +49,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t* const h_off = W.off;
   uint32_t* const h_hb = W.hb;
   uint32_t* const h_pre = W.pre;
-  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 32768u));
+  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u));
   const DevIndex& ix = a.ix;
   const uint32_t n_front = (uint32_t)a.n_reps[0];
   const uint32_t i_end = n_front + (uint32_t)a.n_reps[1];
   for (uint32_t i = blockIdx.x * 4 + wv; i < i_end; i += gridDim.x * 4) {
     // heavy sets from the front of the list, the others from its back (k_dedup_rep)
     const uint32_t t = i < n_front ? a.rep_list[i] : a.rep_list[a.t1 - 1 - (i - n_front)];
-    // (MQ_OPT_SET_EXP bit 15) a heavy set's wave issues ahead of the light sets' waves on its SIMD
-    if (exp_bits & 32768u) {
-      if (i < n_front) __builtin_amdgcn_s_setprio(3);
-      else __builtin_amdgcn_s_setprio(0);
-    }
     const bool stamp = a.work != nullptr;
     const uint64_t c_start = stamp ? clock64() : 0ull;
     uint32_t w_ent = 0, w_rec = 0, w_link = 0;

@@ -160,16 +160,26 @@ __device__ __forceinline__ void walk_topic(uint32_t t, const uint8_t* __restrict
   }
 }
 
+// k_walk's parameters as they lie in the kernarg segment
+struct WalkParams {
+  const uint8_t* tb;
+  const uint64_t* to;
+  uint32_t n;
+  DevIndex ix;
+};
+
 // list == null: thread per topic t < n. Else the topics list[0, *n_list), grid-stride (the
 // frontier walk's fallback: its length is known on the device only).
 template <bool FILL, bool LISTS, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_walk(const uint8_t* __restrict__ tb,
                                               const uint64_t* __restrict__ to, uint32_t n,
-                                              DevIndex ix, TopicCount* __restrict__ cnt,
+                                              DevIndex ix_, TopicCount* __restrict__ cnt,
                                               const TopicOff* __restrict__ off,
                                               uint32_t* __restrict__ gathers, uint32_t* __restrict__ ovf,
                                               const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
                                               bool clamp) {
+  (void)ix_;
+  const DevIndex& ix = kernarg_at<DevIndex>(offsetof(WalkParams, ix));
   __shared__ uint2 path[kWalkPath][256];  // level d: the '+' / '#' children of the particle at depth d
   const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (!list) {
@@ -235,8 +245,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // the fused desc's arguments, read from the kernarg segment where the epilogue uses them: a
   // by-value parameter is loaded at the kernel's entry and held across the walk (~60 scalar
   // registers spilled to vector lanes, read back in the epilogue)
-  const DescArgs& dk = *(const DescArgs*)((const __attribute__((address_space(4))) char*)
-                                              __builtin_amdgcn_kernarg_segment_ptr() + offsetof(WalkfParams, da));
+  const DescArgs& dk = kernarg_at<DescArgs>(offsetof(WalkfParams, da));
   constexpr uint32_t kTopics = 256 / G;  // topics per workgroup
   // levels and gathers a group holds: 8-lane groups keep 32 topics per workgroup within 20 KB of
   // LDS (8 workgroups per CU: twice the topics in flight of 16-lane groups); a topic beyond them
