@@ -38,7 +38,9 @@
                                      their partner links instead of the record-keyed fold (round 5); bits 10 / 11
                                      (exact) that fold for merge gathers of up to two passes / any number of
                                      passes over their visits (default: one pass, kBigFill visits); bit 13
-                                     (exact) k_merge's set pass instead of k_set (round 5) */
+                                     (exact) k_merge's set pass instead of k_set (round 5); bit 14 (exact)
+                                     k_set's record-keyed fold at k_merge's table size (kBigFill visits, not
+                                     its own kSetBigFill) */
 #define MQ_OPT_PATCH_CODES 20     /* host span results: 1 (default) 4-byte patch codes when the index allows them
                                      (MQ_SPANS_PATCH_CODES); 0: 8-byte mq_patch records */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than

@@ -156,7 +156,11 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
       V.cv.wait(g, [&] { return V.writers == 0; });
     }
     std::lock_guard<FifoMutex> lk(L.mu);
-    return f();
+    if (!slow_on()) return f();
+    slow_begin();
+    const int r = f();
+    slow_report(access == Access::kUpdate ? "update" : "read", 0.0);
+    return r;
   } catch (const HipError& e) {
     return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
   } catch (const std::bad_alloc&) {

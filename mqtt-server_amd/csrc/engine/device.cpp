@@ -45,6 +45,37 @@ size_t pin_cap(size_t bytes) {
 }
 }  // namespace
 
+namespace {
+struct SlowLog {
+  std::chrono::steady_clock::time_point t0;
+  char buf[512];
+  size_t len = 0;
+};
+thread_local SlowLog g_slow;
+const double g_slow_ms = [] {
+  const char* e = getenv("MQ_SLOW_MS");
+  return e ? atof(e) : 0.0;
+}();
+}  // namespace
+
+bool slow_on() { return g_slow_ms > 0; }
+void slow_begin() {
+  if (!slow_on()) return;
+  g_slow.t0 = std::chrono::steady_clock::now();
+  g_slow.len = 0;
+  g_slow.buf[0] = 0;
+}
+void slow_mark(const char* what) {
+  if (!slow_on() || g_slow.len + 48 >= sizeof(g_slow.buf)) return;
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_slow.t0).count();
+  g_slow.len += (size_t)snprintf(g_slow.buf + g_slow.len, sizeof(g_slow.buf) - g_slow.len, " %s@%.2f", what, ms);
+}
+void slow_report(const char* call, double) {
+  if (!slow_on()) return;
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_slow.t0).count();
+  if (ms > g_slow_ms) fprintf(stderr, "mq slow: %s %.2f ms:%s\n", call, ms, g_slow.buf);
+}
+
 void* pinned_alloc(size_t bytes) {
   const size_t cap = pin_cap(bytes);
   {
@@ -70,7 +101,9 @@ void* pinned_alloc(size_t bytes) {
     }
   }
   void* p = nullptr;
+  slow_mark("hipHostMalloc");
   if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess || !p) throw std::bad_alloc();
+  slow_mark("pinned");
   return p;
 }
 
@@ -126,7 +159,9 @@ void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
   if (!d || m.epoch != epoch || cap < n) {
     release();
     cap = std::max<size_t>(std::max(m.h.capacity(), n), 1);
+    slow_mark("mirror-realloc");
     hip_check(hipMalloc(&d, cap * sizeof(T)), "hipMalloc(mirror)");
+    slow_mark("mirror-malloc");
     epoch = m.epoch;
     full = true;
   }
@@ -565,8 +600,10 @@ void Device::stage_inputs(const uint8_t* tb, const uint64_t* to, uint32_t n, hip
 // allocation, so the device drains first (rare: buffers only grow).
 static void grow(DevBuf& b, size_t bytes) {
   if (bytes <= b.bytes && b.p) return;
+  slow_mark("grow");
   if (b.p) hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(grow)");
   b.ensure(bytes);
+  slow_mark("grown");
 }
 
 hipStream_t Device::host_stream() {
@@ -1071,7 +1108,12 @@ void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   mq_xlist x;
   trace_runs = 1;
   spans_begin(ix, d_tb, d_to, n, s, &x, one_sync_);
-  if (spans_end(ix, nullptr, 0, s, host, out, ready, issued)) return;
+  slow_mark("begin");
+  if (spans_end(ix, nullptr, 0, s, host, out, ready, issued)) {
+    slow_mark("end");
+    return;
+  }
+  slow_mark("end-rerun");
   trace_runs = 2;
   // the one-sync run's buffers did not hold the batch: again, sized by the host
   spans_begin(ix, d_tb, d_to, n, s, &x, false);
@@ -1082,7 +1124,9 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
                          mq_xlist* x, bool one_sync, bool shard_sync) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   flush_host_copy();  // (a pipelined batch's copy: before this batch reuses any stage)
+  slow_mark("flush");
   sync(ix, s);
+  slow_mark("sync");
   memset(x, 0, sizeof(*x));
   x->n_topics = n;
   x->shard = ix.shard();

@@ -68,6 +68,12 @@ struct DevMirror {
 // GB/s, into pinned memory at PCIe rate. Blocks are pooled (page-locking is slow) and elements are
 // default-initialised (resize does not zero gigabytes of rows that the D2H overwrites).
 void* pinned_alloc(size_t bytes);
+// MQ_SLOW_MS=<ms> (diagnosis): a C-ABI call that holds the handle lock longer than that prints the
+// milestones its thread marked (slow_mark: the name and the ms since slow_begin) to stderr
+bool slow_on();
+void slow_begin();
+void slow_mark(const char* what);
+void slow_report(const char* call, double threshold_ms);
 void pinned_free(void* p, size_t bytes);
 
 template <class T>

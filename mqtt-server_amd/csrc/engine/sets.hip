@@ -27,8 +27,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // pair-block headers
   constexpr uint32_t kWsWords = 2 * kMapSlots + 3 * kPairMax;
   static_assert(kBigSlots <= kWsWords, "the record-keyed fold's table must fit the wave's words");
+  // the record-keyed fold's table: the wave's words and kSetBigExtra more (eight workgroups of
+  // four waves still fit a CU's 160 KB of LDS), so gathers of up to kSetBigFill visits fold
+  // instead of resolving through their partner links
+  constexpr uint32_t kSetBigExtra = 192;
+  constexpr uint32_t kSetBigSlots = kWsWords + kSetBigExtra;
+  constexpr uint32_t kSetBigFill = kSetBigSlots * 3 / 4;
   struct WaveLds {  // (one block per wave: every array an immediate offset from one base)
     uint32_t ws[kWsWords];
+    uint32_t ws_big[kSetBigExtra];  // (contiguous with ws: the record-keyed fold's table continues here)
     uint32_t node[kPairMax];     // merge gather x's particle (gather order = DFS order)
     uint32_t ga[kHitMax];        // staged hit lists (g, h): g's merge gather,
     uint32_t off[kHitMax];       //   the list's offset in the pair-list pool,
@@ -49,7 +56,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t* const h_off = W.off;
   uint32_t* const h_hb = W.hb;
   uint32_t* const h_pre = W.pre;
-  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u));
+  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 16384u));
   const DevIndex& ix = a.ix;
   const uint32_t n_front = (uint32_t)a.n_reps[0];
   const uint32_t i_end = n_front + (uint32_t)a.n_reps[1];
@@ -319,8 +326,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       wave_sync_lds();
     };
-    // big: one merge gather's lists [j0, j1), at most kBigFill visits, keyed by k alone:
-    // (k + 1) << 5 | kBit* per record over the wave's kBigSlots words; the record's own meta and
+    // big: one merge gather's lists [j0, j1), at most kSetBigFill visits, keyed by k alone:
+    // (k + 1) << 5 | kBit* per record over the wave's kSetBigSlots words; the record's own meta and
     // identifier are read from the pool at the emission
     auto fold_big = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
       map_ok = false;
@@ -328,7 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const uint32_t sub_off = ix.lists[mg_node[xa]].sub_off;
       const uint32_t v0 = h_pre[j0], v1 = h_pre[j1];
       // the table sized to the visits (at most 2/3 full: short probe runs, and a short emission scan)
-      const uint32_t ns = min(kBigSlots, ((v1 - v0) * 3 / 2 + 63) & ~63u);
+      const uint32_t ns = min(kSetBigSlots, ((v1 - v0) * 3 / 2 + 63) & ~63u);
       for (uint32_t q = lane; q < ns; q += 64) ws[q] = 0u;
       uint32_t jj_next, jb = j0;
       PairSlot e_next = locate_run(v0, jb, j1, jj_next, jb);
@@ -344,7 +351,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                 ((pm & 3u) == 1u ? kBitQos1 : 0u) | ((pm & 3u) == 2u ? kBitQos2 : 0u);
           const uint32_t key = (e.k + 1u) << 5;
           uint32_t sl = __umulhi(hash32(e.k), ns);
-          for (;;) {  // (at most kBigFill keys in ns >= 3/2 of them slots: a free slot is always found)
+          for (;;) {  // (at most kSetBigFill keys in ns >= 4/3 of them slots: a free slot is always found)
             const uint32_t prev = atomicCAS(&ws[sl], 0u, key | bits);
             if (prev == 0u) break;
             if ((prev & ~31u) == key) {
@@ -398,12 +405,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       wave_sync_lds();
     };
     // the staged lists in chunks of whole merge gathers: up to kFoldCap visits folded together; a
-    // gather beyond that alone in the record-keyed fold while kBigFill holds it, else its links
+    // gather beyond that alone in the record-keyed fold while kSetBigFill holds it (MQ_OPT_SET_EXP
+    // bit 14: kBigFill, k_merge's table), else its links
     auto fold_hits = [&]() __attribute__((always_inline)) {
       if (lane == 0) h_pre[n_hit] = tot;
       wave_sync_lds();
       const uint32_t fcap = (exp_bits & 256u) ? 16u : kFoldCap;
-      const uint32_t big_max = (exp_bits & 512u) ? 0u : kBigFill;
+      const uint32_t big_max = (exp_bits & 512u) ? 0u : (exp_bits & 16384u) ? kBigFill : kSetBigFill;
       uint32_t j0 = 0;
       while (j0 < n_hit) {  // wave-uniform
         const uint32_t b = h_pre[j0];
