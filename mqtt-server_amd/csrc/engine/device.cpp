@@ -1466,14 +1466,28 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   }
   XSrc* const h_src = h_xsrc_;  // (pinned: its copy runs in order with the batch; the previous batch
                                 //  synchronised before this one writes it again)
-  for (uint32_t f = 0; f < nf; f++) {  // import: per-topic offsets of each foreign list
+  XScanArgs xs;  // import: per-topic offsets of every foreign list, one batched scan
+  memset(&xs, 0, sizeof(xs));
+  for (uint32_t f = 0; f < nf; f++) {
     if (xf[f].n_topics != n || (xf[f].n_ents && (!xf[f].counts || !xf[f].ents)))
       throw HipError{hipErrorInvalidValue, "foreign list does not match the batch"};
-    grow(x_foff_[f], (size_t)(n + 1) * sizeof(TopicOff));
-    launch_counts(xf[f].counts, n, counts_.as<TopicCount>(), s);
-    launch_scan(counts_.as<TopicCount>(), n, bsum_.as<TopicOff>(), bpre_.as<TopicOff>(), x_foff_[f].as<TopicOff>(), s);
+    grow(x_foff_[f], (size_t)(n + 1) * sizeof(uint32_t));
+    if (!xf[f].counts && n) {  // (an export of nothing may come without counts: zeros)
+      if (x_zero_.bytes < (size_t)n * sizeof(uint32_t)) {
+        grow(x_zero_, (size_t)n * sizeof(uint32_t));
+        hip_check(hipMemsetAsync(x_zero_.p, 0, x_zero_.bytes, s), "memset");
+      }
+    }
+    xs.in[f] = xf[f].counts ? xf[f].counts : x_zero_.as<uint32_t>();
+    xs.out[f] = x_foff_[f].as<uint32_t>();
+    h_src[f] = XSrc{x_foff_[f].as<uint32_t>(), reinterpret_cast<const XEnt*>(xf[f].ents)};
+  }
+  if (nf && n) {
+    const size_t rows = (size_t)nf * ((n + kScanBlock - 1) / kScanBlock + 1) * sizeof(uint32_t);
+    grow(x_bsum_, rows);
+    grow(x_bpre_, rows);
+    launch_xscan(xs, nf, n, x_bsum_.as<uint32_t>(), x_bpre_.as<uint32_t>(), s);
     hip_check(hipGetLastError(), "import");
-    h_src[f] = XSrc{x_foff_[f].as<TopicOff>(), reinterpret_cast<const XEnt*>(xf[f].ents)};
   }
   if (nf) {
     grow(x_src_, sizeof(h_src));

@@ -365,6 +365,8 @@ class Device {
   DevBuf sp_work_;                   // MQ_PROF_WORK counters (kPatchRegions x kWork)
   // sharded: the exported list (offsets, entries, counts) and the imported lists' offsets
   DevBuf x_off_, x_ents_, x_cnt_, x_src_, x_foff_[kMaxShards - 1];
+  DevBuf x_bsum_, x_bpre_;  // the import's batched scan (block sums, prefixes: a row per shard)
+  DevBuf x_zero_;           // zero counts for an export that came without them
   DevBuf x_stride_, xbsum_, xbpre_, x_tot_;  // sharded one-sync begins: k_desc's export, its scan, total
   XSrc* h_xsrc_ = nullptr;                   // pinned: the imported lists' sources (no stack copy)
   struct SpanBatch {               // between spans_begin and spans_end

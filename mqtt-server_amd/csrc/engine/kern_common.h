@@ -157,6 +157,19 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
   return x - v;
 }
 
+// inclusive u32 scan over a 256-thread workgroup (wt: 4 words of LDS)
+__device__ __forceinline__ uint32_t block_scan_incl32(uint32_t v, uint32_t* wt /*4*/) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t tot;
+  const uint32_t ex = wave_excl_scan(v, lane, &tot);
+  if (lane == 0) wt[wv] = tot;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t w = 0; w < wv; w++) add += wt[w];
+  __syncthreads();
+  return ex + v + add;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);

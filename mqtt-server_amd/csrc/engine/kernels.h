@@ -132,10 +132,18 @@ constexpr uint32_t kDescMerge = 1u << 31;
 constexpr uint32_t kMaxShards = 16;  // sharded index: shards a batch's exchange can join
 
 // One imported cross-shard list: per-topic offsets (.g) into its entries.
-struct XSrc {
-  const struct TopicOff* xoff;
+struct XSrc {  // another shard's export: topic t's entries xent[xoff[t], xoff[t + 1])
+  const uint32_t* xoff;
   const XEnt* xent;
 };
+// The imported lists' per-topic offsets: exclusive scans of nf shards' per-topic counts (u32,
+// n + 1 each, out[f]) in three launches whatever nf is. bsum / bpre: nf * (nb + 1) words, nb =
+// ceil(n / kScanBlock).
+struct XScanArgs {
+  const uint32_t* in[kMaxShards - 1];
+  uint32_t* out[kMaxShards - 1];
+};
+void launch_xscan(const XScanArgs& a, uint32_t nf, uint64_t n, uint32_t* bsum, uint32_t* bpre, hipStream_t s);
 
 // Span-format records (include/mqmatch.h mq_span / mq_patch / mq_topic_spans).
 struct SpanRec {  // one gathered particle: subs[sub_off, + n_sub), shr[shr_off, + n_shr)

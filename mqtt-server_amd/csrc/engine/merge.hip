@@ -46,8 +46,8 @@ __global__ __launch_bounds__(1024) void k_dedup_rep(DedupArgs a) {
       // sharded: the same cross-shard entries of every other shard, in the same order
       for (uint32_t f = 0; eq && f < a.n_xf; f++) {
         const XSrc src = a.xsrc[f];
-        const uint64_t t0 = src.xoff[t].g, t1 = src.xoff[t + 1].g, v0 = src.xoff[v].g;
-        eq = src.xoff[v + 1].g - v0 == t1 - t0;
+        const uint64_t t0 = src.xoff[t], t1 = src.xoff[t + 1], v0 = src.xoff[v];
+        eq = src.xoff[v + 1] - v0 == t1 - t0;
         for (uint64_t k = 0; eq && k < t1 - t0; k++) {
           const XEnt p = src.xent[t0 + k], q = src.xent[v0 + k];
           eq = p.fid == q.fid && p.rank == q.rank;
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void k_xsig(XSigArgs a) {
   uint32_t fc = 0;
   for (uint32_t f = 0; f < a.n_xf; f++) {
     const XSrc src = a.xsrc[f];
-    const uint64_t x0 = src.xoff[t].g, x1 = src.xoff[t + 1].g;
+    const uint64_t x0 = src.xoff[t], x1 = src.xoff[t + 1];
     for (uint64_t k = x0; k < x1; k++) {
       const XEnt e = src.xent[k];
       sig = mix64(sig ^ ((uint64_t)f << 56 | (uint64_t)fc << 32 | e.fid)) + e.rank;
@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t n_ent = n_map;
     for (uint32_t f = 0; XS && f < a.n_xf; f++) {
       const XSrc src = a.xsrc[f];
-      const uint64_t x0 = src.xoff[t].g, x1 = src.xoff[t + 1].g;
+      const uint64_t x0 = src.xoff[t], x1 = src.xoff[t + 1];
       for (uint64_t k0 = x0; k0 < x1; k0 += 64) {
         const uint64_t k = k0 + lane;
         const uint32_t x = n_ent + (uint32_t)(k - x0);
@@ -748,7 +748,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (XS && (h & kForeign)) {
         for (uint32_t f = 0; f < a.n_xf; f++) {
           const XSrc src = a.xsrc[f];
-          for (uint64_t k = src.xoff[t].g; k < src.xoff[t + 1].g; k++)
+          for (uint64_t k = src.xoff[t]; k < src.xoff[t + 1]; k++)
             if ((kForeign | src.xent[k].fid) == h) return Pos{src.xent[k].rank, kNone, true};
         }
         return Pos{0, kNone, false};

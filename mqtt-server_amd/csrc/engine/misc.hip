@@ -394,4 +394,66 @@ void launch_readback(const ReadbackArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_readback, dim3(1), dim3(64), 0, s, a);
 }
 
+// The imported lists' offsets (XScanArgs): the u32 scan of k_scan32_* with one row of blocks per
+// foreign shard (blockIdx.y), so the import costs three launches for any number of shards, and 4
+// bytes per topic and shard where a TopicOff scan wrote 40.
+__global__ __launch_bounds__(256) void k_xscan_reduce(XScanArgs a, uint64_t n, uint32_t nb, uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t wt[4];
+  const uint32_t* in = a.in[blockIdx.y];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  uint32_t v = 0;
+  for (int k = 0; k < 4; k++)
+    if (base + k < n) v += in[base + k];
+  v = block_scan_incl32(v, wt);
+  if (threadIdx.x == 255) bsum[(uint64_t)blockIdx.y * (nb + 1) + blockIdx.x] = v;
+}
+
+__global__ __launch_bounds__(256) void k_xscan_blocks(uint32_t nb, const uint32_t* __restrict__ bsum,
+                                                      uint32_t* __restrict__ bpre) {
+  __shared__ uint32_t wt[4];
+  __shared__ uint32_t carry;
+  const uint64_t row = (uint64_t)blockIdx.x * (nb + 1);
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t v = b < nb ? bsum[row + b] : 0u;
+    const uint32_t incl = block_scan_incl32(v, wt);
+    if (b < nb) bpre[row + b] = carry + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 255) carry += incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bpre[row + nb] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_xscan_apply(XScanArgs a, uint64_t n, uint32_t nb,
+                                                     const uint32_t* __restrict__ bpre) {
+  __shared__ uint32_t wt[4];
+  const uint32_t* in = a.in[blockIdx.y];
+  uint32_t* out = a.out[blockIdx.y];
+  const uint64_t row = (uint64_t)blockIdx.y * (nb + 1);
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
+  uint32_t c[4], v = 0;
+  for (int k = 0; k < 4; k++) {
+    c[k] = base + k < n ? in[base + k] : 0u;
+    v += c[k];
+  }
+  const uint32_t incl = block_scan_incl32(v, wt);
+  uint32_t ex = bpre[row + blockIdx.x] + incl - v;
+  for (int k = 0; k < 4; k++) {
+    if (base + k < n) out[base + k] = ex;
+    ex += c[k];
+  }
+  if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = bpre[row + nb];
+}
+
+void launch_xscan(const XScanArgs& a, uint32_t nf, uint64_t n, uint32_t* bsum, uint32_t* bpre, hipStream_t s) {
+  if (!nf || !n) return;
+  const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+  hipLaunchKernelGGL(k_xscan_reduce, dim3(nb, nf), dim3(256), 0, s, a, n, nb, bsum);
+  hipLaunchKernelGGL(k_xscan_blocks, dim3(nf), dim3(256), 0, s, nb, bsum, bpre);
+  hipLaunchKernelGGL(k_xscan_apply, dim3(nb, nf), dim3(256), 0, s, a, n, nb, bpre);
+}
+
 }  // namespace mq

@@ -320,17 +320,6 @@ void launch_msg_place(uint32_t n, const TopicCount* cnt, const TopicOff* off, co
 // more than one particle this is the only fan-out: the wave's lanes take the run's particles,
 // and a lane keeps deeper fan-outs on a small frame stack.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t block_scan_incl32(uint32_t v, uint32_t* wt /*4*/) {
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t tot;
-  const uint32_t ex = wave_excl_scan(v, lane, &tot);
-  if (lane == 0) wt[wv] = tot;
-  __syncthreads();
-  uint32_t add = 0;
-  for (uint32_t w = 0; w < wv; w++) add += wt[w];
-  __syncthreads();
-  return ex + v + add;
-}
 
 __global__ __launch_bounds__(256) void k_scan32_reduce(const uint32_t* __restrict__ in, uint64_t n,
                                                        uint32_t* __restrict__ bsum) {
