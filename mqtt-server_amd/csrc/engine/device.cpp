@@ -1542,6 +1542,10 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       xa.g_stride = sb_.fused ? kGatherCap : 0u;
       xa.tc = sb_.tc;
       xa.desc = desc_[0].as<GDesc>();
+      xa.dd_keys = sb_.walk_inserted ? nullptr : dd.keys;  // (the insert on the finished signatures)
+      xa.dd_vals = dd.vals;
+      xa.dd_mask = dd.table_mask;
+      xa.dd_tslot = dd.tslot;
       prof.begin(s, "xsig");
       launch_xsig(xa, s);
       prof.end("xsig", s);
@@ -1549,7 +1553,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       dd.fcount = xa.fcount;
     }
     prof.begin(s, "dedup");
-    launch_dedup(dd, s, !sb_.walk_inserted);
+    launch_dedup(dd, s, !sb_.walk_inserted && !nf);
     prof.end("dedup", s);
     hip_check(hipGetLastError(), "k_dedup");
     sb_.n_sets = 0;

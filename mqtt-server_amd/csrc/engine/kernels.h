@@ -341,6 +341,12 @@ struct XSigArgs {
   struct GDesc* desc;
   uint32_t g_stride;                // the walk-fused layout: topic t's gathers at t * g_stride, their
   const struct TopicCount* tc;      //   number tc[t].gathers (off unused)
+  // non-null: k_dedup_insert's work too, on the finished signatures (DedupArgs keys / vals /
+  // table_mask / tslot), so the dedup runs k_dedup_rep alone
+  unsigned long long* dd_keys;
+  uint32_t* dd_vals;
+  uint64_t dd_mask;
+  uint32_t* dd_tslot;
 };
 void launch_xsig(const XSigArgs& a, hipStream_t s);
 // The merge set pass of an index that is not sharded (sets.hip): k_merge<spans, SET>'s results with

@@ -275,22 +275,34 @@ void launch_host_rebase(uint32_t n, const uint32_t* rep, const uint64_t* nbase, 
 
 __global__ __launch_bounds__(256) void k_xsig(XSigArgs a) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.n) return;
+  const bool act = t < a.n;  // (no early exit: the dedup insert below is wave-cooperative)
   uint64_t sig = 0;
-  uint32_t fc = 0;
-  for (uint32_t f = 0; f < a.n_xf; f++) {
-    const XSrc src = a.xsrc[f];
-    const uint64_t x0 = src.xoff[t], x1 = src.xoff[t + 1];
-    for (uint64_t k = x0; k < x1; k++) {
-      const XEnt e = src.xent[k];
-      sig = mix64(sig ^ ((uint64_t)f << 56 | (uint64_t)fc << 32 | e.fid)) + e.rank;
-      fc++;
+  uint32_t fc = 0, mc = 0;
+  unsigned long long msig = 0;
+  if (act) {
+    for (uint32_t f = 0; f < a.n_xf; f++) {
+      const XSrc src = a.xsrc[f];
+      const uint64_t x0 = src.xoff[t], x1 = src.xoff[t + 1];
+      for (uint64_t k = x0; k < x1; k++) {
+        const XEnt e = src.xent[k];
+        sig = mix64(sig ^ ((uint64_t)f << 56 | (uint64_t)fc << 32 | e.fid)) + e.rank;
+        fc++;
+      }
+    }
+    a.fcount[t] = fc;
+    mc = a.mcount[t];
+    if (mc) msig = a.msig[t];
+    if (fc && mc) {
+      msig = mix64(msig ^ sig) | 1ull;
+      a.msig[t] = msig;
     }
   }
-  a.fcount[t] = fc;
-  const uint32_t mc = a.mcount[t];
-  if (!fc || !mc) return;
-  a.msig[t] = mix64(a.msig[t] ^ sig) | 1ull;
+  if (a.dd_keys) {  // k_dedup_insert's work (the merge gathers and the other shards' entries must fit k_merge's map)
+    const bool ok = act && mc != 0 && mc <= kPairMax && mc + fc < kMapSlots;
+    const uint32_t slot = dedup_insert(a.dd_keys, a.dd_vals, a.dd_mask, t, ok, ok ? msig : 0ull);
+    if (act) a.dd_tslot[t] = slot;
+  }
+  if (!act || !fc || !mc) return;
   if (mc <= kPairMax && mc + fc >= kMapSlots) {  // k_merge's slow path reads GDesc records
     if (a.g_stride) {  // the walk-fused layout (the gather words at the spans' positions)
       const uint64_t g0 = (uint64_t)t * a.g_stride;
