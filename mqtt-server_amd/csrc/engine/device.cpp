@@ -1648,9 +1648,10 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       // persistent waves striding over the list
       const uint32_t set_blocks = set_grid_ ? std::max<uint32_t>(1, (uint32_t)((sb_.n_sets + 3) / 4))
                                             : (merge_blocks_ ? merge_blocks_ : n_cus_ * 8);
-      // k_set (sets.hip) unless the index is sharded (rank keys), a measurement variant of k_merge's
-      // set pass is asked for (MQ_OPT_SET_EXP bit 7, the attribution bits 0-4), or bit 13
-      if (!ix.sharded() && !(set_exp_ & (0x1Fu | 128u | 8192u)) && merge_wpe == kMergeWavesPerEU)
+      // k_set (sets.hip; a sharded index's with its rank keys) unless a sharded index holds filters
+      // deeper than 32 levels (their keys can tie: k_merge's deep tie-break), a measurement variant
+      // of k_merge's set pass is asked for (MQ_OPT_SET_EXP bit 7, the attribution bits 0-4), or bit 13
+      if (!(ix.sharded() && a.ix.deep) && !(set_exp_ & (0x1Fu | 128u | 8192u)) && merge_wpe == kMergeWavesPerEU)
         launch_set(a, set_blocks, s);
       else
         launch_merge(a, true, merge_wpe, set_blocks, s);

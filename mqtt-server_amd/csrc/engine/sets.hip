@@ -15,7 +15,12 @@
 
 namespace mq {
 
-template <int WPE>
+// XS (a sharded index, round 5): a set's entries are its merge gathers and then the other shards'
+// exported nodes of its representative (kForeign | fid, with their rank keys), the pair analysis
+// covers pairs (merge gather, any entry), and DFS order between an entry of another shard and a
+// merge gather here is the rank keys' (k_merge<spans, XS, SET>'s results; an index with filters
+// deeper than 32 levels, whose keys can tie, keeps k_merge).
+template <int WPE, bool XS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_set(EmitArgs args) {
   // the arguments, read from the kernarg segment where they are used: a by-value parameter is
   // loaded whole at the kernel's entry, and its ~40 pointers and counts held across the kernel
@@ -30,13 +35,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // the record-keyed fold's table: the wave's words and kSetBigExtra more (eight workgroups of
   // four waves still fit a CU's 160 KB of LDS), so gathers of up to kSetBigFill visits fold
   // instead of resolving through their partner links
-  constexpr uint32_t kSetBigExtra = 192;
+  constexpr uint32_t kSetBigExtra = XS ? 0 : 192;  // (XS: the LDS holds the rank keys instead)
   constexpr uint32_t kSetBigSlots = kWsWords + kSetBigExtra;
+  constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // entries: merge gathers (+ XS: other shards' nodes)
   constexpr uint32_t kSetBigFill = kSetBigSlots * 3 / 4;
   struct WaveLds {  // (one block per wave: every array an immediate offset from one base)
     uint32_t ws[kWsWords];
-    uint32_t ws_big[kSetBigExtra];  // (contiguous with ws: the record-keyed fold's table continues here)
-    uint32_t node[kPairMax];     // merge gather x's particle (gather order = DFS order)
+    uint32_t ws_big[XS ? 1 : kSetBigExtra];  // (contiguous with ws: the record-keyed fold's table continues here)
+    uint32_t node[kEnt];         // entry x's particle: merge gathers in gather order (= DFS order), then
+                                 //   (XS) other shards' nodes as kForeign | fid
+    uint64_t rank[XS ? kEnt : 1];  // (XS) entry x's rank key
     uint32_t ga[kHitMax];        // staged hit lists (g, h): g's merge gather,
     uint32_t off[kHitMax];       //   the list's offset in the pair-list pool,
     uint32_t hb[kHitMax];        //   h's merge gather,
@@ -74,8 +82,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       mg_node[lane] = a.mlist[k];
       ent_off[lane] = P.x;
       ent_mask[lane] = P.y;
+      if (XS) W.rank[lane] = a.mrank[k];
+    }
+    uint32_t n_ent = lc;  // (XS: the other shards' nodes of the set join as entries lc..; k_dedup
+                          //  admitted the set only if they fit the map: n_ent < kMapSlots)
+    for (uint32_t f = 0; XS && f < a.n_xf; f++) {
+      const XSrc src = a.xsrc[f];
+      const uint32_t x0 = src.xoff[t], x1 = src.xoff[t + 1];
+      for (uint32_t k0 = x0; k0 < x1; k0 += 64) {
+        const uint32_t k = k0 + lane, x = n_ent + (k - x0);
+        if (k < x1 && x < kEnt) {
+          const XEnt e = src.xent[k];
+          mg_node[x] = kForeign | e.fid;
+          W.rank[x] = e.rank;
+        }
+      }
+      n_ent += x1 - x0;
     }
     wave_sync_lds();
+    // does entry xh come before the set's merge gather xg in DFS order?
+    auto before = [&](uint32_t xh, uint32_t xg) __attribute__((always_inline)) -> bool {
+      if constexpr (!XS) {
+        return xh < xg;
+      } else {
+        if (xh < lc) return xh < xg;  // both merge gathers here: gather order is DFS order
+        const uint64_t rh = W.rank[xh], rg = W.rank[xg];
+        if (rh != rg) return rh < rg;
+        atomicOr(ix.err, kErrDeepRank);  // (not reached: an index with deep filters runs k_merge)
+        return false;
+      }
+    };
     const uint64_t c_map = stamp ? clock64() : 0ull;
     // --- the patch range, reserved once the visits are counted -----------------------------------
     unsigned long long resv = 0;
@@ -97,10 +133,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (want && pfit) a.spatches[pbase + n_patch + prefix_before(m)] = PatchRec{row, meta};
       n_patch += (uint32_t)__popcll(m);
     };
-    // --- pair analysis: ordered pairs (g, h) of merge gathers; g's pair block lists the slots
-    // whose client also subscribes at h. p = g * lc + h, g by a multiply (p < 4096, lc <= 64)
-    const uint32_t np = lc * lc;
-    const uint32_t inv = (1u << 20) / lc + 1u;  // (p * inv) >> 20 == p / lc for p < 4096
+    // --- pair analysis: ordered pairs (g, h), g a merge gather and h an entry; g's pair block lists
+    // the slots whose client also subscribes at h. p = g * ne + h, g by a multiply: (p * inv) >> 24
+    // == p / ne for p < 2^24 / ne (p < 64 * 127)
+    const uint32_t ne = XS ? n_ent : lc;
+    const uint32_t np = lc * ne;
+    const uint32_t inv = (1u << 24) / ne + 1u;
     uint32_t n_hit = 0, tot = 0;
     uint64_t tot_all = 0;
     bool staged_all = true;
@@ -110,8 +148,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         bool hit = false;
         uint32_t ga = 0, hb = 0, e_off = 0, e_cnt = 0;
         if (p < np) {
-          ga = (p * inv) >> 20;
-          hb = p - ga * lc;
+          ga = (p * inv) >> 24;
+          hb = p - ga * ne;
           const uint32_t mask = ent_mask[ga];
           if (ga != hb && mask != kNone) {
             const uint32_t hn = mg_node[hb], eo = ent_off[ga];
@@ -186,11 +224,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     auto map_rebuild = [&]() __attribute__((always_inline)) {
       for (uint32_t q = lane; q < kMapSlots; q += 64) map_key[q] = kNone;
       wave_sync_lds();
-      if (lane < lc) {
-        const uint32_t node = mg_node[lane];
+      for (uint32_t x = lane; x < n_ent; x += 64) {
+        const uint32_t node = mg_node[x];
         uint32_t sl = hash32(node) & (kMapSlots - 1);
         while (atomicCAS(&map_key[sl], kNone, node) != kNone) sl = (sl + 1) & (kMapSlots - 1);
-        map_val[sl] = lane;
+        map_val[sl] = x;
       }
       wave_sync_lds();
       map_ok = true;
@@ -233,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
               other = first != via;
             }
             bound = true;
-            if (hx < gx) {
+            if (before(hx, gx)) {
               base = false;
               continue;
             }
@@ -301,7 +339,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             sl = (sl + 1) & (kFoldSlots - 1);
           }
           const uint32_t pm = e.meta >> kSlotPartShift;  // the partner's Qos | NoLocal << 2
-          atomicOr(&f_val[sl], (e.meta & kSlotOwnMask) | (hb < xa ? kFoldNonBase : 0u) |
+          atomicOr(&f_val[sl], (e.meta & kSlotOwnMask) | (before(hb, xa) ? kFoldNonBase : 0u) |
                                    ((pm & 4u) ? kFoldNoLocal : 0u) | (kFoldQos0 << (pm & 3u)));
         }
         w_rec += r < v1;
@@ -347,7 +385,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (r0 + 64 < v1) e_next = locate_run(r0 + 64, jb, j1, jj_next, jb);  // wave-uniform
         if (r < v1) {
           const uint32_t pm = e.meta >> kSlotPartShift;
-          const uint32_t bits = (h_hb[jj] < xa ? kBitNonBase : 0u) | ((pm & 4u) ? kBitNoLocal : 0u) |
+          const uint32_t bits = (before(h_hb[jj], xa) ? kBitNonBase : 0u) | ((pm & 4u) ? kBitNoLocal : 0u) |
                                 ((pm & 3u) == 1u ? kBitQos1 : 0u) | ((pm & 3u) == 2u ? kBitQos2 : 0u);
           const uint32_t key = (e.k + 1u) << 5;
           uint32_t sl = __umulhi(hash32(e.k), ns);
@@ -489,7 +527,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 void launch_set(const EmitArgs& a, uint32_t blocks, hipStream_t s) {
   if (!blocks) return;
-  hipLaunchKernelGGL(k_set<kMergeWavesPerEU>, dim3(blocks), dim3(256), 0, s, a);
+  if (a.ix.xinfo) hipLaunchKernelGGL((k_set<6, true>), dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_set<kMergeWavesPerEU>, dim3(blocks), dim3(256), 0, s, a);
 }
 
 }  // namespace mq
