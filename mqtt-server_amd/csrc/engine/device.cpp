@@ -1201,9 +1201,10 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     if (!dd_nwave_.p) dd_nwave_.ensure(sizeof(unsigned long long));
     ResetArgs ra;
     memset(&ra, 0, sizeof(ra));
-    void* ps[] = {unsafe_.p, ovf_.p, fb_cnt_.p, dd_nsets_.p, dd_spcount_.p, sp_pcount_.p, dd_nwave_.p};
-    const uint32_t bs[] = {4, 4, 4, 3 * 8, kPatchRegions * 8, kPatchRegions * 8, 8};
-    ra.n = 7;
+    if (!x_gt_.p) x_gt_.ensure(sizeof(TopicOff));
+    void* ps[] = {unsafe_.p, ovf_.p, fb_cnt_.p, dd_nsets_.p, dd_spcount_.p, sp_pcount_.p, dd_nwave_.p, x_gt_.p};
+    const uint32_t bs[] = {4, 4, 4, 3 * 8, kPatchRegions * 8, kPatchRegions * 8, 8, (uint32_t)sizeof(TopicOff)};
+    ra.n = 8;
     for (uint32_t k = 0; k < ra.n; k++) {
       ra.p[k] = ps[k];
       ra.bytes[k] = bs[k];
@@ -1344,18 +1345,31 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     grow(x_ents_, sizeof(XEnt));
     auto pack = [&]() {
       prof.begin(s, "xpack");
-      // (walk-fused: the scan also totals the batch's gathers, in .rows)
-      if (fused) launch_xcounts(x_cnt_.as<uint32_t>(), sp_tc_.as<TopicCount>(), n, counts_.as<TopicCount>(), s);
-      else launch_counts(x_cnt_.as<uint32_t>(), n, counts_.as<TopicCount>(), s);
-      launch_scan(counts_.as<TopicCount>(), n, xbsum_.as<TopicOff>(), xbpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
-      launch_xpack(n, offs_.as<TopicOff>(), fused ? kGatherCap : 0u, x_cnt_.as<uint32_t>(), x_off_.as<TopicOff>(),
-                   xbpre_.as<TopicOff>() + nb, x_stride_.as<XEnt>(), x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt),
-                   unsafe_.as<uint32_t>(), x_tot_.as<unsigned long long>(), s);
+      if (fused) {  // a u32 scan of the export's counts (k_xpack32 totals the batch's gathers too)
+        grow(x_off32_, (size_t)(n + 1) * sizeof(uint32_t));
+        const size_t rows = ((n + kScanBlock - 1) / kScanBlock + 1) * sizeof(uint32_t);
+        grow(x_bsum_, rows);
+        grow(x_bpre_, rows);
+        XScanArgs xs;
+        memset(&xs, 0, sizeof(xs));
+        xs.in[0] = x_cnt_.as<uint32_t>();
+        xs.out[0] = x_off32_.as<uint32_t>();
+        launch_xscan(xs, 1, n, x_bsum_.as<uint32_t>(), x_bpre_.as<uint32_t>(), s);
+        launch_xpack32(n, kGatherCap, x_cnt_.as<uint32_t>(), x_off32_.as<uint32_t>(), sp_tc_.as<TopicCount>(),
+                       x_stride_.as<XEnt>(), x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt), unsafe_.as<uint32_t>(),
+                       x_tot_.as<unsigned long long>(), x_gt_.as<TopicOff>(), s);
+      } else {
+        launch_counts(x_cnt_.as<uint32_t>(), n, counts_.as<TopicCount>(), s);
+        launch_scan(counts_.as<TopicCount>(), n, xbsum_.as<TopicOff>(), xbpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
+        launch_xpack(n, offs_.as<TopicOff>(), 0u, x_cnt_.as<uint32_t>(), x_off_.as<TopicOff>(), xbpre_.as<TopicOff>() + nb,
+                     x_stride_.as<XEnt>(), x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt), unsafe_.as<uint32_t>(),
+                     x_tot_.as<unsigned long long>(), s);
+      }
       prof.end("xpack", s);
       hip_check(hipGetLastError(), "k_xpack");
       ReadbackArgs rb;
       memset(&rb, 0, sizeof(rb));
-      rb.tot = fused ? xbpre_.as<TopicOff>() + nb : bpre_.as<TopicOff>() + nb;
+      rb.tot = fused ? x_gt_.as<TopicOff>() : bpre_.as<TopicOff>() + nb;
       rb.ovf = ovf_.as<uint32_t>();
       rb.fallback = walk_group_ ? fb_cnt_.as<uint32_t>() : nullptr;
       rb.unsafe = unsafe_.as<uint32_t>();
@@ -1382,6 +1396,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
       x_ents_.release();
       x_ents_.ensure(std::max<uint64_t>(h_fast_->n_sets[0] + h_fast_->n_sets[0] / 4 + 1024, 1) * sizeof(XEnt));
       hip_check(hipMemsetAsync(unsafe_.p, 0, sizeof(uint32_t), s), "memset");
+      if (fused) hip_check(hipMemsetAsync(x_gt_.p, 0, sizeof(TopicOff), s), "memset");  // (k_xpack32 sums again)
       pack();
       if (h_fast_->unsafe) throw HipError{hipErrorUnknown, "k_xpack: the export did not fit the grown buffer"};
     }

@@ -368,6 +368,8 @@ class Device {
   DevBuf x_bsum_, x_bpre_;  // the import's batched scan (block sums, prefixes: a row per shard)
   DevBuf x_zero_;           // zero counts for an export that came without them
   DevBuf x_stride_, xbsum_, xbpre_, x_tot_;  // sharded one-sync begins: k_desc's export, its scan, total
+  DevBuf x_off32_, x_gt_;  // walk-fused sharded begins: the export's u32 offsets; its totals (.g
+                           //   entries, .rows gathers) for k_readback
   XSrc* h_xsrc_ = nullptr;                   // pinned: the imported lists' sources (no stack copy)
   struct SpanBatch {               // between spans_begin and spans_end
     bool pending = false;

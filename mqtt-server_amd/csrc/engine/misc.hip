@@ -456,4 +456,31 @@ void launch_xscan(const XScanArgs& a, uint32_t nf, uint64_t n, uint32_t* bsum, u
   hipLaunchKernelGGL(k_xscan_apply, dim3(nb, nf), dim3(256), 0, s, a, n, nb, bpre);
 }
 
+__global__ __launch_bounds__(256) void k_xpack32(uint32_t n, uint32_t g_stride, const uint32_t* __restrict__ xcount,
+                                                 const uint32_t* __restrict__ xoff, const TopicCount* __restrict__ tc,
+                                                 const XEnt* __restrict__ xents, XEnt* __restrict__ ents, uint64_t cap,
+                                                 uint32_t* unsafe, unsigned long long* total, TopicOff* gt) {
+  const uint64_t all = xoff[n];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) {
+    total[0] = all;
+    gt->g = all;
+    if (all > cap) atomicOr(unsafe, kUnsafeXEnts);
+  }
+  const uint32_t g = wave_sum(t < n ? tc[t].gathers : 0u);
+  if ((threadIdx.x & 63) == 0 && g) atomicAdd((unsigned long long*)&gt->rows, (unsigned long long)g);
+  if (t >= n || all > cap) return;
+  const uint32_t c = xcount[t];
+  const uint64_t src = (uint64_t)t * g_stride, dst = xoff[t];
+  for (uint32_t k = 0; k < c; k++) ents[dst + k] = xents[src + k];
+}
+
+void launch_xpack32(uint32_t n, uint32_t g_stride, const uint32_t* xcount, const uint32_t* xoff, const TopicCount* tc,
+                    const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total,
+                    TopicOff* gt, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_xpack32, dim3((n + 255) / 256), dim3(256), 0, s, n, g_stride, xcount, xoff, tc, xents, ents,
+                     cap, unsafe, total, gt);
+}
+
 }  // namespace mq
