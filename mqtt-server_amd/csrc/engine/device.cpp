@@ -1201,10 +1201,9 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     if (!dd_nwave_.p) dd_nwave_.ensure(sizeof(unsigned long long));
     ResetArgs ra;
     memset(&ra, 0, sizeof(ra));
-    if (!x_gt_.p) x_gt_.ensure(sizeof(TopicOff));
-    void* ps[] = {unsafe_.p, ovf_.p, fb_cnt_.p, dd_nsets_.p, dd_spcount_.p, sp_pcount_.p, dd_nwave_.p, x_gt_.p};
-    const uint32_t bs[] = {4, 4, 4, 3 * 8, kPatchRegions * 8, kPatchRegions * 8, 8, (uint32_t)sizeof(TopicOff)};
-    ra.n = 8;
+    void* ps[] = {unsafe_.p, ovf_.p, fb_cnt_.p, dd_nsets_.p, dd_spcount_.p, sp_pcount_.p, dd_nwave_.p};
+    const uint32_t bs[] = {4, 4, 4, 3 * 8, kPatchRegions * 8, kPatchRegions * 8, 8};
+    ra.n = 7;
     for (uint32_t k = 0; k < ra.n; k++) {
       ra.p[k] = ps[k];
       ra.bytes[k] = bs[k];
@@ -1345,19 +1344,23 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     grow(x_ents_, sizeof(XEnt));
     auto pack = [&]() {
       prof.begin(s, "xpack");
-      if (fused) {  // a u32 scan of the export's counts (k_xpack32 totals the batch's gathers too)
+      if (fused) {  // u32 scans: the export's counts, and (total only) the topics' gathers
         grow(x_off32_, (size_t)(n + 1) * sizeof(uint32_t));
-        const size_t rows = ((n + kScanBlock - 1) / kScanBlock + 1) * sizeof(uint32_t);
-        grow(x_bsum_, rows);
-        grow(x_bpre_, rows);
+        if (!x_gt_.p) x_gt_.ensure(sizeof(TopicOff));
+        const uint32_t nb32 = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+        grow(x_bsum_, 2 * (nb32 + 1) * sizeof(uint32_t));
+        grow(x_bpre_, 2 * (nb32 + 1) * sizeof(uint32_t));
         XScanArgs xs;
         memset(&xs, 0, sizeof(xs));
         xs.in[0] = x_cnt_.as<uint32_t>();
         xs.out[0] = x_off32_.as<uint32_t>();
-        launch_xscan(xs, 1, n, x_bsum_.as<uint32_t>(), x_bpre_.as<uint32_t>(), s);
-        launch_xpack32(n, kGatherCap, x_cnt_.as<uint32_t>(), x_off32_.as<uint32_t>(), sp_tc_.as<TopicCount>(),
-                       x_stride_.as<XEnt>(), x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt), unsafe_.as<uint32_t>(),
-                       x_tot_.as<unsigned long long>(), x_gt_.as<TopicOff>(), s);
+        xs.in[1] = reinterpret_cast<const uint32_t*>(sp_tc_.as<TopicCount>()) + offsetof(TopicCount, gathers) / 4;
+        xs.stride[1] = sizeof(TopicCount) / 4;
+        launch_xscan(xs, 2, n, x_bsum_.as<uint32_t>(), x_bpre_.as<uint32_t>(), s);
+        launch_xpack32(n, kGatherCap, x_cnt_.as<uint32_t>(), x_off32_.as<uint32_t>(), x_stride_.as<XEnt>(),
+                       x_ents_.as<XEnt>(), x_ents_.bytes / sizeof(XEnt), unsafe_.as<uint32_t>(),
+                       x_tot_.as<unsigned long long>(), x_bpre_.as<uint32_t>() + (nb32 + 1) + nb32, x_gt_.as<TopicOff>(),
+                       s);
       } else {
         launch_counts(x_cnt_.as<uint32_t>(), n, counts_.as<TopicCount>(), s);
         launch_scan(counts_.as<TopicCount>(), n, xbsum_.as<TopicOff>(), xbpre_.as<TopicOff>(), x_off_.as<TopicOff>(), s);
@@ -1396,7 +1399,6 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
       x_ents_.release();
       x_ents_.ensure(std::max<uint64_t>(h_fast_->n_sets[0] + h_fast_->n_sets[0] / 4 + 1024, 1) * sizeof(XEnt));
       hip_check(hipMemsetAsync(unsafe_.p, 0, sizeof(uint32_t), s), "memset");
-      if (fused) hip_check(hipMemsetAsync(x_gt_.p, 0, sizeof(TopicOff), s), "memset");  // (k_xpack32 sums again)
       pack();
       if (h_fast_->unsafe) throw HipError{hipErrorUnknown, "k_xpack: the export did not fit the grown buffer"};
     }

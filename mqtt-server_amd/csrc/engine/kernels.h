@@ -141,15 +141,16 @@ struct XSrc {  // another shard's export: topic t's entries xent[xoff[t], xoff[t
 // ceil(n / kScanBlock).
 struct XScanArgs {
   const uint32_t* in[kMaxShards - 1];
-  uint32_t* out[kMaxShards - 1];
+  uint32_t* out[kMaxShards - 1];     // null: the row's total only (bpre[row * (nb + 1) + nb])
+  uint32_t stride[kMaxShards - 1];   // element i of row f at in[f][i * stride[f]] (0 or 1: packed)
 };
 void launch_xscan(const XScanArgs& a, uint32_t nf, uint64_t n, uint32_t* bsum, uint32_t* bpre, hipStream_t s);
 // The walk-fused sharded begin's pack: topic t's exported entries from xents[t * g_stride, + xcount[t])
 // to ents[xoff[t], ...) (u32 offsets, xoff[n] the total) unless the total passes cap (*unsafe |=
-// kUnsafeXEnts); *total = the total; gt (zeroed by k_reset): .g the total, .rows the batch's
-// gathers (tc[t].gathers summed), for k_readback.
-void launch_xpack32(uint32_t n, uint32_t g_stride, const uint32_t* xcount, const uint32_t* xoff, const TopicCount* tc,
-                    const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total,
+// kUnsafeXEnts); *total = the total; *gt = {the total, *gathers (the batch's gathers, a second
+// row of the same batched scan), 0, 0, 0} for k_readback.
+void launch_xpack32(uint32_t n, uint32_t g_stride, const uint32_t* xcount, const uint32_t* xoff, const XEnt* xents,
+                    XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total, const uint32_t* gathers,
                     TopicOff* gt, hipStream_t s);
 
 // Span-format records (include/mqmatch.h mq_span / mq_patch / mq_topic_spans).

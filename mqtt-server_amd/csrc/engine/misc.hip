@@ -400,10 +400,11 @@ void launch_readback(const ReadbackArgs& a, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_xscan_reduce(XScanArgs a, uint64_t n, uint32_t nb, uint32_t* __restrict__ bsum) {
   __shared__ uint32_t wt[4];
   const uint32_t* in = a.in[blockIdx.y];
+  const uint64_t st = a.stride[blockIdx.y] ? a.stride[blockIdx.y] : 1u;
   const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
   uint32_t v = 0;
   for (int k = 0; k < 4; k++)
-    if (base + k < n) v += in[base + k];
+    if (base + k < n) v += in[(base + k) * st];
   v = block_scan_incl32(v, wt);
   if (threadIdx.x == 255) bsum[(uint64_t)blockIdx.y * (nb + 1) + blockIdx.x] = v;
 }
@@ -432,11 +433,13 @@ __global__ __launch_bounds__(256) void k_xscan_apply(XScanArgs a, uint64_t n, ui
   __shared__ uint32_t wt[4];
   const uint32_t* in = a.in[blockIdx.y];
   uint32_t* out = a.out[blockIdx.y];
+  if (!out) return;  // (block-uniform: a row whose total alone is wanted)
+  const uint64_t st = a.stride[blockIdx.y] ? a.stride[blockIdx.y] : 1u;
   const uint64_t row = (uint64_t)blockIdx.y * (nb + 1);
   const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x * 4;
   uint32_t c[4], v = 0;
   for (int k = 0; k < 4; k++) {
-    c[k] = base + k < n ? in[base + k] : 0u;
+    c[k] = base + k < n ? in[(base + k) * st] : 0u;
     v += c[k];
   }
   const uint32_t incl = block_scan_incl32(v, wt);
@@ -457,30 +460,29 @@ void launch_xscan(const XScanArgs& a, uint32_t nf, uint64_t n, uint32_t* bsum, u
 }
 
 __global__ __launch_bounds__(256) void k_xpack32(uint32_t n, uint32_t g_stride, const uint32_t* __restrict__ xcount,
-                                                 const uint32_t* __restrict__ xoff, const TopicCount* __restrict__ tc,
+                                                 const uint32_t* __restrict__ xoff,
                                                  const XEnt* __restrict__ xents, XEnt* __restrict__ ents, uint64_t cap,
-                                                 uint32_t* unsafe, unsigned long long* total, TopicOff* gt) {
+                                                 uint32_t* unsafe, unsigned long long* total,
+                                                 const uint32_t* __restrict__ gathers, TopicOff* gt) {
   const uint64_t all = xoff[n];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t == 0) {
     total[0] = all;
-    gt->g = all;
+    *gt = TopicOff{all, *gathers, 0, 0, 0};
     if (all > cap) atomicOr(unsafe, kUnsafeXEnts);
   }
-  const uint32_t g = wave_sum(t < n ? tc[t].gathers : 0u);
-  if ((threadIdx.x & 63) == 0 && g) atomicAdd((unsigned long long*)&gt->rows, (unsigned long long)g);
   if (t >= n || all > cap) return;
   const uint32_t c = xcount[t];
   const uint64_t src = (uint64_t)t * g_stride, dst = xoff[t];
   for (uint32_t k = 0; k < c; k++) ents[dst + k] = xents[src + k];
 }
 
-void launch_xpack32(uint32_t n, uint32_t g_stride, const uint32_t* xcount, const uint32_t* xoff, const TopicCount* tc,
-                    const XEnt* xents, XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total,
+void launch_xpack32(uint32_t n, uint32_t g_stride, const uint32_t* xcount, const uint32_t* xoff, const XEnt* xents,
+                    XEnt* ents, uint64_t cap, uint32_t* unsafe, unsigned long long* total, const uint32_t* gathers,
                     TopicOff* gt, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_xpack32, dim3((n + 255) / 256), dim3(256), 0, s, n, g_stride, xcount, xoff, tc, xents, ents,
-                     cap, unsafe, total, gt);
+  hipLaunchKernelGGL(k_xpack32, dim3((n + 255) / 256), dim3(256), 0, s, n, g_stride, xcount, xoff, xents, ents, cap,
+                     unsafe, total, gathers, gt);
 }
 
 }  // namespace mq

@@ -1,8 +1,8 @@
-# Round 5: k_set for sharded indexes (rank keys; k_merge kept for indexes with deep filters) —
+# Round 5: sharded validation (k_set with rank keys, the u32 export pack) —
 # the sharded tests, then 8 / 4 / 2 simulated shards at 10M
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05/kset_xs
+O=gpurun_out/r05/xpack32
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_shard.py tests/test_dist_engine.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_shard.log 2>&1 || exit 1
 for k in 8 4 2; do
