@@ -143,8 +143,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint64_t tot_all = 0;
     bool staged_all = true;
     auto pairs = [&](bool counting, auto&& flush) __attribute__((always_inline)) {
-      // one round of 64 pairs, staged in pair order (g-major: a merge gather's lists adjacent)
-      auto stage = [&](bool hit, uint32_t ga, uint32_t hb, uint32_t e_off, uint32_t e_cnt) __attribute__((always_inline)) {
+      for (uint32_t p0 = 0; p0 < np; p0 += 64) {
+        const uint32_t p = p0 + lane;
+        bool hit = false;
+        uint32_t ga = 0, hb = 0, e_off = 0, e_cnt = 0;
+        if (p < np) {
+          ga = (p * inv) >> 24;
+          hb = p - ga * ne;
+          const uint32_t mask = ent_mask[ga];
+          if (ga != hb && mask != kNone) {
+            const uint32_t hn = mg_node[hb], eo = ent_off[ga];
+            uint32_t sl = pair_hash(hn) & mask;
+            for (uint32_t probes = 0; probes <= mask; probes += 4) {  // four slots per load round
+              PairEnt pe[4];
+#pragma unroll
+              for (uint32_t u = 0; u < 4; u++) pe[u] = ix.pent[eo + ((sl + u) & mask)];
+              w_ent += 4;
+              bool stop = false;
+#pragma unroll
+              for (uint32_t u = 0; u < 4; u++) {
+                if (stop) continue;
+                if (pe[u].h == hn) {
+                  hit = true;
+                  e_off = pe[u].off;
+                  e_cnt = pe[u].cnt;
+                  stop = true;
+                } else if (pe[u].h == kNone) {
+                  stop = true;
+                }
+              }
+              if (stop) break;
+              sl = (sl + 4) & mask;
+            }
+          }
+        }
         const uint64_t bh = __ballot(hit);
         const uint32_t nh = (uint32_t)__popcll(bh);
         uint32_t ct;
@@ -153,7 +185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           tot_all += ct;
           if (!staged_all || n_hit + nh > kHitMax) {  // wave-uniform
             staged_all = false;
-            return;
+            continue;
           }
         } else if (n_hit + nh > kHitMax) {
           flush();
@@ -167,70 +199,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         n_hit += nh;
         tot += ct;
-      };
-      // two rounds per step, their first probes (a pair's home slot, where pair tables at load <= 1/4
-      // end most lookups) loaded together: the pair analysis of a heavy set is a chain of dependent
-      // table loads, one latency per round before
-      for (uint32_t p0 = 0; p0 < np; p0 += 128) {
-        uint32_t ga[2], hb[2], hn[2], eo[2], mask[2], sl[2];
-        bool live[2];
-        PairEnt pe[2];
-#pragma unroll
-        for (uint32_t u = 0; u < 2; u++) {
-          const uint32_t p = p0 + 64 * u + lane;
-          ga[u] = hb[u] = hn[u] = eo[u] = sl[u] = 0;
-          mask[u] = kNone;
-          live[u] = false;
-          if (p < np) {
-            ga[u] = (p * inv) >> 24;
-            hb[u] = p - ga[u] * ne;
-            mask[u] = ent_mask[ga[u]];
-            live[u] = ga[u] != hb[u] && mask[u] != kNone;
-          }
-          if (live[u]) {
-            hn[u] = mg_node[hb[u]];
-            eo[u] = ent_off[ga[u]];
-            sl[u] = pair_hash(hn[u]) & mask[u];
-            pe[u] = ix.pent[eo[u] + sl[u]];
-            w_ent += 1;
-          }
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 2; u++) {
-          bool hit = false, stop = !live[u];
-          uint32_t e_off = 0, e_cnt = 0;
-          if (!stop) {
-            if (pe[u].h == hn[u]) {
-              hit = true;
-              e_off = pe[u].off;
-              e_cnt = pe[u].cnt;
-              stop = true;
-            } else if (pe[u].h == kNone) {
-              stop = true;
-            }
-          }
-          // past the home slot: rounds of four
-          for (uint32_t probes = 1; !stop && probes <= mask[u]; probes += 4) {
-            const uint32_t s0 = (sl[u] + probes) & mask[u];
-            PairEnt q[4];
-#pragma unroll
-            for (uint32_t v = 0; v < 4; v++) q[v] = ix.pent[eo[u] + ((s0 + v) & mask[u])];
-            w_ent += 4;
-#pragma unroll
-            for (uint32_t v = 0; v < 4; v++) {
-              if (stop) continue;
-              if (q[v].h == hn[u]) {
-                hit = true;
-                e_off = q[v].off;
-                e_cnt = q[v].cnt;
-                stop = true;
-              } else if (q[v].h == kNone) {
-                stop = true;
-              }
-            }
-          }
-          if (p0 + 64 * u < np) stage(hit, ga[u], hb[u], e_off, e_cnt);  // (wave-uniform)
-        }
       }
     };
     // the visits [R, R + 64) of the staged lists [., j1), jb the list holding visit R, a lane
