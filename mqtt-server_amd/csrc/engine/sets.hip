@@ -39,6 +39,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   constexpr uint32_t kSetBigSlots = kWsWords + kSetBigExtra;
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // entries: merge gathers (+ XS: other shards' nodes)
   constexpr uint32_t kSetBigFill = kSetBigSlots * 3 / 4;
+  // the hash fold's table: key and value words over the same block
+  constexpr uint32_t kSetFoldSlots = (kSetBigSlots / 2) & ~63u;
+  constexpr uint32_t kSetFoldCap = kSetFoldSlots * 3 / 4;
+  static_assert(2 * kSetFoldSlots <= kSetBigSlots && kSetFoldSlots >= kFoldSlots, "the hash fold's table must fit the block");
   struct WaveLds {  // (one block per wave: every array an immediate offset from one base)
     uint32_t ws[kWsWords];
     uint32_t ws_big[XS ? 1 : kSetBigExtra];  // (contiguous with ws: the record-keyed fold's table continues here)
@@ -64,7 +68,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t* const h_off = W.off;
   uint32_t* const h_hb = W.hb;
   uint32_t* const h_pre = W.pre;
-  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 16384u));
+  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 16384u | 32768u));
+  const bool small_fold = (exp_bits & 32768u) != 0;  // (MQ_OPT_SET_EXP bit 15: k_merge's 128-slot fold)
   const DevIndex& ix = a.ix;
   const uint32_t n_front = (uint32_t)a.n_reps[0];
   const uint32_t i_end = n_front + (uint32_t)a.n_reps[1];
@@ -311,12 +316,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // holding it), and each pair slot carries the partner's Qos / NoLocal, so no partner link is
     // read: the record is a non-base entry iff a visit's h comes before g, else the base with the
     // max Qos and OR'd NoLocal over its visits (k_merge's fold_lists / fold_big) ---------------------
-    // small: lists [j0, j1) of whole merge gathers, at most kFoldCap visits, keyed x << 26 | k
+    // small: lists [j0, j1) of whole merge gathers, at most kSetFoldCap visits, keyed x << 26 | k,
+    // keys and values over the wave's whole block (the pair analysis is done with it), the table
+    // sized to the chunk's visits (at most 3/4 full) so its clear and emission scan are too:
+    // fewer, larger chunks, each paying its first pair-slot load's latency once
     auto fold_lists = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
-      uint32_t* __restrict__ f_key = map_key;
-      uint32_t* __restrict__ f_val = map_val;
       const uint32_t v0 = h_pre[j0], v1 = h_pre[j1];
-      for (uint32_t q = lane; q < kFoldSlots; q += 64) {
+      const uint32_t ns = small_fold ? kFoldSlots : min(kSetFoldSlots, ((v1 - v0) * 4 / 3 + 63) & ~63u);
+      uint32_t* __restrict__ f_key = ws;
+      uint32_t* __restrict__ f_val = ws + ns;
+      for (uint32_t q = lane; q < ns; q += 64) {
         f_key[q] = kNone;
         f_val[q] = 0;
       }
@@ -332,11 +341,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (r < v1) {
           const uint32_t xa = h_ga[jj], hb = h_hb[jj];
           const uint32_t key = xa << kSetRowBits | e.k;
-          uint32_t sl = hash32(key) & (kFoldSlots - 1);
+          uint32_t sl = __umulhi(hash32(key), ns);
           for (;;) {
             const uint32_t prev = atomicCAS(&f_key[sl], kNone, key);
             if (prev == kNone || prev == key) break;
-            sl = (sl + 1) & (kFoldSlots - 1);
+            sl = sl + 1 == ns ? 0u : sl + 1;
           }
           const uint32_t pm = e.meta >> kSlotPartShift;  // the partner's Qos | NoLocal << 2
           atomicOr(&f_val[sl], (e.meta & kSlotOwnMask) | (before(hb, xa) ? kFoldNonBase : 0u) |
@@ -345,7 +354,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         w_rec += r < v1;
       }
       wave_sync_lds();
-      for (uint32_t s0 = 0; s0 < kFoldSlots; s0 += 64) {
+      for (uint32_t s0 = 0; s0 < ns; s0 += 64) {
         const uint32_t key = f_key[s0 + lane], v = f_val[s0 + lane];
         const bool occ = key != kNone;
         const uint32_t rmeta = v & kSlotMetaMask;
@@ -448,7 +457,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     auto fold_hits = [&]() __attribute__((always_inline)) {
       if (lane == 0) h_pre[n_hit] = tot;
       wave_sync_lds();
-      const uint32_t fcap = (exp_bits & 256u) ? 16u : kFoldCap;
+      const uint32_t fcap = (exp_bits & 256u) ? 16u : small_fold ? kFoldCap : kSetFoldCap;
       const uint32_t big_max = (exp_bits & 512u) ? 0u : (exp_bits & 16384u) ? kBigFill : kSetBigFill;
       uint32_t j0 = 0;
       while (j0 < n_hit) {  // wave-uniform
