@@ -33,19 +33,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   constexpr uint32_t kWsWords = 2 * kMapSlots + 3 * kPairMax;
   static_assert(kBigSlots <= kWsWords, "the record-keyed fold's table must fit the wave's words");
   // the record-keyed fold's table: the wave's words and kSetBigExtra more (eight workgroups of
-  // four waves still fit a CU's 160 KB of LDS), so gathers of up to kSetBigFill visits fold
-  // instead of resolving through their partner links
-  constexpr uint32_t kSetBigExtra = XS ? 0 : 192;  // (XS: the LDS holds the rank keys instead)
+  // four waves still fit a CU's 160 KB of LDS; XS, with its rank keys, six), so gathers of up to
+  // kSetBigFill visits fold instead of resolving through their partner links
+  constexpr uint32_t kSetBigExtra = 192;
   constexpr uint32_t kSetBigSlots = kWsWords + kSetBigExtra;
   constexpr uint32_t kEnt = XS ? kMapSlots : kPairMax;  // entries: merge gathers (+ XS: other shards' nodes)
   constexpr uint32_t kSetBigFill = kSetBigSlots * 3 / 4;
   // the hash fold's table: key and value words over the same block
   constexpr uint32_t kSetFoldSlots = (kSetBigSlots / 2) & ~63u;
-  constexpr uint32_t kSetFoldCap = kSetFoldSlots * 3 / 4;
+  constexpr uint32_t kSetFoldCap = kSetFoldSlots * 2 / 3;
   static_assert(2 * kSetFoldSlots <= kSetBigSlots && kSetFoldSlots >= kFoldSlots, "the hash fold's table must fit the block");
   struct WaveLds {  // (one block per wave: every array an immediate offset from one base)
     uint32_t ws[kWsWords];
-    uint32_t ws_big[XS ? 1 : kSetBigExtra];  // (contiguous with ws: the record-keyed fold's table continues here)
+    uint32_t ws_big[kSetBigExtra];  // (contiguous with ws: the record-keyed fold's table continues here)
     uint32_t node[kEnt];         // entry x's particle: merge gathers in gather order (= DFS order), then
                                  //   (XS) other shards' nodes as kForeign | fid
     uint64_t rank[XS ? kEnt : 1];  // (XS) entry x's rank key
@@ -68,8 +68,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t* const h_off = W.off;
   uint32_t* const h_hb = W.hb;
   uint32_t* const h_pre = W.pre;
-  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 16384u | 32768u));
+  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 16384u | 32768u | 65536u));
   const bool small_fold = (exp_bits & 32768u) != 0;  // (MQ_OPT_SET_EXP bit 15: k_merge's 128-slot fold)
+  const bool dense_fold = (exp_bits & 65536u) != 0;  // (bit 16: the hash fold up to 3/4 full, not 2/3)
   const DevIndex& ix = a.ix;
   const uint32_t n_front = (uint32_t)a.n_reps[0];
   const uint32_t i_end = n_front + (uint32_t)a.n_reps[1];
@@ -318,11 +319,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // max Qos and OR'd NoLocal over its visits (k_merge's fold_lists / fold_big) ---------------------
     // small: lists [j0, j1) of whole merge gathers, at most kSetFoldCap visits, keyed x << 26 | k,
     // keys and values over the wave's whole block (the pair analysis is done with it), the table
-    // sized to the chunk's visits (at most 3/4 full) so its clear and emission scan are too:
+    // sized to the chunk's visits (at most 2/3 full) so its clear and emission scan are too:
     // fewer, larger chunks, each paying its first pair-slot load's latency once
     auto fold_lists = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
       const uint32_t v0 = h_pre[j0], v1 = h_pre[j1];
-      const uint32_t ns = small_fold ? kFoldSlots : min(kSetFoldSlots, ((v1 - v0) * 4 / 3 + 63) & ~63u);
+      const uint32_t nv = v1 - v0;
+      const uint32_t ns = small_fold ? kFoldSlots : min(kSetFoldSlots, ((dense_fold ? nv * 4 / 3 : nv * 3 / 2) + 63) & ~63u);
       uint32_t* __restrict__ f_key = ws;
       uint32_t* __restrict__ f_val = ws + ns;
       for (uint32_t q = lane; q < ns; q += 64) {
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     auto fold_hits = [&]() __attribute__((always_inline)) {
       if (lane == 0) h_pre[n_hit] = tot;
       wave_sync_lds();
-      const uint32_t fcap = (exp_bits & 256u) ? 16u : small_fold ? kFoldCap : kSetFoldCap;
+      const uint32_t fcap = (exp_bits & 256u) ? 16u : small_fold ? kFoldCap : dense_fold ? kSetFoldSlots * 3 / 4 : kSetFoldCap;
       const uint32_t big_max = (exp_bits & 512u) ? 0u : (exp_bits & 16384u) ? kBigFill : kSetBigFill;
       uint32_t j0 = 0;
       while (j0 < n_hit) {  // wave-uniform
