@@ -42,7 +42,7 @@
                                      k_set's record-keyed fold at k_merge's table size (kBigFill visits, not
                                      its own kSetBigFill); bit 15 (exact) k_set's hash fold at k_merge's
                                      128-slot table (kFoldCap visits per chunk, not its sized table of up to
-                                     kSetFoldCap); bit 16 (exact) that table up to 3/4 full (default: 2/3) */
+                                     kSetFoldCap); bit 16 (exact) that table up to 3/4 full (default: 2/3); bit 17 (exact) up to 3/5 */
 #define MQ_OPT_PATCH_CODES 20     /* host span results: 1 (default) 4-byte patch codes when the index allows them
                                      (MQ_SPANS_PATCH_CODES); 0: 8-byte mq_patch records */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than

@@ -68,9 +68,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t* const h_off = W.off;
   uint32_t* const h_hb = W.hb;
   uint32_t* const h_pre = W.pre;
-  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 16384u | 32768u | 65536u));
+  const uint32_t exp_bits = kDevBuild ? a.exp : (a.exp & (256u | 512u | 1024u | 2048u | 16384u | 32768u | 65536u | 131072u));
   const bool small_fold = (exp_bits & 32768u) != 0;  // (MQ_OPT_SET_EXP bit 15: k_merge's 128-slot fold)
   const bool dense_fold = (exp_bits & 65536u) != 0;  // (bit 16: the hash fold up to 3/4 full, not 2/3)
+  const bool sparse_fold = (exp_bits & 131072u) != 0;  // (bit 17: up to 3/5 full)
   const DevIndex& ix = a.ix;
   const uint32_t n_front = (uint32_t)a.n_reps[0];
   const uint32_t i_end = n_front + (uint32_t)a.n_reps[1];
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     auto fold_lists = [&](uint32_t j0, uint32_t j1) __attribute__((always_inline)) {
       const uint32_t v0 = h_pre[j0], v1 = h_pre[j1];
       const uint32_t nv = v1 - v0;
-      const uint32_t ns = small_fold ? kFoldSlots : min(kSetFoldSlots, ((dense_fold ? nv * 4 / 3 : nv * 3 / 2) + 63) & ~63u);
+      const uint32_t ns = small_fold ? kFoldSlots : min(kSetFoldSlots, ((dense_fold ? nv * 4 / 3 : sparse_fold ? nv * 5 / 3 : nv * 3 / 2) + 63) & ~63u);
       uint32_t* __restrict__ f_key = ws;
       uint32_t* __restrict__ f_val = ws + ns;
       for (uint32_t q = lane; q < ns; q += 64) {
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     auto fold_hits = [&]() __attribute__((always_inline)) {
       if (lane == 0) h_pre[n_hit] = tot;
       wave_sync_lds();
-      const uint32_t fcap = (exp_bits & 256u) ? 16u : small_fold ? kFoldCap : dense_fold ? kSetFoldSlots * 3 / 4 : kSetFoldCap;
+      const uint32_t fcap = (exp_bits & 256u) ? 16u : small_fold ? kFoldCap : dense_fold ? kSetFoldSlots * 3 / 4 : sparse_fold ? kSetFoldSlots * 3 / 5 : kSetFoldCap;
       const uint32_t big_max = (exp_bits & 512u) ? 0u : (exp_bits & 16384u) ? kBigFill : kSetBigFill;
       uint32_t j0 = 0;
       while (j0 < n_hit) {  // wave-uniform
