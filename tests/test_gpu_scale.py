@@ -146,6 +146,47 @@ def test_iot_5m_subscriptions(gpu_available):
 
 
 @pytest.mark.timeout(900)
+def test_iot_5m_half_load_edge_table(gpu_available):
+    """Config 4's probe regime at a tenth of its size: the 50M IoT index is held at an edge table
+    of 2^30 slots at most half full (mqmatch.h MQ_OPT_EDGE_LOAD), where probe chains are longest;
+    here the 5M IoT index is forced to the same bound (MQ_OPT_EDGE_LOAD 2). The timed path —
+    one-sync mq_match_spans_device over a 256k-topic batch: the walk trials, then each walk
+    forced — and host spans, the first 20k topics digest-equal to the oracle (topics.go:593-648)."""
+    import torch
+    from mqmatch import engine as E
+    from mqmatch import workload as W
+    ns = 20000
+    w = W.gen_subscriptions(5_000_000, 5_000_000, seed=W.BASE_SEED + 40, mix=W.MIX_IOT)
+    eng = E.Engine(expected_subs=5_000_000)
+    eng.set_option(E.OPT_EDGE_LOAD, 2)
+    new = eng.subscribe_bulk(w)
+    st = eng.stats()
+    assert st["edge_load"] == 2 and st["edges"] * 4 >= st["edge_capacity"], st  # 1/4 .. 1/2 full
+    tb, to = W.gen_topics(w, 1 << 18, seed=W.BASE_SEED + 41, mix=W.MIX_IOT)
+    orc = O.OracleIndex()
+    assert (orc.subscribe_bulk(w) == new).all()
+    od, ocnt, _ = orc.digest_batch(tb, to[:ns + 1], nthreads=THREADS)
+    orc.close()
+    del orc
+    dg, cnt = engine_digests(eng.match_batch_spans(tb, to[:ns + 1]))
+    _check(dg, cnt, od, ocnt, "host spans")
+    n = len(to) - 1
+    d_tb = torch.from_numpy(tb).cuda()
+    d_to = torch.from_numpy(to.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    runs = [(f"trial {k + 1}", None) for k in range(6)] + [("chosen walk", None),
+            ("frontier walk + fused desc", 16), ("walk thread per topic", 0)]
+    for what, group in runs:
+        if group is not None:
+            eng.set_option(E.OPT_WALK_GROUP, group)
+        r = eng.match_spans_device(d_tb.data_ptr(), d_to.data_ptr(), n, None)
+        dg, cnt = engine_digests(E.expand_device_spans(r, n, ns))
+        _check(dg, cnt, od, ocnt, f"device spans, {what}")
+    del d_tb, d_to
+    eng.close()
+
+
+@pytest.mark.timeout(900)
 def test_messages_10m_retained_100k_filters(gpu_available):
     """Config 5 at a tenth of its size (bench_messages.py's default workload and seeds): 10M
     retained topics (1k $SYS) x 100k wildcard filters through mq_messages_device, every filter's
