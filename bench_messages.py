@@ -1,8 +1,11 @@
 """Secondary benchmark: the retained-message reverse match (Messages, topics.go:525-579) —
 BASELINE.json config 5 ("100M retained topics x 100k wildcard subscribe filters"), scaled by
 --retained (default 10M retained topics, 10 % of config 5; the 100M-topic host image does not
-fit the build container). A step is mq_messages_device over a batch of --filters filters already
-in HBM (k_msg count pass, scan, k_msg fill pass writing every retained handle).
+fit the build container). A step is one Messages batch of --filters filters already in HBM:
+--format runs (the default, round 6): mq_messages_runs_device — the walk over the level-order
+retained image (k_msgq count pass, scan, place pass) leaves each filter's result as runs of the
+image's handle array, as SURVEY.md §7 step 8 plans ("expanded at the boundary"); --format
+handles: mq_messages_device, the same walk plus k_msg_copy writing every handle.
 
 Prints one JSON line like bench.py's: throughput, output handles per filter, the k_msg roofline
 (algorithmic bytes B = 8·L + 4 + 16·P + 16·O per filter, SURVEY.md §8d, from the oracle's exact
@@ -39,13 +42,14 @@ def log(msg):
     print(f"[bench_messages {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def read_msg_traffic(n_retained, n_filters):
+def read_msg_traffic(n_retained, n_filters, fmt="handles"):
     """HBM bytes per Messages step (k_msgq passes + k_msg_copy: FETCH_SIZE x1 for the walks' random
     loads, x2 for k_msg_copy's streams, + WRITE_SIZE) from a committed rocprofv3 PMC summary of the
-    same configuration (retained topics, filters per step, export threshold), if present."""
+    same configuration (retained topics, filters per step, export threshold, output format), if
+    present."""
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
-            e = json.load(f).get("messages", {}).get(str(n_retained))
+            e = json.load(f).get("messages" if fmt == "handles" else "messages_runs", {}).get(str(n_retained))
         if e is None or int(e["filters"]) != n_filters or int(e.get("export", 1)) != 1:
             return None
         return float(e["hbm_bytes_per_step"])
@@ -166,6 +170,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--format", choices=["runs", "handles"], default="runs",
+                    help="runs: mq_messages_runs_device (each filter's result as runs of the image's handles); "
+                         "handles: mq_messages_device (every handle copied out)")
     ap.add_argument("--walk", action="store_true",
                     help="Messages by the particle walk (MQ_OPT_MSG_IMAGE 0) instead of the level-order image")
     ap.add_argument("--no-img-edges", action="store_true",
@@ -216,7 +223,11 @@ def main():
     eng.sync(stream.cuda_stream)
     torch.cuda.synchronize()
 
+    runs = args.format == "runs"
+
     def step():
+        if runs:
+            return eng.messages_runs_device(d_fb.data_ptr(), d_fo.data_ptr(), n, stream.cuda_stream)
         return eng.messages_device(d_fb.data_ptr(), d_fo.data_ptr(), n, stream.cuda_stream)
 
     eng.profile(True)  # the first step builds the level-order image: timed apart
@@ -232,7 +243,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     prof = eng.profile_read()
     eng.profile(False)
-    handles = int(r.n_handles)
+    handles = int(r.n_expanded) if runs else int(r.n_handles)
     out = {
         "metric": "Messages filters/sec (retained reverse match)", "value": n * args.steps / elapsed,
         "unit": "filters/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -240,9 +251,10 @@ def main():
         "data": "synthetic (SURVEY.md §8d generator, retained seed +3)",
         "config": {"workload": f"config 5 scaled: {len(ro) - 1} retained topics ({args.sys} $SYS), "
                                f"{n} wildcard filters per step", "retained": len(ro) - 1, "filters": n},
-        "handles_per_step": handles, "handles_per_filter": handles / max(1, n),
+        "format": args.format, "handles_per_step": handles, "handles_per_filter": handles / max(1, n),
+        "runs_per_step": int(r.n_runs_total) if runs else None,
         "kernels_ms_per_step": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
-        "path": "particle walk (k_msg)" if args.walk else ("level-order image (k_msgq + k_msg_copy), literal lookups "
+        "path": "particle walk (k_msg)" if args.walk else ("level-order image (k_msgq" + (", runs out" if runs else " + k_msg_copy") + "), literal lookups "
                                                           + ("through the index's edge table" if args.no_img_edges
                                                              else "in the image's edge table")),
         "image_build_ms": build[1] if build else None,
@@ -261,14 +273,38 @@ def main():
         ns = o["sample_filters"]
         dg = np.array([int(x, 16) for x in o["digests"]], np.uint64)
         cnt = np.array(o["counts"], np.uint32)
-        base, count, hs = eng.messages_batch(fb, fo[:ns + 1])
-        out["parity_sample"] = {"filters": ns, "counts_equal": bool((count == cnt).all()),
-                                "digests_equal": bool((handle_digests(base, count, hs) == dg).all())}
-        del base, count, hs
         if "all_digests" in o:
             t0 = time.time()
-            out["parity_all"] = full_parity(eng, fb, fo, o)
+            if runs:  # the timed batch's own device result, every filter
+                sys.path.insert(0, os.path.join(REPO, "oracle"))
+                import oracle as O
+                dres = E.device_messages_runs(r, n)
+                want = np.array([int(x, 16) for x in o["all_digests"]], np.uint64)
+                wcnt = np.array(o["all_counts"], np.uint64)
+                bad_c = int((dres["count"].astype(np.uint64) != wcnt).sum())
+                bad_d = int((O.run_digests(dres, nthreads=16) != want).sum())
+                out["parity_all"] = {"filters": n, "result": "the last timed step's device runs (mq_messages_runs_device)",
+                                     "counts_differ": bad_c, "digests_differ": bad_d,
+                                     "digests_equal": bad_c == 0 and bad_d == 0,
+                                     "against": o.get("all_note", "fast restatement")}
+                del dres
+            else:
+                out["parity_all"] = full_parity(eng, fb, fo, o)
             log(f"parity over all {n} filters in {time.time() - t0:.1f}s: {out['parity_all']}")
+        # (after parity_all, which reads the timed step's device result: this batch overwrites it)
+        if runs:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle as O
+            res = eng.messages_runs_batch(fb, fo[:ns + 1])
+            out["parity_sample"] = {"filters": ns, "counts_equal": bool((res["count"] == cnt).all()),
+                                    "digests_equal": bool((O.run_digests(res) == dg).all()),
+                                    "result": "mq_messages_runs_batch (host runs)"}
+            del res
+        else:
+            base, count, hs = eng.messages_batch(fb, fo[:ns + 1])
+            out["parity_sample"] = {"filters": ns, "counts_equal": bool((count == cnt).all()),
+                                    "digests_equal": bool((handle_digests(base, count, hs) == dg).all())}
+            del base, count, hs
         per = o["per_filter"]
         b = 8 * per["L"] + 4 + 16 * per["P"] + 16 * per["O"]
         out["alg_bytes_per_filter"] = {"B": b, **per, "sample_filters": ns}
@@ -278,16 +314,19 @@ def main():
             # emitted handle read once from the image and written once to the output. SURVEY
             # §8d's B also prices the reference walk's child enumerations (16·P), which the image
             # path does not perform: that rate is reported beside it (it can exceed HBM peak).
-            handles_per_filter = r.n_handles / max(1, n)
-            b_img = 8 * per["L"] + 4 + 16 * handles_per_filter
+            if runs:  # a run record (16 B) and each filter's run base, run count, base, count (24 B)
+                b_img = 8 * per["L"] + 4 + 24 + 16 * int(r.n_runs_total) / max(1, n)
+                bytes_note = "8 B per level + 4 B offset + 24 B of counts per filter, 16 B per run written"
+            else:
+                b_img = 8 * per["L"] + 4 + 16 * int(r.n_handles) / max(1, n)
+                bytes_note = "8 B per level + 4 B offset per filter, 16 B per emitted handle (read + write)"
             ach = b_img * n / (kms * 1e-3) / 1e9
-            traffic = read_msg_traffic(args.retained, n) if not args.walk else None  # (keyed by --retained)
+            traffic = read_msg_traffic(args.retained, n, args.format) if not args.walk else None  # (keyed by --retained)
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                               "kernel": ("k_msgq (count, wide count, place, wide place) + k_msg_copy" if not args.walk
-                                          else "k_msg (count + fill)"),
-                               "bytes": "8 B per level + 4 B offset per filter, 16 B per emitted handle (read + write)",
-                               "bytes_per_step": b_img * n, "ms_per_step": kms}
+                               "kernel": ("k_msgq (count, wide count, place, wide place)" + ("" if runs else " + k_msg_copy")
+                                          if not args.walk else "k_msg (count + fill)"),
+                               "bytes": bytes_note, "bytes_per_step": b_img * n, "ms_per_step": kms}
             if traffic:  # the measured HBM bytes (calibrated PMC, profiles/pmc_traffic.json) over the same time
                 out["roofline"]["hbm_traffic_GBps"] = traffic / (kms * 1e-3) / 1e9
                 out["roofline"]["hbm_traffic_frac"] = out["roofline"]["hbm_traffic_GBps"] / HBM_PEAK_GBS

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 8
+#define MQ_ABI_VERSION 9
 
 /* error codes (negative errno) */
 #define MQ_EINVAL (-22)
@@ -461,6 +461,50 @@ int mq_messages_batch(mq_index* idx, const uint8_t* filter_bytes, const uint64_t
                       uint32_t n, mq_msg_result** out);
 int mq_messages_device(mq_index* idx, const uint8_t* d_filter_bytes, const uint64_t* d_offsets,
                        uint32_t n, void* hip_stream, mq_msg_result* out);
+
+/* Messages as runs (round 6; SURVEY.md §7 step 8: `x/#` and `+` results kept as contiguous
+ * intervals, expanded at the boundary). The walk over the level-order retained image finds each
+ * filter's handles as runs of consecutive entries of one array — every particle's children are
+ * one image range, so a final '+' is one run per run of parents and a final '#' one run per level
+ * (topics.go:547-566) — and the result names those runs instead of copying the handles: filter i
+ * has runs[run_base[i], + n_runs[i]), run r is handles[r.first, + r.count), and r.at is where the
+ * run starts in the batch's expanded output (filter i's handles are [base[i], + count[i]) of it:
+ * the same layout as mq_msg_result). `handles` is the retained image's handle array (level order),
+ * or, for a batch that took the particle walk (the Q6 "" entry live, nesting beyond 16 fan-outs),
+ * the batch's own handles with one run per filter. Handle order within a filter is unspecified, as
+ * in mq_msg_result. */
+typedef struct mq_msg_run {
+  uint32_t first; /* index of the run's first handle in the result's handles */
+  uint32_t count; /* handles in the run */
+  uint64_t at;    /* where the run starts in the batch's expanded output */
+} mq_msg_run;
+
+typedef struct mq_msg_runs_result {
+  uint32_t n_filters;
+  uint32_t reserved;
+  const uint64_t* run_base; /* n_filters: each filter's first run */
+  const uint32_t* n_runs;   /* n_filters */
+  const uint64_t* base;     /* n_filters: each filter's first handle in the expanded output */
+  const uint32_t* count;    /* n_filters: each filter's handles */
+  const mq_msg_run* runs;
+  uint64_t n_runs_total;
+  const uint64_t* handles;  /* the array the runs index */
+  uint64_t n_handles;       /* its length */
+  uint64_t n_expanded;      /* handles of the whole batch (sum of count) */
+} mq_msg_runs_result;
+
+/* Device result: every pointer is device memory owned by the index, valid until its next
+ * Messages call (the image array until the retained set changes and a Messages call rebuilds it). */
+int mq_messages_runs_device(mq_index* idx, const uint8_t* d_filter_bytes, const uint64_t* d_offsets,
+                            uint32_t n, void* hip_stream, mq_msg_runs_result* out);
+/* Host result (mq_result_free): the runs copied to host memory, `handles` a host copy of the image
+ * shared by the results of one image version (copied once per version). */
+int mq_messages_runs_batch(mq_index* idx, const uint8_t* filter_bytes, const uint64_t* offsets,
+                           uint32_t n, mq_msg_runs_result** out);
+/* Expand filters [first, first + count) of a host runs result into out (cap handles), in filter
+ * order (filter i's handles at out[base[i] - base[first] ...]); *n_out: handles written. */
+int mq_msg_runs_expand(const mq_msg_runs_result* r, uint32_t first, uint32_t count, uint64_t* out,
+                       uint64_t cap, uint64_t* n_out);
 
 /* Batched auth.MatchTopic (hooks/auth/ledger.go:90-118): the ACL ledger's
  * filter/topic test that the fan-out runs per recipient (server.go:1029 -> Ledger.ACLOk ->

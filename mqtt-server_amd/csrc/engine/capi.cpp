@@ -26,22 +26,24 @@
 
 using namespace mq;
 
-// The handle's lock (the reference's root lock, topics.go:402): `mu` serialises the handle's work
-// (updates, and the GPU round trip of a match). It prefers updates, as Go's sync.RWMutex prefers
-// writers: an update announces itself (`views.writers`) before it takes `mu`, and a call that is
-// not an update waits while one is announced, so readers matching back to back cannot starve
-// updates. Host span results point into the host image's subscription pools until
-// mq_result_free; `views` records them by generation, and the index copies a slab before it
-// changes one that a live result may see and keeps what it frees until no live result can see it
-// (Index::begin_op), so an update never waits for results — only for the match in flight, if any.
-// The one exception is a bulk subscribe (mq_subscribe_bulk), which rewrites the pools in place:
-// it also announces itself as a drain (`views.drains`) and waits, without holding `mu`, for the
-// live results to be freed; a call that would publish a new result waits while a drain is
-// announced. `views` has its own mutex, never held across GPU work, so freeing a result never
-// waits for a match in flight. Results hold a reference, so freeing one after mq_index_destroy is
-// safe.
+// The handle's locks (the reference's root lock, topics.go:402). `mu` guards the host image: updates
+// take it, and a match takes it only while it syncs the device image and snapshots what its
+// batch reads (Device::prepare) — the match's GPU work then runs without it, so an update never
+// waits for a running match (round 6; before, every update queued behind the match in flight,
+// which a stalled match made ~15 ms). `dev_mu` serialises the work on the handle's device
+// (matches, Messages, syncs, checks) and is always taken before `mu`; updates never take it. `mu`
+// prefers updates, as Go's sync.RWMutex prefers writers: an update announces itself
+// (`views.writers`) before it takes `mu`, and a call that is not an update waits while one is
+// announced. Host span results point into the host image's subscription pools until
+// mq_result_free; `views` records them by generation — a match reserves its generation while it
+// holds `mu`, before its kernels run — and the index copies a slab before it changes one that a
+// live result may see and keeps what it frees until no live result can see it
+// (Index::begin_op), so an update never waits for results either. `views` has its own mutex,
+// never held across GPU work, so freeing a result never waits for a match in flight. Results
+// hold a reference, so freeing one after mq_index_destroy is safe.
 struct IndexLock {
-  FifoMutex mu;  // (in arrival order: fifo_mutex.h)
+  FifoMutex dev_mu;  // the device's work (taken before mu)
+  FifoMutex mu;      // the host image (in arrival order: fifo_mutex.h)
   ViewTracker views;
   Device* dev = nullptr;  // the index's device, while it lives (pipelined results flush through it)
 };
@@ -89,12 +91,16 @@ struct MsgHolder {
   PinnedVec<uint32_t> count;
   PinnedVec<uint64_t> handles;
 };
+struct MsgRunsHolder {
+  mq_msg_runs_result pub;
+  HostMsgRuns data;
+};
 struct AclHolder {
   mq_acl_result pub;
   HostAcl data;
 };
 std::mutex g_res_mu;
-std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages, 3 = acl, 4 = spans
+std::unordered_map<void*, int> g_results;  // 1 = match, 2 = messages, 3 = acl, 4 = spans, 5 = message runs
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -102,28 +108,56 @@ int fail(int code, const std::string& msg) {
 }
 
 // What a guarded call does to the host image (IndexLock).
-// kUpdate: copy-on-write against the live results, never waits for them (a bulk subscribe too: it
-// takes the per-entry path while a result is live); kPin: publishes a host span result.
-enum class Access { kRead, kUpdate, kPin };
+// kUpdate: takes only `mu`; copy-on-write against the live results, never waits for them (a bulk
+// subscribe too: it takes the per-entry path while a result is live). kRead: the device's work
+// and the host image, for the whole call. Matches: guarded_match.
+enum class Access { kRead, kUpdate };
 
 // The calling thread's HIP runtime state for device dev, set up once per thread: a thread's first
 // HIP calls cost ~10 ms, which a match must not pay while it holds the handle
-// lock that updates wait for. (The Go batching stage also keeps its loop on one OS thread.)
+// lock that updates wait for. (The Go batching stage also keeps its loop on one OS thread.) A
+// thread that serves indexes on several devices keeps one bit per device; the warm-up's event is
+// recorded on a non-blocking stream of the thread's own, not on the null stream (which would
+// wait behind every blocking stream of the device).
 void thread_warm(int dev) {
-  static thread_local int warmed = -1;
-  if (warmed == dev) return;
+  static thread_local uint64_t warmed[4] = {0, 0, 0, 0};
+  if (dev < 0 || dev >= 256) return;
+  if (warmed[dev / 64] >> (dev % 64) & 1) return;
   if (hipSetDevice(dev) != hipSuccess) {
     (void)hipGetLastError();
     return;
   }
+  hipStream_t st = nullptr;
   hipEvent_t e = nullptr;
-  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
-    (void)hipEventRecord(e, nullptr);
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+      hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+    (void)hipEventRecord(e, st);
     (void)hipEventSynchronize(e);
-    (void)hipEventDestroy(e);
   }
+  if (e) (void)hipEventDestroy(e);
+  if (st) (void)hipStreamDestroy(st);
   (void)hipGetLastError();
-  warmed = dev;
+  warmed[dev / 64] |= 1ull << (dev % 64);
+}
+
+// C++ and HIP failures as negative errno codes with the thread's message.
+template <class F>
+int caught(F&& f) {
+  try {
+    return f();
+  } catch (const HipError& e) {
+    return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
+  } catch (const std::bad_alloc&) {
+    return fail(MQ_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(MQ_EIO, e.what());
+  }
+}
+
+// A call that is not an update waits while one is announced (updates are preferred).
+void wait_for_writers(ViewTracker& V) {
+  std::unique_lock<std::mutex> g(V.mu);
+  V.cv.wait(g, [&] { return V.writers == 0; });
 }
 
 // Runs f under the handle's lock (IndexLock).
@@ -144,7 +178,8 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
       V->cv.notify_all();
     }
   } ann;
-  try {
+  return caught([&] {
+    std::unique_lock<FifoMutex> dlk(L.dev_mu, std::defer_lock);
     if (access == Access::kUpdate) {
       {
         std::lock_guard<std::mutex> g(V.mu);
@@ -152,8 +187,8 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
       }
       ann.V = &V;
     } else {
-      std::unique_lock<std::mutex> g(V.mu);
-      V.cv.wait(g, [&] { return V.writers == 0; });
+      dlk.lock();
+      wait_for_writers(V);
     }
     std::lock_guard<FifoMutex> lk(L.mu);
     if (!slow_on()) return f();
@@ -161,14 +196,54 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
     const int r = f();
     slow_report(access == Access::kUpdate ? "update" : "read", 0.0);
     return r;
-  } catch (const HipError& e) {
-    return fail(e.code == hipErrorNoDevice || e.code == hipErrorInvalidDevice ? MQ_ENODEV : MQ_EIO, e.where);
-  } catch (const std::bad_alloc&) {
-    return fail(MQ_ENOMEM, "out of host memory");
-  } catch (const std::exception& e) {
-    return fail(MQ_EIO, e.what());
-  }
+  });
 }
+
+// A match in two phases (IndexLock): prep() under both locks — it syncs the device image and
+// takes the batch's snapshot (Device::prepare), and for host results reserves their generation —
+// then run() with the device's lock only, while updates change the host image.
+template <class P, class R>
+int guarded_match(mq_index* idx, P&& prep, R&& run) {
+  if (!idx) return fail(MQ_EINVAL, "null index");
+  if (idx->dev_ready.load(std::memory_order_acquire)) thread_warm(idx->cfg.device);
+  IndexLock& L = *idx->lk;
+  return caught([&] {
+    std::lock_guard<FifoMutex> dlk(L.dev_mu);
+    wait_for_writers(L.views);
+    if (slow_on()) slow_begin();
+    {
+      std::lock_guard<FifoMutex> lk(L.mu);
+      prep();
+      if (slow_on()) slow_report("match-prepare", 0.0);
+    }
+    slow_mark("unlocked");
+    const int r = run();
+    if (slow_on()) slow_report("match", 0.0);
+    return r;
+  });
+}
+
+// The host pools a host span result names, with its generation (reserved under `mu`, by the
+// match's prepare phase). A result that is not published gives its generation back.
+struct PoolView {
+  const mq_client_row* sub = nullptr;
+  const mq_shared_row* shr = nullptr;
+  uint64_t sub_len = 0, shr_len = 0;
+  ViewTracker* views = nullptr;
+  uint64_t gen = 0;
+  bool published = false;
+  void reserve(mq_index* idx) {  // under mu
+    sub = reinterpret_cast<const mq_client_row*>(idx->ix->subs.m.h.data());
+    shr = reinterpret_cast<const mq_shared_row*>(idx->ix->shr.m.h.data());
+    sub_len = idx->ix->subs.m.size();
+    shr_len = idx->ix->shr.m.size();
+    views = &idx->lk->views;
+    gen = views->publish();
+  }
+  ~PoolView() {
+    if (views && !published) views->release(gen);
+  }
+};
 
 bool bad_str(const void* p, uint32_t len) { return p == nullptr && len != 0; }
 
@@ -219,6 +294,7 @@ int mq_index_create(const mq_config* cfg, mq_index** out) {
 void mq_index_destroy(mq_index* idx) {
   if (!idx) return;
   {
+    std::lock_guard<FifoMutex> dg(idx->lk->dev_mu);
     std::lock_guard<FifoMutex> g(idx->lk->mu);
     idx->lk->dev = nullptr;  // (tickets still held flush through it no more; ~Device issues their copies)
   }
@@ -347,9 +423,10 @@ int mq_match_batch(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
 
 namespace {
 // A host span result: the device arrays copied into h->data, the pools pointing at the host
-// image (copy-on-write keeps what the result sees until mq_result_free). Under the handle lock.
-int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_span_result& dev_out,
-                       mq_span_result** out) {
+// image as the match's prepare phase saw it (copy-on-write keeps what the result sees until
+// mq_result_free).
+int publish_host_spans(std::shared_ptr<IndexLock> lk, std::unique_ptr<SpanHolder> h, const mq_span_result& dev_out,
+                       PoolView& pv, mq_span_result** out) {
   mq_span_result& r = h->pub;
   r = dev_out;  // counts and flags; pointers replaced by the host copies and host pools
   r.topics = reinterpret_cast<const mq_topic_spans*>(h->data.topics.data());
@@ -374,14 +451,15 @@ int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_sp
   r.merge_rows = sets ? h->data.merge_rows.data() : nullptr;
   r.n_merge_rows = sets ? h->data.merge_rows.size() : 0;
   r.merge_row_base = sets ? h->data.merge_base.data() : nullptr;
-  r.sub_pool = reinterpret_cast<const mq_client_row*>(idx->ix->subs.m.h.data());
-  r.shared_pool = reinterpret_cast<const mq_shared_row*>(idx->ix->shr.m.h.data());
-  r.sub_pool_len = idx->ix->subs.m.size();
-  r.shared_pool_len = idx->ix->shr.m.size();
-  h->lk = idx->lk;
-  h->gen = idx->lk->views.publish();
+  r.sub_pool = pv.sub;
+  r.shared_pool = pv.shr;
+  r.sub_pool_len = pv.sub_len;
+  r.shared_pool_len = pv.shr_len;
+  h->lk = std::move(lk);
+  h->gen = pv.gen;
+  pv.published = true;
   *out = &h->pub;
-  std::lock_guard<std::mutex> lk(g_res_mu);
+  std::lock_guard<std::mutex> g(g_res_mu);
   g_results[&h->pub] = 4;
   h.release();
   return 0;
@@ -390,17 +468,23 @@ int publish_host_spans(mq_index* idx, std::unique_ptr<SpanHolder> h, const mq_sp
 
 int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_span_result** out) {
   if (!out || (n && (!to || (!tb && to[n] != 0)))) return fail(MQ_EINVAL, "null argument");
-  return guarded(idx, [&] {
-    Device& d = idx->device();
+  Device* d = nullptr;
+  hipStream_t hs = nullptr;
+  PoolView pv;
+  return guarded_match(idx, [&] {
+    d = &idx->device();
+    hs = d->host_stream();
+    d->prepare(*idx->ix, hs);
+    pv.reserve(idx);
+  }, [&] {
     std::unique_ptr<SpanHolder> h(new SpanHolder());
     const uint8_t* dtb = nullptr;
     const uint64_t* dto = nullptr;
-    hipStream_t hs = d.host_stream();
-    if (n) d.stage_inputs(tb, to, n, hs, &dtb, &dto);
+    if (n) d->stage_inputs(tb, to, n, hs, &dtb, &dto);
     mq_span_result dev_out;
-    d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out);
-    return publish_host_spans(idx, std::move(h), dev_out, out);
-  }, Access::kPin);
+    d->match_spans(dtb, dto, n, hs, &h->data, &dev_out);
+    return publish_host_spans(idx->lk, std::move(h), dev_out, pv, out);
+  });
 }
 
 // A submitted batch: its result, published (its arrays being filled by the copy stream), and the
@@ -415,8 +499,15 @@ struct mq_spans_ticket {
 int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_t n, mq_spans_ticket** out) {
   if (!out || (n && (!to || (!tb && to[n] != 0)))) return fail(MQ_EINVAL, "null argument");
   *out = nullptr;
-  return guarded(idx, [&] {
-    Device& d = idx->device();
+  Device* d = nullptr;
+  hipStream_t hs = nullptr;
+  PoolView pv;
+  return guarded_match(idx, [&] {
+    d = &idx->device();
+    hs = d->host_stream();
+    d->prepare(*idx->ix, hs);
+    pv.reserve(idx);
+  }, [&] {
     std::unique_ptr<mq_spans_ticket> tk(new mq_spans_ticket());
     hip_check(hipEventCreateWithFlags(&tk->ready, hipEventDisableTiming), "hipEventCreate");
     struct EvGuard {  // the event goes if the submit fails
@@ -428,12 +519,11 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
     std::unique_ptr<SpanHolder> h(new SpanHolder());
     const uint8_t* dtb = nullptr;
     const uint64_t* dto = nullptr;
-    hipStream_t hs = d.host_stream();
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    if (n) d.stage_inputs(tb, to, n, hs, &dtb, &dto);  // (ahead of the last batch's copy: below)
+    if (n) d->stage_inputs(tb, to, n, hs, &dtb, &dto);  // (ahead of the last batch's copy: below)
     const auto t1 = clk::now();
-    d.flush_host_copy();
+    d->flush_host_copy();
     const auto t2 = clk::now();
     mq_span_result dev_out;
     struct Disarm {  // a result that is not published takes its armed copy with it
@@ -442,30 +532,30 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
       ~Disarm() {
         if (d) d->drop_pending_copy(f);
       }
-    } da{&d, &tk->issued};
-    d.match_spans(*idx->ix, dtb, dto, n, hs, &h->data, &dev_out, tk->ready, &tk->issued);
+    } da{d, &tk->issued};
+    d->match_spans(dtb, dto, n, hs, &h->data, &dev_out, tk->ready, &tk->issued);
     const auto t3 = clk::now();
     tk->lk = idx->lk;
-    const int rc = publish_host_spans(idx, std::move(h), dev_out, &tk->res);
+    const int rc = publish_host_spans(idx->lk, std::move(h), dev_out, pv, &tk->res);
     static const bool trace = std::getenv("MQ_TRACE_SUBMIT") != nullptr;
     if (trace) {
       auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
       std::fprintf(stderr, "mq_match_spans_submit: upload %.3f flush %.3f match %.3f (runs %d, sync wait %.3f) publish %.3f ms\n",
-                   ms(t0, t1), ms(t1, t2), ms(t2, t3), d.trace_runs, d.trace_sync_ms, ms(t3, clk::now()));
+                   ms(t0, t1), ms(t1, t2), ms(t2, t3), d->trace_runs, d->trace_sync_ms, ms(t3, clk::now()));
     }
     if (rc) return rc;
     da.d = nullptr;
     eg.t = nullptr;
     *out = tk.release();
     return 0;
-  }, Access::kPin);
+  });
 }
 
 int mq_match_spans_wait(mq_spans_ticket* t, mq_span_result** out) {
   if (!t || !out) return fail(MQ_EINVAL, "null argument");
   *out = nullptr;
   if (t->lk) {  // the copy may still be pending (queued behind a next batch's upload)
-    std::lock_guard<FifoMutex> g(t->lk->mu);
+    std::lock_guard<FifoMutex> g(t->lk->dev_mu);
     try {
       if (t->lk->dev) t->lk->dev->flush_host_copy();
     } catch (const HipError& he) {
@@ -496,18 +586,26 @@ int mq_match_spans_wait(mq_spans_ticket* t, mq_span_result** out) {
 int mq_match_spans_end_host(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, mq_span_result** out) {
   if (!out || (n_foreign && !foreign)) return fail(MQ_EINVAL, "null argument");
   return guarded(idx, [&] {
+    Device& d = idx->device();
+    if (d.batch_stale(*idx->ix)) throw HipError{hipErrorInvalidValue, "index updated between spans_begin and spans_end"};
     std::unique_ptr<SpanHolder> h(new SpanHolder());
     mq_span_result dev_out;
-    idx->device().spans_end(*idx->ix, foreign, n_foreign, nullptr, &h->data, &dev_out);
-    return publish_host_spans(idx, std::move(h), dev_out, out);
-  }, Access::kPin);
+    d.spans_end(foreign, n_foreign, nullptr, &h->data, &dev_out);
+    PoolView pv;
+    pv.reserve(idx);
+    return publish_host_spans(idx->lk, std::move(h), dev_out, pv, out);
+  });
 }
 
 int mq_match_spans_device(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, void* stream,
                           mq_span_result* out) {
   if (!out || (n && !d_to)) return fail(MQ_EINVAL, "null argument");
-  return guarded(idx, [&] {
-    idx->device().match_spans(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, nullptr, out);
+  Device* d = nullptr;
+  return guarded_match(idx, [&] {
+    d = &idx->device();
+    d->prepare(*idx->ix, (hipStream_t)stream);
+  }, [&] {
+    d->match_spans(d_tb, d_to, n, (hipStream_t)stream, nullptr, out);
     return 0;
   });
 }
@@ -516,7 +614,9 @@ int mq_match_spans_begin(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_t
                          mq_xlist* exported) {
   if (!exported || (n && !d_to)) return fail(MQ_EINVAL, "null argument");
   return guarded(idx, [&] {
-    idx->device().spans_begin(*idx->ix, d_tb, d_to, n, (hipStream_t)stream, exported, false, true);
+    Device& d = idx->device();
+    d.prepare(*idx->ix, (hipStream_t)stream);
+    d.spans_begin(d_tb, d_to, n, (hipStream_t)stream, exported, false, true);
     return 0;
   });
 }
@@ -524,7 +624,9 @@ int mq_match_spans_begin(mq_index* idx, const uint8_t* d_tb, const uint64_t* d_t
 int mq_match_spans_end(mq_index* idx, const mq_xlist* foreign, uint32_t n_foreign, void* stream, mq_span_result* out) {
   if (!out || (n_foreign && !foreign)) return fail(MQ_EINVAL, "null argument");
   return guarded(idx, [&] {
-    idx->device().spans_end(*idx->ix, foreign, n_foreign, (hipStream_t)stream, nullptr, out);
+    Device& d = idx->device();
+    if (d.batch_stale(*idx->ix)) throw HipError{hipErrorInvalidValue, "index updated between spans_begin and spans_end"};
+    d.spans_end(foreign, n_foreign, (hipStream_t)stream, nullptr, out);
     return 0;
   });
 }
@@ -659,6 +761,69 @@ int mq_messages_device(mq_index* idx, const uint8_t* d_fb, const uint64_t* d_fo,
   });
 }
 
+int mq_messages_runs_device(mq_index* idx, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, void* stream,
+                            mq_msg_runs_result* out) {
+  if (!out || (n && !d_fo)) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    idx->device().messages(*idx->ix, d_fb, d_fo, n, (hipStream_t)stream, nullptr, nullptr, out);
+    return 0;
+  });
+}
+
+int mq_messages_runs_batch(mq_index* idx, const uint8_t* fb, const uint64_t* fo, uint32_t n, mq_msg_runs_result** out) {
+  if (!out || (n && (!fo || (!fb && fo[n] != 0)))) return fail(MQ_EINVAL, "null argument");
+  return guarded(idx, [&] {
+    Device& d = idx->device();
+    std::unique_ptr<MsgRunsHolder> h(new MsgRunsHolder());
+    const uint8_t* dfb = nullptr;
+    const uint64_t* dfo = nullptr;
+    if (n) d.stage_inputs(fb, fo, n, nullptr, &dfb, &dfo);
+    mq_msg_runs_result dev_out;
+    d.messages(*idx->ix, dfb, dfo, n, nullptr, nullptr, nullptr, &dev_out, &h->data);
+    mq_msg_runs_result& r = h->pub;
+    r = dev_out;  // counts; pointers replaced by the host copies
+    r.run_base = h->data.run_base.data();
+    r.n_runs = h->data.n_runs.data();
+    r.base = h->data.base.data();
+    r.count = h->data.count.data();
+    r.runs = reinterpret_cast<const mq_msg_run*>(h->data.runs.data());
+    r.handles = h->data.handles ? h->data.handles->data() : nullptr;
+    *out = &h->pub;
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    g_results[&h->pub] = 5;
+    h.release();
+    return 0;
+  });
+}
+
+int mq_msg_runs_expand(const mq_msg_runs_result* r, uint32_t first, uint32_t count, uint64_t* out, uint64_t cap,
+                       uint64_t* n_out) {
+  if (!r || (uint64_t)first + count > r->n_filters) return fail(MQ_EINVAL, "filter range out of bounds");
+  {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    auto it = g_results.find((void*)r);
+    if (it == g_results.end() || it->second != 5) return fail(MQ_EINVAL, "not a host runs result (mq_messages_runs_batch)");
+  }
+  uint64_t w = 0;
+  for (uint32_t i = first; i < first + count; i++) {
+    if (r->run_base[i] + r->n_runs[i] > r->n_runs_total) return fail(MQ_EIO, "run range out of bounds");
+    if (w + r->count[i] > cap) return fail(MQ_ERANGE, "output capacity");
+    if (r->count[i] && !out) return fail(MQ_EINVAL, "null output");
+    uint64_t got = 0;
+    for (uint64_t k = r->run_base[i]; k < r->run_base[i] + r->n_runs[i]; k++) {
+      const mq_msg_run& run = r->runs[k];
+      if ((uint64_t)run.first + run.count > r->n_handles || got + run.count > r->count[i])
+        return fail(MQ_EIO, "run out of bounds");
+      memcpy(out + w + got, r->handles + run.first, (size_t)run.count * sizeof(uint64_t));
+      got += run.count;
+    }
+    if (got != r->count[i]) return fail(MQ_EIO, "runs disagree with the filter's count");
+    w += got;
+  }
+  if (n_out) *n_out = w;
+  return 0;
+}
+
 int mq_acl_match_batch(mq_index* idx, const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb,
                        const uint64_t* to, uint32_t nt, const uint32_t* pf, const uint32_t* pt, uint64_t n_pairs,
                        mq_acl_result** out) {
@@ -694,6 +859,7 @@ void mq_result_free(void* r) {
   if (kind == 1) delete reinterpret_cast<MatchHolder*>(r);
   if (kind == 2) delete reinterpret_cast<MsgHolder*>(r);
   if (kind == 3) delete reinterpret_cast<AclHolder*>(r);
+  if (kind == 5) delete reinterpret_cast<MsgRunsHolder*>(r);
   if (kind == 4) {
     SpanHolder* h = reinterpret_cast<SpanHolder*>(r);
     std::shared_ptr<IndexLock> lk = h->lk;

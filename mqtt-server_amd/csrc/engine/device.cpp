@@ -153,11 +153,13 @@ void Stager::add(void* dst, const void* src, size_t n) {
 }
 
 template <class T>
-void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager& st) {
+bool DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager& st) {
   const size_t n = m.size();
   bool full = m.all_dirty;
   if (!d || m.epoch != epoch || cap < n) {
-    release();
+    if (d) st.frees.push_back(d);
+    d = nullptr;
+    cap = 0;
     cap = std::max<size_t>(std::max(m.h.capacity(), n), 1);
     slow_mark("mirror-realloc");
     hip_check(hipMalloc(&d, cap * sizeof(T)), "hipMalloc(mirror)");
@@ -209,6 +211,7 @@ void DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
     flush();
   }
   m.clear_dirty();
+  return full;
 }
 
 // ---- profiler ----------------------------------------------------------------------------------
@@ -361,6 +364,7 @@ Device::~Device() {
   } catch (...) {
   }
   (void)hipDeviceSynchronize();  // no kernel of this index still reads a buffer freed below
+  release_retired();
   if (stage_done_) (void)hipEventDestroy(stage_done_);
   pinned_free(h_stage_, h_stage_bytes_);
   if (h_fast_) (void)hipHostFree(h_fast_);
@@ -451,31 +455,37 @@ std::string Device::verify(Index& ix) {
 
 void Device::sync(Index& ix, hipStream_t s) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
+  sync_ix(ix, s);
+  release_retired();
+}
+
+void Device::sync_ix(Index& ix, hipStream_t s) {
   if (ix.version() == synced_version_ && edges_.d) return;
   ix.flush_merge();
   Stager& st = stager_;
   st.runs.clear();
   st.bytes = 0;
-  edges_.sync(ix.edges, s, &uploaded_, st);
-  walk_.sync(ix.walk, s, &uploaded_, st);
-  lists_.sync(ix.lists, s, &uploaded_, st);
-  inls_.sync(ix.inls, s, &uploaded_, st);
-  msg_.sync(ix.msg, s, &uploaded_, st);
-  seginfo_.sync(ix.seginfo, s, &uploaded_, st);
-  segbytes_.sync(ix.segbytes, s, &uploaded_, st);
-  subs_.sync(ix.subs.m, s, &uploaded_, st);
-  mref_.sync(ix.mref, s, &uploaded_, st);
-  mpart_.sync(ix.mpart.m, s, &uploaded_, st);
-  npair_.sync(ix.npair, s, &uploaded_, st);
-  pent_.sync(ix.pent.m, s, &uploaded_, st);
-  plist_.sync(ix.plist.m, s, &uploaded_, st);
-  shr_.sync(ix.shr.m, s, &uploaded_, st);
-  inl_.sync(ix.inl.m, s, &uploaded_, st);
-  children_.sync(ix.children.m, s, &uploaded_, st);
-  if (ix.sharded()) xinfo_.sync(ix.xinfo, s, &uploaded_, st);
+  bool direct = false;
+  direct |= edges_.sync(ix.edges, s, &uploaded_, st);
+  direct |= walk_.sync(ix.walk, s, &uploaded_, st);
+  direct |= lists_.sync(ix.lists, s, &uploaded_, st);
+  direct |= inls_.sync(ix.inls, s, &uploaded_, st);
+  direct |= msg_.sync(ix.msg, s, &uploaded_, st);
+  direct |= seginfo_.sync(ix.seginfo, s, &uploaded_, st);
+  direct |= segbytes_.sync(ix.segbytes, s, &uploaded_, st);
+  direct |= subs_.sync(ix.subs.m, s, &uploaded_, st);
+  direct |= mref_.sync(ix.mref, s, &uploaded_, st);
+  direct |= mpart_.sync(ix.mpart.m, s, &uploaded_, st);
+  direct |= npair_.sync(ix.npair, s, &uploaded_, st);
+  direct |= pent_.sync(ix.pent.m, s, &uploaded_, st);
+  direct |= plist_.sync(ix.plist.m, s, &uploaded_, st);
+  direct |= shr_.sync(ix.shr.m, s, &uploaded_, st);
+  direct |= inl_.sync(ix.inl.m, s, &uploaded_, st);
+  direct |= children_.sync(ix.children.m, s, &uploaded_, st);
+  if (ix.sharded()) direct |= xinfo_.sync(ix.xinfo, s, &uploaded_, st);
   if (ix.deep.size()) {
-    deep_.sync(ix.deep, s, &uploaded_, st);
-    deep_codes_.sync(ix.deep_codes, s, &uploaded_, st);
+    direct |= deep_.sync(ix.deep, s, &uploaded_, st);
+    direct |= deep_codes_.sync(ix.deep_codes, s, &uploaded_, st);
   }
   if (!st.runs.empty()) {  // one staging buffer: the run table, then each run's bytes
     const size_t table = (st.runs.size() * sizeof(ScatterRun) + 15) & ~size_t(15);
@@ -513,12 +523,48 @@ void Device::sync(Index& ix, hipStream_t s) {
     h_stage_bytes_ = kStageInit;
     d_stage_.ensure(kStageInit);
     if (!stage_done_) hip_check(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming), "hipEventCreate");
+    // ... and the scatter kernel loaded by one empty run, so that the first update's sync does
+    // not load its code object under the handle lock
+    *static_cast<ScatterRun*>(h_stage_) = ScatterRun{(uint64_t)(uintptr_t)d_stage_.p, 0, 0};
+    hip_check(hipMemcpyAsync(d_stage_.p, h_stage_, sizeof(ScatterRun), hipMemcpyHostToDevice, s), "H2D staging");
+    launch_scatter(d_stage_.as<ScatterRun>(), 1, d_stage_.as<uint8_t>(), s);
+    hip_check(hipGetLastError(), "k_scatter");
+    hip_check(hipEventRecord(stage_done_, s), "hipEventRecord(stage)");
   }
   retained_len_ = ix.retained_len();
   empty_live_ = ix.empty_topic_live;
   empty_handle_ = ix.empty_topic_handle;
   synced_version_ = ix.version();
+  sync_direct_ = direct;
   syncs_++;
+}
+
+void Device::release_retired() {
+  for (void* p : stager_.frees) (void)hipFree(p);
+  stager_.frees.clear();
+}
+
+void Device::prepare(Index& ix, hipStream_t s) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  sync_ix(ix, s);  // (arrays it replaced are freed by the batch, outside the lock: spans_begin)
+  // an upload straight from the host image (pageable memory) may still read it: done before an
+  // update can touch it
+  if (sync_direct_) {
+    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(prepare)");
+    sync_direct_ = false;
+  }
+  IndexSnap& x = snap_;
+  x.version = ix.version();
+  x.sharded = ix.sharded();
+  x.shard = ix.shard();
+  x.inl_live = ix.inl.live != 0;
+  x.n_nodes = ix.n_nodes();
+  x.n_wild = ix.n_wild_nodes();
+  x.subs_len = ix.subs.m.size();
+  x.shr_len = ix.shr.m.size();
+  x.max_sub_cap = ix.max_sub_cap();
+  x.deep_live = ix.sharded() && ix.deep_live();
+  x.di = dev_index(ix);
 }
 
 DevIndex Device::dev_index(const Index& ix) const {
@@ -541,7 +587,7 @@ DevIndex Device::dev_index(const Index& ix) const {
   d.inl = inl_.d;
   d.children = children_.d;
   d.xinfo = ix.sharded() ? xinfo_.d : nullptr;
-  d.deep = ix.sharded() && ix.deep.size() ? deep_.d : nullptr;
+  d.deep = ix.sharded() && ix.deep_live() ? deep_.d : nullptr;
   d.deep_codes = d.deep ? deep_codes_.d : nullptr;
   d.deep_mask = d.deep ? ix.deep.size() - 1 : 0;
   d.retained_len = retained_len_;
@@ -1103,33 +1149,33 @@ TopicOff Device::walk_scan(const DevIndex& di, const uint8_t* d_tb, const uint64
 // and k_merge resolves the co-matching records into patches; nothing is copied per row. The
 // patch pool grows when a batch reserves more than it holds (the batch's k_merge then runs
 // again); the call ends with the stream synchronised and the guard flags checked.
-void Device::match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+void Device::match_spans(const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                          HostSpans* host, mq_span_result* out, hipEvent_t ready, std::atomic<bool>* issued) {
   mq_xlist x;
   trace_runs = 1;
-  spans_begin(ix, d_tb, d_to, n, s, &x, one_sync_);
+  spans_begin(d_tb, d_to, n, s, &x, one_sync_);
   slow_mark("begin");
-  if (spans_end(ix, nullptr, 0, s, host, out, ready, issued)) {
+  if (spans_end(nullptr, 0, s, host, out, ready, issued)) {
     slow_mark("end");
     return;
   }
   slow_mark("end-rerun");
   trace_runs = 2;
   // the one-sync run's buffers did not hold the batch: again, sized by the host
-  spans_begin(ix, d_tb, d_to, n, s, &x, false);
-  spans_end(ix, nullptr, 0, s, host, out, ready, issued);
+  spans_begin(d_tb, d_to, n, s, &x, false);
+  spans_end(nullptr, 0, s, host, out, ready, issued);
 }
 
-void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+void Device::spans_begin(const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                          mq_xlist* x, bool one_sync, bool shard_sync) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
+  release_retired();
   flush_host_copy();  // (a pipelined batch's copy: before this batch reuses any stage)
   slow_mark("flush");
-  sync(ix, s);
-  slow_mark("sync");
+  const IndexSnap& ix = snap_;  // (Device::prepare: the host image as synced)
   memset(x, 0, sizeof(*x));
   x->n_topics = n;
-  x->shard = ix.shard();
+  x->shard = ix.shard;
   sb_ = SpanBatch{};
   if (!err_.p) {
     err_.ensure(2 * sizeof(uint32_t));
@@ -1137,14 +1183,14 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   }
   // The walk counts only gathers when nothing needs the lists' totals before k_desc: no inline
   // rows to place and no device share pick (k_desc<true> then counts rows / shared / merge).
-  const bool lists = walk_lists_ || select_shared_ || ix.inl.live != 0;
+  const bool lists = walk_lists_ || select_shared_ || ix.inl_live;
   // A sharded index's begin runs as a one-sync batch's does (k_reset, buffers as earlier batches
   // left them, the export written by k_desc and packed by k_xpack) and synchronises once, at its
   // end, for the export's size (the exchange needs it) and the guards; its spans_end is host-sized.
-  const bool xsync = shard_sync && one_sync_ && ix.sharded() && !lists && dedup_ != 0 && set_grid_;
+  const bool xsync = shard_sync && one_sync_ && ix.sharded && !lists && dedup_ != 0 && set_grid_;
   // One host synchronisation for the whole batch (at its end): device results of an index that is
   // not sharded, without inline rows or a device share pick (whose buffers the walk's totals size)
-  one_sync = one_sync && !ix.sharded() && !lists && dedup_ != 0 && set_grid_;
+  one_sync = one_sync && !ix.sharded && !lists && dedup_ != 0 && set_grid_;
   const bool bsync = one_sync || xsync;  // the begin without host synchronisations
   sb_.trial = -1;
   if (one_sync && walk_auto_ && n >= kWalkTrialMin) {
@@ -1155,8 +1201,8 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     // filters) the thread per topic (64 topics per wavefront in flight).
     // a new size, or a new wildcard mix (the share of '+' / '#' particles moved by more than a
     // quarter of itself and by more than 0.02 of all particles): try again
-    const uint64_t nodes = ix.n_nodes();
-    const double wild = nodes ? (double)ix.n_wild_nodes() / (double)nodes : 0.0;
+    const uint64_t nodes = ix.n_nodes;
+    const double wild = nodes ? (double)ix.n_wild / (double)nodes : 0.0;
     const double dw = std::fabs(wild - walk_trial_wild_);
     if (nodes > 2 * walk_trial_nodes_ || 2 * nodes < walk_trial_nodes_ || (dw > 0.02 && dw > 0.25 * walk_trial_wild_)) {
       walk_trial_nodes_ = nodes;
@@ -1215,10 +1261,11 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   } else {
     check_err(s);  // faults flagged by an earlier row-format batch (one-sync batches read it at their end)
   }
-  const DevIndex di = dev_index(ix);
+  snap_.di.err = err_.as<uint32_t>();  // (allocated above on the first batch)
+  const DevIndex di = snap_.di;
   sb_.pending = true;
   sb_.n = n;
-  sb_.version = ix.version();
+  sb_.version = ix.version;
   sb_.di = di;
   if (n == 0) return;
   ensure_streams();
@@ -1249,7 +1296,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     grow(dd_list_, (size_t)n * kPairMax * sizeof(uint32_t));
     grow(dd_mrow_, (size_t)n * kPairMax * sizeof(uint32_t));
     grow(dd_mpair_, (size_t)n * kPairMax * sizeof(uint2));
-    if (ix.sharded()) grow(dd_mrank_, (size_t)n * kPairMax * sizeof(uint64_t));
+    if (ix.sharded) grow(dd_mrank_, (size_t)n * kPairMax * sizeof(uint64_t));
   }
   // k_desc's arguments (the buffers are (re)sized below unless the batch is one-sync)
   auto desc_args = [&]() {
@@ -1271,7 +1318,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
       da.mcount = dd_cnt_.as<uint32_t>();
       da.mlist = dd_list_.as<uint32_t>();
       da.mrow = dd_mrow_.as<uint32_t>();
-      if (ix.sharded()) da.mrank = dd_mrank_.as<uint64_t>();
+      if (ix.sharded) da.mrank = dd_mrank_.as<uint64_t>();
     }
     da.spans_cap = sp_spans_.bytes / sizeof(SpanRec);
     da.desc_cap = desc_[0].bytes / sizeof(GDesc);
@@ -1392,7 +1439,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
         (!fused && gathers_total > desc_[0].bytes / sizeof(GDesc))) {
       // the walk or k_desc outgrew what earlier batches left: the begin again, host-sized
       prof.count("one_sync_retries", 1);
-      spans_begin(ix, d_tb, d_to, n, s, x, false, false);
+      spans_begin(d_tb, d_to, n, s, x, false, false);
       return;
     }
     if (h_fast_->unsafe & kUnsafeXEnts) {  // only the packed export outgrew its buffer: pack again
@@ -1410,7 +1457,7 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
     x->n_ents = h_fast_->n_sets[0];
     prof.count("xents", x->n_ents);
     prof.count("topics", n);
-  } else if (ix.sharded()) {  // export: each topic's gathered cross-shard nodes
+  } else if (ix.sharded) {  // export: each topic's gathered cross-shard nodes
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     grow(x_off_, (size_t)(n + 1) * sizeof(TopicOff));
     grow(x_cnt_, (size_t)n * sizeof(uint32_t));
@@ -1435,24 +1482,24 @@ void Device::spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, u
   }
 }
 
-bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host,
+bool Device::spans_end(const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host,
                        mq_span_result* out, hipEvent_t ready, std::atomic<bool>* issued) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   memset(out, 0, sizeof(*out));
   if (host) *host = HostSpans{};
   if (!sb_.pending) throw HipError{hipErrorInvalidValue, "spans_end without spans_begin"};
   sb_.pending = false;
-  if (ix.version() != sb_.version) throw HipError{hipErrorInvalidValue, "index updated between spans_begin and spans_end"};
+  const IndexSnap& ix = snap_;
   const DevIndex di = sb_.di;
   const uint32_t n = sb_.n;
   TopicOff tot = sb_.tot;
   out->sub_pool = reinterpret_cast<const mq_client_row*>(di.subs);
   out->shared_pool = reinterpret_cast<const mq_shared_row*>(di.shr);
-  out->sub_pool_len = ix.subs.m.size();
-  out->shared_pool_len = ix.shr.m.size();
+  out->sub_pool_len = ix.subs_len;
+  out->shared_pool_len = ix.shr_len;
   out->flags = select_shared_ ? MQ_SPANS_PICKED : 0u;
   if (nf > kMaxShards - 1) throw HipError{hipErrorInvalidValue, "more foreign lists than kMaxShards - 1"};
-  if (nf && !ix.sharded()) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
+  if (nf && !ix.sharded) throw HipError{hipErrorInvalidValue, "foreign lists for an index that is not sharded"};
   if (n == 0) {
     if (ready) hip_check(hipEventRecord(ready, s), "hipEventRecord");
     if (issued) issued->store(true);
@@ -1463,8 +1510,8 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   // codes while every subscription list is shorter than 2^23 (set rows) and the rows of a topic
   // fit 29 bits (MQ_SPANS_PATCH_CODES)
   HostStage* hs = nullptr;
-  const bool codes = host && patch_codes_ && ix.max_sub_cap() <= (1u << kCodeSetRowBits) &&
-                     ix.subs.m.size() < (1ull << 29);
+  const bool codes = host && patch_codes_ && ix.max_sub_cap <= (1u << kCodeSetRowBits) &&
+                     ix.subs_len < (1ull << 29);
   if (host) {
     host->codes = codes;
     ensure_hcopy();
@@ -1617,7 +1664,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
   a.rep = nullptr;
   a.tslot = nullptr;
   a.dd_phase = 0;
-  a.mrank = ix.sharded() && sb_.dedup ? dd_mrank_.as<uint64_t>() : nullptr;
+  a.mrank = ix.sharded && sb_.dedup ? dd_mrank_.as<uint64_t>() : nullptr;
   a.desc_cap = desc_[0].bytes / sizeof(GDesc);
   a.unsafe = one_sync ? unsafe_.as<uint32_t>() : nullptr;
   a.g_stride = sb_.fused ? kGatherCap : 0u;
@@ -1668,7 +1715,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       // k_set (sets.hip; a sharded index's with its rank keys) unless a sharded index holds filters
       // deeper than 32 levels (their keys can tie: k_merge's deep tie-break), a measurement variant
       // of k_merge's set pass is asked for (MQ_OPT_SET_EXP bit 7, the attribution bits 0-4), or bit 13
-      if (!(ix.sharded() && a.ix.deep) && !(set_exp_ & (0x1Fu | 128u | 8192u)) && merge_wpe == kMergeWavesPerEU)
+      if (!(ix.sharded && a.ix.deep) && !(set_exp_ & (0x1Fu | 128u | 8192u)) && merge_wpe == kMergeWavesPerEU)
         launch_set(a, set_blocks, s);
       else
         launch_merge(a, true, merge_wpe, set_blocks, s);
@@ -1836,7 +1883,7 @@ bool Device::spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s
       if (sb_.xsync) {  // sharded: the begin's results and the imported lists stand; the end again,
         sb_.pending = true;  // host-sized
         sb_.xsync = false;
-        return spans_end(ix, xf, nf, s, host, out, ready, issued);
+        return spans_end(xf, nf, s, host, out, ready, issued);
       }
       return false;
     }
@@ -2147,14 +2194,22 @@ MsgImg Device::msg_img() const {
   m.n_pos = img_n_pos_;
   m.cyc = nullptr;
   m.work = nullptr;
+  m.run_base = nullptr;
+  m.run_cnt = nullptr;
   return m;
 }
 
 // k_msgq count pass, scan, fill pass, k_msg_copy. Returns false (nothing written) when a filter's
 // fan-out nesting exceeded kMsgStack: the batch then takes the particle walk.
 bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
-                          hipStream_t s, TopicOff* tot) {
+                          hipStream_t s, TopicOff* tot, bool run_out) {
   MsgImg img = msg_img();
+  if (run_out) {  // runs at the boundary: a piece per run, nothing copied (k_msg_copy not launched)
+    msg_rbase_.ensure((size_t)n * sizeof(uint64_t));
+    msg_rcnt_.ensure((size_t)n * sizeof(uint32_t));
+    img.run_base = msg_rbase_.as<uint64_t>();
+    img.run_cnt = msg_rcnt_.as<uint32_t>();
+  }
   const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
   if (prof.work()) {  // MQ_PROF_WORK: per-filter clocks and fan-out work of the count pass
     grow(msg_cyc_, (size_t)n * sizeof(uint32_t) + 4 * sizeof(unsigned long long));
@@ -2219,6 +2274,7 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
       prof.end("msgq_wide_fill", s);
     }
     hip_check(hipGetLastError(), "k_msgq<fill>");
+    if (run_out) return;
     prof.begin(s, "msg_copy");
     if (n_pieces)
       launch_msg_copy_dev(msg_pieces_.as<MsgPiece>(), n_pieces, msg_pieces_.bytes / sizeof(MsgPiece), img.h,
@@ -2240,8 +2296,8 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
     if (!msg_gate_.p) msg_gate_.ensure(2 * sizeof(uint64_t));
     uint32_t* gate = msg_gate_.as<uint32_t>();
     uint64_t* n_pieces = msg_gate_.as<uint64_t>() + 1;
-    launch_msg_gate(bpre_.as<TopicOff>() + nb, msg_handles_.bytes / sizeof(uint64_t), msg_pieces_.bytes / sizeof(MsgPiece),
-                    gate, n_pieces, s);
+    launch_msg_gate(bpre_.as<TopicOff>() + nb, run_out ? ~0ull : msg_handles_.bytes / sizeof(uint64_t),
+                    msg_pieces_.bytes / sizeof(MsgPiece), gate, n_pieces, s);
     hip_check(hipGetLastError(), "k_msg_gate");
     fill_copy(gate, n_pieces);
     uint32_t e = 0, g = 0;
@@ -2256,7 +2312,7 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
     if (e) check_err(s);  // throws with the tripped guard's name
     if (!g) {
       prof.count("msg_one_sync_retries", 1);
-      msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
+      if (!run_out) msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
       msg_pieces_.ensure(std::max<uint64_t>(tot->g, 1) * sizeof(MsgPiece));
       fill_copy(nullptr, nullptr);
     }
@@ -2291,7 +2347,7 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
     prof.count("msg_lane_walk_filters", w[1]);
     prof.count("msg_lane_walk_particles", w[2]);
   }
-  msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
+  if (!run_out) msg_handles_.ensure(std::max<uint64_t>(tot->rows, 1) * sizeof(uint64_t));
   msg_base_.ensure((size_t)n * sizeof(uint64_t));
   msg_count_.ensure((size_t)n * sizeof(uint32_t));
   msg_pieces_.ensure(std::max<uint64_t>(tot->g, 1) * sizeof(MsgPiece));
@@ -2343,11 +2399,16 @@ void Device::messages_walk(Index& ix, const DevIndex& di, const uint8_t* d_fb, c
 }
 
 void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
-                      hipStream_t s, HostMsg* host, mq_msg_result* out) {
+                      hipStream_t s, HostMsg* host, mq_msg_result* out, mq_msg_runs_result* runs,
+                      HostMsgRuns* hruns) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   sync(ix, s);
+  mq_msg_result unused;
+  if (!out) out = &unused;
   *out = mq_msg_result{};
   if (host) *host = HostMsg{};
+  if (runs) *runs = mq_msg_runs_result{};
+  if (hruns) *hruns = HostMsgRuns{};
   if (!err_.p) {
     err_.ensure(2 * sizeof(uint32_t));
     hip_check(hipMemsetAsync(err_.p, 0, 2 * sizeof(uint32_t), s), "hipMemsetAsync(err)");
@@ -2370,9 +2431,63 @@ void Device::messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint
   bool done = false;
   if (img_path) {
     ensure_img(ix, di, s);
-    done = messages_img(di, d_fb, d_fo, n, s, &tot);
+    done = messages_img(di, d_fb, d_fo, n, s, &tot, runs != nullptr);
   }
   if (!done) messages_walk(ix, di, d_fb, d_fo, n, s, &tot);
+  if (runs) {
+    if (!done) {  // the particle walk's own handles, one run per filter
+      if (tot.rows >> 32) throw HipError{hipErrorInvalidValue, "Messages runs: a walked batch of 2^32 handles or more"};
+      msg_rbase_.ensure((size_t)n * sizeof(uint64_t));
+      msg_rcnt_.ensure((size_t)n * sizeof(uint32_t));
+      msg_pieces_.ensure((size_t)n * sizeof(MsgPiece));
+      launch_msg_runs_of(n, msg_base_.as<uint64_t>(), msg_count_.as<uint32_t>(), msg_pieces_.as<MsgPiece>(),
+                         msg_rbase_.as<uint64_t>(), msg_rcnt_.as<uint32_t>(), s);
+      hip_check(hipGetLastError(), "k_msg_runs_of");
+      tot.g = n;
+    }
+    static_assert(sizeof(MsgPiece) == sizeof(mq_msg_run), "a piece is the ABI's run");
+    runs->n_filters = n;
+    runs->run_base = msg_rbase_.as<uint64_t>();
+    runs->n_runs = msg_rcnt_.as<uint32_t>();
+    runs->base = msg_base_.as<uint64_t>();
+    runs->count = msg_count_.as<uint32_t>();
+    runs->runs = msg_pieces_.as<mq_msg_run>();
+    runs->n_runs_total = tot.g;
+    runs->handles = done ? img_h_.as<uint64_t>() : msg_handles_.as<uint64_t>();
+    runs->n_handles = done ? img_live_ : tot.rows;
+    runs->n_expanded = tot.rows;
+    if (hruns) {
+      hruns->run_base.resize(n);
+      hruns->n_runs.resize(n);
+      hruns->base.resize(n);
+      hruns->count.resize(n);
+      hruns->runs.resize(tot.g);
+      auto d2h = [&](void* dst, const void* src, size_t bytes) {
+        if (bytes) hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "D2H runs");
+      };
+      d2h(hruns->run_base.data(), runs->run_base, n * sizeof(uint64_t));
+      d2h(hruns->n_runs.data(), runs->n_runs, n * sizeof(uint32_t));
+      d2h(hruns->base.data(), runs->base, n * sizeof(uint64_t));
+      d2h(hruns->count.data(), runs->count, n * sizeof(uint32_t));
+      d2h(hruns->runs.data(), runs->runs, tot.g * sizeof(MsgPiece));
+      if (done) {  // the image's handles: one host copy per image version, shared by the results
+        if (!host_img_ || host_img_version_ != img_version_) {
+          auto hv = std::make_shared<PinnedVec<uint64_t>>(img_live_);
+          d2h(hv->data(), img_h_.p, img_live_ * sizeof(uint64_t));
+          host_img_ = std::move(hv);
+          host_img_version_ = img_version_;
+        }
+        hruns->handles = host_img_;
+      } else {
+        auto hv = std::make_shared<PinnedVec<uint64_t>>(tot.rows);
+        d2h(hv->data(), msg_handles_.p, tot.rows * sizeof(uint64_t));
+        hruns->handles = std::move(hv);
+      }
+      hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+      check_err(s);
+    }
+    return;
+  }
   out->n_filters = n;
   out->base = msg_base_.as<uint64_t>();
   out->count = msg_count_.as<uint32_t>();

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <memory>
 
 #include <new>
 #include <string>
@@ -47,6 +48,8 @@ struct Stager {
   };
   std::vector<Run> runs;
   size_t bytes = 0;
+  std::vector<void*> frees;  // device arrays a sync replaced: freed outside the handle lock
+                             //   (hipFree waits for the device; Device::release_retired)
   void add(void* dst, const void* src, size_t n);  // split into runs of <= kScatterRun
 };
 
@@ -59,8 +62,8 @@ struct DevMirror {
   DevMirror(const DevMirror&) = delete;
   DevMirror& operator=(const DevMirror&) = delete;
   ~DevMirror() { release(); }
-  // reallocated or mostly dirty: uploaded whole now; else its dirty pages go to `st`
-  void sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager& st);
+  // reallocated or mostly dirty: uploaded whole now (returns true); else its dirty pages go to `st`
+  bool sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager& st);
   void release();
 };
 
@@ -102,6 +105,16 @@ struct HostMsg {
   PinnedVec<uint64_t> base;
   PinnedVec<uint32_t> count;
   PinnedVec<uint64_t> handles;
+};
+
+// Host-side destination of a Messages runs batch (mq_messages_runs_batch): the runs, and the
+// array they index — a host copy of the retained image's handles, shared by every result of one
+// image version, or the batch's own handles (particle walk).
+struct HostMsgRuns {
+  PinnedVec<uint64_t> run_base, base;
+  PinnedVec<uint32_t> n_runs, count;
+  PinnedVec<MsgPiece> runs;
+  std::shared_ptr<const PinnedVec<uint64_t>> handles;
 };
 
 // Host-side destination of a batched MatchTopic (mq_acl_match_batch).
@@ -179,6 +192,22 @@ class Profiler {
   std::vector<Total> totals_;
 };
 
+// What a span batch reads of the host image, taken when the device image is synced
+// (Device::prepare, under the handle lock): the batch's kernels then run without the lock while
+// updates change the host image (capi.cpp Access::kMatch; topics.go:402 — writers serialise only
+// with each other and with the sync, never with a match's GPU work).
+struct IndexSnap {
+  uint64_t version = ~0ull;
+  bool sharded = false;
+  uint32_t shard = 0;
+  bool inl_live = false;        // inline subscriptions exist
+  uint64_t n_nodes = 0, n_wild = 0;
+  uint64_t subs_len = 0, shr_len = 0;  // the subscription pools' lengths (results name them)
+  uint32_t max_sub_cap = 0;
+  bool deep_live = false;       // a sharded index knows filters deeper than 32 levels
+  DevIndex di{};
+};
+
 class Device {
  public:
   explicit Device(int dev);
@@ -189,6 +218,16 @@ class Device {
 
   // Upload dirty pages of the index image (incremental device-side update).
   void sync(Index& ix, hipStream_t s);
+  // Sync, then take the snapshot the next span batch runs on (under the handle lock; the batch
+  // itself may then run without it). Uploads straight from the host image (a reallocated or
+  // mostly dirty array) are waited for, so an update may change the image once this returns.
+  void prepare(Index& ix, hipStream_t s);
+  const IndexSnap& snap() const { return snap_; }
+  // Free the device arrays that syncs replaced (nothing on the device reads them any more: the
+  // work that did ran under the device lock before the sync).
+  void release_retired();
+  // the index changed since the pending batch's spans_begin (the two-phase sharded calls)
+  bool batch_stale(const Index& ix) const { return ix.version() != sb_.version; }
   // Diagnostic: sync, then read every device array back and compare it with the host mirror;
   // returns "" or the first difference.
   std::string verify(Index& ix);
@@ -205,7 +244,8 @@ class Device {
   // device does next (the next batch's kernels), and `ready` is recorded when it is done; without
   // it the call returns after the copy. `issued` (with ready) is set when the deferred copy is queued:
   // a copy that was dropped (its flush failed) leaves it false, and the waiter reports MQ_EIO.
-  void match_spans(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
+  // Runs on the snapshot of the last prepare().
+  void match_spans(const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                    HostSpans* host, mq_span_result* out, hipEvent_t ready = nullptr,
                    std::atomic<bool>* issued = nullptr);
   // Issue the pipelined host batch's copy that is still pending (match_spans with `ready` defers
@@ -225,13 +265,16 @@ class Device {
   // one_sync (match_spans only): the batch may run with one host synchronisation (at its end),
   // its buffers sized by earlier batches; spans_end then returns false when they did not hold it
   // and the caller runs the batch again without one_sync (host-sized buffers).
-  void spans_begin(Index& ix, const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x,
+  void spans_begin(const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s, mq_xlist* x,
                    bool one_sync = false, bool shard_sync = false);
-  bool spans_end(Index& ix, const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out,
+  bool spans_end(const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans* host, mq_span_result* out,
                  hipEvent_t ready = nullptr, std::atomic<bool>* issued = nullptr);
   // Messages for n filters resident on the device (topics.go:525): handle sets per filter.
+  // runs (mq_messages_runs_*): the runs instead of the handles (out then unused), into *runs
+  // (device pointers) and, with hruns, copied to the host
   void messages(Index& ix, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
-                HostMsg* host, mq_msg_result* out);
+                HostMsg* host, mq_msg_result* out, mq_msg_runs_result* runs = nullptr,
+                HostMsgRuns* hruns = nullptr);
   // auth.MatchTopic over (filter, topic) pairs of two host string tables (k_acl).
   void acl(const uint8_t* fb, const uint64_t* fo, uint32_t nf, const uint8_t* tb, const uint64_t* to,
            uint32_t nt, const uint32_t* pf, const uint32_t* pt, uint64_t n_pairs, HostAcl* out);
@@ -256,6 +299,7 @@ class Device {
 
  private:
   DevIndex dev_index(const Index& ix) const;
+  void sync_ix(Index& ix, hipStream_t s);  // sync() without freeing the arrays it replaced
   void check_err(hipStream_t s);
   // walk (count) + scan of n topics; returns the batch totals (synchronises s)
   // (one_sync: the totals are not read back - the returned TopicOff is zero - and every topic's
@@ -269,12 +313,14 @@ class Device {
   void ensure_img(const Index& ix, const DevIndex& di, hipStream_t s);
   MsgImg msg_img() const;
   bool messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n, hipStream_t s,
-                    TopicOff* tot);
+                    TopicOff* tot, bool run_out = false);
   void messages_walk(Index& ix, const DevIndex& di, const uint8_t* d_fb, const uint64_t* d_fo, uint32_t n,
                      hipStream_t s, TopicOff* tot);
 
   int dev_;
   uint64_t synced_version_ = ~0ull;
+  IndexSnap snap_;
+  bool sync_direct_ = false;  // the last sync uploaded from the host image directly (pageable)
   uint64_t uploaded_ = 0, syncs_ = 0;
   uint32_t last_chunks_ = 0;
   uint64_t chunk_rows_budget_;
@@ -418,6 +464,9 @@ class Device {
   bool msg_edges_on_ = true;          // MQ_OPT_MSG_EDGES
   DevBuf msg_pieces_;               // k_msgq copy pieces of a batch
   DevBuf msg_runs_, msg_nruns_;     // k_msgq runs recorded by the count pass (kMsgRuns)
+  DevBuf msg_rbase_, msg_rcnt_;     // runs at the boundary: each filter's first run, run count
+  std::shared_ptr<PinnedVec<uint64_t>> host_img_;  // host copy of img_h_ (runs host results)
+  uint64_t host_img_version_ = ~0ull;
   uint64_t img_version_ = ~0ull;    // ix.retained_version() the image was built at
   uint32_t img_n_ = 0, img_n_pos_ = 0, img_levels_ = 0;
   uint64_t img_live_ = 0;

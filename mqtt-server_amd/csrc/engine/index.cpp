@@ -230,8 +230,38 @@ void Index::set_rank(uint32_t n, uint32_t parent, std::string_view seg, bool mar
 // The order of two deep paths whose rank keys tie (layout.h DeepTail): filter fid's codes for its
 // levels 33.., kept for the device's tie-break (merge.hip deep_before). Entries are overwritten
 // when a filter id is seen again (a filter id names one filter while it is subscribed).
+size_t Index::deep_find(uint32_t fid) const {
+  const size_t mask = deep.size() - 1;
+  size_t sl = mix64(fid) & mask;
+  while (deep.h[sl].fid != kNone && deep.h[sl].fid != fid) sl = (sl + 1) & mask;
+  return sl;
+}
+
+void Index::deep_rebuild(size_t slots) {
+  std::vector<DeepTail> old;
+  old.swap(deep.h);
+  std::vector<uint32_t> codes;
+  codes.swap(deep_codes.h);
+  deep.h.assign(slots, DeepTail{kNone, 0, 0, 0});
+  deep_codes.h.clear();
+  for (const DeepTail& e : old) {
+    if (e.fid == kNone || e.fid == kDeepTomb) continue;
+    const uint32_t off = (uint32_t)deep_codes.h.size();
+    deep_codes.h.insert(deep_codes.h.end(), codes.begin() + e.off, codes.begin() + e.off + e.n);
+    deep.h[deep_find(e.fid)] = DeepTail{e.fid, off, e.n, 0};
+  }
+  n_deep_ = n_deep_live_;
+  deep_garbage_ = 0;
+  deep.epoch++;
+  deep.all_dirty = true;
+  deep_codes.epoch++;
+  deep_codes.all_dirty = true;
+  version_++;
+}
+
 void Index::note_deep(uint32_t fid, const uint32_t* segs, uint32_t depth) {
   if (depth <= 32 || fid == kNone) return;
+  deep_refs_[fid]++;
   const uint32_t n = (depth - 32 + 15) / 16;
   thread_local std::vector<uint32_t> w;
   w.assign(n, 0u);
@@ -240,32 +270,41 @@ void Index::note_deep(uint32_t fid, const uint32_t* segs, uint32_t depth) {
     const uint32_t j = i - 32;
     w[j / 16] |= code << (30 - 2 * (j % 16));
   }
-  auto find = [&](uint32_t f) -> size_t {
-    const size_t mask = deep.size() - 1;
-    size_t sl = mix64(f) & mask;
-    while (deep.h[sl].fid != kNone && deep.h[sl].fid != f) sl = (sl + 1) & mask;
-    return sl;
-  };
   if (deep.size()) {
-    const DeepTail& e = deep.h[find(fid)];
+    const DeepTail& e = deep.h[deep_find(fid)];
     if (e.fid == fid && e.n == n && std::equal(w.begin(), w.end(), deep_codes.h.begin() + e.off)) return;
   }
-  if ((n_deep_ + 1) * 2 > deep.size()) {  // at most half full: rehash into twice the slots
-    std::vector<DeepTail> old;
-    old.swap(deep.h);
-    deep.h.assign(std::max<size_t>(64, old.size() * 2), DeepTail{kNone, 0, 0, 0});
-    deep.epoch++;
-    deep.all_dirty = true;
-    for (const DeepTail& e : old)
-      if (e.fid != kNone) deep.h[find(e.fid)] = e;
+  if ((n_deep_ + 1) * 2 > deep.size()) {  // at most half full (tombstones count): rehash
+    size_t slots = 64;
+    while (slots < 4 * (size_t)(n_deep_live_ + 1)) slots *= 2;
+    deep_rebuild(slots);
   }
-  const size_t sl = find(fid);
-  if (deep.h[sl].fid == kNone) n_deep_++;
+  const size_t sl = deep_find(fid);
+  if (deep.h[sl].fid == kNone) {
+    n_deep_++;
+    n_deep_live_++;
+  } else {
+    deep_garbage_ += deep.h[sl].n;  // (an id reused for another deep path while still referenced)
+  }
   const uint32_t off = (uint32_t)deep_codes.size();
   deep_codes.grow_to(off + n, 0u);
   for (uint32_t k = 0; k < n; k++) deep_codes.at_w(off + k) = w[k];
   deep.at_w(sl) = DeepTail{fid, off, n, 0};
   version_++;
+}
+
+void Index::deep_unref(uint32_t fid) {
+  auto it = deep_refs_.find(fid);
+  if (it == deep_refs_.end() || --it->second) return;
+  deep_refs_.erase(it);
+  if (!deep.size()) return;
+  const size_t sl = deep_find(fid);
+  if (deep.h[sl].fid != fid) return;
+  deep_garbage_ += deep.h[sl].n;
+  deep.at_w(sl) = DeepTail{kDeepTomb, 0, 0, 0};  // (probes for other ids pass over it)
+  n_deep_live_--;
+  version_++;
+  if (deep_garbage_ > 4096 && deep_garbage_ > deep_codes.size() / 2) deep_rebuild(deep.size());
 }
 
 void Index::note_deep_node(uint32_t n, uint32_t fid) {
@@ -553,7 +592,10 @@ void Index::remove_node(uint32_t n) {
   lists.at_w(n) = kEmptyLists;
   if (inls.h[n].cnt || inls.h[n].off) inls.at_w(n) = NodeInl{0, 0};
   msg.at_w(n) = NodeMsg{};
-  if (sharded()) xinfo.at_w(n) = XInfo{kNone, 0, 0};
+  if (sharded()) {
+    if (xinfo.h[n].fid != kNone && h.depth > 32) deep_unref(xinfo.h[n].fid);
+    xinfo.at_w(n) = XInfo{kNone, 0, 0};
+  }
   n_wild_nodes_ -= h.str <= 1;
   h = NodeHost{};
   free_nodes_.push_back(n);
@@ -1373,6 +1415,7 @@ void Index::foreign_unsubscribe(uint32_t client, uint32_t fid) {
     v.erase(std::find(v.begin(), v.end(), i));
     if (v.empty()) client_foreign_.erase(cf);
   }
+  if (fsubs_[i].depth > 32) deep_unref(fid);
   fsubs_[i].depth = 0;
   fsub_free_.push_back(i);
 }

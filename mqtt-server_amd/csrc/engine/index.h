@@ -396,6 +396,7 @@ class Index {
   uint64_t n_nodes() const { return n_live_nodes_; }
   uint64_t n_wild_nodes() const { return n_wild_nodes_; }  // '+' / '#' particles
   uint32_t max_sub_cap() const { return max_sub_cap_; }     // the largest subscription slab ever
+  bool deep_live() const { return n_deep_live_ != 0; }       // a filter deeper than 32 levels is known
   uint64_t n_edges() const { return n_edges_; }
   // edge table: at most 1/load of its slots used (MQ_OPT_EDGE_LOAD); from the next growth. A
   // table of 2^30 slots or more keeps load <= 1/2 (32 GB of slots at 2^30).
@@ -470,9 +471,18 @@ class Index {
   // (mark = false: a parallel bulk build, which marks the whole array dirty itself)
   void set_rank(uint32_t n, uint32_t parent, std::string_view seg, bool mark = true);
   // a deep filter's DeepTail from its segment string ids (path_strs / fpaths_: 0 '+', 1 '#')
+  // Each call is one reference to fid's entry (a node that took fid, or a foreign subscription);
+  // deep_unref drops one, and the entry goes (a tombstone) with the last, so a filter id that is
+  // reused for another filter never finds a stale entry.
   void note_deep(uint32_t fid, const uint32_t* segs, uint32_t depth);
   void note_deep_node(uint32_t n, uint32_t fid);
-  uint32_t n_deep_ = 0;
+  void deep_unref(uint32_t fid);
+  void deep_rebuild(size_t slots);  // live entries only into `slots` slots, codes compacted
+  size_t deep_find(uint32_t fid) const;  // fid's slot, or the free slot that ends its probe
+  uint32_t n_deep_ = 0;       // used slots, tombstones included (the table's load)
+  uint32_t n_deep_live_ = 0;  // entries
+  size_t deep_garbage_ = 0;   // words of deep_codes no entry names
+  std::unordered_map<uint32_t, uint32_t> deep_refs_;
   // (mark = false: the whole list moves to a new slab; no slot changes its place k)
   void move_slot(uint32_t n, uint32_t from, uint32_t to, bool mark = true);
   void part_set(uint32_t pos, const std::vector<uint32_t>& nodes);

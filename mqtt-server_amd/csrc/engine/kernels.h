@@ -526,12 +526,21 @@ struct MsgImg {
   // frontier outgrew LDS (per-lane walk), [2] particles those walked per lane
   uint32_t* cyc;
   unsigned long long* work;
+  // Runs at the boundary (mq_messages_runs_*, round 6): every run the walk finds is one MsgPiece
+  // (== mq_msg_run) and nothing is copied; the fill passes also write each filter's first run and
+  // run count (null: handles, as before)
+  uint64_t* run_base;
+  uint32_t* run_cnt;
 };
-// A run of h copied to the output: out[dst + k] = h[h0 + k], k < len.
+// A run of h copied to the output: out[dst + k] = h[h0 + k], k < len. (Runs at the boundary: the
+// result's mq_msg_run, include/mqmatch.h: first, count, at.)
 struct MsgPiece {
   uint32_t h0, len;
   uint64_t dst;
 };
+// runs at the boundary for a batch the particle walk answered: filter t's handles as one run
+void launch_msg_runs_of(uint32_t n, const uint64_t* base, const uint32_t* count, MsgPiece* runs, uint64_t* run_base,
+                        uint32_t* run_cnt, hipStream_t s);
 constexpr uint32_t kMsgPiece = 4096;    // handles per copy piece (a wavefront's work item)
 constexpr uint32_t kMsgDirect = 8;      // runs this short are copied by the walk itself
 constexpr uint32_t kMsgStack = 16;      // nested fan-outs a lane can hold (deeper: kErrMsgNest)

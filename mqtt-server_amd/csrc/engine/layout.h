@@ -194,6 +194,7 @@ struct XEnt {  // 16 B
 // in their keys are ordered by their first differing word (a proper prefix first). Entries sit
 // in an open-addressed table keyed by filter id (Index::deep; fid kNone: a free slot), holding
 // every deep filter the shard knows: its own nodes' and its foreign partners'.
+constexpr uint32_t kDeepTomb = 0xFFFFFFFEu;  // a removed entry (sharded filter ids are < 2^31)
 struct DeepTail {  // 16 B
   uint32_t fid;
   uint32_t off, n;

@@ -606,8 +606,14 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
     obase = FILL ? off[t].rows : 0;
     pbase = FILL ? off[t].g : 0;
   }
+  // runs at the boundary: every run one piece record (uncut), no handle copied
+  const bool run_out = img.run_base != nullptr;
   // one piece record per kMsgPiece handles of a long run
   auto put_pieces = [&](uint32_t h0, uint32_t len, uint32_t dst, uint32_t slot) __attribute__((always_inline)) {
+    if (run_out) {
+      pieces[pbase + slot] = MsgPiece{h0, len, obase + dst};
+      return;
+    }
     const uint32_t npc = (len + kMsgPiece - 1) / kMsgPiece;
     for (uint32_t i = 0; i < npc; i++)
       pieces[pbase + slot + i] = MsgPiece{h0 + i * kMsgPiece, (uint32_t)min(kMsgPiece, len - i * kMsgPiece),
@@ -619,13 +625,17 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       const MsgRun* __restrict__ fr = runs + (uint64_t)t * run_cap;
       for (uint32_t k = lane; k < nr; k += 64) {
         const MsgRun r = fr[k];
-        if (r.len > kMsgDirect) put_pieces(r.h0, r.len, r.dst, r.pslot);
+        if (r.len > kMsgDirect || run_out) put_pieces(r.h0, r.len, r.dst, r.pslot);
         else
           for (uint32_t j = 0; j < r.len; j++) handles[obase + r.dst + j] = img.h[r.h0 + j];
       }
       if (lane == 0) {
         base_out[t] = obase;
         count_out[t] = cnt[t].rows;
+        if (run_out) {
+          img.run_base[t] = pbase;
+          img.run_cnt[t] = cnt[t].gathers;
+        }
       }
       return;
     }
@@ -637,7 +647,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
   uint32_t nh = 0, np = 0;  // count pass: this lane's handles and pieces
   auto emit = [&](uint32_t h0, uint32_t len) __attribute__((always_inline)) {
     if (len == 0) return;
-    const uint32_t npc = len > kMsgDirect ? (len + kMsgPiece - 1) / kMsgPiece : 0u;
+    const uint32_t npc = run_out ? 1u : len > kMsgDirect ? (len + kMsgPiece - 1) / kMsgPiece : 0u;
     if (!FILL) {
       nh += len;
       np += npc;
@@ -892,7 +902,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         pbase = off[t].g + it.pslot;
         for (uint32_t k = lane; k < it.n_runs; k += 64) {
           const MsgRun r = w.scratch[(uint64_t)it.run_off + k];
-          if (r.len > kMsgDirect) put_pieces(r.h0, r.len, r.dst, r.pslot);
+          if (r.len > kMsgDirect || run_out) put_pieces(r.h0, r.len, r.dst, r.pslot);
           else
             for (uint32_t j = 0; j < r.len; j++) handles[obase + r.dst + j] = img.h[r.h0 + j];
         }
@@ -998,6 +1008,10 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
   } else if (lane == 0) {
     base_out[t] = obase;
     count_out[t] = cnt[t].rows;
+    if (run_out) {
+      img.run_base[t] = pbase;
+      img.run_cnt[t] = cnt[t].gathers;
+    }
   }
 }
 
@@ -1055,6 +1069,22 @@ void launch_msg_copy_dev(const MsgPiece* pieces, const uint64_t* n_pieces, uint6
   if (!cap_g) return;
   hipLaunchKernelGGL(k_msg_copy, dim3((unsigned)std::min<uint64_t>((cap_g + 3) / 4, kMaxWaveBlocks)), dim3(256), 0, s,
                      pieces, cap_g, h, out, n_pieces);
+}
+
+__global__ __launch_bounds__(256) void k_msg_runs_of(uint32_t n, const uint64_t* __restrict__ base,
+                                                     const uint32_t* __restrict__ count, MsgPiece* __restrict__ runs,
+                                                     uint64_t* __restrict__ run_base, uint32_t* __restrict__ run_cnt) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  runs[t] = MsgPiece{(uint32_t)base[t], count[t], base[t]};
+  run_base[t] = t;
+  run_cnt[t] = 1u;
+}
+
+void launch_msg_runs_of(uint32_t n, const uint64_t* base, const uint32_t* count, MsgPiece* runs, uint64_t* run_base,
+                        uint32_t* run_cnt, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_msg_runs_of, dim3((n + 255) / 256), dim3(256), 0, s, n, base, count, runs, run_base, run_cnt);
 }
 
 __global__ void k_msg_gate(const TopicOff* tot, uint64_t cap_rows, uint64_t cap_g, uint32_t* gate, uint64_t* n_pieces) {

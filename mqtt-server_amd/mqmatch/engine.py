@@ -93,6 +93,17 @@ class MsgResult(C.Structure):
                 ("count", C.c_void_p), ("handles", C.c_void_p), ("n_handles", C.c_uint64)]
 
 
+class MsgRunsResult(C.Structure):  # mq_msg_runs_result
+    _fields_ = [("n_filters", C.c_uint32), ("reserved", C.c_uint32), ("run_base", C.c_void_p),
+                ("n_runs", C.c_void_p), ("base", C.c_void_p), ("count", C.c_void_p), ("runs", C.c_void_p),
+                ("n_runs_total", C.c_uint64), ("handles", C.c_void_p), ("n_handles", C.c_uint64),
+                ("n_expanded", C.c_uint64)]
+
+
+# mq_msg_run: first handle, count, where the run starts in the batch's expanded output
+MSG_RUN_DT = np.dtype([("first", np.uint32), ("count", np.uint32), ("at", np.uint64)])
+
+
 class AclResult(C.Structure):
     _fields_ = [("n_pairs", C.c_uint64), ("matched", C.c_void_p), ("n_elems", C.c_void_p),
                 ("elem_base", C.c_void_p), ("elems", C.c_void_p)]
@@ -121,7 +132,8 @@ EXPORTS = [
     "mq_acl_match_batch", "mq_select_shared_device", "mq_match_spans", "mq_match_spans_device",
     "mq_spans_expand", "mq_set_option", "mq_match_spans_begin", "mq_match_spans_end",
     "mq_match_spans_end_host", "mq_device_check", "mq_match_spans_submit", "mq_match_spans_wait",
-    "mq_unsubscribe_bulk", "mq_thread_warm",
+    "mq_unsubscribe_bulk", "mq_thread_warm", "mq_messages_runs_device", "mq_messages_runs_batch",
+    "mq_msg_runs_expand",
 ]
 
 CFG_SELECT_SHARED = 1  # MQ_CFG_SELECT_SHARED
@@ -186,6 +198,10 @@ def lib():
                                          C.c_uint64, C.POINTER(C.POINTER(AclResult))]),
         "mq_messages_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MsgResult))]),
         "mq_messages_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MsgResult)]),
+        "mq_messages_runs_device": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.POINTER(MsgRunsResult)]),
+        "mq_messages_runs_batch": (C.c_int, [vp, _u8p, _u64p, C.c_uint32, C.POINTER(C.POINTER(MsgRunsResult))]),
+        "mq_msg_runs_expand": (C.c_int, [C.POINTER(MsgRunsResult), C.c_uint32, C.c_uint32, _u64p, C.c_uint64,
+                                         _u64p]),
         "mq_result_free": (None, [vp]),
         "mq_sync": (C.c_int, [vp, vp]),
         "mq_index_stats": (C.c_int, [vp, C.POINTER(Stats)]),
@@ -610,6 +626,43 @@ class Engine:
             lib().mq_result_free(rp)
         return base, count, hs
 
+    def messages_runs_batch(self, bytes_, offs, expand=False):
+        """mq_messages_runs_batch -> dict of numpy arrays: run_base, n_runs, base, count, runs
+        (MSG_RUN_DT) and handles (the array the runs index); with expand, also the expanded
+        (base, count, handles) through mq_msg_runs_expand."""
+        n = len(offs) - 1
+        rp = C.POINTER(MsgRunsResult)()
+        _check(lib().mq_messages_runs_batch(self.h, _p(bytes_, _u8p), _p(offs, _u64p), n, C.byref(rp)),
+               "mq_messages_runs_batch")
+        try:
+            r = rp.contents
+
+            def arr(ptr, count, dtype):
+                if count == 0 or not ptr:
+                    return np.zeros(0, dtype)
+                buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+                return np.frombuffer(buf, dtype).copy()
+            out = {"run_base": arr(r.run_base, n, np.uint64), "n_runs": arr(r.n_runs, n, np.uint32),
+                   "base": arr(r.base, n, np.uint64), "count": arr(r.count, n, np.uint32),
+                   "runs": arr(r.runs, r.n_runs_total, MSG_RUN_DT), "handles": arr(r.handles, r.n_handles, np.uint64),
+                   "n_expanded": int(r.n_expanded)}
+            if expand:
+                hs = np.zeros(int(r.n_expanded), np.uint64)
+                got = C.c_uint64(0)
+                _check(lib().mq_msg_runs_expand(rp, 0, n, _p(hs, _u64p), len(hs), C.byref(got)), "mq_msg_runs_expand")
+                assert got.value == len(hs)
+                out["expanded"] = hs
+        finally:
+            lib().mq_result_free(rp)
+        return out
+
+    def messages_runs_device(self, d_bytes, d_offs, n, stream=None):
+        r = MsgRunsResult()
+        _check(lib().mq_messages_runs_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_offs), n,
+                                             C.c_void_p(stream) if stream else None, C.byref(r)),
+               "mq_messages_runs_device")
+        return r
+
     def messages_device(self, d_bytes, d_offs, n, stream=None):
         r = MsgResult()
         _check(lib().mq_messages_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_offs), n,
@@ -853,6 +906,23 @@ def device_messages(r, n):
         if a.nbytes and p:
             assert hip.hipMemcpy(a.ctypes.data, p, a.nbytes, 2) == 0  # hipMemcpyDeviceToHost
     return base, count, hs
+
+
+def device_messages_runs(r, n):
+    """Copy a DEVICE Messages runs result (mq_messages_runs_device) to the host: a dict as
+    Engine.messages_runs_batch returns (the handle array the runs index copied whole)."""
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipDeviceSynchronize() == 0
+    out = {"run_base": np.zeros(n, np.uint64), "n_runs": np.zeros(n, np.uint32), "base": np.zeros(n, np.uint64),
+           "count": np.zeros(n, np.uint32), "runs": np.zeros(int(r.n_runs_total), MSG_RUN_DT),
+           "handles": np.zeros(int(r.n_handles), np.uint64), "n_expanded": int(r.n_expanded)}
+    for k, p in (("run_base", r.run_base), ("n_runs", r.n_runs), ("base", r.base), ("count", r.count),
+                 ("runs", r.runs), ("handles", r.handles)):
+        a = out[k]
+        if a.nbytes and p:
+            assert hip.hipMemcpy(a.ctypes.data, p, a.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+    return out
 
 
 ROW_IDENT = 0x40000000  # MQ_ROW_IDENT (include/mqmatch.h)

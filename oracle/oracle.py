@@ -86,6 +86,7 @@ def lib():
     L.orc_root_children.argtypes = [C.c_void_p]
     L.orc_root_children.restype = C.c_uint64
     L.orc_handle_digests.argtypes = [_u64p, _u32p, _u64p, C.c_uint64, C.c_uint32, _u64p]
+    L.orc_run_digests.argtypes = [_u64p, _u32p, _u32p, _u64p, C.c_uint64, C.c_uint32, _u64p]
     _LIB = L
     return L
 
@@ -141,6 +142,20 @@ def handle_digests(base, count, handles, nthreads=8):
     dig = np.zeros(n, np.uint64)
     lib().orc_handle_digests(_ptr(base, _u64p), _ptr(count, _u32p), _ptr(handles, _u64p), n, nthreads,
                              _ptr(dig, _u64p))
+    return dig
+
+
+def run_digests(res, nthreads=8):
+    """Per-filter digests of an engine Messages runs result (a dict of run_base, n_runs, runs,
+    handles: Engine.messages_runs_batch / engine.device_messages_runs), as handle_digests."""
+    n = len(res["n_runs"])
+    rb = np.ascontiguousarray(res["run_base"], np.uint64)
+    nr = np.ascontiguousarray(res["n_runs"], np.uint32)
+    runs = np.ascontiguousarray(res["runs"]).view(np.uint32)
+    hs = np.ascontiguousarray(res["handles"], np.uint64)
+    dig = np.zeros(n, np.uint64)
+    lib().orc_run_digests(_ptr(rb, _u64p), _ptr(nr, _u32p), _ptr(runs, _u32p), _ptr(hs, _u64p), n, nthreads,
+                          _ptr(dig, _u64p))
     return dig
 
 

@@ -343,6 +343,32 @@ int orc_handle_digests(const uint64_t* base, const uint32_t* count, const uint64
   return 0;
 }
 
+// The same digest of an engine Messages runs result (mq_messages_runs_*): filter i's handles are
+// handles[r.first, + r.count) over its runs runs[run_base[i], + n_runs[i]) (runs: first u32,
+// count u32, at u64 — mq_msg_run), any order.
+int orc_run_digests(const uint64_t* run_base, const uint32_t* n_runs, const uint32_t* runs, const uint64_t* handles,
+                    uint64_t n, uint32_t nthreads, uint64_t* digests) {
+  if (nthreads == 0) nthreads = 1;
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nthreads; t++) {
+    th.emplace_back([&, t] {
+      std::vector<uint64_t> hs;
+      for (uint64_t i = t; i < n; i += nthreads) {
+        hs.clear();
+        for (uint64_t k = run_base[i]; k < run_base[i] + n_runs[i]; k++)
+          hs.insert(hs.end(), handles + runs[4 * k], handles + runs[4 * k] + runs[4 * k + 1]);
+        std::sort(hs.begin(), hs.end());
+        uint64_t d = 0x6d716d61ull;
+        d = fold(d, hs.size());
+        for (uint64_t x : hs) d = fold(d, x);
+        digests[i] = d;
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  return 0;
+}
+
 // CPU baseline: `nthreads` std::threads each call Subscribers(topic) on the
 // frozen shared index, as Go connection goroutines do (topics.go:583 takes no writer lock).
 // Returns wall seconds; *sink receives a value derived from every result.

@@ -345,13 +345,6 @@ static void TestConcurrentReadersAndUpdates() {
   // device set-up outside the timing: the first batches allocate the device buffers and both
   // host-result stages (one-time costs, not update latency)
   for (int k = 0; k < 6; k++) ix.SubscribersBatch(std::vector<std::string>{"s/" + std::to_string(k) + "/x", "t/0"});
-  // ... and the update path's: an update then a match uploads the dirty pages through the staging
-  // buffers and the scatter kernel for the first time
-  for (int k = 0; k < 2; k++) {
-    ix.Subscribe("warm", S("w/" + std::to_string(k), 1));
-    ix.SubscribersBatch(std::vector<std::string>{"w/" + std::to_string(k), "t/0"});
-    ix.Unsubscribe("w/" + std::to_string(k), "warm");
-  }
   std::atomic<bool> stop{false}, done{false};
   std::atomic<int> bad{0}, late{0};
   std::atomic<long> progress[5];

@@ -28,7 +28,7 @@ def test_library_exports_all_symbols():
     L = E.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.mq_abi_version() == 8
+    assert L.mq_abi_version() == 9
 
 
 def test_errors_are_reported():
@@ -239,7 +239,7 @@ def test_header_compiles_as_c(tmp_path):
     if cc is None:
         pytest.skip("no C compiler")
     src = tmp_path / "h.c"
-    src.write_text('#include "mqmatch.h"\nint main(void) { return (int)MQ_ABI_VERSION - 8; }\n')
+    src.write_text('#include "mqmatch.h"\nint main(void) { return (int)MQ_ABI_VERSION - 9; }\n')
     r = subprocess.run([cc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-fsyntax-only",
                         "-I", os.path.join(REPO, "include"), str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr

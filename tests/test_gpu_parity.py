@@ -1008,6 +1008,99 @@ def test_messages_workload_parity(image, spec_mb, edges, gpu_available):
         assert d == od[i], i
 
 
+def _runs_sets(res, n):
+    """Per-filter sorted handle lists of a Messages runs result (dict: run_base, n_runs, runs,
+    handles), with each filter's runs checked to tile its [base, + count) of the expanded output."""
+    out = []
+    hs = res["handles"]
+    for i in range(n):
+        rb, nr = int(res["run_base"][i]), int(res["n_runs"][i])
+        runs = res["runs"][rb:rb + nr]
+        got = []
+        at = sorted((int(r["at"]), int(r["count"])) for r in runs)
+        pos = int(res["base"][i])
+        for a, c in at:  # the runs tile the filter's part of the expanded output
+            assert a == pos, (i, at)
+            pos += c
+        assert pos == int(res["base"][i]) + int(res["count"][i]), i
+        for r in runs:
+            got += hs[int(r["first"]):int(r["first"]) + int(r["count"])].tolist()
+        out.append(sorted(got))
+    return out
+
+
+@pytest.mark.parametrize("q6", [False, True])
+@pytest.mark.parametrize("seed", range(3))
+def test_messages_runs_parity(seed, q6, gpu_available):
+    """Messages as runs at the boundary (mq_messages_runs_batch / _device):
+    each filter's runs index the retained image's handles (or, q6 — the "" entry live, the
+    particle walk — the batch's own, one run per filter), tile its part of the expanded output,
+    expand (mq_msg_runs_expand) to the handle result, and equal the oracle (topics.go:525-579)."""
+    import torch
+    from mqmatch import engine as E
+    r = random.Random(3000 + seed)
+    topics = ["/".join(r.choice(MSEGS) for _ in range(r.randint(1, 5))) for _ in range(400)]
+    topics = [t for t in topics if t != ""] + ([""] if q6 else [])
+    e, o = E.Engine(), O.OracleIndex()
+    for i, t in enumerate(topics):
+        pl = 0 if (r.random() < 0.1 and t != "") else 1
+        ret = r.random() < 0.9
+        assert e.retain_message(t, i + 1, pl, ret) == o.retain_message(t, i + 1, pl, ret), t
+    for t in topics[::11]:
+        if t:
+            e.retained_delete(t)
+            o.retained_delete(t)
+    filters = ["/".join(r.choice(MSEGS + ["+", "+", "#"]) for _ in range(r.randint(1, 5))) for _ in range(300)]
+    filters += ["#", "+", "+/+", "$SYS/#", "$SYS/+", "a/#", "a/+/#", "", "a", "a/b", "+/#", "+/+/#"]
+    fb, fo = E.pack_strings(filters)
+    n = len(filters)
+    want = [o.messages(f) for f in filters]
+    res = e.messages_runs_batch(fb, fo, expand=True)
+    assert _runs_sets(res, n) == want
+    for i in range(n):  # the expansion lays each filter out at its base
+        b, c = int(res["base"][i]), int(res["count"][i])
+        assert sorted(res["expanded"][b:b + c].tolist()) == want[i], filters[i]
+    d_fb = torch.from_numpy(np.concatenate([fb, np.zeros(16, np.uint8)])).cuda()
+    d_fo = torch.from_numpy(fo.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    dres = E.device_messages_runs(e.messages_runs_device(d_fb.data_ptr(), d_fo.data_ptr(), n), n)
+    assert _runs_sets(dres, n) == want
+    assert (dres["n_runs"] == 1).all() == q6  # (q6: the particle walk's one run per filter)
+    e.close()
+
+
+@pytest.mark.parametrize("export", [1, 0])
+def test_messages_runs_workload(export, gpu_available):
+    """Runs on a config-5-shaped workload (100k retained, 5k filters; wide fan-outs exported to
+    work items or not): device and host runs digest-equal to the oracle, and far fewer runs than
+    handles (the point of the format)."""
+    import torch
+    from mqmatch import workload as W
+    from mqmatch import engine as E
+    rb, ro, hd, rh = W.gen_retained(100000, n_sys=1000, seed=61)
+    fb, fo = W.gen_msg_filters(rh, 5000, seed=62)
+    n = len(fo) - 1
+    eng, orc = E.Engine(), O.OracleIndex()
+    eng.set_option(E.OPT_MSG_EXPORT, export)
+    eng.retain_bulk(rb, ro, hd)
+    orc.retain_bulk(rb, ro, hd)
+    od, ocnt, _ = orc.messages_digest_batch(fb, fo)
+    res = eng.messages_runs_batch(fb, fo)
+    assert (res["count"] == ocnt).all()
+    assert (O.run_digests(res) == od).all()
+    d_fb = torch.from_numpy(np.concatenate([fb, np.zeros(16, np.uint8)])).cuda()
+    d_fo = torch.from_numpy(fo.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    for _ in range(2):  # (the second batch on the buffers the first left: one synchronisation)
+        dres = E.device_messages_runs(eng.messages_runs_device(d_fb.data_ptr(), d_fo.data_ptr(), n), n)
+        assert (dres["count"] == ocnt).all()
+        assert (O.run_digests(dres) == od).all()
+    assert len(dres["runs"]) * 4 < int(ocnt.sum())
+    base, count, hs = eng.messages_batch(fb, fo)  # the handle format after runs: unchanged
+    assert (O.handle_digests(base, count, hs) == od).all()
+    eng.close()
+
+
 def test_messages_edge_table_tiers(gpu_available):
     """The retained image's edge table at each of its size tiers (device.cpp build_image: at most
     1/16 full within the budget, 1/8 within 4x the budget, else ~1/4 or denser). The product budget

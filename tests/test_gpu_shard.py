@@ -179,3 +179,59 @@ def test_sharded_deep_ties_match_oracle(device, gpu_available):
     assert len(bad) == 0, f"topics {[topics[i] for i in bad]} differ"
     for e in shards:
         e.check()
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_sharded_deep_filter_id_reuse(device, gpu_available):
+    """A filter id that named a deep filter (beyond 32 levels: a DeepTail entry, layout.h) is reused
+    for a 32-level filter once the deep one is gone from every shard: the entry went
+    with its last holder (Index::deep_unref), so the 32-level filter's tie with a deeper filter on
+    another shard is ordered as its proper prefix — first — and the merged
+    rows equal the oracle's."""
+    from mqmatch import engine as E
+    shards = [E.Engine(shard=k, n_shards=2) for k in range(2)]
+    o = O.OracleIndex()
+
+    def sub(c, f, fid, q, nl=False, ident=0):
+        own = [e.subscribe(f, c, fid, q, 1 if nl else 0, ident) for e in shards]
+        o.subscribe(f"c{c}", f, q, ident, nl, client_id=c, filter_id=fid)
+        return own
+
+    def unsub(c, f):
+        for e in shards:
+            e.unsubscribe(f, c)
+        o.unsubscribe(f, f"c{c}")
+
+    def owner(f):
+        own = [e.subscribe(f, 999, 77, 0, 0, 0) for e in shards]
+        for e in shards:
+            e.unsubscribe(f, 999)
+        return own.index(1)
+
+    for j in range(64):  # a 32-level prefix whose filter and its '#' child live on different shards
+        pre = "/".join(f"p{j}x{i}" for i in range(32))
+        if owner(pre) != owner(pre + "/#"):
+            break
+    else:
+        pytest.fail("no prefix splits over the shards")
+    topics = [pre, pre + "/x", pre + "/x/y"]
+    tb, to = E.pack_strings(topics)
+    # fid 5 names the deep filter pre/#, which reaches the device, then leaves every shard
+    for c in range(12):
+        sub(c, pre + "/#", 5, c % 3)
+        sub(c, pre + "/x/+", 8, (c + 1) % 3)
+    _sharded_digests(shards, tb, to, device=device)
+    for c in range(12):
+        unsub(c, pre + "/#")
+    # fid 5 reused for the 32-level pre; pre/# back under fid 6
+    for c in range(12):
+        sub(c, pre, 5, c % 3, nl=c % 4 == 0, ident=c % 5)
+        sub(c, pre + "/#", 6, (c + 2) % 3, ident=(c + 1) % 4)
+    dg, cnt, n_ents = _sharded_digests(shards, tb, to, device=device)
+    od, ocnt, _ = o.digest_batch(tb, to, nthreads=2)
+    assert n_ents > 0
+    assert (cnt == ocnt).all()
+    bad = np.nonzero(dg != od)[0]
+    assert len(bad) == 0, f"topics {[topics[i] for i in bad]} differ"
+    for e in shards:
+        e.check()
