@@ -18,16 +18,18 @@
 // load), waits up to max_delay for more; a lone topic on an idle stage is matched at once.
 // max_batch bounds a batch.
 //
-// Errors: a match call that throws is tried once more (a transient failure costs one retry, not
-// the batch); if that throws too, every ticket of the batch rethrows it from get() — the callers
-// of that one batch see the error, the stage goes on with the next batch (the Go shim's batcher
-// answers them with empty results instead, go/topics_gpu.go).
+// Errors: a match call that throws is tried again after 0, 1, 4, 16, 64 and 256 ms (kRetryDelays:
+// a transient failure — a kernel guard tripped by one batch, a device reset — costs retries, not
+// the batch's deliveries); if every attempt throws, every ticket of the batch rethrows the error
+// from get(): the callers see it, nothing is answered empty (there is no CPU matching path), and
+// the stage goes on with the next batch. The Go shim's batcher does the same (go/topics_gpu.go).
 //   PublishBatcher      tickets of Subscribers (the Go-shaped maps, TopicsIndex::SubscribersBatch)
 //   PublishViewBatcher  tickets of TopicView (the recipients as a view over the batch's span
 //                       result, TopicsIndex::SubscribersViews: no maps are built)
 #pragma once
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -76,7 +78,8 @@ class BasicBatcher {
   struct Stats {
     uint64_t batches = 0;     // match calls
     uint64_t retried = 0;     // batches whose first match call failed
-    uint64_t failed = 0;      // batches whose retry failed too (their tickets throw)
+    uint64_t attempts = 0;    // match calls that failed and were tried again
+    uint64_t failed = 0;      // batches whose every attempt failed (their tickets throw)
     uint64_t topics = 0;      // topics matched
     uint64_t largest = 0;     // largest batch
     // the dispatcher's time (ns): waiting for topics, sealing, in the match call, completing
@@ -217,7 +220,12 @@ class BasicBatcher {
       std::exception_ptr err;
       const auto c2 = Clock::now();
       bool retried = false;
-      for (int attempt = 0; attempt < 2 && !res; attempt++) {
+      uint64_t again = 0;
+      for (size_t attempt = 0; attempt <= kRetryDelays.size() && !res; attempt++) {
+        if (attempt) {
+          again++;
+          if (kRetryDelays[attempt - 1].count()) std::this_thread::sleep_for(kRetryDelays[attempt - 1]);
+        }
         try {
           err = nullptr;
           res = match_(batch);
@@ -245,6 +253,7 @@ class BasicBatcher {
       std::lock_guard<std::mutex> lk(mu_);
       st_.batches++;
       st_.retried += retried;
+      st_.attempts += again;
       st_.failed += err != nullptr;
       st_.topics += n;
       st_.largest = std::max<uint64_t>(st_.largest, n);
@@ -255,6 +264,10 @@ class BasicBatcher {
     }
   }
 
+  // the waits before a failed batch's further attempts (about a third of a second in all)
+  static constexpr std::array<std::chrono::milliseconds, 6> kRetryDelays = {
+      std::chrono::milliseconds(0), std::chrono::milliseconds(1),  std::chrono::milliseconds(4),
+      std::chrono::milliseconds(16), std::chrono::milliseconds(64), std::chrono::milliseconds(256)};
   MatchFn match_;
   const size_t max_batch_;
   const std::chrono::microseconds max_delay_;

@@ -203,11 +203,18 @@ func (r *RetainedPackets) Delete(id string) {
 // stored subscriptions.
 //
 // Errors: the reference's index cannot fail; the engine can (a lost device, MQ_EIO from a kernel
-// guard). An update that fails is logged and answers false (nothing changed); a match batch that
-// fails is tried once more, then logged, and its callers get empty results — one publish is lost,
-// the broker stays up (server.go:984-1021 delivers to no one for an empty Subscribers).
+// guard). An update that fails is logged and answers false (nothing changed). A match batch that
+// fails is tried again with backoff (retryDelays: about a third of a second in all), so a
+// transient failure costs latency, not deliveries. A batch that fails every attempt has no answer
+// to give — there is no CPU matching path — and it is not answered empty (round 6: that silently
+// dropped the publish): SubscribersE / MessagesE return the error, and Subscribers / Messages,
+// whose reference signatures cannot, hand it to EngineFailure (default: panic, the broker stops
+// rather than acknowledge publishes it did not deliver; a broker may set it to log and carry on).
 type TopicsIndex struct {
 	Retained *RetainedPackets
+	// EngineFailure is called when Subscribers or Messages cannot be answered (the batch failed
+	// every attempt); nil: panic. op is "Subscribers" or "Messages", item the topic or filter.
+	EngineFailure func(op, item string, err error)
 	h        *C.mq_index
 	upd      sync.Mutex
 	tables   sync.RWMutex
@@ -484,6 +491,21 @@ func (x *TopicsIndex) Messages(filter string) []packets.Packet {
 		}
 		return pks
 	}
+	pks, err := x.MessagesE(filter)
+	if err != nil {
+		x.engineFailed("Messages", filter, err)
+		return []packets.Packet{}
+	}
+	return pks
+}
+
+// MessagesE is Messages with the engine's failure returned (wildcard filters: a batch that failed
+// every attempt).
+func (x *TopicsIndex) MessagesE(filter string) ([]packets.Packet, error) {
+	if len(filter) == 0 || x.Retained.Len() == 0 ||
+		(!strings.ContainsRune(filter, '#') && !strings.ContainsRune(filter, '+')) {
+		return x.Messages(filter), nil
+	}
 	x.msgOnce.Do(func() { x.msgBatcher = NewMessagesBatcher(x, DefaultMaxBatch, DefaultMinFill, DefaultMaxDelay) })
 	return x.msgBatcher.get(filter)
 }
@@ -503,40 +525,49 @@ func (x *TopicsIndex) MessagesBatch(filters []string) ([][]packets.Packet, error
 	return out, nil
 }
 
-// msgView is one mq_messages_batch result, shared by the callers whose filters it matched.
+// msgView is one mq_messages_runs_batch result, shared by the callers whose filters it matched:
+// each filter's handles as runs of the retained image's handle array (round 6: the engine no longer
+// copies every handle out; the runs are expanded here, on the caller's goroutine).
 type msgView struct {
-	x      *TopicsIndex
-	r      *C.mq_msg_result
-	stamp  uint64
-	refs   atomic.Int32
-	base   []C.uint64_t
-	count  []C.uint32_t
-	handle []uint64
+	x       *TopicsIndex
+	r       *C.mq_msg_runs_result
+	stamp   uint64
+	refs    atomic.Int32
+	runBase []C.uint64_t
+	nRuns   []C.uint32_t
+	count   []C.uint32_t
+	runs    []C.mq_msg_run
+	handle  []uint64
 }
 
 func (x *TopicsIndex) matchMessages(filters []string) (*msgView, error) {
 	stamp := x.ep.begin()
 	buf, offs := pack(filters)
-	var r *C.mq_msg_result
-	if _, err := check(C.mq_messages_batch(x.h, (*C.uint8_t)(&buf[0]), (*C.uint64_t)(&offs[0]), C.uint32_t(len(filters)), &r),
-		"mq_messages_batch"); err != nil {
+	var r *C.mq_msg_runs_result
+	if _, err := check(C.mq_messages_runs_batch(x.h, (*C.uint8_t)(&buf[0]), (*C.uint64_t)(&offs[0]), C.uint32_t(len(filters)), &r),
+		"mq_messages_runs_batch"); err != nil {
 		x.ep.end(stamp)
 		return nil, err
 	}
 	v := &msgView{x: x, r: r, stamp: stamp}
-	v.base = unsafe.Slice(r.base, int(r.n_filters))
-	v.count = unsafe.Slice(r.count, int(r.n_filters))
+	n := int(r.n_filters)
+	v.runBase = unsafe.Slice(r.run_base, n)
+	v.nRuns = unsafe.Slice(r.n_runs, n)
+	v.count = unsafe.Slice(r.count, n)
+	v.runs = unsafe.Slice(r.runs, int(r.n_runs_total))
 	v.handle = unsafe.Slice((*uint64)(unsafe.Pointer(r.handles)), int(r.n_handles))
 	return v, nil
 }
 
-// get resolves filter i's handles to packets, on the caller's goroutine.
+// get expands filter i's runs and resolves the handles to packets, on the caller's goroutine.
 func (v *msgView) get(i int) []packets.Packet {
-	hs := v.handle[v.base[i] : v.base[i]+C.uint64_t(v.count[i])]
-	topics := make([]string, len(hs))
+	topics := make([]string, 0, int(v.count[i]))
+	rs := v.runs[v.runBase[i] : v.runBase[i]+C.uint64_t(v.nRuns[i])]
 	v.x.tables.RLock()
-	for k, h := range hs {
-		topics[k] = v.x.topics.strs[h]
+	for _, run := range rs {
+		for _, h := range v.handle[run.first : run.first+run.count] {
+			topics = append(topics, v.x.topics.strs[h])
+		}
 	}
 	v.x.tables.RUnlock()
 	pks := []packets.Packet{}
@@ -561,8 +592,28 @@ func (v *msgView) release() {
 // keeps calling Subscribers unchanged. The maps are built here, on the caller's goroutine, from the
 // batch's shared span result, as the reference builds them on every connection goroutine.
 func (x *TopicsIndex) Subscribers(topic string) *Subscribers {
+	s, err := x.SubscribersE(topic)
+	if err != nil {
+		x.engineFailed("Subscribers", topic, err)
+		return emptySubscribers()
+	}
+	return s
+}
+
+// SubscribersE is Subscribers with the engine's failure returned (a batch that failed every
+// attempt) — for a caller that can refuse the publish instead (INTEGRATION.md §3).
+func (x *TopicsIndex) SubscribersE(topic string) (*Subscribers, error) {
 	x.batcherOnce.Do(func() { x.batcher = NewMatchBatcher(x, DefaultMaxBatch, DefaultMinFill, DefaultMaxDelay) })
 	return x.batcher.get(topic)
+}
+
+// engineFailed: Subscribers / Messages could not be answered (EngineFailure, default panic).
+func (x *TopicsIndex) engineFailed(op, item string, err error) {
+	if x.EngineFailure != nil {
+		x.EngineFailure(op, item, err)
+		return
+	}
+	panic(fmt.Errorf("mqmatch: %s(%q) failed on every attempt: %w", op, item, err))
 }
 
 func emptySubscribers() *Subscribers {
@@ -606,21 +657,25 @@ type batchReply[T any] struct {
 // previous batch is done — under load, what arrived while it was matched — and matches the batch
 // with one engine call (run). When the previous batch held more than one request (there is
 // concurrent load), a batch with fewer than minFill items first waits up to maxDelay for more; a
-// lone request on an idle stage is matched at once. A failed engine call is tried once more; if
-// that fails too, every caller of the batch gets the empty answer (the error is logged by check).
+// lone request on an idle stage is matched at once. A failed engine call is tried again after each
+// of retryDelays; if every attempt fails, every caller of the batch gets the error (logged by
+// check), never an empty answer.
 type batcher[T any] struct {
 	run      func(items []string) (batchView[T], error)
-	empty    func() T
 	in       chan batchReq[T]
 	maxBatch int
 	minFill  int
 	maxDelay time.Duration
 	done     chan struct{}
 	replies  sync.Pool
-	failed   atomic.Uint64 // batches whose callers got the empty answer
+	failed   atomic.Uint64 // batches whose callers got the error
 }
 
-func newBatcher[T any](run func([]string) (batchView[T], error), empty func() T, maxBatch, minFill int,
+// retryDelays: the waits before a failed batch's further attempts (about a third of a second).
+var retryDelays = []time.Duration{0, time.Millisecond, 4 * time.Millisecond, 16 * time.Millisecond,
+	64 * time.Millisecond, 256 * time.Millisecond}
+
+func newBatcher[T any](run func([]string) (batchView[T], error), maxBatch, minFill int,
 	maxDelay time.Duration) *batcher[T] {
 	if maxBatch <= 0 {
 		maxBatch = DefaultMaxBatch
@@ -628,28 +683,30 @@ func newBatcher[T any](run func([]string) (batchView[T], error), empty func() T,
 	if minFill <= 0 || minFill > maxBatch {
 		minFill = maxBatch
 	}
-	b := &batcher[T]{run: run, empty: empty, in: make(chan batchReq[T], 4*maxBatch), maxBatch: maxBatch,
+	b := &batcher[T]{run: run, in: make(chan batchReq[T], 4*maxBatch), maxBatch: maxBatch,
 		minFill: minFill, maxDelay: maxDelay, done: make(chan struct{})}
 	b.replies.New = func() any { return make(chan batchReply[T], 1) }
 	go b.loop()
 	return b
 }
 
-// get enqueues item, waits for the batch it joins and builds its answer.
-func (b *batcher[T]) get(item string) T {
+// get enqueues item, waits for the batch it joins and builds its answer (or returns the batch's
+// error: every attempt failed).
+func (b *batcher[T]) get(item string) (T, error) {
 	r := b.replies.Get().(chan batchReply[T])
 	b.in <- batchReq[T]{item, r}
 	rep := <-r
 	b.replies.Put(r)
 	if rep.err != nil {
-		return b.empty()
+		var zero T
+		return zero, rep.err
 	}
 	v := rep.view.get(rep.i)
 	rep.view.release()
-	return v
+	return v, nil
 }
 
-// Failed counts the batches whose callers got the empty answer.
+// Failed counts the batches whose callers got the error.
 func (b *batcher[T]) Failed() uint64 { return b.failed.Load() }
 
 // Close matches what is queued and stops the loop; no get may follow.
@@ -716,8 +773,9 @@ func (b *batcher[T]) loop() {
 			items = append(items, r.item)
 		}
 		v, err := b.call(items)
-		if err != nil {
-			v, err = b.call(items) // once more: a transient failure costs one retry, not the batch
+		for k := 0; err != nil && k < len(retryDelays); k++ { // a transient failure costs retries, not the batch
+			time.Sleep(retryDelays[k])
+			v, err = b.call(items)
 		}
 		if err != nil {
 			b.failed.Add(1)
@@ -764,7 +822,7 @@ func NewMatchBatcher(x *TopicsIndex, maxBatch, minFill int, maxDelay time.Durati
 		}
 		return v, nil
 	}
-	return newBatcher[*Subscribers](run, emptySubscribers, maxBatch, minFill, maxDelay)
+	return newBatcher[*Subscribers](run, maxBatch, minFill, maxDelay)
 }
 
 // NewMessagesBatcher starts a Messages batching stage over x (wildcard filters only).
@@ -776,8 +834,7 @@ func NewMessagesBatcher(x *TopicsIndex, maxBatch, minFill int, maxDelay time.Dur
 		}
 		return v, nil
 	}
-	return newBatcher[[]packets.Packet](run, func() []packets.Packet { return []packets.Packet{} }, maxBatch, minFill,
-		maxDelay)
+	return newBatcher[[]packets.Packet](run, maxBatch, minFill, maxDelay)
 }
 
 func (v *msgView) setRefs(n int)  { v.refs.Store(int32(n)) }

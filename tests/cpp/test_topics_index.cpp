@@ -561,42 +561,6 @@ static void TestViewHeldAcrossUpdates() {
 // The batching stage's failure path: a match call that fails (an injected MQ_EIO, as a kernel
 // guard would raise) is retried once; when the retry fails as well, that batch's tickets throw
 // the EngineError and the stage goes on with the next batch.
-static void TestBatcherEngineError() {
-  TopicsIndex ix;
-  for (int i = 0; i < 20; i++) ix.Subscribe("e" + std::to_string(i), S("e/+", 1));
-  std::atomic<int> fail_next{0};
-  mq::host::BasicBatcher<mq::host::ViewsPolicy> b(
-      [&](const mq::host::PackedTopics& t) {
-        if (fail_next > 0) {
-          fail_next--;
-          throw mq::host::EngineError(MQ_EIO, "injected MQ_EIO");
-        }
-        return ix.SubscribersSpans(t);
-      },
-      64, std::chrono::microseconds(100));
-  fail_next = 1;  // the first call fails, its retry succeeds
-  size_t n = 0;
-  b.Submit("e/a").get().for_each_row([&](const mq_client_row&) { n++; });
-  REQUIRE(n == 20);
-  fail_next = 2;  // both fail: the ticket throws
-  bool threw = false;
-  try {
-    b.Submit("e/b").get();
-  } catch (const mq::host::EngineError& e) {
-    threw = e.code == MQ_EIO;
-  }
-  REQUIRE(threw);
-  n = 0;  // the next batch is matched as usual
-  b.Submit("e/c").get().for_each_row([&](const mq_client_row&) { n++; });
-  REQUIRE(n == 20);
-  auto st = b.stats();  // (a batch's stats are recorded just after its tickets complete)
-  for (int i = 0; i < 1000 && st.batches < 3; i++) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(1));
-    st = b.stats();
-  }
-  REQUIRE(st.retried == 2 && st.failed == 1 && st.batches == 3);
-}
-
 // The batching stage under many submitters, checked against the ORACLE (the CPU restatement of
 // the Go TopicsIndex, oracle/liboracle.so, test infrastructure): 32 threads keep 64 topics each
 // in flight through PublishBatcher; a sample of the tickets is compared with the oracle's
@@ -779,6 +743,59 @@ static void TestBatcherManySubmittersVsOracle() {
   REQUIRE(st.largest > 64);  // submitters' topics were matched together
   orc_free(orc);
 }
+
+// A failing engine (MQ_EIO injected into the batch's match call, as a tripped kernel guard
+// returns it): the batch is tried again with backoff, and its callers get the ORACLE's answer, not
+// an empty one, while the failures last no longer than the retries; a batch that fails every
+// attempt makes its tickets throw (nothing is delivered as an empty Subscribers), and the next
+// batch is matched as usual (server.go:1000-1020).
+static void TestBatcherEngineError() {
+  TopicsIndex ix;
+  void* orc = orc_new();
+  for (int i = 0; i < 20; i++) {
+    const std::string c = "e" + std::to_string(i), f = i % 3 ? "e/+" : "e/#";
+    ix.Subscribe(c, S(f, (uint8_t)(i % 3)));
+    orc_subscribe(orc, c.data(), (uint32_t)c.size(), f.data(), (uint32_t)f.size(), (uint32_t)i, i % 3 ? 1u : 2u,
+                  (uint8_t)(i % 3), 0, 0);
+  }
+  ix.Subscribe("e0", S("e/a", 2, 7));
+  orc_subscribe(orc, "e0", 2, "e/a", 3, 0, 3, 2, 0, 7);
+  std::atomic<int> fail_next{0};
+  mq::host::BasicBatcher<mq::host::MapsPolicy> b(
+      [&](const mq::host::PackedTopics& t) {
+        if (fail_next > 0) {
+          fail_next--;
+          throw mq::host::EngineError(MQ_EIO, "injected MQ_EIO");
+        }
+        return std::make_shared<const std::vector<mq::host::Subscribers>>(ix.SubscribersBatch(t));
+      },
+      64, std::chrono::microseconds(100));
+  for (int k : {1, 3, 6}) {  // k failures in a row: the retries outlast them
+    fail_next = k;
+    for (const char* t : {"e/a", "e/b"}) {
+      auto tk = b.Submit(t);
+      REQUIRE(subscribers_json(tk.get()) == oracle_json(orc, t));
+      REQUIRE(!tk.get().Subscriptions.empty());
+    }
+  }
+  fail_next = 7;  // more than the retries: the ticket throws
+  bool threw = false;
+  try {
+    b.Submit("e/c").get();
+  } catch (const mq::host::EngineError& e) {
+    threw = e.code == MQ_EIO;
+  }
+  REQUIRE(threw);
+  REQUIRE(subscribers_json(b.Submit("e/d").get()) == oracle_json(orc, "e/d"));  // the next batch
+  auto st = b.stats();  // (a batch's stats are recorded just after its tickets complete)
+  for (int i = 0; i < 1000 && st.batches < 8; i++) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    st = b.stats();
+  }
+  REQUIRE(st.batches == 8 && st.retried == 4 && st.failed == 1 && st.attempts == 1 + 3 + 6 + 6);
+  orc_free(orc);
+}
+
 
 // progress on stderr: a test that does not return is named by the last line
 #define RUN(f)                             \
