@@ -201,7 +201,11 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
 
 // A match in two phases (IndexLock): prep() under both locks — it syncs the device image and
 // takes the batch's snapshot (Device::prepare), and for host results reserves their generation —
-// then run() with the device's lock only, while updates change the host image.
+// then run() with the device's lock only, while updates change the host image. What the sync
+// will allocate (arrays that grew, staging for the dirty pages) is allocated first, without `mu`
+// (Device::sync_plan / prealloc). A match holds `mu` only for the sync itself, so it does not wait
+// for announced updates (FifoMutex order is fair): with updates arriving back to back, waiting
+// for none to be announced starved the readers (172 matches during 3,200 updates).
 template <class P, class R>
 int guarded_match(mq_index* idx, P&& prep, R&& run) {
   if (!idx) return fail(MQ_EINVAL, "null index");
@@ -209,12 +213,21 @@ int guarded_match(mq_index* idx, P&& prep, R&& run) {
   IndexLock& L = *idx->lk;
   return caught([&] {
     std::lock_guard<FifoMutex> dlk(L.dev_mu);
-    wait_for_writers(L.views);
     if (slow_on()) slow_begin();
-    {
-      std::lock_guard<FifoMutex> lk(L.mu);
-      prep();
-      if (slow_on()) slow_report("match-prepare", 0.0);
+    for (int round = 0;; round++) {
+      Device::SyncPlan plan;
+      {
+        std::lock_guard<FifoMutex> lk(L.mu);
+        plan = idx->device().sync_plan(*idx->ix);
+        if (!plan.any || round == 2) {  // (still short after two rounds of updates: allocate under mu)
+          prep();
+          if (slow_on()) slow_report("match-prepare", 0.0);
+          break;
+        }
+      }
+      slow_mark("prealloc");
+      idx->dev->prealloc(plan);
+      slow_mark("preallocated");
     }
     slow_mark("unlocked");
     const int r = run();

@@ -144,6 +144,9 @@ void DevMirror<T>::release() {
   if (d) (void)hipFree(d);
   d = nullptr;
   cap = 0;
+  if (spare) (void)hipFree(spare);
+  spare = nullptr;
+  spare_bytes = 0;
 }
 
 void Stager::add(void* dst, const void* src, size_t n) {
@@ -161,9 +164,16 @@ bool DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
     d = nullptr;
     cap = 0;
     cap = std::max<size_t>(std::max(m.h.capacity(), n), 1);
-    slow_mark("mirror-realloc");
-    hip_check(hipMalloc(&d, cap * sizeof(T)), "hipMalloc(mirror)");
-    slow_mark("mirror-malloc");
+    if (spare && spare_bytes >= cap * sizeof(T)) {  // made ahead, outside the handle lock
+      d = static_cast<T*>(spare);
+      cap = spare_bytes / sizeof(T);
+      spare = nullptr;
+      spare_bytes = 0;
+    } else {
+      slow_mark("mirror-realloc");
+      hip_check(hipMalloc(&d, cap * sizeof(T)), "hipMalloc(mirror)");
+      slow_mark("mirror-malloc");
+    }
     epoch = m.epoch;
     full = true;
   }
@@ -367,6 +377,7 @@ Device::~Device() {
   release_retired();
   if (stage_done_) (void)hipEventDestroy(stage_done_);
   pinned_free(h_stage_, h_stage_bytes_);
+  pinned_free(h_stage_spare_, h_stage_spare_bytes_);
   if (h_fast_) (void)hipHostFree(h_fast_);
   for (int k = 0; k < 2; k++) {
     if (copy_done_[k]) (void)hipEventDestroy(copy_done_[k]);
@@ -496,8 +507,20 @@ void Device::sync_ix(Index& ix, hipStream_t s) {
     // returns at once)
     if (h_stage_bytes_ < need) {
       pinned_free(h_stage_, h_stage_bytes_);
-      h_stage_ = pinned_alloc(need);
-      h_stage_bytes_ = need;
+      if (h_stage_spare_ && h_stage_spare_bytes_ >= need) {  // (made ahead: prealloc)
+        h_stage_ = h_stage_spare_;
+        h_stage_bytes_ = h_stage_spare_bytes_;
+        h_stage_spare_ = nullptr;
+        h_stage_spare_bytes_ = 0;
+      } else {
+        slow_mark("stage-alloc");
+        h_stage_ = pinned_alloc(need);
+        h_stage_bytes_ = need;
+      }
+    }
+    if (d_stage_.bytes < need && d_stage_spare_.bytes >= need) {
+      std::swap(d_stage_.p, d_stage_spare_.p);
+      std::swap(d_stage_.bytes, d_stage_spare_.bytes);
     }
     d_stage_.ensure(need);
     uint8_t* hs = static_cast<uint8_t*>(h_stage_);
@@ -537,6 +560,89 @@ void Device::sync_ix(Index& ix, hipStream_t s) {
   synced_version_ = ix.version();
   sync_direct_ = direct;
   syncs_++;
+}
+
+template <class F>
+void Device::each_mirror(const Index& ix, F f) const {
+  Device* me = const_cast<Device*>(this);  // (f gets the mirrors; plan reads, prealloc writes)
+  f(0, me->edges_, ix.edges);
+  f(1, me->walk_, ix.walk);
+  f(2, me->lists_, ix.lists);
+  f(3, me->inls_, ix.inls);
+  f(4, me->msg_, ix.msg);
+  f(5, me->seginfo_, ix.seginfo);
+  f(6, me->segbytes_, ix.segbytes);
+  f(7, me->subs_, ix.subs.m);
+  f(8, me->mref_, ix.mref);
+  f(9, me->mpart_, ix.mpart.m);
+  f(10, me->npair_, ix.npair);
+  f(11, me->pent_, ix.pent.m);
+  f(12, me->plist_, ix.plist.m);
+  f(13, me->shr_, ix.shr.m);
+  f(14, me->inl_, ix.inl.m);
+  f(15, me->children_, ix.children.m);
+  if (ix.sharded()) f(16, me->xinfo_, ix.xinfo);
+  if (ix.deep.size()) {
+    f(17, me->deep_, ix.deep);
+    f(18, me->deep_codes_, ix.deep_codes);
+  }
+}
+
+Device::SyncPlan Device::sync_plan(const Index& ix) const {
+  SyncPlan p;
+  if (ix.version() == synced_version_ && edges_.d) return p;
+  size_t dirty = 0;
+  each_mirror(ix, [&](int k, auto& dm, const auto& m) {
+    using T = typename std::decay_t<decltype(m.h)>::value_type;
+    const size_t b = dm.need_bytes(m);
+    p.mirror[k] = b;
+    if (b && dm.spare_bytes < b) p.any = true;
+    if (!b && !m.all_dirty) dirty += m.dirty_pages * std::max<size_t>(Mirror<T>::per_page() * sizeof(T), 16);
+  });
+  // the staging buffers: the dirty pages, a run record and 16 B of alignment per page at most
+  p.stage = dirty ? dirty + dirty / 16 * (sizeof(ScatterRun) + 16) + 4096 : 0;
+  if (p.stage > h_stage_bytes_ && p.stage > h_stage_spare_bytes_) p.any = true;
+  if (p.stage > d_stage_.bytes && p.stage > d_stage_spare_.bytes) p.any = true;
+  return p;
+}
+
+void Device::prealloc(const SyncPlan& p) {
+  hip_check(hipSetDevice(dev_), "hipSetDevice");
+  auto one = [&](auto& dm, size_t b) {
+    if (!b || dm.spare_bytes >= b) return;
+    if (dm.spare) (void)hipFree(dm.spare);
+    dm.spare = nullptr;
+    dm.spare_bytes = 0;
+    hip_check(hipMalloc(&dm.spare, b), "hipMalloc(mirror spare)");
+    dm.spare_bytes = b;
+  };
+  one(edges_, p.mirror[0]);
+  one(walk_, p.mirror[1]);
+  one(lists_, p.mirror[2]);
+  one(inls_, p.mirror[3]);
+  one(msg_, p.mirror[4]);
+  one(seginfo_, p.mirror[5]);
+  one(segbytes_, p.mirror[6]);
+  one(subs_, p.mirror[7]);
+  one(mref_, p.mirror[8]);
+  one(mpart_, p.mirror[9]);
+  one(npair_, p.mirror[10]);
+  one(pent_, p.mirror[11]);
+  one(plist_, p.mirror[12]);
+  one(shr_, p.mirror[13]);
+  one(inl_, p.mirror[14]);
+  one(children_, p.mirror[15]);
+  one(xinfo_, p.mirror[16]);
+  one(deep_, p.mirror[17]);
+  one(deep_codes_, p.mirror[18]);
+  if (p.stage > h_stage_bytes_ && p.stage > h_stage_spare_bytes_) {
+    pinned_free(h_stage_spare_, h_stage_spare_bytes_);
+    h_stage_spare_ = nullptr;
+    h_stage_spare_bytes_ = 0;
+    h_stage_spare_ = pinned_alloc(p.stage);
+    h_stage_spare_bytes_ = p.stage;
+  }
+  if (p.stage > d_stage_.bytes && p.stage > d_stage_spare_.bytes) d_stage_spare_.ensure(p.stage);
 }
 
 void Device::release_retired() {

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <memory>
 
@@ -58,6 +59,14 @@ struct DevMirror {
   T* d = nullptr;
   size_t cap = 0;
   uint64_t epoch = ~0ull;
+  void* spare = nullptr;  // an allocation made ahead, outside the handle lock (Device::prealloc)
+  size_t spare_bytes = 0;
+  // bytes the next sync of m allocates (0: none)
+  size_t need_bytes(const Mirror<T>& m) const {
+    const size_t n = m.size();
+    if (d && m.epoch == epoch && cap >= n) return 0;
+    return std::max<size_t>(std::max(m.h.capacity(), n), 1) * sizeof(T);
+  }
   DevMirror() = default;
   DevMirror(const DevMirror&) = delete;
   DevMirror& operator=(const DevMirror&) = delete;
@@ -223,6 +232,16 @@ class Device {
   // mostly dirty array) are waited for, so an update may change the image once this returns.
   void prepare(Index& ix, hipStream_t s);
   const IndexSnap& snap() const { return snap_; }
+  // The allocations the next sync of ix would make (device arrays that grew, the staging buffers
+  // for its dirty pages), read under the handle lock, so that prealloc makes them outside it:
+  // hipMalloc and hipHostMalloc take milliseconds, which an update would otherwise wait for.
+  struct SyncPlan {
+    size_t mirror[19] = {};
+    size_t stage = 0;
+    bool any = false;  // something the spares do not cover yet
+  };
+  SyncPlan sync_plan(const Index& ix) const;
+  void prealloc(const SyncPlan& p);
   // Free the device arrays that syncs replaced (nothing on the device reads them any more: the
   // work that did ran under the device lock before the sync).
   void release_retired();
@@ -373,6 +392,11 @@ class Device {
   DevBuf d_stage_;                 // the staging buffer on the device
   void* h_stage_ = nullptr;        // ... and its pinned host side
   size_t h_stage_bytes_ = 0;
+  DevBuf d_stage_spare_;           // larger staging buffers made ahead (prealloc)
+  void* h_stage_spare_ = nullptr;
+  size_t h_stage_spare_bytes_ = 0;
+  template <class F>
+  void each_mirror(const Index& ix, F f) const;  // f(k, DevMirror&, const Mirror&) for the synced arrays
   hipEvent_t stage_done_ = nullptr;  // the last scatter finished reading both
   hipStream_t side_ = nullptr;
   hipStream_t hstream_ = nullptr;  // host_stream()

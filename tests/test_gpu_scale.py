@@ -220,4 +220,11 @@ def test_messages_10m_retained_100k_filters(gpu_available):
     bad = np.nonzero(dg != fd)[0]
     assert len(bad) == 0, f"{len(bad)} of {n} filters differ, first {bad[:5]}"
     assert int(count.sum()) > 10 * n  # the filters fan out
+    del hs
+    # the same batch as runs at the boundary (mq_messages_runs_device: bench_messages.py's step)
+    res = E.device_messages_runs(eng.messages_runs_device(d_fb.data_ptr(), d_fo.data_ptr(), n, None), n)
+    assert (res["count"] == fcnt).all()
+    bad = np.nonzero(O.run_digests(res, nthreads=THREADS) != fd)[0]
+    assert len(bad) == 0, f"runs: {len(bad)} of {n} filters differ, first {bad[:5]}"
+    assert len(res["runs"]) * 8 < int(fcnt.sum())
     eng.close()
