@@ -501,8 +501,9 @@ int mq_messages_runs_device(mq_index* idx, const uint8_t* d_filter_bytes, const 
  * shared by the results of one image version (copied once per version). */
 int mq_messages_runs_batch(mq_index* idx, const uint8_t* filter_bytes, const uint64_t* offsets,
                            uint32_t n, mq_msg_runs_result** out);
-/* Expand filters [first, first + count) of a host runs result into out (cap handles), in filter
- * order (filter i's handles at out[base[i] - base[first] ...]); *n_out: handles written. */
+/* Expand filters [first, first + count) of a host runs result into out (cap handles) in the
+ * expanded layout: filter i's handles at out[base[i] - base[first], + count[i]) (a batch the
+ * particle walk answered may leave gaps between filters); *n_out: the end of the last one. */
 int mq_msg_runs_expand(const mq_msg_runs_result* r, uint32_t first, uint32_t count, uint64_t* out,
                        uint64_t cap, uint64_t* n_out);
 

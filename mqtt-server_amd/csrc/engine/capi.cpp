@@ -3,6 +3,7 @@
 // and HIP failures into negative errno codes with a thread-local message.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <memory>
@@ -817,9 +818,14 @@ int mq_msg_runs_expand(const mq_msg_runs_result* r, uint32_t first, uint32_t cou
     auto it = g_results.find((void*)r);
     if (it == g_results.end() || it->second != 5) return fail(MQ_EINVAL, "not a host runs result (mq_messages_runs_batch)");
   }
-  uint64_t w = 0;
+  // filter i at out[base[i] - base[first]] (the expanded layout: a batch the particle walk answered
+  // may leave gaps between filters, where its count pass reserved more than the filter holds)
+  uint64_t end = 0;
+  const uint64_t b0 = count ? r->base[first] : 0;
   for (uint32_t i = first; i < first + count; i++) {
     if (r->run_base[i] + r->n_runs[i] > r->n_runs_total) return fail(MQ_EIO, "run range out of bounds");
+    if (r->base[i] < b0) return fail(MQ_EIO, "filter bases out of order");
+    const uint64_t w = r->base[i] - b0;
     if (w + r->count[i] > cap) return fail(MQ_ERANGE, "output capacity");
     if (r->count[i] && !out) return fail(MQ_EINVAL, "null output");
     uint64_t got = 0;
@@ -831,9 +837,9 @@ int mq_msg_runs_expand(const mq_msg_runs_result* r, uint32_t first, uint32_t cou
       got += run.count;
     }
     if (got != r->count[i]) return fail(MQ_EIO, "runs disagree with the filter's count");
-    w += got;
+    end = std::max(end, w + got);
   }
-  if (n_out) *n_out = w;
+  if (n_out) *n_out = end;
   return 0;
 }
 

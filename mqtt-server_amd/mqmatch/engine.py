@@ -650,7 +650,7 @@ class Engine:
                 hs = np.zeros(int(r.n_expanded), np.uint64)
                 got = C.c_uint64(0)
                 _check(lib().mq_msg_runs_expand(rp, 0, n, _p(hs, _u64p), len(hs), C.byref(got)), "mq_msg_runs_expand")
-                assert got.value == len(hs)
+                assert got.value <= len(hs)
                 out["expanded"] = hs
         finally:
             lib().mq_result_free(rp)

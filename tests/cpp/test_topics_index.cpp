@@ -405,13 +405,19 @@ static void TestConcurrentReadersAndUpdates() {
         }
         if (dt > kUpdateDeadline) late++;
       };
+      auto matched = [&] { return progress[0].load() + progress[1].load() + progress[2].load(); };
       for (int i = 0; i < 400; i++) {
+        const long m0 = matched();
         const std::string c = "tmp" + std::to_string(u) + "_" + std::to_string(i);
         timed([&] { ix.Subscribe(c, S("t/" + std::to_string(i % 7))); });
         timed([&] { ix.Subscribe(c, S("s/" + std::to_string(i % 10) + "/+")); });
         timed([&] { ix.Unsubscribe("t/" + std::to_string(i % 7), c); });
         timed([&] { ix.Unsubscribe("s/" + std::to_string(i % 10) + "/+", c); });
         progress[3 + u]++;
+        // the updates are fast (they wait for no match): pace them with the readers, so that
+        // matches run all through the update phase (at least one per round, 20 ms at most)
+        const auto t0 = clk::now();
+        while (matched() == m0 && clk::now() - t0 < std::chrono::milliseconds(20)) std::this_thread::yield();
       }
     });
   // a third updater on the engine handle itself (mq_subscribe / mq_unsubscribe, no mirror tables):
