@@ -54,8 +54,11 @@
 #define MQ_OPT_MSG_EDGE_BUDGET 22  /* Messages: the image edge table's budget in MiB at 1/16 load (default 8192;
                                      4x that at 1/8, else 1/4): a small budget forces the sparser tables'
                                      fallbacks at a small index (their parity test) */
-#define MQ_OPT_FAIL_NEXT 23       /* test hook: the next v span batches fail as if a kernel guard had tripped
-                                     (MQ_EIO), to exercise the callers' error paths */
+#define MQ_OPT_FAIL_NEXT 23       /* test hook, product-visible on purpose: the next v span batches fail as if a
+                                     kernel guard had tripped (MQ_EIO), so that the error paths of the library a
+                                     broker ships (pipelined tickets, the batching stages' retries) are tested on
+                                     that library itself; it changes no result of a batch that is not failed, and
+                                     a broker never sets it */
 #define MQ_OPT_WALK_EXP 24        /* development builds: bit 0 looks every topic's level-0 child up in a kernel ahead
                                      of the frontier walk (k_root_hint), which then reads it instead of probing: the
                                      walk's saving bounds what staging the root's children in LDS could save */

@@ -399,6 +399,7 @@ Device::~Device() {
   if (h_plan_) (void)hipHostFree(h_plan_);
   if (h_pin_) (void)hipHostFree(h_pin_);
   if (h_xsrc_) (void)hipHostFree(h_xsrc_);
+  if (xsrc_done_) (void)hipEventDestroy(xsrc_done_);
 }
 
 uint64_t Device::device_bytes() const {
@@ -1634,8 +1635,10 @@ bool Device::spans_end(const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans
     hip_check(hipHostMalloc(&hp, (kMaxShards - 1) * sizeof(XSrc), hipHostMallocDefault), "hipHostMalloc");
     h_xsrc_ = static_cast<XSrc*>(hp);
   }
-  XSrc* const h_src = h_xsrc_;  // (pinned: its copy runs in order with the batch; the previous batch
-                                //  synchronised before this one writes it again)
+  XSrc* const h_src = h_xsrc_;  // (pinned: its copy runs in order with the batch; the previous
+                                //  batch's copy of it is waited for before it is written again —
+                                //  a batch that threw after queueing the copy did not synchronise)
+  if (nf && xsrc_done_) hip_check(hipEventSynchronize(xsrc_done_), "hipEventSynchronize(xsrc)");
   XScanArgs xs;  // import: per-topic offsets of every foreign list, one batched scan
   memset(&xs, 0, sizeof(xs));
   for (uint32_t f = 0; f < nf; f++) {
@@ -1660,8 +1663,10 @@ bool Device::spans_end(const mq_xlist* xf, uint32_t nf, hipStream_t s, HostSpans
     hip_check(hipGetLastError(), "import");
   }
   if (nf) {
-    grow(x_src_, sizeof(h_src));
+    grow(x_src_, (kMaxShards - 1) * sizeof(XSrc));
     hip_check(hipMemcpyAsync(x_src_.p, h_src, nf * sizeof(XSrc), hipMemcpyHostToDevice, s), "H2D xsrc");
+    if (!xsrc_done_) hip_check(hipEventCreateWithFlags(&xsrc_done_, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(xsrc_done_, s), "hipEventRecord(xsrc)");
     a.xsrc = x_src_.as<XSrc>();
   }
   if (sb_.dedup) {  // merge-set dedup: each topic's representative (DedupArgs)

@@ -441,6 +441,7 @@ class Device {
   DevBuf x_off32_, x_gt_;  // walk-fused sharded begins: the export's u32 offsets; its totals (.g
                            //   entries, .rows gathers) for k_readback
   XSrc* h_xsrc_ = nullptr;                   // pinned: the imported lists' sources (no stack copy)
+  hipEvent_t xsrc_done_ = nullptr;           // ... its last copy to the device is done
   struct SpanBatch {               // between spans_begin and spans_end
     bool pending = false;
     uint32_t n = 0;
