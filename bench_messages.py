@@ -243,6 +243,17 @@ def main():
     elapsed = time.perf_counter() - t_start
     prof = eng.profile_read()
     eng.profile(False)
+    # one more, untimed step with the count pass's work counters (MQ_PROF_WORK: image edge-table
+    # lookups of the fan-outs, for the roofline's bytes)
+    eng.profile(True, work=True)
+    eng.profile_reset()
+    step()
+    torch.cuda.synchronize()
+    wk = eng.profile_read()
+    eng.profile(False)
+    lookups = wk.get("msg_fanout_lookups", (0, 0.0))[0]
+    r = step()  # (the result the parity checks read: a plain step's)
+    torch.cuda.synchronize()
     handles = int(r.n_expanded) if runs else int(r.n_handles)
     out = {
         "metric": "Messages filters/sec (retained reverse match)", "value": n * args.steps / elapsed,
@@ -253,6 +264,7 @@ def main():
                                f"{n} wildcard filters per step", "retained": len(ro) - 1, "filters": n},
         "format": args.format, "handles_per_step": handles, "handles_per_filter": handles / max(1, n),
         "runs_per_step": int(r.n_runs_total) if runs else None,
+        "fanout_lookups_per_step": lookups,
         "kernels_ms_per_step": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
         "path": "particle walk (k_msg)" if args.walk else ("level-order image (k_msgq" + (", runs out" if runs else " + k_msg_copy") + "), literal lookups "
                                                           + ("through the index's edge table" if args.no_img_edges
@@ -314,9 +326,15 @@ def main():
             # emitted handle read once from the image and written once to the output. SURVEY
             # §8d's B also prices the reference walk's child enumerations (16·P), which the image
             # path does not perform: that rate is reported beside it (it can exceed HBM peak).
-            if runs:  # a run record (16 B) and each filter's run base, run count, base, count (24 B)
-                b_img = 8 * per["L"] + 4 + 24 + 16 * int(r.n_runs_total) / max(1, n)
-                bytes_note = "8 B per level + 4 B offset + 24 B of counts per filter, 16 B per run written"
+            if runs:
+                # what the runs path reads and writes: the filter (8 B per level) and a 32 B image
+                # edge slot per literal level, a 32 B slot per fan-out lookup (work counter), the
+                # image's child range (16 B) and live prefix (16 B) per run, the run written (16 B)
+                # and each filter's run base, run count, base and count (24 B + 4 B offset)
+                rpf = int(r.n_runs_total) / max(1, n)
+                b_img = 40 * per["L"] + 28 + 32 * lookups / max(1, n) + 48 * rpf
+                bytes_note = ("40 B per level (filter bytes + an image edge slot), 28 B per filter, 32 B per fan-out "
+                              "lookup, 48 B per run (children range, live prefix, the run written)")
             else:
                 b_img = 8 * per["L"] + 4 + 16 * int(r.n_handles) / max(1, n)
                 bytes_note = "8 B per level + 4 B offset per filter, 16 B per emitted handle (read + write)"

@@ -474,6 +474,7 @@ void Device::sync(Index& ix, hipStream_t s) {
 void Device::sync_ix(Index& ix, hipStream_t s) {
   if (ix.version() == synced_version_ && edges_.d) return;
   ix.flush_merge();
+  slow_mark("flushed");
   Stager& st = stager_;
   st.runs.clear();
   st.bytes = 0;
@@ -499,6 +500,7 @@ void Device::sync_ix(Index& ix, hipStream_t s) {
     direct |= deep_.sync(ix.deep, s, &uploaded_, st);
     direct |= deep_codes_.sync(ix.deep_codes, s, &uploaded_, st);
   }
+  slow_mark("mirrors");
   if (!st.runs.empty()) {  // one staging buffer: the run table, then each run's bytes
     const size_t table = (st.runs.size() * sizeof(ScatterRun) + 15) & ~size_t(15);
     const size_t need = table + st.bytes + 16 * st.runs.size();
@@ -589,9 +591,11 @@ void Device::each_mirror(const Index& ix, F f) const {
   }
 }
 
-Device::SyncPlan Device::sync_plan(const Index& ix) const {
+Device::SyncPlan Device::sync_plan(Index& ix) const {
   SyncPlan p;
   if (ix.version() == synced_version_ && edges_.d) return p;
+  ix.flush_merge();  // (the deferred merge-record rebuilds grow arrays too: mref follows subs)
+  slow_mark("plan-flushed");
   size_t dirty = 0;
   each_mirror(ix, [&](int k, auto& dm, const auto& m) {
     using T = typename std::decay_t<decltype(m.h)>::value_type;

@@ -240,7 +240,7 @@ class Device {
     size_t stage = 0;
     bool any = false;  // something the spares do not cover yet
   };
-  SyncPlan sync_plan(const Index& ix) const;
+  SyncPlan sync_plan(Index& ix) const;  // (runs the index's deferred merge-record rebuilds first)
   void prealloc(const SyncPlan& p);
   // Free the device arrays that syncs replaced (nothing on the device reads them any more: the
   // work that did ran under the device lock before the sync).
