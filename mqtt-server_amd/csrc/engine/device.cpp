@@ -657,6 +657,7 @@ void Device::release_retired() {
 
 void Device::prepare(Index& ix, hipStream_t s) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
+  slow_mark("setdev");
   sync_ix(ix, s);  // (arrays it replaced are freed by the batch, outside the lock: spans_begin)
   // an upload straight from the host image (pageable memory) may still read it: done before an
   // update can touch it
@@ -765,6 +766,7 @@ static void grow(DevBuf& b, size_t bytes) {
 
 hipStream_t Device::host_stream() {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
+  slow_mark("hs-setdev");
   if (!hstream_) {
     // the copy stream right after it: streams share the device's few hardware queues (4 by
     // default), and a copy stream on the host stream's queue would run each batch's result copy
