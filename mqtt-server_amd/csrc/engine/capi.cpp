@@ -215,6 +215,8 @@ int guarded_match(mq_index* idx, P&& prep, R&& run) {
   return caught([&] {
     std::lock_guard<FifoMutex> dlk(L.dev_mu);
     if (slow_on()) slow_begin();
+    idx->device().begin_prepare();  // (HIP calls before the host-image lock, none under it)
+    slow_mark("begun");
     for (int round = 0;; round++) {
       Device::SyncPlan plan;
       {
@@ -487,7 +489,7 @@ int mq_match_spans(mq_index* idx, const uint8_t* tb, const uint64_t* to, uint32_
   PoolView pv;
   return guarded_match(idx, [&] {
     d = &idx->device();
-    hs = d->host_stream();
+    hs = d->host_stream_made();
     d->prepare(*idx->ix, hs);
     pv.reserve(idx);
   }, [&] {
@@ -518,7 +520,7 @@ int mq_match_spans_submit(mq_index* idx, const uint8_t* tb, const uint64_t* to, 
   PoolView pv;
   return guarded_match(idx, [&] {
     d = &idx->device();
-    hs = d->host_stream();
+    hs = d->host_stream_made();
     d->prepare(*idx->ix, hs);
     pv.reserve(idx);
   }, [&] {

@@ -180,7 +180,13 @@ bool DevMirror<T>::sync(Mirror<T>& m, hipStream_t s, uint64_t* uploaded, Stager&
   const size_t pp = Mirror<T>::per_page();
   const size_t npages = (n + pp - 1) / pp;
   if (!full) full = m.dirty_pages * 4 > npages * 3;  // mostly dirty: one plain copy
-  if (full) {
+  if (full && n * sizeof(T) <= kStageWhole) {
+    // a small array whole through the pinned staging buffer (copied on the host now, uploaded and
+    // scattered with the dirty pages): no pageable copy to wait for under the handle lock
+    if (n) st.add(d, m.h.data(), n * sizeof(T));
+    *uploaded += n * sizeof(T);
+    full = false;
+  } else if (full) {
     // pieces of at most 1 GiB: one pageable H2D copy of a multi-GiB array (the 100M-retained
     // image has 10 GB arrays) is not relied on
     const size_t bytes = n * sizeof(T), piece = 1ull << 30;
@@ -468,11 +474,29 @@ std::string Device::verify(Index& ix) {
 void Device::sync(Index& ix, hipStream_t s) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
   sync_ix(ix, s);
+  issue_staged(s);
   release_retired();
+}
+
+void Device::issue_staged(hipStream_t s) {
+  if (!staged_runs_) return;
+  hip_check(hipMemcpyAsync(d_stage_.p, h_stage_, staged_bytes_, hipMemcpyHostToDevice, s), "H2D staging");
+  launch_scatter(d_stage_.as<ScatterRun>(), staged_runs_, d_stage_.as<uint8_t>(), s);
+  hip_check(hipGetLastError(), "k_scatter");
+  hip_check(hipEventRecord(stage_done_, s), "hipEventRecord(stage)");
+  staged_runs_ = 0;
+  staged_bytes_ = 0;
+  staged_pending_ = true;
+}
+
+void Device::wait_staged() {
+  if (staged_pending_ && stage_done_) hip_check(hipEventSynchronize(stage_done_), "hipEventSynchronize(stage)");
+  staged_pending_ = false;
 }
 
 void Device::sync_ix(Index& ix, hipStream_t s) {
   if (ix.version() == synced_version_ && edges_.d) return;
+  if (staged_runs_) issue_staged(s);  // (a batch that failed before issuing its upload: now)
   ix.flush_merge();
   slow_mark("flushed");
   Stager& st = stager_;
@@ -504,10 +528,10 @@ void Device::sync_ix(Index& ix, hipStream_t s) {
   if (!st.runs.empty()) {  // one staging buffer: the run table, then each run's bytes
     const size_t table = (st.runs.size() * sizeof(ScatterRun) + 15) & ~size_t(15);
     const size_t need = table + st.bytes + 16 * st.runs.size();
-    if (stage_done_) hip_check(hipEventSynchronize(stage_done_), "hipEventSynchronize(stage)");
-    else hip_check(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming), "hipEventCreate");
-    // (the event is recorded only once a scatter has used it; before that, synchronising on it
-    // returns at once)
+    // (the last upload finished reading the pinned buffer: wait_staged, before the handle lock;
+    // the event is recorded only once a scatter has used it, before that waiting returns at once)
+    if (!stage_done_) hip_check(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming), "hipEventCreate");
+    if (staged_pending_) hip_check(hipEventSynchronize(stage_done_), "hipEventSynchronize(stage)");
     if (h_stage_bytes_ < need) {
       pinned_free(h_stage_, h_stage_bytes_);
       if (h_stage_spare_ && h_stage_spare_bytes_ >= need) {  // (made ahead: prealloc)
@@ -536,10 +560,10 @@ void Device::sync_ix(Index& ix, hipStream_t s) {
       tab[k] = ScatterRun{(uint64_t)(uintptr_t)r.dst, o, r.bytes};
       o += r.bytes;
     }
-    hip_check(hipMemcpyAsync(d_stage_.p, hs, o, hipMemcpyHostToDevice, s), "H2D staging");
-    launch_scatter(d_stage_.as<ScatterRun>(), (uint32_t)st.runs.size(), d_stage_.as<uint8_t>(), s);
-    hip_check(hipGetLastError(), "k_scatter");
-    hip_check(hipEventRecord(stage_done_, s), "hipEventRecord(stage)");
+    // the upload itself (H2D of the staging buffer, k_scatter) is issued by issue_staged: after
+    // the handle lock, on the batch's stream, ahead of its kernels
+    staged_bytes_ = o;
+    staged_runs_ = (uint32_t)st.runs.size();
   }
   if (!h_stage_) {  // the first sync (a whole upload): the staging buffers for the updates' dirty
     // pages, sized for ordinary update bursts, so that the first update after it does not
@@ -556,6 +580,7 @@ void Device::sync_ix(Index& ix, hipStream_t s) {
     launch_scatter(d_stage_.as<ScatterRun>(), 1, d_stage_.as<uint8_t>(), s);
     hip_check(hipGetLastError(), "k_scatter");
     hip_check(hipEventRecord(stage_done_, s), "hipEventRecord(stage)");
+    staged_pending_ = true;
   }
   retained_len_ = ix.retained_len();
   empty_live_ = ix.empty_topic_live;
@@ -602,9 +627,12 @@ Device::SyncPlan Device::sync_plan(Index& ix) const {
     const size_t b = dm.need_bytes(m);
     p.mirror[k] = b;
     if (b && dm.spare_bytes < b) p.any = true;
-    if (!b && !m.all_dirty) dirty += m.dirty_pages * std::max<size_t>(Mirror<T>::per_page() * sizeof(T), 16);
+    const size_t whole = m.size() * sizeof(T);
+    if ((b || m.all_dirty) && whole <= kStageWhole) dirty += whole;  // (whole through the staging)
+    else if (!b && !m.all_dirty) dirty += m.dirty_pages * std::max<size_t>(Mirror<T>::per_page() * sizeof(T), 16);
   });
   // the staging buffers: the dirty pages, a run record and 16 B of alignment per page at most
+  // (a run record and 16 B of alignment per 64 B page, or per kScatterRun of a whole array)
   p.stage = dirty ? dirty + dirty / 16 * (sizeof(ScatterRun) + 16) + 4096 : 0;
   if (p.stage > h_stage_bytes_ && p.stage > h_stage_spare_bytes_) p.any = true;
   if (p.stage > d_stage_.bytes && p.stage > d_stage_spare_.bytes) p.any = true;
@@ -655,9 +683,14 @@ void Device::release_retired() {
   stager_.frees.clear();
 }
 
+void Device::begin_prepare() {
+  (void)host_stream();  // (sets the device; creates the host-result streams on first use)
+  wait_staged();
+}
+
 void Device::prepare(Index& ix, hipStream_t s) {
-  hip_check(hipSetDevice(dev_), "hipSetDevice");
-  slow_mark("setdev");
+  // (host work under the handle lock: the caller set the device and waited for the last staged
+  // upload first — begin_prepare — so that no HIP call here waits behind another thread's)
   sync_ix(ix, s);  // (arrays it replaced are freed by the batch, outside the lock: spans_begin)
   // an upload straight from the host image (pageable memory) may still read it: done before an
   // update can touch it
@@ -1282,6 +1315,7 @@ void Device::match_spans(const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, 
 void Device::spans_begin(const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, hipStream_t s,
                          mq_xlist* x, bool one_sync, bool shard_sync) {
   hip_check(hipSetDevice(dev_), "hipSetDevice");
+  issue_staged(s);  // (the prepare phase's upload of the dirty pages, ahead of the kernels)
   release_retired();
   flush_host_copy();  // (a pipelined batch's copy: before this batch reuses any stage)
   slow_mark("flush");

@@ -54,6 +54,10 @@ struct Stager {
   void add(void* dst, const void* src, size_t n);  // split into runs of <= kScatterRun
 };
 
+// A reallocated or mostly dirty array this small goes whole through the pinned staging buffer
+// (DevMirror::sync): no pageable copy, and no wait for one, under the handle lock.
+constexpr size_t kStageWhole = 8u << 20;
+
 template <class T>
 struct DevMirror {
   T* d = nullptr;
@@ -224,6 +228,7 @@ class Device {
   int device() const { return dev_; }
   // The stream of host-buffer calls (mq_match_spans): its own, non-blocking.
   hipStream_t host_stream();
+  hipStream_t host_stream_made() const { return hstream_; }  // (after begin_prepare: no HIP call)
 
   // Upload dirty pages of the index image (incremental device-side update).
   void sync(Index& ix, hipStream_t s);
@@ -231,6 +236,9 @@ class Device {
   // itself may then run without it). Uploads straight from the host image (a reallocated or
   // mostly dirty array) are waited for, so an update may change the image once this returns.
   void prepare(Index& ix, hipStream_t s);
+  // Before the handle lock: the device set on this thread, the last staged upload done (prepare
+  // then makes no HIP call that could wait behind another thread's).
+  void begin_prepare();
   const IndexSnap& snap() const { return snap_; }
   // The allocations the next sync of ix would make (device arrays that grew, the staging buffers
   // for its dirty pages), read under the handle lock, so that prealloc makes them outside it:
@@ -318,7 +326,12 @@ class Device {
 
  private:
   DevIndex dev_index(const Index& ix) const;
-  void sync_ix(Index& ix, hipStream_t s);  // sync() without freeing the arrays it replaced
+  void sync_ix(Index& ix, hipStream_t s);  // sync() on the host: the upload is left to issue_staged
+  void issue_staged(hipStream_t s);         // the staged dirty pages' H2D copy and k_scatter on s
+  void wait_staged();                       // the last staged upload has read the pinned buffer
+  uint64_t staged_bytes_ = 0;               // a staged upload not yet issued (bytes, runs)
+  uint32_t staged_runs_ = 0;
+  bool staged_pending_ = false;             // an issued upload may still read the pinned buffer
   void check_err(hipStream_t s);
   // walk (count) + scan of n topics; returns the batch totals (synchronises s)
   // (one_sync: the totals are not read back - the returned TopicOff is zero - and every topic's
