@@ -61,7 +61,8 @@
                                      a broker never sets it */
 #define MQ_OPT_WALK_EXP 24        /* development builds: bit 0 looks every topic's level-0 child up in a kernel ahead
                                      of the frontier walk (k_root_hint), which then reads it instead of probing: the
-                                     walk's saving bounds what staging the root's children in LDS could save */
+                                     walk's saving bounds what staging the root's children in LDS could save;
+                                     bit 1 (round 6): levels 0 and 1 (the frontier's level-1 probes too) */
 #define MQ_OPT_MAX 24             /* the highest option number mq_set_option admits */
 #define MQ_OPT_FUSE_DESC 17       /* one-sync span batches: 1 (default) runs k_desc in the frontier walk's
                                      epilogue (spans and merge lists at t * 64, no scan); 0: walk, scan, k_desc */

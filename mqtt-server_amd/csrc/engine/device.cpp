@@ -1491,13 +1491,15 @@ void Device::spans_begin(const uint8_t* d_tb, const uint64_t* d_to, uint32_t n, 
     while (slots < 2ull * n) slots <<= 1;
     fda.dd_mask = slots - 1;
     fda.dd_tslot = dd_slot_.as<uint32_t>();
-    if (walk_exp_ & 1u) {  // MQ_OPT_WALK_EXP bit 0: the level-0 probes ahead of the walk
-      grow(root_hint_, (size_t)n * sizeof(uint4));
+    if (walk_exp_ & 3u) {  // MQ_OPT_WALK_EXP bit 0: the level-0 probes ahead of the walk; bit 1: levels 0, 1
+      const uint32_t levels = (walk_exp_ & 2u) ? 2u : 1u;
+      grow(root_hint_, (size_t)n * (levels == 2 ? 3 : 1) * sizeof(uint4));
       prof.begin(s, "root_hint");
-      launch_root_hint(d_tb, d_to, n, di, root_hint_.as<uint4>(), s);
+      launch_root_hint(d_tb, d_to, n, di, root_hint_.as<uint4>(), levels, s);
       prof.end("root_hint", s);
       hip_check(hipGetLastError(), "k_root_hint");
       fda.root_hint = root_hint_.as<uint4>();
+      fda.hint_levels = levels;
     }
   }
   TopicOff tot = walk_scan(di, d_tb, d_to, n, s, &gathers, &gstride, sb_.lists, bsync, fused ? &fda : nullptr);

@@ -276,8 +276,11 @@ struct DescArgs {
   uint32_t* gw_out;  // sharded, walk-fused: every gather word at its span's position (k_xsig's GDesc
                      //   records for k_merge's linear paths are made from them)
   // MQ_OPT_WALK_EXP bit 0 (development builds, an attribution of the walk's level-0 probes):
-  // topic t's root child (child, '+', '#') looked up before the walk by k_root_hint
+  // topic t's root child (child, '+', '#') looked up before the walk by k_root_hint; bit 1 (round
+  // 6) levels 0 and 1: root_hint[3t] the root child, [3t + 1] its literal child of segment 1,
+  // [3t + 2] the root's '+' child's literal child of segment 1 (the two level-1 probes)
   const uint4* root_hint;
+  uint32_t hint_levels;
   // one-sync batches (Device, MQ_OPT_ONE_SYNC): the capacities of spans / desc in records; a topic
   // that would write past them writes nothing and sets bit 1 of *unsafe (the batch is run again
   // with host-sized buffers). unsafe == null: sized by the host (no checks).
@@ -417,7 +420,8 @@ void launch_walk_desc(uint32_t group, uint32_t wpe, const uint8_t* tb, const uin
 void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bpre, TopicOff* off,
                  hipStream_t s);
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s);
-void launch_root_hint(const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix, uint4* out, hipStream_t s);
+void launch_root_hint(const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix, uint4* out, uint32_t levels,
+                      hipStream_t s);
 void launch_copy(const EmitArgs& a, uint32_t max_blocks, hipStream_t s);
 void launch_merge(const EmitArgs& a, bool spans, uint32_t wpe, uint32_t max_blocks, hipStream_t s);
 

@@ -339,8 +339,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     EdgeHit h{kNone, kNone, kNone};
     // a literal "+" segment: the reference visits the '+' child twice alike (topics.go:603)
     if (mine && !plusseg) {
-      if (DESC && kDevBuild && dk.root_hint && d == 0) {  // (MQ_OPT_WALK_EXP bit 0: level 0 looked up before the walk)
-        const uint4 rh = dk.root_hint[t];
+      if (DESC && kDevBuild && dk.root_hint && d < dk.hint_levels) {  // (MQ_OPT_WALK_EXP: looked up before the walk)
+        // level 0: the root's child; level 1 (bit 1): the literal child of the root's literal or
+        // '+' child, by how the frontier entry's path starts
+        const uint32_t k = dk.hint_levels == 1 ? t : 3 * t + (d == 0 ? 0u : (fe.code >> 30) == 1u ? 1u : 2u);
+        const uint4 rh = dk.root_hint[k];
         h = EdgeHit{rh.x, rh.y, rh.z};
       } else {
         h = lookup_edge(ix, fe.node, key, tbase + s, len);
@@ -769,26 +772,46 @@ void launch_scan(const TopicCount* cnt, uint32_t n, TopicOff* bsum, TopicOff* bp
 // child of its first segment), thread per topic, ahead of the walk — the walk then reads it instead
 // of probing, so the two kernels' times attribute the level-0 probes (the north star's "hot trie
 // levels staged in LDS" would save at most that much)
+// Bit 1 (round 6): levels 0 and 1 — also the level-1 probes of the frontier's two possible
+// entries (the root's literal child and its '+' child), so that the walk's time without them bounds
+// staging both hot levels in LDS.
 __global__ __launch_bounds__(256) void k_root_hint(const uint8_t* __restrict__ tb, const uint64_t* __restrict__ to,
-                                                   uint32_t n, DevIndex ix, uint4* __restrict__ out) {
+                                                   uint32_t n, DevIndex ix, uint4* __restrict__ out, uint32_t levels) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const uint64_t a0 = to[t], a1 = to[t + 1];
   const uint8_t* tbase = tb + (a0 & ~15ull);
   const uint32_t b0 = (uint32_t)(a0 & 15), b1 = b0 + (uint32_t)(a1 - a0);
-  EdgeHit h{kNone, kNone, kNone};
+  EdgeHit h{kNone, kNone, kNone}, hl{kNone, kNone, kNone}, hp{kNone, kNone, kNone};
   if (a1 > a0) {
     ByteReaderT<uint32_t> R(tbase);
     const uint32_t e = find_slash(R, b0, b1);
     const bool plusseg = e - b0 == 1 && R.at(b0) == '+';
     if (!plusseg) h = lookup_edge(ix, kRoot, key_of(R, b0, e), tbase + b0, e - b0);
+    if (levels > 1 && e < b1) {
+      const uint32_t s1 = e + 1, e1 = find_slash(R, s1, b1);
+      const bool plus1 = e1 - s1 == 1 && R.at(s1) == '+';
+      if (!plus1) {
+        const SegKey k1 = key_of(R, s1, e1);
+        if (h.child != kNone) hl = lookup_edge(ix, h.child, k1, tbase + s1, e1 - s1);
+        const uint32_t rp = ix.walk[kRoot].plus_child;
+        if (rp != kNone) hp = lookup_edge(ix, rp, k1, tbase + s1, e1 - s1);
+      }
+    }
   }
-  out[t] = make_uint4(h.child, h.plus, h.hash, 0u);
+  if (levels > 1) {
+    out[3 * t] = make_uint4(h.child, h.plus, h.hash, 0u);
+    out[3 * t + 1] = make_uint4(hl.child, hl.plus, hl.hash, 0u);
+    out[3 * t + 2] = make_uint4(hp.child, hp.plus, hp.hash, 0u);
+  } else {
+    out[t] = make_uint4(h.child, h.plus, h.hash, 0u);
+  }
 }
 
-void launch_root_hint(const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix, uint4* out, hipStream_t s) {
+void launch_root_hint(const uint8_t* tb, const uint64_t* to, uint32_t n, const DevIndex& ix, uint4* out, uint32_t levels,
+                      hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(k_root_hint, dim3((n + 255) / 256), dim3(256), 0, s, tb, to, n, ix, out);
+  hipLaunchKernelGGL(k_root_hint, dim3((n + 255) / 256), dim3(256), 0, s, tb, to, n, ix, out, levels);
 }
 
 void launch_desc(const DescArgs& a, bool spans, hipStream_t s) {
