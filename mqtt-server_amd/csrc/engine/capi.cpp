@@ -191,9 +191,10 @@ int guarded(mq_index* idx, F&& f, Access access = Access::kRead) {
       dlk.lock();
       wait_for_writers(V);
     }
+    if (slow_on()) slow_begin();  // (the wait for the lock included)
     std::lock_guard<FifoMutex> lk(L.mu);
     if (!slow_on()) return f();
-    slow_begin();
+    slow_mark("locked");
     const int r = f();
     slow_report(access == Access::kUpdate ? "update" : "read", 0.0);
     return r;

@@ -122,7 +122,9 @@ void pinned_free(void* p, size_t bytes) {
       return;
     }
   }
+  slow_mark("hipHostFree");
   (void)hipHostFree(p);
+  slow_mark("freed-pinned");
 }
 
 void DevBuf::ensure(size_t b) {
@@ -480,6 +482,7 @@ void Device::sync(Index& ix, hipStream_t s) {
 
 void Device::issue_staged(hipStream_t s) {
   if (!staged_runs_) return;
+  slow_mark("issue");
   hip_check(hipMemcpyAsync(d_stage_.p, h_stage_, staged_bytes_, hipMemcpyHostToDevice, s), "H2D staging");
   launch_scatter(d_stage_.as<ScatterRun>(), staged_runs_, d_stage_.as<uint8_t>(), s);
   hip_check(hipGetLastError(), "k_scatter");
@@ -619,6 +622,7 @@ void Device::each_mirror(const Index& ix, F f) const {
 Device::SyncPlan Device::sync_plan(Index& ix) const {
   SyncPlan p;
   if (ix.version() == synced_version_ && edges_.d) return p;
+  slow_mark("plan");
   ix.flush_merge();  // (the deferred merge-record rebuilds grow arrays too: mref follows subs)
   slow_mark("plan-flushed");
   size_t dirty = 0;
@@ -679,8 +683,11 @@ void Device::prealloc(const SyncPlan& p) {
 }
 
 void Device::release_retired() {
+  if (stager_.frees.empty()) return;
+  slow_mark("retire-free");
   for (void* p : stager_.frees) (void)hipFree(p);
   stager_.frees.clear();
+  slow_mark("retired");
 }
 
 void Device::begin_prepare() {
