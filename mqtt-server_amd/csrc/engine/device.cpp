@@ -129,8 +129,12 @@ void pinned_free(void* p, size_t bytes) {
 
 void DevBuf::ensure(size_t b) {
   if (b <= bytes && p) return;
+  // a buffer that grows again takes half as much again as asked: results and scratch that follow
+  // a growing index (a batch's rows, patches, spans) would otherwise be reallocated at every step
+  // of it, and each hipFree / hipMalloc stalls the process's other threads for milliseconds
+  const size_t grown = p ? b + b / 2 : b;
   release();
-  size_t nb = std::max<size_t>(b, 256);
+  size_t nb = std::max<size_t>(grown, 256);
   hip_check(hipMalloc(&p, nb), "hipMalloc");
   bytes = nb;
 }
@@ -356,6 +360,10 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
       return true;
     case MQ_OPT_MSG_IMAGE: msg_img_on_ = v != 0; return true;
     case MQ_OPT_PATCH_CODES: patch_codes_ = v != 0; return true;
+    case MQ_OPT_MSG_KEYIDX:
+      msg_kx_on_ = v != 0;
+      img_version_ = ~0ull;  // (rebuilt with or without it)
+      return true;
     case MQ_OPT_MSG_EDGES:
       msg_edges_on_ = v != 0;
       img_version_ = ~0ull;  // (the image is rebuilt, with or without its table)
@@ -2332,12 +2340,88 @@ void Device::ensure_img(const Index& ix, const DevIndex& di, hipStream_t s) {
     hip_check(hipGetLastError(), "k_img_edges");
     img_edge_mask_ = slots2 - 1;
   }
+  kx_built_ = false;
+  if (msg_kx_on_) build_key_index(di, lo, slots, s);
   prof.end("msg_image", s);
   img_n_ = lo;
   img_n_pos_ = slots;
   img_levels_ = levels;
   img_live_ = live;
   img_version_ = ix.retained_version();
+}
+
+// The image's key index (kernels.h MsgImg.kx_*): its edges collected, sorted stably by parent
+// position then by key hash (so one key's entries are contiguous and ordered by parent), and a
+// table from key hash to the range. Skipped when its transient arrays (~90 B per image particle)
+// would not fit a quarter of the device's free memory.
+void Device::build_key_index(const DevIndex& di, uint32_t n_img, uint32_t n_pos, hipStream_t s) {
+  kx_par_.release();
+  kx_chd_.release();
+  kx_k0_.release();
+  kx_k1_.release();
+  kx_tab_.release();
+  kx_mask_ = 0;
+  if (n_img < 2) return;
+  size_t freeb = 0, total = 0;
+  if (hipMemGetInfo(&freeb, &total) == hipSuccess && (uint64_t)n_img * 96 > freeb / 4) return;
+  const uint32_t cap = n_img;
+  DevBuf a_par, a_chd, a_k0, a_k1, a_h, perm0, t_par, perm1, t_h, perm2, s_h, cnt, temp;
+  a_par.ensure((size_t)cap * 4);
+  a_chd.ensure((size_t)cap * 4);
+  a_k0.ensure((size_t)cap * 8);
+  a_k1.ensure((size_t)cap * 8);
+  a_h.ensure((size_t)cap * 8);
+  perm0.ensure((size_t)cap * 4);
+  cnt.ensure(2 * sizeof(unsigned long long));
+  hip_check(hipMemsetAsync(cnt.p, 0, 2 * sizeof(unsigned long long), s), "memset");
+  launch_kx_collect(di, img_node_.as<uint32_t>(), img_pos_.as<uint32_t>(), n_img, n_pos, a_par.as<uint32_t>(),
+                    a_chd.as<uint32_t>(), a_k0.as<uint64_t>(), a_k1.as<uint64_t>(), a_h.as<uint64_t>(),
+                    perm0.as<uint32_t>(), cnt.as<unsigned long long>(), s);
+  hip_check(hipGetLastError(), "k_kx_collect");
+  unsigned long long ne = 0;
+  hip_check(hipMemcpyAsync(&ne, cnt.p, sizeof(ne), hipMemcpyDeviceToHost, s), "D2H kx count");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (ne == 0 || ne > cap) return;
+  const uint32_t n = (uint32_t)ne;
+  t_par.ensure((size_t)n * 4);
+  perm1.ensure((size_t)n * 4);
+  t_h.ensure((size_t)n * 8);
+  perm2.ensure((size_t)n * 4);
+  s_h.ensure((size_t)n * 8);
+  const size_t tb = std::max(kx_sort_u32(nullptr, 0, a_par.as<uint32_t>(), t_par.as<uint32_t>(), perm0.as<uint32_t>(),
+                                         perm1.as<uint32_t>(), n, s),
+                             kx_sort_u64(nullptr, 0, t_h.as<uint64_t>(), s_h.as<uint64_t>(), perm1.as<uint32_t>(),
+                                         perm2.as<uint32_t>(), n, s));
+  temp.ensure(tb);
+  kx_sort_u32(temp.p, tb, a_par.as<uint32_t>(), t_par.as<uint32_t>(), perm0.as<uint32_t>(), perm1.as<uint32_t>(), n, s);
+  hip_check(hipGetLastError(), "kx sort (parents)");
+  launch_kx_gather64(a_h.as<uint64_t>(), perm1.as<uint32_t>(), t_h.as<uint64_t>(), n, s);
+  kx_sort_u64(temp.p, tb, t_h.as<uint64_t>(), s_h.as<uint64_t>(), perm1.as<uint32_t>(), perm2.as<uint32_t>(), n, s);
+  hip_check(hipGetLastError(), "kx sort (keys)");
+  kx_par_.ensure((size_t)n * 4);
+  kx_chd_.ensure((size_t)n * 4);
+  kx_k0_.ensure((size_t)n * 8);
+  kx_k1_.ensure((size_t)n * 8);
+  launch_kx_gather32(a_par.as<uint32_t>(), perm2.as<uint32_t>(), kx_par_.as<uint32_t>(), n, s);
+  launch_kx_gather32(a_chd.as<uint32_t>(), perm2.as<uint32_t>(), kx_chd_.as<uint32_t>(), n, s);
+  launch_kx_gather64(a_k0.as<uint64_t>(), perm2.as<uint32_t>(), kx_k0_.as<uint64_t>(), n, s);
+  launch_kx_gather64(a_k1.as<uint64_t>(), perm2.as<uint32_t>(), kx_k1_.as<uint64_t>(), n, s);
+  launch_kx_count_keys(s_h.as<uint64_t>(), n, cnt.as<unsigned long long>() + 1, s);
+  hip_check(hipGetLastError(), "kx gathers");
+  unsigned long long keys = 0;
+  hip_check(hipMemcpyAsync(&keys, cnt.as<unsigned long long>() + 1, sizeof(keys), hipMemcpyDeviceToHost, s), "D2H kx keys");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  uint64_t slots = 1024;
+  while (slots < 2 * keys) slots <<= 1;
+  kx_tab_.ensure(slots * sizeof(KxSlot));
+  hip_check(hipMemsetAsync(kx_tab_.p, 0, slots * sizeof(KxSlot), s), "memset kx table");
+  launch_kx_table(s_h.as<uint64_t>(), n, kx_tab_.as<KxSlot>(), slots - 1, err_.as<uint32_t>(), s);
+  hip_check(hipGetLastError(), "k_kx_table");
+  hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");  // (the temporaries go at return)
+  kx_mask_ = slots - 1;
+  kx_built_ = true;
+  prof.count("msg_kx_entries", n);
+  prof.count("msg_kx_keys", keys);
 }
 
 MsgImg Device::msg_img() const {
@@ -2356,6 +2440,12 @@ MsgImg Device::msg_img() const {
   m.work = nullptr;
   m.run_base = nullptr;
   m.run_cnt = nullptr;
+  m.kx_tab = kx_built_ ? kx_tab_.as<KxSlot>() : nullptr;
+  m.kx_mask = kx_mask_;
+  m.kx_par = kx_par_.as<uint32_t>();
+  m.kx_chd = kx_chd_.as<uint32_t>();
+  m.kx_k0 = kx_k0_.as<uint64_t>();
+  m.kx_k1 = kx_k1_.as<uint64_t>();
   return m;
 }
 

@@ -497,6 +497,11 @@ class Device {
   uint64_t patch_cap_init_ = 1ull << 24;
   DevBuf img_node_, img_pos_, img_cl_, img_lp_, img_h_, img_cnt_, img_coff_, img_bsum_, img_bpre_;
   DevBuf img_edges_;                  // the image's edge table (MsgImg.edges)
+  DevBuf kx_par_, kx_chd_, kx_k0_, kx_k1_, kx_tab_;  // the image's key index (MsgImg.kx_*)
+  uint64_t kx_mask_ = 0;
+  bool kx_built_ = false;
+  bool msg_kx_on_ = true;             // MQ_OPT_MSG_KEYIDX
+  void build_key_index(const DevIndex& di, uint32_t n_img, uint32_t n_pos, hipStream_t s);
   DevBuf msg_gate_;                   // one-sync Messages batches: the gate and the piece count (k_msg_gate)
   uint64_t img_edge_mask_ = 0;
   bool msg_edges_on_ = true;          // MQ_OPT_MSG_EDGES

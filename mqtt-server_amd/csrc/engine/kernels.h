@@ -515,6 +515,25 @@ struct ImgEdge {  // 32 B, two per 64 B line; parent kImgEdgeEmpty: free
   uint64_t k0, k1, pad;
 };
 constexpr uint32_t kImgEdgeEmpty = 0xFFFFFFFFu;
+struct KxSlot {  // the key index's table: key hash (0: free) -> entries [start, start + count)
+  uint64_t h;
+  uint32_t start, count;
+};
+constexpr uint32_t kKxMin = 64;  // particles under which a literal level probes them one by one
+MQ_HD uint64_t kx_hash(uint64_t k0, uint64_t k1) { return mix64(k0 ^ mix64(k1 + 0x9e3779b97f4a7c15ull)) | 1ull; }
+// Key index build (Device::ensure_img): collect the image edges, sort them, fill the table.
+void launch_kx_collect(const DevIndex& ix, const uint32_t* node, const uint32_t* pos, uint32_t n, uint32_t n_pos,
+                       uint32_t* par, uint32_t* chd, uint64_t* k0, uint64_t* k1, uint64_t* h, uint32_t* perm,
+                       unsigned long long* count, hipStream_t s);
+// hipcub radix sorts (stable): temp == null returns the temp bytes needed
+size_t kx_sort_u32(void* temp, size_t temp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                   uint32_t* vout, uint32_t n, hipStream_t s);
+size_t kx_sort_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
+                   uint32_t* vout, uint32_t n, hipStream_t s);
+void launch_kx_gather32(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint32_t n, hipStream_t s);
+void launch_kx_gather64(const uint64_t* src, const uint32_t* perm, uint64_t* dst, uint32_t n, hipStream_t s);
+void launch_kx_count_keys(const uint64_t* h, uint32_t n, unsigned long long* keys, hipStream_t s);
+void launch_kx_table(const uint64_t* h, uint32_t n, KxSlot* tab, uint64_t mask, uint32_t* err, hipStream_t s);
 struct MsgImg {
   const uint32_t* node;  // image position -> particle
   const uint32_t* pos;   // particle -> image position (valid iff node[pos[p]] == p; n_pos entries)
@@ -530,6 +549,17 @@ struct MsgImg {
   // frontier outgrew LDS (per-lane walk), [2] particles those walked per lane
   uint32_t* cyc;
   unsigned long long* work;
+  // The image's key index (round 6; null: none): every image edge (parent position, key) ->
+  // child position, sorted by (key hash, parent position) — kx_par / kx_chd / kx_k0 / kx_k1 — and a
+  // table key hash -> its entries' range (kx_tab, kx_mask + 1 slots). A literal segment under runs
+  // of particles is then one table probe and two binary searches per run (the children with that
+  // key whose parent lies in the run), not one edge-table probe per particle of the runs.
+  const struct KxSlot* kx_tab;
+  uint64_t kx_mask;
+  const uint32_t* kx_par;
+  const uint32_t* kx_chd;
+  const uint64_t* kx_k0;
+  const uint64_t* kx_k1;
   // Runs at the boundary (mq_messages_runs_*, round 6): every run the walk finds is one MsgPiece
   // (== mq_msg_run) and nothing is copied; the fill passes also write each filter's first run and
   // run count (null: handles, as before)

@@ -1,6 +1,7 @@
 // gfx950 Messages: the particle walk k_msg, the level-order retained image and k_msgq (DESIGN.md
 // §4.8).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -546,6 +547,160 @@ __device__ __forceinline__ uint32_t img_child(const MsgImg& img, const DevIndex&
   return kNone;
 }
 
+// ---- the image's key index (round 6) -----------------------------------------------------------
+// Thread per slot of the index's edge table: every edge between image particles, as (parent and
+// child image positions, the key, its hash), in any order (k_kx_collect), then stably sorted by
+// parent position and by key hash (hipcub radix sorts, gathers), so that one key's entries are
+// contiguous and ordered by parent position.
+__global__ __launch_bounds__(256) void k_kx_collect(DevIndex ix, const uint32_t* __restrict__ node,
+                                                    const uint32_t* __restrict__ pos, uint32_t n, uint32_t n_pos,
+                                                    uint32_t* __restrict__ par, uint32_t* __restrict__ chd,
+                                                    uint64_t* __restrict__ k0, uint64_t* __restrict__ k1,
+                                                    uint64_t* __restrict__ h, uint32_t* __restrict__ perm,
+                                                    unsigned long long* __restrict__ count) {
+  auto in_img = [&](uint32_t c) __attribute__((always_inline)) -> uint32_t {
+    if (c >= n_pos) return kNone;
+    const uint32_t q = pos[c];
+    return (q < n && node[q] == c) ? q : kNone;
+  };
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i <= ix.edge_mask; i += (uint64_t)gridDim.x * 256) {
+    const EdgeSlot e = ix.edges[i];
+    if (e.parent >= kEdgeTomb) continue;  // a free slot
+    const uint32_t qc = in_img(e.child);
+    if (qc == kNone) continue;
+    const uint32_t qp = in_img(e.parent);
+    if (qp == kNone) continue;
+    const uint32_t j = (uint32_t)atomicAdd(count, 1ull);
+    par[j] = qp;
+    chd[j] = qc;
+    k0[j] = e.k0;
+    k1[j] = e.k1;
+    h[j] = kx_hash(e.k0, e.k1);
+    perm[j] = j;
+  }
+}
+
+void launch_kx_collect(const DevIndex& ix, const uint32_t* node, const uint32_t* pos, uint32_t n, uint32_t n_pos,
+                       uint32_t* par, uint32_t* chd, uint64_t* k0, uint64_t* k1, uint64_t* h, uint32_t* perm,
+                       unsigned long long* count, hipStream_t s) {
+  const uint64_t slots = ix.edge_mask + 1;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 1u << 20);
+  hipLaunchKernelGGL(k_kx_collect, dim3(g), dim3(256), 0, s, ix, node, pos, n, n_pos, par, chd, k0, k1, h, perm, count);
+}
+
+size_t kx_sort_u32(void* temp, size_t temp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                   uint32_t* vout, uint32_t n, hipStream_t s) {
+  size_t b = temp_bytes;
+  (void)hipcub::DeviceRadixSort::SortPairs(temp, b, kin, kout, vin, vout, (int)n, 0, 32, s);
+  return b;
+}
+
+size_t kx_sort_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
+                   uint32_t* vout, uint32_t n, hipStream_t s) {
+  size_t b = temp_bytes;
+  (void)hipcub::DeviceRadixSort::SortPairs(temp, b, kin, kout, vin, vout, (int)n, 0, 64, s);
+  return b;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_kx_gather(const T* __restrict__ src, const uint32_t* __restrict__ perm,
+                                                   T* __restrict__ dst, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = src[perm[i]];
+}
+
+void launch_kx_gather32(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_kx_gather<uint32_t>, dim3((n + 255) / 256), dim3(256), 0, s, src, perm, dst, n);
+}
+
+void launch_kx_gather64(const uint64_t* src, const uint32_t* perm, uint64_t* dst, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_kx_gather<uint64_t>, dim3((n + 255) / 256), dim3(256), 0, s, src, perm, dst, n);
+}
+
+// distinct key hashes (run starts of the sorted hashes), one atomic per wavefront
+__global__ __launch_bounds__(256) void k_kx_count_keys(const uint64_t* __restrict__ h, uint32_t n,
+                                                       unsigned long long* __restrict__ keys) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const bool st = i < n && (i == 0 || h[i] != h[i - 1]);
+  const uint32_t c = (uint32_t)__popcll(__ballot(st));
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(keys, (unsigned long long)c);
+}
+
+void launch_kx_count_keys(const uint64_t* h, uint32_t n, unsigned long long* keys, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_kx_count_keys, dim3((n + 255) / 256), dim3(256), 0, s, h, n, keys);
+}
+
+// a run of equal hashes [i, j) becomes one slot; the thread at the run's start walks to its end
+// (runs are short: one key's parents — a hot key's run is long, but there is one per key)
+__global__ __launch_bounds__(256) void k_kx_table(const uint64_t* __restrict__ h, uint32_t n, KxSlot* __restrict__ tab,
+                                                  uint64_t mask, uint32_t* __restrict__ err) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || (i != 0 && h[i] == h[i - 1])) return;
+  const uint64_t k = h[i];
+  // the run's end: doubling, then a binary search (sorted hashes)
+  uint32_t lo = i, step = 1;
+  while (lo + step < n && h[lo + step] == k) {
+    lo += step;
+    step *= 2;
+  }
+  uint32_t hi = min(n, lo + step);  // h[lo] == k, h[hi] != k or hi == n
+  while (hi - lo > 1) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (h[m] == k) lo = m;
+    else hi = m;
+  }
+  uint64_t sl = mix64(k) & mask;
+  for (uint64_t probes = 0; probes <= mask; probes++) {
+    if (atomicCAS(reinterpret_cast<unsigned long long*>(&tab[sl].h), 0ull, (unsigned long long)k) == 0ull) {
+      tab[sl].start = i;
+      tab[sl].count = hi - i;
+      return;
+    }
+    sl = (sl + 1) & mask;
+  }
+  atomicOr(err, kErrWalkGuard);  // (the table holds twice the keys: not reached)
+}
+
+void launch_kx_table(const uint64_t* h, uint32_t n, KxSlot* tab, uint64_t mask, uint32_t* err, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_kx_table, dim3((n + 255) / 256), dim3(256), 0, s, h, n, tab, mask, err);
+}
+
+// the key's entries [x, y) (x == y: no image edge has that key)
+__device__ __forceinline__ uint2 kx_range(const MsgImg& img, const SegKey& k) {
+  const uint64_t h = kx_hash(k.k0, k.k1);
+  uint64_t sl = mix64(h) & img.kx_mask;
+  for (uint64_t probes = 0; probes <= img.kx_mask; probes++) {
+    const KxSlot e = img.kx_tab[sl];
+    if (e.h == h) return make_uint2(e.start, e.start + e.count);
+    if (e.h == 0) break;
+    sl = (sl + 1) & img.kx_mask;
+  }
+  return make_uint2(0u, 0u);
+}
+
+// the first entry of [a, b) whose parent position is >= x (entries of one key hash are sorted by it)
+__device__ __forceinline__ uint32_t kx_lower(const uint32_t* __restrict__ par, uint32_t a, uint32_t b, uint32_t x) {
+  while (a < b) {
+    const uint32_t m = (a + b) >> 1;
+    if (par[m] < x) a = m + 1;
+    else b = m;
+  }
+  return a;
+}
+
+// entry j's child if its key is the segment's (a hash shared by two keys interleaves their
+// entries; a long segment's bytes are compared as the edge lookups do), else kNone
+__device__ __forceinline__ uint32_t kx_hit(const MsgImg& img, const DevIndex& ix, uint32_t j, const SegKey& k,
+                                           const uint8_t* seg, uint32_t len) {
+  if (img.kx_k0[j] != k.k0 || img.kx_k1[j] != k.k1) return kNone;
+  const uint32_t c = img.kx_chd[j];
+  if (!seg_is_long(k)) return c;
+  const SegInfo si = ix.seginfo[ix.walk[img.node[c]].seg];
+  bool eq = si.len == len;
+  for (uint32_t i = 0; eq && i < len; i++) eq = ix.segbytes[si.off + i] == seg[i];
+  return eq ? c : kNone;
+}
+
 struct MsgFrame {  // a fan-out in progress: particles [cur, end) still to take segment s
   uint32_t cur, end, s;
 };
@@ -802,9 +957,31 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
           tot += ct;
         }
         if (lane == 0) mpre[wv][nr] = tot;
-        if (!FILL && img.work && lane == 0) atomicAdd(img.work + 0, (unsigned long long)tot);
+        // wide runs (round 6): the key index — one table probe, then per run the range of the key's
+        // entries whose parent lies in it (two binary searches); the level's work is then its hits
+        const bool kx = img.kx_tab != nullptr && tot > kKxMin;
+        uint32_t ri0[kMsgFront / 64], ri1[kMsgFront / 64];
+        uint32_t hits = 0;
+        if (kx) {
+          const uint2 kr = kx_range(img, key);
+#pragma unroll
+          for (uint32_t k = 0; k < kMsgFront / 64; k++) {
+            const uint32_t r = k * 64 + lane;
+            uint32_t a = 0, b = 0;
+            if (r < nr && kr.y > kr.x) {
+              a = kx_lower(img.kx_par, kr.x, kr.y, cur[r].x);
+              b = kx_lower(img.kx_par, a, kr.y, cur[r].y);
+            }
+            ri0[k] = a;
+            ri1[k] = b;
+            hits += wave_sum(b - a);
+          }
+        }
+        if (!FILL && img.work && lane == 0)
+          atomicAdd(img.work + 0, (unsigned long long)(kx ? hits + 2 * nr : tot));  // (edge-table probes, or
+                                                                                   //  hits + searches)
         wave_sync_lds();
-        if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && tot > w.min_tot) {
+        if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && (kx ? hits : tot) > w.min_tot) {
           if (FILL) {  // the count pass exported from here: its items write the rest
             if (cnt[t].shared) break;
           } else {
@@ -839,6 +1016,24 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
             }  // (the queue is full: this filter walks alone, as a fill walk will)
           }
         }
+        if (kx) {  // the runs become their entry ranges, the prefix counts their entries
+          wave_sync_lds();
+          uint32_t htot = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < kMsgFront / 64; k++) {
+            const uint32_t r = k * 64 + lane;
+            uint32_t ct;
+            const uint32_t ex = wave_excl_scan(r < nr ? ri1[k] - ri0[k] : 0u, lane, &ct);
+            if (r < nr) {
+              mpre[wv][r] = htot + ex;
+              cur[r] = make_uint2(ri0[k], ri1[k]);
+            }
+            htot += ct;
+          }
+          if (lane == 0) mpre[wv][nr] = htot;
+          tot = htot;
+          wave_sync_lds();
+        }
         for (uint32_t p0 = 0; p0 < tot; p0 += 64) {
           const uint32_t p = p0 + lane;
           uint32_t qc = kNone;
@@ -849,8 +1044,8 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
               if (mpre[wv][mid] <= p) lo = mid;
               else hi = mid;
             }
-            const uint32_t u = cur[lo].x + (p - mpre[wv][lo]);
-            qc = img_child(img, ix, u, key, fb + ls, len);
+            const uint32_t u = cur[lo].x + (p - mpre[wv][lo]);  // (a particle, or with the key index an entry)
+            qc = kx ? kx_hit(img, ix, u, key, fb + ls, len) : img_child(img, ix, u, key, fb + ls, len);
           }
           if (last) {
             if (qc != kNone) emit(img.lp[qc], img.lp[qc + 1] - img.lp[qc]);

@@ -84,8 +84,8 @@ OPT_MSG_IMAGE, OPT_WALK_WAVES, OPT_WALK_LISTS, OPT_MERGE_DEDUP = 8, 9, 10, 12
 OPT_SET_GRID, OPT_WALK_GROUP, OPT_ONE_SYNC, OPT_FUSE_DESC, OPT_SET_EXP, OPT_MSG_EXPORT = 14, 15, 16, 17, 18, 19
 OPT_PATCH_CODES = 20
 OPT_MSG_EDGES = 21
-OPT_MSG_EDGE_BUDGET, OPT_FAIL_NEXT, OPT_WALK_EXP = 22, 23, 24
-OPT_MAX = 24  # (include/mqmatch_dev.h MQ_OPT_MAX)
+OPT_MSG_EDGE_BUDGET, OPT_FAIL_NEXT, OPT_WALK_EXP, OPT_MSG_KEYIDX = 22, 23, 24, 25
+OPT_MAX = 25  # (include/mqmatch_dev.h MQ_OPT_MAX)
 
 
 class MsgResult(C.Structure):

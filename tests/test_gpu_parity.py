@@ -1008,6 +1008,41 @@ def test_messages_workload_parity(image, spec_mb, edges, gpu_available):
         assert d == od[i], i
 
 
+@pytest.mark.parametrize("keyidx", [1, 0])
+def test_messages_key_index(keyidx, gpu_available):
+    """Literal segments under wide runs (MQ_OPT_MSG_KEYIDX: the image's key index — one table
+    probe and two binary searches per run — or one edge-table probe per particle): short and
+    long (hashed, byte-verified) keys, keys that no particle of the run has, keys some runs share,
+    dense and sparse hits, nested fan-outs; every filter equal to the oracle (topics.go:547-576)."""
+    from mqmatch import engine as E
+    e, o = E.Engine(), O.OracleIndex()
+    e.set_option(E.OPT_MSG_KEYIDX, keyidx)
+    longa, longb = "l" * 20 + "a", "l" * 20 + "b"
+    topics, h = [], 0
+    for i in range(700):
+        topics.append(f"w/{i}/x")
+        if i % 3 == 0:
+            topics.append(f"w/{i}/{longa}")
+        if i % 7 == 0:
+            topics.append(f"w/{i}/{longb}/z")
+        if i % 50 == 0:
+            topics.append(f"v/{i}/x/q/{i % 4}")
+        topics.append(f"v/{i}/y")
+    for t in topics:
+        h += 1
+        assert e.retain_message(t, h, 1, True) == o.retain_message(t, h, 1, True)
+    filters = ["w/+/x", f"w/+/{longa}", f"w/+/{longb}/+", f"w/+/{longb}/#", "w/+/nope", f"w/+/{'l' * 20}c",
+               "+/+/x", "+/+/x/q/+", "+/+/x/+/1", "v/+/x/#", "+/+/y", "+/+/" + longa, "w/+/x/#", "+/+/+/q/#"] * 8
+    fb, fo = E.pack_strings(filters)
+    base, count, hs = e.messages_batch(fb, fo)
+    for i, f in enumerate(filters):
+        got = sorted(hs[int(base[i]):int(base[i]) + int(count[i])].tolist())
+        assert got == o.messages(f), f
+    res = e.messages_runs_batch(fb, fo)
+    assert _runs_sets(res, len(filters)) == [o.messages(f) for f in filters]
+    e.close()
+
+
 def _runs_sets(res, n):
     """Per-filter sorted handle lists of a Messages runs result (dict: run_base, n_runs, runs,
     handles), with each filter's runs checked to tile its [base, + count) of the expanded output."""
