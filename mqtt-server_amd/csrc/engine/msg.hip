@@ -925,6 +925,8 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       const uint32_t len = (uint32_t)(e - ls);
       const uint32_t c0 = len == 1 ? R.at(ls) : 0u;
       uint32_t nn = 0;  // the next frontier's runs (wave-uniform)
+      bool kx = false;  // a literal level through the key index (below)
+      uint2 rpx[kMsgFront / 64];  // ... the runs' particles (a frontier too wide for LDS walks them again)
       if (c0 == '+' || c0 == '#') {
         for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
           const uint32_t r = r0 + lane;
@@ -959,7 +961,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         if (lane == 0) mpre[wv][nr] = tot;
         // wide runs (round 6): the key index — one table probe, then per run the range of the key's
         // entries whose parent lies in it (two binary searches); the level's work is then its hits
-        const bool kx = img.kx_tab != nullptr && tot > kKxMin;
+        kx = img.kx_tab != nullptr && tot > kKxMin;
         uint32_t ri0[kMsgFront / 64], ri1[kMsgFront / 64];
         uint32_t hits = 0;
         if (kx) {
@@ -1026,6 +1028,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
             const uint32_t ex = wave_excl_scan(r < nr ? ri1[k] - ri0[k] : 0u, lane, &ct);
             if (r < nr) {
               mpre[wv][r] = htot + ex;
+              rpx[k] = cur[r];
               cur[r] = make_uint2(ri0[k], ri1[k]);
             }
             htot += ct;
@@ -1060,6 +1063,13 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       }
       if (last) break;
       if (nn > kMsgFront) {  // too wide for LDS: the per-lane walk from this level
+        if (kx) {  // the runs are the key index's entry ranges: their particles again
+          wave_sync_lds();
+#pragma unroll
+          for (uint32_t k = 0; k < kMsgFront / 64; k++)
+            if (k * 64 + lane < nr) cur[k * 64 + lane] = rpx[k];
+          wave_sync_lds();
+        }
         if (!FILL && img.work && lane == 0) {
           uint32_t np = 0;
           for (uint32_t r = 0; r < nr; r++) np += cur[r].y - cur[r].x;
