@@ -177,6 +177,9 @@ def main():
                     help="Messages by the particle walk (MQ_OPT_MSG_IMAGE 0) instead of the level-order image")
     ap.add_argument("--no-img-edges", action="store_true",
                     help="literal lookups through the index's edge table instead of the image's (MQ_OPT_MSG_EDGES 0)")
+    ap.add_argument("--no-key-index", action="store_true",
+                    help="a literal under wide runs probes each particle, without the image's key index "
+                         "(MQ_OPT_MSG_KEYIDX 0)")
     ap.add_argument("--oracle-only", metavar="OUT",
                     help="CPU side only (no GPU): build the oracle, write its sample digests, counters and "
                          "CPU baseline to OUT (JSON). At config 5's full size the oracle and the engine's "
@@ -215,6 +218,8 @@ def main():
         eng.set_option(E.OPT_MSG_IMAGE, 0)
     if args.no_img_edges:
         eng.set_option(E.OPT_MSG_EDGES, 0)
+    if args.no_key_index:
+        eng.set_option(E.OPT_MSG_KEYIDX, 0)
     eng.retain_bulk(rb, ro, hd)
     log(f"engine index built in {time.time() - t0:.1f}s: {eng.stats()}")
     stream = torch.cuda.current_stream()
@@ -268,7 +273,8 @@ def main():
         "kernels_ms_per_step": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
         "path": "particle walk (k_msg)" if args.walk else ("level-order image (k_msgq" + (", runs out" if runs else " + k_msg_copy") + "), literal lookups "
                                                           + ("through the index's edge table" if args.no_img_edges
-                                                             else "in the image's edge table")),
+                                                             else "in the image's edge table")
+                                                          + ("" if args.no_key_index else "; under wide runs the key index")),
         "image_build_ms": build[1] if build else None,
     }
     cpu = None

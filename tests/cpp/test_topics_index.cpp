@@ -349,6 +349,8 @@ static void TestConcurrentReadersAndUpdates() {
   std::atomic<int> bad{0}, late{0};
   std::atomic<long> progress[5];
   std::atomic<long> worst_us{0};
+  std::atomic<long> worst_warm_us{0};  // updates that started once every reader had matched a batch
+  std::atomic<int> readers_warm{0};
   std::mutex slow_mu;
   std::vector<std::pair<long, long>> slow;  // (us, ms since the start) of updates over 2 ms
   std::vector<std::pair<long, long>> slow_reads;  //   and of matches
@@ -387,18 +389,22 @@ static void TestConcurrentReadersAndUpdates() {
           if (kv.first.rfind("base", 0) != 0 && kv.first.rfind("tmp", 0) != 0) bad++;
         for (auto& kv : res[1].Subscriptions)
           if (kv.first.rfind("tmp", 0) != 0) bad++;
-        progress[w]++;
+        if (progress[w]++ == 0) readers_warm++;
       }
     });
   for (int u = 0; u < 2; u++)
     th.emplace_back([&, u] {
       auto timed = [&](auto&& f) {
+        const bool warm = readers_warm.load() == 3;
         const auto t0 = clk::now();
         f();
         const auto dt = clk::now() - t0;
         const long us = (long)std::chrono::duration_cast<std::chrono::microseconds>(dt).count();
         for (long w = worst_us.load(); us > w && !worst_us.compare_exchange_weak(w, us);) {
         }
+        if (warm)
+          for (long w = worst_warm_us.load(); us > w && !worst_warm_us.compare_exchange_weak(w, us);) {
+          }
         if (us > 2000) {
           std::lock_guard<std::mutex> g(slow_mu);
           slow.emplace_back(us, (long)std::chrono::duration_cast<std::chrono::milliseconds>(t0 - t_start).count());
@@ -443,6 +449,8 @@ static void TestConcurrentReadersAndUpdates() {
   std::fprintf(stderr, "  readers matched %ld batches during 3200 updates; slowest update %.1f ms\n",
                progress[0].load() + progress[1].load() + progress[2].load(), worst_us.load() / 1000.0);
   std::sort(slow.begin(), slow.end(), std::greater<std::pair<long, long>>());
+  std::fprintf(stderr, "  slowest update once every reader had matched a batch (its threads' first HIP calls done): %.2f ms\n",
+               worst_warm_us.load() / 1000.0);
   std::fprintf(stderr, "  engine-handle updates (no mirror): slowest %.1f ms\n", raw_worst_us.load() / 1000.0);
   std::fprintf(stderr, "  updates' longest waits: update lock %.1f ms (longest hold %.1f ms), tables %.1f ms, engine call %.1f ms\n",
                ix.update_waits().upd.load() / 1e3, ix.update_waits().held.load() / 1e3,
