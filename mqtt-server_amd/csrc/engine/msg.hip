@@ -688,6 +688,23 @@ __device__ __forceinline__ uint32_t kx_lower(const uint32_t* __restrict__ par, u
   return a;
 }
 
+// the same, the wave together (a, b, x wave-uniform; every lane calls): 64 samples a step narrow
+// [a, b) 64-fold, so a search is a few dependent loads instead of one per halving
+__device__ __forceinline__ uint32_t kx_lower_wave(const uint32_t* __restrict__ par, uint32_t a, uint32_t b, uint32_t x,
+                                                  uint32_t lane) {
+  while (b - a > 64) {
+    const uint32_t step = (b - a + 63) / 64;
+    const uint32_t i = a + lane * step;
+    const uint32_t c = (uint32_t)__popcll(__ballot(i < b && par[i] < x));  // samples below x: a prefix
+    if (c == 0) return a;
+    const uint32_t na = a + (c - 1) * step + 1;  // the sample before the bound is below x,
+    b = min(b, a + c * step);                    // the next one (or b) is not
+    a = na;
+  }
+  const uint32_t i = a + lane;
+  return a + (uint32_t)__popcll(__ballot(i < b && par[i] < x));
+}
+
 // entry j's child if its key is the segment's (a hash shared by two keys interleaves their
 // entries; a long segment's bytes are compared as the edge lookups do), else kNone
 __device__ __forceinline__ uint32_t kx_hit(const MsgImg& img, const DevIndex& ix, uint32_t j, const SegKey& k,
@@ -959,24 +976,52 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
           tot += ct;
         }
         if (lane == 0) mpre[wv][nr] = tot;
-        // wide runs (round 6): the key index — one table probe, then per run the range of the key's
-        // entries whose parent lies in it (two binary searches); the level's work is then its hits
-        kx = img.kx_tab != nullptr && tot > kKxMin;
+        // wide runs (round 6): the key index — one table probe, the key's entries narrowed to the
+        // frontier's span by two wave-wide searches, then per run the entries whose parent lies in
+        // it (wave-wide searches one run after another, or a binary search per lane); the level's
+        // work is then its hits. Taken when those searches take fewer dependent rounds than the
+        // probes of every particle (64 a round)
         uint32_t ri0[kMsgFront / 64], ri1[kMsgFront / 64];
-        uint32_t hits = 0;
-        if (kx) {
-          const uint2 kr = kx_range(img, key);
 #pragma unroll
-          for (uint32_t k = 0; k < kMsgFront / 64; k++) {
-            const uint32_t r = k * 64 + lane;
-            uint32_t a = 0, b = 0;
-            if (r < nr && kr.y > kr.x) {
-              a = kx_lower(img.kx_par, kr.x, kr.y, cur[r].x);
-              b = kx_lower(img.kx_par, a, kr.y, cur[r].y);
+        for (uint32_t k = 0; k < kMsgFront / 64; k++) ri0[k] = ri1[k] = 0;
+        uint32_t hits = 0;
+        kx = false;
+        const uint32_t probe_rounds = (tot + 63) / 64;
+        if (img.kx_tab != nullptr && probe_rounds > kKxMinRounds) {
+          const uint2 kr = kx_range(img, key);
+          const uint32_t n0 = kx_lower_wave(img.kx_par, kr.x, kr.y, cur[0].x, lane);
+          const uint32_t n1 = kx_lower_wave(img.kx_par, n0, kr.y, cur[nr - 1].y, lane);
+          const uint32_t span = n1 - n0;
+          uint32_t wave_steps = 1;  // a wave-wide search over the span: 64 samples a step
+          for (uint32_t m = span; m > 64; m = (m + 63) / 64) wave_steps++;
+          const uint32_t wave_cost = 2 * nr * wave_steps;
+          const uint32_t lane_cost = 2 * (32 - __clz(span)) * ((nr + 63) / 64);
+          if (nr <= 64 && wave_cost <= lane_cost && wave_cost < probe_rounds) {
+            kx = true;
+            for (uint32_t r = 0; r < nr; r++) {
+              const uint2 ru = cur[r];
+              const uint32_t a = kx_lower_wave(img.kx_par, n0, n1, ru.x, lane);
+              const uint32_t b = kx_lower_wave(img.kx_par, a, n1, ru.y, lane);
+              if (lane == r) {
+                ri0[0] = a;
+                ri1[0] = b;
+              }
+              hits += b - a;
             }
-            ri0[k] = a;
-            ri1[k] = b;
-            hits += wave_sum(b - a);
+          } else if (lane_cost < probe_rounds) {
+            kx = true;
+#pragma unroll
+            for (uint32_t k = 0; k < kMsgFront / 64; k++) {
+              const uint32_t r = k * 64 + lane;
+              uint32_t a = 0, b = 0;
+              if (r < nr) {
+                a = kx_lower(img.kx_par, n0, n1, cur[r].x);
+                b = kx_lower(img.kx_par, a, n1, cur[r].y);
+              }
+              ri0[k] = a;
+              ri1[k] = b;
+              hits += wave_sum(b - a);
+            }
           }
         }
         if (!FILL && img.work && lane == 0)

@@ -1011,15 +1011,20 @@ def test_messages_workload_parity(image, spec_mb, edges, gpu_available):
 @pytest.mark.parametrize("keyidx", [1, 0])
 def test_messages_key_index(keyidx, gpu_available):
     """Literal segments under wide runs (MQ_OPT_MSG_KEYIDX: the image's key index — one table
-    probe and two binary searches per run — or one edge-table probe per particle): short and
-    long (hashed, byte-verified) keys, keys that no particle of the run has, keys some runs share,
-    dense and sparse hits, nested fan-outs; every filter equal to the oracle (topics.go:547-576)."""
+    probe, then per run wave-wide searches or a binary search per lane — or one edge-table probe
+    per particle): short and long (hashed, byte-verified) keys, keys that no particle of the run
+    has, keys some runs share, dense and sparse hits, one wide run (w/+/...) and some hundred runs
+    (u/+/k/+/...), nested fan-outs; every filter equal to the oracle (topics.go:547-576)."""
     from mqmatch import engine as E
     e, o = E.Engine(), O.OracleIndex()
     e.set_option(E.OPT_MSG_KEYIDX, keyidx)
     longa, longb = "l" * 20 + "a", "l" * 20 + "b"
     topics, h = [], 0
-    for i in range(700):
+    for i in range(200):
+        for j in range(40):
+            topics.append(f"u/{i}/k/{j}/{'m' if j % 3 else 'n'}")
+        topics.append(f"u/{i}/j/0/m")
+    for i in range(3000):
         topics.append(f"w/{i}/x")
         if i % 3 == 0:
             topics.append(f"w/{i}/{longa}")
@@ -1032,7 +1037,8 @@ def test_messages_key_index(keyidx, gpu_available):
         h += 1
         assert e.retain_message(t, h, 1, True) == o.retain_message(t, h, 1, True)
     filters = ["w/+/x", f"w/+/{longa}", f"w/+/{longb}/+", f"w/+/{longb}/#", "w/+/nope", f"w/+/{'l' * 20}c",
-               "+/+/x", "+/+/x/q/+", "+/+/x/+/1", "v/+/x/#", "+/+/y", "+/+/" + longa, "w/+/x/#", "+/+/+/q/#"] * 8
+               "+/+/x", "+/+/x/q/+", "+/+/x/+/1", "v/+/x/#", "+/+/y", "+/+/" + longa, "w/+/x/#", "+/+/+/q/#",
+               "u/+/k/+/m", "u/+/k/+/n/#", "u/+/+/+/m", "+/+/k/+/n", "u/+/k/+/z"] * 8
     fb, fo = E.pack_strings(filters)
     base, count, hs = e.messages_batch(fb, fo)
     for i, f in enumerate(filters):
