@@ -42,7 +42,7 @@ def log(msg):
     print(f"[bench_messages {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def read_msg_traffic(n_retained, n_filters, fmt="handles"):
+def read_msg_traffic(n_retained, n_filters, fmt="handles", key_index=True):
     """HBM bytes per Messages step (k_msgq passes + k_msg_copy: FETCH_SIZE x1 for the walks' random
     loads, x2 for k_msg_copy's streams, + WRITE_SIZE) from a committed rocprofv3 PMC summary of the
     same configuration (retained topics, filters per step, export threshold, output format), if
@@ -51,6 +51,8 @@ def read_msg_traffic(n_retained, n_filters, fmt="handles"):
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
             e = json.load(f).get("messages" if fmt == "handles" else "messages_runs", {}).get(str(n_retained))
         if e is None or int(e["filters"]) != n_filters or int(e.get("export", 1)) != 1:
+            return None
+        if bool(e.get("key_index", False)) != key_index:  # (the round-6 entries were taken with the key index)
             return None
         return float(e["hbm_bytes_per_step"])
     except (OSError, ValueError, KeyError, TypeError):
@@ -180,6 +182,9 @@ def main():
     ap.add_argument("--no-key-index", action="store_true",
                     help="a literal under wide runs probes each particle, without the image's key index "
                          "(MQ_OPT_MSG_KEYIDX 0)")
+    ap.add_argument("--key-index-rounds", type=int, default=0,
+                    help="MQ_OPT_MSG_KEYIDX N (N >= 2): a literal level tries the key index above N rounds "
+                         "of particle probes instead of kKxMinRounds")
     ap.add_argument("--oracle-only", metavar="OUT",
                     help="CPU side only (no GPU): build the oracle, write its sample digests, counters and "
                          "CPU baseline to OUT (JSON). At config 5's full size the oracle and the engine's "
@@ -220,6 +225,8 @@ def main():
         eng.set_option(E.OPT_MSG_EDGES, 0)
     if args.no_key_index:
         eng.set_option(E.OPT_MSG_KEYIDX, 0)
+    elif args.key_index_rounds >= 2:
+        eng.set_option(E.OPT_MSG_KEYIDX, args.key_index_rounds)
     eng.retain_bulk(rb, ro, hd)
     log(f"engine index built in {time.time() - t0:.1f}s: {eng.stats()}")
     stream = torch.cuda.current_stream()
@@ -345,7 +352,7 @@ def main():
                 b_img = 8 * per["L"] + 4 + 16 * int(r.n_handles) / max(1, n)
                 bytes_note = "8 B per level + 4 B offset per filter, 16 B per emitted handle (read + write)"
             ach = b_img * n / (kms * 1e-3) / 1e9
-            traffic = read_msg_traffic(args.retained, n, args.format) if not args.walk else None  # (keyed by --retained)
+            traffic = read_msg_traffic(args.retained, n, args.format, not args.no_key_index) if not args.walk else None  # (keyed by --retained)
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                                "kernel": ("k_msgq (count, wide count, place, wide place)" + ("" if runs else " + k_msg_copy")

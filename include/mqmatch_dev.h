@@ -64,8 +64,10 @@
                                      walk's saving bounds what staging the root's children in LDS could save;
                                      bit 1 (round 6): levels 0 and 1 (the frontier's level-1 probes too) */
 #define MQ_OPT_MSG_KEYIDX 25      /* Messages: 1 (default) builds the retained image's key index with the image
-                                     (edges sorted by key, then parent): a literal segment under runs of more than
-                                     kKxMin particles is one table probe and two binary searches per run; 0: one
+                                     (edges sorted by key hash, then parent): a literal segment under runs whose
+                                     particles take more than kKxMinRounds rounds of probes (64 a round) is one
+                                     table probe and searches of the key's entries, when those take fewer
+                                     dependent rounds; v >= 2: the same with v in place of kKxMinRounds; 0: one
                                      edge-table probe per particle of the runs */
 #define MQ_OPT_MAX 25             /* the highest option number mq_set_option admits */
 #define MQ_OPT_FUSE_DESC 17       /* one-sync span batches: 1 (default) runs k_desc in the frontier walk's

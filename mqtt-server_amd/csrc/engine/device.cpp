@@ -362,6 +362,7 @@ bool Device::set_option(uint32_t opt, uint64_t v) {
     case MQ_OPT_PATCH_CODES: patch_codes_ = v != 0; return true;
     case MQ_OPT_MSG_KEYIDX:
       msg_kx_on_ = v != 0;
+      msg_kx_min_ = v >= 2 ? (uint32_t)v : kKxMinRounds;
       img_version_ = ~0ull;  // (rebuilt with or without it)
       return true;
     case MQ_OPT_MSG_EDGES:
@@ -2442,6 +2443,7 @@ MsgImg Device::msg_img() const {
   m.run_cnt = nullptr;
   m.kx_tab = kx_built_ ? kx_tab_.as<KxSlot>() : nullptr;
   m.kx_mask = kx_mask_;
+  m.kx_min_rounds = msg_kx_min_;
   m.kx_par = kx_par_.as<uint32_t>();
   m.kx_chd = kx_chd_.as<uint32_t>();
   m.kx_k0 = kx_k0_.as<uint64_t>();

@@ -501,6 +501,7 @@ class Device {
   uint64_t kx_mask_ = 0;
   bool kx_built_ = false;
   bool msg_kx_on_ = true;             // MQ_OPT_MSG_KEYIDX
+  uint32_t msg_kx_min_ = kKxMinRounds;  // ... its probe rounds below which a level does not try it
   void build_key_index(const DevIndex& di, uint32_t n_img, uint32_t n_pos, hipStream_t s);
   DevBuf msg_gate_;                   // one-sync Messages batches: the gate and the piece count (k_msg_gate)
   uint64_t img_edge_mask_ = 0;

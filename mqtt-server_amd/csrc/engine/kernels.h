@@ -558,6 +558,7 @@ struct MsgImg {
   // key whose parent lies in the run), not one edge-table probe per particle of the runs.
   const struct KxSlot* kx_tab;
   uint64_t kx_mask;
+  uint32_t kx_min_rounds;  // kKxMinRounds, or MQ_OPT_MSG_KEYIDX's value
   const uint32_t* kx_par;
   const uint32_t* kx_chd;
   const uint64_t* kx_k0;

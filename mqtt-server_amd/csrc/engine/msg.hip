@@ -987,15 +987,17 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         uint32_t hits = 0;
         kx = false;
         const uint32_t probe_rounds = (tot + 63) / 64;
-        if (img.kx_tab != nullptr && probe_rounds > kKxMinRounds) {
+        if (img.kx_tab != nullptr && probe_rounds > img.kx_min_rounds) {
           const uint2 kr = kx_range(img, key);
           const uint32_t n0 = kx_lower_wave(img.kx_par, kr.x, kr.y, cur[0].x, lane);
           const uint32_t n1 = kx_lower_wave(img.kx_par, n0, kr.y, cur[nr - 1].y, lane);
           const uint32_t span = n1 - n0;
           uint32_t wave_steps = 1;  // a wave-wide search over the span: 64 samples a step
           for (uint32_t m = span; m > 64; m = (m + 63) / 64) wave_steps++;
-          const uint32_t wave_cost = 2 * nr * wave_steps;
-          const uint32_t lane_cost = 2 * (32 - __clz(span)) * ((nr + 63) / 64);
+          // dependent rounds: the searches, then a load per hit (at most the span's entries)
+          const uint32_t hit_rounds = (span + 63) / 64;
+          const uint32_t wave_cost = 2 * nr * wave_steps + hit_rounds;
+          const uint32_t lane_cost = 2 * (32 - __clz(span)) * ((nr + 63) / 64) + hit_rounds;
           if (nr <= 64 && wave_cost <= lane_cost && wave_cost < probe_rounds) {
             kx = true;
             for (uint32_t r = 0; r < nr; r++) {
