@@ -42,7 +42,7 @@ def log(msg):
     print(f"[bench_messages {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def read_msg_traffic(n_retained, n_filters, fmt="handles", key_index=True):
+def read_msg_traffic(n_retained, n_filters, fmt="handles", key_index=True, export=1):
     """HBM bytes per Messages step (k_msgq passes + k_msg_copy: FETCH_SIZE x1 for the walks' random
     loads, x2 for k_msg_copy's streams, + WRITE_SIZE) from a committed rocprofv3 PMC summary of the
     same configuration (retained topics, filters per step, export threshold, output format), if
@@ -50,7 +50,7 @@ def read_msg_traffic(n_retained, n_filters, fmt="handles", key_index=True):
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
             e = json.load(f).get("messages" if fmt == "handles" else "messages_runs", {}).get(str(n_retained))
-        if e is None or int(e["filters"]) != n_filters or int(e.get("export", 1)) != 1:
+        if e is None or int(e["filters"]) != n_filters or int(e.get("export", 1)) != export:
             return None
         if bool(e.get("key_index", False)) != key_index:  # (the round-6 entries were taken with the key index)
             return None
@@ -185,6 +185,9 @@ def main():
     ap.add_argument("--key-index-rounds", type=int, default=0,
                     help="MQ_OPT_MSG_KEYIDX N (N >= 2): a literal level tries the key index above N rounds "
                          "of particle probes instead of kKxMinRounds")
+    ap.add_argument("--export", type=int, default=1,
+                    help="MQ_OPT_MSG_EXPORT: 0 off, 1 kMsgExportMin (default), else the threshold (hits under the "
+                         "key index, particles without it) above which a filter's literal level goes to work items")
     ap.add_argument("--oracle-only", metavar="OUT",
                     help="CPU side only (no GPU): build the oracle, write its sample digests, counters and "
                          "CPU baseline to OUT (JSON). At config 5's full size the oracle and the engine's "
@@ -223,6 +226,8 @@ def main():
         eng.set_option(E.OPT_MSG_IMAGE, 0)
     if args.no_img_edges:
         eng.set_option(E.OPT_MSG_EDGES, 0)
+    if args.export != 1:
+        eng.set_option(E.OPT_MSG_EXPORT, args.export)
     if args.no_key_index:
         eng.set_option(E.OPT_MSG_KEYIDX, 0)
     elif args.key_index_rounds >= 2:
@@ -352,7 +357,7 @@ def main():
                 b_img = 8 * per["L"] + 4 + 16 * int(r.n_handles) / max(1, n)
                 bytes_note = "8 B per level + 4 B offset per filter, 16 B per emitted handle (read + write)"
             ach = b_img * n / (kms * 1e-3) / 1e9
-            traffic = read_msg_traffic(args.retained, n, args.format, not args.no_key_index) if not args.walk else None  # (keyed by --retained)
+            traffic = read_msg_traffic(args.retained, n, args.format, not args.no_key_index, args.export) if not args.walk else None  # (keyed by --retained)
             out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                                "kernel": ("k_msgq (count, wide count, place, wide place)" + ("" if runs else " + k_msg_copy")

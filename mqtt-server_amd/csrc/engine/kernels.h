@@ -645,7 +645,9 @@ struct MsgWide {
   MsgRun* scratch;        // the counting wavefronts' recorded runs: wavefront w's at [w * per_wave, ...)
   uint32_t per_wave;
 };
-constexpr uint32_t kMsgChunk = 256;       // particles per exported work item
+constexpr uint32_t kMsgChunk = 256;       // particles per exported work item (or key-index entries)
+constexpr uint32_t kMsgWorkEntries = 1u << 31;  // MsgWork.s: the item's [x, y) is a range of key-index entries
+static_assert(kMsgChunk <= 256, "an entry item's hits must fit the fan-out frontier (kMsgFront)");
 constexpr uint32_t kMsgWorkCap = 1u << 20;  // work items per batch (32 MB)
 constexpr uint32_t kMsgWideRuns = 4096;     // recorded runs per wide-count wavefront (64 KB each)
 constexpr uint32_t kMsgExportMin = 512;   // export a literal level under a fan-out of more particles (10M: 2048 -> 512, 2.75 -> 2.50 ms)

@@ -928,7 +928,9 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
   // a frame stack). The filter's own count pass may export the fan-out to work items (MsgWide)
   // instead; an item runs the same fan-out from its run (the wide modes).
   bool exported = false;  // the count pass handed the filter's fan-out to work items (MsgWide)
-  auto fan_out = [&](uint32_t fa, uint32_t fbnd, uint64_t fs) __attribute__((always_inline)) {
+  // entries: [fa, fbnd) is a range of the key index's entries for the literal segment at fs (an item
+  // exported from a literal level that took the key index), not a run of particles
+  auto fan_out = [&](uint32_t fa, uint32_t fbnd, uint64_t fs, bool entries) __attribute__((always_inline)) {
     uint2* cur = mfront[wv][0];
     uint2* nxt = mfront[wv][1];
     uint32_t nr = 1;
@@ -936,6 +938,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
     if (lane == 0) cur[0] = make_uint2(fa, fbnd);
     wave_sync_lds();
     uint64_t ls = fs;  // the segment the frontier's runs take next
+    bool ent = entries;
     for (uint32_t guard = 0; guard < 4096; guard++) {
       const uint64_t e = find_slash(R, ls, b1);
       const bool last = e >= b1;
@@ -943,6 +946,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       const uint32_t c0 = len == 1 ? R.at(ls) : 0u;
       uint32_t nn = 0;  // the next frontier's runs (wave-uniform)
       bool kx = false;  // a literal level through the key index (below)
+      bool ent_level = false;  // ... whose runs are entry ranges already (an exported item's first level)
       uint2 rpx[kMsgFront / 64];  // ... the runs' particles (a frontier too wide for LDS walks them again)
       if (c0 == '+' || c0 == '#') {
         for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
@@ -985,9 +989,12 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
 #pragma unroll
         for (uint32_t k = 0; k < kMsgFront / 64; k++) ri0[k] = ri1[k] = 0;
         uint32_t hits = 0;
-        kx = false;
+        ent_level = ent;
+        ent = false;
+        kx = ent_level;
+        if (ent_level) hits = tot;
         const uint32_t probe_rounds = (tot + 63) / 64;
-        if (img.kx_tab != nullptr && probe_rounds > img.kx_min_rounds) {
+        if (!ent_level && img.kx_tab != nullptr && probe_rounds > img.kx_min_rounds) {
           const uint2 kr = kx_range(img, key);
           const uint32_t n0 = kx_lower_wave(img.kx_par, kr.x, kr.y, cur[0].x, lane);
           const uint32_t n1 = kx_lower_wave(img.kx_par, n0, kr.y, cur[nr - 1].y, lane);
@@ -1034,30 +1041,30 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
           if (FILL) {  // the count pass exported from here: its items write the rest
             if (cnt[t].shared) break;
           } else {
-            // the runs as items of at most kMsgChunk particles (one reservation for all)
+            // the runs as items of at most kMsgChunk particles — or, through the key index, the
+            // runs' entry ranges as items of at most kMsgChunk entries (one reservation for all)
             uint32_t nit = 0;
-            for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-              const uint32_t r = r0 + lane;
-              const uint32_t c = r < nr ? (cur[r].y - cur[r].x + kMsgChunk - 1) / kMsgChunk : 0u;
-              nit += wave_sum(c);
+#pragma unroll
+            for (uint32_t k = 0; k < kMsgFront / 64; k++) {
+              const uint32_t r = k * 64 + lane;
+              const uint32_t x = r < nr ? (kx ? ri0[k] : cur[r].x) : 0u, y = r < nr ? (kx ? ri1[k] : cur[r].y) : 0u;
+              nit += wave_sum((y - x + kMsgChunk - 1) / kMsgChunk);
             }
             uint32_t ib = 0;
             if (lane == 0) ib = atomicAdd(w.n_items, nit);
             ib = __shfl(ib, 0, 64);
             if (ib + nit <= w.cap) {
-              for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
-                const uint32_t r = r0 + lane;
-                uint32_t x = 0, y = 0;
-                if (r < nr) {
-                  x = cur[r].x;
-                  y = cur[r].y;
-                }
+              const uint32_t s_item = (uint32_t)(ls - b0) | (kx ? kMsgWorkEntries : 0u);
+#pragma unroll
+              for (uint32_t k = 0; k < kMsgFront / 64; k++) {
+                const uint32_t r = k * 64 + lane;
+                const uint32_t x = r < nr ? (kx ? ri0[k] : cur[r].x) : 0u, y = r < nr ? (kx ? ri1[k] : cur[r].y) : 0u;
                 const uint32_t c = (y - x + kMsgChunk - 1) / kMsgChunk;
                 uint32_t ct;
                 const uint32_t ex = wave_excl_scan(c, lane, &ct);
-                for (uint32_t k = 0; k < c; k++)
-                  w.items[ib + ex + k] = MsgWork{t, x + k * kMsgChunk, (uint32_t)min((uint32_t)y, (uint32_t)(x + (k + 1) * kMsgChunk)),
-                                                 (uint32_t)(ls - b0), 0u, 0u, 0u, kNone};
+                for (uint32_t j = 0; j < c; j++)
+                  w.items[ib + ex + j] = MsgWork{t, x + j * kMsgChunk, (uint32_t)min((uint32_t)y, (uint32_t)(x + (j + 1) * kMsgChunk)),
+                                                 s_item, 0u, 0u, 0u, kNone};
                 ib += ct;
               }
               exported = true;
@@ -1065,7 +1072,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
             }  // (the queue is full: this filter walks alone, as a fill walk will)
           }
         }
-        if (kx) {  // the runs become their entry ranges, the prefix counts their entries
+        if (kx && !ent_level) {  // the runs become their entry ranges, the prefix counts their entries
           wave_sync_lds();
           uint32_t htot = 0;
 #pragma unroll
@@ -1110,6 +1117,10 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
       }
       if (last) break;
       if (nn > kMsgFront) {  // too wide for LDS: the per-lane walk from this level
+        if (ent_level) {  // (not reached: an item's entries are at most kMsgChunk <= kMsgFront hits)
+          if (lane == 0) atomicOr(ix.err, kErrMsgNest);
+          break;
+        }
         if (kx) {  // the runs are the key index's entry ranges: their particles again
           wave_sync_lds();
 #pragma unroll
@@ -1175,7 +1186,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         pbase = off[t].g;
       }
       wave_sync_lds();
-      fan_out(it.x, it.y, b0 + it.s);
+      fan_out(it.x, it.y, b0 + (it.s & ~kMsgWorkEntries), (it.s & kMsgWorkEntries) != 0);
       wave_sync_lds();
       if (!FILL && lane == 0) {  // the item's place in its filter's output: after the count pass's own part
         const uint32_t r1 = rcur[wv];
@@ -1245,7 +1256,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
         b = qc + 1;
         s = e + 1;
       }
-      if (fan) fan_out(a, b, s);
+      if (fan) fan_out(a, b, s, false);
     }
   }
   if (!FILL) {
