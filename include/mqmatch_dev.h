@@ -46,8 +46,9 @@
 #define MQ_OPT_PATCH_CODES 20     /* host span results: 1 (default) 4-byte patch codes when the index allows them
                                      (MQ_SPANS_PATCH_CODES); 0: 8-byte mq_patch records */
 #define MQ_OPT_MSG_EXPORT 19      /* Messages: 1 (default) hands a literal level under a fan-out of more than
-                                     kMsgExportMin particles to work items any wavefront takes; > 1: that
-                                     threshold; 0: the filter's wavefront walks it alone */
+                                     kMsgExportMin particles (through the key index: more than
+                                     kMsgExportMinHits candidate entries) to work items any wavefront takes;
+                                     > 1: that threshold for both; 0: the filter's wavefront walks it alone */
 #define MQ_OPT_MSG_EDGES 21       /* Messages: 1 (default) looks a literal segment up in the retained image's own
                                      edge table (parent image position, segment) -> child image position, one
                                      probe; 0: the index's edge table, then the particle's image position */

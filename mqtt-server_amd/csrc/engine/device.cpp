@@ -2491,6 +2491,7 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
     wide.n_items = reinterpret_cast<uint32_t*>(wide.items + kMsgWorkCap);
     wide.cap = kMsgWorkCap;
     wide.min_tot = msg_export_ > 1 ? msg_export_ : kMsgExportMin;
+    wide.min_hits = msg_export_ > 1 ? msg_export_ : kMsgExportMinHits;
     msg_wscratch_.ensure((size_t)n_cus_ * 8 * 4 * kMsgWideRuns * sizeof(MsgRun));
     wide.scratch = msg_wscratch_.as<MsgRun>();
     wide.per_wave = kMsgWideRuns;

@@ -641,10 +641,14 @@ struct MsgWork {  // filter t: particles [x, y) of a fan-out, to take the filter
 struct MsgWide {
   MsgWork* items;
   uint32_t cap, min_tot;  // min_tot 0: no export
+  uint32_t min_hits;      // ... a level through the key index: more than min_hits candidate entries
   uint32_t* n_items;      // items reserved (a reservation past cap fails: that filter walks alone)
   MsgRun* scratch;        // the counting wavefronts' recorded runs: wavefront w's at [w * per_wave, ...)
   uint32_t per_wave;
 };
+// a literal level through the key index exports more than this many candidate entries (its items
+// look up entries, not particles; 10M retained: 512 -> 128, 83.4M -> 127.8M filters/s, r06/p)
+constexpr uint32_t kMsgExportMinHits = 128;
 constexpr uint32_t kMsgChunk = 256;       // particles per exported work item (or key-index entries)
 constexpr uint32_t kMsgWorkEntries = 1u << 31;  // MsgWork.s: the item's [x, y) is a range of key-index entries
 static_assert(kMsgChunk <= 256, "an entry item's hits must fit the fan-out frontier (kMsgFront)");

@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, co
           atomicAdd(img.work + 0, (unsigned long long)(kx ? hits + 2 * nr : tot));  // (edge-table probes, or
                                                                                    //  hits + searches)
         wave_sync_lds();
-        if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && (kx ? hits : tot) > w.min_tot) {
+        if ((RUNS || MODE == kMsgFill || MODE == kMsgPlace) && w.min_tot && (kx ? hits > w.min_hits : tot > w.min_tot)) {
           if (FILL) {  // the count pass exported from here: its items write the rest
             if (cnt[t].shared) break;
           } else {
