@@ -7,6 +7,10 @@ cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r06/final
 mkdir -p $O
+# a line a minute under gpurun_out while the long steps build their 10M-subscription indexes in silence
+( while true; do date >> $O/heartbeat.log; sleep 60; done ) &
+HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu > $O/trace.json 2> $O/trace.err || exit 1
 cd $R
 timeout -k 10 500 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 1
