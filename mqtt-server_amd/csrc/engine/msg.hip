@@ -746,8 +746,18 @@ struct MsgqParams {
   MsgWide w;
 };
 
+// waves per SIMD asked of the register allocator, per pass (MQ_MSGQ_WAVES_RUNS / _OTHER: build-time
+// A/B); the passes are latency-bound probe rounds, so occupancy pays while nothing spills
+#ifndef MQ_MSGQ_WAVES_RUNS
+#define MQ_MSGQ_WAVES_RUNS 1
+#endif
+#ifndef MQ_MSGQ_WAVES_OTHER
+#define MQ_MSGQ_WAVES_OTHER 1
+#endif
+constexpr int msgq_waves(int mode) { return mode == kMsgRuns ? MQ_MSGQ_WAVES_RUNS : MQ_MSGQ_WAVES_OTHER; }
+
 template <int MODE>
-__global__ __launch_bounds__(256) void k_msgq(const uint8_t* __restrict__ fb, const uint64_t* __restrict__ fo,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(msgq_waves(MODE)))) void k_msgq(const uint8_t* __restrict__ fb, const uint64_t* __restrict__ fo,
                                               uint32_t n, DevIndex ix_, MsgImg img_,
                                               TopicCount* __restrict__ cnt, const TopicOff* __restrict__ off,
                                               MsgPiece* __restrict__ pieces, uint64_t* __restrict__ handles,
