@@ -282,6 +282,9 @@ def main():
         "format": args.format, "handles_per_step": handles, "handles_per_filter": handles / max(1, n),
         "runs_per_step": int(r.n_runs_total) if runs else None,
         "fanout_lookups_per_step": lookups,
+        "count_pass_filter_clocks": {k[len("msg_cyc16_"):]: 16 * wk[k][0] for k in wk if k.startswith("msg_cyc16_")},
+        "count_pass_lane_walks": {"filters": wk.get("msg_lane_walk_filters", (0, 0))[0],
+                                  "particles": wk.get("msg_lane_walk_particles", (0, 0))[0]},
         "kernels_ms_per_step": {k: v[1] / args.steps for k, v in prof.items() if v[1] > 0},
         "path": "particle walk (k_msg)" if args.walk else ("level-order image (k_msgq" + (", runs out" if runs else " + k_msg_copy") + "), literal lookups "
                                                           + ("through the index's edge table" if args.no_img_edges

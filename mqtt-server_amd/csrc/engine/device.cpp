@@ -2594,6 +2594,8 @@ bool Device::messages_img(const DevIndex& di, const uint8_t* d_fb, const uint64_
     }
     prof.count("msg_cyc16_total", tot_c);
     prof.count("msg_cyc16_max", n ? c[0] : 0);
+    prof.count("msg_cyc16_p50", n ? c[n / 2] : 0);
+    prof.count("msg_cyc16_p99", n ? c[n / 100] : 0);
     prof.count("msg_cyc16_top1pct", top1);
     prof.count("msg_cyc16_top01pct", top01);
     prof.count("msg_fanout_lookups", w[0]);
