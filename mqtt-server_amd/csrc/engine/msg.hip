@@ -870,10 +870,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(msgq_waves(
     }
   };
   ByteReader R(fb);
-  auto dfs_run = [&](uint32_t ra, uint32_t rb, uint64_t rs) __attribute__((always_inline)) {
+  // ent: [ra, rb) are key-index entries of the literal segment (ek, at els, elen bytes) just before
+  // rs; each lane starts from its entries' children instead of from particles
+  auto dfs_run = [&](uint32_t ra, uint32_t rb, uint64_t rs, bool ent, const SegKey& ek, uint64_t els,
+                     uint32_t elen) __attribute__((always_inline)) {
     MsgFrame st[kMsgStack];
     for (uint32_t u = ra + lane; u < rb; u += 64) {
-      uint32_t sp = 0, ua = u, ub = u + 1;
+      uint32_t ua = u;
+      if (ent) {
+        ua = kx_hit(img, ix, u, ek, fb + els, elen);
+        if (ua == kNone) continue;
+      }
+      uint32_t sp = 0, ub = ua + 1;
       uint64_t us = rs;
       for (uint64_t guard = 0;; guard++) {
         if (guard > kWalkGuard) {
@@ -957,7 +965,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(msgq_waves(
       uint32_t nn = 0;  // the next frontier's runs (wave-uniform)
       bool kx = false;  // a literal level through the key index (below)
       bool ent_level = false;  // ... whose runs are entry ranges already (an exported item's first level)
-      uint2 rpx[kMsgFront / 64];  // ... the runs' particles (a frontier too wide for LDS walks them again)
+      SegKey lit_key{0, 0};  // ... its key (a frontier too wide for LDS walks on from its entries)
       if (c0 == '+' || c0 == '#') {
         for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
           const uint32_t r = r0 + lane;
@@ -980,6 +988,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(msgq_waves(
         // literal: every particle of every run looks the segment up; particle p of the
         // frontier is found through the runs' prefix sums
         const SegKey key = key_of(R, ls, e);
+        lit_key = key;
         uint32_t tot = 0;
         for (uint32_t r0 = 0; r0 < nr; r0 += 64) {
           const uint32_t r = r0 + lane;
@@ -1092,7 +1101,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(msgq_waves(
             const uint32_t ex = wave_excl_scan(r < nr ? ri1[k] - ri0[k] : 0u, lane, &ct);
             if (r < nr) {
               mpre[wv][r] = htot + ex;
-              rpx[k] = cur[r];
               cur[r] = make_uint2(ri0[k], ri1[k]);
             }
             htot += ct;
@@ -1131,13 +1139,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(msgq_waves(
           if (lane == 0) atomicOr(ix.err, kErrMsgNest);
           break;
         }
-        if (kx) {  // the runs are the key index's entry ranges: their particles again
-          wave_sync_lds();
-#pragma unroll
-          for (uint32_t k = 0; k < kMsgFront / 64; k++)
-            if (k * 64 + lane < nr) cur[k * 64 + lane] = rpx[k];
-          wave_sync_lds();
-        }
+        // (through the key index the runs are entry ranges: the lanes walk on from their hits)
         if (!FILL && img.work && lane == 0) {
           uint32_t np = 0;
           for (uint32_t r = 0; r < nr; r++) np += cur[r].y - cur[r].x;
@@ -1146,7 +1148,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(msgq_waves(
         }
         for (uint32_t r = 0; r < nr; r++) {
           const uint2 ru = cur[r];
-          dfs_run(ru.x, ru.y, ls);
+          if (kx) dfs_run(ru.x, ru.y, e + 1, true, lit_key, ls, len);
+          else dfs_run(ru.x, ru.y, ls, false, lit_key, ls, len);
         }
         break;
       }
