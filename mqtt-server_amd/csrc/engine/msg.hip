@@ -749,7 +749,7 @@ struct MsgqParams {
 // waves per SIMD asked of the register allocator, per pass (MQ_MSGQ_WAVES_RUNS / _OTHER: build-time
 // A/B); the passes are latency-bound probe rounds, so occupancy pays while nothing spills
 #ifndef MQ_MSGQ_WAVES_RUNS
-#define MQ_MSGQ_WAVES_RUNS 6  // (r06/v: 80 VGPRs, 28 spilled in the cold paths, against 96 at 5: count 0.378 -> 0.356 ms)
+#define MQ_MSGQ_WAVES_RUNS 6  // (r06/v: 80 VGPRs with 28 spilled, against 96 at 5 waves: count 0.378 -> 0.356 ms)
 #endif
 #ifndef MQ_MSGQ_WAVES_OTHER
 #define MQ_MSGQ_WAVES_OTHER 1
