@@ -251,7 +251,8 @@ def main():
     for _ in range(args.warmup):
         r = step()
     torch.cuda.synchronize()
-    build = eng.profile_read().get("msg_image")
+    _pb = eng.profile_read()
+    build, kxb = _pb.get("msg_image"), _pb.get("msg_kx_build")
     eng.profile_reset()
     t_start = time.perf_counter()
     for _ in range(args.steps):
@@ -290,7 +291,8 @@ def main():
                                                           + ("through the index's edge table" if args.no_img_edges
                                                              else "in the image's edge table")
                                                           + ("" if args.no_key_index else "; under wide runs the key index")),
-        "image_build_ms": build[1] if build else None,
+        "image_build_ms": (build[1] if build else 0.0) + (kxb[1] if kxb else 0.0) if build else None,
+        "image_build_parts_ms": {"image": build[1] if build else None, "key_index": kxb[1] if kxb else None},
     }
     cpu = None
     o = None

@@ -2342,8 +2342,12 @@ void Device::ensure_img(const Index& ix, const DevIndex& di, hipStream_t s) {
     img_edge_mask_ = slots2 - 1;
   }
   kx_built_ = false;
-  if (msg_kx_on_) build_key_index(di, lo, slots, s);
-  prof.end("msg_image", s);
+  prof.end("msg_image", s);  // (the profiler does not nest: the key index is timed apart)
+  if (msg_kx_on_) {
+    prof.begin(s, "msg_kx_build");
+    build_key_index(di, lo, slots, s);
+    prof.end("msg_kx_build", s);
+  }
   img_n_ = lo;
   img_n_pos_ = slots;
   img_levels_ = levels;
