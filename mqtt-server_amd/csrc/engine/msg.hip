@@ -548,50 +548,77 @@ __device__ __forceinline__ uint32_t img_child(const MsgImg& img, const DevIndex&
 }
 
 // ---- the image's key index (round 6) -----------------------------------------------------------
-// Thread per slot of the index's edge table: every edge between image particles, as (parent and
-// child image positions, the key, its hash), in any order (k_kx_collect), then stably sorted by
-// parent position and by key hash (hipcub radix sorts, gathers), so that one key's entries are
-// contiguous and ordered by parent position.
+// Every edge of the index's edge table between image particles, as (parent and child image
+// positions, the key, its hash), in any order (k_kx_collect), then stably sorted by parent
+// position and by key hash (hipcub radix sorts, gathers), so that one key's entries are contiguous
+// and ordered by parent position. A workgroup per chunk of edge slots, two passes over it: count,
+// one atomic for the chunk's range, write (one atomic per wavefront on a single counter took
+// 98 ms at 10M retained: ~4M same-address atomics; the edge slots are sparse)
 __global__ __launch_bounds__(256) void k_kx_collect(DevIndex ix, const uint32_t* __restrict__ node,
                                                     const uint32_t* __restrict__ pos, uint32_t n, uint32_t n_pos,
-                                                    uint32_t* __restrict__ par, uint32_t* __restrict__ chd,
-                                                    uint64_t* __restrict__ k0, uint64_t* __restrict__ k1,
-                                                    uint64_t* __restrict__ h, uint32_t* __restrict__ perm,
+                                                    uint64_t chunk, uint32_t* __restrict__ par,
+                                                    uint32_t* __restrict__ chd, uint64_t* __restrict__ k0,
+                                                    uint64_t* __restrict__ k1, uint64_t* __restrict__ h,
+                                                    uint32_t* __restrict__ perm,
                                                     unsigned long long* __restrict__ count) {
+  __shared__ uint32_t wcnt[4];
+  __shared__ unsigned long long base_s;
   auto in_img = [&](uint32_t c) __attribute__((always_inline)) -> uint32_t {
     if (c >= n_pos) return kNone;
     const uint32_t q = pos[c];
     return (q < n && node[q] == c) ? q : kNone;
   };
-  // (wave-uniform trip count: the wave's entries take one atomic together — one per edge on a
-  // single counter serialised the 100M-retained build, 203 ms)
-  const uint64_t slots = ix.edge_mask + 1, stride = (uint64_t)gridDim.x * 256;
-  const uint64_t i0 = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u);
-  for (uint64_t w = i0; w < slots; w += stride) {
-    const uint64_t i = w + (threadIdx.x & 63u);
-    uint32_t qc = kNone, qp = kNone;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t slots = ix.edge_mask + 1;
+  const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = min(slots, c0 + chunk);
+  auto look = [&](uint64_t i, EdgeSlot& e, uint32_t& qc, uint32_t& qp) __attribute__((always_inline)) -> bool {
+    qc = qp = kNone;
+    if (i >= c1) return false;
+    e = ix.edges[i];
+    if (e.parent >= kEdgeTomb) return false;  // a free slot
+    qc = in_img(e.child);
+    if (qc == kNone) return false;
+    qp = in_img(e.parent);
+    return qp != kNone;
+  };
+  uint32_t c = 0;
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += 256) {
+    EdgeSlot e;
+    uint32_t qc, qp;
+    c += look(i, e, qc, qp) ? 1u : 0u;
+  }
+  c = wave_sum(c);
+  if (lane == 0) wcnt[wv] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    base_s = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  unsigned long long off = base_s;
+  for (uint64_t i0 = c0; i0 < c1; i0 += 256) {  // (workgroup-uniform trip count)
     EdgeSlot e{};
-    if (i < slots) {
-      e = ix.edges[i];
-      if (e.parent < kEdgeTomb) {  // (else a free slot)
-        qc = in_img(e.child);
-        if (qc != kNone) qp = in_img(e.parent);
-      }
-    }
-    const bool take = qc != kNone && qp != kNone;
+    uint32_t qc, qp;
+    const bool take = look(i0 + threadIdx.x, e, qc, qp);
     const uint64_t m = __ballot(take);
-    if (!m) continue;
-    unsigned long long b = 0;
-    if ((threadIdx.x & 63u) == 0) b = atomicAdd(count, (unsigned long long)__popcll(m));
-    b = __shfl(b, 0, 64);
-    if (!take) continue;
-    const uint32_t j = (uint32_t)(b + prefix_before(m));
-    par[j] = qp;
-    chd[j] = qc;
-    k0[j] = e.k0;
-    k1[j] = e.k1;
-    h[j] = kx_hash(e.k0, e.k1);
-    perm[j] = j;
+    __syncthreads();  // (the last round's counts are read)
+    if (lane == 0) wcnt[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+      before += k < wv ? wcnt[k] : 0u;
+      tot += wcnt[k];
+    }
+    if (take) {
+      const uint32_t j = (uint32_t)(off + before + prefix_before(m));
+      par[j] = qp;
+      chd[j] = qc;
+      k0[j] = e.k0;
+      k1[j] = e.k1;
+      h[j] = kx_hash(e.k0, e.k1);
+      perm[j] = j;
+    }
+    off += tot;
   }
 }
 
@@ -599,8 +626,10 @@ void launch_kx_collect(const DevIndex& ix, const uint32_t* node, const uint32_t*
                        uint32_t* par, uint32_t* chd, uint64_t* k0, uint64_t* k1, uint64_t* h, uint32_t* perm,
                        unsigned long long* count, hipStream_t s) {
   const uint64_t slots = ix.edge_mask + 1;
-  const uint32_t g = (uint32_t)std::min<uint64_t>((slots + 255) / 256, 1u << 20);
-  hipLaunchKernelGGL(k_kx_collect, dim3(g), dim3(256), 0, s, ix, node, pos, n, n_pos, par, chd, k0, k1, h, perm, count);
+  const uint64_t chunk = std::max<uint64_t>(256, ((slots + 4095) / 4096 + 255) & ~255ull);  // ~4k workgroups
+  const uint32_t g = (uint32_t)((slots + chunk - 1) / chunk);
+  hipLaunchKernelGGL(k_kx_collect, dim3(g), dim3(256), 0, s, ix, node, pos, n, n_pos, chunk, par, chd, k0, k1, h,
+                     perm, count);
 }
 
 size_t kx_sort_u32(void* temp, size_t temp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
