@@ -649,7 +649,10 @@ struct MsgWide {
 // a literal level through the key index exports more than this many candidate entries (its items
 // look up entries, not particles; 10M retained: 512 -> 128, 83.4M -> 127.8M filters/s, r06/p)
 constexpr uint32_t kMsgExportMinHits = 128;
-constexpr uint32_t kMsgChunk = 256;       // particles per exported work item (or key-index entries)
+#ifndef MQ_MSG_CHUNK
+#define MQ_MSG_CHUNK 256
+#endif
+constexpr uint32_t kMsgChunk = MQ_MSG_CHUNK;  // particles per exported work item (or key-index entries)
 constexpr uint32_t kMsgWorkEntries = 1u << 31;  // MsgWork.s: the item's [x, y) is a range of key-index entries
 static_assert(kMsgChunk <= 256, "an entry item's hits must fit the fan-out frontier (kMsgFront)");
 constexpr uint32_t kMsgWorkCap = 1u << 20;  // work items per batch (32 MB)
